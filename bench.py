@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""bench.py — dpgo edges·iters/sec (+ LC candidates verified/sec) on MI355X.
+
+Contract (see task statement / DESIGN.md "Measurement"):
+  python bench.py --gpus N --steps K --warmup W
+  (N > 1 is launched by torch.distributed.run, one rank per GPU over RCCL).
+A "step" is one synchronous RBCD round (dpgo_ros UPDATE -> PGOAgent::iterate of
+every robot block, drawio:2058-2066) over the synthetic configs[3] graph
+(100k poses / 500k edges, 20 % outlier loop closures, 8 robot blocks), with the
+GNC weight update every 20 rounds inside the timed region. The robot blocks are
+split across ranks (strong scaling of the fixed graph, as north_star asks:
+">= 6x further scaling at 8 GPUs" of the same 100k graph).
+
+value = sum over ranks of edges·iters (sum over executed block updates of the
+block's local-problem edge count) / max-over-ranks wall time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "kimera-multi_amd"))
+
+PEAK_HBM = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="synth100k")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-lcd", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no cpu / lcd)")
+    return ap.parse_args()
+
+
+def make_workload(name):
+    from kmx.synth import config, lift, lifting_matrix
+    g = config(name, seed=0)
+    Y = lifting_matrix(5, seed=1)
+    X0 = {a: lift(g.init_R[a], g.init_t[a], Y) for a in range(g.n_robots)}
+    return g, X0
+
+
+def params():
+    from kmx.dpgo.params import PGOAgentParameters
+    P = PGOAgentParameters(r=5)
+    P.localOptimizationParams.RTR_iterations = 1
+    P.localOptimizationParams.RTR_tCG_iterations = 10
+    P.robustOptInnerIters = 20
+    P.robustOptNumWeightUpdates = 10**9
+    P.schedule = 1
+    return P
+
+
+def cpu_baseline(g, X0, P, seconds):
+    """The C restatement (oracle/) on this host, single thread (dpgo runs one
+    agent per process); bounded sample of whole rounds of the same workload."""
+    sys.path.insert(0, str(ROOT))
+    from oracle.oracle import OraclePGO
+    o = OraclePGO(P.to_c(), g)
+    for a in range(g.n_robots):
+        o.set_iterate(a, X0[a])
+    edges_iters, rounds = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        st = o.iterate(threads=1)
+        edges_iters += sum(s["edges"] for s in st if s["updated"] and s["tcg_stop"] != "skipped")
+        rounds += 1
+        if rounds % P.robustOptInnerIters == 0:
+            o.update_weights()
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": edges_iters / el, "unit": "edges*iters/s", "cores": 1, "kind": "port",
+            "sample": f"{rounds} RBCD rounds of {P and 'configs[3]'} (8 blocks, 1 RTR step, <=10 tCG) "
+                      f"from the same initial iterate, oracle/dpgo_oracle.c -O3 x86-64-v3, 1 thread, {el:.1f} s"}
+
+
+def load_traffic():
+    f = ROOT / "profiles" / "hessvec_traffic.json"
+    if f.exists():
+        try:
+            return json.loads(f.read_text())
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from kmx.dpgo.driver import RBCDDriver
+
+    g, X0 = make_workload(args.config)
+    P = params()
+    drv = RBCDDriver(P, g, rank=rank, world=world, device=local_rank if world > 1 else 0)
+    drv.initialize(X0)
+
+    def barrier_sync():
+        drv.solver.sync()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    drv.run_async(args.warmup)
+    barrier_sync()
+    drv.solver.read_counters()  # reset device counters and event pool
+    drv.solver.enable_timing(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    drv.run_async(args.steps)
+    barrier_sync()
+    el = time.perf_counter() - t0
+    drv.solver.enable_timing(False)
+    cnt = drv.solver.read_counters()
+    edges_iters = float(cnt["edges_iters"])
+    hv_ms, hv_bytes, hv_n = cnt["hessvec_ms_total"], cnt["hessvec_alg_bytes"], cnt["hessvec_launches"]
+    if dist is not None:
+        t = torch.tensor([el, -el, edges_iters, hv_ms, hv_bytes, float(hv_n)], dtype=torch.float64, device="cuda")
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        parts = torch.stack(parts).cpu().numpy()
+        el = float(parts[:, 0].max())
+        edges_iters = float(parts[:, 2].sum())
+        hv_ms, hv_bytes, hv_n = float(parts[:, 3].sum()), float(parts[:, 4].sum()), int(parts[:, 5].sum())
+    value = edges_iters / el
+    achieved = hv_bytes / (hv_ms * 1e-3) if hv_ms > 0 else 0.0
+    traffic = load_traffic()
+    out = {
+        "metric": "dpgo edges*iters/sec",
+        "value": value,
+        "unit": "edges*iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * el / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded numpy PCG64; Campus bags unavailable offline)",
+        "config": {
+            "workload": f"configs[3] {args.config}: {g.n_total} poses / {g.m} edges, {g.n_robots} robot blocks, "
+                        f"20% outlier LCs, f_inter 0.10, GNC-TLS every 20 rounds",
+            "robots": g.n_robots, "poses": g.n_total, "edges": g.m, "r": P.r,
+            "rtr_iterations": 1, "tcg_max": 10, "schedule": "concurrent",
+            "parallelism": f"robot blocks {g.n_robots} over {world} GPU(s)",
+        },
+        "roofline": {
+            "kernel": "k_hess (tCG Hessian-vector product)",
+            "bound": "hbm",
+            "achieved": achieved / 1e9,
+            "peak": PEAK_HBM / 1e9,
+            "unit": "GB/s",
+            "frac": achieved / PEAK_HBM,
+            "traffic": (traffic or {}).get("bytes_per_launch") if traffic else None,
+            "launches": hv_n,
+            "avg_launch_us": 1e3 * hv_ms / max(hv_n, 1),
+            "alg_bytes_per_launch": hv_bytes / max(hv_n, 1),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu and not args.profile:
+        out["cpu_baseline"] = cpu_baseline(g, X0, P, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

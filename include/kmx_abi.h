@@ -1,0 +1,313 @@
+/*
+ * kmx_abi.h — the C ABI of the MI355X-native dpgo / Kimera-Multi-LCD hot path.
+ *
+ * This is the drop-in boundary. Every entry point replaces the
+ * bottom of one reference interface. The reference sources are NOT vendored in
+ * /root/reference (SURVEY.md §0 finding 1); the interfaces are cited from the
+ * fork author's call-flow diagram `images/kimera-multi.drawio` (drawio:N) and the
+ * in-tree parameter files.
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes, no C++/torch types.
+ *   - Every function returns int: 0 = ok, < 0 = error (KMX_E*). kmx_last_error()
+ *     returns a thread-local message for the last failing call.
+ *   - Host arrays are owned by the caller and only read/written during the call.
+ *     Device buffers are owned by the handle, except the exchange buffers of
+ *     kmx_pgo_pack_public / kmx_pgo_unpack_public, which are caller-owned device
+ *     pointers (e.g. torch tensors used with RCCL).
+ *   - A handle is not thread-safe. All of its device work is enqueued on one HIP
+ *     stream (its own, or the caller's via kmx_pgo_set_stream); calls that return
+ *     host data synchronise that stream.
+ *   - Lifted pose layout: pose i of a robot block is X_i = [Y_i p_i] in
+ *     R^{r x (d+1)}, stored row-major: X[i*4r + a*4 + c], a < r, c < 4 (c = 3 is p).
+ *     d = 3 is fixed.
+ */
+#ifndef KMX_ABI_H
+#define KMX_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KMX_ABI_VERSION 1
+
+/* error codes */
+#define KMX_OK 0
+#define KMX_EINVAL (-1)   /* bad argument / shape */
+#define KMX_EHIP (-2)     /* HIP runtime error */
+#define KMX_ESTATE (-3)   /* call out of order (e.g. iterate before set_graph) */
+#define KMX_ENOMEM (-4)
+#define KMX_EUNSUP (-5)   /* unsupported parameter value (e.g. relaxation rank) */
+
+const char* kmx_last_error(void);
+int kmx_abi_version(void);
+/* number of visible HIP devices (0 when no GPU). Does not create a context. */
+int kmx_device_count(int* out);
+
+/* ------------------------------------------------------------------------- */
+/* dpgo: distributed pose-graph optimisation (RBCD on lifted SE(3) with GNC)  */
+/* ------------------------------------------------------------------------- */
+
+/* Robust cost selector. Reference: dpgo RobustCostType, selector `GNC_TLS`
+ * (drawio:2175). Only L2 and GNC_TLS are on the hot path. */
+#define KMX_COST_L2 0
+#define KMX_COST_GNC_TLS 1
+
+/* Block-update schedule across robots (SURVEY.md §0 finding 6). */
+#define KMX_SCHEDULE_SEQUENTIAL 0 /* one executing robot per round (dpgo_ros sync) */
+#define KMX_SCHEDULE_CONCURRENT 1 /* every active robot per round (Jacobi)        */
+
+/* Mirrors dpgo PGOAgentParameters + ROptParameters + RobustCostParameters
+ * (drawio:2457-2513). Values in comments are the defaults kmx.dpgo uses. */
+typedef struct kmx_pgo_params {
+  int d;                    /* 3 (only 3 is supported)                        */
+  int r;                    /* relaxation rank, 3..8 (5)                      */
+  int rtr_iterations;       /* RTR outer iterations per block update (1)      */
+  int tcg_max_iterations;   /* truncated-CG inner iterations (10)             */
+  double tcg_kappa;         /* tCG linear-convergence target (0.1)            */
+  double tcg_theta;         /* tCG superlinear exponent (1.0)                 */
+  double rtr_initial_radius;/* trust radius at the start of a block update (100) */
+  double rtr_max_radius;    /* (1e4)                                          */
+  double rtr_accept_rho;    /* accept the step if rho > this (0.1)            */
+  double gradnorm_tol;      /* skip the block update if ||grad|| < tol (1e-2) */
+  int use_preconditioner;   /* block-Jacobi preconditioner on/off (1)         */
+  double precond_shift;     /* lambda added to each 4x4 diagonal block (1e-1) */
+  int robust_cost;          /* KMX_COST_* (GNC_TLS)                           */
+  double gnc_barc;          /* TLS error threshold c-bar (5.0)                */
+  double gnc_mu_init;       /* GNC initial mu (1e-5)                          */
+  double gnc_mu_step;       /* mu <- mu * step after each weight update (1.4) */
+  int reserved[8];
+} kmx_pgo_params;
+
+/* Per-robot statistics of one RBCD round (what dpgo logs to dpgo_log_*.csv via
+ * logIteration, drawio:2136-2142). */
+typedef struct kmx_iter_stats {
+  int updated;          /* 1 if this robot executed a block update this round  */
+  int tcg_iterations;   /* inner iterations of the last RTR iteration          */
+  int tcg_stop;         /* KMX_TCG_*                                           */
+  int accepted;         /* last RTR step accepted                              */
+  double f_init;        /* local cost before the update                        */
+  double gradnorm_init; /* Riemannian gradient norm before the update          */
+  double f_final;       /* local cost after the update                         */
+  double rho;           /* actual / predicted decrease of the last RTR step    */
+  double radius;        /* trust radius after the last RTR step                */
+  double rel_change;    /* ||X_new - X_old||_F / sqrt(n) (dpgo relativeChange) */
+  int64_t edges;        /* edges in the block's local problem (metric unit)    */
+  int64_t hessvecs;     /* Hessian-vector products evaluated                   */
+} kmx_iter_stats;
+
+#define KMX_TCG_NONE 0
+#define KMX_TCG_NEGATIVE_CURVATURE 1
+#define KMX_TCG_EXCEEDED_TR 2
+#define KMX_TCG_LINEAR 3      /* ||r|| <= ||r0|| kappa        */
+#define KMX_TCG_SUPERLINEAR 4 /* ||r|| <= ||r0||^(1+theta)    */
+#define KMX_TCG_MAX_ITER 5
+#define KMX_TCG_SKIPPED 6     /* gradient below tolerance: no step */
+
+typedef struct kmx_pgo kmx_pgo;
+
+/* Replaces `PGOAgent(id, PGOAgentParameters)` (drawio:1943-1957, 2457).
+ * `device` is the HIP ordinal used by this handle. */
+int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo** out);
+int kmx_pgo_destroy(kmx_pgo* h);
+/* Use the caller's HIP stream (e.g. torch.cuda.current_stream().cuda_stream). */
+int kmx_pgo_set_stream(kmx_pgo* h, void* hip_stream);
+
+/* Replaces the pose-graph intake `PGOAgent::addMeasurement` ->
+ * PoseGraph::addOdometry / addPrivateLoopClosure / addSharedLoopClosure
+ * (drawio:2142, 2779-2826). Edges are the GLOBAL measurement list of the team:
+ * measurement e goes from pose (r1[e],p1[e]) to (r2[e],p2[e]) with rotation
+ * R[9e..9e+8] (row-major) and translation t[3e..3e+2], precisions kappa / tau,
+ * weight w and fixedWeight flag (odometry). `local[a]` marks robots whose blocks
+ * live on this handle; edges with no local endpoint are dropped. Shared loop
+ * closures (r1 != r2) are owned by min(r1, r2) for GNC weights (drawio:2198). */
+int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_poses,
+                      const uint8_t* local, int64_t m, const int32_t* r1,
+                      const int32_t* p1, const int32_t* r2, const int32_t* p2,
+                      const double* R, const double* t, const double* kappa,
+                      const double* tau, const double* weight,
+                      const uint8_t* fixed_weight);
+
+/* Replaces `initialize(...)` with an injected initial iterate:
+ * X is n_poses[robot] * 4r doubles. get_iterate reads the current block back. */
+int kmx_pgo_set_iterate(kmx_pgo* h, int robot, const double* X);
+int kmx_pgo_get_iterate(kmx_pgo* h, int robot, double* X);
+
+/* Public-pose exchange (publishPublicPoses -> updateNeighborPoses,
+ * drawio:2340-2355). The team's public poses (every endpoint of a shared loop
+ * closure) form one global table ordered by (robot, pose); its size is
+ * kmx_pgo_public_count. pack writes this handle's OWNED rows
+ * [first, first+count) of the table (count * 4r doubles) to a caller device
+ * buffer; unpack installs a full table (n_public * 4r doubles, device) as the
+ * fixed neighbour poses. refresh_local does pack+unpack in-device for the case
+ * where every robot is local. set_neighbor_poses is the host-side variant
+ * (updateNeighborPoses with a PoseDict): rows for the given (robot,pose). */
+int kmx_pgo_public_count(kmx_pgo* h, int64_t* n_public, int64_t* first_owned,
+                         int64_t* n_owned);
+int kmx_pgo_pack_public(kmx_pgo* h, void* dev_out);
+int kmx_pgo_unpack_public(kmx_pgo* h, const void* dev_table);
+int kmx_pgo_refresh_local(kmx_pgo* h);
+int kmx_pgo_set_neighbor_poses(kmx_pgo* h, int64_t count, const int32_t* robot,
+                               const int32_t* pose, const double* X);
+
+/* One RBCD round: `PGOAgent::iterate(doOptimization)` of every robot with
+ * active[a] != 0 (drawio:2058-2066, 2513), all using the current neighbour
+ * table. stats (may be NULL) receives one record per robot of the team
+ * (n_robots records; non-local / inactive robots get updated = 0). */
+int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats* stats);
+/* Enqueue `rounds` concurrent rounds (all local robots active) without any
+ * host synchronisation; used by the benchmark. stats are not produced. When
+ * refresh_local != 0 every round starts with kmx_pgo_refresh_local (the
+ * single-device public-pose exchange); otherwise the caller exchanges. When
+ * gnc_every > 0, a GNC weight update runs after every gnc_every-th round
+ * (counted across calls), as dpgo_ros does on UPDATE_WEIGHT. */
+int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local,
+                          int gnc_every);
+/* Wait for all work enqueued on the handle's stream. */
+int kmx_pgo_sync(kmx_pgo* h);
+
+/* GNC: `updateMeasurementWeights()` (drawio:2215) for every non-fixed edge owned
+ * by a local robot, evaluated at the current iterate and neighbour table, then
+ * mu <- mu * mu_step. mu_out (may be NULL) gets the mu used. */
+int kmx_pgo_update_weights(kmx_pgo* h, double* mu_out);
+int kmx_pgo_get_mu(kmx_pgo* h, double* mu);
+int kmx_pgo_set_mu(kmx_pgo* h, double mu);
+/* `setMeasurementWeight` (drawio:2268) in bulk: weights indexed by global edge
+ * id (m doubles). get returns the weights of edges with a local endpoint (others
+ * untouched). set installs all; the handle rebuilds its preconditioner. */
+int kmx_pgo_get_weights(kmx_pgo* h, double* w);
+int kmx_pgo_set_weights(kmx_pgo* h, const double* w);
+/* Shared-edge weight exchange for multi-GPU GNC (owner -> peer, drawio:2198):
+ * the team's shared loop closures in global edge order; pack writes owned
+ * entries and zeros elsewhere (n_shared doubles, device), unpack installs the
+ * all-reduced table. */
+int kmx_pgo_shared_count(kmx_pgo* h, int64_t* n_shared);
+int kmx_pgo_pack_shared_weights(kmx_pgo* h, void* dev_out);
+int kmx_pgo_unpack_shared_weights(kmx_pgo* h, const void* dev_table);
+
+/* Rounded trajectory in the anchor frame: `getTrajectoryInGlobalFrame` /
+ * publishTrajectory (drawio:2148-2151) with the global anchor of
+ * `setGlobalAnchor` (drawio:2396). anchor = 4r doubles [Y0 p0] (lifted pose of
+ * robot 0, pose 0). out: n_poses[robot] * 12 doubles = R (row-major 3x3) then t. */
+int kmx_pgo_get_trajectory(kmx_pgo* h, int robot, const double* anchor,
+                           double* out);
+
+/* Primitive evaluation for parity tests (one robot block, current neighbour
+ * table). mode: KMX_EVAL_*. V/out are n_poses[robot]*4r doubles; scalar gets the
+ * cost (COST_EGRAD) or <V, out> otherwise. HESS modes evaluate at the current
+ * iterate. */
+#define KMX_EVAL_COST_EGRAD 0 /* out = Euclidean gradient at X=V, scalar = f(V) */
+#define KMX_EVAL_EHESS 1      /* out = Euclidean Hessian-vector product Q V      */
+#define KMX_EVAL_RGRAD 2      /* out = Riemannian gradient at X (V ignored)      */
+#define KMX_EVAL_RHESS 3      /* out = Riemannian Hessian at X applied to V      */
+#define KMX_EVAL_PRECON 4     /* out = preconditioner at X applied to V          */
+#define KMX_EVAL_RETRACT 5    /* out = R_X(V)                                    */
+int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, double* out,
+                 double* scalar);
+
+/* Edges in robot `robot`'s local problem (private + shared incident edges). */
+int kmx_pgo_local_edges(kmx_pgo* h, int robot, int64_t* m_local);
+/* Live instrumentation of the dominant kernel (the Hessian-vector product of
+ * the tCG loop). When enabled, every Hessian-vector launch enqueued by
+ * kmx_pgo_iterate / kmx_pgo_iterate_async is bracketed by a HIP event pair on
+ * the handle's stream. read_timing synchronises, sums the event durations and
+ * the device-side work counters accumulated since the last read, and resets
+ * them. hessvec_alg_bytes follows SURVEY.md §8d: per launch and per robot whose
+ * tCG was running, 128 B per local edge + 2 * 8 * r(d+1) B per pose. */
+typedef struct kmx_pgo_counters {
+  double hessvec_ms_total;     /* summed device time of Hessian-vector launches */
+  int64_t hessvec_launches;    /* launches bracketed by events                  */
+  double hessvec_alg_bytes;    /* algorithmic bytes those launches processed    */
+  int64_t edges_iters;         /* sum over executed block updates of m_alpha    */
+  int64_t block_updates;       /* executed block updates (tCG ran)              */
+  int64_t hessvecs;            /* robot-level Hessian-vector products           */
+} kmx_pgo_counters;
+int kmx_pgo_enable_timing(kmx_pgo* h, int enable);
+int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out);
+
+/* ------------------------------------------------------------------------- */
+/* Kimera-Multi-LCD: descriptor matching + geometric verification             */
+/* ------------------------------------------------------------------------- */
+
+#define KMX_NORM_L1 0      /* BruteForce-L1 over bytes: reference build      */
+#define KMX_NORM_HAMMING 1 /* BruteForce-Hamming over 256 bits: north_star  */
+
+/* sampler variants of std::uniform_int_distribution<int>(0, INT_MAX) over
+ * std::mt19937 (SURVEY.md §0 finding 5) */
+#define KMX_RNG_GCC9 0   /* rejection of x >= 2^31, returns x (ROS Noetic)  */
+#define KMX_RNG_GCC11 1  /* Lemire: returns x >> 1                          */
+
+/* LcdParams (params/D455/LcdParams.yaml:16-17, 51-66). */
+typedef struct kmx_lcd_params {
+  int norm;                   /* KMX_NORM_* (L1: matcher_type 3 + patch:33-35) */
+  float lowe_ratio;           /* 0.7                                           */
+  int min_2d2d_inliers;       /* 10                                            */
+  int min_3d3d_inliers;       /* 5                                             */
+  double ransac_threshold_2d2d; /* 1e-6 (1 - cos)                              */
+  double ransac_threshold_3d3d; /* 0.3 m                                       */
+  int ransac_max_iterations;  /* 500                                           */
+  double ransac_probability;  /* 0.995                                         */
+  int ransac_randomize;       /* 0: fixed seed                                 */
+  uint32_t ransac_seed;       /* 12345                                         */
+  int rng_variant;            /* KMX_RNG_*                                     */
+  int use_1point_3d3d;        /* 1: translation-only 3D-3D given the 2D-2D R   */
+  int reserved[8];
+} kmx_lcd_params;
+
+/* computeMatchedIndices (drawio:2583-2586): k=2 brute-force match of every
+ * query descriptor against the match frame + Lowe ratio. desc are 32-byte ORB
+ * descriptors. Output pairs (i_query, i_match) in query order; *k = count. */
+int kmx_lcd_knn2(int norm, float lowe_ratio, const uint8_t* q, int32_t nq,
+                 const uint8_t* mdesc, int32_t nm, int32_t* pairs_out,
+                 int32_t* k);
+
+/* Batched verification of candidates (verifyLoopSpin -> computeMatchedIndices
+ * -> geometricVerificationNister -> recoverPose, drawio:2638-2657). */
+typedef struct kmx_lcd_batch_desc {
+  int32_t n_frames;       /* frames in the descriptor/feature pool           */
+  int32_t max_feats;      /* features per frame (stride)                     */
+  const int32_t* n_feats; /* [n_frames]                                       */
+  const uint8_t* desc;    /* [n_frames][max_feats][32]                        */
+  const double* bearings; /* [n_frames][max_feats][3] unit bearing vectors    */
+  const double* points;   /* [n_frames][max_feats][3] stereo points (or NaN)  */
+  int32_t n_cand;
+  const int32_t* cand_query; /* [n_cand] frame ids */
+  const int32_t* cand_match; /* [n_cand] frame ids */
+} kmx_lcd_batch_desc;
+
+typedef struct kmx_lcd_result {
+  int32_t n_matches;      /* after kNN + Lowe                                 */
+  int32_t mono_inliers;   /* 2D-2D RANSAC inliers                             */
+  int32_t stereo_inliers; /* 3D-3D inliers                                    */
+  int32_t accepted;       /* mono >= min_2d2d && stereo >= min_3d3d           */
+  int32_t iterations_2d2d;
+  int32_t pad;
+  double T_query_match[12]; /* R row-major, t                                 */
+} kmx_lcd_result;
+
+typedef struct kmx_lcd kmx_lcd;
+int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd** out);
+int kmx_lcd_destroy(kmx_lcd* h);
+int kmx_lcd_set_stream(kmx_lcd* h, void* hip_stream);
+/* Upload the frame pool (host arrays) to the device; kept until replaced. */
+int kmx_lcd_set_frames(kmx_lcd* h, const kmx_lcd_batch_desc* pool);
+/* Verify n_cand candidates against the resident pool. results: n_cand records.
+ * inlier masks (optional, may be NULL): [n_cand][max_feats] bytes, bit0 = 2D-2D
+ * inlier, bit1 = 3D-3D inlier, indexed by match index (position in the pair
+ * list of kmx_lcd_knn2 order). */
+int kmx_lcd_verify(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
+                   const int32_t* cand_match, kmx_lcd_result* results,
+                   uint8_t* inlier_masks);
+/* Enqueue verification of candidates already resident on the device without
+ * host synchronisation (benchmark path). */
+int kmx_lcd_verify_async(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
+                         const int32_t* cand_match);
+int kmx_lcd_sync(kmx_lcd* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMX_ABI_H */

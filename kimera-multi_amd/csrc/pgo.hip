@@ -1,0 +1,1649 @@
+// pgo.hip — MI355X (gfx950) RBCD block updates on lifted SE(3) with GNC-TLS.
+//
+// Replaces dpgo's PGOAgent::iterate / updateMeasurementWeights hot path
+// (drawio:2058-2066, 2215, 2513). Design:
+//   * Every local robot block lives in HBM; all blocks are updated by the same
+//     launches (batched RBCD). Workgroup tiles never straddle robots, so every
+//     reduction is per robot and its control scalars (trust radius, tCG alpha /
+//     beta, ...) live on the device in a Ctl record per robot. The host never
+//     reads a scalar inside a round: the tCG loop is a fixed launch sequence and
+//     finished robots' tiles exit at their first instruction.
+//   * Thread <-> (pose, row): the Euclidean Hessian-vector product X -> XQ acts
+//     on each of the r rows of a pose independently, so a lane owns one row
+//     (4 doubles) of one pose and a pose is a group of r lanes of one wave.
+//     Only the Stiefel projection / retraction need sums over the r rows, done
+//     with in-group shuffles in a fixed order.
+//   * Node-centric gather over a CSR incidence list (no atomics): every output
+//     element accumulates its incident edges in increasing edge id, the same
+//     order as the CPU restatement's edge loop, and kernels are built with
+//     -ffp-contract=off, so per-element results match the oracle bit for bit.
+//   * Reductions: one partial per workgroup tile, reduced in fixed order by a
+//     one-workgroup control kernel that also runs the RTR / tCG scalar logic.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+constexpr int WAVES = 4;
+constexpr int BLOCK = 64 * WAVES;
+constexpr int NPART = 4;  // partial sums per tile
+
+enum Phase { PH_IDLE = 0, PH_START = 1, PH_TCG = 2, PH_STEP = 3 };
+enum Mode { MODE_INTERIOR = 0, MODE_BOUNDARY = 1 };
+enum RedKind { RED_GRAD = 0, RED_HESS = 1, RED_UPDATE = 2, RED_COST = 3 };
+
+struct Ctl {
+  int phase, rtr_iter, tcg_iter, tcg_stop;
+  int mode, accepted, commit, updated;
+  int hessvecs, skipped, pad0, pad1;
+  double Delta, f_init, gn_init, f_cur;
+  double f_final, norm_r0, z_r, e_Pe;
+  double e_Pd, d_Pd, alpha, beta;
+  double coef, rho, chg_acc, rel_change;
+};
+
+struct Counters {
+  unsigned long long edges_iters;
+  unsigned long long block_updates;
+  unsigned long long hessvecs;
+  unsigned long long pad;
+  double hess_alg_bytes;
+  double pad2[3];
+};
+
+struct Params {
+  int tcg_max, rtr_iters, use_precond, robust;
+  double kappa, theta, Delta0, Delta_max, accept_rho, gn_tol, shift, barc;
+};
+
+struct Dev {
+  int ntiles, L, nloc, npub;
+  const int* tile_robot;
+  const int* tile_p0;
+  const int* tile_np;
+  const int* rtile0;  // [L+1]
+  const int* inc_ptr; // [nloc+1]
+  const int2* inc;    // x = other (>=0 local pose, <0 -> public slot -1-x); y = edge | tail<<31
+  double* erec;       // [mloc][16]: R(9) t(3) kappa tau w pad
+  double *X, *Xt, *g, *r, *z, *eta, *del, *hd, *S, *Pinv, *pub;
+  double* part;       // [ntiles][NPART]
+  Ctl* ctl;
+  Counters* cnt;
+  const long long* m_robot;  // [L] local-problem edges per robot
+  const int* n_robot;        // [L] poses per robot
+  Params p;
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Sum over all BLOCK threads in fixed order; every thread gets the result.
+__device__ __forceinline__ double block_sum(double v, double* lds) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < WAVES; ++w) s += lds[w];
+  return s;
+}
+
+// Sum of x over the R lanes of this lane's pose group, lane order 0..R-1
+// (the order of the oracle's row loop); identical in every lane of the group.
+template <int R>
+__device__ __forceinline__ double gsum(double x, int base) {
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < R; ++k) s += __shfl(x, base + k, 64);
+  return s;
+}
+
+__device__ __forceinline__ void load4(const double* p, double v[4]) {
+  const double2* q = reinterpret_cast<const double2*>(p);
+  double2 a = q[0], b = q[1];
+  v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+}
+__device__ __forceinline__ void store4(double* p, const double v[4]) {
+  double2* q = reinterpret_cast<double2*>(p);
+  q[0] = make_double2(v[0], v[1]);
+  q[1] = make_double2(v[2], v[3]);
+}
+
+struct Edge {
+  double R[9], t[3], wk, wt;
+};
+__device__ __forceinline__ void load_edge(const double* erec, int e, Edge& E) {
+  const double2* q = reinterpret_cast<const double2*>(erec + 16 * (size_t)e);
+  double2 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5], v6 = q[6], v7 = q[7];
+  E.R[0] = v0.x; E.R[1] = v0.y; E.R[2] = v1.x; E.R[3] = v1.y; E.R[4] = v2.x;
+  E.R[5] = v2.y; E.R[6] = v3.x; E.R[7] = v3.y; E.R[8] = v4.x;
+  E.t[0] = v4.y; E.t[1] = v5.x; E.t[2] = v5.y;
+  const double kappa = v6.x, tau = v6.y, w = v7.x;
+  E.wk = w * kappa;
+  E.wt = w * tau;
+}
+
+// Accumulate the contribution of one incidence to row a of pose `self`.
+// vs = self row, vo = other endpoint row (zeros for a Hessian product across a
+// shared edge). Expressions mirror oracle/dpgo_oracle.c edge_eval exactly.
+// Returns the row's share of 1/2 w (kappa |E_R|^2 + tau E_t^2).
+__device__ __forceinline__ double incidence_row(const Edge& E, bool self_tail, const double vs[4],
+                                                const double vo[4], double acc[4]) {
+  double ER[3], Et;
+  if (self_tail) {  // self = i (tail), other = j (head)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      ER[c] = vo[c] - (vs[0] * E.R[0 * 3 + c] + vs[1] * E.R[1 * 3 + c] + vs[2] * E.R[2 * 3 + c]);
+    Et = vo[3] - vs[3] - (vs[0] * E.t[0] + vs[1] * E.t[1] + vs[2] * E.t[2]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      acc[c] -= E.wk * (ER[0] * E.R[c * 3 + 0] + ER[1] * E.R[c * 3 + 1] + ER[2] * E.R[c * 3 + 2]) +
+                E.wt * Et * E.t[c];
+    acc[3] -= E.wt * Et;
+  } else {  // self = j (head), other = i (tail)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      ER[c] = vs[c] - (vo[0] * E.R[0 * 3 + c] + vo[1] * E.R[1 * 3 + c] + vo[2] * E.R[2 * 3 + c]);
+    Et = vs[3] - vo[3] - (vo[0] * E.t[0] + vo[1] * E.t[1] + vo[2] * E.t[2]);
+    acc[0] += E.wk * ER[0];
+    acc[1] += E.wk * ER[1];
+    acc[2] += E.wk * ER[2];
+    acc[3] += E.wt * Et;
+  }
+  return 0.5 * (E.wk * (ER[0] * ER[0] + ER[1] * ER[1] + ER[2] * ER[2]) + E.wt * Et * Et);
+}
+
+// Gather row a of (VQ [+ G]) for pose `pose`. V = block vector for private
+// neighbours; shared neighbours read the public table when `pub` != nullptr,
+// else are zero. cost (optional) accumulates this row's share of f:
+// private edges are seen from both endpoints (x 1/2), shared from one.
+template <int R>
+__device__ __forceinline__ void gather_row(const Dev& d, int pose, int a, const double* V,
+                                           const double* pub, double acc[4], double* cost) {
+  double vs[4], vo[4];
+  load4(V + (size_t)pose * 4 * R + 4 * a, vs);
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  const int k0 = d.inc_ptr[pose], k1 = d.inc_ptr[pose + 1];
+  for (int k = k0; k < k1; ++k) {
+    const int2 in = d.inc[k];
+    const bool tail = (in.y >> 31) & 1;
+    const int e = in.y & 0x7fffffff;
+    Edge E;
+    load_edge(d.erec, e, E);
+    bool priv = in.x >= 0;
+    if (priv) {
+      load4(V + (size_t)in.x * 4 * R + 4 * a, vo);
+    } else if (pub) {
+      load4(pub + (size_t)(-1 - in.x) * 4 * R + 4 * a, vo);
+    } else {
+      vo[0] = vo[1] = vo[2] = vo[3] = 0.0;
+    }
+    const double c = incidence_row(E, tail, vs, vo, acc);
+    if (cost) *cost += priv ? 0.5 * c : c;
+  }
+}
+
+// S = sym(Y^T G_Y) for the pose group (9 entries, identical in all R lanes).
+template <int R>
+__device__ __forceinline__ void group_symYtG(const double y[4], const double G[4], int base, double S[9]) {
+  double M[9];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) M[c * 3 + k] = gsum<R>(y[c] * G[k], base);
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) S[c * 3 + k] = 0.5 * (M[c * 3 + k] + M[k * 3 + c]);
+}
+
+// Tangent projection of row V at Y (group-cooperative): V_Y - Y sym(Y^T V_Y).
+template <int R>
+__device__ __forceinline__ void group_proj(const double y[4], const double V[4], int base, double out[4]) {
+  double S[9];
+  group_symYtG<R>(y, V, base, S);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) out[c] = V[c] - (y[0] * S[0 * 3 + c] + y[1] * S[1 * 3 + c] + y[2] * S[2 * 3 + c]);
+  out[3] = V[3];
+}
+
+template <int R>
+__device__ __forceinline__ void group_precon(const Dev& d, int pose, bool valid, const double y[4],
+                                             const double V[4], int base, double out[4]) {
+  double buf[4];
+  if (d.p.use_precond) {
+    double P[16];
+    if (valid) {
+      const double2* q = reinterpret_cast<const double2*>(d.Pinv + 16 * (size_t)pose);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        double2 v = q[i];
+        P[2 * i] = v.x;
+        P[2 * i + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) P[i] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      buf[k] = V[0] * P[0 * 4 + k] + V[1] * P[1 * 4 + k] + V[2] * P[2 * 4 + k] + V[3] * P[3 * 4 + k];
+    group_proj<R>(y, buf, base, out);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = V[k];
+  }
+}
+
+// Riemannian Hessian row of V given the Euclidean Hessian row H:
+// P_Y(H_Y - V_Y S) ; p-part H_p.
+template <int R>
+__device__ __forceinline__ void group_rhess(const double y[4], const double V[4], const double H[4],
+                                            const double S[9], int base, double out[4]) {
+  double buf[4];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) buf[k] = H[k] - (V[0] * S[0 * 3 + k] + V[1] * S[1 * 3 + k] + V[2] * S[2 * 3 + k]);
+  buf[3] = H[3];
+  group_proj<R>(y, buf, base, out);
+}
+
+// QF retraction (modified Gram-Schmidt over the 3 columns, positive diagonal).
+template <int R>
+__device__ __forceinline__ void group_retract(const double x[4], const double v[4], int base, double out[4]) {
+  double A[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) A[c] = x[c] + v[c];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int k = 0; k < c; ++k) {
+      const double s = gsum<R>(A[k] * A[c], base);
+      A[c] -= s * A[k];
+    }
+    const double nn = gsum<R>(A[c] * A[c], base);
+    const double inv = 1.0 / sqrt(nn);
+    A[c] *= inv;
+  }
+  out[0] = A[0]; out[1] = A[1]; out[2] = A[2];
+  out[3] = x[3] + v[3];
+}
+
+struct Lane {
+  int tile, l, w, ln, pw, a, base, pose;
+  bool valid;
+};
+template <int R>
+__device__ __forceinline__ Lane lane_map(const Dev& d) {
+  constexpr int PPW = 64 / R;
+  Lane L;
+  L.tile = blockIdx.x;
+  L.l = d.tile_robot[L.tile];
+  L.w = threadIdx.x >> 6;
+  L.ln = threadIdx.x & 63;
+  L.pw = L.ln / R;
+  L.a = L.ln - L.pw * R;
+  L.base = L.pw * R;
+  const int local = L.w * PPW + L.pw;
+  L.valid = (L.pw < PPW) && (local < d.tile_np[L.tile]);
+  L.pose = d.tile_p0[L.tile] + (L.valid ? local : 0);
+  if (L.base + R > 64) L.base = 64 - R;  // idle tail lanes shuffle within range
+  return L;
+}
+
+__device__ __forceinline__ void write_partials(const Dev& d, int tile, const double* vals, int n, double* lds) {
+  for (int s = 0; s < n; ++s) {
+    const double t = block_sum(vals[s], lds);
+    if (threadIdx.x == 0) d.part[(size_t)tile * NPART + s] = t;
+  }
+}
+
+// ---------------------------------------------------------------- kernels --
+// Start of an RTR iteration: egrad (gather X with public neighbours), cost,
+// S = sym(Y^T egrad_Y), g = P_Y(egrad), r = g, z = precon(g).
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_grad(Dev d) {
+  __shared__ double lds[WAVES];
+  const Lane L = lane_map<R>(d);
+  if (d.ctl[L.l].phase != PH_START) return;
+  double y[4] = {0, 0, 0, 0}, G[4] = {0, 0, 0, 0}, cost = 0.0;
+  if (L.valid) {
+    gather_row<R>(d, L.pose, L.a, d.X, d.pub, G, &cost);
+    load4(d.X + (size_t)L.pose * 4 * R + 4 * L.a, y);
+  }
+  double S[9], gr[4], zr[4];
+  group_symYtG<R>(y, G, L.base, S);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) gr[c] = G[c] - (y[0] * S[0 * 3 + c] + y[1] * S[1 * 3 + c] + y[2] * S[2 * 3 + c]);
+  gr[3] = G[3];
+  group_precon<R>(d, L.pose, L.valid, y, gr, L.base, zr);
+  double vals[3] = {0.0, 0.0, 0.0};
+  if (L.valid) {
+    const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+    store4(d.g + o, gr);
+    store4(d.r + o, gr);
+    store4(d.z + o, zr);
+    if (L.a == 0) {
+      double* Sp = d.S + 9 * (size_t)L.pose;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Sp[i] = S[i];
+    }
+    vals[0] = cost;
+    vals[1] = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2] + gr[3] * gr[3];
+    vals[2] = zr[0] * gr[0] + zr[1] * gr[1] + zr[2] * gr[2] + zr[3] * gr[3];
+  }
+  write_partials(d, L.tile, vals, 3, lds);
+}
+
+// tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
+// linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old.
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_hess(Dev d) {
+  __shared__ double lds[WAVES];
+  const Lane L = lane_map<R>(d);
+  const Ctl& c = d.ctl[L.l];
+  if (c.phase != PH_TCG) return;
+  const bool first = (c.tcg_iter == 0);
+  const double beta = c.beta;
+  double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4] = {0, 0, 0, 0}, S[9];
+  const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+  if (L.valid) {
+    gather_row<R>(d, L.pose, L.a, d.z, nullptr, H, nullptr);
+    load4(d.z + o, zs);
+    load4(d.X + o, y);
+    const double* Sp = d.S + 9 * (size_t)L.pose;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) S[i] = Sp[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) S[i] = 0.0;
+  }
+  double hz[4];
+  group_rhess<R>(y, zs, H, S, L.base, hz);
+  double v = 0.0;
+  if (L.valid) {
+    double dl[4], hdl[4];
+    if (first) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { dl[k] = -zs[k]; hdl[k] = -hz[k]; }
+    } else {
+      double dold[4], hold[4];
+      load4(d.del + o, dold);
+      load4(d.hd + o, hold);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        dl[k] = -zs[k] + beta * dold[k];
+        hdl[k] = -hz[k] + beta * hold[k];
+      }
+    }
+    store4(d.del + o, dl);
+    store4(d.hd + o, hdl);
+    v = dl[0] * hdl[0] + dl[1] * hdl[1] + dl[2] * hdl[2] + dl[3] * hdl[3];
+  }
+  write_partials(d, L.tile, &v, 1, lds);
+}
+
+// tCG step, part 2: eta += coef delta, r += coef Hdelta; interior steps also
+// z = precon(r) and partial <r,r>, <z,r>.
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_update(Dev d) {
+  __shared__ double lds[WAVES];
+  const Lane L = lane_map<R>(d);
+  const Ctl& c = d.ctl[L.l];
+  if (c.phase != PH_TCG) return;
+  const bool first = (c.tcg_iter == 1);
+  const double coef = c.coef;
+  const bool interior = (c.mode == MODE_INTERIOR);
+  const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+  double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0};
+  if (L.valid) {
+    double dl[4], hdl[4], et[4];
+    load4(d.del + o, dl);
+    load4(d.hd + o, hdl);
+    load4(d.r + o, rr);
+    if (first) {
+      et[0] = et[1] = et[2] = et[3] = 0.0;
+    } else {
+      load4(d.eta + o, et);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      et[k] += coef * dl[k];
+      rr[k] += coef * hdl[k];
+    }
+    store4(d.eta + o, et);
+    store4(d.r + o, rr);
+    if (interior) load4(d.X + o, y);
+  }
+  if (!interior) return;  // uniform per robot
+  double zr[4];
+  group_precon<R>(d, L.pose, L.valid, y, rr, L.base, zr);
+  double vals[2] = {0.0, 0.0};
+  if (L.valid) {
+    store4(d.z + o, zr);
+    vals[0] = rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2] + rr[3] * rr[3];
+    vals[1] = zr[0] * rr[0] + zr[1] * rr[1] + zr[2] * rr[2] + zr[3] * rr[3];
+  }
+  write_partials(d, L.tile, vals, 2, lds);
+}
+
+// Trial point Xt = R_X(eta); partials: model m(eta) = 1/2 <eta, g + r> (r = g +
+// H eta by the tCG recurrence) and ||Xt - X||^2.
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
+  __shared__ double lds[WAVES];
+  const Lane L = lane_map<R>(d);
+  if (d.ctl[L.l].phase != PH_STEP) return;
+  const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+  double x[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0};
+  if (L.valid) {
+    load4(d.X + o, x);
+    load4(d.eta + o, et);
+  }
+  double xt[4];
+  group_retract<R>(x, et, L.base, xt);
+  double vals[2] = {0.0, 0.0};
+  if (L.valid) {
+    store4(d.Xt + o, xt);
+    double gg[4], rr[4];
+    load4(d.g + o, gg);
+    load4(d.r + o, rr);
+    double m = 0.0, ch = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      m += et[k] * (gg[k] + rr[k]);
+      const double dd = xt[k] - x[k];
+      ch += dd * dd;
+    }
+    vals[0] = m;
+    vals[1] = ch;
+  }
+  // partial slots 2,3 (slot 0 is reused by k_cost)
+  for (int s = 0; s < 2; ++s) {
+    const double t = block_sum(vals[s], lds);
+    if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART + 2 + s] = t;
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_cost(Dev d) {
+  __shared__ double lds[WAVES];
+  const Lane L = lane_map<R>(d);
+  if (d.ctl[L.l].phase != PH_STEP) return;
+  double acc[4], cost = 0.0;
+  if (L.valid) gather_row<R>(d, L.pose, L.a, d.Xt, d.pub, acc, &cost);
+  write_partials(d, L.tile, &cost, 1, lds);
+}
+
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_commit(Dev d) {
+  const Lane L = lane_map<R>(d);
+  if (!d.ctl[L.l].commit) return;
+  if (!L.valid) return;
+  const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+  double v[4];
+  load4(d.Xt + o, v);
+  store4(d.X + o, v);
+}
+
+// One workgroup: per-robot fixed-order reduction of the tile partials and the
+// RTR / tCG scalar logic (mirrors oracle block_update control flow).
+__global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int track_bytes, int R_) {
+  __shared__ double lds[WAVES];
+  for (int l = 0; l < d.L; ++l) {
+    Ctl& c = d.ctl[l];
+    const int ph = c.phase;
+    bool act = false;
+    if (kind == RED_GRAD) act = ph == PH_START;
+    if (kind == RED_HESS || kind == RED_UPDATE) act = ph == PH_TCG;
+    if (kind == RED_COST) act = ph == PH_STEP;
+    if (!act) continue;
+    if (kind == RED_UPDATE && c.mode == MODE_BOUNDARY) {
+      if (threadIdx.x == 0) c.phase = PH_STEP;
+      __syncthreads();
+      continue;
+    }
+    const int nsum = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
+    double tot[4] = {0.0, 0.0, 0.0, 0.0};
+    const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
+    for (int s = 0; s < nsum; ++s) {
+      double v = 0.0;
+      for (int t = t0 + (int)threadIdx.x; t < t1; t += BLOCK) v += d.part[(size_t)t * NPART + s];
+      tot[s] = block_sum(v, lds);
+    }
+    if (threadIdx.x == 0) {
+      const Params& P = d.p;
+      if (kind == RED_GRAD) {
+        const double f = tot[0], gn = sqrt(tot[1]);
+        if (c.rtr_iter == 0) { c.f_init = f; c.gn_init = gn; }
+        c.f_cur = f;
+        c.f_final = f;
+        c.commit = 0;
+        if (gn < P.gn_tol) {
+          c.phase = PH_IDLE;
+          c.tcg_stop = KMX_TCG_SKIPPED;
+          c.tcg_iter = 0;
+          c.accepted = 0;
+          c.skipped = 1;
+        } else {
+          c.phase = PH_TCG;
+          c.tcg_iter = 0;
+          c.norm_r0 = gn;
+          c.z_r = tot[2];
+          c.d_Pd = tot[2];
+          c.e_Pd = 0.0;
+          c.e_Pe = 0.0;
+          c.beta = 0.0;
+          c.tcg_stop = KMX_TCG_MAX_ITER;
+          if (c.rtr_iter == 0) {
+            d.cnt->edges_iters += (unsigned long long)d.m_robot[l];
+            d.cnt->block_updates += 1ull;
+          }
+        }
+      } else if (kind == RED_HESS) {
+        const double d_Hd = tot[0];
+        const double alpha = c.z_r / d_Hd;
+        const double e_Pe_new = c.e_Pe + 2.0 * alpha * c.e_Pd + alpha * alpha * c.d_Pd;
+        const double D2 = c.Delta * c.Delta;
+        c.tcg_iter += 1;
+        c.hessvecs += 1;
+        d.cnt->hessvecs += 1ull;
+        if (track_bytes)
+          d.cnt->hess_alg_bytes += 128.0 * (double)d.m_robot[l] + 2.0 * 8.0 * R_ * 4.0 * (double)d.n_robot[l];
+        if (d_Hd <= 0.0 || e_Pe_new >= D2) {
+          const double tau = (-c.e_Pd + sqrt(c.e_Pd * c.e_Pd + c.d_Pd * (D2 - c.e_Pe))) / c.d_Pd;
+          c.coef = tau;
+          c.mode = MODE_BOUNDARY;
+          c.tcg_stop = d_Hd <= 0.0 ? KMX_TCG_NEGATIVE_CURVATURE : KMX_TCG_EXCEEDED_TR;
+        } else {
+          c.alpha = alpha;
+          c.coef = alpha;
+          c.e_Pe = e_Pe_new;
+          c.mode = MODE_INTERIOR;
+        }
+      } else if (kind == RED_UPDATE) {
+        const double norm_r = sqrt(tot[0]);
+        const double zr_new = tot[1];
+        const double pw = pow(c.norm_r0, P.theta);
+        if (norm_r <= c.norm_r0 * fmin(pw, P.kappa)) {
+          c.tcg_stop = (P.kappa < pw) ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
+          c.phase = PH_STEP;
+        } else if (c.tcg_iter >= P.tcg_max) {
+          c.tcg_stop = KMX_TCG_MAX_ITER;
+          c.phase = PH_STEP;
+        } else {
+          const double beta = zr_new / c.z_r;
+          c.e_Pd = beta * (c.e_Pd + c.alpha * c.d_Pd);
+          c.d_Pd = zr_new + beta * beta * c.d_Pd;
+          c.z_r = zr_new;
+          c.beta = beta;
+        }
+      } else {  // RED_COST: tot[0] = f(Xt), tot[2] = 2 m(eta), tot[3] = ||Xt-X||^2
+        const double ft = tot[0];
+        const double model_dec = -0.5 * tot[2];
+        const double rho = (model_dec > 0.0) ? (c.f_cur - ft) / model_dec : -1.0;
+        const bool boundary = (c.tcg_stop == KMX_TCG_NEGATIVE_CURVATURE || c.tcg_stop == KMX_TCG_EXCEEDED_TR);
+        if (!(rho >= 0.25)) c.Delta *= 0.25;
+        else if (rho > 0.75 && boundary) c.Delta = fmin(2.0 * c.Delta, P.Delta_max);
+        c.rho = rho;
+        if (rho > P.accept_rho) {
+          c.accepted = 1;
+          c.commit = 1;
+          c.f_final = ft;
+          c.chg_acc += tot[3];
+        } else {
+          c.accepted = 0;
+          c.commit = 0;
+          c.f_final = c.f_cur;
+        }
+        c.rtr_iter += 1;
+        c.phase = (c.rtr_iter < P.rtr_iters) ? PH_START : PH_IDLE;
+        c.rel_change = sqrt(c.chg_acc / (double)d.n_robot[l]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_round_begin(Dev d, const unsigned char* active) {
+  const int l = threadIdx.x;
+  if (l >= d.L) return;
+  Ctl& c = d.ctl[l];
+  const bool a = active ? active[l] != 0 : true;
+  const Ctl zero = {};
+  c = zero;
+  c.phase = a ? PH_START : PH_IDLE;
+  c.updated = a ? 1 : 0;
+  c.Delta = d.p.Delta0;
+}
+
+__global__ void k_publish(const double* X, double* pub, const int* src, int nslots, int ps) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long s = i / ps;
+  if (s >= nslots) return;
+  const int q = (int)(i - s * ps);
+  const int p = src[s];
+  if (p >= 0) pub[s * ps + q] = X[(long long)p * ps + q];
+}
+
+__global__ void k_pack(const double* X, double* out, const int* src, int first, int count, int ps) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long s = i / ps;
+  if (s >= count) return;
+  const int q = (int)(i - s * ps);
+  out[s * ps + q] = X[(long long)src[first + s] * ps + q];
+}
+
+// 4x4 diagonal blocks of Q (+ shift) per pose, Cholesky-inverted. Same
+// accumulation order and expressions as oracle build_precond.
+__global__ void k_precond(Dev d) {
+  const int pose = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pose >= d.nloc) return;
+  double A[16];
+  for (int i = 0; i < 16; ++i) A[i] = 0.0;
+  for (int k = d.inc_ptr[pose]; k < d.inc_ptr[pose + 1]; ++k) {
+    const int2 in = d.inc[k];
+    const bool tail = (in.y >> 31) & 1;
+    const int e = in.y & 0x7fffffff;
+    const double* er = d.erec + 16 * (size_t)e;
+    const double wk = er[14] * er[12], wt = er[14] * er[13];
+    const double* tt = er + 9;
+    if (tail) {
+      for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) A[i * 4 + j] += wt * tt[i] * tt[j] + (i == j ? wk : 0.0);
+        A[i * 4 + 3] += wt * tt[i];
+        A[3 * 4 + i] += wt * tt[i];
+      }
+      A[15] += wt;
+    } else {
+      A[0] += wk; A[5] += wk; A[10] += wk; A[15] += wt;
+    }
+  }
+  for (int j = 0; j < 4; ++j) A[j * 5] += d.p.shift;
+  double Lm[16], Li[16];
+  for (int i = 0; i < 16; ++i) { Lm[i] = 0.0; Li[i] = 0.0; }
+  for (int j = 0; j < 4; ++j) {
+    double s = A[j * 4 + j];
+    for (int k = 0; k < j; ++k) s -= Lm[j * 4 + k] * Lm[j * 4 + k];
+    Lm[j * 4 + j] = sqrt(s);
+    for (int ii = j + 1; ii < 4; ++ii) {
+      double t = A[ii * 4 + j];
+      for (int k = 0; k < j; ++k) t -= Lm[ii * 4 + k] * Lm[j * 4 + k];
+      Lm[ii * 4 + j] = t / Lm[j * 4 + j];
+    }
+  }
+  for (int c = 0; c < 4; ++c)
+    for (int ii = 0; ii < 4; ++ii) {
+      double s = (ii == c) ? 1.0 : 0.0;
+      for (int k = c; k < ii; ++k) s -= Lm[ii * 4 + k] * Li[k * 4 + c];
+      Li[ii * 4 + c] = (ii < c) ? 0.0 : s / Lm[ii * 4 + ii];
+    }
+  double* Pi = d.Pinv + 16 * (size_t)pose;
+  for (int x = 0; x < 4; ++x)
+    for (int y = 0; y < 4; ++y) {
+      double s = 0.0;
+      for (int k = 0; k < 4; ++k) s += Li[k * 4 + x] * Li[k * 4 + y];
+      Pi[x * 4 + y] = s;
+    }
+}
+
+// GNC-TLS weight sweep over owned non-fixed local edges (owner's view of the
+// endpoints: its own robot from X, the other robot from the public table).
+__global__ void k_gnc(double* erec, const int* gnc_edge, const int2* gnc_ends, int n, const double* X,
+                      const double* pub, int R_, double mu, double barc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int e = gnc_edge[i];
+  const int2 en = gnc_ends[i];
+  const int ps = 4 * R_;
+  const double* Xi = en.x >= 0 ? X + (size_t)en.x * ps : pub + (size_t)(-1 - en.x) * ps;
+  const double* Xj = en.y >= 0 ? X + (size_t)en.y * ps : pub + (size_t)(-1 - en.y) * ps;
+  double* er = erec + 16 * (size_t)e;
+  const double* Rt = er;
+  const double* tt = er + 9;
+  double sR = 0.0, sT = 0.0;
+  for (int a = 0; a < R_; ++a) {
+    const double* yi = Xi + 4 * a;
+    const double* yj = Xj + 4 * a;
+    for (int c = 0; c < 3; ++c) {
+      const double q = yj[c] - (yi[0] * Rt[0 * 3 + c] + yi[1] * Rt[1 * 3 + c] + yi[2] * Rt[2 * 3 + c]);
+      sR += q * q;
+    }
+    const double et = yj[3] - yi[3] - (yi[0] * tt[0] + yi[1] * tt[1] + yi[2] * tt[2]);
+    sT += et * et;
+  }
+  const double rSq = er[12] * sR + er[13] * sT;
+  const double barcSq = barc * barc;
+  const double upper = (mu + 1.0) / mu * barcSq;
+  const double lower = mu / (mu + 1.0) * barcSq;
+  double w;
+  if (rSq >= upper) w = 0.0;
+  else if (rSq <= lower) w = 1.0;
+  else w = sqrt(barcSq * mu * (mu + 1.0) / rSq) - mu;
+  er[14] = w;
+}
+
+__global__ void k_shared_pack(const double* erec, const int* sh_edge, const int* sh_idx, int n, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[sh_idx[i]] = erec[16 * (size_t)sh_edge[i] + 14];
+}
+__global__ void k_shared_unpack(double* erec, const int* sh_edge, const int* sh_idx, int n, const double* tab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  erec[16 * (size_t)sh_edge[i] + 14] = tab[sh_idx[i]];
+}
+
+// --- rounding to SE(3) in the anchor frame (same algorithm as the oracle) --
+__device__ void jacobi3(double A[9], double V[9]) {
+  for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    for (int p = 0; p < 2; ++p)
+      for (int q = p + 1; q < 3; ++q) {
+        const double apq = A[p * 3 + q];
+        if (apq == 0.0) continue;
+        const double app = A[p * 3 + p], aqq = A[q * 3 + q];
+        const double theta = (aqq - app) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
+        for (int k = 0; k < 3; ++k) {
+          const double akp = A[k * 3 + p], akq = A[k * 3 + q];
+          A[k * 3 + p] = cs * akp - sn * akq;
+          A[k * 3 + q] = sn * akp + cs * akq;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double apk = A[p * 3 + k], aqk = A[q * 3 + k];
+          A[p * 3 + k] = cs * apk - sn * aqk;
+          A[q * 3 + k] = sn * apk + cs * aqk;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double vkp = V[k * 3 + p], vkq = V[k * 3 + q];
+          V[k * 3 + p] = cs * vkp - sn * vkq;
+          V[k * 3 + q] = sn * vkp + cs * vkq;
+        }
+      }
+  }
+}
+
+__global__ void k_traj(const double* X, int n, int R_, const double* anchor, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* Xi = X + (size_t)i * 4 * R_;
+  double M[9], tv[3];
+  for (int x = 0; x < 3; ++x) {
+    for (int y = 0; y < 3; ++y) {
+      double s = 0.0;
+      for (int k = 0; k < R_; ++k) s += anchor[4 * k + x] * Xi[4 * k + y];
+      M[x * 3 + y] = s;
+    }
+    double s = 0.0;
+    for (int k = 0; k < R_; ++k) s += anchor[4 * k + x] * (Xi[4 * k + 3] - anchor[4 * k + 3]);
+    tv[x] = s;
+  }
+  double A[9], V[9];
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) {
+      double s = 0.0;
+      for (int k = 0; k < 3; ++k) s += M[k * 3 + a] * M[k * 3 + b];
+      A[a * 3 + b] = s;
+    }
+  jacobi3(A, V);
+  const double det = M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) +
+                     M[2] * (M[3] * M[7] - M[4] * M[6]);
+  int kmin = 0;
+  for (int k = 1; k < 3; ++k)
+    if (A[k * 4] < A[kmin * 4]) kmin = k;
+  double Rr[9];
+  for (int q = 0; q < 9; ++q) Rr[q] = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    const double sig = sqrt(fmax(A[k * 4], 0.0));
+    double u[3];
+    for (int q = 0; q < 3; ++q) u[q] = (M[q * 3 + 0] * V[0 * 3 + k] + M[q * 3 + 1] * V[1 * 3 + k] + M[q * 3 + 2] * V[2 * 3 + k]) / sig;
+    const double s = (k == kmin && det < 0.0) ? -1.0 : 1.0;
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) Rr[a * 3 + b] += s * u[a] * V[b * 3 + k];
+  }
+  double* o = out + (size_t)i * 12;
+  for (int q = 0; q < 9; ++q) o[q] = Rr[q];
+  o[9] = tv[0]; o[10] = tv[1]; o[11] = tv[2];
+}
+
+// Primitive evaluation for parity tests, one robot (tiles t0..t1 via grid).
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_eval(Dev d, int robot, int mode, const double* V, double* out) {
+  __shared__ double lds[WAVES];
+  const Lane L = lane_map<R>(d);
+  if (L.l != robot) return;
+  const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+  double res[4] = {0, 0, 0, 0}, cost = 0.0, v[4] = {0, 0, 0, 0};
+  if (mode == KMX_EVAL_COST_EGRAD) {
+    if (L.valid) gather_row<R>(d, L.pose, L.a, V, d.pub, res, &cost);
+  } else if (mode == KMX_EVAL_EHESS) {
+    if (L.valid) {
+      gather_row<R>(d, L.pose, L.a, V, nullptr, res, nullptr);
+      load4(V + o, v);
+    }
+  } else {
+    double y[4] = {0, 0, 0, 0}, G[4] = {0, 0, 0, 0};
+    if (L.valid) {
+      gather_row<R>(d, L.pose, L.a, d.X, d.pub, G, nullptr);
+      load4(d.X + o, y);
+      load4(V + o, v);
+    }
+    double S[9];
+    group_symYtG<R>(y, G, L.base, S);
+    if (mode == KMX_EVAL_RGRAD) {
+      for (int c = 0; c < 3; ++c) res[c] = G[c] - (y[0] * S[0 * 3 + c] + y[1] * S[1 * 3 + c] + y[2] * S[2 * 3 + c]);
+      res[3] = G[3];
+      for (int k = 0; k < 4; ++k) v[k] = res[k];
+    } else if (mode == KMX_EVAL_RHESS) {
+      double H[4] = {0, 0, 0, 0};
+      if (L.valid) gather_row<R>(d, L.pose, L.a, V, nullptr, H, nullptr);
+      group_rhess<R>(y, v, H, S, L.base, res);
+    } else if (mode == KMX_EVAL_PRECON) {
+      group_precon<R>(d, L.pose, L.valid, y, v, L.base, res);
+    } else if (mode == KMX_EVAL_RETRACT) {
+      group_retract<R>(y, v, L.base, res);
+      for (int k = 0; k < 4; ++k) v[k] = 0.0;
+    }
+  }
+  double s = 0.0;
+  if (L.valid) {
+    store4(out + o, res);
+    s = (mode == KMX_EVAL_COST_EGRAD) ? cost : v[0] * res[0] + v[1] * res[1] + v[2] * res[2] + v[3] * res[3];
+  }
+  write_partials(d, L.tile, &s, 1, lds);
+}
+
+}  // namespace
+
+// ============================================================== handle ====
+struct kmx_pgo {
+  kmx_pgo_params P{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  bool have_graph = false;
+  // team
+  int n_robots = 0;
+  std::vector<int> npose;
+  std::vector<int> local_of;  // robot -> local index or -1
+  std::vector<int> robots;    // local index -> robot
+  std::vector<int> loff;      // local robot -> first local pose
+  int nloc = 0;
+  int64_t m_global = 0;
+  // public table
+  int64_t npub = 0, first_owned = 0, n_owned = 0;
+  std::vector<int64_t> pub_key;  // sorted (robot<<32 | pose)
+  // local edges
+  int mloc = 0;
+  std::vector<int64_t> loc_edge_gid;
+  std::vector<double> erec_h;
+  int64_t nshared = 0;
+  int n_sh_local = 0, n_gnc = 0;
+  std::vector<long long> m_robot;
+  int ntiles = 0, tile_poses = 0;
+  double mu = 0.0;
+  long long round_counter = 0;
+  // device
+  Dev dv{};
+  int *d_tile_robot = nullptr, *d_tile_p0 = nullptr, *d_tile_np = nullptr, *d_rtile0 = nullptr;
+  int* d_inc_ptr = nullptr;
+  int2* d_inc = nullptr;
+  double* d_erec = nullptr;
+  double* d_vec = nullptr;  // X Xt g r z eta del hd
+  double *d_S = nullptr, *d_Pinv = nullptr, *d_pub = nullptr, *d_part = nullptr;
+  Ctl* d_ctl = nullptr;
+  Counters* d_cnt = nullptr;
+  long long* d_m_robot = nullptr;
+  int* d_n_robot = nullptr;
+  int* d_pub_src = nullptr;  // slot -> local pose (-1 if not local)
+  int* d_own_src = nullptr;  // owned slot k -> local pose (index first_owned + k)
+  int* d_gnc_edge = nullptr;
+  int2* d_gnc_ends = nullptr;
+  int *d_sh_edge = nullptr, *d_sh_idx = nullptr;
+  int *d_osh_edge = nullptr, *d_osh_idx = nullptr;
+  int n_osh = 0;
+  unsigned char* d_active = nullptr;
+  double* d_scratch = nullptr;  // eval in/out
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * count);
+  if (e != hipSuccess) return kmx::fail(KMX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return 0;
+}
+
+void free_dev(kmx_pgo* h) {
+  void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_inc,
+                  h->d_erec, h->d_vec, h->d_S, h->d_Pinv, h->d_pub, h->d_part, h->d_ctl, h->d_cnt,
+                  h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src, h->d_gnc_edge, h->d_gnc_ends,
+                  h->d_sh_edge, h->d_sh_idx, h->d_osh_edge, h->d_osh_idx, h->d_active, h->d_scratch};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
+  h->d_inc = nullptr; h->d_erec = h->d_vec = h->d_S = h->d_Pinv = h->d_pub = h->d_part = nullptr;
+  h->d_ctl = nullptr; h->d_cnt = nullptr; h->d_m_robot = nullptr; h->d_n_robot = nullptr;
+  h->d_pub_src = h->d_own_src = h->d_gnc_edge = nullptr; h->d_gnc_ends = nullptr;
+  h->d_sh_edge = h->d_sh_idx = nullptr; h->d_osh_edge = h->d_osh_idx = nullptr; h->d_active = nullptr; h->d_scratch = nullptr;
+}
+
+template <int R>
+void launch_tiles(kmx_pgo* h, void (*kern)(Dev)) {
+  hipLaunchKernelGGL(kern, dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv);
+}
+
+#define KMX_DISPATCH_R(R_, CALL) \
+  switch (R_) {                  \
+    case 3: { constexpr int RR = 3; CALL; } break; \
+    case 4: { constexpr int RR = 4; CALL; } break; \
+    case 5: { constexpr int RR = 5; CALL; } break; \
+    case 6: { constexpr int RR = 6; CALL; } break; \
+    case 7: { constexpr int RR = 7; CALL; } break; \
+    case 8: { constexpr int RR = 8; CALL; } break; \
+    default: break;              \
+  }
+
+void reduce(kmx_pgo* h, int kind, int track) {
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BLOCK), 0, h->stream, h->dv, kind, track, h->P.r);
+}
+
+hipEvent_t next_event(kmx_pgo* h) {
+  if (h->ev_used == h->ev_pool.size()) {
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    h->ev_pool.push_back(e);
+  }
+  return h->ev_pool[h->ev_used++];
+}
+
+void enqueue_publish(kmx_pgo* h) {
+  const int ps = 4 * h->P.r;
+  const long long tot = h->npub * ps;
+  if (tot == 0) return;
+  hipLaunchKernelGGL(k_publish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
+                     h->d_pub, h->d_pub_src, (int)h->npub, ps);
+}
+
+void enqueue_precond(kmx_pgo* h) {
+  if (h->nloc == 0) return;
+  hipLaunchKernelGGL(k_precond, dim3((h->nloc + 127) / 128), dim3(128), 0, h->stream, h->dv);
+}
+
+void enqueue_gnc(kmx_pgo* h) {
+  if (h->n_gnc > 0)
+    hipLaunchKernelGGL(k_gnc, dim3((h->n_gnc + 255) / 256), dim3(256), 0, h->stream, h->d_erec,
+                       h->d_gnc_edge, h->d_gnc_ends, h->n_gnc, (const double*)h->d_vec,
+                       (const double*)h->d_pub, h->P.r, h->mu, h->P.gnc_barc);
+  h->mu *= h->P.gnc_mu_step;
+  enqueue_precond(h);
+}
+
+// One RBCD round for the robots whose d_active flag is set.
+void enqueue_round(kmx_pgo* h, const unsigned char* d_active) {
+  const int R_ = h->P.r;
+  hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(std::max(64, ((h->dv.L + 63) / 64) * 64)), 0, h->stream,
+                     h->dv, d_active);
+  for (int it = 0; it < h->P.rtr_iterations; ++it) {
+    KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_grad<RR>));
+    reduce(h, RED_GRAD, 0);
+    for (int j = 0; j < h->P.tcg_max_iterations; ++j) {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (h->timing) {
+        e0 = next_event(h);
+        e1 = next_event(h);
+        (void)hipEventRecord(e0, h->stream);
+      }
+      KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_hess<RR>));
+      if (h->timing) (void)hipEventRecord(e1, h->stream);
+      reduce(h, RED_HESS, h->timing ? 1 : 0);
+      KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_update<RR>));
+      reduce(h, RED_UPDATE, 0);
+    }
+    KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_retract<RR>));
+    KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_cost<RR>));
+    reduce(h, RED_COST, 0);
+    KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_commit<RR>));
+  }
+}
+
+bool ready(kmx_pgo* h) { return h && h->d_vec != nullptr; }
+
+}  // namespace
+
+// ================================================================ ABI =====
+extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo** out) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(params && out, KMX_EINVAL, "null argument");
+  KMX_CHECK(params->d == 3, KMX_EUNSUP, "only d = 3 is supported");
+  KMX_CHECK(params->r >= 3 && params->r <= 8, KMX_EUNSUP, "relaxation rank must be in [3, 8]");
+  KMX_CHECK(params->rtr_iterations >= 1 && params->tcg_max_iterations >= 1, KMX_EINVAL,
+            "rtr_iterations and tcg_max_iterations must be >= 1");
+  int ndev = 0;
+  KMX_HIP(hipGetDeviceCount(&ndev));
+  KMX_CHECK(device >= 0 && device < ndev, KMX_EINVAL, "bad HIP device ordinal");
+  KMX_HIP(hipSetDevice(device));
+  kmx_pgo* h = new kmx_pgo();
+  h->P = *params;
+  h->device = device;
+  h->mu = params->gnc_mu_init;
+  hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete h;
+    return kmx::fail(KMX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  h->own_stream = true;
+  *out = h;
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_destroy(kmx_pgo* h) {
+  if (!h) return KMX_OK;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  free_dev(h);
+  for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_set_stream(kmx_pgo* h, void* s) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_HIP(hipSetDevice(h->device));
+  if (h->own_stream && h->stream) {
+    KMX_HIP(hipStreamSynchronize(h->stream));
+    KMX_HIP(hipStreamDestroy(h->stream));
+  }
+  h->own_stream = false;
+  h->stream = reinterpret_cast<hipStream_t>(s);
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_poses, const uint8_t* local,
+                                 int64_t m, const int32_t* r1, const int32_t* p1, const int32_t* r2,
+                                 const int32_t* p2, const double* R, const double* t, const double* kappa,
+                                 const double* tau, const double* weight, const uint8_t* fixed_weight) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_CHECK(n_robots > 0 && n_poses && local, KMX_EINVAL, "bad robot arrays");
+  KMX_CHECK(m >= 0 && m < (1ll << 31) - 1, KMX_EINVAL, "edge count out of range");
+  KMX_CHECK(m == 0 || (r1 && p1 && r2 && p2 && R && t && kappa && tau && weight && fixed_weight), KMX_EINVAL,
+            "null edge array");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  free_dev(h);
+  const int r = h->P.r, ps = 4 * r;
+  h->n_robots = n_robots;
+  h->npose.assign(n_poses, n_poses + n_robots);
+  h->local_of.assign(n_robots, -1);
+  h->robots.clear();
+  h->loff.clear();
+  int nloc = 0;
+  for (int a = 0; a < n_robots; ++a) {
+    KMX_CHECK(n_poses[a] >= 0, KMX_EINVAL, "negative pose count");
+    if (local[a]) {
+      h->local_of[a] = (int)h->robots.size();
+      h->robots.push_back(a);
+      h->loff.push_back(nloc);
+      nloc += n_poses[a];
+    }
+  }
+  h->nloc = nloc;
+  const int L = (int)h->robots.size();
+  KMX_CHECK(L > 0, KMX_EINVAL, "no local robot");
+  KMX_CHECK(L <= 1024, KMX_EUNSUP, "at most 1024 local robots per handle");
+  h->m_global = m;
+  // validate + public table (team-wide, so every handle agrees on slot ids)
+  std::vector<int64_t> keys;
+  for (int64_t e = 0; e < m; ++e) {
+    KMX_CHECK(r1[e] >= 0 && r1[e] < n_robots && r2[e] >= 0 && r2[e] < n_robots, KMX_EINVAL,
+              "edge robot id out of range");
+    KMX_CHECK(p1[e] >= 0 && p1[e] < n_poses[r1[e]] && p2[e] >= 0 && p2[e] < n_poses[r2[e]], KMX_EINVAL,
+              "edge pose id out of range");
+    KMX_CHECK(!(r1[e] == r2[e] && p1[e] == p2[e]), KMX_EINVAL, "self-loop edge");
+    if (r1[e] != r2[e]) {
+      keys.push_back(((int64_t)r1[e] << 32) | (uint32_t)p1[e]);
+      keys.push_back(((int64_t)r2[e] << 32) | (uint32_t)p2[e]);
+    }
+  }
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  h->pub_key = keys;
+  h->npub = (int64_t)keys.size();
+  auto slot_of = [&](int rb, int pp) -> int64_t {
+    const int64_t k = ((int64_t)rb << 32) | (uint32_t)pp;
+    auto it = std::lower_bound(h->pub_key.begin(), h->pub_key.end(), k);
+    return (it != h->pub_key.end() && *it == k) ? (int64_t)(it - h->pub_key.begin()) : -1;
+  };
+  std::vector<int> pub_src(std::max<int64_t>(h->npub, 1), -1);
+  int64_t first = -1, last = -1;
+  for (int64_t s = 0; s < h->npub; ++s) {
+    const int rb = (int)(keys[s] >> 32), pp = (int)(keys[s] & 0xffffffff);
+    if (h->local_of[rb] >= 0) {
+      pub_src[s] = h->loff[h->local_of[rb]] + pp;
+      if (first < 0) first = s;
+      KMX_CHECK(last < 0 || last == s - 1, KMX_EUNSUP,
+                "local robots must own a contiguous range of the public table (assign robot ranges to ranks)");
+      last = s;
+    }
+  }
+  h->first_owned = first < 0 ? 0 : first;
+  h->n_owned = first < 0 ? 0 : last - first + 1;
+  // local edges, incidences
+  auto lpose = [&](int rb, int pp) { return h->loff[h->local_of[rb]] + pp; };
+  std::vector<int64_t> ledges;
+  for (int64_t e = 0; e < m; ++e)
+    if (h->local_of[r1[e]] >= 0 || h->local_of[r2[e]] >= 0) ledges.push_back(e);
+  h->mloc = (int)ledges.size();
+  h->loc_edge_gid = ledges;
+  h->erec_h.assign((size_t)h->mloc * 16, 0.0);
+  std::vector<int> deg(nloc + 1, 0);
+  h->m_robot.assign(L, 0);
+  std::vector<int> shared_index_of_gid;  // computed lazily below
+  for (int k = 0; k < h->mloc; ++k) {
+    const int64_t e = ledges[k];
+    double* rec = &h->erec_h[(size_t)k * 16];
+    for (int q = 0; q < 9; ++q) rec[q] = R[9 * e + q];
+    for (int q = 0; q < 3; ++q) rec[9 + q] = t[3 * e + q];
+    rec[12] = kappa[e];
+    rec[13] = tau[e];
+    rec[14] = weight[e];
+    const int a1 = h->local_of[r1[e]], a2 = h->local_of[r2[e]];
+    if (a1 >= 0) { deg[lpose(r1[e], p1[e])]++; h->m_robot[a1]++; }
+    if (a2 >= 0) { deg[lpose(r2[e], p2[e])]++; if (r2[e] != r1[e]) h->m_robot[a2]++; }
+  }
+  std::vector<int> inc_ptr(nloc + 1, 0);
+  for (int i = 0; i < nloc; ++i) inc_ptr[i + 1] = inc_ptr[i] + deg[i];
+  std::vector<int2> inc(std::max(inc_ptr[nloc], 1));
+  std::vector<int> fill(inc_ptr.begin(), inc_ptr.end() - 1);
+  for (int k = 0; k < h->mloc; ++k) {  // increasing global edge id per pose
+    const int64_t e = ledges[k];
+    const bool priv = r1[e] == r2[e];
+    if (h->local_of[r1[e]] >= 0) {
+      const int sp = lpose(r1[e], p1[e]);
+      const int other = priv ? lpose(r2[e], p2[e]) : (int)(-1 - slot_of(r2[e], p2[e]));
+      inc[fill[sp]++] = make_int2(other, (int)(k | 0x80000000u));
+    }
+    if (h->local_of[r2[e]] >= 0) {
+      const int sp = lpose(r2[e], p2[e]);
+      const int other = priv ? lpose(r1[e], p1[e]) : (int)(-1 - slot_of(r1[e], p1[e]));
+      inc[fill[sp]++] = make_int2(other, k);
+    }
+  }
+  // GNC ownership (owner = lower robot id, drawio:2198) and shared-weight table
+  std::vector<int> gnc_edge, sh_edge, sh_idx, osh_edge, osh_idx;
+  std::vector<int2> gnc_ends;
+  int64_t nsh = 0;
+  {
+    size_t k = 0;
+    for (int64_t e = 0; e < m; ++e) {
+      if (r1[e] == r2[e]) continue;
+      const int64_t si = nsh++;
+      while (k < ledges.size() && ledges[k] < e) ++k;
+      if (k < ledges.size() && ledges[k] == e) {
+        sh_edge.push_back((int)k);
+        sh_idx.push_back((int)si);
+        if (h->local_of[std::min(r1[e], r2[e])] >= 0) {
+          osh_edge.push_back((int)k);
+          osh_idx.push_back((int)si);
+        }
+      }
+    }
+  }
+  h->nshared = nsh;
+  for (int k = 0; k < h->mloc; ++k) {
+    const int64_t e = ledges[k];
+    if (fixed_weight[e]) continue;
+    const int owner = std::min(r1[e], r2[e]);
+    if (h->local_of[owner] < 0) continue;
+    auto enc = [&](int rb, int pp) -> int {
+      if (rb == owner) return lpose(rb, pp);
+      return (int)(-1 - slot_of(rb, pp));
+    };
+    gnc_edge.push_back(k);
+    gnc_ends.push_back(make_int2(enc(r1[e], p1[e]), enc(r2[e], p2[e])));
+  }
+  h->n_gnc = (int)gnc_edge.size();
+  h->n_sh_local = (int)sh_edge.size();
+  h->n_osh = (int)osh_edge.size();
+  // tiles
+  const int PPW = 64 / r;
+  h->tile_poses = WAVES * PPW;
+  std::vector<int> tr, tp0, tnp, rt0(L + 1, 0);
+  for (int l = 0; l < L; ++l) {
+    const int n = n_poses[h->robots[l]];
+    rt0[l] = (int)tr.size();
+    for (int p0 = 0; p0 < n; p0 += h->tile_poses) {
+      tr.push_back(l);
+      tp0.push_back(h->loff[l] + p0);
+      tnp.push_back(std::min(h->tile_poses, n - p0));
+    }
+  }
+  rt0[L] = (int)tr.size();
+  h->ntiles = (int)tr.size();
+  std::vector<int> own_src(std::max<int64_t>(h->n_owned, 1), 0);
+  for (int64_t k = 0; k < h->n_owned; ++k) own_src[k] = pub_src[h->first_owned + k];
+  std::vector<int> nrob(L);
+  for (int l = 0; l < L; ++l) nrob[l] = n_poses[h->robots[l]];
+  // device
+  int rc;
+  const size_t vec = (size_t)std::max(nloc, 1) * ps;
+  if ((rc = dalloc(&h->d_tile_robot, h->ntiles)) || (rc = dalloc(&h->d_tile_p0, h->ntiles)) ||
+      (rc = dalloc(&h->d_tile_np, h->ntiles)) || (rc = dalloc(&h->d_rtile0, L + 1)) ||
+      (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_inc, inc.size())) ||
+      (rc = dalloc(&h->d_erec, (size_t)std::max(h->mloc, 1) * 16)) || (rc = dalloc(&h->d_vec, vec * 8)) ||
+      (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 9)) ||
+      (rc = dalloc(&h->d_Pinv, (size_t)std::max(nloc, 1) * 16)) ||
+      (rc = dalloc(&h->d_pub, (size_t)std::max<int64_t>(h->npub, 1) * ps)) ||
+      (rc = dalloc(&h->d_part, (size_t)std::max(h->ntiles, 1) * NPART)) || (rc = dalloc(&h->d_ctl, L)) ||
+      (rc = dalloc(&h->d_cnt, 1)) || (rc = dalloc(&h->d_m_robot, L)) || (rc = dalloc(&h->d_n_robot, L)) ||
+      (rc = dalloc(&h->d_pub_src, pub_src.size())) || (rc = dalloc(&h->d_own_src, own_src.size())) ||
+      (rc = dalloc(&h->d_gnc_edge, std::max(h->n_gnc, 1))) ||
+      (rc = dalloc(&h->d_gnc_ends, std::max(h->n_gnc, 1))) ||
+      (rc = dalloc(&h->d_sh_edge, std::max(h->n_sh_local, 1))) ||
+      (rc = dalloc(&h->d_sh_idx, std::max(h->n_sh_local, 1))) || (rc = dalloc(&h->d_active, L)) ||
+      (rc = dalloc(&h->d_osh_edge, std::max(h->n_osh, 1))) || (rc = dalloc(&h->d_osh_idx, std::max(h->n_osh, 1))) ||
+      (rc = dalloc(&h->d_scratch, vec * 2))) {
+    free_dev(h);
+    return rc;
+  }
+  auto up = [&](void* dst, const void* src, size_t bytes) {
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream);
+  };
+  KMX_HIP(up(h->d_tile_robot, tr.data(), sizeof(int) * tr.size()));
+  KMX_HIP(up(h->d_tile_p0, tp0.data(), sizeof(int) * tp0.size()));
+  KMX_HIP(up(h->d_tile_np, tnp.data(), sizeof(int) * tnp.size()));
+  KMX_HIP(up(h->d_rtile0, rt0.data(), sizeof(int) * rt0.size()));
+  KMX_HIP(up(h->d_inc_ptr, inc_ptr.data(), sizeof(int) * inc_ptr.size()));
+  KMX_HIP(up(h->d_inc, inc.data(), sizeof(int2) * inc.size()));
+  if (h->mloc) KMX_HIP(up(h->d_erec, h->erec_h.data(), sizeof(double) * h->erec_h.size()));
+  KMX_HIP(hipMemsetAsync(h->d_vec, 0, sizeof(double) * vec * 8, h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_pub, 0, sizeof(double) * std::max<int64_t>(h->npub, 1) * ps, h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_ctl, 0, sizeof(Ctl) * L, h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_cnt, 0, sizeof(Counters), h->stream));
+  KMX_HIP(up(h->d_m_robot, h->m_robot.data(), sizeof(long long) * L));
+  KMX_HIP(up(h->d_n_robot, nrob.data(), sizeof(int) * L));
+  KMX_HIP(up(h->d_pub_src, pub_src.data(), sizeof(int) * pub_src.size()));
+  KMX_HIP(up(h->d_own_src, own_src.data(), sizeof(int) * own_src.size()));
+  if (h->n_gnc) {
+    KMX_HIP(up(h->d_gnc_edge, gnc_edge.data(), sizeof(int) * gnc_edge.size()));
+    KMX_HIP(up(h->d_gnc_ends, gnc_ends.data(), sizeof(int2) * gnc_ends.size()));
+  }
+  if (h->n_sh_local) {
+    KMX_HIP(up(h->d_sh_edge, sh_edge.data(), sizeof(int) * sh_edge.size()));
+    KMX_HIP(up(h->d_sh_idx, sh_idx.data(), sizeof(int) * sh_idx.size()));
+  }
+  if (h->n_osh) {
+    KMX_HIP(up(h->d_osh_edge, osh_edge.data(), sizeof(int) * osh_edge.size()));
+    KMX_HIP(up(h->d_osh_idx, osh_idx.data(), sizeof(int) * osh_idx.size()));
+  }
+  std::vector<unsigned char> ones(L, 1);
+  KMX_HIP(up(h->d_active, ones.data(), L));
+  // host vectors must outlive the async copies
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  Dev& d = h->dv;
+  d.ntiles = h->ntiles; d.L = L; d.nloc = nloc; d.npub = (int)h->npub;
+  d.tile_robot = h->d_tile_robot; d.tile_p0 = h->d_tile_p0; d.tile_np = h->d_tile_np; d.rtile0 = h->d_rtile0;
+  d.inc_ptr = h->d_inc_ptr; d.inc = h->d_inc; d.erec = h->d_erec;
+  d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
+  d.z = h->d_vec + 4 * vec; d.eta = h->d_vec + 5 * vec; d.del = h->d_vec + 6 * vec; d.hd = h->d_vec + 7 * vec;
+  d.S = h->d_S; d.Pinv = h->d_Pinv; d.pub = h->d_pub; d.part = h->d_part; d.ctl = h->d_ctl; d.cnt = h->d_cnt;
+  d.m_robot = h->d_m_robot; d.n_robot = h->d_n_robot;
+  d.p.tcg_max = h->P.tcg_max_iterations; d.p.rtr_iters = h->P.rtr_iterations;
+  d.p.use_precond = h->P.use_preconditioner; d.p.robust = h->P.robust_cost;
+  d.p.kappa = h->P.tcg_kappa; d.p.theta = h->P.tcg_theta; d.p.Delta0 = h->P.rtr_initial_radius;
+  d.p.Delta_max = h->P.rtr_max_radius; d.p.accept_rho = h->P.rtr_accept_rho; d.p.gn_tol = h->P.gradnorm_tol;
+  d.p.shift = h->P.precond_shift; d.p.barc = h->P.gnc_barc;
+  enqueue_precond(h);
+  KMX_HIP(hipGetLastError());
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  h->round_counter = 0;
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+static int check_robot(kmx_pgo* h, int robot) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(robot >= 0 && robot < h->n_robots && h->local_of[robot] >= 0, KMX_EINVAL, "robot is not local");
+  return 0;
+}
+
+extern "C" int kmx_pgo_set_iterate(kmx_pgo* h, int robot, const double* X) {
+  if (int rc = check_robot(h, robot)) return rc;
+  KMX_CHECK(X, KMX_EINVAL, "null X");
+  KMX_HIP(hipSetDevice(h->device));
+  const int ps = 4 * h->P.r, l = h->local_of[robot];
+  KMX_HIP(hipMemcpyAsync(h->d_vec + (size_t)h->loff[l] * ps, X, sizeof(double) * h->npose[robot] * ps,
+                         hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_get_iterate(kmx_pgo* h, int robot, double* X) {
+  if (int rc = check_robot(h, robot)) return rc;
+  KMX_CHECK(X, KMX_EINVAL, "null X");
+  KMX_HIP(hipSetDevice(h->device));
+  const int ps = 4 * h->P.r, l = h->local_of[robot];
+  KMX_HIP(hipMemcpyAsync(X, h->d_vec + (size_t)h->loff[l] * ps, sizeof(double) * h->npose[robot] * ps,
+                         hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_public_count(kmx_pgo* h, int64_t* n_public, int64_t* first_owned, int64_t* n_owned) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  if (n_public) *n_public = h->npub;
+  if (first_owned) *first_owned = h->first_owned;
+  if (n_owned) *n_owned = h->n_owned;
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_pack_public(kmx_pgo* h, void* dev_out) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(dev_out || h->n_owned == 0, KMX_EINVAL, "null device buffer");
+  KMX_HIP(hipSetDevice(h->device));
+  const int ps = 4 * h->P.r;
+  const long long tot = h->n_owned * ps;
+  if (tot)
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
+                       (double*)dev_out, h->d_own_src, 0, (int)h->n_owned, ps);
+  KMX_HIP(hipGetLastError());
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_unpack_public(kmx_pgo* h, const void* dev_table) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(dev_table || h->npub == 0, KMX_EINVAL, "null device buffer");
+  KMX_HIP(hipSetDevice(h->device));
+  if (h->npub)
+    KMX_HIP(hipMemcpyAsync(h->d_pub, dev_table, sizeof(double) * h->npub * 4 * h->P.r, hipMemcpyDeviceToDevice,
+                           h->stream));
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_refresh_local(kmx_pgo* h) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_HIP(hipSetDevice(h->device));
+  enqueue_publish(h);
+  KMX_HIP(hipGetLastError());
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_set_neighbor_poses(kmx_pgo* h, int64_t count, const int32_t* robot, const int32_t* pose,
+                                          const double* X) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(count == 0 || (robot && pose && X), KMX_EINVAL, "null argument");
+  KMX_HIP(hipSetDevice(h->device));
+  const int ps = 4 * h->P.r;
+  std::vector<double> tab((size_t)std::max<int64_t>(h->npub, 1) * ps);
+  KMX_HIP(hipMemcpyAsync(tab.data(), h->d_pub, sizeof(double) * h->npub * ps, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  for (int64_t i = 0; i < count; ++i) {
+    const int64_t k = ((int64_t)robot[i] << 32) | (uint32_t)pose[i];
+    auto it = std::lower_bound(h->pub_key.begin(), h->pub_key.end(), k);
+    KMX_CHECK(it != h->pub_key.end() && *it == k, KMX_EINVAL, "pose is not public (no shared edge)");
+    std::memcpy(&tab[(size_t)(it - h->pub_key.begin()) * ps], X + (size_t)i * ps, sizeof(double) * ps);
+  }
+  KMX_HIP(hipMemcpyAsync(h->d_pub, tab.data(), sizeof(double) * h->npub * ps, hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats* stats) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(active, KMX_EINVAL, "null active mask");
+  KMX_HIP(hipSetDevice(h->device));
+  const int L = (int)h->robots.size();
+  std::vector<unsigned char> act(L);
+  for (int l = 0; l < L; ++l) act[l] = active[h->robots[l]] ? 1 : 0;
+  KMX_HIP(hipMemcpyAsync(h->d_active, act.data(), L, hipMemcpyHostToDevice, h->stream));
+  enqueue_round(h, h->d_active);
+  KMX_HIP(hipGetLastError());
+  std::vector<Ctl> ctl(L);
+  KMX_HIP(hipMemcpyAsync(ctl.data(), h->d_ctl, sizeof(Ctl) * L, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  // restore the all-active mask used by iterate_async
+  std::vector<unsigned char> ones(L, 1);
+  KMX_HIP(hipMemcpyAsync(h->d_active, ones.data(), L, hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  if (stats) {
+    for (int a = 0; a < h->n_robots; ++a) std::memset(&stats[a], 0, sizeof(kmx_iter_stats));
+    for (int l = 0; l < L; ++l) {
+      const Ctl& c = ctl[l];
+      kmx_iter_stats& s = stats[h->robots[l]];
+      s.updated = c.updated;
+      s.tcg_iterations = c.tcg_iter;
+      s.tcg_stop = c.tcg_stop;
+      s.accepted = c.accepted;
+      s.f_init = c.f_init;
+      s.gradnorm_init = c.gn_init;
+      s.f_final = c.f_final;
+      s.rho = c.rho;
+      s.radius = c.Delta;
+      s.rel_change = c.rel_change;
+      s.edges = h->m_robot[l];
+      s.hessvecs = c.hessvecs;
+    }
+  }
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local, int gnc_every) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(rounds >= 0, KMX_EINVAL, "negative rounds");
+  KMX_HIP(hipSetDevice(h->device));
+  for (int i = 0; i < rounds; ++i) {
+    if (refresh_local) enqueue_publish(h);
+    enqueue_round(h, h->d_active);
+    h->round_counter++;
+    if (gnc_every > 0 && h->P.robust_cost == KMX_COST_GNC_TLS && h->round_counter % gnc_every == 0) {
+      if (refresh_local) enqueue_publish(h);
+      enqueue_gnc(h);
+    }
+  }
+  KMX_HIP(hipGetLastError());
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_sync(kmx_pgo* h) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_update_weights(kmx_pgo* h, double* mu_out) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_HIP(hipSetDevice(h->device));
+  if (mu_out) *mu_out = h->mu;
+  if (h->P.robust_cost != KMX_COST_GNC_TLS) return KMX_OK;
+  enqueue_gnc(h);
+  KMX_HIP(hipGetLastError());
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_get_mu(kmx_pgo* h, double* mu) {
+  KMX_CHECK(h && mu, KMX_EINVAL, "null argument");
+  *mu = h->mu;
+  return KMX_OK;
+}
+extern "C" int kmx_pgo_set_mu(kmx_pgo* h, double mu) {
+  KMX_CHECK(h && mu > 0.0, KMX_EINVAL, "mu must be positive");
+  h->mu = mu;
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_get_weights(kmx_pgo* h, double* w) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(ready(h) && w, KMX_EINVAL, "null argument / no graph");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipMemcpyAsync(h->erec_h.data(), h->d_erec, sizeof(double) * h->erec_h.size(), hipMemcpyDeviceToHost,
+                         h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  for (int k = 0; k < h->mloc; ++k) w[h->loc_edge_gid[k]] = h->erec_h[(size_t)k * 16 + 14];
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_set_weights(kmx_pgo* h, const double* w) {
+  KMX_CHECK(ready(h) && w, KMX_EINVAL, "null argument / no graph");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipMemcpyAsync(h->erec_h.data(), h->d_erec, sizeof(double) * h->erec_h.size(), hipMemcpyDeviceToHost,
+                         h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  for (int k = 0; k < h->mloc; ++k) h->erec_h[(size_t)k * 16 + 14] = w[h->loc_edge_gid[k]];
+  KMX_HIP(hipMemcpyAsync(h->d_erec, h->erec_h.data(), sizeof(double) * h->erec_h.size(), hipMemcpyHostToDevice,
+                         h->stream));
+  enqueue_precond(h);
+  KMX_HIP(hipGetLastError());
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_shared_count(kmx_pgo* h, int64_t* n_shared) {
+  KMX_CHECK(ready(h) && n_shared, KMX_EINVAL, "null argument / no graph");
+  *n_shared = h->nshared;
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_pack_shared_weights(kmx_pgo* h, void* dev_out) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(dev_out || h->nshared == 0, KMX_EINVAL, "null device buffer");
+  KMX_HIP(hipSetDevice(h->device));
+  if (h->nshared == 0) return KMX_OK;
+  KMX_HIP(hipMemsetAsync(dev_out, 0, sizeof(double) * h->nshared, h->stream));
+  if (h->n_osh)
+    hipLaunchKernelGGL(k_shared_pack, dim3((h->n_osh + 255) / 256), dim3(256), 0, h->stream,
+                       (const double*)h->d_erec, h->d_osh_edge, h->d_osh_idx, h->n_osh, (double*)dev_out);
+  KMX_HIP(hipGetLastError());
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_unpack_shared_weights(kmx_pgo* h, const void* dev_table) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(dev_table || h->nshared == 0, KMX_EINVAL, "null device buffer");
+  KMX_HIP(hipSetDevice(h->device));
+  if (h->n_sh_local)
+    hipLaunchKernelGGL(k_shared_unpack, dim3((h->n_sh_local + 255) / 256), dim3(256), 0, h->stream, h->d_erec,
+                       h->d_sh_edge, h->d_sh_idx, h->n_sh_local, (const double*)dev_table);
+  enqueue_precond(h);
+  KMX_HIP(hipGetLastError());
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_get_trajectory(kmx_pgo* h, int robot, const double* anchor, double* out) {
+  KMX_GUARD_BEGIN
+  if (int rc = check_robot(h, robot)) return rc;
+  KMX_CHECK(anchor && out, KMX_EINVAL, "null argument");
+  KMX_HIP(hipSetDevice(h->device));
+  const int ps = 4 * h->P.r, l = h->local_of[robot], n = h->npose[robot];
+  double* d_anchor = h->d_scratch;
+  double* d_out = h->d_scratch + ps;
+  KMX_CHECK((size_t)ps + (size_t)n * 12 <= (size_t)std::max(h->nloc, 1) * ps * 2, KMX_EINVAL, "scratch too small");
+  KMX_HIP(hipMemcpyAsync(d_anchor, anchor, sizeof(double) * ps, hipMemcpyHostToDevice, h->stream));
+  if (n)
+    hipLaunchKernelGGL(k_traj, dim3((n + 127) / 128), dim3(128), 0, h->stream,
+                       (const double*)(h->d_vec + (size_t)h->loff[l] * ps), n, h->P.r, (const double*)d_anchor, d_out);
+  KMX_HIP(hipGetLastError());
+  KMX_HIP(hipMemcpyAsync(out, d_out, sizeof(double) * n * 12, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, double* out, double* scalar) {
+  KMX_GUARD_BEGIN
+  if (int rc = check_robot(h, robot)) return rc;
+  KMX_CHECK(mode >= KMX_EVAL_COST_EGRAD && mode <= KMX_EVAL_RETRACT, KMX_EINVAL, "bad eval mode");
+  KMX_CHECK(out && (V || mode == KMX_EVAL_RGRAD), KMX_EINVAL, "null argument");
+  KMX_HIP(hipSetDevice(h->device));
+  const int ps = 4 * h->P.r, l = h->local_of[robot], n = h->npose[robot];
+  const size_t vec = (size_t)std::max(h->nloc, 1) * ps;
+  double* dV = h->d_scratch;
+  double* dO = h->d_scratch + vec;
+  const size_t o = (size_t)h->loff[l] * ps;
+  KMX_HIP(hipMemsetAsync(h->d_scratch, 0, sizeof(double) * vec * 2, h->stream));
+  if (V) KMX_HIP(hipMemcpyAsync(dV + o, V, sizeof(double) * n * ps, hipMemcpyHostToDevice, h->stream));
+  const int R_ = h->P.r;
+  KMX_DISPATCH_R(R_, hipLaunchKernelGGL(k_eval<RR>, dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, l, mode,
+                                        (const double*)dV, dO));
+  KMX_HIP(hipGetLastError());
+  KMX_HIP(hipMemcpyAsync(out, dO + o, sizeof(double) * n * ps, hipMemcpyDeviceToHost, h->stream));
+  std::vector<int> rt0(2);
+  std::vector<double> part((size_t)h->ntiles * NPART);
+  KMX_HIP(hipMemcpyAsync(part.data(), h->d_part, sizeof(double) * part.size(), hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  // tiles of robot l are contiguous: recompute their range on the host
+  int t0 = 0;
+  for (int q = 0; q < l; ++q) t0 += (h->npose[h->robots[q]] + h->tile_poses - 1) / h->tile_poses;
+  const int nt = (n + h->tile_poses - 1) / h->tile_poses;
+  double s = 0.0;
+  for (int tt = t0; tt < t0 + nt; ++tt) s += part[(size_t)tt * NPART];
+  if (scalar) *scalar = s;
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_local_edges(kmx_pgo* h, int robot, int64_t* m_local) {
+  if (int rc = check_robot(h, robot)) return rc;
+  KMX_CHECK(m_local, KMX_EINVAL, "null argument");
+  *m_local = h->m_robot[h->local_of[robot]];
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_enable_timing(kmx_pgo* h, int enable) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  h->timing = enable != 0;
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out) {
+  KMX_CHECK(ready(h) && out, KMX_EINVAL, "null argument / no graph");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  Counters c;
+  KMX_HIP(hipMemcpy(&c, h->d_cnt, sizeof(Counters), hipMemcpyDeviceToHost));
+  double ms_total = 0.0;
+  for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
+    float ms = 0.f;
+    KMX_HIP(hipEventElapsedTime(&ms, h->ev_pool[i], h->ev_pool[i + 1]));
+    ms_total += ms;
+  }
+  out->hessvec_ms_total = ms_total;
+  out->hessvec_launches = (int64_t)(h->ev_used / 2);
+  out->hessvec_alg_bytes = c.hess_alg_bytes;
+  out->edges_iters = (int64_t)c.edges_iters;
+  out->block_updates = (int64_t)c.block_updates;
+  out->hessvecs = (int64_t)c.hessvecs;
+  h->ev_used = 0;
+  KMX_HIP(hipMemset(h->d_cnt, 0, sizeof(Counters)));
+  return KMX_OK;
+}

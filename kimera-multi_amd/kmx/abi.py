@@ -1,0 +1,194 @@
+"""ctypes binding of include/kmx_abi.h (the drop-in C ABI).
+
+The product path has exactly one backend: the in-tree HIP library
+``kmx/libkmx.so`` built for gfx950 by ``csrc/Makefile``. There is no CPU
+fallback: if the library is missing or no HIP device is visible, the handles
+raise ``KmxError`` (the CPU restatement in ``oracle/`` is test infrastructure
+and is never reached from here).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_LIB_PATH = Path(__file__).resolve().parent / "libkmx.so"
+
+KMX_OK = 0
+KMX_COST_L2 = 0
+KMX_COST_GNC_TLS = 1
+KMX_SCHEDULE_SEQUENTIAL = 0
+KMX_SCHEDULE_CONCURRENT = 1
+KMX_EVAL_COST_EGRAD = 0
+KMX_EVAL_EHESS = 1
+KMX_EVAL_RGRAD = 2
+KMX_EVAL_RHESS = 3
+KMX_EVAL_PRECON = 4
+KMX_EVAL_RETRACT = 5
+KMX_NORM_L1 = 0
+KMX_NORM_HAMMING = 1
+KMX_RNG_GCC9 = 0
+KMX_RNG_GCC11 = 1
+
+TCG_STOP_NAMES = {0: "none", 1: "negative_curvature", 2: "exceeded_trust_region",
+                  3: "linear", 4: "superlinear", 5: "max_iterations", 6: "skipped"}
+
+
+class KmxError(RuntimeError):
+    pass
+
+
+class PgoParams(C.Structure):
+    _fields_ = [
+        ("d", C.c_int), ("r", C.c_int), ("rtr_iterations", C.c_int),
+        ("tcg_max_iterations", C.c_int), ("tcg_kappa", C.c_double),
+        ("tcg_theta", C.c_double), ("rtr_initial_radius", C.c_double),
+        ("rtr_max_radius", C.c_double), ("rtr_accept_rho", C.c_double),
+        ("gradnorm_tol", C.c_double), ("use_preconditioner", C.c_int),
+        ("precond_shift", C.c_double), ("robust_cost", C.c_int),
+        ("gnc_barc", C.c_double), ("gnc_mu_init", C.c_double),
+        ("gnc_mu_step", C.c_double), ("reserved", C.c_int * 8),
+    ]
+
+
+class IterStats(C.Structure):
+    _fields_ = [
+        ("updated", C.c_int), ("tcg_iterations", C.c_int), ("tcg_stop", C.c_int),
+        ("accepted", C.c_int), ("f_init", C.c_double), ("gradnorm_init", C.c_double),
+        ("f_final", C.c_double), ("rho", C.c_double), ("radius", C.c_double),
+        ("rel_change", C.c_double), ("edges", C.c_int64), ("hessvecs", C.c_int64),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {name: getattr(self, name) for name, _ in self._fields_}
+        d["tcg_stop"] = TCG_STOP_NAMES.get(self.tcg_stop, str(self.tcg_stop))
+        return d
+
+
+class PgoCounters(C.Structure):
+    _fields_ = [
+        ("hessvec_ms_total", C.c_double), ("hessvec_launches", C.c_int64),
+        ("hessvec_alg_bytes", C.c_double), ("edges_iters", C.c_int64),
+        ("block_updates", C.c_int64), ("hessvecs", C.c_int64),
+    ]
+
+
+class LcdParams(C.Structure):
+    _fields_ = [
+        ("norm", C.c_int), ("lowe_ratio", C.c_float), ("min_2d2d_inliers", C.c_int),
+        ("min_3d3d_inliers", C.c_int), ("ransac_threshold_2d2d", C.c_double),
+        ("ransac_threshold_3d3d", C.c_double), ("ransac_max_iterations", C.c_int),
+        ("ransac_probability", C.c_double), ("ransac_randomize", C.c_int),
+        ("ransac_seed", C.c_uint32), ("rng_variant", C.c_int),
+        ("use_1point_3d3d", C.c_int), ("reserved", C.c_int * 8),
+    ]
+
+
+class LcdResult(C.Structure):
+    _fields_ = [
+        ("n_matches", C.c_int32), ("mono_inliers", C.c_int32),
+        ("stereo_inliers", C.c_int32), ("accepted", C.c_int32),
+        ("iterations_2d2d", C.c_int32), ("pad", C.c_int32),
+        ("T_query_match", C.c_double * 12),
+    ]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libkmx.so (once). Raises KmxError when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = Path(os.environ.get("KMX_LIB", _LIB_PATH))
+    if not path.exists():
+        raise KmxError(
+            f"HIP library {path} not found: build it with `make -C kimera-multi_amd/csrc` "
+            "(or __graft_entry__.build()). There is no CPU fallback.")
+    L = C.CDLL(str(path))
+    P, i32, i64, f64, u8 = C.c_void_p, C.c_int32, C.c_int64, C.c_double, C.c_uint8
+    pi32, pf64, pu8, pi64 = C.POINTER(i32), C.POINTER(f64), C.POINTER(u8), C.POINTER(i64)
+    sig = {
+        "kmx_last_error": ([], C.c_char_p),
+        "kmx_abi_version": ([], C.c_int),
+        "kmx_device_count": ([C.POINTER(C.c_int)], C.c_int),
+        "kmx_pgo_create": ([C.POINTER(PgoParams), C.c_int, C.POINTER(P)], C.c_int),
+        "kmx_pgo_destroy": ([P], C.c_int),
+        "kmx_pgo_set_stream": ([P, P], C.c_int),
+        "kmx_pgo_set_graph": ([P, C.c_int, pi32, pu8, i64, pi32, pi32, pi32, pi32,
+                               pf64, pf64, pf64, pf64, pf64, pu8], C.c_int),
+        "kmx_pgo_set_iterate": ([P, C.c_int, pf64], C.c_int),
+        "kmx_pgo_get_iterate": ([P, C.c_int, pf64], C.c_int),
+        "kmx_pgo_public_count": ([P, pi64, pi64, pi64], C.c_int),
+        "kmx_pgo_pack_public": ([P, P], C.c_int),
+        "kmx_pgo_unpack_public": ([P, P], C.c_int),
+        "kmx_pgo_refresh_local": ([P], C.c_int),
+        "kmx_pgo_set_neighbor_poses": ([P, i64, pi32, pi32, pf64], C.c_int),
+        "kmx_pgo_iterate": ([P, pu8, C.POINTER(IterStats)], C.c_int),
+        "kmx_pgo_iterate_async": ([P, C.c_int, C.c_int, C.c_int], C.c_int),
+        "kmx_pgo_sync": ([P], C.c_int),
+        "kmx_pgo_update_weights": ([P, pf64], C.c_int),
+        "kmx_pgo_get_mu": ([P, pf64], C.c_int),
+        "kmx_pgo_set_mu": ([P, f64], C.c_int),
+        "kmx_pgo_get_weights": ([P, pf64], C.c_int),
+        "kmx_pgo_set_weights": ([P, pf64], C.c_int),
+        "kmx_pgo_shared_count": ([P, pi64], C.c_int),
+        "kmx_pgo_pack_shared_weights": ([P, P], C.c_int),
+        "kmx_pgo_unpack_shared_weights": ([P, P], C.c_int),
+        "kmx_pgo_get_trajectory": ([P, C.c_int, pf64, pf64], C.c_int),
+        "kmx_pgo_eval": ([P, C.c_int, C.c_int, pf64, pf64, pf64], C.c_int),
+        "kmx_pgo_local_edges": ([P, C.c_int, pi64], C.c_int),
+        "kmx_pgo_enable_timing": ([P, C.c_int], C.c_int),
+        "kmx_pgo_read_counters": ([P, C.POINTER(PgoCounters)], C.c_int),
+    }
+    optional = {
+        "kmx_lcd_knn2": ([C.c_int, C.c_float, pu8, i32, pu8, i32, pi32, pi32], C.c_int),
+        "kmx_lcd_create": ([C.POINTER(LcdParams), C.c_int, C.POINTER(P)], C.c_int),
+        "kmx_lcd_destroy": ([P], C.c_int),
+        "kmx_lcd_set_stream": ([P, P], C.c_int),
+        "kmx_lcd_set_frames": ([P, P], C.c_int),
+        "kmx_lcd_verify": ([P, i32, pi32, pi32, C.POINTER(LcdResult), pu8], C.c_int),
+        "kmx_lcd_verify_async": ([P, i32, pi32, pi32], C.c_int),
+        "kmx_lcd_sync": ([P], C.c_int),
+    }
+    for name, (argt, rest) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = argt
+        fn.restype = rest
+    for name, (argt, rest) in optional.items():
+        if hasattr(L, name):
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = rest
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != KMX_OK:
+        msg = lib().kmx_last_error().decode(errors="replace")
+        raise KmxError(f"{what} failed ({rc}): {msg}")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().kmx_device_count(C.byref(n)), "kmx_device_count")
+    return n.value
+
+
+def fptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags.c_contiguous, (a.dtype, a.flags)
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def iptr(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def u8ptr(a: np.ndarray):
+    assert a.dtype == np.uint8 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))

@@ -1,0 +1,157 @@
+"""RBCDDriver — the dpgo_ros synchronous scheduler on MI355X.
+
+Reference control flow (drawio:1954-2066, 2071, 2466-2481):
+  * every round the executing robots run PGOAgent::iterate(doOptimization)
+    against the neighbour poses they last received (publishPublicPoses ->
+    updateNeighborPoses, drawio:2340-2355);
+  * every ``robustOptInnerIters`` rounds the leader sends UPDATE_WEIGHT and every
+    agent runs updateMeasurementWeights (drawio:2212-2215); the owner of a
+    shared loop closure (lower robot id) sends its weight to the peer
+    (publishMeasurementWeights, drawio:2195-2198);
+  * schedule: dpgo_ros lets ONE robot iterate per round (``sequential``,
+    drawio:2478-2481); the MI355X layout updates every block each round
+    (``concurrent``, SURVEY.md §0 finding 6, §8e).
+
+Placement: robot blocks are dealt to ranks in contiguous ranges (one process
+per GPU). ROS topics become collectives over RCCL/xGMI:
+  public_poses          -> one all_gather of the owned public-pose rows per round
+  measurement_weights   -> all_reduce(SUM) of the owner-packed shared weights
+  lifting_matrix/anchor -> injected at initialisation (identical on all ranks)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .params import PGOAgentParameters
+from .solver import BlockSolver
+
+
+def robot_ranges(n_robots: int, world: int) -> list[tuple[int, int]]:
+    out = []
+    for k in range(world):
+        out.append((k * n_robots // world, (k + 1) * n_robots // world))
+    return out
+
+
+class RBCDDriver:
+    def __init__(self, params: PGOAgentParameters, graph, *, rank: int = 0, world: int = 1,
+                 device: int = 0, seed: int = 0):
+        if world > graph.n_robots:
+            raise ValueError("need at least one robot block per rank")
+        self.params = params
+        self.graph = graph
+        self.rank, self.world = rank, world
+        lo, hi = robot_ranges(graph.n_robots, world)[rank]
+        self.robots = list(range(lo, hi))
+        local = np.zeros(graph.n_robots, np.uint8)
+        local[lo:hi] = 1
+        self.local = local
+        self.solver = BlockSolver(params, device)
+        self.rng = np.random.Generator(np.random.PCG64(seed))
+        self.round_index = 0
+        self.weight_updates = 0
+        self._torch = None
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            self._torch, self._dist = torch, dist
+            self.solver.set_stream(torch.cuda.current_stream().cuda_stream)
+        self.solver.set_graph_data(graph, local)
+        self.n_pub, self.first_owned, self.n_owned = self.solver.public_count()
+        self.m_local = {a: self.solver.local_edges(a) for a in self.robots}
+        if world > 1:
+            self._setup_exchange()
+
+    # ------------------------------------------------------ collectives ---
+    def _setup_exchange(self):
+        torch, dist = self._torch, self._dist
+        ps = 4 * self.params.r
+        counts = [None] * self.world
+        dist.all_gather_object(counts, (self.first_owned, self.n_owned))
+        self.max_owned = max(max(c[1] for c in counts), 1)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self._send = torch.zeros(self.max_owned * ps, dtype=torch.float64, device=dev)
+        self._recv = torch.zeros(self.world * self.max_owned * ps, dtype=torch.float64, device=dev)
+        # rows of the gathered buffer in public-table order
+        idx = np.full(max(self.n_pub, 1), 0, dtype=np.int64)
+        for k, (first, n) in enumerate(counts):
+            idx[first:first + n] = k * self.max_owned + np.arange(n)
+        self._row_index = torch.as_tensor(idx[: max(self.n_pub, 1)], device=dev)
+        self._table = torch.zeros(max(self.n_pub, 1) * ps, dtype=torch.float64, device=dev)
+        self.n_shared = self.solver.shared_count()
+        self._wshared = torch.zeros(max(self.n_shared, 1), dtype=torch.float64, device=dev)
+
+    def exchange_public(self):
+        """publishPublicPoses -> updateNeighborPoses for the whole team."""
+        if self.world == 1:
+            self.solver.refresh_local()
+            return
+        torch, dist = self._torch, self._dist
+        ps = 4 * self.params.r
+        self.solver.pack_public(self._send.data_ptr())
+        dist.all_gather_into_tensor(self._recv, self._send)
+        if self.n_pub:
+            rows = self._recv.view(-1, ps).index_select(0, self._row_index)
+            self._table.view(-1, ps).copy_(rows)
+            self.solver.unpack_public(self._table.data_ptr())
+
+    def update_weights(self) -> float:
+        """UPDATE_WEIGHT: every agent re-weights the loop closures it owns, then
+        owners send shared-edge weights to their peers."""
+        self.exchange_public()
+        mu = self.solver.update_weights()
+        if self.world > 1 and self.n_shared:
+            self.solver.pack_shared_weights(self._wshared.data_ptr())
+            self._dist.all_reduce(self._wshared)
+            self.solver.unpack_shared_weights(self._wshared.data_ptr())
+        self.weight_updates += 1
+        return mu
+
+    # ------------------------------------------------------------ rounds ---
+    def initialize(self, X_by_robot: dict):
+        for a in self.robots:
+            self.solver.set_iterate(a, X_by_robot[a])
+
+    def should_update_weights(self) -> bool:
+        """shouldUpdateMeasurementWeights (drawio:2466-2469), iteration-count form."""
+        rc = self.params.robustCostParams
+        if int(rc.costType) == 0:
+            return False
+        if self.weight_updates >= self.params.robustOptNumWeightUpdates:
+            return False
+        return self.round_index > 0 and self.round_index % self.params.robustOptInnerIters == 0
+
+    def active_mask(self) -> np.ndarray:
+        act = np.zeros(self.graph.n_robots, np.uint8)
+        if self.params.schedule == 0:  # sequential: leader picks one executing robot
+            act[self.round_index % self.graph.n_robots] = 1
+        else:
+            act[:] = 1
+        return act
+
+    def step(self, with_stats: bool = True):
+        """One synchronous round. Returns per-robot stats (team-indexed)."""
+        self.exchange_public()
+        stats = None
+        if with_stats or self.params.schedule == 0:
+            stats = self.solver.iterate(self.active_mask())
+        else:
+            self.solver.iterate_async(1, refresh_local=False, gnc_every=0)
+        self.round_index += 1
+        if self.should_update_weights():
+            self.update_weights()
+        return stats
+
+    def run_async(self, rounds: int):
+        """Benchmark path: enqueue `rounds` concurrent rounds with no host sync
+        (single GPU: one C call; multi-GPU: collectives between rounds)."""
+        if self.world == 1 and self.params.schedule == 1:
+            gnc = self.params.robustOptInnerIters if int(self.params.robustCostParams.costType) != 0 else 0
+            self.solver.iterate_async(rounds, refresh_local=True, gnc_every=gnc)
+            self.round_index += rounds
+            return
+        for _ in range(rounds):
+            self.step(with_stats=False)
+
+    def iterate_of(self, robot: int) -> np.ndarray:
+        return self.solver.get_iterate(robot)

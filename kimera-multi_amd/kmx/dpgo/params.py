@@ -1,0 +1,80 @@
+"""dpgo parameter structs (PGOAgentParameters, ROptParameters,
+RobustCostParameters) as dataclasses, convertible to the C ABI struct.
+
+Defaults follow dpgo as recalled in SURVEY.md §9.2 ([U] items: r = 5,
+GNC mu0 = 1e-5, mu step = 1.4, c-bar = 5; RTR initial radius 100; tCG kappa
+0.1 / theta 1) and SURVEY.md §8d for the benchmark (1 RTR iteration with at
+most 10 tCG steps per block update, GNC weight update every 20 rounds).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from enum import IntEnum
+
+from ..abi import KMX_COST_GNC_TLS, KMX_COST_L2, PgoParams
+
+
+class RobustCostType(IntEnum):
+    L2 = KMX_COST_L2
+    GNC_TLS = KMX_COST_GNC_TLS
+
+
+def error_threshold_at_quantile(quantile: float, dimension: int = 3) -> float:
+    """c-bar = sqrt(chi2inv(quantile, dof)) with dof = d(d+1)/2 (the SE(d)
+    residual's degrees of freedom); the dpgo_ros GNC_quantile parameter."""
+    from scipy.stats import chi2
+    dof = dimension * (dimension + 1) // 2
+    return math.sqrt(float(chi2.ppf(quantile, dof)))
+
+
+@dataclass
+class RobustCostParameters:
+    costType: RobustCostType = RobustCostType.GNC_TLS
+    GNCBarc: float = 5.0
+    GNCMuStep: float = 1.4
+    GNCInitMu: float = 1e-5
+
+
+@dataclass
+class ROptParameters:
+    RTR_iterations: int = 1
+    RTR_tCG_iterations: int = 10
+    RTR_initial_radius: float = 100.0
+    RTR_max_radius: float = 1e4
+    RTR_accept_rho: float = 0.1
+    tCG_kappa: float = 0.1
+    tCG_theta: float = 1.0
+    gradnorm_tol: float = 1e-2
+    use_preconditioner: bool = True
+    precond_shift: float = 1e-1
+
+
+@dataclass
+class PGOAgentParameters:
+    d: int = 3
+    r: int = 5
+    num_robots: int = 1
+    localOptimizationParams: ROptParameters = field(default_factory=ROptParameters)
+    robustCostParams: RobustCostParameters = field(default_factory=RobustCostParameters)
+    maxNumIters: int = 1000
+    relChangeTol: float = 1e-3
+    robustOptInnerIters: int = 20          # rounds between GNC weight updates
+    robustOptNumWeightUpdates: int = 50    # after this many updates weights freeze
+    robustOptMinConvergenceRatio: float = 0.8
+    schedule: int = 1                      # 0 sequential (dpgo_ros sync), 1 concurrent
+
+    def to_c(self) -> PgoParams:
+        lo, rc = self.localOptimizationParams, self.robustCostParams
+        p = PgoParams()
+        p.d, p.r = self.d, self.r
+        p.rtr_iterations = lo.RTR_iterations
+        p.tcg_max_iterations = lo.RTR_tCG_iterations
+        p.tcg_kappa, p.tcg_theta = lo.tCG_kappa, lo.tCG_theta
+        p.rtr_initial_radius, p.rtr_max_radius = lo.RTR_initial_radius, lo.RTR_max_radius
+        p.rtr_accept_rho, p.gradnorm_tol = lo.RTR_accept_rho, lo.gradnorm_tol
+        p.use_preconditioner = 1 if lo.use_preconditioner else 0
+        p.precond_shift = lo.precond_shift
+        p.robust_cost = int(rc.costType)
+        p.gnc_barc, p.gnc_mu_init, p.gnc_mu_step = rc.GNCBarc, rc.GNCInitMu, rc.GNCMuStep
+        return p

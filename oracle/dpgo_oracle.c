@@ -1,0 +1,676 @@
+/*
+ * oracle/dpgo_oracle.c — CPU restatement of dpgo's RBCD block update with
+ * GNC-TLS weights. TEST INFRASTRUCTURE ONLY: it is the parity checker for the
+ * HIP path and the timed CPU baseline of bench.py (cpu_baseline.kind = "port").
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it; the product path (kimera-multi_amd/kmx) never does.
+ *
+ * PARITY STATUS: the dpgo / ROPTLIB sources are not vendored in
+ * /root/reference (SURVEY.md §0 finding 1, §8c) and the reference ships no
+ * golden vectors or tests for this path. This restatement is
+ * therefore "parity unpinned" against upstream dpgo; it is pinned instead by
+ * analytic known answers (noise-free graphs converge to ground truth up to
+ * gauge; gradient/Hessian vs finite differences; an independent numpy
+ * restatement) — see tests/test_oracle_dpgo.py.
+ *
+ * What it restates (SURVEY.md §8a rows, §9.1 formulas):
+ *   D1  edge classification / storage ......... PoseGraph::addMeasurement (drawio:2779-2826)
+ *   D2/D3 cost, Euclidean gradient, Hess-vec .. QuadraticProblem inside PGOAgent::iterate (drawio:2513)
+ *         f(X) = 1/2 sum_e w_e (kappa_e ||Y_j - Y_i R_e||^2 + tau_e ||p_j - p_i - Y_i t_e||^2)
+ *         over the robot's private and shared edges; neighbour poses fixed.
+ *   D4  Stiefel projection, Riemannian Hessian (Weingarten term), QF retraction
+ *   D5  RTR outer step + preconditioned Steihaug-Toint tCG (ROPTLIB RTRNewton)
+ *   D6  GNC_TLS weights + mu schedule ......... updateMeasurementWeights (drawio:2215, 2466-2469)
+ *   D8  rounding to SE(3) in the anchor frame . getTrajectoryInGlobalFrame / publishTrajectory (drawio:2148)
+ *   D9  concurrent / sequential round ......... runOnceSynchronous (drawio:2071, 2478-2481)
+ * Edge-centric (scatter to both endpoints), deliberately unlike the GPU's
+ * node-centric gather, so the two implementations are independent.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/kmx_abi.h"
+
+#define D 3
+
+typedef struct {
+  kmx_pgo_params P;
+  int R;          /* robots */
+  int* npose;     /* [R] */
+  int64_t* poff;  /* [R+1] global pose offsets */
+  int64_t ntot;
+  int64_t m;
+  int32_t *r1, *p1, *r2, *p2;
+  double *Rm, *tv, *kappa, *tau, *w;
+  uint8_t* fixed;
+  int64_t** redges; /* per robot: edge ids touching it */
+  int64_t* nredges;
+  double* X;    /* ntot * 4r current iterate */
+  double* nbr;  /* ntot * 4r neighbour snapshot (public poses) */
+  double mu;
+} orc_pgo;
+
+static int PS(const orc_pgo* h) { return 4 * h->P.r; } /* doubles per pose */
+
+/* ---------------------------------------------------------------- setup -- */
+void* orc_pgo_create(const kmx_pgo_params* p) {
+  orc_pgo* h = (orc_pgo*)calloc(1, sizeof(orc_pgo));
+  h->P = *p;
+  h->mu = p->gnc_mu_init;
+  return h;
+}
+
+static void free_graph(orc_pgo* h) {
+  free(h->npose); free(h->poff);
+  free(h->r1); free(h->p1); free(h->r2); free(h->p2);
+  free(h->Rm); free(h->tv); free(h->kappa); free(h->tau); free(h->w); free(h->fixed);
+  if (h->redges) for (int a = 0; a < h->R; ++a) free(h->redges[a]);
+  free(h->redges); free(h->nredges); free(h->X); free(h->nbr);
+}
+
+void orc_pgo_destroy(void* vh) {
+  orc_pgo* h = (orc_pgo*)vh;
+  if (!h) return;
+  free_graph(h);
+  free(h);
+}
+
+int orc_pgo_set_graph(void* vh, int n_robots, const int32_t* n_poses, int64_t m,
+                      const int32_t* r1, const int32_t* p1, const int32_t* r2,
+                      const int32_t* p2, const double* R, const double* t,
+                      const double* kappa, const double* tau, const double* w,
+                      const uint8_t* fixed) {
+  orc_pgo* h = (orc_pgo*)vh;
+  free_graph(h);
+  h->R = n_robots;
+  h->npose = (int*)malloc(sizeof(int) * n_robots);
+  h->poff = (int64_t*)malloc(sizeof(int64_t) * (n_robots + 1));
+  h->poff[0] = 0;
+  for (int a = 0; a < n_robots; ++a) {
+    h->npose[a] = n_poses[a];
+    h->poff[a + 1] = h->poff[a] + n_poses[a];
+  }
+  h->ntot = h->poff[n_robots];
+  h->m = m;
+#define DUP(dst, src, T, k) do { dst = (T*)malloc(sizeof(T) * (size_t)(k) + 1); memcpy(dst, src, sizeof(T) * (size_t)(k)); } while (0)
+  DUP(h->r1, r1, int32_t, m); DUP(h->p1, p1, int32_t, m);
+  DUP(h->r2, r2, int32_t, m); DUP(h->p2, p2, int32_t, m);
+  DUP(h->Rm, R, double, 9 * m); DUP(h->tv, t, double, 3 * m);
+  DUP(h->kappa, kappa, double, m); DUP(h->tau, tau, double, m);
+  DUP(h->w, w, double, m); DUP(h->fixed, fixed, uint8_t, m);
+#undef DUP
+  for (int64_t e = 0; e < m; ++e) {
+    if (r1[e] < 0 || r1[e] >= n_robots || r2[e] < 0 || r2[e] >= n_robots) return KMX_EINVAL;
+    if (p1[e] < 0 || p1[e] >= n_poses[r1[e]] || p2[e] < 0 || p2[e] >= n_poses[r2[e]]) return KMX_EINVAL;
+  }
+  h->nredges = (int64_t*)calloc(n_robots, sizeof(int64_t));
+  h->redges = (int64_t**)calloc(n_robots, sizeof(int64_t*));
+  for (int64_t e = 0; e < m; ++e) {
+    h->nredges[r1[e]]++;
+    if (r2[e] != r1[e]) h->nredges[r2[e]]++;
+  }
+  for (int a = 0; a < n_robots; ++a) h->redges[a] = (int64_t*)malloc(sizeof(int64_t) * (h->nredges[a] + 1));
+  int64_t* fill = (int64_t*)calloc(n_robots, sizeof(int64_t));
+  for (int64_t e = 0; e < m; ++e) {
+    h->redges[r1[e]][fill[r1[e]]++] = e;
+    if (r2[e] != r1[e]) h->redges[r2[e]][fill[r2[e]]++] = e;
+  }
+  free(fill);
+  h->X = (double*)calloc((size_t)h->ntot * PS(h) + 1, sizeof(double));
+  h->nbr = (double*)calloc((size_t)h->ntot * PS(h) + 1, sizeof(double));
+  return 0;
+}
+
+int orc_pgo_set_iterate(void* vh, int a, const double* X) {
+  orc_pgo* h = (orc_pgo*)vh;
+  memcpy(h->X + h->poff[a] * PS(h), X, sizeof(double) * (size_t)h->npose[a] * PS(h));
+  return 0;
+}
+int orc_pgo_get_iterate(void* vh, int a, double* X) {
+  orc_pgo* h = (orc_pgo*)vh;
+  memcpy(X, h->X + h->poff[a] * PS(h), sizeof(double) * (size_t)h->npose[a] * PS(h));
+  return 0;
+}
+/* neighbour table := current iterate of every robot (publishPublicPoses of all) */
+int orc_pgo_refresh(void* vh) {
+  orc_pgo* h = (orc_pgo*)vh;
+  memcpy(h->nbr, h->X, sizeof(double) * (size_t)h->ntot * PS(h));
+  return 0;
+}
+int orc_pgo_get_weights(void* vh, double* w) {
+  orc_pgo* h = (orc_pgo*)vh;
+  memcpy(w, h->w, sizeof(double) * h->m);
+  return 0;
+}
+int orc_pgo_set_weights(void* vh, const double* w) {
+  orc_pgo* h = (orc_pgo*)vh;
+  memcpy(h->w, w, sizeof(double) * h->m);
+  return 0;
+}
+double orc_pgo_get_mu(void* vh) { return ((orc_pgo*)vh)->mu; }
+void orc_pgo_set_mu(void* vh, double mu) { ((orc_pgo*)vh)->mu = mu; }
+int64_t orc_pgo_local_edges(void* vh, int a) { return ((orc_pgo*)vh)->nredges[a]; }
+
+/* ------------------------------------------------------- block algebra -- */
+typedef struct {
+  orc_pgo* h;
+  int a;       /* robot */
+  int n;       /* poses in block */
+  int r;
+  int ps;      /* 4r */
+  int64_t off; /* global offset */
+} blk;
+
+static double dot(const double* x, const double* y, int64_t k) {
+  double s = 0.0;
+  for (int64_t i = 0; i < k; ++i) s += x[i] * y[i];
+  return s;
+}
+
+/* Edge-centric evaluation of the block's quadratic model.
+ * V: block vector (n*4r). If use_nbr, non-local endpoints take the neighbour
+ * snapshot (cost / gradient); else they are 0 (Hessian-vector: the linear term
+ * G of shared edges drops out). out = d/dV of 1/2 sum_e w(kappa|E_R|^2 + tau|E_t|^2). */
+static double edge_eval(const blk* b, const double* V, int use_nbr, double* out) {
+  orc_pgo* h = b->h;
+  const int r = b->r, ps = b->ps;
+  memset(out, 0, sizeof(double) * (size_t)b->n * ps);
+  double cost = 0.0;
+  double zero[4 * 8];
+  memset(zero, 0, sizeof(zero));
+  for (int64_t k = 0; k < h->nredges[b->a]; ++k) {
+    const int64_t e = h->redges[b->a][k];
+    const int ti = (h->r1[e] == b->a), hi = (h->r2[e] == b->a);
+    const double* Vi;
+    const double* Vj;
+    if (ti) Vi = V + (int64_t)h->p1[e] * ps;
+    else Vi = use_nbr ? h->nbr + (h->poff[h->r1[e]] + h->p1[e]) * ps : zero;
+    if (hi) Vj = V + (int64_t)h->p2[e] * ps;
+    else Vj = use_nbr ? h->nbr + (h->poff[h->r2[e]] + h->p2[e]) * ps : zero;
+    const double* Rt = h->Rm + 9 * e;
+    const double* tt = h->tv + 3 * e;
+    const double wk = h->w[e] * h->kappa[e];
+    const double wt = h->w[e] * h->tau[e];
+    for (int a = 0; a < r; ++a) {
+      const double* yi = Vi + 4 * a;
+      const double* yj = Vj + 4 * a;
+      double ER[3], Et;
+      for (int c = 0; c < 3; ++c)
+        ER[c] = yj[c] - (yi[0] * Rt[0 * 3 + c] + yi[1] * Rt[1 * 3 + c] + yi[2] * Rt[2 * 3 + c]);
+      Et = yj[3] - yi[3] - (yi[0] * tt[0] + yi[1] * tt[1] + yi[2] * tt[2]);
+      cost += 0.5 * (wk * (ER[0] * ER[0] + ER[1] * ER[1] + ER[2] * ER[2]) + wt * Et * Et);
+      if (hi) {
+        double* oj = out + (int64_t)h->p2[e] * ps + 4 * a;
+        oj[0] += wk * ER[0]; oj[1] += wk * ER[1]; oj[2] += wk * ER[2];
+        oj[3] += wt * Et;
+      }
+      if (ti) {
+        double* oi = out + (int64_t)h->p1[e] * ps + 4 * a;
+        for (int c = 0; c < 3; ++c)
+          oi[c] -= wk * (ER[0] * Rt[c * 3 + 0] + ER[1] * Rt[c * 3 + 1] + ER[2] * Rt[c * 3 + 2]) + wt * Et * tt[c];
+        oi[3] -= wt * Et;
+      }
+    }
+  }
+  return cost;
+}
+
+/* per pose: S = sym(Y^T G_Y) (3x3) */
+static void sym_YtG(int r, const double* X, const double* G, double* S) {
+  double M[9];
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < 3; ++k) {
+      double s = 0.0;
+      for (int a = 0; a < r; ++a) s += X[4 * a + c] * G[4 * a + k];
+      M[c * 3 + k] = s;
+    }
+  for (int c = 0; c < 3; ++c)
+    for (int k = 0; k < 3; ++k) S[c * 3 + k] = 0.5 * (M[c * 3 + k] + M[k * 3 + c]);
+}
+
+/* tangent projection at X of V (in place on out): out_Y = V_Y - Y sym(Y^T V_Y) */
+static void proj_pose(int r, const double* X, const double* V, double* out) {
+  double S[9];
+  sym_YtG(r, X, V, S);
+  for (int a = 0; a < r; ++a) {
+    for (int c = 0; c < 3; ++c)
+      out[4 * a + c] = V[4 * a + c] - (X[4 * a + 0] * S[0 * 3 + c] + X[4 * a + 1] * S[1 * 3 + c] + X[4 * a + 2] * S[2 * 3 + c]);
+    out[4 * a + 3] = V[4 * a + 3];
+  }
+}
+
+/* 4x4 diagonal block of Q for each pose of the block + shift, inverted. */
+static void build_precond(const blk* b, double* Pinv /* n*16 */) {
+  orc_pgo* h = b->h;
+  double* Dm = (double*)calloc((size_t)b->n * 16, sizeof(double));
+  for (int64_t k = 0; k < h->nredges[b->a]; ++k) {
+    const int64_t e = h->redges[b->a][k];
+    const double wk = h->w[e] * h->kappa[e], wt = h->w[e] * h->tau[e];
+    const double* tt = h->tv + 3 * e;
+    if (h->r1[e] == b->a) { /* tail: w[[kI + tau t t^T, tau t],[tau t^T, tau]] */
+      double* M = Dm + (int64_t)h->p1[e] * 16;
+      for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) M[i * 4 + j] += wt * tt[i] * tt[j] + (i == j ? wk : 0.0);
+        M[i * 4 + 3] += wt * tt[i];
+        M[3 * 4 + i] += wt * tt[i];
+      }
+      M[15] += wt;
+    }
+    if (h->r2[e] == b->a) { /* head: w diag(kappa I, tau) */
+      double* M = Dm + (int64_t)h->p2[e] * 16;
+      M[0] += wk; M[5] += wk; M[10] += wk; M[15] += wt;
+    }
+  }
+  for (int i = 0; i < b->n; ++i) {
+    double A[16], L[16] = {0}, Li[16] = {0};
+    memcpy(A, Dm + (int64_t)i * 16, sizeof(A));
+    for (int j = 0; j < 4; ++j) A[j * 5] += h->P.precond_shift;
+    /* Cholesky A = L L^T */
+    for (int j = 0; j < 4; ++j) {
+      double s = A[j * 4 + j];
+      for (int k = 0; k < j; ++k) s -= L[j * 4 + k] * L[j * 4 + k];
+      L[j * 4 + j] = sqrt(s);
+      for (int ii = j + 1; ii < 4; ++ii) {
+        double t = A[ii * 4 + j];
+        for (int k = 0; k < j; ++k) t -= L[ii * 4 + k] * L[j * 4 + k];
+        L[ii * 4 + j] = t / L[j * 4 + j];
+      }
+    }
+    /* L^{-1} by forward substitution */
+    for (int c = 0; c < 4; ++c) {
+      for (int ii = 0; ii < 4; ++ii) {
+        double s = (ii == c) ? 1.0 : 0.0;
+        for (int k = c; k < ii; ++k) s -= L[ii * 4 + k] * Li[k * 4 + c];
+        Li[ii * 4 + c] = (ii < c) ? 0.0 : s / L[ii * 4 + ii];
+      }
+    }
+    /* A^{-1} = L^{-T} L^{-1} */
+    double* Pi = Pinv + (int64_t)i * 16;
+    for (int x = 0; x < 4; ++x)
+      for (int y = 0; y < 4; ++y) {
+        double s = 0.0;
+        for (int k = 0; k < 4; ++k) s += Li[k * 4 + x] * Li[k * 4 + y];
+        Pi[x * 4 + y] = s;
+      }
+  }
+  free(Dm);
+}
+
+typedef struct {
+  double* Xb;   /* block iterate (points into h->X) */
+  double* eg;   /* Euclidean gradient */
+  double* g;    /* Riemannian gradient */
+  double* S;    /* n*9 curvature sym(Y^T egrad_Y) */
+  double* Pinv; /* n*16 */
+  double* tmp;
+} ctx;
+
+static void rhess(const blk* b, const ctx* c, const double* V, double* out) {
+  edge_eval(b, V, 0, c->tmp); /* Euclidean Hess-vec Q V */
+  const int r = b->r, ps = b->ps;
+  double buf[32];
+  for (int i = 0; i < b->n; ++i) {
+    const double* Xi = c->Xb + (int64_t)i * ps;
+    const double* Vi = V + (int64_t)i * ps;
+    const double* Hi = c->tmp + (int64_t)i * ps;
+    const double* Si = c->S + (int64_t)i * 9;
+    for (int a = 0; a < r; ++a) {
+      for (int k = 0; k < 3; ++k)
+        buf[4 * a + k] = Hi[4 * a + k] - (Vi[4 * a + 0] * Si[0 * 3 + k] + Vi[4 * a + 1] * Si[1 * 3 + k] + Vi[4 * a + 2] * Si[2 * 3 + k]);
+      buf[4 * a + 3] = Hi[4 * a + 3];
+    }
+    proj_pose(r, Xi, buf, out + (int64_t)i * ps);
+  }
+}
+
+static void precon(const blk* b, const ctx* c, const double* V, double* out) {
+  const int r = b->r, ps = b->ps;
+  if (!b->h->P.use_preconditioner) {
+    memcpy(out, V, sizeof(double) * (size_t)b->n * ps);
+    return;
+  }
+  double buf[32];
+  for (int i = 0; i < b->n; ++i) {
+    const double* Vi = V + (int64_t)i * ps;
+    const double* P = c->Pinv + (int64_t)i * 16;
+    for (int a = 0; a < r; ++a)
+      for (int k = 0; k < 4; ++k)
+        buf[4 * a + k] = Vi[4 * a + 0] * P[0 * 4 + k] + Vi[4 * a + 1] * P[1 * 4 + k] + Vi[4 * a + 2] * P[2 * 4 + k] + Vi[4 * a + 3] * P[3 * 4 + k];
+    proj_pose(r, c->Xb + (int64_t)i * ps, buf, out + (int64_t)i * ps);
+  }
+}
+
+/* QF retraction per pose: Y' = qf(Y + V_Y) (modified Gram-Schmidt, positive
+ * diagonal), p' = p + V_p. */
+static void retract_pose(int r, const double* X, const double* V, double* out) {
+  double A[8 * 3];
+  for (int a = 0; a < r; ++a)
+    for (int c = 0; c < 3; ++c) A[a * 3 + c] = X[4 * a + c] + V[4 * a + c];
+  for (int c = 0; c < 3; ++c) {
+    for (int k = 0; k < c; ++k) {
+      double s = 0.0;
+      for (int a = 0; a < r; ++a) s += A[a * 3 + k] * A[a * 3 + c];
+      for (int a = 0; a < r; ++a) A[a * 3 + c] -= s * A[a * 3 + k];
+    }
+    double nn = 0.0;
+    for (int a = 0; a < r; ++a) nn += A[a * 3 + c] * A[a * 3 + c];
+    const double inv = 1.0 / sqrt(nn);
+    for (int a = 0; a < r; ++a) A[a * 3 + c] *= inv;
+  }
+  for (int a = 0; a < r; ++a) {
+    for (int c = 0; c < 3; ++c) out[4 * a + c] = A[a * 3 + c];
+    out[4 * a + 3] = X[4 * a + 3] + V[4 * a + 3];
+  }
+}
+
+/* --------------------------------------------------------- block update -- */
+static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
+  blk b = {h, a, h->npose[a], h->P.r, PS(h), h->poff[a]};
+  const int64_t N = (int64_t)b.n * b.ps;
+  ctx c;
+  c.Xb = h->X + b.off * b.ps;
+  c.eg = (double*)malloc(sizeof(double) * N + 8);
+  c.g = (double*)malloc(sizeof(double) * N + 8);
+  c.S = (double*)malloc(sizeof(double) * (size_t)b.n * 9 + 8);
+  c.Pinv = (double*)malloc(sizeof(double) * (size_t)b.n * 16 + 8);
+  c.tmp = (double*)malloc(sizeof(double) * N + 8);
+  double* eta = (double*)malloc(sizeof(double) * N + 8);
+  double* Heta = (double*)malloc(sizeof(double) * N + 8);
+  double* rr = (double*)malloc(sizeof(double) * N + 8);
+  double* z = (double*)malloc(sizeof(double) * N + 8);
+  double* del = (double*)malloc(sizeof(double) * N + 8);
+  double* Hd = (double*)malloc(sizeof(double) * N + 8);
+  double* Xt = (double*)malloc(sizeof(double) * N + 8);
+  double* X0 = (double*)malloc(sizeof(double) * N + 8);
+  memcpy(X0, c.Xb, sizeof(double) * N);
+  build_precond(&b, c.Pinv);
+
+  memset(st, 0, sizeof(*st));
+  st->updated = 1;
+  st->edges = h->nredges[a];
+  double Delta = h->P.rtr_initial_radius;
+  for (int it = 0; it < h->P.rtr_iterations; ++it) {
+    double f = edge_eval(&b, c.Xb, 1, c.eg);
+    for (int i = 0; i < b.n; ++i) {
+      sym_YtG(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.S + (int64_t)i * 9);
+      proj_pose(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.g + (int64_t)i * b.ps);
+    }
+    const double gn = sqrt(dot(c.g, c.g, N));
+    if (it == 0) { st->f_init = f; st->gradnorm_init = gn; }
+    st->f_final = f;
+    if (gn < h->P.gradnorm_tol) {
+      st->tcg_stop = KMX_TCG_SKIPPED;
+      st->tcg_iterations = 0;
+      st->accepted = 0;
+      break;
+    }
+    /* ---- preconditioned Steihaug-Toint truncated CG ---- */
+    memset(eta, 0, sizeof(double) * N);
+    memset(Heta, 0, sizeof(double) * N);
+    memcpy(rr, c.g, sizeof(double) * N);
+    double e_Pe = 0.0, e_Pd = 0.0;
+    const double norm_r0 = sqrt(dot(rr, rr, N));
+    precon(&b, &c, rr, z);
+    double z_r = dot(z, rr, N);
+    double d_Pd = z_r;
+    for (int64_t k = 0; k < N; ++k) del[k] = -z[k];
+    int stop = KMX_TCG_MAX_ITER, j;
+    for (j = 1; j <= h->P.tcg_max_iterations; ++j) {
+      rhess(&b, &c, del, Hd);
+      st->hessvecs++;
+      const double d_Hd = dot(del, Hd, N);
+      const double alpha = z_r / d_Hd;
+      const double e_Pe_new = e_Pe + 2.0 * alpha * e_Pd + alpha * alpha * d_Pd;
+      if (d_Hd <= 0.0 || e_Pe_new >= Delta * Delta) {
+        const double tau = (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (Delta * Delta - e_Pe))) / d_Pd;
+        for (int64_t k = 0; k < N; ++k) { eta[k] += tau * del[k]; Heta[k] += tau * Hd[k]; }
+        stop = d_Hd <= 0.0 ? KMX_TCG_NEGATIVE_CURVATURE : KMX_TCG_EXCEEDED_TR;
+        break;
+      }
+      e_Pe = e_Pe_new;
+      for (int64_t k = 0; k < N; ++k) {
+        eta[k] += alpha * del[k];
+        Heta[k] += alpha * Hd[k];
+        rr[k] += alpha * Hd[k];
+      }
+      const double norm_r = sqrt(dot(rr, rr, N));
+      if (norm_r <= norm_r0 * fmin(pow(norm_r0, h->P.tcg_theta), h->P.tcg_kappa)) {
+        stop = (h->P.tcg_kappa < pow(norm_r0, h->P.tcg_theta)) ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
+        break;
+      }
+      if (j == h->P.tcg_max_iterations) break;
+      precon(&b, &c, rr, z);
+      const double zold_rold = z_r;
+      z_r = dot(z, rr, N);
+      const double beta = z_r / zold_rold;
+      for (int64_t k = 0; k < N; ++k) del[k] = -z[k] + beta * del[k];
+      e_Pd = beta * (e_Pd + alpha * d_Pd);
+      d_Pd = z_r + beta * beta * d_Pd;
+    }
+    st->tcg_iterations = j > h->P.tcg_max_iterations ? h->P.tcg_max_iterations : j;
+    st->tcg_stop = stop;
+    /* ---- trial point, model decrease, acceptance ---- */
+    for (int i = 0; i < b.n; ++i)
+      retract_pose(b.r, c.Xb + (int64_t)i * b.ps, eta + (int64_t)i * b.ps, Xt + (int64_t)i * b.ps);
+    const double ft = edge_eval(&b, Xt, 1, c.tmp);
+    const double model_dec = -(dot(eta, c.g, N) + 0.5 * dot(eta, Heta, N));
+    const double rho = (model_dec > 0.0) ? (f - ft) / model_dec : -1.0;
+    const int boundary = (stop == KMX_TCG_NEGATIVE_CURVATURE || stop == KMX_TCG_EXCEEDED_TR);
+    if (!(rho >= 0.25)) Delta *= 0.25;
+    else if (rho > 0.75 && boundary) Delta = fmin(2.0 * Delta, h->P.rtr_max_radius);
+    st->rho = rho;
+    st->radius = Delta;
+    if (rho > h->P.rtr_accept_rho) {
+      memcpy(c.Xb, Xt, sizeof(double) * N);
+      st->accepted = 1;
+      st->f_final = ft;
+    } else {
+      st->accepted = 0;
+      st->f_final = f;
+    }
+  }
+  double ch = 0.0;
+  for (int64_t k = 0; k < N; ++k) { const double dd = c.Xb[k] - X0[k]; ch += dd * dd; }
+  st->rel_change = sqrt(ch / (double)b.n);
+  free(c.eg); free(c.g); free(c.S); free(c.Pinv); free(c.tmp);
+  free(eta); free(Heta); free(rr); free(z); free(del); free(Hd); free(Xt); free(X0);
+}
+
+/* One RBCD round: neighbour table = iterate at round start (every robot
+ * published after its previous iterate), then every active robot updates its
+ * block against that table. */
+int orc_pgo_round(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
+  orc_pgo* h = (orc_pgo*)vh;
+  orc_pgo_refresh(h);
+  for (int a = 0; a < h->R; ++a) {
+    kmx_iter_stats st;
+    memset(&st, 0, sizeof(st));
+    if (active[a]) block_update(h, a, &st);
+    if (stats) stats[a] = st;
+  }
+  return 0;
+}
+
+/* Same round with the robot blocks spread over `threads` OpenMP threads (one
+ * block per thread at a time; blocks write disjoint iterate slices). This is
+ * the all-cores CPU baseline of BASELINE.md §2.4. */
+int orc_pgo_round_mt(void* vh, const uint8_t* active, kmx_iter_stats* stats, int threads) {
+  orc_pgo* h = (orc_pgo*)vh;
+  orc_pgo_refresh(h);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+  for (int a = 0; a < h->R; ++a) {
+    kmx_iter_stats st;
+    memset(&st, 0, sizeof(st));
+    if (active[a]) block_update(h, a, &st);
+    if (stats) stats[a] = st;
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------- GNC-TLS -- */
+/* RobustCost::weight for GNC_TLS (Yang et al. 2020 eq. 14), on squared residual. */
+static double gnc_tls_weight(double rSq, double mu, double barc) {
+  const double barcSq = barc * barc;
+  const double upper = (mu + 1.0) / mu * barcSq;
+  const double lower = mu / (mu + 1.0) * barcSq;
+  if (rSq >= upper) return 0.0;
+  if (rSq <= lower) return 1.0;
+  return sqrt(barcSq * mu * (mu + 1.0) / rSq) - mu;
+}
+
+/* r^2 = kappa ||Y_j - Y_i R||^2 + tau ||p_j - p_i - Y_i t||^2 on lifted poses */
+static double residual_sq(const orc_pgo* h, int64_t e, const double* Xi, const double* Xj) {
+  const double* Rt = h->Rm + 9 * e;
+  const double* tt = h->tv + 3 * e;
+  double sR = 0.0, sT = 0.0;
+  for (int a = 0; a < h->P.r; ++a) {
+    const double* yi = Xi + 4 * a;
+    const double* yj = Xj + 4 * a;
+    for (int c = 0; c < 3; ++c) {
+      const double er = yj[c] - (yi[0] * Rt[0 * 3 + c] + yi[1] * Rt[1 * 3 + c] + yi[2] * Rt[2 * 3 + c]);
+      sR += er * er;
+    }
+    const double et = yj[3] - yi[3] - (yi[0] * tt[0] + yi[1] * tt[1] + yi[2] * tt[2]);
+    sT += et * et;
+  }
+  return h->kappa[e] * sR + h->tau[e] * sT;
+}
+
+int orc_pgo_update_weights(void* vh, double* mu_used) {
+  orc_pgo* h = (orc_pgo*)vh;
+  if (mu_used) *mu_used = h->mu;
+  if (h->P.robust_cost != KMX_COST_GNC_TLS) return 0;
+  const int ps = PS(h);
+  for (int64_t e = 0; e < h->m; ++e) {
+    if (h->fixed[e]) continue;
+    const double* Xi = h->X + (h->poff[h->r1[e]] + h->p1[e]) * ps;
+    const double* Xj = h->X + (h->poff[h->r2[e]] + h->p2[e]) * ps;
+    h->w[e] = gnc_tls_weight(residual_sq(h, e, Xi, Xj), h->mu, h->P.gnc_barc);
+  }
+  h->mu *= h->P.gnc_mu_step;
+  return 0;
+}
+
+/* ------------------------------------------------------------ rounding -- */
+/* symmetric 3x3 Jacobi eigen-decomposition (cyclic, fixed sweeps) */
+static void jacobi3(double A[9], double V[9]) {
+  for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    for (int p = 0; p < 2; ++p)
+      for (int q = p + 1; q < 3; ++q) {
+        const double apq = A[p * 3 + q];
+        if (apq == 0.0) continue;
+        const double app = A[p * 3 + p], aqq = A[q * 3 + q];
+        const double theta = (aqq - app) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
+        for (int k = 0; k < 3; ++k) { /* A = J^T A J */
+          const double akp = A[k * 3 + p], akq = A[k * 3 + q];
+          A[k * 3 + p] = cs * akp - sn * akq;
+          A[k * 3 + q] = sn * akp + cs * akq;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double apk = A[p * 3 + k], aqk = A[q * 3 + k];
+          A[p * 3 + k] = cs * apk - sn * aqk;
+          A[q * 3 + k] = sn * apk + cs * aqk;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double vkp = V[k * 3 + p], vkq = V[k * 3 + q];
+          V[k * 3 + p] = cs * vkp - sn * vkq;
+          V[k * 3 + q] = sn * vkp + cs * vkq;
+        }
+      }
+  }
+}
+
+/* nearest rotation: R = U diag(1,1,sign det M) V^T via M^T M = V L V^T */
+static void proj_so3(const double M[9], double Rout[9]) {
+  double A[9], V[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < 3; ++k) s += M[k * 3 + i] * M[k * 3 + j];
+      A[i * 3 + j] = s;
+    }
+  jacobi3(A, V);
+  const double det = M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) + M[2] * (M[3] * M[7] - M[4] * M[6]);
+  int kmin = 0;
+  for (int k = 1; k < 3; ++k) if (A[k * 4] < A[kmin * 4]) kmin = k;
+  for (int i = 0; i < 9; ++i) Rout[i] = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    const double sig = sqrt(fmax(A[k * 4], 0.0));
+    double u[3];
+    for (int i = 0; i < 3; ++i) u[i] = (M[i * 3 + 0] * V[0 * 3 + k] + M[i * 3 + 1] * V[1 * 3 + k] + M[i * 3 + 2] * V[2 * 3 + k]) / sig;
+    const double s = (k == kmin && det < 0.0) ? -1.0 : 1.0;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Rout[i * 3 + j] += s * u[i] * V[j * 3 + k];
+  }
+}
+
+int orc_pgo_get_trajectory(void* vh, int a, const double* anchor, double* out) {
+  orc_pgo* h = (orc_pgo*)vh;
+  const int r = h->P.r, ps = PS(h);
+  for (int i = 0; i < h->npose[a]; ++i) {
+    const double* Xi = h->X + (h->poff[a] + i) * ps;
+    double M[9];
+    for (int x = 0; x < 3; ++x) {
+      for (int y = 0; y < 3; ++y) {
+        double s = 0.0;
+        for (int k = 0; k < r; ++k) s += anchor[4 * k + x] * Xi[4 * k + y];
+        M[x * 3 + y] = s;
+      }
+      double s = 0.0;
+      for (int k = 0; k < r; ++k) s += anchor[4 * k + x] * (Xi[4 * k + 3] - anchor[4 * k + 3]);
+      out[(int64_t)i * 12 + 9 + x] = s;
+    }
+    proj_so3(M, out + (int64_t)i * 12);
+  }
+  return 0;
+}
+
+/* ------------------------------------------------ primitive evaluation -- */
+int orc_pgo_eval(void* vh, int a, int mode, const double* V, double* out, double* scalar) {
+  orc_pgo* h = (orc_pgo*)vh;
+  blk b = {h, a, h->npose[a], h->P.r, PS(h), h->poff[a]};
+  const int64_t N = (int64_t)b.n * b.ps;
+  ctx c;
+  c.Xb = h->X + b.off * b.ps;
+  c.eg = (double*)malloc(sizeof(double) * N + 8);
+  c.g = (double*)malloc(sizeof(double) * N + 8);
+  c.S = (double*)malloc(sizeof(double) * (size_t)b.n * 9 + 8);
+  c.Pinv = (double*)malloc(sizeof(double) * (size_t)b.n * 16 + 8);
+  c.tmp = (double*)malloc(sizeof(double) * N + 8);
+  double s = 0.0;
+  if (mode == KMX_EVAL_COST_EGRAD) {
+    s = edge_eval(&b, V, 1, out);
+  } else if (mode == KMX_EVAL_EHESS) {
+    edge_eval(&b, V, 0, out);
+    s = dot(V, out, N);
+  } else {
+    edge_eval(&b, c.Xb, 1, c.eg);
+    for (int i = 0; i < b.n; ++i) {
+      sym_YtG(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.S + (int64_t)i * 9);
+      proj_pose(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.g + (int64_t)i * b.ps);
+    }
+    build_precond(&b, c.Pinv);
+    if (mode == KMX_EVAL_RGRAD) {
+      memcpy(out, c.g, sizeof(double) * N);
+      s = dot(out, out, N);
+    } else if (mode == KMX_EVAL_RHESS) {
+      rhess(&b, &c, V, out);
+      s = dot(V, out, N);
+    } else if (mode == KMX_EVAL_PRECON) {
+      precon(&b, &c, V, out);
+      s = dot(V, out, N);
+    } else if (mode == KMX_EVAL_RETRACT) {
+      for (int i = 0; i < b.n; ++i)
+        retract_pose(b.r, c.Xb + (int64_t)i * b.ps, V + (int64_t)i * b.ps, out + (int64_t)i * b.ps);
+    }
+  }
+  if (scalar) *scalar = s;
+  free(c.eg); free(c.g); free(c.S); free(c.Pinv); free(c.tmp);
+  return 0;
+}

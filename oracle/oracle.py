@@ -1,0 +1,174 @@
+"""ctypes wrapper of the CPU restatement (oracle/build/liborc.so).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product package. It mirrors the
+product handle (kmx.dpgo.solver.BlockSolver) so parity tests read the same on
+both sides. Parity status: see the header of dpgo_oracle.c ("parity unpinned"
+against upstream dpgo; pinned by analytic known answers).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "build" / "liborc.so"
+
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        _lib = C.CDLL(str(LIB))
+        _setup(_lib)
+    return _lib
+
+
+def _setup(L):
+    import sys
+    sys.path.insert(0, str(HERE.parent / "kimera-multi_amd"))
+    from kmx.abi import IterStats, PgoParams, LcdParams, LcdResult  # struct layouts only
+    P, i32, i64, f64, u8 = C.c_void_p, C.c_int32, C.c_int64, C.c_double, C.c_uint8
+    pi32, pf64, pu8 = C.POINTER(i32), C.POINTER(f64), C.POINTER(u8)
+    sigs = {
+        "orc_pgo_create": ([C.POINTER(PgoParams)], P),
+        "orc_pgo_destroy": ([P], None),
+        "orc_pgo_set_graph": ([P, C.c_int, pi32, i64, pi32, pi32, pi32, pi32, pf64, pf64, pf64, pf64, pf64, pu8], C.c_int),
+        "orc_pgo_set_iterate": ([P, C.c_int, pf64], C.c_int),
+        "orc_pgo_get_iterate": ([P, C.c_int, pf64], C.c_int),
+        "orc_pgo_refresh": ([P], C.c_int),
+        "orc_pgo_get_weights": ([P, pf64], C.c_int),
+        "orc_pgo_set_weights": ([P, pf64], C.c_int),
+        "orc_pgo_get_mu": ([P], f64),
+        "orc_pgo_set_mu": ([P, f64], None),
+        "orc_pgo_local_edges": ([P, C.c_int], i64),
+        "orc_pgo_round": ([P, pu8, C.POINTER(IterStats)], C.c_int),
+        "orc_pgo_round_mt": ([P, pu8, C.POINTER(IterStats), C.c_int], C.c_int),
+        "orc_pgo_update_weights": ([P, pf64], C.c_int),
+        "orc_pgo_get_trajectory": ([P, C.c_int, pf64, pf64], C.c_int),
+        "orc_pgo_eval": ([P, C.c_int, C.c_int, pf64, pf64, pf64], C.c_int),
+    }
+    for name, (a, r) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = a
+        fn.restype = r
+    if hasattr(L, "orc_lcd_knn2"):
+        L.orc_lcd_knn2.argtypes = [C.c_int, C.c_float, pu8, i32, pu8, i32, pi32, pi32]
+        L.orc_lcd_knn2.restype = C.c_int
+
+
+def _f(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _i(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def _u(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+class OraclePGO:
+    """All robots of the team in one CPU process (Jacobi rounds like the GPU)."""
+
+    def __init__(self, params, graph):
+        from kmx.abi import PgoParams, IterStats  # noqa: F401
+        self.L = lib()
+        self.params = params
+        self.r = params.r
+        self.h = self.L.orc_pgo_create(C.byref(params))
+        g = graph
+        self.n_robots = g.n_robots
+        self.n_poses = np.ascontiguousarray(g.n_poses, dtype=np.int32)
+        self._keep = [np.ascontiguousarray(x) for x in (g.r1, g.p1, g.r2, g.p2)]
+        self._R = np.ascontiguousarray(g.R.reshape(-1), dtype=np.float64)
+        self._t = np.ascontiguousarray(g.t.reshape(-1), dtype=np.float64)
+        self._k = np.ascontiguousarray(g.kappa, dtype=np.float64)
+        self._tau = np.ascontiguousarray(g.tau, dtype=np.float64)
+        self._w = np.ascontiguousarray(g.weight, dtype=np.float64)
+        self._fx = np.ascontiguousarray(g.fixed, dtype=np.uint8)
+        r1, p1, r2, p2 = self._keep
+        rc = self.L.orc_pgo_set_graph(self.h, g.n_robots, _i(self.n_poses), g.m, _i(r1), _i(p1), _i(r2), _i(p2),
+                                      _f(self._R), _f(self._t), _f(self._k), _f(self._tau), _f(self._w), _u(self._fx))
+        assert rc == 0, rc
+        self.m = g.m
+
+    def __del__(self):
+        try:
+            self.L.orc_pgo_destroy(self.h)
+        except Exception:
+            pass
+
+    def set_iterate(self, robot, X):
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        assert X.size == self.n_poses[robot] * 4 * self.r
+        self.L.orc_pgo_set_iterate(self.h, robot, _f(X))
+
+    def get_iterate(self, robot):
+        X = np.empty((self.n_poses[robot], self.r, 4))
+        self.L.orc_pgo_get_iterate(self.h, robot, _f(X))
+        return X
+
+    def refresh(self):
+        self.L.orc_pgo_refresh(self.h)
+
+    def iterate(self, active=None, threads=1):
+        from kmx.abi import IterStats
+        act = np.ones(self.n_robots, np.uint8) if active is None else np.ascontiguousarray(active, dtype=np.uint8)
+        stats = (IterStats * self.n_robots)()
+        if threads > 1:
+            self.L.orc_pgo_round_mt(self.h, _u(act), stats, threads)
+        else:
+            self.L.orc_pgo_round(self.h, _u(act), stats)
+        return [s.as_dict() for s in stats]
+
+    def update_weights(self):
+        mu = C.c_double(0)
+        self.L.orc_pgo_update_weights(self.h, C.byref(mu))
+        return mu.value
+
+    def get_weights(self):
+        w = np.empty(self.m)
+        self.L.orc_pgo_get_weights(self.h, _f(w))
+        return w
+
+    def set_weights(self, w):
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        self.L.orc_pgo_set_weights(self.h, _f(w))
+
+    @property
+    def mu(self):
+        return self.L.orc_pgo_get_mu(self.h)
+
+    @mu.setter
+    def mu(self, v):
+        self.L.orc_pgo_set_mu(self.h, float(v))
+
+    def local_edges(self, robot):
+        return int(self.L.orc_pgo_local_edges(self.h, robot))
+
+    def trajectory(self, robot, anchor):
+        anchor = np.ascontiguousarray(anchor, dtype=np.float64)
+        out = np.empty((self.n_poses[robot], 12))
+        self.L.orc_pgo_get_trajectory(self.h, robot, _f(anchor), _f(out))
+        return out
+
+    def eval(self, robot, mode, V=None):
+        n = int(self.n_poses[robot])
+        Vin = np.zeros((n, self.r, 4)) if V is None else np.ascontiguousarray(V, dtype=np.float64)
+        out = np.empty((n, self.r, 4))
+        s = C.c_double(0)
+        self.L.orc_pgo_eval(self.h, robot, mode, _f(Vin), _f(out), C.byref(s))
+        return out, s.value

@@ -1,0 +1,169 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU restatement.
+
+Tolerances (north_star: "optimized poses within 1e-6 Frobenius of reference"):
+  * primitives (cost / egrad / Hess-vec / projections / retraction): the
+    kernels accumulate every output element in the oracle's order with
+    -ffp-contract=off, so they must agree to 1e-12 relative (bit-exact in
+    practice; reductions differ only in summation order);
+  * full RBCD rounds: per-pose Frobenius difference <= 1e-6 after every round.
+"""
+import numpy as np
+import pytest
+
+from kmx import abi
+from kmx.dpgo.params import PGOAgentParameters, RobustCostType
+from kmx.dpgo.solver import BlockSolver
+from kmx.synth import lift, lifting_matrix, make_pose_graph
+from kmx.synth.pose_graph import _expm_so3
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(n_robots=3, n=300, m=900, r=5, robust=True, seed=0, perturb=0.05, outlier=0.2):
+    g = make_pose_graph(n_robots, n, m, outlier_frac=outlier, seed=seed)
+    P = PGOAgentParameters(r=r)
+    if not robust:
+        P.robustCostParams.costType = RobustCostType.L2
+    Y = lifting_matrix(r, seed=1)
+    rng = np.random.default_rng(seed + 7)
+    X0 = {}
+    for a in range(g.n_robots):
+        k = int(g.n_poses[a])
+        Rp = g.init_R[a] @ _expm_so3(rng.normal(0, perturb, (k, 3)))
+        X0[a] = lift(Rp, g.init_t[a] + rng.normal(0, 5 * perturb, (k, 3)), Y)
+    return g, P, X0
+
+
+def _pair(g, P, X0):
+    from oracle.oracle import OraclePGO
+    s = BlockSolver(P, 0)
+    s.set_graph_data(g)
+    o = OraclePGO(P.to_c(), g)
+    for a in range(g.n_robots):
+        s.set_iterate(a, X0[a])
+        o.set_iterate(a, X0[a])
+    s.refresh_local()
+    o.refresh()
+    return s, o
+
+
+@pytest.mark.parametrize("r", [3, 5, 8])
+def test_primitives_match_oracle(gpu, r):
+    g, P, X0 = _setup(r=r)
+    # non-trivial GNC weights so w*kappa paths are exercised
+    g.weight = np.random.default_rng(3).uniform(0.0, 1.0, g.m)
+    s, o = _pair(g, P, X0)
+    rng = np.random.default_rng(11)
+    for a in range(g.n_robots):
+        V = rng.standard_normal(X0[a].shape)
+        for mode in (abi.KMX_EVAL_COST_EGRAD, abi.KMX_EVAL_EHESS, abi.KMX_EVAL_RGRAD, abi.KMX_EVAL_RHESS,
+                     abi.KMX_EVAL_PRECON, abi.KMX_EVAL_RETRACT):
+            Vin = X0[a] if mode == abi.KMX_EVAL_COST_EGRAD else V
+            if mode == abi.KMX_EVAL_RETRACT:
+                Vin = 0.1 * V
+            gout, gs = s.eval(a, mode, Vin)
+            oout, os_ = o.eval(a, mode, Vin)
+            scale = max(1.0, np.abs(oout).max())
+            assert np.abs(gout - oout).max() <= 1e-12 * scale, (mode, np.abs(gout - oout).max())
+            assert abs(gs - os_) <= 1e-10 * max(1.0, abs(os_)), (mode, gs, os_)
+
+
+@pytest.mark.parametrize("robust", [False, True])
+def test_rounds_match_oracle(gpu, robust):
+    g, P, X0 = _setup(robust=robust)
+    s, o = _pair(g, P, X0)
+    for it in range(12):
+        s.refresh_local()
+        sg = s.iterate()
+        so = o.iterate()
+        for a in range(g.n_robots):
+            assert sg[a]["tcg_iterations"] == so[a]["tcg_iterations"], (it, a, sg[a], so[a])
+            assert sg[a]["accepted"] == so[a]["accepted"]
+            assert abs(sg[a]["f_init"] - so[a]["f_init"]) <= 1e-9 * max(1.0, abs(so[a]["f_init"]))
+            d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
+            assert d <= 1e-6, (it, a, d)
+        if robust and it % 4 == 3:
+            s.refresh_local()
+            mu_g = s.update_weights()
+            mu_o = o.update_weights()
+            assert mu_g == mu_o
+            wg, wo = s.get_weights(), o.get_weights()
+            assert np.abs(wg - wo).max() <= 1e-9, np.abs(wg - wo).max()
+
+
+def test_sequential_schedule(gpu):
+    g, P, X0 = _setup()
+    s, o = _pair(g, P, X0)
+    for it in range(6):
+        act = np.zeros(g.n_robots, np.uint8)
+        act[it % g.n_robots] = 1
+        s.refresh_local()
+        sg = s.iterate(act)
+        so = o.iterate(act)
+        for a in range(g.n_robots):
+            assert sg[a]["updated"] == act[a] == so[a]["updated"]
+            d = np.abs(s.get_iterate(a) - o.get_iterate(a)).max()
+            assert d <= 1e-8, (it, a, d)
+
+
+def test_trajectory_matches_oracle(gpu):
+    g, P, X0 = _setup()
+    s, o = _pair(g, P, X0)
+    for _ in range(3):
+        s.refresh_local()
+        s.iterate()
+        o.iterate()
+    anchor = s.get_iterate(0)[0]
+    for a in range(g.n_robots):
+        tg, to = s.trajectory(a, anchor), o.trajectory(a, anchor)
+        assert np.abs(tg - to).max() <= 1e-9
+        Rg = tg[:, :9].reshape(-1, 3, 3)
+        assert np.abs(np.einsum("nji,njk->nik", Rg, Rg) - np.eye(3)).max() < 1e-9
+        assert np.all(np.linalg.det(Rg) > 0)
+
+
+def test_async_rounds_equal_sync_rounds(gpu):
+    """The benchmark path (no host sync, device-side control) computes the same
+    iterates as the stats path."""
+    g, P, X0 = _setup()
+    s1 = BlockSolver(P, 0)
+    s1.set_graph_data(g)
+    s2 = BlockSolver(P, 0)
+    s2.set_graph_data(g)
+    for a in range(g.n_robots):
+        s1.set_iterate(a, X0[a])
+        s2.set_iterate(a, X0[a])
+    for _ in range(5):
+        s1.refresh_local()
+        s1.iterate()
+    s2.iterate_async(5, refresh_local=True, gnc_every=0)
+    s2.sync()
+    for a in range(g.n_robots):
+        assert np.array_equal(s1.get_iterate(a), s2.get_iterate(a))
+    c = s2.read_counters()
+    assert c["block_updates"] == 5 * g.n_robots
+
+
+def test_noise_free_converges_to_ground_truth(gpu):
+    g = make_pose_graph(2, 200, 300, outlier_frac=0.0, noise_free=True, seed=0)
+    P = PGOAgentParameters(r=5)
+    P.robustCostParams.costType = RobustCostType.L2
+    P.localOptimizationParams.RTR_tCG_iterations = 50
+    Y = lifting_matrix(5)
+    rng = np.random.default_rng(0)
+    s = BlockSolver(P, 0)
+    s.set_graph_data(g)
+    for a in range(2):
+        k = int(g.n_poses[a])
+        Rp = g.init_R[a] @ _expm_so3(rng.normal(0, 0.1, (k, 3)))
+        s.set_iterate(a, lift(Rp, g.init_t[a] + rng.normal(0, 0.5, (k, 3)), Y))
+    s.iterate_async(200, refresh_local=True)
+    s.sync()
+    anchor = s.get_iterate(0)[0]
+    R0, t0 = g.gt_R[0][0], g.gt_t[0][0]
+    for a in range(2):
+        T = s.trajectory(a, anchor)
+        Rg = np.einsum("ji,njk->nik", R0, g.gt_R[a])
+        tg = (g.gt_t[a] - t0) @ R0
+        assert np.abs(T[:, 9:] - tg).max() < 1e-4
+        assert np.abs(T[:, :9].reshape(-1, 3, 3) - Rg).max() < 1e-4
