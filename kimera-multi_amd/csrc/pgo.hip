@@ -22,7 +22,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <numeric>
@@ -73,11 +75,16 @@ struct Dev {
   const int* rtile0;  // [L+1]
   const int* inc_ptr; // [nloc+1]
   const int2* inc;    // x = other (>=0 local pose, <0 -> public slot -1-x); y = edge | tail<<31
-  double* erec;       // [mloc][16]: R(9) t(3) kappa tau w pad
+  double* irec;       // [ninc][16] per-incidence edge record in CSR order: R(9) t(3) w*kappa w*tau 0 0
+  double* ekappa;     // [mloc] per local edge
+  double* etau;
+  double* ew;         // GNC weight
+  const int2* eipos;  // [mloc] incidence positions (tail, head) of each local edge, -1 if not local
   double *X, *Xt, *g, *r, *z, *eta, *del, *hd, *S, *Pinv, *pub;
   double* part;       // [ntiles][NPART]
   Ctl* ctl;
   Counters* cnt;
+  unsigned* tickets;         // [L] per-robot arrival counters (zero between launches)
   const long long* m_robot;  // [L] local-problem edges per robot
   const int* n_robot;        // [L] poses per robot
   Params p;
@@ -125,17 +132,6 @@ __device__ __forceinline__ void store4(double* p, const double v[4]) {
 struct Edge {
   double R[9], t[3], wk, wt;
 };
-__device__ __forceinline__ void load_edge(const double* erec, int e, Edge& E) {
-  const double2* q = reinterpret_cast<const double2*>(erec + 16 * (size_t)e);
-  double2 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3], v4 = q[4], v5 = q[5], v6 = q[6], v7 = q[7];
-  E.R[0] = v0.x; E.R[1] = v0.y; E.R[2] = v1.x; E.R[3] = v1.y; E.R[4] = v2.x;
-  E.R[5] = v2.y; E.R[6] = v3.x; E.R[7] = v3.y; E.R[8] = v4.x;
-  E.t[0] = v4.y; E.t[1] = v5.x; E.t[2] = v5.y;
-  const double kappa = v6.x, tau = v6.y, w = v7.x;
-  E.wk = w * kappa;
-  E.wt = w * tau;
-}
-
 // Accumulate the contribution of one incidence to row a of pose `self`.
 // vs = self row, vo = other endpoint row (zeros for a Hessian product across a
 // shared edge). Expressions mirror oracle/dpgo_oracle.c edge_eval exactly.
@@ -164,36 +160,6 @@ __device__ __forceinline__ double incidence_row(const Edge& E, bool self_tail, c
     acc[3] += E.wt * Et;
   }
   return 0.5 * (E.wk * (ER[0] * ER[0] + ER[1] * ER[1] + ER[2] * ER[2]) + E.wt * Et * Et);
-}
-
-// Gather row a of (VQ [+ G]) for pose `pose`. V = block vector for private
-// neighbours; shared neighbours read the public table when `pub` != nullptr,
-// else are zero. cost (optional) accumulates this row's share of f:
-// private edges are seen from both endpoints (x 1/2), shared from one.
-template <int R>
-__device__ __forceinline__ void gather_row(const Dev& d, int pose, int a, const double* V,
-                                           const double* pub, double acc[4], double* cost) {
-  double vs[4], vo[4];
-  load4(V + (size_t)pose * 4 * R + 4 * a, vs);
-  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  const int k0 = d.inc_ptr[pose], k1 = d.inc_ptr[pose + 1];
-  for (int k = k0; k < k1; ++k) {
-    const int2 in = d.inc[k];
-    const bool tail = (in.y >> 31) & 1;
-    const int e = in.y & 0x7fffffff;
-    Edge E;
-    load_edge(d.erec, e, E);
-    bool priv = in.x >= 0;
-    if (priv) {
-      load4(V + (size_t)in.x * 4 * R + 4 * a, vo);
-    } else if (pub) {
-      load4(pub + (size_t)(-1 - in.x) * 4 * R + 4 * a, vo);
-    } else {
-      vo[0] = vo[1] = vo[2] = vo[3] = 0.0;
-    }
-    const double c = incidence_row(E, tail, vs, vo, acc);
-    if (cost) *cost += priv ? 0.5 * c : c;
-  }
 }
 
 // S = sym(Y^T G_Y) for the pose group (9 entries, identical in all R lanes).
@@ -289,7 +255,15 @@ template <int R>
 __device__ __forceinline__ Lane lane_map(const Dev& d) {
   constexpr int PPW = 64 / R;
   Lane L;
-  L.tile = blockIdx.x;
+  // XCD-aware, bijective block -> tile remap (cdna_hip_programming.md T1):
+  // blocks b and b + 8 share an XCD, so each XCD gets one contiguous range of
+  // tiles — i.e. (about) one robot block, whose iterate then stays in that
+  // XCD's 4 MiB L2 across the gathers of every kernel of the round.
+  {
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int q = nwg >> 3, rr = nwg & 7, x = b & 7;
+    L.tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
+  }
   L.l = d.tile_robot[L.tile];
   L.w = threadIdx.x >> 6;
   L.ln = threadIdx.x & 63;
@@ -303,26 +277,421 @@ __device__ __forceinline__ Lane lane_map(const Dev& d) {
   return L;
 }
 
-__device__ __forceinline__ void write_partials(const Dev& d, int tile, const double* vals, int n, double* lds) {
-  for (int s = 0; s < n; ++s) {
-    const double t = block_sum(vals[s], lds);
-    if (threadIdx.x == 0) d.part[(size_t)tile * NPART + s] = t;
+// ---------------------------------------------------------------- kernels --
+// Direct variant (G = 0): each (pose, row) lane walks its pose's incidences
+// with per-lane global loads (every lane of the pose loads the edge record).
+struct EdgeRaw {
+  double2 q[8];
+};
+__device__ __forceinline__ void edge_from_raw(const EdgeRaw& w, Edge& E) {
+  E.R[0] = w.q[0].x; E.R[1] = w.q[0].y; E.R[2] = w.q[1].x; E.R[3] = w.q[1].y; E.R[4] = w.q[2].x;
+  E.R[5] = w.q[2].y; E.R[6] = w.q[3].x; E.R[7] = w.q[3].y; E.R[8] = w.q[4].x;
+  E.t[0] = w.q[4].y; E.t[1] = w.q[5].x; E.t[2] = w.q[5].y;
+  E.wk = w.q[6].x;
+  E.wt = w.q[6].y;
+}
+
+template <int R, bool PUB>
+__device__ __forceinline__ void fetch_incidence(const Dev& d, const double* V, const double* pub, int a, int k,
+                                                int2 in, EdgeRaw& w, double2& v0, double2& v1) {
+  const double2* q2 = reinterpret_cast<const double2*>(d.irec + 16 * (size_t)k);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w.q[i] = q2[i];
+  const int o = in.x;
+  const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V);
+  const double2* b2 = reinterpret_cast<const double2*>(base + 4 * a);
+  v0 = b2[0];
+  v1 = b2[1];
+  if (!PUB && o < 0) v0 = v1 = make_double2(0.0, 0.0);
+}
+
+// Direct variant (G = 0): each (pose, row) lane walks its pose's incidences in
+// CSR order, software-pipelined: incidence k+1's edge record and neighbour row
+// are in flight while k is computed, and the CSR entry of k+2 while k+1 loads.
+template <int R, bool PUB>
+__device__ __forceinline__ void lane_gather(const Dev& d, const Lane& L, const double* V, const double* pub,
+                                            double acc[4], double* cost) {
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  if (!L.valid) return;
+  double vs[4];
+  load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
+  const int k0 = d.inc_ptr[L.pose], k1 = d.inc_ptr[L.pose + 1];
+  if (k0 >= k1) return;
+  int2 inA = d.inc[k0];
+  int2 inB = (k0 + 1 < k1) ? d.inc[k0 + 1] : inA;
+  EdgeRaw wA, wB;
+  double2 a0, a1, b0, b1;
+  fetch_incidence<R, PUB>(d, V, pub, L.a, k0, inA, wA, a0, a1);
+  for (int k = k0; k < k1; ++k) {
+    const bool more = (k + 1 < k1);
+    if (more) fetch_incidence<R, PUB>(d, V, pub, L.a, k + 1, inB, wB, b0, b1);
+    const int2 inC = (k + 2 < k1) ? d.inc[k + 2] : inB;
+    Edge E;
+    edge_from_raw(wA, E);
+    const double vo[4] = {a0.x, a0.y, a1.x, a1.y};
+    const bool tail = (inA.y >> 31) & 1;
+    const double c = incidence_row(E, tail, vs, vo, acc);
+    if (cost) *cost += (inA.x >= 0) ? 0.5 * c : c;
+    wA = wB;
+    a0 = b0;
+    a1 = b1;
+    inA = inB;
+    inB = inC;
   }
 }
 
-// ---------------------------------------------------------------- kernels --
+// Incidence-parallel tile gather (variant G = 1). A tile's poses are
+// contiguous, so its incidences are one contiguous CSR range. The tile walks
+// it in chunks of CI = 256 / r incidences:
+//   * the tile's CSR entries and its own pose rows are staged in LDS once;
+//   * per chunk, every edge record is loaded ONCE (8 lanes x 16 B) into LDS,
+//     and lane (incidence i, row a) loads neighbour row a straight into
+//     registers (r lanes read one contiguous 32r-byte pose row);
+//   * lane (i, a) forms its incidence's contribution to row a of the self pose
+//     and parks it in LDS; then each (pose, row) lane adds its pose's
+//     contributions in CSR (= increasing edge id) order — the same order and
+//     the same (exactly negated) terms as the oracle, so results stay bitwise
+//     identical;
+//   * the next chunk's loads are issued before the current chunk is computed.
+template <int R>
+struct Smem {
+  static constexpr int PPW = 64 / R;
+  static constexpr int TP = WAVES * PPW;           // poses per tile
+  static constexpr int CI = BLOCK / R;             // incidences per chunk
+  static constexpr int MAXI = 512;                 // CSR entries staged per segment
+  static constexpr int inc_off = 0;                                   // int2[MAXI]
+  static constexpr int ptr_off = inc_off + MAXI * 8;                  // int[TP + 1]
+  static constexpr int x_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;  // double[TP][R][4]
+  static constexpr int edge_off = x_off + TP * R * 32;                // double[CI][16]
+  static constexpr int con_off = edge_off + CI * 128;                 // double[CI][R][4]
+  static constexpr int red_off = con_off + CI * R * 32;               // double[WAVES] + flag
+  static constexpr int bytes = red_off + 64;
+};
+
+template <int R, bool PUB>
+__device__ __forceinline__ void tile_gather(const Dev& d, const Lane& L, const double* V, const double* pub,
+                                            double acc[4], double* cost, char* smem) {
+  using SM = Smem<R>;
+  constexpr int CI = SM::CI;
+  constexpr int E_IT = (CI * 8 + BLOCK - 1) / BLOCK;
+  int2* sinc = reinterpret_cast<int2*>(smem + SM::inc_off);
+  int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
+  double* sx = reinterpret_cast<double*>(smem + SM::x_off);
+  double* sedge = reinterpret_cast<double*>(smem + SM::edge_off);
+  double* scon = reinterpret_cast<double*>(smem + SM::con_off);
+  const int tid = threadIdx.x;
+  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
+  const int K0 = d.inc_ptr[p0], K1 = d.inc_ptr[p0 + np];
+  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
+  {
+    const double2* src = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
+    double2* dst = reinterpret_cast<double2*>(sx);
+    for (int q = tid; q < np * 2 * R; q += BLOCK) dst[q] = src[q];
+  }
+  int kp0 = 0, kp1 = 0;
+  if (L.valid) {
+    kp0 = d.inc_ptr[L.pose];
+    kp1 = d.inc_ptr[L.pose + 1];
+  }
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  const int ci = tid / R, ca = tid - ci * R;  // compute lane (incidence, row)
+  double csum = 0.0;
+  for (int seg = K0; seg < K1; seg += SM::MAXI) {
+    const int nseg = min(SM::MAXI, K1 - seg);
+    for (int q = tid; q < nseg; q += BLOCK) sinc[q] = d.inc[seg + q];
+    __syncthreads();
+    static_assert(E_IT <= 3, "edge staging assumes <= 3 pieces per lane");
+    double2 eb0 = make_double2(0.0, 0.0), eb1 = eb0, eb2 = eb0, v0 = eb0, v1 = eb0;
+#define KMX_LOAD_CHUNK(CB)                                                                         \
+    {                                                                                              \
+      const int n_ = min(CI, nseg - (CB));                                                         \
+      const double2* er2 = reinterpret_cast<const double2*>(d.irec);                               \
+      {                                                                                            \
+        const int q = tid, qc = (q < n_ * 8) ? q : 0;                                              \
+        eb0 = er2[16 / 2 * (size_t)(seg + (CB) + (qc >> 3)) + (qc & 7)];                          \
+      }                                                                                            \
+      if constexpr (E_IT > 1) {                                                                    \
+        const int q = tid + BLOCK, qc = (q < n_ * 8) ? q : 0;                                      \
+        eb1 = er2[16 / 2 * (size_t)(seg + (CB) + (qc >> 3)) + (qc & 7)];                          \
+      }                                                                                            \
+      if constexpr (E_IT > 2) {                                                                    \
+        const int q = tid + 2 * BLOCK, qc = (q < n_ * 8) ? q : 0;                                  \
+        eb2 = er2[16 / 2 * (size_t)(seg + (CB) + (qc >> 3)) + (qc & 7)];                          \
+      }                                                                                            \
+      const int ic = (ci < n_) ? ci : 0;                                                           \
+      const int o = sinc[(CB) + ic].x;                                                             \
+      const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V); \
+      const double2* b2 = reinterpret_cast<const double2*>(base + 4 * ca);                         \
+      v0 = b2[0];                                                                                  \
+      v1 = b2[1];                                                                                  \
+      if (!PUB && o < 0) v0 = v1 = make_double2(0.0, 0.0);                                         \
+    }
+    KMX_LOAD_CHUNK(0)
+    for (int cb = 0; cb < nseg; cb += CI) {
+      const int n = min(CI, nseg - cb);
+      if (tid < n * 8) reinterpret_cast<double2*>(sedge)[tid] = eb0;
+      if (E_IT > 1 && tid + BLOCK < n * 8) reinterpret_cast<double2*>(sedge)[tid + BLOCK] = eb1;
+      if (E_IT > 2 && tid + 2 * BLOCK < n * 8) reinterpret_cast<double2*>(sedge)[tid + 2 * BLOCK] = eb2;
+      const double2 c0 = v0, c1 = v1;
+      __syncthreads();
+      if (cb + CI < nseg) KMX_LOAD_CHUNK(cb + CI)  // next chunk in flight during compute
+      if (ci < n && tid < CI * R) {
+        const int kk = (seg - K0) + cb + ci;  // tile-relative incidence index
+        int lo = 0, hi = np;                  // self pose: sptr[lo] <= kk < sptr[lo + 1]
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (sptr[mid] <= kk) lo = mid;
+          else hi = mid;
+        }
+        const int2 in = sinc[cb + ci];
+        const bool tail = (in.y >> 31) & 1;
+        const double2* q2 = reinterpret_cast<const double2*>(sedge + 16 * ci);
+        double2 w0 = q2[0], w1 = q2[1], w2 = q2[2], w3 = q2[3], w4 = q2[4], w5 = q2[5], w6 = q2[6];
+        Edge E;
+        E.R[0] = w0.x; E.R[1] = w0.y; E.R[2] = w1.x; E.R[3] = w1.y; E.R[4] = w2.x;
+        E.R[5] = w2.y; E.R[6] = w3.x; E.R[7] = w3.y; E.R[8] = w4.x;
+        E.t[0] = w4.y; E.t[1] = w5.x; E.t[2] = w5.y;
+        E.wk = w6.x;
+        E.wt = w6.y;
+        double vs[4], vo[4] = {c0.x, c0.y, c1.x, c1.y}, con[4] = {0.0, 0.0, 0.0, 0.0};
+        load4(sx + (lo * R + ca) * 4, vs);
+        const double c = incidence_row(E, tail, vs, vo, con);
+        csum += (in.x >= 0) ? 0.5 * c : c;
+        store4(scon + (ci * R + ca) * 4, con);
+      }
+      __syncthreads();
+      if (L.valid) {
+        const int A = seg + cb;
+        const int ka = max(kp0, A), kb = min(kp1, A + n);
+        for (int k = ka; k < kb; ++k) {
+          double cv[4];
+          load4(scon + ((k - A) * R + L.a) * 4, cv);
+          acc[0] += cv[0]; acc[1] += cv[1]; acc[2] += cv[2]; acc[3] += cv[3];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (cost) *cost += csum;
+#undef KMX_LOAD_CHUNK
+}
+
+// Plain direct variant (G = 2, diagnostic): no software pipelining.
+template <int R, bool PUB>
+__device__ __forceinline__ void lane_gather_plain(const Dev& d, const Lane& L, const double* V, const double* pub,
+                                                  double acc[4], double* cost) {
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  if (!L.valid) return;
+  double vs[4];
+  load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
+  const int k0 = d.inc_ptr[L.pose], k1 = d.inc_ptr[L.pose + 1];
+  for (int k = k0; k < k1; ++k) {
+    const int2 in = d.inc[k];
+    EdgeRaw w;
+    double2 b0, b1;
+    fetch_incidence<R, PUB>(d, V, pub, L.a, k, in, w, b0, b1);
+    Edge E;
+    edge_from_raw(w, E);
+    const double vo[4] = {b0.x, b0.y, b1.x, b1.y};
+    const double c = incidence_row(E, (in.y >> 31) & 1, vs, vo, acc);
+    if (cost) *cost += (in.x >= 0) ? 0.5 * c : c;
+  }
+}
+
+template <int R, int G, bool PUB>
+__device__ __forceinline__ void gather(const Dev& d, const Lane& L, const double* V, const double* pub,
+                                       double acc[4], double* cost, char* smem) {
+  if constexpr (G == 0) lane_gather<R, PUB>(d, L, V, pub, acc, cost);
+  else if constexpr (G == 2) lane_gather_plain<R, PUB>(d, L, V, pub, acc, cost);
+  else tile_gather<R, PUB>(d, L, V, pub, acc, cost, smem);
+}
+
+// -------------------------------------------- fused per-robot reductions --
+// Each tile of robot l publishes its partial sums, then takes a ticket on
+// robot l's counter (agent-scope release / acquire, cdna_hip_programming.md
+// Guideline 16). The tile that draws the last ticket reduces robot l's
+// partials in tile order (deterministic) and runs the RTR / tCG scalar logic
+// on thread 0 — no separate reduction launch, robots reduce in parallel.
+__device__ void control(const Dev& d, int l, int kind, const double* tot, int R_);
+
+template <int KIND, int NV, int FUSED>
+__device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const double* vals, char* smem_red,
+                                            int R_) {
+  double* lds = reinterpret_cast<double*>(smem_red);
+  int* flag = reinterpret_cast<int*>(smem_red + 8 * WAVES);
+  double tv[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int s = 0; s < NV; ++s) tv[s] = block_sum(vals[s], lds);
+  if constexpr (!FUSED) {
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int s = 0; s < NV; ++s) d.part[(size_t)L.tile * NPART + s] = tv[s];
+    }
+    return;
+  } else {
+    // Write-through (sc1) partial stores, drained, then one agent-scope
+    // ticket per tile; the last arriver reads the partials with sc1 loads
+    // (MI355X_MICROARCH.md "Valid forms", table row 1).
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int s = 0; s < NV; ++s)
+        __hip_atomic_store(d.part + (size_t)L.tile * NPART + s, tv[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned ntl = (unsigned)(d.rtile0[L.l + 1] - d.rtile0[L.l]);
+      const unsigned t = __hip_atomic_fetch_add(d.tickets + L.l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (t == ntl - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int NS = (KIND == RED_COST) ? 4 : NV;
+    double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+    const int t0 = d.rtile0[L.l], t1 = d.rtile0[L.l + 1];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      double v = 0.0;
+      for (int t = t0 + (int)threadIdx.x; t < t1; t += BLOCK)
+        v += __hip_atomic_load(d.part + (size_t)t * NPART + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tot[s] = block_sum(v, lds);
+    }
+    if (threadIdx.x == 0) {
+      control(d, L.l, KIND, tot, R_);
+      __hip_atomic_store(d.tickets + L.l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__device__ void control(const Dev& d, int l, int kind, const double* tot, int R_) {
+  Ctl& c = d.ctl[l];
+  const Params& P = d.p;
+  if (kind == RED_GRAD) {
+    const double f = tot[0], gn = sqrt(tot[1]);
+    if (c.rtr_iter == 0) { c.f_init = f; c.gn_init = gn; }
+    c.f_cur = f;
+    c.f_final = f;
+    c.commit = 0;
+    if (gn < P.gn_tol) {
+      c.phase = PH_IDLE;
+      c.tcg_stop = KMX_TCG_SKIPPED;
+      c.tcg_iter = 0;
+      c.accepted = 0;
+      c.skipped = 1;
+    } else {
+      c.phase = PH_TCG;
+      c.tcg_iter = 0;
+      c.norm_r0 = gn;
+      c.z_r = tot[2];
+      c.d_Pd = tot[2];
+      c.e_Pd = 0.0;
+      c.e_Pe = 0.0;
+      c.beta = 0.0;
+      c.tcg_stop = KMX_TCG_MAX_ITER;
+      if (c.rtr_iter == 0) {
+        atomicAdd(&d.cnt->edges_iters, (unsigned long long)d.m_robot[l]);
+        atomicAdd(&d.cnt->block_updates, 1ull);
+      }
+    }
+  } else if (kind == RED_HESS) {
+    const double d_Hd = tot[0];
+    const double alpha = c.z_r / d_Hd;
+    const double e_Pe_new = c.e_Pe + 2.0 * alpha * c.e_Pd + alpha * alpha * c.d_Pd;
+    const double D2 = c.Delta * c.Delta;
+    c.tcg_iter += 1;
+    c.hessvecs += 1;
+    atomicAdd(&d.cnt->hessvecs, 1ull);
+    atomicAdd(&d.cnt->hess_alg_bytes, 128.0 * (double)d.m_robot[l] + 2.0 * 8.0 * R_ * 4.0 * (double)d.n_robot[l]);
+    if (d_Hd <= 0.0 || e_Pe_new >= D2) {
+      const double tau = (-c.e_Pd + sqrt(c.e_Pd * c.e_Pd + c.d_Pd * (D2 - c.e_Pe))) / c.d_Pd;
+      c.coef = tau;
+      c.mode = MODE_BOUNDARY;
+      c.tcg_stop = d_Hd <= 0.0 ? KMX_TCG_NEGATIVE_CURVATURE : KMX_TCG_EXCEEDED_TR;
+    } else {
+      c.alpha = alpha;
+      c.coef = alpha;
+      c.e_Pe = e_Pe_new;
+      c.mode = MODE_INTERIOR;
+    }
+  } else if (kind == RED_UPDATE) {
+    if (c.mode == MODE_BOUNDARY) {
+      c.phase = PH_STEP;
+      return;
+    }
+    const double norm_r = sqrt(tot[0]);
+    const double zr_new = tot[1];
+    const double pw = pow(c.norm_r0, P.theta);
+    if (norm_r <= c.norm_r0 * fmin(pw, P.kappa)) {
+      c.tcg_stop = (P.kappa < pw) ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
+      c.phase = PH_STEP;
+    } else if (c.tcg_iter >= P.tcg_max) {
+      c.tcg_stop = KMX_TCG_MAX_ITER;
+      c.phase = PH_STEP;
+    } else {
+      const double beta = zr_new / c.z_r;
+      c.e_Pd = beta * (c.e_Pd + c.alpha * c.d_Pd);
+      c.d_Pd = zr_new + beta * beta * c.d_Pd;
+      c.z_r = zr_new;
+      c.beta = beta;
+    }
+  } else {  // RED_COST: tot[0] = f(Xt), tot[2] = 2 m(eta), tot[3] = ||Xt - X||^2
+    const double ft = tot[0];
+    const double model_dec = -0.5 * tot[2];
+    const double rho = (model_dec > 0.0) ? (c.f_cur - ft) / model_dec : -1.0;
+    const bool boundary = (c.tcg_stop == KMX_TCG_NEGATIVE_CURVATURE || c.tcg_stop == KMX_TCG_EXCEEDED_TR);
+    if (!(rho >= 0.25)) c.Delta *= 0.25;
+    else if (rho > 0.75 && boundary) c.Delta = fmin(2.0 * c.Delta, P.Delta_max);
+    c.rho = rho;
+    if (rho > P.accept_rho) {
+      c.accepted = 1;
+      c.commit = 1;
+      c.f_final = ft;
+      c.chg_acc += tot[3];
+    } else {
+      c.accepted = 0;
+      c.commit = 0;
+      c.f_final = c.f_cur;
+    }
+    c.rtr_iter += 1;
+    c.phase = (c.rtr_iter < P.rtr_iters) ? PH_START : PH_IDLE;
+    c.rel_change = sqrt(c.chg_acc / (double)d.n_robot[l]);
+  }
+}
+
+// Separate-launch reduction (variant F = 0): one workgroup per robot.
+__global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_) {
+  __shared__ double lds[WAVES];
+  const int l = blockIdx.x;
+  const int ph = d.ctl[l].phase;
+  bool act = false;
+  if (kind == RED_GRAD) act = ph == PH_START;
+  if (kind == RED_HESS || kind == RED_UPDATE) act = ph == PH_TCG;
+  if (kind == RED_COST) act = ph == PH_STEP;
+  if (!act) return;
+  const int ns = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
+  double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+  const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
+#pragma unroll
+  for (int s = 0; s < NPART; ++s) {
+    if (s < ns) {
+      double v = 0.0;
+      for (int t = t0 + (int)threadIdx.x; t < t1; t += BLOCK) v += d.part[(size_t)t * NPART + s];
+      tot[s] = block_sum(v, lds);
+    }
+  }
+  if (threadIdx.x == 0) control(d, l, kind, tot, R_);
+}
+
+#define KMX_SMEM extern __shared__ __attribute__((aligned(16))) char smem[]
+
 // Start of an RTR iteration: egrad (gather X with public neighbours), cost,
 // S = sym(Y^T egrad_Y), g = P_Y(egrad), r = g, z = precon(g).
-template <int R>
+template <int R, int GV, int F>
 __global__ __launch_bounds__(BLOCK) void k_grad(Dev d) {
-  __shared__ double lds[WAVES];
+  KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_START) return;
-  double y[4] = {0, 0, 0, 0}, G[4] = {0, 0, 0, 0}, cost = 0.0;
-  if (L.valid) {
-    gather_row<R>(d, L.pose, L.a, d.X, d.pub, G, &cost);
-    load4(d.X + (size_t)L.pose * 4 * R + 4 * L.a, y);
-  }
+  double y[4] = {0, 0, 0, 0}, G[4], cost = 0.0;
+  gather<R, GV, true>(d, L, d.X, d.pub, G, &cost, smem);
+  if (L.valid) load4(d.X + (size_t)L.pose * 4 * R + 4 * L.a, y);
   double S[9], gr[4], zr[4];
   group_symYtG<R>(y, G, L.base, S);
 #pragma unroll
@@ -330,6 +699,13 @@ __global__ __launch_bounds__(BLOCK) void k_grad(Dev d) {
   gr[3] = G[3];
   group_precon<R>(d, L.pose, L.valid, y, gr, L.base, zr);
   double vals[3] = {0.0, 0.0, 0.0};
+  vals[0] = cost;  // the incidence-parallel gather accumulates cost on non-pose lanes too
+  if (L.valid) {
+    vals[1] = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2] + gr[3] * gr[3];
+    vals[2] = zr[0] * gr[0] + zr[1] * gr[1] + zr[2] * gr[2] + zr[3] * gr[3];
+  }
+  // ticket first: the fused reduction's drain then waits only for the partials
+  finish_tile<RED_GRAD, 3, F>(d, L, vals, smem + Smem<R>::red_off, R);
   if (L.valid) {
     const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
     store4(d.g + o, gr);
@@ -340,27 +716,23 @@ __global__ __launch_bounds__(BLOCK) void k_grad(Dev d) {
 #pragma unroll
       for (int i = 0; i < 9; ++i) Sp[i] = S[i];
     }
-    vals[0] = cost;
-    vals[1] = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2] + gr[3] * gr[3];
-    vals[2] = zr[0] * gr[0] + zr[1] * gr[1] + zr[2] * gr[2] + zr[3] * gr[3];
   }
-  write_partials(d, L.tile, vals, 3, lds);
 }
 
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old.
-template <int R>
+template <int R, int GV, int F>
 __global__ __launch_bounds__(BLOCK) void k_hess(Dev d) {
-  __shared__ double lds[WAVES];
+  KMX_SMEM;
   const Lane L = lane_map<R>(d);
   const Ctl& c = d.ctl[L.l];
   if (c.phase != PH_TCG) return;
   const bool first = (c.tcg_iter == 0);
   const double beta = c.beta;
-  double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4] = {0, 0, 0, 0}, S[9];
+  double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4], S[9];
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+  gather<R, GV, false>(d, L, d.z, nullptr, H, nullptr, smem);
   if (L.valid) {
-    gather_row<R>(d, L.pose, L.a, d.z, nullptr, H, nullptr);
     load4(d.z + o, zs);
     load4(d.X + o, y);
     const double* Sp = d.S + 9 * (size_t)L.pose;
@@ -373,8 +745,8 @@ __global__ __launch_bounds__(BLOCK) void k_hess(Dev d) {
   double hz[4];
   group_rhess<R>(y, zs, H, S, L.base, hz);
   double v = 0.0;
+  double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
   if (L.valid) {
-    double dl[4], hdl[4];
     if (first) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) { dl[k] = -zs[k]; hdl[k] = -hz[k]; }
@@ -388,18 +760,20 @@ __global__ __launch_bounds__(BLOCK) void k_hess(Dev d) {
         hdl[k] = -hz[k] + beta * hold[k];
       }
     }
-    store4(d.del + o, dl);
-    store4(d.hd + o, hdl);
     v = dl[0] * hdl[0] + dl[1] * hdl[1] + dl[2] * hdl[2] + dl[3] * hdl[3];
   }
-  write_partials(d, L.tile, &v, 1, lds);
+  finish_tile<RED_HESS, 1, F>(d, L, &v, smem + Smem<R>::red_off, R);
+  if (L.valid) {
+    store4(d.del + o, dl);
+    store4(d.hd + o, hdl);
+  }
 }
 
 // tCG step, part 2: eta += coef delta, r += coef Hdelta; interior steps also
 // z = precon(r) and partial <r,r>, <z,r>.
-template <int R>
+template <int R, int GV, int F>
 __global__ __launch_bounds__(BLOCK) void k_update(Dev d) {
-  __shared__ double lds[WAVES];
+  KMX_SMEM;
   const Lane L = lane_map<R>(d);
   const Ctl& c = d.ctl[L.l];
   if (c.phase != PH_TCG) return;
@@ -407,43 +781,41 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d) {
   const double coef = c.coef;
   const bool interior = (c.mode == MODE_INTERIOR);
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-  double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0};
+  double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0};
   if (L.valid) {
-    double dl[4], hdl[4], et[4];
+    double dl[4], hdl[4];
     load4(d.del + o, dl);
     load4(d.hd + o, hdl);
     load4(d.r + o, rr);
-    if (first) {
-      et[0] = et[1] = et[2] = et[3] = 0.0;
-    } else {
-      load4(d.eta + o, et);
-    }
+    if (!first) load4(d.eta + o, et);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       et[k] += coef * dl[k];
       rr[k] += coef * hdl[k];
     }
-    store4(d.eta + o, et);
-    store4(d.r + o, rr);
     if (interior) load4(d.X + o, y);
   }
-  if (!interior) return;  // uniform per robot
-  double zr[4];
-  group_precon<R>(d, L.pose, L.valid, y, rr, L.base, zr);
-  double vals[2] = {0.0, 0.0};
-  if (L.valid) {
-    store4(d.z + o, zr);
-    vals[0] = rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2] + rr[3] * rr[3];
-    vals[1] = zr[0] * rr[0] + zr[1] * rr[1] + zr[2] * rr[2] + zr[3] * rr[3];
+  double vals[2] = {0.0, 0.0}, zr[4] = {0, 0, 0, 0};
+  if (interior) {  // uniform per robot
+    group_precon<R>(d, L.pose, L.valid, y, rr, L.base, zr);
+    if (L.valid) {
+      vals[0] = rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2] + rr[3] * rr[3];
+      vals[1] = zr[0] * rr[0] + zr[1] * rr[1] + zr[2] * rr[2] + zr[3] * rr[3];
+    }
   }
-  write_partials(d, L.tile, vals, 2, lds);
+  finish_tile<RED_UPDATE, 2, F>(d, L, vals, smem + Smem<R>::red_off, R);
+  if (L.valid) {
+    store4(d.eta + o, et);
+    store4(d.r + o, rr);
+    if (interior) store4(d.z + o, zr);
+  }
 }
 
 // Trial point Xt = R_X(eta); partials: model m(eta) = 1/2 <eta, g + r> (r = g +
-// H eta by the tCG recurrence) and ||Xt - X||^2.
+// H eta by the tCG recurrence) and ||Xt - X||^2 (slots 2, 3; k_cost reduces).
 template <int R>
 __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
-  __shared__ double lds[WAVES];
+  KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
@@ -470,21 +842,21 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
     vals[0] = m;
     vals[1] = ch;
   }
-  // partial slots 2,3 (slot 0 is reused by k_cost)
+  double* lds = reinterpret_cast<double*>(smem + Smem<R>::red_off);
   for (int s = 0; s < 2; ++s) {
     const double t = block_sum(vals[s], lds);
     if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART + 2 + s] = t;
   }
 }
 
-template <int R>
+template <int R, int GV, int F>
 __global__ __launch_bounds__(BLOCK) void k_cost(Dev d) {
-  __shared__ double lds[WAVES];
+  KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
   double acc[4], cost = 0.0;
-  if (L.valid) gather_row<R>(d, L.pose, L.a, d.Xt, d.pub, acc, &cost);
-  write_partials(d, L.tile, &cost, 1, lds);
+  gather<R, GV, true>(d, L, d.Xt, d.pub, acc, &cost, smem);
+  finish_tile<RED_COST, 1, F>(d, L, &cost, smem + Smem<R>::red_off, R);
 }
 
 template <int R>
@@ -498,125 +870,6 @@ __global__ __launch_bounds__(BLOCK) void k_commit(Dev d) {
   store4(d.X + o, v);
 }
 
-// One workgroup: per-robot fixed-order reduction of the tile partials and the
-// RTR / tCG scalar logic (mirrors oracle block_update control flow).
-__global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int track_bytes, int R_) {
-  __shared__ double lds[WAVES];
-  for (int l = 0; l < d.L; ++l) {
-    Ctl& c = d.ctl[l];
-    const int ph = c.phase;
-    bool act = false;
-    if (kind == RED_GRAD) act = ph == PH_START;
-    if (kind == RED_HESS || kind == RED_UPDATE) act = ph == PH_TCG;
-    if (kind == RED_COST) act = ph == PH_STEP;
-    if (!act) continue;
-    if (kind == RED_UPDATE && c.mode == MODE_BOUNDARY) {
-      if (threadIdx.x == 0) c.phase = PH_STEP;
-      __syncthreads();
-      continue;
-    }
-    const int nsum = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
-    double tot[4] = {0.0, 0.0, 0.0, 0.0};
-    const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
-    for (int s = 0; s < nsum; ++s) {
-      double v = 0.0;
-      for (int t = t0 + (int)threadIdx.x; t < t1; t += BLOCK) v += d.part[(size_t)t * NPART + s];
-      tot[s] = block_sum(v, lds);
-    }
-    if (threadIdx.x == 0) {
-      const Params& P = d.p;
-      if (kind == RED_GRAD) {
-        const double f = tot[0], gn = sqrt(tot[1]);
-        if (c.rtr_iter == 0) { c.f_init = f; c.gn_init = gn; }
-        c.f_cur = f;
-        c.f_final = f;
-        c.commit = 0;
-        if (gn < P.gn_tol) {
-          c.phase = PH_IDLE;
-          c.tcg_stop = KMX_TCG_SKIPPED;
-          c.tcg_iter = 0;
-          c.accepted = 0;
-          c.skipped = 1;
-        } else {
-          c.phase = PH_TCG;
-          c.tcg_iter = 0;
-          c.norm_r0 = gn;
-          c.z_r = tot[2];
-          c.d_Pd = tot[2];
-          c.e_Pd = 0.0;
-          c.e_Pe = 0.0;
-          c.beta = 0.0;
-          c.tcg_stop = KMX_TCG_MAX_ITER;
-          if (c.rtr_iter == 0) {
-            d.cnt->edges_iters += (unsigned long long)d.m_robot[l];
-            d.cnt->block_updates += 1ull;
-          }
-        }
-      } else if (kind == RED_HESS) {
-        const double d_Hd = tot[0];
-        const double alpha = c.z_r / d_Hd;
-        const double e_Pe_new = c.e_Pe + 2.0 * alpha * c.e_Pd + alpha * alpha * c.d_Pd;
-        const double D2 = c.Delta * c.Delta;
-        c.tcg_iter += 1;
-        c.hessvecs += 1;
-        d.cnt->hessvecs += 1ull;
-        if (track_bytes)
-          d.cnt->hess_alg_bytes += 128.0 * (double)d.m_robot[l] + 2.0 * 8.0 * R_ * 4.0 * (double)d.n_robot[l];
-        if (d_Hd <= 0.0 || e_Pe_new >= D2) {
-          const double tau = (-c.e_Pd + sqrt(c.e_Pd * c.e_Pd + c.d_Pd * (D2 - c.e_Pe))) / c.d_Pd;
-          c.coef = tau;
-          c.mode = MODE_BOUNDARY;
-          c.tcg_stop = d_Hd <= 0.0 ? KMX_TCG_NEGATIVE_CURVATURE : KMX_TCG_EXCEEDED_TR;
-        } else {
-          c.alpha = alpha;
-          c.coef = alpha;
-          c.e_Pe = e_Pe_new;
-          c.mode = MODE_INTERIOR;
-        }
-      } else if (kind == RED_UPDATE) {
-        const double norm_r = sqrt(tot[0]);
-        const double zr_new = tot[1];
-        const double pw = pow(c.norm_r0, P.theta);
-        if (norm_r <= c.norm_r0 * fmin(pw, P.kappa)) {
-          c.tcg_stop = (P.kappa < pw) ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
-          c.phase = PH_STEP;
-        } else if (c.tcg_iter >= P.tcg_max) {
-          c.tcg_stop = KMX_TCG_MAX_ITER;
-          c.phase = PH_STEP;
-        } else {
-          const double beta = zr_new / c.z_r;
-          c.e_Pd = beta * (c.e_Pd + c.alpha * c.d_Pd);
-          c.d_Pd = zr_new + beta * beta * c.d_Pd;
-          c.z_r = zr_new;
-          c.beta = beta;
-        }
-      } else {  // RED_COST: tot[0] = f(Xt), tot[2] = 2 m(eta), tot[3] = ||Xt-X||^2
-        const double ft = tot[0];
-        const double model_dec = -0.5 * tot[2];
-        const double rho = (model_dec > 0.0) ? (c.f_cur - ft) / model_dec : -1.0;
-        const bool boundary = (c.tcg_stop == KMX_TCG_NEGATIVE_CURVATURE || c.tcg_stop == KMX_TCG_EXCEEDED_TR);
-        if (!(rho >= 0.25)) c.Delta *= 0.25;
-        else if (rho > 0.75 && boundary) c.Delta = fmin(2.0 * c.Delta, P.Delta_max);
-        c.rho = rho;
-        if (rho > P.accept_rho) {
-          c.accepted = 1;
-          c.commit = 1;
-          c.f_final = ft;
-          c.chg_acc += tot[3];
-        } else {
-          c.accepted = 0;
-          c.commit = 0;
-          c.f_final = c.f_cur;
-        }
-        c.rtr_iter += 1;
-        c.phase = (c.rtr_iter < P.rtr_iters) ? PH_START : PH_IDLE;
-        c.rel_change = sqrt(c.chg_acc / (double)d.n_robot[l]);
-      }
-    }
-    __syncthreads();
-  }
-}
-
 __global__ void k_round_begin(Dev d, const unsigned char* active) {
   const int l = threadIdx.x;
   if (l >= d.L) return;
@@ -627,6 +880,21 @@ __global__ void k_round_begin(Dev d, const unsigned char* active) {
   c.phase = a ? PH_START : PH_IDLE;
   c.updated = a ? 1 : 0;
   c.Delta = d.p.Delta0;
+}
+
+// Host-visible progress word after a tCG step: number of robots still in
+// tCG, tagged with a sequence number (system-scope stores into host-mapped
+// memory). The host enqueues further tCG steps only while robots remain.
+struct HostStatus {
+  unsigned long long seq;
+  unsigned long long running;
+};
+__global__ void k_status(Dev d, HostStatus* hs, unsigned long long seq) {
+  if (threadIdx.x != 0) return;
+  unsigned long long n = 0;
+  for (int l = 0; l < d.L; ++l) n += (d.ctl[l].phase == PH_TCG) ? 1ull : 0ull;
+  __hip_atomic_store(&hs->running, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&hs->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_publish(const double* X, double* pub, const int* src, int nslots, int ps) {
@@ -656,9 +924,8 @@ __global__ void k_precond(Dev d) {
   for (int k = d.inc_ptr[pose]; k < d.inc_ptr[pose + 1]; ++k) {
     const int2 in = d.inc[k];
     const bool tail = (in.y >> 31) & 1;
-    const int e = in.y & 0x7fffffff;
-    const double* er = d.erec + 16 * (size_t)e;
-    const double wk = er[14] * er[12], wt = er[14] * er[13];
+    const double* er = d.irec + 16 * (size_t)k;
+    const double wk = er[12], wt = er[13];
     const double* tt = er + 9;
     if (tail) {
       for (int i = 0; i < 3; ++i) {
@@ -701,16 +968,16 @@ __global__ void k_precond(Dev d) {
 
 // GNC-TLS weight sweep over owned non-fixed local edges (owner's view of the
 // endpoints: its own robot from X, the other robot from the public table).
-__global__ void k_gnc(double* erec, const int* gnc_edge, const int2* gnc_ends, int n, const double* X,
-                      const double* pub, int R_, double mu, double barc) {
+__global__ void k_gnc(Dev d, const int* gnc_edge, const int2* gnc_ends, int n, int R_, double mu, double barc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int e = gnc_edge[i];
   const int2 en = gnc_ends[i];
   const int ps = 4 * R_;
-  const double* Xi = en.x >= 0 ? X + (size_t)en.x * ps : pub + (size_t)(-1 - en.x) * ps;
-  const double* Xj = en.y >= 0 ? X + (size_t)en.y * ps : pub + (size_t)(-1 - en.y) * ps;
-  double* er = erec + 16 * (size_t)e;
+  const double* Xi = en.x >= 0 ? d.X + (size_t)en.x * ps : d.pub + (size_t)(-1 - en.x) * ps;
+  const double* Xj = en.y >= 0 ? d.X + (size_t)en.y * ps : d.pub + (size_t)(-1 - en.y) * ps;
+  const int2 ip = d.eipos[e];
+  const double* er = d.irec + 16 * (size_t)(ip.x >= 0 ? ip.x : ip.y);
   const double* Rt = er;
   const double* tt = er + 9;
   double sR = 0.0, sT = 0.0;
@@ -724,7 +991,7 @@ __global__ void k_gnc(double* erec, const int* gnc_edge, const int2* gnc_ends, i
     const double et = yj[3] - yi[3] - (yi[0] * tt[0] + yi[1] * tt[1] + yi[2] * tt[2]);
     sT += et * et;
   }
-  const double rSq = er[12] * sR + er[13] * sT;
+  const double rSq = d.ekappa[e] * sR + d.etau[e] * sT;
   const double barcSq = barc * barc;
   const double upper = (mu + 1.0) / mu * barcSq;
   const double lower = mu / (mu + 1.0) * barcSq;
@@ -732,18 +999,29 @@ __global__ void k_gnc(double* erec, const int* gnc_edge, const int2* gnc_ends, i
   if (rSq >= upper) w = 0.0;
   else if (rSq <= lower) w = 1.0;
   else w = sqrt(barcSq * mu * (mu + 1.0) / rSq) - mu;
-  er[14] = w;
+  d.ew[e] = w;
 }
 
-__global__ void k_shared_pack(const double* erec, const int* sh_edge, const int* sh_idx, int n, double* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  out[sh_idx[i]] = erec[16 * (size_t)sh_edge[i] + 14];
+// Push the per-edge weights into both incidence copies (w*kappa, w*tau).
+__global__ void k_apply_weights(Dev d, int mloc) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= mloc) return;
+  const double w = d.ew[e];
+  const double wk = w * d.ekappa[e], wt = w * d.etau[e];
+  const int2 ip = d.eipos[e];
+  if (ip.x >= 0) { d.irec[16 * (size_t)ip.x + 12] = wk; d.irec[16 * (size_t)ip.x + 13] = wt; }
+  if (ip.y >= 0) { d.irec[16 * (size_t)ip.y + 12] = wk; d.irec[16 * (size_t)ip.y + 13] = wt; }
 }
-__global__ void k_shared_unpack(double* erec, const int* sh_edge, const int* sh_idx, int n, const double* tab) {
+
+__global__ void k_shared_pack(const double* ew, const int* sh_edge, const int* sh_idx, int n, double* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  erec[16 * (size_t)sh_edge[i] + 14] = tab[sh_idx[i]];
+  out[sh_idx[i]] = ew[sh_edge[i]];
+}
+__global__ void k_shared_unpack(double* ew, const int* sh_edge, const int* sh_idx, int n, const double* tab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  ew[sh_edge[i]] = tab[sh_idx[i]];
 }
 
 // --- rounding to SE(3) in the anchor frame (same algorithm as the oracle) --
@@ -820,25 +1098,23 @@ __global__ void k_traj(const double* X, int n, int R_, const double* anchor, dou
   o[9] = tv[0]; o[10] = tv[1]; o[11] = tv[2];
 }
 
-// Primitive evaluation for parity tests, one robot (tiles t0..t1 via grid).
-template <int R>
+// Primitive evaluation for parity tests (tiles of one robot).
+template <int R, int GV>
 __global__ __launch_bounds__(BLOCK) void k_eval(Dev d, int robot, int mode, const double* V, double* out) {
-  __shared__ double lds[WAVES];
+  KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (L.l != robot) return;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   double res[4] = {0, 0, 0, 0}, cost = 0.0, v[4] = {0, 0, 0, 0};
   if (mode == KMX_EVAL_COST_EGRAD) {
-    if (L.valid) gather_row<R>(d, L.pose, L.a, V, d.pub, res, &cost);
+    gather<R, GV, true>(d, L, V, d.pub, res, &cost, smem);
   } else if (mode == KMX_EVAL_EHESS) {
-    if (L.valid) {
-      gather_row<R>(d, L.pose, L.a, V, nullptr, res, nullptr);
-      load4(V + o, v);
-    }
+    gather<R, GV, false>(d, L, V, nullptr, res, nullptr, smem);
+    if (L.valid) load4(V + o, v);
   } else {
-    double y[4] = {0, 0, 0, 0}, G[4] = {0, 0, 0, 0};
+    double y[4] = {0, 0, 0, 0}, G[4];
+    gather<R, GV, true>(d, L, d.X, d.pub, G, nullptr, smem);
     if (L.valid) {
-      gather_row<R>(d, L.pose, L.a, d.X, d.pub, G, nullptr);
       load4(d.X + o, y);
       load4(V + o, v);
     }
@@ -849,8 +1125,8 @@ __global__ __launch_bounds__(BLOCK) void k_eval(Dev d, int robot, int mode, cons
       res[3] = G[3];
       for (int k = 0; k < 4; ++k) v[k] = res[k];
     } else if (mode == KMX_EVAL_RHESS) {
-      double H[4] = {0, 0, 0, 0};
-      if (L.valid) gather_row<R>(d, L.pose, L.a, V, nullptr, H, nullptr);
+      double H[4];
+      gather<R, GV, false>(d, L, V, nullptr, H, nullptr, smem);
       group_rhess<R>(y, v, H, S, L.base, res);
     } else if (mode == KMX_EVAL_PRECON) {
       group_precon<R>(d, L.pose, L.valid, y, v, L.base, res);
@@ -859,12 +1135,54 @@ __global__ __launch_bounds__(BLOCK) void k_eval(Dev d, int robot, int mode, cons
       for (int k = 0; k < 4; ++k) v[k] = 0.0;
     }
   }
-  double s = 0.0;
+  double s = (mode == KMX_EVAL_COST_EGRAD) ? cost : 0.0;
   if (L.valid) {
     store4(out + o, res);
-    s = (mode == KMX_EVAL_COST_EGRAD) ? cost : v[0] * res[0] + v[1] * res[1] + v[2] * res[2] + v[3] * res[3];
+    if (mode != KMX_EVAL_COST_EGRAD) s = v[0] * res[0] + v[1] * res[1] + v[2] * res[2] + v[3] * res[3];
   }
-  write_partials(d, L.tile, &s, 1, lds);
+  const double t = block_sum(s, reinterpret_cast<double*>(smem + Smem<R>::red_off));
+  if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
+}
+
+// Diagnostic ablation of the plain direct gather: ABL bit0 -> every edge load
+// reads record 0 (cache-resident), bit1 -> neighbour row = own row.
+template <int R, int ABL>
+__global__ __launch_bounds__(BLOCK) void k_gablate(Dev d, const double* V, double* out) {
+  KMX_SMEM;
+  const Lane L = lane_map<R>(d);
+  double acc[4] = {0, 0, 0, 0}, cost = 0.0;
+  if (L.valid) {
+    double vs[4];
+    load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
+    const int k0 = d.inc_ptr[L.pose], k1 = d.inc_ptr[L.pose + 1];
+    for (int k = k0; k < k1; ++k) {
+      int2 in = d.inc[k];
+      if (ABL & 2) in.x = L.pose;
+      EdgeRaw w;
+      double2 b0, b1;
+      fetch_incidence<R, true>(d, V, d.pub, L.a, (ABL & 1) ? 0 : k, in, w, b0, b1);
+      Edge E;
+      edge_from_raw(w, E);
+      const double vo[4] = {b0.x, b0.y, b1.x, b1.y};
+      cost += incidence_row(E, (in.y >> 31) & 1, vs, vo, acc);
+    }
+    store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
+  }
+  const double t = block_sum(cost, reinterpret_cast<double*>(smem + Smem<R>::red_off));
+  if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
+}
+
+// Diagnostic: the gather primitive alone (as in k_cost), for A/B timing of
+// gather variants and occupancy bounds (kmx_pgo_debug_gather_bench).
+template <int R, int GV, int LBW>
+__global__ __launch_bounds__(BLOCK, LBW) void k_gbench(Dev d, const double* V, double* out) {
+  KMX_SMEM;
+  const Lane L = lane_map<R>(d);
+  double acc[4], cost = 0.0;
+  gather<R, GV, true>(d, L, V, d.pub, acc, &cost, smem);
+  if (L.valid) store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
+  const double t = block_sum(cost, reinterpret_cast<double*>(smem + Smem<R>::red_off));
+  if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
 }
 
 }  // namespace
@@ -890,7 +1208,8 @@ struct kmx_pgo {
   // local edges
   int mloc = 0;
   std::vector<int64_t> loc_edge_gid;
-  std::vector<double> erec_h;
+  std::vector<double> ek_h, et_h;  // per local edge kappa / tau
+  int ninc = 0;
   int64_t nshared = 0;
   int n_sh_local = 0, n_gnc = 0;
   std::vector<long long> m_robot;
@@ -902,11 +1221,14 @@ struct kmx_pgo {
   int *d_tile_robot = nullptr, *d_tile_p0 = nullptr, *d_tile_np = nullptr, *d_rtile0 = nullptr;
   int* d_inc_ptr = nullptr;
   int2* d_inc = nullptr;
-  double* d_erec = nullptr;
+  double* d_irec = nullptr;
+  double *d_ekappa = nullptr, *d_etau = nullptr, *d_ew = nullptr;
+  int2* d_eipos = nullptr;
   double* d_vec = nullptr;  // X Xt g r z eta del hd
   double *d_S = nullptr, *d_Pinv = nullptr, *d_pub = nullptr, *d_part = nullptr;
   Ctl* d_ctl = nullptr;
   Counters* d_cnt = nullptr;
+  unsigned* d_tickets = nullptr;
   long long* d_m_robot = nullptr;
   int* d_n_robot = nullptr;
   int* d_pub_src = nullptr;  // slot -> local pose (-1 if not local)
@@ -918,6 +1240,13 @@ struct kmx_pgo {
   int n_osh = 0;
   unsigned char* d_active = nullptr;
   double* d_scratch = nullptr;  // eval in/out
+  // kernel variants (KMX_GATHER: 0 direct / 1 LDS-staged; KMX_FUSED: 0 separate
+  // reduce launch / 1 last-arriving-tile reduction)
+  int gvar = 2, fvar = 0;
+  HostStatus* hstat = nullptr;  // host-mapped progress word
+  unsigned long long seq = 0;
+  bool poll = true;             // KMX_POLL=0 enqueues every tCG step blindly
+  bool poll_timeout = false;
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -937,21 +1266,16 @@ int dalloc(T** p, size_t count) {
 
 void free_dev(kmx_pgo* h) {
   void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_inc,
-                  h->d_erec, h->d_vec, h->d_S, h->d_Pinv, h->d_pub, h->d_part, h->d_ctl, h->d_cnt,
+                  h->d_irec, h->d_ekappa, h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_pub, h->d_part, h->d_ctl, h->d_cnt,
                   h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src, h->d_gnc_edge, h->d_gnc_ends,
-                  h->d_sh_edge, h->d_sh_idx, h->d_osh_edge, h->d_osh_idx, h->d_active, h->d_scratch};
+                  h->d_sh_edge, h->d_sh_idx, h->d_osh_edge, h->d_osh_idx, h->d_active, h->d_scratch, h->d_tickets};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
-  h->d_inc = nullptr; h->d_erec = h->d_vec = h->d_S = h->d_Pinv = h->d_pub = h->d_part = nullptr;
+  h->d_inc = nullptr; h->d_eipos = nullptr; h->d_irec = h->d_ekappa = h->d_etau = h->d_ew = nullptr; h->d_vec = h->d_S = h->d_Pinv = h->d_pub = h->d_part = nullptr;
   h->d_ctl = nullptr; h->d_cnt = nullptr; h->d_m_robot = nullptr; h->d_n_robot = nullptr;
   h->d_pub_src = h->d_own_src = h->d_gnc_edge = nullptr; h->d_gnc_ends = nullptr;
-  h->d_sh_edge = h->d_sh_idx = nullptr; h->d_osh_edge = h->d_osh_idx = nullptr; h->d_active = nullptr; h->d_scratch = nullptr;
-}
-
-template <int R>
-void launch_tiles(kmx_pgo* h, void (*kern)(Dev)) {
-  hipLaunchKernelGGL(kern, dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv);
+  h->d_sh_edge = h->d_sh_idx = nullptr; h->d_osh_edge = h->d_osh_idx = nullptr; h->d_active = nullptr; h->d_scratch = nullptr; h->d_tickets = nullptr;
 }
 
 #define KMX_DISPATCH_R(R_, CALL) \
@@ -964,10 +1288,6 @@ void launch_tiles(kmx_pgo* h, void (*kern)(Dev)) {
     case 8: { constexpr int RR = 8; CALL; } break; \
     default: break;              \
   }
-
-void reduce(kmx_pgo* h, int kind, int track) {
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(BLOCK), 0, h->stream, h->dv, kind, track, h->P.r);
-}
 
 hipEvent_t next_event(kmx_pgo* h) {
   if (h->ev_used == h->ev_pool.size()) {
@@ -991,40 +1311,106 @@ void enqueue_precond(kmx_pgo* h) {
   hipLaunchKernelGGL(k_precond, dim3((h->nloc + 127) / 128), dim3(128), 0, h->stream, h->dv);
 }
 
+void enqueue_apply_weights(kmx_pgo* h) {
+  if (h->mloc > 0)
+    hipLaunchKernelGGL(k_apply_weights, dim3((h->mloc + 255) / 256), dim3(256), 0, h->stream, h->dv, h->mloc);
+  enqueue_precond(h);
+}
+
 void enqueue_gnc(kmx_pgo* h) {
   if (h->n_gnc > 0)
-    hipLaunchKernelGGL(k_gnc, dim3((h->n_gnc + 255) / 256), dim3(256), 0, h->stream, h->d_erec,
-                       h->d_gnc_edge, h->d_gnc_ends, h->n_gnc, (const double*)h->d_vec,
-                       (const double*)h->d_pub, h->P.r, h->mu, h->P.gnc_barc);
+    hipLaunchKernelGGL(k_gnc, dim3((h->n_gnc + 255) / 256), dim3(256), 0, h->stream, h->dv, h->d_gnc_edge,
+                       h->d_gnc_ends, h->n_gnc, h->P.r, h->mu, h->P.gnc_barc);
   h->mu *= h->P.gnc_mu_step;
-  enqueue_precond(h);
+  enqueue_apply_weights(h);
+}
+
+template <int R, int G, int F>
+void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
+  const dim3 grid(h->ntiles), blk(BLOCK);
+  const size_t sm = Smem<R>::bytes;
+  auto red = [&](int kind) {
+    if (!F) hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(BLOCK), 0, h->stream, h->dv, kind, R);
+  };
+  auto tcg_step = [&]() {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->timing) {
+      e0 = next_event(h);
+      e1 = next_event(h);
+      (void)hipEventRecord(e0, h->stream);
+    }
+    hipLaunchKernelGGL((k_hess<R, G, F>), grid, blk, sm, h->stream, h->dv);
+    if (h->timing) (void)hipEventRecord(e1, h->stream);
+    red(RED_HESS);
+    hipLaunchKernelGGL((k_update<R, G, F>), grid, blk, sm, h->stream, h->dv);
+    red(RED_UPDATE);
+    if (h->poll) {
+      h->seq += 1;
+      hipLaunchKernelGGL(k_status, dim3(1), dim3(64), 0, h->stream, h->dv, h->hstat, h->seq);
+    }
+    return h->seq;
+  };
+  auto wait_running = [&](unsigned long long seq) -> unsigned long long {
+    volatile HostStatus* hs = h->hstat;
+    (void)hipStreamQuery(h->stream);  // make sure queued work is submitted
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) < seq) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+        h->poll_timeout = true;  // device stalled: stop polling, enqueue blindly
+        h->poll = false;
+        return 1ull;
+      }
+    }
+    return hs->running;
+  };
+  hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(std::max(64, ((h->dv.L + 63) / 64) * 64)), 0, h->stream,
+                     h->dv, d_active);
+  for (int it = 0; it < h->P.rtr_iterations; ++it) {
+    hipLaunchKernelGGL((k_grad<R, G, F>), grid, blk, sm, h->stream, h->dv);
+    red(RED_GRAD);
+    const int J = h->P.tcg_max_iterations;
+    if (!h->poll) {
+      for (int j = 0; j < J; ++j) tcg_step();
+    } else {
+      // Keep exactly one tCG step queued beyond the last one known to be
+      // needed; stop enqueuing once every robot has left tCG.
+      unsigned long long s_prev = tcg_step();
+      int issued = 1;
+      while (issued < J) {
+        const unsigned long long s_next = tcg_step();
+        ++issued;
+        if (wait_running(s_prev) == 0) break;
+        s_prev = s_next;
+      }
+    }
+    hipLaunchKernelGGL((k_retract<R>), grid, blk, sm, h->stream, h->dv);
+    hipLaunchKernelGGL((k_cost<R, G, F>), grid, blk, sm, h->stream, h->dv);
+    red(RED_COST);
+    hipLaunchKernelGGL((k_commit<R>), grid, blk, 0, h->stream, h->dv);
+  }
+}
+
+template <int R>
+void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
+  switch (h->gvar * 2 + h->fvar) {
+    case 0: enqueue_round_t<R, 0, 0>(h, d_active); break;
+    case 1: enqueue_round_t<R, 0, 1>(h, d_active); break;
+    case 2: enqueue_round_t<R, 1, 0>(h, d_active); break;
+    case 3: enqueue_round_t<R, 1, 1>(h, d_active); break;
+    case 4: enqueue_round_t<R, 2, 0>(h, d_active); break;
+    default: enqueue_round_t<R, 2, 1>(h, d_active); break;
+  }
 }
 
 // One RBCD round for the robots whose d_active flag is set.
 void enqueue_round(kmx_pgo* h, const unsigned char* d_active) {
-  const int R_ = h->P.r;
-  hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(std::max(64, ((h->dv.L + 63) / 64) * 64)), 0, h->stream,
-                     h->dv, d_active);
-  for (int it = 0; it < h->P.rtr_iterations; ++it) {
-    KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_grad<RR>));
-    reduce(h, RED_GRAD, 0);
-    for (int j = 0; j < h->P.tcg_max_iterations; ++j) {
-      hipEvent_t e0 = nullptr, e1 = nullptr;
-      if (h->timing) {
-        e0 = next_event(h);
-        e1 = next_event(h);
-        (void)hipEventRecord(e0, h->stream);
-      }
-      KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_hess<RR>));
-      if (h->timing) (void)hipEventRecord(e1, h->stream);
-      reduce(h, RED_HESS, h->timing ? 1 : 0);
-      KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_update<RR>));
-      reduce(h, RED_UPDATE, 0);
-    }
-    KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_retract<RR>));
-    KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_cost<RR>));
-    reduce(h, RED_COST, 0);
-    KMX_DISPATCH_R(R_, launch_tiles<RR>(h, k_commit<RR>));
+  switch (h->P.r) {
+    case 3: enqueue_round_r<3>(h, d_active); break;
+    case 4: enqueue_round_r<4>(h, d_active); break;
+    case 5: enqueue_round_r<5>(h, d_active); break;
+    case 6: enqueue_round_r<6>(h, d_active); break;
+    case 7: enqueue_round_r<7>(h, d_active); break;
+    default: enqueue_round_r<8>(h, d_active); break;
   }
 }
 
@@ -1054,6 +1440,17 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     return kmx::fail(KMX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
   h->own_stream = true;
+  if (const char* v = std::getenv("KMX_GATHER")) h->gvar = std::min(2, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("KMX_FUSED")) h->fvar = std::atoi(v) ? 1 : 0;
+  if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->hstat), sizeof(HostStatus),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    (void)hipStreamDestroy(h->stream);
+    delete h;
+    return kmx::fail(KMX_ENOMEM, "hipHostMalloc(status) failed");
+  }
+  h->hstat->seq = 0;
+  h->hstat->running = 0;
   *out = h;
   return KMX_OK;
   KMX_GUARD_END
@@ -1066,6 +1463,7 @@ extern "C" int kmx_pgo_destroy(kmx_pgo* h) {
   free_dev(h);
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->hstat) (void)hipHostFree(h->hstat);
   delete h;
   return KMX_OK;
 }
@@ -1159,37 +1557,49 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     if (h->local_of[r1[e]] >= 0 || h->local_of[r2[e]] >= 0) ledges.push_back(e);
   h->mloc = (int)ledges.size();
   h->loc_edge_gid = ledges;
-  h->erec_h.assign((size_t)h->mloc * 16, 0.0);
+  h->ek_h.assign(std::max(h->mloc, 1), 0.0);
+  h->et_h.assign(std::max(h->mloc, 1), 0.0);
+  std::vector<double> ew_h(std::max(h->mloc, 1), 0.0);
   std::vector<int> deg(nloc + 1, 0);
   h->m_robot.assign(L, 0);
-  std::vector<int> shared_index_of_gid;  // computed lazily below
   for (int k = 0; k < h->mloc; ++k) {
     const int64_t e = ledges[k];
-    double* rec = &h->erec_h[(size_t)k * 16];
-    for (int q = 0; q < 9; ++q) rec[q] = R[9 * e + q];
-    for (int q = 0; q < 3; ++q) rec[9 + q] = t[3 * e + q];
-    rec[12] = kappa[e];
-    rec[13] = tau[e];
-    rec[14] = weight[e];
+    h->ek_h[k] = kappa[e];
+    h->et_h[k] = tau[e];
+    ew_h[k] = weight[e];
     const int a1 = h->local_of[r1[e]], a2 = h->local_of[r2[e]];
     if (a1 >= 0) { deg[lpose(r1[e], p1[e])]++; h->m_robot[a1]++; }
     if (a2 >= 0) { deg[lpose(r2[e], p2[e])]++; if (r2[e] != r1[e]) h->m_robot[a2]++; }
   }
   std::vector<int> inc_ptr(nloc + 1, 0);
   for (int i = 0; i < nloc; ++i) inc_ptr[i + 1] = inc_ptr[i] + deg[i];
+  h->ninc = inc_ptr[nloc];
   std::vector<int2> inc(std::max(inc_ptr[nloc], 1));
+  std::vector<double> irec((size_t)std::max(inc_ptr[nloc], 1) * 16, 0.0);
+  std::vector<int2> eipos(std::max(h->mloc, 1), make_int2(-1, -1));
   std::vector<int> fill(inc_ptr.begin(), inc_ptr.end() - 1);
+  auto put_rec = [&](int pos, int64_t e) {  // per-incidence copy of the edge record
+    double* rec = &irec[(size_t)pos * 16];
+    for (int q = 0; q < 9; ++q) rec[q] = R[9 * e + q];
+    for (int q = 0; q < 3; ++q) rec[9 + q] = t[3 * e + q];
+    rec[12] = weight[e] * kappa[e];
+    rec[13] = weight[e] * tau[e];
+  };
   for (int k = 0; k < h->mloc; ++k) {  // increasing global edge id per pose
     const int64_t e = ledges[k];
     const bool priv = r1[e] == r2[e];
     if (h->local_of[r1[e]] >= 0) {
       const int sp = lpose(r1[e], p1[e]);
       const int other = priv ? lpose(r2[e], p2[e]) : (int)(-1 - slot_of(r2[e], p2[e]));
+      eipos[k].x = fill[sp];
+      put_rec(fill[sp], e);
       inc[fill[sp]++] = make_int2(other, (int)(k | 0x80000000u));
     }
     if (h->local_of[r2[e]] >= 0) {
       const int sp = lpose(r2[e], p2[e]);
       const int other = priv ? lpose(r1[e], p1[e]) : (int)(-1 - slot_of(r1[e], p1[e]));
+      eipos[k].y = fill[sp];
+      put_rec(fill[sp], e);
       inc[fill[sp]++] = make_int2(other, k);
     }
   }
@@ -1254,12 +1664,14 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   if ((rc = dalloc(&h->d_tile_robot, h->ntiles)) || (rc = dalloc(&h->d_tile_p0, h->ntiles)) ||
       (rc = dalloc(&h->d_tile_np, h->ntiles)) || (rc = dalloc(&h->d_rtile0, L + 1)) ||
       (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_inc, inc.size())) ||
-      (rc = dalloc(&h->d_erec, (size_t)std::max(h->mloc, 1) * 16)) || (rc = dalloc(&h->d_vec, vec * 8)) ||
+      (rc = dalloc(&h->d_irec, irec.size())) || (rc = dalloc(&h->d_ekappa, h->ek_h.size())) ||
+      (rc = dalloc(&h->d_etau, h->et_h.size())) || (rc = dalloc(&h->d_ew, ew_h.size())) ||
+      (rc = dalloc(&h->d_eipos, eipos.size())) || (rc = dalloc(&h->d_vec, vec * 8)) ||
       (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 9)) ||
       (rc = dalloc(&h->d_Pinv, (size_t)std::max(nloc, 1) * 16)) ||
       (rc = dalloc(&h->d_pub, (size_t)std::max<int64_t>(h->npub, 1) * ps)) ||
       (rc = dalloc(&h->d_part, (size_t)std::max(h->ntiles, 1) * NPART)) || (rc = dalloc(&h->d_ctl, L)) ||
-      (rc = dalloc(&h->d_cnt, 1)) || (rc = dalloc(&h->d_m_robot, L)) || (rc = dalloc(&h->d_n_robot, L)) ||
+      (rc = dalloc(&h->d_cnt, 1)) || (rc = dalloc(&h->d_tickets, L)) || (rc = dalloc(&h->d_m_robot, L)) || (rc = dalloc(&h->d_n_robot, L)) ||
       (rc = dalloc(&h->d_pub_src, pub_src.size())) || (rc = dalloc(&h->d_own_src, own_src.size())) ||
       (rc = dalloc(&h->d_gnc_edge, std::max(h->n_gnc, 1))) ||
       (rc = dalloc(&h->d_gnc_ends, std::max(h->n_gnc, 1))) ||
@@ -1279,11 +1691,16 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(up(h->d_rtile0, rt0.data(), sizeof(int) * rt0.size()));
   KMX_HIP(up(h->d_inc_ptr, inc_ptr.data(), sizeof(int) * inc_ptr.size()));
   KMX_HIP(up(h->d_inc, inc.data(), sizeof(int2) * inc.size()));
-  if (h->mloc) KMX_HIP(up(h->d_erec, h->erec_h.data(), sizeof(double) * h->erec_h.size()));
+  KMX_HIP(up(h->d_irec, irec.data(), sizeof(double) * irec.size()));
+  KMX_HIP(up(h->d_ekappa, h->ek_h.data(), sizeof(double) * h->ek_h.size()));
+  KMX_HIP(up(h->d_etau, h->et_h.data(), sizeof(double) * h->et_h.size()));
+  KMX_HIP(up(h->d_ew, ew_h.data(), sizeof(double) * ew_h.size()));
+  KMX_HIP(up(h->d_eipos, eipos.data(), sizeof(int2) * eipos.size()));
   KMX_HIP(hipMemsetAsync(h->d_vec, 0, sizeof(double) * vec * 8, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_pub, 0, sizeof(double) * std::max<int64_t>(h->npub, 1) * ps, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_ctl, 0, sizeof(Ctl) * L, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_cnt, 0, sizeof(Counters), h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_tickets, 0, sizeof(unsigned) * L, h->stream));
   KMX_HIP(up(h->d_m_robot, h->m_robot.data(), sizeof(long long) * L));
   KMX_HIP(up(h->d_n_robot, nrob.data(), sizeof(int) * L));
   KMX_HIP(up(h->d_pub_src, pub_src.data(), sizeof(int) * pub_src.size()));
@@ -1307,10 +1724,11 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   Dev& d = h->dv;
   d.ntiles = h->ntiles; d.L = L; d.nloc = nloc; d.npub = (int)h->npub;
   d.tile_robot = h->d_tile_robot; d.tile_p0 = h->d_tile_p0; d.tile_np = h->d_tile_np; d.rtile0 = h->d_rtile0;
-  d.inc_ptr = h->d_inc_ptr; d.inc = h->d_inc; d.erec = h->d_erec;
+  d.inc_ptr = h->d_inc_ptr; d.inc = h->d_inc; d.irec = h->d_irec;
+  d.ekappa = h->d_ekappa; d.etau = h->d_etau; d.ew = h->d_ew; d.eipos = h->d_eipos;
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
   d.z = h->d_vec + 4 * vec; d.eta = h->d_vec + 5 * vec; d.del = h->d_vec + 6 * vec; d.hd = h->d_vec + 7 * vec;
-  d.S = h->d_S; d.Pinv = h->d_Pinv; d.pub = h->d_pub; d.part = h->d_part; d.ctl = h->d_ctl; d.cnt = h->d_cnt;
+  d.S = h->d_S; d.Pinv = h->d_Pinv; d.pub = h->d_pub; d.part = h->d_part; d.ctl = h->d_ctl; d.cnt = h->d_cnt; d.tickets = h->d_tickets;
   d.m_robot = h->d_m_robot; d.n_robot = h->d_n_robot;
   d.p.tcg_max = h->P.tcg_max_iterations; d.p.rtr_iters = h->P.rtr_iterations;
   d.p.use_precond = h->P.use_preconditioner; d.p.robust = h->P.robust_cost;
@@ -1505,10 +1923,10 @@ extern "C" int kmx_pgo_get_weights(kmx_pgo* h, double* w) {
   KMX_GUARD_BEGIN
   KMX_CHECK(ready(h) && w, KMX_EINVAL, "null argument / no graph");
   KMX_HIP(hipSetDevice(h->device));
-  KMX_HIP(hipMemcpyAsync(h->erec_h.data(), h->d_erec, sizeof(double) * h->erec_h.size(), hipMemcpyDeviceToHost,
-                         h->stream));
+  std::vector<double> ew(std::max(h->mloc, 1));
+  KMX_HIP(hipMemcpyAsync(ew.data(), h->d_ew, sizeof(double) * h->mloc, hipMemcpyDeviceToHost, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  for (int k = 0; k < h->mloc; ++k) w[h->loc_edge_gid[k]] = h->erec_h[(size_t)k * 16 + 14];
+  for (int k = 0; k < h->mloc; ++k) w[h->loc_edge_gid[k]] = ew[k];
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -1516,13 +1934,10 @@ extern "C" int kmx_pgo_get_weights(kmx_pgo* h, double* w) {
 extern "C" int kmx_pgo_set_weights(kmx_pgo* h, const double* w) {
   KMX_CHECK(ready(h) && w, KMX_EINVAL, "null argument / no graph");
   KMX_HIP(hipSetDevice(h->device));
-  KMX_HIP(hipMemcpyAsync(h->erec_h.data(), h->d_erec, sizeof(double) * h->erec_h.size(), hipMemcpyDeviceToHost,
-                         h->stream));
-  KMX_HIP(hipStreamSynchronize(h->stream));
-  for (int k = 0; k < h->mloc; ++k) h->erec_h[(size_t)k * 16 + 14] = w[h->loc_edge_gid[k]];
-  KMX_HIP(hipMemcpyAsync(h->d_erec, h->erec_h.data(), sizeof(double) * h->erec_h.size(), hipMemcpyHostToDevice,
-                         h->stream));
-  enqueue_precond(h);
+  std::vector<double> ew(std::max(h->mloc, 1));
+  for (int k = 0; k < h->mloc; ++k) ew[k] = w[h->loc_edge_gid[k]];
+  KMX_HIP(hipMemcpyAsync(h->d_ew, ew.data(), sizeof(double) * h->mloc, hipMemcpyHostToDevice, h->stream));
+  enqueue_apply_weights(h);
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipStreamSynchronize(h->stream));
   return KMX_OK;
@@ -1542,7 +1957,7 @@ extern "C" int kmx_pgo_pack_shared_weights(kmx_pgo* h, void* dev_out) {
   KMX_HIP(hipMemsetAsync(dev_out, 0, sizeof(double) * h->nshared, h->stream));
   if (h->n_osh)
     hipLaunchKernelGGL(k_shared_pack, dim3((h->n_osh + 255) / 256), dim3(256), 0, h->stream,
-                       (const double*)h->d_erec, h->d_osh_edge, h->d_osh_idx, h->n_osh, (double*)dev_out);
+                       (const double*)h->d_ew, h->d_osh_edge, h->d_osh_idx, h->n_osh, (double*)dev_out);
   KMX_HIP(hipGetLastError());
   return KMX_OK;
 }
@@ -1552,9 +1967,9 @@ extern "C" int kmx_pgo_unpack_shared_weights(kmx_pgo* h, const void* dev_table) 
   KMX_CHECK(dev_table || h->nshared == 0, KMX_EINVAL, "null device buffer");
   KMX_HIP(hipSetDevice(h->device));
   if (h->n_sh_local)
-    hipLaunchKernelGGL(k_shared_unpack, dim3((h->n_sh_local + 255) / 256), dim3(256), 0, h->stream, h->d_erec,
+    hipLaunchKernelGGL(k_shared_unpack, dim3((h->n_sh_local + 255) / 256), dim3(256), 0, h->stream, h->d_ew,
                        h->d_sh_edge, h->d_sh_idx, h->n_sh_local, (const double*)dev_table);
-  enqueue_precond(h);
+  enqueue_apply_weights(h);
   KMX_HIP(hipGetLastError());
   return KMX_OK;
 }
@@ -1593,8 +2008,16 @@ extern "C" int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, do
   KMX_HIP(hipMemsetAsync(h->d_scratch, 0, sizeof(double) * vec * 2, h->stream));
   if (V) KMX_HIP(hipMemcpyAsync(dV + o, V, sizeof(double) * n * ps, hipMemcpyHostToDevice, h->stream));
   const int R_ = h->P.r;
-  KMX_DISPATCH_R(R_, hipLaunchKernelGGL(k_eval<RR>, dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, l, mode,
-                                        (const double*)dV, dO));
+  if (h->gvar == 1) {
+    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 1>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
+                                          h->dv, l, mode, (const double*)dV, dO));
+  } else if (h->gvar == 2) {
+    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 2>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
+                                          h->dv, l, mode, (const double*)dV, dO));
+  } else {
+    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 0>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
+                                          h->dv, l, mode, (const double*)dV, dO));
+  }
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipMemcpyAsync(out, dO + o, sizeof(double) * n * ps, hipMemcpyDeviceToHost, h->stream));
   std::vector<int> rt0(2);
@@ -1645,5 +2068,45 @@ extern "C" int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out) {
   out->hessvecs = (int64_t)c.hessvecs;
   h->ev_used = 0;
   KMX_HIP(hipMemset(h->d_cnt, 0, sizeof(Counters)));
+  return KMX_OK;
+}
+
+// Diagnostic entry point (not used by the product path): time `reps` launches
+// of the gather primitive variant (GV, LBW) = (variant / 10, variant % 10 ->
+// min waves per SIMD {0: none, 1: 4, 2: 6, 3: 8}) over the current iterate.
+extern "C" int kmx_pgo_debug_gather_bench(kmx_pgo* h, int variant, int reps, double* ms_out) {
+  KMX_CHECK(ready(h) && ms_out && reps > 0, KMX_EINVAL, "bad argument");
+  KMX_CHECK(h->P.r == 5, KMX_EUNSUP, "gather bench is built for r = 5");
+  KMX_HIP(hipSetDevice(h->device));
+  const size_t vec = (size_t)std::max(h->nloc, 1) * 4 * h->P.r;
+  double* out = h->d_scratch + vec;
+  hipEvent_t e0, e1;
+  KMX_HIP(hipEventCreate(&e0));
+  KMX_HIP(hipEventCreate(&e1));
+  const dim3 grid(h->ntiles), blk(BLOCK);
+  const size_t sm = Smem<5>::bytes;
+  auto launch = [&]() -> bool {
+    switch (variant) {
+#define KMX_GB(V, G, W) case V: hipLaunchKernelGGL((k_gbench<5, G, W>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
+      KMX_GB(0, 0, 1) KMX_GB(1, 0, 4) KMX_GB(2, 0, 6) KMX_GB(3, 0, 8)
+      KMX_GB(10, 1, 1) KMX_GB(11, 1, 4) KMX_GB(12, 1, 6)
+      KMX_GB(20, 2, 1) KMX_GB(21, 2, 4) KMX_GB(22, 2, 6) KMX_GB(23, 2, 8)
+#undef KMX_GB
+#define KMX_GA(V, A) case V: hipLaunchKernelGGL((k_gablate<5, A>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
+      KMX_GA(30, 0) KMX_GA(31, 1) KMX_GA(32, 2) KMX_GA(33, 3)
+#undef KMX_GA
+      default: return false;
+    }
+  };
+  if (!launch()) return kmx::fail(KMX_EINVAL, "unknown gather variant");
+  KMX_HIP(hipEventRecord(e0, h->stream));
+  for (int i = 0; i < reps; ++i) launch();
+  KMX_HIP(hipEventRecord(e1, h->stream));
+  KMX_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  KMX_HIP(hipEventElapsedTime(&ms, e0, e1));
+  *ms_out = (double)ms / reps;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   return KMX_OK;
 }
