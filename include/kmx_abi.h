@@ -243,7 +243,7 @@ int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out);
 /* LcdParams (params/D455/LcdParams.yaml:16-17, 51-66). */
 typedef struct kmx_lcd_params {
   int norm;                   /* KMX_NORM_* (L1: matcher_type 3 + patch:33-35) */
-  float lowe_ratio;           /* 0.7                                           */
+  double lowe_ratio;          /* 0.7 (compared in double, as LcdParams' double) */
   int min_2d2d_inliers;       /* 10                                            */
   int min_3d3d_inliers;       /* 5                                             */
   double ransac_threshold_2d2d; /* 1e-6 (1 - cos)                              */
@@ -260,7 +260,7 @@ typedef struct kmx_lcd_params {
 /* computeMatchedIndices (drawio:2583-2586): k=2 brute-force match of every
  * query descriptor against the match frame + Lowe ratio. desc are 32-byte ORB
  * descriptors. Output pairs (i_query, i_match) in query order; *k = count. */
-int kmx_lcd_knn2(int norm, float lowe_ratio, const uint8_t* q, int32_t nq,
+int kmx_lcd_knn2(int norm, double lowe_ratio, const uint8_t* q, int32_t nq,
                  const uint8_t* mdesc, int32_t nm, int32_t* pairs_out,
                  int32_t* k);
 

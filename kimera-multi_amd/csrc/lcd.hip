@@ -1,0 +1,997 @@
+// lcd.hip — Kimera-Multi-LCD loop-closure verification on MI355X (gfx950).
+//
+// Replaces LoopClosureDetector::computeMatchedIndices / geometricVerification-
+// Nister / recoverPose (drawio:2583-2598) behind kmx_lcd_* (include/kmx_abi.h).
+// Design (DESIGN.md "LCD"):
+//   * k_knn2: one workgroup per candidate. The match frame's descriptors sit in
+//     LDS (32 B each, read as broadcast); each lane owns a contiguous run of
+//     query descriptors, computes L1 (v_sad_u8 on 4-byte words) or Hamming
+//     (xor + popcount) to every match descriptor, keeps the two smallest
+//     (distance, index) pairs with OpenCV's strict-'<' insertion, applies Lowe,
+//     and the workgroup compacts the pairs in query order with a prefix sum.
+//   * k_ransac: one wavefront per candidate, one RANSAC pass (hypothesis) per
+//     lane: 64 consecutive passes of the opengv loop are evaluated at once
+//     (5-point solve + scoring of all K correspondences held in LDS), then lane
+//     0 replays the serial loop control (skips, best model, adaptive k,
+//     max-iteration stop) over the batch in pass order, so the accepted model
+//     and inlier set are the serial loop's. Samples come from a host-built
+//     table of the opengv sampler (std::mt19937, seed 12345, GCC-9 or GCC-11
+//     uniform_int_distribution) indexed by K.
+//   * 3D-3D (1-point given rotation) voting on the 2D-2D inliers in the same
+//     wavefront.
+// The solver code is a line-by-line port of oracle/lcd_oracle.c and this file
+// is compiled with -ffp-contract=off, so the inlier sets are bit-exact.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+constexpr int KNN_BLOCK = 256;
+constexpr int RS_BLOCK = 64;          // one wavefront per candidate
+constexpr int MAX_FEATS = 1024;
+
+__constant__ int MUL11[4][4] = {{0, 1, 2, 6}, {1, 3, 4, 7}, {2, 4, 5, 8}, {6, 7, 8, 9}};
+__constant__ int MUL21[10][4] = {{0, 2, 4, 5},    {2, 3, 8, 9},    {4, 8, 10, 11},  {3, 1, 6, 7},
+                                 {8, 6, 13, 14},  {10, 13, 16, 17}, {5, 9, 11, 12}, {9, 7, 14, 15},
+                                 {11, 14, 17, 18}, {12, 15, 18, 19}};
+
+// ------------------------------------------------------------------ knn2 --
+__global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const int* nfeat, int N,
+                                                    const int* cq, const int* cm, int norm, double lowe,
+                                                    int2* pairs, int* Kout) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm_u32[];
+  uint32_t* sdesc = sm_u32;                    // [nm][8]
+  int* scnt = reinterpret_cast<int*>(sm_u32 + (size_t)N * 8);  // [KNN_BLOCK + 1]
+  const int c = blockIdx.x;
+  const int q = cq[c], m = cm[c];
+  const int nq = nfeat[q], nm = nfeat[m];
+  const uint32_t* dq = desc + (size_t)q * N * 8;
+  const uint32_t* dm = desc + (size_t)m * N * 8;
+  for (int i = threadIdx.x; i < nm * 8; i += KNN_BLOCK) sdesc[i] = dm[i];
+  __syncthreads();
+  const int per = (nq + KNN_BLOCK - 1) / KNN_BLOCK;
+  const int i0 = threadIdx.x * per, i1 = min(nq, i0 + per);
+  int found = 0;
+  int bestj[8];  // per <= 4 for N <= 1024
+  bool pass[8];
+  for (int u = 0; u < 8; ++u) { bestj[u] = -1; pass[u] = false; }
+  if (nm >= 2) {
+    for (int i = i0, u = 0; i < i1; ++i, ++u) {
+      uint32_t a[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) a[w] = dq[(size_t)i * 8 + w];
+      int d0 = INT_MAX, d1 = INT_MAX, j0 = -1;
+      for (int j = 0; j < nm; ++j) {
+        const uint32_t* b = sdesc + j * 8;
+        int d = 0;
+        if (norm == KMX_NORM_HAMMING) {
+#pragma unroll
+          for (int w = 0; w < 8; ++w) d += __popc(a[w] ^ b[w]);
+        } else {
+          uint32_t acc = 0;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) acc = __builtin_amdgcn_sad_u8(a[w], b[w], acc);
+          d = (int)acc;
+        }
+        if (d < d1) {
+          if (d < d0) { d1 = d0; d0 = d; j0 = j; }
+          else d1 = d;
+        }
+      }
+      bestj[u] = j0;
+      pass[u] = (double)(float)d0 < lowe * (double)(float)d1;
+      found += pass[u] ? 1 : 0;
+    }
+  }
+  // exclusive prefix sum of per-thread counts (query order = thread order)
+  scnt[threadIdx.x] = found;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int t = 0; t < KNN_BLOCK; ++t) {
+      const int v = scnt[t];
+      scnt[t] = s;
+      s += v;
+    }
+    scnt[KNN_BLOCK] = s;
+  }
+  __syncthreads();
+  int pos = scnt[threadIdx.x];
+  int2* out = pairs + (size_t)c * N;
+  for (int i = i0, u = 0; i < i1; ++i, ++u)
+    if (pass[u]) out[pos++] = make_int2(i, bestj[u]);
+  if (threadIdx.x == 0) Kout[c] = scnt[KNN_BLOCK];
+}
+
+// --------------------------------------------------- small linear algebra --
+__device__ void cross3(const double a[3], const double b[3], double c[3]) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+__device__ double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ double det3(const double M[9]) {
+  return M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) + M[2] * (M[3] * M[7] - M[4] * M[6]);
+}
+
+__device__ void sym_eig3(double A[9], double V[9]) {
+  for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    for (int p = 0; p < 2; ++p)
+      for (int q = p + 1; q < 3; ++q) {
+        const double apq = A[p * 3 + q];
+        if (apq == 0.0) continue;
+        const double app = A[p * 3 + p], aqq = A[q * 3 + q];
+        const double theta = (aqq - app) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
+        for (int k = 0; k < 3; ++k) {
+          const double akp = A[k * 3 + p], akq = A[k * 3 + q];
+          A[k * 3 + p] = cs * akp - sn * akq;
+          A[k * 3 + q] = sn * akp + cs * akq;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double apk = A[p * 3 + k], aqk = A[q * 3 + k];
+          A[p * 3 + k] = cs * apk - sn * aqk;
+          A[q * 3 + k] = sn * apk + cs * aqk;
+        }
+        for (int k = 0; k < 3; ++k) {
+          const double vkp = V[k * 3 + p], vkq = V[k * 3 + q];
+          V[k * 3 + p] = cs * vkp - sn * vkq;
+          V[k * 3 + q] = sn * vkp + cs * vkq;
+        }
+      }
+  }
+}
+
+__device__ void svd3(const double E[9], double U[9], double s[3], double V[9]) {
+  double A[9], W[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double acc = 0.0;
+      for (int k = 0; k < 3; ++k) acc += E[k * 3 + i] * E[k * 3 + j];
+      A[i * 3 + j] = acc;
+    }
+  sym_eig3(A, W);
+  int ord[3] = {0, 1, 2};
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 2 - a; ++b)
+      if (A[ord[b] * 4] < A[ord[b + 1] * 4]) { const int t = ord[b]; ord[b] = ord[b + 1]; ord[b + 1] = t; }
+  for (int c = 0; c < 3; ++c) {
+    s[c] = sqrt(fmax(A[ord[c] * 4], 0.0));
+    for (int r = 0; r < 3; ++r) V[r * 3 + c] = W[r * 3 + ord[c]];
+  }
+  double u[3][3];
+  for (int c = 0; c < 2; ++c) {
+    for (int r = 0; r < 3; ++r) u[c][r] = (E[r * 3 + 0] * V[0 * 3 + c] + E[r * 3 + 1] * V[1 * 3 + c] + E[r * 3 + 2] * V[2 * 3 + c]);
+    const double n = sqrt(dot3(u[c], u[c]));
+    for (int r = 0; r < 3; ++r) u[c][r] = (n > 0.0) ? u[c][r] / n : 0.0;
+  }
+  cross3(u[0], u[1], u[2]);
+  for (int c = 0; c < 3; ++c)
+    for (int r = 0; r < 3; ++r) U[r * 3 + c] = u[c][r];
+}
+
+// ------------------------------------------------ 5-point (Nister 2004) --
+__device__ void mul11(const double* a, const double* b, double* out) {
+  for (int k = 0; k < 10; ++k) out[k] = 0.0;
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) out[MUL11[i][j]] += a[i] * b[j];
+}
+__device__ void mul21(const double* a, const double* b, double* out) {
+  for (int k = 0; k < 20; ++k) out[k] = 0.0;
+  for (int i = 0; i < 10; ++i)
+    for (int j = 0; j < 4; ++j) out[MUL21[i][j]] += a[i] * b[j];
+}
+
+__device__ void nullspace_5x9(const double Q[5][9], double N[4][9]) {
+  double A[9][5];
+  for (int i = 0; i < 9; ++i)
+    for (int j = 0; j < 5; ++j) A[i][j] = Q[j][i];
+  double vs[5][9];
+  for (int k = 0; k < 5; ++k) {
+    double nx = 0.0;
+    for (int i = k; i < 9; ++i) nx += A[i][k] * A[i][k];
+    nx = sqrt(nx);
+    const double alpha = (A[k][k] >= 0.0) ? -nx : nx;
+    double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = k; i < 9; ++i) v[i] = A[i][k];
+    v[k] -= alpha;
+    double nv = 0.0;
+    for (int i = k; i < 9; ++i) nv += v[i] * v[i];
+    nv = sqrt(nv);
+    for (int i = 0; i < 9; ++i) vs[k][i] = (nv > 0.0 && i >= k) ? v[i] / nv : 0.0;
+    for (int j = k; j < 5; ++j) {
+      double d = 0.0;
+      for (int i = k; i < 9; ++i) d += vs[k][i] * A[i][j];
+      for (int i = k; i < 9; ++i) A[i][j] -= 2.0 * vs[k][i] * d;
+    }
+  }
+  for (int c = 0; c < 4; ++c) {
+    double x[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    x[5 + c] = 1.0;
+    for (int k = 4; k >= 0; --k) {
+      double d = 0.0;
+      for (int i = k; i < 9; ++i) d += vs[k][i] * x[i];
+      for (int i = k; i < 9; ++i) x[i] -= 2.0 * vs[k][i] * d;
+    }
+    for (int i = 0; i < 9; ++i) N[c][i] = x[i];
+  }
+}
+
+__device__ double poly_eval(const double* c, int deg, double z) {
+  double v = c[deg];
+  for (int i = deg - 1; i >= 0; --i) v = v * z + c[i];
+  return v;
+}
+
+__device__ int sign_changes(const double S[11][11], const int* sd, int ns, double z) {
+  int ch = 0;
+  double prev = 0.0;
+  for (int s = 0; s < ns; ++s) {
+    const double v = poly_eval(S[s], sd[s], z);
+    if (v != 0.0) {
+      if (prev != 0.0 && ((v < 0.0) != (prev < 0.0))) ++ch;
+      prev = v;
+    }
+  }
+  return ch;
+}
+
+__device__ int real_roots(const double* coef, int deg_in, double* roots) {
+  int deg = deg_in;
+  while (deg > 0 && coef[deg] == 0.0) --deg;
+  if (deg <= 0) return 0;
+  double S[11][11];
+  int sd[11];
+  for (int i = 0; i <= deg; ++i) S[0][i] = coef[i] / coef[deg];
+  sd[0] = deg;
+  for (int i = 0; i < deg; ++i) S[1][i] = (double)(i + 1) * S[0][i + 1];
+  sd[1] = deg - 1;
+  int ns = 2;
+  while (sd[ns - 1] > 0 && ns < 11) {
+    double r[11];
+    const int da = sd[ns - 2], db = sd[ns - 1];
+    for (int i = 0; i <= da; ++i) r[i] = S[ns - 2][i];
+    for (int k = da - db; k >= 0; --k) {
+      const double f = r[k + db] / S[ns - 1][db];
+      for (int i = 0; i <= db; ++i) r[k + i] -= f * S[ns - 1][i];
+    }
+    int dr = db - 1;
+    double mx = 0.0;
+    for (int i = 0; i <= da; ++i) mx = fmax(mx, fabs(S[ns - 2][i]));
+    while (dr >= 0 && fabs(r[dr]) <= 1e-14 * mx) --dr;
+    if (dr < 0) break;
+    for (int i = 0; i <= dr; ++i) S[ns][i] = -r[i];
+    sd[ns] = dr;
+    ++ns;
+  }
+  double bound = 0.0;
+  for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(S[0][i]));
+  bound += 1.0;
+  double st_lo[64], st_hi[64];
+  int st_vl[64], st_vh[64], st_d[64];
+  int sp = 0, nr = 0;
+  const int vlo = sign_changes(S, sd, ns, -bound);
+  const int vhi = sign_changes(S, sd, ns, bound);
+  st_lo[sp] = -bound; st_hi[sp] = bound; st_vl[sp] = vlo; st_vh[sp] = vhi; st_d[sp] = 0; ++sp;
+  while (sp > 0) {
+    --sp;
+    const double lo = st_lo[sp], hi = st_hi[sp];
+    const int vl = st_vl[sp], vh = st_vh[sp], dep = st_d[sp];
+    const int cnt = vl - vh;
+    if (cnt <= 0) continue;
+    if (cnt == 1 || dep >= 50) {
+      double a = lo, b = hi;
+      double fa = poly_eval(S[0], deg, a);
+      for (int it = 0; it < 80; ++it) {
+        const double mid = 0.5 * (a + b);
+        const double fm = poly_eval(S[0], deg, mid);
+        if (fm == 0.0) { a = b = mid; break; }
+        if ((fm < 0.0) == (fa < 0.0)) { a = mid; fa = fm; }
+        else b = mid;
+      }
+      if (nr < 10) roots[nr++] = 0.5 * (a + b);
+      continue;
+    }
+    const double mid = 0.5 * (lo + hi);
+    const int vm = sign_changes(S, sd, ns, mid);
+    if (sp + 2 <= 64) {
+      st_lo[sp] = mid; st_hi[sp] = hi; st_vl[sp] = vm; st_vh[sp] = vh; st_d[sp] = dep + 1; ++sp;
+      st_lo[sp] = lo; st_hi[sp] = mid; st_vl[sp] = vl; st_vh[sp] = vm; st_d[sp] = dep + 1; ++sp;
+    }
+  }
+  for (int a = 0; a < nr; ++a)
+    for (int b = 0; b + 1 < nr - a; ++b)
+      if (roots[b] > roots[b + 1]) { const double t = roots[b]; roots[b] = roots[b + 1]; roots[b + 1] = t; }
+  return nr;
+}
+
+__device__ void pmul(const double* a, int da, const double* b, int db, double* out) {
+  for (int i = 0; i <= da + db; ++i) out[i] = 0.0;
+  for (int i = 0; i <= da; ++i)
+    for (int j = 0; j <= db; ++j) out[i + j] += a[i] * b[j];
+}
+
+__device__ int fivept_nister(const double* f1, const double* f2, double* Es) {
+  double Q[5][9];
+  for (int i = 0; i < 5; ++i)
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) Q[i][a * 3 + b] = f1[3 * i + a] * f2[3 * i + b];
+  double N[4][9];
+  nullspace_5x9(Q, N);
+  double E[9][4];
+  for (int e = 0; e < 9; ++e)
+    for (int c = 0; c < 4; ++c) E[e][c] = N[c][e];
+  double A[10][20];
+  {
+    double t1[10], t2[10], c2[10], m[20];
+    for (int k = 0; k < 20; ++k) A[9][k] = 0.0;
+    mul11(E[4], E[8], t1); mul11(E[5], E[7], t2);
+    for (int k = 0; k < 10; ++k) c2[k] = t1[k] - t2[k];
+    mul21(c2, E[0], m);
+    for (int k = 0; k < 20; ++k) A[9][k] += m[k];
+    mul11(E[3], E[8], t1); mul11(E[5], E[6], t2);
+    for (int k = 0; k < 10; ++k) c2[k] = t1[k] - t2[k];
+    mul21(c2, E[1], m);
+    for (int k = 0; k < 20; ++k) A[9][k] -= m[k];
+    mul11(E[3], E[7], t1); mul11(E[4], E[6], t2);
+    for (int k = 0; k < 10; ++k) c2[k] = t1[k] - t2[k];
+    mul21(c2, E[2], m);
+    for (int k = 0; k < 20; ++k) A[9][k] += m[k];
+  }
+  {
+    double EEt[9][10], tr[10], t[10], m[20];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        for (int k = 0; k < 10; ++k) EEt[i * 3 + j][k] = 0.0;
+        for (int l = 0; l < 3; ++l) {
+          mul11(E[i * 3 + l], E[j * 3 + l], t);
+          for (int k = 0; k < 10; ++k) EEt[i * 3 + j][k] += t[k];
+        }
+      }
+    for (int k = 0; k < 10; ++k) tr[k] = EEt[0][k] + EEt[4][k] + EEt[8][k];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double* r = A[i * 3 + j];
+        for (int k = 0; k < 20; ++k) r[k] = 0.0;
+        for (int l = 0; l < 3; ++l) {
+          mul21(EEt[i * 3 + l], E[l * 3 + j], m);
+          for (int k = 0; k < 20; ++k) r[k] += 2.0 * m[k];
+        }
+        mul21(tr, E[i * 3 + j], m);
+        for (int k = 0; k < 20; ++k) r[k] -= m[k];
+      }
+  }
+  for (int k = 0; k < 10; ++k) {
+    int p = k;
+    for (int i = k + 1; i < 10; ++i)
+      if (fabs(A[i][k]) > fabs(A[p][k])) p = i;
+    if (A[p][k] == 0.0) return 0;
+    if (p != k)
+      for (int c = 0; c < 20; ++c) { const double t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t; }
+    const double inv = 1.0 / A[k][k];
+    for (int c = 0; c < 20; ++c) A[k][c] *= inv;
+    for (int i = 0; i < 10; ++i) {
+      if (i == k) continue;
+      const double f = A[i][k];
+      if (f == 0.0) continue;
+      for (int c = 0; c < 20; ++c) A[i][c] -= f * A[k][c];
+    }
+  }
+  double Bp[3][3][5];
+  for (int q = 0; q < 3; ++q) {
+    const double* e = &A[4 + 2 * q][10];
+    const double* f = &A[5 + 2 * q][10];
+    double* px = Bp[q][0];
+    double* py = Bp[q][1];
+    double* pc = Bp[q][2];
+    px[0] = e[2]; px[1] = e[1] - f[2]; px[2] = e[0] - f[1]; px[3] = -f[0]; px[4] = 0.0;
+    py[0] = e[5]; py[1] = e[4] - f[5]; py[2] = e[3] - f[4]; py[3] = -f[3]; py[4] = 0.0;
+    pc[0] = e[9]; pc[1] = e[8] - f[9]; pc[2] = e[7] - f[8]; pc[3] = e[6] - f[7]; pc[4] = -f[6];
+  }
+  double n[11];
+  {
+    double c1[8], c2[8], c3[8], t1[8], t2[8];
+    pmul(Bp[1][1], 3, Bp[2][2], 4, t1); pmul(Bp[1][2], 4, Bp[2][1], 3, t2);
+    for (int i = 0; i < 8; ++i) c1[i] = t1[i] - t2[i];
+    pmul(Bp[1][0], 3, Bp[2][2], 4, t1); pmul(Bp[1][2], 4, Bp[2][0], 3, t2);
+    for (int i = 0; i < 8; ++i) c2[i] = t1[i] - t2[i];
+    pmul(Bp[1][0], 3, Bp[2][1], 3, t1); pmul(Bp[1][1], 3, Bp[2][0], 3, t2);
+    for (int i = 0; i < 7; ++i) c3[i] = t1[i] - t2[i];
+    c3[7] = 0.0;
+    double u1[11], u2[11], u3[11];
+    pmul(Bp[0][0], 3, c1, 7, u1);
+    pmul(Bp[0][1], 3, c2, 7, u2);
+    pmul(Bp[0][2], 4, c3, 6, u3);
+    for (int i = 0; i < 11; ++i) n[i] = u1[i] - u2[i] + u3[i];
+  }
+  double roots[10];
+  const int nr = real_roots(n, 10, roots);
+  int ns = 0;
+  for (int ri = 0; ri < nr; ++ri) {
+    const double z = roots[ri];
+    double row[3][3];
+    for (int q = 0; q < 3; ++q)
+      for (int c = 0; c < 3; ++c) row[q][c] = poly_eval(Bp[q][c], c == 2 ? 4 : 3, z);
+    double v[3];
+    cross3(row[0], row[1], v);
+    if (v[2] == 0.0) continue;
+    const double x = v[0] / v[2], y = v[1] / v[2];
+    double* Eo = Es + 9 * ns;
+    double nn = 0.0;
+    for (int e = 0; e < 9; ++e) {
+      Eo[e] = x * N[0][e] + y * N[1][e] + z * N[2][e] + N[3][e];
+      nn += Eo[e] * Eo[e];
+    }
+    nn = sqrt(nn);
+    if (!(nn > 0.0)) continue;
+    for (int e = 0; e < 9; ++e) Eo[e] /= nn;
+    ++ns;
+  }
+  return ns;
+}
+
+__device__ double model_error(const double R[9], const double t[3], const double f1[3], const double f2[3]) {
+  double f2u[3];
+  for (int i = 0; i < 3; ++i) f2u[i] = R[i * 3 + 0] * f2[0] + R[i * 3 + 1] * f2[1] + R[i * 3 + 2] * f2[2];
+  const double b0 = dot3(t, f1), b1 = dot3(t, f2u);
+  const double a00 = dot3(f1, f1), a10 = dot3(f1, f2u), a01 = -a10, a11 = -dot3(f2u, f2u);
+  const double det = a00 * a11 - a01 * a10;
+  const double l0 = (a11 * b0 - a01 * b1) / det;
+  const double l1 = (-a10 * b0 + a00 * b1) / det;
+  double p[3];
+  for (int i = 0; i < 3; ++i) p[i] = 0.5 * (l0 * f1[i] + (t[i] + l1 * f2u[i]));
+  double q[3], d[3];
+  for (int i = 0; i < 3; ++i) d[i] = p[i] - t[i];
+  for (int i = 0; i < 3; ++i) q[i] = R[0 * 3 + i] * d[0] + R[1 * 3 + i] * d[1] + R[2 * 3 + i] * d[2];
+  const double np = sqrt(dot3(p, p)), nq = sqrt(dot3(q, q));
+  const double e1 = 1.0 - (f1[0] * p[0] + f1[1] * p[1] + f1[2] * p[2]) / np;
+  const double e2 = 1.0 - (f2[0] * q[0] + f2[1] * q[1] + f2[2] * q[2]) / nq;
+  return e1 + e2;
+}
+
+__device__ int model_from_sample(const double* F1, const double* F2, const int* smp, double R[9], double t[3]) {
+  double f1[15], f2[15];
+  for (int i = 0; i < 5; ++i)
+    for (int c = 0; c < 3; ++c) {
+      f1[3 * i + c] = F1[3 * smp[i] + c];
+      f2[3 * i + c] = F2[3 * smp[i] + c];
+    }
+  double Es[90];
+  const int ne = fivept_nister(f1, f2, Es);
+  if (ne == 0) return 0;
+  double best = DBL_MAX;
+  int found = 0;
+  for (int e = 0; e < ne; ++e) {
+    double U[9], s[3], V[9];
+    svd3(Es + 9 * e, U, s, V);
+    double Ra[9], Rb[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        const double uw0 = U[i * 3 + 1], uw1 = -U[i * 3 + 0], uw2 = U[i * 3 + 2];
+        Ra[i * 3 + j] = uw0 * V[j * 3 + 0] + uw1 * V[j * 3 + 1] + uw2 * V[j * 3 + 2];
+        const double uv0 = -U[i * 3 + 1], uv1 = U[i * 3 + 0], uv2 = U[i * 3 + 2];
+        Rb[i * 3 + j] = uv0 * V[j * 3 + 0] + uv1 * V[j * 3 + 1] + uv2 * V[j * 3 + 2];
+      }
+    if (det3(Ra) < 0.0)
+      for (int i = 0; i < 9; ++i) Ra[i] = -Ra[i];
+    if (det3(Rb) < 0.0)
+      for (int i = 0; i < 9; ++i) Rb[i] = -Rb[i];
+    const double tu[3] = {U[0 * 3 + 2], U[1 * 3 + 2], U[2 * 3 + 2]};
+    for (int cand = 0; cand < 4; ++cand) {
+      const double* Rc = (cand < 2) ? Ra : Rb;
+      const double sg = (cand & 1) ? -1.0 : 1.0;
+      const double tc[3] = {sg * tu[0], sg * tu[1], sg * tu[2]};
+      double err = 0.0;
+      for (int i = 0; i < 5; ++i) err += model_error(Rc, tc, f1 + 3 * i, f2 + 3 * i);
+      if (err < best) {
+        best = err;
+        for (int i = 0; i < 9; ++i) R[i] = Rc[i];
+        for (int i = 0; i < 3; ++i) t[i] = tc[i];
+        found = 1;
+      }
+    }
+  }
+  return found;
+}
+
+// ---------------------------------------------------------- RANSAC kernel --
+struct RsParams {
+  double thr2d, thr3d, prob;
+  int max_iter, min2d, min3d, pmax;
+};
+
+__global__ __launch_bounds__(RS_BLOCK) void k_ransac(const double* bearings, const double* points, int N,
+                                                     const int* cq, const int* cm, const int2* pairs,
+                                                     const int* Kin, const short* table, RsParams P,
+                                                     kmx_lcd_result* res, unsigned char* masks) {
+  extern __shared__ __attribute__((aligned(16))) double sm_d[];
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int K = Kin[c];
+  const int q = cq[c], m = cm[c];
+  double* F1 = sm_d;                  // [K][3]
+  double* F2 = F1 + 3 * N;            // [K][3]
+  double* models = F2 + 3 * N;        // [64][12]
+  double* bestm = models + 64 * 12;   // [12]
+  int* okc = reinterpret_cast<int*>(bestm + 12);  // [64] ok flags, [64] counts, ctrl[4]
+  int* cnt = okc + 64;
+  int* ctrl = cnt + 64;
+  unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
+  kmx_lcd_result* R_ = res + c;
+  for (int j = lane; j < N && mask; j += RS_BLOCK) mask[j] = 0;
+  if (K < 5) {
+    if (lane == 0) {
+      kmx_lcd_result r = {};
+      r.n_matches = K;
+      *R_ = r;
+    }
+    return;
+  }
+  const int2* pl = pairs + (size_t)c * N;
+  for (int j = lane; j < K; j += RS_BLOCK) {
+    const int2 pr = pl[j];
+    for (int k = 0; k < 3; ++k) {
+      F1[3 * j + k] = bearings[((size_t)q * N + pr.x) * 3 + k];
+      F2[3 * j + k] = bearings[((size_t)m * N + pr.y) * 3 + k];
+    }
+  }
+  __syncthreads();
+  // serial-loop state (lane 0)
+  int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
+  double kk = 1.0;
+  const int max_skip = P.max_iter * 10;
+  const short* tab = table + (size_t)(K - 5) * P.pmax * 5;
+  for (int base = 0;; base += RS_BLOCK) {
+    const int p = base + lane;
+    int ok = 0, count = 0;
+    double Rm[9], tm[3];
+    if (p < P.pmax) {
+      int smp[5];
+      for (int i = 0; i < 5; ++i) smp[i] = tab[(size_t)p * 5 + i];
+      ok = model_from_sample(F1, F2, smp, Rm, tm);
+      if (ok)
+        for (int j = 0; j < K; ++j)
+          if (model_error(Rm, tm, F1 + 3 * j, F2 + 3 * j) < P.thr2d) ++count;
+    }
+    okc[lane] = ok;
+    cnt[lane] = count;
+    if (ok) {
+      for (int i = 0; i < 9; ++i) models[lane * 12 + i] = Rm[i];
+      for (int i = 0; i < 3; ++i) models[lane * 12 + 9 + i] = tm[i];
+    }
+    __syncthreads();
+    if (lane == 0) {
+      int done = 0;
+      for (int l = 0; l < RS_BLOCK; ++l) {
+        if (!(iterations < kk && skipped < max_skip) || base + l >= P.pmax) { done = 1; break; }
+        if (!okc[l]) { ++skipped; continue; }
+        if (cnt[l] > best_cnt) {
+          best_cnt = cnt[l];
+          for (int i = 0; i < 12; ++i) bestm[i] = models[l * 12 + i];
+          have = 1;
+          const double w = (double)cnt[l] / (double)K;
+          double p_no = 1.0 - pow(w, 5.0);
+          p_no = fmax(DBL_EPSILON, p_no);
+          p_no = fmin(1.0 - DBL_EPSILON, p_no);
+          kk = log(1.0 - P.prob) / log(p_no);
+        }
+        ++iterations;
+        if (iterations > P.max_iter) { done = 1; break; }
+      }
+      if (!done && base + RS_BLOCK >= P.pmax) done = 1;
+      ctrl[0] = done;
+      ctrl[1] = have;
+      ctrl[2] = iterations;
+    }
+    __syncthreads();
+    if (ctrl[0]) break;
+  }
+  const int have_model = ctrl[1];
+  const int iters = ctrl[2];
+  if (!have_model) {
+    if (lane == 0) {
+      kmx_lcd_result r = {};
+      r.n_matches = K;
+      r.iterations_2d2d = iters;
+      *R_ = r;
+    }
+    return;
+  }
+  double Rb[9], tb[3];
+  for (int i = 0; i < 9; ++i) Rb[i] = bestm[i];
+  for (int i = 0; i < 3; ++i) tb[i] = bestm[9 + i];
+  // final inlier set of the best model; compact stereo points of inliers
+  int n_in = 0;
+  for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
+    const int j = j0 + lane;
+    const bool in = (j < K) && model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d;
+    if (j < K && mask) mask[j] = in ? 1 : 0;
+    n_in += __popcll(__ballot(in));
+  }
+  kmx_lcd_result r = {};
+  r.n_matches = K;
+  r.mono_inliers = n_in;
+  r.iterations_2d2d = iters;
+  for (int i = 0; i < 9; ++i) r.T_query_match[i] = Rb[i];
+  for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = tb[i];
+  if (n_in < P.min2d) {
+    if (lane == 0) *R_ = r;
+    return;
+  }
+  // 3D-3D given rotation: T_j = p_q - R p_m over the 2D-2D inliers in pair order
+  __syncthreads();
+  double* T = F2;  // reuse: [n3][3] translations
+  unsigned char* valid = reinterpret_cast<unsigned char*>(models);  // [N] bytes
+  int* idx = reinterpret_cast<int*>(F1);  // [n3] pair positions (F1 no longer needed)
+  if (lane == 0) {
+    int n3 = 0;
+    for (int j = 0; j < K; ++j) {
+      // recompute the inlier predicate identically (lane 0 walks the pair list)
+      if (!(model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d)) continue;
+      idx[n3++] = j;  // safe: idx[n3] overwrites F1 words of entries < j only
+    }
+    ctrl[3] = n3;
+  }
+  __syncthreads();
+  const int n3 = ctrl[3];
+  for (int k = lane; k < n3; k += RS_BLOCK) {
+    const int j = idx[k];
+    const int2 pr = pl[j];
+    const double* a = points + ((size_t)q * N + pr.x) * 3;
+    const double* b = points + ((size_t)m * N + pr.y) * 3;
+    const bool v = !(isnan(a[0]) || isnan(a[1]) || isnan(a[2]) || isnan(b[0]) || isnan(b[1]) || isnan(b[2]));
+    valid[k] = v ? 1 : 0;
+    for (int i = 0; i < 3; ++i) T[3 * k + i] = a[i] - (Rb[i * 3 + 0] * b[0] + Rb[i * 3 + 1] * b[1] + Rb[i * 3 + 2] * b[2]);
+  }
+  __syncthreads();
+  const double thr2 = P.thr3d * P.thr3d;
+  int my_best = -1, my_cnt = 0;
+  for (int i = lane; i < n3; i += RS_BLOCK) {
+    if (!valid[i]) continue;
+    int cc = 0;
+    for (int j = 0; j < n3; ++j) {
+      if (!valid[j]) continue;
+      const double dx = T[3 * j] - T[3 * i], dy = T[3 * j + 1] - T[3 * i + 1], dz = T[3 * j + 2] - T[3 * i + 2];
+      if (dx * dx + dy * dy + dz * dz < thr2) ++cc;
+    }
+    if (cc > my_cnt) { my_cnt = cc; my_best = i; }
+  }
+  // wave reduction: max count, then smallest index
+  for (int off = 32; off > 0; off >>= 1) {
+    const int oc = __shfl_xor(my_cnt, off, 64);
+    const int ob = __shfl_xor(my_best, off, 64);
+    if (oc > my_cnt || (oc == my_cnt && ob >= 0 && (my_best < 0 || ob < my_best))) {
+      my_cnt = oc;
+      my_best = ob;
+    }
+  }
+  if (lane == 0) {
+    const int best = my_best;
+    if (best >= 0) {
+      int cc = 0;
+      double s[3] = {0.0, 0.0, 0.0};
+      for (int j = 0; j < n3; ++j) {
+        int in = 0;
+        if (valid[j]) {
+          const double dx = T[3 * j] - T[3 * best], dy = T[3 * j + 1] - T[3 * best + 1], dz = T[3 * j + 2] - T[3 * best + 2];
+          in = dx * dx + dy * dy + dz * dz < thr2;
+        }
+        if (in) {
+          for (int i = 0; i < 3; ++i) s[i] += T[3 * j + i];
+          ++cc;
+          if (mask) mask[idx[j]] |= 2;
+        }
+      }
+      for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = s[i] / (double)cc;
+      r.stereo_inliers = cc;
+      r.accepted = (cc >= P.min3d) ? 1 : 0;
+    } else {
+      for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = 0.0;
+    }
+    *R_ = r;
+  }
+}
+
+}  // namespace
+
+// ============================================================== handle ====
+struct kmx_lcd {
+  kmx_lcd_params P{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int F = 0, N = 0;
+  uint32_t* d_desc = nullptr;
+  double* d_bear = nullptr;
+  double* d_pts = nullptr;
+  int* d_nfeat = nullptr;
+  short* d_table = nullptr;
+  int pmax = 0;
+  // candidate buffers
+  int cap = 0;
+  int *d_cq = nullptr, *d_cm = nullptr, *d_K = nullptr;
+  int2* d_pairs = nullptr;
+  kmx_lcd_result* d_res = nullptr;
+  unsigned char* d_mask = nullptr;
+};
+
+namespace {
+
+void lcd_free_pool(kmx_lcd* h) {
+  void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat, h->d_table};
+  for (void* x : p)
+    if (x) (void)hipFree(x);
+  h->d_desc = nullptr; h->d_bear = h->d_pts = nullptr; h->d_nfeat = nullptr; h->d_table = nullptr;
+}
+void lcd_free_cand(kmx_lcd* h) {
+  void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask};
+  for (void* x : p)
+    if (x) (void)hipFree(x);
+  h->d_cq = h->d_cm = h->d_K = nullptr; h->d_pairs = nullptr; h->d_res = nullptr; h->d_mask = nullptr;
+  h->cap = 0;
+}
+
+// opengv sampler table: for every K in [5, N], the 5 indices drawn by each of
+// the first pmax passes (std::mt19937 seeded per problem; drawIndexSample swap
+// shuffle over a persistent index vector; GCC-9 or GCC-11 uniform_int).
+void build_table(const kmx_lcd_params& P, int N, int pmax, std::vector<short>& tab) {
+  tab.assign((size_t)std::max(N - 4, 1) * pmax * 5, 0);
+  std::vector<int> sh;
+  for (int K = 5; K <= N; ++K) {
+    std::mt19937 rng(P.ransac_seed);
+    sh.resize(K);
+    for (int i = 0; i < K; ++i) sh[i] = i;
+    short* out = tab.data() + (size_t)(K - 5) * pmax * 5;
+    for (int p = 0; p < pmax; ++p) {
+      for (int i = 0; i < 5; ++i) {
+        uint32_t x;
+        if (P.rng_variant == KMX_RNG_GCC11) {
+          x = (uint32_t)rng() >> 1;
+        } else {
+          do x = (uint32_t)rng();
+          while (x >= 0x80000000u);
+        }
+        const int j = i + (int)((size_t)x % (size_t)(K - i));
+        std::swap(sh[i], sh[j]);
+      }
+      for (int i = 0; i < 5; ++i) out[p * 5 + i] = (short)sh[i];
+    }
+  }
+}
+
+int ensure_cap(kmx_lcd* h, int n) {
+  if (n <= h->cap) return 0;
+  lcd_free_cand(h);
+  const int cap = std::max(n, 1024);
+  if (hipMalloc(&h->d_cq, sizeof(int) * cap) != hipSuccess || hipMalloc(&h->d_cm, sizeof(int) * cap) != hipSuccess ||
+      hipMalloc(&h->d_K, sizeof(int) * cap) != hipSuccess ||
+      hipMalloc(&h->d_pairs, sizeof(int2) * (size_t)cap * h->N) != hipSuccess ||
+      hipMalloc(&h->d_res, sizeof(kmx_lcd_result) * cap) != hipSuccess ||
+      hipMalloc(&h->d_mask, (size_t)cap * h->N) != hipSuccess) {
+    lcd_free_cand(h);
+    return kmx::fail(KMX_ENOMEM, "candidate buffers");
+  }
+  h->cap = cap;
+  return 0;
+}
+
+size_t ransac_smem(int N) { return sizeof(double) * (6 * (size_t)N + 64 * 12 + 12) + sizeof(int) * (64 + 64 + 4); }
+
+int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
+  if (n == 0) return 0;
+  const size_t knn_smem = (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1);
+  hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), knn_smem, h->stream, (const uint32_t*)h->d_desc,
+                     (const int*)h->d_nfeat, h->N, (const int*)h->d_cq, (const int*)h->d_cm, h->P.norm,
+                     h->P.lowe_ratio, h->d_pairs, h->d_K);
+  RsParams rp;
+  rp.thr2d = h->P.ransac_threshold_2d2d;
+  rp.thr3d = h->P.ransac_threshold_3d3d;
+  rp.prob = h->P.ransac_probability;
+  rp.max_iter = h->P.ransac_max_iterations;
+  rp.min2d = h->P.min_2d2d_inliers;
+  rp.min3d = h->P.min_3d3d_inliers;
+  rp.pmax = h->pmax;
+  hipLaunchKernelGGL(k_ransac, dim3(n), dim3(RS_BLOCK), ransac_smem(h->N), h->stream, (const double*)h->d_bear,
+                     (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
+                     (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
+                     want_masks ? h->d_mask : nullptr);
+  KMX_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd** out) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(params && out, KMX_EINVAL, "null argument");
+  KMX_CHECK(params->norm == KMX_NORM_L1 || params->norm == KMX_NORM_HAMMING, KMX_EINVAL, "bad norm");
+  KMX_CHECK(params->rng_variant == KMX_RNG_GCC9 || params->rng_variant == KMX_RNG_GCC11, KMX_EINVAL,
+            "bad rng variant");
+  KMX_CHECK(params->ransac_randomize == 0, KMX_EUNSUP, "ransac_randomize = 1 is not reproducible; use 0");
+  KMX_CHECK(params->use_1point_3d3d == 1, KMX_EUNSUP, "only the 1-point (given-rotation) 3D-3D check is built");
+  KMX_CHECK(params->ransac_max_iterations > 0, KMX_EINVAL, "ransac_max_iterations must be > 0");
+  int ndev = 0;
+  KMX_HIP(hipGetDeviceCount(&ndev));
+  KMX_CHECK(device >= 0 && device < ndev, KMX_EINVAL, "bad HIP device ordinal");
+  KMX_HIP(hipSetDevice(device));
+  kmx_lcd* h = new kmx_lcd();
+  h->P = *params;
+  h->device = device;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return kmx::fail(KMX_EHIP, "hipStreamCreate");
+  }
+  h->own_stream = true;
+  *out = h;
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_lcd_destroy(kmx_lcd* h) {
+  if (!h) return KMX_OK;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  lcd_free_pool(h);
+  lcd_free_cand(h);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return KMX_OK;
+}
+
+extern "C" int kmx_lcd_set_stream(kmx_lcd* h, void* s) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_HIP(hipSetDevice(h->device));
+  if (h->own_stream && h->stream) {
+    KMX_HIP(hipStreamSynchronize(h->stream));
+    KMX_HIP(hipStreamDestroy(h->stream));
+  }
+  h->own_stream = false;
+  h->stream = reinterpret_cast<hipStream_t>(s);
+  return KMX_OK;
+}
+
+extern "C" int kmx_lcd_set_frames(kmx_lcd* h, const kmx_lcd_batch_desc* pool) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(h && pool, KMX_EINVAL, "null argument");
+  KMX_CHECK(pool->n_frames > 0 && pool->max_feats >= 5 && pool->max_feats <= MAX_FEATS, KMX_EINVAL,
+            "need n_frames > 0 and 5 <= max_feats <= 1024");
+  KMX_CHECK(pool->n_feats && pool->desc && pool->bearings && pool->points, KMX_EINVAL, "null pool array");
+  for (int f = 0; f < pool->n_frames; ++f)
+    KMX_CHECK(pool->n_feats[f] >= 0 && pool->n_feats[f] <= pool->max_feats, KMX_EINVAL, "bad n_feats");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  const bool regrow = pool->max_feats != h->N;
+  lcd_free_pool(h);
+  if (regrow) lcd_free_cand(h);
+  h->F = pool->n_frames;
+  h->N = pool->max_feats;
+  const size_t FN = (size_t)h->F * h->N;
+  KMX_HIP(hipMalloc(&h->d_desc, FN * 32));
+  KMX_HIP(hipMalloc(&h->d_bear, FN * 3 * sizeof(double)));
+  KMX_HIP(hipMalloc(&h->d_pts, FN * 3 * sizeof(double)));
+  KMX_HIP(hipMalloc(&h->d_nfeat, sizeof(int) * h->F));
+  KMX_HIP(hipMemcpy(h->d_desc, pool->desc, FN * 32, hipMemcpyHostToDevice));
+  KMX_HIP(hipMemcpy(h->d_bear, pool->bearings, FN * 3 * sizeof(double), hipMemcpyHostToDevice));
+  KMX_HIP(hipMemcpy(h->d_pts, pool->points, FN * 3 * sizeof(double), hipMemcpyHostToDevice));
+  KMX_HIP(hipMemcpy(h->d_nfeat, pool->n_feats, sizeof(int) * h->F, hipMemcpyHostToDevice));
+  // every pass the serial loop can reach: (max_iter + 1) iterations + 10 * max_iter skips
+  h->pmax = h->P.ransac_max_iterations + 1 + 10 * h->P.ransac_max_iterations;
+  std::vector<short> tab;
+  build_table(h->P, h->N, h->pmax, tab);
+  KMX_HIP(hipMalloc(&h->d_table, sizeof(short) * tab.size()));
+  KMX_HIP(hipMemcpy(h->d_table, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+static int check_cands(kmx_lcd* h, int32_t n, const int32_t* cq, const int32_t* cm) {
+  KMX_CHECK(h && h->d_desc, KMX_ESTATE, "set_frames first");
+  KMX_CHECK(n >= 0 && (n == 0 || (cq && cm)), KMX_EINVAL, "bad candidate arrays");
+  for (int i = 0; i < n; ++i)
+    KMX_CHECK(cq[i] >= 0 && cq[i] < h->F && cm[i] >= 0 && cm[i] < h->F, KMX_EINVAL, "candidate frame id out of range");
+  return 0;
+}
+
+extern "C" int kmx_lcd_verify(kmx_lcd* h, int32_t n, const int32_t* cq, const int32_t* cm, kmx_lcd_result* results,
+                              uint8_t* inlier_masks) {
+  KMX_GUARD_BEGIN
+  if (int rc = check_cands(h, n, cq, cm)) return rc;
+  KMX_CHECK(results || n == 0, KMX_EINVAL, "null results");
+  KMX_HIP(hipSetDevice(h->device));
+  if (int rc = ensure_cap(h, n)) return rc;
+  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  if (int rc = enqueue_verify(h, n, inlier_masks != nullptr)) return rc;
+  if (n) KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, h->stream));
+  if (n && inlier_masks)
+    KMX_HIP(hipMemcpyAsync(inlier_masks, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_lcd_verify_async(kmx_lcd* h, int32_t n, const int32_t* cq, const int32_t* cm) {
+  KMX_GUARD_BEGIN
+  if (int rc = check_cands(h, n, cq, cm)) return rc;
+  KMX_HIP(hipSetDevice(h->device));
+  if (int rc = ensure_cap(h, n)) return rc;
+  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));  // host arrays may go away after return
+  return enqueue_verify(h, n, false);
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_lcd_sync(kmx_lcd* h) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+}
+
+// Stand-alone computeMatchedIndices on two host descriptor sets (one
+// candidate through the same kernel; uses a temporary context on device 0
+// of the calling thread's current device).
+extern "C" int kmx_lcd_knn2(int norm, double lowe_ratio, const uint8_t* q, int32_t nq, const uint8_t* mdesc,
+                            int32_t nm, int32_t* pairs_out, int32_t* k) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(k && pairs_out && (nq == 0 || q) && (nm == 0 || mdesc), KMX_EINVAL, "null argument");
+  KMX_CHECK(nq >= 0 && nm >= 0 && nq <= MAX_FEATS && nm <= MAX_FEATS, KMX_EINVAL, "at most 1024 descriptors");
+  KMX_CHECK(norm == KMX_NORM_L1 || norm == KMX_NORM_HAMMING, KMX_EINVAL, "bad norm");
+  const int N = std::max(std::max(nq, nm), 1);
+  std::vector<uint8_t> pool((size_t)2 * N * 32, 0);
+  if (nq) std::memcpy(pool.data(), q, (size_t)nq * 32);
+  if (nm) std::memcpy(pool.data() + (size_t)N * 32, mdesc, (size_t)nm * 32);
+  int nf[2] = {nq, nm}, cq = 0, cm = 1;
+  uint32_t* d_desc = nullptr;
+  int *d_nf = nullptr, *d_c = nullptr, *d_K = nullptr;
+  int2* d_pairs = nullptr;
+  auto cleanup = [&]() {
+    if (d_desc) (void)hipFree(d_desc);
+    if (d_nf) (void)hipFree(d_nf);
+    if (d_c) (void)hipFree(d_c);
+    if (d_K) (void)hipFree(d_K);
+    if (d_pairs) (void)hipFree(d_pairs);
+  };
+  if (hipMalloc(&d_desc, pool.size()) != hipSuccess || hipMalloc(&d_nf, sizeof(nf)) != hipSuccess ||
+      hipMalloc(&d_c, 2 * sizeof(int)) != hipSuccess || hipMalloc(&d_K, sizeof(int)) != hipSuccess ||
+      hipMalloc(&d_pairs, sizeof(int2) * N) != hipSuccess) {
+    cleanup();
+    return kmx::fail(KMX_ENOMEM, "hipMalloc");
+  }
+  int cc[2] = {cq, cm};
+  hipError_t e = hipMemcpy(d_desc, pool.data(), pool.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_nf, nf, sizeof(nf), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_c, cc, sizeof(cc), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_knn2, dim3(1), dim3(KNN_BLOCK), (size_t)N * 32 + sizeof(int) * (KNN_BLOCK + 1), 0,
+                       (const uint32_t*)d_desc, (const int*)d_nf, N, (const int*)d_c, (const int*)(d_c + 1), norm,
+                       lowe_ratio, d_pairs, d_K);
+    e = hipGetLastError();
+  }
+  int K = 0;
+  std::vector<int2> pr(N);
+  if (e == hipSuccess) e = hipMemcpy(&K, d_K, sizeof(int), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && K > 0) e = hipMemcpy(pr.data(), d_pairs, sizeof(int2) * K, hipMemcpyDeviceToHost);
+  cleanup();
+  if (e != hipSuccess) return kmx::fail(KMX_EHIP, hipGetErrorString(e));
+  for (int i = 0; i < K; ++i) {
+    pairs_out[2 * i] = pr[i].x;
+    pairs_out[2 * i + 1] = pr[i].y;
+  }
+  *k = K;
+  return KMX_OK;
+  KMX_GUARD_END
+}

@@ -77,7 +77,7 @@ class PgoCounters(C.Structure):
 
 class LcdParams(C.Structure):
     _fields_ = [
-        ("norm", C.c_int), ("lowe_ratio", C.c_float), ("min_2d2d_inliers", C.c_int),
+        ("norm", C.c_int), ("lowe_ratio", C.c_double), ("min_2d2d_inliers", C.c_int),
         ("min_3d3d_inliers", C.c_int), ("ransac_threshold_2d2d", C.c_double),
         ("ransac_threshold_3d3d", C.c_double), ("ransac_max_iterations", C.c_int),
         ("ransac_probability", C.c_double), ("ransac_randomize", C.c_int),
@@ -145,7 +145,7 @@ def lib() -> C.CDLL:
         "kmx_pgo_read_counters": ([P, C.POINTER(PgoCounters)], C.c_int),
     }
     optional = {
-        "kmx_lcd_knn2": ([C.c_int, C.c_float, pu8, i32, pu8, i32, pi32, pi32], C.c_int),
+        "kmx_lcd_knn2": ([C.c_int, C.c_double, pu8, i32, pu8, i32, pi32, pi32], C.c_int),
         "kmx_lcd_create": ([C.POINTER(LcdParams), C.c_int, C.POINTER(P)], C.c_int),
         "kmx_lcd_destroy": ([P], C.c_int),
         "kmx_lcd_set_stream": ([P, P], C.c_int),

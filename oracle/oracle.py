@@ -63,9 +63,7 @@ def _setup(L):
         fn = getattr(L, name)
         fn.argtypes = a
         fn.restype = r
-    if hasattr(L, "orc_lcd_knn2"):
-        L.orc_lcd_knn2.argtypes = [C.c_int, C.c_float, pu8, i32, pu8, i32, pi32, pi32]
-        L.orc_lcd_knn2.restype = C.c_int
+    _lcd_setup(L)
 
 
 def _f(a):
@@ -172,3 +170,83 @@ class OraclePGO:
         s = C.c_double(0)
         self.L.orc_pgo_eval(self.h, robot, mode, _f(Vin), _f(out), C.byref(s))
         return out, s.value
+
+
+# ------------------------------------------------------------------ LCD ---
+class LcdBatchDesc(C.Structure):
+    _fields_ = [
+        ("n_frames", C.c_int32), ("max_feats", C.c_int32), ("n_feats", C.POINTER(C.c_int32)),
+        ("desc", C.POINTER(C.c_uint8)), ("bearings", C.POINTER(C.c_double)), ("points", C.POINTER(C.c_double)),
+        ("n_cand", C.c_int32), ("cand_query", C.POINTER(C.c_int32)), ("cand_match", C.POINTER(C.c_int32)),
+    ]
+
+
+def batch_desc(pool):
+    """ctypes view of an LcdPool (keeps references alive on the struct)."""
+    d = LcdBatchDesc()
+    d._keep = [np.ascontiguousarray(pool.n_feats, dtype=np.int32), np.ascontiguousarray(pool.desc, dtype=np.uint8),
+               np.ascontiguousarray(pool.bearings, dtype=np.float64), np.ascontiguousarray(pool.points, dtype=np.float64),
+               np.ascontiguousarray(pool.cand_query, dtype=np.int32), np.ascontiguousarray(pool.cand_match, dtype=np.int32)]
+    nf, de, be, pt, cq, cm = d._keep
+    d.n_frames, d.max_feats = pool.n_frames, pool.max_feats
+    d.n_feats, d.desc, d.bearings, d.points = _i(nf), _u(de), _f(be), _f(pt)
+    d.n_cand, d.cand_query, d.cand_match = cq.shape[0], _i(cq), _i(cm)
+    return d
+
+
+def _lcd_setup(L):
+    from kmx.abi import LcdParams, LcdResult
+    i32, u8, f64 = C.c_int32, C.c_uint8, C.c_double
+    L.orc_mt19937_stream.argtypes = [C.c_uint32, C.c_int, i32, C.POINTER(i32)]
+    L.orc_ransac_samples.argtypes = [C.c_uint32, C.c_int, i32, i32, C.POINTER(i32)]
+    L.orc_lcd_knn2.argtypes = [C.c_int, f64, C.POINTER(u8), i32, C.POINTER(u8), i32, C.POINTER(i32), C.POINTER(i32)]
+    L.orc_fivept_nister.argtypes = [C.POINTER(f64), C.POINTER(f64), C.POINTER(f64)]
+    L.orc_lcd_verify_batch.argtypes = [C.POINTER(LcdParams), C.POINTER(LcdBatchDesc), i32, C.POINTER(i32),
+                                       C.POINTER(i32), C.POINTER(LcdResult), C.POINTER(u8)]
+    for n in ("orc_mt19937_stream", "orc_ransac_samples", "orc_lcd_knn2", "orc_fivept_nister", "orc_lcd_verify_batch"):
+        getattr(L, n).restype = C.c_int
+
+
+def mt19937_stream(seed, variant, n):
+    L = lib(); _lcd_setup(L)
+    out = np.empty(n, np.int32)
+    L.orc_mt19937_stream(seed, variant, n, _i(out))
+    return out
+
+
+def ransac_samples(seed, variant, K, passes):
+    L = lib(); _lcd_setup(L)
+    out = np.empty((passes, 5), np.int32)
+    rc = L.orc_ransac_samples(seed, variant, K, passes, _i(out))
+    assert rc == 0
+    return out
+
+
+def knn2(norm, lowe, q, m):
+    L = lib(); _lcd_setup(L)
+    q = np.ascontiguousarray(q, dtype=np.uint8); m = np.ascontiguousarray(m, dtype=np.uint8)
+    pairs = np.empty((max(q.shape[0], 1), 2), np.int32)
+    k = C.c_int32()
+    L.orc_lcd_knn2(norm, lowe, _u(q), q.shape[0], _u(m), m.shape[0], _i(pairs), C.byref(k))
+    return pairs[: k.value].copy()
+
+
+def fivept(f1, f2):
+    L = lib(); _lcd_setup(L)
+    f1 = np.ascontiguousarray(f1, dtype=np.float64); f2 = np.ascontiguousarray(f2, dtype=np.float64)
+    Es = np.empty((10, 9))
+    n = L.orc_fivept_nister(_f(f1), _f(f2), _f(Es))
+    return Es[:n].reshape(-1, 3, 3)
+
+
+def lcd_verify(params, pool, cand_query=None, cand_match=None, masks=True):
+    from kmx.abi import LcdResult
+    L = lib(); _lcd_setup(L)
+    cq = np.ascontiguousarray(pool.cand_query if cand_query is None else cand_query, dtype=np.int32)
+    cm = np.ascontiguousarray(pool.cand_match if cand_match is None else cand_match, dtype=np.int32)
+    d = batch_desc(pool)
+    res = (LcdResult * cq.shape[0])()
+    mk = np.zeros((cq.shape[0], pool.max_feats), np.uint8) if masks else None
+    L.orc_lcd_verify_batch(C.byref(params), C.byref(d), cq.shape[0], _i(cq), _i(cm), res,
+                           _u(mk) if masks else None)
+    return res, mk

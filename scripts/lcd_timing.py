@@ -1,0 +1,17 @@
+"""Quick LCD throughput probe (diagnostic)."""
+import sys, time
+from pathlib import Path
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "kimera-multi_amd"))
+import numpy as np
+from kmx.lcd import LcdParams, LoopClosureDetector
+from kmx.synth.lcd import make_lcd_pool
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+t = time.time(); pool = make_lcd_pool(n, 500, seed=0); print("gen", time.time() - t, flush=True)
+det = LoopClosureDetector(LcdParams()); det.set_pool(pool)
+det.verify(pool.cand_query[:64], pool.cand_match[:64])
+for rep in range(2):
+    t = time.time(); res, _ = det.verify(pool.cand_query, pool.cand_match); el = time.time() - t
+    acc = sum(r["accepted"] for r in res)
+    print(f"{n} candidates in {el*1e3:.1f} ms -> {n/el:.0f} cand/s, accepted {acc}, mean iters "
+          f"{np.mean([r['iterations_2d2d'] for r in res[0::2]]):.1f}", flush=True)

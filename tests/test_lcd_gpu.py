@@ -1,0 +1,51 @@
+"""GPU parity of the LCD verification path against the CPU restatement.
+
+Bar: bit-exact — identical match lists, identical 2D-2D / 3D-3D inlier sets
+(masks), identical iteration counts and identical poses (the RANSAC file is
+built with -ffp-contract=off and ports the oracle line by line)."""
+import numpy as np
+import pytest
+
+from kmx.lcd import LcdParams, LoopClosureDetector
+from kmx.synth.lcd import make_lcd_pool
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("norm", ["l1", "hamming"])
+def test_knn2_matches_oracle(gpu, norm):
+    from oracle import oracle as O
+    rng = np.random.default_rng(5)
+    for nq, nm in [(0, 10), (10, 0), (1, 1), (7, 2), (300, 500), (500, 300), (64, 1024)]:
+        q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+        m = rng.integers(0, 256, (nm, 32), dtype=np.uint8)
+        if nq and nm:  # plant near-duplicates and exact ties
+            k = min(nq, nm) // 2
+            q[:k] = m[:k] ^ (rng.random((k, 32)) < 0.02).astype(np.uint8)
+            if nm > 3:
+                m[nm - 1] = m[0]
+        gi, gj = LoopClosureDetector.compute_matched_indices(q, m, 0.7, norm)
+        nrm = 1 if norm == "hamming" else 0
+        ref = O.knn2(nrm, 0.7, q, m)
+        assert np.array_equal(gi, ref[:, 0]) and np.array_equal(gj, ref[:, 1]), (nq, nm)
+
+
+@pytest.mark.parametrize("variant,norm", [("gcc9", "l1"), ("gcc11", "hamming")])
+def test_verify_bit_exact(gpu, variant, norm):
+    from oracle import oracle as O
+    pool = make_lcd_pool(24, 300, seed=3)
+    p = LcdParams(rng_variant=variant, norm=norm)
+    det = LoopClosureDetector(p)
+    det.set_pool(pool)
+    got, gm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    ref, rm = O.lcd_verify(p.to_c(), pool)
+    for i in range(len(got)):
+        r = ref[i]
+        g = got[i]
+        assert (g["n_matches"], g["mono_inliers"], g["stereo_inliers"], g["accepted"], g["iterations_2d2d"]) == \
+            (r.n_matches, r.mono_inliers, r.stereo_inliers, bool(r.accepted), r.iterations_2d2d), i
+        assert np.array_equal(g["T_query_match"], np.array(r.T_query_match[:])), i
+    assert np.array_equal(gm, rm)
+    # planted loop closures are found, random pairs rejected
+    acc = np.array([g["accepted"] for g in got])
+    assert acc[0::2].all() and not acc[1::2].any()
