@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lcd", action="store_true")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no cpu / lcd)")
+    ap.add_argument("--lcd-frames", type=int, default=50_000)
+    ap.add_argument("--lcd-steps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -85,6 +87,49 @@ def cpu_baseline(g, X0, P, seconds):
     return {"value": edges_iters / el, "unit": "edges*iters/s", "cores": 1, "kind": "port",
             "sample": f"{rounds} RBCD rounds of {P and 'configs[3]'} (8 blocks, 1 RTR step, <=10 tCG) "
                       f"from the same initial iterate, oracle/dpgo_oracle.c -O3 x86-64-v3, 1 thread, {el:.1f} s"}
+
+
+def lcd_leg(args, rank, world, barrier_sync):
+    """configs[2]: 50k keyframes x 500 ORB descriptors, one candidate per query
+    (half planted loop closures), kNN2 + Lowe -> 2D-2D 5-point RANSAC -> 3D-3D.
+    Candidates are sharded across ranks (independent; no collective)."""
+    from kmx.lcd import LcdParams, LoopClosureDetector
+    from kmx.synth.lcd import make_lcd_pool
+    pool = make_lcd_pool(args.lcd_frames, 500, seed=0)
+    det = LoopClosureDetector(LcdParams(), device=int(os.environ.get("LOCAL_RANK", "0")))
+    det.set_pool(pool)
+    cq = pool.cand_query[rank::world].copy()
+    cm = pool.cand_match[rank::world].copy()
+    det.verify_async(cq, cm)  # warmup
+    det.sync()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.lcd_steps):
+        det.verify_async(cq, cm)
+    det.sync()
+    barrier_sync()
+    el = time.perf_counter() - t0
+    res, _ = det.verify(cq[:256], cm[:256])
+    out = {"metric": "LC candidates verified/sec", "n_local": int(cq.shape[0]), "steps": args.lcd_steps,
+           "elapsed": el, "accepted_frac_first256": sum(r["accepted"] for r in res) / max(len(res), 1),
+           "workload": f"configs[2]: {args.lcd_frames} keyframes x 500 ORB descriptors (32 B), "
+                       f"{pool.cand_query.shape[0]} candidates, L1 matcher, Lowe 0.7, 5-point RANSAC "
+                       "(thr 1e-6, <=500 it, p 0.995, seed 12345, GCC-9 sampler), 1-point 3D-3D 0.3 m"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, str(ROOT))
+        from oracle import oracle as O
+        p = LcdParams().to_c()
+        n, t0c, done = 0, time.perf_counter(), 0.0
+        while done < args.cpu_seconds * 0.5:
+            O.lcd_verify(p, pool, cand_query=pool.cand_query[n:n + 64], cand_match=pool.cand_match[n:n + 64],
+                         masks=False)
+            n += 64
+            done = time.perf_counter() - t0c
+        cpu = {"value": n / done, "unit": "candidates/s", "cores": 1, "kind": "port",
+               "sample": f"first {n} candidates of configs[2] (half planted), oracle/lcd_oracle.c, 1 thread, "
+                         f"{done:.1f} s"}
+    return out, cpu
 
 
 def load_traffic():
@@ -147,7 +192,7 @@ def main():
     achieved = hv_bytes / (hv_ms * 1e-3) if hv_ms > 0 else 0.0
     traffic = load_traffic()
     out = {
-        "metric": "dpgo edges*iters/sec",
+        "metric": "dpgo edges*iters/sec (+ LC candidates verified/sec in 'lcd')",
         "value": value,
         "unit": "edges*iters/s",
         "n_gpus": world,
@@ -181,6 +226,22 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu and not args.profile:
         out["cpu_baseline"] = cpu_baseline(g, X0, P, args.cpu_seconds)
+    if not args.no_lcd and not args.profile:
+        lcd, lcd_cpu = lcd_leg(args, rank, world, barrier_sync)
+        n_local, lel = float(lcd["n_local"] * lcd["steps"]), lcd["elapsed"]
+        if dist is not None:
+            t = torch.tensor([n_local, lel], dtype=torch.float64, device="cuda")
+            parts = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+            parts = torch.stack(parts).cpu().numpy()
+            n_local, lel = float(parts[:, 0].sum()), float(parts[:, 1].max())
+        lcd["value"] = n_local / lel
+        lcd["unit"] = "candidates/s"
+        lcd["ms_per_step"] = 1e3 * lel / lcd["steps"]
+        del lcd["elapsed"]
+        if lcd_cpu:
+            lcd["cpu_baseline"] = lcd_cpu
+        out["lcd"] = lcd
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -91,13 +91,17 @@ def make_lcd_pool(n_frames: int, n_feats: int = 500, *, true_frac: float = 0.5, 
     # true correspondences: same scene point, similar descriptor
     pts[mf[:, None], im_true] = pm_true
     pts[qf[:, None], iq_true] = pq_true
-    flips = rng.random((P, nt, 256)) < flip_frac
-    bits = np.unpackbits(desc[mf[:, None], im_true], axis=-1) ^ flips.astype(np.uint8)
-    desc[qf[:, None], iq_true] = np.packbits(bits, axis=-1)
+
+    def flip_masks(k):  # uint8 [P, k, 32] with each bit set w.p. flip_frac (chunked: bounded memory)
+        out = np.empty((P, k, 32), np.uint8)
+        for c0 in range(0, P, 1024):
+            c1 = min(P, c0 + 1024)
+            out[c0:c1] = np.packbits(rng.integers(0, 1 << 16, (c1 - c0, k, 256), dtype=np.uint16)
+                                     < int(flip_frac * (1 << 16)), axis=-1)
+        return out
+    desc[qf[:, None], iq_true] = desc[mf[:, None], im_true] ^ flip_masks(nt)
     # false look-alikes: similar descriptor, unrelated geometry
-    flips = rng.random((P, nf, 256)) < flip_frac
-    bits = np.unpackbits(desc[mf[:, None], im_false], axis=-1) ^ flips.astype(np.uint8)
-    desc[qf[:, None], iq_false] = np.packbits(bits, axis=-1)
+    desc[qf[:, None], iq_false] = desc[mf[:, None], im_false] ^ flip_masks(nf)
     bearings = _bearing(pts, rng, sb)
     if sp > 0:
         pts = pts + rng.normal(0, sp, pts.shape)
