@@ -35,7 +35,11 @@ def robot_ranges(n_robots: int, world: int) -> list[tuple[int, int]]:
 
 class RBCDDriver:
     def __init__(self, params: PGOAgentParameters, graph, *, rank: int = 0, world: int = 1,
-                 device: int = 0, seed: int = 0):
+                 device: int = 0, seed: int = 0, solver=None, exchange_device: str | None = None):
+        """`solver` defaults to a BlockSolver on HIP device `device`; any object
+        with the same exchange interface can be injected (the CPU gloo tests do).
+        `exchange_device` is where the collective buffers live ("cuda" for RCCL,
+        "cpu" for gloo)."""
         if world > graph.n_robots:
             raise ValueError("need at least one robot block per rank")
         self.params = params
@@ -46,16 +50,20 @@ class RBCDDriver:
         local = np.zeros(graph.n_robots, np.uint8)
         local[lo:hi] = 1
         self.local = local
-        self.solver = BlockSolver(params, device)
+        self.solver = solver if solver is not None else BlockSolver(params, device)
         self.rng = np.random.Generator(np.random.PCG64(seed))
         self.round_index = 0
         self.weight_updates = 0
         self._torch = None
+        self._xdev = exchange_device
         if world > 1:
             import torch
             import torch.distributed as dist
             self._torch, self._dist = torch, dist
-            self.solver.set_stream(torch.cuda.current_stream().cuda_stream)
+            if self._xdev is None:
+                self._xdev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+            if self._xdev == "cuda":
+                self.solver.set_stream(torch.cuda.current_stream().cuda_stream)
         self.solver.set_graph_data(graph, local)
         self.n_pub, self.first_owned, self.n_owned = self.solver.public_count()
         self.m_local = {a: self.solver.local_edges(a) for a in self.robots}
@@ -69,7 +77,7 @@ class RBCDDriver:
         counts = [None] * self.world
         dist.all_gather_object(counts, (self.first_owned, self.n_owned))
         self.max_owned = max(max(c[1] for c in counts), 1)
-        dev = torch.device("cuda", torch.cuda.current_device())
+        dev = torch.device("cuda", torch.cuda.current_device()) if self._xdev == "cuda" else torch.device("cpu")
         self._send = torch.zeros(self.max_owned * ps, dtype=torch.float64, device=dev)
         self._recv = torch.zeros(self.world * self.max_owned * ps, dtype=torch.float64, device=dev)
         # rows of the gathered buffer in public-table order
@@ -81,6 +89,14 @@ class RBCDDriver:
         self.n_shared = self.solver.shared_count()
         self._wshared = torch.zeros(max(self.n_shared, 1), dtype=torch.float64, device=dev)
 
+    def _all_gather(self, out, inp):
+        """One all-gather of equal-size chunks (RCCL: into one tensor; gloo has
+        no all_gather_into_tensor, so gather a list of views)."""
+        if self._xdev == "cuda":
+            self._dist.all_gather_into_tensor(out, inp)
+        else:
+            self._dist.all_gather(list(out.chunk(self.world)), inp)
+
     def exchange_public(self):
         """publishPublicPoses -> updateNeighborPoses for the whole team."""
         if self.world == 1:
@@ -89,7 +105,7 @@ class RBCDDriver:
         torch, dist = self._torch, self._dist
         ps = 4 * self.params.r
         self.solver.pack_public(self._send.data_ptr())
-        dist.all_gather_into_tensor(self._recv, self._send)
+        self._all_gather(self._recv, self._send)
         if self.n_pub:
             rows = self._recv.view(-1, ps).index_select(0, self._row_index)
             self._table.view(-1, ps).copy_(rows)

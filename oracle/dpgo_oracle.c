@@ -140,6 +140,19 @@ int orc_pgo_refresh(void* vh) {
   memcpy(h->nbr, h->X, sizeof(double) * (size_t)h->ntot * PS(h));
   return 0;
 }
+/* updateNeighborPoses: overwrite neighbour-table rows (robot, pose) with X rows */
+int orc_pgo_set_nbr_rows(void* vh, int64_t n, const int32_t* robot, const int32_t* pose, const double* X) {
+  orc_pgo* h = (orc_pgo*)vh;
+  for (int64_t i = 0; i < n; ++i)
+    memcpy(h->nbr + (h->poff[robot[i]] + pose[i]) * PS(h), X + i * PS(h), sizeof(double) * PS(h));
+  return 0;
+}
+int orc_pgo_get_x_rows(void* vh, int64_t n, const int32_t* robot, const int32_t* pose, double* X) {
+  orc_pgo* h = (orc_pgo*)vh;
+  for (int64_t i = 0; i < n; ++i)
+    memcpy(X + i * PS(h), h->X + (h->poff[robot[i]] + pose[i]) * PS(h), sizeof(double) * PS(h));
+  return 0;
+}
 int orc_pgo_get_weights(void* vh, double* w) {
   orc_pgo* h = (orc_pgo*)vh;
   memcpy(w, h->w, sizeof(double) * h->m);
@@ -494,6 +507,19 @@ int orc_pgo_round(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
   return 0;
 }
 
+/* Round against the neighbour table as last installed (no refresh): the
+ * multi-process form, where neighbour rows arrive by exchange. */
+int orc_pgo_round_nbr(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
+  orc_pgo* h = (orc_pgo*)vh;
+  for (int a = 0; a < h->R; ++a) {
+    kmx_iter_stats st;
+    memset(&st, 0, sizeof(st));
+    if (active[a]) block_update(h, a, &st);
+    if (stats) stats[a] = st;
+  }
+  return 0;
+}
+
 /* Same round with the robot blocks spread over `threads` OpenMP threads (one
  * block per thread at a time; blocks write disjoint iterate slices). This is
  * the all-cores CPU baseline of BASELINE.md §2.4. */
@@ -548,6 +574,26 @@ int orc_pgo_update_weights(void* vh, double* mu_used) {
     if (h->fixed[e]) continue;
     const double* Xi = h->X + (h->poff[h->r1[e]] + h->p1[e]) * ps;
     const double* Xj = h->X + (h->poff[h->r2[e]] + h->p2[e]) * ps;
+    h->w[e] = gnc_tls_weight(residual_sq(h, e, Xi, Xj), h->mu, h->P.gnc_barc);
+  }
+  h->mu *= h->P.gnc_mu_step;
+  return 0;
+}
+
+/* Owner's-view sweep for a process that holds only the robots in `local`:
+ * edges owned by a local robot (owner = min(r1, r2), drawio:2198); the owner's
+ * endpoint from its iterate, the other robot's from the neighbour table. */
+int orc_pgo_update_weights_owned(void* vh, const uint8_t* local, double* mu_used) {
+  orc_pgo* h = (orc_pgo*)vh;
+  if (mu_used) *mu_used = h->mu;
+  if (h->P.robust_cost != KMX_COST_GNC_TLS) return 0;
+  const int ps = PS(h);
+  for (int64_t e = 0; e < h->m; ++e) {
+    if (h->fixed[e]) continue;
+    const int owner = h->r1[e] < h->r2[e] ? h->r1[e] : h->r2[e];
+    if (!local[owner]) continue;
+    const double* Xi = (h->r1[e] == owner ? h->X : h->nbr) + (h->poff[h->r1[e]] + h->p1[e]) * ps;
+    const double* Xj = (h->r2[e] == owner ? h->X : h->nbr) + (h->poff[h->r2[e]] + h->p2[e]) * ps;
     h->w[e] = gnc_tls_weight(residual_sq(h, e, Xi, Xj), h->mu, h->P.gnc_barc);
   }
   h->mu *= h->P.gnc_mu_step;

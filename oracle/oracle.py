@@ -55,6 +55,10 @@ def _setup(L):
         "orc_pgo_local_edges": ([P, C.c_int], i64),
         "orc_pgo_round": ([P, pu8, C.POINTER(IterStats)], C.c_int),
         "orc_pgo_round_mt": ([P, pu8, C.POINTER(IterStats), C.c_int], C.c_int),
+        "orc_pgo_round_nbr": ([P, pu8, C.POINTER(IterStats)], C.c_int),
+        "orc_pgo_update_weights_owned": ([P, pu8, pf64], C.c_int),
+        "orc_pgo_set_nbr_rows": ([P, i64, pi32, pi32, pf64], C.c_int),
+        "orc_pgo_get_x_rows": ([P, i64, pi32, pi32, pf64], C.c_int),
         "orc_pgo_update_weights": ([P, pf64], C.c_int),
         "orc_pgo_get_trajectory": ([P, C.c_int, pf64, pf64], C.c_int),
         "orc_pgo_eval": ([P, C.c_int, C.c_int, pf64, pf64, pf64], C.c_int),
@@ -132,9 +136,34 @@ class OraclePGO:
             self.L.orc_pgo_round(self.h, _u(act), stats)
         return [s.as_dict() for s in stats]
 
+    def iterate_nbr(self, active=None):
+        """Round against the installed neighbour table (no refresh)."""
+        from kmx.abi import IterStats
+        act = np.ones(self.n_robots, np.uint8) if active is None else np.ascontiguousarray(active, dtype=np.uint8)
+        stats = (IterStats * self.n_robots)()
+        self.L.orc_pgo_round_nbr(self.h, _u(act), stats)
+        return [s.as_dict() for s in stats]
+
+    def set_nbr_rows(self, robots, poses, X):
+        r = np.ascontiguousarray(robots, dtype=np.int32); p = np.ascontiguousarray(poses, dtype=np.int32)
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        self.L.orc_pgo_set_nbr_rows(self.h, r.shape[0], _i(r), _i(p), _f(X))
+
+    def get_x_rows(self, robots, poses):
+        r = np.ascontiguousarray(robots, dtype=np.int32); p = np.ascontiguousarray(poses, dtype=np.int32)
+        X = np.empty((r.shape[0], self.r, 4))
+        self.L.orc_pgo_get_x_rows(self.h, r.shape[0], _i(r), _i(p), _f(X))
+        return X
+
     def update_weights(self):
         mu = C.c_double(0)
         self.L.orc_pgo_update_weights(self.h, C.byref(mu))
+        return mu.value
+
+    def update_weights_owned(self, local):
+        loc = np.ascontiguousarray(local, dtype=np.uint8)
+        mu = C.c_double(0)
+        self.L.orc_pgo_update_weights_owned(self.h, _u(loc), C.byref(mu))
         return mu.value
 
     def get_weights(self):

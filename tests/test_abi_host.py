@@ -1,0 +1,82 @@
+"""C-ABI library and host logic (no GPU needed)."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_library_exports_every_header_symbol():
+    from kmx import abi
+    L = abi.lib()
+    hdr = (ROOT / "include" / "kmx_abi.h").read_text()
+    names = sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(kmx_\w+)\s*\(", hdr, re.M)))
+    assert len(names) > 30
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert L.kmx_abi_version() == 1
+
+
+def test_no_cpu_fallback_without_gpu():
+    from kmx import abi
+    if abi.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    from kmx.dpgo.params import PGOAgentParameters
+    from kmx.dpgo.solver import BlockSolver
+    with pytest.raises(abi.KmxError):
+        BlockSolver(PGOAgentParameters(), 0)
+    from kmx.lcd import LoopClosureDetector
+    with pytest.raises(abi.KmxError):
+        LoopClosureDetector()
+
+
+def test_params_to_c_and_yaml(tmp_path):
+    from kmx.dpgo.params import PGOAgentParameters, error_threshold_at_quantile
+    c = PGOAgentParameters(r=6).to_c()
+    assert (c.d, c.r, c.tcg_max_iterations, c.robust_cost) == (3, 6, 10, 1)
+    assert abs(error_threshold_at_quantile(0.9, 3) - 3.26261) < 1e-4  # sqrt(chi2inv(0.9, 6) = 10.6446)
+    from kmx.lcd import LcdParams
+    y = tmp_path / "LcdParams.yaml"
+    y.write_text("%YAML:1.0\nlowe_ratio: 0.8\nmatcher_type: 4\nransac_max_iterations: 100\n"
+                 "min_nr_2d2d_inliers: 12\nransac_threshold_3d3d: 0.25\n")
+    p = LcdParams.from_yaml(str(y))
+    assert (p.lowe_ratio, p.norm, p.ransac_max_iterations, p.min_nr_2d2d_inliers) == (0.8, "hamming", 100, 12)
+    cp = p.to_c()
+    assert cp.norm == 1 and cp.ransac_threshold_3d3d == 0.25
+
+
+def test_reference_lcdparams_yaml_if_present():
+    f = Path("/root/reference/params/D455/LcdParams.yaml")
+    if not f.exists():
+        pytest.skip("reference not mounted")
+    from kmx.lcd import LcdParams
+    p = LcdParams.from_yaml(str(f))
+    assert (p.lowe_ratio, p.norm, p.ransac_max_iterations, p.ransac_probability) == (0.7, "l1", 500, 0.995)
+    assert (p.min_nr_2d2d_inliers, p.min_nr_3d3d_inliers, p.ransac_threshold_2d2d) == (10, 5, 1e-6)
+
+
+def test_synthetic_generators_are_deterministic():
+    from kmx.synth import make_pose_graph
+    from kmx.synth.lcd import make_lcd_pool
+    a, b = make_pose_graph(3, 300, 900, seed=5), make_pose_graph(3, 300, 900, seed=5)
+    for f in ("r1", "p1", "r2", "p2", "R", "t", "fixed"):
+        assert np.array_equal(getattr(a, f), getattr(b, f))
+    assert a.m == 900 and a.n_total == 300
+    sh = a.r1 != a.r2
+    assert 0 < sh.sum() < a.m
+    # measurements are rotations
+    assert np.abs(np.einsum("nji,njk->nik", a.R, a.R) - np.eye(3)).max() < 1e-12
+    p, q = make_lcd_pool(8, 64, seed=1), make_lcd_pool(8, 64, seed=1)
+    assert np.array_equal(p.desc, q.desc) and np.array_equal(p.bearings, q.bearings)
+    assert np.allclose(np.linalg.norm(p.bearings, axis=-1), 1.0)
+
+
+def test_robot_ranges_and_lifting():
+    from kmx.dpgo.driver import robot_ranges
+    from kmx.synth import lifting_matrix
+    assert robot_ranges(8, 3) == [(0, 2), (2, 5), (5, 8)]
+    assert robot_ranges(8, 8)[7] == (7, 8)
+    Y = lifting_matrix(5)
+    assert np.abs(Y.T @ Y - np.eye(3)).max() < 1e-14
