@@ -218,7 +218,11 @@ def main():
             "peak": PEAK_HBM / 1e9,
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM,
-            "traffic": (traffic or {}).get("bytes_per_launch") if traffic else None,
+            # PMC bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section),
+            # measured as a ratio to the algorithmic bytes of the same dispatches
+            # (scripts/gpu_pmc_hess.sh -> profiles/hessvec_traffic.json) and applied to this run's launches
+            "traffic": (traffic["traffic_over_alg"] * hv_bytes / max(hv_n, 1)) if traffic else None,
+            "traffic_over_alg": traffic["traffic_over_alg"] if traffic else None,
             "launches": hv_n,
             "avg_launch_us": 1e3 * hv_ms / max(hv_n, 1),
             "alg_bytes_per_launch": hv_bytes / max(hv_n, 1),

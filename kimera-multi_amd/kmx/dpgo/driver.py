@@ -38,8 +38,9 @@ class RBCDDriver:
                  device: int = 0, seed: int = 0, solver=None, exchange_device: str | None = None):
         """`solver` defaults to a BlockSolver on HIP device `device`; any object
         with the same exchange interface can be injected (the CPU gloo tests do).
-        `exchange_device` is where the collective buffers live ("cuda" for RCCL,
-        "cpu" for gloo)."""
+        `exchange_device` is where the collective runs ("cuda" for RCCL, "cpu"
+        for gloo). A GPU solver under gloo packs into device buffers and stages
+        them through host copies (used to test N ranks on one GPU)."""
         if world > graph.n_robots:
             raise ValueError("need at least one robot block per rank")
         self.params = params
@@ -62,7 +63,7 @@ class RBCDDriver:
             self._torch, self._dist = torch, dist
             if self._xdev is None:
                 self._xdev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-            if self._xdev == "cuda":
+            if getattr(self.solver, "device_pointers", False):  # order kmx work with torch's copies
                 self.solver.set_stream(torch.cuda.current_stream().cuda_stream)
         self.solver.set_graph_data(graph, local)
         self.n_pub, self.first_owned, self.n_owned = self.solver.public_count()
@@ -77,7 +78,9 @@ class RBCDDriver:
         counts = [None] * self.world
         dist.all_gather_object(counts, (self.first_owned, self.n_owned))
         self.max_owned = max(max(c[1] for c in counts), 1)
-        dev = torch.device("cuda", torch.cuda.current_device()) if self._xdev == "cuda" else torch.device("cpu")
+        on_gpu = bool(getattr(self.solver, "device_pointers", False))
+        self._stage = on_gpu and self._xdev != "cuda"
+        dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
         self._send = torch.zeros(self.max_owned * ps, dtype=torch.float64, device=dev)
         self._recv = torch.zeros(self.world * self.max_owned * ps, dtype=torch.float64, device=dev)
         # rows of the gathered buffer in public-table order
@@ -94,6 +97,11 @@ class RBCDDriver:
         no all_gather_into_tensor, so gather a list of views)."""
         if self._xdev == "cuda":
             self._dist.all_gather_into_tensor(out, inp)
+        elif self._stage:
+            self.solver.sync()
+            ho, hi = out.cpu(), inp.cpu()
+            self._dist.all_gather(list(ho.chunk(self.world)), hi)
+            out.copy_(ho)
         else:
             self._dist.all_gather(list(out.chunk(self.world)), inp)
 
@@ -118,7 +126,13 @@ class RBCDDriver:
         mu = self.solver.update_weights()
         if self.world > 1 and self.n_shared:
             self.solver.pack_shared_weights(self._wshared.data_ptr())
-            self._dist.all_reduce(self._wshared)
+            if self._stage:
+                self.solver.sync()
+                hw = self._wshared.cpu()
+                self._dist.all_reduce(hw)
+                self._wshared.copy_(hw)
+            else:
+                self._dist.all_reduce(self._wshared)
             self.solver.unpack_shared_weights(self._wshared.data_ptr())
         self.weight_updates += 1
         return mu

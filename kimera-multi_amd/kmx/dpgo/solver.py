@@ -16,6 +16,8 @@ from .params import PGOAgentParameters
 
 
 class BlockSolver:
+    device_pointers = True  # pack/unpack take HIP device pointers
+
     def __init__(self, params: PGOAgentParameters, device: int = 0):
         self.params = params
         self.r = params.r

@@ -1,0 +1,16 @@
+# usage: bash scripts/gpu_pmc_hess.sh [tag] — HBM traffic of the dpgo kernels:
+# separate rocprofv3 --pmc passes (kernel trace only) over `bench.py --profile --warmup 0`,
+# so every profiled k_hess dispatch is also counted in the bench JSON of that pass.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${1:-pmc}
+mkdir -p gpurun_out/$TAG
+i=0
+for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $C -d gpurun_out/$TAG/p$i -o run --output-format csv -- python3 bench.py --steps 6 --warmup 0 --profile > gpurun_out/$TAG/p$i.json 2> gpurun_out/$TAG/p$i.err
+  rc=$?; echo "pmc pass $i ($C) rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0

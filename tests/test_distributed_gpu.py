@@ -1,0 +1,91 @@
+"""Two ranks on one MI355X (gloo exchange staged through host copies) running
+the real HIP solver: the distributed RBCD iterates and GNC weights must equal
+the single-process GPU run bit for bit (per-robot reductions are ordered the
+same whatever the rank placement)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from kmx.synth import lift, lifting_matrix, make_pose_graph
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph():
+    return make_pose_graph(4, 2000, 5000, seed=3)
+
+
+def _params():
+    from kmx.dpgo.params import PGOAgentParameters
+    P = PGOAgentParameters(r=5)
+    P.robustOptInnerIters = 4
+    P.schedule = 1
+    return P
+
+
+def _x0(g):
+    Y = lifting_matrix(5, seed=1)
+    return {a: lift(g.init_R[a], g.init_t[a], Y) for a in range(g.n_robots)}
+
+
+def _run(drv, rounds):
+    for _ in range(rounds):
+        drv.step(with_stats=True)
+    drv.solver.sync()
+    return {a: drv.iterate_of(a) for a in drv.robots}, drv.solver.get_weights()
+
+
+def _worker(rank, world, port, rounds, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kmx.dpgo.driver import RBCDDriver
+    g, P = _graph(), _params()
+    drv = RBCDDriver(P, g, rank=rank, world=world, device=0, exchange_device="cpu")
+    drv.initialize(_x0(g))
+    X, w = _run(drv, rounds)
+    q.put((rank, X, w, list(drv.robots)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(600)
+def test_two_ranks_one_gpu_match_single_process(gpu):
+    from kmx.dpgo.driver import RBCDDriver
+    rounds = 10
+    g, P = _graph(), _params()
+    drv = RBCDDriver(P, g, device=0)
+    drv.initialize(_x0(g))
+    X1, w1 = _run(drv, rounds)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in procs:
+            rank, X, w, robots = q.get(timeout=420)
+            got.update(X)
+            sel = np.isin(g.r1, robots) | np.isin(g.r2, robots)  # edges this rank's blocks see
+            assert np.array_equal(w[sel], w1[sel]), rank
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for a in range(g.n_robots):
+        assert np.array_equal(got[a], X1[a]), a
