@@ -77,6 +77,18 @@ class OracleBlockSolver:
     def sync(self):
         pass
 
+    def set_neighbor_poses(self, robots, poses, X):
+        self.o.set_nbr_rows(np.asarray(robots, np.int32), np.asarray(poses, np.int32), np.asarray(X, np.float64))
+
+    def get_weights(self, base=None):
+        return self.o.get_weights()
+
+    def set_weights(self, w):
+        self.o.set_weights(np.asarray(w, np.float64))
+
+    def trajectory(self, robot, anchor):
+        return self.o.trajectory(robot, anchor)
+
     def update_weights(self):
         return self.o.update_weights_owned(self.local)
 
