@@ -15,8 +15,9 @@
 //     with in-group shuffles in a fixed order.
 //   * Node-centric gather over a CSR incidence list (no atomics): every output
 //     element accumulates its incident edges in increasing edge id, the same
-//     order as the CPU restatement's edge loop, and kernels are built with
-//     -ffp-contract=off, so per-element results match the oracle bit for bit.
+//     order as the CPU restatement's edge loop (FMA contraction on: per-element
+//     results agree with the oracle to ~1e-15; `make FPC=off` reproduces its
+//     roundings).
 //   * Reductions: one partial per workgroup tile, reduced in fixed order by a
 //     one-workgroup control kernel that also runs the RTR / tCG scalar logic.
 #include <hip/hip_runtime.h>
