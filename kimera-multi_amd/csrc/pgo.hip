@@ -37,6 +37,11 @@
 namespace {
 
 constexpr int WAVES = 4;
+// Minimum waves per SIMD for the gather kernels (k_grad / k_hess / k_cost):
+// caps their VGPRs so enough waves are resident to hide the gather latency.
+#ifndef KMX_LB_GATHER
+#define KMX_LB_GATHER 5
+#endif
 constexpr int BLOCK = 64 * WAVES;
 constexpr int NPART = 4;  // partial sums per tile
 
@@ -77,6 +82,14 @@ struct Dev {
   const int* inc_ptr; // [nloc+1]
   const int2* inc;    // x = other (>=0 local pose, <0 -> public slot -1-x); y = edge | tail<<31
   double* irec;       // [ninc][16] per-incidence edge record in CSR order: R(9) t(3) w*kappa w*tau 0 0
+  double* crec;       // [ninc][12] compact record (gather variant 3): R rows 0-1 (6) t(3) w*kappa w*tau
+                      // {other, edge|tail<<31} — R row 2 = row 0 x row 1 (used only when every
+                      // local measurement rotation satisfies that to 1e-12; see kmx_pgo_set_graph)
+  double* ocrec;      // [m_own][12] compact records of the owner incidences only (each local edge
+                      // once: the tail of a local-local edge, the local end of a shared one), CSR by pose
+  const int* optr;    // [nloc+1] CSR pointers into ocrec
+  const int2* eopos;  // [mloc] positions of each local edge in ocrec (a shared edge with both
+                      // robots on this handle has two owner incidences; -1 = none)
   double* ekappa;     // [mloc] per local edge
   double* etau;
   double* ew;         // GNC weight
@@ -163,18 +176,24 @@ __device__ __forceinline__ double incidence_row(const Edge& E, bool self_tail, c
   return 0.5 * (E.wk * (ER[0] * ER[0] + ER[1] * ER[1] + ER[2] * ER[2]) + E.wt * Et * Et);
 }
 
-// S = sym(Y^T G_Y) for the pose group (9 entries, identical in all R lanes).
+// S = sym(Y^T G_Y) for the pose group (9 entries, identical in all R lanes):
+// the 6 distinct entries are group sums of the symmetrised products. Each sum
+// is chained to the previous one (empty asm) so only one sum's R shuffles are
+// in flight: interleaving all of them held ~90 VGPRs and capped k_hess at 3
+// waves/SIMD.
 template <int R>
 __device__ __forceinline__ void group_symYtG(const double y[4], const double G[4], int base, double S[9]) {
-  double M[9];
+  double prev = 0.0;
 #pragma unroll
   for (int c = 0; c < 3; ++c)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) M[c * 3 + k] = gsum<R>(y[c] * G[k], base);
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) S[c * 3 + k] = 0.5 * (M[c * 3 + k] + M[k * 3 + c]);
+    for (int k = c; k < 3; ++k) {
+      double x = 0.5 * (y[c] * G[k] + y[k] * G[c]);
+      asm volatile("" : "+v"(x) : "v"(prev));
+      prev = gsum<R>(x, base);
+      S[c * 3 + k] = prev;
+      S[k * 3 + c] = prev;
+    }
 }
 
 // Tangent projection of row V at Y (group-cooperative): V_Y - Y sym(Y^T V_Y).
@@ -190,24 +209,18 @@ __device__ __forceinline__ void group_proj(const double y[4], const double V[4],
 template <int R>
 __device__ __forceinline__ void group_precon(const Dev& d, int pose, bool valid, const double y[4],
                                              const double V[4], int base, double out[4]) {
-  double buf[4];
+  double buf[4] = {0.0, 0.0, 0.0, 0.0};
   if (d.p.use_precond) {
-    double P[16];
-    if (valid) {
-      const double2* q = reinterpret_cast<const double2*>(d.Pinv + 16 * (size_t)pose);
+    // buf = V P, one 4-double row of P at a time (keeps 8 VGPRs of P live)
+    const double* Pp = d.Pinv + 16 * (size_t)pose;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        double2 v = q[i];
-        P[2 * i] = v.x;
-        P[2 * i + 1] = v.y;
-      }
-    } else {
+    for (int i = 0; i < 4; ++i) {
+      double Pr[4] = {0.0, 0.0, 0.0, 0.0};
+      if (valid) load4(Pp + 4 * i, Pr);
+      asm volatile("" : "+v"(Pr[0]), "+v"(Pr[1]), "+v"(Pr[2]), "+v"(Pr[3]) : "v"(buf[0]));
 #pragma unroll
-      for (int i = 0; i < 16; ++i) P[i] = 0.0;
+      for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * Pr[k] : buf[k] + V[i] * Pr[k];
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      buf[k] = V[0] * P[0 * 4 + k] + V[1] * P[1 * 4 + k] + V[2] * P[2 * 4 + k] + V[3] * P[3 * 4 + k];
     group_proj<R>(y, buf, base, out);
   } else {
 #pragma unroll
@@ -499,11 +512,63 @@ __device__ __forceinline__ void lane_gather_plain(const Dev& d, const Lane& L, c
   }
 }
 
+// Compact-record variant (G = 3): 96-B records carry the neighbour index, so
+// the incidence loop reads one record (6 x 16 B) and one neighbour row — no
+// separate CSR entry — and the third rotation row is rebuilt as row0 x row1.
+// OWN (cost only, G = 4): visit each edge once — the tail incidence of a
+// local-local edge, or the only local incidence of a shared edge — from a
+// second compact array holding just those records (half the record bytes).
+__device__ __forceinline__ int2 unpack_int2(double v) {
+  const long long b = __double_as_longlong(v);
+  return make_int2((int)(b & 0xffffffffll), (int)(b >> 32));
+}
+__device__ __forceinline__ void edge_from_compact(const double2 q[6], Edge& E) {
+  E.R[0] = q[0].x; E.R[1] = q[0].y; E.R[2] = q[1].x;
+  E.R[3] = q[1].y; E.R[4] = q[2].x; E.R[5] = q[2].y;
+  E.R[6] = E.R[1] * E.R[5] - E.R[2] * E.R[4];
+  E.R[7] = E.R[2] * E.R[3] - E.R[0] * E.R[5];
+  E.R[8] = E.R[0] * E.R[4] - E.R[1] * E.R[3];
+  E.t[0] = q[3].x; E.t[1] = q[3].y; E.t[2] = q[4].x;
+  E.wk = q[4].y;
+  E.wt = q[5].x;
+}
+
+template <int R, bool PUB, bool OWN>
+__device__ __forceinline__ void lane_gather_compact(const Dev& d, const Lane& L, const double* V,
+                                                    const double* pub, double acc[4], double* cost) {
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  if (!L.valid) return;
+  double vs[4];
+  load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
+  const int* ptr = OWN ? d.optr : d.inc_ptr;
+  const double* rec = OWN ? d.ocrec : d.crec;
+  const int k0 = ptr[L.pose], k1 = ptr[L.pose + 1];
+  for (int k = k0; k < k1; ++k) {
+    const double2* q2 = reinterpret_cast<const double2*>(rec + 12 * (size_t)k);
+    double2 q[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = q2[i];
+    const int2 in = unpack_int2(q[5].y);
+    const int o = in.x;
+    const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V);
+    const double2* b2 = reinterpret_cast<const double2*>(base + 4 * L.a);
+    double2 v0 = b2[0], v1 = b2[1];
+    if (!PUB && o < 0) v0 = v1 = make_double2(0.0, 0.0);
+    Edge E;
+    edge_from_compact(q, E);
+    const double vo[4] = {v0.x, v0.y, v1.x, v1.y};
+    const double c = incidence_row(E, (in.y >> 31) & 1, vs, vo, acc);
+    if (cost) *cost += (OWN || o < 0) ? c : 0.5 * c;
+  }
+}
+
 template <int R, int G, bool PUB>
 __device__ __forceinline__ void gather(const Dev& d, const Lane& L, const double* V, const double* pub,
                                        double acc[4], double* cost, char* smem) {
   if constexpr (G == 0) lane_gather<R, PUB>(d, L, V, pub, acc, cost);
   else if constexpr (G == 2) lane_gather_plain<R, PUB>(d, L, V, pub, acc, cost);
+  else if constexpr (G == 3) lane_gather_compact<R, PUB, false>(d, L, V, pub, acc, cost);
+  else if constexpr (G == 4) lane_gather_compact<R, PUB, true>(d, L, V, pub, acc, cost);
   else tile_gather<R, PUB>(d, L, V, pub, acc, cost, smem);
 }
 
@@ -686,7 +751,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_) {
 // Start of an RTR iteration: egrad (gather X with public neighbours), cost,
 // S = sym(Y^T egrad_Y), g = P_Y(egrad), r = g, z = precon(g).
 template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK) void k_grad(Dev d) {
+__global__ __launch_bounds__(BLOCK, KMX_LB_GATHER) void k_grad(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_START) return;
@@ -705,25 +770,30 @@ __global__ __launch_bounds__(BLOCK) void k_grad(Dev d) {
     vals[1] = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2] + gr[3] * gr[3];
     vals[2] = zr[0] * gr[0] + zr[1] * gr[1] + zr[2] * gr[2] + zr[3] * gr[3];
   }
-  // ticket first: the fused reduction's drain then waits only for the partials
-  finish_tile<RED_GRAD, 3, F>(d, L, vals, smem + Smem<R>::red_off, R);
-  if (L.valid) {
-    const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-    store4(d.g + o, gr);
-    store4(d.r + o, gr);
-    store4(d.z + o, zr);
-    if (L.a == 0) {
-      double* Sp = d.S + 9 * (size_t)L.pose;
+  auto store = [&]() {
+    if (L.valid) {
+      const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+      store4(d.g + o, gr);
+      store4(d.r + o, gr);
+      store4(d.z + o, zr);
+      if (L.a == 0) {
+        double* Sp = d.S + 9 * (size_t)L.pose;
 #pragma unroll
-      for (int i = 0; i < 9; ++i) Sp[i] = S[i];
+        for (int i = 0; i < 9; ++i) Sp[i] = S[i];
+      }
     }
-  }
+  };
+  // separate reduce launch: store first (frees S, g, z before the block sum);
+  // fused reduction: ticket first, so its drain waits only for the partials
+  if constexpr (!F) store();
+  finish_tile<RED_GRAD, 3, F>(d, L, vals, smem + Smem<R>::red_off, R);
+  if constexpr (F) store();
 }
 
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old.
 template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK) void k_hess(Dev d) {
+__global__ __launch_bounds__(BLOCK, KMX_LB_GATHER) void k_hess(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   const Ctl& c = d.ctl[L.l];
@@ -733,6 +803,7 @@ __global__ __launch_bounds__(BLOCK) void k_hess(Dev d) {
   double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4], S[9];
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   gather<R, GV, false>(d, L, d.z, nullptr, H, nullptr, smem);
+  asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
   if (L.valid) {
     load4(d.z + o, zs);
     load4(d.X + o, y);
@@ -851,12 +922,12 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
 }
 
 template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK) void k_cost(Dev d) {
+__global__ __launch_bounds__(BLOCK, KMX_LB_GATHER) void k_cost(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
   double acc[4], cost = 0.0;
-  gather<R, GV, true>(d, L, d.Xt, d.pub, acc, &cost, smem);
+  gather<R, (GV == 3 ? 4 : GV), true>(d, L, d.Xt, d.pub, acc, &cost, smem);
   finish_tile<RED_COST, 1, F>(d, L, &cost, smem + Smem<R>::red_off, R);
 }
 
@@ -1012,6 +1083,13 @@ __global__ void k_apply_weights(Dev d, int mloc) {
   const int2 ip = d.eipos[e];
   if (ip.x >= 0) { d.irec[16 * (size_t)ip.x + 12] = wk; d.irec[16 * (size_t)ip.x + 13] = wt; }
   if (ip.y >= 0) { d.irec[16 * (size_t)ip.y + 12] = wk; d.irec[16 * (size_t)ip.y + 13] = wt; }
+  if (d.crec) {
+    if (ip.x >= 0) { d.crec[12 * (size_t)ip.x + 9] = wk; d.crec[12 * (size_t)ip.x + 10] = wt; }
+    if (ip.y >= 0) { d.crec[12 * (size_t)ip.y + 9] = wk; d.crec[12 * (size_t)ip.y + 10] = wt; }
+    const int2 op = d.eopos[e];
+    if (op.x >= 0) { d.ocrec[12 * (size_t)op.x + 9] = wk; d.ocrec[12 * (size_t)op.x + 10] = wt; }
+    if (op.y >= 0) { d.ocrec[12 * (size_t)op.y + 9] = wk; d.ocrec[12 * (size_t)op.y + 10] = wt; }
+  }
 }
 
 __global__ void k_shared_pack(const double* ew, const int* sh_edge, const int* sh_idx, int n, double* out) {
@@ -1223,6 +1301,11 @@ struct kmx_pgo {
   int* d_inc_ptr = nullptr;
   int2* d_inc = nullptr;
   double* d_irec = nullptr;
+  double* d_crec = nullptr;  // compact records (gather variant 3), null when not usable
+  double* d_ocrec = nullptr;
+  int* d_optr = nullptr;
+  int2* d_eopos = nullptr;
+  bool compact_ok = false;
   double *d_ekappa = nullptr, *d_etau = nullptr, *d_ew = nullptr;
   int2* d_eipos = nullptr;
   double* d_vec = nullptr;  // X Xt g r z eta del hd
@@ -1244,6 +1327,7 @@ struct kmx_pgo {
   // kernel variants (KMX_GATHER: 0 direct / 1 LDS-staged; KMX_FUSED: 0 separate
   // reduce launch / 1 last-arriving-tile reduction)
   int gvar = 2, fvar = 0;
+  int gvar_req = -1;  // KMX_GATHER override; default: 3 when compact records are valid, else 2
   HostStatus* hstat = nullptr;  // host-mapped progress word
   unsigned long long seq = 0;
   bool poll = true;             // KMX_POLL=0 enqueues every tCG step blindly
@@ -1267,13 +1351,13 @@ int dalloc(T** p, size_t count) {
 
 void free_dev(kmx_pgo* h) {
   void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_inc,
-                  h->d_irec, h->d_ekappa, h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_pub, h->d_part, h->d_ctl, h->d_cnt,
+                  h->d_irec, h->d_crec, h->d_ocrec, h->d_optr, h->d_eopos, h->d_ekappa, h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_pub, h->d_part, h->d_ctl, h->d_cnt,
                   h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src, h->d_gnc_edge, h->d_gnc_ends,
                   h->d_sh_edge, h->d_sh_idx, h->d_osh_edge, h->d_osh_idx, h->d_active, h->d_scratch, h->d_tickets};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
-  h->d_inc = nullptr; h->d_eipos = nullptr; h->d_irec = h->d_ekappa = h->d_etau = h->d_ew = nullptr; h->d_vec = h->d_S = h->d_Pinv = h->d_pub = h->d_part = nullptr;
+  h->d_inc = nullptr; h->d_eipos = nullptr; h->d_optr = nullptr; h->d_eopos = nullptr; h->d_irec = h->d_crec = h->d_ocrec = h->d_ekappa = h->d_etau = h->d_ew = nullptr; h->d_vec = h->d_S = h->d_Pinv = h->d_pub = h->d_part = nullptr;
   h->d_ctl = nullptr; h->d_cnt = nullptr; h->d_m_robot = nullptr; h->d_n_robot = nullptr;
   h->d_pub_src = h->d_own_src = h->d_gnc_edge = nullptr; h->d_gnc_ends = nullptr;
   h->d_sh_edge = h->d_sh_idx = nullptr; h->d_osh_edge = h->d_osh_idx = nullptr; h->d_active = nullptr; h->d_scratch = nullptr; h->d_tickets = nullptr;
@@ -1399,7 +1483,9 @@ void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
     case 2: enqueue_round_t<R, 1, 0>(h, d_active); break;
     case 3: enqueue_round_t<R, 1, 1>(h, d_active); break;
     case 4: enqueue_round_t<R, 2, 0>(h, d_active); break;
-    default: enqueue_round_t<R, 2, 1>(h, d_active); break;
+    case 5: enqueue_round_t<R, 2, 1>(h, d_active); break;
+    case 6: enqueue_round_t<R, 3, 0>(h, d_active); break;
+    default: enqueue_round_t<R, 3, 1>(h, d_active); break;
   }
 }
 
@@ -1441,7 +1527,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     return kmx::fail(KMX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
   h->own_stream = true;
-  if (const char* v = std::getenv("KMX_GATHER")) h->gvar = std::min(2, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("KMX_GATHER")) h->gvar_req = std::min(3, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("KMX_FUSED")) h->fvar = std::atoi(v) ? 1 : 0;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
   if (hipHostMalloc(reinterpret_cast<void**>(&h->hstat), sizeof(HostStatus),
@@ -1662,6 +1748,51 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   // device
   int rc;
   const size_t vec = (size_t)std::max(nloc, 1) * ps;
+  // Compact records: valid when every local rotation's third row equals row0 x
+  // row1 to 1e-12 (measurements in SO(3)); the gathers then rebuild row 2.
+  std::vector<double> crec, ocrec;
+  std::vector<int> optr;
+  std::vector<int2> eopos;
+  {
+    bool ok = true;
+    for (int k = 0; k < h->mloc && ok; ++k) {
+      const double* Q = R + 9 * ledges[k];
+      const double c0 = Q[1] * Q[5] - Q[2] * Q[4], c1 = Q[2] * Q[3] - Q[0] * Q[5], c2 = Q[0] * Q[4] - Q[1] * Q[3];
+      ok = std::fabs(c0 - Q[6]) <= 1e-12 && std::fabs(c1 - Q[7]) <= 1e-12 && std::fabs(c2 - Q[8]) <= 1e-12;
+    }
+    h->compact_ok = ok;
+    const bool want = (h->gvar_req < 0 || h->gvar_req == 3);
+    h->gvar = (ok && want) ? 3 : (h->gvar_req >= 0 && h->gvar_req < 3 ? h->gvar_req : 2);
+    if (h->gvar == 3) {
+      const size_t ni = (size_t)std::max(h->ninc, 1);
+      crec.assign(ni * 12, 0.0);
+      for (size_t k = 0; k < (size_t)h->ninc; ++k) {
+        const double* a = &irec[k * 16];
+        double* c = &crec[k * 12];
+        for (int q = 0; q < 6; ++q) c[q] = a[q];
+        c[6] = a[9]; c[7] = a[10]; c[8] = a[11];
+        c[9] = a[12]; c[10] = a[13];
+        const long long bits = (long long)(unsigned)inc[k].x | ((long long)inc[k].y << 32);
+        std::memcpy(&c[11], &bits, 8);
+      }
+      // owner incidences, in CSR order
+      optr.assign(nloc + 1, 0);
+      eopos.assign(std::max(h->mloc, 1), make_int2(-1, -1));
+      for (int p = 0; p < nloc; ++p) {
+        optr[p + 1] = optr[p];
+        for (int k = inc_ptr[p]; k < inc_ptr[p + 1]; ++k) {
+          const bool own = inc[k].x < 0 || (((unsigned)inc[k].y) >> 31);
+          if (!own) continue;
+          const int pos = optr[p + 1]++;
+          ocrec.insert(ocrec.end(), crec.begin() + 12 * (size_t)k, crec.begin() + 12 * (size_t)(k + 1));
+          int2& ep = eopos[inc[k].y & 0x7fffffff];
+          if (ep.x < 0) ep.x = pos;
+          else ep.y = pos;
+        }
+      }
+      if (ocrec.empty()) ocrec.assign(12, 0.0);
+    }
+  }
   if ((rc = dalloc(&h->d_tile_robot, h->ntiles)) || (rc = dalloc(&h->d_tile_p0, h->ntiles)) ||
       (rc = dalloc(&h->d_tile_np, h->ntiles)) || (rc = dalloc(&h->d_rtile0, L + 1)) ||
       (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_inc, inc.size())) ||
@@ -1693,6 +1824,17 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(up(h->d_inc_ptr, inc_ptr.data(), sizeof(int) * inc_ptr.size()));
   KMX_HIP(up(h->d_inc, inc.data(), sizeof(int2) * inc.size()));
   KMX_HIP(up(h->d_irec, irec.data(), sizeof(double) * irec.size()));
+  if (h->gvar == 3) {
+    if ((rc = dalloc(&h->d_crec, crec.size())) || (rc = dalloc(&h->d_ocrec, ocrec.size())) ||
+        (rc = dalloc(&h->d_optr, optr.size())) || (rc = dalloc(&h->d_eopos, eopos.size()))) {
+      free_dev(h);
+      return rc;
+    }
+    KMX_HIP(up(h->d_crec, crec.data(), sizeof(double) * crec.size()));
+    KMX_HIP(up(h->d_ocrec, ocrec.data(), sizeof(double) * ocrec.size()));
+    KMX_HIP(up(h->d_optr, optr.data(), sizeof(int) * optr.size()));
+    KMX_HIP(up(h->d_eopos, eopos.data(), sizeof(int2) * eopos.size()));
+  }
   KMX_HIP(up(h->d_ekappa, h->ek_h.data(), sizeof(double) * h->ek_h.size()));
   KMX_HIP(up(h->d_etau, h->et_h.data(), sizeof(double) * h->et_h.size()));
   KMX_HIP(up(h->d_ew, ew_h.data(), sizeof(double) * ew_h.size()));
@@ -1725,7 +1867,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   Dev& d = h->dv;
   d.ntiles = h->ntiles; d.L = L; d.nloc = nloc; d.npub = (int)h->npub;
   d.tile_robot = h->d_tile_robot; d.tile_p0 = h->d_tile_p0; d.tile_np = h->d_tile_np; d.rtile0 = h->d_rtile0;
-  d.inc_ptr = h->d_inc_ptr; d.inc = h->d_inc; d.irec = h->d_irec;
+  d.inc_ptr = h->d_inc_ptr; d.inc = h->d_inc; d.irec = h->d_irec; d.crec = h->d_crec;
+  d.ocrec = h->d_ocrec; d.optr = h->d_optr; d.eopos = h->d_eopos;
   d.ekappa = h->d_ekappa; d.etau = h->d_etau; d.ew = h->d_ew; d.eipos = h->d_eipos;
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
   d.z = h->d_vec + 4 * vec; d.eta = h->d_vec + 5 * vec; d.del = h->d_vec + 6 * vec; d.hd = h->d_vec + 7 * vec;
@@ -2015,6 +2158,9 @@ extern "C" int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, do
   } else if (h->gvar == 2) {
     KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 2>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
                                           h->dv, l, mode, (const double*)dV, dO));
+  } else if (h->gvar == 3) {
+    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 3>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
+                                          h->dv, l, mode, (const double*)dV, dO));
   } else {
     KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 0>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
                                           h->dv, l, mode, (const double*)dV, dO));
@@ -2092,6 +2238,7 @@ extern "C" int kmx_pgo_debug_gather_bench(kmx_pgo* h, int variant, int reps, dou
       KMX_GB(0, 0, 1) KMX_GB(1, 0, 4) KMX_GB(2, 0, 6) KMX_GB(3, 0, 8)
       KMX_GB(10, 1, 1) KMX_GB(11, 1, 4) KMX_GB(12, 1, 6)
       KMX_GB(20, 2, 1) KMX_GB(21, 2, 4) KMX_GB(22, 2, 6) KMX_GB(23, 2, 8)
+      KMX_GB(40, 3, 1) KMX_GB(41, 3, 4) KMX_GB(42, 3, 6) KMX_GB(45, 4, 1)
 #undef KMX_GB
 #define KMX_GA(V, A) case V: hipLaunchKernelGGL((k_gablate<5, A>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
       KMX_GA(30, 0) KMX_GA(31, 1) KMX_GA(32, 2) KMX_GA(33, 3)
@@ -2099,6 +2246,7 @@ extern "C" int kmx_pgo_debug_gather_bench(kmx_pgo* h, int variant, int reps, dou
       default: return false;
     }
   };
+  KMX_CHECK(variant < 40 || h->d_crec, KMX_EINVAL, "compact records not built (KMX_GATHER / non-SO(3) input)");
   if (!launch()) return kmx::fail(KMX_EINVAL, "unknown gather variant");
   KMX_HIP(hipEventRecord(e0, h->stream));
   for (int i = 0; i < reps; ++i) launch();

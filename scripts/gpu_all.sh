@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-run}
 mkdir -p gpurun_out/$TAG
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/$TAG/pytest_gpu.log 2>&1
+timeout -k 10 600 python -m pytest tests -x -q -m gpu --timeout 300 > gpurun_out/$TAG/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/$TAG/pytest_gpu.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 python bench.py --steps 40 --warmup 5 ${BENCH_ARGS} > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err

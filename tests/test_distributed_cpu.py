@@ -57,18 +57,22 @@ def test_two_rank_gloo_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q), daemon=True) for r in range(2)]
     for p in procs:
         p.start()
     got = {}
     wu = []
-    for _ in procs:
-        rank, X, w = q.get(timeout=240)
-        got.update(X)
-        wu.append(w)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    try:
+        for _ in procs:
+            rank, X, w = q.get(timeout=240)
+            got.update(X)
+            wu.append(w)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
     # single-process reference: same rounds, same GNC schedule
     g, P = _graph(), _params()
     o = OraclePGO(P.to_c(), g)

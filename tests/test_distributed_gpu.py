@@ -73,19 +73,23 @@ def test_two_ranks_one_gpu_match_single_process(gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q), daemon=True) for r in range(2)]
     for p in procs:
         p.start()
-    got = {}
+    results = []
     try:
-        for _ in procs:
-            rank, X, w, robots = q.get(timeout=420)
-            got.update(X)
-            sel = np.isin(g.r1, robots) | np.isin(g.r2, robots)  # edges this rank's blocks see
-            assert np.array_equal(w[sel], w1[sel]), rank
+        for _ in procs:  # drain the queue before asserting, so workers can exit
+            results.append(q.get(timeout=420))
     finally:
         for p in procs:
             p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
     assert all(p.exitcode == 0 for p in procs)
+    got = {}
+    for rank, X, w, robots in results:
+        got.update(X)
+        sel = np.isin(g.r1, robots) | np.isin(g.r2, robots)  # edges this rank's blocks see
+        assert np.array_equal(w[sel], w1[sel]), rank
     for a in range(g.n_robots):
         assert np.array_equal(got[a], X1[a]), a

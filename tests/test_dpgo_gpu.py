@@ -68,8 +68,12 @@ def test_primitives_match_oracle(gpu, r):
             assert abs(gs - os_) <= 1e-10 * max(1.0, abs(os_)), (mode, gs, os_)
 
 
-@pytest.mark.parametrize("robust", [False, True])
-def test_rounds_match_oracle(gpu, robust):
+@pytest.mark.parametrize("robust,gather", [(False, None), (True, None), (True, "2")])
+def test_rounds_match_oracle(gpu, robust, gather, monkeypatch):
+    """gather None = default (compact 96-B records on SO(3) input); "2" forces
+    the full 128-B record gather."""
+    if gather is not None:
+        monkeypatch.setenv("KMX_GATHER", gather)
     g, P, X0 = _setup(robust=robust)
     s, o = _pair(g, P, X0)
     for it in range(12):
@@ -167,3 +171,19 @@ def test_noise_free_converges_to_ground_truth(gpu):
         tg = (g.gt_t[a] - t0) @ R0
         assert np.abs(T[:, 9:] - tg).max() < 1e-4
         assert np.abs(T[:, :9].reshape(-1, 3, 3) - Rg).max() < 1e-4
+
+
+def test_non_rotation_measurement_uses_full_records(gpu):
+    """A measurement whose rotation is not in SO(3) to 1e-12 must not go
+    through the compact records (which rebuild row 2 = row0 x row1)."""
+    g, P, X0 = _setup()
+    g.R[5] = g.R[5] + 1e-6 * np.random.default_rng(1).standard_normal((3, 3))
+    s, o = _pair(g, P, X0)
+    rng = np.random.default_rng(2)
+    for a in range(g.n_robots):
+        V = rng.standard_normal(X0[a].shape)
+        for mode in (abi.KMX_EVAL_COST_EGRAD, abi.KMX_EVAL_EHESS):
+            Vin = X0[a] if mode == abi.KMX_EVAL_COST_EGRAD else V
+            gout, _ = s.eval(a, mode, Vin)
+            oout, _ = o.eval(a, mode, Vin)
+            assert np.abs(gout - oout).max() <= 1e-12 * max(1.0, np.abs(oout).max()), mode
