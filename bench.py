@@ -132,6 +132,50 @@ def lcd_leg(args, rank, world, barrier_sync):
     return out, cpu
 
 
+def bow_leg(args, rank, world, barrier_sync):
+    """BoW candidate stage (configs[2] "BoW query", timed separately): robot 1's
+    keyframes query robot 0's database (detectLoopWithRobot: DBoW2 queryL1,
+    max_db_results 50) on a synthetic 100k-word vocabulary. Queries are
+    sharded across ranks (independent; no collective)."""
+    from kmx.lcd.bow import BowDatabase
+    from kmx.synth.bow import make_bow_stream
+    n = args.lcd_frames // 2
+    st = make_bow_stream(2, n, n_words=100_000, seed=0)
+    db = st.subset(np.nonzero(st.robot == 0)[0])
+    qi = np.nonzero(st.robot == 1)[0][rank::world]
+    qs = st.subset(qi)
+    G = BowDatabase(st.n_words, device=int(os.environ.get("LOCAL_RANK", "0")))
+    G.set_entries(db.vptr, db.words, db.weights)
+    G.query_async(qs.vptr, qs.words, qs.weights, 50)  # warmup
+    G.sync()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.lcd_steps):
+        G.query_async(qs.vptr, qs.words, qs.weights, 50)
+    G.sync()
+    barrier_sync()
+    el = time.perf_counter() - t0
+    postings = float(np.bincount(db.words, minlength=st.n_words)[qs.words].sum())
+    out = {"metric": "BoW queries/sec", "n_local": int(qs.n), "steps": args.lcd_steps, "elapsed": el,
+           "postings_per_query": postings / max(qs.n, 1),
+           "workload": f"{qs.n} queries (robot 1) x {db.n}-entry database (robot 0), {st.n_words} words, "
+                       f"~{st.words.shape[0] // st.n} words per BowVector, queryL1 top-50"}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, str(ROOT))
+        from oracle import oracle as O
+        D = O.OracleBowDb(st.n_words, db.vptr, db.words, db.weights)
+        k, t0c, done = 0, time.perf_counter(), 0.0
+        while done < args.cpu_seconds * 0.25 and k < qs.n:
+            sub = qs.subset(np.arange(k, min(k + 256, qs.n)))
+            D.query(sub.vptr, sub.words, sub.weights, 50)
+            k += sub.n
+            done = time.perf_counter() - t0c
+        cpu = {"value": k / done, "unit": "queries/s", "cores": 1, "kind": "port",
+               "sample": f"first {k} queries, oracle/bow_oracle.c (DBoW2 queryL1 restated), 1 thread, {done:.1f} s"}
+    return out, cpu
+
+
 def load_traffic():
     f = ROOT / "profiles" / "hessvec_traffic.json"
     if f.exists():
@@ -245,6 +289,21 @@ def main():
         del lcd["elapsed"]
         if lcd_cpu:
             lcd["cpu_baseline"] = lcd_cpu
+        bow, bow_cpu = bow_leg(args, rank, world, barrier_sync)
+        n_local, bel = float(bow["n_local"] * bow["steps"]), bow["elapsed"]
+        if dist is not None:
+            t = torch.tensor([n_local, bel], dtype=torch.float64, device="cuda")
+            parts = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+            parts = torch.stack(parts).cpu().numpy()
+            n_local, bel = float(parts[:, 0].sum()), float(parts[:, 1].max())
+        bow["value"] = n_local / bel
+        bow["unit"] = "queries/s"
+        bow["ms_per_step"] = 1e3 * bel / bow["steps"]
+        del bow["elapsed"]
+        if bow_cpu:
+            bow["cpu_baseline"] = bow_cpu
+        lcd["bow"] = bow
         out["lcd"] = lcd
     if rank == 0:
         print(json.dumps(out), flush=True)

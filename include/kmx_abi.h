@@ -307,6 +307,42 @@ int kmx_lcd_verify_async(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
                          const int32_t* cand_match);
 int kmx_lcd_sync(kmx_lcd* h);
 
+
+/* ------------------------------------------------------------------------- */
+/* Kimera-Multi-LCD BoW candidate stage: DBoW2 inverted-file L1 query         */
+/* ------------------------------------------------------------------------- */
+/* Replaces DBoW2 Database::queryL1 and L1Scoring::score as used by
+ * LoopClosureDetector::detectLoop / detectLoopWithRobot (drawio:2574-2580,
+ * 2612-2633; LcdParams.yaml:3-12). BowVectors are CSR: vptr[n+1] (int64),
+ * words (uint32, strictly increasing per vector) and weights (L1-normalised
+ * double). Entry id = position in the database. */
+typedef struct kmx_bow kmx_bow;
+int kmx_bow_create(int device, kmx_bow** out);
+int kmx_bow_destroy(kmx_bow* h);
+int kmx_bow_set_stream(kmx_bow* h, void* hip_stream);
+/* Build the inverted file of entries 0..n_entries-1 (Database::add in order). */
+int kmx_bow_set_database(kmx_bow* h, int32_t n_words, int32_t n_entries,
+                         const int64_t* vptr, const uint32_t* words,
+                         const double* weights);
+/* queryL1 for nq query vectors: results with entry id < max_id[q] (NULL or
+ * -1: all), sorted by score descending (ties: lower entry id first), at most
+ * max_results (<= 256) each. out_n[nq]; out_ids / out_scores [nq][max_results];
+ * score = 1 - 1/2 |v - w|_1. */
+int kmx_bow_query(kmx_bow* h, int32_t nq, const int64_t* qptr,
+                  const uint32_t* words, const double* weights,
+                  const int32_t* max_id, int32_t max_results, int32_t* out_n,
+                  int32_t* out_ids, double* out_scores);
+/* Enqueue only (benchmark path); kmx_bow_sync waits. */
+int kmx_bow_query_async(kmx_bow* h, int32_t nq, const int64_t* qptr,
+                        const uint32_t* words, const double* weights,
+                        const int32_t* max_id, int32_t max_results);
+int kmx_bow_sync(kmx_bow* h);
+/* L1Scoring::score of n pairs (a_i, b_i) (the nss factor). */
+int kmx_bow_score_pairs(kmx_bow* h, int32_t n, const int64_t* aptr,
+                        const uint32_t* aw, const double* av,
+                        const int64_t* bptr, const uint32_t* bw,
+                        const double* bv, double* out);
+
 #ifdef __cplusplus
 }
 #endif

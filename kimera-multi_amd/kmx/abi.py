@@ -144,6 +144,25 @@ def lib() -> C.CDLL:
         "kmx_pgo_enable_timing": ([P, C.c_int], C.c_int),
         "kmx_pgo_read_counters": ([P, C.POINTER(PgoCounters)], C.c_int),
     }
+    pu32 = C.POINTER(C.c_uint32)
+    sig.update({
+        "kmx_lcd_knn2": ([C.c_int, C.c_double, pu8, i32, pu8, i32, pi32, pi32], C.c_int),
+        "kmx_lcd_create": ([C.POINTER(LcdParams), C.c_int, C.POINTER(P)], C.c_int),
+        "kmx_lcd_destroy": ([P], C.c_int),
+        "kmx_lcd_set_stream": ([P, P], C.c_int),
+        "kmx_lcd_set_frames": ([P, P], C.c_int),
+        "kmx_lcd_verify": ([P, i32, pi32, pi32, C.POINTER(LcdResult), pu8], C.c_int),
+        "kmx_lcd_verify_async": ([P, i32, pi32, pi32], C.c_int),
+        "kmx_lcd_sync": ([P], C.c_int),
+        "kmx_bow_create": ([C.c_int, C.POINTER(P)], C.c_int),
+        "kmx_bow_destroy": ([P], C.c_int),
+        "kmx_bow_set_stream": ([P, P], C.c_int),
+        "kmx_bow_set_database": ([P, i32, i32, pi64, pu32, pf64], C.c_int),
+        "kmx_bow_query": ([P, i32, pi64, pu32, pf64, pi32, i32, pi32, pi32, pf64], C.c_int),
+        "kmx_bow_query_async": ([P, i32, pi64, pu32, pf64, pi32, i32], C.c_int),
+        "kmx_bow_sync": ([P], C.c_int),
+        "kmx_bow_score_pairs": ([P, i32, pi64, pu32, pf64, pi64, pu32, pf64, pf64], C.c_int),
+    })
     optional = {
         "kmx_lcd_knn2": ([C.c_int, C.c_double, pu8, i32, pu8, i32, pi32, pi32], C.c_int),
         "kmx_lcd_create": ([C.POINTER(LcdParams), C.c_int, C.POINTER(P)], C.c_int),
@@ -187,6 +206,16 @@ def fptr(a: np.ndarray):
 def iptr(a: np.ndarray):
     assert a.dtype == np.int32 and a.flags.c_contiguous
     return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def i64ptr(a: np.ndarray):
+    assert a.dtype == np.int64 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_int64))
+
+
+def u32ptr(a: np.ndarray):
+    assert a.dtype == np.uint32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
 
 
 def u8ptr(a: np.ndarray):

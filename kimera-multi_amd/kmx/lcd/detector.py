@@ -34,6 +34,17 @@ class LcdParams:
     ransac_seed: int = 12345
     rng_variant: str = "gcc9"           # libstdc++ of ROS Noetic (SURVEY.md §0 finding 5)
     ransac_use_1point_3d3d: int = 1
+    # BoW detection (LcdParams.yaml:3-12)
+    use_nss: int = 1
+    alpha: float = 0.4
+    min_temporal_matches: int = 1
+    recent_frames_window: int = 100
+    max_db_results: int = 50
+    min_nss_factor: float = 0.05
+    min_matches_per_island: int = 1
+    max_intraisland_gap: int = 3
+    max_nrFrames_between_islands: int = 3
+    max_nrFrames_between_queries: int = 2
 
     @classmethod
     def from_yaml(cls, path: str, **overrides) -> "LcdParams":
@@ -44,7 +55,9 @@ class LcdParams:
         p = cls()
         for k in ("lowe_ratio", "min_nr_2d2d_inliers", "min_nr_3d3d_inliers", "ransac_threshold_2d2d",
                   "ransac_threshold_3d3d", "ransac_max_iterations", "ransac_probability", "ransac_randomize",
-                  "ransac_use_1point_3d3d"):
+                  "ransac_use_1point_3d3d", "use_nss", "alpha", "min_temporal_matches", "recent_frames_window",
+                  "max_db_results", "min_nss_factor", "min_matches_per_island", "max_intraisland_gap",
+                  "max_nrFrames_between_islands", "max_nrFrames_between_queries"):
             if k in y:
                 setattr(p, k, type(getattr(p, k))(y[k]))
         if "matcher_type" in y:  # OpenCV MatcherType: 3 = BRUTEFORCE_L1, 4 = BRUTEFORCE_HAMMING

@@ -68,6 +68,26 @@ def _setup(L):
         fn.argtypes = a
         fn.restype = r
     _lcd_setup(L)
+    _bow_setup(L)
+
+
+def _bow_setup(L):
+    P, i32, i64, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    pi32, pi64, pf64, pu32 = C.POINTER(i32), C.POINTER(i64), C.POINTER(f64), C.POINTER(C.c_uint32)
+    sigs = {
+        "orc_bow_score": ([pu32, pf64, C.c_int, pu32, pf64, C.c_int], f64),
+        "orc_bowdb_create": ([C.c_int, C.c_int, pi64, pu32, pf64], P),
+        "orc_bowdb_destroy": ([P], None),
+        "orc_bowdb_query": ([P, pu32, pf64, C.c_int, C.c_int, C.c_int, pi32, pf64], C.c_int),
+        "orc_bow_islands": ([C.c_int, pi32, pf64, C.c_int, C.c_int, C.c_void_p], C.c_int),
+        "orc_bow_temporal": ([pi32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int], C.c_int),
+        "orc_bow_detect_batch": ([P, C.c_int, pi64, pu32, pf64, pi64, pu32, pf64, C.c_int, f64, f64, pi32, pf64,
+                                  pf64], None),
+    }
+    for name, (a, r) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = a
+        fn.restype = r
 
 
 def _f(a):
@@ -279,3 +299,122 @@ def lcd_verify(params, pool, cand_query=None, cand_match=None, masks=True):
     L.orc_lcd_verify_batch(C.byref(params), C.byref(d), cq.shape[0], _i(cq), _i(cm), res,
                            _u(mk) if masks else None)
     return res, mk
+
+
+# ------------------------------------------------------------------ BoW ----
+def _u32(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+def _i64(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int64))
+
+
+def bow_score(w1, v1, w2, v2):
+    """DBoW2 L1Scoring::score (restated in oracle/bow_oracle.c)."""
+    L = lib()
+    w1, w2 = np.ascontiguousarray(w1, np.uint32), np.ascontiguousarray(w2, np.uint32)
+    v1, v2 = np.ascontiguousarray(v1, np.float64), np.ascontiguousarray(v2, np.float64)
+    return L.orc_bow_score(_u32(w1), _f(v1), w1.shape[0], _u32(w2), _f(v2), w2.shape[0])
+
+
+class OracleBowDb:
+    """DBoW2 Database (L1) restatement: inverted file + queryL1."""
+
+    def __init__(self, n_words, vptr, words, weights):
+        self.L = lib()
+        self.vptr = np.ascontiguousarray(vptr, np.int64)
+        self.words = np.ascontiguousarray(words, np.uint32)
+        self.weights = np.ascontiguousarray(weights, np.float64)
+        self.n = self.vptr.shape[0] - 1
+        self.h = self.L.orc_bowdb_create(int(n_words), self.n, _i64(self.vptr), _u32(self.words), _f(self.weights))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.orc_bowdb_destroy(self.h)
+            self.h = None
+
+    def query(self, qptr, words, weights, max_results=50, max_id=None):
+        qptr = np.ascontiguousarray(qptr, np.int64)
+        words = np.ascontiguousarray(words, np.uint32)
+        weights = np.ascontiguousarray(weights, np.float64)
+        nq = qptr.shape[0] - 1
+        n = np.zeros(nq, np.int32)
+        ids = np.full((nq, max_results), -1, np.int32)
+        sc = np.zeros((nq, max_results))
+        for q in range(nq):
+            mid = -1 if max_id is None else int(max_id[q])
+            a, b = qptr[q], qptr[q + 1]
+            n[q] = self.L.orc_bowdb_query(self.h, _u32(words[a:]), _f(weights[a:]), int(b - a), max_results, mid,
+                                          _i(ids[q]), _f(sc[q]))
+        return n, ids, sc
+
+    def detect_batch(self, qptr, qw, qv, pptr, pw, pv, max_results=50, alpha=0.4, min_nss=0.05):
+        """detectLoopWithRobot over a batch (previous-keyframe vectors in p*)."""
+        qptr, pptr = np.ascontiguousarray(qptr, np.int64), np.ascontiguousarray(pptr, np.int64)
+        qw, pw = np.ascontiguousarray(qw, np.uint32), np.ascontiguousarray(pw, np.uint32)
+        qv, pv = np.ascontiguousarray(qv, np.float64), np.ascontiguousarray(pv, np.float64)
+        nq = qptr.shape[0] - 1
+        match = np.zeros(nq, np.int32)
+        score = np.zeros(nq)
+        nss = np.zeros(nq)
+        self.L.orc_bow_detect_batch(self.h, nq, _i64(qptr), _u32(qw), _f(qv), _i64(pptr), _u32(pw), _f(pv),
+                                    max_results, alpha, min_nss, _i(match), _f(score), _f(nss))
+        return match, score, nss
+
+
+class _Island(C.Structure):
+    _fields_ = [("start", C.c_int), ("end", C.c_int), ("best_id", C.c_int), ("score", C.c_double),
+                ("best_score", C.c_double)]
+
+
+def detect_loop_stream(db: "OracleBowDb", vptr, words, weights, first_frame, p):
+    """Single-robot detectLoop over consecutive keyframes (restated control:
+    max_id = frame - recent_frames_window, nss vs the previous keyframe,
+    alpha cut, islands, temporal constraint). p: kmx.lcd.LcdParams."""
+    L = lib()
+    vptr = np.ascontiguousarray(vptr, np.int64)
+    words = np.ascontiguousarray(words, np.uint32)
+    weights = np.ascontiguousarray(weights, np.float64)
+    nq = vptr.shape[0] - 1
+    fids = np.arange(first_frame, first_frame + nq)
+    max_id = np.maximum(fids - p.recent_frames_window, 0)
+    n, ids, sc = db.query(vptr, words, weights, p.max_db_results, max_id)
+    state = np.zeros(4, np.int32)
+    isl = (_Island * max(p.max_db_results, 1))()
+    out = []
+    for q in range(nq):
+        fid = int(fids[q])
+        if n[q] == 0:
+            out.append((fid, "NO_MATCHES", -1, 0.0))
+            continue
+        nss = 1.0
+        if p.use_nss:
+            if q == 0:
+                out.append((fid, "LOW_NSS_FACTOR", -1, 0.0))
+                continue
+            a, b = slice(vptr[q], vptr[q + 1]), slice(vptr[q - 1], vptr[q])
+            nss = bow_score(words[a], weights[a], words[b], weights[b])
+            if nss < p.min_nss_factor:
+                out.append((fid, "LOW_NSS_FACTOR", -1, 0.0))
+                continue
+        k = 0
+        while k < n[q] and sc[q, k] >= p.alpha * nss:
+            k += 1
+        if k == 0:
+            out.append((fid, "LOW_SCORE", -1, 0.0))
+            continue
+        qi = np.ascontiguousarray(ids[q, :k])
+        qs = np.ascontiguousarray(sc[q, :k])
+        ni = L.orc_bow_islands(k, _i(qi), _f(qs), p.max_intraisland_gap, p.min_matches_per_island, C.byref(isl))
+        if ni == 0:
+            out.append((fid, "NO_GROUPS", -1, 0.0))
+            continue
+        best = max(range(ni), key=lambda j: isl[j].score)  # first maximum, like std::max_element
+        b = isl[best]
+        if not L.orc_bow_temporal(_i(state), fid, b.start, b.end, p.max_nrFrames_between_queries,
+                                  p.max_nrFrames_between_islands, p.min_temporal_matches):
+            out.append((fid, "FAILED_TEMPORAL_CONSTRAINT", b.best_id, b.best_score))
+            continue
+        out.append((fid, "LOOP_DETECTED", b.best_id, b.best_score))
+    return out
