@@ -68,6 +68,19 @@ struct Counters {
   double pad2[3];
 };
 
+// Host-visible progress of one robot after a tCG step, written by the robot's
+// k_reduce(RED_UPDATE) workgroup into host-mapped memory as ONE 64-bit word
+// (seq << 1 | still-in-tCG): a single relaxed system-scope store needs no
+// release fence, so no L2 writeback is forced. The host enqueues further tCG
+// steps only while a robot is in tCG.
+struct HostStatus {
+  unsigned long long word;
+};
+__device__ __forceinline__ void post_status(HostStatus* hs, int l, unsigned long long seq, bool running) {
+  __hip_atomic_store(&hs[l].word, (seq << 1) | (running ? 1ull : 0ull), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct Params {
   int tcg_max, rtr_iters, use_precond, robust;
   double kappa, theta, Delta0, Delta_max, accept_rho, gn_tol, shift, barc;
@@ -723,7 +736,8 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
 }
 
 // Separate-launch reduction (variant F = 0): one workgroup per robot.
-__global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_) {
+__global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_, HostStatus* hs,
+                                                 unsigned long long seq) {
   __shared__ double lds[WAVES];
   const int l = blockIdx.x;
   const int ph = d.ctl[l].phase;
@@ -731,7 +745,10 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_) {
   if (kind == RED_GRAD) act = ph == PH_START;
   if (kind == RED_HESS || kind == RED_UPDATE) act = ph == PH_TCG;
   if (kind == RED_COST) act = ph == PH_STEP;
-  if (!act) return;
+  if (!act) {
+    if (hs && threadIdx.x == 0) post_status(hs, l, seq, false);  // not in tCG after this step
+    return;
+  }
   const int ns = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
   double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
   const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
@@ -743,7 +760,10 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_) {
       tot[s] = block_sum(v, lds);
     }
   }
-  if (threadIdx.x == 0) control(d, l, kind, tot, R_);
+  if (threadIdx.x == 0) {
+    control(d, l, kind, tot, R_);
+    if (hs) post_status(hs, l, seq, d.ctl[l].phase == PH_TCG);
+  }
 }
 
 #define KMX_SMEM extern __shared__ __attribute__((aligned(16))) char smem[]
@@ -952,21 +972,6 @@ __global__ void k_round_begin(Dev d, const unsigned char* active) {
   c.phase = a ? PH_START : PH_IDLE;
   c.updated = a ? 1 : 0;
   c.Delta = d.p.Delta0;
-}
-
-// Host-visible progress word after a tCG step: number of robots still in
-// tCG, tagged with a sequence number (system-scope stores into host-mapped
-// memory). The host enqueues further tCG steps only while robots remain.
-struct HostStatus {
-  unsigned long long seq;
-  unsigned long long running;
-};
-__global__ void k_status(Dev d, HostStatus* hs, unsigned long long seq) {
-  if (threadIdx.x != 0) return;
-  unsigned long long n = 0;
-  for (int l = 0; l < d.L; ++l) n += (d.ctl[l].phase == PH_TCG) ? 1ull : 0ull;
-  __hip_atomic_store(&hs->running, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&hs->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_publish(const double* X, double* pub, const int* src, int nslots, int ps) {
@@ -1328,7 +1333,8 @@ struct kmx_pgo {
   // reduce launch / 1 last-arriving-tile reduction)
   int gvar = 2, fvar = 0;
   int gvar_req = -1;  // KMX_GATHER override; default: 3 when compact records are valid, else 2
-  HostStatus* hstat = nullptr;  // host-mapped progress word
+  HostStatus* hstat = nullptr;  // [L] host-mapped tCG progress per local robot
+  int hstat_cap = 0;
   unsigned long long seq = 0;
   bool poll = true;             // KMX_POLL=0 enqueues every tCG step blindly
   bool poll_timeout = false;
@@ -1414,8 +1420,8 @@ template <int R, int G, int F>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   const dim3 grid(h->ntiles), blk(BLOCK);
   const size_t sm = Smem<R>::bytes;
-  auto red = [&](int kind) {
-    if (!F) hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(BLOCK), 0, h->stream, h->dv, kind, R);
+  auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0) {
+    if (!F) hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(BLOCK), 0, h->stream, h->dv, kind, R, hs, seq);
   };
   auto tcg_step = [&]() {
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1428,10 +1434,11 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
     if (h->timing) (void)hipEventRecord(e1, h->stream);
     red(RED_HESS);
     hipLaunchKernelGGL((k_update<R, G, F>), grid, blk, sm, h->stream, h->dv);
-    red(RED_UPDATE);
-    if (h->poll) {
+    if (h->poll && !F) {  // the per-robot reduction also reports tCG progress
       h->seq += 1;
-      hipLaunchKernelGGL(k_status, dim3(1), dim3(64), 0, h->stream, h->dv, h->hstat, h->seq);
+      red(RED_UPDATE, h->hstat, h->seq);
+    } else {
+      red(RED_UPDATE);
     }
     return h->seq;
   };
@@ -1439,14 +1446,19 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
     volatile HostStatus* hs = h->hstat;
     (void)hipStreamQuery(h->stream);  // make sure queued work is submitted
     const auto t0 = std::chrono::steady_clock::now();
-    while (__atomic_load_n(&hs->seq, __ATOMIC_ACQUIRE) < seq) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
-        h->poll_timeout = true;  // device stalled: stop polling, enqueue blindly
-        h->poll = false;
-        return 1ull;
+    unsigned long long running = 0;
+    for (int l = 0; l < h->dv.L; ++l) {
+      unsigned long long w;
+      while (((w = __atomic_load_n(&hs[l].word, __ATOMIC_ACQUIRE)) >> 1) < seq) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+          h->poll_timeout = true;  // device stalled: stop polling, enqueue blindly
+          h->poll = false;
+          return 1ull;
+        }
       }
+      running |= w & 1ull;
     }
-    return hs->running;
+    return running;
   };
   hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(std::max(64, ((h->dv.L + 63) / 64) * 64)), 0, h->stream,
                      h->dv, d_active);
@@ -1454,7 +1466,7 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
     hipLaunchKernelGGL((k_grad<R, G, F>), grid, blk, sm, h->stream, h->dv);
     red(RED_GRAD);
     const int J = h->P.tcg_max_iterations;
-    if (!h->poll) {
+    if (!h->poll || F) {  // the fused variant has no per-robot reduce launch to report progress
       for (int j = 0; j < J; ++j) tcg_step();
     } else {
       // Keep exactly one tCG step queued beyond the last one known to be
@@ -1530,14 +1542,6 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   if (const char* v = std::getenv("KMX_GATHER")) h->gvar_req = std::min(3, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("KMX_FUSED")) h->fvar = std::atoi(v) ? 1 : 0;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
-  if (hipHostMalloc(reinterpret_cast<void**>(&h->hstat), sizeof(HostStatus),
-                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-    (void)hipStreamDestroy(h->stream);
-    delete h;
-    return kmx::fail(KMX_ENOMEM, "hipHostMalloc(status) failed");
-  }
-  h->hstat->seq = 0;
-  h->hstat->running = 0;
   *out = h;
   return KMX_OK;
   KMX_GUARD_END
@@ -1842,6 +1846,16 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(hipMemsetAsync(h->d_vec, 0, sizeof(double) * vec * 8, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_pub, 0, sizeof(double) * std::max<int64_t>(h->npub, 1) * ps, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_ctl, 0, sizeof(Ctl) * L, h->stream));
+  if (L > h->hstat_cap) {  // host-mapped per-robot tCG progress
+    if (h->hstat) (void)hipHostFree(h->hstat);
+    h->hstat = nullptr;
+    h->hstat_cap = 0;
+    KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->hstat), sizeof(HostStatus) * L,
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    h->hstat_cap = L;
+  }
+  for (int l = 0; l < L; ++l) h->hstat[l].word = 0;
+  h->seq = 0;
   KMX_HIP(hipMemsetAsync(h->d_cnt, 0, sizeof(Counters), h->stream));
   KMX_HIP(hipMemsetAsync(h->d_tickets, 0, sizeof(unsigned) * L, h->stream));
   KMX_HIP(up(h->d_m_robot, h->m_robot.data(), sizeof(long long) * L));

@@ -15,3 +15,5 @@ rc=$?; echo "bench rc=$rc"; cat gpurun_out/$TAG/bench.json; tail -3 gpurun_out/$
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG/prof -o run --output-format csv -- python3 bench.py --steps 40 --warmup 5 --profile > gpurun_out/$TAG/prof.log 2>&1
 echo "prof rc=$?"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG/prof_noev -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-lcd --no-events > gpurun_out/$TAG/prof_noev.log 2>&1
+echo "prof_noev rc=$?"
