@@ -254,7 +254,12 @@ typedef struct kmx_lcd_params {
   uint32_t ransac_seed;       /* 12345                                         */
   int rng_variant;            /* KMX_RNG_*                                     */
   int use_1point_3d3d;        /* 1: translation-only 3D-3D given the 2D-2D R   */
-  int reserved[8];
+  int pose_recovery_type;     /* 0: 3D-3D (reference config), 1: PnP            */
+  int min_2d3d_inliers;       /* 20 (LcdParams.yaml:53)                        */
+  double ransac_threshold_2d3d; /* PnP inlier threshold in (1 - cos) units: from
+                                 a pixel threshold px and focal length f,
+                                 1 - cos(atan(px / f)) (LcdParams.yaml:57)     */
+  int reserved[4];
 } kmx_lcd_params;
 
 /* computeMatchedIndices (drawio:2583-2586): k=2 brute-force match of every
@@ -282,9 +287,10 @@ typedef struct kmx_lcd_result {
   int32_t n_matches;      /* after kNN + Lowe                                 */
   int32_t mono_inliers;   /* 2D-2D RANSAC inliers                             */
   int32_t stereo_inliers; /* 3D-3D inliers                                    */
-  int32_t accepted;       /* mono >= min_2d2d && stereo >= min_3d3d           */
+  int32_t accepted;       /* mono >= min_2d2d && (stereo >= min_3d3d, or
+                             pnp >= min_2d3d with pose_recovery_type 1)     */
   int32_t iterations_2d2d;
-  int32_t pad;
+  int32_t pnp_inliers;    /* 2D-3D inliers (pose_recovery_type 1)              */
   double T_query_match[12]; /* R row-major, t                                 */
 } kmx_lcd_result;
 

@@ -507,9 +507,300 @@ __device__ int model_from_sample(const double* F1, const double* F2, const int* 
 }
 
 // ---------------------------------------------------------- RANSAC kernel --
+// ------------------------------------------------------------- EPnP ------
+// Port of oracle/lcd_oracle.c orc_epnp for the RANSAC minimal sample (n = 6):
+// same operations in the same order, so models are bit-identical.
+constexpr int PNP_S = 6;
+
+__device__ void jacobi_sym12(double* A, double* V) {
+  constexpr int n = 12;
+  for (int i = 0; i < n * n; ++i) V[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) off += A[p * n + q] * A[p * n + q];
+    if (off == 0.0) break;
+    for (int p = 0; p < n - 1; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        const double apq = A[p * n + q];
+        if (apq == 0.0) continue;
+        const double app = A[p * n + p], aqq = A[q * n + q];
+        const double theta = (aqq - app) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
+        for (int k = 0; k < n; ++k) {
+          const double akp = A[k * n + p], akq = A[k * n + q];
+          A[k * n + p] = cs * akp - sn * akq;
+          A[k * n + q] = sn * akp + cs * akq;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double apk = A[p * n + k], aqk = A[q * n + k];
+          A[p * n + k] = cs * apk - sn * aqk;
+          A[q * n + k] = sn * apk + cs * aqk;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double vkp = V[k * n + p], vkq = V[k * n + q];
+          V[k * n + p] = cs * vkp - sn * vkq;
+          V[k * n + q] = sn * vkp + cs * vkq;
+        }
+      }
+  }
+}
+
+__device__ int qr_lsq(int m, int n, double* A, double* b, double* x) {
+  for (int k = 0; k < n; ++k) {
+    double nrm = 0.0;
+    for (int i = k; i < m; ++i) nrm += A[i * n + k] * A[i * n + k];
+    nrm = sqrt(nrm);
+    if (nrm == 0.0) return 0;
+    const double alpha = (A[k * n + k] > 0.0) ? -nrm : nrm;
+    double vk = A[k * n + k] - alpha;
+    double vnorm2 = vk * vk;
+    for (int i = k + 1; i < m; ++i) vnorm2 += A[i * n + k] * A[i * n + k];
+    if (vnorm2 == 0.0) return 0;
+    for (int j = k + 1; j < n; ++j) {
+      double sdot = vk * A[k * n + j];
+      for (int i = k + 1; i < m; ++i) sdot += A[i * n + k] * A[i * n + j];
+      const double f = 2.0 * sdot / vnorm2;
+      A[k * n + j] -= f * vk;
+      for (int i = k + 1; i < m; ++i) A[i * n + j] -= f * A[i * n + k];
+    }
+    {
+      double sdot = vk * b[k];
+      for (int i = k + 1; i < m; ++i) sdot += A[i * n + k] * b[i];
+      const double f = 2.0 * sdot / vnorm2;
+      b[k] -= f * vk;
+      for (int i = k + 1; i < m; ++i) b[i] -= f * A[i * n + k];
+    }
+    A[k * n + k] = alpha;
+  }
+  for (int k = n - 1; k >= 0; --k) {
+    double sacc = b[k];
+    for (int j = k + 1; j < n; ++j) sacc -= A[k * n + j] * x[j];
+    x[k] = sacc / A[k * n + k];
+  }
+  return 1;
+}
+
+__constant__ int PAIR_A[6] = {0, 0, 0, 1, 1, 2};
+__constant__ int PAIR_B[6] = {1, 2, 3, 2, 3, 3};
+__constant__ int BCOLS[3][5] = {{0, 1, 3, 6, 0}, {0, 1, 2, 0, 0}, {0, 1, 2, 3, 4}};
+
+__device__ void epnp_gauss_newton(const double L[60], const double rho[6], double bt[4]) {
+  for (int it = 0; it < 5; ++it) {
+    double A[24], b[6], x[4];
+    for (int i = 0; i < 6; ++i) {
+      const double* l = L + 10 * i;
+      A[4 * i + 0] = 2 * l[0] * bt[0] + l[1] * bt[1] + l[3] * bt[2] + l[6] * bt[3];
+      A[4 * i + 1] = l[1] * bt[0] + 2 * l[2] * bt[1] + l[4] * bt[2] + l[7] * bt[3];
+      A[4 * i + 2] = l[3] * bt[0] + l[4] * bt[1] + 2 * l[5] * bt[2] + l[8] * bt[3];
+      A[4 * i + 3] = l[6] * bt[0] + l[7] * bt[1] + l[8] * bt[2] + 2 * l[9] * bt[3];
+      b[i] = rho[i] - (l[0] * bt[0] * bt[0] + l[1] * bt[0] * bt[1] + l[2] * bt[1] * bt[1] + l[3] * bt[0] * bt[2] +
+                       l[4] * bt[1] * bt[2] + l[5] * bt[2] * bt[2] + l[6] * bt[0] * bt[3] + l[7] * bt[1] * bt[3] +
+                       l[8] * bt[2] * bt[3] + l[9] * bt[3] * bt[3]);
+    }
+    if (!qr_lsq(6, 4, A, b, x)) return;
+    for (int k = 0; k < 4; ++k) bt[k] += x[k];
+  }
+}
+
+__device__ double epnp_R_t(const double* pw, const double* uv, const double* alphas, const double V4[4][12],
+                           const double bt[4], double R[9], double t[3]) {
+  constexpr int n = PNP_S;
+  double ccs[12];
+  for (int j = 0; j < 12; ++j) ccs[j] = bt[0] * V4[0][j] + bt[1] * V4[1][j] + bt[2] * V4[2][j] + bt[3] * V4[3][j];
+  double pc[3 * n];
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c)
+      pc[3 * i + c] = alphas[4 * i + 0] * ccs[c] + alphas[4 * i + 1] * ccs[3 + c] + alphas[4 * i + 2] * ccs[6 + c] +
+                      alphas[4 * i + 3] * ccs[9 + c];
+  if (pc[2] < 0.0)
+    for (int i = 0; i < 3 * n; ++i) pc[i] = -pc[i];
+  double c0[3] = {0, 0, 0}, w0[3] = {0, 0, 0};
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c) {
+      c0[c] += pc[3 * i + c];
+      w0[c] += pw[3 * i + c];
+    }
+  for (int c = 0; c < 3; ++c) {
+    c0[c] /= n;
+    w0[c] /= n;
+  }
+  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) H[a * 3 + b] += (pc[3 * i + a] - c0[a]) * (pw[3 * i + b] - w0[b]);
+  double U[9], sv[3], Vm[9];
+  svd3(H, U, sv, Vm);
+  if (det3(Vm) < 0.0)
+    for (int a = 0; a < 3; ++a) U[a * 3 + 2] = -U[a * 3 + 2];
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) R[a * 3 + b] = U[a * 3 + 0] * Vm[b * 3 + 0] + U[a * 3 + 1] * Vm[b * 3 + 1] + U[a * 3 + 2] * Vm[b * 3 + 2];
+  if (det3(R) < 0.0)
+    for (int b = 0; b < 3; ++b) R[2 * 3 + b] = -R[2 * 3 + b];
+  for (int a = 0; a < 3; ++a) t[a] = c0[a] - (R[a * 3 + 0] * w0[0] + R[a * 3 + 1] * w0[1] + R[a * 3 + 2] * w0[2]);
+  double err = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double x[3];
+    for (int a = 0; a < 3; ++a)
+      x[a] = R[a * 3 + 0] * pw[3 * i + 0] + R[a * 3 + 1] * pw[3 * i + 1] + R[a * 3 + 2] * pw[3 * i + 2] + t[a];
+    const double du = uv[2 * i] - x[0] / x[2], dv = uv[2 * i + 1] - x[1] / x[2];
+    err += sqrt(du * du + dv * dv);
+  }
+  return err / n;
+}
+
+// EPnP on a 6-point sample: camera pose (R_wc, t_wc) in the points' frame.
+__device__ int epnp6(const double* pw, const double* f, double R_out[9], double t_out[3]) {
+  constexpr int n = PNP_S;
+  double uv[2 * n], alphas[4 * n];
+  for (int i = 0; i < n; ++i) {
+    uv[2 * i] = f[3 * i] / f[3 * i + 2];
+    uv[2 * i + 1] = f[3 * i + 1] / f[3 * i + 2];
+  }
+  double cw[12];
+  for (int c = 0; c < 3; ++c) cw[c] = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c) cw[c] += pw[3 * i + c];
+  for (int c = 0; c < 3; ++c) cw[c] /= n;
+  double C3[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, E3[9];
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) C3[a * 3 + b] += (pw[3 * i + a] - cw[a]) * (pw[3 * i + b] - cw[b]);
+  sym_eig3(C3, E3);
+  for (int k = 0; k < 3; ++k) {
+    const double sc = sqrt(fmax(C3[k * 4], 0.0) / n);
+    for (int c = 0; c < 3; ++c) cw[3 * (k + 1) + c] = cw[c] + sc * E3[c * 3 + k];
+  }
+  double CC[9], CI[9];
+  for (int r = 0; r < 3; ++r)
+    for (int k = 0; k < 3; ++k) CC[r * 3 + k] = cw[3 * (k + 1) + r] - cw[r];
+  const double dC = det3(CC);
+  if (!(dC != 0.0)) return 0;
+  CI[0] = (CC[4] * CC[8] - CC[5] * CC[7]) / dC;
+  CI[1] = (CC[2] * CC[7] - CC[1] * CC[8]) / dC;
+  CI[2] = (CC[1] * CC[5] - CC[2] * CC[4]) / dC;
+  CI[3] = (CC[5] * CC[6] - CC[3] * CC[8]) / dC;
+  CI[4] = (CC[0] * CC[8] - CC[2] * CC[6]) / dC;
+  CI[5] = (CC[2] * CC[3] - CC[0] * CC[5]) / dC;
+  CI[6] = (CC[3] * CC[7] - CC[4] * CC[6]) / dC;
+  CI[7] = (CC[1] * CC[6] - CC[0] * CC[7]) / dC;
+  CI[8] = (CC[0] * CC[4] - CC[1] * CC[3]) / dC;
+  for (int i = 0; i < n; ++i) {
+    const double d[3] = {pw[3 * i] - cw[0], pw[3 * i + 1] - cw[1], pw[3 * i + 2] - cw[2]};
+    double s1 = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      const double a = CI[k * 3 + 0] * d[0] + CI[k * 3 + 1] * d[1] + CI[k * 3 + 2] * d[2];
+      alphas[4 * i + 1 + k] = a;
+      s1 += a;
+    }
+    alphas[4 * i] = 1.0 - s1;
+  }
+  double V4[4][12], L[60], rho[6];
+  {
+    double MtM[144], W[144];
+    for (int i = 0; i < 144; ++i) MtM[i] = 0.0;
+    for (int i = 0; i < n; ++i) {
+      double m1[12], m2[12];
+      for (int j = 0; j < 4; ++j) {
+        const double a = alphas[4 * i + j];
+        m1[3 * j] = a; m1[3 * j + 1] = 0.0; m1[3 * j + 2] = -a * uv[2 * i];
+        m2[3 * j] = 0.0; m2[3 * j + 1] = a; m2[3 * j + 2] = -a * uv[2 * i + 1];
+      }
+      for (int r = 0; r < 12; ++r)
+        for (int c = 0; c < 12; ++c) MtM[r * 12 + c] += m1[r] * m1[c] + m2[r] * m2[c];
+    }
+    jacobi_sym12(MtM, W);
+    int ord[12];
+    for (int i = 0; i < 12; ++i) ord[i] = i;
+    for (int a = 0; a < 12; ++a)
+      for (int b = 0; b < 11 - a; ++b)
+        if (MtM[ord[b + 1] * 13] < MtM[ord[b] * 13]) { const int tt = ord[b]; ord[b] = ord[b + 1]; ord[b + 1] = tt; }
+    for (int k = 0; k < 4; ++k)
+      for (int j = 0; j < 12; ++j) V4[k][j] = W[j * 12 + ord[k]];
+  }
+  for (int pi = 0; pi < 6; ++pi) {
+    const int a = PAIR_A[pi], b = PAIR_B[pi];
+    double dv[4][3];
+    for (int k = 0; k < 4; ++k)
+      for (int c = 0; c < 3; ++c) dv[k][c] = V4[k][3 * a + c] - V4[k][3 * b + c];
+    double* l = L + 10 * pi;
+    l[0] = dot3(dv[0], dv[0]);
+    l[1] = 2.0 * dot3(dv[0], dv[1]);
+    l[2] = dot3(dv[1], dv[1]);
+    l[3] = 2.0 * dot3(dv[0], dv[2]);
+    l[4] = 2.0 * dot3(dv[1], dv[2]);
+    l[5] = dot3(dv[2], dv[2]);
+    l[6] = 2.0 * dot3(dv[0], dv[3]);
+    l[7] = 2.0 * dot3(dv[1], dv[3]);
+    l[8] = 2.0 * dot3(dv[2], dv[3]);
+    l[9] = dot3(dv[3], dv[3]);
+    double d[3];
+    for (int c = 0; c < 3; ++c) d[c] = cw[3 * a + c] - cw[3 * b + c];
+    rho[pi] = dot3(d, d);
+  }
+  double best_err = DBL_MAX, Rb[9], tb[3];
+  int found = 0;
+  for (int approx = 1; approx <= 3; ++approx) {
+    const int nc = approx == 1 ? 4 : approx == 2 ? 3 : 5;
+    double A[30], b[6], x[5], bt[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 6; ++i) {
+      for (int k = 0; k < nc; ++k) A[i * nc + k] = L[10 * i + BCOLS[approx - 1][k]];
+      b[i] = rho[i];
+    }
+    if (!qr_lsq(6, nc, A, b, x)) continue;
+    if (approx == 1) {
+      if (x[0] < 0.0) {
+        bt[0] = sqrt(-x[0]);
+        bt[1] = -x[1] / bt[0]; bt[2] = -x[2] / bt[0]; bt[3] = -x[3] / bt[0];
+      } else {
+        bt[0] = sqrt(x[0]);
+        bt[1] = x[1] / bt[0]; bt[2] = x[2] / bt[0]; bt[3] = x[3] / bt[0];
+      }
+    } else {
+      if (x[0] < 0.0) {
+        bt[0] = sqrt(-x[0]);
+        bt[1] = (x[2] < 0.0) ? sqrt(-x[2]) : 0.0;
+      } else {
+        bt[0] = sqrt(x[0]);
+        bt[1] = (x[2] > 0.0) ? sqrt(x[2]) : 0.0;
+      }
+      if (x[1] < 0.0) bt[0] = -bt[0];
+      if (approx == 3) bt[2] = x[3] / bt[0];
+    }
+    epnp_gauss_newton(L, rho, bt);
+    double R[9], t[3];
+    const double err = epnp_R_t(pw, uv, alphas, V4, bt, R, t);
+    if (err < best_err) {
+      best_err = err;
+      for (int i = 0; i < 9; ++i) Rb[i] = R[i];
+      for (int i = 0; i < 3; ++i) tb[i] = t[i];
+      found = 1;
+    }
+  }
+  if (!found) return 0;
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) R_out[a * 3 + b] = Rb[b * 3 + a];
+  for (int a = 0; a < 3; ++a) t_out[a] = -(Rb[0 * 3 + a] * tb[0] + Rb[1 * 3 + a] * tb[1] + Rb[2 * 3 + a] * tb[2]);
+  return 1;
+}
+
+__device__ double pnp_error(const double R[9], const double t[3], const double p[3], const double f[3]) {
+  const double d[3] = {p[0] - t[0], p[1] - t[1], p[2] - t[2]};
+  double q[3];
+  for (int i = 0; i < 3; ++i) q[i] = R[0 * 3 + i] * d[0] + R[1 * 3 + i] * d[1] + R[2 * 3 + i] * d[2];
+  const double nq = sqrt(dot3(q, q));
+  return 1.0 - (q[0] * f[0] + q[1] * f[1] + q[2] * f[2]) / nq;
+}
+
 struct RsParams {
   double thr2d, thr3d, prob;
   int max_iter, min2d, min3d, pmax;
+  int pnp;  // pose_recovery_type 1: k_ransac stops after 2D-2D, k_pnp recovers the pose
+};
+struct PnpParams {
+  double thr, prob;
+  int max_iter, min2d, min_pnp, pmax;
 };
 
 __global__ __launch_bounds__(RS_BLOCK) void k_ransac(const double* bearings, const double* points, int N,
@@ -630,6 +921,13 @@ __global__ __launch_bounds__(RS_BLOCK) void k_ransac(const double* bearings, con
     if (lane == 0) *R_ = r;
     return;
   }
+  if (P.pnp) {  // k_pnp takes over from the 2D-2D inlier mask
+    if (lane == 0) {
+      for (int i = 0; i < 12; ++i) r.T_query_match[i] = 0.0;
+      *R_ = r;
+    }
+    return;
+  }
   // 3D-3D given rotation: T_j = p_q - R p_m over the 2D-2D inliers in pair order
   __syncthreads();
   double* T = F2;  // reuse: [n3][3] translations
@@ -704,6 +1002,135 @@ __global__ __launch_bounds__(RS_BLOCK) void k_ransac(const double* bearings, con
   }
 }
 
+// PnP pose recovery (pose_recovery_type 1): opengv RANSAC over the
+// AbsolutePoseSacProblem with EPnP (sample size 6) on the 2D-2D inliers whose
+// stereo points are valid — query bearings against match-frame points — one
+// wavefront per candidate, one pass per lane, serial control replayed by lane
+// 0 exactly as in k_ransac.
+__global__ __launch_bounds__(RS_BLOCK) void k_pnp(const double* bearings, const double* points, int N,
+                                                  const int* cq, const int* cm, const int2* pairs, const int* Kin,
+                                                  const short* table, PnpParams P, kmx_lcd_result* res,
+                                                  unsigned char* masks) {
+  extern __shared__ __attribute__((aligned(16))) double sm_d[];
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  kmx_lcd_result* R_ = res + c;
+  if (R_->mono_inliers < P.min2d) return;
+  const int K = Kin[c];
+  const int q = cq[c], m = cm[c];
+  double* Fq = sm_d;                  // [n2][3]
+  double* Pw = Fq + 3 * N;            // [n2][3]
+  double* models = Pw + 3 * N;        // [64][12]
+  double* bestm = models + 64 * 12;   // [12]
+  int* okc = reinterpret_cast<int*>(bestm + 12);
+  int* cnt = okc + 64;
+  int* ctrl = cnt + 64;               // [4]
+  int* id2 = ctrl + 4;                // [n2]
+  unsigned char* mask = masks + (size_t)c * N;
+  const int2* pl = pairs + (size_t)c * N;
+  if (lane == 0) {
+    int n2 = 0;
+    for (int j = 0; j < K; ++j) {
+      if (!(mask[j] & 1)) continue;
+      const int2 pr = pl[j];
+      const double* a = points + ((size_t)q * N + pr.x) * 3;
+      const double* b = points + ((size_t)m * N + pr.y) * 3;
+      if (isnan(a[0]) || isnan(a[1]) || isnan(a[2]) || isnan(b[0]) || isnan(b[1]) || isnan(b[2])) continue;
+      for (int k = 0; k < 3; ++k) {
+        Fq[3 * n2 + k] = bearings[((size_t)q * N + pr.x) * 3 + k];
+        Pw[3 * n2 + k] = b[k];
+      }
+      id2[n2++] = j;
+    }
+    ctrl[3] = n2;
+    ctrl[1] = 0;
+  }
+  __syncthreads();
+  const int n2 = ctrl[3];
+  int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
+  double kk = 1.0;
+  const int max_skip = P.max_iter * 10;
+  if (n2 >= PNP_S) {
+    const short* tab = table + (size_t)(n2 - PNP_S) * P.pmax * PNP_S;
+    for (int base = 0;; base += RS_BLOCK) {
+      const int p = base + lane;
+      int ok = 0, count = 0;
+      double Rm[9], tm[3];
+      if (p < P.pmax) {
+        double sp[3 * PNP_S], sf[3 * PNP_S];
+        for (int i = 0; i < PNP_S; ++i) {
+          const int id = tab[(size_t)p * PNP_S + i];
+          for (int k = 0; k < 3; ++k) {
+            sp[3 * i + k] = Pw[3 * id + k];
+            sf[3 * i + k] = Fq[3 * id + k];
+          }
+        }
+        ok = epnp6(sp, sf, Rm, tm);
+        if (ok)
+          for (int j = 0; j < n2; ++j)
+            if (pnp_error(Rm, tm, Pw + 3 * j, Fq + 3 * j) < P.thr) ++count;
+      }
+      okc[lane] = ok;
+      cnt[lane] = count;
+      if (ok) {
+        for (int i = 0; i < 9; ++i) models[lane * 12 + i] = Rm[i];
+        for (int i = 0; i < 3; ++i) models[lane * 12 + 9 + i] = tm[i];
+      }
+      __syncthreads();
+      if (lane == 0) {
+        int done = 0;
+        for (int l = 0; l < RS_BLOCK; ++l) {
+          if (!(iterations < kk && skipped < max_skip) || base + l >= P.pmax) { done = 1; break; }
+          if (!okc[l]) { ++skipped; continue; }
+          if (cnt[l] > best_cnt) {
+            best_cnt = cnt[l];
+            for (int i = 0; i < 12; ++i) bestm[i] = models[l * 12 + i];
+            have = 1;
+            const double w = (double)cnt[l] / (double)n2;
+            double p_no = 1.0 - pow(w, (double)PNP_S);
+            p_no = fmax(DBL_EPSILON, p_no);
+            p_no = fmin(1.0 - DBL_EPSILON, p_no);
+            kk = log(1.0 - P.prob) / log(p_no);
+          }
+          ++iterations;
+          if (iterations > P.max_iter) { done = 1; break; }
+        }
+        if (!done && base + RS_BLOCK >= P.pmax) done = 1;
+        ctrl[0] = done;
+        ctrl[1] = have;
+      }
+      __syncthreads();
+      if (ctrl[0]) break;
+    }
+  }
+  __syncthreads();
+  const int have_model = ctrl[1];
+  int np = 0;
+  double Ro[9], to[3];
+  if (have_model) {
+    for (int i = 0; i < 9; ++i) Ro[i] = bestm[i];
+    for (int i = 0; i < 3; ++i) to[i] = bestm[9 + i];
+    for (int j0 = 0; j0 < n2; j0 += RS_BLOCK) {
+      const int j = j0 + lane;
+      const bool in = (j < n2) && pnp_error(Ro, to, Pw + 3 * j, Fq + 3 * j) < P.thr;
+      if (in) mask[id2[j]] |= 2;
+      np += __popcll(__ballot(in));
+    }
+  }
+  if (lane == 0) {
+    kmx_lcd_result r = *R_;
+    r.pnp_inliers = np;
+    if (have_model) {
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) r.T_query_match[a * 3 + b] = Ro[b * 3 + a];
+      for (int a = 0; a < 3; ++a)
+        r.T_query_match[9 + a] = -(Ro[0 * 3 + a] * to[0] + Ro[1 * 3 + a] * to[1] + Ro[2 * 3 + a] * to[2]);
+    }
+    r.accepted = (have_model && np >= P.min_pnp) ? 1 : 0;
+    *R_ = r;
+  }
+}
+
 }  // namespace
 
 // ============================================================== handle ====
@@ -718,6 +1145,7 @@ struct kmx_lcd {
   double* d_pts = nullptr;
   int* d_nfeat = nullptr;
   short* d_table = nullptr;
+  short* d_table6 = nullptr;  // 6-point samples (PnP), built when pose_recovery_type == 1
   int pmax = 0;
   // candidate buffers
   int cap = 0;
@@ -730,10 +1158,10 @@ struct kmx_lcd {
 namespace {
 
 void lcd_free_pool(kmx_lcd* h) {
-  void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat, h->d_table};
+  void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat, h->d_table, h->d_table6};
   for (void* x : p)
     if (x) (void)hipFree(x);
-  h->d_desc = nullptr; h->d_bear = h->d_pts = nullptr; h->d_nfeat = nullptr; h->d_table = nullptr;
+  h->d_desc = nullptr; h->d_bear = h->d_pts = nullptr; h->d_nfeat = nullptr; h->d_table = nullptr; h->d_table6 = nullptr;
 }
 void lcd_free_cand(kmx_lcd* h) {
   void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask};
@@ -746,16 +1174,16 @@ void lcd_free_cand(kmx_lcd* h) {
 // opengv sampler table: for every K in [5, N], the 5 indices drawn by each of
 // the first pmax passes (std::mt19937 seeded per problem; drawIndexSample swap
 // shuffle over a persistent index vector; GCC-9 or GCC-11 uniform_int).
-void build_table(const kmx_lcd_params& P, int N, int pmax, std::vector<short>& tab) {
-  tab.assign((size_t)std::max(N - 4, 1) * pmax * 5, 0);
+void build_table(const kmx_lcd_params& P, int N, int pmax, std::vector<short>& tab, int S = 5) {
+  tab.assign((size_t)std::max(N - S + 1, 1) * pmax * S, 0);
   std::vector<int> sh;
-  for (int K = 5; K <= N; ++K) {
+  for (int K = S; K <= N; ++K) {
     std::mt19937 rng(P.ransac_seed);
     sh.resize(K);
     for (int i = 0; i < K; ++i) sh[i] = i;
-    short* out = tab.data() + (size_t)(K - 5) * pmax * 5;
+    short* out = tab.data() + (size_t)(K - S) * pmax * S;
     for (int p = 0; p < pmax; ++p) {
-      for (int i = 0; i < 5; ++i) {
+      for (int i = 0; i < S; ++i) {
         uint32_t x;
         if (P.rng_variant == KMX_RNG_GCC11) {
           x = (uint32_t)rng() >> 1;
@@ -766,7 +1194,7 @@ void build_table(const kmx_lcd_params& P, int N, int pmax, std::vector<short>& t
         const int j = i + (int)((size_t)x % (size_t)(K - i));
         std::swap(sh[i], sh[j]);
       }
-      for (int i = 0; i < 5; ++i) out[p * 5 + i] = (short)sh[i];
+      for (int i = 0; i < S; ++i) out[p * S + i] = (short)sh[i];
     }
   }
 }
@@ -803,10 +1231,25 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   rp.min2d = h->P.min_2d2d_inliers;
   rp.min3d = h->P.min_3d3d_inliers;
   rp.pmax = h->pmax;
+  rp.pnp = (h->P.pose_recovery_type == 1) ? 1 : 0;
   hipLaunchKernelGGL(k_ransac, dim3(n), dim3(RS_BLOCK), ransac_smem(h->N), h->stream, (const double*)h->d_bear,
                      (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
                      (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
-                     want_masks ? h->d_mask : nullptr);
+                     (want_masks || rp.pnp) ? h->d_mask : nullptr);
+  if (rp.pnp) {
+    PnpParams pp;
+    pp.thr = h->P.ransac_threshold_2d3d;
+    pp.prob = h->P.ransac_probability;
+    pp.max_iter = h->P.ransac_max_iterations;
+    pp.min2d = h->P.min_2d2d_inliers;
+    pp.min_pnp = h->P.min_2d3d_inliers;
+    pp.pmax = h->pmax;
+    const size_t smem = sizeof(double) * (6 * (size_t)h->N + 64 * 12 + 12) + sizeof(int) * (64 + 64 + 4 + (size_t)h->N);
+    hipLaunchKernelGGL(k_pnp, dim3(n), dim3(RS_BLOCK), smem, h->stream, (const double*)h->d_bear,
+                       (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
+                       (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table6, pp, h->d_res,
+                       h->d_mask);
+  }
   KMX_HIP(hipGetLastError());
   return 0;
 }
@@ -892,6 +1335,11 @@ extern "C" int kmx_lcd_set_frames(kmx_lcd* h, const kmx_lcd_batch_desc* pool) {
   build_table(h->P, h->N, h->pmax, tab);
   KMX_HIP(hipMalloc(&h->d_table, sizeof(short) * tab.size()));
   KMX_HIP(hipMemcpy(h->d_table, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
+  if (h->P.pose_recovery_type == 1) {
+    build_table(h->P, h->N, h->pmax, tab, PNP_S);
+    KMX_HIP(hipMalloc(&h->d_table6, sizeof(short) * tab.size()));
+    KMX_HIP(hipMemcpy(h->d_table6, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
+  }
   return KMX_OK;
   KMX_GUARD_END
 }

@@ -82,7 +82,8 @@ class LcdParams(C.Structure):
         ("ransac_threshold_3d3d", C.c_double), ("ransac_max_iterations", C.c_int),
         ("ransac_probability", C.c_double), ("ransac_randomize", C.c_int),
         ("ransac_seed", C.c_uint32), ("rng_variant", C.c_int),
-        ("use_1point_3d3d", C.c_int), ("reserved", C.c_int * 8),
+        ("use_1point_3d3d", C.c_int), ("pose_recovery_type", C.c_int), ("min_2d3d_inliers", C.c_int),
+        ("ransac_threshold_2d3d", C.c_double), ("reserved", C.c_int * 4),
     ]
 
 
@@ -90,7 +91,7 @@ class LcdResult(C.Structure):
     _fields_ = [
         ("n_matches", C.c_int32), ("mono_inliers", C.c_int32),
         ("stereo_inliers", C.c_int32), ("accepted", C.c_int32),
-        ("iterations_2d2d", C.c_int32), ("pad", C.c_int32),
+        ("iterations_2d2d", C.c_int32), ("pnp_inliers", C.c_int32),
         ("T_query_match", C.c_double * 12),
     ]
 

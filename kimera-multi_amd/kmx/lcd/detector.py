@@ -34,6 +34,11 @@ class LcdParams:
     ransac_seed: int = 12345
     rng_variant: str = "gcc9"           # libstdc++ of ROS Noetic (SURVEY.md §0 finding 5)
     ransac_use_1point_3d3d: int = 1
+    # PnP pose recovery (pose_recovery_type 1: EPnP RANSAC, LcdParams.yaml:53,57,63,74)
+    pose_recovery_type: int = 0
+    min_nr_2d3d_inliers: int = 20
+    ransac_threshold_2d3d: float = 1.0   # pixels
+    focal_length: float = 380.0          # px, converts the 2D-3D threshold to (1 - cos) [U: D455 intrinsics]
     # BoW detection (LcdParams.yaml:3-12)
     use_nss: int = 1
     alpha: float = 0.4
@@ -55,7 +60,8 @@ class LcdParams:
         p = cls()
         for k in ("lowe_ratio", "min_nr_2d2d_inliers", "min_nr_3d3d_inliers", "ransac_threshold_2d2d",
                   "ransac_threshold_3d3d", "ransac_max_iterations", "ransac_probability", "ransac_randomize",
-                  "ransac_use_1point_3d3d", "use_nss", "alpha", "min_temporal_matches", "recent_frames_window",
+                  "ransac_use_1point_3d3d", "pose_recovery_type", "min_nr_2d3d_inliers", "ransac_threshold_2d3d",
+                  "use_nss", "alpha", "min_temporal_matches", "recent_frames_window",
                   "max_db_results", "min_nss_factor", "min_matches_per_island", "max_intraisland_gap",
                   "max_nrFrames_between_islands", "max_nrFrames_between_queries"):
             if k in y:
@@ -80,6 +86,9 @@ class LcdParams:
         c.ransac_seed = int(self.ransac_seed)
         c.rng_variant = abi.KMX_RNG_GCC11 if self.rng_variant == "gcc11" else abi.KMX_RNG_GCC9
         c.use_1point_3d3d = int(self.ransac_use_1point_3d3d)
+        c.pose_recovery_type = int(self.pose_recovery_type)
+        c.min_2d3d_inliers = int(self.min_nr_2d3d_inliers)
+        c.ransac_threshold_2d3d = 1.0 - np.cos(np.arctan(float(self.ransac_threshold_2d3d) / float(self.focal_length)))
         return c
 
 
@@ -158,7 +167,8 @@ class LoopClosureDetector:
         for i in range(n):
             r = res[i]
             out.append({"n_matches": r.n_matches, "mono_inliers": r.mono_inliers,
-                        "stereo_inliers": r.stereo_inliers, "accepted": bool(r.accepted),
+                        "stereo_inliers": r.stereo_inliers, "pnp_inliers": r.pnp_inliers,
+                        "accepted": bool(r.accepted),
                         "iterations_2d2d": r.iterations_2d2d, "T_query_match": np.array(r.T_query_match[:])})
         return out, masks
 

@@ -660,6 +660,382 @@ static int ransac_2d2d(const kmx_lcd_params* P, const double* F1, const double* 
   return 1;
 }
 
+/* ------------------------------------------- EPnP (Lepetit et al. 2009) -- */
+/* opengv absolute_pose::epnp as used by AbsolutePoseSacProblem(EPNP) for the
+ * PnP pose recovery (LcdParams.yaml:53,57,63,74). Bearings f (camera) and
+ * points p (world = match frame); image coordinates u = f0/f2, v = f1/f2
+ * (unit focal, zero principal point). Restated algorithm:
+ *   control points: centroid + principal axes scaled by sqrt(eig / n);
+ *   barycentric alphas; M (2n x 12); MtM eigen (cyclic Jacobi) -> the 4
+ *   eigenvectors of the smallest eigenvalues; L_6x10 and rho; betas from the
+ *   three linearisations (L_6x4, L_6x3, L_6x5 least squares by Householder
+ *   QR) each refined by 5 Gauss-Newton steps; R, t by Horn/Umeyama (SVD of
+ *   the 3x3 cross-covariance); the solution with the smallest mean
+ *   reprojection error wins. Returns (R_wc, t_wc) = camera orientation and
+ *   position in the world frame (opengv convention). [U: opengv solves the
+ *   linear systems with SVD; parity unpinned.] */
+static void jacobi_sym(int n, double* A, double* V) {
+  for (int i = 0; i < n * n; ++i) V[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) off += A[p * n + q] * A[p * n + q];
+    if (off == 0.0) break;
+    for (int p = 0; p < n - 1; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        const double apq = A[p * n + q];
+        if (apq == 0.0) continue;
+        const double app = A[p * n + p], aqq = A[q * n + q];
+        const double theta = (aqq - app) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
+        for (int k = 0; k < n; ++k) {
+          const double akp = A[k * n + p], akq = A[k * n + q];
+          A[k * n + p] = cs * akp - sn * akq;
+          A[k * n + q] = sn * akp + cs * akq;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double apk = A[p * n + k], aqk = A[q * n + k];
+          A[p * n + k] = cs * apk - sn * aqk;
+          A[q * n + k] = sn * apk + cs * aqk;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double vkp = V[k * n + p], vkq = V[k * n + q];
+          V[k * n + p] = cs * vkp - sn * vkq;
+          V[k * n + q] = sn * vkp + cs * vkq;
+        }
+      }
+  }
+}
+
+/* least squares min |A x - b| for A (m x n, row-major, m >= n) by Householder
+ * QR; A and b are overwritten. Returns 0 when rank deficient. */
+static int qr_lsq(int m, int n, double* A, double* b, double* x) {
+  for (int k = 0; k < n; ++k) {
+    double nrm = 0.0;
+    for (int i = k; i < m; ++i) nrm += A[i * n + k] * A[i * n + k];
+    nrm = sqrt(nrm);
+    if (nrm == 0.0) return 0;
+    const double alpha = (A[k * n + k] > 0.0) ? -nrm : nrm;
+    double vk = A[k * n + k] - alpha;
+    double vnorm2 = vk * vk;
+    for (int i = k + 1; i < m; ++i) vnorm2 += A[i * n + k] * A[i * n + k];
+    if (vnorm2 == 0.0) return 0;
+    /* v = (vk, A[k+1..m-1][k]); H = I - 2 v v^T / (v^T v) */
+    for (int j = k + 1; j < n; ++j) {
+      double sdot = vk * A[k * n + j];
+      for (int i = k + 1; i < m; ++i) sdot += A[i * n + k] * A[i * n + j];
+      const double f = 2.0 * sdot / vnorm2;
+      A[k * n + j] -= f * vk;
+      for (int i = k + 1; i < m; ++i) A[i * n + j] -= f * A[i * n + k];
+    }
+    {
+      double sdot = vk * b[k];
+      for (int i = k + 1; i < m; ++i) sdot += A[i * n + k] * b[i];
+      const double f = 2.0 * sdot / vnorm2;
+      b[k] -= f * vk;
+      for (int i = k + 1; i < m; ++i) b[i] -= f * A[i * n + k];
+    }
+    A[k * n + k] = alpha;
+  }
+  for (int k = n - 1; k >= 0; --k) {
+    double sacc = b[k];
+    for (int j = k + 1; j < n; ++j) sacc -= A[k * n + j] * x[j];
+    x[k] = sacc / A[k * n + k];
+  }
+  return 1;
+}
+
+static const int PAIR_A[6] = {0, 0, 0, 1, 1, 2}, PAIR_B[6] = {1, 2, 3, 2, 3, 3};
+
+static void epnp_gauss_newton(const double L[60], const double rho[6], double bt[4]) {
+  for (int it = 0; it < 5; ++it) {
+    double A[24], b[6], x[4];
+    for (int i = 0; i < 6; ++i) {
+      const double* l = L + 10 * i;
+      A[4 * i + 0] = 2 * l[0] * bt[0] + l[1] * bt[1] + l[3] * bt[2] + l[6] * bt[3];
+      A[4 * i + 1] = l[1] * bt[0] + 2 * l[2] * bt[1] + l[4] * bt[2] + l[7] * bt[3];
+      A[4 * i + 2] = l[3] * bt[0] + l[4] * bt[1] + 2 * l[5] * bt[2] + l[8] * bt[3];
+      A[4 * i + 3] = l[6] * bt[0] + l[7] * bt[1] + l[8] * bt[2] + 2 * l[9] * bt[3];
+      b[i] = rho[i] - (l[0] * bt[0] * bt[0] + l[1] * bt[0] * bt[1] + l[2] * bt[1] * bt[1] + l[3] * bt[0] * bt[2] +
+                       l[4] * bt[1] * bt[2] + l[5] * bt[2] * bt[2] + l[6] * bt[0] * bt[3] + l[7] * bt[1] * bt[3] +
+                       l[8] * bt[2] * bt[3] + l[9] * bt[3] * bt[3]);
+    }
+    if (!qr_lsq(6, 4, A, b, x)) return;
+    for (int k = 0; k < 4; ++k) bt[k] += x[k];
+  }
+}
+
+/* camera-frame control points from betas, then R, t (world -> camera) by
+ * Horn; returns the mean reprojection error. */
+static double epnp_R_t(int n, const double* pw, const double* uv, const double* alphas, const double V4[4][12],
+                       const double bt[4], double R[9], double t[3]) {
+  double ccs[12];
+  for (int j = 0; j < 12; ++j) ccs[j] = bt[0] * V4[0][j] + bt[1] * V4[1][j] + bt[2] * V4[2][j] + bt[3] * V4[3][j];
+  double* pc = (double*)malloc(sizeof(double) * 3 * (size_t)n);
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c)
+      pc[3 * i + c] = alphas[4 * i + 0] * ccs[c] + alphas[4 * i + 1] * ccs[3 + c] + alphas[4 * i + 2] * ccs[6 + c] +
+                      alphas[4 * i + 3] * ccs[9 + c];
+  if (pc[2] < 0.0) /* solve_for_sign: the first point in front of the camera */
+    for (int i = 0; i < 3 * n; ++i) pc[i] = -pc[i];
+  double c0[3] = {0, 0, 0}, w0[3] = {0, 0, 0};
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c) {
+      c0[c] += pc[3 * i + c];
+      w0[c] += pw[3 * i + c];
+    }
+  for (int c = 0; c < 3; ++c) {
+    c0[c] /= n;
+    w0[c] /= n;
+  }
+  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) H[a * 3 + b] += (pc[3 * i + a] - c0[a]) * (pw[3 * i + b] - w0[b]);
+  double U[9], sv[3], Vm[9];
+  svd3(H, U, sv, Vm);
+  /* svd3's U is right-handed (u3 = u1 x u2): for a proper rotation the third
+   * left vector carries det(V) (Umeyama: R = U diag(1, 1, det U det V) V^T) */
+  if (det3(Vm) < 0.0)
+    for (int a = 0; a < 3; ++a) U[a * 3 + 2] = -U[a * 3 + 2];
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) R[a * 3 + b] = U[a * 3 + 0] * Vm[b * 3 + 0] + U[a * 3 + 1] * Vm[b * 3 + 1] + U[a * 3 + 2] * Vm[b * 3 + 2];
+  if (det3(R) < 0.0)
+    for (int b = 0; b < 3; ++b) R[2 * 3 + b] = -R[2 * 3 + b];
+  for (int a = 0; a < 3; ++a) t[a] = c0[a] - (R[a * 3 + 0] * w0[0] + R[a * 3 + 1] * w0[1] + R[a * 3 + 2] * w0[2]);
+  double err = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double x[3];
+    for (int a = 0; a < 3; ++a)
+      x[a] = R[a * 3 + 0] * pw[3 * i + 0] + R[a * 3 + 1] * pw[3 * i + 1] + R[a * 3 + 2] * pw[3 * i + 2] + t[a];
+    const double du = uv[2 * i] - x[0] / x[2], dv = uv[2 * i + 1] - x[1] / x[2];
+    err += sqrt(du * du + dv * dv);
+  }
+  free(pc);
+  return err / n;
+}
+
+int orc_epnp(int n, const double* pw, const double* f, double R_out[9], double t_out[3]) {
+  if (n < 4) return 0;
+  double* uv = (double*)malloc(sizeof(double) * 2 * (size_t)n);
+  double* alphas = (double*)malloc(sizeof(double) * 4 * (size_t)n);
+  for (int i = 0; i < n; ++i) {
+    uv[2 * i] = f[3 * i] / f[3 * i + 2];
+    uv[2 * i + 1] = f[3 * i + 1] / f[3 * i + 2];
+  }
+  /* control points */
+  double cw[12];
+  for (int c = 0; c < 3; ++c) cw[c] = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c) cw[c] += pw[3 * i + c];
+  for (int c = 0; c < 3; ++c) cw[c] /= n;
+  double C3[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, E3[9];
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) C3[a * 3 + b] += (pw[3 * i + a] - cw[a]) * (pw[3 * i + b] - cw[b]);
+  sym_eig3(C3, E3);
+  for (int k = 0; k < 3; ++k) {
+    const double sc = sqrt(fmax(C3[k * 4], 0.0) / n);
+    for (int c = 0; c < 3; ++c) cw[3 * (k + 1) + c] = cw[c] + sc * E3[c * 3 + k];
+  }
+  /* barycentric coordinates */
+  double CC[9], CI[9];
+  for (int r = 0; r < 3; ++r)
+    for (int k = 0; k < 3; ++k) CC[r * 3 + k] = cw[3 * (k + 1) + r] - cw[r];
+  const double dC = det3(CC);
+  int ok = (dC != 0.0);
+  if (ok) {
+    CI[0] = (CC[4] * CC[8] - CC[5] * CC[7]) / dC;
+    CI[1] = (CC[2] * CC[7] - CC[1] * CC[8]) / dC;
+    CI[2] = (CC[1] * CC[5] - CC[2] * CC[4]) / dC;
+    CI[3] = (CC[5] * CC[6] - CC[3] * CC[8]) / dC;
+    CI[4] = (CC[0] * CC[8] - CC[2] * CC[6]) / dC;
+    CI[5] = (CC[2] * CC[3] - CC[0] * CC[5]) / dC;
+    CI[6] = (CC[3] * CC[7] - CC[4] * CC[6]) / dC;
+    CI[7] = (CC[1] * CC[6] - CC[0] * CC[7]) / dC;
+    CI[8] = (CC[0] * CC[4] - CC[1] * CC[3]) / dC;
+    for (int i = 0; i < n; ++i) {
+      const double d[3] = {pw[3 * i] - cw[0], pw[3 * i + 1] - cw[1], pw[3 * i + 2] - cw[2]};
+      double s1 = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        const double a = CI[k * 3 + 0] * d[0] + CI[k * 3 + 1] * d[1] + CI[k * 3 + 2] * d[2];
+        alphas[4 * i + 1 + k] = a;
+        s1 += a;
+      }
+      alphas[4 * i] = 1.0 - s1;
+    }
+  }
+  double V4[4][12];
+  double L[60], rho[6];
+  if (ok) {
+    /* MtM accumulated row pair by row pair */
+    double MtM[144], W[144];
+    for (int i = 0; i < 144; ++i) MtM[i] = 0.0;
+    for (int i = 0; i < n; ++i) {
+      double m1[12], m2[12];
+      for (int j = 0; j < 4; ++j) {
+        const double a = alphas[4 * i + j];
+        m1[3 * j] = a; m1[3 * j + 1] = 0.0; m1[3 * j + 2] = -a * uv[2 * i];
+        m2[3 * j] = 0.0; m2[3 * j + 1] = a; m2[3 * j + 2] = -a * uv[2 * i + 1];
+      }
+      for (int r = 0; r < 12; ++r)
+        for (int c = 0; c < 12; ++c) MtM[r * 12 + c] += m1[r] * m1[c] + m2[r] * m2[c];
+    }
+    jacobi_sym(12, MtM, W);
+    /* the 4 smallest eigenvalues, ascending (stable on ties) */
+    int ord[12];
+    for (int i = 0; i < 12; ++i) ord[i] = i;
+    for (int a = 0; a < 12; ++a)
+      for (int b = 0; b < 11 - a; ++b)
+        if (MtM[ord[b + 1] * 13] < MtM[ord[b] * 13]) { const int tt = ord[b]; ord[b] = ord[b + 1]; ord[b + 1] = tt; }
+    for (int k = 0; k < 4; ++k)
+      for (int j = 0; j < 12; ++j) V4[k][j] = W[j * 12 + ord[k]];
+    for (int pi = 0; pi < 6; ++pi) {
+      const int a = PAIR_A[pi], b = PAIR_B[pi];
+      double dv[4][3];
+      for (int k = 0; k < 4; ++k)
+        for (int c = 0; c < 3; ++c) dv[k][c] = V4[k][3 * a + c] - V4[k][3 * b + c];
+      double* l = L + 10 * pi;
+      l[0] = dot3(dv[0], dv[0]);
+      l[1] = 2.0 * dot3(dv[0], dv[1]);
+      l[2] = dot3(dv[1], dv[1]);
+      l[3] = 2.0 * dot3(dv[0], dv[2]);
+      l[4] = 2.0 * dot3(dv[1], dv[2]);
+      l[5] = dot3(dv[2], dv[2]);
+      l[6] = 2.0 * dot3(dv[0], dv[3]);
+      l[7] = 2.0 * dot3(dv[1], dv[3]);
+      l[8] = 2.0 * dot3(dv[2], dv[3]);
+      l[9] = dot3(dv[3], dv[3]);
+      double d[3];
+      for (int c = 0; c < 3; ++c) d[c] = cw[3 * a + c] - cw[3 * b + c];
+      rho[pi] = dot3(d, d);
+    }
+  }
+  double best_err = DBL_MAX, Rb[9], tb[3];
+  int found = 0;
+  for (int approx = 1; ok && approx <= 3; ++approx) {
+    static const int COLS1[4] = {0, 1, 3, 6}, COLS2[3] = {0, 1, 2}, COLS3[5] = {0, 1, 2, 3, 4};
+    const int nc = approx == 1 ? 4 : approx == 2 ? 3 : 5;
+    const int* cols = approx == 1 ? COLS1 : approx == 2 ? COLS2 : COLS3;
+    double A[30], b[6], x[5], bt[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 6; ++i) {
+      for (int k = 0; k < nc; ++k) A[i * nc + k] = L[10 * i + cols[k]];
+      b[i] = rho[i];
+    }
+    if (!qr_lsq(6, nc, A, b, x)) continue;
+    if (approx == 1) {
+      if (x[0] < 0.0) {
+        bt[0] = sqrt(-x[0]);
+        bt[1] = -x[1] / bt[0]; bt[2] = -x[2] / bt[0]; bt[3] = -x[3] / bt[0];
+      } else {
+        bt[0] = sqrt(x[0]);
+        bt[1] = x[1] / bt[0]; bt[2] = x[2] / bt[0]; bt[3] = x[3] / bt[0];
+      }
+    } else {
+      if (x[0] < 0.0) {
+        bt[0] = sqrt(-x[0]);
+        bt[1] = (x[2] < 0.0) ? sqrt(-x[2]) : 0.0;
+      } else {
+        bt[0] = sqrt(x[0]);
+        bt[1] = (x[2] > 0.0) ? sqrt(x[2]) : 0.0;
+      }
+      if (x[1] < 0.0) bt[0] = -bt[0];
+      if (approx == 3) bt[2] = x[3] / bt[0];
+    }
+    epnp_gauss_newton(L, rho, bt);
+    double R[9], t[3];
+    const double err = epnp_R_t(n, pw, uv, alphas, V4, bt, R, t);
+    if (err < best_err) {
+      best_err = err;
+      memcpy(Rb, R, sizeof(Rb));
+      memcpy(tb, t, sizeof(tb));
+      found = 1;
+    }
+  }
+  free(uv);
+  free(alphas);
+  if (!found) return 0;
+  /* opengv returns the camera pose in the world: R_wc = R^T, t_wc = -R^T t */
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) R_out[a * 3 + b] = Rb[b * 3 + a];
+  for (int a = 0; a < 3; ++a) t_out[a] = -(Rb[0 * 3 + a] * tb[0] + Rb[1 * 3 + a] * tb[1] + Rb[2 * 3 + a] * tb[2]);
+  return 1;
+}
+
+/* AbsolutePoseSacProblem error: 1 - f . normalize(R^T (p - t)) */
+static double pnp_error(const double R[9], const double t[3], const double p[3], const double f[3]) {
+  const double d[3] = {p[0] - t[0], p[1] - t[1], p[2] - t[2]};
+  double q[3];
+  for (int i = 0; i < 3; ++i) q[i] = R[0 * 3 + i] * d[0] + R[1 * 3 + i] * d[1] + R[2 * 3 + i] * d[2];
+  const double nq = sqrt(dot3(q, q));
+  return 1.0 - (q[0] * f[0] + q[1] * f[1] + q[2] * f[2]) / nq;
+}
+
+/* opengv sac::Ransac over the AbsolutePoseSacProblem (sample size 6, EPnP). */
+static int ransac_pnp(const kmx_lcd_params* P, const double* Fq, const double* Pm, int K, double R[9], double t[3],
+                      uint8_t* inl, int* n_inl) {
+  *n_inl = 0;
+  const int S = 6;
+  if (K < S) return 0;
+  orc_mt19937 m;
+  mt_seed(&m, P->ransac_seed);
+  int32_t* sh = (int32_t*)malloc(sizeof(int32_t) * K);
+  for (int i = 0; i < K; ++i) sh[i] = i;
+  int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
+  const int max_skip = P->ransac_max_iterations * 10;
+  double k = 1.0;
+  double bR[9], bt[3];
+  while (iterations < k && skipped < max_skip) {
+    double sp[18], sf[18];
+    for (int i = 0; i < S; ++i) {
+      const int r = uid_draw(&m, P->rng_variant);
+      const int j = i + (int)((size_t)r % (size_t)(K - i));
+      const int32_t tt = sh[i];
+      sh[i] = sh[j];
+      sh[j] = tt;
+    }
+    for (int i = 0; i < S; ++i)
+      for (int c = 0; c < 3; ++c) {
+        sp[3 * i + c] = Pm[3 * sh[i] + c];
+        sf[3 * i + c] = Fq[3 * sh[i] + c];
+      }
+    double Rm[9], tm[3];
+    if (!orc_epnp(S, sp, sf, Rm, tm)) {
+      ++skipped;
+      continue;
+    }
+    int cnt = 0;
+    for (int j = 0; j < K; ++j)
+      if (pnp_error(Rm, tm, Pm + 3 * j, Fq + 3 * j) < P->ransac_threshold_2d3d) ++cnt;
+    if (cnt > best_cnt) {
+      best_cnt = cnt;
+      memcpy(bR, Rm, sizeof(bR));
+      memcpy(bt, tm, sizeof(bt));
+      have = 1;
+      const double w = (double)cnt / (double)K;
+      double p_no = 1.0 - pow(w, (double)S);
+      p_no = fmax(DBL_EPSILON, p_no);
+      p_no = fmin(1.0 - DBL_EPSILON, p_no);
+      k = log(1.0 - P->ransac_probability) / log(p_no);
+    }
+    ++iterations;
+    if (iterations > P->ransac_max_iterations) break;
+  }
+  free(sh);
+  if (!have) return 0;
+  int c = 0;
+  for (int j = 0; j < K; ++j) {
+    const int in = pnp_error(bR, bt, Pm + 3 * j, Fq + 3 * j) < P->ransac_threshold_2d3d;
+    inl[j] = (uint8_t)in;
+    c += in;
+  }
+  *n_inl = c;
+  memcpy(R, bR, sizeof(bR));
+  memcpy(t, bt, sizeof(bt));
+  return 1;
+}
+
 /* 1-point 3D-3D given the 2D-2D rotation (ransac_use_1point_3d3d = 1). */
 static int given_rotation_3d3d(const kmx_lcd_params* P, const double R[9], const double* Pq, const double* Pm,
                                const uint8_t* valid, int K, double t_out[3], uint8_t* inl) {
@@ -746,15 +1122,49 @@ int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int3
       ++n3;
     }
     uint8_t* in3 = (uint8_t*)calloc((size_t)n3 + 1, 1);
-    double t3[3];
-    const int c3 = given_rotation_3d3d(P, R, Pq, Pm, valid, n3, t3, in3);
-    res->stereo_inliers = c3;
-    if (mask)
-      for (int j = 0; j < n3; ++j)
-        if (in3[j]) mask[idx[j]] |= 2;
-    for (int i = 0; i < 9; ++i) res->T_query_match[i] = R[i];
-    for (int i = 0; i < 3; ++i) res->T_query_match[9 + i] = t3[i];
-    res->accepted = (c3 >= P->min_3d3d_inliers) ? 1 : 0;
+    if (P->pose_recovery_type == 1) {
+      /* PnP: query bearings vs match-frame points of the 2D-2D inliers with
+       * a valid stereo point, in pair-list order */
+      double* Fq = (double*)malloc(sizeof(double) * 3 * (n3 + 1));
+      double* Pw = (double*)malloc(sizeof(double) * 3 * (n3 + 1));
+      int32_t* id2 = (int32_t*)malloc(sizeof(int32_t) * (n3 + 1));
+      int n2 = 0;
+      for (int j = 0; j < n3; ++j) {
+        if (!valid[j]) continue;
+        const int pj = idx[j];
+        for (int c = 0; c < 3; ++c) {
+          Fq[3 * n2 + c] = F1[3 * pj + c];
+          Pw[3 * n2 + c] = Pm[3 * j + c];
+        }
+        id2[n2++] = pj;
+      }
+      double Ro[9], to[3];
+      int np = 0;
+      const int okp = ransac_pnp(P, Fq, Pw, n2, Ro, to, in3, &np);
+      res->pnp_inliers = okp ? np : 0;
+      if (okp) {
+        if (mask)
+          for (int j = 0; j < n2; ++j)
+            if (in3[j]) mask[id2[j]] |= 2;
+        /* camera pose (R_o, t_o) in the match frame -> T_query_match: p_q = R p_m + t */
+        for (int a = 0; a < 3; ++a)
+          for (int b = 0; b < 3; ++b) res->T_query_match[a * 3 + b] = Ro[b * 3 + a];
+        for (int a = 0; a < 3; ++a)
+          res->T_query_match[9 + a] = -(Ro[0 * 3 + a] * to[0] + Ro[1 * 3 + a] * to[1] + Ro[2 * 3 + a] * to[2]);
+      }
+      res->accepted = (okp && np >= P->min_2d3d_inliers) ? 1 : 0;
+      free(Fq); free(Pw); free(id2);
+    } else {
+      double t3[3];
+      const int c3 = given_rotation_3d3d(P, R, Pq, Pm, valid, n3, t3, in3);
+      res->stereo_inliers = c3;
+      if (mask)
+        for (int j = 0; j < n3; ++j)
+          if (in3[j]) mask[idx[j]] |= 2;
+      for (int i = 0; i < 9; ++i) res->T_query_match[i] = R[i];
+      for (int i = 0; i < 3; ++i) res->T_query_match[9 + i] = t3[i];
+      res->accepted = (c3 >= P->min_3d3d_inliers) ? 1 : 0;
+    }
     free(Pq); free(Pm); free(valid); free(idx); free(in3);
   } else if (ok) {
     for (int i = 0; i < 9; ++i) res->T_query_match[i] = R[i];

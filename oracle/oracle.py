@@ -288,6 +288,21 @@ def fivept(f1, f2):
     return Es[:n].reshape(-1, 3, 3)
 
 
+def epnp(pw, f):
+    """EPnP restatement (oracle/lcd_oracle.c orc_epnp): camera pose (R_wc, t_wc)
+    in the world frame of the points, or None."""
+    L = lib()
+    L.orc_epnp.argtypes = [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                           C.POINTER(C.c_double)]
+    L.orc_epnp.restype = C.c_int
+    pw = np.ascontiguousarray(pw, np.float64)
+    f = np.ascontiguousarray(f, np.float64)
+    R = np.empty((3, 3))
+    t = np.empty(3)
+    ok = L.orc_epnp(pw.shape[0], _f(pw), _f(f), _f(R), _f(t))
+    return (R, t) if ok else None
+
+
 def lcd_verify(params, pool, cand_query=None, cand_match=None, masks=True):
     from kmx.abi import LcdResult
     L = lib(); _lcd_setup(L)

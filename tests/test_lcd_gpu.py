@@ -30,11 +30,12 @@ def test_knn2_matches_oracle(gpu, norm):
         assert np.array_equal(gi, ref[:, 0]) and np.array_equal(gj, ref[:, 1]), (nq, nm)
 
 
-@pytest.mark.parametrize("variant,norm", [("gcc9", "l1"), ("gcc11", "hamming")])
-def test_verify_bit_exact(gpu, variant, norm):
+@pytest.mark.parametrize("variant,norm,recovery", [("gcc9", "l1", 0), ("gcc11", "hamming", 0), ("gcc9", "l1", 1)])
+def test_verify_bit_exact(gpu, variant, norm, recovery):
+    """recovery 0: 1-point 3D-3D (reference config); 1: EPnP RANSAC (LC4)."""
     from oracle import oracle as O
     pool = make_lcd_pool(24, 300, seed=3)
-    p = LcdParams(rng_variant=variant, norm=norm)
+    p = LcdParams(rng_variant=variant, norm=norm, pose_recovery_type=recovery)
     det = LoopClosureDetector(p)
     det.set_pool(pool)
     got, gm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)
@@ -42,8 +43,9 @@ def test_verify_bit_exact(gpu, variant, norm):
     for i in range(len(got)):
         r = ref[i]
         g = got[i]
-        assert (g["n_matches"], g["mono_inliers"], g["stereo_inliers"], g["accepted"], g["iterations_2d2d"]) == \
-            (r.n_matches, r.mono_inliers, r.stereo_inliers, bool(r.accepted), r.iterations_2d2d), i
+        assert (g["n_matches"], g["mono_inliers"], g["stereo_inliers"], g["pnp_inliers"], g["accepted"],
+                g["iterations_2d2d"]) == (r.n_matches, r.mono_inliers, r.stereo_inliers, r.pnp_inliers,
+                                          bool(r.accepted), r.iterations_2d2d), i
         assert np.array_equal(g["T_query_match"], np.array(r.T_query_match[:])), i
     assert np.array_equal(gm, rm)
     # planted loop closures are found, random pairs rejected

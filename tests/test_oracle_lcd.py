@@ -132,3 +132,33 @@ def test_verify_noise_free_pool():
             assert inl == true & {tuple(x) for x in pairs.tolist()}
         else:
             assert not r.accepted
+
+
+def test_epnp_recovers_camera_pose():
+    """EPnP restatement (LC4): noise-free correspondences give the exact camera
+    pose (R_wc, t_wc) for 6..40 points."""
+    rng = np.random.default_rng(0)
+    for trial in range(100):
+        R = _expm_so3(rng.normal(0, 0.5, (1, 3)))[0]
+        t = rng.normal(0, 1, 3)
+        n = int(rng.integers(6, 40))
+        pc = np.c_[rng.uniform(-3, 3, (n, 2)), rng.uniform(2, 15, n)]  # camera frame
+        pw = (pc - t) @ R  # pc = R pw + t
+        Rwc, twc = O.epnp(pw, pc / np.linalg.norm(pc, axis=1, keepdims=True))
+        assert np.abs(Rwc - R.T).max() < 1e-9 and np.abs(twc + R.T @ t).max() < 1e-8, trial
+
+
+def test_verify_pnp_noise_free_pool():
+    pool = make_lcd_pool(12, 200, noise_free=True, seed=4)
+    p = LcdParams(pose_recovery_type=1).to_c()
+    res, masks = O.lcd_verify(p, pool)
+    for c in range(len(res)):
+        r = res[c]
+        if c % 2 == 0:
+            assert r.accepted and r.pnp_inliers >= 90 and r.stereo_inliers == 0
+            T = np.array(r.T_query_match[:])
+            assert np.abs(T[:9].reshape(3, 3) - pool.R_qm[c // 2]).max() < 1e-9
+            assert np.abs(T[9:] - pool.t_qm[c // 2]).max() < 1e-8
+            assert np.count_nonzero(masks[c] & 2) == r.pnp_inliers
+        else:
+            assert not r.accepted
