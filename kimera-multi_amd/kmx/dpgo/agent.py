@@ -151,9 +151,13 @@ class PGOAgent:
             ts[i + 1] = ts[i] + Rs[i] @ m.t
         return Rs, ts
 
-    def initialize(self, TInit=None):
+    def initialize(self, TInit=None, neighbor_global_poses=None):
         """INITIALIZE: build the local problem and the initial lifted iterate.
-        TInit: dpgo PoseArray (d x (d+1)n) or [n, 3, 4]; default: odometry chain."""
+        TInit: dpgo PoseArray (d x (d+1)n) or [n, 3, 4]; default: odometry chain.
+        neighbor_global_poses: {(robot, pose): (R, t)} of neighbours already in
+        the global frame -> the local trajectory is aligned to it by robust
+        single-pose averaging over the shared loop closures (kmx.dpgo.init;
+        drawio:2271-2307). Robot 0 defines the global frame."""
         if self.state == PGOAgentState.WAIT_FOR_DATA:
             raise ValueError("no measurements")
         if self.YLift is None:
@@ -194,6 +198,14 @@ class PGOAgent:
             if T.shape == (self.d, (self.d + 1) * self.n):
                 T = T.reshape(self.d, self.n, self.d + 1).transpose(1, 0, 2)
             Rs, ts = T[:, :, :3], T[:, :, 3]
+        self.alignment = None
+        if neighbor_global_poses and self.mID != 0:
+            from .init import align_to_world, transform_trajectory
+            out = align_to_world(self.shared_lcs, self.mID, Rs, ts, neighbor_global_poses)
+            if out is not None:
+                R_WA, t_WA, w = out
+                Rs, ts = transform_trajectory(R_WA, t_WA, Rs, ts)
+                self.alignment = (R_WA, t_WA, w)
         self.solver.set_iterate(self.mID, lift(Rs, ts, self.YLift))
         self._apply_missing_neighbours()
         self.iteration = 0

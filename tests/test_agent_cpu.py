@@ -117,3 +117,25 @@ def test_agent_states_outputs_and_reset():
     assert st.agentID == 1 and st.iterationNumber == 5
     ag.reset()
     assert ag.getState() == PGOAgentState.WAIT_FOR_DATA and ag.instance_number() == 1
+
+
+def test_agent_initialize_in_global_frame():
+    """Robot 1 aligns its odometry-chain initialisation to robot 0's global
+    frame through the shared loop closures (row f4)."""
+    g = make_pose_graph(2, 400, 1200, outlier_frac=0.2, f_inter=0.3, noise_free=True, seed=9)
+    P = PGOAgentParameters(r=5)
+    Y = lifting_matrix(5)
+    a0 = PGOAgent(0, P, solver=OracleBlockSolver(P))
+    a1 = PGOAgent(1, P, solver=OracleBlockSolver(P))
+    for ag in (a0, a1):
+        for m in _measurements(g, ag.getID()):
+            ag.addMeasurement(m)
+        ag.setLiftingMatrix(Y)
+    T0 = np.concatenate([g.gt_R[0], g.gt_t[0][:, :, None]], axis=2)
+    a0.initialize(T0)
+    world = {(0, i): (g.gt_R[0][i], g.gt_t[0][i]) for i in range(int(g.n_poses[0]))}
+    a1.initialize(neighbor_global_poses=world)
+    X = a1.getX()
+    Rw = np.einsum("ab,nac->nbc", Y, X[:, :, :3])
+    assert np.abs(Rw - g.gt_R[1]).max() < 1e-8
+    assert a1.alignment is not None and 0 < a1.alignment[2].sum() < len(a1.alignment[2])
