@@ -27,6 +27,7 @@
 #include <cfloat>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -248,6 +249,28 @@ __device__ int sign_changes(const double S[11][11], const int* sd, int ns, doubl
   return ch;
 }
 
+constexpr int RR_SPLIT = 64, RR_DEPTH = 12;
+
+// Safeguarded Newton on an isolating interval (oracle refine_root).
+__device__ double refine_root(const double* c, int deg, double a, double b) {
+  double dc[10];
+  for (int i = 0; i < deg; ++i) dc[i] = (double)(i + 1) * c[i + 1];
+  double fa = poly_eval(c, deg, a);
+  double x = 0.5 * (a + b);
+  for (int it = 0; it < 60; ++it) {
+    const double fx = poly_eval(c, deg, x);
+    if (fx == 0.0) return x;
+    if ((fx < 0.0) == (fa < 0.0)) { a = x; fa = fx; }
+    else b = x;
+    const double dfx = poly_eval(dc, deg - 1, x);
+    double xn = (dfx != 0.0) ? x - fx / dfx : 0.5 * (a + b);
+    if (!(xn > a && xn < b)) xn = 0.5 * (a + b);
+    if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;
+    x = xn;
+  }
+  return x;
+}
+
 __device__ int real_roots(const double* coef, int deg_in, double* roots) {
   int deg = deg_in;
   while (deg > 0 && coef[deg] == 0.0) --deg;
@@ -279,8 +302,11 @@ __device__ int real_roots(const double* coef, int deg_in, double* roots) {
   double bound = 0.0;
   for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(S[0][i]));
   bound += 1.0;
-  double st_lo[64], st_hi[64];
-  int st_vl[64], st_vh[64], st_d[64];
+  // 64-ary isolation / refinement, the oracle's sequence of points
+  // (oracle/lcd_oracle.c real_roots); k_ransac_coop evaluates a level's 63
+  // points in one wavefront. At most deg intervals with roots are alive.
+  double st_lo[16], st_hi[16];
+  int st_vl[16], st_vh[16], st_d[16];
   int sp = 0, nr = 0;
   const int vlo = sign_changes(S, sd, ns, -bound);
   const int vhi = sign_changes(S, sd, ns, bound);
@@ -291,24 +317,21 @@ __device__ int real_roots(const double* coef, int deg_in, double* roots) {
     const int vl = st_vl[sp], vh = st_vh[sp], dep = st_d[sp];
     const int cnt = vl - vh;
     if (cnt <= 0) continue;
-    if (cnt == 1 || dep >= 50) {
-      double a = lo, b = hi;
-      double fa = poly_eval(S[0], deg, a);
-      for (int it = 0; it < 80; ++it) {
-        const double mid = 0.5 * (a + b);
-        const double fm = poly_eval(S[0], deg, mid);
-        if (fm == 0.0) { a = b = mid; break; }
-        if ((fm < 0.0) == (fa < 0.0)) { a = mid; fa = fm; }
-        else b = mid;
-      }
-      if (nr < 10) roots[nr++] = 0.5 * (a + b);
+    if (cnt == 1 || dep >= RR_DEPTH) {
+      if (nr < 10) roots[nr++] = refine_root(S[0], deg, lo, hi);
       continue;
     }
-    const double mid = 0.5 * (lo + hi);
-    const int vm = sign_changes(S, sd, ns, mid);
-    if (sp + 2 <= 64) {
-      st_lo[sp] = mid; st_hi[sp] = hi; st_vl[sp] = vm; st_vh[sp] = vh; st_d[sp] = dep + 1; ++sp;
-      st_lo[sp] = lo; st_hi[sp] = mid; st_vl[sp] = vl; st_vh[sp] = vm; st_d[sp] = dep + 1; ++sp;
+    const double w = (hi - lo) / RR_SPLIT;
+    int vprev = vh;
+    double xprev = hi;
+    for (int j = RR_SPLIT - 1; j >= 0; --j) {
+      const double xj = (j == 0) ? lo : lo + (double)j * w;
+      const int vj = (j == 0) ? vl : sign_changes(S, sd, ns, xj);
+      if (vj - vprev > 0 && sp < 16) {
+        st_lo[sp] = xj; st_hi[sp] = xprev; st_vl[sp] = vj; st_vh[sp] = vprev; st_d[sp] = dep + 1; ++sp;
+      }
+      vprev = vj;
+      xprev = xj;
     }
   }
   for (int a = 0; a < nr; ++a)
@@ -797,13 +820,675 @@ struct RsParams {
   double thr2d, thr3d, prob;
   int max_iter, min2d, min3d, pmax;
   int pnp;  // pose_recovery_type 1: k_ransac stops after 2D-2D, k_pnp recovers the pose
+  int prof; // diagnostic phase timers (k_ransac_coop)
 };
 struct PnpParams {
   double thr, prob;
   int max_iter, min2d, min_pnp, pmax;
 };
 
-__global__ __launch_bounds__(RS_BLOCK) void k_ransac(const double* bearings, const double* points, int N,
+// ---------------------------------------------- cooperative 2D-2D RANSAC --
+// k_ransac_coop: one wavefront per candidate, one hypothesis at a time with
+// all 64 lanes cooperating on the 5-point solve (LDS workspace, ~6 KB), so
+// no lane holds the 10x20 system or the Sturm sequence in registers (the
+// lane-per-hypothesis k_ransac spills 4.9 KB/lane to scratch at 1 wave/SIMD).
+// Every element is computed with the same operations in the same order as
+// the serial code (oracle/lcd_oracle.c), so models, inlier sets and iteration
+// counts stay bit-identical; hypotheses run in the serial loop's order, so no
+// work is spent past the adaptive iteration count.
+struct CoopWS {
+  double f1[15], f2[15];
+  double N[4][9];             // null space (until the essentials are formed)
+  union {
+    struct {                  // nullspace + system construction
+      double vs[5][9];
+      double QA[9][5];
+      double c2[3][10];
+      double EEt[9][10];
+      double tr[10];
+    };
+    struct {                  // roots
+      double S[11][11];
+      double val[RR_SPLIT];
+      double st_lo[16], st_hi[16];
+      int st_vl[16], st_vh[16], st_d[16];
+      int sd[11];
+      int vi[RR_SPLIT];
+    };
+  };
+  union {
+    struct {                  // system + elimination
+      double A[10][20];
+      double fk[10];
+    };
+    struct {                  // models (A is dead once Bp is extracted)
+      double Es[10][9];
+      double berr[10];
+      double bR[10][9], bt[10][3];
+    };
+  };
+  double Bp[3][3][5];
+  double nco[11];
+  double roots[10];
+  double iv_lo[10], iv_hi[10];  // isolating intervals
+  double mR[9], mt[3];       // model of the current hypothesis
+  double bestm[12];          // best model so far
+  int ns, deg, nr, ne, sp, ok, bfound;
+};
+
+__device__ __forceinline__ void wsync() { __syncthreads(); }  // the block is one wavefront
+
+// nullspace_5x9 (Householder QR of Q^T, lane 0) + the 4 back-substitutions (lanes 0-3)
+__device__ void coop_nullspace(CoopWS& w, int lane) {
+  if (lane == 0) {
+    for (int i = 0; i < 9; ++i)
+      for (int j = 0; j < 5; ++j) w.QA[i][j] = w.f1[3 * j + i / 3] * w.f2[3 * j + i % 3];
+    for (int k = 0; k < 5; ++k) {
+      double nx = 0.0;
+      for (int i = k; i < 9; ++i) nx += w.QA[i][k] * w.QA[i][k];
+      nx = sqrt(nx);
+      const double alpha = (w.QA[k][k] >= 0.0) ? -nx : nx;
+      double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (int i = k; i < 9; ++i) v[i] = w.QA[i][k];
+      v[k] -= alpha;
+      double nv = 0.0;
+      for (int i = k; i < 9; ++i) nv += v[i] * v[i];
+      nv = sqrt(nv);
+      for (int i = 0; i < 9; ++i) w.vs[k][i] = (nv > 0.0 && i >= k) ? v[i] / nv : 0.0;
+      for (int j = k; j < 5; ++j) {
+        double d = 0.0;
+        for (int i = k; i < 9; ++i) d += w.vs[k][i] * w.QA[i][j];
+        for (int i = k; i < 9; ++i) w.QA[i][j] -= 2.0 * w.vs[k][i] * d;
+      }
+    }
+  }
+  wsync();
+  if (lane < 4) {
+    double x[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    x[5 + lane] = 1.0;
+    for (int k = 4; k >= 0; --k) {
+      double d = 0.0;
+      for (int i = k; i < 9; ++i) d += w.vs[k][i] * x[i];
+      for (int i = k; i < 9; ++i) x[i] -= 2.0 * w.vs[k][i] * d;
+    }
+    for (int i = 0; i < 9; ++i) w.N[lane][i] = x[i];
+  }
+  wsync();
+}
+
+// E[e][c] = N[c][e]. Coefficient k of mul11(a, b) / mul21(a, b): its terms in
+// the serial loop's (i, j) order (T11 / T21 list them), summed from 0.0.
+__constant__ signed char T11[10][2][2] = {{{0, 0}, {-1, -1}}, {{0, 1}, {1, 0}}, {{0, 2}, {2, 0}}, {{1, 1}, {-1, -1}},
+                                          {{1, 2}, {2, 1}}, {{2, 2}, {-1, -1}}, {{0, 3}, {3, 0}}, {{1, 3}, {3, 1}},
+                                          {{2, 3}, {3, 2}}, {{3, 3}, {-1, -1}}};
+__constant__ signed char T21[20][3][2] = {
+    {{0, 0}, {-1, -1}, {-1, -1}}, {{3, 1}, {-1, -1}, {-1, -1}}, {{0, 1}, {1, 0}, {-1, -1}},
+    {{1, 1}, {3, 0}, {-1, -1}},   {{0, 2}, {2, 0}, {-1, -1}},   {{0, 3}, {6, 0}, {-1, -1}},
+    {{3, 2}, {4, 1}, {-1, -1}},   {{3, 3}, {7, 1}, {-1, -1}},   {{1, 2}, {2, 1}, {4, 0}},
+    {{1, 3}, {6, 1}, {7, 0}},     {{2, 2}, {5, 0}, {-1, -1}},   {{2, 3}, {6, 2}, {8, 0}},
+    {{6, 3}, {9, 0}, {-1, -1}},   {{4, 2}, {5, 1}, {-1, -1}},   {{4, 3}, {7, 2}, {8, 1}},
+    {{7, 3}, {9, 1}, {-1, -1}},   {{5, 2}, {-1, -1}, {-1, -1}}, {{5, 3}, {8, 2}, {-1, -1}},
+    {{8, 3}, {9, 2}, {-1, -1}},   {{9, 3}, {-1, -1}, {-1, -1}}};
+__device__ __forceinline__ double mul11_k(const double* a, const double* b, int k) {
+  double s = 0.0;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int i = T11[k][t][0];
+    if (i >= 0) s += a[i] * b[T11[k][t][1]];
+  }
+  return s;
+}
+__device__ __forceinline__ double mul21_k(const double* a, const double* b, int k) {
+  double s = 0.0;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int i = T21[k][t][0];
+    if (i >= 0) s += a[i] * b[T21[k][t][1]];
+  }
+  return s;
+}
+
+// row 9 (det E = 0): c2_q = mul11(E[C2P[q][0]], E[C2P[q][1]]) - mul11(E[C2P[q][2]], E[C2P[q][3]])
+__constant__ int C2P[3][4] = {{4, 8, 5, 7}, {3, 8, 5, 6}, {3, 7, 4, 6}};
+
+__device__ void coop_system(CoopWS& w, int lane) {
+  // E as [9][4] rows: E_e[c] = N[c][e]
+  auto Erow = [&](int e, double* out) {
+    for (int c = 0; c < 4; ++c) out[c] = w.N[c][e];
+  };
+  // EEt[ij][k] = sum_l mul11(E[i*3+l], E[j*3+l])[k] (l = 0, 1, 2 in order); c2 for row 9
+  for (int t = lane; t < 90 + 30; t += 64) {
+    if (t < 90) {
+      const int ij = t / 10, k = t % 10, i = ij / 3, j = ij % 3;
+      double acc = 0.0;
+      for (int l = 0; l < 3; ++l) {
+        double a[4], b[4];
+        Erow(i * 3 + l, a);
+        Erow(j * 3 + l, b);
+        acc += mul11_k(a, b, k);
+      }
+      w.EEt[ij][k] = acc;
+    } else {
+      const int q = (t - 90) / 10, k = (t - 90) % 10;  // q: 0 -> (4,8)-(5,7), 1 -> (3,8)-(5,6), 2 -> (3,7)-(4,6)
+      double a[4], b[4], c[4], d[4];
+      Erow(C2P[q][0], a); Erow(C2P[q][1], b); Erow(C2P[q][2], c); Erow(C2P[q][3], d);
+      w.c2[q][k] = mul11_k(a, b, k) - mul11_k(c, d, k);
+    }
+  }
+  wsync();
+  if (lane < 10) w.tr[lane] = w.EEt[0][lane] + w.EEt[4][lane] + w.EEt[8][lane];
+  wsync();
+  // rows 0..8: r[k] = sum_l 2 mul21(EEt[i*3+l], E[l*3+j])[k] - mul21(tr, E[ij])[k]; row 9
+  for (int t = lane; t < 200; t += 64) {
+    const int row = t / 20, k = t % 20;
+    double r = 0.0;
+    if (row < 9) {
+      const int i = row / 3, j = row % 3;
+      for (int l = 0; l < 3; ++l) {
+        double b[4];
+        Erow(l * 3 + j, b);
+        r += 2.0 * mul21_k(w.EEt[i * 3 + l], b, k);
+      }
+      double b[4];
+      Erow(row, b);
+      r -= mul21_k(w.tr, b, k);
+    } else {
+      double b0[4], b1[4], b2[4];
+      Erow(0, b0); Erow(1, b1); Erow(2, b2);
+      r += mul21_k(w.c2[0], b0, k);
+      r -= mul21_k(w.c2[1], b1, k);
+      r += mul21_k(w.c2[2], b2, k);
+    }
+    w.A[row][k] = r;
+  }
+  wsync();
+}
+
+// Gauss-Jordan with partial pivoting on the 10x20 system (serial order per
+// element; lanes own columns). Returns 0 on a zero pivot.
+__device__ int coop_gj(CoopWS& w, int lane) {
+  for (int k = 0; k < 10; ++k) {
+    int p = k;
+    for (int i = k + 1; i < 10; ++i)
+      if (fabs(w.A[i][k]) > fabs(w.A[p][k])) p = i;
+    if (w.A[p][k] == 0.0) return 0;  // uniform
+    if (p != k && lane < 20) {
+      const double t = w.A[k][lane]; w.A[k][lane] = w.A[p][lane]; w.A[p][lane] = t;
+    }
+    wsync();
+    const double inv = 1.0 / w.A[k][k];
+    wsync();
+    if (lane < 20) w.A[k][lane] *= inv;
+    if (lane < 10) w.fk[lane] = w.A[lane][k];
+    wsync();
+    if (lane < 20)
+      for (int i = 0; i < 10; ++i) {
+        if (i == k) continue;
+        const double f = (i < 10) ? w.fk[i] : 0.0;
+        if (f == 0.0) continue;
+        w.A[i][lane] -= f * w.A[k][lane];
+      }
+    wsync();
+  }
+  return 1;
+}
+
+__device__ int coop_sign_changes(const CoopWS& w, double z) {
+  int ch = 0;
+  double prev = 0.0;
+  for (int s = 0; s < w.ns; ++s) {
+    const double v = poly_eval(w.S[s], w.sd[s], z);
+    if (v != 0.0) {
+      if (prev != 0.0 && ((v < 0.0) != (prev < 0.0))) ++ch;
+      prev = v;
+    }
+  }
+  return ch;
+}
+
+// Bp, the degree-10 polynomial, its Sturm sequence (lane 0); then the 64-ary
+// isolation / refinement with one point per lane. Leaves w.nr sorted roots.
+__device__ void coop_roots(CoopWS& w, int lane) {
+  if (lane == 0) {
+    for (int q = 0; q < 3; ++q) {
+      const double* e = &w.A[4 + 2 * q][10];
+      const double* f = &w.A[5 + 2 * q][10];
+      double* px = w.Bp[q][0];
+      double* py = w.Bp[q][1];
+      double* pc = w.Bp[q][2];
+      px[0] = e[2]; px[1] = e[1] - f[2]; px[2] = e[0] - f[1]; px[3] = -f[0]; px[4] = 0.0;
+      py[0] = e[5]; py[1] = e[4] - f[5]; py[2] = e[3] - f[4]; py[3] = -f[3]; py[4] = 0.0;
+      pc[0] = e[9]; pc[1] = e[8] - f[9]; pc[2] = e[7] - f[8]; pc[3] = e[6] - f[7]; pc[4] = -f[6];
+    }
+    double c1[8], c2[8], c3[8], t1[8], t2[8];
+    pmul(w.Bp[1][1], 3, w.Bp[2][2], 4, t1); pmul(w.Bp[1][2], 4, w.Bp[2][1], 3, t2);
+    for (int i = 0; i < 8; ++i) c1[i] = t1[i] - t2[i];
+    pmul(w.Bp[1][0], 3, w.Bp[2][2], 4, t1); pmul(w.Bp[1][2], 4, w.Bp[2][0], 3, t2);
+    for (int i = 0; i < 8; ++i) c2[i] = t1[i] - t2[i];
+    pmul(w.Bp[1][0], 3, w.Bp[2][1], 3, t1); pmul(w.Bp[1][1], 3, w.Bp[2][0], 3, t2);
+    for (int i = 0; i < 7; ++i) c3[i] = t1[i] - t2[i];
+    c3[7] = 0.0;
+    double u1[11], u2[11], u3[11];
+    pmul(w.Bp[0][0], 3, c1, 7, u1);
+    pmul(w.Bp[0][1], 3, c2, 7, u2);
+    pmul(w.Bp[0][2], 4, c3, 6, u3);
+    for (int i = 0; i < 11; ++i) w.nco[i] = u1[i] - u2[i] + u3[i];
+    // Sturm sequence (same construction as real_roots)
+    int deg = 10;
+    while (deg > 0 && w.nco[deg] == 0.0) --deg;
+    w.deg = deg;
+    w.nr = 0;
+    w.ns = 0;
+    if (deg > 0) {
+      for (int i = 0; i <= deg; ++i) w.S[0][i] = w.nco[i] / w.nco[deg];
+      w.sd[0] = deg;
+      for (int i = 0; i < deg; ++i) w.S[1][i] = (double)(i + 1) * w.S[0][i + 1];
+      w.sd[1] = deg - 1;
+      int ns = 2;
+      while (w.sd[ns - 1] > 0 && ns < 11) {
+        double r[11];
+        const int da = w.sd[ns - 2], db = w.sd[ns - 1];
+        for (int i = 0; i <= da; ++i) r[i] = w.S[ns - 2][i];
+        for (int k = da - db; k >= 0; --k) {
+          const double f = r[k + db] / w.S[ns - 1][db];
+          for (int i = 0; i <= db; ++i) r[k + i] -= f * w.S[ns - 1][i];
+        }
+        int dr = db - 1;
+        double mx = 0.0;
+        for (int i = 0; i <= da; ++i) mx = fmax(mx, fabs(w.S[ns - 2][i]));
+        while (dr >= 0 && fabs(r[dr]) <= 1e-14 * mx) --dr;
+        if (dr < 0) break;
+        for (int i = 0; i <= dr; ++i) w.S[ns][i] = -r[i];
+        w.sd[ns] = dr;
+        ++ns;
+      }
+      w.ns = ns;
+      double bound = 0.0;
+      for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(w.S[0][i]));
+      bound += 1.0;
+      w.st_lo[0] = -bound; w.st_hi[0] = bound; w.st_d[0] = 0;
+      w.st_vl[0] = coop_sign_changes(w, -bound);
+      w.st_vh[0] = coop_sign_changes(w, bound);
+      w.sp = 1;
+    } else {
+      w.sp = 0;
+    }
+  }
+  wsync();
+  const int deg = w.deg;
+  while (w.sp > 0) {  // uniform: the stack lives in LDS
+    const int sp = w.sp - 1;
+    const double lo = w.st_lo[sp], hi = w.st_hi[sp];
+    const int vl = w.st_vl[sp], vh = w.st_vh[sp], dep = w.st_d[sp];
+    const int cnt = vl - vh;
+    wsync();
+    if (lane == 0) w.sp = sp;
+    wsync();
+    if (cnt <= 0) continue;
+    if (cnt == 1 || dep >= RR_DEPTH) {  // isolated: refined below, one lane per root
+      if (lane == 0 && w.nr < 10) {
+        w.iv_lo[w.nr] = lo;
+        w.iv_hi[w.nr] = hi;
+        ++w.nr;
+      }
+      wsync();
+      continue;
+    }
+    const double wd = (hi - lo) / RR_SPLIT;
+    if (lane >= 1) {
+      const double x = lo + (double)lane * wd;
+      w.val[lane] = x;
+      w.vi[lane] = coop_sign_changes(w, x);
+    } else {
+      w.val[0] = lo;
+      w.vi[0] = vl;
+    }
+    wsync();
+    if (lane == 0) {  // push pieces right to left (popped in increasing x)
+      int vprev = vh;
+      double xprev = hi;
+      int spn = w.sp;
+      for (int j = RR_SPLIT - 1; j >= 0; --j) {
+        const double xj = w.val[j];
+        const int vj = w.vi[j];
+        if (vj - vprev > 0 && spn < 16) {
+          w.st_lo[spn] = xj; w.st_hi[spn] = xprev; w.st_vl[spn] = vj; w.st_vh[spn] = vprev; w.st_d[spn] = dep + 1;
+          ++spn;
+        }
+        vprev = vj;
+        xprev = xj;
+      }
+      w.sp = spn;
+    }
+    wsync();
+  }
+  if (lane < w.nr) w.roots[lane] = refine_root(w.S[0], deg, w.iv_lo[lane], w.iv_hi[lane]);
+  wsync();
+  if (lane == 0) {  // ascending order
+    for (int a = 0; a < w.nr; ++a)
+      for (int b = 0; b + 1 < w.nr - a; ++b)
+        if (w.roots[b] > w.roots[b + 1]) { const double t = w.roots[b]; w.roots[b] = w.roots[b + 1]; w.roots[b + 1] = t; }
+  }
+  wsync();
+}
+
+// Essential matrices from the roots (lane per root), then per E (lane per E)
+// the 4 decompositions scored on the sample; the first minimum in (E, cand)
+// order wins, as in model_from_sample. Result in w.mR / w.mt, w.ok.
+__device__ void coop_models(CoopWS& w, int lane) {
+  const int nr = w.nr;
+  int ok_root = 0;
+  double Eo[9];
+  if (lane < nr) {
+    const double z = w.roots[lane];
+    double row[3][3];
+    for (int q = 0; q < 3; ++q)
+      for (int c = 0; c < 3; ++c) row[q][c] = poly_eval(w.Bp[q][c], c == 2 ? 4 : 3, z);
+    double v[3];
+    cross3(row[0], row[1], v);
+    if (v[2] != 0.0) {
+      const double x = v[0] / v[2], y = v[1] / v[2];
+      double nn = 0.0;
+      for (int e = 0; e < 9; ++e) {
+        Eo[e] = x * w.N[0][e] + y * w.N[1][e] + z * w.N[2][e] + w.N[3][e];
+        nn += Eo[e] * Eo[e];
+      }
+      nn = sqrt(nn);
+      if (nn > 0.0) {
+        for (int e = 0; e < 9; ++e) Eo[e] /= nn;
+        ok_root = 1;
+      }
+    }
+  }
+  // compact the surviving roots in root order (fivept_nister's ns counter)
+  const unsigned long long m = __ballot(ok_root);
+  const int slot = __popcll(m & ((1ull << lane) - 1ull));
+  if (ok_root)
+    for (int e = 0; e < 9; ++e) w.Es[slot][e] = Eo[e];
+  const int ne = __popcll(m);
+  wsync();
+  double best = DBL_MAX;
+  if (lane < ne) {
+    double U[9], s[3], V[9];
+    svd3(w.Es[lane], U, s, V);
+    double Ra[9], Rb[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        const double uw0 = U[i * 3 + 1], uw1 = -U[i * 3 + 0], uw2 = U[i * 3 + 2];
+        Ra[i * 3 + j] = uw0 * V[j * 3 + 0] + uw1 * V[j * 3 + 1] + uw2 * V[j * 3 + 2];
+        const double uv0 = -U[i * 3 + 1], uv1 = U[i * 3 + 0], uv2 = U[i * 3 + 2];
+        Rb[i * 3 + j] = uv0 * V[j * 3 + 0] + uv1 * V[j * 3 + 1] + uv2 * V[j * 3 + 2];
+      }
+    if (det3(Ra) < 0.0)
+      for (int i = 0; i < 9; ++i) Ra[i] = -Ra[i];
+    if (det3(Rb) < 0.0)
+      for (int i = 0; i < 9; ++i) Rb[i] = -Rb[i];
+    const double tu[3] = {U[0 * 3 + 2], U[1 * 3 + 2], U[2 * 3 + 2]};
+    for (int cand = 0; cand < 4; ++cand) {
+      const double* Rc = (cand < 2) ? Ra : Rb;
+      const double sg = (cand & 1) ? -1.0 : 1.0;
+      const double tc[3] = {sg * tu[0], sg * tu[1], sg * tu[2]};
+      double err = 0.0;
+      for (int i = 0; i < 5; ++i) err += model_error(Rc, tc, w.f1 + 3 * i, w.f2 + 3 * i);
+      if (err < best) {
+        best = err;
+        for (int i = 0; i < 9; ++i) w.bR[lane][i] = Rc[i];
+        for (int i = 0; i < 3; ++i) w.bt[lane][i] = tc[i];
+      }
+    }
+    w.berr[lane] = best;
+  }
+  wsync();
+  if (lane == 0) {
+    int win = -1;
+    double bb = DBL_MAX;
+    for (int e = 0; e < ne; ++e)
+      if (w.berr[e] < bb) { bb = w.berr[e]; win = e; }
+    w.ok = (win >= 0) ? 1 : 0;
+    if (win >= 0) {
+      for (int i = 0; i < 9; ++i) w.mR[i] = w.bR[win][i];
+      for (int i = 0; i < 3; ++i) w.mt[i] = w.bt[win][i];
+    }
+  }
+  wsync();
+}
+
+// Diagnostic phase timers (kmx_lcd_debug_phase_times): cycles per phase summed
+// over the first 64 candidates' hypotheses.
+__device__ unsigned long long g_phase[16];
+#define KMX_PT(i)                                                              \
+  do {                                                                         \
+    if (prof && lane == 0) {                                                   \
+      const unsigned long long t_ = wall_clock64();                            \
+      atomicAdd(&g_phase[i], t_ - t_prev);                                     \
+      t_prev = t_;                                                             \
+    }                                                                          \
+  } while (0)
+
+// One hypothesis: sample -> models (w.ok, w.mR, w.mt).
+__device__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const double* F2, const short* smp,
+                                bool prof) {
+  unsigned long long t_prev = prof ? wall_clock64() : 0;
+  if (lane < 15) {
+    const int i = lane / 3, c = lane % 3;
+    w.f1[lane] = F1[3 * smp[i] + c];
+    w.f2[lane] = F2[3 * smp[i] + c];
+  }
+  wsync();
+  KMX_PT(0);
+  coop_nullspace(w, lane);
+  KMX_PT(1);
+  coop_system(w, lane);
+  KMX_PT(2);
+  if (!coop_gj(w, lane)) {
+    if (lane == 0) w.ok = 0;
+    wsync();
+    return;
+  }
+  KMX_PT(3);
+  coop_roots(w, lane);
+  KMX_PT(4);
+  if (w.nr == 0) {
+    if (lane == 0) w.ok = 0;
+    wsync();
+    return;
+  }
+  coop_models(w, lane);
+  KMX_PT(5);
+}
+
+template <int LB>
+__global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bearings, const double* points, int N,
+                                                          const int* cq, const int* cm, const int2* pairs,
+                                                          const int* Kin, const short* table, RsParams P,
+                                                          kmx_lcd_result* res, unsigned char* masks,
+                                                          double* fbuf) {
+  __shared__ CoopWS w;
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int K = Kin[c];
+  const int q = cq[c], m = cm[c];
+  unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
+  kmx_lcd_result* R_ = res + c;
+  for (int j = lane; j < N && mask; j += RS_BLOCK) mask[j] = 0;
+  if (K < 5) {
+    if (lane == 0) {
+      kmx_lcd_result r = {};
+      r.n_matches = K;
+      *R_ = r;
+    }
+    return;
+  }
+  // compact bearings of the match pairs (global scratch, L1/L2 resident)
+  double* F1 = fbuf + (size_t)c * 6 * N;
+  double* F2 = F1 + 3 * N;
+  const int2* pl = pairs + (size_t)c * N;
+  for (int j = lane; j < K; j += RS_BLOCK) {
+    const int2 pr = pl[j];
+    for (int k = 0; k < 3; ++k) {
+      F1[3 * j + k] = bearings[((size_t)q * N + pr.x) * 3 + k];
+      F2[3 * j + k] = bearings[((size_t)m * N + pr.y) * 3 + k];
+    }
+  }
+  __threadfence_block();
+  wsync();
+  int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
+  double kk = 1.0;
+  const int max_skip = P.max_iter * 10;
+  const short* tab = table + (size_t)(K - 5) * P.pmax * 5;
+  for (int p = 0; p < P.pmax; ++p) {
+    if (!(iterations < kk && skipped < max_skip)) break;  // uniform
+    const bool prof = (c < 64) && P.prof;
+    unsigned long long t_prev = prof ? wall_clock64() : 0;
+    coop_hypothesis(w, lane, F1, F2, tab + (size_t)p * 5, prof);
+    if (prof && lane == 0) t_prev = wall_clock64();
+    if (!w.ok) {
+      ++skipped;
+      wsync();
+      continue;
+    }
+    double Rm[9], tm[3];
+    for (int i = 0; i < 9; ++i) Rm[i] = w.mR[i];
+    for (int i = 0; i < 3; ++i) tm[i] = w.mt[i];
+    int cnt = 0;
+    for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
+      const int j = j0 + lane;
+      const bool in = (j < K) && model_error(Rm, tm, F1 + 3 * j, F2 + 3 * j) < P.thr2d;
+      cnt += __popcll(__ballot(in));
+    }
+    KMX_PT(6);
+    if (cnt > best_cnt) {
+      best_cnt = cnt;
+      if (lane == 0) {
+        for (int i = 0; i < 9; ++i) w.bestm[i] = Rm[i];
+        for (int i = 0; i < 3; ++i) w.bestm[9 + i] = tm[i];
+      }
+      have = 1;
+      const double wr = (double)cnt / (double)K;
+      double p_no = 1.0 - pow(wr, 5.0);
+      p_no = fmax(DBL_EPSILON, p_no);
+      p_no = fmin(1.0 - DBL_EPSILON, p_no);
+      kk = log(1.0 - P.prob) / log(p_no);
+    }
+    ++iterations;
+    wsync();
+    if (iterations > P.max_iter) break;
+  }
+  if (!have) {
+    if (lane == 0) {
+      kmx_lcd_result r = {};
+      r.n_matches = K;
+      r.iterations_2d2d = iterations;
+      *R_ = r;
+    }
+    return;
+  }
+  double Rb[9], tb[3];
+  for (int i = 0; i < 9; ++i) Rb[i] = w.bestm[i];
+  for (int i = 0; i < 3; ++i) tb[i] = w.bestm[9 + i];
+  int n_in = 0;
+  for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
+    const int j = j0 + lane;
+    const bool in = (j < K) && model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d;
+    if (j < K && mask) mask[j] = in ? 1 : 0;
+    n_in += __popcll(__ballot(in));
+  }
+  kmx_lcd_result r = {};
+  r.n_matches = K;
+  r.mono_inliers = n_in;
+  r.iterations_2d2d = iterations;
+  for (int i = 0; i < 9; ++i) r.T_query_match[i] = Rb[i];
+  for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = tb[i];
+  if (n_in < P.min2d) {
+    if (lane == 0) *R_ = r;
+    return;
+  }
+  if (P.pnp) {
+    if (lane == 0) {
+      for (int i = 0; i < 12; ++i) r.T_query_match[i] = 0.0;
+      *R_ = r;
+    }
+    return;
+  }
+  // 1-point 3D-3D given the rotation over the 2D-2D inliers (pair order):
+  // T_j = p_q - R p_m; the largest consistent set (ties: smallest index)
+  // reuses F2's scratch slot for T and the workspace for the index list.
+  double* T = F2;
+  wsync();
+  int n3 = 0;
+  for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {  // compact inlier positions in pair order
+    const int j = j0 + lane;
+    const bool in = (j < K) && model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d;
+    const unsigned long long bm = __ballot(in);
+    const int pos = n3 + __popcll(bm & ((1ull << lane) - 1ull));
+    if (in) reinterpret_cast<int*>(F1)[pos] = j;  // F1 rows < j0 + 64 are no longer read
+    n3 += __popcll(bm);
+    wsync();
+  }
+  const int* idx = reinterpret_cast<const int*>(F1);
+  unsigned char* valid = reinterpret_cast<unsigned char*>(F1) + sizeof(int) * (size_t)N;
+  // note: F1's first N ints hold idx; valid bytes follow within F1's 3N doubles
+  wsync();
+  for (int k = lane; k < n3; k += RS_BLOCK) {
+    const int j = idx[k];
+    const int2 pr = pl[j];
+    const double* a = points + ((size_t)q * N + pr.x) * 3;
+    const double* b = points + ((size_t)m * N + pr.y) * 3;
+    const bool v = !(isnan(a[0]) || isnan(a[1]) || isnan(a[2]) || isnan(b[0]) || isnan(b[1]) || isnan(b[2]));
+    valid[k] = v ? 1 : 0;
+    for (int i = 0; i < 3; ++i) T[3 * k + i] = a[i] - (Rb[i * 3 + 0] * b[0] + Rb[i * 3 + 1] * b[1] + Rb[i * 3 + 2] * b[2]);
+  }
+  __threadfence_block();
+  wsync();
+  const double thr2 = P.thr3d * P.thr3d;
+  int my_best = -1, my_cnt = 0;
+  for (int i = lane; i < n3; i += RS_BLOCK) {
+    if (!valid[i]) continue;
+    int cc = 0;
+    for (int j = 0; j < n3; ++j) {
+      if (!valid[j]) continue;
+      const double dx = T[3 * j] - T[3 * i], dy = T[3 * j + 1] - T[3 * i + 1], dz = T[3 * j + 2] - T[3 * i + 2];
+      if (dx * dx + dy * dy + dz * dz < thr2) ++cc;
+    }
+    if (cc > my_cnt) { my_cnt = cc; my_best = i; }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const int oc = __shfl_xor(my_cnt, off, 64);
+    const int ob = __shfl_xor(my_best, off, 64);
+    if (oc > my_cnt || (oc == my_cnt && ob >= 0 && (my_best < 0 || ob < my_best))) {
+      my_cnt = oc;
+      my_best = ob;
+    }
+  }
+  if (lane == 0) {
+    const int best = my_best;
+    if (best >= 0) {
+      int cc = 0;
+      double s[3] = {0.0, 0.0, 0.0};
+      for (int j = 0; j < n3; ++j) {
+        int in = 0;
+        if (valid[j]) {
+          const double dx = T[3 * j] - T[3 * best], dy = T[3 * j + 1] - T[3 * best + 1], dz = T[3 * j + 2] - T[3 * best + 2];
+          in = dx * dx + dy * dy + dz * dz < thr2;
+        }
+        if (in) {
+          for (int i = 0; i < 3; ++i) s[i] += T[3 * j + i];
+          ++cc;
+          if (mask) mask[idx[j]] |= 2;
+        }
+      }
+      for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = s[i] / (double)cc;
+      r.stereo_inliers = cc;
+      r.accepted = (cc >= P.min3d) ? 1 : 0;
+    } else {
+      for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = 0.0;
+    }
+    *R_ = r;
+  }
+}
+
+template <int LB>
+__global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac(const double* bearings, const double* points, int N,
                                                      const int* cq, const int* cm, const int2* pairs,
                                                      const int* Kin, const short* table, RsParams P,
                                                      kmx_lcd_result* res, unsigned char* masks) {
@@ -1153,6 +1838,9 @@ struct kmx_lcd {
   int2* d_pairs = nullptr;
   kmx_lcd_result* d_res = nullptr;
   unsigned char* d_mask = nullptr;
+  double* d_fbuf = nullptr;  // [cap][2][N][3] compact match bearings (k_ransac_coop)
+  int ransac = 1;            // KMX_RANSAC: 1 cooperative (default), 0 lane-per-hypothesis
+  int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
 };
 
 namespace {
@@ -1164,10 +1852,11 @@ void lcd_free_pool(kmx_lcd* h) {
   h->d_desc = nullptr; h->d_bear = h->d_pts = nullptr; h->d_nfeat = nullptr; h->d_table = nullptr; h->d_table6 = nullptr;
 }
 void lcd_free_cand(kmx_lcd* h) {
-  void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask};
+  void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask, h->d_fbuf};
   for (void* x : p)
     if (x) (void)hipFree(x);
   h->d_cq = h->d_cm = h->d_K = nullptr; h->d_pairs = nullptr; h->d_res = nullptr; h->d_mask = nullptr;
+  h->d_fbuf = nullptr;
   h->cap = 0;
 }
 
@@ -1207,7 +1896,8 @@ int ensure_cap(kmx_lcd* h, int n) {
       hipMalloc(&h->d_K, sizeof(int) * cap) != hipSuccess ||
       hipMalloc(&h->d_pairs, sizeof(int2) * (size_t)cap * h->N) != hipSuccess ||
       hipMalloc(&h->d_res, sizeof(kmx_lcd_result) * cap) != hipSuccess ||
-      hipMalloc(&h->d_mask, (size_t)cap * h->N) != hipSuccess) {
+      hipMalloc(&h->d_mask, (size_t)cap * h->N) != hipSuccess ||
+      hipMalloc(&h->d_fbuf, sizeof(double) * 6 * (size_t)cap * h->N) != hipSuccess) {
     lcd_free_cand(h);
     return kmx::fail(KMX_ENOMEM, "candidate buffers");
   }
@@ -1232,10 +1922,32 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   rp.min3d = h->P.min_3d3d_inliers;
   rp.pmax = h->pmax;
   rp.pnp = (h->P.pose_recovery_type == 1) ? 1 : 0;
-  hipLaunchKernelGGL(k_ransac, dim3(n), dim3(RS_BLOCK), ransac_smem(h->N), h->stream, (const double*)h->d_bear,
-                     (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
-                     (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
-                     (want_masks || rp.pnp) ? h->d_mask : nullptr);
+  rp.prof = h->prof;
+  {
+    // KMX_RS_LB: minimum waves per SIMD for k_ransac (diagnostic; 1 = the
+    // compiler's choice, 256 VGPRs)
+    static const int lb = [] {
+      const char* v = std::getenv("KMX_RS_LB");
+      return v ? std::atoi(v) : 1;
+    }();
+    if (h->ransac == 1) {
+      static const int clb = [] {
+        const char* v = std::getenv("KMX_COOP_LB");
+        return v ? std::atoi(v) : 8;
+      }();
+      auto kc = (clb >= 8) ? k_ransac_coop<8> : k_ransac_coop<4>;
+      hipLaunchKernelGGL(kc, dim3(n), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
+                         (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
+                         (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
+                         (want_masks || rp.pnp) ? h->d_mask : nullptr, h->d_fbuf);
+    } else {
+      auto k = (lb >= 4) ? k_ransac<4> : (lb >= 2) ? k_ransac<2> : k_ransac<1>;
+      hipLaunchKernelGGL(k, dim3(n), dim3(RS_BLOCK), ransac_smem(h->N), h->stream, (const double*)h->d_bear,
+                         (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
+                         (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
+                         (want_masks || rp.pnp) ? h->d_mask : nullptr);
+    }
+  }
   if (rp.pnp) {
     PnpParams pp;
     pp.thr = h->P.ransac_threshold_2d3d;
@@ -1277,6 +1989,8 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
     return kmx::fail(KMX_EHIP, "hipStreamCreate");
   }
   h->own_stream = true;
+  if (const char* v = std::getenv("KMX_RANSAC")) h->ransac = std::atoi(v) ? 1 : 0;
+  if (const char* v = std::getenv("KMX_RS_PROF")) h->prof = std::atoi(v) ? 1 : 0;
   *out = h;
   return KMX_OK;
   KMX_GUARD_END
@@ -1442,4 +2156,12 @@ extern "C" int kmx_lcd_knn2(int norm, double lowe_ratio, const uint8_t* q, int32
   *k = K;
   return KMX_OK;
   KMX_GUARD_END
+}
+
+// Diagnostic: read (and reset) the k_ransac_coop phase timers (wall-clock ticks).
+extern "C" int kmx_lcd_debug_phase_times(unsigned long long* out16) {
+  KMX_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 16));
+  unsigned long long z[16] = {};
+  KMX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
+  return KMX_OK;
 }

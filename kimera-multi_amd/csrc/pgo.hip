@@ -575,6 +575,111 @@ __device__ __forceinline__ void lane_gather_compact(const Dev& d, const Lane& L,
   }
 }
 
+// Degree-balanced compact gather (G = 5; G = 6: owner-only cost). A tile's
+// incidences are one contiguous CSR range; it is cut into TP equal segments,
+// one per lane group, so every group walks ~the mean degree instead of the
+// wave waiting for its highest-degree pose (capping the per-pose walk at the
+// mean degree halves the gather time: k_gcap). A segment can
+// span several poses; each (group, pose) partial is flushed to LDS: the
+// first group of a pose writes A[pose], a group that starts inside a pose
+// (the continuation) writes H[group]. The (pose, row) lanes then add
+// A[pose] + H[g] for the pose's later segments in order, so the result is
+// deterministic and independent of everything but the tiling.
+template <int R, bool PUB, bool OWN>
+__device__ __forceinline__ void tile_gather_bal(const Dev& d, const Lane& L, const double* V, const double* pub,
+                                                double acc[4], double* cost, char* smem) {
+  using SM = Smem<R>;
+  constexpr int TP = SM::TP;
+  int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);          // [TP + 1] tile-local CSR
+  double* A = reinterpret_cast<double*>(smem + SM::x_off);         // [TP][R][4]
+  double* H = reinterpret_cast<double*>(smem + SM::con_off);       // [TP][R][4]
+  const int* ptr = OWN ? d.optr : d.inc_ptr;
+  const double* rec = OWN ? d.ocrec : d.crec;
+  const int tid = threadIdx.x;
+  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
+  const int K0 = ptr[p0];
+  __syncthreads();  // LDS reuse across consecutive gathers in one kernel (k_eval)
+  if (tid <= np) sptr[tid] = ptr[p0 + tid] - K0;
+  if constexpr (!OWN)
+    for (int i = tid; i < TP * R * 4; i += BLOCK) A[i] = 0.0;
+  __syncthreads();
+  const int n = sptr[np];
+  const int S = max(1, (n + TP - 1) / TP);
+  const int g = L.w * (64 / R) + L.pw;  // group = (wave, pose slot)
+  double part[4] = {0.0, 0.0, 0.0, 0.0};
+  double csum = 0.0;
+  const bool gvalid = (L.pw < 64 / R);
+  const int s0 = gvalid ? g * S : n, s1 = gvalid ? min(s0 + S, n) : n;
+  if (s0 < s1) {
+    int lo = 0, hi = np;  // pose containing s0: sptr[lo] <= s0 < sptr[lo + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (sptr[mid] <= s0) lo = mid;
+      else hi = mid;
+    }
+    while (sptr[lo + 1] <= s0) ++lo;  // skip zero-degree poses
+    int p = lo;
+    bool head = s0 > sptr[p];
+    // self row of the current pose, and (prefetched) of the next pose with
+    // incidences, so crossing a pose boundary does not wait on memory
+    auto next_pose = [&](int q) {
+      do ++q;
+      while (q < np - 1 && sptr[q + 1] == sptr[q]);
+      return q;
+    };
+    double vs[4], vn[4] = {0.0, 0.0, 0.0, 0.0};
+    load4(V + (size_t)(p0 + p) * 4 * R + 4 * L.a, vs);
+    int pn = next_pose(p);
+    if (pn < np && sptr[pn] < s1) load4(V + (size_t)(p0 + pn) * 4 * R + 4 * L.a, vn);
+    int pend = sptr[p + 1];
+    for (int k = s0; k < s1; ++k) {
+      if (k >= pend) {  // next pose: flush this one's partial
+        if constexpr (!OWN) store4((head ? H + (g * R + L.a) * 4 : A + (p * R + L.a) * 4), part);
+        part[0] = part[1] = part[2] = part[3] = 0.0;
+        head = false;
+        p = pn;
+        pend = sptr[p + 1];
+        vs[0] = vn[0]; vs[1] = vn[1]; vs[2] = vn[2]; vs[3] = vn[3];
+        pn = next_pose(p);
+        if (pn < np && sptr[pn] < s1) load4(V + (size_t)(p0 + pn) * 4 * R + 4 * L.a, vn);
+      }
+      const double2* q2 = reinterpret_cast<const double2*>(rec + 12 * (size_t)(K0 + k));
+      double2 q[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) q[i] = q2[i];
+      const int2 in = unpack_int2(q[5].y);
+      const int o = in.x;
+      const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V);
+      const double2* b2 = reinterpret_cast<const double2*>(base + 4 * L.a);
+      double2 v0 = b2[0], v1 = b2[1];
+      if (!PUB && o < 0) v0 = v1 = make_double2(0.0, 0.0);
+      Edge E;
+      edge_from_compact(q, E);
+      const double vo[4] = {v0.x, v0.y, v1.x, v1.y};
+      const double c = incidence_row(E, (in.y >> 31) & 1, vs, vo, part);
+      csum += (OWN || o < 0) ? c : 0.5 * c;
+    }
+    if constexpr (!OWN) store4((head ? H + (g * R + L.a) * 4 : A + (p * R + L.a) * 4), part);
+  }
+  if (cost) *cost += csum;
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  if constexpr (!OWN) {
+    __syncthreads();
+    if (L.valid) {
+      const int p = L.pose - p0;
+      load4(A + (p * R + L.a) * 4, acc);
+      if (sptr[p + 1] > sptr[p]) {
+        const int gf = sptr[p] / S, gl = (sptr[p + 1] - 1) / S;
+        for (int gg = gf + 1; gg <= gl; ++gg) {
+          double h[4];
+          load4(H + (gg * R + L.a) * 4, h);
+          acc[0] += h[0]; acc[1] += h[1]; acc[2] += h[2]; acc[3] += h[3];
+        }
+      }
+    }
+  }
+}
+
 template <int R, int G, bool PUB>
 __device__ __forceinline__ void gather(const Dev& d, const Lane& L, const double* V, const double* pub,
                                        double acc[4], double* cost, char* smem) {
@@ -582,6 +687,8 @@ __device__ __forceinline__ void gather(const Dev& d, const Lane& L, const double
   else if constexpr (G == 2) lane_gather_plain<R, PUB>(d, L, V, pub, acc, cost);
   else if constexpr (G == 3) lane_gather_compact<R, PUB, false>(d, L, V, pub, acc, cost);
   else if constexpr (G == 4) lane_gather_compact<R, PUB, true>(d, L, V, pub, acc, cost);
+  else if constexpr (G == 5) tile_gather_bal<R, PUB, false>(d, L, V, pub, acc, cost, smem);
+  else if constexpr (G == 6) tile_gather_bal<R, PUB, true>(d, L, V, pub, acc, cost, smem);
   else tile_gather<R, PUB>(d, L, V, pub, acc, cost, smem);
 }
 
@@ -947,7 +1054,7 @@ __global__ __launch_bounds__(BLOCK, KMX_LB_GATHER) void k_cost(Dev d) {
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
   double acc[4], cost = 0.0;
-  gather<R, (GV == 3 ? 4 : GV), true>(d, L, d.Xt, d.pub, acc, &cost, smem);
+  gather<R, (GV == 3 ? 4 : GV == 5 ? 6 : GV), true>(d, L, d.Xt, d.pub, acc, &cost, smem);
   finish_tile<RED_COST, 1, F>(d, L, &cost, smem + Smem<R>::red_off, R);
 }
 
@@ -1256,6 +1363,38 @@ __global__ __launch_bounds__(BLOCK) void k_gablate(Dev d, const double* V, doubl
   if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
 }
 
+// Diagnostic: the compact gather with each pose's incidence loop capped at CAP
+// (wrong results; bounds what a degree-balanced gather could gain).
+template <int R, int CAP>
+__global__ __launch_bounds__(BLOCK) void k_gcap(Dev d, const double* V, double* out) {
+  KMX_SMEM;
+  const Lane L = lane_map<R>(d);
+  double acc[4] = {0, 0, 0, 0}, cost = 0.0;
+  if (L.valid) {
+    double vs[4];
+    load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
+    const int k0 = d.inc_ptr[L.pose], k1 = min(d.inc_ptr[L.pose + 1], k0 + CAP);
+    for (int k = k0; k < k1; ++k) {
+      const double2* q2 = reinterpret_cast<const double2*>(d.crec + 12 * (size_t)k);
+      double2 q[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) q[i] = q2[i];
+      const int2 in = unpack_int2(q[5].y);
+      const int o = in.x;
+      const double* base = (o >= 0) ? V + (size_t)o * 4 * R : d.pub + (size_t)(-1 - o) * 4 * R;
+      const double2* b2 = reinterpret_cast<const double2*>(base + 4 * L.a);
+      const double2 v0 = b2[0], v1 = b2[1];
+      Edge E;
+      edge_from_compact(q, E);
+      const double vo[4] = {v0.x, v0.y, v1.x, v1.y};
+      cost += incidence_row(E, (in.y >> 31) & 1, vs, vo, acc);
+    }
+    store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
+  }
+  const double t = block_sum(cost, reinterpret_cast<double*>(smem + Smem<R>::red_off));
+  if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
+}
+
 // Diagnostic: the gather primitive alone (as in k_cost), for A/B timing of
 // gather variants and occupancy bounds (kmx_pgo_debug_gather_bench).
 template <int R, int GV, int LBW>
@@ -1497,7 +1636,9 @@ void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
     case 4: enqueue_round_t<R, 2, 0>(h, d_active); break;
     case 5: enqueue_round_t<R, 2, 1>(h, d_active); break;
     case 6: enqueue_round_t<R, 3, 0>(h, d_active); break;
-    default: enqueue_round_t<R, 3, 1>(h, d_active); break;
+    case 7: enqueue_round_t<R, 3, 1>(h, d_active); break;
+    case 10: enqueue_round_t<R, 5, 0>(h, d_active); break;
+    default: enqueue_round_t<R, 5, 1>(h, d_active); break;
   }
 }
 
@@ -1539,7 +1680,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     return kmx::fail(KMX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
   h->own_stream = true;
-  if (const char* v = std::getenv("KMX_GATHER")) h->gvar_req = std::min(3, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("KMX_GATHER")) h->gvar_req = std::min(5, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("KMX_FUSED")) h->fvar = std::atoi(v) ? 1 : 0;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
   *out = h;
@@ -1765,9 +1906,9 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       ok = std::fabs(c0 - Q[6]) <= 1e-12 && std::fabs(c1 - Q[7]) <= 1e-12 && std::fabs(c2 - Q[8]) <= 1e-12;
     }
     h->compact_ok = ok;
-    const bool want = (h->gvar_req < 0 || h->gvar_req == 3);
-    h->gvar = (ok && want) ? 3 : (h->gvar_req >= 0 && h->gvar_req < 3 ? h->gvar_req : 2);
-    if (h->gvar == 3) {
+    const bool want = (h->gvar_req < 0 || h->gvar_req == 3 || h->gvar_req == 5);
+    h->gvar = (ok && want) ? (h->gvar_req == 3 ? 3 : 5) : (h->gvar_req >= 0 && h->gvar_req < 3 ? h->gvar_req : 2);
+    if (h->gvar == 3 || h->gvar == 5) {
       const size_t ni = (size_t)std::max(h->ninc, 1);
       crec.assign(ni * 12, 0.0);
       for (size_t k = 0; k < (size_t)h->ninc; ++k) {
@@ -1828,7 +1969,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(up(h->d_inc_ptr, inc_ptr.data(), sizeof(int) * inc_ptr.size()));
   KMX_HIP(up(h->d_inc, inc.data(), sizeof(int2) * inc.size()));
   KMX_HIP(up(h->d_irec, irec.data(), sizeof(double) * irec.size()));
-  if (h->gvar == 3) {
+  if (h->gvar == 3 || h->gvar == 5) {
     if ((rc = dalloc(&h->d_crec, crec.size())) || (rc = dalloc(&h->d_ocrec, ocrec.size())) ||
         (rc = dalloc(&h->d_optr, optr.size())) || (rc = dalloc(&h->d_eopos, eopos.size()))) {
       free_dev(h);
@@ -2175,6 +2316,9 @@ extern "C" int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, do
   } else if (h->gvar == 3) {
     KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 3>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
                                           h->dv, l, mode, (const double*)dV, dO));
+  } else if (h->gvar == 5) {
+    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 5>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
+                                          h->dv, l, mode, (const double*)dV, dO));
   } else {
     KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 0>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
                                           h->dv, l, mode, (const double*)dV, dO));
@@ -2253,6 +2397,10 @@ extern "C" int kmx_pgo_debug_gather_bench(kmx_pgo* h, int variant, int reps, dou
       KMX_GB(10, 1, 1) KMX_GB(11, 1, 4) KMX_GB(12, 1, 6)
       KMX_GB(20, 2, 1) KMX_GB(21, 2, 4) KMX_GB(22, 2, 6) KMX_GB(23, 2, 8)
       KMX_GB(40, 3, 1) KMX_GB(41, 3, 4) KMX_GB(42, 3, 6) KMX_GB(45, 4, 1)
+      KMX_GB(60, 5, 1) KMX_GB(61, 5, 4) KMX_GB(62, 5, 6) KMX_GB(65, 6, 1)
+#define KMX_GC(V, C) case V: hipLaunchKernelGGL((k_gcap<5, C>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
+      KMX_GC(50, 1000) KMX_GC(51, 12) KMX_GC(52, 10) KMX_GC(53, 8) KMX_GC(54, 4)
+#undef KMX_GC
 #undef KMX_GB
 #define KMX_GA(V, A) case V: hipLaunchKernelGGL((k_gablate<5, A>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
       KMX_GA(30, 0) KMX_GA(31, 1) KMX_GA(32, 2) KMX_GA(33, 3)

@@ -299,6 +299,28 @@ static double poly_eval(const double* c, int deg, double z) {
   return v;
 }
 
+/* Safeguarded Newton on an isolating interval [a, b]: Newton steps that
+ * leave the bracket fall back to bisection; the bracket follows the sign at
+ * its left end; stops when a step moves less than 1e-15 relative. */
+static double refine_root(const double* c, int deg, double a, double b) {
+  double dc[10];
+  for (int i = 0; i < deg; ++i) dc[i] = (double)(i + 1) * c[i + 1];
+  double fa = poly_eval(c, deg, a);
+  double x = 0.5 * (a + b);
+  for (int it = 0; it < 60; ++it) {
+    const double fx = poly_eval(c, deg, x);
+    if (fx == 0.0) return x;
+    if ((fx < 0.0) == (fa < 0.0)) { a = x; fa = fx; }
+    else b = x;
+    const double dfx = poly_eval(dc, deg - 1, x);
+    double xn = (dfx != 0.0) ? x - fx / dfx : 0.5 * (a + b);
+    if (!(xn > a && xn < b)) xn = 0.5 * (a + b);
+    if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;
+    x = xn;
+  }
+  return x;
+}
+
 /* real roots of a polynomial (ascending coefficients) by Sturm-sequence
  * bisection; deterministic fixed-depth refinement. */
 static int real_roots(const double* coef, int deg_in, double* roots) {
@@ -346,9 +368,16 @@ static int real_roots(const double* coef, int deg_in, double* roots) {
     }                                                          \
     (out) = ch_;                                               \
   } while (0)
-  /* explicit stack of intervals: (lo, hi, V(lo), V(hi), depth) */
-  double st_lo[64], st_hi[64];
-  int st_vl[64], st_vh[64], st_d[64];
+  /* 64-ary Sturm isolation: an interval is cut at the 63 points
+   * lo + i * ((hi - lo) / 64); the root counts of the 64 pieces come from the
+   * sign-change counts at those points (pieces with count 1 are refined by
+   * refine_root, count > 1 recurse, up to RR_DEPTH levels). The GPU evaluates
+   * the 63 points of a level in one wavefront, so both sides use exactly
+   * these points, and refines all isolated roots in parallel lanes. */
+#define RR_SPLIT 64
+#define RR_DEPTH 12
+  double st_lo[RR_SPLIT * RR_DEPTH + 1], st_hi[RR_SPLIT * RR_DEPTH + 1];
+  int st_vl[RR_SPLIT * RR_DEPTH + 1], st_vh[RR_SPLIT * RR_DEPTH + 1], st_d[RR_SPLIT * RR_DEPTH + 1];
   int sp = 0, nr = 0;
   int vlo, vhi;
   SIGNCH(-bound, vlo);
@@ -360,27 +389,23 @@ static int real_roots(const double* coef, int deg_in, double* roots) {
     const int vl = st_vl[sp], vh = st_vh[sp], dep = st_d[sp];
     const int cnt = vl - vh;
     if (cnt <= 0) continue;
-    if (cnt == 1 || dep >= 50) {
-      /* one root in (lo, hi]: bisection on the sign of the polynomial */
-      double a = lo, b = hi;
-      double fa = poly_eval(S[0], deg, a);
-      for (int it = 0; it < 80; ++it) {
-        const double mid = 0.5 * (a + b);
-        const double fm = poly_eval(S[0], deg, mid);
-        if (fm == 0.0) { a = b = mid; break; }
-        if ((fm < 0.0) == (fa < 0.0)) { a = mid; fa = fm; }
-        else b = mid;
-      }
-      if (nr < 10) roots[nr++] = 0.5 * (a + b);
+    if (cnt == 1 || dep >= RR_DEPTH) {
+      if (nr < 10) roots[nr++] = refine_root(S[0], deg, lo, hi);
       continue;
     }
-    const double mid = 0.5 * (lo + hi);
-    int vm;
-    SIGNCH(mid, vm);
-    if (sp + 2 <= 64) {
-      st_lo[sp] = mid; st_hi[sp] = hi; st_vl[sp] = vm; st_vh[sp] = vh; st_d[sp] = dep + 1; ++sp;
-      st_lo[sp] = lo; st_hi[sp] = mid; st_vl[sp] = vl; st_vh[sp] = vm; st_d[sp] = dep + 1; ++sp;
+    const double w = (hi - lo) / RR_SPLIT;
+    int v[RR_SPLIT + 1];
+    double x[RR_SPLIT + 1];
+    x[0] = lo; v[0] = vl;
+    x[RR_SPLIT] = hi; v[RR_SPLIT] = vh;
+    for (int i = 1; i < RR_SPLIT; ++i) {
+      x[i] = lo + (double)i * w;
+      SIGNCH(x[i], v[i]);
     }
+    for (int j = RR_SPLIT - 1; j >= 0; --j) /* pushed right to left: popped in increasing x */
+      if (v[j] - v[j + 1] > 0) {
+        st_lo[sp] = x[j]; st_hi[sp] = x[j + 1]; st_vl[sp] = v[j]; st_vh[sp] = v[j + 1]; st_d[sp] = dep + 1; ++sp;
+      }
   }
 #undef SIGNCH
   /* ascending order */

@@ -14,4 +14,7 @@ for rep in range(2):
     t = time.time(); res, _ = det.verify(pool.cand_query, pool.cand_match); el = time.time() - t
     acc = sum(r["accepted"] for r in res)
     print(f"{n} candidates in {el*1e3:.1f} ms -> {n/el:.0f} cand/s, accepted {acc}, mean iters "
-          f"{np.mean([r['iterations_2d2d'] for r in res[0::2]]):.1f}", flush=True)
+          f"{np.mean([r['iterations_2d2d'] for r in res[0::2]]):.1f} (true) "
+          f"{np.mean([r['iterations_2d2d'] for r in res[1::2]]):.1f} (false), mean K "
+          f"{np.mean([r['n_matches'] for r in res[0::2]]):.0f} / {np.mean([r['n_matches'] for r in res[1::2]]):.0f}",
+          flush=True)

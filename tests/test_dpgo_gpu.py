@@ -47,8 +47,10 @@ def _pair(g, P, X0):
     return s, o
 
 
-@pytest.mark.parametrize("r", [3, 5, 8])
-def test_primitives_match_oracle(gpu, r):
+@pytest.mark.parametrize("r,gather", [(3, None), (5, None), (8, None), (5, "3"), (5, "2")])
+def test_primitives_match_oracle(gpu, r, gather, monkeypatch):
+    if gather is not None:
+        monkeypatch.setenv("KMX_GATHER", gather)
     g, P, X0 = _setup(r=r)
     # non-trivial GNC weights so w*kappa paths are exercised
     g.weight = np.random.default_rng(3).uniform(0.0, 1.0, g.m)
@@ -68,10 +70,10 @@ def test_primitives_match_oracle(gpu, r):
             assert abs(gs - os_) <= 1e-10 * max(1.0, abs(os_)), (mode, gs, os_)
 
 
-@pytest.mark.parametrize("robust,gather", [(False, None), (True, None), (True, "2")])
+@pytest.mark.parametrize("robust,gather", [(False, None), (True, None), (True, "2"), (True, "3")])
 def test_rounds_match_oracle(gpu, robust, gather, monkeypatch):
-    """gather None = default (compact 96-B records on SO(3) input); "2" forces
-    the full 128-B record gather."""
+    """gather None = default (degree-balanced gather over compact 96-B records on
+    SO(3) input); "3" the per-pose compact gather; "2" the full 128-B records."""
     if gather is not None:
         monkeypatch.setenv("KMX_GATHER", gather)
     g, P, X0 = _setup(robust=robust)
