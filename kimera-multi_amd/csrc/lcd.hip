@@ -128,6 +128,7 @@ __device__ double det3(const double M[9]) {
 __device__ void sym_eig3(double A[9], double V[9]) {
   for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 12; ++sweep) {
+    if (A[1] == 0.0 && A[2] == 0.0 && A[5] == 0.0) break;  // every rotation would be skipped
     for (int p = 0; p < 2; ++p)
       for (int q = p + 1; q < 3; ++q) {
         const double apq = A[p * 3 + q];
@@ -164,13 +165,19 @@ __device__ void svd3(const double E[9], double U[9], double s[3], double V[9]) {
       A[i * 3 + j] = acc;
     }
   sym_eig3(A, W);
-  int ord[3] = {0, 1, 2};
-  for (int a = 0; a < 3; ++a)
-    for (int b = 0; b < 2 - a; ++b)
-      if (A[ord[b] * 4] < A[ord[b + 1] * 4]) { const int t = ord[b]; ord[b] = ord[b + 1]; ord[b + 1] = t; }
+  // descending bubble sort of the eigenvalues (register selects, no indexing)
+  auto ev = [&](int o) { return o == 0 ? A[0] : (o == 1 ? A[4] : A[8]); };
+  int o0 = 0, o1 = 1, o2 = 2, tt;
+  if (ev(o0) < ev(o1)) { tt = o0; o0 = o1; o1 = tt; }
+  if (ev(o1) < ev(o2)) { tt = o1; o1 = o2; o2 = tt; }
+  if (ev(o0) < ev(o1)) { tt = o0; o0 = o1; o1 = tt; }
+  const int ord[3] = {o0, o1, o2};
+#pragma unroll
   for (int c = 0; c < 3; ++c) {
-    s[c] = sqrt(fmax(A[ord[c] * 4], 0.0));
-    for (int r = 0; r < 3; ++r) V[r * 3 + c] = W[r * 3 + ord[c]];
+    const int o = ord[c];
+    s[c] = sqrt(fmax(ev(o), 0.0));
+#pragma unroll
+    for (int r = 0; r < 3; ++r) V[r * 3 + c] = (o == 0) ? W[r * 3] : (o == 1 ? W[r * 3 + 1] : W[r * 3 + 2]);
   }
   double u[3][3];
   for (int c = 0; c < 2; ++c) {
@@ -264,11 +271,33 @@ __device__ double refine_root(const double* c, int deg, double a, double b) {
     else b = x;
     const double dfx = poly_eval(dc, deg - 1, x);
     double xn = (dfx != 0.0) ? x - fx / dfx : 0.5 * (a + b);
-    if (!(xn > a && xn < b)) xn = 0.5 * (a + b);
-    if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;
+    if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;  // converged (before the safeguard)
+    if (!(xn > a && xn < b)) {
+      xn = 0.5 * (a + b);
+      if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;
+    }
     x = xn;
   }
   return x;
+}
+
+// Fujiwara root bound with power-of-two terms (oracle/lcd_oracle.c root_bound)
+__device__ __forceinline__ int root_bound_term(double ai, int m) {  // INT_MIN: none
+  if (!(ai != 0.0) || !isfinite(ai)) return INT_MIN;
+  const int x = ilogb(ai) + 1;
+  return x >= 0 ? (x + m - 1) / m : -((-x) / m);
+}
+__device__ double root_bound(const double* a, int deg) {
+  int kmax = INT_MIN, fin = 1;
+  double cauchy = 0.0;
+  for (int i = 0; i < deg; ++i) {
+    cauchy = fmax(cauchy, fabs(a[i]));
+    if (!isfinite(a[i])) fin = 0;
+    kmax = max(kmax, root_bound_term(a[i], deg - i));
+  }
+  if (!fin) return cauchy + 1.0;
+  if (kmax == INT_MIN) return 1.0;
+  return ldexp(1.0, kmax + 1);
 }
 
 __device__ int real_roots(const double* coef, int deg_in, double* roots) {
@@ -299,9 +328,7 @@ __device__ int real_roots(const double* coef, int deg_in, double* roots) {
     sd[ns] = dr;
     ++ns;
   }
-  double bound = 0.0;
-  for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(S[0][i]));
-  bound += 1.0;
+  const double bound = root_bound(S[0], deg);
   // 64-ary isolation / refinement, the oracle's sequence of points
   // (oracle/lcd_oracle.c real_roots); k_ransac_coop evaluates a level's 63
   // points in one wavefront. At most deg intervals with roots are alive.
@@ -827,6 +854,18 @@ struct PnpParams {
   int max_iter, min2d, min_pnp, pmax;
 };
 
+// Diagnostic phase timers (kmx_lcd_debug_phase_times): cycles per phase summed
+// over the first 64 candidates' hypotheses.
+__device__ unsigned long long g_phase[16];
+#define KMX_PT(i)                                                              \
+  do {                                                                         \
+    if (prof && lane == 0) {                                                   \
+      const unsigned long long t_ = wall_clock64();                            \
+      atomicAdd(&g_phase[i], t_ - t_prev);                                     \
+      t_prev = t_;                                                             \
+    }                                                                          \
+  } while (0)
+
 // ---------------------------------------------- cooperative 2D-2D RANSAC --
 // k_ransac_coop: one wavefront per candidate, one hypothesis at a time with
 // all 64 lanes cooperating on the 5-point solve (LDS workspace, ~6 KB), so
@@ -842,75 +881,102 @@ struct CoopWS {
   union {
     struct {                  // nullspace + system construction
       double vs[5][9];
-      double QA[9][5];
       double c2[3][10];
       double EEt[9][10];
       double tr[10];
     };
     struct {                  // roots
-      double S[11][11];
-      double val[RR_SPLIT];
+      double S[11][11];       // Sturm sequence, zero padded
+      double cc[3][8];        // c1, c2, c3 of the degree-10 polynomial
       double st_lo[16], st_hi[16];
       int st_vl[16], st_vh[16], st_d[16];
-      int sd[11];
-      int vi[RR_SPLIT];
     };
   };
   union {
     struct {                  // system + elimination
       double A[10][20];
-      double fk[10];
     };
     struct {                  // models (A is dead once Bp is extracted)
-      double Es[10][9];
-      double berr[10];
-      double bR[10][9], bt[10][3];
+      double Rab[10][2][9];   // per E: the two rotations (det fixed)
+      double tu[10][3];       // per E: U's third column
     };
   };
   double Bp[3][3][5];
-  double nco[11];
   double roots[10];
-  double iv_lo[10], iv_hi[10];  // isolating intervals
   double mR[9], mt[3];       // model of the current hypothesis
   double bestm[12];          // best model so far
-  int ns, deg, nr, ne, sp, ok, bfound;
+  int nr, ok;
+  signed char t11[10][2][2], t21[20][3][2];  // LDS copies of T11 / T21
 };
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // the block is one wavefront
 
-// nullspace_5x9 (Householder QR of Q^T, lane 0) + the 4 back-substitutions (lanes 0-3)
+__device__ __forceinline__ double rdlane(double v, int src) {  // src wave-uniform
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, src);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double wave_fmax(double v) {  // exact in any order
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// nullspace_5x9: Householder QR of Q^T with lane 9j+i holding A[i][j]
+// (column j in 9 consecutive lanes); the column norms and the reflector are
+// formed from readlane broadcasts in the serial order, each d_j from a
+// 9-term gather of column j. Then the 4 back-substitutions (lanes 0-3).
 __device__ void coop_nullspace(CoopWS& w, int lane) {
-  if (lane == 0) {
-    for (int i = 0; i < 9; ++i)
-      for (int j = 0; j < 5; ++j) w.QA[i][j] = w.f1[3 * j + i / 3] * w.f2[3 * j + i % 3];
-    for (int k = 0; k < 5; ++k) {
-      double nx = 0.0;
-      for (int i = k; i < 9; ++i) nx += w.QA[i][k] * w.QA[i][k];
-      nx = sqrt(nx);
-      const double alpha = (w.QA[k][k] >= 0.0) ? -nx : nx;
-      double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      for (int i = k; i < 9; ++i) v[i] = w.QA[i][k];
-      v[k] -= alpha;
-      double nv = 0.0;
-      for (int i = k; i < 9; ++i) nv += v[i] * v[i];
-      nv = sqrt(nv);
-      for (int i = 0; i < 9; ++i) w.vs[k][i] = (nv > 0.0 && i >= k) ? v[i] / nv : 0.0;
-      for (int j = k; j < 5; ++j) {
-        double d = 0.0;
-        for (int i = k; i < 9; ++i) d += w.vs[k][i] * w.QA[i][j];
-        for (int i = k; i < 9; ++i) w.QA[i][j] -= 2.0 * w.vs[k][i] * d;
-      }
+  const int li = lane % 9, lj = lane / 9;  // lanes >= 45 carry a dummy column
+  double a = (lane < 45) ? w.f1[3 * lj + li / 3] * w.f2[3 * lj + li % 3] : 0.0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    double v[9];
+    double nx = 0.0;
+#pragma unroll
+    for (int i = k; i < 9; ++i) {
+      v[i] = rdlane(a, 9 * k + i);
+      nx += v[i] * v[i];
     }
+    nx = sqrt(nx);
+    const double alpha = (v[k] >= 0.0) ? -nx : nx;
+    v[k] -= alpha;
+    double nv = 0.0;
+#pragma unroll
+    for (int i = k; i < 9; ++i) nv += v[i] * v[i];
+    nv = sqrt(nv);
+    double vs[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) vs[i] = (nv > 0.0 && i >= k) ? v[i] / nv : 0.0;
+    if (lane < 9) {
+      double x = 0.0;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) x = (lane == i) ? vs[i] : x;
+      w.vs[k][lane] = x;
+    }
+    // d_j = sum_{i >= k} vs[i] A[i][j] over this lane's column j
+    double d = 0.0;
+#pragma unroll
+    for (int i = k; i < 9; ++i) d += vs[i] * __shfl(a, 9 * lj + i, 64);
+    double my_vs = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) my_vs = (li == i) ? vs[i] : my_vs;
+    if (lane < 45 && li >= k && lj >= k) a -= 2.0 * my_vs * d;
   }
   wsync();
   if (lane < 4) {
-    double x[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    x[5 + lane] = 1.0;
+    double x[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) x[i] = (i == 5 + lane) ? 1.0 : 0.0;
+#pragma unroll
     for (int k = 4; k >= 0; --k) {
       double d = 0.0;
+#pragma unroll
       for (int i = k; i < 9; ++i) d += w.vs[k][i] * x[i];
+#pragma unroll
       for (int i = k; i < 9; ++i) x[i] -= 2.0 * w.vs[k][i] * d;
     }
+#pragma unroll
     for (int i = 0; i < 9; ++i) w.N[lane][i] = x[i];
   }
   wsync();
@@ -929,75 +995,57 @@ __constant__ signed char T21[20][3][2] = {
     {{6, 3}, {9, 0}, {-1, -1}},   {{4, 2}, {5, 1}, {-1, -1}},   {{4, 3}, {7, 2}, {8, 1}},
     {{7, 3}, {9, 1}, {-1, -1}},   {{5, 2}, {-1, -1}, {-1, -1}}, {{5, 3}, {8, 2}, {-1, -1}},
     {{8, 3}, {9, 2}, {-1, -1}},   {{9, 3}, {-1, -1}, {-1, -1}}};
-__device__ __forceinline__ double mul11_k(const double* a, const double* b, int k) {
+// Coefficient k of mul11(E_ea, E_eb) / mul21(a, E_eb), E_e[c] = N[c][e]:
+// the terms of the serial loop in its (i, j) order (LDS copies of T11 / T21).
+__device__ __forceinline__ double mul11_e(const CoopWS& w, int ea, int eb, int k) {
   double s = 0.0;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const int i = T11[k][t][0];
-    if (i >= 0) s += a[i] * b[T11[k][t][1]];
+    const int i = w.t11[k][t][0];
+    if (i >= 0) s += w.N[i][ea] * w.N[w.t11[k][t][1]][eb];
   }
   return s;
 }
-__device__ __forceinline__ double mul21_k(const double* a, const double* b, int k) {
+__device__ __forceinline__ double mul21_e(const double* a, const CoopWS& w, int eb, int k) {
   double s = 0.0;
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
-    const int i = T21[k][t][0];
-    if (i >= 0) s += a[i] * b[T21[k][t][1]];
+    const int i = w.t21[k][t][0];
+    if (i >= 0) s += a[i] * w.N[w.t21[k][t][1]][eb];
   }
   return s;
 }
 
-// row 9 (det E = 0): c2_q = mul11(E[C2P[q][0]], E[C2P[q][1]]) - mul11(E[C2P[q][2]], E[C2P[q][3]])
-__constant__ int C2P[3][4] = {{4, 8, 5, 7}, {3, 8, 5, 6}, {3, 7, 4, 6}};
-
 __device__ void coop_system(CoopWS& w, int lane) {
-  // E as [9][4] rows: E_e[c] = N[c][e]
-  auto Erow = [&](int e, double* out) {
-    for (int c = 0; c < 4; ++c) out[c] = w.N[c][e];
-  };
-  // EEt[ij][k] = sum_l mul11(E[i*3+l], E[j*3+l])[k] (l = 0, 1, 2 in order); c2 for row 9
-  for (int t = lane; t < 90 + 30; t += 64) {
+  // EEt[ij][k] = sum_l mul11(E[i*3+l], E[j*3+l])[k] (l = 0, 1, 2 in order); c2 for row 9:
+  // c2_q = mul11(E_a, E_b) - mul11(E_c, E_d), (a, b, c, d) = (4,8,5,7), (3,8,5,6), (3,7,4,6)
+  for (int t = lane; t < 90 + 30; t += RS_BLOCK) {
     if (t < 90) {
       const int ij = t / 10, k = t % 10, i = ij / 3, j = ij % 3;
       double acc = 0.0;
-      for (int l = 0; l < 3; ++l) {
-        double a[4], b[4];
-        Erow(i * 3 + l, a);
-        Erow(j * 3 + l, b);
-        acc += mul11_k(a, b, k);
-      }
+      for (int l = 0; l < 3; ++l) acc += mul11_e(w, i * 3 + l, j * 3 + l, k);
       w.EEt[ij][k] = acc;
     } else {
-      const int q = (t - 90) / 10, k = (t - 90) % 10;  // q: 0 -> (4,8)-(5,7), 1 -> (3,8)-(5,6), 2 -> (3,7)-(4,6)
-      double a[4], b[4], c[4], d[4];
-      Erow(C2P[q][0], a); Erow(C2P[q][1], b); Erow(C2P[q][2], c); Erow(C2P[q][3], d);
-      w.c2[q][k] = mul11_k(a, b, k) - mul11_k(c, d, k);
+      const int q = (t - 90) / 10, k = (t - 90) % 10;
+      const int ea = q == 0 ? 4 : 3, eb = q == 2 ? 7 : 8, ec = q == 2 ? 4 : 5, ed = q == 0 ? 7 : 6;
+      w.c2[q][k] = mul11_e(w, ea, eb, k) - mul11_e(w, ec, ed, k);
     }
   }
   wsync();
   if (lane < 10) w.tr[lane] = w.EEt[0][lane] + w.EEt[4][lane] + w.EEt[8][lane];
   wsync();
   // rows 0..8: r[k] = sum_l 2 mul21(EEt[i*3+l], E[l*3+j])[k] - mul21(tr, E[ij])[k]; row 9
-  for (int t = lane; t < 200; t += 64) {
+  for (int t = lane; t < 200; t += RS_BLOCK) {
     const int row = t / 20, k = t % 20;
     double r = 0.0;
     if (row < 9) {
       const int i = row / 3, j = row % 3;
-      for (int l = 0; l < 3; ++l) {
-        double b[4];
-        Erow(l * 3 + j, b);
-        r += 2.0 * mul21_k(w.EEt[i * 3 + l], b, k);
-      }
-      double b[4];
-      Erow(row, b);
-      r -= mul21_k(w.tr, b, k);
+      for (int l = 0; l < 3; ++l) r += 2.0 * mul21_e(w.EEt[i * 3 + l], w, l * 3 + j, k);
+      r -= mul21_e(w.tr, w, row, k);
     } else {
-      double b0[4], b1[4], b2[4];
-      Erow(0, b0); Erow(1, b1); Erow(2, b2);
-      r += mul21_k(w.c2[0], b0, k);
-      r -= mul21_k(w.c2[1], b1, k);
-      r += mul21_k(w.c2[2], b2, k);
+      r += mul21_e(w.c2[0], w, 0, k);
+      r -= mul21_e(w.c2[1], w, 1, k);
+      r += mul21_e(w.c2[2], w, 2, k);
     }
     w.A[row][k] = r;
   }
@@ -1006,38 +1054,58 @@ __device__ void coop_system(CoopWS& w, int lane) {
 
 // Gauss-Jordan with partial pivoting on the 10x20 system (serial order per
 // element; lanes own columns). Returns 0 on a zero pivot.
+// Every lane reads column k at once (10 independent broadcast loads) and picks
+// the pivot in registers; the multipliers are column k after the swap; each
+// lane then updates its own column row by row.
 __device__ int coop_gj(CoopWS& w, int lane) {
+  const int cl = lane < 20 ? lane : 19;  // lanes >= 20 shadow column 19, never store
   for (int k = 0; k < 10; ++k) {
+    double col[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) col[i] = w.A[i][k];
     int p = k;
-    for (int i = k + 1; i < 10; ++i)
-      if (fabs(w.A[i][k]) > fabs(w.A[p][k])) p = i;
-    if (w.A[p][k] == 0.0) return 0;  // uniform
-    if (p != k && lane < 20) {
-      const double t = w.A[k][lane]; w.A[k][lane] = w.A[p][lane]; w.A[p][lane] = t;
+    double pv = 0.0, pa = -1.0, ck = 0.0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      if (i == k) { ck = col[i]; pv = ck; pa = fabs(ck); }
+      else if (i > k && fabs(col[i]) > pa) { p = i; pv = col[i]; pa = fabs(col[i]); }
     }
-    wsync();
-    const double inv = 1.0 / w.A[k][k];
-    wsync();
-    if (lane < 20) w.A[k][lane] *= inv;
-    if (lane < 10) w.fk[lane] = w.A[lane][k];
-    wsync();
-    if (lane < 20)
-      for (int i = 0; i < 10; ++i) {
-        if (i == k) continue;
-        const double f = (i < 10) ? w.fk[i] : 0.0;
-        if (f == 0.0) continue;
-        w.A[i][lane] -= f * w.A[k][lane];
+    if (pv == 0.0) return 0;  // uniform
+    const double inv = 1.0 / pv;
+    const double ak = w.A[k][cl], ap = w.A[p][cl];
+    const double rk = (p != k ? ap : ak) * inv;  // swapped, scaled pivot row
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      double ai;
+      if (i == k) {
+        ai = rk;
+      } else {
+        ai = (i == p) ? ak : w.A[i][cl];        // row p now holds the old row k
+        const double f = (i == p) ? ck : col[i];  // column k after the swap
+        if (f != 0.0) ai -= f * rk;
       }
+      if (lane < 20) w.A[i][lane] = ai;
+    }
     wsync();
   }
   return 1;
 }
 
+// Sign changes of the (zero-padded) Sturm sequence at z. Horner over the 11
+// padded coefficients of each row gives the same value as
+// poly_eval over sd[s] (leading zeros contribute exact signed zeros that the
+// first non-zero coefficient absorbs), rows >= ns are all zero and skipped.
 __device__ int coop_sign_changes(const CoopWS& w, double z) {
   int ch = 0;
   double prev = 0.0;
-  for (int s = 0; s < w.ns; ++s) {
-    const double v = poly_eval(w.S[s], w.sd[s], z);
+#pragma unroll 1
+  for (int s = 0; s < 11; ++s) {
+    double c[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) c[i] = w.S[s][i];
+    double v = c[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) v = v * z + c[i];
     if (v != 0.0) {
       if (prev != 0.0 && ((v < 0.0) != (prev < 0.0))) ++ch;
       prev = v;
@@ -1046,130 +1114,188 @@ __device__ int coop_sign_changes(const CoopWS& w, double z) {
   return ch;
 }
 
-// Bp, the degree-10 polynomial, its Sturm sequence (lane 0); then the 64-ary
-// isolation / refinement with one point per lane. Leaves w.nr sorted roots.
-__device__ void coop_roots(CoopWS& w, int lane) {
-  if (lane == 0) {
-    for (int q = 0; q < 3; ++q) {
-      const double* e = &w.A[4 + 2 * q][10];
-      const double* f = &w.A[5 + 2 * q][10];
-      double* px = w.Bp[q][0];
-      double* py = w.Bp[q][1];
-      double* pc = w.Bp[q][2];
-      px[0] = e[2]; px[1] = e[1] - f[2]; px[2] = e[0] - f[1]; px[3] = -f[0]; px[4] = 0.0;
-      py[0] = e[5]; py[1] = e[4] - f[5]; py[2] = e[3] - f[4]; py[3] = -f[3]; py[4] = 0.0;
-      pc[0] = e[9]; pc[1] = e[8] - f[9]; pc[2] = e[7] - f[8]; pc[3] = e[6] - f[7]; pc[4] = -f[6];
+// pmul coefficient k (terms in increasing i from 0.0, as pmul accumulates)
+__device__ __forceinline__ double pmul_k(const double* a, int da, const double* b, int db, int k) {
+  double s = 0.0;
+  for (int i = 0; i <= da; ++i) {
+    const int j = k - i;
+    if (j >= 0 && j <= db) s += a[i] * b[j];
+  }
+  return s;
+}
+
+// Newton refinement (refine_root) with the polynomial in registers; the
+// derivative coefficients (i + 1) * c[i + 1] are formed on the fly.
+__device__ double refine_root_reg(const double c[11], double a, double b) {
+  auto ev = [&](double z) {
+    double v = c[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) v = v * z + c[i];
+    return v;
+  };
+  double fa = ev(a);
+  double x = 0.5 * (a + b);
+  for (int it = 0; it < 60; ++it) {
+    double fx = c[10], dfx = 10.0 * c[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) {
+      fx = fx * x + c[i];
+      if (i >= 1) dfx = dfx * x + (double)i * c[i];
     }
-    double c1[8], c2[8], c3[8], t1[8], t2[8];
-    pmul(w.Bp[1][1], 3, w.Bp[2][2], 4, t1); pmul(w.Bp[1][2], 4, w.Bp[2][1], 3, t2);
-    for (int i = 0; i < 8; ++i) c1[i] = t1[i] - t2[i];
-    pmul(w.Bp[1][0], 3, w.Bp[2][2], 4, t1); pmul(w.Bp[1][2], 4, w.Bp[2][0], 3, t2);
-    for (int i = 0; i < 8; ++i) c2[i] = t1[i] - t2[i];
-    pmul(w.Bp[1][0], 3, w.Bp[2][1], 3, t1); pmul(w.Bp[1][1], 3, w.Bp[2][0], 3, t2);
-    for (int i = 0; i < 7; ++i) c3[i] = t1[i] - t2[i];
-    c3[7] = 0.0;
-    double u1[11], u2[11], u3[11];
-    pmul(w.Bp[0][0], 3, c1, 7, u1);
-    pmul(w.Bp[0][1], 3, c2, 7, u2);
-    pmul(w.Bp[0][2], 4, c3, 6, u3);
-    for (int i = 0; i < 11; ++i) w.nco[i] = u1[i] - u2[i] + u3[i];
-    // Sturm sequence (same construction as real_roots)
-    int deg = 10;
-    while (deg > 0 && w.nco[deg] == 0.0) --deg;
-    w.deg = deg;
-    w.nr = 0;
-    w.ns = 0;
-    if (deg > 0) {
-      for (int i = 0; i <= deg; ++i) w.S[0][i] = w.nco[i] / w.nco[deg];
-      w.sd[0] = deg;
-      for (int i = 0; i < deg; ++i) w.S[1][i] = (double)(i + 1) * w.S[0][i + 1];
-      w.sd[1] = deg - 1;
-      int ns = 2;
-      while (w.sd[ns - 1] > 0 && ns < 11) {
-        double r[11];
-        const int da = w.sd[ns - 2], db = w.sd[ns - 1];
-        for (int i = 0; i <= da; ++i) r[i] = w.S[ns - 2][i];
-        for (int k = da - db; k >= 0; --k) {
-          const double f = r[k + db] / w.S[ns - 1][db];
-          for (int i = 0; i <= db; ++i) r[k + i] -= f * w.S[ns - 1][i];
-        }
-        int dr = db - 1;
-        double mx = 0.0;
-        for (int i = 0; i <= da; ++i) mx = fmax(mx, fabs(w.S[ns - 2][i]));
-        while (dr >= 0 && fabs(r[dr]) <= 1e-14 * mx) --dr;
-        if (dr < 0) break;
-        for (int i = 0; i <= dr; ++i) w.S[ns][i] = -r[i];
-        w.sd[ns] = dr;
-        ++ns;
+    if (fx == 0.0) return x;
+    if ((fx < 0.0) == (fa < 0.0)) { a = x; fa = fx; }
+    else b = x;
+    double xn = (dfx != 0.0) ? x - fx / dfx : 0.5 * (a + b);
+    if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;  // converged (before the safeguard)
+    if (!(xn > a && xn < b)) {
+      xn = 0.5 * (a + b);
+      if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;
+    }
+    x = xn;
+  }
+  return x;
+}
+
+// Bp, the degree-10 polynomial and its Sturm sequence with lanes owning
+// coefficients (same operations per element as fivept_nister / real_roots),
+// then the 64-ary isolation with one point per lane and one lane per root.
+// Leaves w.nr roots in ascending order in w.roots.
+__device__ void coop_roots(CoopWS& w, int lane, bool prof) {
+  unsigned long long t_prev = prof ? wall_clock64() : 0;
+  if (lane < 45) {  // Bp[q][c][i]
+    const int q = lane / 15, c = (lane / 5) % 3, i = lane % 5;
+    const double* e = &w.A[4 + 2 * q][10];
+    const double* f = &w.A[5 + 2 * q][10];
+    const int base = (c == 2) ? 9 : 3 * c + 2, imax = (c == 2) ? 3 : 2;
+    double v;
+    if (i == 0) v = e[base];
+    else if (i <= imax) v = e[base - i] - f[base - i + 1];
+    else if (i == imax + 1) v = -f[base - imax];
+    else v = 0.0;
+    w.Bp[q][c][i] = v;
+  }
+  for (int t = lane; t < 121; t += RS_BLOCK) (&w.S[0][0])[t] = 0.0;
+  wsync();
+  if (lane < 24) {  // c1 (8), c2 (8), c3 (7 + the zero c3[7])
+    const int g = lane / 8, k = lane % 8;
+    double v;
+    if (g == 0) v = pmul_k(w.Bp[1][1], 3, w.Bp[2][2], 4, k) - pmul_k(w.Bp[1][2], 4, w.Bp[2][1], 3, k);
+    else if (g == 1) v = pmul_k(w.Bp[1][0], 3, w.Bp[2][2], 4, k) - pmul_k(w.Bp[1][2], 4, w.Bp[2][0], 3, k);
+    else v = (k < 7) ? pmul_k(w.Bp[1][0], 3, w.Bp[2][1], 3, k) - pmul_k(w.Bp[1][1], 3, w.Bp[2][0], 3, k) : 0.0;
+    w.cc[g][k] = v;
+  }
+  wsync();
+  double nco = 0.0;
+  if (lane < 11)
+    nco = pmul_k(w.Bp[0][0], 3, w.cc[0], 7, lane) - pmul_k(w.Bp[0][1], 3, w.cc[1], 7, lane) +
+          pmul_k(w.Bp[0][2], 4, w.cc[2], 6, lane);
+  KMX_PT(7);
+  // degree: highest non-zero coefficient (0 when none)
+  const unsigned long long nzm = __ballot(lane >= 1 && lane <= 10 && !(nco == 0.0)) ;
+  const int deg = nzm ? 63 - __clzll(nzm) : 0;
+  int nr = 0;
+  double my_lo = 0.0, my_hi = 0.0;  // lane r: isolating interval of root r
+  double c0 = 0.0;                  // lane i: S[0][i]
+  if (deg > 0) {
+    const double lead = rdlane(nco, deg);
+    double a = (lane <= deg) ? nco / lead : 0.0;
+    c0 = a;
+    const double a_up = __shfl(a, (lane + 1) & 63, 64);
+    double b = (lane < deg) ? (double)(lane + 1) * a_up : 0.0;
+    if (lane <= deg) w.S[0][lane] = a;
+    if (lane < deg) w.S[1][lane] = b;
+    int ns = 2, da = deg, db = deg - 1;
+    while (db > 0 && ns < 11) {
+      double r = a;
+      const double bd = rdlane(b, db);
+      for (int k = da - db; k >= 0; --k) {
+        const double fk = rdlane(r, k + db) / bd;
+        const double bs = __shfl(b, (lane - k) & 63, 64);
+        if (lane >= k && lane <= k + db) r -= fk * bs;
       }
-      w.ns = ns;
-      double bound = 0.0;
-      for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(w.S[0][i]));
-      bound += 1.0;
+      const double mx = wave_fmax((lane <= da) ? fabs(a) : 0.0);
+      const unsigned long long keep = __ballot(lane < db && !(fabs(r) <= 1e-14 * mx));
+      if (!keep) break;
+      const int dr = 63 - __clzll(keep);
+      const double nb = (lane <= dr) ? -r : 0.0;
+      if (lane <= dr) w.S[ns][lane] = nb;
+      a = b;
+      b = nb;
+      da = db;
+      db = dr;
+      ++ns;
+    }
+    // root_bound, lane-parallel (max over exact integer terms)
+    const bool nonfin = lane < deg && !isfinite(c0);
+    double bound;
+    if (__ballot(nonfin)) {
+      bound = wave_fmax((lane < deg) ? fabs(c0) : 0.0) + 1.0;
+    } else {
+      int km = (lane < deg) ? root_bound_term(c0, deg - lane) : INT_MIN;
+      for (int off = 32; off > 0; off >>= 1) km = max(km, __shfl_xor(km, off, 64));
+      bound = (km == INT_MIN) ? 1.0 : ldexp(1.0, km + 1);
+    }
+    wsync();
+    KMX_PT(8);
+    // 64-ary isolation; the stack (LDS) is popped uniformly, pieces are
+    // pushed right to left so the leftmost is popped first (real_roots)
+    if (lane == 0) {
       w.st_lo[0] = -bound; w.st_hi[0] = bound; w.st_d[0] = 0;
-      w.st_vl[0] = coop_sign_changes(w, -bound);
-      w.st_vh[0] = coop_sign_changes(w, bound);
-      w.sp = 1;
-    } else {
-      w.sp = 0;
     }
-  }
-  wsync();
-  const int deg = w.deg;
-  while (w.sp > 0) {  // uniform: the stack lives in LDS
-    const int sp = w.sp - 1;
-    const double lo = w.st_lo[sp], hi = w.st_hi[sp];
-    const int vl = w.st_vl[sp], vh = w.st_vh[sp], dep = w.st_d[sp];
-    const int cnt = vl - vh;
+    const int v_lo = coop_sign_changes(w, -bound);
+    const int v_hi = coop_sign_changes(w, bound);
+    if (lane == 0) { w.st_vl[0] = v_lo; w.st_vh[0] = v_hi; }
+    int sp = 1;
     wsync();
-    if (lane == 0) w.sp = sp;
-    wsync();
-    if (cnt <= 0) continue;
-    if (cnt == 1 || dep >= RR_DEPTH) {  // isolated: refined below, one lane per root
-      if (lane == 0 && w.nr < 10) {
-        w.iv_lo[w.nr] = lo;
-        w.iv_hi[w.nr] = hi;
-        ++w.nr;
-      }
-      wsync();
-      continue;
-    }
-    const double wd = (hi - lo) / RR_SPLIT;
-    if (lane >= 1) {
-      const double x = lo + (double)lane * wd;
-      w.val[lane] = x;
-      w.vi[lane] = coop_sign_changes(w, x);
-    } else {
-      w.val[0] = lo;
-      w.vi[0] = vl;
-    }
-    wsync();
-    if (lane == 0) {  // push pieces right to left (popped in increasing x)
-      int vprev = vh;
-      double xprev = hi;
-      int spn = w.sp;
-      for (int j = RR_SPLIT - 1; j >= 0; --j) {
-        const double xj = w.val[j];
-        const int vj = w.vi[j];
-        if (vj - vprev > 0 && spn < 16) {
-          w.st_lo[spn] = xj; w.st_hi[spn] = xprev; w.st_vl[spn] = vj; w.st_vh[spn] = vprev; w.st_d[spn] = dep + 1;
-          ++spn;
+    while (sp > 0) {
+      --sp;
+      const double lo = w.st_lo[sp], hi = w.st_hi[sp];
+      const int vl = w.st_vl[sp], vh = w.st_vh[sp], dep = w.st_d[sp];
+      const int cnt = vl - vh;
+      if (cnt <= 0) continue;
+      if (cnt == 1 || dep >= RR_DEPTH) {
+        if (nr < 10) {
+          if (lane == nr) { my_lo = lo; my_hi = hi; }
+          ++nr;
         }
-        vprev = vj;
-        xprev = xj;
+        continue;
       }
-      w.sp = spn;
+      const double wd = (hi - lo) / RR_SPLIT;
+      const double x = (lane == 0) ? lo : lo + (double)lane * wd;
+      const int v = (lane == 0) ? vl : coop_sign_changes(w, x);
+      double xn = __shfl(x, (lane + 1) & 63, 64);
+      int vn = __shfl(v, (lane + 1) & 63, 64);
+      if (lane == RS_BLOCK - 1) { xn = hi; vn = vh; }
+      const bool has = v - vn > 0;
+      const unsigned long long hm = __ballot(has);
+      const int above = (lane == RS_BLOCK - 1) ? 0 : __popcll(hm >> (lane + 1));
+      const int slot = sp + above;
+      wsync();  // the popped entry has been read by every lane
+      if (has && slot < 16) {
+        w.st_lo[slot] = x; w.st_hi[slot] = xn; w.st_vl[slot] = v; w.st_vh[slot] = vn; w.st_d[slot] = dep + 1;
+      }
+      sp = min(sp + __popcll(hm), 16);
+      wsync();
     }
-    wsync();
   }
-  if (lane < w.nr) w.roots[lane] = refine_root(w.S[0], deg, w.iv_lo[lane], w.iv_hi[lane]);
-  wsync();
-  if (lane == 0) {  // ascending order
-    for (int a = 0; a < w.nr; ++a)
-      for (int b = 0; b + 1 < w.nr - a; ++b)
-        if (w.roots[b] > w.roots[b + 1]) { const double t = w.roots[b]; w.roots[b] = w.roots[b + 1]; w.roots[b + 1] = t; }
+  KMX_PT(9);
+  double root = 0.0;
+  if (lane < nr) {
+    double c[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) c[i] = w.S[0][i];
+    root = refine_root_reg(c, my_lo, my_hi);
   }
+  // ascending order (stable rank = the bubble sort's order)
+  int rank = 0;
+  for (int j = 0; j < nr; ++j) {
+    const double rj = rdlane(root, j);
+    if (rj < root || (rj == root && j < lane)) ++rank;
+  }
+  if (lane < nr) w.roots[rank] = root;
+  if (lane == 0) w.nr = nr;
   wsync();
+  KMX_PT(10);
 }
 
 // Essential matrices from the roots (lane per root), then per E (lane per E)
@@ -1203,14 +1329,11 @@ __device__ void coop_models(CoopWS& w, int lane) {
   // compact the surviving roots in root order (fivept_nister's ns counter)
   const unsigned long long m = __ballot(ok_root);
   const int slot = __popcll(m & ((1ull << lane) - 1ull));
-  if (ok_root)
-    for (int e = 0; e < 9; ++e) w.Es[slot][e] = Eo[e];
   const int ne = __popcll(m);
-  wsync();
-  double best = DBL_MAX;
-  if (lane < ne) {
+  if (ok_root) {
+    // the two rotations and the translation direction of E (lane per E)
     double U[9], s[3], V[9];
-    svd3(w.Es[lane], U, s, V);
+    svd3(Eo, U, s, V);
     double Ra[9], Rb[9];
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) {
@@ -1219,54 +1342,41 @@ __device__ void coop_models(CoopWS& w, int lane) {
         const double uv0 = -U[i * 3 + 1], uv1 = U[i * 3 + 0], uv2 = U[i * 3 + 2];
         Rb[i * 3 + j] = uv0 * V[j * 3 + 0] + uv1 * V[j * 3 + 1] + uv2 * V[j * 3 + 2];
       }
-    if (det3(Ra) < 0.0)
-      for (int i = 0; i < 9; ++i) Ra[i] = -Ra[i];
-    if (det3(Rb) < 0.0)
-      for (int i = 0; i < 9; ++i) Rb[i] = -Rb[i];
-    const double tu[3] = {U[0 * 3 + 2], U[1 * 3 + 2], U[2 * 3 + 2]};
-    for (int cand = 0; cand < 4; ++cand) {
-      const double* Rc = (cand < 2) ? Ra : Rb;
-      const double sg = (cand & 1) ? -1.0 : 1.0;
-      const double tc[3] = {sg * tu[0], sg * tu[1], sg * tu[2]};
-      double err = 0.0;
-      for (int i = 0; i < 5; ++i) err += model_error(Rc, tc, w.f1 + 3 * i, w.f2 + 3 * i);
-      if (err < best) {
-        best = err;
-        for (int i = 0; i < 9; ++i) w.bR[lane][i] = Rc[i];
-        for (int i = 0; i < 3; ++i) w.bt[lane][i] = tc[i];
-      }
+    const bool na = det3(Ra) < 0.0, nb = det3(Rb) < 0.0;
+    for (int i = 0; i < 9; ++i) {
+      w.Rab[slot][0][i] = na ? -Ra[i] : Ra[i];
+      w.Rab[slot][1][i] = nb ? -Rb[i] : Rb[i];
     }
-    w.berr[lane] = best;
+    for (int i = 0; i < 3; ++i) w.tu[slot][i] = U[i * 3 + 2];
   }
   wsync();
-  if (lane == 0) {
-    int win = -1;
-    double bb = DBL_MAX;
-    for (int e = 0; e < ne; ++e)
-      if (w.berr[e] < bb) { bb = w.berr[e]; win = e; }
-    w.ok = (win >= 0) ? 1 : 0;
-    if (win >= 0) {
-      for (int i = 0; i < 9; ++i) w.mR[i] = w.bR[win][i];
-      for (int i = 0; i < 3; ++i) w.mt[i] = w.bt[win][i];
-    }
+  // lane per (E, candidate): error of the decomposition on the sample
+  const bool act = lane < 4 * ne;
+  double err = DBL_MAX;
+  double R[9], t[3];
+  if (act) {
+    const int e = lane >> 2, cand = lane & 3;
+    for (int i = 0; i < 9; ++i) R[i] = w.Rab[e][cand >> 1][i];
+    const double sg = (cand & 1) ? -1.0 : 1.0;
+    for (int i = 0; i < 3; ++i) t[i] = sg * w.tu[e][i];
+    err = 0.0;
+    for (int i = 0; i < 5; ++i) err += model_error(R, t, w.f1 + 3 * i, w.f2 + 3 * i);
+  }
+  // the first minimum in (E, candidate) order among errors < DBL_MAX
+  const bool valid = act && err < DBL_MAX;
+  double mn = valid ? err : DBL_MAX;
+  for (int off = 32; off > 0; off >>= 1) mn = fmin(mn, __shfl_xor(mn, off, 64));
+  const unsigned long long wm = __ballot(valid && err == mn);
+  if (lane == 0) w.ok = wm ? 1 : 0;
+  if (wm && lane == __ffsll((long long)wm) - 1) {
+    for (int i = 0; i < 9; ++i) w.mR[i] = R[i];
+    for (int i = 0; i < 3; ++i) w.mt[i] = t[i];
   }
   wsync();
 }
 
-// Diagnostic phase timers (kmx_lcd_debug_phase_times): cycles per phase summed
-// over the first 64 candidates' hypotheses.
-__device__ unsigned long long g_phase[16];
-#define KMX_PT(i)                                                              \
-  do {                                                                         \
-    if (prof && lane == 0) {                                                   \
-      const unsigned long long t_ = wall_clock64();                            \
-      atomicAdd(&g_phase[i], t_ - t_prev);                                     \
-      t_prev = t_;                                                             \
-    }                                                                          \
-  } while (0)
-
 // One hypothesis: sample -> models (w.ok, w.mR, w.mt).
-__device__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const double* F2, const short* smp,
+__device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const double* F2, const short* smp,
                                 bool prof) {
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   if (lane < 15) {
@@ -1286,7 +1396,7 @@ __device__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const dou
     return;
   }
   KMX_PT(3);
-  coop_roots(w, lane);
+  coop_roots(w, lane, prof);
   KMX_PT(4);
   if (w.nr == 0) {
     if (lane == 0) w.ok = 0;
@@ -1330,6 +1440,8 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
       F2[3 * j + k] = bearings[((size_t)m * N + pr.y) * 3 + k];
     }
   }
+  for (int t = lane; t < 40; t += RS_BLOCK) (&w.t11[0][0][0])[t] = (&T11[0][0][0])[t];
+  for (int t = lane; t < 120; t += RS_BLOCK) (&w.t21[0][0][0])[t] = (&T21[0][0][0])[t];
   __threadfence_block();
   wsync();
   int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
@@ -1933,9 +2045,10 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
     if (h->ransac == 1) {
       static const int clb = [] {
         const char* v = std::getenv("KMX_COOP_LB");
-        return v ? std::atoi(v) : 8;
+        return v ? std::atoi(v) : 4;
       }();
-      auto kc = (clb >= 8) ? k_ransac_coop<8> : k_ransac_coop<4>;
+      auto kc = (clb >= 8) ? k_ransac_coop<8> : (clb >= 6) ? k_ransac_coop<6> : (clb >= 5) ? k_ransac_coop<5>
+                                                                                             : k_ransac_coop<4>;
       hipLaunchKernelGGL(kc, dim3(n), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
                          (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
                          (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,

@@ -167,6 +167,7 @@ static double det3(const double M[9]) {
 static void sym_eig3(double A[9], double V[9]) {
   for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 12; ++sweep) {
+    if (A[1] == 0.0 && A[2] == 0.0 && A[5] == 0.0) break; /* every rotation would be skipped */
     for (int p = 0; p < 2; ++p)
       for (int q = p + 1; q < 3; ++q) {
         const double apq = A[p * 3 + q];
@@ -314,11 +315,38 @@ static double refine_root(const double* c, int deg, double a, double b) {
     else b = x;
     const double dfx = poly_eval(dc, deg - 1, x);
     double xn = (dfx != 0.0) ? x - fx / dfx : 0.5 * (a + b);
-    if (!(xn > a && xn < b)) xn = 0.5 * (a + b);
-    if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;
+    if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;  /* converged (before the safeguard) */
+    if (!(xn > a && xn < b)) {
+      xn = 0.5 * (a + b);
+      if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;
+    }
     x = xn;
   }
   return x;
+}
+
+/* Root bound of the monic a (degree deg), Fujiwara's
+ *   |z| <= 2 max_i |a_i|^(1/(deg-i))
+ * with every term rounded up to a power of two by exponent arithmetic only
+ * (ilogb / ldexp are exact, so host and device agree bit for bit):
+ * |a_i| < 2^(e+1), e = ilogb(a_i) => term <= 2^ceil((e+1)/(deg-i)). Non-finite
+ * coefficients fall back to Cauchy's 1 + max |a_i|; p = z^deg gives 1. */
+static double root_bound(const double* a, int deg) {
+  int kmax = INT_MIN, fin = 1;
+  double cauchy = 0.0;
+  for (int i = 0; i < deg; ++i) {
+    cauchy = fmax(cauchy, fabs(a[i]));
+    if (!isfinite(a[i])) {
+      fin = 0;
+    } else if (a[i] != 0.0) {
+      const int x = ilogb(a[i]) + 1, m = deg - i;
+      const int k = x >= 0 ? (x + m - 1) / m : -((-x) / m);
+      if (k > kmax) kmax = k;
+    }
+  }
+  if (!fin) return cauchy + 1.0;
+  if (kmax == INT_MIN) return 1.0;
+  return ldexp(1.0, kmax + 1);
 }
 
 /* real roots of a polynomial (ascending coefficients) by Sturm-sequence
@@ -352,9 +380,7 @@ static int real_roots(const double* coef, int deg_in, double* roots) {
     sd[ns] = dr;
     ++ns;
   }
-  double bound = 0.0;
-  for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(S[0][i]));
-  bound += 1.0;
+  const double bound = root_bound(S[0], deg);
 #define SIGNCH(zv, out)                                        \
   do {                                                         \
     int ch_ = 0;                                               \

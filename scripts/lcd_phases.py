@@ -25,3 +25,5 @@ tot = sum(buf[i] for i in range(7))
 print(f"hypotheses (first 64 candidates): {hyp}")
 for i, n in enumerate(names):
     print(f"{n:10s} {buf[i] / 100.0 / max(hyp, 1):9.2f} us/hypothesis  {100.0 * buf[i] / max(tot, 1):5.1f} %")
+for i, n in zip(range(7, 11), ["  poly", "  sturm", "  isolate", "  refine"]):
+    print(f"{n:10s} {buf[i] / 100.0 / max(hyp, 1):9.2f} us/hypothesis (within roots)")

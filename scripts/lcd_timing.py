@@ -11,6 +11,8 @@ t = time.time(); pool = make_lcd_pool(n, 500, seed=0); print("gen", time.time() 
 det = LoopClosureDetector(LcdParams()); det.set_pool(pool)
 det.verify(pool.cand_query[:64], pool.cand_match[:64])
 for rep in range(2):
+    t = time.time(); det.verify_async(pool.cand_query, pool.cand_match); det.sync(); el_gpu = time.time() - t
+    print(f"verify_async: {n} candidates in {el_gpu*1e3:.1f} ms -> {n/el_gpu:.0f} cand/s", flush=True)
     t = time.time(); res, _ = det.verify(pool.cand_query, pool.cand_match); el = time.time() - t
     acc = sum(r["accepted"] for r in res)
     print(f"{n} candidates in {el*1e3:.1f} ms -> {n/el:.0f} cand/s, accepted {acc}, mean iters "
