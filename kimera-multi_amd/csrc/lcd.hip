@@ -134,6 +134,13 @@ __device__ void sym_eig3(double A[9], double V[9]) {
         const double apq = A[p * 3 + q];
         if (apq == 0.0) continue;
         const double app = A[p * 3 + p], aqq = A[q * 3 + q];
+        // negligible next to both diagonal entries: zero it (Numerical Recipes' jacobi rule)
+        const double g = 100.0 * fabs(apq);
+        if (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq)) {
+          A[p * 3 + q] = 0.0;
+          A[q * 3 + p] = 0.0;
+          continue;
+        }
         const double theta = (aqq - app) / (2.0 * apq);
         const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
         const double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
@@ -886,7 +893,7 @@ struct CoopWS {
       double tr[10];
     };
     struct {                  // roots
-      double S[11][11];       // Sturm sequence, zero padded
+      double S[12][11];       // Sturm sequence, zero padded (row 11: always zero)
       double cc[3][8];        // c1, c2, c3 of the degree-10 polynomial
       double st_lo[16], st_hi[16];
       int st_vl[16], st_vh[16], st_d[16];
@@ -1054,15 +1061,18 @@ __device__ void coop_system(CoopWS& w, int lane) {
 
 // Gauss-Jordan with partial pivoting on the 10x20 system (serial order per
 // element; lanes own columns). Returns 0 on a zero pivot.
-// Every lane reads column k at once (10 independent broadcast loads) and picks
-// the pivot in registers; the multipliers are column k after the swap; each
-// lane then updates its own column row by row.
+// Lanes own columns (lane c < 20 holds A[0..9][c] in registers); column k
+// is broadcast with readlane, so a pivot step touches no LDS. Same
+// operations per element as the serial elimination (fivept_nister).
 __device__ int coop_gj(CoopWS& w, int lane) {
   const int cl = lane < 20 ? lane : 19;  // lanes >= 20 shadow column 19, never store
+  double a[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) a[i] = w.A[i][cl];
   for (int k = 0; k < 10; ++k) {
     double col[10];
 #pragma unroll
-    for (int i = 0; i < 10; ++i) col[i] = w.A[i][k];
+    for (int i = 0; i < 10; ++i) col[i] = rdlane(a[i], k);
     int p = k;
     double pv = 0.0, pa = -1.0, ck = 0.0;
 #pragma unroll
@@ -1072,22 +1082,30 @@ __device__ int coop_gj(CoopWS& w, int lane) {
     }
     if (pv == 0.0) return 0;  // uniform
     const double inv = 1.0 / pv;
-    const double ak = w.A[k][cl], ap = w.A[p][cl];
-    const double rk = (p != k ? ap : ak) * inv;  // swapped, scaled pivot row
+    double ak = 0.0, ap = 0.0;
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-      double ai;
+      ak = (i == k) ? a[i] : ak;
+      ap = (i == p) ? a[i] : ap;
+    }
+    const double rk = ap * inv;  // swapped (p == k: ap == ak), scaled pivot row
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
       if (i == k) {
-        ai = rk;
+        a[i] = rk;
       } else {
-        ai = (i == p) ? ak : w.A[i][cl];        // row p now holds the old row k
+        double ai = (i == p) ? ak : a[i];         // row p now holds the old row k
         const double f = (i == p) ? ck : col[i];  // column k after the swap
         if (f != 0.0) ai -= f * rk;
+        a[i] = ai;
       }
-      if (lane < 20) w.A[i][lane] = ai;
     }
-    wsync();
   }
+  if (lane < 20) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) w.A[i][lane] = a[i];
+  }
+  wsync();
   return 1;
 }
 
@@ -1098,18 +1116,28 @@ __device__ int coop_gj(CoopWS& w, int lane) {
 __device__ int coop_sign_changes(const CoopWS& w, double z) {
   int ch = 0;
   double prev = 0.0;
-#pragma unroll 1
-  for (int s = 0; s < 11; ++s) {
-    double c[11];
-#pragma unroll
-    for (int i = 0; i < 11; ++i) c[i] = w.S[s][i];
-    double v = c[10];
-#pragma unroll
-    for (int i = 9; i >= 0; --i) v = v * z + c[i];
+  auto step = [&](double v) {
     if (v != 0.0) {
       if (prev != 0.0 && ((v < 0.0) != (prev < 0.0))) ++ch;
       prev = v;
     }
+  };
+#pragma unroll 1
+  for (int s = 0; s < 12; s += 2) {  // two independent Horner chains (row 11 is zero)
+    double c0[11], c1[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) {
+      c0[i] = w.S[s][i];
+      c1[i] = w.S[s + 1][i];
+    }
+    double v0 = c0[10], v1 = c1[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) {
+      v0 = v0 * z + c0[i];
+      v1 = v1 * z + c1[i];
+    }
+    step(v0);
+    step(v1);
   }
   return ch;
 }
@@ -1174,7 +1202,7 @@ __device__ void coop_roots(CoopWS& w, int lane, bool prof) {
     else v = 0.0;
     w.Bp[q][c][i] = v;
   }
-  for (int t = lane; t < 121; t += RS_BLOCK) (&w.S[0][0])[t] = 0.0;
+  for (int t = lane; t < 132; t += RS_BLOCK) (&w.S[0][0])[t] = 0.0;
   wsync();
   if (lane < 24) {  // c1 (8), c2 (8), c3 (7 + the zero c3[7])
     const int g = lane / 8, k = lane % 8;
@@ -1213,7 +1241,9 @@ __device__ void coop_roots(CoopWS& w, int lane, bool prof) {
         const double bs = __shfl(b, (lane - k) & 63, 64);
         if (lane >= k && lane <= k + db) r -= fk * bs;
       }
-      const double mx = wave_fmax((lane <= da) ? fabs(a) : 0.0);
+      double mx = 0.0;  // max |S[ns-2][i]|, i <= da (lanes above da hold 0)
+#pragma unroll
+      for (int i = 0; i < 11; ++i) mx = fmax(mx, fabs(rdlane(a, i)));
       const unsigned long long keep = __ballot(lane < db && !(fabs(r) <= 1e-14 * mx));
       if (!keep) break;
       const int dr = 63 - __clzll(keep);

@@ -173,6 +173,13 @@ static void sym_eig3(double A[9], double V[9]) {
         const double apq = A[p * 3 + q];
         if (apq == 0.0) continue;
         const double app = A[p * 3 + p], aqq = A[q * 3 + q];
+        /* negligible next to both diagonal entries: zero it (Numerical Recipes' jacobi rule) */
+        const double g = 100.0 * fabs(apq);
+        if (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq)) {
+          A[p * 3 + q] = 0.0;
+          A[q * 3 + p] = 0.0;
+          continue;
+        }
         const double theta = (aqq - app) / (2.0 * apq);
         const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
         const double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
