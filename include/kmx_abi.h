@@ -150,6 +150,14 @@ int kmx_pgo_public_count(kmx_pgo* h, int64_t* n_public, int64_t* first_owned,
 int kmx_pgo_pack_public(kmx_pgo* h, void* dev_out);
 int kmx_pgo_unpack_public(kmx_pgo* h, const void* dev_table);
 int kmx_pgo_refresh_local(kmx_pgo* h);
+/* Sparse form of the same exchange (one all-to-all instead of an all-gather):
+ * gather_public_rows writes the rows of `n` public slots OWNED by this handle
+ * (dev_slots: int32 device array of table slots) to dev_out (n * 4r doubles);
+ * scatter_public_rows installs n rows received from peers at the given slots.
+ * Only the neighbour rows a handle's shared loop closures reference cross the
+ * link; refresh_local fills the owned slots. */
+int kmx_pgo_gather_public_rows(kmx_pgo* h, const int32_t* dev_slots, int64_t n, void* dev_out);
+int kmx_pgo_scatter_public_rows(kmx_pgo* h, const int32_t* dev_slots, int64_t n, const void* dev_rows);
 int kmx_pgo_set_neighbor_poses(kmx_pgo* h, int64_t count, const int32_t* robot,
                                const int32_t* pose, const double* X);
 

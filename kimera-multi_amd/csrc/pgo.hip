@@ -585,7 +585,7 @@ __device__ __forceinline__ void lane_gather_compact(const Dev& d, const Lane& L,
 // (the continuation) writes H[group]. The (pose, row) lanes then add
 // A[pose] + H[g] for the pose's later segments in order, so the result is
 // deterministic and independent of everything but the tiling.
-template <int R, bool PUB, bool OWN>
+template <int R, bool PUB, bool OWN, bool COOP = false>
 __device__ __forceinline__ void tile_gather_bal(const Dev& d, const Lane& L, const double* V, const double* pub,
                                                 double acc[4], double* cost, char* smem) {
   using SM = Smem<R>;
@@ -645,8 +645,25 @@ __device__ __forceinline__ void tile_gather_bal(const Dev& d, const Lane& L, con
       }
       const double2* q2 = reinterpret_cast<const double2*>(rec + 12 * (size_t)(K0 + k));
       double2 q[6];
+      if constexpr (COOP) {
+        // the group's lanes load the record's six 16-B chunks once between
+        // them (chunk i in lane i % R) and broadcast them by shuffles
+        constexpr int NL = (6 + R - 1) / R;
+        double2 mine[NL];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) q[i] = q2[i];
+        for (int u = 0; u < NL; ++u) {
+          const int ci = L.a + u * R;
+          mine[u] = (ci < 6) ? q2[ci] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          q[i].x = __shfl(mine[i / R].x, L.base + i % R, 64);
+          q[i].y = __shfl(mine[i / R].y, L.base + i % R, 64);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) q[i] = q2[i];
+      }
       const int2 in = unpack_int2(q[5].y);
       const int o = in.x;
       const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V);
@@ -680,6 +697,180 @@ __device__ __forceinline__ void tile_gather_bal(const Dev& d, const Lane& L, con
   }
 }
 
+// LDS-staged chunked gather (G = 7; G = 8: owner-only cost). The tile's
+// incidences are cut into segments of SEG consecutive incidences; chunk c
+// holds the NG = TP segments [c NG, (c + 1) NG), one per lane group. Per chunk:
+//   * the chunk's compact records (one contiguous range, 96 B each) are
+//     copied into LDS by the whole workgroup with full-line 16-B loads, so an
+//     edge record crosses L2 -> L1 once instead of once per row lane and per
+//     partially used line; the NEXT chunk's records are loaded into registers
+//     while this chunk is computed (register-staged double buffer);
+//   * every group reads its SEG neighbour indices from LDS and issues all SEG
+//     neighbour-row loads at once, then consumes them in order;
+//   * (group, pose) partials are flushed as in G = 5: the segment holding a
+//     pose's first incidence writes A[pose], a segment that starts inside a
+//     pose writes H[group]; after a barrier the (pose, row) lanes add their
+//     pose's continuation segments of the chunk in segment order.
+// Every pose's sum is therefore a fixed function of the tiling (deterministic).
+template <int R, int SEG>
+struct SmemL {
+  static constexpr int PPW = 64 / R;
+  static constexpr int TP = WAVES * PPW;  // poses per tile = lane groups per workgroup
+  static constexpr int NG = TP;
+  static constexpr int CH = NG * SEG;     // incidences per chunk
+  static constexpr int NSL = (CH * 6 + BLOCK - 1) / BLOCK;  // 16-B staging slots per thread
+  static constexpr int ptr_off = 0;                                      // int[TP + 1]
+  static constexpr int a_off = ((TP + 1) * 4 + 15) / 16 * 16;            // double[TP][R][4]
+  static constexpr int h_off = a_off + TP * R * 32;                      // double[NG][R][4]
+  static constexpr int rec_off = h_off + NG * R * 32;                    // double[CH][12]
+  static constexpr int red_off = rec_off + CH * 96;
+  static constexpr int bytes = red_off + 64;
+};
+#ifndef KMX_SEG
+#define KMX_SEG 4
+#endif
+#ifndef KMX_GATHER_DEFAULT
+#define KMX_GATHER_DEFAULT 5
+#endif
+
+template <int R, bool PUB, bool OWN, int SEG>
+__device__ __forceinline__ void tile_gather_lds(const Dev& d, const Lane& L, const double* V, const double* pub,
+                                                double acc[4], double* cost, char* smem) {
+  using SM = SmemL<R, SEG>;
+  constexpr int NG = SM::NG, CH = SM::CH, NSL = SM::NSL;
+  int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
+  double* A = reinterpret_cast<double*>(smem + SM::a_off);
+  double* H = reinterpret_cast<double*>(smem + SM::h_off);
+  double2* lrec = reinterpret_cast<double2*>(smem + SM::rec_off);
+  const int* ptr = OWN ? d.optr : d.inc_ptr;
+  const double2* grec = reinterpret_cast<const double2*>(OWN ? d.ocrec : d.crec);
+  const int tid = threadIdx.x;
+  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
+  const int K0 = ptr[p0];
+  grec += (size_t)K0 * 6;
+  __syncthreads();  // LDS reuse across consecutive gathers in one kernel (k_eval)
+  if (tid <= np) sptr[tid] = ptr[p0 + tid] - K0;
+  __syncthreads();
+  const int n = sptr[np];
+  const int nch = (n + CH - 1) / CH;
+  const int g = L.w * (64 / R) + L.pw;
+  const bool gvalid = (L.pw < 64 / R);
+  double2 stg[NSL];
+  auto issue = [&](int c) {
+    const int base = c * CH * 6, cnt = min(CH, n - c * CH) * 6;
+#pragma unroll
+    for (int i = 0; i < NSL; ++i) {
+      const int j = tid + i * BLOCK;
+      if (j < cnt) stg[i] = grec[base + j];
+    }
+  };
+  auto commit = [&](int c) {
+    const int cnt = min(CH, n - c * CH) * 6;
+#pragma unroll
+    for (int i = 0; i < NSL; ++i) {
+      const int j = tid + i * BLOCK;
+      if (j < cnt) lrec[j] = stg[i];
+    }
+  };
+  double csum = 0.0;
+  if (nch > 0) issue(0);
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();  // the previous chunk's records and H are no longer read
+    commit(c);
+    __syncthreads();
+    const int s = c * NG + g;
+    const int k0 = s * SEG, k1 = min(k0 + SEG, n);
+    const bool work = gvalid && k0 < k1;
+    double2 nb[SEG][2];
+    if (work) {
+#pragma unroll
+      for (int j = 0; j < SEG; ++j) {
+        nb[j][0] = nb[j][1] = make_double2(0.0, 0.0);
+        if (k0 + j < k1) {
+          const int o = unpack_int2(lrec[(k0 + j - c * CH) * 6 + 5].y).x;
+          if (o >= 0 || PUB) {
+            const double* base = (o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R;
+            const double2* b2 = reinterpret_cast<const double2*>(base + 4 * L.a);
+            nb[j][0] = b2[0];
+            nb[j][1] = b2[1];
+          }
+        }
+      }
+    }
+    if (c + 1 < nch) issue(c + 1);  // next chunk's records fly while this one computes
+    if (work) {
+      int lo = 0, hi = np;  // pose containing k0: sptr[lo] <= k0 < sptr[lo + 1]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (sptr[mid] <= k0) lo = mid;
+        else hi = mid;
+      }
+      while (sptr[lo + 1] <= k0) ++lo;  // skip zero-degree poses
+      int p = lo;
+      bool head = k0 > sptr[p];
+      int pend = sptr[p + 1];
+      double vs[4];
+      load4(V + (size_t)(p0 + p) * 4 * R + 4 * L.a, vs);
+      double part[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int j = 0; j < SEG; ++j) {
+        const int k = k0 + j;
+        if (k < k1) {
+          if (k >= pend) {  // next pose: flush this one's partial
+            if constexpr (!OWN) store4((head ? H + (g * R + L.a) * 4 : A + (p * R + L.a) * 4), part);
+            part[0] = part[1] = part[2] = part[3] = 0.0;
+            head = false;
+            do ++p;
+            while (sptr[p + 1] <= k);
+            pend = sptr[p + 1];
+            load4(V + (size_t)(p0 + p) * 4 * R + 4 * L.a, vs);
+          }
+          const double2* q2 = lrec + (k - c * CH) * 6;
+          double2 q[6];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) q[i] = q2[i];
+          Edge E;
+          edge_from_compact(q, E);
+          const int2 in = unpack_int2(q[5].y);
+          const double vo[4] = {nb[j][0].x, nb[j][0].y, nb[j][1].x, nb[j][1].y};
+          const double cc = incidence_row(E, (in.y >> 31) & 1, vs, vo, part);
+          csum += (OWN || in.x < 0) ? cc : 0.5 * cc;
+        }
+      }
+      if constexpr (!OWN) store4((head ? H + (g * R + L.a) * 4 : A + (p * R + L.a) * 4), part);
+    }
+    if constexpr (!OWN) {
+      __syncthreads();
+      if (L.valid) {  // fold this chunk's continuation segments of the lane's pose
+        const int p = L.pose - p0;
+        const int e0 = sptr[p], e1 = sptr[p + 1];
+        if (e1 > e0) {
+          const int sf = e0 / SEG, sl = (e1 - 1) / SEG;
+          const int lo = max(sf + 1, c * NG), hi = min(sl, c * NG + NG - 1);
+          if (lo <= hi) {
+            double a4[4];
+            load4(A + (p * R + L.a) * 4, a4);
+            for (int ss = lo; ss <= hi; ++ss) {
+              double h4[4];
+              load4(H + ((ss - c * NG) * R + L.a) * 4, h4);
+              a4[0] += h4[0]; a4[1] += h4[1]; a4[2] += h4[2]; a4[3] += h4[3];
+            }
+            store4(A + (p * R + L.a) * 4, a4);
+          }
+        }
+      }
+    }
+  }
+  if (cost) *cost += csum;
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  if constexpr (!OWN) {
+    if (L.valid) {
+      const int p = L.pose - p0;
+      if (sptr[p + 1] > sptr[p]) load4(A + (p * R + L.a) * 4, acc);  // the last fold's own writes
+    }
+  }
+}
+
 template <int R, int G, bool PUB>
 __device__ __forceinline__ void gather(const Dev& d, const Lane& L, const double* V, const double* pub,
                                        double acc[4], double* cost, char* smem) {
@@ -689,8 +880,27 @@ __device__ __forceinline__ void gather(const Dev& d, const Lane& L, const double
   else if constexpr (G == 4) lane_gather_compact<R, PUB, true>(d, L, V, pub, acc, cost);
   else if constexpr (G == 5) tile_gather_bal<R, PUB, false>(d, L, V, pub, acc, cost, smem);
   else if constexpr (G == 6) tile_gather_bal<R, PUB, true>(d, L, V, pub, acc, cost, smem);
+  else if constexpr (G == 7) tile_gather_lds<R, PUB, false, KMX_SEG>(d, L, V, pub, acc, cost, smem);
+  else if constexpr (G == 8) tile_gather_lds<R, PUB, true, KMX_SEG>(d, L, V, pub, acc, cost, smem);
+  else if constexpr (G == 9) tile_gather_bal<R, PUB, false, true>(d, L, V, pub, acc, cost, smem);
+  else if constexpr (G == 10) tile_gather_bal<R, PUB, true, true>(d, L, V, pub, acc, cost, smem);
   else tile_gather<R, PUB>(d, L, V, pub, acc, cost, smem);
 }
+
+// LDS footprint of a gather kernel by variant (the reduction scratch follows it).
+template <int R, int G>
+struct SmemG {
+  static constexpr int red_off = Smem<R>::red_off;
+  static constexpr int bytes = Smem<R>::bytes;
+};
+template <int R>
+struct SmemG<R, 7> {
+  static constexpr int red_off = SmemL<R, KMX_SEG>::red_off;
+  static constexpr int bytes = SmemL<R, KMX_SEG>::bytes;
+};
+template <int R>
+struct SmemG<R, 8> : SmemG<R, 7> {};
+
 
 // -------------------------------------------- fused per-robot reductions --
 // Each tile of robot l publishes its partial sums, then takes a ticket on
@@ -878,7 +1088,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_, HostS
 // Start of an RTR iteration: egrad (gather X with public neighbours), cost,
 // S = sym(Y^T egrad_Y), g = P_Y(egrad), r = g, z = precon(g).
 template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK, KMX_LB_GATHER) void k_grad(Dev d) {
+__global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_grad(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_START) return;
@@ -913,14 +1123,14 @@ __global__ __launch_bounds__(BLOCK, KMX_LB_GATHER) void k_grad(Dev d) {
   // separate reduce launch: store first (frees S, g, z before the block sum);
   // fused reduction: ticket first, so its drain waits only for the partials
   if constexpr (!F) store();
-  finish_tile<RED_GRAD, 3, F>(d, L, vals, smem + Smem<R>::red_off, R);
+  finish_tile<RED_GRAD, 3, F>(d, L, vals, smem + SmemG<R, GV>::red_off, R);
   if constexpr (F) store();
 }
 
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old.
 template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK, KMX_LB_GATHER) void k_hess(Dev d) {
+__global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_hess(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   const Ctl& c = d.ctl[L.l];
@@ -961,7 +1171,7 @@ __global__ __launch_bounds__(BLOCK, KMX_LB_GATHER) void k_hess(Dev d) {
     }
     v = dl[0] * hdl[0] + dl[1] * hdl[1] + dl[2] * hdl[2] + dl[3] * hdl[3];
   }
-  finish_tile<RED_HESS, 1, F>(d, L, &v, smem + Smem<R>::red_off, R);
+  finish_tile<RED_HESS, 1, F>(d, L, &v, smem + SmemG<R, GV>::red_off, R);
   if (L.valid) {
     store4(d.del + o, dl);
     store4(d.hd + o, hdl);
@@ -1049,13 +1259,13 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
 }
 
 template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK, KMX_LB_GATHER) void k_cost(Dev d) {
+__global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_cost(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
   double acc[4], cost = 0.0;
-  gather<R, (GV == 3 ? 4 : GV == 5 ? 6 : GV), true>(d, L, d.Xt, d.pub, acc, &cost, smem);
-  finish_tile<RED_COST, 1, F>(d, L, &cost, smem + Smem<R>::red_off, R);
+  gather<R, (GV == 3 ? 4 : GV == 5 ? 6 : GV == 7 ? 8 : GV), true>(d, L, d.Xt, d.pub, acc, &cost, smem);
+  finish_tile<RED_COST, 1, F>(d, L, &cost, smem + SmemG<R, GV>::red_off, R);
 }
 
 template <int R>
@@ -1088,6 +1298,29 @@ __global__ void k_publish(const double* X, double* pub, const int* src, int nslo
   const int q = (int)(i - s * ps);
   const int p = src[s];
   if (p >= 0) pub[s * ps + q] = X[(long long)p * ps + q];
+}
+
+// Sparse exchange: rows of the given public slots (owned by this handle) from
+// the iterate, and rows received from peers written into the table.
+// A slot outside the table (or, for gather, not owned here) is skipped
+// (gather writes zeros), so a bad index list cannot fault the device.
+__global__ void k_gather_slots(const double* X, const int* pub_src, const int* slots, long long n, int npub,
+                               double* out, int ps) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long s = i / ps;
+  if (s >= n) return;
+  const int q = (int)(i - s * ps);
+  const int sl = slots[s];
+  const int p = (sl >= 0 && sl < npub) ? pub_src[sl] : -1;
+  out[i] = (p >= 0) ? X[(long long)p * ps + q] : 0.0;
+}
+__global__ void k_scatter_slots(double* pub, const int* slots, long long n, int npub, const double* rows, int ps) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long s = i / ps;
+  if (s >= n) return;
+  const int q = (int)(i - s * ps);
+  const int sl = slots[s];
+  if (sl >= 0 && sl < npub) pub[(long long)sl * ps + q] = rows[i];
 }
 
 __global__ void k_pack(const double* X, double* out, const int* src, int first, int count, int ps) {
@@ -1331,7 +1564,7 @@ __global__ __launch_bounds__(BLOCK) void k_eval(Dev d, int robot, int mode, cons
     store4(out + o, res);
     if (mode != KMX_EVAL_COST_EGRAD) s = v[0] * res[0] + v[1] * res[1] + v[2] * res[2] + v[3] * res[3];
   }
-  const double t = block_sum(s, reinterpret_cast<double*>(smem + Smem<R>::red_off));
+  const double t = block_sum(s, reinterpret_cast<double*>(smem + SmemG<R, GV>::red_off));
   if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
 }
 
@@ -1404,7 +1637,7 @@ __global__ __launch_bounds__(BLOCK, LBW) void k_gbench(Dev d, const double* V, d
   double acc[4], cost = 0.0;
   gather<R, GV, true>(d, L, V, d.pub, acc, &cost, smem);
   if (L.valid) store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
-  const double t = block_sum(cost, reinterpret_cast<double*>(smem + Smem<R>::red_off));
+  const double t = block_sum(cost, reinterpret_cast<double*>(smem + SmemG<R, GV>::red_off));
   if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
 }
 
@@ -1437,6 +1670,7 @@ struct kmx_pgo {
   int n_sh_local = 0, n_gnc = 0;
   std::vector<long long> m_robot;
   int ntiles = 0, tile_poses = 0;
+  std::vector<int> rt0_h;  // [L + 1] first tile of each local robot
   double mu = 0.0;
   long long round_counter = 0;
   // device
@@ -1528,12 +1762,14 @@ hipEvent_t next_event(kmx_pgo* h) {
   return h->ev_pool[h->ev_used++];
 }
 
+// Local rows of the public table: this handle's robots own one contiguous
+// slot range [first_owned, first_owned + n_owned).
 void enqueue_publish(kmx_pgo* h) {
   const int ps = 4 * h->P.r;
-  const long long tot = h->npub * ps;
+  const long long tot = h->n_owned * ps;
   if (tot == 0) return;
   hipLaunchKernelGGL(k_publish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
-                     h->d_pub, h->d_pub_src, (int)h->npub, ps);
+                     h->d_pub + (size_t)h->first_owned * ps, h->d_pub_src + h->first_owned, (int)h->n_owned, ps);
 }
 
 void enqueue_precond(kmx_pgo* h) {
@@ -1558,7 +1794,7 @@ void enqueue_gnc(kmx_pgo* h) {
 template <int R, int G, int F>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   const dim3 grid(h->ntiles), blk(BLOCK);
-  const size_t sm = Smem<R>::bytes;
+  const size_t sm = Smem<R>::bytes, smg = SmemG<R, G>::bytes;
   auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0) {
     if (!F) hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(BLOCK), 0, h->stream, h->dv, kind, R, hs, seq);
   };
@@ -1569,7 +1805,7 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
       e1 = next_event(h);
       (void)hipEventRecord(e0, h->stream);
     }
-    hipLaunchKernelGGL((k_hess<R, G, F>), grid, blk, sm, h->stream, h->dv);
+    hipLaunchKernelGGL((k_hess<R, G, F>), grid, blk, smg, h->stream, h->dv);
     if (h->timing) (void)hipEventRecord(e1, h->stream);
     red(RED_HESS);
     hipLaunchKernelGGL((k_update<R, G, F>), grid, blk, sm, h->stream, h->dv);
@@ -1602,7 +1838,7 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(std::max(64, ((h->dv.L + 63) / 64) * 64)), 0, h->stream,
                      h->dv, d_active);
   for (int it = 0; it < h->P.rtr_iterations; ++it) {
-    hipLaunchKernelGGL((k_grad<R, G, F>), grid, blk, sm, h->stream, h->dv);
+    hipLaunchKernelGGL((k_grad<R, G, F>), grid, blk, smg, h->stream, h->dv);
     red(RED_GRAD);
     const int J = h->P.tcg_max_iterations;
     if (!h->poll || F) {  // the fused variant has no per-robot reduce launch to report progress
@@ -1620,7 +1856,7 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
       }
     }
     hipLaunchKernelGGL((k_retract<R>), grid, blk, sm, h->stream, h->dv);
-    hipLaunchKernelGGL((k_cost<R, G, F>), grid, blk, sm, h->stream, h->dv);
+    hipLaunchKernelGGL((k_cost<R, G, F>), grid, blk, smg, h->stream, h->dv);
     red(RED_COST);
     hipLaunchKernelGGL((k_commit<R>), grid, blk, 0, h->stream, h->dv);
   }
@@ -1638,7 +1874,9 @@ void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
     case 6: enqueue_round_t<R, 3, 0>(h, d_active); break;
     case 7: enqueue_round_t<R, 3, 1>(h, d_active); break;
     case 10: enqueue_round_t<R, 5, 0>(h, d_active); break;
-    default: enqueue_round_t<R, 5, 1>(h, d_active); break;
+    case 11: enqueue_round_t<R, 5, 1>(h, d_active); break;
+    case 14: enqueue_round_t<R, 7, 0>(h, d_active); break;
+    default: enqueue_round_t<R, 7, 1>(h, d_active); break;
   }
 }
 
@@ -1680,7 +1918,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     return kmx::fail(KMX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
   h->own_stream = true;
-  if (const char* v = std::getenv("KMX_GATHER")) h->gvar_req = std::min(5, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("KMX_GATHER")) h->gvar_req = std::min(7, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("KMX_FUSED")) h->fvar = std::atoi(v) ? 1 : 0;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
   *out = h;
@@ -1875,16 +2113,37 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   const int PPW = 64 / r;
   h->tile_poses = WAVES * PPW;
   std::vector<int> tr, tp0, tnp, rt0(L + 1, 0);
+  // Incidence-balanced tiles: a tile holds at most tile_poses poses and about
+  // the robot's mean incidences per full tile, so every workgroup's gather
+  // walks about the same number of incidences (segments of equal length S =
+  // ceil(incidences / groups)); KMX_TILEBAL=0 cuts plain runs of tile_poses.
+  bool tilebal = true;
+  if (const char* v = std::getenv("KMX_TILEBAL")) tilebal = std::atoi(v) != 0;
   for (int l = 0; l < L; ++l) {
     const int n = n_poses[h->robots[l]];
+    const int base = h->loff[l];
     rt0[l] = (int)tr.size();
-    for (int p0 = 0; p0 < n; p0 += h->tile_poses) {
+    const int64_t inc_l = (int64_t)inc_ptr[base + n] - inc_ptr[base];
+    const int64_t full = std::max<int64_t>(1, (n + h->tile_poses - 1) / h->tile_poses);
+    const int64_t cap = tilebal ? std::max<int64_t>(1, (inc_l * 21 / 20 + full - 1) / full) : INT64_MAX;
+    int p0 = 0;
+    while (p0 < n) {
+      int np = 0;
+      int64_t cum = 0;
+      while (p0 + np < n && np < h->tile_poses) {
+        const int64_t dg = inc_ptr[base + p0 + np + 1] - inc_ptr[base + p0 + np];
+        if (np > 0 && cum + dg > cap) break;
+        cum += dg;
+        ++np;
+      }
       tr.push_back(l);
-      tp0.push_back(h->loff[l] + p0);
-      tnp.push_back(std::min(h->tile_poses, n - p0));
+      tp0.push_back(base + p0);
+      tnp.push_back(np);
+      p0 += np;
     }
   }
   rt0[L] = (int)tr.size();
+  h->rt0_h = rt0;
   h->ntiles = (int)tr.size();
   std::vector<int> own_src(std::max<int64_t>(h->n_owned, 1), 0);
   for (int64_t k = 0; k < h->n_owned; ++k) own_src[k] = pub_src[h->first_owned + k];
@@ -1906,9 +2165,10 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       ok = std::fabs(c0 - Q[6]) <= 1e-12 && std::fabs(c1 - Q[7]) <= 1e-12 && std::fabs(c2 - Q[8]) <= 1e-12;
     }
     h->compact_ok = ok;
-    const bool want = (h->gvar_req < 0 || h->gvar_req == 3 || h->gvar_req == 5);
-    h->gvar = (ok && want) ? (h->gvar_req == 3 ? 3 : 5) : (h->gvar_req >= 0 && h->gvar_req < 3 ? h->gvar_req : 2);
-    if (h->gvar == 3 || h->gvar == 5) {
+    const bool want = (h->gvar_req < 0 || h->gvar_req == 3 || h->gvar_req == 5 || h->gvar_req == 7);
+    h->gvar = (ok && want) ? (h->gvar_req < 0 ? KMX_GATHER_DEFAULT : h->gvar_req)
+                           : (h->gvar_req >= 0 && h->gvar_req < 3 ? h->gvar_req : 2);
+    if (h->gvar == 3 || h->gvar == 5 || h->gvar == 7) {
       const size_t ni = (size_t)std::max(h->ninc, 1);
       crec.assign(ni * 12, 0.0);
       for (size_t k = 0; k < (size_t)h->ninc; ++k) {
@@ -1969,7 +2229,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(up(h->d_inc_ptr, inc_ptr.data(), sizeof(int) * inc_ptr.size()));
   KMX_HIP(up(h->d_inc, inc.data(), sizeof(int2) * inc.size()));
   KMX_HIP(up(h->d_irec, irec.data(), sizeof(double) * irec.size()));
-  if (h->gvar == 3 || h->gvar == 5) {
+  if (h->gvar == 3 || h->gvar == 5 || h->gvar == 7) {
     if ((rc = dalloc(&h->d_crec, crec.size())) || (rc = dalloc(&h->d_ocrec, ocrec.size())) ||
         (rc = dalloc(&h->d_optr, optr.size())) || (rc = dalloc(&h->d_eopos, eopos.size()))) {
       free_dev(h);
@@ -2098,6 +2358,32 @@ extern "C" int kmx_pgo_unpack_public(kmx_pgo* h, const void* dev_table) {
   if (h->npub)
     KMX_HIP(hipMemcpyAsync(h->d_pub, dev_table, sizeof(double) * h->npub * 4 * h->P.r, hipMemcpyDeviceToDevice,
                            h->stream));
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_gather_public_rows(kmx_pgo* h, const int32_t* dev_slots, int64_t n, void* dev_out) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(n >= 0 && (n == 0 || (dev_slots && dev_out)), KMX_EINVAL, "bad argument");
+  KMX_HIP(hipSetDevice(h->device));
+  const int ps = 4 * h->P.r;
+  const long long tot = (long long)n * ps;
+  if (tot)
+    hipLaunchKernelGGL(k_gather_slots, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
+                       h->d_pub_src, (const int*)dev_slots, (long long)n, (int)h->npub, (double*)dev_out, ps);
+  KMX_HIP(hipGetLastError());
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_scatter_public_rows(kmx_pgo* h, const int32_t* dev_slots, int64_t n, const void* dev_rows) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(n >= 0 && (n == 0 || (dev_slots && dev_rows)), KMX_EINVAL, "bad argument");
+  KMX_HIP(hipSetDevice(h->device));
+  const int ps = 4 * h->P.r;
+  const long long tot = (long long)n * ps;
+  if (tot)
+    hipLaunchKernelGGL(k_scatter_slots, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_pub,
+                       (const int*)dev_slots, (long long)n, (int)h->npub, (const double*)dev_rows, ps);
+  KMX_HIP(hipGetLastError());
   return KMX_OK;
 }
 
@@ -2319,6 +2605,9 @@ extern "C" int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, do
   } else if (h->gvar == 5) {
     KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 5>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
                                           h->dv, l, mode, (const double*)dV, dO));
+  } else if (h->gvar == 7) {
+    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 7>), dim3(h->ntiles), dim3(BLOCK), (SmemG<RR, 7>::bytes), h->stream,
+                                          h->dv, l, mode, (const double*)dV, dO));
   } else {
     KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 0>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
                                           h->dv, l, mode, (const double*)dV, dO));
@@ -2329,10 +2618,8 @@ extern "C" int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, do
   std::vector<double> part((size_t)h->ntiles * NPART);
   KMX_HIP(hipMemcpyAsync(part.data(), h->d_part, sizeof(double) * part.size(), hipMemcpyDeviceToHost, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  // tiles of robot l are contiguous: recompute their range on the host
-  int t0 = 0;
-  for (int q = 0; q < l; ++q) t0 += (h->npose[h->robots[q]] + h->tile_poses - 1) / h->tile_poses;
-  const int nt = (n + h->tile_poses - 1) / h->tile_poses;
+  // tiles of robot l are contiguous
+  const int t0 = h->rt0_h[l], nt = h->rt0_h[l + 1] - h->rt0_h[l];
   double s = 0.0;
   for (int tt = t0; tt < t0 + nt; ++tt) s += part[(size_t)tt * NPART];
   if (scalar) *scalar = s;
@@ -2398,6 +2685,10 @@ extern "C" int kmx_pgo_debug_gather_bench(kmx_pgo* h, int variant, int reps, dou
       KMX_GB(20, 2, 1) KMX_GB(21, 2, 4) KMX_GB(22, 2, 6) KMX_GB(23, 2, 8)
       KMX_GB(40, 3, 1) KMX_GB(41, 3, 4) KMX_GB(42, 3, 6) KMX_GB(45, 4, 1)
       KMX_GB(60, 5, 1) KMX_GB(61, 5, 4) KMX_GB(62, 5, 6) KMX_GB(65, 6, 1)
+#undef KMX_GB
+#define KMX_GB(V, G, W) case V: hipLaunchKernelGGL((k_gbench<5, G, W>), grid, blk, (SmemG<5, G>::bytes), h->stream, h->dv, (const double*)h->dv.X, out); return true;
+      KMX_GB(70, 7, 1) KMX_GB(71, 7, 4) KMX_GB(72, 7, 5) KMX_GB(75, 8, 1)
+      KMX_GB(90, 9, 1) KMX_GB(91, 9, 6) KMX_GB(95, 10, 1)
 #define KMX_GC(V, C) case V: hipLaunchKernelGGL((k_gcap<5, C>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
       KMX_GC(50, 1000) KMX_GC(51, 12) KMX_GC(52, 10) KMX_GC(53, 8) KMX_GC(54, 4)
 #undef KMX_GC

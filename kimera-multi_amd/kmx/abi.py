@@ -127,6 +127,8 @@ def lib() -> C.CDLL:
         "kmx_pgo_pack_public": ([P, P], C.c_int),
         "kmx_pgo_unpack_public": ([P, P], C.c_int),
         "kmx_pgo_refresh_local": ([P], C.c_int),
+        "kmx_pgo_gather_public_rows": ([P, P, i64, P], C.c_int),
+        "kmx_pgo_scatter_public_rows": ([P, P, i64, P], C.c_int),
         "kmx_pgo_set_neighbor_poses": ([P, i64, pi32, pi32, pf64], C.c_int),
         "kmx_pgo_iterate": ([P, pu8, C.POINTER(IterStats)], C.c_int),
         "kmx_pgo_iterate_async": ([P, C.c_int, C.c_int, C.c_int], C.c_int),

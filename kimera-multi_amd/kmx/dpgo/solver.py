@@ -100,6 +100,14 @@ class BlockSolver:
     def unpack_public(self, dev_ptr: int):
         check(self.L.kmx_pgo_unpack_public(self.h, C.c_void_p(dev_ptr)), "kmx_pgo_unpack_public")
 
+    def gather_public_rows(self, slots_ptr: int, n: int, out_ptr: int):
+        check(self.L.kmx_pgo_gather_public_rows(self.h, C.c_void_p(slots_ptr), int(n), C.c_void_p(out_ptr)),
+              "kmx_pgo_gather_public_rows")
+
+    def scatter_public_rows(self, slots_ptr: int, n: int, rows_ptr: int):
+        check(self.L.kmx_pgo_scatter_public_rows(self.h, C.c_void_p(slots_ptr), int(n), C.c_void_p(rows_ptr)),
+              "kmx_pgo_scatter_public_rows")
+
     def refresh_local(self):
         check(self.L.kmx_pgo_refresh_local(self.h), "kmx_pgo_refresh_local")
 

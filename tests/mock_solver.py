@@ -60,6 +60,21 @@ class OracleBlockSolver:
         X = np.frombuffer(buf, dtype=np.float64).reshape(n, self.r, 4).copy()
         self.o.set_nbr_rows(self.pub_robot, self.pub_pose, X)
 
+    def gather_public_rows(self, slots_ptr, n, out_ptr):
+        if n == 0:
+            return
+        sl = np.frombuffer((C.c_int32 * n).from_address(slots_ptr), dtype=np.int32).copy()
+        X = np.ascontiguousarray(self.o.get_x_rows(self.pub_robot[sl], self.pub_pose[sl]))
+        C.memmove(out_ptr, X.ctypes.data, X.nbytes)
+
+    def scatter_public_rows(self, slots_ptr, n, rows_ptr):
+        if n == 0:
+            return
+        sl = np.frombuffer((C.c_int32 * n).from_address(slots_ptr), dtype=np.int32).copy()
+        buf = (C.c_double * (n * self._rows())).from_address(rows_ptr)
+        X = np.frombuffer(buf, dtype=np.float64).reshape(n, self.r, 4).copy()
+        self.o.set_nbr_rows(self.pub_robot[sl], self.pub_pose[sl], X)
+
     def refresh_local(self):
         X = self.o.get_x_rows(self.pub_robot, self.pub_pose)
         self.o.set_nbr_rows(self.pub_robot, self.pub_pose, X)

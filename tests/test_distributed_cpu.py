@@ -1,6 +1,7 @@
-"""world_size-2 gloo run of the multi-process RBCD driver (public-pose
-all-gather + owner -> peer GNC weight all-reduce) on the CPU restatement:
-the distributed iterates must equal the single-process team run bit for bit."""
+"""world_size-2/3 gloo runs of the multi-process RBCD driver (public-pose
+all-to-all or all-gather + owner -> peer GNC weight all-reduce) on the CPU
+restatement: the distributed iterates must equal the single-process team run
+bit for bit. Plus the host-side consistency of the sparse exchange plan."""
 import os
 import socket
 
@@ -27,14 +28,15 @@ def _x0(g):
     return {a: lift(g.init_R[a], g.init_t[a], Y) for a in range(g.n_robots)}
 
 
-def _worker(rank, world, port, rounds, q):
+def _worker(rank, world, port, rounds, q, exchange):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from kmx.dpgo.driver import RBCDDriver
     from tests.mock_solver import OracleBlockSolver
     g, P = _graph(), _params()
-    drv = RBCDDriver(P, g, rank=rank, world=world, solver=OracleBlockSolver(P), exchange_device="cpu")
+    drv = RBCDDriver(P, g, rank=rank, world=world, solver=OracleBlockSolver(P), exchange_device="cpu",
+                     exchange=exchange)
     drv.initialize(_x0(g))
     for _ in range(rounds):
         drv.step(with_stats=True)
@@ -51,13 +53,15 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_matches_single_process():
+@pytest.mark.parametrize("world,exchange", [(2, "alltoall"), (2, "allgather"), (3, "alltoall")])
+def test_gloo_ranks_match_single_process(world, exchange):
     from oracle.oracle import OraclePGO
     rounds = 7
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q), daemon=True) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, rounds, q, exchange), daemon=True)
+             for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -83,6 +87,43 @@ def test_two_rank_gloo_matches_single_process():
         if k % P.robustOptInnerIters == 0:
             o.refresh()
             o.update_weights()
-    assert wu == [rounds // P.robustOptInnerIters] * 2
+    assert wu == [rounds // P.robustOptInnerIters] * world
     for a in range(g.n_robots):
         assert np.array_equal(got[a], o.get_iterate(a)), a
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_exchange_plan_consistent(world):
+    """Every rank receives exactly the foreign public poses its shared loop
+    closures reference, in the order its peers send them."""
+    from kmx.dpgo.driver import exchange_plan, robot_ranges
+    g = make_pose_graph(6, 1200, 4000, seed=5)
+    plans = [exchange_plan(g, world, k) for k in range(world)]
+    sh = g.r1 != g.r2
+    keys = np.unique(np.concatenate([(g.r1[sh].astype(np.int64) << 32) | g.p1[sh],
+                                     (g.r2[sh].astype(np.int64) << 32) | g.p2[sh]]))
+    rank_of = np.empty(g.n_robots, np.int64)
+    for k, (lo, hi) in enumerate(robot_ranges(g.n_robots, world)):
+        rank_of[lo:hi] = k
+    for q in range(world):
+        send_q, sc_q, recv_q, rc_q = plans[q]
+        assert int(sc_q.sum()) == send_q.shape[0] and int(rc_q.sum()) == recv_q.shape[0]
+        # what q must receive: the foreign endpoints of its shared loop closures
+        need = set()
+        for e in np.nonzero(sh)[0]:
+            a, b = rank_of[g.r1[e]], rank_of[g.r2[e]]
+            if a == b:
+                continue
+            if a == q:
+                need.add(int(np.searchsorted(keys, (int(g.r2[e]) << 32) | int(g.p2[e]))))
+            if b == q:
+                need.add(int(np.searchsorted(keys, (int(g.r1[e]) << 32) | int(g.p1[e]))))
+        assert sorted(need) == recv_q.tolist()
+        off_r = np.concatenate([[0], np.cumsum(rc_q)])
+        for k in range(world):
+            send_k, sc_k, _, _ = plans[k]
+            off_s = np.concatenate([[0], np.cumsum(sc_k)])
+            seg_sent = send_k[off_s[q]:off_s[q + 1]]
+            seg_recv = recv_q[off_r[k]:off_r[k + 1]]
+            assert np.array_equal(seg_sent, seg_recv), (k, q)
+            assert np.all(rank_of[keys[seg_sent] >> 32] == k)

@@ -38,7 +38,7 @@ def _run(drv, rounds):
     return {a: drv.iterate_of(a) for a in drv.robots}, drv.solver.get_weights()
 
 
-def _worker(rank, world, port, rounds, q):
+def _worker(rank, world, port, rounds, q, exchange):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -46,7 +46,7 @@ def _worker(rank, world, port, rounds, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from kmx.dpgo.driver import RBCDDriver
     g, P = _graph(), _params()
-    drv = RBCDDriver(P, g, rank=rank, world=world, device=0, exchange_device="cpu")
+    drv = RBCDDriver(P, g, rank=rank, world=world, device=0, exchange_device="cpu", exchange=exchange)
     drv.initialize(_x0(g))
     X, w = _run(drv, rounds)
     q.put((rank, X, w, list(drv.robots)))
@@ -63,7 +63,8 @@ def _free_port():
 
 
 @pytest.mark.timeout(600)
-def test_two_ranks_one_gpu_match_single_process(gpu):
+@pytest.mark.parametrize("exchange", ["alltoall", "allgather"])
+def test_two_ranks_one_gpu_match_single_process(gpu, exchange):
     from kmx.dpgo.driver import RBCDDriver
     rounds = 10
     g, P = _graph(), _params()
@@ -73,7 +74,7 @@ def test_two_ranks_one_gpu_match_single_process(gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q), daemon=True) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q, exchange), daemon=True) for r in range(2)]
     for p in procs:
         p.start()
     results = []
