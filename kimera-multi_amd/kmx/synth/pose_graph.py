@@ -123,6 +123,12 @@ def _gt_trajectory(rng, n, box, start):
     return R, p
 
 
+def _workers() -> int:
+    """Threads for the KD-tree queries (results do not depend on it)."""
+    import os
+    return max(1, min(16, os.cpu_count() or 1))
+
+
 def make_pose_graph(n_robots: int, n_poses_total: int, n_edges_total: int, *,
                     outlier_frac: float = 0.2, f_inter: float = 0.10,
                     sigma_R: float = 0.01, sigma_t: float = 0.1,
@@ -188,7 +194,7 @@ def make_pose_graph(n_robots: int, n_poses_total: int, n_edges_total: int, *,
         while need > 0:
             cand = rng.integers(0, allp.shape[0], size=2 * need + 16)
             # k nearest neighbours, then choose one at random among those within radius
-            dist, nb = tree.query(allp[cand], k=32, distance_upper_bound=lc_radius)
+            dist, nb = tree.query(allp[cand], k=32, distance_upper_bound=lc_radius, workers=_workers())
             choice = rng.integers(0, 32, size=cand.shape[0])
             j = nb[np.arange(cand.shape[0]), choice]
             ok = j < allp.shape[0]
