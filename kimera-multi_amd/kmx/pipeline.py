@@ -1,0 +1,320 @@
+"""kmx.pipeline — configs[4]: the multi-robot back end end to end on MI355X.
+
+Reference flow (Kimera-Multi, images/kimera-multi.drawio):
+  * Kimera-Distributed's verification thread takes inter-robot loop-closure
+    candidates and runs computeMatchedIndices -> geometricVerificationNister ->
+    recoverPose (drawio:246, 405, 2583-2598); accepted loop closures become
+    shared loop closures of the pose graph (addSharedLoopClosure, drawio:2817);
+  * dpgo_ros requests the pose graph (drawio:557-574, 623-632), initialises
+    every robot in its own frame and aligns it to the global frame over the
+    shared loop closures (INITIALIZE, drawio:2271-2307; kmx.dpgo.init), then
+    runs synchronous RBCD rounds with GNC-TLS (drawio:2058-2066, 2212-2215).
+
+Here every stage runs on the MI355X path of this package: the candidates are
+verified in one batched kmx_lcd_verify call per rank (candidates sharded by
+query robot, no collective), the accepted loop closures are gathered to every
+rank (one small all_gather), and the RBCD rounds run through RBCDDriver
+(robot blocks dealt to ranks, one all_to_all of public poses per round).
+
+Synthetic inputs (the Campus bags are unavailable offline): a team pose graph
+without inter-robot loop closures (kmx.synth.make_pose_graph with f_inter = 0
+and outlier_scope = "robot": its outlier loop closures join poses of one
+robot), and a loop-closure stream whose
+keyframe pairs observe a common scene under the GROUND-TRUTH relative pose of
+the two robot poses (true candidates) or are unrelated frames (false ones).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .dpgo.init import align_to_world, transform_trajectory
+from .synth.lcd import LcdPool, make_lcd_pool
+from .synth.pose_graph import PoseGraphData, _compose_scan
+
+
+@dataclass
+class LcStream:
+    """Inter-robot loop-closure candidates. Candidate c asks whether keyframe
+    (r_q[c], p_q[c]) sees the place of (r_m[c], p_m[c]); its frames in `pool`
+    are cand_query[c] / cand_match[c]; truth[c] marks a planted loop closure."""
+    pool: LcdPool
+    r_q: np.ndarray
+    p_q: np.ndarray
+    r_m: np.ndarray
+    p_m: np.ndarray
+    cand_query: np.ndarray
+    cand_match: np.ndarray
+    truth: np.ndarray
+
+
+def _flat(g: PoseGraphData):
+    rob = np.concatenate([np.full(int(n), a, np.int32) for a, n in enumerate(g.n_poses)])
+    idx = np.concatenate([np.arange(int(n), dtype=np.int32) for n in g.n_poses])
+    return rob, idx, np.concatenate(g.gt_R), np.concatenate(g.gt_t)
+
+
+def make_lc_stream(g: PoseGraphData, n_true: int, n_false: int, *, n_feats: int = 500, radius: float = 3.0,
+                   max_angle: float = np.pi / 6, seed: int = 1) -> LcStream:
+    """`n_true` true candidates: pose pairs of different robots whose ground
+    truth positions are within `radius` and whose relative rotation is below
+    `max_angle` (the views overlap); the keyframe pair plants the ground-truth
+    relative pose T_q^-1 T_m. `n_false` false candidates pair the query frame
+    of one true candidate with the match frame of another candidate of a
+    different robot (unrelated scenes)."""
+    from scipy.spatial import cKDTree
+    rng = np.random.Generator(np.random.PCG64(seed))
+    rob, idx, Rw, tw = _flat(g)
+    pairs = cKDTree(tw).query_pairs(radius, output_type="ndarray")
+    pairs = pairs[rob[pairs[:, 0]] != rob[pairs[:, 1]]]
+    Rrel = np.einsum("kji,kjl->kil", Rw[pairs[:, 0]], Rw[pairs[:, 1]])
+    cosang = np.clip((np.trace(Rrel, axis1=1, axis2=2) - 1.0) / 2.0, -1.0, 1.0)
+    pairs = pairs[np.arccos(cosang) <= max_angle]
+    if pairs.shape[0] < n_true:
+        raise ValueError(f"only {pairs.shape[0]} overlapping inter-robot pose pairs for {n_true} true candidates")
+    sel = pairs[np.sort(rng.choice(pairs.shape[0], n_true, replace=False))]
+    swap = rng.random(n_true) < 0.5
+    q = np.where(swap, sel[:, 1], sel[:, 0])
+    m = np.where(swap, sel[:, 0], sel[:, 1])
+    R_qm = np.einsum("kji,kjl->kil", Rw[q], Rw[m])
+    t_qm = np.einsum("kji,kj->ki", Rw[q], tw[m] - tw[q])
+    pool = make_lcd_pool(2 * n_true, n_feats, R_qm=R_qm, t_qm=t_qm, seed=seed)
+    # false candidates: query frame of pair k with the match frame of pair k2 (other robot)
+    fk = rng.integers(0, n_true, n_false)
+    fk2 = rng.integers(0, n_true, n_false)
+    for _ in range(64):
+        bad = (fk2 == fk) | (rob[m[fk2]] == rob[q[fk]])
+        if not bad.any():
+            break
+        fk2[bad] = rng.integers(0, n_true, int(bad.sum()))
+    keep = (fk2 != fk) & (rob[m[fk2]] != rob[q[fk]])
+    fk, fk2 = fk[keep], fk2[keep]
+    k = np.arange(n_true)
+    cq = np.concatenate([2 * k, 2 * fk]).astype(np.int32)
+    cm = np.concatenate([2 * k + 1, 2 * fk2 + 1]).astype(np.int32)
+    qq = np.concatenate([q, q[fk]])
+    mm = np.concatenate([m, m[fk2]])
+    order = np.argsort(rob[qq], kind="stable")  # grouped by query robot (sharding)
+    truth = np.concatenate([np.ones(n_true, bool), np.zeros(fk.shape[0], bool)])
+    return LcStream(pool=pool, r_q=rob[qq][order], p_q=idx[qq][order], r_m=rob[mm][order], p_m=idx[mm][order],
+                    cand_query=cq[order], cand_match=cm[order], truth=truth[order])
+
+
+@dataclass
+class Accepted:
+    """Verified loop closures (query -> match): T_q^-1 T_m = (R, t)."""
+    r1: np.ndarray
+    p1: np.ndarray
+    r2: np.ndarray
+    p2: np.ndarray
+    R: np.ndarray
+    t: np.ndarray
+    truth: np.ndarray
+    n_verified: int = 0
+    stats: dict = field(default_factory=dict)
+
+
+def accepted_from_results(stream: LcStream, sel: np.ndarray, results) -> Accepted:
+    """Turn kmx_lcd_result records (dicts of LoopClosureDetector.verify) of the
+    candidates `sel` into loop-closure measurements."""
+    ok = np.array([r["accepted"] for r in results], bool)
+    T = np.array([r["T_query_match"] for r in results], np.float64).reshape(-1, 12)
+    s = sel[ok]
+    return Accepted(r1=stream.r_q[s], p1=stream.p_q[s], r2=stream.r_m[s], p2=stream.p_m[s],
+                    R=T[ok, :9].reshape(-1, 3, 3), t=T[ok, 9:].reshape(-1, 3), truth=stream.truth[s],
+                    n_verified=int(sel.shape[0]))
+
+
+def merge_accepted(parts) -> Accepted:
+    parts = list(parts)
+    cat = lambda name: np.concatenate([getattr(a, name) for a in parts])  # noqa: E731
+    out = Accepted(r1=cat("r1"), p1=cat("p1"), r2=cat("r2"), p2=cat("p2"), R=cat("R").reshape(-1, 3, 3),
+                   t=cat("t").reshape(-1, 3), truth=cat("truth"), n_verified=sum(a.n_verified for a in parts))
+    order = np.lexsort((out.p2, out.r2, out.p1, out.r1))
+    for k in ("r1", "p1", "r2", "p2", "R", "t", "truth"):
+        setattr(out, k, getattr(out, k)[order])
+    return out
+
+
+def team_graph(g0: PoseGraphData, acc: Accepted, kappa: float, tau: float) -> PoseGraphData:
+    """The base graph plus the accepted loop closures as shared loop closures
+    (weight 1, not fixed: GNC may reject them)."""
+    k = acc.r1.shape[0]
+    cat = np.concatenate
+    return PoseGraphData(
+        n_robots=g0.n_robots, n_poses=g0.n_poses,
+        r1=cat([g0.r1, acc.r1]).astype(np.int32), p1=cat([g0.p1, acc.p1]).astype(np.int32),
+        r2=cat([g0.r2, acc.r2]).astype(np.int32), p2=cat([g0.p2, acc.p2]).astype(np.int32),
+        R=np.ascontiguousarray(cat([g0.R, acc.R])), t=np.ascontiguousarray(cat([g0.t, acc.t])),
+        kappa=cat([g0.kappa, np.full(k, kappa)]), tau=cat([g0.tau, np.full(k, tau)]),
+        weight=cat([g0.weight, np.ones(k)]), fixed=cat([g0.fixed, np.zeros(k, np.uint8)]),
+        outlier=cat([g0.outlier, ~acc.truth]), gt_R=g0.gt_R, gt_t=g0.gt_t, init_R=g0.init_R, init_t=g0.init_t)
+
+
+def odometry_init(g: PoseGraphData):
+    """Each robot's odometry chain in its own frame (first pose = identity),
+    from the graph's odometry edges (fixed, same robot, p -> p + 1)."""
+    out = {}
+    for a in range(g.n_robots):
+        n = int(g.n_poses[a])
+        sel = np.nonzero((g.r1 == a) & (g.r2 == a) & (g.p2 == g.p1 + 1) & (g.fixed == 1))[0]
+        sel = sel[np.argsort(g.p1[sel], kind="stable")]
+        if sel.shape[0] != n - 1 or not np.array_equal(g.p1[sel], np.arange(n - 1)):
+            raise ValueError(f"robot {a}: odometry chain incomplete")
+        out[a] = _compose_scan(g.R[sel], g.t[sel], np.eye(3), np.zeros(3))
+    return out
+
+
+@dataclass
+class _Lc:
+    r1: int
+    p1: int
+    r2: int
+    p2: int
+    R: np.ndarray
+    t: np.ndarray
+    kappa: float
+    tau: float
+
+
+def global_init(g: PoseGraphData, own: dict, *, first: int = 0):
+    """Distributed initialisation: robot `first` defines the
+    world frame; the others are aligned in breadth-first order over the
+    robot graph of shared loop closures by GNC-TLS robust single-pose
+    averaging (kmx.dpgo.init.align_to_world). Returns ({robot: (R, t)} in the
+    world frame, {robot: (R_WA, t_WA, inlier weights)})."""
+    sh = np.nonzero(g.r1 != g.r2)[0]
+    lcs = [_Lc(int(g.r1[e]), int(g.p1[e]), int(g.r2[e]), int(g.p2[e]), g.R[e], g.t[e], float(g.kappa[e]),
+               float(g.tau[e])) for e in sh]
+    world = {first: own[first]}
+    frames = {first: (np.eye(3), np.zeros(3), None)}
+    nbr_global = {}
+
+    def publish(a):
+        R, t = world[a]
+        for lc in lcs:
+            for (r, p) in ((lc.r1, lc.p1), (lc.r2, lc.p2)):
+                if r == a:
+                    nbr_global[(r, p)] = (R[p], t[p])
+
+    publish(first)
+    pending = [a for a in range(g.n_robots) if a != first]
+    while pending:
+        progress = False
+        for a in list(pending):
+            mine = [lc for lc in lcs if lc.r1 == a or lc.r2 == a]
+            res = align_to_world(mine, a, own[a][0], own[a][1], nbr_global)
+            if res is None:
+                continue
+            R_WA, t_WA, w = res
+            world[a] = transform_trajectory(R_WA, t_WA, *own[a])
+            frames[a] = (R_WA, t_WA, w)
+            publish(a)
+            pending.remove(a)
+            progress = True
+        if not progress:
+            raise ValueError(f"robots {pending} share no loop closure with the initialised team")
+    return world, frames
+
+
+def rounded(X: np.ndarray, YLift: np.ndarray):
+    """dpgo rounding: T_i = YLift^T X_i, R projected to SO(3)."""
+    T = np.einsum("ad,nac->ndc", YLift, X)
+    U, _, Vt = np.linalg.svd(T[:, :, :3])
+    D = np.ones((X.shape[0], 3))
+    D[:, 2] = np.sign(np.linalg.det(U @ Vt))
+    return (U * D[:, None, :]) @ Vt, T[:, :, 3].copy()
+
+
+def ate_rmse(g: PoseGraphData, traj: dict, *, anchor_robot: int = 0) -> float:
+    """Position RMSE over the team after expressing both the estimate and the
+    ground truth relative to `anchor_robot`'s first pose."""
+    Re0, te0 = traj[anchor_robot][0][0], traj[anchor_robot][1][0]
+    Rg0, tg0 = g.gt_R[anchor_robot][0], g.gt_t[anchor_robot][0]
+    err = []
+    for a, (R, t) in traj.items():
+        pe = (t - te0) @ Re0
+        pg = (g.gt_t[a] - tg0) @ Rg0
+        err.append(((pe - pg) ** 2).sum(1))
+    return float(np.sqrt(np.concatenate(err).mean()))
+
+
+def run_pipeline(g0: PoseGraphData, stream: LcStream, params, lcd_params, *, rank: int = 0, world: int = 1,
+                 device: int = 0, rounds: int = 100, verifier=None, solver=None, exchange_device=None) -> dict:
+    """One team run: LCD verification of this rank's candidates (query robot
+    in the rank's robot range) -> all_gather of the accepted loop closures ->
+    team graph -> global initialisation -> `rounds` concurrent RBCD rounds
+    with GNC. `verifier(cand_query, cand_match) -> result dicts` and `solver`
+    replace the HIP LoopClosureDetector / BlockSolver (the CPU tests inject
+    the restatement). Returns stage timings and metrics (identical on every
+    rank)."""
+    import time
+
+    from .dpgo.driver import RBCDDriver, robot_ranges
+    from .synth.pose_graph import lift, lifting_matrix
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+    lo, hi = robot_ranges(g0.n_robots, world)[rank]
+    sel = np.nonzero((stream.r_q >= lo) & (stream.r_q < hi))[0]
+    out = {"rank": rank, "world": world, "candidates": int(stream.truth.shape[0])}
+    # 1. LCD (candidates of this rank's query robots; pool upload outside the timed region)
+    if verifier is None:
+        from .lcd import LoopClosureDetector
+        det = LoopClosureDetector(lcd_params, device=device)
+        det.set_pool(stream.pool)
+        det.sync()
+        verifier = lambda q, m: det.verify(q, m)[0]  # noqa: E731
+    t0 = time.perf_counter()
+    results = verifier(stream.cand_query[sel], stream.cand_match[sel])
+    t_lcd = time.perf_counter() - t0
+    acc = accepted_from_results(stream, sel, results)
+    if dist is not None:
+        parts = [None] * world
+        dist.all_gather_object(parts, (acc, t_lcd))
+        acc = merge_accepted([p[0] for p in parts])
+        t_lcd = max(p[1] for p in parts)
+    else:
+        acc = merge_accepted([acc])
+    out["lcd"] = {"verified": acc.n_verified, "accepted": int(acc.r1.shape[0]),
+                  "true_positives": int(acc.truth.sum()), "planted": int(stream.truth.sum()),
+                  "seconds": t_lcd, "candidates_per_s": acc.n_verified / max(t_lcd, 1e-12)}
+    # 2. team graph + distributed initialisation (host control, identical on every rank)
+    t0 = time.perf_counter()
+    rc = lcd_params
+    g = team_graph(g0, acc, getattr(rc, "kappa", 1e4), getattr(rc, "tau", 1e2))
+    traj0, frames = global_init(g, odometry_init(g))
+    out["init"] = {"seconds": time.perf_counter() - t0, "ate_m": ate_rmse(g, traj0),
+                   "edges": g.m, "shared_loop_closures": int((g.r1 != g.r2).sum())}
+    # 3. RBCD + GNC rounds
+    Y = lifting_matrix(params.r, seed=1)
+    drv = RBCDDriver(params, g, rank=rank, world=world, device=device, solver=solver,
+                     exchange_device=exchange_device)
+    drv.initialize({a: lift(traj0[a][0], traj0[a][1], Y) for a in drv.robots})
+    counters = getattr(drv.solver, "read_counters", None)
+    if counters:
+        drv.solver.sync()
+        counters()
+    t0 = time.perf_counter()
+    drv.run_async(rounds)
+    drv.solver.sync()
+    t_pgo = time.perf_counter() - t0
+    ei = float(counters()["edges_iters"]) if counters else float("nan")
+    mine = {a: rounded(drv.iterate_of(a), Y) for a in drv.robots}
+    if dist is not None:
+        parts = [None] * world
+        dist.all_gather_object(parts, (mine, t_pgo, ei))
+        mine = {k: v for p in parts for k, v in p[0].items()}
+        t_pgo = max(p[1] for p in parts)
+        ei = sum(p[2] for p in parts)
+    w = drv.solver.get_weights() if hasattr(drv.solver, "get_weights") else None
+    out["dpgo"] = {"rounds": rounds, "seconds": t_pgo, "edges_iters_per_s": ei / max(t_pgo, 1e-12),
+                   "ate_m": ate_rmse(g, mine)}
+    if w is not None and world == 1:
+        lc = g.fixed == 0
+        out["dpgo"]["gnc_weight_mean_inlier_lc"] = float(w[lc & ~g.outlier].mean()) if (lc & ~g.outlier).any() else None
+        out["dpgo"]["gnc_weight_mean_outlier_lc"] = float(w[lc & g.outlier].mean()) if (lc & g.outlier).any() else None
+    if hasattr(drv.solver, "close"):
+        drv.solver.close()
+    return out

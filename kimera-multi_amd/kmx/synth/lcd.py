@@ -49,7 +49,11 @@ def _bearing(p, rng, sigma):
 
 def make_lcd_pool(n_frames: int, n_feats: int = 500, *, true_frac: float = 0.5, false_frac: float = 0.2,
                   flip_frac: float = 0.05, bearing_sigma: float = 1e-4, point_sigma: float = 0.05,
-                  noise_free: bool = False, seed: int = 0) -> LcdPool:
+                  noise_free: bool = False, seed: int = 0, R_qm: np.ndarray | None = None,
+                  t_qm: np.ndarray | None = None) -> LcdPool:
+    """`R_qm` / `t_qm` ([n_frames / 2, 3, 3] / [.., 3]) plant given relative
+    poses instead of random ones (the loop-closure stream of kmx.pipeline);
+    the random draws are made either way, so every other array is unchanged."""
     if n_frames % 2:
         raise ValueError("n_frames must be even (frames come in pairs)")
     rng = np.random.Generator(np.random.PCG64(seed))
@@ -63,6 +67,9 @@ def make_lcd_pool(n_frames: int, n_feats: int = 500, *, true_frac: float = 0.5, 
     tdir = rng.normal(size=(P, 3))
     tdir /= np.linalg.norm(tdir, axis=1, keepdims=True)
     t = tdir * rng.uniform(0.2, 2.0, P)[:, None]
+    if R_qm is not None:
+        R = np.ascontiguousarray(np.asarray(R_qm, np.float64).reshape(P, 3, 3))
+        t = np.ascontiguousarray(np.asarray(t_qm, np.float64).reshape(P, 3))
     # scene points in the match frame, in front of both cameras
     def scene(k):
         z = rng.uniform(1.0, 20.0, (P, k))

@@ -133,7 +133,10 @@ def make_pose_graph(n_robots: int, n_poses_total: int, n_edges_total: int, *,
                     outlier_frac: float = 0.2, f_inter: float = 0.10,
                     sigma_R: float = 0.01, sigma_t: float = 0.1,
                     lc_radius: float = 5.0, box: float | None = None,
-                    noise_free: bool = False, seed: int = 0) -> PoseGraphData:
+                    noise_free: bool = False, outlier_scope: str = "team", seed: int = 0) -> PoseGraphData:
+    """`outlier_scope` "team": outlier loop closures join random pose pairs of
+    the whole team; "robot": both ends on the same robot (the inter-robot loop
+    closures of kmx.pipeline come from the verified LCD stream instead)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     R_ = n_robots
     base = n_poses_total // R_
@@ -220,9 +223,16 @@ def make_pose_graph(n_robots: int, n_poses_total: int, n_edges_total: int, *,
         E_fixed.append(np.zeros(k, np.uint8)); E_out.append(np.zeros(k, bool))
     if n_out > 0:
         gi = rng.integers(0, allp.shape[0], n_out)
-        gj = rng.integers(0, allp.shape[0], n_out)
-        bad = gi == gj
-        gj[bad] = (gj[bad] + 1) % allp.shape[0]
+        if outlier_scope == "robot":
+            off = np.concatenate([[0], np.cumsum(n_poses)[:-1]])
+            ri = rob_of[gi]
+            gj = off[ri] + (rng.random(n_out) * n_poses[ri]).astype(np.int64)
+            bad = gj == gi
+            gj[bad] = off[ri[bad]] + (idx_of[gi[bad]] + 2) % n_poses[ri[bad]]
+        else:
+            gj = rng.integers(0, allp.shape[0], n_out)
+            bad = gi == gj
+            gj[bad] = (gj[bad] + 1) % allp.shape[0]
         E_r1.append(rob_of[gi]); E_p1.append(idx_of[gi]); E_r2.append(rob_of[gj]); E_p2.append(idx_of[gj])
         E_R.append(random_rotations(rng, n_out)); E_t.append(rng.uniform(-10, 10, (n_out, 3)))
         E_fixed.append(np.zeros(n_out, np.uint8)); E_out.append(np.ones(n_out, bool))

@@ -84,10 +84,16 @@ class OracleBlockSolver:
         return self.o.iterate_nbr(act)
 
     def iterate_async(self, rounds, refresh_local=True, gnc_every=0):
+        # same schedule as kmx_pgo_iterate_async: GNC after every gnc_every-th round
         for _ in range(rounds):
             if refresh_local:
                 self.refresh_local()
             self.o.iterate_nbr(self.local)
+            self.rounds_done = getattr(self, "rounds_done", 0) + 1
+            if gnc_every > 0 and int(self.params.robustCostParams.costType) != 0 and self.rounds_done % gnc_every == 0:
+                if refresh_local:
+                    self.refresh_local()
+                self.update_weights()
 
     def sync(self):
         pass
