@@ -24,7 +24,9 @@ def main():
     ap.add_argument("--edges-per-pose", type=float, default=5.0)
     ap.add_argument("--true-per-robot", type=int, default=1000)
     ap.add_argument("--false-per-robot", type=int, default=500)
-    ap.add_argument("--rounds", type=int, default=200)
+    ap.add_argument("--rounds", type=int, default=500)
+    ap.add_argument("--sigma-r", type=float, default=0.002, help="odometry rotation noise per keyframe (rad)")
+    ap.add_argument("--sigma-t", type=float, default=0.02, help="odometry translation noise per keyframe (m)")
     ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -41,13 +43,15 @@ def main():
     from kmx.synth import make_pose_graph
     t0 = time.perf_counter()
     n = a.robots * a.poses
-    g0 = make_pose_graph(a.robots, n, int(a.edges_per_pose * n), f_inter=0.0, outlier_scope="robot", seed=a.seed)
+    g0 = make_pose_graph(a.robots, n, int(a.edges_per_pose * n), f_inter=0.0, outlier_scope="robot",
+                         sigma_R=a.sigma_r, sigma_t=a.sigma_t, seed=a.seed)
     stream = PL.make_lc_stream(g0, a.robots * a.true_per_robot, a.robots * a.false_per_robot, seed=a.seed + 1)
     gen = time.perf_counter() - t0
     out = PL.run_pipeline(g0, stream, bench.params(), LcdParams(), rank=rank, world=world, device=local_rank,
                           rounds=a.rounds)
     out["config"] = {"workload": f"configs[4]: {a.robots} robots x {a.poses} poses, {g0.m} base edges "
-                                 f"(intra-robot loop closures, 20% intra outliers), LC stream "
+                                 f"(intra-robot loop closures, 20% intra outliers, odometry noise "
+                                 f"{a.sigma_r} rad / {a.sigma_t} m), LC stream "
                                  f"{stream.truth.shape[0]} candidates ({int(stream.truth.sum())} planted)",
                      "n_gpus": world, "generation_s": round(gen, 1)}
     if rank == 0:
