@@ -585,7 +585,7 @@ __device__ __forceinline__ void lane_gather_compact(const Dev& d, const Lane& L,
 // (the continuation) writes H[group]. The (pose, row) lanes then add
 // A[pose] + H[g] for the pose's later segments in order, so the result is
 // deterministic and independent of everything but the tiling.
-template <int R, bool PUB, bool OWN, bool COOP = false>
+template <int R, bool PUB, bool OWN>
 __device__ __forceinline__ void tile_gather_bal(const Dev& d, const Lane& L, const double* V, const double* pub,
                                                 double acc[4], double* cost, char* smem) {
   using SM = Smem<R>;
@@ -645,25 +645,8 @@ __device__ __forceinline__ void tile_gather_bal(const Dev& d, const Lane& L, con
       }
       const double2* q2 = reinterpret_cast<const double2*>(rec + 12 * (size_t)(K0 + k));
       double2 q[6];
-      if constexpr (COOP) {
-        // the group's lanes load the record's six 16-B chunks once between
-        // them (chunk i in lane i % R) and broadcast them by shuffles
-        constexpr int NL = (6 + R - 1) / R;
-        double2 mine[NL];
 #pragma unroll
-        for (int u = 0; u < NL; ++u) {
-          const int ci = L.a + u * R;
-          mine[u] = (ci < 6) ? q2[ci] : make_double2(0.0, 0.0);
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          q[i].x = __shfl(mine[i / R].x, L.base + i % R, 64);
-          q[i].y = __shfl(mine[i / R].y, L.base + i % R, 64);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) q[i] = q2[i];
-      }
+      for (int i = 0; i < 6; ++i) q[i] = q2[i];
       const int2 in = unpack_int2(q[5].y);
       const int o = in.x;
       const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V);
@@ -882,8 +865,6 @@ __device__ __forceinline__ void gather(const Dev& d, const Lane& L, const double
   else if constexpr (G == 6) tile_gather_bal<R, PUB, true>(d, L, V, pub, acc, cost, smem);
   else if constexpr (G == 7) tile_gather_lds<R, PUB, false, KMX_SEG>(d, L, V, pub, acc, cost, smem);
   else if constexpr (G == 8) tile_gather_lds<R, PUB, true, KMX_SEG>(d, L, V, pub, acc, cost, smem);
-  else if constexpr (G == 9) tile_gather_bal<R, PUB, false, true>(d, L, V, pub, acc, cost, smem);
-  else if constexpr (G == 10) tile_gather_bal<R, PUB, true, true>(d, L, V, pub, acc, cost, smem);
   else tile_gather<R, PUB>(d, L, V, pub, acc, cost, smem);
 }
 
@@ -2688,7 +2669,6 @@ extern "C" int kmx_pgo_debug_gather_bench(kmx_pgo* h, int variant, int reps, dou
 #undef KMX_GB
 #define KMX_GB(V, G, W) case V: hipLaunchKernelGGL((k_gbench<5, G, W>), grid, blk, (SmemG<5, G>::bytes), h->stream, h->dv, (const double*)h->dv.X, out); return true;
       KMX_GB(70, 7, 1) KMX_GB(71, 7, 4) KMX_GB(72, 7, 5) KMX_GB(75, 8, 1)
-      KMX_GB(90, 9, 1) KMX_GB(91, 9, 6) KMX_GB(95, 10, 1)
 #define KMX_GC(V, C) case V: hipLaunchKernelGGL((k_gcap<5, C>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
       KMX_GC(50, 1000) KMX_GC(51, 12) KMX_GC(52, 10) KMX_GC(53, 8) KMX_GC(54, 4)
 #undef KMX_GC
