@@ -116,7 +116,7 @@ def lcd_leg(args, rank, world, barrier_sync):
     from kmx.lcd import LcdParams, LoopClosureDetector
     from kmx.synth.lcd import make_lcd_pool
     pool = make_lcd_pool(args.lcd_frames, 500, seed=0)
-    det = LoopClosureDetector(LcdParams(), device=int(os.environ.get("LOCAL_RANK", "0")))
+    det = LoopClosureDetector(LcdParams(), device=int(os.environ.get("KMX_BENCH_DEVICE", "0")))
     det.set_pool(pool)
     cq = pool.cand_query[rank::world].copy()
     cm = pool.cand_match[rank::world].copy()
@@ -164,7 +164,7 @@ def bow_leg(args, rank, world, barrier_sync):
     db = st.subset(np.nonzero(st.robot == 0)[0])
     qi = np.nonzero(st.robot == 1)[0][rank::world]
     qs = st.subset(qi)
-    G = BowDatabase(st.n_words, device=int(os.environ.get("LOCAL_RANK", "0")))
+    G = BowDatabase(st.n_words, device=int(os.environ.get("KMX_BENCH_DEVICE", "0")))
     G.set_entries(db.vptr, db.words, db.weights)
     G.query_async(qs.vptr, qs.words, qs.weights, 50)  # warmup
     G.sync()
@@ -204,6 +204,10 @@ def load_traffic():
         except Exception:
             return None
     return None
+
+
+def _coll_device(dist):
+    return "cuda" if dist.get_backend() == "nccl" else "cpu"
 
 
 def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, roofline=True):
@@ -249,7 +253,7 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, roof
     xs, xr = drv.exchange_rows
     if dist is not None:
         t = torch.tensor([el, edges_iters, hv_ms, hv_bytes, float(hv_n), float(xs), float(xr)],
-                         dtype=torch.float64, device="cuda")
+                         dtype=torch.float64, device=_coll_device(dist))
         parts = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(parts, t)
         parts = torch.stack(parts).cpu().numpy()
@@ -266,13 +270,21 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    # one GPU per rank; modulo the visible count only when rehearsing several ranks on one GPU
+    local_rank = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    os.environ["KMX_BENCH_DEVICE"] = str(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # KMX_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
+        # (exchange staged through host copies); the benchmark itself runs over RCCL
+        backend = os.environ.get("KMX_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         torch.cuda.synchronize()
@@ -358,7 +370,7 @@ def main():
         lcd, lcd_cpu = lcd_leg(args, rank, world, barrier)
         n_local, lel = float(lcd["n_local"] * lcd["steps"]), lcd["elapsed"]
         if dist is not None:
-            t = torch.tensor([n_local, lel], dtype=torch.float64, device="cuda")
+            t = torch.tensor([n_local, lel], dtype=torch.float64, device=_coll_device(dist))
             parts = [torch.zeros_like(t) for _ in range(world)]
             dist.all_gather(parts, t)
             parts = torch.stack(parts).cpu().numpy()
@@ -372,7 +384,7 @@ def main():
         bow, bow_cpu = bow_leg(args, rank, world, barrier)
         n_local, bel = float(bow["n_local"] * bow["steps"]), bow["elapsed"]
         if dist is not None:
-            t = torch.tensor([n_local, bel], dtype=torch.float64, device="cuda")
+            t = torch.tensor([n_local, bel], dtype=torch.float64, device=_coll_device(dist))
             parts = [torch.zeros_like(t) for _ in range(world)]
             dist.all_gather(parts, t)
             parts = torch.stack(parts).cpu().numpy()
