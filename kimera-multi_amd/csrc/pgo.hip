@@ -107,6 +107,10 @@ struct Dev {
   double* etau;
   double* ew;         // GNC weight
   const int2* eipos;  // [mloc] incidence positions (tail, head) of each local edge, -1 if not local
+  const int2* cipos;  // [mloc] the same positions in crec (differs from eipos in the segment-major layout)
+  const int* trec0;   // [ntiles] segment-major layout (rect): first crec record of each tile
+  const int* torec0;  // [ntiles] ... and of ocrec
+  int rect;           // crec / ocrec in segment-major order (gather G = 5/6 only)
   double *X, *Xt, *g, *r, *z, *eta, *del, *hd, *S, *Pinv, *pub;
   double* part;       // [ntiles][NPART]
   Ctl* ctl;
@@ -598,6 +602,8 @@ __device__ __forceinline__ void tile_gather_bal(const Dev& d, const Lane& L, con
   const int tid = threadIdx.x;
   const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
   const int K0 = ptr[p0];
+  const bool rect = d.rect != 0;
+  const int rbase = rect ? (OWN ? d.torec0 : d.trec0)[L.tile] : 0;
   __syncthreads();  // LDS reuse across consecutive gathers in one kernel (k_eval)
   if (tid <= np) sptr[tid] = ptr[p0 + tid] - K0;
   if constexpr (!OWN)
@@ -643,7 +649,10 @@ __device__ __forceinline__ void tile_gather_bal(const Dev& d, const Lane& L, con
         pn = next_pose(p);
         if (pn < np && sptr[pn] < s1) load4(V + (size_t)(p0 + pn) * 4 * R + 4 * L.a, vn);
       }
-      const double2* q2 = reinterpret_cast<const double2*>(rec + 12 * (size_t)(K0 + k));
+      // segment-major layout: step j of every group of the tile is one run of
+      // consecutive records, so a wave's 12 groups read 1152 contiguous bytes
+      const size_t ri = rect ? (size_t)rbase + (size_t)(k - s0) * TP + g : (size_t)(K0 + k);
+      const double2* q2 = reinterpret_cast<const double2*>(rec + 12 * ri);
       double2 q[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) q[i] = q2[i];
@@ -1410,8 +1419,9 @@ __global__ void k_apply_weights(Dev d, int mloc) {
   if (ip.x >= 0) { d.irec[16 * (size_t)ip.x + 12] = wk; d.irec[16 * (size_t)ip.x + 13] = wt; }
   if (ip.y >= 0) { d.irec[16 * (size_t)ip.y + 12] = wk; d.irec[16 * (size_t)ip.y + 13] = wt; }
   if (d.crec) {
-    if (ip.x >= 0) { d.crec[12 * (size_t)ip.x + 9] = wk; d.crec[12 * (size_t)ip.x + 10] = wt; }
-    if (ip.y >= 0) { d.crec[12 * (size_t)ip.y + 9] = wk; d.crec[12 * (size_t)ip.y + 10] = wt; }
+    const int2 cp = d.cipos[e];
+    if (cp.x >= 0) { d.crec[12 * (size_t)cp.x + 9] = wk; d.crec[12 * (size_t)cp.x + 10] = wt; }
+    if (cp.y >= 0) { d.crec[12 * (size_t)cp.y + 9] = wk; d.crec[12 * (size_t)cp.y + 10] = wt; }
     const int2 op = d.eopos[e];
     if (op.x >= 0) { d.ocrec[12 * (size_t)op.x + 9] = wk; d.ocrec[12 * (size_t)op.x + 10] = wt; }
     if (op.y >= 0) { d.ocrec[12 * (size_t)op.y + 9] = wk; d.ocrec[12 * (size_t)op.y + 10] = wt; }
@@ -1665,6 +1675,10 @@ struct kmx_pgo {
   int* d_optr = nullptr;
   int2* d_eopos = nullptr;
   bool compact_ok = false;
+  bool rect = false;                // crec / ocrec in segment-major order (G = 5)
+  int* d_trec0 = nullptr;
+  int* d_torec0 = nullptr;
+  int2* d_cipos = nullptr;
   double *d_ekappa = nullptr, *d_etau = nullptr, *d_ew = nullptr;
   int2* d_eipos = nullptr;
   double* d_vec = nullptr;  // X Xt g r z eta del hd
@@ -1713,12 +1727,14 @@ void free_dev(kmx_pgo* h) {
   void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_inc,
                   h->d_irec, h->d_crec, h->d_ocrec, h->d_optr, h->d_eopos, h->d_ekappa, h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_pub, h->d_part, h->d_ctl, h->d_cnt,
                   h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src, h->d_gnc_edge, h->d_gnc_ends,
-                  h->d_sh_edge, h->d_sh_idx, h->d_osh_edge, h->d_osh_idx, h->d_active, h->d_scratch, h->d_tickets};
+                  h->d_sh_edge, h->d_sh_idx, h->d_osh_edge, h->d_osh_idx, h->d_active, h->d_scratch, h->d_tickets,
+                  h->d_trec0, h->d_torec0, h->d_cipos};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
   h->d_inc = nullptr; h->d_eipos = nullptr; h->d_optr = nullptr; h->d_eopos = nullptr; h->d_irec = h->d_crec = h->d_ocrec = h->d_ekappa = h->d_etau = h->d_ew = nullptr; h->d_vec = h->d_S = h->d_Pinv = h->d_pub = h->d_part = nullptr;
   h->d_ctl = nullptr; h->d_cnt = nullptr; h->d_m_robot = nullptr; h->d_n_robot = nullptr;
+  h->d_trec0 = h->d_torec0 = nullptr; h->d_cipos = nullptr;
   h->d_pub_src = h->d_own_src = h->d_gnc_edge = nullptr; h->d_gnc_ends = nullptr;
   h->d_sh_edge = h->d_sh_idx = nullptr; h->d_osh_edge = h->d_osh_idx = nullptr; h->d_active = nullptr; h->d_scratch = nullptr; h->d_tickets = nullptr;
 }
@@ -2179,6 +2195,56 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       if (ocrec.empty()) ocrec.assign(12, 0.0);
     }
   }
+  // Segment-major record layout for the degree-balanced gather (G = 5/6): a
+  // tile's n incidences form TP lane-group segments of S = ceil(n / TP); the
+  // record of (segment g, step j) is stored at tile base + j*TP + g, so at every
+  // step the groups of a wave read consecutive records (full cache lines)
+  // instead of TP records S apart. KMX_RECT=0 keeps CSR order.
+  std::vector<int> trec0, torec0;
+  std::vector<int2> cipos;
+  h->rect = false;
+  {
+    bool want = true;
+    if (const char* v = std::getenv("KMX_RECT")) want = std::atoi(v) != 0;
+    if (want && h->gvar == 5) {
+      const int TP = WAVES * (64 / r);
+      auto transpose = [&](const std::vector<int>& ptr, std::vector<double>& rec, std::vector<int>& base,
+                           std::vector<int64_t>& map) {
+        base.assign(h->ntiles + 1, 0);
+        int64_t tot = 0;
+        for (int t = 0; t < h->ntiles; ++t) {
+          const int n = ptr[tp0[t] + tnp[t]] - ptr[tp0[t]];
+          base[t] = (int)tot;
+          tot += (int64_t)TP * std::max(1, (n + TP - 1) / TP);
+        }
+        base[h->ntiles] = (int)tot;
+        std::vector<double> out((size_t)std::max<int64_t>(tot, 1) * 12, 0.0);
+        map.assign(rec.size() / 12, -1);
+        for (int t = 0; t < h->ntiles; ++t) {
+          const int K0 = ptr[tp0[t]], n = ptr[tp0[t] + tnp[t]] - K0;
+          const int S = std::max(1, (n + TP - 1) / TP);
+          for (int k = 0; k < n; ++k) {
+            const int64_t dst = base[t] + (int64_t)(k % S) * TP + k / S;
+            std::memcpy(&out[(size_t)dst * 12], &rec[(size_t)(K0 + k) * 12], 12 * sizeof(double));
+            map[K0 + k] = dst;
+          }
+        }
+        rec.swap(out);
+      };
+      std::vector<int64_t> cmap, omap;
+      transpose(inc_ptr, crec, trec0, cmap);
+      transpose(optr, ocrec, torec0, omap);
+      cipos.assign(std::max(h->mloc, 1), make_int2(-1, -1));
+      for (int k = 0; k < h->mloc; ++k) {
+        cipos[k].x = eipos[k].x >= 0 ? (int)cmap[eipos[k].x] : -1;
+        cipos[k].y = eipos[k].y >= 0 ? (int)cmap[eipos[k].y] : -1;
+        int2& ep = eopos[k];
+        ep.x = ep.x >= 0 ? (int)omap[ep.x] : -1;
+        ep.y = ep.y >= 0 ? (int)omap[ep.y] : -1;
+      }
+      h->rect = true;
+    }
+  }
   if ((rc = dalloc(&h->d_tile_robot, h->ntiles)) || (rc = dalloc(&h->d_tile_p0, h->ntiles)) ||
       (rc = dalloc(&h->d_tile_np, h->ntiles)) || (rc = dalloc(&h->d_rtile0, L + 1)) ||
       (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_inc, inc.size())) ||
@@ -2220,6 +2286,16 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     KMX_HIP(up(h->d_ocrec, ocrec.data(), sizeof(double) * ocrec.size()));
     KMX_HIP(up(h->d_optr, optr.data(), sizeof(int) * optr.size()));
     KMX_HIP(up(h->d_eopos, eopos.data(), sizeof(int2) * eopos.size()));
+  }
+  if (h->rect) {
+    if ((rc = dalloc(&h->d_trec0, trec0.size())) || (rc = dalloc(&h->d_torec0, torec0.size())) ||
+        (rc = dalloc(&h->d_cipos, cipos.size()))) {
+      free_dev(h);
+      return rc;
+    }
+    KMX_HIP(up(h->d_trec0, trec0.data(), sizeof(int) * trec0.size()));
+    KMX_HIP(up(h->d_torec0, torec0.data(), sizeof(int) * torec0.size()));
+    KMX_HIP(up(h->d_cipos, cipos.data(), sizeof(int2) * cipos.size()));
   }
   KMX_HIP(up(h->d_ekappa, h->ek_h.data(), sizeof(double) * h->ek_h.size()));
   KMX_HIP(up(h->d_etau, h->et_h.data(), sizeof(double) * h->et_h.size()));
@@ -2266,6 +2342,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   d.inc_ptr = h->d_inc_ptr; d.inc = h->d_inc; d.irec = h->d_irec; d.crec = h->d_crec;
   d.ocrec = h->d_ocrec; d.optr = h->d_optr; d.eopos = h->d_eopos;
   d.ekappa = h->d_ekappa; d.etau = h->d_etau; d.ew = h->d_ew; d.eipos = h->d_eipos;
+  d.cipos = h->rect ? h->d_cipos : h->d_eipos;
+  d.trec0 = h->d_trec0; d.torec0 = h->d_torec0; d.rect = h->rect ? 1 : 0;
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
   d.z = h->d_vec + 4 * vec; d.eta = h->d_vec + 5 * vec; d.del = h->d_vec + 6 * vec; d.hd = h->d_vec + 7 * vec;
   d.S = h->d_S; d.Pinv = h->d_Pinv; d.pub = h->d_pub; d.part = h->d_part; d.ctl = h->d_ctl; d.cnt = h->d_cnt; d.tickets = h->d_tickets;
