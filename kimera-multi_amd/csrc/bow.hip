@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -174,6 +175,244 @@ __global__ __launch_bounds__(BOW_BLOCK) void k_bow_query(BowDb db, int nq, const
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_bow_query_lds: the same queryL1 with the accumulator in LDS.
+//   * The database's entries are cut into chunks of `ch` (<= LCH) entries; a
+//     chunk's accumulator is an LDS array, so the per-posting read-modify-write
+//     that bounds k_bow_query (a dependent HBM round trip per word, then a
+//     workgroup barrier) becomes an LDS one.
+//   * Within a chunk, wave v of the LW_WAVES owns the entry sub-range
+//     [v*sch, (v+1)*sch): it walks the query's words in order over its own
+//     part of each posting list ([cptr[w][s], cptr[w][s+1]), s = sub-chunk;
+//     lists ascend in entry id). No two waves touch an entry and a wave's LDS
+//     operations complete in order, so every entry accumulates in DBoW2's
+//     word order with no barrier at all, and each wave keeps the postings of
+//     the next 12 words in flight (a ring of four 4-word register sets).
+//   * After each chunk, the chunk's K best (acc, id) are selected as in
+//     k_bow_query (LDS histograms + bitonic sort) and merged with the running
+//     list by merge-path ranks, so the result equals a top-K over all entries.
+constexpr int LW_WAVES = 16;
+constexpr int LW_BLOCK = 64 * LW_WAVES;
+constexpr int LCH = 15360;     // max entries per chunk (120 KB of LDS), a multiple of LW_WAVES
+constexpr int LSEL = 1024;     // candidate cap per chunk
+constexpr int QW = 128;        // query words staged per batch
+constexpr int PD = 4;          // words per prefetch set (four sets in flight)
+
+__global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int* cptr, int nch, int ch, int nq,
+                                                            const long long* qptr, const unsigned* qw,
+                                                            const double* qv, const int* max_id, int K,
+                                                            int* out_n, int* out_id, double* out_score,
+                                                            int* err) {
+  extern __shared__ __attribute__((aligned(16))) char bsm[];
+  double* acc = reinterpret_cast<double*>(bsm);                   // [ch]
+  double* c_val = acc + LCH;                                        // [LSEL]
+  double* r_val = c_val + LSEL;                                     // [MAX_RESULTS] running best
+  double* m_val = r_val + MAX_RESULTS;                              // [MAX_RESULTS] merge output
+  double* wq = m_val + MAX_RESULTS;                                 // [QW] query weights
+  int* c_id = reinterpret_cast<int*>(wq + QW);                      // [LSEL]
+  int* r_id = c_id + LSEL;                                          // [MAX_RESULTS]
+  int* m_id = r_id + MAX_RESULTS;                                   // [MAX_RESULTS]
+  int* wa = m_id + MAX_RESULTS;                                     // [LW_WAVES][QW] posting range start
+  int* wb = wa + LW_WAVES * QW;                                     // [LW_WAVES][QW] ... and end
+  int* hist = wb + LW_WAVES * QW;                                   // [NBINS]
+  __shared__ int s_ns, s_b, s_cb, s_done, s_nt, s_nr;
+  const int tid = threadIdx.x, v = tid >> 6, lane = tid & 63;
+  const int nsub = nch * LW_WAVES, sch = ch / LW_WAVES;
+  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+    const int mid = max_id ? max_id[q] : -1;
+    const int lim = (mid < 0) ? db.n_entries : min(mid, db.n_entries);  // entries < lim are eligible
+    const long long q0 = qptr[q], q1 = qptr[q + 1];
+    if (tid == 0) s_nr = 0;
+    for (int c = 0; c < nch && c * ch < lim; ++c) {
+      const int lo = c * ch, n_here = min(ch, lim - lo);
+      for (int i = tid; i < n_here; i += LW_BLOCK) acc[i] = 0.0;
+      // ---- accumulation, query words in order, QW words staged at a time
+      for (long long b0 = q0; b0 < q1; b0 += QW) {
+        const int nw = (int)min((long long)QW, q1 - b0);
+        __syncthreads();  // accumulator zeroed / previous batch's word table no longer read
+        for (int k = tid; k < nw * LW_WAVES; k += LW_BLOCK) {
+          const int i = k / LW_WAVES, u = k - i * LW_WAVES;
+          const unsigned w = qw[b0 + i];
+          int a = 0, b = 0;
+          const int sub = c * LW_WAVES + u;
+          if (w < (unsigned)db.n_words && lo + u * sch < lim) {
+            a = cptr[(size_t)w * (nsub + 1) + sub];
+            b = cptr[(size_t)w * (nsub + 1) + sub + 1];
+            if (lo + (u + 1) * sch > lim)  // the sub-range holding max_id: drop entries >= lim
+              while (a < b && db.ent[b - 1] >= lim) --b;
+          }
+          wa[u * QW + i] = a;
+          wb[u * QW + i] = b;
+          if (u == 0) wq[i] = qv[b0 + i];
+        }
+        __syncthreads();
+        const int* my_a = wa + v * QW;
+        const int* my_b = wb + v * QW;
+        auto fetch = [&](int i0, int* e, double* dv) {
+#pragma unroll
+          for (int u = 0; u < PD; ++u) {
+            const int i = i0 + u;
+            e[u] = -1;
+            dv[u] = 0.0;
+            if (i < nw) {
+              const int sl = my_a[i] + lane;
+              if (sl < my_b[i]) { e[u] = db.ent[sl]; dv[u] = db.wt[sl]; }
+            }
+          }
+        };
+        auto process = [&](int i0, const int* e, const double* dv) {
+#pragma unroll
+          for (int u = 0; u < PD; ++u) {
+            const int i = i0 + u;
+            if (i < nw) {
+              const double qval = wq[i];
+              if (e[u] >= 0) acc[e[u] - lo] += fabs(qval - dv[u]) - fabs(qval) - fabs(dv[u]);
+              if (my_b[i] - my_a[i] > 64) {  // rare: a word with > 64 postings in this sub-range
+                for (int sl = my_a[i] + 64 + lane; sl < my_b[i]; sl += 64) {
+                  const double d = db.wt[sl];
+                  acc[db.ent[sl] - lo] += fabs(qval - d) - fabs(qval) - fabs(d);
+                }
+              }
+            }
+          }
+        };
+        int eA[PD], eB[PD], eC[PD], eD[PD];
+        double dA[PD], dB[PD], dC[PD], dD[PD];
+        fetch(0, eA, dA);
+        fetch(PD, eB, dB);
+        fetch(2 * PD, eC, dC);
+        for (int i0 = 0; i0 < nw; i0 += 4 * PD) {
+          fetch(i0 + 3 * PD, eD, dD);
+          process(i0, eA, dA);
+          fetch(i0 + 4 * PD, eA, dA);
+          process(i0 + PD, eB, dB);
+          fetch(i0 + 5 * PD, eB, dB);
+          process(i0 + 2 * PD, eC, dC);
+          fetch(i0 + 6 * PD, eC, dC);
+          process(i0 + 3 * PD, eD, dD);
+        }
+      }
+      __syncthreads();
+      // ---- this chunk's best min(K, touched) by (acc, id): LDS histogram narrowing
+      if (tid == 0) { s_nt = 0; s_ns = 0; s_done = 0; }
+      __syncthreads();
+      {
+        int cnt = 0;
+        for (int i = tid; i < n_here; i += LW_BLOCK) cnt += (acc[i] != 0.0) ? 1 : 0;
+        if (cnt) atomicAdd(&s_nt, cnt);
+      }
+      __syncthreads();
+      const int nt = s_nt;
+      const int need0 = min(K, nt);
+      int need = need0;
+      double lvl_lo[LEVELS], lvl_w[LEVELS];
+      int lvl_b[LEVELS];
+      auto bin_of = [&](double a, int l) {
+        int bb = (int)floor((a - lvl_lo[l]) / lvl_w[l]);
+        return bb < 0 ? 0 : (bb >= NBINS ? NBINS - 1 : bb);
+      };
+      auto in_play = [&](double a, int level) {
+        for (int l = 0; l < level; ++l)
+          if (bin_of(a, l) != lvl_b[l]) return false;
+        return true;
+      };
+      for (int level = 0; level < LEVELS && need > 0; ++level) {
+        lvl_lo[level] = level == 0 ? -2.0 : lvl_lo[level - 1] + lvl_b[level - 1] * lvl_w[level - 1];
+        lvl_w[level] = (level == 0 ? 2.0 : lvl_w[level - 1]) / NBINS;
+        for (int b = tid; b < NBINS; b += LW_BLOCK) hist[b] = 0;
+        __syncthreads();
+        for (int i = tid; i < n_here; i += LW_BLOCK) {
+          const double a = acc[i];
+          if (a != 0.0 && in_play(a, level)) atomicAdd(&hist[bin_of(a, level)], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          int cum = 0, b = 0;
+          for (; b < NBINS; ++b) {
+            if (cum + hist[b] >= need) break;
+            cum += hist[b];
+          }
+          if (b == NBINS) b = NBINS - 1;
+          s_b = b;
+          s_cb = cum;
+          s_done = (s_ns + cum + hist[b] <= LSEL) ? 1 : 0;
+        }
+        __syncthreads();
+        const int b = s_b, done = s_done, cb = s_cb;
+        lvl_b[level] = b;
+        for (int i = tid; i < n_here; i += LW_BLOCK) {
+          const double a = acc[i];
+          if (a == 0.0 || !in_play(a, level)) continue;
+          const int bb = bin_of(a, level);
+          if (bb < b || (done && bb == b)) {
+            const int slot = atomicAdd(&s_ns, 1);
+            if (slot < LSEL) { c_val[slot] = a; c_id[slot] = lo + i; }
+          }
+        }
+        __syncthreads();
+        if (done) { need = 0; break; }
+        need -= cb;
+      }
+      if (need > 0 && tid == 0) atomicExch(err, 1);  // > LSEL exactly tied scores
+      const int nc = min(s_ns, LSEL);
+      int n2 = 1;
+      while (n2 < nc) n2 <<= 1;
+      for (int i = nc + tid; i < n2; i += LW_BLOCK) { c_val[i] = 1.0; c_id[i] = 0x7fffffff; }
+      __syncthreads();
+      for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = tid; i < n2; i += LW_BLOCK) {
+            const int l = i ^ j;
+            if (l > i) {
+              const bool up = (i & k) == 0;
+              const bool sw = up ? key_less(c_val[l], c_id[l], c_val[i], c_id[i])
+                                 : key_less(c_val[i], c_id[i], c_val[l], c_id[l]);
+              if (sw) {
+                const double tv = c_val[i]; c_val[i] = c_val[l]; c_val[l] = tv;
+                const int ti = c_id[i]; c_id[i] = c_id[l]; c_id[l] = ti;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      // ---- merge the chunk's sorted best (na) into the running best (nr) by ranks
+      const int na = min(need0, nc), nr = s_nr;
+      const int nm = min(K, na + nr);
+      for (int i = tid; i < na + nr; i += LW_BLOCK) {
+        const bool fromA = i < na;
+        const int k = fromA ? i : i - na;
+        const double val = fromA ? c_val[k] : r_val[k];
+        const int id = fromA ? c_id[k] : r_id[k];
+        int l = 0, h = fromA ? nr : na;  // elements of the other list ordered before (val, id)
+        while (l < h) {
+          const int m = (l + h) >> 1;
+          const bool before = fromA ? key_less(r_val[m], r_id[m], val, id) : key_less(c_val[m], c_id[m], val, id);
+          if (before) l = m + 1;
+          else h = m;
+        }
+        const int pos = k + l;
+        if (pos < nm) { m_val[pos] = val; m_id[pos] = id; }
+      }
+      __syncthreads();
+      for (int i = tid; i < nm; i += LW_BLOCK) { r_val[i] = m_val[i]; r_id[i] = m_id[i]; }
+      if (tid == 0) s_nr = nm;
+      __syncthreads();
+    }
+    __syncthreads();
+    const int nout = s_nr;
+    for (int i = tid; i < nout; i += LW_BLOCK) {
+      out_id[(size_t)q * K + i] = r_id[i];
+      out_score[(size_t)q * K + i] = -r_val[i] / 2.0;
+    }
+    if (tid == 0) out_n[q] = nout;
+    __syncthreads();
+  }
+}
+constexpr size_t LDS_BOW = sizeof(double) * (LCH + LSEL + 2 * MAX_RESULTS + QW) +
+                           sizeof(int) * (LSEL + 2 * MAX_RESULTS + 2 * LW_WAVES * QW + NBINS);
+static_assert(LDS_BOW + 64 <= 160 * 1024, "k_bow_query_lds exceeds the 160 KiB of LDS per CU");
+
 // L1Scoring::score of pairs (a_i, b_i): merge of the two sorted word lists.
 __global__ void k_bow_pair_score(int n, const long long* aptr, const unsigned* aw, const double* av,
                                  const long long* bptr, const unsigned* bw, const double* bv, double* out) {
@@ -219,6 +458,10 @@ struct kmx_bow {
   double* d_acc = nullptr;
   int* d_touched = nullptr;
   int* d_err = nullptr;
+  // LDS-accumulator query (k_bow_query_lds): per-word chunk split points
+  bool lds = true;
+  int ch = 0, nch = 0;
+  int* d_cptr = nullptr;
   size_t qcap = 0, wcap = 0;
   long long* d_qptr = nullptr;
   unsigned* d_qw = nullptr;
@@ -236,9 +479,10 @@ struct kmx_bow {
 
 namespace {
 void bow_free_db(kmx_bow* h) {
-  for (void* p : {(void*)h->d_ptr, (void*)h->d_ent, (void*)h->d_wt, (void*)h->d_acc, (void*)h->d_touched})
+  for (void* p : {(void*)h->d_ptr, (void*)h->d_ent, (void*)h->d_wt, (void*)h->d_acc, (void*)h->d_touched,
+                  (void*)h->d_cptr})
     if (p) (void)hipFree(p);
-  h->d_ptr = h->d_ent = nullptr;
+  h->d_ptr = h->d_ent = h->d_cptr = nullptr;
   h->d_wt = nullptr;
   h->d_acc = nullptr;
   h->d_touched = nullptr;
@@ -340,22 +584,45 @@ extern "C" int kmx_bow_set_database(kmx_bow* h, int32_t n_words, int32_t n_entri
   bow_free_db(h);
   h->n_words = n_words;
   h->n_entries = n_entries;
-  // persistent query workgroups: each owns an acc / touched scratch of n_entries
+  // KMX_BOW_LDS=0 selects the HBM-accumulator kernel; KMX_BOW_CHUNK sets the
+  // entries per LDS chunk (tests use small chunks to cover the merge)
+  h->lds = true;
+  if (const char* v = std::getenv("KMX_BOW_LDS")) h->lds = std::atoi(v) != 0;
+  h->ch = LCH;
+  if (const char* v = std::getenv("KMX_BOW_CHUNK")) h->ch = std::max(1, std::min(LCH, std::atoi(v)));
+  h->ch = (h->ch + LW_WAVES - 1) / LW_WAVES * LW_WAVES;  // whole sub-ranges, one per wave
+  h->nch = std::max(1, (n_entries + h->ch - 1) / h->ch);
+  std::vector<int> cptr;
+  if (h->lds) {  // first posting of each wave sub-range in every word's (ascending) list
+    const int nsub = h->nch * LW_WAVES, sch = h->ch / LW_WAVES;
+    cptr.assign((size_t)n_words * (nsub + 1), 0);
+    for (int w = 0; w < n_words; ++w) {
+      int p = ptr[w];
+      for (int c = 0; c <= nsub; ++c) {
+        const long long bound = (long long)c * sch;
+        while (p < ptr[w + 1] && ent[p] < bound) ++p;
+        cptr[(size_t)w * (nsub + 1) + c] = (c == nsub) ? ptr[w + 1] : p;
+      }
+    }
+  }
+  // persistent query workgroups: the HBM kernel gives each an acc / touched
+  // scratch of n_entries; the LDS kernel runs one workgroup per CU
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
-  h->n_wg = std::max(1, cus * 4);
+  h->n_wg = h->lds ? std::max(1, cus) : std::max(1, cus * 4);
+  const size_t scratch = h->lds ? 1 : (size_t)h->n_wg * std::max(n_entries, 1);
   int rc;
   if ((rc = bow_alloc(&h->d_ptr, ptr.size())) || (rc = bow_alloc(&h->d_ent, ent.size())) ||
-      (rc = bow_alloc(&h->d_wt, wt.size())) ||
-      (rc = bow_alloc(&h->d_acc, (size_t)h->n_wg * std::max(n_entries, 1))) ||
-      (rc = bow_alloc(&h->d_touched, (size_t)h->n_wg * std::max(n_entries, 1)))) {
+      (rc = bow_alloc(&h->d_wt, wt.size())) || (rc = bow_alloc(&h->d_acc, scratch)) ||
+      (rc = bow_alloc(&h->d_touched, scratch)) || (h->lds && (rc = bow_alloc(&h->d_cptr, cptr.size())))) {
     bow_free_db(h);
     return rc;
   }
+  if (h->lds) KMX_HIP(hipMemcpy(h->d_cptr, cptr.data(), sizeof(int) * cptr.size(), hipMemcpyHostToDevice));
   KMX_HIP(hipMemcpy(h->d_ptr, ptr.data(), sizeof(int) * ptr.size(), hipMemcpyHostToDevice));
   KMX_HIP(hipMemcpy(h->d_ent, ent.data(), sizeof(int) * ent.size(), hipMemcpyHostToDevice));
   KMX_HIP(hipMemcpy(h->d_wt, wt.data(), sizeof(double) * wt.size(), hipMemcpyHostToDevice));
-  KMX_HIP(hipMemset(h->d_acc, 0, sizeof(double) * (size_t)h->n_wg * std::max(n_entries, 1)));
+  KMX_HIP(hipMemset(h->d_acc, 0, sizeof(double) * scratch));
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -401,6 +668,15 @@ extern "C" int kmx_bow_query_async(kmx_bow* h, int32_t nq, const int64_t* qptr, 
   KMX_HIP(hipMemsetAsync(h->d_err, 0, sizeof(int), h->stream));
   BowDb db{h->d_ptr, h->d_ent, h->d_wt, h->n_words, h->n_entries};
   const int grid = std::min(nq, h->n_wg);
+  if (h->lds) {
+    hipLaunchKernelGGL(k_bow_query_lds, dim3(grid), dim3(LW_BLOCK), LDS_BOW, h->stream, db,
+                       (const int*)h->d_cptr, h->nch, h->ch, nq, (const long long*)h->d_qptr,
+                       (const unsigned*)h->d_qw, (const double*)h->d_qv,
+                       max_id ? (const int*)h->d_maxid : nullptr, max_results, h->d_n, h->d_id, h->d_score,
+                       h->d_err);
+    KMX_HIP(hipGetLastError());
+    return KMX_OK;
+  }
   hipLaunchKernelGGL(k_bow_query, dim3(grid), dim3(BOW_BLOCK), 0, h->stream, db, nq,
                      (const long long*)h->d_qptr, (const unsigned*)h->d_qw, (const double*)h->d_qv,
                      max_id ? (const int*)h->d_maxid : nullptr, max_results, h->d_acc, h->d_touched, h->d_n,
@@ -424,7 +700,7 @@ extern "C" int kmx_bow_query(kmx_bow* h, int32_t nq, const int64_t* qptr, const 
                          h->stream));
   KMX_HIP(hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  KMX_CHECK(!err, KMX_EUNSUP, "more than 2048 exactly tied scores at the max_results cut");
+  KMX_CHECK(!err, KMX_EUNSUP, "too many exactly tied scores at the max_results cut");
   return KMX_OK;
   KMX_GUARD_END
 }

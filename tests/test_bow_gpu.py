@@ -16,7 +16,13 @@ def stream():
     return make_bow_stream(2, 1500, n_words=50_000, seed=7)
 
 
-def test_query_bit_exact(gpu, stream):
+@pytest.mark.parametrize("env", [{}, {"KMX_BOW_CHUNK": "512"}, {"KMX_BOW_CHUNK": "97"}, {"KMX_BOW_LDS": "0"}])
+def test_query_bit_exact(gpu, stream, env, monkeypatch):
+    """Default: LDS accumulator in one chunk (1500 entries); small chunks cover
+    the per-chunk selection and the merge (and max_id cutting a chunk);
+    KMX_BOW_LDS=0 is the HBM-accumulator kernel."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     db = stream.subset(np.nonzero(stream.robot == 1)[0])
     qs = stream.subset(np.nonzero(stream.robot == 0)[0])
     G = BowDatabase(stream.n_words)
@@ -32,7 +38,10 @@ def test_query_bit_exact(gpu, stream):
             assert np.array_equal(sc[q, :n[q]], sc0[q, :n[q]]), (K, q)
 
 
-def test_edge_cases(gpu, stream):
+@pytest.mark.parametrize("env", [{}, {"KMX_BOW_CHUNK": "7"}, {"KMX_BOW_LDS": "0"}])
+def test_edge_cases(gpu, stream, env, monkeypatch):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     G = BowDatabase(stream.n_words)
     G.set_entries(np.zeros(1, np.int64), np.zeros(0, np.uint32), np.zeros(0))  # empty database
     n, _, _ = G.query(stream.vptr[:3], stream.words, stream.weights, 10)
