@@ -46,12 +46,46 @@ __device__ __forceinline__ bool key_less(double a, int ia, double b, int ib) {
   return a < b || (a == b && ia < ib);
 }
 
+// First histogram bin b at which the running count reaches `need` (the last
+// bin if none does), and the count strictly before it: a block-wide prefix
+// sum over NBINS bins (NBINS / BLOCK consecutive bins per thread), replacing
+// a serial walk over the bins by one thread. Results in *sb, *scb; needs a
+// __syncthreads() before they are read. `wsum` holds BLOCK / 64 ints.
+template <int BLOCK>
+__device__ __forceinline__ void find_bin(const int* hist, int need, int* wsum, int* sb, int* scb) {
+  constexpr int PER = NBINS / BLOCK;
+  static_assert(PER * BLOCK == NBINS, "NBINS must be a multiple of the block size");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int h[PER], mine = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) { h[k] = hist[tid * PER + k]; mine += h[k]; }
+  int incl = mine;  // inclusive scan over the wave
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += t;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int k = 0; k < w; ++k) base += wsum[k];
+  int cum = base + incl - mine;  // count before this thread's first bin
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int b = tid * PER + k;
+    if (cum < need && cum + h[k] >= need) { *sb = b; *scb = cum; }
+    else if (b == NBINS - 1 && cum + h[k] < need) { *sb = b; *scb = cum; }
+    cum += h[k];
+  }
+}
+
 __global__ __launch_bounds__(BOW_BLOCK) void k_bow_query(BowDb db, int nq, const long long* qptr,
                                                          const unsigned* qw, const double* qv,
                                                          const int* max_id, int K, double* acc_all,
                                                          int* touched_all, int* out_n, int* out_id,
                                                          double* out_score, int* err) {
   __shared__ int s_nt, s_ns, s_b, s_cb, s_done;
+  __shared__ int s_wsum[BOW_BLOCK / 64];
   __shared__ int hist[NBINS];
   __shared__ double c_val[SEL_CAP];
   __shared__ int c_id[SEL_CAP];
@@ -111,17 +145,9 @@ __global__ __launch_bounds__(BOW_BLOCK) void k_bow_query(BowDb db, int nq, const
         if (in_play(a, level)) atomicAdd(&hist[bin_of(a, level)], 1);
       }
       __syncthreads();
-      if (tid == 0) {  // first bin where the running count reaches `need`
-        int cum = 0, b = 0;
-        for (; b < NBINS; ++b) {
-          if (cum + hist[b] >= need) break;
-          cum += hist[b];
-        }
-        if (b == NBINS) b = NBINS - 1;
-        s_b = b;
-        s_cb = cum;  // entries in play strictly before bin b
-        s_done = (s_ns + cum + hist[b] <= SEL_CAP) ? 1 : 0;
-      }
+      find_bin<BOW_BLOCK>(hist, need, s_wsum, &s_b, &s_cb);  // first bin reaching `need`
+      __syncthreads();
+      if (tid == 0) s_done = (s_ns + s_cb + hist[s_b] <= SEL_CAP) ? 1 : 0;
       __syncthreads();
       const int b = s_b, done = s_done, cb = s_cb;
       lvl_b[level] = b;
@@ -186,36 +212,44 @@ __global__ __launch_bounds__(BOW_BLOCK) void k_bow_query(BowDb db, int nq, const
 //     part of each posting list ([cptr[w][s], cptr[w][s+1]), s = sub-chunk;
 //     lists ascend in entry id). No two waves touch an entry and a wave's LDS
 //     operations complete in order, so every entry accumulates in DBoW2's
-//     word order with no barrier at all, and each wave keeps the postings of
-//     the next 12 words in flight (a ring of four 4-word register sets).
+//     word order with no barrier at all. The wave applies several words'
+//     pieces per step (collisions detected by LDS marks) and keeps three
+//     steps of postings in flight (unconditional clamped loads, so the
+//     compiler waits only for the step being applied).
 //   * After each chunk, the chunk's K best (acc, id) are selected as in
 //     k_bow_query (LDS histograms + bitonic sort) and merged with the running
 //     list by merge-path ranks, so the result equals a top-K over all entries.
 constexpr int LW_WAVES = 16;
 constexpr int LW_BLOCK = 64 * LW_WAVES;
-constexpr int LCH = 15360;     // max entries per chunk (120 KB of LDS), a multiple of LW_WAVES
+constexpr int LCH = 14336;     // max entries per chunk (112 KB of LDS), a multiple of LW_WAVES
 constexpr int LSEL = 1024;     // candidate cap per chunk
 constexpr int QW = 128;        // query words staged per batch
-constexpr int PD = 4;          // words per prefetch set (four sets in flight)
+#ifndef KMX_BOW_PG
+#define KMX_BOW_PG 8
+#endif
+constexpr int PG = KMX_BOW_PG;  // lanes per piece group: a step applies 64 / PG pieces of <= PG postings
+constexpr int NGRP = 64 / PG;
+constexpr int PC = 176;        // pieces per wave table
 
 __global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int* cptr, int nch, int ch, int nq,
                                                             const long long* qptr, const unsigned* qw,
                                                             const double* qv, const int* max_id, int K,
                                                             int* out_n, int* out_id, double* out_score,
-                                                            int* err) {
+                                                            int* err, int dbg) {
   extern __shared__ __attribute__((aligned(16))) char bsm[];
   double* acc = reinterpret_cast<double*>(bsm);                   // [ch]
-  double* c_val = acc + LCH;                                        // [LSEL]
-  double* r_val = c_val + LSEL;                                     // [MAX_RESULTS] running best
-  double* m_val = r_val + MAX_RESULTS;                              // [MAX_RESULTS] merge output
-  double* wq = m_val + MAX_RESULTS;                                 // [QW] query weights
-  int* c_id = reinterpret_cast<int*>(wq + QW);                      // [LSEL]
-  int* r_id = c_id + LSEL;                                          // [MAX_RESULTS]
-  int* m_id = r_id + MAX_RESULTS;                                   // [MAX_RESULTS]
-  int* wa = m_id + MAX_RESULTS;                                     // [LW_WAVES][QW] posting range start
-  int* wb = wa + LW_WAVES * QW;                                     // [LW_WAVES][QW] ... and end
-  int* hist = wb + LW_WAVES * QW;                                   // [NBINS]
+  double* c_val = acc + LCH;                                        // [LSEL]        \  selection scratch;
+  double* m_val = c_val + LSEL;                                     // [MAX_RESULTS]  | the accumulation's
+  int* c_id = reinterpret_cast<int*>(m_val + MAX_RESULTS);          // [LSEL]         | conflict marks
+  int* m_id = c_id + LSEL;                                          // [MAX_RESULTS] /  alias it
+  double* r_val = reinterpret_cast<double*>(m_id + MAX_RESULTS);    // [MAX_RESULTS] running best
+  double* wq = r_val + MAX_RESULTS;                                 // [QW] query weights
+  int* r_id = reinterpret_cast<int*>(wq + QW);                      // [MAX_RESULTS]
+  int* pstart = r_id + MAX_RESULTS;                                 // [LW_WAVES][PC] piece: first posting
+  unsigned short* pinfo = reinterpret_cast<unsigned short*>(pstart + LW_WAVES * PC);  // len-1 | word << 4
+  int* hist = reinterpret_cast<int*>(pinfo + LW_WAVES * PC);        // [NBINS]
   __shared__ int s_ns, s_b, s_cb, s_done, s_nt, s_nr;
+  __shared__ int s_wsum[LW_WAVES];
   const int tid = threadIdx.x, v = tid >> 6, lane = tid & 63;
   const int nsub = nch * LW_WAVES, sch = ch / LW_WAVES;
   for (int q = blockIdx.x; q < nq; q += gridDim.x) {
@@ -226,74 +260,125 @@ __global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int*
     for (int c = 0; c < nch && c * ch < lim; ++c) {
       const int lo = c * ch, n_here = min(ch, lim - lo);
       for (int i = tid; i < n_here; i += LW_BLOCK) acc[i] = 0.0;
-      // ---- accumulation, query words in order, QW words staged at a time
-      for (long long b0 = q0; b0 < q1; b0 += QW) {
-        const int nw = (int)min((long long)QW, q1 - b0);
-        __syncthreads();  // accumulator zeroed / previous batch's word table no longer read
-        for (int k = tid; k < nw * LW_WAVES; k += LW_BLOCK) {
-          const int i = k / LW_WAVES, u = k - i * LW_WAVES;
-          const unsigned w = qw[b0 + i];
-          int a = 0, b = 0;
-          const int sub = c * LW_WAVES + u;
-          if (w < (unsigned)db.n_words && lo + u * sch < lim) {
-            a = cptr[(size_t)w * (nsub + 1) + sub];
-            b = cptr[(size_t)w * (nsub + 1) + sub + 1];
-            if (lo + (u + 1) * sch > lim)  // the sub-range holding max_id: drop entries >= lim
-              while (a < b && db.ent[b - 1] >= lim) --b;
-          }
-          wa[u * QW + i] = a;
-          wb[u * QW + i] = b;
-          if (u == 0) wq[i] = qv[b0 + i];
-        }
-        __syncthreads();
-        const int* my_a = wa + v * QW;
-        const int* my_b = wb + v * QW;
-        auto fetch = [&](int i0, int* e, double* dv) {
-#pragma unroll
-          for (int u = 0; u < PD; ++u) {
-            const int i = i0 + u;
-            e[u] = -1;
-            dv[u] = 0.0;
-            if (i < nw) {
-              const int sl = my_a[i] + lane;
-              if (sl < my_b[i]) { e[u] = db.ent[sl]; dv[u] = db.wt[sl]; }
+      // ---- accumulation, query words in order, QW words staged at a time.
+      // Each wave turns its sub-range of the batch's posting lists into pieces
+      // of <= PG postings (a long list becomes consecutive pieces of the same
+      // word) and applies 64 / PG pieces per step, one per PG-lane group
+      // (PG = 8: 8 pieces; 16 and 32 measured 5 % and 29 % slower). Pieces of
+      // different words may hit the same entry: the lanes mark their entries
+      // with their group and read the marks back; on a collision the step's
+      // pieces are applied one after another, so every entry still
+      // accumulates in word order.
+      int* my_start = pstart + v * PC;
+      unsigned short* my_info = pinfo + v * PC;
+      // volatile: the read-back must see other lanes' writes (no store-to-load forwarding)
+      volatile unsigned char* mark = reinterpret_cast<unsigned char*>(c_val) + v * sch;
+      const int g = lane / PG, j = lane - g * PG;
+      const int sub = c * LW_WAVES + v;
+      const bool sub_live = lo + v * sch < lim;
+      const bool sub_cut = lo + (v + 1) * sch > lim;  // the sub-range holding max_id: drop entries >= lim
+      const int mlo = lo + v * sch;
+      auto run = [&](int np) {  // apply this wave's piece table [0, np)
+        const int nst = (np + NGRP - 1) / NGRP;
+        auto fetch = [&](int st, int& e, double& dv, int& wi, bool& ok) {
+          const int pc = min(NGRP * st + g, max(np - 1, 0));
+          const unsigned info = my_info[pc];
+          ok = (NGRP * st + g < np) && (j <= (int)(info & 31u));
+          wi = (int)(info >> 5);
+          const int idx = ok ? my_start[pc] + j : 0;
+          e = db.ent[idx];
+          dv = db.wt[idx];
+        };
+        auto apply = [&](int e, double dv, int wi, bool ok) {
+          const int el = e - mlo;
+          if (ok) mark[el] = (unsigned char)g;
+          bool clash = ok && mark[el] != (unsigned char)g;
+          const double qval = wq[wi];
+          const double val = fabs(qval - dv) - fabs(qval) - fabs(dv);
+          if (!__any(clash)) {
+            if (ok) acc[e - lo] += val;
+          } else {  // one group at a time, in piece (= word) order
+            volatile double* vacc = acc;
+            for (int gg = 0; gg < NGRP; ++gg) {
+              if (ok && g == gg) vacc[e - lo] = vacc[e - lo] + val;
+              __builtin_amdgcn_wave_barrier();
+              asm volatile("" ::: "memory");
             }
           }
         };
-        auto process = [&](int i0, const int* e, const double* dv) {
+        int e0, e1, e2, e3, w0, w1, w2, w3;
+        double d0, d1, d2, d3;
+        bool k0, k1, k2, k3;
+        fetch(0, e0, d0, w0, k0);
+        fetch(1, e1, d1, w1, k1);
+        fetch(2, e2, d2, w2, k2);
+        for (int st = 0; st < nst; st += 4) {
+          fetch(st + 3, e3, d3, w3, k3);
+          apply(e0, d0, w0, k0);
+          if (st + 1 >= nst) break;
+          fetch(st + 4, e0, d0, w0, k0);
+          apply(e1, d1, w1, k1);
+          if (st + 2 >= nst) break;
+          fetch(st + 5, e1, d1, w1, k1);
+          apply(e2, d2, w2, k2);
+          if (st + 3 >= nst) break;
+          fetch(st + 6, e2, d2, w2, k2);
+          apply(e3, d3, w3, k3);
+        }
+      };
+      for (long long b0 = q0; b0 < q1 && !(dbg & 1); b0 += QW) {
+        const int nw = (int)min((long long)QW, q1 - b0);
+        __syncthreads();  // accumulator zeroed / previous batch's weights no longer read
+        for (int i = tid; i < nw; i += LW_BLOCK) wq[i] = qv[b0 + i];
+        __syncthreads();
+        int np = 0;
+        for (int w0 = 0; w0 < nw; w0 += 64) {
+          // this lane's word: posting range in the wave's sub-range, piece count
+          const int i = w0 + lane;
+          int a = 0, b = 0;
+          if (i < nw && sub_live) {
+            const unsigned w = qw[b0 + i];
+            if (w < (unsigned)db.n_words) {
+              a = cptr[(size_t)w * (nsub + 1) + sub];
+              b = cptr[(size_t)w * (nsub + 1) + sub + 1];
+              if (sub_cut)
+                while (a < b && db.ent[b - 1] >= lim) --b;
+            }
+          }
+          const int cnt = (b - a + PG - 1) / PG;
+          int incl = cnt;  // inclusive scan of the piece counts over the wave
 #pragma unroll
-          for (int u = 0; u < PD; ++u) {
-            const int i = i0 + u;
-            if (i < nw) {
-              const double qval = wq[i];
-              if (e[u] >= 0) acc[e[u] - lo] += fabs(qval - dv[u]) - fabs(qval) - fabs(dv[u]);
-              if (my_b[i] - my_a[i] > 64) {  // rare: a word with > 64 postings in this sub-range
-                for (int sl = my_a[i] + 64 + lane; sl < my_b[i]; sl += 64) {
-                  const double d = db.wt[sl];
-                  acc[db.ent[sl] - lo] += fabs(qval - d) - fabs(qval) - fabs(d);
-                }
+          for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += t;
+          }
+          const int gtot = __shfl(incl, 63, 64);
+          if (np + gtot > PC) {  // table full: apply it first
+            run(np);
+            np = 0;
+          }
+          if (gtot > PC) {  // one 64-word group with very long lists: plain order-preserving loop
+            for (int k = 0; k < 64 && w0 + k < nw; ++k) {
+              const int ak = __shfl(a, k, 64), bk = __shfl(b, k, 64);
+              const double qval = wq[w0 + k];
+              for (int sl = ak + lane; sl < bk; sl += 64) {
+                const double d = db.wt[sl];
+                acc[db.ent[sl] - lo] += fabs(qval - d) - fabs(qval) - fabs(d);
               }
             }
+            continue;
           }
-        };
-        int eA[PD], eB[PD], eC[PD], eD[PD];
-        double dA[PD], dB[PD], dC[PD], dD[PD];
-        fetch(0, eA, dA);
-        fetch(PD, eB, dB);
-        fetch(2 * PD, eC, dC);
-        for (int i0 = 0; i0 < nw; i0 += 4 * PD) {
-          fetch(i0 + 3 * PD, eD, dD);
-          process(i0, eA, dA);
-          fetch(i0 + 4 * PD, eA, dA);
-          process(i0 + PD, eB, dB);
-          fetch(i0 + 5 * PD, eB, dB);
-          process(i0 + 2 * PD, eC, dC);
-          fetch(i0 + 6 * PD, eC, dC);
-          process(i0 + 3 * PD, eD, dD);
+          for (int k = 0, pos = np + incl - cnt; k < cnt; ++k, ++pos) {
+            my_start[pos] = a + k * PG;
+            my_info[pos] = (unsigned short)((min(PG, b - a - k * PG) - 1) | (i << 5));
+          }
+          np += gtot;
         }
+        run(np);
       }
       __syncthreads();
       // ---- this chunk's best min(K, touched) by (acc, id): LDS histogram narrowing
+      if (dbg & 2) continue;  // diagnostic: accumulation only
       if (tid == 0) { s_nt = 0; s_ns = 0; s_done = 0; }
       __syncthreads();
       {
@@ -326,17 +411,9 @@ __global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int*
           if (a != 0.0 && in_play(a, level)) atomicAdd(&hist[bin_of(a, level)], 1);
         }
         __syncthreads();
-        if (tid == 0) {
-          int cum = 0, b = 0;
-          for (; b < NBINS; ++b) {
-            if (cum + hist[b] >= need) break;
-            cum += hist[b];
-          }
-          if (b == NBINS) b = NBINS - 1;
-          s_b = b;
-          s_cb = cum;
-          s_done = (s_ns + cum + hist[b] <= LSEL) ? 1 : 0;
-        }
+        find_bin<LW_BLOCK>(hist, need, s_wsum, &s_b, &s_cb);  // first bin reaching `need`
+        __syncthreads();
+        if (tid == 0) s_done = (s_ns + s_cb + hist[s_b] <= LSEL) ? 1 : 0;
         __syncthreads();
         const int b = s_b, done = s_done, cb = s_cb;
         lvl_b[level] = b;
@@ -410,7 +487,11 @@ __global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int*
   }
 }
 constexpr size_t LDS_BOW = sizeof(double) * (LCH + LSEL + 2 * MAX_RESULTS + QW) +
-                           sizeof(int) * (LSEL + 2 * MAX_RESULTS + 2 * LW_WAVES * QW + NBINS);
+                           sizeof(int) * (LSEL + 2 * MAX_RESULTS + LW_WAVES * PC + NBINS) +
+                           sizeof(unsigned short) * LW_WAVES * PC;
+static_assert(LW_WAVES * (LCH / LW_WAVES) <= sizeof(double) * (LSEL + MAX_RESULTS) + sizeof(int) * (LSEL + MAX_RESULTS),
+              "conflict marks must fit the selection scratch");
+static_assert(QW <= 2048 && PG <= 32 && 64 % PG == 0, "piece info packs len - 1 in 5 bits and the word in 11");
 static_assert(LDS_BOW + 64 <= 160 * 1024, "k_bow_query_lds exceeds the 160 KiB of LDS per CU");
 
 // L1Scoring::score of pairs (a_i, b_i): merge of the two sorted word lists.
@@ -460,6 +541,7 @@ struct kmx_bow {
   int* d_err = nullptr;
   // LDS-accumulator query (k_bow_query_lds): per-word chunk split points
   bool lds = true;
+  int dbg = 0;  // KMX_BOW_DBG (diagnostic timing only): bit 0 skips accumulation, bit 1 the top-K
   int ch = 0, nch = 0;
   int* d_cptr = nullptr;
   size_t qcap = 0, wcap = 0;
@@ -588,6 +670,7 @@ extern "C" int kmx_bow_set_database(kmx_bow* h, int32_t n_words, int32_t n_entri
   // entries per LDS chunk (tests use small chunks to cover the merge)
   h->lds = true;
   if (const char* v = std::getenv("KMX_BOW_LDS")) h->lds = std::atoi(v) != 0;
+  if (const char* v = std::getenv("KMX_BOW_DBG")) h->dbg = std::atoi(v);
   h->ch = LCH;
   if (const char* v = std::getenv("KMX_BOW_CHUNK")) h->ch = std::max(1, std::min(LCH, std::atoi(v)));
   h->ch = (h->ch + LW_WAVES - 1) / LW_WAVES * LW_WAVES;  // whole sub-ranges, one per wave
@@ -673,7 +756,7 @@ extern "C" int kmx_bow_query_async(kmx_bow* h, int32_t nq, const int64_t* qptr, 
                        (const int*)h->d_cptr, h->nch, h->ch, nq, (const long long*)h->d_qptr,
                        (const unsigned*)h->d_qw, (const double*)h->d_qv,
                        max_id ? (const int*)h->d_maxid : nullptr, max_results, h->d_n, h->d_id, h->d_score,
-                       h->d_err);
+                       h->d_err, h->dbg);
     KMX_HIP(hipGetLastError());
     return KMX_OK;
   }
