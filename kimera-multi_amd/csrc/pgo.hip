@@ -1100,8 +1100,7 @@ __global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_grad(D
   auto store = [&]() {
     if (L.valid) {
       const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-      store4(d.g + o, gr);
-      store4(d.r + o, gr);
+      store4(d.g + o, gr);  // r = g at the start of tCG: k_update's first step reads g
       store4(d.z + o, zr);
       if (L.a == 0) {
         double* Sp = d.S + 9 * (size_t)L.pose;
@@ -1185,7 +1184,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d) {
     double dl[4], hdl[4];
     load4(d.del + o, dl);
     load4(d.hd + o, hdl);
-    load4(d.r + o, rr);
+    load4((first ? d.g : d.r) + o, rr);  // r_0 = g (k_grad does not store r)
     if (!first) load4(d.eta + o, et);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
