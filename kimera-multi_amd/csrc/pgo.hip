@@ -111,6 +111,12 @@ struct Dev {
   const int* trec0;   // [ntiles] segment-major layout (rect): first crec record of each tile
   const int* torec0;  // [ntiles] ... and of ocrec
   int rect;           // crec / ocrec in segment-major order (gather G = 5/6 only)
+  double* hrec;       // [ninc + 1][12] compact records in CSR order for the G = 9 Hessian gather
+                      // (+ one zero pad record), null when that gather is off
+  double* hD;         // [nloc][16] diagonal blocks of Q per pose (G = 9), written by k_precond
+  double* hocrec;     // [m_own + 1][12] owner compact records in CSR order (G = 9 k_cost) + pad
+  const int2* heopos; // [mloc] positions of each local edge in hocrec
+  int dbg;            // diagnostic ablations (KMX_PGO_DBG; 0 in the product path)
   double *X, *Xt, *g, *r, *z, *eta, *del, *hd, *S, *Pinv, *pub;
   double* part;       // [ntiles][NPART]
   Ctl* ctl;
@@ -198,47 +204,96 @@ __device__ __forceinline__ double incidence_row(const Edge& E, bool self_tail, c
 // is chained to the previous one (empty asm) so only one sum's R shuffles are
 // in flight: interleaving all of them held ~90 VGPRs and capped k_hess at 3
 // waves/SIMD.
-template <int R>
-__device__ __forceinline__ void group_symYtG(const double y[4], const double G[4], int base, double S[9]) {
-  double prev = 0.0;
+//
+// LDS = true (kernels that own a free BLOCK x 6-double LDS scratch `scr`): every
+// lane writes its 6 products, then reads its group's R x 6 back and adds them
+// in the same lane order, so the 6 sums cost one LDS round trip instead of 6
+// chained shuffle chains. Only lanes of one wave exchange data (in-order LDS
+// queue; no workgroup barrier).
+template <int R, bool LDS = false>
+__device__ __forceinline__ void group_symYtG(const double y[4], const double G[4], int base, double S[9],
+                                             double* scr = nullptr) {
+  if constexpr (LDS) {
+    double* mine = scr + 6 * threadIdx.x;
+    {
+      int j = 0;
 #pragma unroll
-  for (int c = 0; c < 3; ++c)
+      for (int c = 0; c < 3; ++c)
 #pragma unroll
-    for (int k = c; k < 3; ++k) {
-      double x = 0.5 * (y[c] * G[k] + y[k] * G[c]);
-      asm volatile("" : "+v"(x) : "v"(prev));
-      prev = gsum<R>(x, base);
-      S[c * 3 + k] = prev;
-      S[k * 3 + c] = prev;
+        for (int k = c; k < 3; ++k) mine[j++] = 0.5 * (y[c] * G[k] + y[k] * G[c]);
     }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    const double* grp = scr + 6 * ((threadIdx.x & ~63u) + base);
+    double t[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int m = 0; m < R; ++m)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) t[j] += grp[6 * m + j];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    int j = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int k = c; k < 3; ++k, ++j) {
+        S[c * 3 + k] = t[j];
+        S[k * 3 + c] = t[j];
+      }
+  } else {
+    double prev = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int k = c; k < 3; ++k) {
+        double x = 0.5 * (y[c] * G[k] + y[k] * G[c]);
+        asm volatile("" : "+v"(x) : "v"(prev));
+        prev = gsum<R>(x, base);
+        S[c * 3 + k] = prev;
+        S[k * 3 + c] = prev;
+      }
+  }
 }
 
 // Tangent projection of row V at Y (group-cooperative): V_Y - Y sym(Y^T V_Y).
-template <int R>
-__device__ __forceinline__ void group_proj(const double y[4], const double V[4], int base, double out[4]) {
+template <int R, bool LDS = false>
+__device__ __forceinline__ void group_proj(const double y[4], const double V[4], int base, double out[4],
+                                           double* scr = nullptr) {
   double S[9];
-  group_symYtG<R>(y, V, base, S);
+  group_symYtG<R, LDS>(y, V, base, S, scr);
 #pragma unroll
   for (int c = 0; c < 3; ++c) out[c] = V[c] - (y[0] * S[0 * 3 + c] + y[1] * S[1 * 3 + c] + y[2] * S[2 * 3 + c]);
   out[3] = V[3];
 }
 
-template <int R>
+template <int R, bool LDS = false>
 __device__ __forceinline__ void group_precon(const Dev& d, int pose, bool valid, const double y[4],
-                                             const double V[4], int base, double out[4]) {
+                                             const double V[4], int base, double out[4], double* scr = nullptr) {
   double buf[4] = {0.0, 0.0, 0.0, 0.0};
   if (d.p.use_precond) {
-    // buf = V P, one 4-double row of P at a time (keeps 8 VGPRs of P live)
     const double* Pp = d.Pinv + 16 * (size_t)pose;
+    if constexpr (LDS) {
+      // the 128-VGPR kernels: all of P in flight at once (pose is a valid
+      // index on every lane: lane_map clamps idle lanes to the tile's first pose)
+      double P[16];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      double Pr[4] = {0.0, 0.0, 0.0, 0.0};
-      if (valid) load4(Pp + 4 * i, Pr);
-      asm volatile("" : "+v"(Pr[0]), "+v"(Pr[1]), "+v"(Pr[2]), "+v"(Pr[3]) : "v"(buf[0]));
+      for (int i = 0; i < 4; ++i) load4(Pp + 4 * i, P + 4 * i);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * Pr[k] : buf[k] + V[i] * Pr[k];
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * P[k] : buf[k] + V[i] * P[4 * i + k];
+    } else {
+      // buf = V P, one 4-double row of P at a time (keeps 8 VGPRs of P live)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        double Pr[4] = {0.0, 0.0, 0.0, 0.0};
+        if (valid) load4(Pp + 4 * i, Pr);
+        asm volatile("" : "+v"(Pr[0]), "+v"(Pr[1]), "+v"(Pr[2]), "+v"(Pr[3]) : "v"(buf[0]));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * Pr[k] : buf[k] + V[i] * Pr[k];
+      }
     }
-    group_proj<R>(y, buf, base, out);
+    group_proj<R, LDS>(y, buf, base, out, scr);
   } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k) out[k] = V[k];
@@ -247,14 +302,14 @@ __device__ __forceinline__ void group_precon(const Dev& d, int pose, bool valid,
 
 // Riemannian Hessian row of V given the Euclidean Hessian row H:
 // P_Y(H_Y - V_Y S) ; p-part H_p.
-template <int R>
+template <int R, bool LDS = false>
 __device__ __forceinline__ void group_rhess(const double y[4], const double V[4], const double H[4],
-                                            const double S[9], int base, double out[4]) {
+                                            const double S[9], int base, double out[4], double* scr = nullptr) {
   double buf[4];
 #pragma unroll
   for (int k = 0; k < 3; ++k) buf[k] = H[k] - (V[0] * S[0 * 3 + k] + V[1] * S[1 * 3 + k] + V[2] * S[2 * 3 + k]);
   buf[3] = H[3];
-  group_proj<R>(y, buf, base, out);
+  group_proj<R, LDS>(y, buf, base, out, scr);
 }
 
 // QF retraction (modified Gram-Schmidt over the 3 columns, positive diagonal).
@@ -890,7 +945,206 @@ struct SmemG<R, 7> {
 };
 template <int R>
 struct SmemG<R, 8> : SmemG<R, 7> {};
+// G = 9 (k_hess only; k_grad / k_cost run G = 5 / 6): the G = 5 layout here.
+template <int R>
+struct SmemG<R, 9> : SmemG<R, 5> {};
 
+// Incidence-parallel Hessian gather (G = 9, k_hess). Q's diagonal block D_i
+// (k_precond) is applied once per pose, so an incidence only contributes its
+// off-diagonal block B_e applied to the other endpoint's row: one lane per
+// incidence reads the 96-B record once (not once per row as in G = 5) and the
+// whole r x 4 neighbour row, and writes the R contribution rows to LDS; the
+// (pose, row) lanes then add their pose's incidences in CSR order
+// (deterministic). out_i = D_i v_i + sum_{e at i} B_e v_other(e), with a
+// public neighbour's row taken as zero (Hessian of the local problem).
+template <int R>
+struct SmemH {
+  static constexpr int TP = WAVES * (64 / R);
+  static constexpr int CH = TP * R;                                       // incidences per chunk (<= BLOCK)
+  static constexpr int c_off = 0;                                         // double[CH][R][4]
+  static constexpr int ptr_off = CH * R * 32;                             // int[TP + 1]
+  static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
+  static constexpr int bytes = red_off + 64;
+};
+// group_symYtG<R, true> scratch: BLOCK x 6 doubles at the start of the LDS
+static_assert(WAVES * 64 * 6 * 8 <= SmemH<3>::ptr_off && WAVES * 64 * 6 * 8 <= SmemH<8>::ptr_off, "scratch");
+static_assert(WAVES * 64 * 6 * 8 <= Smem<5>::red_off && WAVES * 64 * 6 * 8 <= Smem<8>::red_off, "scratch");
+template <int R, int GV>
+struct SmemHess : SmemG<R, GV> {};
+template <int R>
+struct SmemHess<R, 9> : SmemH<R> {};
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops but
+// not for its outstanding global loads (__syncthreads waits vmcnt(0), which
+// would drain the next chunk's prefetched records).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int R>
+__device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const double* V, double acc[4],
+                                            char* smem) {
+  using SM = SmemH<R>;
+  constexpr int CH = SM::CH;
+  static_assert(CH <= BLOCK, "one incidence per thread per chunk");
+  double* Cs = reinterpret_cast<double*>(smem + SM::c_off);
+  int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
+  const int tid = threadIdx.x;
+  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
+  const int K0 = d.inc_ptr[p0];
+  const int n = d.inc_ptr[p0 + np] - K0;
+  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
+  const int pl = L.pose - p0;
+  const int lt = min(tid, CH - 1);
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  // clamped, unconditional record loads (hrec holds one zero pad record, so
+  // an empty tile at the end of the array still reads inside it)
+  auto ld = [&](int c0, double2 q[6]) {
+    const int k = max(min(c0 + lt, n - 1), 0);
+    const double2* q2 = reinterpret_cast<const double2*>(d.hrec + 12 * (size_t)(K0 + k));
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = q2[i];
+  };
+  double2 q[6];
+  ld(0, q);
+  __syncthreads();  // sptr
+  for (int c0 = 0; c0 < n; c0 += CH) {
+    Edge E;
+    edge_from_compact(q, E);
+    const int2 in = unpack_int2(q[5].y);
+    const int o = in.x;
+    const bool tail = (in.y >> 31) & 1;
+    const double2* b2 = reinterpret_cast<const double2*>(V + (size_t)max(o, 0) * 4 * R);
+    double2 vr[2 * R];
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) vr[i] = b2[i];
+    if (tid < CH && c0 + tid < n) {
+      const double wk = (o >= 0) ? E.wk : 0.0, wt = (o >= 0) ? E.wt : 0.0;
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        const double v0 = vr[2 * a].x, v1 = vr[2 * a].y, v2 = vr[2 * a + 1].x, v3 = vr[2 * a + 1].y;
+        double h[4];
+        if (tail) {  // self = i: row(j) Q_ji = -w [kappa row(j)_Y R^T + tau p_j t^T, tau p_j]
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            h[c] = -(wk * (v0 * E.R[c * 3 + 0] + v1 * E.R[c * 3 + 1] + v2 * E.R[c * 3 + 2]) + wt * v3 * E.t[c]);
+          h[3] = -(wt * v3);
+        } else {  // self = j: row(i) Q_ij = -w [kappa row(i)_Y R, tau (p_i + row(i)_Y t)]
+#pragma unroll
+          for (int c = 0; c < 3; ++c) h[c] = -(wk * (v0 * E.R[0 * 3 + c] + v1 * E.R[1 * 3 + c] + v2 * E.R[2 * 3 + c]));
+          h[3] = -(wt * (v3 + (v0 * E.t[0] + v1 * E.t[1] + v2 * E.t[2])));
+        }
+        store4(Cs + (tid * R + a) * 4, h);
+      }
+    }
+    // the next chunk's records, issued once this chunk's rows are consumed, stay
+    // in flight across the LDS hand-off and the reduction
+    asm volatile("" ::: "memory");
+    ld(c0 + CH, q);
+    lds_barrier();
+    if (L.valid) {
+      const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
+      for (int j = j0; j < j1; ++j) {
+        double h[4];
+        load4(Cs + (j * R + L.a) * 4, h);
+        acc[0] += h[0]; acc[1] += h[1]; acc[2] += h[2]; acc[3] += h[3];
+      }
+    }
+    lds_barrier();
+  }
+  if (L.valid) {
+    double vs[4];
+    load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
+    const double* Dp = d.hD + 16 * (size_t)L.pose;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double dr[4];
+      load4(Dp + 4 * c, dr);
+      acc[c] += vs[0] * dr[0] + vs[1] * dr[1] + vs[2] * dr[2] + vs[3] * dr[3];
+    }
+  }
+}
+
+
+// Gradient and cost, incidence-parallel (G = 9 k_grad). As hinc_gather, but a
+// lane evaluates its whole incidence with incidence_row (diagonal and
+// off-diagonal terms, the public neighbour row from the table), so it also
+// reads its own pose's row (found by a binary search of the tile CSR), and
+// adds the incidence's cost share (1/2 per endpoint; all of it for a shared
+// edge). The pose sums run in CSR order.
+template <int R>
+__device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const double* V, const double* pub,
+                                          double acc[4], double* cost, char* smem) {
+  using SM = SmemH<R>;
+  constexpr int CH = SM::CH;
+  double* Cs = reinterpret_cast<double*>(smem + SM::c_off);
+  int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
+  const int tid = threadIdx.x;
+  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
+  const int K0 = d.inc_ptr[p0];
+  const int n = d.inc_ptr[p0 + np] - K0;
+  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
+  const int pl = L.pose - p0;
+  const int lt = min(tid, CH - 1);
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  double csum = 0.0;
+  auto ld = [&](int c0, double2 q[6]) {
+    const int k = max(min(c0 + lt, n - 1), 0);
+    const double2* q2 = reinterpret_cast<const double2*>(d.hrec + 12 * (size_t)(K0 + k));
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = q2[i];
+  };
+  double2 q[6];
+  ld(0, q);
+  __syncthreads();  // sptr
+  for (int c0 = 0; c0 < n; c0 += CH) {
+    const int k = max(min(c0 + lt, n - 1), 0);
+    int lo = 0, hi = np;  // owning pose: sptr[lo] <= k < sptr[lo + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (sptr[mid] <= k) lo = mid;
+      else hi = mid;
+    }
+    const int2 in = unpack_int2(q[5].y);
+    const int o = in.x;
+    const bool tail = (in.y >> 31) & 1;
+    const double2* s2 = reinterpret_cast<const double2*>(V + (size_t)(p0 + lo) * 4 * R);
+    const double2* o2 = reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
+    double2 vo2[2 * R];
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) vo2[i] = o2[i];
+    Edge E;
+    edge_from_compact(q, E);
+    if (tid < CH && c0 + tid < n) {
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        // own rows: neighbouring lanes share the pose, so these hit in L1
+        const double2 sa = s2[2 * a], sb = s2[2 * a + 1];
+        const double vs[4] = {sa.x, sa.y, sb.x, sb.y};
+        const double vo[4] = {vo2[2 * a].x, vo2[2 * a].y, vo2[2 * a + 1].x, vo2[2 * a + 1].y};
+        double h[4] = {0.0, 0.0, 0.0, 0.0};
+        const double c = incidence_row(E, tail, vs, vo, h);
+        csum += (o < 0) ? c : 0.5 * c;
+        store4(Cs + (tid * R + a) * 4, h);
+      }
+    }
+    asm volatile("" ::: "memory");
+    ld(c0 + CH, q);
+    lds_barrier();
+    if (L.valid) {
+      const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
+      for (int j = j0; j < j1; ++j) {
+        double h[4];
+        load4(Cs + (j * R + L.a) * 4, h);
+        acc[0] += h[0]; acc[1] += h[1]; acc[2] += h[2]; acc[3] += h[3];
+      }
+    }
+    lds_barrier();
+  }
+  *cost += csum;
+}
+template <int R, int GV>
+struct SmemGrad : SmemG<R, GV> {};
+template <int R>
+struct SmemGrad<R, 9> : SmemH<R> {};
 
 // -------------------------------------------- fused per-robot reductions --
 // Each tile of robot l publishes its partial sums, then takes a ticket on
@@ -1045,7 +1299,7 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
 // Separate-launch reduction (variant F = 0): one workgroup per robot.
 __global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_, HostStatus* hs,
                                                  unsigned long long seq) {
-  __shared__ double lds[WAVES];
+  __shared__ double lds[NPART * WAVES];
   const int l = blockIdx.x;
   const int ph = d.ctl[l].phase;
   bool act = false;
@@ -1059,13 +1313,27 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_, HostS
   const int ns = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
   double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
   const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
+  // all slots in one pass and one LDS round (same per-thread, per-wave and
+  // wave-order summation as a block_sum per slot, so the sums are unchanged)
+  static_assert(NPART == 4, "two 16-B loads per tile");
+  double v[NPART] = {0.0, 0.0, 0.0, 0.0};
+  for (int t = t0 + (int)threadIdx.x; t < t1; t += BLOCK) {
+    const double2* p2 = reinterpret_cast<const double2*>(d.part + (size_t)t * NPART);
+    const double2 a = p2[0], b = p2[1];
+    v[0] += a.x; v[1] += a.y; v[2] += b.x; v[3] += b.y;
+  }
 #pragma unroll
   for (int s = 0; s < NPART; ++s) {
-    if (s < ns) {
-      double v = 0.0;
-      for (int t = t0 + (int)threadIdx.x; t < t1; t += BLOCK) v += d.part[(size_t)t * NPART + s];
-      tot[s] = block_sum(v, lds);
-    }
+    const double w = wave_sum(v[s]);
+    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < NPART; ++s) {
+    double acc = 0.0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) acc += lds[s * WAVES + w];
+    tot[s] = s < ns ? acc : 0.0;
   }
   if (threadIdx.x == 0) {
     control(d, l, kind, tot, R_);
@@ -1078,19 +1346,30 @@ __global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_, HostS
 // Start of an RTR iteration: egrad (gather X with public neighbours), cost,
 // S = sym(Y^T egrad_Y), g = P_Y(egrad), r = g, z = precon(g).
 template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_grad(Dev d) {
+__global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) void k_grad(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_START) return;
   double y[4] = {0, 0, 0, 0}, G[4], cost = 0.0;
-  gather<R, GV, true>(d, L, d.X, d.pub, G, &cost, smem);
+  if constexpr (GV == 9) hinc_grad<R>(d, L, d.X, d.pub, G, &cost, smem);
+  else gather<R, GV, true>(d, L, d.X, d.pub, G, &cost, smem);
   if (L.valid) load4(d.X + (size_t)L.pose * 4 * R + 4 * L.a, y);
   double S[9], gr[4], zr[4];
-  group_symYtG<R>(y, G, L.base, S);
+  // G = 9: the gather's chunk buffer is free now (its last barrier passed)
+  double* scr = reinterpret_cast<double*>(smem + SmemH<R>::c_off);
+  if (d.dbg & 2) {
+    for (int i = 0; i < 9; ++i) S[i] = 0.0;
+  } else {
+    group_symYtG<R, GV == 9>(y, G, L.base, S, scr);
+  }
 #pragma unroll
   for (int c = 0; c < 3; ++c) gr[c] = G[c] - (y[0] * S[0 * 3 + c] + y[1] * S[1 * 3 + c] + y[2] * S[2 * 3 + c]);
   gr[3] = G[3];
-  group_precon<R>(d, L.pose, L.valid, y, gr, L.base, zr);
+  if (d.dbg & 1) {
+    for (int i = 0; i < 4; ++i) zr[i] = gr[i];
+  } else {
+    group_precon<R, GV == 9>(d, L.pose, L.valid, y, gr, L.base, zr, scr);
+  }
   double vals[3] = {0.0, 0.0, 0.0};
   vals[0] = cost;  // the incidence-parallel gather accumulates cost on non-pose lanes too
   if (L.valid) {
@@ -1112,14 +1391,14 @@ __global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_grad(D
   // separate reduce launch: store first (frees S, g, z before the block sum);
   // fused reduction: ticket first, so its drain waits only for the partials
   if constexpr (!F) store();
-  finish_tile<RED_GRAD, 3, F>(d, L, vals, smem + SmemG<R, GV>::red_off, R);
+  finish_tile<RED_GRAD, 3, F>(d, L, vals, smem + SmemGrad<R, GV>::red_off, R);
   if constexpr (F) store();
 }
 
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old.
 template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_hess(Dev d) {
+__global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) void k_hess(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   const Ctl& c = d.ctl[L.l];
@@ -1128,7 +1407,8 @@ __global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_hess(D
   const double beta = c.beta;
   double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4], S[9];
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-  gather<R, GV, false>(d, L, d.z, nullptr, H, nullptr, smem);
+  if constexpr (GV == 9) hinc_gather<R>(d, L, d.z, H, smem);
+  else gather<R, GV, false>(d, L, d.z, nullptr, H, nullptr, smem);
   asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
   if (L.valid) {
     load4(d.z + o, zs);
@@ -1141,7 +1421,7 @@ __global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_hess(D
     for (int i = 0; i < 9; ++i) S[i] = 0.0;
   }
   double hz[4];
-  group_rhess<R>(y, zs, H, S, L.base, hz);
+  group_rhess<R, GV == 9>(y, zs, H, S, L.base, hz, reinterpret_cast<double*>(smem + SmemH<R>::c_off));
   double v = 0.0;
   double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
   if (L.valid) {
@@ -1160,7 +1440,7 @@ __global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_hess(D
     }
     v = dl[0] * hdl[0] + dl[1] * hdl[1] + dl[2] * hdl[2] + dl[3] * hdl[3];
   }
-  finish_tile<RED_HESS, 1, F>(d, L, &v, smem + SmemG<R, GV>::red_off, R);
+  finish_tile<RED_HESS, 1, F>(d, L, &v, smem + SmemHess<R, GV>::red_off, R);
   if (L.valid) {
     store4(d.del + o, dl);
     store4(d.hd + o, hdl);
@@ -1195,7 +1475,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d) {
   }
   double vals[2] = {0.0, 0.0}, zr[4] = {0, 0, 0, 0};
   if (interior) {  // uniform per robot
-    group_precon<R>(d, L.pose, L.valid, y, rr, L.base, zr);
+    group_precon<R, GV == 9>(d, L.pose, L.valid, y, rr, L.base, zr, reinterpret_cast<double*>(smem));
     if (L.valid) {
       vals[0] = rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2] + rr[3] * rr[3];
       vals[1] = zr[0] * rr[0] + zr[1] * rr[1] + zr[2] * rr[2] + zr[3] * rr[3];
@@ -1247,14 +1527,75 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
   }
 }
 
+// Trial cost, one lane per owner incidence (G = 9): each local edge is
+// visited once by the lane that owns it, which reads the record and both
+// endpoint rows and sums the R rows' residual terms; no per-pose reduction.
+template <int R>
+struct SmemC {
+  static constexpr int TP = WAVES * (64 / R);
+  static constexpr int ptr_off = 0;                                  // int[TP + 1]
+  static constexpr int red_off = ((TP + 1) * 4 + 15) / 16 * 16;
+  static constexpr int bytes = red_off + 64;
+};
+template <int R, int GV>
+struct SmemCost : SmemG<R, GV> {};
+template <int R>
+struct SmemCost<R, 9> : SmemC<R> {};
+
+template <int R>
+__device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, const double* V, const double* pub,
+                                                 char* smem) {
+  int* sptr = reinterpret_cast<int*>(smem + SmemC<R>::ptr_off);
+  const int tid = threadIdx.x;
+  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
+  const int K0 = d.optr[p0];
+  const int n = d.optr[p0 + np] - K0;
+  if (tid <= np) sptr[tid] = d.optr[p0 + tid] - K0;
+  __syncthreads();
+  double cost = 0.0;
+  for (int k = tid; k < n; k += BLOCK) {
+    int lo = 0, hi = np;  // owning pose: sptr[lo] <= k < sptr[lo + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (sptr[mid] <= k) lo = mid;
+      else hi = mid;
+    }
+    const double2* q2 = reinterpret_cast<const double2*>(d.hocrec + 12 * (size_t)(K0 + k));
+    double2 q[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = q2[i];
+    const int2 in = unpack_int2(q[5].y);
+    const int o = in.x;
+    const bool tail = (in.y >> 31) & 1;
+    const double2* s2 = reinterpret_cast<const double2*>(V + (size_t)(p0 + lo) * 4 * R);
+    const double2* o2 = reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
+    double2 vs2[2 * R], vo2[2 * R];
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) { vs2[i] = s2[i]; vo2[i] = o2[i]; }
+    Edge E;
+    edge_from_compact(q, E);
+    double c = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      const double vs[4] = {vs2[2 * a].x, vs2[2 * a].y, vs2[2 * a + 1].x, vs2[2 * a + 1].y};
+      const double vo[4] = {vo2[2 * a].x, vo2[2 * a].y, vo2[2 * a + 1].x, vo2[2 * a + 1].y};
+      double dummy[4] = {0.0, 0.0, 0.0, 0.0};
+      c += incidence_row(E, tail, vs, vo, dummy);
+    }
+    cost += c;
+  }
+  return cost;
+}
+
 template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK, (GV == 7 ? 4 : KMX_LB_GATHER)) void k_cost(Dev d) {
+__global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) void k_cost(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
   double acc[4], cost = 0.0;
-  gather<R, (GV == 3 ? 4 : GV == 5 ? 6 : GV == 7 ? 8 : GV), true>(d, L, d.Xt, d.pub, acc, &cost, smem);
-  finish_tile<RED_COST, 1, F>(d, L, &cost, smem + SmemG<R, GV>::red_off, R);
+  if constexpr (GV == 9) cost = inc_owner_cost<R>(d, L, d.Xt, d.pub, smem);
+  else gather<R, (GV == 3 ? 4 : GV == 5 ? 6 : GV == 7 ? 8 : GV), true>(d, L, d.Xt, d.pub, acc, &cost, smem);
+  finish_tile<RED_COST, 1, F>(d, L, &cost, smem + SmemCost<R, GV>::red_off, R);
 }
 
 template <int R>
@@ -1344,6 +1685,8 @@ __global__ void k_precond(Dev d) {
       A[0] += wk; A[5] += wk; A[10] += wk; A[15] += wt;
     }
   }
+  if (d.hD)
+    for (int i = 0; i < 16; ++i) d.hD[16 * (size_t)pose + i] = A[i];
   for (int j = 0; j < 4; ++j) A[j * 5] += d.p.shift;
   double Lm[16], Li[16];
   for (int i = 0; i < 16; ++i) { Lm[i] = 0.0; Li[i] = 0.0; }
@@ -1417,6 +1760,15 @@ __global__ void k_apply_weights(Dev d, int mloc) {
   const int2 ip = d.eipos[e];
   if (ip.x >= 0) { d.irec[16 * (size_t)ip.x + 12] = wk; d.irec[16 * (size_t)ip.x + 13] = wt; }
   if (ip.y >= 0) { d.irec[16 * (size_t)ip.y + 12] = wk; d.irec[16 * (size_t)ip.y + 13] = wt; }
+  if (d.hocrec) {
+    const int2 hp = d.heopos[e];
+    if (hp.x >= 0) { d.hocrec[12 * (size_t)hp.x + 9] = wk; d.hocrec[12 * (size_t)hp.x + 10] = wt; }
+    if (hp.y >= 0) { d.hocrec[12 * (size_t)hp.y + 9] = wk; d.hocrec[12 * (size_t)hp.y + 10] = wt; }
+  }
+  if (d.hrec) {  // CSR order: the incidence positions
+    if (ip.x >= 0) { d.hrec[12 * (size_t)ip.x + 9] = wk; d.hrec[12 * (size_t)ip.x + 10] = wt; }
+    if (ip.y >= 0) { d.hrec[12 * (size_t)ip.y + 9] = wk; d.hrec[12 * (size_t)ip.y + 10] = wt; }
+  }
   if (d.crec) {
     const int2 cp = d.cipos[e];
     if (cp.x >= 0) { d.crec[12 * (size_t)cp.x + 9] = wk; d.crec[12 * (size_t)cp.x + 10] = wt; }
@@ -1631,6 +1983,145 @@ __global__ __launch_bounds__(BLOCK, LBW) void k_gbench(Dev d, const double* V, d
   if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
 }
 
+// 4x4 diagonal blocks D_i of Q per pose (k_precond's accumulation, no shift).
+__global__ void k_diag(Dev d, double* D) {
+  const int pose = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pose >= d.nloc) return;
+  double A[16];
+  for (int i = 0; i < 16; ++i) A[i] = 0.0;
+  for (int k = d.inc_ptr[pose]; k < d.inc_ptr[pose + 1]; ++k) {
+    const bool tail = (d.inc[k].y >> 31) & 1;
+    const double* er = d.irec + 16 * (size_t)k;
+    const double wk = er[12], wt = er[13];
+    const double* tt = er + 9;
+    if (tail) {
+      for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) A[i * 4 + j] += wt * tt[i] * tt[j] + (i == j ? wk : 0.0);
+        A[i * 4 + 3] += wt * tt[i];
+        A[3 * 4 + i] += wt * tt[i];
+      }
+      A[15] += wt;
+    } else {
+      A[0] += wk; A[5] += wk; A[10] += wk; A[15] += wt;
+    }
+  }
+  for (int i = 0; i < 16; ++i) D[16 * (size_t)pose + i] = A[i];
+}
+
+// Prototype (diagnostic, G = 9): lane per incidence. out_i = D_i v_i +
+// sum_{e at i} B_e v_other(e): the off-diagonal block of every incidence is
+// applied by one lane to all R rows of the other endpoint (no per-row record
+// redundancy), the R x 4 results go to LDS, and the (pose, row) lanes add
+// their pose's incidences in CSR order. REC 0: 128-B records + inc; REC 1:
+// 96-B compact records (CSR order, KMX_RECT=0).
+template <int R, int REC, int CH>
+__global__ __launch_bounds__(BLOCK, 4) void k_hinc(Dev d, const double* V, const double* Dg, double* out) {
+  extern __shared__ __attribute__((aligned(16))) double hsm[];
+  double* Cs = hsm;                                    // [CH][R][4]
+  int* sptr = reinterpret_cast<int*>(hsm + CH * R * 4);  // [TP + 1]
+  const Lane L = lane_map<R>(d);
+  const int tid = threadIdx.x;
+  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
+  const int K0 = d.inc_ptr[p0];
+  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
+  __syncthreads();
+  const int n = sptr[np];
+  const int pl = L.pose - p0;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int c0 = 0; c0 < n; c0 += CH) {
+    const int k = c0 + tid;
+    if (tid < CH && k < n) {
+      double Rm[9], t[3], wk, wt;
+      int o;
+      bool tail;
+      if constexpr (REC == 0) {
+        const double2* q2 = reinterpret_cast<const double2*>(d.irec + 16 * (size_t)(K0 + k));
+        double2 q[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) q[i] = q2[i];
+        const int2 in = d.inc[K0 + k];
+        Rm[0] = q[0].x; Rm[1] = q[0].y; Rm[2] = q[1].x; Rm[3] = q[1].y; Rm[4] = q[2].x;
+        Rm[5] = q[2].y; Rm[6] = q[3].x; Rm[7] = q[3].y; Rm[8] = q[4].x;
+        t[0] = q[4].y; t[1] = q[5].x; t[2] = q[5].y;
+        wk = q[6].x; wt = q[6].y;
+        o = in.x; tail = (in.y >> 31) & 1;
+      } else {
+        const double2* q2 = reinterpret_cast<const double2*>(d.crec + 12 * (size_t)(K0 + k));
+        double2 q[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) q[i] = q2[i];
+        Edge E;
+        edge_from_compact(q, E);
+        const int2 in = unpack_int2(q[5].y);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Rm[i] = E.R[i];
+        t[0] = E.t[0]; t[1] = E.t[1]; t[2] = E.t[2];
+        wk = E.wk; wt = E.wt;
+        o = in.x; tail = (in.y >> 31) & 1;
+      }
+      const double* base = (o >= 0) ? V + (size_t)o * 4 * R : d.pub + (size_t)(-1 - o) * 4 * R;
+      const double2* b2 = reinterpret_cast<const double2*>(base);
+      double2 vr[2 * R];
+#pragma unroll
+      for (int i = 0; i < 2 * R; ++i) vr[i] = b2[i];
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        const double v0 = vr[2 * a].x, v1 = vr[2 * a].y, v2 = vr[2 * a + 1].x, v3 = vr[2 * a + 1].y;
+        double h[4];
+        if (tail) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) h[c] = -(wk * (v0 * Rm[c * 3 + 0] + v1 * Rm[c * 3 + 1] + v2 * Rm[c * 3 + 2]) + wt * v3 * t[c]);
+          h[3] = -(wt * v3);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) h[c] = -(wk * (v0 * Rm[0 * 3 + c] + v1 * Rm[1 * 3 + c] + v2 * Rm[2 * 3 + c]));
+          h[3] = -(wt * (v3 + (v0 * t[0] + v1 * t[1] + v2 * t[2])));
+        }
+        store4(Cs + (tid * R + a) * 4, h);
+      }
+    }
+    __syncthreads();
+    if (L.valid) {
+      const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
+      for (int j = j0; j < j1; ++j) {
+        double h[4];
+        load4(Cs + (j * R + L.a) * 4, h);
+        acc[0] += h[0]; acc[1] += h[1]; acc[2] += h[2]; acc[3] += h[3];
+      }
+    }
+    __syncthreads();
+  }
+  if (L.valid) {
+    const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+    double vs[4];
+    load4(V + o, vs);
+    const double* Dp = Dg + 16 * (size_t)L.pose;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double dr[4];
+      load4(Dp + 4 * c, dr);
+      acc[c] += vs[0] * dr[0] + vs[1] * dr[1] + vs[2] * dr[2] + vs[3] * dr[3];
+    }
+    store4(out + o, acc);
+  }
+}
+
+// Diagnostic: the product G = 9 Hessian gather alone (needs the handle's
+// incidence-parallel records, i.e. KMX_HINC on).
+template <int R, bool GRAD>
+__global__ __launch_bounds__(BLOCK, 4) void k_gbench_hinc(Dev d, const double* V, double* out) {
+  KMX_SMEM;
+  const Lane L = lane_map<R>(d);
+  double acc[4], cost = 0.0;
+  if constexpr (GRAD) hinc_grad<R>(d, L, V, d.pub, acc, &cost, smem);
+  else hinc_gather<R>(d, L, V, acc, smem);
+  if (L.valid) store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
+  if constexpr (GRAD) {
+    const double t = block_sum(cost, reinterpret_cast<double*>(smem + SmemH<R>::red_off));
+    if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
+  }
+}
+
 }  // namespace
 
 // ============================================================== handle ====
@@ -1671,6 +2162,11 @@ struct kmx_pgo {
   double* d_irec = nullptr;
   double* d_crec = nullptr;  // compact records (gather variant 3), null when not usable
   double* d_ocrec = nullptr;
+  bool hinc = false;  // k_hess runs the incidence-parallel gather (G = 9)
+  double* d_hrec = nullptr;
+  double* d_hD = nullptr;
+  double* d_hocrec = nullptr;
+  int2* d_heopos = nullptr;
   int* d_optr = nullptr;
   int2* d_eopos = nullptr;
   bool compact_ok = false;
@@ -1727,13 +2223,13 @@ void free_dev(kmx_pgo* h) {
                   h->d_irec, h->d_crec, h->d_ocrec, h->d_optr, h->d_eopos, h->d_ekappa, h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_pub, h->d_part, h->d_ctl, h->d_cnt,
                   h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src, h->d_gnc_edge, h->d_gnc_ends,
                   h->d_sh_edge, h->d_sh_idx, h->d_osh_edge, h->d_osh_idx, h->d_active, h->d_scratch, h->d_tickets,
-                  h->d_trec0, h->d_torec0, h->d_cipos};
+                  h->d_trec0, h->d_torec0, h->d_cipos, h->d_hrec, h->d_hD, h->d_hocrec, h->d_heopos};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
   h->d_inc = nullptr; h->d_eipos = nullptr; h->d_optr = nullptr; h->d_eopos = nullptr; h->d_irec = h->d_crec = h->d_ocrec = h->d_ekappa = h->d_etau = h->d_ew = nullptr; h->d_vec = h->d_S = h->d_Pinv = h->d_pub = h->d_part = nullptr;
   h->d_ctl = nullptr; h->d_cnt = nullptr; h->d_m_robot = nullptr; h->d_n_robot = nullptr;
-  h->d_trec0 = h->d_torec0 = nullptr; h->d_cipos = nullptr;
+  h->d_trec0 = h->d_torec0 = nullptr; h->d_cipos = nullptr; h->d_hrec = h->d_hD = nullptr; h->d_hocrec = nullptr; h->d_heopos = nullptr;
   h->d_pub_src = h->d_own_src = h->d_gnc_edge = nullptr; h->d_gnc_ends = nullptr;
   h->d_sh_edge = h->d_sh_idx = nullptr; h->d_osh_edge = h->d_osh_idx = nullptr; h->d_active = nullptr; h->d_scratch = nullptr; h->d_tickets = nullptr;
 }
@@ -1790,7 +2286,8 @@ void enqueue_gnc(kmx_pgo* h) {
 template <int R, int G, int F>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   const dim3 grid(h->ntiles), blk(BLOCK);
-  const size_t sm = Smem<R>::bytes, smg = SmemG<R, G>::bytes;
+  const size_t sm = Smem<R>::bytes, smg = SmemG<R, G>::bytes, smh = SmemHess<R, G>::bytes,
+               smc = SmemCost<R, G>::bytes, smr = SmemGrad<R, G>::bytes;
   auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0) {
     if (!F) hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(BLOCK), 0, h->stream, h->dv, kind, R, hs, seq);
   };
@@ -1801,7 +2298,7 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
       e1 = next_event(h);
       (void)hipEventRecord(e0, h->stream);
     }
-    hipLaunchKernelGGL((k_hess<R, G, F>), grid, blk, smg, h->stream, h->dv);
+    hipLaunchKernelGGL((k_hess<R, G, F>), grid, blk, smh, h->stream, h->dv);
     if (h->timing) (void)hipEventRecord(e1, h->stream);
     red(RED_HESS);
     hipLaunchKernelGGL((k_update<R, G, F>), grid, blk, sm, h->stream, h->dv);
@@ -1834,7 +2331,7 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(std::max(64, ((h->dv.L + 63) / 64) * 64)), 0, h->stream,
                      h->dv, d_active);
   for (int it = 0; it < h->P.rtr_iterations; ++it) {
-    hipLaunchKernelGGL((k_grad<R, G, F>), grid, blk, smg, h->stream, h->dv);
+    hipLaunchKernelGGL((k_grad<R, G, F>), grid, blk, smr, h->stream, h->dv);
     red(RED_GRAD);
     const int J = h->P.tcg_max_iterations;
     if (!h->poll || F) {  // the fused variant has no per-robot reduce launch to report progress
@@ -1852,7 +2349,7 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
       }
     }
     hipLaunchKernelGGL((k_retract<R>), grid, blk, sm, h->stream, h->dv);
-    hipLaunchKernelGGL((k_cost<R, G, F>), grid, blk, smg, h->stream, h->dv);
+    hipLaunchKernelGGL((k_cost<R, G, F>), grid, blk, smc, h->stream, h->dv);
     red(RED_COST);
     hipLaunchKernelGGL((k_commit<R>), grid, blk, 0, h->stream, h->dv);
   }
@@ -1869,8 +2366,8 @@ void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
     case 5: enqueue_round_t<R, 2, 1>(h, d_active); break;
     case 6: enqueue_round_t<R, 3, 0>(h, d_active); break;
     case 7: enqueue_round_t<R, 3, 1>(h, d_active); break;
-    case 10: enqueue_round_t<R, 5, 0>(h, d_active); break;
-    case 11: enqueue_round_t<R, 5, 1>(h, d_active); break;
+    case 10: h->hinc ? enqueue_round_t<R, 9, 0>(h, d_active) : enqueue_round_t<R, 5, 0>(h, d_active); break;
+    case 11: h->hinc ? enqueue_round_t<R, 9, 1>(h, d_active) : enqueue_round_t<R, 5, 1>(h, d_active); break;
     case 14: enqueue_round_t<R, 7, 0>(h, d_active); break;
     default: enqueue_round_t<R, 7, 1>(h, d_active); break;
   }
@@ -2194,6 +2691,23 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       if (ocrec.empty()) ocrec.assign(12, 0.0);
     }
   }
+  // The incidence-parallel kernels (G = 9: k_hess, k_cost) read the compact
+  // records in CSR order; k_grad keeps the degree-balanced gather.
+  std::vector<double> hrec, hocrec;
+  std::vector<int2> heopos;
+  h->hinc = false;
+  if (h->gvar == 5) {
+    bool want = true;
+    if (const char* v = std::getenv("KMX_HINC")) want = std::atoi(v) != 0;
+    if (want) {
+      hrec.assign(crec.begin(), crec.begin() + 12 * (size_t)h->ninc);
+      hrec.resize(hrec.size() + 12, 0.0);  // pad record (clamped loads of an empty tile)
+      hocrec = ocrec;
+      hocrec.resize(hocrec.size() + 12, 0.0);
+      heopos = eopos;
+      h->hinc = true;
+    }
+  }
   // Segment-major record layout for the degree-balanced gather (G = 5/6): a
   // tile's n incidences form TP lane-group segments of S = ceil(n / TP); the
   // record of (segment g, step j) is stored at tile base + j*TP + g, so at every
@@ -2286,6 +2800,16 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     KMX_HIP(up(h->d_optr, optr.data(), sizeof(int) * optr.size()));
     KMX_HIP(up(h->d_eopos, eopos.data(), sizeof(int2) * eopos.size()));
   }
+  if (h->hinc) {
+    if ((rc = dalloc(&h->d_hrec, hrec.size())) || (rc = dalloc(&h->d_hD, (size_t)std::max(nloc, 1) * 16)) ||
+        (rc = dalloc(&h->d_hocrec, hocrec.size())) || (rc = dalloc(&h->d_heopos, heopos.size()))) {
+      free_dev(h);
+      return rc;
+    }
+    KMX_HIP(up(h->d_hrec, hrec.data(), sizeof(double) * hrec.size()));
+    KMX_HIP(up(h->d_hocrec, hocrec.data(), sizeof(double) * hocrec.size()));
+    KMX_HIP(up(h->d_heopos, heopos.data(), sizeof(int2) * heopos.size()));
+  }
   if (h->rect) {
     if ((rc = dalloc(&h->d_trec0, trec0.size())) || (rc = dalloc(&h->d_torec0, torec0.size())) ||
         (rc = dalloc(&h->d_cipos, cipos.size()))) {
@@ -2343,6 +2867,10 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   d.ekappa = h->d_ekappa; d.etau = h->d_etau; d.ew = h->d_ew; d.eipos = h->d_eipos;
   d.cipos = h->rect ? h->d_cipos : h->d_eipos;
   d.trec0 = h->d_trec0; d.torec0 = h->d_torec0; d.rect = h->rect ? 1 : 0;
+  d.hrec = h->hinc ? h->d_hrec : nullptr; d.hD = h->hinc ? h->d_hD : nullptr;
+  d.hocrec = h->hinc ? h->d_hocrec : nullptr; d.heopos = h->hinc ? h->d_heopos : nullptr;
+  d.dbg = 0;
+  if (const char* v = std::getenv("KMX_PGO_DBG")) d.dbg = std::atoi(v);
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
   d.z = h->d_vec + 4 * vec; d.eta = h->d_vec + 5 * vec; d.del = h->d_vec + 6 * vec; d.hd = h->d_vec + 7 * vec;
   d.S = h->d_S; d.Pinv = h->d_Pinv; d.pub = h->d_pub; d.part = h->d_part; d.ctl = h->d_ctl; d.cnt = h->d_cnt; d.tickets = h->d_tickets;
@@ -2721,45 +3249,77 @@ extern "C" int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out) {
   return KMX_OK;
 }
 
+// Diagnostic launcher shared by the gather bench / compare entry points.
+static bool gbench_launch(kmx_pgo* h, int variant, double* out, const double* Dg) {
+  const dim3 grid(h->ntiles), blk(BLOCK);
+  const size_t sm = Smem<5>::bytes;
+  constexpr int HCH = 240;
+  const size_t smh = sizeof(double) * HCH * 5 * 4 + sizeof(int) * (Smem<5>::TP + 1);
+  switch (variant) {
+#define KMX_GB(V, G, W) case V: hipLaunchKernelGGL((k_gbench<5, G, W>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
+    KMX_GB(0, 0, 1) KMX_GB(1, 0, 4) KMX_GB(2, 0, 6) KMX_GB(3, 0, 8)
+    KMX_GB(10, 1, 1) KMX_GB(11, 1, 4) KMX_GB(12, 1, 6)
+    KMX_GB(20, 2, 1) KMX_GB(21, 2, 4) KMX_GB(22, 2, 6) KMX_GB(23, 2, 8)
+    KMX_GB(40, 3, 1) KMX_GB(41, 3, 4) KMX_GB(42, 3, 6) KMX_GB(45, 4, 1)
+    KMX_GB(60, 5, 1) KMX_GB(61, 5, 4) KMX_GB(62, 5, 6) KMX_GB(65, 6, 1)
+#undef KMX_GB
+#define KMX_GB(V, G, W) case V: hipLaunchKernelGGL((k_gbench<5, G, W>), grid, blk, (SmemG<5, G>::bytes), h->stream, h->dv, (const double*)h->dv.X, out); return true;
+    KMX_GB(70, 7, 1) KMX_GB(71, 7, 4) KMX_GB(72, 7, 5) KMX_GB(75, 8, 1)
+#define KMX_GC(V, C) case V: hipLaunchKernelGGL((k_gcap<5, C>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
+    KMX_GC(50, 1000) KMX_GC(51, 12) KMX_GC(52, 10) KMX_GC(53, 8) KMX_GC(54, 4)
+#undef KMX_GC
+#undef KMX_GB
+#define KMX_GA(V, A) case V: hipLaunchKernelGGL((k_gablate<5, A>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
+    KMX_GA(30, 0) KMX_GA(31, 1) KMX_GA(32, 2) KMX_GA(33, 3)
+#undef KMX_GA
+    case 90: hipLaunchKernelGGL((k_hinc<5, 0, HCH>), grid, blk, smh, h->stream, h->dv, (const double*)h->dv.X, Dg, out); return true;
+    case 91: hipLaunchKernelGGL((k_hinc<5, 1, HCH>), grid, blk, smh, h->stream, h->dv, (const double*)h->dv.X, Dg, out); return true;
+    case 92:
+      if (!h->hinc) return false;
+      hipLaunchKernelGGL((k_gbench_hinc<5, false>), grid, blk, SmemH<5>::bytes, h->stream, h->dv, (const double*)h->dv.X, out);
+      return true;
+    case 93:
+      if (!h->hinc) return false;
+      hipLaunchKernelGGL((k_gbench_hinc<5, true>), grid, blk, SmemH<5>::bytes, h->stream, h->dv, (const double*)h->dv.X, out);
+      return true;
+    default: return false;
+  }
+}
+
+static int gbench_check(kmx_pgo* h, int variant) {
+  KMX_CHECK(variant < 40 || variant == 90 || h->d_crec, KMX_EINVAL, "compact records not built (KMX_GATHER / non-SO(3) input)");
+  KMX_CHECK(variant < 91 || !h->rect, KMX_EINVAL, "variant 91 reads CSR-order compact records (KMX_RECT=0)");
+  return KMX_OK;
+}
+
+// D_i blocks for the lane-per-incidence prototype (caller frees).
+static int gbench_diag(kmx_pgo* h, double** D) {
+  KMX_HIP(hipMalloc(D, sizeof(double) * 16 * (size_t)std::max(h->nloc, 1)));
+  hipLaunchKernelGGL(k_diag, dim3((h->nloc + 255) / 256), dim3(256), 0, h->stream, h->dv, *D);
+  KMX_HIP(hipGetLastError());
+  return KMX_OK;
+}
+
 // Diagnostic entry point (not used by the product path): time `reps` launches
 // of the gather primitive variant (GV, LBW) = (variant / 10, variant % 10 ->
-// min waves per SIMD {0: none, 1: 4, 2: 6, 3: 8}) over the current iterate.
+// min waves per SIMD {0: none, 1: 4, 2: 6, 3: 8}) over the current iterate;
+// 90 / 91: the lane-per-incidence prototype (k_hinc).
 extern "C" int kmx_pgo_debug_gather_bench(kmx_pgo* h, int variant, int reps, double* ms_out) {
   KMX_CHECK(ready(h) && ms_out && reps > 0, KMX_EINVAL, "bad argument");
   KMX_CHECK(h->P.r == 5, KMX_EUNSUP, "gather bench is built for r = 5");
   KMX_HIP(hipSetDevice(h->device));
+  int rc = gbench_check(h, variant);
+  if (rc) return rc;
   const size_t vec = (size_t)std::max(h->nloc, 1) * 4 * h->P.r;
   double* out = h->d_scratch + vec;
+  double* Dg = nullptr;
+  if ((rc = gbench_diag(h, &Dg))) return rc;
   hipEvent_t e0, e1;
   KMX_HIP(hipEventCreate(&e0));
   KMX_HIP(hipEventCreate(&e1));
-  const dim3 grid(h->ntiles), blk(BLOCK);
-  const size_t sm = Smem<5>::bytes;
-  auto launch = [&]() -> bool {
-    switch (variant) {
-#define KMX_GB(V, G, W) case V: hipLaunchKernelGGL((k_gbench<5, G, W>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
-      KMX_GB(0, 0, 1) KMX_GB(1, 0, 4) KMX_GB(2, 0, 6) KMX_GB(3, 0, 8)
-      KMX_GB(10, 1, 1) KMX_GB(11, 1, 4) KMX_GB(12, 1, 6)
-      KMX_GB(20, 2, 1) KMX_GB(21, 2, 4) KMX_GB(22, 2, 6) KMX_GB(23, 2, 8)
-      KMX_GB(40, 3, 1) KMX_GB(41, 3, 4) KMX_GB(42, 3, 6) KMX_GB(45, 4, 1)
-      KMX_GB(60, 5, 1) KMX_GB(61, 5, 4) KMX_GB(62, 5, 6) KMX_GB(65, 6, 1)
-#undef KMX_GB
-#define KMX_GB(V, G, W) case V: hipLaunchKernelGGL((k_gbench<5, G, W>), grid, blk, (SmemG<5, G>::bytes), h->stream, h->dv, (const double*)h->dv.X, out); return true;
-      KMX_GB(70, 7, 1) KMX_GB(71, 7, 4) KMX_GB(72, 7, 5) KMX_GB(75, 8, 1)
-#define KMX_GC(V, C) case V: hipLaunchKernelGGL((k_gcap<5, C>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
-      KMX_GC(50, 1000) KMX_GC(51, 12) KMX_GC(52, 10) KMX_GC(53, 8) KMX_GC(54, 4)
-#undef KMX_GC
-#undef KMX_GB
-#define KMX_GA(V, A) case V: hipLaunchKernelGGL((k_gablate<5, A>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
-      KMX_GA(30, 0) KMX_GA(31, 1) KMX_GA(32, 2) KMX_GA(33, 3)
-#undef KMX_GA
-      default: return false;
-    }
-  };
-  KMX_CHECK(variant < 40 || h->d_crec, KMX_EINVAL, "compact records not built (KMX_GATHER / non-SO(3) input)");
-  if (!launch()) return kmx::fail(KMX_EINVAL, "unknown gather variant");
+  if (!gbench_launch(h, variant, out, Dg)) { (void)hipFree(Dg); return kmx::fail(KMX_EINVAL, "unknown gather variant"); }
   KMX_HIP(hipEventRecord(e0, h->stream));
-  for (int i = 0; i < reps; ++i) launch();
+  for (int i = 0; i < reps; ++i) gbench_launch(h, variant, out, Dg);
   KMX_HIP(hipEventRecord(e1, h->stream));
   KMX_HIP(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -2767,5 +3327,36 @@ extern "C" int kmx_pgo_debug_gather_bench(kmx_pgo* h, int variant, int reps, dou
   *ms_out = (double)ms / reps;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  KMX_HIP(hipFree(Dg));
+  return KMX_OK;
+}
+
+// Diagnostic: run gather variants va and vb over the current iterate and
+// report max |out_a - out_b| and max |out_a| (valid pose rows only).
+extern "C" int kmx_pgo_debug_gather_cmp(kmx_pgo* h, int va, int vb, double* maxdiff, double* maxabs) {
+  KMX_CHECK(ready(h) && maxdiff && maxabs, KMX_EINVAL, "bad argument");
+  KMX_CHECK(h->P.r == 5, KMX_EUNSUP, "gather bench is built for r = 5");
+  KMX_HIP(hipSetDevice(h->device));
+  int rc;
+  if ((rc = gbench_check(h, va)) || (rc = gbench_check(h, vb))) return rc;
+  const size_t vec = (size_t)std::max(h->nloc, 1) * 4 * h->P.r;
+  double* out = h->d_scratch + vec;
+  double* Dg = nullptr;
+  if ((rc = gbench_diag(h, &Dg))) return rc;
+  std::vector<double> A(vec), B(vec);
+  bool ok = gbench_launch(h, va, out, Dg);
+  KMX_HIP(hipMemcpyAsync(A.data(), out, sizeof(double) * vec, hipMemcpyDeviceToHost, h->stream));
+  ok = ok && gbench_launch(h, vb, out, Dg);
+  KMX_HIP(hipMemcpyAsync(B.data(), out, sizeof(double) * vec, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  KMX_HIP(hipFree(Dg));
+  if (!ok) return kmx::fail(KMX_EINVAL, "unknown gather variant");
+  double md = 0.0, ma = 0.0;
+  for (size_t i = 0; i < vec; ++i) {
+    md = std::max(md, std::fabs(A[i] - B[i]));
+    ma = std::max(ma, std::fabs(A[i]));
+  }
+  *maxdiff = md;
+  *maxabs = ma;
   return KMX_OK;
 }

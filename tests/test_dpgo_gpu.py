@@ -70,11 +70,14 @@ def test_primitives_match_oracle(gpu, r, gather, monkeypatch):
             assert abs(gs - os_) <= 1e-10 * max(1.0, abs(os_)), (mode, gs, os_)
 
 
-@pytest.mark.parametrize("robust,gather", [(False, None), (True, None), (True, "2"), (True, "3")])
+@pytest.mark.parametrize("robust,gather", [(False, None), (True, None), (True, "nohinc"), (True, "2"), (True, "3")])
 def test_rounds_match_oracle(gpu, robust, gather, monkeypatch):
     """gather None = default (degree-balanced gather over compact 96-B records on
-    SO(3) input); "3" the per-pose compact gather; "2" the full 128-B records."""
-    if gather is not None:
+    SO(3) input, incidence-parallel Hessian gather); "nohinc" the degree-balanced
+    gather in k_hess too; "3" the per-pose compact gather; "2" the full 128-B records."""
+    if gather == "nohinc":
+        monkeypatch.setenv("KMX_HINC", "0")
+    elif gather is not None:
         monkeypatch.setenv("KMX_GATHER", gather)
     g, P, X0 = _setup(robust=robust)
     s, o = _pair(g, P, X0)

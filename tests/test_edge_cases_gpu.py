@@ -42,12 +42,14 @@ def _hub_graph(seed=9):
         init_R=[g.init_R[0][:4], g.init_R[1], g.init_R[2]], init_t=[g.init_t[0][:4], g.init_t[1], g.init_t[2]])
 
 
-@pytest.mark.parametrize("gather,tilebal", [(None, "1"), (None, "0"), ("7", "1"), ("3", "1")])
+@pytest.mark.parametrize("gather,tilebal", [(None, "1"), (None, "0"), ("nohinc", "1"), ("7", "1"), ("3", "1")])
 def test_hub_pose_and_tiny_robot(gpu, gather, tilebal, monkeypatch):
     from kmx.dpgo.params import PGOAgentParameters
     from kmx.dpgo.solver import BlockSolver
     from oracle.oracle import OraclePGO
-    if gather is not None:
+    if gather == "nohinc":
+        monkeypatch.setenv("KMX_HINC", "0")
+    elif gather is not None:
         monkeypatch.setenv("KMX_GATHER", gather)
     monkeypatch.setenv("KMX_TILEBAL", tilebal)
     g = _hub_graph()
