@@ -1042,6 +1042,7 @@ __device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const d
     lds_barrier();
     if (L.valid) {
       const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
+      #pragma unroll 4
       for (int j = j0; j < j1; ++j) {
         double h[4];
         load4(Cs + (j * R + L.a) * 4, h);
@@ -1070,18 +1071,36 @@ __device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const d
 // reads its own pose's row (found by a binary search of the tile CSR), and
 // adds the incidence's cost share (1/2 per endpoint; all of it for a shared
 // edge). The pose sums run in CSR order.
+// k_grad's LDS: a smaller chunk buffer, plus the tile's own rows (every lane
+// reads its incidence's own row from LDS instead of L1).
+template <int R>
+struct SmemHG {
+  static constexpr int TP = WAVES * (64 / R);
+  static constexpr int CH = 192;                                          // incidences per chunk
+  static constexpr int c_off = 0;                                         // double[CH][R][4]
+  static constexpr int x_off = CH * R * 32;                               // double[TP][R][4]
+  static constexpr int ptr_off = x_off + TP * R * 32;                     // int[TP + 1]
+  static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
+  static constexpr int bytes = red_off + 64;
+};
+
 template <int R>
 __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const double* V, const double* pub,
                                           double acc[4], double* cost, char* smem) {
-  using SM = SmemH<R>;
+  using SM = SmemHG<R>;
   constexpr int CH = SM::CH;
   double* Cs = reinterpret_cast<double*>(smem + SM::c_off);
+  double2* xs = reinterpret_cast<double2*>(smem + SM::x_off);
   int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
   const int tid = threadIdx.x;
   const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
   const int K0 = d.inc_ptr[p0];
   const int n = d.inc_ptr[p0 + np] - K0;
   if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
+  {
+    const double2* v2 = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
+    for (int i = tid; i < np * 2 * R; i += BLOCK) xs[i] = v2[i];
+  }
   const int pl = L.pose - p0;
   const int lt = min(tid, CH - 1);
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
@@ -1106,7 +1125,7 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
     const int2 in = unpack_int2(q[5].y);
     const int o = in.x;
     const bool tail = (in.y >> 31) & 1;
-    const double2* s2 = reinterpret_cast<const double2*>(V + (size_t)(p0 + lo) * 4 * R);
+    const double2* s2 = xs + lo * 2 * R;
     const double2* o2 = reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
     double2 vo2[2 * R];
 #pragma unroll
@@ -1116,8 +1135,7 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
     if (tid < CH && c0 + tid < n) {
 #pragma unroll
       for (int a = 0; a < R; ++a) {
-        // own rows: neighbouring lanes share the pose, so these hit in L1
-        const double2 sa = s2[2 * a], sb = s2[2 * a + 1];
+        const double2 sa = s2[2 * a], sb = s2[2 * a + 1];  // own row, from LDS
         const double vs[4] = {sa.x, sa.y, sb.x, sb.y};
         const double vo[4] = {vo2[2 * a].x, vo2[2 * a].y, vo2[2 * a + 1].x, vo2[2 * a + 1].y};
         double h[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1131,6 +1149,7 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
     lds_barrier();
     if (L.valid) {
       const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
+      #pragma unroll 4
       for (int j = j0; j < j1; ++j) {
         double h[4];
         load4(Cs + (j * R + L.a) * 4, h);
@@ -1144,7 +1163,7 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
 template <int R, int GV>
 struct SmemGrad : SmemG<R, GV> {};
 template <int R>
-struct SmemGrad<R, 9> : SmemH<R> {};
+struct SmemGrad<R, 9> : SmemHG<R> {};
 
 // -------------------------------------------- fused per-robot reductions --
 // Each tile of robot l publishes its partial sums, then takes a ticket on
@@ -1356,7 +1375,8 @@ __global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) vo
   if (L.valid) load4(d.X + (size_t)L.pose * 4 * R + 4 * L.a, y);
   double S[9], gr[4], zr[4];
   // G = 9: the gather's chunk buffer is free now (its last barrier passed)
-  double* scr = reinterpret_cast<double*>(smem + SmemH<R>::c_off);
+  double* scr = reinterpret_cast<double*>(smem + SmemHG<R>::c_off);
+  static_assert(WAVES * 64 * 6 * 8 <= SmemHG<R>::x_off, "scratch");
   if (d.dbg & 2) {
     for (int i = 0; i < 9; ++i) S[i] = 0.0;
   } else {
@@ -2117,7 +2137,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_gbench_hinc(Dev d, const double* V
   else hinc_gather<R>(d, L, V, acc, smem);
   if (L.valid) store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
   if constexpr (GRAD) {
-    const double t = block_sum(cost, reinterpret_cast<double*>(smem + SmemH<R>::red_off));
+    const double t = block_sum(cost, reinterpret_cast<double*>(smem + SmemHG<R>::red_off));
     if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
   }
 }
@@ -3280,7 +3300,7 @@ static bool gbench_launch(kmx_pgo* h, int variant, double* out, const double* Dg
       return true;
     case 93:
       if (!h->hinc) return false;
-      hipLaunchKernelGGL((k_gbench_hinc<5, true>), grid, blk, SmemH<5>::bytes, h->stream, h->dv, (const double*)h->dv.X, out);
+      hipLaunchKernelGGL((k_gbench_hinc<5, true>), grid, blk, SmemHG<5>::bytes, h->stream, h->dv, (const double*)h->dv.X, out);
       return true;
     default: return false;
   }
