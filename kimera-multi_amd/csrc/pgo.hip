@@ -1553,8 +1553,9 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
 template <int R>
 struct SmemC {
   static constexpr int TP = WAVES * (64 / R);
-  static constexpr int ptr_off = 0;                                  // int[TP + 1]
-  static constexpr int red_off = ((TP + 1) * 4 + 15) / 16 * 16;
+  static constexpr int x_off = 0;                                    // double[TP][R][4] own rows
+  static constexpr int ptr_off = TP * R * 32;                        // int[TP + 1]
+  static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
   static constexpr int bytes = red_off + 64;
 };
 template <int R, int GV>
@@ -1566,11 +1567,16 @@ template <int R>
 __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, const double* V, const double* pub,
                                                  char* smem) {
   int* sptr = reinterpret_cast<int*>(smem + SmemC<R>::ptr_off);
+  double2* xs = reinterpret_cast<double2*>(smem + SmemC<R>::x_off);
   const int tid = threadIdx.x;
   const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
   const int K0 = d.optr[p0];
   const int n = d.optr[p0 + np] - K0;
   if (tid <= np) sptr[tid] = d.optr[p0 + tid] - K0;
+  {
+    const double2* v2 = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
+    for (int i = tid; i < np * 2 * R; i += BLOCK) xs[i] = v2[i];
+  }
   __syncthreads();
   double cost = 0.0;
   for (int k = tid; k < n; k += BLOCK) {
@@ -1587,7 +1593,7 @@ __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, co
     const int2 in = unpack_int2(q[5].y);
     const int o = in.x;
     const bool tail = (in.y >> 31) & 1;
-    const double2* s2 = reinterpret_cast<const double2*>(V + (size_t)(p0 + lo) * 4 * R);
+    const double2* s2 = xs + lo * 2 * R;  // own row, from LDS
     const double2* o2 = reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
     double2 vs2[2 * R], vo2[2 * R];
 #pragma unroll
