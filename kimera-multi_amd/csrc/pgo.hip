@@ -1635,9 +1635,7 @@ __global__ __launch_bounds__(BLOCK) void k_commit(Dev d) {
   store4(d.X + o, v);
 }
 
-__global__ void k_round_begin(Dev d, const unsigned char* active) {
-  const int l = threadIdx.x;
-  if (l >= d.L) return;
+__device__ __forceinline__ void begin_robot(const Dev& d, const unsigned char* active, int l) {
   Ctl& c = d.ctl[l];
   const bool a = active ? active[l] != 0 : true;
   const Ctl zero = {};
@@ -1645,6 +1643,29 @@ __global__ void k_round_begin(Dev d, const unsigned char* active) {
   c.phase = a ? PH_START : PH_IDLE;
   c.updated = a ? 1 : 0;
   c.Delta = d.p.Delta0;
+}
+
+__global__ void k_round_begin(Dev d, const unsigned char* active) {
+  const int l = threadIdx.x;
+  if (l >= d.L) return;
+  begin_robot(d, active, l);
+}
+
+// Round start fused with k_publish (iterate_async with refresh_local): block 0
+// activates the robots, the other blocks copy the owned public rows. The two
+// touch disjoint data, so one launch replaces two.
+__global__ void k_round_begin_pub(Dev d, const unsigned char* active, const double* X, double* pub, const int* src,
+                                  int nslots, int ps) {
+  if (blockIdx.x == 0) {
+    for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
+    return;
+  }
+  const long long i = (long long)(blockIdx.x - 1) * blockDim.x + threadIdx.x;
+  const long long s = i / ps;
+  if (s >= nslots) return;
+  const int q = (int)(i - s * ps);
+  const int p = src[s];
+  if (p >= 0) pub[s * ps + q] = X[(long long)p * ps + q];
 }
 
 __global__ void k_publish(const double* X, double* pub, const int* src, int nslots, int ps) {
@@ -2189,6 +2210,7 @@ struct kmx_pgo {
   double* d_crec = nullptr;  // compact records (gather variant 3), null when not usable
   double* d_ocrec = nullptr;
   bool hinc = false;  // k_hess runs the incidence-parallel gather (G = 9)
+  bool publish_in_begin = false;  // the next enqueue_round also publishes the owned rows
   double* d_hrec = nullptr;
   double* d_hD = nullptr;
   double* d_hocrec = nullptr;
@@ -2354,8 +2376,15 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
     }
     return running;
   };
-  hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(std::max(64, ((h->dv.L + 63) / 64) * 64)), 0, h->stream,
-                     h->dv, d_active);
+  const long long npub_el = h->n_owned * 4 * h->P.r;
+  if (h->publish_in_begin && npub_el > 0) {
+    hipLaunchKernelGGL(k_round_begin_pub, dim3((unsigned)(1 + (npub_el + 255) / 256)), dim3(256), 0, h->stream,
+                       h->dv, d_active, (const double*)h->d_vec, h->d_pub + (size_t)h->first_owned * 4 * h->P.r,
+                       (const int*)(h->d_pub_src + h->first_owned), (int)h->n_owned, 4 * h->P.r);
+  } else {
+    hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(std::max(64, ((h->dv.L + 63) / 64) * 64)), 0, h->stream,
+                       h->dv, d_active);
+  }
   for (int it = 0; it < h->P.rtr_iterations; ++it) {
     hipLaunchKernelGGL((k_grad<R, G, F>), grid, blk, smr, h->stream, h->dv);
     red(RED_GRAD);
@@ -3075,8 +3104,9 @@ extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local, 
   KMX_CHECK(rounds >= 0, KMX_EINVAL, "negative rounds");
   KMX_HIP(hipSetDevice(h->device));
   for (int i = 0; i < rounds; ++i) {
-    if (refresh_local) enqueue_publish(h);
+    h->publish_in_begin = refresh_local != 0;  // k_publish folded into the round's first launch
     enqueue_round(h, h->d_active);
+    h->publish_in_begin = false;
     h->round_counter++;
     if (gnc_every > 0 && h->P.robust_cost == KMX_COST_GNC_TLS && h->round_counter % gnc_every == 0) {
       if (refresh_local) enqueue_publish(h);
