@@ -2751,7 +2751,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   std::vector<double> hrec, hocrec;
   std::vector<int2> heopos;
   h->hinc = false;
-  if (h->gvar == 5) {
+  if (h->gvar == 5 && r <= 5) {  // r >= 6 spills at 128 VGPRs: keep the row gather there
     bool want = true;
     if (const char* v = std::getenv("KMX_HINC")) want = std::atoi(v) != 0;
     if (want) {

@@ -100,6 +100,25 @@ def test_rounds_match_oracle(gpu, robust, gather, monkeypatch):
             assert np.abs(wg - wo).max() <= 1e-9, np.abs(wg - wo).max()
 
 
+@pytest.mark.parametrize("r", [3, 4, 8])
+def test_rounds_match_oracle_rank(gpu, r):
+    """The incidence-parallel kernels (and their LDS layouts: chunk of TP*r
+    incidences, 64 // r poses per wave) at other relaxation ranks, GNC on."""
+    g, P, X0 = _setup(r=r)
+    s, o = _pair(g, P, X0)
+    for it in range(8):
+        s.refresh_local()
+        sg = s.iterate()
+        so = o.iterate()
+        for a in range(g.n_robots):
+            assert sg[a]["tcg_iterations"] == so[a]["tcg_iterations"], (it, a, sg[a], so[a])
+            d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
+            assert d <= 1e-6, (it, a, d)
+        if it % 4 == 3:
+            s.refresh_local()
+            assert s.update_weights() == o.update_weights()
+
+
 def test_sequential_schedule(gpu):
     g, P, X0 = _setup()
     s, o = _pair(g, P, X0)
