@@ -2667,13 +2667,25 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   // ceil(incidences / groups)); KMX_TILEBAL=0 cuts plain runs of tile_poses.
   bool tilebal = true;
   if (const char* v = std::getenv("KMX_TILEBAL")) tilebal = std::atoi(v) != 0;
+  // The incidence-parallel kernels (G = 9) walk a tile in chunks of TP * r
+  // incidences, one LDS hand-off each: capping tiles at two chunks takes the
+  // Hessian gather from ~3 to 2 hand-offs (32 -> 30 us at configs[3]).
+  // KMX_TILECAP overrides (0 = no cap).
+  int64_t tilecap = INT64_MAX;
+  {
+    const char* hv = std::getenv("KMX_HINC");
+    const bool g9 = r <= 5 && (h->gvar_req < 0 || h->gvar_req == 5) && !(hv && std::atoi(hv) == 0);
+    if (g9) tilecap = 2 * (int64_t)(WAVES * (64 / r) * r);
+    if (const char* v = std::getenv("KMX_TILECAP")) tilecap = std::atoi(v) > 0 ? std::atoi(v) : INT64_MAX;
+  }
   for (int l = 0; l < L; ++l) {
     const int n = n_poses[h->robots[l]];
     const int base = h->loff[l];
     rt0[l] = (int)tr.size();
     const int64_t inc_l = (int64_t)inc_ptr[base + n] - inc_ptr[base];
     const int64_t full = std::max<int64_t>(1, (n + h->tile_poses - 1) / h->tile_poses);
-    const int64_t cap = tilebal ? std::max<int64_t>(1, (inc_l * 21 / 20 + full - 1) / full) : INT64_MAX;
+    const int64_t cap =
+        std::min(tilecap, tilebal ? std::max<int64_t>(1, (inc_l * 21 / 20 + full - 1) / full) : INT64_MAX);
     int p0 = 0;
     while (p0 < n) {
       int np = 0;
@@ -3344,7 +3356,7 @@ static bool gbench_launch(kmx_pgo* h, int variant, double* out, const double* Dg
 
 static int gbench_check(kmx_pgo* h, int variant) {
   KMX_CHECK(variant < 40 || variant == 90 || h->d_crec, KMX_EINVAL, "compact records not built (KMX_GATHER / non-SO(3) input)");
-  KMX_CHECK(variant < 91 || !h->rect, KMX_EINVAL, "variant 91 reads CSR-order compact records (KMX_RECT=0)");
+  KMX_CHECK(variant != 91 || !h->rect, KMX_EINVAL, "variant 91 reads CSR-order compact records (KMX_RECT=0)");
   return KMX_OK;
 }
 
