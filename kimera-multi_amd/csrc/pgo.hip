@@ -1073,10 +1073,13 @@ __device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const d
 // edge). The pose sums run in CSR order.
 // k_grad's LDS: a smaller chunk buffer, plus the tile's own rows (every lane
 // reads its incidence's own row from LDS instead of L1).
+#ifndef KMX_HG_CH
+#define KMX_HG_CH 240
+#endif
 template <int R>
 struct SmemHG {
   static constexpr int TP = WAVES * (64 / R);
-  static constexpr int CH = 192;                                          // incidences per chunk
+  static constexpr int CH = KMX_HG_CH;                                    // incidences per chunk
   static constexpr int c_off = 0;                                         // double[CH][R][4]
   static constexpr int x_off = CH * R * 32;                               // double[TP][R][4]
   static constexpr int ptr_off = x_off + TP * R * 32;                     // int[TP + 1]
@@ -2334,7 +2337,7 @@ void enqueue_gnc(kmx_pgo* h) {
 template <int R, int G, int F>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   const dim3 grid(h->ntiles), blk(BLOCK);
-  const size_t sm = Smem<R>::bytes, smg = SmemG<R, G>::bytes, smh = SmemHess<R, G>::bytes,
+  const size_t sm = Smem<R>::bytes, smh = SmemHess<R, G>::bytes,
                smc = SmemCost<R, G>::bytes, smr = SmemGrad<R, G>::bytes;
   auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0) {
     if (!F) hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(BLOCK), 0, h->stream, h->dv, kind, R, hs, seq);
