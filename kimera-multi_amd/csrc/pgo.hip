@@ -1654,6 +1654,19 @@ __global__ void k_round_begin(Dev d, const unsigned char* active) {
   begin_robot(d, active, l);
 }
 
+// One 16-B part i of the owned public rows: slot s = i / (ps / 2) (ps = 4r is
+// even, rows are 16-B aligned).
+__device__ __forceinline__ void publish_part(const double* X, double* pub, const int* src, int nslots, int ps,
+                                             long long i) {
+  const int ps2 = ps >> 1;
+  const long long s = i / ps2;
+  if (s >= nslots) return;
+  const int q = (int)(i - s * ps2);
+  const int p = src[s];
+  if (p >= 0)
+    reinterpret_cast<double2*>(pub)[s * ps2 + q] = reinterpret_cast<const double2*>(X)[(long long)p * ps2 + q];
+}
+
 // Round start fused with k_publish (iterate_async with refresh_local): block 0
 // activates the robots, the other blocks copy the owned public rows. The two
 // touch disjoint data, so one launch replaces two.
@@ -1663,21 +1676,11 @@ __global__ void k_round_begin_pub(Dev d, const unsigned char* active, const doub
     for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
     return;
   }
-  const long long i = (long long)(blockIdx.x - 1) * blockDim.x + threadIdx.x;
-  const long long s = i / ps;
-  if (s >= nslots) return;
-  const int q = (int)(i - s * ps);
-  const int p = src[s];
-  if (p >= 0) pub[s * ps + q] = X[(long long)p * ps + q];
+  publish_part(X, pub, src, nslots, ps, (long long)(blockIdx.x - 1) * blockDim.x + threadIdx.x);
 }
 
 __global__ void k_publish(const double* X, double* pub, const int* src, int nslots, int ps) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long s = i / ps;
-  if (s >= nslots) return;
-  const int q = (int)(i - s * ps);
-  const int p = src[s];
-  if (p >= 0) pub[s * ps + q] = X[(long long)p * ps + q];
+  publish_part(X, pub, src, nslots, ps, (long long)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // Sparse exchange: rows of the given public slots (owned by this handle) from
@@ -2311,7 +2314,7 @@ void enqueue_publish(kmx_pgo* h) {
   const int ps = 4 * h->P.r;
   const long long tot = h->n_owned * ps;
   if (tot == 0) return;
-  hipLaunchKernelGGL(k_publish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
+  hipLaunchKernelGGL(k_publish, dim3((unsigned)((tot / 2 + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
                      h->d_pub + (size_t)h->first_owned * ps, h->d_pub_src + h->first_owned, (int)h->n_owned, ps);
 }
 
@@ -2381,7 +2384,7 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   };
   const long long npub_el = h->n_owned * 4 * h->P.r;
   if (h->publish_in_begin && npub_el > 0) {
-    hipLaunchKernelGGL(k_round_begin_pub, dim3((unsigned)(1 + (npub_el + 255) / 256)), dim3(256), 0, h->stream,
+    hipLaunchKernelGGL(k_round_begin_pub, dim3((unsigned)(1 + (npub_el / 2 + 255) / 256)), dim3(256), 0, h->stream,
                        h->dv, d_active, (const double*)h->d_vec, h->d_pub + (size_t)h->first_owned * 4 * h->P.r,
                        (const int*)(h->d_pub_src + h->first_owned), (int)h->n_owned, 4 * h->P.r);
   } else {
