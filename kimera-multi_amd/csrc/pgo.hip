@@ -1520,19 +1520,18 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-  double x[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0};
-  if (L.valid) {
+  double x[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0}, gg[4] = {0, 0, 0, 0}, rr[4] = {0, 0, 0, 0};
+  if (L.valid) {  // all four rows in flight before the Gram-Schmidt chain
     load4(d.X + o, x);
     load4(d.eta + o, et);
+    load4(d.g + o, gg);
+    load4(d.r + o, rr);
   }
   double xt[4];
   group_retract<R>(x, et, L.base, xt);
   double vals[2] = {0.0, 0.0};
   if (L.valid) {
     store4(d.Xt + o, xt);
-    double gg[4], rr[4];
-    load4(d.g + o, gg);
-    load4(d.r + o, rr);
     double m = 0.0, ch = 0.0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
