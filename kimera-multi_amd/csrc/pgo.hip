@@ -44,6 +44,8 @@ constexpr int WAVES = 4;
 #endif
 constexpr int BLOCK = 64 * WAVES;
 constexpr int NPART = 4;  // partial sums per tile
+// per-kernel LDS reduction area: NPART x WAVES wave sums + the ticket flag
+constexpr int RED_BYTES = 8 * NPART * WAVES + 16;
 
 enum Phase { PH_IDLE = 0, PH_START = 1, PH_TCG = 2, PH_STEP = 3 };
 enum Mode { MODE_INTERIOR = 0, MODE_BOUNDARY = 1 };
@@ -451,7 +453,7 @@ struct Smem {
   static constexpr int edge_off = x_off + TP * R * 32;                // double[CI][16]
   static constexpr int con_off = edge_off + CI * 128;                 // double[CI][R][4]
   static constexpr int red_off = con_off + CI * R * 32;               // double[WAVES] + flag
-  static constexpr int bytes = red_off + 64;
+  static constexpr int bytes = red_off + RED_BYTES;
 };
 
 template <int R, bool PUB>
@@ -771,7 +773,7 @@ struct SmemL {
   static constexpr int h_off = a_off + TP * R * 32;                      // double[NG][R][4]
   static constexpr int rec_off = h_off + NG * R * 32;                    // double[CH][12]
   static constexpr int red_off = rec_off + CH * 96;
-  static constexpr int bytes = red_off + 64;
+  static constexpr int bytes = red_off + RED_BYTES;
 };
 #ifndef KMX_SEG
 #define KMX_SEG 4
@@ -964,7 +966,7 @@ struct SmemH {
   static constexpr int c_off = 0;                                         // double[CH][R][4]
   static constexpr int ptr_off = CH * R * 32;                             // int[TP + 1]
   static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
-  static constexpr int bytes = red_off + 64;
+  static constexpr int bytes = red_off + RED_BYTES;
 };
 // group_symYtG<R, true> scratch: BLOCK x 6 doubles at the start of the LDS
 static_assert(WAVES * 64 * 6 * 8 <= SmemH<3>::ptr_off && WAVES * 64 * 6 * 8 <= SmemH<8>::ptr_off, "scratch");
@@ -1084,7 +1086,7 @@ struct SmemHG {
   static constexpr int x_off = CH * R * 32;                               // double[TP][R][4]
   static constexpr int ptr_off = x_off + TP * R * 32;                     // int[TP + 1]
   static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
-  static constexpr int bytes = red_off + 64;
+  static constexpr int bytes = red_off + RED_BYTES;
 };
 
 template <int R>
@@ -1180,17 +1182,32 @@ template <int KIND, int NV, int FUSED>
 __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const double* vals, char* smem_red,
                                             int R_) {
   double* lds = reinterpret_cast<double*>(smem_red);
-  int* flag = reinterpret_cast<int*>(smem_red + 8 * WAVES);
+  int* flag = reinterpret_cast<int*>(smem_red + 8 * NPART * WAVES);
+  static_assert(NV <= NPART && WAVES == 4, "reduction area");
   double tv[NV > 0 ? NV : 1];
-#pragma unroll
-  for (int s = 0; s < NV; ++s) tv[s] = block_sum(vals[s], lds);
   if constexpr (!FUSED) {
+    // all NV sums in one LDS round (same wave and wave-order summation as
+    // block_sum); only thread 0 needs them. The area is used once per launch,
+    // and the barrier is LDS-only, so the caller's row stores keep draining.
+#pragma unroll
+    for (int s = 0; s < NV; ++s) {
+      const double w = wave_sum(vals[s]);
+      if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
+    }
+    lds_barrier();
     if (threadIdx.x == 0) {
 #pragma unroll
-      for (int s = 0; s < NV; ++s) d.part[(size_t)L.tile * NPART + s] = tv[s];
+      for (int s = 0; s < NV; ++s) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
+        d.part[(size_t)L.tile * NPART + s] = t;
+      }
     }
     return;
   } else {
+#pragma unroll
+    for (int s = 0; s < NV; ++s) tv[s] = block_sum(vals[s], lds);
     // Write-through (sc1) partial stores, drained, then one agent-scope
     // ticket per tile; the last arriver reads the partials with sc1 loads
     // (MI355X_MICROARCH.md "Valid forms", table row 1).
@@ -1558,7 +1575,7 @@ struct SmemC {
   static constexpr int x_off = 0;                                    // double[TP][R][4] own rows
   static constexpr int ptr_off = TP * R * 32;                        // int[TP + 1]
   static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
-  static constexpr int bytes = red_off + 64;
+  static constexpr int bytes = red_off + RED_BYTES;
 };
 template <int R, int GV>
 struct SmemCost : SmemG<R, GV> {};
