@@ -1,22 +1,31 @@
 #!/usr/bin/env python3
 """bench.py — dpgo edges·iters/sec (+ LC candidates verified/sec) on MI355X.
 
-Contract (see task statement / DESIGN.md "Measurement"):
+Contract (see task statement / DESIGN.md §6 "Measurement"):
   python bench.py --gpus N --steps K --warmup W
   (N > 1 is launched by torch.distributed.run, one rank per GPU over RCCL).
+
 A "step" is one synchronous RBCD round (dpgo_ros UPDATE -> PGOAgent::iterate of
-every robot block, drawio:2058-2066) with the GNC weight update every 20 rounds
-inside the timed region. At N = 1 the graph is configs[3]: 100k poses / 500k
-edges, 20 % outlier loop closures, 8 robot blocks.
+every robot block, drawio:2058-2066), with GNC-TLS weight updates decided by
+the schedule inside the timed region. The graph is configs[3]: 100k poses /
+500k edges, 20 % outlier loop closures, 8 robot blocks.
+
+The timed window is a fixed, stated slice of the solve:
+  rounds [B, B + W)          untimed: B = --burn-in (default 40) rounds in which
+                              tCG stops after 1-5 steps, then the W warmup rounds
+  rounds [B + W, B + W + K)  timed (value), K = --steps
+The window is replayed from a snapshot of the solver state (iterate, GNC
+weights and schedule state, statuses) with HIP events around every
+Hessian-vector launch: the roofline describes exactly the timed rounds (the
+replay must reproduce their work counters). The CPU baseline restarts the
+restatement from the same snapshot and times the same rounds.
 
 Multi-GPU (one process per GPU, robot blocks dealt to ranks, one all-to-all of
-public poses per round over RCCL):
-  --scaling weak (default): every GPU holds a configs[3]-shaped shard, i.e. the
-      team graph has 8N robot blocks, N x 100k poses and N x 500k edges (same
-      density, outlier and inter-robot fractions); value is the whole team's
-      rate. The fixed configs[3] graph split over the N GPUs (strong scaling)
-      is timed in the same run and reported under "strong".
-  --scaling strong: value is the fixed configs[3] graph split over N GPUs.
+public poses + status words per round over RCCL):
+  --scaling strong (default): the fixed configs[3] graph split over the N GPUs
+      (north_star's "further scaling at 8 GPUs"); value is the team's rate.
+  --scaling weak: every GPU holds a configs[3]-shaped shard (8N robot blocks,
+      N x 100k poses / N x 500k edges). Timed in the same run as an extra.
 
 value = sum over ranks of edges·iters (sum over executed block updates of the
 block's local-problem edge count) / max-over-ranks wall time.
@@ -26,6 +35,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -35,38 +45,41 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "kimera-multi_amd"))
 
-PEAK_HBM = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+PEAK_HBM = 8.0e12      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+PEAK_VALU_OPS = 78.6e12  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="synth100k")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="N > 1: weak = a configs[3]-shaped shard per GPU; strong = configs[3] split over N")
-    ap.add_argument("--strong-steps", type=int, default=None,
-                    help="weak scaling at N > 1: rounds of the extra strong-scaling leg (default --steps; 0 = skip)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--burn-in", type=int, default=40, help="untimed rounds before the warmup (steady-state window)")
+    ap.add_argument("--config", default="synth100k", help="synth100k (configs[3]) or synth1m (the cold 1M/5M graph)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="N > 1: strong = configs[3] split over N (value); weak = a configs[3]-shaped shard per GPU")
+    ap.add_argument("--extra-steps", type=int, default=None,
+                    help="N > 1: rounds of the other scaling leg (default --steps; 0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample per variant")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lcd", action="store_true")
-    ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no cpu / lcd)")
-    ap.add_argument("--no-events", action="store_true", help="skip the HIP-event roofline pass (gap profiling)")
+    ap.add_argument("--no-replay", action="store_true", help="skip the evented replay (roofline)")
+    ap.add_argument("--profile", action="store_true", help="short run for rocprofv3: timed rounds only")
     ap.add_argument("--lcd-frames", type=int, default=50_000)
     ap.add_argument("--lcd-steps", type=int, default=3)
     return ap.parse_args()
 
 
 def make_workload(name, world=1, scaling="strong"):
-    """The named configs graph, or for weak scaling at N > 1 the N-shard team
-    graph of the same shape per GPU (configs[3]: 8 robots / 100k poses / 500k
-    edges per shard; identical to configs[3] at N = 1)."""
+    """The named graph, or for weak scaling at N > 1 the N-shard team graph of
+    the configs[3] shape per GPU (identical to configs[3] at N = 1)."""
     from kmx.synth import config, lift, lifting_matrix, make_pose_graph
     if scaling == "weak" and world > 1:
         if name != "synth100k":
             raise SystemExit("--scaling weak is defined for configs[3] (synth100k)")
         g = make_pose_graph(8 * world, 100_000 * world, 500_000 * world, seed=0)
+    elif name == "synth1m":  # the cold config (SURVEY.md §8d): ~1 GB working set, past the Infinity Cache
+        g = make_pose_graph(8, 1_000_000, 5_000_000, seed=0)
     else:
         g = config(name, seed=0)
     Y = lifting_matrix(5, seed=1)
@@ -85,30 +98,88 @@ def params():
     return P
 
 
-def cpu_baseline(g, X0, P, seconds):
-    """The C restatement (oracle/) on this host, single thread (dpgo runs one
-    agent per process); bounded sample of whole rounds of the same workload."""
+# ---------------------------------------------------------------- snapshot ---
+def snapshot(drv):
+    s = drv.solver
+    return {"X": {a: drv.iterate_of(a) for a in drv.robots}, "w": s.get_weights(), "gnc": s.gnc_state(),
+            "status": s.status()}
+
+
+def restore(drv, snap):
+    s = drv.solver
+    for a in drv.robots:
+        s.set_iterate(a, snap["X"][a])
+    s.set_weights(snap["w"])
+    s.set_gnc_state(snap["gnc"])
+    s.set_status(snap["status"])
+
+
+# --------------------------------------------------------------- CPU legs ---
+def _native_oracle():
+    """Build the restatement for this host (-march=native) outside the repo;
+    returns (path, march) or (None, prebuilt march) when gcc fails."""
+    out = Path(os.environ.get("TMPDIR", "/tmp")) / f"kmx_liborc_native_{os.getpid()}.so"
+    src = [str(ROOT / "oracle" / f) for f in ("dpgo_oracle.c", "lcd_oracle.c", "bow_oracle.c")]
+    cmd = ["gcc", "-O3", "-march=native", "-ffp-contract=off", "-fPIC", "-fopenmp", "-shared", "-o", str(out), *src,
+           "-lm"]
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, timeout=120)
+        return str(out), "native"
+    except Exception:
+        return None, "x86-64-v3"
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(g, P, snap, steps, seconds, threads_list):
+    """The C restatement (oracle/, -march=native) on this host from the
+    snapshot of the timed window's first round: the same rounds as the GPU's
+    timed window (GNC by the host mirror of the schedule), bounded by
+    `seconds` per variant. threads = one per robot block (dpgo runs one agent
+    per process) and 1."""
+    from kmx.dpgo.schedule import GncSchedule
     sys.path.insert(0, str(ROOT))
     from oracle.oracle import OraclePGO
-    o = OraclePGO(P.to_c(), g)
-    for a in range(g.n_robots):
-        o.set_iterate(a, X0[a])
-    edges_iters, rounds = 0, 0
-    t0 = time.perf_counter()
-    while True:
-        st = o.iterate(threads=1)
-        edges_iters += sum(s["edges"] for s in st if s["updated"] and s["tcg_stop"] != "skipped")
-        rounds += 1
-        if rounds % P.robustOptInnerIters == 0:
-            o.update_weights()
+    out = {}
+    for threads in threads_list:
+        o = OraclePGO(P.to_c(), g)
+        for a, X in snap["X"].items():
+            o.set_iterate(a, X)
+        o.set_weights(snap["w"])
+        o.mu = snap["gnc"]["mu"]
+        sched = GncSchedule.from_params(P)
+        sched.inner, sched.updates, sched.mu = snap["gnc"]["inner_iter"], snap["gnc"]["updates"], snap["gnc"]["mu"]
+        relc = np.array(snap["status"], dtype=np.float64)
+        edges_iters, hv, rounds = 0, 0, 0
+        t0 = time.perf_counter()
+        while rounds < steps:
+            if sched.should_update(relc):
+                o.refresh()
+                o.update_weights()
+                sched.updated()
+            st = o.iterate(threads=threads)
+            sched.round_done()
+            relc = np.array([s["rel_change"] if s["updated"] else relc[a] for a, s in enumerate(st)])
+            edges_iters += sum(s["edges"] for s in st if s["updated"] and s["tcg_stop"] != "skipped")
+            hv += sum(s["hessvecs"] for s in st)
+            rounds += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
         el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": edges_iters / el, "unit": "edges*iters/s", "cores": 1, "kind": "port",
-            "sample": f"{rounds} RBCD rounds of {P and 'configs[3]'} (8 blocks, 1 RTR step, <=10 tCG) "
-                      f"from the same initial iterate, oracle/dpgo_oracle.c -O3 x86-64-v3, 1 thread, {el:.1f} s"}
+        out[threads] = {"value": edges_iters / el, "rounds": rounds, "seconds": el, "hessvecs": hv,
+                        "ms_per_step": 1e3 * el / rounds}
+    return out
 
 
+# ---------------------------------------------------------------- LCD legs ---
 def lcd_leg(args, rank, world, barrier_sync):
     """configs[2]: 50k keyframes x 500 ORB descriptors, one candidate per query
     (half planted loop closures), kNN2 + Lowe -> 2D-2D 5-point RANSAC -> 3D-3D.
@@ -129,12 +200,28 @@ def lcd_leg(args, rank, world, barrier_sync):
     det.sync()
     barrier_sync()
     el = time.perf_counter() - t0
+    # evented pass: kNN2 and RANSAC kernel times of one step
+    det.enable_timing(True)
+    det.verify_async(cq, cm)
+    det.sync()
+    tk = det.read_timing()
+    det.enable_timing(False)
     res, _ = det.verify(cq[:256], cm[:256])
+    nf = pool.n_feats.astype(np.int64)
+    pair_evals = float((nf[cq] * nf[cm]).sum())
+    lane_ops = pair_evals * 8  # 32 B per pair: 8 v_sad_u8 lane-ops (L1, the reference matcher)
     out = {"metric": "LC candidates verified/sec", "n_local": int(cq.shape[0]), "steps": args.lcd_steps,
            "elapsed": el, "accepted_frac_first256": sum(r["accepted"] for r in res) / max(len(res), 1),
            "workload": f"configs[2]: {args.lcd_frames} keyframes x 500 ORB descriptors (32 B), "
                        f"{pool.cand_query.shape[0]} candidates, L1 matcher, Lowe 0.7, 5-point RANSAC "
-                       "(thr 1e-6, <=500 it, p 0.995, seed 12345, GCC-9 sampler), 1-point 3D-3D 0.3 m"}
+                       "(thr 1e-6, <=500 it, p 0.995, seed 12345, GCC-9 sampler), 1-point 3D-3D 0.3 m",
+           "roofline": {"kernel": "k_knn2 (kNN2 + Lowe)", "bound": "valu", "unit": "lane-op/s",
+                        "achieved": lane_ops / (tk["knn_ms"] * 1e-3) if tk["knn_ms"] > 0 else 0.0,
+                        "peak": PEAK_VALU_OPS,
+                        "frac": (lane_ops / (tk["knn_ms"] * 1e-3)) / PEAK_VALU_OPS if tk["knn_ms"] > 0 else 0.0,
+                        "algorithmic": f"{pair_evals:.3e} descriptor pairs x 8 v_sad_u8 lane-ops (32 B each)",
+                        "knn_ms": tk["knn_ms"], "ransac_ms": tk["ransac_ms"],
+                        "ransac_share": tk["ransac_ms"] / max(tk["knn_ms"] + tk["ransac_ms"], 1e-12)}}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, str(ROOT))
@@ -210,11 +297,22 @@ def _coll_device(dist):
     return "cuda" if dist.get_backend() == "nccl" else "cpu"
 
 
-def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, roofline=True):
-    """Warm up, time `steps` concurrent RBCD rounds (max over ranks), then (if
-    `roofline`) continue with HIP events around every k_hess launch. Returns
-    the team totals."""
+def _gather(dist, world, vals, ops):
+    """Combine per-rank scalars across ranks: ops[i] in {"max", "sum"}."""
+    if dist is None:
+        return vals
     import torch
+    t = torch.tensor(vals, dtype=torch.float64, device=_coll_device(dist))
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    a = torch.stack(parts).cpu().numpy()
+    return [float(a[:, i].max() if op == "max" else a[:, i].sum()) for i, op in enumerate(ops)]
+
+
+def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, replay=True, want_snapshot=False):
+    """Burn-in + warmup, snapshot, time `steps` rounds (max over ranks), then
+    replay the same rounds from the snapshot with HIP events around every
+    Hess-vec launch. Returns the team totals."""
     from kmx.dpgo.driver import RBCDDriver
     drv = RBCDDriver(P, g, rank=rank, world=world, device=local_rank if world > 1 else 0)
     drv.initialize(X0)
@@ -223,47 +321,48 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, roof
         drv.solver.sync()
         barrier()
 
-    drv.run_async(args.warmup)
-    sync()
-    drv.solver.read_counters()  # reset device counters and event pool
-    sync()
-    el, edges_iters = 0.0, 0.0
-    if not args.profile:  # --profile: every profiled k_hess dispatch is also in the roofline counters
+    hv_ms, hv_bytes, hv_n, same, snap = 0.0, 0.0, 0, None, None
+    if args.profile:  # every round evented and counted (the rocprofv3 / PMC passes divide by these)
+        drv.solver.read_counters()
+        drv.solver.enable_timing(True)
+        t0 = time.perf_counter()
+        drv.run_async(args.burn_in + args.warmup + steps)
+        sync()
+        el = time.perf_counter() - t0
+        c = drv.solver.read_counters()
+        hv_ms, hv_bytes, hv_n = c["hessvec_ms_total"], c["hessvec_alg_bytes"], c["hessvec_launches"]
+    else:
+        drv.run_async(args.burn_in + args.warmup)
+        sync()
+        snap = snapshot(drv) if (replay or want_snapshot) else None
+        drv.solver.read_counters()  # reset device counters and event pool
+        sync()
         t0 = time.perf_counter()
         drv.run_async(steps)
         sync()
         el = time.perf_counter() - t0
-        edges_iters = float(drv.solver.read_counters()["edges_iters"])
-    # roofline pass: the same rounds continued with HIP events around every
-    # k_hess launch (events add a few us per launch, so they stay out of `value`)
-    rsteps = steps if args.profile else (0 if (args.no_events or not roofline) else max(1, min(steps, 20)))
-    hv_ms, hv_bytes, hv_n = 0.0, 0.0, 0
-    if rsteps:
-        drv.solver.enable_timing(True)
-        t0 = time.perf_counter()
-        drv.run_async(rsteps)
+        c = drv.solver.read_counters()
+    if snap is not None and replay:
+        restore(drv, snap)
         sync()
-        if args.profile:
-            el = time.perf_counter() - t0
+        drv.solver.enable_timing(True)
+        drv.run_async(steps)
+        sync()
         drv.solver.enable_timing(False)
-        cnt = drv.solver.read_counters()
-        if args.profile:
-            edges_iters = float(cnt["edges_iters"])
-        hv_ms, hv_bytes, hv_n = cnt["hessvec_ms_total"], cnt["hessvec_alg_bytes"], cnt["hessvec_launches"]
+        r = drv.solver.read_counters()
+        hv_ms, hv_bytes, hv_n = r["hessvec_ms_total"], r["hessvec_alg_bytes"], r["hessvec_launches"]
+        same = all(r[k] == c[k] for k in ("edges_iters", "hessvecs", "block_updates", "gnc_updates"))
     xs, xr = drv.exchange_rows
-    if dist is not None:
-        t = torch.tensor([el, edges_iters, hv_ms, hv_bytes, float(hv_n), float(xs), float(xr)],
-                         dtype=torch.float64, device=_coll_device(dist))
-        parts = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(parts, t)
-        parts = torch.stack(parts).cpu().numpy()
-        el = float(parts[:, 0].max())
-        edges_iters = float(parts[:, 1].sum())
-        hv_ms, hv_bytes, hv_n = float(parts[:, 2].sum()), float(parts[:, 3].sum()), int(parts[:, 4].sum())
-        xs, xr = int(parts[:, 5].max()), int(parts[:, 6].max())
+    mem = drv.solver.memory()[0]
+    tot = _gather(dist, world, [el, float(c["edges_iters"]), float(c["hessvecs"]), float(c["block_updates"]),
+                                float(c["gnc_updates"]), hv_ms, hv_bytes, float(hv_n), float(xs), float(xr),
+                                float(mem), 1.0 if same in (None, True) else 0.0],
+                  ["max", "sum", "sum", "sum", "max", "sum", "sum", "sum", "max", "max", "max", "sum"])
     drv.solver.close()
-    return {"el": el, "edges_iters": edges_iters, "hv": (hv_ms, hv_bytes, hv_n), "rsteps": rsteps,
-            "xrows": (xs, xr)}
+    return {"el": tot[0], "edges_iters": tot[1], "hessvecs": tot[2], "block_updates": tot[3],
+            "gnc_updates": int(tot[4]), "hv": (tot[5], tot[6], int(tot[7])), "xrows": (int(tot[8]), int(tot[9])),
+            "mem_max": int(tot[10]), "replay_identical": (tot[11] == world) if replay and snap is not None else None,
+            "snap": snap}
 
 
 def main():
@@ -293,25 +392,32 @@ def main():
             torch.cuda.synchronize()
 
     P = params()
-    weak = args.scaling == "weak" and world > 1
+    headline = args.scaling if world > 1 else "strong"
     t_gen = time.perf_counter()
-    g, X0 = make_workload(args.config, world, args.scaling)
+    g, X0 = make_workload(args.config, world, headline)
     gen_s = time.perf_counter() - t_gen
-    leg = dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, args.steps, barrier)
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu and not args.profile
+    leg = dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, args.steps, barrier,
+                   replay=not args.no_replay and not args.profile, want_snapshot=want_cpu)
+    if args.profile:
+        args.steps += args.burn_in + args.warmup  # the profile run counts every round
     el, edges_iters = leg["el"], leg["edges_iters"]
     hv_ms, hv_bytes, hv_n = leg["hv"]
     value = edges_iters / el
     achieved = hv_bytes / (hv_ms * 1e-3) if hv_ms > 0 else 0.0
     traffic = load_traffic()
     ps_bytes = 8 * 4 * P.r
-    if weak:
+    w0 = args.burn_in + args.warmup
+    if headline == "weak" and world > 1:
         workload = (f"configs[3] shape per GPU (weak scaling): {g.n_total} poses / {g.m} edges, {g.n_robots} robot "
                     f"blocks over {world} GPUs ({g.n_robots // world} per GPU, 100k poses / 500k edges each), "
-                    "20% outlier LCs, f_inter 0.10, GNC-TLS every 20 rounds")
+                    "20% outlier LCs, f_inter 0.10, GNC-TLS (inner iterations 20)")
     else:
-        workload = (f"configs[3] {args.config}: {g.n_total} poses / {g.m} edges, {g.n_robots} robot blocks"
-                    + (f" split over {world} GPUs" if world > 1 else "")
-                    + ", 20% outlier LCs, f_inter 0.10, GNC-TLS every 20 rounds")
+        name = "configs[3] synth100k" if args.config == "synth100k" else f"{args.config} (cold config)"
+        workload = (f"{name}: {g.n_total} poses / {g.m} edges, {g.n_robots} robot blocks"
+                    + (f" split over {world} GPUs (strong scaling)" if world > 1 else "")
+                    + ", 20% outlier LCs, f_inter 0.10, GNC-TLS (inner iterations 20)")
+    nr = max(args.steps, 1)
     out = {
         "metric": "dpgo edges*iters/sec (+ LC candidates verified/sec in 'lcd')",
         "value": value,
@@ -319,9 +425,9 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * el / args.steps,
+        "ms_per_step": 1e3 * el / nr,
         "higher_is_better": True,
-        "scaling": args.scaling,
+        "scaling": headline,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded numpy PCG64; Campus bags unavailable offline)",
@@ -329,13 +435,26 @@ def main():
             "workload": workload,
             "robots": g.n_robots, "poses": g.n_total, "edges": g.m, "r": P.r,
             "rtr_iterations": 1, "tcg_max": 10, "schedule": "concurrent",
+            "timed_rounds": [w0, w0 + args.steps] if not args.profile else [0, args.steps],
+            "burn_in_rounds": 0 if args.profile else args.burn_in,
             "parallelism": f"robot blocks {g.n_robots} over {world} GPU(s)"
-                           + (", public poses by one RCCL all_to_all per round" if world > 1 else ""),
+                           + (", public poses + status by one RCCL all_to_all per round" if world > 1 else ""),
             "exchange_rows_per_round": {"sent_max": leg["xrows"][0], "recv_max": leg["xrows"][1],
                                         "recv_bytes_max": leg["xrows"][1] * ps_bytes},
             "graph_gen_s": round(gen_s, 1),
+            "device_bytes_per_gpu": leg["mem_max"],
         },
-        "roofline": {
+        "work": {
+            "hessvecs_per_round": leg["hessvecs"] / nr,
+            "hessvecs_per_block_update": leg["hessvecs"] / max(leg["block_updates"], 1),
+            "edges_hessvecs_per_s": None,
+            "gnc_updates_in_window": leg["gnc_updates"],
+        },
+    }
+    # edges x Hess-vecs: every Hess-vec of a block update touches its block's edges
+    out["work"]["edges_hessvecs_per_s"] = value * out["work"]["hessvecs_per_block_update"]
+    if hv_n:
+        out["roofline"] = {
             "kernel": "k_hess (tCG Hessian-vector product)",
             "bound": "hbm",
             "achieved": achieved / 1e9,
@@ -348,33 +467,46 @@ def main():
             "traffic": (traffic["traffic_over_alg"] * hv_bytes / max(hv_n, 1)) if traffic else None,
             "traffic_over_alg": traffic["traffic_over_alg"] if traffic else None,
             "launches": hv_n,
-            "measured_over": f"{leg['rsteps']} further rounds with HIP events around each k_hess launch",
+            "measured_over": (f"replay of the timed rounds {w0}..{w0 + args.steps} from their snapshot, HIP events "
+                              "around each k_hess launch that ran a Hess-vec") if not args.profile else
+                             f"rounds 0..{args.steps} (profile run), HIP events around each k_hess launch that ran "
+                             "a Hess-vec",
+            "replay_identical": leg["replay_identical"],
             "avg_launch_us": 1e3 * hv_ms / max(hv_n, 1),
+            "hess_ms_per_round": hv_ms / nr,
             "alg_bytes_per_launch": hv_bytes / max(hv_n, 1),
-        },
-    }
-    sst = args.steps if args.strong_steps is None else args.strong_steps
-    if weak and sst > 0 and not args.profile:
+            "alg_bytes_rule": "128 B per local edge + 2 x 160 B per pose of every robot in tCG (SURVEY.md §8d)",
+        }
+    xst = args.steps if args.extra_steps is None else args.extra_steps
+    if world > 1 and xst > 0 and not args.profile:
+        other = "weak" if headline == "strong" else "strong"
         del g, X0
-        gs, X0s = make_workload(args.config, 1, "strong")
-        st = dpgo_leg(gs, X0s, P, args, rank, world, local_rank, dist, sst, barrier, roofline=False)
-        out["strong"] = {"value": st["edges_iters"] / st["el"], "unit": "edges*iters/s", "steps": sst,
-                         "ms_per_step": 1e3 * st["el"] / sst,
-                         "workload": f"configs[3] {args.config}: {gs.n_total} poses / {gs.m} edges, "
-                                     f"{gs.n_robots} robot blocks split over {world} GPUs (strong scaling)",
-                         "exchange_rows_per_round": {"sent_max": st["xrows"][0], "recv_max": st["xrows"][1]}}
-        g, X0 = gs, X0s
-    if rank == 0 and world == 1 and not args.no_cpu and not args.profile:
-        out["cpu_baseline"] = cpu_baseline(g, X0, P, args.cpu_seconds)
+        go, X0o = make_workload(args.config, world, other)
+        st = dpgo_leg(go, X0o, P, args, rank, world, local_rank, dist, xst, barrier, replay=False)
+        out[other] = {"value": st["edges_iters"] / st["el"], "unit": "edges*iters/s", "steps": xst,
+                      "ms_per_step": 1e3 * st["el"] / max(xst, 1),
+                      "workload": f"{go.n_total} poses / {go.m} edges, {go.n_robots} robot blocks over {world} GPUs "
+                                  f"({other} scaling)",
+                      "exchange_rows_per_round": {"sent_max": st["xrows"][0], "recv_max": st["xrows"][1]}}
+        g, X0 = go, X0o
+    if want_cpu and leg["snap"] is not None:
+        lib, march = _native_oracle()
+        if lib:
+            os.environ["ORC_LIB"] = lib
+        cpu = cpu_baseline(g, P, leg["snap"], args.steps, args.cpu_seconds, (g.n_robots, 1))
+        team, one = cpu[g.n_robots], cpu[1]
+        out["cpu_baseline"] = {
+            "value": team["value"], "unit": "edges*iters/s", "cores": g.n_robots, "kind": "port",
+            "sample": f"rounds {w0}..{w0 + team['rounds']} of the timed window (the GPU's snapshot), "
+                      f"oracle/dpgo_oracle.c -O3 -march={march}, one OpenMP thread per robot block "
+                      f"({g.n_robots}), {team['seconds']:.1f} s",
+            "ms_per_step": team["ms_per_step"], "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "single_thread": {"value": one["value"], "cores": 1, "rounds": one["rounds"],
+                              "ms_per_step": one["ms_per_step"]},
+        }
     if not args.no_lcd and not args.profile:
         lcd, lcd_cpu = lcd_leg(args, rank, world, barrier)
-        n_local, lel = float(lcd["n_local"] * lcd["steps"]), lcd["elapsed"]
-        if dist is not None:
-            t = torch.tensor([n_local, lel], dtype=torch.float64, device=_coll_device(dist))
-            parts = [torch.zeros_like(t) for _ in range(world)]
-            dist.all_gather(parts, t)
-            parts = torch.stack(parts).cpu().numpy()
-            n_local, lel = float(parts[:, 0].sum()), float(parts[:, 1].max())
+        n_local, lel = _gather(dist, world, [float(lcd["n_local"] * lcd["steps"]), lcd["elapsed"]], ["sum", "max"])
         lcd["value"] = n_local / lel
         lcd["unit"] = "candidates/s"
         lcd["ms_per_step"] = 1e3 * lel / lcd["steps"]
@@ -382,13 +514,7 @@ def main():
         if lcd_cpu:
             lcd["cpu_baseline"] = lcd_cpu
         bow, bow_cpu = bow_leg(args, rank, world, barrier)
-        n_local, bel = float(bow["n_local"] * bow["steps"]), bow["elapsed"]
-        if dist is not None:
-            t = torch.tensor([n_local, bel], dtype=torch.float64, device=_coll_device(dist))
-            parts = [torch.zeros_like(t) for _ in range(world)]
-            dist.all_gather(parts, t)
-            parts = torch.stack(parts).cpu().numpy()
-            n_local, bel = float(parts[:, 0].sum()), float(parts[:, 1].max())
+        n_local, bel = _gather(dist, world, [float(bow["n_local"] * bow["steps"]), bow["elapsed"]], ["sum", "max"])
         bow["value"] = n_local / bel
         bow["unit"] = "queries/s"
         bow["ms_per_step"] = 1e3 * bel / bow["steps"]

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KMX_ABI_VERSION 1
+#define KMX_ABI_VERSION 2
 
 /* error codes */
 #define KMX_OK 0
@@ -158,6 +158,18 @@ int kmx_pgo_refresh_local(kmx_pgo* h);
  * link; refresh_local fills the owned slots. */
 int kmx_pgo_gather_public_rows(kmx_pgo* h, const int32_t* dev_slots, int64_t n, void* dev_out);
 int kmx_pgo_scatter_public_rows(kmx_pgo* h, const int32_t* dev_slots, int64_t n, const void* dev_rows);
+/* The same exchange with the team status piggy-backed (dpgo Status message,
+ * drawio:2375, used by shouldUpdateMeasurementWeights' "all agents converged"):
+ * the rows are cut into n_seg per-peer segments, segment k = rows
+ * [seg[k], seg[k+1]) (dev_seg: n_seg + 1 int32, device), and each segment is
+ * followed by ONE double, so segment k starts at double seg[k]*4r + k. pack
+ * writes this handle's largest relative change (of its robots' last block
+ * updates) after every segment; unpack installs the rows and keeps the n_seg
+ * received status values for the next round-begin GNC decision. */
+int kmx_pgo_exchange_pack(kmx_pgo* h, const int32_t* dev_slots, int64_t n, const int32_t* dev_seg,
+                          int n_seg, void* dev_out);
+int kmx_pgo_exchange_unpack(kmx_pgo* h, const int32_t* dev_slots, int64_t n, const int32_t* dev_seg,
+                            int n_seg, const void* dev_in);
 int kmx_pgo_set_neighbor_poses(kmx_pgo* h, int64_t count, const int32_t* robot,
                                const int32_t* pose, const double* X);
 
@@ -168,19 +180,45 @@ int kmx_pgo_set_neighbor_poses(kmx_pgo* h, int64_t count, const int32_t* robot,
 int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats* stats);
 /* Enqueue `rounds` concurrent rounds (all local robots active) without any
  * host synchronisation; used by the benchmark. stats are not produced. When
- * refresh_local != 0 every round starts with kmx_pgo_refresh_local (the
- * single-device public-pose exchange); otherwise the caller exchanges. When
- * gnc_every > 0, a GNC weight update runs after every gnc_every-th round
- * (counted across calls), as dpgo_ros does on UPDATE_WEIGHT. */
-int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local,
-                          int gnc_every);
+ * refresh_local != 0 the owned public rows are published before the first
+ * round (every round republishes the rows it commits): the single-device
+ * exchange; otherwise the caller exchanges between rounds. */
+int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local);
 /* Wait for all work enqueued on the handle's stream. */
 int kmx_pgo_sync(kmx_pgo* h);
 
-/* GNC: `updateMeasurementWeights()` (drawio:2215) for every non-fixed edge owned
- * by a local robot, evaluated at the current iterate and neighbour table, then
- * mu <- mu * mu_step. mu_out (may be NULL) gets the mu used. */
+/* GNC: `updateMeasurementWeights()` (drawio:2215) for every non-fixed edge with
+ * a local endpoint, evaluated at the current iterate and neighbour table, then
+ * mu <- mu * mu_step, inner iterations <- 0, updates += 1. mu_out (may be
+ * NULL) gets the mu used. A shared loop closure is evaluated identically on
+ * the handles of both its robots (same two rows), which yields the owner's
+ * weight on both sides (publishMeasurementWeights, drawio:2195-2198). */
 int kmx_pgo_update_weights(kmx_pgo* h, double* mu_out);
+/* GNC schedule run on the device at the start of every round (iterate and
+ * iterate_async) when enabled: shouldUpdateMeasurementWeights
+ * (drawio:2466-2469) = GNC_TLS cost, fewer than max_updates updates so far,
+ * and (more than inner_iters rounds since the last update, or every agent of
+ * the team converged: relative change of its last block update <=
+ * rel_change_tol, this handle's robots and the statuses received by
+ * kmx_pgo_exchange_unpack). Disabled by default (the agent API decides on the
+ * host and calls kmx_pgo_update_weights). */
+typedef struct kmx_gnc_state {
+  int32_t inner_iter;  /* rounds since the last weight update (dpgo mRobustOptInnerIter) */
+  int32_t updates;     /* weight updates so far                                         */
+  int32_t last_fired;  /* the last round began with a weight update                      */
+  int32_t rounds;      /* rounds completed                                               */
+  double mu;           /* GNC mu of the next update                                      */
+  double reserved[3];
+} kmx_gnc_state;
+int kmx_pgo_set_gnc_schedule(kmx_pgo* h, int enabled, int inner_iters, int max_updates,
+                             double rel_change_tol);
+int kmx_pgo_get_gnc_state(kmx_pgo* h, kmx_gnc_state* out);
+int kmx_pgo_set_gnc_state(kmx_pgo* h, const kmx_gnc_state* in);
+/* Per-robot relative change of the last block update (dpgo Status
+ * relativeChange, drawio:2375; +inf before the first update): n_robots
+ * doubles, local robots written/read only. */
+int kmx_pgo_get_status(kmx_pgo* h, double* rel_change);
+int kmx_pgo_set_status(kmx_pgo* h, const double* rel_change);
 int kmx_pgo_get_mu(kmx_pgo* h, double* mu);
 int kmx_pgo_set_mu(kmx_pgo* h, double mu);
 /* `setMeasurementWeight` (drawio:2268) in bulk: weights indexed by global edge
@@ -218,6 +256,10 @@ int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, double* out,
 
 /* Edges in robot `robot`'s local problem (private + shared incident edges). */
 int kmx_pgo_local_edges(kmx_pgo* h, int robot, int64_t* m_local);
+/* Resident device bytes of the handle and the bytes of one incidence record
+ * (96: compact, rotation row 2 rebuilt as row0 x row1; 128: full rotation,
+ * when some measurement rotation is not in SO(3) to 1e-12). */
+int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_bytes);
 /* Live instrumentation of the dominant kernel (the Hessian-vector product of
  * the tCG loop). When enabled, every Hessian-vector launch enqueued by
  * kmx_pgo_iterate / kmx_pgo_iterate_async is bracketed by a HIP event pair on
@@ -232,6 +274,7 @@ typedef struct kmx_pgo_counters {
   int64_t edges_iters;         /* sum over executed block updates of m_alpha    */
   int64_t block_updates;       /* executed block updates (tCG ran)              */
   int64_t hessvecs;            /* robot-level Hessian-vector products           */
+  int64_t gnc_updates;         /* GNC weight updates run                        */
 } kmx_pgo_counters;
 int kmx_pgo_enable_timing(kmx_pgo* h, int enable);
 int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out);
@@ -320,6 +363,11 @@ int kmx_lcd_verify(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
 int kmx_lcd_verify_async(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
                          const int32_t* cand_match);
 int kmx_lcd_sync(kmx_lcd* h);
+/* Instrumentation: when enabled, every verification brackets its kNN2 launch
+ * and its RANSAC launches with HIP events; read_timing synchronises and
+ * returns the device times (ms) of the last evented verification. */
+int kmx_lcd_enable_timing(kmx_lcd* h, int enable);
+int kmx_lcd_read_timing(kmx_lcd* h, double* knn_ms, double* ransac_ms);
 
 
 /* ------------------------------------------------------------------------- */

@@ -1983,6 +1983,10 @@ struct kmx_lcd {
   double* d_fbuf = nullptr;  // [cap][2][N][3] compact match bearings (k_ransac_coop)
   int ransac = 1;            // KMX_RANSAC: 1 cooperative (default), 0 lane-per-hypothesis
   int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
+  // kmx_lcd_enable_timing: events around the kNN2 and the RANSAC launches
+  bool timing = false;
+  bool ev_ok = false;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -2052,9 +2056,17 @@ size_t ransac_smem(int N) { return sizeof(double) * (6 * (size_t)N + 64 * 12 + 1
 int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   if (n == 0) return 0;
   const size_t knn_smem = (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1);
+  if (h->timing) {
+    if (!h->ev_ok) {
+      for (auto& e : h->ev) KMX_HIP(hipEventCreate(&e));
+      h->ev_ok = true;
+    }
+    KMX_HIP(hipEventRecord(h->ev[0], h->stream));
+  }
   hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), knn_smem, h->stream, (const uint32_t*)h->d_desc,
                      (const int*)h->d_nfeat, h->N, (const int*)h->d_cq, (const int*)h->d_cm, h->P.norm,
                      h->P.lowe_ratio, h->d_pairs, h->d_K);
+  if (h->timing) KMX_HIP(hipEventRecord(h->ev[1], h->stream));
   RsParams rp;
   rp.thr2d = h->P.ransac_threshold_2d2d;
   rp.thr3d = h->P.ransac_threshold_3d3d;
@@ -2105,6 +2117,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
                        (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table6, pp, h->d_res,
                        h->d_mask);
   }
+  if (h->timing) KMX_HIP(hipEventRecord(h->ev[2], h->stream));
   KMX_HIP(hipGetLastError());
   return 0;
 }
@@ -2145,6 +2158,8 @@ extern "C" int kmx_lcd_destroy(kmx_lcd* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   lcd_free_pool(h);
   lcd_free_cand(h);
+  if (h->ev_ok)
+    for (auto e : h->ev) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return KMX_OK;
@@ -2237,6 +2252,25 @@ extern "C" int kmx_lcd_verify_async(kmx_lcd* h, int32_t n, const int32_t* cq, co
   KMX_HIP(hipStreamSynchronize(h->stream));  // host arrays may go away after return
   return enqueue_verify(h, n, false);
   KMX_GUARD_END
+}
+
+extern "C" int kmx_lcd_enable_timing(kmx_lcd* h, int enable) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  h->timing = enable != 0;
+  return KMX_OK;
+}
+
+extern "C" int kmx_lcd_read_timing(kmx_lcd* h, double* knn_ms, double* ransac_ms) {
+  KMX_CHECK(h && knn_ms && ransac_ms, KMX_EINVAL, "null argument");
+  KMX_CHECK(h->ev_ok, KMX_ESTATE, "no evented verification yet (kmx_lcd_enable_timing)");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  float a = 0.f, b = 0.f;
+  KMX_HIP(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
+  KMX_HIP(hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
+  *knn_ms = a;
+  *ransac_ms = b;
+  return KMX_OK;
 }
 
 extern "C" int kmx_lcd_sync(kmx_lcd* h) {

@@ -1,25 +1,33 @@
 // pgo.hip — MI355X (gfx950) RBCD block updates on lifted SE(3) with GNC-TLS.
 //
 // Replaces dpgo's PGOAgent::iterate / updateMeasurementWeights hot path
-// (drawio:2058-2066, 2215, 2513). Design:
-//   * Every local robot block lives in HBM; all blocks are updated by the same
-//     launches (batched RBCD). Workgroup tiles never straddle robots, so every
-//     reduction is per robot and its control scalars (trust radius, tCG alpha /
-//     beta, ...) live on the device in a Ctl record per robot. The host never
-//     reads a scalar inside a round: the tCG loop is a fixed launch sequence and
-//     finished robots' tiles exit at their first instruction.
-//   * Thread <-> (pose, row): the Euclidean Hessian-vector product X -> XQ acts
-//     on each of the r rows of a pose independently, so a lane owns one row
-//     (4 doubles) of one pose and a pose is a group of r lanes of one wave.
-//     Only the Stiefel projection / retraction need sums over the r rows, done
-//     with in-group shuffles in a fixed order.
-//   * Node-centric gather over a CSR incidence list (no atomics): every output
-//     element accumulates its incident edges in increasing edge id, the same
-//     order as the CPU restatement's edge loop (FMA contraction on: per-element
-//     results agree with the oracle to ~1e-15; `make FPC=off` reproduces its
-//     roundings).
-//   * Reductions: one partial per workgroup tile, reduced in fixed order by a
-//     one-workgroup control kernel that also runs the RTR / tCG scalar logic.
+// (drawio:2058-2066, 2215, 2466-2469, 2513).
+// Design:
+//   * Every local robot block lives in HBM and all blocks are updated by the
+//     same launches (batched RBCD). Workgroup tiles never straddle robots, so
+//     every reduction is per robot and its RTR / tCG scalars live on the device
+//     in one Ctl record per robot.
+//   * No scalar reaches the host inside a round, and no reduction has a launch
+//     of its own: each tile publishes its partial sums and takes a ticket on its
+//     robot's counter; the tile that draws the last ticket reduces the robot's
+//     partials in tile order (deterministic) and runs the control logic. The
+//     tCG loop is a fixed launch sequence of tcg_max (Hess-vec, update) pairs;
+//     a robot whose tCG has stopped exits at its first instruction, so the host
+//     never waits on the device (no polling).
+//   * Edge data: one 96-B compact record per incidence in CSR order (R rows
+//     0-1, t, w kappa, w tau, {other, edge | tail << 31}; row 2 = row0 x row1 for
+//     measurements in SO(3)), or a 128-B record with the full rotation when some
+//     measurement is not a rotation to 1e-12. The gathers are incidence-parallel:
+//     one lane per incidence evaluates its block against the neighbour's whole
+//     r x 4 row and parks the r contribution rows in LDS; the (pose, row) lanes
+//     then add their pose's contributions in CSR (= increasing edge id) order.
+//     No atomics: every sum has a fixed order, so results are deterministic and
+//     independent of rank placement.
+//   * GNC-TLS on the device: the round-begin launch decides
+//     shouldUpdateMeasurementWeights (drawio:2466-2469: inner iterations >
+//     robustOptInnerIters, or every agent converged; capped at
+//     robustOptNumWeightUpdates) from device state and re-weights the loop
+//     closures in the same launch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,7 +35,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <map>
+#include <limits>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -37,11 +45,6 @@
 namespace {
 
 constexpr int WAVES = 4;
-// Minimum waves per SIMD for the gather kernels (k_grad / k_hess / k_cost):
-// caps their VGPRs so enough waves are resident to hide the gather latency.
-#ifndef KMX_LB_GATHER
-#define KMX_LB_GATHER 5
-#endif
 constexpr int BLOCK = 64 * WAVES;
 constexpr int NPART = 4;  // partial sums per tile
 // per-kernel LDS reduction area: NPART x WAVES wave sums + the ticket flag
@@ -59,33 +62,52 @@ struct Ctl {
   double f_final, norm_r0, z_r, e_Pe;
   double e_Pd, d_Pd, alpha, beta;
   double coef, rho, chg_acc, rel_change;
+  double pad2[10];  // 256 B: one robot's record never shares a line with the next
 };
+static_assert(sizeof(Ctl) == 256, "Ctl is 256 B");
 
 struct Counters {
   unsigned long long edges_iters;
   unsigned long long block_updates;
   unsigned long long hessvecs;
-  unsigned long long pad;
+  unsigned long long gnc_updates;
   double hess_alg_bytes;
   double pad2[3];
 };
 
-// Host-visible progress of one robot after a tCG step, written by the robot's
-// k_reduce(RED_UPDATE) workgroup into host-mapped memory as ONE 64-bit word
-// (seq << 1 | still-in-tCG): a single relaxed system-scope store needs no
-// release fence, so no L2 writeback is forced. The host enqueues further tCG
-// steps only while a robot is in tCG.
+// GNC schedule state (dpgo PGOAgent: mRobustOptInnerIter, mWeightUpdateCount, mu).
+struct Gnc {
+  int inner;    // rounds since the last weight update
+  int updates;  // weight updates so far
+  int fired;    // the last round-begin launch updated the weights
+  int rounds;   // rounds completed
+  double mu;
+  double pad[3];
+};
+
+// Host-visible tCG progress of one robot, written after every tCG step by the
+// last-arriving tile of the robot's k_update (or its first tile when it is
+// not in tCG) into host-mapped memory as ONE 64-bit word (seq << 1 |
+// still-in-tCG): a single relaxed system-scope store, no release fence, so no
+// L2 writeback. The host keeps one tCG step queued beyond the last one known
+// to be needed and stops enqueueing once no robot is in tCG.
 struct HostStatus {
   unsigned long long word;
 };
 __device__ __forceinline__ void post_status(HostStatus* hs, int l, unsigned long long seq, bool running) {
-  __hip_atomic_store(&hs[l].word, (seq << 1) | (running ? 1ull : 0ull), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&hs[l].word, (seq << 1) | (running ? 1ull : 0ull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Per-launch instrumentation passed to the tCG kernels.
+struct Post {
+  HostStatus* hs = nullptr;     // k_update: progress words (nullptr: no polling)
+  unsigned long long seq = 0;
+  int slot = -1;                // k_hess with timing on: event-pair index
+};
 
 struct Params {
   int tcg_max, rtr_iters, use_precond, robust;
-  double kappa, theta, Delta0, Delta_max, accept_rho, gn_tol, shift, barc;
+  double kappa, theta, Delta0, Delta_max, accept_rho, gn_tol, shift, barc, mu_step, rel_tol;
+  int gnc_on, inner_iters, max_updates, n_ext;
 };
 
 struct Dev {
@@ -93,41 +115,36 @@ struct Dev {
   const int* tile_robot;
   const int* tile_p0;
   const int* tile_np;
-  const int* rtile0;  // [L+1]
-  const int* inc_ptr; // [nloc+1]
-  const int2* inc;    // x = other (>=0 local pose, <0 -> public slot -1-x); y = edge | tail<<31
-  double* irec;       // [ninc][16] per-incidence edge record in CSR order: R(9) t(3) w*kappa w*tau 0 0
-  double* crec;       // [ninc][12] compact record (gather variant 3): R rows 0-1 (6) t(3) w*kappa w*tau
-                      // {other, edge|tail<<31} — R row 2 = row 0 x row 1 (used only when every
-                      // local measurement rotation satisfies that to 1e-12; see kmx_pgo_set_graph)
-  double* ocrec;      // [m_own][12] compact records of the owner incidences only (each local edge
-                      // once: the tail of a local-local edge, the local end of a shared one), CSR by pose
-  const int* optr;    // [nloc+1] CSR pointers into ocrec
-  const int2* eopos;  // [mloc] positions of each local edge in ocrec (a shared edge with both
-                      // robots on this handle has two owner incidences; -1 = none)
-  double* ekappa;     // [mloc] per local edge
+  const int* rtile0;   // [L+1]
+  const int* inc_ptr;  // [nloc+1]
+  double* rec;         // [ninc + 1][RW] incidence records in CSR order (+ one zero pad record)
+  double* ekappa;      // [mloc] per local edge
   double* etau;
-  double* ew;         // GNC weight
-  const int2* eipos;  // [mloc] incidence positions (tail, head) of each local edge, -1 if not local
-  const int2* cipos;  // [mloc] the same positions in crec (differs from eipos in the segment-major layout)
-  const int* trec0;   // [ntiles] segment-major layout (rect): first crec record of each tile
-  const int* torec0;  // [ntiles] ... and of ocrec
-  int rect;           // crec / ocrec in segment-major order (gather G = 5/6 only)
-  double* hrec;       // [ninc + 1][12] compact records in CSR order for the G = 9 Hessian gather
-                      // (+ one zero pad record), null when that gather is off
-  double* hD;         // [nloc][16] diagonal blocks of Q per pose (G = 9), written by k_precond
-  double* hocrec;     // [m_own + 1][12] owner compact records in CSR order (G = 9 k_cost) + pad
-  const int2* heopos; // [mloc] positions of each local edge in hocrec
-  int dbg;            // diagnostic ablations (KMX_PGO_DBG; 0 in the product path)
-  double *X, *Xt, *g, *r, *z, *eta, *del, *hd, *S, *Pinv, *pub;
-  double* part;       // [ntiles][NPART]
+  double* ew;          // GNC weight
+  const int2* eipos;   // [mloc] record positions (tail, head) of each local edge, -1 if not local
+  double *X, *Xt, *g, *r, *z, *eta, *del, *hd, *S, *Pinv, *hD, *pub;
+  double* part;        // [ntiles][NPART]
   Ctl* ctl;
   Counters* cnt;
-  unsigned* tickets;         // [L] per-robot arrival counters (zero between launches)
-  const long long* m_robot;  // [L] local-problem edges per robot
-  const int* n_robot;        // [L] poses per robot
+  unsigned* tickets;          // [L] per-robot arrival counters (zero between launches)
+  const long long* m_robot;   // [L] local-problem edges per robot
+  const int* n_robot;         // [L] poses per robot
+  const int* pose_slot;       // [nloc] owned public-table slot of a pose, or -1
+  double* relc;               // [L] relative change of each robot's last block update (inf: none yet)
+  Gnc* gnc;                   // schedule state
+  Gnc* gnc_next;              // state after the current round-begin launch (k_precond commits it)
+  const double* ext;          // [n_ext] peers' largest relative change (multi-process team status)
+  const int* gnc_edge;        // [n_gnc] local edges re-weighted here (non-fixed, >= 1 local endpoint)
+  const int2* gnc_ends;       // [n_gnc] endpoints: >= 0 local pose, < 0 public slot -1-x
+  int n_gnc;
+  int* hv_launch;             // [HV_SLOTS] robots that ran a Hess-vec in timed launch k
+  const int* rgroup0;         // [L+1] first ticket group of each robot (GS tiles per group)
+  unsigned* gtickets;         // [groups] group arrival counters (zero between launches)
+  double* gpart;              // [groups][NPART] group partial sums
   Params p;
 };
+constexpr int GS = 16;  // tiles per ticket group
+constexpr int HV_SLOTS = 1 << 16;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -168,13 +185,58 @@ __device__ __forceinline__ void store4(double* p, const double v[4]) {
   q[1] = make_double2(v[2], v[3]);
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops but
+// not for its outstanding global loads (__syncthreads waits vmcnt(0), which
+// would drain the next chunk's prefetched records).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ------------------------------------------------------------ edge records --
 struct Edge {
   double R[9], t[3], wk, wt;
 };
-// Accumulate the contribution of one incidence to row a of pose `self`.
-// vs = self row, vo = other endpoint row (zeros for a Hessian product across a
-// shared edge). Expressions mirror oracle/dpgo_oracle.c edge_eval exactly.
-// Returns the row's share of 1/2 w (kappa |E_R|^2 + tau E_t^2).
+
+__device__ __forceinline__ int2 unpack_int2(double v) {
+  const long long b = __double_as_longlong(v);
+  return make_int2((int)(b & 0xffffffffll), (int)(b >> 32));
+}
+
+// RW = 12: compact record (R rows 0-1, t, w kappa, w tau, {other, edge|tail});
+// RW = 16: full record (R, t, w kappa, w tau, {other, edge|tail}, pad).
+template <int RW>
+struct Rec {
+  static constexpr int Q = RW / 2;        // 16-B parts
+  static constexpr int WK = RW == 12 ? 9 : 12;  // index of w kappa (w tau follows)
+  __device__ static __forceinline__ void load(const double* base, size_t k, double2 q[Q]) {
+    const double2* q2 = reinterpret_cast<const double2*>(base + (size_t)RW * k);
+#pragma unroll
+    for (int i = 0; i < Q; ++i) q[i] = q2[i];
+  }
+  __device__ static __forceinline__ void edge(const double2 q[Q], Edge& E) {
+    if constexpr (RW == 12) {
+      E.R[0] = q[0].x; E.R[1] = q[0].y; E.R[2] = q[1].x;
+      E.R[3] = q[1].y; E.R[4] = q[2].x; E.R[5] = q[2].y;
+      E.R[6] = E.R[1] * E.R[5] - E.R[2] * E.R[4];
+      E.R[7] = E.R[2] * E.R[3] - E.R[0] * E.R[5];
+      E.R[8] = E.R[0] * E.R[4] - E.R[1] * E.R[3];
+      E.t[0] = q[3].x; E.t[1] = q[3].y; E.t[2] = q[4].x;
+      E.wk = q[4].y;
+      E.wt = q[5].x;
+    } else {
+      E.R[0] = q[0].x; E.R[1] = q[0].y; E.R[2] = q[1].x; E.R[3] = q[1].y; E.R[4] = q[2].x;
+      E.R[5] = q[2].y; E.R[6] = q[3].x; E.R[7] = q[3].y; E.R[8] = q[4].x;
+      E.t[0] = q[4].y; E.t[1] = q[5].x; E.t[2] = q[5].y;
+      E.wk = q[6].x;
+      E.wt = q[6].y;
+    }
+  }
+  __device__ static __forceinline__ int2 inc(const double2 q[Q]) {
+    return unpack_int2(RW == 12 ? q[5].y : q[7].x);
+  }
+};
+
+// Contribution of one incidence to row a of pose `self`. vs = self row, vo =
+// other endpoint row. Expressions mirror oracle/dpgo_oracle.c edge_eval
+// exactly. Returns the row's share of 1/2 w (kappa |E_R|^2 + tau E_t^2).
 __device__ __forceinline__ double incidence_row(const Edge& E, bool self_tail, const double vs[4],
                                                 const double vo[4], double acc[4]) {
   double ER[3], Et;
@@ -201,17 +263,14 @@ __device__ __forceinline__ double incidence_row(const Edge& E, bool self_tail, c
   return 0.5 * (E.wk * (ER[0] * ER[0] + ER[1] * ER[1] + ER[2] * ER[2]) + E.wt * Et * Et);
 }
 
-// S = sym(Y^T G_Y) for the pose group (9 entries, identical in all R lanes):
-// the 6 distinct entries are group sums of the symmetrised products. Each sum
-// is chained to the previous one (empty asm) so only one sum's R shuffles are
-// in flight: interleaving all of them held ~90 VGPRs and capped k_hess at 3
-// waves/SIMD.
-//
-// LDS = true (kernels that own a free BLOCK x 6-double LDS scratch `scr`): every
+// ------------------------------------------------------ Stiefel group ops --
+// S = sym(Y^T G_Y) for the pose group (9 entries, identical in all R lanes).
+// LDS = true (kernels with a free BLOCK x 6-double LDS scratch `scr`): every
 // lane writes its 6 products, then reads its group's R x 6 back and adds them
-// in the same lane order, so the 6 sums cost one LDS round trip instead of 6
-// chained shuffle chains. Only lanes of one wave exchange data (in-order LDS
-// queue; no workgroup barrier).
+// in lane order: one LDS round trip instead of 6 chained shuffle chains. Only
+// lanes of one wave exchange data (in-order LDS queue; no workgroup barrier).
+// LDS = false: 6 shuffle sums, each chained to the previous one (empty asm) so
+// only one sum's R shuffles are in flight (VGPR pressure).
 template <int R, bool LDS = false>
 __device__ __forceinline__ void group_symYtG(const double y[4], const double G[4], int base, double S[9],
                                              double* scr = nullptr) {
@@ -268,38 +327,36 @@ __device__ __forceinline__ void group_proj(const double y[4], const double V[4],
   out[3] = V[3];
 }
 
+// Preconditioner: P_Y(V Pinv_i) (block-Jacobi on Q's 4x4 diagonal blocks).
 template <int R, bool LDS = false>
 __device__ __forceinline__ void group_precon(const Dev& d, int pose, bool valid, const double y[4],
                                              const double V[4], int base, double out[4], double* scr = nullptr) {
-  double buf[4] = {0.0, 0.0, 0.0, 0.0};
-  if (d.p.use_precond) {
-    const double* Pp = d.Pinv + 16 * (size_t)pose;
-    if constexpr (LDS) {
-      // the 128-VGPR kernels: all of P in flight at once (pose is a valid
-      // index on every lane: lane_map clamps idle lanes to the tile's first pose)
-      double P[16];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) load4(Pp + 4 * i, P + 4 * i);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * P[k] : buf[k] + V[i] * P[4 * i + k];
-    } else {
-      // buf = V P, one 4-double row of P at a time (keeps 8 VGPRs of P live)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        double Pr[4] = {0.0, 0.0, 0.0, 0.0};
-        if (valid) load4(Pp + 4 * i, Pr);
-        asm volatile("" : "+v"(Pr[0]), "+v"(Pr[1]), "+v"(Pr[2]), "+v"(Pr[3]) : "v"(buf[0]));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * Pr[k] : buf[k] + V[i] * Pr[k];
-      }
-    }
-    group_proj<R, LDS>(y, buf, base, out, scr);
-  } else {
+  if (!d.p.use_precond) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) out[k] = V[k];
+    return;
   }
+  double buf[4] = {0.0, 0.0, 0.0, 0.0};
+  const double* Pp = d.Pinv + 16 * (size_t)pose;
+  if constexpr (LDS) {  // 128-VGPR kernels: all of P in flight (pose is valid on every lane)
+    double P[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) load4(Pp + 4 * i, P + 4 * i);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * P[k] : buf[k] + V[i] * P[4 * i + k];
+  } else {  // one 4-double row of P at a time (8 VGPRs of P live)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double Pr[4] = {0.0, 0.0, 0.0, 0.0};
+      if (valid) load4(Pp + 4 * i, Pr);
+      asm volatile("" : "+v"(Pr[0]), "+v"(Pr[1]), "+v"(Pr[2]), "+v"(Pr[3]) : "v"(buf[0]));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * Pr[k] : buf[k] + V[i] * Pr[k];
+    }
+  }
+  group_proj<R, LDS>(y, buf, base, out, scr);
 }
 
 // Riemannian Hessian row of V given the Euclidean Hessian row H:
@@ -335,6 +392,7 @@ __device__ __forceinline__ void group_retract(const double x[4], const double v[
   out[3] = x[3] + v[3];
 }
 
+// ------------------------------------------------------------- lane map ----
 struct Lane {
   int tile, l, w, ln, pw, a, base, pose;
   bool valid;
@@ -345,8 +403,7 @@ __device__ __forceinline__ Lane lane_map(const Dev& d) {
   Lane L;
   // XCD-aware, bijective block -> tile remap (cdna_hip_programming.md T1):
   // blocks b and b + 8 share an XCD, so each XCD gets one contiguous range of
-  // tiles — i.e. (about) one robot block, whose iterate then stays in that
-  // XCD's 4 MiB L2 across the gathers of every kernel of the round.
+  // tiles — about one robot block, whose rows then stay in that XCD's L2.
   {
     const int nwg = gridDim.x, b = blockIdx.x;
     const int q = nwg >> 3, rr = nwg & 7, x = b & 7;
@@ -365,628 +422,54 @@ __device__ __forceinline__ Lane lane_map(const Dev& d) {
   return L;
 }
 
-// ---------------------------------------------------------------- kernels --
-// Direct variant (G = 0): each (pose, row) lane walks its pose's incidences
-// with per-lane global loads (every lane of the pose loads the edge record).
-struct EdgeRaw {
-  double2 q[8];
-};
-__device__ __forceinline__ void edge_from_raw(const EdgeRaw& w, Edge& E) {
-  E.R[0] = w.q[0].x; E.R[1] = w.q[0].y; E.R[2] = w.q[1].x; E.R[3] = w.q[1].y; E.R[4] = w.q[2].x;
-  E.R[5] = w.q[2].y; E.R[6] = w.q[3].x; E.R[7] = w.q[3].y; E.R[8] = w.q[4].x;
-  E.t[0] = w.q[4].y; E.t[1] = w.q[5].x; E.t[2] = w.q[5].y;
-  E.wk = w.q[6].x;
-  E.wt = w.q[6].y;
-}
-
-template <int R, bool PUB>
-__device__ __forceinline__ void fetch_incidence(const Dev& d, const double* V, const double* pub, int a, int k,
-                                                int2 in, EdgeRaw& w, double2& v0, double2& v1) {
-  const double2* q2 = reinterpret_cast<const double2*>(d.irec + 16 * (size_t)k);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w.q[i] = q2[i];
-  const int o = in.x;
-  const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V);
-  const double2* b2 = reinterpret_cast<const double2*>(base + 4 * a);
-  v0 = b2[0];
-  v1 = b2[1];
-  if (!PUB && o < 0) v0 = v1 = make_double2(0.0, 0.0);
-}
-
-// Direct variant (G = 0): each (pose, row) lane walks its pose's incidences in
-// CSR order, software-pipelined: incidence k+1's edge record and neighbour row
-// are in flight while k is computed, and the CSR entry of k+2 while k+1 loads.
-template <int R, bool PUB>
-__device__ __forceinline__ void lane_gather(const Dev& d, const Lane& L, const double* V, const double* pub,
-                                            double acc[4], double* cost) {
-  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  if (!L.valid) return;
-  double vs[4];
-  load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
-  const int k0 = d.inc_ptr[L.pose], k1 = d.inc_ptr[L.pose + 1];
-  if (k0 >= k1) return;
-  int2 inA = d.inc[k0];
-  int2 inB = (k0 + 1 < k1) ? d.inc[k0 + 1] : inA;
-  EdgeRaw wA, wB;
-  double2 a0, a1, b0, b1;
-  fetch_incidence<R, PUB>(d, V, pub, L.a, k0, inA, wA, a0, a1);
-  for (int k = k0; k < k1; ++k) {
-    const bool more = (k + 1 < k1);
-    if (more) fetch_incidence<R, PUB>(d, V, pub, L.a, k + 1, inB, wB, b0, b1);
-    const int2 inC = (k + 2 < k1) ? d.inc[k + 2] : inB;
-    Edge E;
-    edge_from_raw(wA, E);
-    const double vo[4] = {a0.x, a0.y, a1.x, a1.y};
-    const bool tail = (inA.y >> 31) & 1;
-    const double c = incidence_row(E, tail, vs, vo, acc);
-    if (cost) *cost += (inA.x >= 0) ? 0.5 * c : c;
-    wA = wB;
-    a0 = b0;
-    a1 = b1;
-    inA = inB;
-    inB = inC;
-  }
-}
-
-// Incidence-parallel tile gather (variant G = 1). A tile's poses are
-// contiguous, so its incidences are one contiguous CSR range. The tile walks
-// it in chunks of CI = 256 / r incidences:
-//   * the tile's CSR entries and its own pose rows are staged in LDS once;
-//   * per chunk, every edge record is loaded ONCE (8 lanes x 16 B) into LDS,
-//     and lane (incidence i, row a) loads neighbour row a straight into
-//     registers (r lanes read one contiguous 32r-byte pose row);
-//   * lane (i, a) forms its incidence's contribution to row a of the self pose
-//     and parks it in LDS; then each (pose, row) lane adds its pose's
-//     contributions in CSR (= increasing edge id) order — the same order and
-//     the same (exactly negated) terms as the oracle, so results stay bitwise
-//     identical;
-//   * the next chunk's loads are issued before the current chunk is computed.
+// --------------------------------------------------------------- gathers ---
+// LDS layouts. A tile holds TP = WAVES * (64 / R) poses; its incidences are one
+// contiguous CSR range walked in chunks of CH incidences (one lane each).
 template <int R>
-struct Smem {
-  static constexpr int PPW = 64 / R;
-  static constexpr int TP = WAVES * PPW;           // poses per tile
-  static constexpr int CI = BLOCK / R;             // incidences per chunk
-  static constexpr int MAXI = 512;                 // CSR entries staged per segment
-  static constexpr int inc_off = 0;                                   // int2[MAXI]
-  static constexpr int ptr_off = inc_off + MAXI * 8;                  // int[TP + 1]
-  static constexpr int x_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;  // double[TP][R][4]
-  static constexpr int edge_off = x_off + TP * R * 32;                // double[CI][16]
-  static constexpr int con_off = edge_off + CI * 128;                 // double[CI][R][4]
-  static constexpr int red_off = con_off + CI * R * 32;               // double[WAVES] + flag
-  static constexpr int bytes = red_off + RED_BYTES;
-};
-
-template <int R, bool PUB>
-__device__ __forceinline__ void tile_gather(const Dev& d, const Lane& L, const double* V, const double* pub,
-                                            double acc[4], double* cost, char* smem) {
-  using SM = Smem<R>;
-  constexpr int CI = SM::CI;
-  constexpr int E_IT = (CI * 8 + BLOCK - 1) / BLOCK;
-  int2* sinc = reinterpret_cast<int2*>(smem + SM::inc_off);
-  int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
-  double* sx = reinterpret_cast<double*>(smem + SM::x_off);
-  double* sedge = reinterpret_cast<double*>(smem + SM::edge_off);
-  double* scon = reinterpret_cast<double*>(smem + SM::con_off);
-  const int tid = threadIdx.x;
-  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
-  const int K0 = d.inc_ptr[p0], K1 = d.inc_ptr[p0 + np];
-  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
-  {
-    const double2* src = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
-    double2* dst = reinterpret_cast<double2*>(sx);
-    for (int q = tid; q < np * 2 * R; q += BLOCK) dst[q] = src[q];
-  }
-  int kp0 = 0, kp1 = 0;
-  if (L.valid) {
-    kp0 = d.inc_ptr[L.pose];
-    kp1 = d.inc_ptr[L.pose + 1];
-  }
-  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  const int ci = tid / R, ca = tid - ci * R;  // compute lane (incidence, row)
-  double csum = 0.0;
-  for (int seg = K0; seg < K1; seg += SM::MAXI) {
-    const int nseg = min(SM::MAXI, K1 - seg);
-    for (int q = tid; q < nseg; q += BLOCK) sinc[q] = d.inc[seg + q];
-    __syncthreads();
-    static_assert(E_IT <= 3, "edge staging assumes <= 3 pieces per lane");
-    double2 eb0 = make_double2(0.0, 0.0), eb1 = eb0, eb2 = eb0, v0 = eb0, v1 = eb0;
-#define KMX_LOAD_CHUNK(CB)                                                                         \
-    {                                                                                              \
-      const int n_ = min(CI, nseg - (CB));                                                         \
-      const double2* er2 = reinterpret_cast<const double2*>(d.irec);                               \
-      {                                                                                            \
-        const int q = tid, qc = (q < n_ * 8) ? q : 0;                                              \
-        eb0 = er2[16 / 2 * (size_t)(seg + (CB) + (qc >> 3)) + (qc & 7)];                          \
-      }                                                                                            \
-      if constexpr (E_IT > 1) {                                                                    \
-        const int q = tid + BLOCK, qc = (q < n_ * 8) ? q : 0;                                      \
-        eb1 = er2[16 / 2 * (size_t)(seg + (CB) + (qc >> 3)) + (qc & 7)];                          \
-      }                                                                                            \
-      if constexpr (E_IT > 2) {                                                                    \
-        const int q = tid + 2 * BLOCK, qc = (q < n_ * 8) ? q : 0;                                  \
-        eb2 = er2[16 / 2 * (size_t)(seg + (CB) + (qc >> 3)) + (qc & 7)];                          \
-      }                                                                                            \
-      const int ic = (ci < n_) ? ci : 0;                                                           \
-      const int o = sinc[(CB) + ic].x;                                                             \
-      const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V); \
-      const double2* b2 = reinterpret_cast<const double2*>(base + 4 * ca);                         \
-      v0 = b2[0];                                                                                  \
-      v1 = b2[1];                                                                                  \
-      if (!PUB && o < 0) v0 = v1 = make_double2(0.0, 0.0);                                         \
-    }
-    KMX_LOAD_CHUNK(0)
-    for (int cb = 0; cb < nseg; cb += CI) {
-      const int n = min(CI, nseg - cb);
-      if (tid < n * 8) reinterpret_cast<double2*>(sedge)[tid] = eb0;
-      if (E_IT > 1 && tid + BLOCK < n * 8) reinterpret_cast<double2*>(sedge)[tid + BLOCK] = eb1;
-      if (E_IT > 2 && tid + 2 * BLOCK < n * 8) reinterpret_cast<double2*>(sedge)[tid + 2 * BLOCK] = eb2;
-      const double2 c0 = v0, c1 = v1;
-      __syncthreads();
-      if (cb + CI < nseg) KMX_LOAD_CHUNK(cb + CI)  // next chunk in flight during compute
-      if (ci < n && tid < CI * R) {
-        const int kk = (seg - K0) + cb + ci;  // tile-relative incidence index
-        int lo = 0, hi = np;                  // self pose: sptr[lo] <= kk < sptr[lo + 1]
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (sptr[mid] <= kk) lo = mid;
-          else hi = mid;
-        }
-        const int2 in = sinc[cb + ci];
-        const bool tail = (in.y >> 31) & 1;
-        const double2* q2 = reinterpret_cast<const double2*>(sedge + 16 * ci);
-        double2 w0 = q2[0], w1 = q2[1], w2 = q2[2], w3 = q2[3], w4 = q2[4], w5 = q2[5], w6 = q2[6];
-        Edge E;
-        E.R[0] = w0.x; E.R[1] = w0.y; E.R[2] = w1.x; E.R[3] = w1.y; E.R[4] = w2.x;
-        E.R[5] = w2.y; E.R[6] = w3.x; E.R[7] = w3.y; E.R[8] = w4.x;
-        E.t[0] = w4.y; E.t[1] = w5.x; E.t[2] = w5.y;
-        E.wk = w6.x;
-        E.wt = w6.y;
-        double vs[4], vo[4] = {c0.x, c0.y, c1.x, c1.y}, con[4] = {0.0, 0.0, 0.0, 0.0};
-        load4(sx + (lo * R + ca) * 4, vs);
-        const double c = incidence_row(E, tail, vs, vo, con);
-        csum += (in.x >= 0) ? 0.5 * c : c;
-        store4(scon + (ci * R + ca) * 4, con);
-      }
-      __syncthreads();
-      if (L.valid) {
-        const int A = seg + cb;
-        const int ka = max(kp0, A), kb = min(kp1, A + n);
-        for (int k = ka; k < kb; ++k) {
-          double cv[4];
-          load4(scon + ((k - A) * R + L.a) * 4, cv);
-          acc[0] += cv[0]; acc[1] += cv[1]; acc[2] += cv[2]; acc[3] += cv[3];
-        }
-      }
-      __syncthreads();
-    }
-  }
-  if (cost) *cost += csum;
-#undef KMX_LOAD_CHUNK
-}
-
-// Plain direct variant (G = 2, diagnostic): no software pipelining.
-template <int R, bool PUB>
-__device__ __forceinline__ void lane_gather_plain(const Dev& d, const Lane& L, const double* V, const double* pub,
-                                                  double acc[4], double* cost) {
-  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  if (!L.valid) return;
-  double vs[4];
-  load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
-  const int k0 = d.inc_ptr[L.pose], k1 = d.inc_ptr[L.pose + 1];
-  for (int k = k0; k < k1; ++k) {
-    const int2 in = d.inc[k];
-    EdgeRaw w;
-    double2 b0, b1;
-    fetch_incidence<R, PUB>(d, V, pub, L.a, k, in, w, b0, b1);
-    Edge E;
-    edge_from_raw(w, E);
-    const double vo[4] = {b0.x, b0.y, b1.x, b1.y};
-    const double c = incidence_row(E, (in.y >> 31) & 1, vs, vo, acc);
-    if (cost) *cost += (in.x >= 0) ? 0.5 * c : c;
-  }
-}
-
-// Compact-record variant (G = 3): 96-B records carry the neighbour index, so
-// the incidence loop reads one record (6 x 16 B) and one neighbour row — no
-// separate CSR entry — and the third rotation row is rebuilt as row0 x row1.
-// OWN (cost only, G = 4): visit each edge once — the tail incidence of a
-// local-local edge, or the only local incidence of a shared edge — from a
-// second compact array holding just those records (half the record bytes).
-__device__ __forceinline__ int2 unpack_int2(double v) {
-  const long long b = __double_as_longlong(v);
-  return make_int2((int)(b & 0xffffffffll), (int)(b >> 32));
-}
-__device__ __forceinline__ void edge_from_compact(const double2 q[6], Edge& E) {
-  E.R[0] = q[0].x; E.R[1] = q[0].y; E.R[2] = q[1].x;
-  E.R[3] = q[1].y; E.R[4] = q[2].x; E.R[5] = q[2].y;
-  E.R[6] = E.R[1] * E.R[5] - E.R[2] * E.R[4];
-  E.R[7] = E.R[2] * E.R[3] - E.R[0] * E.R[5];
-  E.R[8] = E.R[0] * E.R[4] - E.R[1] * E.R[3];
-  E.t[0] = q[3].x; E.t[1] = q[3].y; E.t[2] = q[4].x;
-  E.wk = q[4].y;
-  E.wt = q[5].x;
-}
-
-template <int R, bool PUB, bool OWN>
-__device__ __forceinline__ void lane_gather_compact(const Dev& d, const Lane& L, const double* V,
-                                                    const double* pub, double acc[4], double* cost) {
-  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  if (!L.valid) return;
-  double vs[4];
-  load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
-  const int* ptr = OWN ? d.optr : d.inc_ptr;
-  const double* rec = OWN ? d.ocrec : d.crec;
-  const int k0 = ptr[L.pose], k1 = ptr[L.pose + 1];
-  for (int k = k0; k < k1; ++k) {
-    const double2* q2 = reinterpret_cast<const double2*>(rec + 12 * (size_t)k);
-    double2 q[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) q[i] = q2[i];
-    const int2 in = unpack_int2(q[5].y);
-    const int o = in.x;
-    const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V);
-    const double2* b2 = reinterpret_cast<const double2*>(base + 4 * L.a);
-    double2 v0 = b2[0], v1 = b2[1];
-    if (!PUB && o < 0) v0 = v1 = make_double2(0.0, 0.0);
-    Edge E;
-    edge_from_compact(q, E);
-    const double vo[4] = {v0.x, v0.y, v1.x, v1.y};
-    const double c = incidence_row(E, (in.y >> 31) & 1, vs, vo, acc);
-    if (cost) *cost += (OWN || o < 0) ? c : 0.5 * c;
-  }
-}
-
-// Degree-balanced compact gather (G = 5; G = 6: owner-only cost). A tile's
-// incidences are one contiguous CSR range; it is cut into TP equal segments,
-// one per lane group, so every group walks ~the mean degree instead of the
-// wave waiting for its highest-degree pose (capping the per-pose walk at the
-// mean degree halves the gather time: k_gcap). A segment can
-// span several poses; each (group, pose) partial is flushed to LDS: the
-// first group of a pose writes A[pose], a group that starts inside a pose
-// (the continuation) writes H[group]. The (pose, row) lanes then add
-// A[pose] + H[g] for the pose's later segments in order, so the result is
-// deterministic and independent of everything but the tiling.
-template <int R, bool PUB, bool OWN>
-__device__ __forceinline__ void tile_gather_bal(const Dev& d, const Lane& L, const double* V, const double* pub,
-                                                double acc[4], double* cost, char* smem) {
-  using SM = Smem<R>;
-  constexpr int TP = SM::TP;
-  int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);          // [TP + 1] tile-local CSR
-  double* A = reinterpret_cast<double*>(smem + SM::x_off);         // [TP][R][4]
-  double* H = reinterpret_cast<double*>(smem + SM::con_off);       // [TP][R][4]
-  const int* ptr = OWN ? d.optr : d.inc_ptr;
-  const double* rec = OWN ? d.ocrec : d.crec;
-  const int tid = threadIdx.x;
-  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
-  const int K0 = ptr[p0];
-  const bool rect = d.rect != 0;
-  const int rbase = rect ? (OWN ? d.torec0 : d.trec0)[L.tile] : 0;
-  __syncthreads();  // LDS reuse across consecutive gathers in one kernel (k_eval)
-  if (tid <= np) sptr[tid] = ptr[p0 + tid] - K0;
-  if constexpr (!OWN)
-    for (int i = tid; i < TP * R * 4; i += BLOCK) A[i] = 0.0;
-  __syncthreads();
-  const int n = sptr[np];
-  const int S = max(1, (n + TP - 1) / TP);
-  const int g = L.w * (64 / R) + L.pw;  // group = (wave, pose slot)
-  double part[4] = {0.0, 0.0, 0.0, 0.0};
-  double csum = 0.0;
-  const bool gvalid = (L.pw < 64 / R);
-  const int s0 = gvalid ? g * S : n, s1 = gvalid ? min(s0 + S, n) : n;
-  if (s0 < s1) {
-    int lo = 0, hi = np;  // pose containing s0: sptr[lo] <= s0 < sptr[lo + 1]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (sptr[mid] <= s0) lo = mid;
-      else hi = mid;
-    }
-    while (sptr[lo + 1] <= s0) ++lo;  // skip zero-degree poses
-    int p = lo;
-    bool head = s0 > sptr[p];
-    // self row of the current pose, and (prefetched) of the next pose with
-    // incidences, so crossing a pose boundary does not wait on memory
-    auto next_pose = [&](int q) {
-      do ++q;
-      while (q < np - 1 && sptr[q + 1] == sptr[q]);
-      return q;
-    };
-    double vs[4], vn[4] = {0.0, 0.0, 0.0, 0.0};
-    load4(V + (size_t)(p0 + p) * 4 * R + 4 * L.a, vs);
-    int pn = next_pose(p);
-    if (pn < np && sptr[pn] < s1) load4(V + (size_t)(p0 + pn) * 4 * R + 4 * L.a, vn);
-    int pend = sptr[p + 1];
-    for (int k = s0; k < s1; ++k) {
-      if (k >= pend) {  // next pose: flush this one's partial
-        if constexpr (!OWN) store4((head ? H + (g * R + L.a) * 4 : A + (p * R + L.a) * 4), part);
-        part[0] = part[1] = part[2] = part[3] = 0.0;
-        head = false;
-        p = pn;
-        pend = sptr[p + 1];
-        vs[0] = vn[0]; vs[1] = vn[1]; vs[2] = vn[2]; vs[3] = vn[3];
-        pn = next_pose(p);
-        if (pn < np && sptr[pn] < s1) load4(V + (size_t)(p0 + pn) * 4 * R + 4 * L.a, vn);
-      }
-      // segment-major layout: step j of every group of the tile is one run of
-      // consecutive records, so a wave's 12 groups read 1152 contiguous bytes
-      const size_t ri = rect ? (size_t)rbase + (size_t)(k - s0) * TP + g : (size_t)(K0 + k);
-      const double2* q2 = reinterpret_cast<const double2*>(rec + 12 * ri);
-      double2 q[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) q[i] = q2[i];
-      const int2 in = unpack_int2(q[5].y);
-      const int o = in.x;
-      const double* base = (o >= 0) ? V + (size_t)o * 4 * R : (PUB ? pub + (size_t)(-1 - o) * 4 * R : V);
-      const double2* b2 = reinterpret_cast<const double2*>(base + 4 * L.a);
-      double2 v0 = b2[0], v1 = b2[1];
-      if (!PUB && o < 0) v0 = v1 = make_double2(0.0, 0.0);
-      Edge E;
-      edge_from_compact(q, E);
-      const double vo[4] = {v0.x, v0.y, v1.x, v1.y};
-      const double c = incidence_row(E, (in.y >> 31) & 1, vs, vo, part);
-      csum += (OWN || o < 0) ? c : 0.5 * c;
-    }
-    if constexpr (!OWN) store4((head ? H + (g * R + L.a) * 4 : A + (p * R + L.a) * 4), part);
-  }
-  if (cost) *cost += csum;
-  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  if constexpr (!OWN) {
-    __syncthreads();
-    if (L.valid) {
-      const int p = L.pose - p0;
-      load4(A + (p * R + L.a) * 4, acc);
-      if (sptr[p + 1] > sptr[p]) {
-        const int gf = sptr[p] / S, gl = (sptr[p + 1] - 1) / S;
-        for (int gg = gf + 1; gg <= gl; ++gg) {
-          double h[4];
-          load4(H + (gg * R + L.a) * 4, h);
-          acc[0] += h[0]; acc[1] += h[1]; acc[2] += h[2]; acc[3] += h[3];
-        }
-      }
-    }
-  }
-}
-
-// LDS-staged chunked gather (G = 7; G = 8: owner-only cost). The tile's
-// incidences are cut into segments of SEG consecutive incidences; chunk c
-// holds the NG = TP segments [c NG, (c + 1) NG), one per lane group. Per chunk:
-//   * the chunk's compact records (one contiguous range, 96 B each) are
-//     copied into LDS by the whole workgroup with full-line 16-B loads, so an
-//     edge record crosses L2 -> L1 once instead of once per row lane and per
-//     partially used line; the NEXT chunk's records are loaded into registers
-//     while this chunk is computed (register-staged double buffer);
-//   * every group reads its SEG neighbour indices from LDS and issues all SEG
-//     neighbour-row loads at once, then consumes them in order;
-//   * (group, pose) partials are flushed as in G = 5: the segment holding a
-//     pose's first incidence writes A[pose], a segment that starts inside a
-//     pose writes H[group]; after a barrier the (pose, row) lanes add their
-//     pose's continuation segments of the chunk in segment order.
-// Every pose's sum is therefore a fixed function of the tiling (deterministic).
-template <int R, int SEG>
-struct SmemL {
-  static constexpr int PPW = 64 / R;
-  static constexpr int TP = WAVES * PPW;  // poses per tile = lane groups per workgroup
-  static constexpr int NG = TP;
-  static constexpr int CH = NG * SEG;     // incidences per chunk
-  static constexpr int NSL = (CH * 6 + BLOCK - 1) / BLOCK;  // 16-B staging slots per thread
-  static constexpr int ptr_off = 0;                                      // int[TP + 1]
-  static constexpr int a_off = ((TP + 1) * 4 + 15) / 16 * 16;            // double[TP][R][4]
-  static constexpr int h_off = a_off + TP * R * 32;                      // double[NG][R][4]
-  static constexpr int rec_off = h_off + NG * R * 32;                    // double[CH][12]
-  static constexpr int red_off = rec_off + CH * 96;
-  static constexpr int bytes = red_off + RED_BYTES;
-};
-#ifndef KMX_SEG
-#define KMX_SEG 4
-#endif
-#ifndef KMX_GATHER_DEFAULT
-#define KMX_GATHER_DEFAULT 5
-#endif
-
-template <int R, bool PUB, bool OWN, int SEG>
-__device__ __forceinline__ void tile_gather_lds(const Dev& d, const Lane& L, const double* V, const double* pub,
-                                                double acc[4], double* cost, char* smem) {
-  using SM = SmemL<R, SEG>;
-  constexpr int NG = SM::NG, CH = SM::CH, NSL = SM::NSL;
-  int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
-  double* A = reinterpret_cast<double*>(smem + SM::a_off);
-  double* H = reinterpret_cast<double*>(smem + SM::h_off);
-  double2* lrec = reinterpret_cast<double2*>(smem + SM::rec_off);
-  const int* ptr = OWN ? d.optr : d.inc_ptr;
-  const double2* grec = reinterpret_cast<const double2*>(OWN ? d.ocrec : d.crec);
-  const int tid = threadIdx.x;
-  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
-  const int K0 = ptr[p0];
-  grec += (size_t)K0 * 6;
-  __syncthreads();  // LDS reuse across consecutive gathers in one kernel (k_eval)
-  if (tid <= np) sptr[tid] = ptr[p0 + tid] - K0;
-  __syncthreads();
-  const int n = sptr[np];
-  const int nch = (n + CH - 1) / CH;
-  const int g = L.w * (64 / R) + L.pw;
-  const bool gvalid = (L.pw < 64 / R);
-  double2 stg[NSL];
-  auto issue = [&](int c) {
-    const int base = c * CH * 6, cnt = min(CH, n - c * CH) * 6;
-#pragma unroll
-    for (int i = 0; i < NSL; ++i) {
-      const int j = tid + i * BLOCK;
-      if (j < cnt) stg[i] = grec[base + j];
-    }
-  };
-  auto commit = [&](int c) {
-    const int cnt = min(CH, n - c * CH) * 6;
-#pragma unroll
-    for (int i = 0; i < NSL; ++i) {
-      const int j = tid + i * BLOCK;
-      if (j < cnt) lrec[j] = stg[i];
-    }
-  };
-  double csum = 0.0;
-  if (nch > 0) issue(0);
-  for (int c = 0; c < nch; ++c) {
-    __syncthreads();  // the previous chunk's records and H are no longer read
-    commit(c);
-    __syncthreads();
-    const int s = c * NG + g;
-    const int k0 = s * SEG, k1 = min(k0 + SEG, n);
-    const bool work = gvalid && k0 < k1;
-    double2 nb[SEG][2];
-    if (work) {
-#pragma unroll
-      for (int j = 0; j < SEG; ++j) {
-        nb[j][0] = nb[j][1] = make_double2(0.0, 0.0);
-        if (k0 + j < k1) {
-          const int o = unpack_int2(lrec[(k0 + j - c * CH) * 6 + 5].y).x;
-          if (o >= 0 || PUB) {
-            const double* base = (o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R;
-            const double2* b2 = reinterpret_cast<const double2*>(base + 4 * L.a);
-            nb[j][0] = b2[0];
-            nb[j][1] = b2[1];
-          }
-        }
-      }
-    }
-    if (c + 1 < nch) issue(c + 1);  // next chunk's records fly while this one computes
-    if (work) {
-      int lo = 0, hi = np;  // pose containing k0: sptr[lo] <= k0 < sptr[lo + 1]
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (sptr[mid] <= k0) lo = mid;
-        else hi = mid;
-      }
-      while (sptr[lo + 1] <= k0) ++lo;  // skip zero-degree poses
-      int p = lo;
-      bool head = k0 > sptr[p];
-      int pend = sptr[p + 1];
-      double vs[4];
-      load4(V + (size_t)(p0 + p) * 4 * R + 4 * L.a, vs);
-      double part[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int j = 0; j < SEG; ++j) {
-        const int k = k0 + j;
-        if (k < k1) {
-          if (k >= pend) {  // next pose: flush this one's partial
-            if constexpr (!OWN) store4((head ? H + (g * R + L.a) * 4 : A + (p * R + L.a) * 4), part);
-            part[0] = part[1] = part[2] = part[3] = 0.0;
-            head = false;
-            do ++p;
-            while (sptr[p + 1] <= k);
-            pend = sptr[p + 1];
-            load4(V + (size_t)(p0 + p) * 4 * R + 4 * L.a, vs);
-          }
-          const double2* q2 = lrec + (k - c * CH) * 6;
-          double2 q[6];
-#pragma unroll
-          for (int i = 0; i < 6; ++i) q[i] = q2[i];
-          Edge E;
-          edge_from_compact(q, E);
-          const int2 in = unpack_int2(q[5].y);
-          const double vo[4] = {nb[j][0].x, nb[j][0].y, nb[j][1].x, nb[j][1].y};
-          const double cc = incidence_row(E, (in.y >> 31) & 1, vs, vo, part);
-          csum += (OWN || in.x < 0) ? cc : 0.5 * cc;
-        }
-      }
-      if constexpr (!OWN) store4((head ? H + (g * R + L.a) * 4 : A + (p * R + L.a) * 4), part);
-    }
-    if constexpr (!OWN) {
-      __syncthreads();
-      if (L.valid) {  // fold this chunk's continuation segments of the lane's pose
-        const int p = L.pose - p0;
-        const int e0 = sptr[p], e1 = sptr[p + 1];
-        if (e1 > e0) {
-          const int sf = e0 / SEG, sl = (e1 - 1) / SEG;
-          const int lo = max(sf + 1, c * NG), hi = min(sl, c * NG + NG - 1);
-          if (lo <= hi) {
-            double a4[4];
-            load4(A + (p * R + L.a) * 4, a4);
-            for (int ss = lo; ss <= hi; ++ss) {
-              double h4[4];
-              load4(H + ((ss - c * NG) * R + L.a) * 4, h4);
-              a4[0] += h4[0]; a4[1] += h4[1]; a4[2] += h4[2]; a4[3] += h4[3];
-            }
-            store4(A + (p * R + L.a) * 4, a4);
-          }
-        }
-      }
-    }
-  }
-  if (cost) *cost += csum;
-  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  if constexpr (!OWN) {
-    if (L.valid) {
-      const int p = L.pose - p0;
-      if (sptr[p + 1] > sptr[p]) load4(A + (p * R + L.a) * 4, acc);  // the last fold's own writes
-    }
-  }
-}
-
-template <int R, int G, bool PUB>
-__device__ __forceinline__ void gather(const Dev& d, const Lane& L, const double* V, const double* pub,
-                                       double acc[4], double* cost, char* smem) {
-  if constexpr (G == 0) lane_gather<R, PUB>(d, L, V, pub, acc, cost);
-  else if constexpr (G == 2) lane_gather_plain<R, PUB>(d, L, V, pub, acc, cost);
-  else if constexpr (G == 3) lane_gather_compact<R, PUB, false>(d, L, V, pub, acc, cost);
-  else if constexpr (G == 4) lane_gather_compact<R, PUB, true>(d, L, V, pub, acc, cost);
-  else if constexpr (G == 5) tile_gather_bal<R, PUB, false>(d, L, V, pub, acc, cost, smem);
-  else if constexpr (G == 6) tile_gather_bal<R, PUB, true>(d, L, V, pub, acc, cost, smem);
-  else if constexpr (G == 7) tile_gather_lds<R, PUB, false, KMX_SEG>(d, L, V, pub, acc, cost, smem);
-  else if constexpr (G == 8) tile_gather_lds<R, PUB, true, KMX_SEG>(d, L, V, pub, acc, cost, smem);
-  else tile_gather<R, PUB>(d, L, V, pub, acc, cost, smem);
-}
-
-// LDS footprint of a gather kernel by variant (the reduction scratch follows it).
-template <int R, int G>
-struct SmemG {
-  static constexpr int red_off = Smem<R>::red_off;
-  static constexpr int bytes = Smem<R>::bytes;
-};
-template <int R>
-struct SmemG<R, 7> {
-  static constexpr int red_off = SmemL<R, KMX_SEG>::red_off;
-  static constexpr int bytes = SmemL<R, KMX_SEG>::bytes;
-};
-template <int R>
-struct SmemG<R, 8> : SmemG<R, 7> {};
-// G = 9 (k_hess only; k_grad / k_cost run G = 5 / 6): the G = 5 layout here.
-template <int R>
-struct SmemG<R, 9> : SmemG<R, 5> {};
-
-// Incidence-parallel Hessian gather (G = 9, k_hess). Q's diagonal block D_i
-// (k_precond) is applied once per pose, so an incidence only contributes its
-// off-diagonal block B_e applied to the other endpoint's row: one lane per
-// incidence reads the 96-B record once (not once per row as in G = 5) and the
-// whole r x 4 neighbour row, and writes the R contribution rows to LDS; the
-// (pose, row) lanes then add their pose's incidences in CSR order
-// (deterministic). out_i = D_i v_i + sum_{e at i} B_e v_other(e), with a
-// public neighbour's row taken as zero (Hessian of the local problem).
-template <int R>
-struct SmemH {
+struct SmemH {  // Hessian gather (k_hess, eval EHESS)
   static constexpr int TP = WAVES * (64 / R);
-  static constexpr int CH = TP * R;                                       // incidences per chunk (<= BLOCK)
+  static constexpr int CH = TP * R;                                       // <= BLOCK
   static constexpr int c_off = 0;                                         // double[CH][R][4]
   static constexpr int ptr_off = CH * R * 32;                             // int[TP + 1]
   static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
   static constexpr int bytes = red_off + RED_BYTES;
 };
-// group_symYtG<R, true> scratch: BLOCK x 6 doubles at the start of the LDS
-static_assert(WAVES * 64 * 6 * 8 <= SmemH<3>::ptr_off && WAVES * 64 * 6 * 8 <= SmemH<8>::ptr_off, "scratch");
-static_assert(WAVES * 64 * 6 * 8 <= Smem<5>::red_off && WAVES * 64 * 6 * 8 <= Smem<8>::red_off, "scratch");
-template <int R, int GV>
-struct SmemHess : SmemG<R, GV> {};
 template <int R>
-struct SmemHess<R, 9> : SmemH<R> {};
-
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops but
-// not for its outstanding global loads (__syncthreads waits vmcnt(0), which
-// would drain the next chunk's prefetched records).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
+struct SmemHG {  // gradient / cost gathers: a chunk buffer plus the tile's own rows
+  static constexpr int TP = WAVES * (64 / R);
+  static constexpr int CH = 240;                                          // incidences per chunk
+  static constexpr int c_off = 0;                                         // double[CH][R][4]
+  static constexpr int x_off = CH * R * 32;                               // double[TP][R][4]
+  static constexpr int ptr_off = x_off + TP * R * 32;                     // int[TP + 1]
+  static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
+  static constexpr int bytes = red_off + RED_BYTES;
+};
 template <int R>
+struct SmemC {  // trial cost: own rows + CSR pointers only
+  static constexpr int TP = WAVES * (64 / R);
+  static constexpr int x_off = 0;
+  static constexpr int ptr_off = TP * R * 32;
+  static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
+  static constexpr int bytes = red_off + RED_BYTES;
+};
+constexpr int SCR_BYTES = BLOCK * 6 * 8;  // group_symYtG<R, true> scratch
+struct SmemU {                            // element-wise kernels: scratch + reduction
+  static constexpr int red_off = SCR_BYTES;
+  static constexpr int bytes = red_off + RED_BYTES;
+};
+static_assert(SCR_BYTES <= SmemH<3>::ptr_off && SCR_BYTES <= SmemH<8>::ptr_off, "scratch");
+static_assert(SCR_BYTES <= SmemHG<3>::x_off, "scratch");
+
+// Euclidean Hessian-vector product Q V of the tile's poses (the local problem:
+// a public neighbour's row counts as zero). Q's diagonal block D_i (k_precond)
+// is applied once per pose; an incidence contributes only its off-diagonal
+// block applied to the other endpoint's whole r x 4 row.
+template <int R, int RW>
 __device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const double* V, double acc[4],
                                             char* smem) {
   using SM = SmemH<R>;
+  using RC = Rec<RW>;
   constexpr int CH = SM::CH;
-  static_assert(CH <= BLOCK, "one incidence per thread per chunk");
   double* Cs = reinterpret_cast<double*>(smem + SM::c_off);
   int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
   const int tid = threadIdx.x;
@@ -997,21 +480,16 @@ __device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const d
   const int pl = L.pose - p0;
   const int lt = min(tid, CH - 1);
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  // clamped, unconditional record loads (hrec holds one zero pad record, so
-  // an empty tile at the end of the array still reads inside it)
-  auto ld = [&](int c0, double2 q[6]) {
-    const int k = max(min(c0 + lt, n - 1), 0);
-    const double2* q2 = reinterpret_cast<const double2*>(d.hrec + 12 * (size_t)(K0 + k));
-#pragma unroll
-    for (int i = 0; i < 6; ++i) q[i] = q2[i];
-  };
-  double2 q[6];
+  // clamped, unconditional record loads (the pad record keeps an empty tile
+  // at the end of the array inside it)
+  auto ld = [&](int c0, double2* q) { RC::load(d.rec, (size_t)(K0 + max(min(c0 + lt, n - 1), 0)), q); };
+  double2 q[RC::Q];
   ld(0, q);
   __syncthreads();  // sptr
   for (int c0 = 0; c0 < n; c0 += CH) {
     Edge E;
-    edge_from_compact(q, E);
-    const int2 in = unpack_int2(q[5].y);
+    RC::edge(q, E);
+    const int2 in = RC::inc(q);
     const int o = in.x;
     const bool tail = (in.y >> 31) & 1;
     const double2* b2 = reinterpret_cast<const double2*>(V + (size_t)max(o, 0) * 4 * R);
@@ -1038,13 +516,13 @@ __device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const d
       }
     }
     // the next chunk's records, issued once this chunk's rows are consumed, stay
-    // in flight across the LDS hand-off and the reduction
+    // in flight across the LDS hand-off and the pose sums
     asm volatile("" ::: "memory");
     ld(c0 + CH, q);
     lds_barrier();
     if (L.valid) {
       const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
-      #pragma unroll 4
+#pragma unroll 4
       for (int j = j0; j < j1; ++j) {
         double h[4];
         load4(Cs + (j * R + L.a) * 4, h);
@@ -1066,33 +544,17 @@ __device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const d
   }
 }
 
-
-// Gradient and cost, incidence-parallel (G = 9 k_grad). As hinc_gather, but a
-// lane evaluates its whole incidence with incidence_row (diagonal and
-// off-diagonal terms, the public neighbour row from the table), so it also
-// reads its own pose's row (found by a binary search of the tile CSR), and
-// adds the incidence's cost share (1/2 per endpoint; all of it for a shared
+// Gradient and cost, incidence-parallel. A lane evaluates its whole incidence
+// with incidence_row (diagonal and off-diagonal terms; a public neighbour's row
+// from the table), reading its own pose's row from an LDS copy of the tile's
+// rows (owning pose found by a binary search of the tile CSR), and adds the
+// incidence's cost share (1/2 per endpoint of a local edge; all of a shared
 // edge). The pose sums run in CSR order.
-// k_grad's LDS: a smaller chunk buffer, plus the tile's own rows (every lane
-// reads its incidence's own row from LDS instead of L1).
-#ifndef KMX_HG_CH
-#define KMX_HG_CH 240
-#endif
-template <int R>
-struct SmemHG {
-  static constexpr int TP = WAVES * (64 / R);
-  static constexpr int CH = KMX_HG_CH;                                    // incidences per chunk
-  static constexpr int c_off = 0;                                         // double[CH][R][4]
-  static constexpr int x_off = CH * R * 32;                               // double[TP][R][4]
-  static constexpr int ptr_off = x_off + TP * R * 32;                     // int[TP + 1]
-  static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
-  static constexpr int bytes = red_off + RED_BYTES;
-};
-
-template <int R>
+template <int R, int RW>
 __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const double* V, const double* pub,
                                           double acc[4], double* cost, char* smem) {
   using SM = SmemHG<R>;
+  using RC = Rec<RW>;
   constexpr int CH = SM::CH;
   double* Cs = reinterpret_cast<double*>(smem + SM::c_off);
   double2* xs = reinterpret_cast<double2*>(smem + SM::x_off);
@@ -1110,15 +572,10 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
   const int lt = min(tid, CH - 1);
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
   double csum = 0.0;
-  auto ld = [&](int c0, double2 q[6]) {
-    const int k = max(min(c0 + lt, n - 1), 0);
-    const double2* q2 = reinterpret_cast<const double2*>(d.hrec + 12 * (size_t)(K0 + k));
-#pragma unroll
-    for (int i = 0; i < 6; ++i) q[i] = q2[i];
-  };
-  double2 q[6];
+  auto ld = [&](int c0, double2* q) { RC::load(d.rec, (size_t)(K0 + max(min(c0 + lt, n - 1), 0)), q); };
+  double2 q[RC::Q];
   ld(0, q);
-  __syncthreads();  // sptr
+  __syncthreads();  // sptr, xs
   for (int c0 = 0; c0 < n; c0 += CH) {
     const int k = max(min(c0 + lt, n - 1), 0);
     int lo = 0, hi = np;  // owning pose: sptr[lo] <= k < sptr[lo + 1]
@@ -1127,16 +584,17 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
       if (sptr[mid] <= k) lo = mid;
       else hi = mid;
     }
-    const int2 in = unpack_int2(q[5].y);
+    const int2 in = RC::inc(q);
     const int o = in.x;
     const bool tail = (in.y >> 31) & 1;
     const double2* s2 = xs + lo * 2 * R;
-    const double2* o2 = reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
+    const double2* o2 =
+        reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
     double2 vo2[2 * R];
 #pragma unroll
     for (int i = 0; i < 2 * R; ++i) vo2[i] = o2[i];
     Edge E;
-    edge_from_compact(q, E);
+    RC::edge(q, E);
     if (tid < CH && c0 + tid < n) {
 #pragma unroll
       for (int a = 0; a < R; ++a) {
@@ -1154,7 +612,7 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
     lds_barrier();
     if (L.valid) {
       const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
-      #pragma unroll 4
+#pragma unroll 4
       for (int j = j0; j < j1; ++j) {
         double h[4];
         load4(Cs + (j * R + L.a) * 4, h);
@@ -1165,78 +623,176 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
   }
   *cost += csum;
 }
-template <int R, int GV>
-struct SmemGrad : SmemG<R, GV> {};
-template <int R>
-struct SmemGrad<R, 9> : SmemHG<R> {};
+
+// Trial cost f(Xt), one lane per incidence of the tile; only the owner
+// incidence of an edge contributes (the tail of a local edge, the local end of
+// a shared one), so each edge of the local problem counts once. The owner lane
+// reads its own row from LDS and the other endpoint's row, and sums the r
+// rows' residual terms: no per-pose reduction.
+template <int R, int RW>
+__device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, const double* V, const double* pub,
+                                                 char* smem) {
+  using SM = SmemC<R>;
+  using RC = Rec<RW>;
+  int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
+  double2* xs = reinterpret_cast<double2*>(smem + SM::x_off);
+  const int tid = threadIdx.x;
+  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
+  const int K0 = d.inc_ptr[p0];
+  const int n = d.inc_ptr[p0 + np] - K0;
+  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
+  {
+    const double2* v2 = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
+    for (int i = tid; i < np * 2 * R; i += BLOCK) xs[i] = v2[i];
+  }
+  __syncthreads();
+  double cost = 0.0;
+  for (int k = tid; k < n; k += BLOCK) {
+    double2 q[RC::Q];
+    RC::load(d.rec, (size_t)(K0 + k), q);
+    const int2 in = RC::inc(q);
+    const int o = in.x;
+    const bool tail = (in.y >> 31) & 1;
+    if (o >= 0 && !tail) continue;  // the head of a local edge: its tail counts it
+    int lo = 0, hi = np;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (sptr[mid] <= k) lo = mid;
+      else hi = mid;
+    }
+    const double2* s2 = xs + lo * 2 * R;
+    const double2* o2 =
+        reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
+    double2 vs2[2 * R], vo2[2 * R];
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) { vs2[i] = s2[i]; vo2[i] = o2[i]; }
+    Edge E;
+    RC::edge(q, E);
+    double c = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      const double vs[4] = {vs2[2 * a].x, vs2[2 * a].y, vs2[2 * a + 1].x, vs2[2 * a + 1].y};
+      const double vo[4] = {vo2[2 * a].x, vo2[2 * a].y, vo2[2 * a + 1].x, vo2[2 * a + 1].y};
+      double dummy[4] = {0.0, 0.0, 0.0, 0.0};
+      c += incidence_row(E, tail, vs, vo, dummy);
+    }
+    cost += c;
+  }
+  return cost;
+}
 
 // -------------------------------------------- fused per-robot reductions --
-// Each tile of robot l publishes its partial sums, then takes a ticket on
-// robot l's counter (agent-scope release / acquire, cdna_hip_programming.md
-// Guideline 16). The tile that draws the last ticket reduces robot l's
-// partials in tile order (deterministic) and runs the RTR / tCG scalar logic
-// on thread 0 — no separate reduction launch, robots reduce in parallel.
+// Each tile of robot l reduces its NV values over the workgroup, stores them
+// write-through (sc1) and takes a ticket on robot l's counter; the tile that
+// draws the last ticket reduces robot l's partials in tile order
+// (deterministic, the same thread-strided + wave + workgroup order everywhere)
+// and runs the RTR / tCG scalar logic. Hand-off form: MI355X_MICROARCH.md
+// "Valid forms", table row 1 (sc1 stores, one agent-scope add per workgroup
+// after its vmcnt wait, the last adder told by the returned value, sc1 loads).
 __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_);
 
-template <int KIND, int NV, int FUSED>
+template <int KIND, int NV, typename Store>
 __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const double* vals, char* smem_red,
-                                            int R_) {
+                                            int R_, Store&& store, const Post& po = Post{}) {
   double* lds = reinterpret_cast<double*>(smem_red);
-  int* flag = reinterpret_cast<int*>(smem_red + 8 * NPART * WAVES);
   static_assert(NV <= NPART && WAVES == 4, "reduction area");
-  double tv[NV > 0 ? NV : 1];
-  if constexpr (!FUSED) {
-    // all NV sums in one LDS round (same wave and wave-order summation as
-    // block_sum); only thread 0 needs them. The area is used once per launch,
-    // and the barrier is LDS-only, so the caller's row stores keep draining.
+#pragma unroll
+  for (int s = 0; s < NV; ++s) {
+    const double w = wave_sum(vals[s]);
+    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
+  }
+  __syncthreads();
+  // Waves 1..3 store their rows and leave; wave 0 publishes the tile's partials
+  // (lane 0: sc1 stores, vmcnt wait, one agent-scope ticket), so the ticket's
+  // round trip holds one wave, not the workgroup, and no row store is queued
+  // ahead of the partials.
+  if (L.w != 0) {
+    store();
+    return;
+  }
+  // Two-level ticket: tiles arrive on their group's counter (GS consecutive
+  // tiles of the robot); the last tile of a group sums the group's partials and
+  // arrives on the robot's counter; the last group sums the group partials and
+  // runs the control logic. Sums run in tile order within a group and in group
+  // order across groups (deterministic); no counter sees more than GS + the
+  // robot's group count arrivals, where one counter per robot serialised ~260.
+  const int t0 = d.rtile0[L.l], t1 = d.rtile0[L.l + 1];
+  const int gl = (L.tile - t0) / GS, g = d.rgroup0[L.l] + gl;
+  const int gsz = min(GS, t1 - t0 - gl * GS);
+  unsigned ticket = 0;
+  if (L.ln == 0) {
 #pragma unroll
     for (int s = 0; s < NV; ++s) {
-      const double w = wave_sum(vals[s]);
-      if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
-    }
-    lds_barrier();
-    if (threadIdx.x == 0) {
+      double t = 0.0;
 #pragma unroll
-      for (int s = 0; s < NV; ++s) {
-        double t = 0.0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
-        d.part[(size_t)L.tile * NPART + s] = t;
-      }
+      for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
+      __hip_atomic_store(d.part + (size_t)L.tile * NPART + s, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    return;
-  } else {
-#pragma unroll
-    for (int s = 0; s < NV; ++s) tv[s] = block_sum(vals[s], lds);
-    // Write-through (sc1) partial stores, drained, then one agent-scope
-    // ticket per tile; the last arriver reads the partials with sc1 loads
-    // (MI355X_MICROARCH.md "Valid forms", table row 1).
-    if (threadIdx.x == 0) {
-#pragma unroll
-      for (int s = 0; s < NV; ++s)
-        __hip_atomic_store(d.part + (size_t)L.tile * NPART + s, tv[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned ntl = (unsigned)(d.rtile0[L.l + 1] - d.rtile0[L.l]);
-      const unsigned t = __hip_atomic_fetch_add(d.tickets + L.l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = (t == ntl - 1) ? 1 : 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ticket = __hip_atomic_fetch_add(d.gtickets + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ticket = __shfl(ticket, 0, 64);
+  store();
+  if (ticket != (unsigned)(gsz - 1)) return;
+  constexpr int NS = (KIND == RED_COST) ? 4 : NV;  // k_cost also sums k_retract's slots 2, 3
+  static_assert(NPART == 4 && GS <= 64, "group layout");
+  // consumer form "ticket -> acquire -> s_waitcnt -> plain loads"
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  double gs[NPART] = {0.0, 0.0, 0.0, 0.0};
+  {
+    double2 a = make_double2(0.0, 0.0), b = make_double2(0.0, 0.0);
+    if (L.ln < gsz) {
+      const double2* p2 = reinterpret_cast<const double2*>(d.part + (size_t)(t0 + gl * GS + L.ln) * NPART);
+      a = p2[0];
+      b = p2[1];
     }
-    __syncthreads();
-    if (!*flag) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    constexpr int NS = (KIND == RED_COST) ? 4 : NV;
-    double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
-    const int t0 = d.rtile0[L.l], t1 = d.rtile0[L.l + 1];
+    for (int k = 0; k < gsz; ++k) {
+      gs[0] += __shfl(a.x, k, 64); gs[1] += __shfl(a.y, k, 64);
+      gs[2] += __shfl(b.x, k, 64); gs[3] += __shfl(b.y, k, 64);
+    }
+  }
+  unsigned top = 0;
+  if (L.ln == 0) {
+    double2* gp = reinterpret_cast<double2*>(d.gpart + (size_t)g * NPART);
+    __hip_atomic_store(&gp->x, gs[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&gp->y, gs[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&gp[1].x, gs[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&gp[1].y, gs[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d.gtickets + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    top = __hip_atomic_fetch_add(d.tickets + L.l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  top = __shfl(top, 0, 64);
+  const int g0 = d.rgroup0[L.l], ng = d.rgroup0[L.l + 1] - g0;
+  if (top != (unsigned)(ng - 1)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+  for (int c = 0; c < ng; c += 64) {
+    const int n = min(64, ng - c);
+    double2 a = make_double2(0.0, 0.0), b = make_double2(0.0, 0.0);
+    if (L.ln < n) {
+      const double2* p2 = reinterpret_cast<const double2*>(d.gpart + (size_t)(g0 + c + L.ln) * NPART);
+      a = p2[0];
+      b = p2[1];
+    }
+    for (int k = 0; k < n; ++k) {
+      tot[0] += __shfl(a.x, k, 64); tot[1] += __shfl(a.y, k, 64);
+      tot[2] += __shfl(b.x, k, 64); tot[3] += __shfl(b.y, k, 64);
+    }
+  }
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      double v = 0.0;
-      for (int t = t0 + (int)threadIdx.x; t < t1; t += BLOCK)
-        v += __hip_atomic_load(d.part + (size_t)t * NPART + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      tot[s] = block_sum(v, lds);
+  for (int s = NS; s < NPART; ++s) tot[s] = 0.0;
+  if (L.ln == 0) {
+    control(d, L.l, KIND, tot, R_);
+    if constexpr (KIND == RED_HESS) {
+      if (po.slot >= 0) atomicAdd(d.hv_launch + po.slot, 1);
     }
-    if (threadIdx.x == 0) {
-      control(d, L.l, KIND, tot, R_);
-      __hip_atomic_store(d.tickets + L.l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (KIND == RED_UPDATE) {
+      if (po.hs) post_status(po.hs, L.l, po.seq, d.ctl[L.l].phase == PH_TCG);
     }
+    __hip_atomic_store(d.tickets + L.l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1249,12 +805,14 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
     c.f_cur = f;
     c.f_final = f;
     c.commit = 0;
-    if (gn < P.gn_tol) {
+    if (gn < P.gn_tol) {  // no step: the iterate does not change
       c.phase = PH_IDLE;
       c.tcg_stop = KMX_TCG_SKIPPED;
       c.tcg_iter = 0;
       c.accepted = 0;
       c.skipped = 1;
+      if (c.rtr_iter == 0) d.relc[l] = 0.0;
+      else d.relc[l] = c.rel_change;
     } else {
       c.phase = PH_TCG;
       c.tcg_iter = 0;
@@ -1332,113 +890,59 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
     c.rtr_iter += 1;
     c.phase = (c.rtr_iter < P.rtr_iters) ? PH_START : PH_IDLE;
     c.rel_change = sqrt(c.chg_acc / (double)d.n_robot[l]);
-  }
-}
-
-// Separate-launch reduction (variant F = 0): one workgroup per robot.
-__global__ __launch_bounds__(BLOCK) void k_reduce(Dev d, int kind, int R_, HostStatus* hs,
-                                                 unsigned long long seq) {
-  __shared__ double lds[NPART * WAVES];
-  const int l = blockIdx.x;
-  const int ph = d.ctl[l].phase;
-  bool act = false;
-  if (kind == RED_GRAD) act = ph == PH_START;
-  if (kind == RED_HESS || kind == RED_UPDATE) act = ph == PH_TCG;
-  if (kind == RED_COST) act = ph == PH_STEP;
-  if (!act) {
-    if (hs && threadIdx.x == 0) post_status(hs, l, seq, false);  // not in tCG after this step
-    return;
-  }
-  const int ns = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
-  double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
-  const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
-  // all slots in one pass and one LDS round (same per-thread, per-wave and
-  // wave-order summation as a block_sum per slot, so the sums are unchanged)
-  static_assert(NPART == 4, "two 16-B loads per tile");
-  double v[NPART] = {0.0, 0.0, 0.0, 0.0};
-  for (int t = t0 + (int)threadIdx.x; t < t1; t += BLOCK) {
-    const double2* p2 = reinterpret_cast<const double2*>(d.part + (size_t)t * NPART);
-    const double2 a = p2[0], b = p2[1];
-    v[0] += a.x; v[1] += a.y; v[2] += b.x; v[3] += b.y;
-  }
-#pragma unroll
-  for (int s = 0; s < NPART; ++s) {
-    const double w = wave_sum(v[s]);
-    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < NPART; ++s) {
-    double acc = 0.0;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) acc += lds[s * WAVES + w];
-    tot[s] = s < ns ? acc : 0.0;
-  }
-  if (threadIdx.x == 0) {
-    control(d, l, kind, tot, R_);
-    if (hs) post_status(hs, l, seq, d.ctl[l].phase == PH_TCG);
+    if (c.phase == PH_IDLE) d.relc[l] = c.rel_change;  // the team status of dpgo's getStatus
   }
 }
 
 #define KMX_SMEM extern __shared__ __attribute__((aligned(16))) char smem[]
 
+// Minimum waves per SIMD of the gather kernels: 4 at r <= 5 (128 VGPRs); the
+// r >= 6 rows need more registers.
+template <int R>
+struct LB {
+  static constexpr int w = R <= 5 ? 4 : 2;
+};
+
 // Start of an RTR iteration: egrad (gather X with public neighbours), cost,
-// S = sym(Y^T egrad_Y), g = P_Y(egrad), r = g, z = precon(g).
-template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) void k_grad(Dev d) {
+// S = sym(Y^T egrad_Y), g = P_Y(egrad), z = precon(g); partials f, |g|^2, <z,g>.
+template <int R, int RW>
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_START) return;
   double y[4] = {0, 0, 0, 0}, G[4], cost = 0.0;
-  if constexpr (GV == 9) hinc_grad<R>(d, L, d.X, d.pub, G, &cost, smem);
-  else gather<R, GV, true>(d, L, d.X, d.pub, G, &cost, smem);
+  hinc_grad<R, RW>(d, L, d.X, d.pub, G, &cost, smem);
   if (L.valid) load4(d.X + (size_t)L.pose * 4 * R + 4 * L.a, y);
   double S[9], gr[4], zr[4];
-  // G = 9: the gather's chunk buffer is free now (its last barrier passed)
-  double* scr = reinterpret_cast<double*>(smem + SmemHG<R>::c_off);
-  static_assert(WAVES * 64 * 6 * 8 <= SmemHG<R>::x_off, "scratch");
-  if (d.dbg & 2) {
-    for (int i = 0; i < 9; ++i) S[i] = 0.0;
-  } else {
-    group_symYtG<R, GV == 9>(y, G, L.base, S, scr);
-  }
+  double* scr = reinterpret_cast<double*>(smem);  // the chunk buffer is free after the gather's last barrier
+  group_symYtG<R, true>(y, G, L.base, S, scr);
 #pragma unroll
   for (int c = 0; c < 3; ++c) gr[c] = G[c] - (y[0] * S[0 * 3 + c] + y[1] * S[1 * 3 + c] + y[2] * S[2 * 3 + c]);
   gr[3] = G[3];
-  if (d.dbg & 1) {
-    for (int i = 0; i < 4; ++i) zr[i] = gr[i];
-  } else {
-    group_precon<R, GV == 9>(d, L.pose, L.valid, y, gr, L.base, zr, scr);
-  }
-  double vals[3] = {0.0, 0.0, 0.0};
-  vals[0] = cost;  // the incidence-parallel gather accumulates cost on non-pose lanes too
+  group_precon<R, true>(d, L.pose, L.valid, y, gr, L.base, zr, scr);
+  double vals[3] = {cost, 0.0, 0.0};  // cost is accumulated on every incidence lane
   if (L.valid) {
     vals[1] = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2] + gr[3] * gr[3];
     vals[2] = zr[0] * gr[0] + zr[1] * gr[1] + zr[2] * gr[2] + zr[3] * gr[3];
   }
-  auto store = [&]() {
-    if (L.valid) {
-      const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-      store4(d.g + o, gr);  // r = g at the start of tCG: k_update's first step reads g
-      store4(d.z + o, zr);
-      if (L.a == 0) {
-        double* Sp = d.S + 9 * (size_t)L.pose;
+  finish_tile<RED_GRAD, 3>(d, L, vals, smem + SmemHG<R>::red_off, R, [&]() {
+    if (!L.valid) return;
+    const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+    store4(d.g + o, gr);  // r = g at the start of tCG: k_update's first step reads g
+    store4(d.z + o, zr);
+    if (L.a == 0) {
+      double* Sp = d.S + 9 * (size_t)L.pose;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) Sp[i] = S[i];
-      }
+      for (int i = 0; i < 9; ++i) Sp[i] = S[i];
     }
-  };
-  // separate reduce launch: store first (frees S, g, z before the block sum);
-  // fused reduction: ticket first, so its drain waits only for the partials
-  if constexpr (!F) store();
-  finish_tile<RED_GRAD, 3, F>(d, L, vals, smem + SmemGrad<R, GV>::red_off, R);
-  if constexpr (F) store();
+  });
 }
 
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
-// linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old.
-template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) void k_hess(Dev d) {
+// linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old;
+// partial <delta, Hdelta>.
+template <int R, int RW>
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   const Ctl& c = d.ctl[L.l];
@@ -1447,8 +951,7 @@ __global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) vo
   const double beta = c.beta;
   double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4], S[9];
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-  if constexpr (GV == 9) hinc_gather<R>(d, L, d.z, H, smem);
-  else gather<R, GV, false>(d, L, d.z, nullptr, H, nullptr, smem);
+  hinc_gather<R, RW>(d, L, d.z, H, smem);
   asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
   if (L.valid) {
     load4(d.z + o, zs);
@@ -1461,7 +964,7 @@ __global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) vo
     for (int i = 0; i < 9; ++i) S[i] = 0.0;
   }
   double hz[4];
-  group_rhess<R, GV == 9>(y, zs, H, S, L.base, hz, reinterpret_cast<double*>(smem + SmemH<R>::c_off));
+  group_rhess<R, true>(y, zs, H, S, L.base, hz, reinterpret_cast<double*>(smem));
   double v = 0.0;
   double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
   if (L.valid) {
@@ -1480,21 +983,27 @@ __global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) vo
     }
     v = dl[0] * hdl[0] + dl[1] * hdl[1] + dl[2] * hdl[2] + dl[3] * hdl[3];
   }
-  finish_tile<RED_HESS, 1, F>(d, L, &v, smem + SmemHess<R, GV>::red_off, R);
-  if (L.valid) {
-    store4(d.del + o, dl);
-    store4(d.hd + o, hdl);
-  }
+  Post po;
+  po.slot = slot;
+  finish_tile<RED_HESS, 1>(d, L, &v, smem + SmemH<R>::red_off, R, [&]() {
+    if (L.valid) {
+      store4(d.del + o, dl);
+      store4(d.hd + o, hdl);
+    }
+  }, po);
 }
 
 // tCG step, part 2: eta += coef delta, r += coef Hdelta; interior steps also
-// z = precon(r) and partial <r,r>, <z,r>.
-template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK) void k_update(Dev d) {
+// z = precon(r) and partials <r,r>, <z,r>.
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   const Ctl& c = d.ctl[L.l];
-  if (c.phase != PH_TCG) return;
+  if (c.phase != PH_TCG) {  // not in tCG: the robot's first tile reports it
+    if (hs && threadIdx.x == 0 && L.tile == d.rtile0[L.l]) post_status(hs, L.l, seq, false);
+    return;
+  }
   const bool first = (c.tcg_iter == 1);
   const double coef = c.coef;
   const bool interior = (c.mode == MODE_INTERIOR);
@@ -1515,18 +1024,22 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d) {
   }
   double vals[2] = {0.0, 0.0}, zr[4] = {0, 0, 0, 0};
   if (interior) {  // uniform per robot
-    group_precon<R, GV == 9>(d, L.pose, L.valid, y, rr, L.base, zr, reinterpret_cast<double*>(smem));
+    group_precon<R, true>(d, L.pose, L.valid, y, rr, L.base, zr, reinterpret_cast<double*>(smem));
     if (L.valid) {
       vals[0] = rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2] + rr[3] * rr[3];
       vals[1] = zr[0] * rr[0] + zr[1] * rr[1] + zr[2] * rr[2] + zr[3] * rr[3];
     }
   }
-  finish_tile<RED_UPDATE, 2, F>(d, L, vals, smem + Smem<R>::red_off, R);
-  if (L.valid) {
-    store4(d.eta + o, et);
-    store4(d.r + o, rr);
-    if (interior) store4(d.z + o, zr);
-  }
+  Post po;
+  po.hs = hs;
+  po.seq = seq;
+  finish_tile<RED_UPDATE, 2>(d, L, vals, smem + SmemU::red_off, R, [&]() {
+    if (L.valid) {
+      store4(d.eta + o, et);
+      store4(d.r + o, rr);
+      if (interior) store4(d.z + o, zr);
+    }
+  }, po);
 }
 
 // Trial point Xt = R_X(eta); partials: model m(eta) = 1/2 <eta, g + r> (r = g +
@@ -1559,99 +1072,112 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
     vals[0] = m;
     vals[1] = ch;
   }
-  double* lds = reinterpret_cast<double*>(smem + Smem<R>::red_off);
+  double* lds = reinterpret_cast<double*>(smem);
+#pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const double t = block_sum(vals[s], lds);
-    if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART + 2 + s] = t;
-  }
-}
-
-// Trial cost, one lane per owner incidence (G = 9): each local edge is
-// visited once by the lane that owns it, which reads the record and both
-// endpoint rows and sums the R rows' residual terms; no per-pose reduction.
-template <int R>
-struct SmemC {
-  static constexpr int TP = WAVES * (64 / R);
-  static constexpr int x_off = 0;                                    // double[TP][R][4] own rows
-  static constexpr int ptr_off = TP * R * 32;                        // int[TP + 1]
-  static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
-  static constexpr int bytes = red_off + RED_BYTES;
-};
-template <int R, int GV>
-struct SmemCost : SmemG<R, GV> {};
-template <int R>
-struct SmemCost<R, 9> : SmemC<R> {};
-
-template <int R>
-__device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, const double* V, const double* pub,
-                                                 char* smem) {
-  int* sptr = reinterpret_cast<int*>(smem + SmemC<R>::ptr_off);
-  double2* xs = reinterpret_cast<double2*>(smem + SmemC<R>::x_off);
-  const int tid = threadIdx.x;
-  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
-  const int K0 = d.optr[p0];
-  const int n = d.optr[p0 + np] - K0;
-  if (tid <= np) sptr[tid] = d.optr[p0 + tid] - K0;
-  {
-    const double2* v2 = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
-    for (int i = tid; i < np * 2 * R; i += BLOCK) xs[i] = v2[i];
+    const double w = wave_sum(vals[s]);
+    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
   }
   __syncthreads();
-  double cost = 0.0;
-  for (int k = tid; k < n; k += BLOCK) {
-    int lo = 0, hi = np;  // owning pose: sptr[lo] <= k < sptr[lo + 1]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (sptr[mid] <= k) lo = mid;
-      else hi = mid;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      double t = 0.0;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
+      d.part[(size_t)L.tile * NPART + 2 + s] = t;
     }
-    const double2* q2 = reinterpret_cast<const double2*>(d.hocrec + 12 * (size_t)(K0 + k));
-    double2 q[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) q[i] = q2[i];
-    const int2 in = unpack_int2(q[5].y);
-    const int o = in.x;
-    const bool tail = (in.y >> 31) & 1;
-    const double2* s2 = xs + lo * 2 * R;  // own row, from LDS
-    const double2* o2 = reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
-    double2 vs2[2 * R], vo2[2 * R];
-#pragma unroll
-    for (int i = 0; i < 2 * R; ++i) { vs2[i] = s2[i]; vo2[i] = o2[i]; }
-    Edge E;
-    edge_from_compact(q, E);
-    double c = 0.0;
-#pragma unroll
-    for (int a = 0; a < R; ++a) {
-      const double vs[4] = {vs2[2 * a].x, vs2[2 * a].y, vs2[2 * a + 1].x, vs2[2 * a + 1].y};
-      const double vo[4] = {vo2[2 * a].x, vo2[2 * a].y, vo2[2 * a + 1].x, vo2[2 * a + 1].y};
-      double dummy[4] = {0.0, 0.0, 0.0, 0.0};
-      c += incidence_row(E, tail, vs, vo, dummy);
-    }
-    cost += c;
   }
-  return cost;
 }
 
-template <int R, int GV, int F>
-__global__ __launch_bounds__(BLOCK, (GV == 7 || GV == 9 ? 4 : KMX_LB_GATHER)) void k_cost(Dev d) {
+template <int R, int RW>
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
-  double acc[4], cost = 0.0;
-  if constexpr (GV == 9) cost = inc_owner_cost<R>(d, L, d.Xt, d.pub, smem);
-  else gather<R, (GV == 3 ? 4 : GV == 5 ? 6 : GV == 7 ? 8 : GV), true>(d, L, d.Xt, d.pub, acc, &cost, smem);
-  finish_tile<RED_COST, 1, F>(d, L, &cost, smem + SmemCost<R, GV>::red_off, R);
+  double cost = inc_owner_cost<R, RW>(d, L, d.Xt, d.pub, smem);
+  finish_tile<RED_COST, 1>(d, L, &cost, smem + SmemC<R>::red_off, R, []() {});
 }
 
+// End of a round: X <- Xt where the step was accepted, and the owned public
+// rows of the committed poses are published (the single-device exchange), so
+// the next round — and a GNC weight update before it — sees the new poses.
+// Tile 0 also counts the round for the GNC schedule.
 template <int R>
 __global__ __launch_bounds__(BLOCK) void k_commit(Dev d) {
   const Lane L = lane_map<R>(d);
-  if (!d.ctl[L.l].commit) return;
-  if (!L.valid) return;
+  if (L.tile == 0 && threadIdx.x == 0) {
+    d.gnc->inner += 1;
+    d.gnc->rounds += 1;
+  }
+  if (!d.ctl[L.l].commit || !L.valid) return;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   double v[4];
   load4(d.Xt + o, v);
   store4(d.X + o, v);
+  const int s = d.pose_slot[L.pose];
+  if (s >= 0) store4(d.pub + (size_t)s * 4 * R + 4 * L.a, v);
+}
+
+// ------------------------------------------------- round begin + GNC-TLS ---
+// shouldUpdateMeasurementWeights (drawio:2466-2469): never for L2 or once
+// robustOptNumWeightUpdates updates were made; otherwise when more than
+// robustOptInnerIters rounds ran since the last update, or when every agent of
+// the team has converged (relative change of its last block update <=
+// relChangeTol; this handle's robots plus the peers' statuses in `ext`).
+__device__ __forceinline__ bool gnc_should_update(const Dev& d) {
+  const Params& P = d.p;
+  if (!P.robust || !P.gnc_on) return false;
+  const Gnc& s = *d.gnc;
+  if (s.updates >= P.max_updates) return false;
+  if (s.inner > P.inner_iters) return true;
+  for (int l = 0; l < d.L; ++l)
+    if (!(d.relc[l] <= P.rel_tol)) return false;
+  for (int k = 0; k < P.n_ext; ++k)
+    if (!(d.ext[k] <= P.rel_tol)) return false;
+  return true;
+}
+
+// TLS weight of one loop closure on the lifted poses (oracle residual_sq and
+// gnc_tls_weight): the owner's and the peer's handles both evaluate a shared
+// loop closure from the same two rows, so both get the owner's value bit for
+// bit without the measurement_weights message (drawio:2195-2198).
+template <int RW>
+__device__ __forceinline__ void gnc_edge(const Dev& d, int i, int R_, double mu) {
+  const int e = d.gnc_edge[i];
+  const int2 en = d.gnc_ends[i];
+  const int ps = 4 * R_;
+  const double* Xi = en.x >= 0 ? d.X + (size_t)en.x * ps : d.pub + (size_t)(-1 - en.x) * ps;
+  const double* Xj = en.y >= 0 ? d.X + (size_t)en.y * ps : d.pub + (size_t)(-1 - en.y) * ps;
+  const int2 ip = d.eipos[e];
+  double2 q[Rec<RW>::Q];
+  Rec<RW>::load(d.rec, (size_t)(ip.x >= 0 ? ip.x : ip.y), q);
+  Edge E;
+  Rec<RW>::edge(q, E);
+  double sR = 0.0, sT = 0.0;
+  for (int a = 0; a < R_; ++a) {
+    const double* yi = Xi + 4 * a;
+    const double* yj = Xj + 4 * a;
+    for (int c = 0; c < 3; ++c) {
+      const double r = yj[c] - (yi[0] * E.R[0 * 3 + c] + yi[1] * E.R[1 * 3 + c] + yi[2] * E.R[2 * 3 + c]);
+      sR += r * r;
+    }
+    const double et = yj[3] - yi[3] - (yi[0] * E.t[0] + yi[1] * E.t[1] + yi[2] * E.t[2]);
+    sT += et * et;
+  }
+  const double rSq = d.ekappa[e] * sR + d.etau[e] * sT;
+  const double barcSq = d.p.barc * d.p.barc;
+  const double upper = (mu + 1.0) / mu * barcSq;
+  const double lower = mu / (mu + 1.0) * barcSq;
+  double w;
+  if (rSq >= upper) w = 0.0;
+  else if (rSq <= lower) w = 1.0;
+  else w = sqrt(barcSq * mu * (mu + 1.0) / rSq) - mu;
+  d.ew[e] = w;
+  const double wk = w * d.ekappa[e], wt = w * d.etau[e];
+  constexpr int WK = Rec<RW>::WK;
+  if (ip.x >= 0) { d.rec[(size_t)RW * ip.x + WK] = wk; d.rec[(size_t)RW * ip.x + WK + 1] = wt; }
+  if (ip.y >= 0) { d.rec[(size_t)RW * ip.y + WK] = wk; d.rec[(size_t)RW * ip.y + WK + 1] = wt; }
 }
 
 __device__ __forceinline__ void begin_robot(const Dev& d, const unsigned char* active, int l) {
@@ -1664,16 +1190,134 @@ __device__ __forceinline__ void begin_robot(const Dev& d, const unsigned char* a
   c.Delta = d.p.Delta0;
 }
 
-__global__ void k_round_begin(Dev d, const unsigned char* active) {
-  const int l = threadIdx.x;
-  if (l >= d.L) return;
-  begin_robot(d, active, l);
+enum BeginMode { BEGIN_ROUND = 1, BEGIN_FORCE_GNC = 2, BEGIN_SOLO = 4 };
+
+// Round begin (BEGIN_ROUND: reset the robots' Ctl) and/or a GNC weight update:
+// scheduled (gnc_should_update) or forced (BEGIN_FORCE_GNC, the explicit
+// updateMeasurementWeights). Every block takes the same decision from the
+// same state; block 0 writes the next state to gnc_next (k_precond commits
+// it), the other blocks re-weight their loop closures and rewrite both
+// incidence records of each.
+template <int RW>
+__global__ void k_begin(Dev d, const unsigned char* active, int mode, int R_) {
+  const bool fire = d.p.robust && ((mode & BEGIN_FORCE_GNC) ? true : gnc_should_update(d));
+  const double mu = d.gnc->mu;
+  if (blockIdx.x == 0) {
+    if (mode & BEGIN_ROUND)
+      for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
+    if (threadIdx.x == 0) {
+      Gnc s = *d.gnc;
+      s.fired = fire ? 1 : 0;
+      if (fire) {
+        s.inner = 0;
+        s.updates += 1;
+        s.mu = mu * d.p.mu_step;
+      }
+      *d.gnc_next = s;
+      if (mode & BEGIN_SOLO) *d.gnc = s;  // one-block launch: no reader of the state is left
+      if (fire) atomicAdd(&d.cnt->gnc_updates, 1ull);
+    }
+    return;
+  }
+  if (!fire) return;
+  const int i = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
+  if (i < d.n_gnc) gnc_edge<RW>(d, i, R_, mu);
 }
 
+// 4x4 diagonal blocks D_i of Q per pose (hD, for the Hessian gather) and the
+// inverse preconditioner blocks (D_i + shift I)^-1 by Cholesky; same
+// accumulation order and expressions as oracle build_precond. `gated`: only
+// after a round-begin launch that re-weighted (then block 0 commits gnc_next).
+template <int RW>
+__global__ void k_precond(Dev d, int gated) {
+  if (gated) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *d.gnc = *d.gnc_next;
+    if (!d.gnc_next->fired) return;
+  }
+  for (int pose = blockIdx.x * blockDim.x + threadIdx.x; pose < d.nloc; pose += gridDim.x * blockDim.x) {
+    // A: the preconditioner's blocks (kappa I for the rotation part, as in the
+    // oracle); Dq: Q's exact diagonal block for the Hessian gather, which with
+    // the full records (measurements off SO(3)) carries w kappa R R^T instead
+    double A[16], Dq[16];
+    for (int i = 0; i < 16; ++i) A[i] = Dq[i] = 0.0;
+    for (int k = d.inc_ptr[pose]; k < d.inc_ptr[pose + 1]; ++k) {
+      double2 q[Rec<RW>::Q];
+      Rec<RW>::load(d.rec, (size_t)k, q);
+      Edge E;
+      Rec<RW>::edge(q, E);
+      const bool tail = (Rec<RW>::inc(q).y >> 31) & 1;
+      const double wk = E.wk, wt = E.wt;
+      const double* tt = E.t;
+      if (tail) {
+        for (int i = 0; i < 3; ++i) {
+          for (int j = 0; j < 3; ++j) {
+            A[i * 4 + j] += wt * tt[i] * tt[j] + (i == j ? wk : 0.0);
+            const double rr = (RW == 12) ? (i == j ? 1.0 : 0.0)
+                                         : E.R[i * 3 + 0] * E.R[j * 3 + 0] + E.R[i * 3 + 1] * E.R[j * 3 + 1] +
+                                               E.R[i * 3 + 2] * E.R[j * 3 + 2];
+            Dq[i * 4 + j] += wt * tt[i] * tt[j] + wk * rr;
+          }
+          A[i * 4 + 3] += wt * tt[i];
+          A[3 * 4 + i] += wt * tt[i];
+          Dq[i * 4 + 3] += wt * tt[i];
+          Dq[3 * 4 + i] += wt * tt[i];
+        }
+        A[15] += wt;
+        Dq[15] += wt;
+      } else {
+        A[0] += wk; A[5] += wk; A[10] += wk; A[15] += wt;
+        Dq[0] += wk; Dq[5] += wk; Dq[10] += wk; Dq[15] += wt;
+      }
+    }
+    for (int i = 0; i < 16; ++i) d.hD[16 * (size_t)pose + i] = Dq[i];
+    for (int j = 0; j < 4; ++j) A[j * 5] += d.p.shift;
+    double Lm[16], Li[16];
+    for (int i = 0; i < 16; ++i) { Lm[i] = 0.0; Li[i] = 0.0; }
+    for (int j = 0; j < 4; ++j) {
+      double s = A[j * 4 + j];
+      for (int k = 0; k < j; ++k) s -= Lm[j * 4 + k] * Lm[j * 4 + k];
+      Lm[j * 4 + j] = sqrt(s);
+      for (int ii = j + 1; ii < 4; ++ii) {
+        double t = A[ii * 4 + j];
+        for (int k = 0; k < j; ++k) t -= Lm[ii * 4 + k] * Lm[j * 4 + k];
+        Lm[ii * 4 + j] = t / Lm[j * 4 + j];
+      }
+    }
+    for (int c = 0; c < 4; ++c)
+      for (int ii = 0; ii < 4; ++ii) {
+        double s = (ii == c) ? 1.0 : 0.0;
+        for (int k = c; k < ii; ++k) s -= Lm[ii * 4 + k] * Li[k * 4 + c];
+        Li[ii * 4 + c] = (ii < c) ? 0.0 : s / Lm[ii * 4 + ii];
+      }
+    double* Pi = d.Pinv + 16 * (size_t)pose;
+    for (int x = 0; x < 4; ++x)
+      for (int y = 0; y < 4; ++y) {
+        double s = 0.0;
+        for (int k = 0; k < 4; ++k) s += Li[k * 4 + x] * Li[k * 4 + y];
+        Pi[x * 4 + y] = s;
+      }
+  }
+}
+
+// setMeasurementWeight in bulk: push the per-edge weights into both incidence
+// records (w kappa, w tau).
+template <int RW>
+__global__ void k_apply_weights(Dev d, int mloc) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= mloc) return;
+  const double w = d.ew[e];
+  const double wk = w * d.ekappa[e], wt = w * d.etau[e];
+  const int2 ip = d.eipos[e];
+  constexpr int WK = Rec<RW>::WK;
+  if (ip.x >= 0) { d.rec[(size_t)RW * ip.x + WK] = wk; d.rec[(size_t)RW * ip.x + WK + 1] = wt; }
+  if (ip.y >= 0) { d.rec[(size_t)RW * ip.y + WK] = wk; d.rec[(size_t)RW * ip.y + WK + 1] = wt; }
+}
+
+// ------------------------------------------------------- public exchange ---
 // One 16-B part i of the owned public rows: slot s = i / (ps / 2) (ps = 4r is
 // even, rows are 16-B aligned).
-__device__ __forceinline__ void publish_part(const double* X, double* pub, const int* src, int nslots, int ps,
-                                             long long i) {
+__global__ void k_publish(const double* X, double* pub, const int* src, int nslots, int ps) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int ps2 = ps >> 1;
   const long long s = i / ps2;
   if (s >= nslots) return;
@@ -1683,43 +1327,50 @@ __device__ __forceinline__ void publish_part(const double* X, double* pub, const
     reinterpret_cast<double2*>(pub)[s * ps2 + q] = reinterpret_cast<const double2*>(X)[(long long)p * ps2 + q];
 }
 
-// Round start fused with k_publish (iterate_async with refresh_local): block 0
-// activates the robots, the other blocks copy the owned public rows. The two
-// touch disjoint data, so one launch replaces two.
-__global__ void k_round_begin_pub(Dev d, const unsigned char* active, const double* X, double* pub, const int* src,
-                                  int nslots, int ps) {
-  if (blockIdx.x == 0) {
-    for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
-    return;
-  }
-  publish_part(X, pub, src, nslots, ps, (long long)(blockIdx.x - 1) * blockDim.x + threadIdx.x);
-}
-
-__global__ void k_publish(const double* X, double* pub, const int* src, int nslots, int ps) {
-  publish_part(X, pub, src, nslots, ps, (long long)blockIdx.x * blockDim.x + threadIdx.x);
-}
-
 // Sparse exchange: rows of the given public slots (owned by this handle) from
-// the iterate, and rows received from peers written into the table.
-// A slot outside the table (or, for gather, not owned here) is skipped
-// (gather writes zeros), so a bad index list cannot fault the device.
+// the iterate, and rows received from peers written into the table. With
+// per-peer segments (nseg > 0, seg[k] = first row of peer k's segment), every
+// segment is followed by one status double (this handle's largest relative
+// change, dpgo's Status message, drawio:2375): segment k starts at row
+// seg[k] * ps + k. A slot outside the table (or, for gather, not owned here)
+// is skipped (gather writes zeros), so a bad index list cannot fault the device.
+__device__ __forceinline__ long long seg_offset(const int* seg, int nseg, long long s) {
+  int k = 0;
+  while (k + 1 < nseg && seg[k + 1] <= s) ++k;
+  return nseg > 0 ? k : 0;
+}
 __global__ void k_gather_slots(const double* X, const int* pub_src, const int* slots, long long n, int npub,
-                               double* out, int ps) {
+                               double* out, int ps, const int* seg, int nseg) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long s = i / ps;
   if (s >= n) return;
   const int q = (int)(i - s * ps);
   const int sl = slots[s];
   const int p = (sl >= 0 && sl < npub) ? pub_src[sl] : -1;
-  out[i] = (p >= 0) ? X[(long long)p * ps + q] : 0.0;
+  out[i + seg_offset(seg, nseg, s)] = (p >= 0) ? X[(long long)p * ps + q] : 0.0;
 }
-__global__ void k_scatter_slots(double* pub, const int* slots, long long n, int npub, const double* rows, int ps) {
+__global__ void k_scatter_slots(double* pub, const int* slots, long long n, int npub, const double* rows, int ps,
+                                const int* seg, int nseg) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long s = i / ps;
   if (s >= n) return;
   const int q = (int)(i - s * ps);
   const int sl = slots[s];
-  if (sl >= 0 && sl < npub) pub[(long long)sl * ps + q] = rows[i];
+  if (sl >= 0 && sl < npub) pub[(long long)sl * ps + q] = rows[i + seg_offset(seg, nseg, s)];
+}
+// status words: write this handle's max relative change after every segment
+// (pack) / read the peers' into ext (unpack)
+__global__ void k_status_pack(const double* relc, int L, double* out, const int* seg, int nseg, int ps) {
+  const int k = threadIdx.x;
+  if (k >= nseg) return;
+  double m = 0.0;
+  for (int l = 0; l < L; ++l) m = (relc[l] > m || relc[l] != relc[l]) ? relc[l] : m;
+  out[(long long)seg[k + 1] * ps + k] = m;
+}
+__global__ void k_status_unpack(const double* in, double* ext, const int* seg, int nseg, int ps) {
+  const int k = threadIdx.x;
+  if (k >= nseg) return;
+  ext[k] = in[(long long)seg[k + 1] * ps + k];
 }
 
 __global__ void k_pack(const double* X, double* out, const int* src, int first, int count, int ps) {
@@ -1728,124 +1379,6 @@ __global__ void k_pack(const double* X, double* out, const int* src, int first, 
   if (s >= count) return;
   const int q = (int)(i - s * ps);
   out[s * ps + q] = X[(long long)src[first + s] * ps + q];
-}
-
-// 4x4 diagonal blocks of Q (+ shift) per pose, Cholesky-inverted. Same
-// accumulation order and expressions as oracle build_precond.
-__global__ void k_precond(Dev d) {
-  const int pose = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pose >= d.nloc) return;
-  double A[16];
-  for (int i = 0; i < 16; ++i) A[i] = 0.0;
-  for (int k = d.inc_ptr[pose]; k < d.inc_ptr[pose + 1]; ++k) {
-    const int2 in = d.inc[k];
-    const bool tail = (in.y >> 31) & 1;
-    const double* er = d.irec + 16 * (size_t)k;
-    const double wk = er[12], wt = er[13];
-    const double* tt = er + 9;
-    if (tail) {
-      for (int i = 0; i < 3; ++i) {
-        for (int j = 0; j < 3; ++j) A[i * 4 + j] += wt * tt[i] * tt[j] + (i == j ? wk : 0.0);
-        A[i * 4 + 3] += wt * tt[i];
-        A[3 * 4 + i] += wt * tt[i];
-      }
-      A[15] += wt;
-    } else {
-      A[0] += wk; A[5] += wk; A[10] += wk; A[15] += wt;
-    }
-  }
-  if (d.hD)
-    for (int i = 0; i < 16; ++i) d.hD[16 * (size_t)pose + i] = A[i];
-  for (int j = 0; j < 4; ++j) A[j * 5] += d.p.shift;
-  double Lm[16], Li[16];
-  for (int i = 0; i < 16; ++i) { Lm[i] = 0.0; Li[i] = 0.0; }
-  for (int j = 0; j < 4; ++j) {
-    double s = A[j * 4 + j];
-    for (int k = 0; k < j; ++k) s -= Lm[j * 4 + k] * Lm[j * 4 + k];
-    Lm[j * 4 + j] = sqrt(s);
-    for (int ii = j + 1; ii < 4; ++ii) {
-      double t = A[ii * 4 + j];
-      for (int k = 0; k < j; ++k) t -= Lm[ii * 4 + k] * Lm[j * 4 + k];
-      Lm[ii * 4 + j] = t / Lm[j * 4 + j];
-    }
-  }
-  for (int c = 0; c < 4; ++c)
-    for (int ii = 0; ii < 4; ++ii) {
-      double s = (ii == c) ? 1.0 : 0.0;
-      for (int k = c; k < ii; ++k) s -= Lm[ii * 4 + k] * Li[k * 4 + c];
-      Li[ii * 4 + c] = (ii < c) ? 0.0 : s / Lm[ii * 4 + ii];
-    }
-  double* Pi = d.Pinv + 16 * (size_t)pose;
-  for (int x = 0; x < 4; ++x)
-    for (int y = 0; y < 4; ++y) {
-      double s = 0.0;
-      for (int k = 0; k < 4; ++k) s += Li[k * 4 + x] * Li[k * 4 + y];
-      Pi[x * 4 + y] = s;
-    }
-}
-
-// GNC-TLS weight sweep over owned non-fixed local edges (owner's view of the
-// endpoints: its own robot from X, the other robot from the public table).
-__global__ void k_gnc(Dev d, const int* gnc_edge, const int2* gnc_ends, int n, int R_, double mu, double barc) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int e = gnc_edge[i];
-  const int2 en = gnc_ends[i];
-  const int ps = 4 * R_;
-  const double* Xi = en.x >= 0 ? d.X + (size_t)en.x * ps : d.pub + (size_t)(-1 - en.x) * ps;
-  const double* Xj = en.y >= 0 ? d.X + (size_t)en.y * ps : d.pub + (size_t)(-1 - en.y) * ps;
-  const int2 ip = d.eipos[e];
-  const double* er = d.irec + 16 * (size_t)(ip.x >= 0 ? ip.x : ip.y);
-  const double* Rt = er;
-  const double* tt = er + 9;
-  double sR = 0.0, sT = 0.0;
-  for (int a = 0; a < R_; ++a) {
-    const double* yi = Xi + 4 * a;
-    const double* yj = Xj + 4 * a;
-    for (int c = 0; c < 3; ++c) {
-      const double q = yj[c] - (yi[0] * Rt[0 * 3 + c] + yi[1] * Rt[1 * 3 + c] + yi[2] * Rt[2 * 3 + c]);
-      sR += q * q;
-    }
-    const double et = yj[3] - yi[3] - (yi[0] * tt[0] + yi[1] * tt[1] + yi[2] * tt[2]);
-    sT += et * et;
-  }
-  const double rSq = d.ekappa[e] * sR + d.etau[e] * sT;
-  const double barcSq = barc * barc;
-  const double upper = (mu + 1.0) / mu * barcSq;
-  const double lower = mu / (mu + 1.0) * barcSq;
-  double w;
-  if (rSq >= upper) w = 0.0;
-  else if (rSq <= lower) w = 1.0;
-  else w = sqrt(barcSq * mu * (mu + 1.0) / rSq) - mu;
-  d.ew[e] = w;
-}
-
-// Push the per-edge weights into both incidence copies (w*kappa, w*tau).
-__global__ void k_apply_weights(Dev d, int mloc) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= mloc) return;
-  const double w = d.ew[e];
-  const double wk = w * d.ekappa[e], wt = w * d.etau[e];
-  const int2 ip = d.eipos[e];
-  if (ip.x >= 0) { d.irec[16 * (size_t)ip.x + 12] = wk; d.irec[16 * (size_t)ip.x + 13] = wt; }
-  if (ip.y >= 0) { d.irec[16 * (size_t)ip.y + 12] = wk; d.irec[16 * (size_t)ip.y + 13] = wt; }
-  if (d.hocrec) {
-    const int2 hp = d.heopos[e];
-    if (hp.x >= 0) { d.hocrec[12 * (size_t)hp.x + 9] = wk; d.hocrec[12 * (size_t)hp.x + 10] = wt; }
-    if (hp.y >= 0) { d.hocrec[12 * (size_t)hp.y + 9] = wk; d.hocrec[12 * (size_t)hp.y + 10] = wt; }
-  }
-  if (d.hrec) {  // CSR order: the incidence positions
-    if (ip.x >= 0) { d.hrec[12 * (size_t)ip.x + 9] = wk; d.hrec[12 * (size_t)ip.x + 10] = wt; }
-    if (ip.y >= 0) { d.hrec[12 * (size_t)ip.y + 9] = wk; d.hrec[12 * (size_t)ip.y + 10] = wt; }
-  }
-  if (d.crec) {
-    const int2 cp = d.cipos[e];
-    if (cp.x >= 0) { d.crec[12 * (size_t)cp.x + 9] = wk; d.crec[12 * (size_t)cp.x + 10] = wt; }
-    if (cp.y >= 0) { d.crec[12 * (size_t)cp.y + 9] = wk; d.crec[12 * (size_t)cp.y + 10] = wt; }
-    const int2 op = d.eopos[e];
-    if (op.x >= 0) { d.ocrec[12 * (size_t)op.x + 9] = wk; d.ocrec[12 * (size_t)op.x + 10] = wt; }
-    if (op.y >= 0) { d.ocrec[12 * (size_t)op.y + 9] = wk; d.ocrec[12 * (size_t)op.y + 10] = wt; }
-  }
 }
 
 __global__ void k_shared_pack(const double* ew, const int* sh_edge, const int* sh_idx, int n, double* out) {
@@ -1923,7 +1456,8 @@ __global__ void k_traj(const double* X, int n, int R_, const double* anchor, dou
   for (int k = 0; k < 3; ++k) {
     const double sig = sqrt(fmax(A[k * 4], 0.0));
     double u[3];
-    for (int q = 0; q < 3; ++q) u[q] = (M[q * 3 + 0] * V[0 * 3 + k] + M[q * 3 + 1] * V[1 * 3 + k] + M[q * 3 + 2] * V[2 * 3 + k]) / sig;
+    for (int q = 0; q < 3; ++q)
+      u[q] = (M[q * 3 + 0] * V[0 * 3 + k] + M[q * 3 + 1] * V[1 * 3 + k] + M[q * 3 + 2] * V[2 * 3 + k]) / sig;
     const double s = (k == kmin && det < 0.0) ? -1.0 : 1.0;
     for (int a = 0; a < 3; ++a)
       for (int b = 0; b < 3; ++b) Rr[a * 3 + b] += s * u[a] * V[b * 3 + k];
@@ -1933,38 +1467,47 @@ __global__ void k_traj(const double* X, int n, int R_, const double* anchor, dou
   o[9] = tv[0]; o[10] = tv[1]; o[11] = tv[2];
 }
 
-// Primitive evaluation for parity tests (tiles of one robot).
-template <int R, int GV>
-__global__ __launch_bounds__(BLOCK) void k_eval(Dev d, int robot, int mode, const double* V, double* out) {
+// Primitive evaluation for parity tests (tiles of one robot), through the same
+// gathers as the round kernels.
+template <int R>
+struct SmemE {
+  static constexpr int g = SmemHG<R>::red_off > SmemH<R>::red_off ? SmemHG<R>::red_off : SmemH<R>::red_off;
+  static constexpr int red_off = g;
+  static constexpr int bytes = red_off + RED_BYTES;
+};
+template <int R, int RW>
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_eval(Dev d, int robot, int mode, const double* V, double* out) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (L.l != robot) return;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   double res[4] = {0, 0, 0, 0}, cost = 0.0, v[4] = {0, 0, 0, 0};
+  double* scr = reinterpret_cast<double*>(smem);
   if (mode == KMX_EVAL_COST_EGRAD) {
-    gather<R, GV, true>(d, L, V, d.pub, res, &cost, smem);
+    hinc_grad<R, RW>(d, L, V, d.pub, res, &cost, smem);
   } else if (mode == KMX_EVAL_EHESS) {
-    gather<R, GV, false>(d, L, V, nullptr, res, nullptr, smem);
+    hinc_gather<R, RW>(d, L, V, res, smem);
     if (L.valid) load4(V + o, v);
   } else {
-    double y[4] = {0, 0, 0, 0}, G[4];
-    gather<R, GV, true>(d, L, d.X, d.pub, G, nullptr, smem);
+    double y[4] = {0, 0, 0, 0}, G[4], c0 = 0.0;
+    hinc_grad<R, RW>(d, L, d.X, d.pub, G, &c0, smem);
     if (L.valid) {
       load4(d.X + o, y);
       load4(V + o, v);
     }
     double S[9];
-    group_symYtG<R>(y, G, L.base, S);
+    group_symYtG<R, true>(y, G, L.base, S, scr);
     if (mode == KMX_EVAL_RGRAD) {
       for (int c = 0; c < 3; ++c) res[c] = G[c] - (y[0] * S[0 * 3 + c] + y[1] * S[1 * 3 + c] + y[2] * S[2 * 3 + c]);
       res[3] = G[3];
       for (int k = 0; k < 4; ++k) v[k] = res[k];
     } else if (mode == KMX_EVAL_RHESS) {
+      __syncthreads();  // the scratch reads are done before the next gather reuses the LDS
       double H[4];
-      gather<R, GV, false>(d, L, V, nullptr, H, nullptr, smem);
-      group_rhess<R>(y, v, H, S, L.base, res);
+      hinc_gather<R, RW>(d, L, V, H, smem);
+      group_rhess<R, true>(y, v, H, S, L.base, res, scr);
     } else if (mode == KMX_EVAL_PRECON) {
-      group_precon<R>(d, L.pose, L.valid, y, v, L.base, res);
+      group_precon<R, true>(d, L.pose, L.valid, y, v, L.base, res, scr);
     } else if (mode == KMX_EVAL_RETRACT) {
       group_retract<R>(y, v, L.base, res);
       for (int k = 0; k < 4; ++k) v[k] = 0.0;
@@ -1975,231 +1518,18 @@ __global__ __launch_bounds__(BLOCK) void k_eval(Dev d, int robot, int mode, cons
     store4(out + o, res);
     if (mode != KMX_EVAL_COST_EGRAD) s = v[0] * res[0] + v[1] * res[1] + v[2] * res[2] + v[3] * res[3];
   }
-  const double t = block_sum(s, reinterpret_cast<double*>(smem + SmemG<R, GV>::red_off));
+  const double t = block_sum(s, reinterpret_cast<double*>(smem + SmemE<R>::red_off));
   if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
-}
-
-// Diagnostic ablation of the plain direct gather: ABL bit0 -> every edge load
-// reads record 0 (cache-resident), bit1 -> neighbour row = own row.
-template <int R, int ABL>
-__global__ __launch_bounds__(BLOCK) void k_gablate(Dev d, const double* V, double* out) {
-  KMX_SMEM;
-  const Lane L = lane_map<R>(d);
-  double acc[4] = {0, 0, 0, 0}, cost = 0.0;
-  if (L.valid) {
-    double vs[4];
-    load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
-    const int k0 = d.inc_ptr[L.pose], k1 = d.inc_ptr[L.pose + 1];
-    for (int k = k0; k < k1; ++k) {
-      int2 in = d.inc[k];
-      if (ABL & 2) in.x = L.pose;
-      EdgeRaw w;
-      double2 b0, b1;
-      fetch_incidence<R, true>(d, V, d.pub, L.a, (ABL & 1) ? 0 : k, in, w, b0, b1);
-      Edge E;
-      edge_from_raw(w, E);
-      const double vo[4] = {b0.x, b0.y, b1.x, b1.y};
-      cost += incidence_row(E, (in.y >> 31) & 1, vs, vo, acc);
-    }
-    store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
-  }
-  const double t = block_sum(cost, reinterpret_cast<double*>(smem + Smem<R>::red_off));
-  if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
-}
-
-// Diagnostic: the compact gather with each pose's incidence loop capped at CAP
-// (wrong results; bounds what a degree-balanced gather could gain).
-template <int R, int CAP>
-__global__ __launch_bounds__(BLOCK) void k_gcap(Dev d, const double* V, double* out) {
-  KMX_SMEM;
-  const Lane L = lane_map<R>(d);
-  double acc[4] = {0, 0, 0, 0}, cost = 0.0;
-  if (L.valid) {
-    double vs[4];
-    load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
-    const int k0 = d.inc_ptr[L.pose], k1 = min(d.inc_ptr[L.pose + 1], k0 + CAP);
-    for (int k = k0; k < k1; ++k) {
-      const double2* q2 = reinterpret_cast<const double2*>(d.crec + 12 * (size_t)k);
-      double2 q[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) q[i] = q2[i];
-      const int2 in = unpack_int2(q[5].y);
-      const int o = in.x;
-      const double* base = (o >= 0) ? V + (size_t)o * 4 * R : d.pub + (size_t)(-1 - o) * 4 * R;
-      const double2* b2 = reinterpret_cast<const double2*>(base + 4 * L.a);
-      const double2 v0 = b2[0], v1 = b2[1];
-      Edge E;
-      edge_from_compact(q, E);
-      const double vo[4] = {v0.x, v0.y, v1.x, v1.y};
-      cost += incidence_row(E, (in.y >> 31) & 1, vs, vo, acc);
-    }
-    store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
-  }
-  const double t = block_sum(cost, reinterpret_cast<double*>(smem + Smem<R>::red_off));
-  if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
-}
-
-// Diagnostic: the gather primitive alone (as in k_cost), for A/B timing of
-// gather variants and occupancy bounds (kmx_pgo_debug_gather_bench).
-template <int R, int GV, int LBW>
-__global__ __launch_bounds__(BLOCK, LBW) void k_gbench(Dev d, const double* V, double* out) {
-  KMX_SMEM;
-  const Lane L = lane_map<R>(d);
-  double acc[4], cost = 0.0;
-  gather<R, GV, true>(d, L, V, d.pub, acc, &cost, smem);
-  if (L.valid) store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
-  const double t = block_sum(cost, reinterpret_cast<double*>(smem + SmemG<R, GV>::red_off));
-  if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
-}
-
-// 4x4 diagonal blocks D_i of Q per pose (k_precond's accumulation, no shift).
-__global__ void k_diag(Dev d, double* D) {
-  const int pose = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pose >= d.nloc) return;
-  double A[16];
-  for (int i = 0; i < 16; ++i) A[i] = 0.0;
-  for (int k = d.inc_ptr[pose]; k < d.inc_ptr[pose + 1]; ++k) {
-    const bool tail = (d.inc[k].y >> 31) & 1;
-    const double* er = d.irec + 16 * (size_t)k;
-    const double wk = er[12], wt = er[13];
-    const double* tt = er + 9;
-    if (tail) {
-      for (int i = 0; i < 3; ++i) {
-        for (int j = 0; j < 3; ++j) A[i * 4 + j] += wt * tt[i] * tt[j] + (i == j ? wk : 0.0);
-        A[i * 4 + 3] += wt * tt[i];
-        A[3 * 4 + i] += wt * tt[i];
-      }
-      A[15] += wt;
-    } else {
-      A[0] += wk; A[5] += wk; A[10] += wk; A[15] += wt;
-    }
-  }
-  for (int i = 0; i < 16; ++i) D[16 * (size_t)pose + i] = A[i];
-}
-
-// Prototype (diagnostic, G = 9): lane per incidence. out_i = D_i v_i +
-// sum_{e at i} B_e v_other(e): the off-diagonal block of every incidence is
-// applied by one lane to all R rows of the other endpoint (no per-row record
-// redundancy), the R x 4 results go to LDS, and the (pose, row) lanes add
-// their pose's incidences in CSR order. REC 0: 128-B records + inc; REC 1:
-// 96-B compact records (CSR order, KMX_RECT=0).
-template <int R, int REC, int CH>
-__global__ __launch_bounds__(BLOCK, 4) void k_hinc(Dev d, const double* V, const double* Dg, double* out) {
-  extern __shared__ __attribute__((aligned(16))) double hsm[];
-  double* Cs = hsm;                                    // [CH][R][4]
-  int* sptr = reinterpret_cast<int*>(hsm + CH * R * 4);  // [TP + 1]
-  const Lane L = lane_map<R>(d);
-  const int tid = threadIdx.x;
-  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
-  const int K0 = d.inc_ptr[p0];
-  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
-  __syncthreads();
-  const int n = sptr[np];
-  const int pl = L.pose - p0;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int c0 = 0; c0 < n; c0 += CH) {
-    const int k = c0 + tid;
-    if (tid < CH && k < n) {
-      double Rm[9], t[3], wk, wt;
-      int o;
-      bool tail;
-      if constexpr (REC == 0) {
-        const double2* q2 = reinterpret_cast<const double2*>(d.irec + 16 * (size_t)(K0 + k));
-        double2 q[7];
-#pragma unroll
-        for (int i = 0; i < 7; ++i) q[i] = q2[i];
-        const int2 in = d.inc[K0 + k];
-        Rm[0] = q[0].x; Rm[1] = q[0].y; Rm[2] = q[1].x; Rm[3] = q[1].y; Rm[4] = q[2].x;
-        Rm[5] = q[2].y; Rm[6] = q[3].x; Rm[7] = q[3].y; Rm[8] = q[4].x;
-        t[0] = q[4].y; t[1] = q[5].x; t[2] = q[5].y;
-        wk = q[6].x; wt = q[6].y;
-        o = in.x; tail = (in.y >> 31) & 1;
-      } else {
-        const double2* q2 = reinterpret_cast<const double2*>(d.crec + 12 * (size_t)(K0 + k));
-        double2 q[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) q[i] = q2[i];
-        Edge E;
-        edge_from_compact(q, E);
-        const int2 in = unpack_int2(q[5].y);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Rm[i] = E.R[i];
-        t[0] = E.t[0]; t[1] = E.t[1]; t[2] = E.t[2];
-        wk = E.wk; wt = E.wt;
-        o = in.x; tail = (in.y >> 31) & 1;
-      }
-      const double* base = (o >= 0) ? V + (size_t)o * 4 * R : d.pub + (size_t)(-1 - o) * 4 * R;
-      const double2* b2 = reinterpret_cast<const double2*>(base);
-      double2 vr[2 * R];
-#pragma unroll
-      for (int i = 0; i < 2 * R; ++i) vr[i] = b2[i];
-#pragma unroll
-      for (int a = 0; a < R; ++a) {
-        const double v0 = vr[2 * a].x, v1 = vr[2 * a].y, v2 = vr[2 * a + 1].x, v3 = vr[2 * a + 1].y;
-        double h[4];
-        if (tail) {
-#pragma unroll
-          for (int c = 0; c < 3; ++c) h[c] = -(wk * (v0 * Rm[c * 3 + 0] + v1 * Rm[c * 3 + 1] + v2 * Rm[c * 3 + 2]) + wt * v3 * t[c]);
-          h[3] = -(wt * v3);
-        } else {
-#pragma unroll
-          for (int c = 0; c < 3; ++c) h[c] = -(wk * (v0 * Rm[0 * 3 + c] + v1 * Rm[1 * 3 + c] + v2 * Rm[2 * 3 + c]));
-          h[3] = -(wt * (v3 + (v0 * t[0] + v1 * t[1] + v2 * t[2])));
-        }
-        store4(Cs + (tid * R + a) * 4, h);
-      }
-    }
-    __syncthreads();
-    if (L.valid) {
-      const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
-      for (int j = j0; j < j1; ++j) {
-        double h[4];
-        load4(Cs + (j * R + L.a) * 4, h);
-        acc[0] += h[0]; acc[1] += h[1]; acc[2] += h[2]; acc[3] += h[3];
-      }
-    }
-    __syncthreads();
-  }
-  if (L.valid) {
-    const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-    double vs[4];
-    load4(V + o, vs);
-    const double* Dp = Dg + 16 * (size_t)L.pose;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      double dr[4];
-      load4(Dp + 4 * c, dr);
-      acc[c] += vs[0] * dr[0] + vs[1] * dr[1] + vs[2] * dr[2] + vs[3] * dr[3];
-    }
-    store4(out + o, acc);
-  }
-}
-
-// Diagnostic: the product G = 9 Hessian gather alone (needs the handle's
-// incidence-parallel records, i.e. KMX_HINC on).
-template <int R, bool GRAD>
-__global__ __launch_bounds__(BLOCK, 4) void k_gbench_hinc(Dev d, const double* V, double* out) {
-  KMX_SMEM;
-  const Lane L = lane_map<R>(d);
-  double acc[4], cost = 0.0;
-  if constexpr (GRAD) hinc_grad<R>(d, L, V, d.pub, acc, &cost, smem);
-  else hinc_gather<R>(d, L, V, acc, smem);
-  if (L.valid) store4(out + (size_t)L.pose * 4 * R + 4 * L.a, acc);
-  if constexpr (GRAD) {
-    const double t = block_sum(cost, reinterpret_cast<double*>(smem + SmemHG<R>::red_off));
-    if (threadIdx.x == 0) d.part[(size_t)L.tile * NPART] = t;
-  }
 }
 
 }  // namespace
 
-// ============================================================== handle ====
+// ============================================================ handle =====
 struct kmx_pgo {
   kmx_pgo_params P{};
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  bool have_graph = false;
   // team
   int n_robots = 0;
   std::vector<int> npose;
@@ -2214,65 +1544,56 @@ struct kmx_pgo {
   // local edges
   int mloc = 0;
   std::vector<int64_t> loc_edge_gid;
-  std::vector<double> ek_h, et_h;  // per local edge kappa / tau
   int ninc = 0;
+  int rw = 12;  // record width (12 compact / 16 full)
   int64_t nshared = 0;
-  int n_sh_local = 0, n_gnc = 0;
+  int n_sh_local = 0, n_gnc = 0, n_osh = 0;
   std::vector<long long> m_robot;
-  int ntiles = 0, tile_poses = 0;
+  int ntiles = 0;
   std::vector<int> rt0_h;  // [L + 1] first tile of each local robot
-  double mu = 0.0;
-  long long round_counter = 0;
+  // GNC schedule (host copy of the parameters)
+  int gnc_on = 0, gnc_inner_iters = 20, gnc_max_updates = 0x7fffffff, n_ext = 0;
+  double gnc_rel_tol = 1e-3;
   // device
   Dev dv{};
   int *d_tile_robot = nullptr, *d_tile_p0 = nullptr, *d_tile_np = nullptr, *d_rtile0 = nullptr;
   int* d_inc_ptr = nullptr;
-  int2* d_inc = nullptr;
-  double* d_irec = nullptr;
-  double* d_crec = nullptr;  // compact records (gather variant 3), null when not usable
-  double* d_ocrec = nullptr;
-  bool hinc = false;  // k_hess runs the incidence-parallel gather (G = 9)
-  bool publish_in_begin = false;  // the next enqueue_round also publishes the owned rows
-  double* d_hrec = nullptr;
-  double* d_hD = nullptr;
-  double* d_hocrec = nullptr;
-  int2* d_heopos = nullptr;
-  int* d_optr = nullptr;
-  int2* d_eopos = nullptr;
-  bool compact_ok = false;
-  bool rect = false;                // crec / ocrec in segment-major order (G = 5)
-  int* d_trec0 = nullptr;
-  int* d_torec0 = nullptr;
-  int2* d_cipos = nullptr;
+  double* d_rec = nullptr;
   double *d_ekappa = nullptr, *d_etau = nullptr, *d_ew = nullptr;
   int2* d_eipos = nullptr;
   double* d_vec = nullptr;  // X Xt g r z eta del hd
-  double *d_S = nullptr, *d_Pinv = nullptr, *d_pub = nullptr, *d_part = nullptr;
+  double *d_S = nullptr, *d_Pinv = nullptr, *d_hD = nullptr, *d_pub = nullptr, *d_part = nullptr;
   Ctl* d_ctl = nullptr;
   Counters* d_cnt = nullptr;
   unsigned* d_tickets = nullptr;
   long long* d_m_robot = nullptr;
   int* d_n_robot = nullptr;
-  int* d_pub_src = nullptr;  // slot -> local pose (-1 if not local)
-  int* d_own_src = nullptr;  // owned slot k -> local pose (index first_owned + k)
+  int* d_pub_src = nullptr;    // slot -> local pose (-1 if not local)
+  int* d_own_src = nullptr;    // owned slot k -> local pose (index first_owned + k)
+  int* d_pose_slot = nullptr;  // local pose -> owned slot or -1
   int* d_gnc_edge = nullptr;
   int2* d_gnc_ends = nullptr;
   int *d_sh_edge = nullptr, *d_sh_idx = nullptr;
   int *d_osh_edge = nullptr, *d_osh_idx = nullptr;
-  int n_osh = 0;
+  double* d_relc = nullptr;
+  Gnc* d_gnc = nullptr;  // [2]: state, next
+  double* d_ext = nullptr;
+  int ext_cap = 0;
   unsigned char* d_active = nullptr;
-  double* d_scratch = nullptr;  // eval in/out
-  // kernel variants (KMX_GATHER: 0 direct / 1 LDS-staged; KMX_FUSED: 0 separate
-  // reduce launch / 1 last-arriving-tile reduction)
-  int gvar = 2, fvar = 0;
-  int gvar_req = -1;  // KMX_GATHER override; default: 3 when compact records are valid, else 2
-  HostStatus* hstat = nullptr;  // [L] host-mapped tCG progress per local robot
+  double* d_scratch = nullptr;  // eval / trajectory in-out, allocated on first use
+  size_t scratch_cap = 0;
+  // tCG progress polling (see HostStatus)
+  HostStatus* hstat = nullptr;
   int hstat_cap = 0;
   unsigned long long seq = 0;
-  bool poll = true;             // KMX_POLL=0 enqueues every tCG step blindly
+  bool poll = true;          // KMX_POLL=0: enqueue every tCG step (finished robots exit at once)
   bool poll_timeout = false;
   // timing
   bool timing = false;
+  int* d_hv_launch = nullptr;
+  int* d_rgroup0 = nullptr;
+  unsigned* d_gtickets = nullptr;
+  double* d_gpart = nullptr;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
 };
@@ -2289,31 +1610,37 @@ int dalloc(T** p, size_t count) {
 }
 
 void free_dev(kmx_pgo* h) {
-  void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_inc,
-                  h->d_irec, h->d_crec, h->d_ocrec, h->d_optr, h->d_eopos, h->d_ekappa, h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_pub, h->d_part, h->d_ctl, h->d_cnt,
-                  h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src, h->d_gnc_edge, h->d_gnc_ends,
-                  h->d_sh_edge, h->d_sh_idx, h->d_osh_edge, h->d_osh_idx, h->d_active, h->d_scratch, h->d_tickets,
-                  h->d_trec0, h->d_torec0, h->d_cipos, h->d_hrec, h->d_hD, h->d_hocrec, h->d_heopos};
+  void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_rec, h->d_ekappa,
+                  h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_hD, h->d_pub, h->d_part,
+                  h->d_ctl, h->d_cnt, h->d_tickets, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
+                  h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
+                  h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
+                  h->d_rgroup0, h->d_gtickets, h->d_gpart};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
-  h->d_inc = nullptr; h->d_eipos = nullptr; h->d_optr = nullptr; h->d_eopos = nullptr; h->d_irec = h->d_crec = h->d_ocrec = h->d_ekappa = h->d_etau = h->d_ew = nullptr; h->d_vec = h->d_S = h->d_Pinv = h->d_pub = h->d_part = nullptr;
-  h->d_ctl = nullptr; h->d_cnt = nullptr; h->d_m_robot = nullptr; h->d_n_robot = nullptr;
-  h->d_trec0 = h->d_torec0 = nullptr; h->d_cipos = nullptr; h->d_hrec = h->d_hD = nullptr; h->d_hocrec = nullptr; h->d_heopos = nullptr;
-  h->d_pub_src = h->d_own_src = h->d_gnc_edge = nullptr; h->d_gnc_ends = nullptr;
-  h->d_sh_edge = h->d_sh_idx = nullptr; h->d_osh_edge = h->d_osh_idx = nullptr; h->d_active = nullptr; h->d_scratch = nullptr; h->d_tickets = nullptr;
+  h->d_rec = h->d_ekappa = h->d_etau = h->d_ew = nullptr;
+  h->d_eipos = nullptr;
+  h->d_vec = h->d_S = h->d_Pinv = h->d_hD = h->d_pub = h->d_part = nullptr;
+  h->d_ctl = nullptr;
+  h->d_cnt = nullptr;
+  h->d_tickets = nullptr;
+  h->d_m_robot = nullptr;
+  h->d_n_robot = h->d_pub_src = h->d_own_src = h->d_pose_slot = h->d_gnc_edge = nullptr;
+  h->d_gnc_ends = nullptr;
+  h->d_sh_edge = h->d_sh_idx = h->d_osh_edge = h->d_osh_idx = nullptr;
+  h->d_relc = nullptr;
+  h->d_gnc = nullptr;
+  h->d_ext = nullptr;
+  h->ext_cap = 0;
+  h->d_active = nullptr;
+  h->d_scratch = nullptr;
+  h->scratch_cap = 0;
+  h->d_hv_launch = nullptr;
+  h->d_rgroup0 = nullptr;
+  h->d_gtickets = nullptr;
+  h->d_gpart = nullptr;
 }
-
-#define KMX_DISPATCH_R(R_, CALL) \
-  switch (R_) {                  \
-    case 3: { constexpr int RR = 3; CALL; } break; \
-    case 4: { constexpr int RR = 4; CALL; } break; \
-    case 5: { constexpr int RR = 5; CALL; } break; \
-    case 6: { constexpr int RR = 6; CALL; } break; \
-    case 7: { constexpr int RR = 7; CALL; } break; \
-    case 8: { constexpr int RR = 8; CALL; } break; \
-    default: break;              \
-  }
 
 hipEvent_t next_event(kmx_pgo* h) {
   if (h->ev_used == h->ev_pool.size()) {
@@ -2324,8 +1651,46 @@ hipEvent_t next_event(kmx_pgo* h) {
   return h->ev_pool[h->ev_used++];
 }
 
-// Local rows of the public table: this handle's robots own one contiguous
-// slot range [first_owned, first_owned + n_owned).
+bool ready(kmx_pgo* h) { return h && h->d_vec != nullptr; }
+
+// Scratch of the diagnostic / output entry points (not resident with the graph).
+int ensure_scratch(kmx_pgo* h, size_t doubles) {
+  if (doubles <= h->scratch_cap) return 0;
+  if (h->d_scratch) {
+    KMX_HIP(hipStreamSynchronize(h->stream));
+    (void)hipFree(h->d_scratch);
+  }
+  h->d_scratch = nullptr;
+  h->scratch_cap = 0;
+  if (int rc = dalloc(&h->d_scratch, doubles)) return rc;
+  h->scratch_cap = doubles;
+  return 0;
+}
+
+void sync_params(kmx_pgo* h) {
+  Params& p = h->dv.p;
+  p.tcg_max = h->P.tcg_max_iterations;
+  p.rtr_iters = h->P.rtr_iterations;
+  p.use_precond = h->P.use_preconditioner;
+  p.robust = h->P.robust_cost == KMX_COST_GNC_TLS ? 1 : 0;
+  p.kappa = h->P.tcg_kappa;
+  p.theta = h->P.tcg_theta;
+  p.Delta0 = h->P.rtr_initial_radius;
+  p.Delta_max = h->P.rtr_max_radius;
+  p.accept_rho = h->P.rtr_accept_rho;
+  p.gn_tol = h->P.gradnorm_tol;
+  p.shift = h->P.precond_shift;
+  p.barc = h->P.gnc_barc;
+  p.mu_step = h->P.gnc_mu_step;
+  p.rel_tol = h->gnc_rel_tol;
+  p.gnc_on = h->gnc_on;
+  p.inner_iters = h->gnc_inner_iters;
+  p.max_updates = h->gnc_max_updates;
+  p.n_ext = h->n_ext;
+  h->dv.ext = h->d_ext;
+}
+
+// Owned public rows into the table (the single-device exchange).
 void enqueue_publish(kmx_pgo* h) {
   const int ps = 4 * h->P.r;
   const long long tot = h->n_owned * ps;
@@ -2334,123 +1699,94 @@ void enqueue_publish(kmx_pgo* h) {
                      h->d_pub + (size_t)h->first_owned * ps, h->d_pub_src + h->first_owned, (int)h->n_owned, ps);
 }
 
-void enqueue_precond(kmx_pgo* h) {
-  if (h->nloc == 0) return;
-  hipLaunchKernelGGL(k_precond, dim3((h->nloc + 127) / 128), dim3(128), 0, h->stream, h->dv);
+template <int RW>
+void enqueue_precond_t(kmx_pgo* h, int gated) {
+  const int blocks = std::max(1, std::min(1024, (h->nloc + 127) / 128));
+  hipLaunchKernelGGL(k_precond<RW>, dim3(blocks), dim3(128), 0, h->stream, h->dv, gated);
+}
+void enqueue_precond(kmx_pgo* h, int gated) {
+  if (h->rw == 12) enqueue_precond_t<12>(h, gated);
+  else enqueue_precond_t<16>(h, gated);
 }
 
-void enqueue_apply_weights(kmx_pgo* h) {
-  if (h->mloc > 0)
-    hipLaunchKernelGGL(k_apply_weights, dim3((h->mloc + 255) / 256), dim3(256), 0, h->stream, h->dv, h->mloc);
-  enqueue_precond(h);
+// Round begin (mode BEGIN_ROUND) and/or GNC update, then the gated
+// preconditioner rebuild that commits the GNC state.
+void enqueue_begin(kmx_pgo* h, const unsigned char* d_active, int mode) {
+  const bool may_fire = h->P.robust_cost == KMX_COST_GNC_TLS && (h->gnc_on || (mode & BEGIN_FORCE_GNC));
+  if (!may_fire) mode |= BEGIN_SOLO;  // no weight update possible: one block, no preconditioner rebuild
+  const unsigned grid = may_fire ? 1 + (unsigned)((h->n_gnc + 255) / 256) : 1;
+  if (h->rw == 12)
+    hipLaunchKernelGGL(k_begin<12>, dim3(grid), dim3(256), 0, h->stream, h->dv, d_active, mode, h->P.r);
+  else
+    hipLaunchKernelGGL(k_begin<16>, dim3(grid), dim3(256), 0, h->stream, h->dv, d_active, mode, h->P.r);
+  if (may_fire) enqueue_precond(h, 1);
 }
 
-void enqueue_gnc(kmx_pgo* h) {
-  if (h->n_gnc > 0)
-    hipLaunchKernelGGL(k_gnc, dim3((h->n_gnc + 255) / 256), dim3(256), 0, h->stream, h->dv, h->d_gnc_edge,
-                       h->d_gnc_ends, h->n_gnc, h->P.r, h->mu, h->P.gnc_barc);
-  h->mu *= h->P.gnc_mu_step;
-  enqueue_apply_weights(h);
+// Wait until every robot with tiles reported tCG step `seq`; returns whether
+// any robot is still in tCG. A device that stops reporting for 30 s switches
+// the handle to blind enqueueing (every tCG step launched).
+bool wait_running(kmx_pgo* h, unsigned long long seq) {
+  volatile HostStatus* hs = h->hstat;
+  (void)hipStreamQuery(h->stream);  // make sure queued work is submitted
+  const auto t0 = std::chrono::steady_clock::now();
+  bool running = false;
+  for (int l = 0; l < h->dv.L; ++l) {
+    if (h->rt0_h[l + 1] == h->rt0_h[l]) continue;  // no tiles: never in tCG
+    unsigned long long w;
+    while (((w = __atomic_load_n(&hs[l].word, __ATOMIC_ACQUIRE)) >> 1) < seq) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+        h->poll_timeout = true;
+        h->poll = false;
+        return true;
+      }
+    }
+    running |= (w & 1ull) != 0;
+  }
+  return running;
 }
 
-template <int R, int G, int F>
+template <int R, int RW>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   const dim3 grid(h->ntiles), blk(BLOCK);
-  const size_t sm = Smem<R>::bytes, smh = SmemHess<R, G>::bytes,
-               smc = SmemCost<R, G>::bytes, smr = SmemGrad<R, G>::bytes;
-  auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0) {
-    if (!F) hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(BLOCK), 0, h->stream, h->dv, kind, R, hs, seq);
-  };
-  auto tcg_step = [&]() {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (h->timing) {
-      e0 = next_event(h);
-      e1 = next_event(h);
-      (void)hipEventRecord(e0, h->stream);
-    }
-    hipLaunchKernelGGL((k_hess<R, G, F>), grid, blk, smh, h->stream, h->dv);
-    if (h->timing) (void)hipEventRecord(e1, h->stream);
-    red(RED_HESS);
-    hipLaunchKernelGGL((k_update<R, G, F>), grid, blk, sm, h->stream, h->dv);
-    if (h->poll && !F) {  // the per-robot reduction also reports tCG progress
-      h->seq += 1;
-      red(RED_UPDATE, h->hstat, h->seq);
-    } else {
-      red(RED_UPDATE);
-    }
-    return h->seq;
-  };
-  auto wait_running = [&](unsigned long long seq) -> unsigned long long {
-    volatile HostStatus* hs = h->hstat;
-    (void)hipStreamQuery(h->stream);  // make sure queued work is submitted
-    const auto t0 = std::chrono::steady_clock::now();
-    unsigned long long running = 0;
-    for (int l = 0; l < h->dv.L; ++l) {
-      unsigned long long w;
-      while (((w = __atomic_load_n(&hs[l].word, __ATOMIC_ACQUIRE)) >> 1) < seq) {
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
-          h->poll_timeout = true;  // device stalled: stop polling, enqueue blindly
-          h->poll = false;
-          return 1ull;
-        }
-      }
-      running |= w & 1ull;
-    }
-    return running;
-  };
-  const long long npub_el = h->n_owned * 4 * h->P.r;
-  if (h->publish_in_begin && npub_el > 0) {
-    hipLaunchKernelGGL(k_round_begin_pub, dim3((unsigned)(1 + (npub_el / 2 + 255) / 256)), dim3(256), 0, h->stream,
-                       h->dv, d_active, (const double*)h->d_vec, h->d_pub + (size_t)h->first_owned * 4 * h->P.r,
-                       (const int*)(h->d_pub_src + h->first_owned), (int)h->n_owned, 4 * h->P.r);
-  } else {
-    hipLaunchKernelGGL(k_round_begin, dim3(1), dim3(std::max(64, ((h->dv.L + 63) / 64) * 64)), 0, h->stream,
-                       h->dv, d_active);
-  }
+  enqueue_begin(h, d_active, BEGIN_ROUND);
   for (int it = 0; it < h->P.rtr_iterations; ++it) {
-    hipLaunchKernelGGL((k_grad<R, G, F>), grid, blk, smr, h->stream, h->dv);
-    red(RED_GRAD);
-    const int J = h->P.tcg_max_iterations;
-    if (!h->poll || F) {  // the fused variant has no per-robot reduce launch to report progress
-      for (int j = 0; j < J; ++j) tcg_step();
-    } else {
-      // Keep exactly one tCG step queued beyond the last one known to be
-      // needed; stop enqueuing once every robot has left tCG.
-      unsigned long long s_prev = tcg_step();
-      int issued = 1;
-      while (issued < J) {
-        const unsigned long long s_next = tcg_step();
-        ++issued;
-        if (wait_running(s_prev) == 0) break;
-        s_prev = s_next;
+    hipLaunchKernelGGL((k_grad<R, RW>), grid, blk, SmemHG<R>::bytes, h->stream, h->dv);
+    // tCG: each step is (k_hess, k_update); with polling, exactly one step
+    // stays queued beyond the last one known to be needed
+    unsigned long long prev = 0;
+    for (int j = 0; j < h->P.tcg_max_iterations; ++j) {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      int slot = -1;
+      if (h->timing && h->ev_used / 2 < (size_t)HV_SLOTS) {
+        slot = (int)(h->ev_used / 2);
+        e0 = next_event(h);
+        e1 = next_event(h);
+        (void)hipEventRecord(e0, h->stream);
+      }
+      hipLaunchKernelGGL((k_hess<R, RW>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot);
+      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+      const bool poll = h->poll && h->hstat;
+      const unsigned long long seq = poll ? ++h->seq : 0;
+      hipLaunchKernelGGL((k_update<R>), grid, blk, SmemU::bytes, h->stream, h->dv, poll ? h->hstat : nullptr, seq);
+      if (poll) {
+        if (j > 0 && !wait_running(h, prev)) break;
+        prev = seq;
       }
     }
-    hipLaunchKernelGGL((k_retract<R>), grid, blk, sm, h->stream, h->dv);
-    hipLaunchKernelGGL((k_cost<R, G, F>), grid, blk, smc, h->stream, h->dv);
-    red(RED_COST);
-    hipLaunchKernelGGL((k_commit<R>), grid, blk, 0, h->stream, h->dv);
+    hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv);
+    hipLaunchKernelGGL((k_cost<R, RW>), grid, blk, SmemC<R>::bytes, h->stream, h->dv);
   }
+  hipLaunchKernelGGL((k_commit<R>), grid, blk, 0, h->stream, h->dv);
 }
 
 template <int R>
 void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
-  switch (h->gvar * 2 + h->fvar) {
-    case 0: enqueue_round_t<R, 0, 0>(h, d_active); break;
-    case 1: enqueue_round_t<R, 0, 1>(h, d_active); break;
-    case 2: enqueue_round_t<R, 1, 0>(h, d_active); break;
-    case 3: enqueue_round_t<R, 1, 1>(h, d_active); break;
-    case 4: enqueue_round_t<R, 2, 0>(h, d_active); break;
-    case 5: enqueue_round_t<R, 2, 1>(h, d_active); break;
-    case 6: enqueue_round_t<R, 3, 0>(h, d_active); break;
-    case 7: enqueue_round_t<R, 3, 1>(h, d_active); break;
-    case 10: h->hinc ? enqueue_round_t<R, 9, 0>(h, d_active) : enqueue_round_t<R, 5, 0>(h, d_active); break;
-    case 11: h->hinc ? enqueue_round_t<R, 9, 1>(h, d_active) : enqueue_round_t<R, 5, 1>(h, d_active); break;
-    case 14: enqueue_round_t<R, 7, 0>(h, d_active); break;
-    default: enqueue_round_t<R, 7, 1>(h, d_active); break;
-  }
+  if (h->rw == 12) enqueue_round_t<R, 12>(h, d_active);
+  else enqueue_round_t<R, 16>(h, d_active);
 }
 
-// One RBCD round for the robots whose d_active flag is set.
+// One RBCD round for the robots whose d_active flag is set; it starts with
+// the scheduled GNC decision when the handle's schedule is enabled.
 void enqueue_round(kmx_pgo* h, const unsigned char* d_active) {
   switch (h->P.r) {
     case 3: enqueue_round_r<3>(h, d_active); break;
@@ -2462,7 +1798,16 @@ void enqueue_round(kmx_pgo* h, const unsigned char* d_active) {
   }
 }
 
-bool ready(kmx_pgo* h) { return h && h->d_vec != nullptr; }
+template <int RW>
+void enqueue_apply_weights_t(kmx_pgo* h) {
+  if (h->mloc > 0)
+    hipLaunchKernelGGL(k_apply_weights<RW>, dim3((h->mloc + 255) / 256), dim3(256), 0, h->stream, h->dv, h->mloc);
+}
+void enqueue_apply_weights(kmx_pgo* h) {
+  if (h->rw == 12) enqueue_apply_weights_t<12>(h);
+  else enqueue_apply_weights_t<16>(h);
+  enqueue_precond(h, 0);
+}
 
 }  // namespace
 
@@ -2474,6 +1819,8 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   KMX_CHECK(params->r >= 3 && params->r <= 8, KMX_EUNSUP, "relaxation rank must be in [3, 8]");
   KMX_CHECK(params->rtr_iterations >= 1 && params->tcg_max_iterations >= 1, KMX_EINVAL,
             "rtr_iterations and tcg_max_iterations must be >= 1");
+  KMX_CHECK(params->robust_cost == KMX_COST_L2 || params->robust_cost == KMX_COST_GNC_TLS, KMX_EUNSUP,
+            "robust cost must be L2 or GNC_TLS");
   int ndev = 0;
   KMX_HIP(hipGetDeviceCount(&ndev));
   KMX_CHECK(device >= 0 && device < ndev, KMX_EINVAL, "bad HIP device ordinal");
@@ -2481,15 +1828,12 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   kmx_pgo* h = new kmx_pgo();
   h->P = *params;
   h->device = device;
-  h->mu = params->gnc_mu_init;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete h;
     return kmx::fail(KMX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
   h->own_stream = true;
-  if (const char* v = std::getenv("KMX_GATHER")) h->gvar_req = std::min(7, std::max(0, std::atoi(v)));
-  if (const char* v = std::getenv("KMX_FUSED")) h->fvar = std::atoi(v) ? 1 : 0;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
   *out = h;
   return KMX_OK;
@@ -2577,11 +1921,13 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     return (it != h->pub_key.end() && *it == k) ? (int64_t)(it - h->pub_key.begin()) : -1;
   };
   std::vector<int> pub_src(std::max<int64_t>(h->npub, 1), -1);
+  std::vector<int> pose_slot(std::max(nloc, 1), -1);
   int64_t first = -1, last = -1;
   for (int64_t s = 0; s < h->npub; ++s) {
     const int rb = (int)(keys[s] >> 32), pp = (int)(keys[s] & 0xffffffff);
     if (h->local_of[rb] >= 0) {
       pub_src[s] = h->loff[h->local_of[rb]] + pp;
+      pose_slot[pub_src[s]] = (int)s;
       if (first < 0) first = s;
       KMX_CHECK(last < 0 || last == s - 1, KMX_EUNSUP,
                 "local robots must own a contiguous range of the public table (assign robot ranges to ranks)");
@@ -2597,33 +1943,47 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     if (h->local_of[r1[e]] >= 0 || h->local_of[r2[e]] >= 0) ledges.push_back(e);
   h->mloc = (int)ledges.size();
   h->loc_edge_gid = ledges;
-  h->ek_h.assign(std::max(h->mloc, 1), 0.0);
-  h->et_h.assign(std::max(h->mloc, 1), 0.0);
+  std::vector<double> ek_h(std::max(h->mloc, 1), 0.0), et_h(std::max(h->mloc, 1), 0.0);
   std::vector<double> ew_h(std::max(h->mloc, 1), 0.0);
   std::vector<int> deg(nloc + 1, 0);
   h->m_robot.assign(L, 0);
   for (int k = 0; k < h->mloc; ++k) {
     const int64_t e = ledges[k];
-    h->ek_h[k] = kappa[e];
-    h->et_h[k] = tau[e];
+    ek_h[k] = kappa[e];
+    et_h[k] = tau[e];
     ew_h[k] = weight[e];
     const int a1 = h->local_of[r1[e]], a2 = h->local_of[r2[e]];
     if (a1 >= 0) { deg[lpose(r1[e], p1[e])]++; h->m_robot[a1]++; }
     if (a2 >= 0) { deg[lpose(r2[e], p2[e])]++; if (r2[e] != r1[e]) h->m_robot[a2]++; }
   }
+  // record width: compact when every local measurement rotation's third row is
+  // row0 x row1 to 1e-12 (the gathers rebuild it), the full rotation otherwise
+  {
+    bool ok = true;
+    for (int k = 0; k < h->mloc && ok; ++k) {
+      const double* Q = R + 9 * ledges[k];
+      const double c0 = Q[1] * Q[5] - Q[2] * Q[4], c1 = Q[2] * Q[3] - Q[0] * Q[5], c2 = Q[0] * Q[4] - Q[1] * Q[3];
+      ok = std::fabs(c0 - Q[6]) <= 1e-12 && std::fabs(c1 - Q[7]) <= 1e-12 && std::fabs(c2 - Q[8]) <= 1e-12;
+    }
+    h->rw = ok ? 12 : 16;
+  }
+  const int RW = h->rw;
   std::vector<int> inc_ptr(nloc + 1, 0);
   for (int i = 0; i < nloc; ++i) inc_ptr[i + 1] = inc_ptr[i] + deg[i];
   h->ninc = inc_ptr[nloc];
-  std::vector<int2> inc(std::max(inc_ptr[nloc], 1));
-  std::vector<double> irec((size_t)std::max(inc_ptr[nloc], 1) * 16, 0.0);
+  std::vector<double> rec((size_t)(h->ninc + 1) * RW, 0.0);  // + one zero pad record
   std::vector<int2> eipos(std::max(h->mloc, 1), make_int2(-1, -1));
   std::vector<int> fill(inc_ptr.begin(), inc_ptr.end() - 1);
-  auto put_rec = [&](int pos, int64_t e) {  // per-incidence copy of the edge record
-    double* rec = &irec[(size_t)pos * 16];
-    for (int q = 0; q < 9; ++q) rec[q] = R[9 * e + q];
-    for (int q = 0; q < 3; ++q) rec[9 + q] = t[3 * e + q];
-    rec[12] = weight[e] * kappa[e];
-    rec[13] = weight[e] * tau[e];
+  auto put_rec = [&](int pos, int64_t e, int other, int code) {
+    double* c = &rec[(size_t)pos * RW];
+    const double* Q = R + 9 * e;
+    int j = 0;
+    for (int q = 0; q < (RW == 12 ? 6 : 9); ++q) c[j++] = Q[q];
+    for (int q = 0; q < 3; ++q) c[j++] = t[3 * e + q];
+    c[j++] = weight[e] * kappa[e];
+    c[j++] = weight[e] * tau[e];
+    const long long bits = (long long)(unsigned)other | ((long long)code << 32);
+    std::memcpy(&c[j], &bits, 8);
   };
   for (int k = 0; k < h->mloc; ++k) {  // increasing global edge id per pose
     const int64_t e = ledges[k];
@@ -2632,18 +1992,18 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       const int sp = lpose(r1[e], p1[e]);
       const int other = priv ? lpose(r2[e], p2[e]) : (int)(-1 - slot_of(r2[e], p2[e]));
       eipos[k].x = fill[sp];
-      put_rec(fill[sp], e);
-      inc[fill[sp]++] = make_int2(other, (int)(k | 0x80000000u));
+      put_rec(fill[sp]++, e, other, (int)(k | 0x80000000u));
     }
     if (h->local_of[r2[e]] >= 0) {
       const int sp = lpose(r2[e], p2[e]);
       const int other = priv ? lpose(r1[e], p1[e]) : (int)(-1 - slot_of(r1[e], p1[e]));
       eipos[k].y = fill[sp];
-      put_rec(fill[sp], e);
-      inc[fill[sp]++] = make_int2(other, k);
+      put_rec(fill[sp]++, e, other, k);
     }
   }
-  // GNC ownership (owner = lower robot id, drawio:2198) and shared-weight table
+  // GNC: every non-fixed local edge is re-weighted here (a shared loop closure
+  // on both handles of its robots, identically); the owner-packed shared-weight
+  // table (owner = lower robot id, drawio:2198) is kept for the explicit exchange.
   std::vector<int> gnc_edge, sh_edge, sh_idx, osh_edge, osh_idx;
   std::vector<int2> gnc_ends;
   int64_t nsh = 0;
@@ -2667,11 +2027,10 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   for (int k = 0; k < h->mloc; ++k) {
     const int64_t e = ledges[k];
     if (fixed_weight[e]) continue;
-    const int owner = std::min(r1[e], r2[e]);
-    if (h->local_of[owner] < 0) continue;
+    // a local endpoint is read from the iterate, a foreign one from the public
+    // table (after the exchange they hold the same row)
     auto enc = [&](int rb, int pp) -> int {
-      if (rb == owner) return lpose(rb, pp);
-      return (int)(-1 - slot_of(rb, pp));
+      return h->local_of[rb] >= 0 ? lpose(rb, pp) : (int)(-1 - slot_of(rb, pp));
     };
     gnc_edge.push_back(k);
     gnc_ends.push_back(make_int2(enc(r1[e], p1[e]), enc(r2[e], p2[e])));
@@ -2679,40 +2038,25 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   h->n_gnc = (int)gnc_edge.size();
   h->n_sh_local = (int)sh_edge.size();
   h->n_osh = (int)osh_edge.size();
-  // tiles
-  const int PPW = 64 / r;
-  h->tile_poses = WAVES * PPW;
+  // tiles: at most TP poses of one robot, cut by incidence count so every
+  // workgroup's gather walks about the same number of incidences (a tile closes
+  // when the next pose would take it past 1.05 x the robot's mean per full tile)
+  // and capped at two chunks of TP * r incidences (two LDS hand-offs in k_hess)
+  const int TP = WAVES * (64 / r);
   std::vector<int> tr, tp0, tnp, rt0(L + 1, 0);
-  // Incidence-balanced tiles: a tile holds at most tile_poses poses and about
-  // the robot's mean incidences per full tile, so every workgroup's gather
-  // walks about the same number of incidences (segments of equal length S =
-  // ceil(incidences / groups)); KMX_TILEBAL=0 cuts plain runs of tile_poses.
-  bool tilebal = true;
-  if (const char* v = std::getenv("KMX_TILEBAL")) tilebal = std::atoi(v) != 0;
-  // The incidence-parallel kernels (G = 9) walk a tile in chunks of TP * r
-  // incidences, one LDS hand-off each: capping tiles at two chunks takes the
-  // Hessian gather from ~3 to 2 hand-offs (32 -> 30 us at configs[3]).
-  // KMX_TILECAP overrides (0 = no cap).
-  int64_t tilecap = INT64_MAX;
-  {
-    const char* hv = std::getenv("KMX_HINC");
-    const bool g9 = r <= 5 && (h->gvar_req < 0 || h->gvar_req == 5) && !(hv && std::atoi(hv) == 0);
-    if (g9) tilecap = 2 * (int64_t)(WAVES * (64 / r) * r);
-    if (const char* v = std::getenv("KMX_TILECAP")) tilecap = std::atoi(v) > 0 ? std::atoi(v) : INT64_MAX;
-  }
+  const int64_t tilecap = 2 * (int64_t)TP * r;
   for (int l = 0; l < L; ++l) {
     const int n = n_poses[h->robots[l]];
     const int base = h->loff[l];
     rt0[l] = (int)tr.size();
     const int64_t inc_l = (int64_t)inc_ptr[base + n] - inc_ptr[base];
-    const int64_t full = std::max<int64_t>(1, (n + h->tile_poses - 1) / h->tile_poses);
-    const int64_t cap =
-        std::min(tilecap, tilebal ? std::max<int64_t>(1, (inc_l * 21 / 20 + full - 1) / full) : INT64_MAX);
+    const int64_t full = std::max<int64_t>(1, (n + TP - 1) / TP);
+    const int64_t cap = std::min(tilecap, std::max<int64_t>(1, (inc_l * 21 / 20 + full - 1) / full));
     int p0 = 0;
     while (p0 < n) {
       int np = 0;
       int64_t cum = 0;
-      while (p0 + np < n && np < h->tile_poses) {
+      while (p0 + np < n && np < TP) {
         const int64_t dg = inc_ptr[base + p0 + np + 1] - inc_ptr[base + p0 + np];
         if (np > 0 && cum + dg > cap) break;
         cum += dg;
@@ -2727,147 +2071,41 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   rt0[L] = (int)tr.size();
   h->rt0_h = rt0;
   h->ntiles = (int)tr.size();
+  KMX_CHECK(h->ntiles > 0, KMX_EINVAL, "no local poses");
   std::vector<int> own_src(std::max<int64_t>(h->n_owned, 1), 0);
   for (int64_t k = 0; k < h->n_owned; ++k) own_src[k] = pub_src[h->first_owned + k];
   std::vector<int> nrob(L);
   for (int l = 0; l < L; ++l) nrob[l] = n_poses[h->robots[l]];
+  std::vector<int> rgroup0(L + 1, 0);  // ticket groups of GS tiles per robot
+  for (int l = 0; l < L; ++l) rgroup0[l + 1] = rgroup0[l] + (rt0[l + 1] - rt0[l] + GS - 1) / GS;
+  const int ngroups = std::max(rgroup0[L], 1);
   // device
   int rc;
   const size_t vec = (size_t)std::max(nloc, 1) * ps;
-  // Compact records: valid when every local rotation's third row equals row0 x
-  // row1 to 1e-12 (measurements in SO(3)); the gathers then rebuild row 2.
-  std::vector<double> crec, ocrec;
-  std::vector<int> optr;
-  std::vector<int2> eopos;
-  {
-    bool ok = true;
-    for (int k = 0; k < h->mloc && ok; ++k) {
-      const double* Q = R + 9 * ledges[k];
-      const double c0 = Q[1] * Q[5] - Q[2] * Q[4], c1 = Q[2] * Q[3] - Q[0] * Q[5], c2 = Q[0] * Q[4] - Q[1] * Q[3];
-      ok = std::fabs(c0 - Q[6]) <= 1e-12 && std::fabs(c1 - Q[7]) <= 1e-12 && std::fabs(c2 - Q[8]) <= 1e-12;
-    }
-    h->compact_ok = ok;
-    const bool want = (h->gvar_req < 0 || h->gvar_req == 3 || h->gvar_req == 5 || h->gvar_req == 7);
-    h->gvar = (ok && want) ? (h->gvar_req < 0 ? KMX_GATHER_DEFAULT : h->gvar_req)
-                           : (h->gvar_req >= 0 && h->gvar_req < 3 ? h->gvar_req : 2);
-    if (h->gvar == 3 || h->gvar == 5 || h->gvar == 7) {
-      const size_t ni = (size_t)std::max(h->ninc, 1);
-      crec.assign(ni * 12, 0.0);
-      for (size_t k = 0; k < (size_t)h->ninc; ++k) {
-        const double* a = &irec[k * 16];
-        double* c = &crec[k * 12];
-        for (int q = 0; q < 6; ++q) c[q] = a[q];
-        c[6] = a[9]; c[7] = a[10]; c[8] = a[11];
-        c[9] = a[12]; c[10] = a[13];
-        const long long bits = (long long)(unsigned)inc[k].x | ((long long)inc[k].y << 32);
-        std::memcpy(&c[11], &bits, 8);
-      }
-      // owner incidences, in CSR order
-      optr.assign(nloc + 1, 0);
-      eopos.assign(std::max(h->mloc, 1), make_int2(-1, -1));
-      for (int p = 0; p < nloc; ++p) {
-        optr[p + 1] = optr[p];
-        for (int k = inc_ptr[p]; k < inc_ptr[p + 1]; ++k) {
-          const bool own = inc[k].x < 0 || (((unsigned)inc[k].y) >> 31);
-          if (!own) continue;
-          const int pos = optr[p + 1]++;
-          ocrec.insert(ocrec.end(), crec.begin() + 12 * (size_t)k, crec.begin() + 12 * (size_t)(k + 1));
-          int2& ep = eopos[inc[k].y & 0x7fffffff];
-          if (ep.x < 0) ep.x = pos;
-          else ep.y = pos;
-        }
-      }
-      if (ocrec.empty()) ocrec.assign(12, 0.0);
-    }
-  }
-  // The incidence-parallel kernels (G = 9: k_hess, k_cost) read the compact
-  // records in CSR order; k_grad keeps the degree-balanced gather.
-  std::vector<double> hrec, hocrec;
-  std::vector<int2> heopos;
-  h->hinc = false;
-  if (h->gvar == 5 && r <= 5) {  // r >= 6 spills at 128 VGPRs: keep the row gather there
-    bool want = true;
-    if (const char* v = std::getenv("KMX_HINC")) want = std::atoi(v) != 0;
-    if (want) {
-      hrec.assign(crec.begin(), crec.begin() + 12 * (size_t)h->ninc);
-      hrec.resize(hrec.size() + 12, 0.0);  // pad record (clamped loads of an empty tile)
-      hocrec = ocrec;
-      hocrec.resize(hocrec.size() + 12, 0.0);
-      heopos = eopos;
-      h->hinc = true;
-    }
-  }
-  // Segment-major record layout for the degree-balanced gather (G = 5/6): a
-  // tile's n incidences form TP lane-group segments of S = ceil(n / TP); the
-  // record of (segment g, step j) is stored at tile base + j*TP + g, so at every
-  // step the groups of a wave read consecutive records (full cache lines)
-  // instead of TP records S apart. KMX_RECT=0 keeps CSR order.
-  std::vector<int> trec0, torec0;
-  std::vector<int2> cipos;
-  h->rect = false;
-  {
-    bool want = true;
-    if (const char* v = std::getenv("KMX_RECT")) want = std::atoi(v) != 0;
-    if (want && h->gvar == 5) {
-      const int TP = WAVES * (64 / r);
-      auto transpose = [&](const std::vector<int>& ptr, std::vector<double>& rec, std::vector<int>& base,
-                           std::vector<int64_t>& map) {
-        base.assign(h->ntiles + 1, 0);
-        int64_t tot = 0;
-        for (int t = 0; t < h->ntiles; ++t) {
-          const int n = ptr[tp0[t] + tnp[t]] - ptr[tp0[t]];
-          base[t] = (int)tot;
-          tot += (int64_t)TP * std::max(1, (n + TP - 1) / TP);
-        }
-        base[h->ntiles] = (int)tot;
-        std::vector<double> out((size_t)std::max<int64_t>(tot, 1) * 12, 0.0);
-        map.assign(rec.size() / 12, -1);
-        for (int t = 0; t < h->ntiles; ++t) {
-          const int K0 = ptr[tp0[t]], n = ptr[tp0[t] + tnp[t]] - K0;
-          const int S = std::max(1, (n + TP - 1) / TP);
-          for (int k = 0; k < n; ++k) {
-            const int64_t dst = base[t] + (int64_t)(k % S) * TP + k / S;
-            std::memcpy(&out[(size_t)dst * 12], &rec[(size_t)(K0 + k) * 12], 12 * sizeof(double));
-            map[K0 + k] = dst;
-          }
-        }
-        rec.swap(out);
-      };
-      std::vector<int64_t> cmap, omap;
-      transpose(inc_ptr, crec, trec0, cmap);
-      transpose(optr, ocrec, torec0, omap);
-      cipos.assign(std::max(h->mloc, 1), make_int2(-1, -1));
-      for (int k = 0; k < h->mloc; ++k) {
-        cipos[k].x = eipos[k].x >= 0 ? (int)cmap[eipos[k].x] : -1;
-        cipos[k].y = eipos[k].y >= 0 ? (int)cmap[eipos[k].y] : -1;
-        int2& ep = eopos[k];
-        ep.x = ep.x >= 0 ? (int)omap[ep.x] : -1;
-        ep.y = ep.y >= 0 ? (int)omap[ep.y] : -1;
-      }
-      h->rect = true;
-    }
-  }
   if ((rc = dalloc(&h->d_tile_robot, h->ntiles)) || (rc = dalloc(&h->d_tile_p0, h->ntiles)) ||
       (rc = dalloc(&h->d_tile_np, h->ntiles)) || (rc = dalloc(&h->d_rtile0, L + 1)) ||
-      (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_inc, inc.size())) ||
-      (rc = dalloc(&h->d_irec, irec.size())) || (rc = dalloc(&h->d_ekappa, h->ek_h.size())) ||
-      (rc = dalloc(&h->d_etau, h->et_h.size())) || (rc = dalloc(&h->d_ew, ew_h.size())) ||
-      (rc = dalloc(&h->d_eipos, eipos.size())) || (rc = dalloc(&h->d_vec, vec * 8)) ||
-      (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 9)) ||
+      (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_rec, rec.size())) ||
+      (rc = dalloc(&h->d_ekappa, ek_h.size())) || (rc = dalloc(&h->d_etau, et_h.size())) ||
+      (rc = dalloc(&h->d_ew, ew_h.size())) || (rc = dalloc(&h->d_eipos, eipos.size())) ||
+      (rc = dalloc(&h->d_vec, vec * 8)) || (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 9)) ||
       (rc = dalloc(&h->d_Pinv, (size_t)std::max(nloc, 1) * 16)) ||
+      (rc = dalloc(&h->d_hD, (size_t)std::max(nloc, 1) * 16)) ||
       (rc = dalloc(&h->d_pub, (size_t)std::max<int64_t>(h->npub, 1) * ps)) ||
-      (rc = dalloc(&h->d_part, (size_t)std::max(h->ntiles, 1) * NPART)) || (rc = dalloc(&h->d_ctl, L)) ||
-      (rc = dalloc(&h->d_cnt, 1)) || (rc = dalloc(&h->d_tickets, L)) || (rc = dalloc(&h->d_m_robot, L)) || (rc = dalloc(&h->d_n_robot, L)) ||
-      (rc = dalloc(&h->d_pub_src, pub_src.size())) || (rc = dalloc(&h->d_own_src, own_src.size())) ||
-      (rc = dalloc(&h->d_gnc_edge, std::max(h->n_gnc, 1))) ||
-      (rc = dalloc(&h->d_gnc_ends, std::max(h->n_gnc, 1))) ||
+      (rc = dalloc(&h->d_part, (size_t)h->ntiles * NPART)) || (rc = dalloc(&h->d_ctl, L)) ||
+      (rc = dalloc(&h->d_cnt, 1)) || (rc = dalloc(&h->d_tickets, L)) || (rc = dalloc(&h->d_m_robot, L)) ||
+      (rc = dalloc(&h->d_n_robot, L)) || (rc = dalloc(&h->d_pub_src, pub_src.size())) ||
+      (rc = dalloc(&h->d_own_src, own_src.size())) || (rc = dalloc(&h->d_pose_slot, pose_slot.size())) ||
+      (rc = dalloc(&h->d_gnc_edge, std::max(h->n_gnc, 1))) || (rc = dalloc(&h->d_gnc_ends, std::max(h->n_gnc, 1))) ||
       (rc = dalloc(&h->d_sh_edge, std::max(h->n_sh_local, 1))) ||
       (rc = dalloc(&h->d_sh_idx, std::max(h->n_sh_local, 1))) || (rc = dalloc(&h->d_active, L)) ||
       (rc = dalloc(&h->d_osh_edge, std::max(h->n_osh, 1))) || (rc = dalloc(&h->d_osh_idx, std::max(h->n_osh, 1))) ||
-      (rc = dalloc(&h->d_scratch, vec * 2))) {
+      (rc = dalloc(&h->d_relc, L)) || (rc = dalloc(&h->d_gnc, 2)) || (rc = dalloc(&h->d_ext, 64)) ||
+      (rc = dalloc(&h->d_hv_launch, HV_SLOTS)) || (rc = dalloc(&h->d_rgroup0, L + 1)) ||
+      (rc = dalloc(&h->d_gtickets, ngroups)) || (rc = dalloc(&h->d_gpart, (size_t)ngroups * NPART))) {
     free_dev(h);
     return rc;
   }
+  h->ext_cap = 64;
   auto up = [&](void* dst, const void* src, size_t bytes) {
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream);
   };
@@ -2876,46 +2114,20 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(up(h->d_tile_np, tnp.data(), sizeof(int) * tnp.size()));
   KMX_HIP(up(h->d_rtile0, rt0.data(), sizeof(int) * rt0.size()));
   KMX_HIP(up(h->d_inc_ptr, inc_ptr.data(), sizeof(int) * inc_ptr.size()));
-  KMX_HIP(up(h->d_inc, inc.data(), sizeof(int2) * inc.size()));
-  KMX_HIP(up(h->d_irec, irec.data(), sizeof(double) * irec.size()));
-  if (h->gvar == 3 || h->gvar == 5 || h->gvar == 7) {
-    if ((rc = dalloc(&h->d_crec, crec.size())) || (rc = dalloc(&h->d_ocrec, ocrec.size())) ||
-        (rc = dalloc(&h->d_optr, optr.size())) || (rc = dalloc(&h->d_eopos, eopos.size()))) {
-      free_dev(h);
-      return rc;
-    }
-    KMX_HIP(up(h->d_crec, crec.data(), sizeof(double) * crec.size()));
-    KMX_HIP(up(h->d_ocrec, ocrec.data(), sizeof(double) * ocrec.size()));
-    KMX_HIP(up(h->d_optr, optr.data(), sizeof(int) * optr.size()));
-    KMX_HIP(up(h->d_eopos, eopos.data(), sizeof(int2) * eopos.size()));
-  }
-  if (h->hinc) {
-    if ((rc = dalloc(&h->d_hrec, hrec.size())) || (rc = dalloc(&h->d_hD, (size_t)std::max(nloc, 1) * 16)) ||
-        (rc = dalloc(&h->d_hocrec, hocrec.size())) || (rc = dalloc(&h->d_heopos, heopos.size()))) {
-      free_dev(h);
-      return rc;
-    }
-    KMX_HIP(up(h->d_hrec, hrec.data(), sizeof(double) * hrec.size()));
-    KMX_HIP(up(h->d_hocrec, hocrec.data(), sizeof(double) * hocrec.size()));
-    KMX_HIP(up(h->d_heopos, heopos.data(), sizeof(int2) * heopos.size()));
-  }
-  if (h->rect) {
-    if ((rc = dalloc(&h->d_trec0, trec0.size())) || (rc = dalloc(&h->d_torec0, torec0.size())) ||
-        (rc = dalloc(&h->d_cipos, cipos.size()))) {
-      free_dev(h);
-      return rc;
-    }
-    KMX_HIP(up(h->d_trec0, trec0.data(), sizeof(int) * trec0.size()));
-    KMX_HIP(up(h->d_torec0, torec0.data(), sizeof(int) * torec0.size()));
-    KMX_HIP(up(h->d_cipos, cipos.data(), sizeof(int2) * cipos.size()));
-  }
-  KMX_HIP(up(h->d_ekappa, h->ek_h.data(), sizeof(double) * h->ek_h.size()));
-  KMX_HIP(up(h->d_etau, h->et_h.data(), sizeof(double) * h->et_h.size()));
+  KMX_HIP(up(h->d_rec, rec.data(), sizeof(double) * rec.size()));
+  KMX_HIP(up(h->d_ekappa, ek_h.data(), sizeof(double) * ek_h.size()));
+  KMX_HIP(up(h->d_etau, et_h.data(), sizeof(double) * et_h.size()));
   KMX_HIP(up(h->d_ew, ew_h.data(), sizeof(double) * ew_h.size()));
   KMX_HIP(up(h->d_eipos, eipos.data(), sizeof(int2) * eipos.size()));
   KMX_HIP(hipMemsetAsync(h->d_vec, 0, sizeof(double) * vec * 8, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_pub, 0, sizeof(double) * std::max<int64_t>(h->npub, 1) * ps, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_ctl, 0, sizeof(Ctl) * L, h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_cnt, 0, sizeof(Counters), h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_tickets, 0, sizeof(unsigned) * L, h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_ext, 0, sizeof(double) * 64, h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_hv_launch, 0, sizeof(int) * HV_SLOTS, h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_gtickets, 0, sizeof(unsigned) * ngroups, h->stream));
+  KMX_HIP(up(h->d_rgroup0, rgroup0.data(), sizeof(int) * (L + 1)));
   if (L > h->hstat_cap) {  // host-mapped per-robot tCG progress
     if (h->hstat) (void)hipHostFree(h->hstat);
     h->hstat = nullptr;
@@ -2926,12 +2138,19 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   }
   for (int l = 0; l < L; ++l) h->hstat[l].word = 0;
   h->seq = 0;
-  KMX_HIP(hipMemsetAsync(h->d_cnt, 0, sizeof(Counters), h->stream));
-  KMX_HIP(hipMemsetAsync(h->d_tickets, 0, sizeof(unsigned) * L, h->stream));
+  {
+    std::vector<double> relc(L);  // no block update yet: not converged (an empty block is)
+    for (int l = 0; l < L; ++l) relc[l] = nrob[l] > 0 ? std::numeric_limits<double>::infinity() : 0.0;
+    KMX_HIP(up(h->d_relc, relc.data(), sizeof(double) * L));
+    Gnc g0[2] = {};
+    g0[0].mu = g0[1].mu = h->P.gnc_mu_init;
+    KMX_HIP(up(h->d_gnc, g0, sizeof(g0)));
+  }
   KMX_HIP(up(h->d_m_robot, h->m_robot.data(), sizeof(long long) * L));
   KMX_HIP(up(h->d_n_robot, nrob.data(), sizeof(int) * L));
   KMX_HIP(up(h->d_pub_src, pub_src.data(), sizeof(int) * pub_src.size()));
   KMX_HIP(up(h->d_own_src, own_src.data(), sizeof(int) * own_src.size()));
+  KMX_HIP(up(h->d_pose_slot, pose_slot.data(), sizeof(int) * pose_slot.size()));
   if (h->n_gnc) {
     KMX_HIP(up(h->d_gnc_edge, gnc_edge.data(), sizeof(int) * gnc_edge.size()));
     KMX_HIP(up(h->d_gnc_ends, gnc_ends.data(), sizeof(int2) * gnc_ends.size()));
@@ -2949,30 +2168,25 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   // host vectors must outlive the async copies
   KMX_HIP(hipStreamSynchronize(h->stream));
   Dev& d = h->dv;
+  d = Dev{};
   d.ntiles = h->ntiles; d.L = L; d.nloc = nloc; d.npub = (int)h->npub;
   d.tile_robot = h->d_tile_robot; d.tile_p0 = h->d_tile_p0; d.tile_np = h->d_tile_np; d.rtile0 = h->d_rtile0;
-  d.inc_ptr = h->d_inc_ptr; d.inc = h->d_inc; d.irec = h->d_irec; d.crec = h->d_crec;
-  d.ocrec = h->d_ocrec; d.optr = h->d_optr; d.eopos = h->d_eopos;
+  d.inc_ptr = h->d_inc_ptr; d.rec = h->d_rec;
   d.ekappa = h->d_ekappa; d.etau = h->d_etau; d.ew = h->d_ew; d.eipos = h->d_eipos;
-  d.cipos = h->rect ? h->d_cipos : h->d_eipos;
-  d.trec0 = h->d_trec0; d.torec0 = h->d_torec0; d.rect = h->rect ? 1 : 0;
-  d.hrec = h->hinc ? h->d_hrec : nullptr; d.hD = h->hinc ? h->d_hD : nullptr;
-  d.hocrec = h->hinc ? h->d_hocrec : nullptr; d.heopos = h->hinc ? h->d_heopos : nullptr;
-  d.dbg = 0;
-  if (const char* v = std::getenv("KMX_PGO_DBG")) d.dbg = std::atoi(v);
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
   d.z = h->d_vec + 4 * vec; d.eta = h->d_vec + 5 * vec; d.del = h->d_vec + 6 * vec; d.hd = h->d_vec + 7 * vec;
-  d.S = h->d_S; d.Pinv = h->d_Pinv; d.pub = h->d_pub; d.part = h->d_part; d.ctl = h->d_ctl; d.cnt = h->d_cnt; d.tickets = h->d_tickets;
-  d.m_robot = h->d_m_robot; d.n_robot = h->d_n_robot;
-  d.p.tcg_max = h->P.tcg_max_iterations; d.p.rtr_iters = h->P.rtr_iterations;
-  d.p.use_precond = h->P.use_preconditioner; d.p.robust = h->P.robust_cost;
-  d.p.kappa = h->P.tcg_kappa; d.p.theta = h->P.tcg_theta; d.p.Delta0 = h->P.rtr_initial_radius;
-  d.p.Delta_max = h->P.rtr_max_radius; d.p.accept_rho = h->P.rtr_accept_rho; d.p.gn_tol = h->P.gradnorm_tol;
-  d.p.shift = h->P.precond_shift; d.p.barc = h->P.gnc_barc;
-  enqueue_precond(h);
+  d.S = h->d_S; d.Pinv = h->d_Pinv; d.hD = h->d_hD; d.pub = h->d_pub; d.part = h->d_part;
+  d.ctl = h->d_ctl; d.cnt = h->d_cnt; d.tickets = h->d_tickets;
+  d.m_robot = h->d_m_robot; d.n_robot = h->d_n_robot; d.pose_slot = h->d_pose_slot;
+  d.relc = h->d_relc; d.gnc = h->d_gnc; d.gnc_next = h->d_gnc + 1;
+  d.gnc_edge = h->d_gnc_edge; d.gnc_ends = h->d_gnc_ends; d.n_gnc = h->n_gnc;
+  d.hv_launch = h->d_hv_launch;
+  d.rgroup0 = h->d_rgroup0; d.gtickets = h->d_gtickets; d.gpart = h->d_gpart;
+  h->n_ext = 0;
+  sync_params(h);
+  enqueue_precond(h, 0);
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipStreamSynchronize(h->stream));
-  h->round_counter = 0;
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -3037,27 +2251,60 @@ extern "C" int kmx_pgo_unpack_public(kmx_pgo* h, const void* dev_table) {
 }
 
 extern "C" int kmx_pgo_gather_public_rows(kmx_pgo* h, const int32_t* dev_slots, int64_t n, void* dev_out) {
+  return kmx_pgo_exchange_pack(h, dev_slots, n, nullptr, 0, dev_out);
+}
+
+extern "C" int kmx_pgo_scatter_public_rows(kmx_pgo* h, const int32_t* dev_slots, int64_t n, const void* dev_rows) {
+  return kmx_pgo_exchange_unpack(h, dev_slots, n, nullptr, 0, dev_rows);
+}
+
+extern "C" int kmx_pgo_exchange_pack(kmx_pgo* h, const int32_t* dev_slots, int64_t n, const int32_t* dev_seg,
+                                     int n_seg, void* dev_out) {
   KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
-  KMX_CHECK(n >= 0 && (n == 0 || (dev_slots && dev_out)), KMX_EINVAL, "bad argument");
+  KMX_CHECK(n >= 0 && n_seg >= 0 && n_seg <= 1024 && (n == 0 || (dev_slots && dev_out)) &&
+                (n_seg == 0 || (dev_seg && dev_out)),
+            KMX_EINVAL, "bad argument");
   KMX_HIP(hipSetDevice(h->device));
   const int ps = 4 * h->P.r;
   const long long tot = (long long)n * ps;
   if (tot)
     hipLaunchKernelGGL(k_gather_slots, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
-                       h->d_pub_src, (const int*)dev_slots, (long long)n, (int)h->npub, (double*)dev_out, ps);
+                       h->d_pub_src, (const int*)dev_slots, (long long)n, (int)h->npub, (double*)dev_out, ps,
+                       (const int*)dev_seg, n_seg);
+  if (n_seg)
+    hipLaunchKernelGGL(k_status_pack, dim3(1), dim3(1024), 0, h->stream, (const double*)h->d_relc, h->dv.L,
+                       (double*)dev_out, (const int*)dev_seg, n_seg, ps);
   KMX_HIP(hipGetLastError());
   return KMX_OK;
 }
 
-extern "C" int kmx_pgo_scatter_public_rows(kmx_pgo* h, const int32_t* dev_slots, int64_t n, const void* dev_rows) {
+extern "C" int kmx_pgo_exchange_unpack(kmx_pgo* h, const int32_t* dev_slots, int64_t n, const int32_t* dev_seg,
+                                       int n_seg, const void* dev_in) {
   KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
-  KMX_CHECK(n >= 0 && (n == 0 || (dev_slots && dev_rows)), KMX_EINVAL, "bad argument");
+  KMX_CHECK(n >= 0 && n_seg >= 0 && n_seg <= 1024 && (n == 0 || (dev_slots && dev_in)) &&
+                (n_seg == 0 || (dev_seg && dev_in)),
+            KMX_EINVAL, "bad argument");
   KMX_HIP(hipSetDevice(h->device));
   const int ps = 4 * h->P.r;
   const long long tot = (long long)n * ps;
   if (tot)
     hipLaunchKernelGGL(k_scatter_slots, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_pub,
-                       (const int*)dev_slots, (long long)n, (int)h->npub, (const double*)dev_rows, ps);
+                       (const int*)dev_slots, (long long)n, (int)h->npub, (const double*)dev_in, ps,
+                       (const int*)dev_seg, n_seg);
+  if (n_seg) {
+    if (n_seg > h->ext_cap) {
+      KMX_HIP(hipStreamSynchronize(h->stream));
+      if (h->d_ext) (void)hipFree(h->d_ext);
+      h->d_ext = nullptr;
+      h->ext_cap = 0;
+      if (int rc = dalloc(&h->d_ext, n_seg)) return rc;
+      h->ext_cap = n_seg;
+    }
+    hipLaunchKernelGGL(k_status_unpack, dim3(1), dim3(1024), 0, h->stream, (const double*)dev_in, h->d_ext,
+                       (const int*)dev_seg, n_seg, ps);
+  }
+  h->n_ext = n_seg;
+  sync_params(h);
   KMX_HIP(hipGetLastError());
   return KMX_OK;
 }
@@ -3133,20 +2380,14 @@ extern "C" int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats
   KMX_GUARD_END
 }
 
-extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local, int gnc_every) {
+extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local) {
   KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
   KMX_CHECK(rounds >= 0, KMX_EINVAL, "negative rounds");
   KMX_HIP(hipSetDevice(h->device));
-  for (int i = 0; i < rounds; ++i) {
-    h->publish_in_begin = refresh_local != 0;  // k_publish folded into the round's first launch
-    enqueue_round(h, h->d_active);
-    h->publish_in_begin = false;
-    h->round_counter++;
-    if (gnc_every > 0 && h->P.robust_cost == KMX_COST_GNC_TLS && h->round_counter % gnc_every == 0) {
-      if (refresh_local) enqueue_publish(h);
-      enqueue_gnc(h);
-    }
-  }
+  // every round's k_commit republishes the committed owned rows, so the
+  // single-device exchange needs one publish per call
+  if (refresh_local && rounds > 0) enqueue_publish(h);
+  for (int i = 0; i < rounds; ++i) enqueue_round(h, h->d_active);
   KMX_HIP(hipGetLastError());
   return KMX_OK;
 }
@@ -3158,26 +2399,99 @@ extern "C" int kmx_pgo_sync(kmx_pgo* h) {
   return KMX_OK;
 }
 
+extern "C" int kmx_pgo_set_gnc_schedule(kmx_pgo* h, int enabled, int inner_iters, int max_updates,
+                                        double rel_change_tol) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(inner_iters >= 0 && max_updates >= 0, KMX_EINVAL, "negative schedule parameter");
+  h->gnc_on = enabled ? 1 : 0;
+  h->gnc_inner_iters = inner_iters;
+  h->gnc_max_updates = max_updates;
+  h->gnc_rel_tol = rel_change_tol;
+  sync_params(h);
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_get_gnc_state(kmx_pgo* h, kmx_gnc_state* out) {
+  KMX_CHECK(ready(h) && out, KMX_EINVAL, "null argument / no graph");
+  KMX_HIP(hipSetDevice(h->device));
+  Gnc g;
+  KMX_HIP(hipMemcpyAsync(&g, h->d_gnc, sizeof(Gnc), hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  std::memset(out, 0, sizeof(*out));
+  out->inner_iter = g.inner;
+  out->updates = g.updates;
+  out->last_fired = g.fired;
+  out->rounds = g.rounds;
+  out->mu = g.mu;
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_set_gnc_state(kmx_pgo* h, const kmx_gnc_state* in) {
+  KMX_CHECK(ready(h) && in && in->mu > 0.0, KMX_EINVAL, "null argument / no graph / mu <= 0");
+  KMX_HIP(hipSetDevice(h->device));
+  Gnc g[2] = {};
+  g[0].inner = in->inner_iter;
+  g[0].updates = in->updates;
+  g[0].fired = in->last_fired;
+  g[0].rounds = in->rounds;
+  g[0].mu = in->mu;
+  g[1] = g[0];
+  KMX_HIP(hipMemcpyAsync(h->d_gnc, g, sizeof(g), hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_get_status(kmx_pgo* h, double* rel_change) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(ready(h) && rel_change, KMX_EINVAL, "null argument / no graph");
+  KMX_HIP(hipSetDevice(h->device));
+  std::vector<double> v(h->robots.size());
+  KMX_HIP(hipMemcpyAsync(v.data(), h->d_relc, sizeof(double) * v.size(), hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  for (size_t l = 0; l < v.size(); ++l) rel_change[h->robots[l]] = v[l];
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_set_status(kmx_pgo* h, const double* rel_change) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(ready(h) && rel_change, KMX_EINVAL, "null argument / no graph");
+  KMX_HIP(hipSetDevice(h->device));
+  std::vector<double> v(h->robots.size());
+  for (size_t l = 0; l < v.size(); ++l) v[l] = rel_change[h->robots[l]];
+  KMX_HIP(hipMemcpyAsync(h->d_relc, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
 extern "C" int kmx_pgo_update_weights(kmx_pgo* h, double* mu_out) {
   KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
   KMX_HIP(hipSetDevice(h->device));
-  if (mu_out) *mu_out = h->mu;
+  Gnc g;
+  KMX_HIP(hipMemcpyAsync(&g, h->d_gnc, sizeof(Gnc), hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  if (mu_out) *mu_out = g.mu;
   if (h->P.robust_cost != KMX_COST_GNC_TLS) return KMX_OK;
-  enqueue_gnc(h);
+  enqueue_begin(h, h->d_active, BEGIN_FORCE_GNC);
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipStreamSynchronize(h->stream));
   return KMX_OK;
 }
 
 extern "C" int kmx_pgo_get_mu(kmx_pgo* h, double* mu) {
-  KMX_CHECK(h && mu, KMX_EINVAL, "null argument");
-  *mu = h->mu;
+  KMX_CHECK(ready(h) && mu, KMX_EINVAL, "null argument / no graph");
+  kmx_gnc_state s;
+  if (int rc = kmx_pgo_get_gnc_state(h, &s)) return rc;
+  *mu = s.mu;
   return KMX_OK;
 }
 extern "C" int kmx_pgo_set_mu(kmx_pgo* h, double mu) {
-  KMX_CHECK(h && mu > 0.0, KMX_EINVAL, "mu must be positive");
-  h->mu = mu;
-  return KMX_OK;
+  KMX_CHECK(ready(h) && mu > 0.0, KMX_EINVAL, "mu must be positive / no graph");
+  kmx_gnc_state s;
+  if (int rc = kmx_pgo_get_gnc_state(h, &s)) return rc;
+  s.mu = mu;
+  return kmx_pgo_set_gnc_state(h, &s);
 }
 
 extern "C" int kmx_pgo_get_weights(kmx_pgo* h, double* w) {
@@ -3193,6 +2507,7 @@ extern "C" int kmx_pgo_get_weights(kmx_pgo* h, double* w) {
 }
 
 extern "C" int kmx_pgo_set_weights(kmx_pgo* h, const double* w) {
+  KMX_GUARD_BEGIN
   KMX_CHECK(ready(h) && w, KMX_EINVAL, "null argument / no graph");
   KMX_HIP(hipSetDevice(h->device));
   std::vector<double> ew(std::max(h->mloc, 1));
@@ -3202,6 +2517,7 @@ extern "C" int kmx_pgo_set_weights(kmx_pgo* h, const double* w) {
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipStreamSynchronize(h->stream));
   return KMX_OK;
+  KMX_GUARD_END
 }
 
 extern "C" int kmx_pgo_shared_count(kmx_pgo* h, int64_t* n_shared) {
@@ -3241,9 +2557,9 @@ extern "C" int kmx_pgo_get_trajectory(kmx_pgo* h, int robot, const double* ancho
   KMX_CHECK(anchor && out, KMX_EINVAL, "null argument");
   KMX_HIP(hipSetDevice(h->device));
   const int ps = 4 * h->P.r, l = h->local_of[robot], n = h->npose[robot];
+  if (int rc = ensure_scratch(h, (size_t)ps + (size_t)std::max(n, 1) * 12)) return rc;
   double* d_anchor = h->d_scratch;
   double* d_out = h->d_scratch + ps;
-  KMX_CHECK((size_t)ps + (size_t)n * 12 <= (size_t)std::max(h->nloc, 1) * ps * 2, KMX_EINVAL, "scratch too small");
   KMX_HIP(hipMemcpyAsync(d_anchor, anchor, sizeof(double) * ps, hipMemcpyHostToDevice, h->stream));
   if (n)
     hipLaunchKernelGGL(k_traj, dim3((n + 127) / 128), dim3(128), 0, h->stream,
@@ -3263,34 +2579,30 @@ extern "C" int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, do
   KMX_HIP(hipSetDevice(h->device));
   const int ps = 4 * h->P.r, l = h->local_of[robot], n = h->npose[robot];
   const size_t vec = (size_t)std::max(h->nloc, 1) * ps;
+  if (int rc = ensure_scratch(h, vec * 2)) return rc;
   double* dV = h->d_scratch;
   double* dO = h->d_scratch + vec;
   const size_t o = (size_t)h->loff[l] * ps;
   KMX_HIP(hipMemsetAsync(h->d_scratch, 0, sizeof(double) * vec * 2, h->stream));
   if (V) KMX_HIP(hipMemcpyAsync(dV + o, V, sizeof(double) * n * ps, hipMemcpyHostToDevice, h->stream));
-  const int R_ = h->P.r;
-  if (h->gvar == 1) {
-    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 1>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
-                                          h->dv, l, mode, (const double*)dV, dO));
-  } else if (h->gvar == 2) {
-    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 2>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
-                                          h->dv, l, mode, (const double*)dV, dO));
-  } else if (h->gvar == 3) {
-    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 3>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
-                                          h->dv, l, mode, (const double*)dV, dO));
-  } else if (h->gvar == 5) {
-    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 5>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
-                                          h->dv, l, mode, (const double*)dV, dO));
-  } else if (h->gvar == 7) {
-    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 7>), dim3(h->ntiles), dim3(BLOCK), (SmemG<RR, 7>::bytes), h->stream,
-                                          h->dv, l, mode, (const double*)dV, dO));
-  } else {
-    KMX_DISPATCH_R(R_, hipLaunchKernelGGL((k_eval<RR, 0>), dim3(h->ntiles), dim3(BLOCK), Smem<RR>::bytes, h->stream,
-                                          h->dv, l, mode, (const double*)dV, dO));
+#define KMX_EVAL_LAUNCH(RR)                                                                                      \
+  if (h->rw == 12)                                                                                               \
+    hipLaunchKernelGGL((k_eval<RR, 12>), dim3(h->ntiles), dim3(BLOCK), SmemE<RR>::bytes, h->stream, h->dv, l, mode, \
+                       (const double*)dV, dO);                                                                   \
+  else                                                                                                           \
+    hipLaunchKernelGGL((k_eval<RR, 16>), dim3(h->ntiles), dim3(BLOCK), SmemE<RR>::bytes, h->stream, h->dv, l, mode, \
+                       (const double*)dV, dO);
+  switch (h->P.r) {
+    case 3: KMX_EVAL_LAUNCH(3) break;
+    case 4: KMX_EVAL_LAUNCH(4) break;
+    case 5: KMX_EVAL_LAUNCH(5) break;
+    case 6: KMX_EVAL_LAUNCH(6) break;
+    case 7: KMX_EVAL_LAUNCH(7) break;
+    default: KMX_EVAL_LAUNCH(8) break;
   }
+#undef KMX_EVAL_LAUNCH
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipMemcpyAsync(out, dO + o, sizeof(double) * n * ps, hipMemcpyDeviceToHost, h->stream));
-  std::vector<int> rt0(2);
   std::vector<double> part((size_t)h->ntiles * NPART);
   KMX_HIP(hipMemcpyAsync(part.data(), h->d_part, sizeof(double) * part.size(), hipMemcpyDeviceToHost, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));
@@ -3310,6 +2622,21 @@ extern "C" int kmx_pgo_local_edges(kmx_pgo* h, int robot, int64_t* m_local) {
   return KMX_OK;
 }
 
+extern "C" int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_bytes) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  const int64_t L = (int64_t)h->robots.size(), n = std::max(h->nloc, 1), ps = 4 * h->P.r;
+  int64_t b = 0;
+  b += (int64_t)(h->ninc + 1) * h->rw * 8 + (int64_t)(h->nloc + 1) * 4;  // records, CSR
+  b += (int64_t)std::max(h->mloc, 1) * (3 * 8 + 8);                      // kappa, tau, w, positions
+  b += n * ps * 8 * 8 + n * (9 + 16 + 16) * 8;                           // vectors, S, Pinv, D
+  b += std::max<int64_t>(h->npub, 1) * (ps * 8 + 4) + n * 4;             // public table + maps
+  b += (int64_t)h->ntiles * (NPART * 8 + 12) + L * (int64_t)(sizeof(Ctl) + 32);
+  b += (int64_t)std::max(h->n_gnc, 1) * 12 + (int64_t)h->scratch_cap * 8;  // GNC lists, scratch in use
+  if (device_bytes) *device_bytes = b;
+  if (record_bytes) *record_bytes = h->rw * 8;
+  return KMX_OK;
+}
+
 extern "C" int kmx_pgo_enable_timing(kmx_pgo* h, int enable) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   h->timing = enable != 0;
@@ -3322,131 +2649,29 @@ extern "C" int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out) {
   KMX_HIP(hipStreamSynchronize(h->stream));
   Counters c;
   KMX_HIP(hipMemcpy(&c, h->d_cnt, sizeof(Counters), hipMemcpyDeviceToHost));
+  // event pairs of k_hess launches in which at least one robot ran a Hess-vec
+  const size_t nl = std::min(h->ev_used / 2, (size_t)HV_SLOTS);
+  std::vector<int> hv(std::max<size_t>(nl, 1), 0);
+  if (nl) KMX_HIP(hipMemcpy(hv.data(), h->d_hv_launch, sizeof(int) * nl, hipMemcpyDeviceToHost));
   double ms_total = 0.0;
-  for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
+  int64_t launches = 0;
+  for (size_t i = 0; i < nl; ++i) {
+    if (hv[i] == 0) continue;
     float ms = 0.f;
-    KMX_HIP(hipEventElapsedTime(&ms, h->ev_pool[i], h->ev_pool[i + 1]));
+    KMX_HIP(hipEventElapsedTime(&ms, h->ev_pool[2 * i], h->ev_pool[2 * i + 1]));
     ms_total += ms;
+    ++launches;
   }
+  if (nl) KMX_HIP(hipMemset(h->d_hv_launch, 0, sizeof(int) * nl));
+  std::memset(out, 0, sizeof(*out));
   out->hessvec_ms_total = ms_total;
-  out->hessvec_launches = (int64_t)(h->ev_used / 2);
+  out->hessvec_launches = launches;
   out->hessvec_alg_bytes = c.hess_alg_bytes;
   out->edges_iters = (int64_t)c.edges_iters;
   out->block_updates = (int64_t)c.block_updates;
   out->hessvecs = (int64_t)c.hessvecs;
+  out->gnc_updates = (int64_t)c.gnc_updates;
   h->ev_used = 0;
   KMX_HIP(hipMemset(h->d_cnt, 0, sizeof(Counters)));
-  return KMX_OK;
-}
-
-// Diagnostic launcher shared by the gather bench / compare entry points.
-static bool gbench_launch(kmx_pgo* h, int variant, double* out, const double* Dg) {
-  const dim3 grid(h->ntiles), blk(BLOCK);
-  const size_t sm = Smem<5>::bytes;
-  constexpr int HCH = 240;
-  const size_t smh = sizeof(double) * HCH * 5 * 4 + sizeof(int) * (Smem<5>::TP + 1);
-  switch (variant) {
-#define KMX_GB(V, G, W) case V: hipLaunchKernelGGL((k_gbench<5, G, W>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
-    KMX_GB(0, 0, 1) KMX_GB(1, 0, 4) KMX_GB(2, 0, 6) KMX_GB(3, 0, 8)
-    KMX_GB(10, 1, 1) KMX_GB(11, 1, 4) KMX_GB(12, 1, 6)
-    KMX_GB(20, 2, 1) KMX_GB(21, 2, 4) KMX_GB(22, 2, 6) KMX_GB(23, 2, 8)
-    KMX_GB(40, 3, 1) KMX_GB(41, 3, 4) KMX_GB(42, 3, 6) KMX_GB(45, 4, 1)
-    KMX_GB(60, 5, 1) KMX_GB(61, 5, 4) KMX_GB(62, 5, 6) KMX_GB(65, 6, 1)
-#undef KMX_GB
-#define KMX_GB(V, G, W) case V: hipLaunchKernelGGL((k_gbench<5, G, W>), grid, blk, (SmemG<5, G>::bytes), h->stream, h->dv, (const double*)h->dv.X, out); return true;
-    KMX_GB(70, 7, 1) KMX_GB(71, 7, 4) KMX_GB(72, 7, 5) KMX_GB(75, 8, 1)
-#define KMX_GC(V, C) case V: hipLaunchKernelGGL((k_gcap<5, C>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
-    KMX_GC(50, 1000) KMX_GC(51, 12) KMX_GC(52, 10) KMX_GC(53, 8) KMX_GC(54, 4)
-#undef KMX_GC
-#undef KMX_GB
-#define KMX_GA(V, A) case V: hipLaunchKernelGGL((k_gablate<5, A>), grid, blk, sm, h->stream, h->dv, (const double*)h->dv.X, out); return true;
-    KMX_GA(30, 0) KMX_GA(31, 1) KMX_GA(32, 2) KMX_GA(33, 3)
-#undef KMX_GA
-    case 90: hipLaunchKernelGGL((k_hinc<5, 0, HCH>), grid, blk, smh, h->stream, h->dv, (const double*)h->dv.X, Dg, out); return true;
-    case 91: hipLaunchKernelGGL((k_hinc<5, 1, HCH>), grid, blk, smh, h->stream, h->dv, (const double*)h->dv.X, Dg, out); return true;
-    case 92:
-      if (!h->hinc) return false;
-      hipLaunchKernelGGL((k_gbench_hinc<5, false>), grid, blk, SmemH<5>::bytes, h->stream, h->dv, (const double*)h->dv.X, out);
-      return true;
-    case 93:
-      if (!h->hinc) return false;
-      hipLaunchKernelGGL((k_gbench_hinc<5, true>), grid, blk, SmemHG<5>::bytes, h->stream, h->dv, (const double*)h->dv.X, out);
-      return true;
-    default: return false;
-  }
-}
-
-static int gbench_check(kmx_pgo* h, int variant) {
-  KMX_CHECK(variant < 40 || variant == 90 || h->d_crec, KMX_EINVAL, "compact records not built (KMX_GATHER / non-SO(3) input)");
-  KMX_CHECK(variant != 91 || !h->rect, KMX_EINVAL, "variant 91 reads CSR-order compact records (KMX_RECT=0)");
-  return KMX_OK;
-}
-
-// D_i blocks for the lane-per-incidence prototype (caller frees).
-static int gbench_diag(kmx_pgo* h, double** D) {
-  KMX_HIP(hipMalloc(D, sizeof(double) * 16 * (size_t)std::max(h->nloc, 1)));
-  hipLaunchKernelGGL(k_diag, dim3((h->nloc + 255) / 256), dim3(256), 0, h->stream, h->dv, *D);
-  KMX_HIP(hipGetLastError());
-  return KMX_OK;
-}
-
-// Diagnostic entry point (not used by the product path): time `reps` launches
-// of the gather primitive variant (GV, LBW) = (variant / 10, variant % 10 ->
-// min waves per SIMD {0: none, 1: 4, 2: 6, 3: 8}) over the current iterate;
-// 90 / 91: the lane-per-incidence prototype (k_hinc).
-extern "C" int kmx_pgo_debug_gather_bench(kmx_pgo* h, int variant, int reps, double* ms_out) {
-  KMX_CHECK(ready(h) && ms_out && reps > 0, KMX_EINVAL, "bad argument");
-  KMX_CHECK(h->P.r == 5, KMX_EUNSUP, "gather bench is built for r = 5");
-  KMX_HIP(hipSetDevice(h->device));
-  int rc = gbench_check(h, variant);
-  if (rc) return rc;
-  const size_t vec = (size_t)std::max(h->nloc, 1) * 4 * h->P.r;
-  double* out = h->d_scratch + vec;
-  double* Dg = nullptr;
-  if ((rc = gbench_diag(h, &Dg))) return rc;
-  hipEvent_t e0, e1;
-  KMX_HIP(hipEventCreate(&e0));
-  KMX_HIP(hipEventCreate(&e1));
-  if (!gbench_launch(h, variant, out, Dg)) { (void)hipFree(Dg); return kmx::fail(KMX_EINVAL, "unknown gather variant"); }
-  KMX_HIP(hipEventRecord(e0, h->stream));
-  for (int i = 0; i < reps; ++i) gbench_launch(h, variant, out, Dg);
-  KMX_HIP(hipEventRecord(e1, h->stream));
-  KMX_HIP(hipEventSynchronize(e1));
-  float ms = 0.f;
-  KMX_HIP(hipEventElapsedTime(&ms, e0, e1));
-  *ms_out = (double)ms / reps;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  KMX_HIP(hipFree(Dg));
-  return KMX_OK;
-}
-
-// Diagnostic: run gather variants va and vb over the current iterate and
-// report max |out_a - out_b| and max |out_a| (valid pose rows only).
-extern "C" int kmx_pgo_debug_gather_cmp(kmx_pgo* h, int va, int vb, double* maxdiff, double* maxabs) {
-  KMX_CHECK(ready(h) && maxdiff && maxabs, KMX_EINVAL, "bad argument");
-  KMX_CHECK(h->P.r == 5, KMX_EUNSUP, "gather bench is built for r = 5");
-  KMX_HIP(hipSetDevice(h->device));
-  int rc;
-  if ((rc = gbench_check(h, va)) || (rc = gbench_check(h, vb))) return rc;
-  const size_t vec = (size_t)std::max(h->nloc, 1) * 4 * h->P.r;
-  double* out = h->d_scratch + vec;
-  double* Dg = nullptr;
-  if ((rc = gbench_diag(h, &Dg))) return rc;
-  std::vector<double> A(vec), B(vec);
-  bool ok = gbench_launch(h, va, out, Dg);
-  KMX_HIP(hipMemcpyAsync(A.data(), out, sizeof(double) * vec, hipMemcpyDeviceToHost, h->stream));
-  ok = ok && gbench_launch(h, vb, out, Dg);
-  KMX_HIP(hipMemcpyAsync(B.data(), out, sizeof(double) * vec, hipMemcpyDeviceToHost, h->stream));
-  KMX_HIP(hipStreamSynchronize(h->stream));
-  KMX_HIP(hipFree(Dg));
-  if (!ok) return kmx::fail(KMX_EINVAL, "unknown gather variant");
-  double md = 0.0, ma = 0.0;
-  for (size_t i = 0; i < vec; ++i) {
-    md = std::max(md, std::fabs(A[i] - B[i]));
-    ma = std::max(ma, std::fabs(A[i]));
-  }
-  *maxdiff = md;
-  *maxabs = ma;
   return KMX_OK;
 }

@@ -17,6 +17,7 @@ import numpy as np
 _LIB_PATH = Path(__file__).resolve().parent / "libkmx.so"
 
 KMX_OK = 0
+ABI_VERSION = 2  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
 KMX_COST_L2 = 0
 KMX_COST_GNC_TLS = 1
 KMX_SCHEDULE_SEQUENTIAL = 0
@@ -71,8 +72,19 @@ class PgoCounters(C.Structure):
     _fields_ = [
         ("hessvec_ms_total", C.c_double), ("hessvec_launches", C.c_int64),
         ("hessvec_alg_bytes", C.c_double), ("edges_iters", C.c_int64),
-        ("block_updates", C.c_int64), ("hessvecs", C.c_int64),
+        ("block_updates", C.c_int64), ("hessvecs", C.c_int64), ("gnc_updates", C.c_int64),
     ]
+
+
+class GncState(C.Structure):
+    _fields_ = [
+        ("inner_iter", C.c_int32), ("updates", C.c_int32), ("last_fired", C.c_int32),
+        ("rounds", C.c_int32), ("mu", C.c_double), ("reserved", C.c_double * 3),
+    ]
+
+    def as_dict(self) -> dict:
+        return {"inner_iter": self.inner_iter, "updates": self.updates, "last_fired": bool(self.last_fired),
+                "rounds": self.rounds, "mu": self.mu}
 
 
 class LcdParams(C.Structure):
@@ -129,13 +141,21 @@ def lib() -> C.CDLL:
         "kmx_pgo_refresh_local": ([P], C.c_int),
         "kmx_pgo_gather_public_rows": ([P, P, i64, P], C.c_int),
         "kmx_pgo_scatter_public_rows": ([P, P, i64, P], C.c_int),
+        "kmx_pgo_exchange_pack": ([P, P, i64, P, C.c_int, P], C.c_int),
+        "kmx_pgo_exchange_unpack": ([P, P, i64, P, C.c_int, P], C.c_int),
         "kmx_pgo_set_neighbor_poses": ([P, i64, pi32, pi32, pf64], C.c_int),
         "kmx_pgo_iterate": ([P, pu8, C.POINTER(IterStats)], C.c_int),
-        "kmx_pgo_iterate_async": ([P, C.c_int, C.c_int, C.c_int], C.c_int),
+        "kmx_pgo_iterate_async": ([P, C.c_int, C.c_int], C.c_int),
         "kmx_pgo_sync": ([P], C.c_int),
         "kmx_pgo_update_weights": ([P, pf64], C.c_int),
         "kmx_pgo_get_mu": ([P, pf64], C.c_int),
         "kmx_pgo_set_mu": ([P, f64], C.c_int),
+        "kmx_pgo_set_gnc_schedule": ([P, C.c_int, C.c_int, C.c_int, f64], C.c_int),
+        "kmx_pgo_get_gnc_state": ([P, C.POINTER(GncState)], C.c_int),
+        "kmx_pgo_set_gnc_state": ([P, C.POINTER(GncState)], C.c_int),
+        "kmx_pgo_get_status": ([P, pf64], C.c_int),
+        "kmx_pgo_set_status": ([P, pf64], C.c_int),
+        "kmx_pgo_memory": ([P, pi64, C.POINTER(C.c_int)], C.c_int),
         "kmx_pgo_get_weights": ([P, pf64], C.c_int),
         "kmx_pgo_set_weights": ([P, pf64], C.c_int),
         "kmx_pgo_shared_count": ([P, pi64], C.c_int),
@@ -157,6 +177,8 @@ def lib() -> C.CDLL:
         "kmx_lcd_verify": ([P, i32, pi32, pi32, C.POINTER(LcdResult), pu8], C.c_int),
         "kmx_lcd_verify_async": ([P, i32, pi32, pi32], C.c_int),
         "kmx_lcd_sync": ([P], C.c_int),
+        "kmx_lcd_enable_timing": ([P, C.c_int], C.c_int),
+        "kmx_lcd_read_timing": ([P, pf64, pf64], C.c_int),
         "kmx_bow_create": ([C.c_int, C.POINTER(P)], C.c_int),
         "kmx_bow_destroy": ([P], C.c_int),
         "kmx_bow_set_stream": ([P, P], C.c_int),
@@ -185,6 +207,8 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = rest
+    if L.kmx_abi_version() != ABI_VERSION:
+        raise KmxError(f"{path} implements ABI {L.kmx_abi_version()}, this binding needs {ABI_VERSION}: rebuild it")
     _lib = L
     return L
 

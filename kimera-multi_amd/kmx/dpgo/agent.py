@@ -35,6 +35,7 @@ from ..synth.pose_graph import PoseGraphData, lift, lifting_matrix
 from .messages import (MeasurementWeights, PGOAgentState, PGOAgentStatus, PoseID, PublicPoses,
                        RelativeSEMeasurement)
 from .params import PGOAgentParameters, RobustCostType
+from .schedule import GncSchedule
 
 
 class PGOAgent:
@@ -54,7 +55,7 @@ class PGOAgent:
         self.shared_lcs: list[RelativeSEMeasurement] = []
         self.state = PGOAgentState.WAIT_FOR_DATA
         self.iteration = 0
-        self.weight_updates = 0
+        self._gnc = GncSchedule.from_params(self.params)
         self.YLift = None
         self.globalAnchor = None
         self.solver = None
@@ -223,10 +224,15 @@ class PGOAgent:
         self.solver.set_weights(w)
 
     # ------------------------------------------------------------ rounds ---
+    @property
+    def weight_updates(self) -> int:
+        return self._gnc.updates
+
     def iterate(self, doOptimization: bool = True) -> bool:
         if self.state != PGOAgentState.INITIALIZED:
             return False
         self.iteration += 1
+        self._gnc.round_done()  # every iterate counts as a GNC inner iteration
         if doOptimization:
             act = np.zeros(self.graph.n_robots, np.uint8)
             act[self.mID] = 1
@@ -273,11 +279,19 @@ class PGOAgent:
 
     # --------------------------------------------------------------- GNC ---
     def shouldUpdateMeasurementWeights(self) -> bool:
-        if int(self.params.robustCostParams.costType) == int(RobustCostType.L2):
-            return False
-        if self.weight_updates >= self.params.robustOptNumWeightUpdates:
-            return False
-        return self.iteration > 0 and self.iteration % self.params.robustOptInnerIters == 0
+        """drawio:2466-2469: never for L2 or after robustOptNumWeightUpdates
+        updates; true once more than robustOptInnerIters iterations ran since
+        the last update, or when every agent of the team (num_robots; own
+        status and the statuses received by setNeighborStatus) has converged
+        (relative change <= relChangeTol)."""
+        team = []
+        for rid in range(max(self.params.num_robots, self.mID + 1)):
+            if rid == self.mID:
+                team.append(self._rel_change)
+            else:
+                st = self.neighbor_status.get(rid)
+                team.append(st.relativeChange if st is not None and st.iterationNumber > 0 else float("inf"))
+        return self._gnc.should_update(team)
 
     def updateMeasurementWeights(self):
         """GNC-TLS update of the loop closures this robot owns (non-fixed,
@@ -293,7 +307,7 @@ class PGOAgent:
                 w[k] = self._weights[k]
         self._weights = w
         self._apply_missing_neighbours()
-        self.weight_updates += 1
+        self._gnc.updated()
 
     def setMeasurementWeight(self, src: PoseID, dst: PoseID, weight: float, fixed_weight: bool = False):
         k = self._edge_index.get((src.robot_id, src.frame_id, dst.robot_id, dst.frame_id))

@@ -4,28 +4,37 @@ Reference control flow (drawio:1954-2066, 2071, 2466-2481):
   * every round the executing robots run PGOAgent::iterate(doOptimization)
     against the neighbour poses they last received (publishPublicPoses ->
     updateNeighborPoses, drawio:2340-2355);
-  * every ``robustOptInnerIters`` rounds the leader sends UPDATE_WEIGHT and every
-    agent runs updateMeasurementWeights (drawio:2212-2215); the owner of a
-    shared loop closure (lower robot id) sends its weight to the peer
-    (publishMeasurementWeights, drawio:2195-2198);
+  * the leader sends UPDATE_WEIGHT when shouldUpdateMeasurementWeights holds
+    (drawio:2466-2469: more than robustOptInnerIters rounds since the last
+    update, or every agent converged; at most robustOptNumWeightUpdates
+    updates) and every agent runs updateMeasurementWeights (drawio:2212-2215);
   * schedule: dpgo_ros lets ONE robot iterate per round (``sequential``,
-    drawio:2478-2481); the MI355X layout updates every block each round
-    (``concurrent``, SURVEY.md §0 finding 6, §8e).
+    drawio:2478-2481; the leader picks it round-robin or uniformly at random,
+    kmx.dpgo.schedule.ExecutingRobot); the MI355X layout updates every block
+    each round (``concurrent``, SURVEY.md §0 finding 6, §8e);
+  * the leader terminates the team once every agent is ready or maxNumIters
+    rounds ran (shouldTerminate, drawio:2027-2030).
 
 Placement: robot blocks are dealt to ranks in contiguous ranges (one process
 per GPU). ROS topics become collectives over RCCL/xGMI:
-  public_poses          -> one all_to_all per round carrying, to every peer,
+  public_poses + status -> ONE all_to_all per round carrying, to every peer,
                            only the public-pose rows its shared loop closures
-                           reference (``exchange="alltoall"``, default); or one
-                           all_gather of every owned public row (``"allgather"``)
-  measurement_weights   -> all_reduce(SUM) of the owner-packed shared weights
+                           reference, plus this rank's status word (its largest
+                           relative change) at the end of every segment
+  measurement_weights   -> none: both ranks of a shared loop closure evaluate
+                           its GNC weight from the same two rows on the device
+                           (bitwise the owner's value, drawio:2195-2198)
   lifting_matrix/anchor -> injected at initialisation (identical on all ranks)
+  UPDATE_WEIGHT         -> decided on the device at the start of each round
+                           from the schedule state and the team status
+  TERMINATE             -> all_reduce(MAX) of the ranks' largest relative change
 """
 from __future__ import annotations
 
 import numpy as np
 
 from .params import PGOAgentParameters
+from .schedule import ExecutingRobot
 from .solver import BlockSolver
 
 
@@ -71,32 +80,25 @@ def exchange_plan(graph, world: int, rank: int):
 
 class RBCDDriver:
     def __init__(self, params: PGOAgentParameters, graph, *, rank: int = 0, world: int = 1,
-                 device: int = 0, seed: int = 0, solver=None, exchange_device: str | None = None,
-                 exchange: str = "alltoall"):
+                 device: int = 0, solver=None, exchange_device: str | None = None):
         """`solver` defaults to a BlockSolver on HIP device `device`; any object
-        with the same exchange interface can be injected (the CPU gloo tests do).
-        `exchange_device` is where the collective runs ("cuda" for RCCL, "cpu"
-        for gloo). A GPU solver under gloo packs into device buffers and stages
-        them through host copies (used to test N ranks on one GPU).
-        `exchange` selects the public-pose collective ("alltoall" or
-        "allgather"); both give bitwise identical iterates."""
+        with the same interface can be injected (the CPU gloo tests inject the
+        restatement). `exchange_device` is where the collective runs ("cuda"
+        for RCCL, "cpu" for gloo). A GPU solver under gloo packs into device
+        buffers and stages them through host copies (N ranks on one GPU)."""
         if world > graph.n_robots:
             raise ValueError("need at least one robot block per rank")
-        if exchange not in ("alltoall", "allgather"):
-            raise ValueError("exchange must be 'alltoall' or 'allgather'")
         self.params = params
         self.graph = graph
         self.rank, self.world = rank, world
-        self.exchange = exchange
         lo, hi = robot_ranges(graph.n_robots, world)[rank]
         self.robots = list(range(lo, hi))
         local = np.zeros(graph.n_robots, np.uint8)
         local[lo:hi] = 1
         self.local = local
         self.solver = solver if solver is not None else BlockSolver(params, device)
-        self.rng = np.random.Generator(np.random.PCG64(seed))
+        self.executing = ExecutingRobot(params.updateRule, params.randomSeed)
         self.round_index = 0
-        self.weight_updates = 0
         self._torch = None
         self._xdev = exchange_device
         if world > 1:
@@ -108,6 +110,9 @@ class RBCDDriver:
             if getattr(self.solver, "device_pointers", False):  # order kmx work with torch's copies
                 self.solver.set_stream(torch.cuda.current_stream().cuda_stream)
         self.solver.set_graph_data(graph, local)
+        P = params
+        self.solver.set_gnc_schedule(int(P.robustCostParams.costType) != 0, P.robustOptInnerIters,
+                                     P.robustOptNumWeightUpdates, P.relChangeTol)
         self.n_pub, self.first_owned, self.n_owned = self.solver.public_count()
         self.m_local = {a: self.solver.local_edges(a) for a in self.robots}
         self.exchange_rows = (0, 0)  # (rows sent, rows received) per round
@@ -116,145 +121,125 @@ class RBCDDriver:
 
     # ------------------------------------------------------ collectives ---
     def _setup_exchange(self):
-        torch, dist = self._torch, self._dist
+        torch = self._torch
         ps = 4 * self.params.r
         on_gpu = bool(getattr(self.solver, "device_pointers", False))
         self._stage = on_gpu and self._xdev != "cuda"
         dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
-        self.n_shared = self.solver.shared_count()
-        self._wshared = torch.zeros(max(self.n_shared, 1), dtype=torch.float64, device=dev)
-        if self.exchange == "alltoall":
-            send_slots, send_counts, recv_slots, recv_counts = exchange_plan(self.graph, self.world, self.rank)
-            self._n_send, self._n_recv = int(send_slots.shape[0]), int(recv_slots.shape[0])
-            self._send_splits = [int(c) * ps for c in send_counts]
-            self._recv_splits = [int(c) * ps for c in recv_counts]
-            one = np.zeros(1, np.int32)
-            self._sslots = torch.as_tensor(send_slots.astype(np.int32) if self._n_send else one, device=dev)
-            self._rslots = torch.as_tensor(recv_slots.astype(np.int32) if self._n_recv else one, device=dev)
-            self._sbuf = torch.zeros(max(self._n_send, 1) * ps, dtype=torch.float64, device=dev)
-            self._rbuf = torch.zeros(max(self._n_recv, 1) * ps, dtype=torch.float64, device=dev)
-            self.exchange_rows = (self._n_send, self._n_recv)
-            return
-        counts = [None] * self.world
-        dist.all_gather_object(counts, (self.first_owned, self.n_owned))
-        self.max_owned = max(max(c[1] for c in counts), 1)
-        self._send = torch.zeros(self.max_owned * ps, dtype=torch.float64, device=dev)
-        self._recv = torch.zeros(self.world * self.max_owned * ps, dtype=torch.float64, device=dev)
-        # rows of the gathered buffer in public-table order
-        idx = np.full(max(self.n_pub, 1), 0, dtype=np.int64)
-        for k, (first, n) in enumerate(counts):
-            idx[first:first + n] = k * self.max_owned + np.arange(n)
-        self._row_index = torch.as_tensor(idx[: max(self.n_pub, 1)], device=dev)
-        self._table = torch.zeros(max(self.n_pub, 1) * ps, dtype=torch.float64, device=dev)
-        self.exchange_rows = (self.n_owned * (self.world - 1), self.n_pub - self.n_owned)
-
-    def _all_gather(self, out, inp):
-        """One all-gather of equal-size chunks (RCCL: into one tensor; gloo has
-        no all_gather_into_tensor, so gather a list of views)."""
-        if self._xdev == "cuda":
-            self._dist.all_gather_into_tensor(out, inp)
-        elif self._stage:
-            self.solver.sync()
-            ho, hi = out.cpu(), inp.cpu()
-            self._dist.all_gather(list(ho.chunk(self.world)), hi)
-            out.copy_(ho)
-        else:
-            self._dist.all_gather(list(out.chunk(self.world)), inp)
+        send_slots, send_counts, recv_slots, recv_counts = exchange_plan(self.graph, self.world, self.rank)
+        self._n_send, self._n_recv = int(send_slots.shape[0]), int(recv_slots.shape[0])
+        # one status double closes every per-peer segment
+        self._send_splits = [int(c) * ps + 1 for c in send_counts]
+        self._recv_splits = [int(c) * ps + 1 for c in recv_counts]
+        one = np.zeros(1, np.int32)
+        self._sslots = torch.as_tensor(send_slots.astype(np.int32) if self._n_send else one, device=dev)
+        self._rslots = torch.as_tensor(recv_slots.astype(np.int32) if self._n_recv else one, device=dev)
+        self._sseg = torch.as_tensor(np.concatenate([[0], np.cumsum(send_counts)]).astype(np.int32), device=dev)
+        self._rseg = torch.as_tensor(np.concatenate([[0], np.cumsum(recv_counts)]).astype(np.int32), device=dev)
+        self._sbuf = torch.zeros(sum(self._send_splits), dtype=torch.float64, device=dev)
+        self._rbuf = torch.zeros(sum(self._recv_splits), dtype=torch.float64, device=dev)
+        self.exchange_rows = (self._n_send, self._n_recv)
 
     def _all_to_all(self, out, inp):
-        """One all-to-all with per-peer row counts (RCCL directly; a GPU solver
-        under gloo stages through host copies)."""
-        o, i = out[: sum(self._recv_splits)], inp[: sum(self._send_splits)]
+        """One all-to-all with per-peer sizes (RCCL directly; a GPU solver under
+        gloo stages through host copies)."""
         if self._stage:
             self.solver.sync()
-            ho, hi = o.cpu(), i.cpu()
+            ho, hi = out.cpu(), inp.cpu()
             self._dist.all_to_all_single(ho, hi, self._recv_splits, self._send_splits)
-            o.copy_(ho)
+            out.copy_(ho)
         else:
-            self._dist.all_to_all_single(o, i, self._recv_splits, self._send_splits)
+            self._dist.all_to_all_single(out, inp, self._recv_splits, self._send_splits)
 
     def exchange_public(self):
-        """publishPublicPoses -> updateNeighborPoses for the whole team."""
+        """publishPublicPoses -> updateNeighborPoses (+ publishStatus) for the
+        whole team."""
+        self.solver.refresh_local()  # the owned slots of the table
         if self.world == 1:
-            self.solver.refresh_local()
             return
-        ps = 4 * self.params.r
-        if self.exchange == "alltoall":
-            self.solver.refresh_local()  # the owned slots of the table
-            self.solver.gather_public_rows(self._sslots.data_ptr(), self._n_send, self._sbuf.data_ptr())
-            self._all_to_all(self._rbuf, self._sbuf)
-            self.solver.scatter_public_rows(self._rslots.data_ptr(), self._n_recv, self._rbuf.data_ptr())
-            return
-        self.solver.pack_public(self._send.data_ptr())
-        self._all_gather(self._recv, self._send)
-        if self.n_pub:
-            rows = self._recv.view(-1, ps).index_select(0, self._row_index)
-            self._table.view(-1, ps).copy_(rows)
-            self.solver.unpack_public(self._table.data_ptr())
+        s = self.solver
+        s.exchange_pack(self._sslots.data_ptr(), self._n_send, self._sseg.data_ptr(), self.world,
+                        self._sbuf.data_ptr())
+        self._all_to_all(self._rbuf, self._sbuf)
+        s.exchange_unpack(self._rslots.data_ptr(), self._n_recv, self._rseg.data_ptr(), self.world,
+                          self._rbuf.data_ptr())
 
     def update_weights(self) -> float:
-        """UPDATE_WEIGHT: every agent re-weights the loop closures it owns, then
-        owners send shared-edge weights to their peers."""
+        """An explicit UPDATE_WEIGHT (outside the schedule): fresh neighbour rows,
+        then every handle re-weights the loop closures it holds."""
         self.exchange_public()
-        mu = self.solver.update_weights()
-        if self.world > 1 and self.n_shared:
-            self.solver.pack_shared_weights(self._wshared.data_ptr())
-            if self._stage:
-                self.solver.sync()
-                hw = self._wshared.cpu()
-                self._dist.all_reduce(hw)
-                self._wshared.copy_(hw)
-            else:
-                self._dist.all_reduce(self._wshared)
-            self.solver.unpack_shared_weights(self._wshared.data_ptr())
-        self.weight_updates += 1
-        return mu
+        return self.solver.update_weights()
+
+    @property
+    def weight_updates(self) -> int:
+        return int(self.solver.gnc_state()["updates"])
 
     # ------------------------------------------------------------ rounds ---
     def initialize(self, X_by_robot: dict):
         for a in self.robots:
             self.solver.set_iterate(a, X_by_robot[a])
 
-    def should_update_weights(self) -> bool:
-        """shouldUpdateMeasurementWeights (drawio:2466-2469), iteration-count form."""
-        rc = self.params.robustCostParams
-        if int(rc.costType) == 0:
-            return False
-        if self.weight_updates >= self.params.robustOptNumWeightUpdates:
-            return False
-        return self.round_index > 0 and self.round_index % self.params.robustOptInnerIters == 0
-
     def active_mask(self) -> np.ndarray:
         act = np.zeros(self.graph.n_robots, np.uint8)
-        if self.params.schedule == 0:  # sequential: leader picks one executing robot
-            act[self.round_index % self.graph.n_robots] = 1
+        if self.params.schedule == 0:  # sequential: the leader picks one executing robot
+            act[self.executing.next(range(self.graph.n_robots))] = 1
         else:
             act[:] = 1
         return act
 
     def step(self, with_stats: bool = True):
-        """One synchronous round. Returns per-robot stats (team-indexed)."""
+        """One synchronous round (its GNC decision runs on the device first).
+        Returns per-robot stats (team-indexed) when with_stats."""
         self.exchange_public()
         stats = None
         if with_stats or self.params.schedule == 0:
             stats = self.solver.iterate(self.active_mask())
         else:
-            self.solver.iterate_async(1, refresh_local=False, gnc_every=0)
+            self.solver.iterate_async(1, refresh_local=False)
         self.round_index += 1
-        if self.should_update_weights():
-            self.update_weights()
         return stats
 
     def run_async(self, rounds: int):
         """Benchmark path: enqueue `rounds` concurrent rounds with no host sync
-        (single GPU: one C call; multi-GPU: collectives between rounds)."""
+        (single GPU: one C call; multi-GPU: one all-to-all between rounds)."""
         if self.world == 1 and self.params.schedule == 1:
-            gnc = self.params.robustOptInnerIters if int(self.params.robustCostParams.costType) != 0 else 0
-            self.solver.iterate_async(rounds, refresh_local=True, gnc_every=gnc)
+            self.solver.iterate_async(rounds, refresh_local=True)
             self.round_index += rounds
             return
         for _ in range(rounds):
             self.step(with_stats=False)
+
+    def team_max_rel_change(self) -> float:
+        """Largest relative change of the team's last block updates (one
+        all_reduce(MAX) of the ranks' status; synchronises)."""
+        v = self.solver.status()
+        local = float(np.max(v[self.robots])) if self.robots else 0.0
+        if self.world == 1:
+            return local
+        t = self._torch.tensor([local], dtype=self._torch.float64,
+                               device="cuda" if self._xdev == "cuda" else "cpu")
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def should_terminate(self) -> bool:
+        """shouldTerminate (drawio:2027-2030): maxNumIters rounds ran, or every
+        agent's relative change is below relChangeTol."""
+        if self.round_index >= self.params.maxNumIters:
+            return True
+        return self.team_max_rel_change() < self.params.relChangeTol
+
+    def run(self, max_rounds: int | None = None, check_every: int = 10) -> int:
+        """Rounds until shouldTerminate (checked every `check_every` rounds and
+        at the end); returns the rounds run."""
+        limit = self.params.maxNumIters if max_rounds is None else max_rounds
+        done = 0
+        while done < limit:
+            k = min(check_every, limit - done)
+            self.run_async(k)
+            done += k
+            if self.should_terminate():
+                break
+        return done
 
     def iterate_of(self, robot: int) -> np.ndarray:
         return self.solver.get_iterate(robot)

@@ -63,6 +63,8 @@ class PGOAgentParameters:
     robustOptNumWeightUpdates: int = 50    # after this many updates weights freeze
     robustOptMinConvergenceRatio: float = 0.8
     schedule: int = 1                      # 0 sequential (dpgo_ros sync), 1 concurrent
+    updateRule: int = 0                    # sequential: 0 round-robin, 1 uniform (dpgo_ros update rule)
+    randomSeed: int = 0                    # seed of the uniform rule's std::mt19937 (dpgo_ros random_seed)
 
     def to_c(self) -> PgoParams:
         lo, rc = self.localOptimizationParams, self.robustCostParams

@@ -108,6 +108,16 @@ class BlockSolver:
         check(self.L.kmx_pgo_scatter_public_rows(self.h, C.c_void_p(slots_ptr), int(n), C.c_void_p(rows_ptr)),
               "kmx_pgo_scatter_public_rows")
 
+    def exchange_pack(self, slots_ptr: int, n: int, seg_ptr: int, n_seg: int, out_ptr: int):
+        """Rows of n owned slots + this handle's status after each of n_seg
+        per-peer segments (kmx_pgo_exchange_pack)."""
+        check(self.L.kmx_pgo_exchange_pack(self.h, C.c_void_p(slots_ptr), int(n), C.c_void_p(seg_ptr), int(n_seg),
+                                           C.c_void_p(out_ptr)), "kmx_pgo_exchange_pack")
+
+    def exchange_unpack(self, slots_ptr: int, n: int, seg_ptr: int, n_seg: int, in_ptr: int):
+        check(self.L.kmx_pgo_exchange_unpack(self.h, C.c_void_p(slots_ptr), int(n), C.c_void_p(seg_ptr),
+                                             int(n_seg), C.c_void_p(in_ptr)), "kmx_pgo_exchange_unpack")
+
     def refresh_local(self):
         check(self.L.kmx_pgo_refresh_local(self.h), "kmx_pgo_refresh_local")
 
@@ -124,14 +134,47 @@ class BlockSolver:
         check(self.L.kmx_pgo_iterate(self.h, u8ptr(act), stats), "kmx_pgo_iterate")
         return [s.as_dict() for s in stats]
 
-    def iterate_async(self, rounds: int, refresh_local: bool = True, gnc_every: int = 0):
-        check(self.L.kmx_pgo_iterate_async(self.h, rounds, 1 if refresh_local else 0, gnc_every),
-              "kmx_pgo_iterate_async")
+    def iterate_async(self, rounds: int, refresh_local: bool = True):
+        check(self.L.kmx_pgo_iterate_async(self.h, rounds, 1 if refresh_local else 0), "kmx_pgo_iterate_async")
 
     def sync(self):
         check(self.L.kmx_pgo_sync(self.h), "kmx_pgo_sync")
 
     # ------------------------------------------------------------- GNC ---
+    def set_gnc_schedule(self, enabled: bool, inner_iters: int = 20, max_updates: int = 2**31 - 1,
+                         rel_change_tol: float = 1e-3):
+        """Device-side shouldUpdateMeasurementWeights at every round begin."""
+        check(self.L.kmx_pgo_set_gnc_schedule(self.h, 1 if enabled else 0, int(inner_iters),
+                                              int(min(max_updates, 2**31 - 1)), float(rel_change_tol)),
+              "kmx_pgo_set_gnc_schedule")
+
+    def gnc_state(self) -> dict:
+        s = abi.GncState()
+        check(self.L.kmx_pgo_get_gnc_state(self.h, C.byref(s)), "kmx_pgo_get_gnc_state")
+        return s.as_dict()
+
+    def set_gnc_state(self, state: dict):
+        s = abi.GncState()
+        s.inner_iter, s.updates = int(state["inner_iter"]), int(state["updates"])
+        s.last_fired, s.rounds, s.mu = int(state.get("last_fired", 0)), int(state.get("rounds", 0)), state["mu"]
+        check(self.L.kmx_pgo_set_gnc_state(self.h, C.byref(s)), "kmx_pgo_set_gnc_state")
+
+    def status(self) -> np.ndarray:
+        """Per-robot relative change of the last block update (inf: none yet)."""
+        v = np.full(self.n_robots, np.nan)
+        check(self.L.kmx_pgo_get_status(self.h, fptr(v)), "kmx_pgo_get_status")
+        return v
+
+    def set_status(self, v: np.ndarray):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        check(self.L.kmx_pgo_set_status(self.h, fptr(v)), "kmx_pgo_set_status")
+
+    def memory(self) -> tuple[int, int]:
+        """(resident device bytes, bytes per incidence record)."""
+        b, rb = C.c_int64(), C.c_int()
+        check(self.L.kmx_pgo_memory(self.h, C.byref(b), C.byref(rb)), "kmx_pgo_memory")
+        return b.value, rb.value
+
     def update_weights(self) -> float:
         mu = C.c_double()
         check(self.L.kmx_pgo_update_weights(self.h, C.byref(mu)), "kmx_pgo_update_weights")

@@ -181,6 +181,16 @@ class LoopClosureDetector:
     def sync(self):
         check(self.L.kmx_lcd_sync(self.h), "kmx_lcd_sync")
 
+    def enable_timing(self, on: bool = True):
+        check(self.L.kmx_lcd_enable_timing(self.h, 1 if on else 0), "kmx_lcd_enable_timing")
+
+    def read_timing(self) -> dict:
+        """Device times (ms) of the kNN2 and RANSAC launches of the last evented
+        verification."""
+        a, b = C.c_double(), C.c_double()
+        check(self.L.kmx_lcd_read_timing(self.h, C.byref(a), C.byref(b)), "kmx_lcd_read_timing")
+        return {"knn_ms": a.value, "ransac_ms": b.value}
+
     # computeMatchedIndices on two descriptor sets (single pair)
     @staticmethod
     def compute_matched_indices(desc_query, desc_match, lowe_ratio: float = 0.7, norm: str = "l1"):

@@ -600,6 +600,27 @@ int orc_pgo_update_weights_owned(void* vh, const uint8_t* local, double* mu_used
   return 0;
 }
 
+/* Sweep of a process that holds only the robots in `local`, as the HIP
+ * handle does: every non-fixed edge with a local endpoint, local endpoints
+ * from the iterate, foreign ones from the neighbour table. A shared loop
+ * closure is evaluated on both robots' processes from the same two rows, so
+ * both get the owner's weight (owner = min(r1, r2), drawio:2195-2198). */
+int orc_pgo_update_weights_local(void* vh, const uint8_t* local, double* mu_used) {
+  orc_pgo* h = (orc_pgo*)vh;
+  if (mu_used) *mu_used = h->mu;
+  if (h->P.robust_cost != KMX_COST_GNC_TLS) return 0;
+  const int ps = PS(h);
+  for (int64_t e = 0; e < h->m; ++e) {
+    if (h->fixed[e]) continue;
+    if (!local[h->r1[e]] && !local[h->r2[e]]) continue;
+    const double* Xi = (local[h->r1[e]] ? h->X : h->nbr) + (h->poff[h->r1[e]] + h->p1[e]) * ps;
+    const double* Xj = (local[h->r2[e]] ? h->X : h->nbr) + (h->poff[h->r2[e]] + h->p2[e]) * ps;
+    h->w[e] = gnc_tls_weight(residual_sq(h, e, Xi, Xj), h->mu, h->P.gnc_barc);
+  }
+  h->mu *= h->P.gnc_mu_step;
+  return 0;
+}
+
 /* ------------------------------------------------------------ rounding -- */
 /* symmetric 3x3 Jacobi eigen-decomposition (cyclic, fixed sweeps) */
 static void jacobi3(double A[9], double V[9]) {

@@ -15,7 +15,10 @@ from pathlib import Path
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB = HERE / "build" / "liborc.so"
+import os  # noqa: E402
+
+# ORC_LIB selects another build of the same sources (bench.py's -march=native one)
+LIB = Path(os.environ.get("ORC_LIB", HERE / "build" / "liborc.so"))
 
 _lib = None
 
@@ -57,6 +60,7 @@ def _setup(L):
         "orc_pgo_round_mt": ([P, pu8, C.POINTER(IterStats), C.c_int], C.c_int),
         "orc_pgo_round_nbr": ([P, pu8, C.POINTER(IterStats)], C.c_int),
         "orc_pgo_update_weights_owned": ([P, pu8, pf64], C.c_int),
+        "orc_pgo_update_weights_local": ([P, pu8, pf64], C.c_int),
         "orc_pgo_set_nbr_rows": ([P, i64, pi32, pi32, pf64], C.c_int),
         "orc_pgo_get_x_rows": ([P, i64, pi32, pi32, pf64], C.c_int),
         "orc_pgo_update_weights": ([P, pf64], C.c_int),
@@ -184,6 +188,12 @@ class OraclePGO:
         loc = np.ascontiguousarray(local, dtype=np.uint8)
         mu = C.c_double(0)
         self.L.orc_pgo_update_weights_owned(self.h, _u(loc), C.byref(mu))
+        return mu.value
+
+    def update_weights_local(self, local):
+        loc = np.ascontiguousarray(local, dtype=np.uint8)
+        mu = C.c_double(0)
+        self.L.orc_pgo_update_weights_local(self.h, _u(loc), C.byref(mu))
         return mu.value
 
     def get_weights(self):

@@ -1,6 +1,7 @@
 # usage: bash scripts/gpu_pmc_hess.sh [tag] — HBM traffic of the dpgo kernels:
-# separate rocprofv3 --pmc passes (kernel trace only) over `bench.py --profile --warmup 0`,
-# so every profiled k_hess dispatch is also counted in the bench JSON of that pass.
+# separate rocprofv3 --pmc passes (kernel trace only) over `bench.py --profile` (burn-in 40 +
+# 10 rounds, every round evented), so every profiled k_hess dispatch is also counted in the
+# bench JSON of that pass (empty dispatches read ~0 bytes and are not counted as launches).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -9,7 +10,7 @@ mkdir -p gpurun_out/$TAG
 i=0
 for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $C -d gpurun_out/$TAG/p$i -o run --output-format csv -- python3 bench.py --steps 6 --warmup 0 --profile > gpurun_out/$TAG/p$i.json 2> gpurun_out/$TAG/p$i.err
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $C -d gpurun_out/$TAG/p$i -o run --output-format csv -- python3 bench.py --steps 10 --warmup 0 --profile --no-cpu --no-lcd > gpurun_out/$TAG/p$i.json 2> gpurun_out/$TAG/p$i.err
   rc=$?; echo "pmc pass $i ($C) rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done

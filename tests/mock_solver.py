@@ -1,11 +1,15 @@
 """CPU stand-in for kmx.dpgo.solver.BlockSolver used ONLY by the gloo tests of
-the multi-process driver path: the same exchange interface (pack / unpack of
-the public-pose table through raw pointers, owner-packed shared weights) on
-top of the CPU restatement. It is test infrastructure (imports oracle/)."""
+the multi-process driver path and the CPU pipeline tests: the same interface
+(exchange pack / unpack through raw pointers with the status word after every
+peer segment, the round-begin GNC schedule, the status of the last block
+updates) on top of the CPU restatement. It is test infrastructure (imports
+oracle/); the schedule is kmx.dpgo.schedule.GncSchedule, the host mirror of
+the device rule in csrc/pgo.hip."""
 import ctypes as C
 
 import numpy as np
 
+from kmx.dpgo.schedule import GncSchedule
 from oracle.oracle import OraclePGO
 
 
@@ -13,12 +17,16 @@ class OracleBlockSolver:
     def __init__(self, params):
         self.params = params
         self.r = params.r
+        self.gnc = GncSchedule.from_params(params)
+        self.gnc_on = False
+        self.ext = np.zeros(0)
 
     def set_stream(self, s):  # pragma: no cover - CPU only
         pass
 
     def set_graph_data(self, g, local):
         self.g = g
+        self.n_robots = g.n_robots
         self.local = np.asarray(local, np.uint8)
         self.o = OraclePGO(self.params.to_c(), g)
         sh = g.r1 != g.r2
@@ -31,8 +39,7 @@ class OracleBlockSolver:
         self.first_owned = int(idx[0]) if idx.size else 0
         self.n_owned = int(idx.size)
         self.shared_edges = np.nonzero(sh)[0]
-        owner = np.minimum(g.r1, g.r2)
-        self.owned_shared = self.local[owner[self.shared_edges]] == 1
+        self.relc = np.where(np.asarray(g.n_poses) > 0, np.inf, 0.0)
 
     def public_count(self):
         return int(self.pub_robot.shape[0]), self.first_owned, self.n_owned
@@ -49,51 +56,78 @@ class OracleBlockSolver:
     def _rows(self):
         return 4 * self.r
 
-    def pack_public(self, ptr):
-        sl = slice(self.first_owned, self.first_owned + self.n_owned)
-        X = np.ascontiguousarray(self.o.get_x_rows(self.pub_robot[sl], self.pub_pose[sl]))
-        C.memmove(ptr, X.ctypes.data, X.nbytes)
+    # ------------------------------------------------------- exchange ---
+    @staticmethod
+    def _i32(ptr, n):
+        return np.frombuffer((C.c_int32 * n).from_address(ptr), dtype=np.int32).copy()
 
-    def unpack_public(self, ptr):
-        n = self.pub_robot.shape[0]
-        buf = (C.c_double * (n * self._rows())).from_address(ptr)
-        X = np.frombuffer(buf, dtype=np.float64).reshape(n, self.r, 4).copy()
-        self.o.set_nbr_rows(self.pub_robot, self.pub_pose, X)
+    def exchange_pack(self, slots_ptr, n, seg_ptr, n_seg, out_ptr):
+        ps = self._rows()
+        seg = self._i32(seg_ptr, n_seg + 1) if n_seg else np.array([0, n], np.int32)
+        sl = self._i32(slots_ptr, n) if n else np.zeros(0, np.int32)
+        X = np.ascontiguousarray(self.o.get_x_rows(self.pub_robot[sl], self.pub_pose[sl])).reshape(n, ps)
+        tot = n * ps + n_seg
+        buf = np.frombuffer((C.c_double * max(tot, 1)).from_address(out_ptr), dtype=np.float64)
+        mine = float(np.max(self.relc[self.local == 1])) if self.local.any() else 0.0
+        for k in range(max(n_seg, 1)):
+            a, b = int(seg[k]), int(seg[k + 1])
+            buf[a * ps + k: b * ps + k] = X[a:b].reshape(-1)
+            if n_seg:
+                buf[b * ps + k] = mine
 
-    def gather_public_rows(self, slots_ptr, n, out_ptr):
-        if n == 0:
-            return
-        sl = np.frombuffer((C.c_int32 * n).from_address(slots_ptr), dtype=np.int32).copy()
-        X = np.ascontiguousarray(self.o.get_x_rows(self.pub_robot[sl], self.pub_pose[sl]))
-        C.memmove(out_ptr, X.ctypes.data, X.nbytes)
-
-    def scatter_public_rows(self, slots_ptr, n, rows_ptr):
-        if n == 0:
-            return
-        sl = np.frombuffer((C.c_int32 * n).from_address(slots_ptr), dtype=np.int32).copy()
-        buf = (C.c_double * (n * self._rows())).from_address(rows_ptr)
-        X = np.frombuffer(buf, dtype=np.float64).reshape(n, self.r, 4).copy()
-        self.o.set_nbr_rows(self.pub_robot[sl], self.pub_pose[sl], X)
+    def exchange_unpack(self, slots_ptr, n, seg_ptr, n_seg, in_ptr):
+        ps = self._rows()
+        seg = self._i32(seg_ptr, n_seg + 1) if n_seg else np.array([0, n], np.int32)
+        sl = self._i32(slots_ptr, n) if n else np.zeros(0, np.int32)
+        tot = n * ps + n_seg
+        buf = np.frombuffer((C.c_double * max(tot, 1)).from_address(in_ptr), dtype=np.float64).copy()
+        rows = np.empty((n, ps))
+        ext = []
+        for k in range(max(n_seg, 1)):
+            a, b = int(seg[k]), int(seg[k + 1])
+            rows[a:b] = buf[a * ps + k: b * ps + k].reshape(-1, ps)
+            if n_seg:
+                ext.append(buf[b * ps + k])
+        if n:
+            self.o.set_nbr_rows(self.pub_robot[sl], self.pub_pose[sl], rows.reshape(n, self.r, 4))
+        self.ext = np.array(ext)
 
     def refresh_local(self):
         X = self.o.get_x_rows(self.pub_robot, self.pub_pose)
-        self.o.set_nbr_rows(self.pub_robot, self.pub_pose, X)
+        own = self.local[self.pub_robot] == 1
+        self.o.set_nbr_rows(self.pub_robot[own], self.pub_pose[own], X[own])
+
+    # --------------------------------------------------------- rounds ---
+    def set_gnc_schedule(self, enabled, inner_iters=20, max_updates=2**31 - 1, rel_change_tol=1e-3):
+        self.gnc_on = bool(enabled)
+        self.gnc.inner_iters, self.gnc.max_updates = int(inner_iters), int(max_updates)
+        self.gnc.rel_change_tol = float(rel_change_tol)
+
+    def gnc_state(self):
+        return {"inner_iter": self.gnc.inner, "updates": self.gnc.updates, "mu": self.o.mu}
+
+    def status(self):
+        return self.relc.copy()
+
+    def _round(self, active):
+        team = np.concatenate([self.relc[self.local == 1], self.ext])
+        if self.gnc_on and self.gnc.should_update(team):
+            self.update_weights()
+        st = self.o.iterate_nbr(np.asarray(active, np.uint8) & self.local)
+        for a, s in enumerate(st):
+            if s["updated"]:
+                self.relc[a] = s["rel_change"]
+        self.gnc.round_done()
+        return st
 
     def iterate(self, active):
-        act = np.asarray(active, np.uint8) & self.local
-        return self.o.iterate_nbr(act)
+        return self._round(active)
 
-    def iterate_async(self, rounds, refresh_local=True, gnc_every=0):
-        # same schedule as kmx_pgo_iterate_async: GNC after every gnc_every-th round
+    def iterate_async(self, rounds, refresh_local=True):
         for _ in range(rounds):
             if refresh_local:
                 self.refresh_local()
-            self.o.iterate_nbr(self.local)
-            self.rounds_done = getattr(self, "rounds_done", 0) + 1
-            if gnc_every > 0 and int(self.params.robustCostParams.costType) != 0 and self.rounds_done % gnc_every == 0:
-                if refresh_local:
-                    self.refresh_local()
-                self.update_weights()
+            self._round(self.local)
 
     def sync(self):
         pass
@@ -111,19 +145,6 @@ class OracleBlockSolver:
         return self.o.trajectory(robot, anchor)
 
     def update_weights(self):
-        return self.o.update_weights_owned(self.local)
-
-    def shared_count(self):
-        return int(self.shared_edges.shape[0])
-
-    def pack_shared_weights(self, ptr):
-        w = self.o.get_weights()[self.shared_edges]
-        w = np.ascontiguousarray(np.where(self.owned_shared, w, 0.0))
-        C.memmove(ptr, w.ctypes.data, w.nbytes)
-
-    def unpack_shared_weights(self, ptr):
-        n = self.shared_edges.shape[0]
-        tab = np.frombuffer((C.c_double * n).from_address(ptr), dtype=np.float64).copy()
-        w = self.o.get_weights()
-        w[self.shared_edges] = tab
-        self.o.set_weights(w)
+        mu = self.o.update_weights_local(self.local)
+        self.gnc.updated()
+        return mu

@@ -16,7 +16,7 @@ def test_library_exports_every_header_symbol():
     assert len(names) > 30
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
-    assert L.kmx_abi_version() == 1
+    assert L.kmx_abi_version() == abi.ABI_VERSION
 
 
 def test_no_cpu_fallback_without_gpu():

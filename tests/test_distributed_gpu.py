@@ -1,7 +1,8 @@
 """Two ranks on one MI355X (gloo exchange staged through host copies) running
 the real HIP solver: the distributed RBCD iterates and GNC weights must equal
 the single-process GPU run bit for bit (per-robot reductions are ordered the
-same whatever the rank placement)."""
+same whatever the rank placement; the GNC schedule is decided on each rank's
+device from the statuses carried by the exchange)."""
 import os
 import socket
 
@@ -18,10 +19,11 @@ def _graph():
     return make_pose_graph(4, 2000, 5000, seed=3)
 
 
-def _params():
+def _params(rel_tol=1e-3):
     from kmx.dpgo.params import PGOAgentParameters
     P = PGOAgentParameters(r=5)
     P.robustOptInnerIters = 4
+    P.relChangeTol = rel_tol
     P.schedule = 1
     return P
 
@@ -38,15 +40,15 @@ def _run(drv, rounds):
     return {a: drv.iterate_of(a) for a in drv.robots}, drv.solver.get_weights()
 
 
-def _worker(rank, world, port, rounds, q, exchange):
+def _worker(rank, world, port, rounds, q, rel_tol):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from kmx.dpgo.driver import RBCDDriver
-    g, P = _graph(), _params()
-    drv = RBCDDriver(P, g, rank=rank, world=world, device=0, exchange_device="cpu", exchange=exchange)
+    g, P = _graph(), _params(rel_tol)
+    drv = RBCDDriver(P, g, rank=rank, world=world, device=0, exchange_device="cpu")
     drv.initialize(_x0(g))
     X, w = _run(drv, rounds)
     q.put((rank, X, w, list(drv.robots)))
@@ -63,18 +65,19 @@ def _free_port():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("exchange", ["alltoall", "allgather"])
-def test_two_ranks_one_gpu_match_single_process(gpu, exchange):
+@pytest.mark.parametrize("rel_tol", [1e-3, 30.0])
+def test_two_ranks_one_gpu_match_single_process(gpu, rel_tol):
     from kmx.dpgo.driver import RBCDDriver
-    rounds = 10
-    g, P = _graph(), _params()
+    rounds = 11
+    g, P = _graph(), _params(rel_tol)
     drv = RBCDDriver(P, g, device=0)
     drv.initialize(_x0(g))
     X1, w1 = _run(drv, rounds)
+    assert drv.weight_updates >= 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q, exchange), daemon=True) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q, rel_tol), daemon=True) for r in range(2)]
     for p in procs:
         p.start()
     results = []

@@ -47,11 +47,18 @@ def _pair(g, P, X0):
     return s, o
 
 
-@pytest.mark.parametrize("r,gather", [(3, None), (5, None), (8, None), (5, "3"), (5, "2")])
-def test_primitives_match_oracle(gpu, r, gather, monkeypatch):
-    if gather is not None:
-        monkeypatch.setenv("KMX_GATHER", gather)
+def _full_records(g):
+    """Make one measurement rotation a non-rotation (1e-6 off SO(3)), so the
+    handle stores the full 128-B records instead of the compact ones."""
+    g.R[5] = g.R[5] + 1e-6 * np.random.default_rng(1).standard_normal((3, 3))
+    return g
+
+
+@pytest.mark.parametrize("r,records", [(3, "compact"), (5, "compact"), (8, "compact"), (5, "full")])
+def test_primitives_match_oracle(gpu, r, records):
     g, P, X0 = _setup(r=r)
+    if records == "full":
+        _full_records(g)
     # non-trivial GNC weights so w*kappa paths are exercised
     g.weight = np.random.default_rng(3).uniform(0.0, 1.0, g.m)
     s, o = _pair(g, P, X0)
@@ -70,17 +77,15 @@ def test_primitives_match_oracle(gpu, r, gather, monkeypatch):
             assert abs(gs - os_) <= 1e-10 * max(1.0, abs(os_)), (mode, gs, os_)
 
 
-@pytest.mark.parametrize("robust,gather", [(False, None), (True, None), (True, "nohinc"), (True, "2"), (True, "3")])
-def test_rounds_match_oracle(gpu, robust, gather, monkeypatch):
-    """gather None = default (degree-balanced gather over compact 96-B records on
-    SO(3) input, incidence-parallel Hessian gather); "nohinc" the degree-balanced
-    gather in k_hess too; "3" the per-pose compact gather; "2" the full 128-B records."""
-    if gather == "nohinc":
-        monkeypatch.setenv("KMX_HINC", "0")
-    elif gather is not None:
-        monkeypatch.setenv("KMX_GATHER", gather)
+@pytest.mark.parametrize("robust,records", [(False, "compact"), (True, "compact"), (True, "full")])
+def test_rounds_match_oracle(gpu, robust, records):
+    """compact: 96-B records (SO(3) input, rotation row 2 rebuilt); full: the
+    128-B records of a graph with a non-rotation measurement."""
     g, P, X0 = _setup(robust=robust)
+    if records == "full":
+        _full_records(g)
     s, o = _pair(g, P, X0)
+    assert s.memory()[1] == (96 if records == "compact" else 128)
     for it in range(12):
         s.refresh_local()
         sg = s.iterate()
@@ -164,7 +169,7 @@ def test_async_rounds_equal_sync_rounds(gpu):
     for _ in range(5):
         s1.refresh_local()
         s1.iterate()
-    s2.iterate_async(5, refresh_local=True, gnc_every=0)
+    s2.iterate_async(5, refresh_local=True)
     s2.sync()
     for a in range(g.n_robots):
         assert np.array_equal(s1.get_iterate(a), s2.get_iterate(a))
@@ -201,8 +206,9 @@ def test_non_rotation_measurement_uses_full_records(gpu):
     """A measurement whose rotation is not in SO(3) to 1e-12 must not go
     through the compact records (which rebuild row 2 = row0 x row1)."""
     g, P, X0 = _setup()
-    g.R[5] = g.R[5] + 1e-6 * np.random.default_rng(1).standard_normal((3, 3))
+    _full_records(g)
     s, o = _pair(g, P, X0)
+    assert s.memory()[1] == 128
     rng = np.random.default_rng(2)
     for a in range(g.n_robots):
         V = rng.standard_normal(X0[a].shape)
@@ -211,3 +217,42 @@ def test_non_rotation_measurement_uses_full_records(gpu):
             gout, _ = s.eval(a, mode, Vin)
             oout, _ = o.eval(a, mode, Vin)
             assert np.abs(gout - oout).max() <= 1e-12 * max(1.0, np.abs(oout).max()), mode
+
+
+@pytest.mark.parametrize("rel_tol", [1e-3, 30.0])
+def test_device_gnc_schedule_matches_host_rule(gpu, rel_tol):
+    """shouldUpdateMeasurementWeights evaluated on the device at every round
+    begin (kmx_pgo_set_gnc_schedule + iterate_async) against the host mirror
+    (kmx.dpgo.schedule.GncSchedule) driving the restatement: the same rounds
+    fire, the same weights and iterates follow. rel_tol 1e-3 fires on the
+    inner-iteration count only; 30 also by team convergence."""
+    from kmx.dpgo.schedule import GncSchedule
+    g, P, X0 = _setup(robust=True)
+    P.robustOptInnerIters = 3
+    P.robustOptNumWeightUpdates = 4
+    P.relChangeTol = rel_tol
+    s, o = _pair(g, P, X0)
+    s.set_gnc_schedule(True, P.robustOptInnerIters, P.robustOptNumWeightUpdates, rel_tol)
+    sched = GncSchedule.from_params(P)
+    relc = np.full(g.n_robots, np.inf)
+    fired = []
+    for it in range(14):
+        if sched.should_update(relc):
+            o.refresh()
+            o.update_weights()
+            sched.updated()
+            fired.append(it)
+        st = o.iterate()
+        relc = np.array([x["rel_change"] for x in st])
+        sched.round_done()
+        s.iterate_async(1, refresh_local=True)
+        gs = s.gnc_state()
+        assert gs["updates"] == sched.updates and gs["inner_iter"] == sched.inner, (it, gs)
+        assert bool(gs["last_fired"]) == (it in fired), it
+        for a in range(g.n_robots):
+            d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
+            assert d <= 1e-6, (it, a, d)
+        assert np.abs(s.get_weights() - o.get_weights()).max() <= 1e-9
+        assert np.abs(s.status() - relc).max() <= 1e-9
+    assert sched.updates == P.robustOptNumWeightUpdates or rel_tol < 1
+    assert len(fired) >= 3

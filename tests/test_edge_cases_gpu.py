@@ -42,17 +42,14 @@ def _hub_graph(seed=9):
         init_R=[g.init_R[0][:4], g.init_R[1], g.init_R[2]], init_t=[g.init_t[0][:4], g.init_t[1], g.init_t[2]])
 
 
-@pytest.mark.parametrize("gather,tilebal", [(None, "1"), (None, "0"), ("nohinc", "1"), ("7", "1"), ("3", "1")])
-def test_hub_pose_and_tiny_robot(gpu, gather, tilebal, monkeypatch):
+@pytest.mark.parametrize("records", ["compact", "full"])
+def test_hub_pose_and_tiny_robot(gpu, records):
     from kmx.dpgo.params import PGOAgentParameters
     from kmx.dpgo.solver import BlockSolver
     from oracle.oracle import OraclePGO
-    if gather == "nohinc":
-        monkeypatch.setenv("KMX_HINC", "0")
-    elif gather is not None:
-        monkeypatch.setenv("KMX_GATHER", gather)
-    monkeypatch.setenv("KMX_TILEBAL", tilebal)
     g = _hub_graph()
+    if records == "full":  # one non-rotation measurement: 128-B records
+        g.R[3] = g.R[3] + 1e-6 * np.random.default_rng(1).standard_normal((3, 3))
     assert np.bincount(np.concatenate([g.p1[g.r1 == 1], g.p2[g.r2 == 1]]))[17] > 300
     P = PGOAgentParameters(r=5)
     Y = lifting_matrix(5, seed=1)
