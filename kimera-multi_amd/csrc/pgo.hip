@@ -691,7 +691,18 @@ __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, co
 // after its vmcnt wait, the last adder told by the returned value, sc1 loads).
 __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_);
 
-template <int KIND, int NV, typename Store>
+// Reduction modes. RM_LAUNCH (default): the tile stores its partials and
+// k_reduce, a one-workgroup-per-robot launch, reduces them and runs the
+// control logic. RM_TICKET (KMX_RED=1): the reduction runs in the producing
+// launch behind two-level agent-scope tickets (below). Measured on configs[3]
+// (steady-state window, profiles/r02): k_hess 47.5 us with tickets vs 39.9 us
+// plus a 4.7 us k_reduce without, k_update +11 us — each workgroup's ticket
+// (write-through partial stores, vmcnt drain, a returning device-scope
+// atomic) keeps its wave and LDS allocated for microseconds after its work,
+// which delays the next generation of workgroups (k_hess runs ~2 per CU slot).
+enum RedMode { RM_LAUNCH = 0, RM_TICKET = 1 };
+
+template <int KIND, int NV, int RM, typename Store>
 __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const double* vals, char* smem_red,
                                             int R_, Store&& store, const Post& po = Post{}) {
   double* lds = reinterpret_cast<double*>(smem_red);
@@ -702,6 +713,19 @@ __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const d
     if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
   }
   __syncthreads();
+  if constexpr (RM == RM_LAUNCH) {
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int s = 0; s < NV; ++s) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
+        d.part[(size_t)L.tile * NPART + s] = t;
+      }
+    }
+    store();
+    return;
+  }
   // Waves 1..3 store their rows and leave; wave 0 publishes the tile's partials
   // (lane 0: sc1 stores, vmcnt wait, one agent-scope ticket), so the ticket's
   // round trip holds one wave, not the workgroup, and no row store is queued
@@ -894,6 +918,65 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
   }
 }
 
+// RM_LAUNCH: one workgroup per robot reduces the robot's tile partials in
+// tile order and runs the control logic (after k_update it also reports the
+// robot's tCG progress to the host).
+constexpr int RBLOCK = 256;  // k_reduce: one workgroup per robot (1024 threads measured slower: 6.3 vs 4.6 us)
+__global__ __launch_bounds__(RBLOCK) void k_reduce(Dev d, int kind, int R_, HostStatus* hs, unsigned long long seq,
+                                                  int slot) {
+  constexpr int RW_ = RBLOCK / 64;
+  __shared__ double lds[NPART * RW_];
+  const int l = blockIdx.x;
+  const int ph = d.ctl[l].phase;
+  bool act = false;
+  if (kind == RED_GRAD) act = ph == PH_START;
+  if (kind == RED_HESS || kind == RED_UPDATE) act = ph == PH_TCG;
+  if (kind == RED_COST) act = ph == PH_STEP;
+  if (!act) {
+    if (hs && threadIdx.x == 0) post_status(hs, l, seq, false);
+    return;
+  }
+  const int ns = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
+  const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
+  // the robot's tile partials, two per thread in flight (512 tiles, ~24k
+  // poses per robot, in one round trip), in tile order within each thread
+  double v[NPART] = {0.0, 0.0, 0.0, 0.0};
+  for (int tb = t0; tb < t1; tb += 2 * RBLOCK) {
+    double2 a[2], b[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = min(tb + (int)threadIdx.x + u * RBLOCK, t1 - 1);
+      const double2* p2 = reinterpret_cast<const double2*>(d.part + (size_t)t * NPART);
+      a[u] = p2[0];
+      b[u] = p2[1];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (tb + (int)threadIdx.x + u * RBLOCK < t1) {
+        v[0] += a[u].x; v[1] += a[u].y; v[2] += b[u].x; v[3] += b[u].y;
+      }
+  }
+#pragma unroll
+  for (int s = 0; s < NPART; ++s) {
+    const double w = wave_sum(v[s]);
+    if ((threadIdx.x & 63) == 0) lds[s * RW_ + (threadIdx.x >> 6)] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot[NPART];
+#pragma unroll
+    for (int s = 0; s < NPART; ++s) {
+      double acc = 0.0;
+#pragma unroll
+      for (int w = 0; w < RW_; ++w) acc += lds[s * RW_ + w];
+      tot[s] = s < ns ? acc : 0.0;
+    }
+    control(d, l, kind, tot, R_);
+    if (kind == RED_HESS && slot >= 0) atomicAdd(d.hv_launch + slot, 1);
+    if (hs) post_status(hs, l, seq, d.ctl[l].phase == PH_TCG);
+  }
+}
+
 #define KMX_SMEM extern __shared__ __attribute__((aligned(16))) char smem[]
 
 // Minimum waves per SIMD of the gather kernels: 4 at r <= 5 (128 VGPRs); the
@@ -905,7 +988,7 @@ struct LB {
 
 // Start of an RTR iteration: egrad (gather X with public neighbours), cost,
 // S = sym(Y^T egrad_Y), g = P_Y(egrad), z = precon(g); partials f, |g|^2, <z,g>.
-template <int R, int RW>
+template <int R, int RW, int RM>
 __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
@@ -925,7 +1008,7 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d) {
     vals[1] = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2] + gr[3] * gr[3];
     vals[2] = zr[0] * gr[0] + zr[1] * gr[1] + zr[2] * gr[2] + zr[3] * gr[3];
   }
-  finish_tile<RED_GRAD, 3>(d, L, vals, smem + SmemHG<R>::red_off, R, [&]() {
+  finish_tile<RED_GRAD, 3, RM>(d, L, vals, smem + SmemHG<R>::red_off, R, [&]() {
     if (!L.valid) return;
     const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
     store4(d.g + o, gr);  // r = g at the start of tCG: k_update's first step reads g
@@ -941,7 +1024,7 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d) {
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old;
 // partial <delta, Hdelta>.
-template <int R, int RW>
+template <int R, int RW, int RM>
 __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
@@ -985,7 +1068,7 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot) {
   }
   Post po;
   po.slot = slot;
-  finish_tile<RED_HESS, 1>(d, L, &v, smem + SmemH<R>::red_off, R, [&]() {
+  finish_tile<RED_HESS, 1, RM>(d, L, &v, smem + SmemH<R>::red_off, R, [&]() {
     if (L.valid) {
       store4(d.del + o, dl);
       store4(d.hd + o, hdl);
@@ -995,7 +1078,7 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot) {
 
 // tCG step, part 2: eta += coef delta, r += coef Hdelta; interior steps also
 // z = precon(r) and partials <r,r>, <z,r>.
-template <int R>
+template <int R, int RM>
 __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
@@ -1033,7 +1116,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
   Post po;
   po.hs = hs;
   po.seq = seq;
-  finish_tile<RED_UPDATE, 2>(d, L, vals, smem + SmemU::red_off, R, [&]() {
+  finish_tile<RED_UPDATE, 2, RM>(d, L, vals, smem + SmemU::red_off, R, [&]() {
     if (L.valid) {
       store4(d.eta + o, et);
       store4(d.r + o, rr);
@@ -1090,13 +1173,13 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
   }
 }
 
-template <int R, int RW>
+template <int R, int RW, int RM>
 __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
   double cost = inc_owner_cost<R, RW>(d, L, d.Xt, d.pub, smem);
-  finish_tile<RED_COST, 1>(d, L, &cost, smem + SmemC<R>::red_off, R, []() {});
+  finish_tile<RED_COST, 1, RM>(d, L, &cost, smem + SmemC<R>::red_off, R, []() {});
 }
 
 // End of a round: X <- Xt where the step was accepted, and the owned public
@@ -1220,8 +1303,8 @@ __global__ void k_begin(Dev d, const unsigned char* active, int mode, int R_) {
     return;
   }
   if (!fire) return;
-  const int i = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
-  if (i < d.n_gnc) gnc_edge<RW>(d, i, R_, mu);
+  for (int i = (blockIdx.x - 1) * blockDim.x + threadIdx.x; i < d.n_gnc; i += (gridDim.x - 1) * blockDim.x)
+    gnc_edge<RW>(d, i, R_, mu);
 }
 
 // 4x4 diagonal blocks D_i of Q per pose (hD, for the Hessian gather) and the
@@ -1587,6 +1670,7 @@ struct kmx_pgo {
   int hstat_cap = 0;
   unsigned long long seq = 0;
   bool poll = true;          // KMX_POLL=0: enqueue every tCG step (finished robots exit at once)
+  int rm = RM_LAUNCH;        // KMX_RED=1: reductions behind tickets in the producing launch (measured slower)
   bool poll_timeout = false;
   // timing
   bool timing = false;
@@ -1701,7 +1785,7 @@ void enqueue_publish(kmx_pgo* h) {
 
 template <int RW>
 void enqueue_precond_t(kmx_pgo* h, int gated) {
-  const int blocks = std::max(1, std::min(1024, (h->nloc + 127) / 128));
+  const int blocks = std::max(1, std::min(gated ? 256 : 1024, (h->nloc + 127) / 128));
   hipLaunchKernelGGL(k_precond<RW>, dim3(blocks), dim3(128), 0, h->stream, h->dv, gated);
 }
 void enqueue_precond(kmx_pgo* h, int gated) {
@@ -1714,7 +1798,8 @@ void enqueue_precond(kmx_pgo* h, int gated) {
 void enqueue_begin(kmx_pgo* h, const unsigned char* d_active, int mode) {
   const bool may_fire = h->P.robust_cost == KMX_COST_GNC_TLS && (h->gnc_on || (mode & BEGIN_FORCE_GNC));
   if (!may_fire) mode |= BEGIN_SOLO;  // no weight update possible: one block, no preconditioner rebuild
-  const unsigned grid = may_fire ? 1 + (unsigned)((h->n_gnc + 255) / 256) : 1;
+  // a capped grid: when the schedule does not fire, the launch costs its dispatch
+  const unsigned grid = may_fire ? 1 + (unsigned)std::min(256, std::max(1, (h->n_gnc + 255) / 256)) : 1;
   if (h->rw == 12)
     hipLaunchKernelGGL(k_begin<12>, dim3(grid), dim3(256), 0, h->stream, h->dv, d_active, mode, h->P.r);
   else
@@ -1745,12 +1830,17 @@ bool wait_running(kmx_pgo* h, unsigned long long seq) {
   return running;
 }
 
-template <int R, int RW>
+template <int R, int RW, int RM>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   const dim3 grid(h->ntiles), blk(BLOCK);
+  auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0, int slot = -1) {
+    if (RM == RM_LAUNCH)
+      hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot);
+  };
   enqueue_begin(h, d_active, BEGIN_ROUND);
   for (int it = 0; it < h->P.rtr_iterations; ++it) {
-    hipLaunchKernelGGL((k_grad<R, RW>), grid, blk, SmemHG<R>::bytes, h->stream, h->dv);
+    hipLaunchKernelGGL((k_grad<R, RW, RM>), grid, blk, SmemHG<R>::bytes, h->stream, h->dv);
+    red(RED_GRAD);
     // tCG: each step is (k_hess, k_update); with polling, exactly one step
     // stays queued beyond the last one known to be needed
     unsigned long long prev = 0;
@@ -1763,26 +1853,36 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
         e1 = next_event(h);
         (void)hipEventRecord(e0, h->stream);
       }
-      hipLaunchKernelGGL((k_hess<R, RW>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot);
+      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot);
       if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+      red(RED_HESS, nullptr, 0, slot);
       const bool poll = h->poll && h->hstat;
       const unsigned long long seq = poll ? ++h->seq : 0;
-      hipLaunchKernelGGL((k_update<R>), grid, blk, SmemU::bytes, h->stream, h->dv, poll ? h->hstat : nullptr, seq);
+      HostStatus* hs = poll ? h->hstat : nullptr;
+      hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv,
+                         RM == RM_TICKET ? hs : nullptr, seq);
+      red(RED_UPDATE, hs, seq);
       if (poll) {
         if (j > 0 && !wait_running(h, prev)) break;
         prev = seq;
       }
     }
     hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv);
-    hipLaunchKernelGGL((k_cost<R, RW>), grid, blk, SmemC<R>::bytes, h->stream, h->dv);
+    hipLaunchKernelGGL((k_cost<R, RW, RM>), grid, blk, SmemC<R>::bytes, h->stream, h->dv);
+    red(RED_COST);
   }
   hipLaunchKernelGGL((k_commit<R>), grid, blk, 0, h->stream, h->dv);
 }
 
 template <int R>
 void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
-  if (h->rw == 12) enqueue_round_t<R, 12>(h, d_active);
-  else enqueue_round_t<R, 16>(h, d_active);
+  if (h->rm == RM_TICKET) {
+    if (h->rw == 12) enqueue_round_t<R, 12, RM_TICKET>(h, d_active);
+    else enqueue_round_t<R, 16, RM_TICKET>(h, d_active);
+  } else {
+    if (h->rw == 12) enqueue_round_t<R, 12, RM_LAUNCH>(h, d_active);
+    else enqueue_round_t<R, 16, RM_LAUNCH>(h, d_active);
+  }
 }
 
 // One RBCD round for the robots whose d_active flag is set; it starts with
@@ -1835,6 +1935,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   }
   h->own_stream = true;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
+  if (const char* v = std::getenv("KMX_RED")) h->rm = std::atoi(v) ? RM_TICKET : RM_LAUNCH;
   *out = h;
   return KMX_OK;
   KMX_GUARD_END
