@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3: timed rounds only")
     ap.add_argument("--lcd-frames", type=int, default=50_000)
     ap.add_argument("--lcd-steps", type=int, default=3)
+    ap.add_argument("--lcd-algo", type=int, default=0,
+                    help="ransac_2d2d_algorithm: 0 Stewenius (the reference config, LcdParams.yaml:73), 1 Nister")
     return ap.parse_args()
 
 
@@ -187,7 +189,8 @@ def lcd_leg(args, rank, world, barrier_sync):
     from kmx.lcd import LcdParams, LoopClosureDetector
     from kmx.synth.lcd import make_lcd_pool
     pool = make_lcd_pool(args.lcd_frames, 500, seed=0)
-    det = LoopClosureDetector(LcdParams(), device=int(os.environ.get("KMX_BENCH_DEVICE", "0")))
+    params = LcdParams(ransac_2d2d_algorithm=args.lcd_algo)
+    det = LoopClosureDetector(params, device=int(os.environ.get("KMX_BENCH_DEVICE", "0")))
     det.set_pool(pool)
     cq = pool.cand_query[rank::world].copy()
     cm = pool.cand_match[rank::world].copy()
@@ -213,7 +216,8 @@ def lcd_leg(args, rank, world, barrier_sync):
     out = {"metric": "LC candidates verified/sec", "n_local": int(cq.shape[0]), "steps": args.lcd_steps,
            "elapsed": el, "accepted_frac_first256": sum(r["accepted"] for r in res) / max(len(res), 1),
            "workload": f"configs[2]: {args.lcd_frames} keyframes x 500 ORB descriptors (32 B), "
-                       f"{pool.cand_query.shape[0]} candidates, L1 matcher, Lowe 0.7, 5-point RANSAC "
+                       f"{pool.cand_query.shape[0]} candidates, L1 matcher, Lowe 0.7, "
+                       f"5-point {'Stewenius' if args.lcd_algo == 0 else 'Nister'} RANSAC "
                        "(thr 1e-6, <=500 it, p 0.995, seed 12345, GCC-9 sampler), 1-point 3D-3D 0.3 m",
            "roofline": {"kernel": "k_knn2 (kNN2 + Lowe)", "bound": "valu", "unit": "lane-op/s",
                         "achieved": lane_ops / (tk["knn_ms"] * 1e-3) if tk["knn_ms"] > 0 else 0.0,
@@ -226,7 +230,7 @@ def lcd_leg(args, rank, world, barrier_sync):
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, str(ROOT))
         from oracle import oracle as O
-        p = LcdParams().to_c()
+        p = params.to_c()
         n, t0c, done = 0, time.perf_counter(), 0.0
         while done < args.cpu_seconds * 0.5:
             O.lcd_verify(p, pool, cand_query=pool.cand_query[n:n + 64], cand_match=pool.cand_match[n:n + 64],

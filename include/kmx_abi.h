@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KMX_ABI_VERSION 2
+#define KMX_ABI_VERSION 3
 
 /* error codes */
 #define KMX_OK 0
@@ -291,6 +291,10 @@ int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out);
 #define KMX_RNG_GCC9 0   /* rejection of x >= 2^31, returns x (ROS Noetic)  */
 #define KMX_RNG_GCC11 1  /* Lemire: returns x >> 1                          */
 
+/* 5-point minimal solver of the 2D-2D RANSAC (opengv CentralRelativePoseSacProblem). */
+#define KMX_ALGO_STEWENIUS 0 /* opengv STEWENIUS: Groebner basis, 10x10 action matrix eigenproblem */
+#define KMX_ALGO_NISTER 1    /* opengv NISTER: degree-10 polynomial in z, Sturm roots            */
+
 /* LcdParams (params/D455/LcdParams.yaml:16-17, 51-66). */
 typedef struct kmx_lcd_params {
   int norm;                   /* KMX_NORM_* (L1: matcher_type 3 + patch:33-35) */
@@ -310,7 +314,9 @@ typedef struct kmx_lcd_params {
   double ransac_threshold_2d3d; /* PnP inlier threshold in (1 - cos) units: from
                                  a pixel threshold px and focal length f,
                                  1 - cos(atan(px / f)) (LcdParams.yaml:57)     */
-  int reserved[4];
+  int algorithm_2d2d;         /* KMX_ALGO_* 5-point minimal solver
+                                 (ransac_2d2d_algorithm, LcdParams.yaml:73)     */
+  int reserved[3];
 } kmx_lcd_params;
 
 /* computeMatchedIndices (drawio:2583-2586): k=2 brute-force match of every

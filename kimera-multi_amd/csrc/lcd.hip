@@ -855,6 +855,7 @@ struct RsParams {
   int max_iter, min2d, min3d, pmax;
   int pnp;  // pose_recovery_type 1: k_ransac stops after 2D-2D, k_pnp recovers the pose
   int prof; // diagnostic phase timers (k_ransac_coop)
+  int algo; // KMX_ALGO_*: 5-point minimal solver (k_ransac_coop; k_ransac is Nister only)
 };
 struct PnpParams {
   double thr, prob;
@@ -897,6 +898,12 @@ struct CoopWS {
       double cc[3][8];        // c1, c2, c3 of the degree-10 polynomial
       double st_lo[16], st_hi[16];
       int st_vl[16], st_vh[16], st_d[16];
+    };
+    struct {                  // Stewenius: action matrix, its Hessenberg form, eigen-solutions
+      double M[10][10];
+      double H[10][10];
+      double wr[10], wi[10];
+      double Es[10][9];
     };
   };
   union {
@@ -1064,11 +1071,14 @@ __device__ void coop_system(CoopWS& w, int lane) {
 // Lanes own columns (lane c < 20 holds A[0..9][c] in registers); column k
 // is broadcast with readlane, so a pivot step touches no LDS. Same
 // operations per element as the serial elimination (fivept_nister).
-__device__ int coop_gj(CoopWS& w, int lane) {
+// graded: the columns are first permuted to Stewenius' graded order GORD.
+__constant__ signed char GORD_D[20] = {0, 2, 4, 3, 8, 10, 1, 6, 13, 16, 5, 9, 11, 7, 14, 17, 12, 15, 18, 19};
+__device__ int coop_gj(CoopWS& w, int lane, bool graded) {
   const int cl = lane < 20 ? lane : 19;  // lanes >= 20 shadow column 19, never store
+  const int src = graded ? GORD_D[cl] : cl;
   double a[10];
 #pragma unroll
-  for (int i = 0; i < 10; ++i) a[i] = w.A[i][cl];
+  for (int i = 0; i < 10; ++i) a[i] = w.A[i][src];
   for (int k = 0; k < 10; ++k) {
     double col[10];
 #pragma unroll
@@ -1328,9 +1338,9 @@ __device__ void coop_roots(CoopWS& w, int lane, bool prof) {
   KMX_PT(10);
 }
 
-// Essential matrices from the roots (lane per root), then per E (lane per E)
-// the 4 decompositions scored on the sample; the first minimum in (E, cand)
-// order wins, as in model_from_sample. Result in w.mR / w.mt, w.ok.
+__device__ void coop_decompose(CoopWS& w, int lane, bool ok_root, const double Eo[9]);
+
+// Essential matrices from the roots (lane per root), then coop_decompose.
 __device__ void coop_models(CoopWS& w, int lane) {
   const int nr = w.nr;
   int ok_root = 0;
@@ -1356,7 +1366,13 @@ __device__ void coop_models(CoopWS& w, int lane) {
       }
     }
   }
-  // compact the surviving roots in root order (fivept_nister's ns counter)
+  coop_decompose(w, lane, ok_root != 0, Eo);
+}
+
+// Per E (lane per E, compacted in the solver's order: fivept_*'s ns counter)
+// the 4 decompositions scored on the sample; the first minimum in (E, cand)
+// order wins, as in model_from_sample. Result in w.mR / w.mt, w.ok.
+__device__ void coop_decompose(CoopWS& w, int lane, bool ok_root, const double Eo[9]) {
   const unsigned long long m = __ballot(ok_root);
   const int slot = __popcll(m & ((1ull << lane) - 1ull));
   const int ne = __popcll(m);
@@ -1405,9 +1421,363 @@ __device__ void coop_models(CoopWS& w, int lane) {
   wsync();
 }
 
+// ------------------------------------------ 5-point (Stewenius 2006) --
+// oracle/lcd_oracle.c orc_fivept_stewenius: action matrix of x on the
+// basis [x^2, xy, xz, y^2, yz, z^2, x, y, z, 1] after the graded
+// Gauss-Jordan, elmhes + hqr eigenvalues, complex eigenvectors, E from the
+// real part of each solution (conjugate pairs once). The Hessenberg
+// reduction and the QR iteration are the oracle's serial code run by lane 0
+// on the LDS copy (data-dependent deflation); the eigenvector solves are
+// column-per-lane complex LUs with the same per-element operations.
+struct cplx_d {
+  double re, im;
+};
+__device__ __forceinline__ cplx_d c_mul(cplx_d a, cplx_d b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+__device__ __forceinline__ cplx_d c_sub(cplx_d a, cplx_d b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cplx_d c_div(cplx_d a, cplx_d d) {
+  cplx_d r;
+  if (fabs(d.re) >= fabs(d.im)) {
+    const double q = d.im / d.re, den = d.re + d.im * q;
+    r.re = (a.re + a.im * q) / den;
+    r.im = (a.im - a.re * q) / den;
+  } else {
+    const double q = d.re / d.im, den = d.re * q + d.im;
+    r.re = (a.re * q + a.im) / den;
+    r.im = (a.im * q - a.re) / den;
+  }
+  return r;
+}
+__device__ __forceinline__ double c_abs1(cplx_d a) { return fabs(a.re) + fabs(a.im); }
+
+// elmhes on w.H: the pivot search and the multipliers are formed from
+// broadcast LDS reads in the serial order; each row / column update is one
+// lane per element (the serial loop's element operations, same order of
+// the dependent steps).
+__device__ void coop_hessenberg(CoopWS& w, int lane) {
+  double (*a)[10] = w.H;
+  const int n = 10;
+  for (int m = 1; m < n - 1; ++m) {
+    double x = 0.0;
+    int i = m;
+    for (int j = m; j < n; ++j) {
+      const double v = a[j][m - 1];
+      if (fabs(v) > fabs(x)) { x = v; i = j; }
+    }
+    wsync();
+    if (i != m) {
+      if (lane >= m - 1 && lane < n) { const double t = a[i][lane]; a[i][lane] = a[m][lane]; a[m][lane] = t; }
+      wsync();
+      if (lane < n) { const double t = a[lane][i]; a[lane][i] = a[lane][m]; a[lane][m] = t; }
+      wsync();
+    }
+    if (x != 0.0) {
+      for (i = m + 1; i < n; ++i) {
+        double y = a[i][m - 1];
+        if (y != 0.0) {  // uniform
+          y /= x;
+          wsync();
+          if (lane == 0) a[i][m - 1] = y;
+          if (lane >= m && lane < n) a[i][lane] -= y * a[m][lane];
+          wsync();
+          if (lane < n) a[lane][m] += y * a[lane][i];
+          wsync();
+        }
+      }
+    }
+  }
+  if (lane >= 2 && lane < n)
+    for (int j = 0; j < lane - 1; ++j) a[lane][j] = 0.0;
+  wsync();
+}
+
+// hqr on w.H with every lane running the scalar control on broadcast reads;
+// the deflation search and the bulge-start search evaluate all candidates
+// at once (lane per candidate; the serial loop's pick = the highest index
+// whose test holds), the Householder row and column updates are one lane per
+// row / column. Eigenvalues to w.wr / w.wi; returns 0 after 30 iterations.
+__device__ int coop_hqr(CoopWS& w, int lane) {
+  double (*a)[10] = w.H;
+  const int n = 10;
+  double anorm = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int j = (i > 0 ? i - 1 : 0); j < n; ++j) anorm += fabs(a[i][j]);
+  int nn = n - 1, l;
+  double t = 0.0, p = 0.0, q = 0.0, r = 0.0, s, wv, x, y, z;
+  while (nn >= 0) {
+    int its = 0;
+    do {
+      bool hit = false;
+      if (lane >= 1 && lane <= nn) {
+        double ss = fabs(a[lane - 1][lane - 1]) + fabs(a[lane][lane]);
+        if (ss == 0.0) ss = anorm;
+        hit = fabs(a[lane][lane - 1]) + ss == ss;
+      }
+      const unsigned long long hm = __ballot(hit);
+      l = hm ? 63 - __clzll(hm) : 0;
+      wsync();
+      if (hm && lane == 0) a[l][l - 1] = 0.0;
+      wsync();
+      x = a[nn][nn];
+      if (l == nn) {
+        if (lane == 0) { w.wr[nn] = x + t; w.wi[nn] = 0.0; }
+        --nn;
+      } else {
+        y = a[nn - 1][nn - 1];
+        wv = a[nn][nn - 1] * a[nn - 1][nn];
+        if (l == nn - 1) {
+          p = 0.5 * (y - x);
+          q = p * p + wv;
+          z = sqrt(fabs(q));
+          x += t;
+          if (lane == 0) {
+            if (q >= 0.0) {
+              z = p + (p >= 0.0 ? fabs(z) : -fabs(z));
+              w.wr[nn - 1] = w.wr[nn] = x + z;
+              if (z != 0.0) w.wr[nn] = x - wv / z;
+              w.wi[nn - 1] = w.wi[nn] = 0.0;
+            } else {
+              w.wr[nn - 1] = w.wr[nn] = x + p;
+              w.wi[nn] = z;
+              w.wi[nn - 1] = -z;
+            }
+          }
+          nn -= 2;
+        } else {
+          if (its == 30) return 0;
+          if (its == 10 || its == 20) {
+            t += x;
+            wsync();
+            if (lane <= nn) a[lane][lane] -= x;
+            wsync();
+            s = fabs(a[nn][nn - 1]) + fabs(a[nn - 1][nn - 2]);
+            y = x = 0.75 * s;
+            wv = -0.4375 * s * s;
+          }
+          ++its;
+          // bulge start: the largest m in [l, nn-2] with m == l or a small
+          // subdiagonal product (lane per m)
+          bool stop = false;
+          double pm = 0.0, qm = 0.0, rm = 0.0;
+          if (lane >= l && lane <= nn - 2) {
+            const int m = lane;
+            const double zz = a[m][m];
+            double rr = x - zz;
+            double ss = y - zz;
+            pm = (rr * ss - wv) / a[m + 1][m] + a[m][m + 1];
+            qm = a[m + 1][m + 1] - zz - rr - ss;
+            rm = a[m + 2][m + 1];
+            ss = fabs(pm) + fabs(qm) + fabs(rm);
+            pm /= ss;
+            qm /= ss;
+            rm /= ss;
+            if (m == l) {
+              stop = true;
+            } else {
+              const double u = fabs(a[m][m - 1]) * (fabs(qm) + fabs(rm));
+              const double v = fabs(pm) * (fabs(a[m - 1][m - 1]) + fabs(zz) + fabs(a[m + 1][m + 1]));
+              stop = u + v == v;
+            }
+          }
+          const unsigned long long sm = __ballot(stop);
+          const int m = 63 - __clzll(sm);  // lane l always stops
+          p = rdlane(pm, m);
+          q = rdlane(qm, m);
+          r = rdlane(rm, m);
+          wsync();
+          if (lane >= m + 2 && lane <= nn) {
+            a[lane][lane - 2] = 0.0;
+            if (lane != m + 2) a[lane][lane - 3] = 0.0;
+          }
+          wsync();
+          for (int k = m; k <= nn - 1; ++k) {
+            if (k != m) {
+              p = a[k][k - 1];
+              q = a[k + 1][k - 1];
+              r = 0.0;
+              if (k != nn - 1) r = a[k + 2][k - 1];
+              if ((x = fabs(p) + fabs(q) + fabs(r)) != 0.0) {
+                p /= x;
+                q /= x;
+                r /= x;
+              }
+            }
+            const double sq = sqrt(p * p + q * q + r * r);
+            if ((s = (p >= 0.0 ? sq : -sq)) != 0.0) {
+              wsync();
+              if (lane == 0) {
+                if (k == m) {
+                  if (l != m) a[k][k - 1] = -a[k][k - 1];
+                } else {
+                  a[k][k - 1] = -s * x;
+                }
+              }
+              p += s;
+              x = p / s;
+              y = q / s;
+              z = r / s;
+              q /= p;
+              r /= p;
+              if (lane >= k && lane <= nn) {
+                const int j = lane;
+                double pp = a[k][j] + q * a[k + 1][j];
+                if (k != nn - 1) {
+                  pp += r * a[k + 2][j];
+                  a[k + 2][j] -= pp * z;
+                }
+                a[k + 1][j] -= pp * y;
+                a[k][j] -= pp * x;
+              }
+              wsync();
+              const int mmin = nn < k + 3 ? nn : k + 3;
+              if (lane >= l && lane <= mmin) {
+                const int i = lane;
+                double pp = x * a[i][k] + y * a[i][k + 1];
+                if (k != nn - 1) {
+                  pp += z * a[i][k + 2];
+                  a[i][k + 2] -= pp * r;
+                }
+                a[i][k + 1] -= pp * q;
+                a[i][k] -= pp;
+              }
+              wsync();
+            }
+          }
+        }
+      }
+    } while (nn >= 0 && l < nn - 1);
+  }
+  wsync();
+  return 1;
+}
+
+
+// Eigenvectors of w.M, normalised to v9 = 1, for up to 6 eigenvalues at
+// once: lanes 10g..10g+9 solve eigenvalue g of the pass, lane 10g+c holding
+// column c of M - lam I (eigvec10's LU with partial pivoting, per element
+// the same operations; the column broadcasts are group shuffles). Returns
+// this group's (v6, v7, v8) real parts; ok = 0 on a zero pivot.
+__device__ __forceinline__ cplx_d shfl_c(cplx_d v, int src) { return {__shfl(v.re, src, 64), __shfl(v.im, src, 64)}; }
+__device__ int coop_eigvec6(const CoopWS& w, int lane, cplx_d lam, double xyz[3]) {
+  const int g0 = (lane / 10) * 10, c = lane - g0 < 10 ? lane - g0 : 9;
+  cplx_d b[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    b[i].re = w.M[i][c];
+    b[i].im = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i)
+    if (i == c) b[i] = c_sub(b[i], lam);
+  int ok = 1;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    cplx_d col[10];
+#pragma unroll
+    for (int i = k; i < 10; ++i) col[i] = shfl_c(b[i], g0 + k);
+    int p = k;
+    double pa = c_abs1(col[k]);
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i)
+      if (c_abs1(col[i]) > pa) { p = i; pa = c_abs1(col[i]); }
+    if (pa == 0.0) ok = 0;
+    cplx_d bk = b[k], bp = b[k], ck = col[k], cp = col[k];
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i)
+      if (i == p) { bp = b[i]; cp = col[i]; }
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i)
+      if (i == p) { b[i] = bk; col[i] = ck; }
+    b[k] = bp;
+    col[k] = cp;
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i) {
+      const cplx_d f = c_div(col[i], col[k]);
+      if (c > k) b[i] = c_sub(b[i], c_mul(f, b[k]));
+    }
+  }
+  cplx_d v[10];
+  v[9].re = 1.0;
+  v[9].im = 0.0;
+#pragma unroll
+  for (int i = 8; i >= 0; --i) {
+    cplx_d s = {0.0, 0.0};
+#pragma unroll
+    for (int j = i + 1; j < 10; ++j) s = c_sub(s, c_mul(shfl_c(b[i], g0 + j), v[j]));
+    v[i] = c_div(s, shfl_c(b[i], g0 + i));
+  }
+  xyz[0] = v[6].re;
+  xyz[1] = v[7].re;
+  xyz[2] = v[8].re;
+  return ok;
+}
+
+// After coop_gj(graded): w.A = [I | C] in graded order. Essentials -> coop_decompose.
+__device__ void coop_stewenius(CoopWS& w, int lane, bool prof) {
+  unsigned long long t_prev = prof ? wall_clock64() : 0;
+  for (int t = lane; t < 100; t += RS_BLOCK) {
+    const int i = t / 10, j = t % 10;
+    double v = (i < 6) ? -w.A[i][10 + j] : 0.0;
+    if ((i == 6 && j == 0) || (i == 7 && j == 1) || (i == 8 && j == 2) || (i == 9 && j == 6)) v = 1.0;
+    w.M[i][j] = v;
+    w.H[i][j] = v;
+  }
+  wsync();
+  coop_hessenberg(w, lane);
+  KMX_PT(7);
+  const int ok_eig = coop_hqr(w, lane);
+  KMX_PT(8);
+  // solutions in eigenvalue order, a conjugate pair once (wi >= 0)
+  unsigned solm = 0;  // bit s: eigenvalue s starts a solution
+  if (ok_eig)
+    for (int s = 0; s < 10; ++s)
+      if (!(w.wi[s] < 0.0)) solm |= 1u << s;
+  const int ns = __popc(solm);
+  unsigned okm = 0;  // bit s: solution s gave an essential (Es[s])
+  for (int b0 = 0; b0 < ns; b0 += 6) {
+    const int g = lane / 10, sidx = b0 + g;
+    const bool act = g < 6 && sidx < ns;
+    unsigned mm = solm;  // eigenvalue of solution sidx: the sidx-th set bit
+    for (int k = 0; k < sidx && k < 10; ++k) mm &= mm - 1;
+    const int si = act ? __ffs(mm) - 1 : 0;
+    double xyz[3] = {0.0, 0.0, 0.0};
+    const int okv = coop_eigvec6(w, lane, cplx_d{act ? w.wr[si] : 0.0, act ? w.wi[si] : 0.0}, xyz);
+    // lane 10g + e (e < 9): entry e of E; the norm over the group's 9 entries in order
+    const int g0 = g * 10, c = lane - g0;
+    const double e = (c < 9) ? xyz[0] * w.N[0][c] + xyz[1] * w.N[1][c] + xyz[2] * w.N[2][c] + w.N[3][c] : 0.0;
+    double nn = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const double ei = __shfl(e, g0 + i < 64 ? g0 + i : 63, 64);
+      nn += ei * ei;
+    }
+    nn = sqrt(nn);
+    const bool good = act && okv && nn > 0.0 && isfinite(nn);
+    if (good && c < 9) w.Es[sidx][c] = e / nn;
+    const unsigned long long gm = __ballot(good && c == 0);
+#pragma unroll
+    for (int gg = 0; gg < 6; ++gg)
+      if ((gm >> (10 * gg)) & 1ull) okm |= 1u << (b0 + gg);
+  }
+  wsync();
+  KMX_PT(9);
+  // compact in solution order (orc_fivept_stewenius's ns counter)
+  const int ne = __popc(okm);
+  double Eo[9];
+  const bool ok = lane < ne;
+  if (ok) {
+    unsigned mm = okm;
+    for (int k = 0; k < lane; ++k) mm &= mm - 1;
+    const int src = __ffs(mm) - 1;
+    for (int i = 0; i < 9; ++i) Eo[i] = w.Es[src][i];
+  }
+  wsync();
+  coop_decompose(w, lane, ok, Eo);
+  KMX_PT(10);
+}
+
 // One hypothesis: sample -> models (w.ok, w.mR, w.mt).
 __device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const double* F2, const short* smp,
-                                bool prof) {
+                                int algo, bool prof) {
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   if (lane < 15) {
     const int i = lane / 3, c = lane % 3;
@@ -1420,12 +1790,18 @@ __device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const doubl
   KMX_PT(1);
   coop_system(w, lane);
   KMX_PT(2);
-  if (!coop_gj(w, lane)) {
+  const bool stew = algo == KMX_ALGO_STEWENIUS;
+  if (!coop_gj(w, lane, stew)) {
     if (lane == 0) w.ok = 0;
     wsync();
     return;
   }
   KMX_PT(3);
+  if (stew) {
+    coop_stewenius(w, lane, prof);
+    KMX_PT(5);
+    return;
+  }
   coop_roots(w, lane, prof);
   KMX_PT(4);
   if (w.nr == 0) {
@@ -1482,7 +1858,7 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
     if (!(iterations < kk && skipped < max_skip)) break;  // uniform
     const bool prof = (c < 64) && P.prof;
     unsigned long long t_prev = prof ? wall_clock64() : 0;
-    coop_hypothesis(w, lane, F1, F2, tab + (size_t)p * 5, prof);
+    coop_hypothesis(w, lane, F1, F2, tab + (size_t)p * 5, P.algo, prof);
     if (prof && lane == 0) t_prev = wall_clock64();
     if (!w.ok) {
       ++skipped;
@@ -2077,6 +2453,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   rp.pmax = h->pmax;
   rp.pnp = (h->P.pose_recovery_type == 1) ? 1 : 0;
   rp.prof = h->prof;
+  rp.algo = h->P.algorithm_2d2d;
   {
     // KMX_RS_LB: minimum waves per SIMD for k_ransac (diagnostic; 1 = the
     // compiler's choice, 256 VGPRs)
@@ -2084,7 +2461,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
       const char* v = std::getenv("KMX_RS_LB");
       return v ? std::atoi(v) : 1;
     }();
-    if (h->ransac == 1) {
+    if (h->ransac == 1 || rp.algo != KMX_ALGO_NISTER) {
       static const int clb = [] {
         const char* v = std::getenv("KMX_COOP_LB");
         return v ? std::atoi(v) : 4;
@@ -2132,6 +2509,8 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
             "bad rng variant");
   KMX_CHECK(params->ransac_randomize == 0, KMX_EUNSUP, "ransac_randomize = 1 is not reproducible; use 0");
   KMX_CHECK(params->use_1point_3d3d == 1, KMX_EUNSUP, "only the 1-point (given-rotation) 3D-3D check is built");
+  KMX_CHECK(params->algorithm_2d2d == KMX_ALGO_STEWENIUS || params->algorithm_2d2d == KMX_ALGO_NISTER, KMX_EUNSUP,
+            "ransac_2d2d_algorithm: 0 (Stewenius) and 1 (Nister) are built");
   KMX_CHECK(params->ransac_max_iterations > 0, KMX_EINVAL, "ransac_max_iterations must be > 0");
   int ndev = 0;
   KMX_HIP(hipGetDeviceCount(&ndev));

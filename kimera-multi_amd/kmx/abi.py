@@ -17,7 +17,7 @@ import numpy as np
 _LIB_PATH = Path(__file__).resolve().parent / "libkmx.so"
 
 KMX_OK = 0
-ABI_VERSION = 2  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
+ABI_VERSION = 3  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
 KMX_COST_L2 = 0
 KMX_COST_GNC_TLS = 1
 KMX_SCHEDULE_SEQUENTIAL = 0
@@ -95,7 +95,7 @@ class LcdParams(C.Structure):
         ("ransac_probability", C.c_double), ("ransac_randomize", C.c_int),
         ("ransac_seed", C.c_uint32), ("rng_variant", C.c_int),
         ("use_1point_3d3d", C.c_int), ("pose_recovery_type", C.c_int), ("min_2d3d_inliers", C.c_int),
-        ("ransac_threshold_2d3d", C.c_double), ("reserved", C.c_int * 4),
+        ("ransac_threshold_2d3d", C.c_double), ("algorithm_2d2d", C.c_int), ("reserved", C.c_int * 3),
     ]
 
 

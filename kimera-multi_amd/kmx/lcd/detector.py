@@ -34,6 +34,11 @@ class LcdParams:
     ransac_seed: int = 12345
     rng_variant: str = "gcc9"           # libstdc++ of ROS Noetic (SURVEY.md §0 finding 5)
     ransac_use_1point_3d3d: int = 1
+    # opengv CentralRelativePoseSacProblem::algorithm_t (LcdParams.yaml:73):
+    # 0 STEWENIUS (the reference config), 1 NISTER
+    ransac_2d2d_algorithm: int = 0
+    # opengv AbsolutePoseSacProblem::algorithm_t (LcdParams.yaml:74): 3 EPNP
+    ransac_2d3d_algorithm: int = 3
     # PnP pose recovery (pose_recovery_type 1: EPnP RANSAC, LcdParams.yaml:53,57,63,74)
     pose_recovery_type: int = 0
     min_nr_2d3d_inliers: int = 20
@@ -53,26 +58,59 @@ class LcdParams:
 
     @classmethod
     def from_yaml(cls, path: str, **overrides) -> "LcdParams":
-        """Read an OpenCV-FileStorage LcdParams.yaml (the %YAML:1.0 header is skipped)."""
+        """Read an OpenCV-FileStorage LcdParams.yaml (the %YAML:1.0 header is
+        skipped). `overrides` replace yaml keys (by yaml name) or dataclass
+        fields before validation. Every key is accounted for: verification
+        and BoW keys map onto fields, keys of stages outside the hot path
+        (ORB extraction, the PGO back end, the tracker) are ignored by name,
+        and anything else, or a value that selects an algorithm this build
+        does not have, raises ValueError (no silent fallback)."""
         import yaml
-        text = open(path).read().split("\n", 1)[1] if open(path).read().startswith("%YAML") else open(path).read()
-        y = yaml.safe_load(text) or {}
+        text = open(path).read()
+        if text.startswith("%YAML"):
+            text = text.split("\n", 1)[1] if "\n" in text else ""
+        y = dict(yaml.safe_load(text) or {})
+        y.update(overrides)
         p = cls()
-        for k in ("lowe_ratio", "min_nr_2d2d_inliers", "min_nr_3d3d_inliers", "ransac_threshold_2d2d",
-                  "ransac_threshold_3d3d", "ransac_max_iterations", "ransac_probability", "ransac_randomize",
-                  "ransac_use_1point_3d3d", "pose_recovery_type", "min_nr_2d3d_inliers", "ransac_threshold_2d3d",
-                  "use_nss", "alpha", "min_temporal_matches", "recent_frames_window",
-                  "max_db_results", "min_nss_factor", "min_matches_per_island", "max_intraisland_gap",
-                  "max_nrFrames_between_islands", "max_nrFrames_between_queries"):
-            if k in y:
-                setattr(p, k, type(getattr(p, k))(y[k]))
-        if "matcher_type" in y:  # OpenCV MatcherType: 3 = BRUTEFORCE_L1, 4 = BRUTEFORCE_HAMMING
-            p.norm = {3: "l1", 4: "hamming"}.get(int(y["matcher_type"]), p.norm)
-        for k, v in overrides.items():
-            setattr(p, k, v)
+        for k, v in y.items():
+            if k in _YAML_FIELDS:
+                setattr(p, k, type(getattr(p, k))(v))
+            elif k == "matcher_type":
+                # OpenCV DescriptorMatcher::MatcherType; 3 is built as BruteForce-L1
+                # (docker/copy/kimera_multi_lcd.patch:33-35)
+                mt = int(v)
+                if mt not in _MATCHER_NORM:
+                    raise ValueError(f"matcher_type {mt} is not built (3: L1, 4/5: Hamming)")
+                p.norm = _MATCHER_NORM[mt]
+            elif k in _YAML_SELECTORS:
+                allowed, field = _YAML_SELECTORS[k]
+                if int(v) not in allowed:
+                    raise ValueError(f"{k}: {v} is not built (supported: {sorted(allowed)})")
+                if field:
+                    setattr(p, field, int(v))
+            elif k in _YAML_IGNORED:
+                continue
+            elif k in cls.__dataclass_fields__:
+                setattr(p, k, v)
+            else:
+                raise ValueError(f"unknown LcdParams key {k!r}")
+        p.validate()
         return p
 
+    def validate(self):
+        if self.norm not in ("l1", "hamming"):
+            raise ValueError(f"norm {self.norm!r}")
+        if self.ransac_2d2d_algorithm not in (ALGO_STEWENIUS, ALGO_NISTER):
+            raise ValueError(f"ransac_2d2d_algorithm {self.ransac_2d2d_algorithm} is not built (0 Stewenius, 1 Nister)")
+        if self.ransac_2d3d_algorithm != 3:
+            raise ValueError("ransac_2d3d_algorithm: only 3 (EPnP) is built")
+        if self.pose_recovery_type not in (0, 1):
+            raise ValueError(f"pose_recovery_type {self.pose_recovery_type}")
+        if self.rng_variant not in ("gcc9", "gcc11"):
+            raise ValueError(f"rng_variant {self.rng_variant!r}")
+
     def to_c(self) -> abi.LcdParams:
+        self.validate()
         c = abi.LcdParams()
         c.norm = abi.KMX_NORM_HAMMING if self.norm == "hamming" else abi.KMX_NORM_L1
         c.lowe_ratio = float(self.lowe_ratio)
@@ -86,10 +124,41 @@ class LcdParams:
         c.ransac_seed = int(self.ransac_seed)
         c.rng_variant = abi.KMX_RNG_GCC11 if self.rng_variant == "gcc11" else abi.KMX_RNG_GCC9
         c.use_1point_3d3d = int(self.ransac_use_1point_3d3d)
+        c.algorithm_2d2d = int(self.ransac_2d2d_algorithm)
         c.pose_recovery_type = int(self.pose_recovery_type)
         c.min_2d3d_inliers = int(self.min_nr_2d3d_inliers)
         c.ransac_threshold_2d3d = 1.0 - np.cos(np.arctan(float(self.ransac_threshold_2d3d) / float(self.focal_length)))
         return c
+
+
+ALGO_STEWENIUS = 0
+ALGO_NISTER = 1
+
+# yaml keys that are dataclass fields of the same name
+_YAML_FIELDS = (
+    "lowe_ratio", "min_nr_2d2d_inliers", "min_nr_3d3d_inliers", "ransac_threshold_2d2d",
+    "ransac_threshold_3d3d", "ransac_max_iterations", "ransac_probability", "ransac_randomize",
+    "ransac_use_1point_3d3d", "pose_recovery_type", "min_nr_2d3d_inliers", "ransac_threshold_2d3d",
+    "ransac_2d2d_algorithm", "ransac_2d3d_algorithm",
+    "use_nss", "alpha", "min_temporal_matches", "recent_frames_window", "max_db_results",
+    "min_nss_factor", "min_matches_per_island", "max_intraisland_gap",
+    "max_nrFrames_between_islands", "max_nrFrames_between_queries")
+_MATCHER_NORM = {3: "l1", 4: "hamming", 5: "hamming"}
+# switches of verification stages: yaml key -> (built values, field or None)
+_YAML_SELECTORS = {
+    "refine_pose": ({0}, None),                       # stereo pose refinement (LcdParams.yaml:14)
+    "ransac_use_2point_2d2d": ({0}, None),            # 2-point 2D-2D given rotation (:59)
+    "optimize_2d2d_pose_from_inliers": ({0}, None),   # nonlinear refits (:67-69)
+    "optimize_3d3d_pose_from_inliers": ({0}, None),
+    "optimize_2d3d_pose_from_inliers": ({0}, None),
+}
+# keys of stages outside the verification hot path (SURVEY.md §8 out of scope):
+# ORB extraction (:19-27), the PGO back end (:29-37), the stereo tracker (:48)
+_YAML_IGNORED = frozenset((
+    "nfeatures", "scale_factor", "nlevels", "edge_threshold", "first_level", "WTA_K", "score_type_id",
+    "patch_sze", "fast_threshold", "betweenRotationPrecision", "betweenTranslationPrecision",
+    "odom_rot_threshold", "odom_trans_threshold", "pcm_rot_threshold", "pcm_trans_threshold", "gnc_alpha",
+    "max_lc_cached_before_optimize", "disparity_threshold"))
 
 
 class _BatchDesc(C.Structure):

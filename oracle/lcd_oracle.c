@@ -448,19 +448,19 @@ static int real_roots(const double* coef, int deg_in, double* roots) {
   return nr;
 }
 
-/* Essential matrices E (row-major, unit Frobenius norm) with f1^T E f2 = 0 for
- * the five bearing pairs; returns their number (<= 10). */
-int orc_fivept_nister(const double* f1 /*5x3*/, const double* f2 /*5x3*/, double* Es /*10x9*/) {
+/* The 5-point constraint system shared by both minimal solvers: the null
+ * space N of the 5x9 epipolar rows (E = x N0 + y N1 + z N2 + N3) and the 10
+ * cubic constraints (rows 0..8: 2 E E^T E - tr(E E^T) E = 0, row 9: det E = 0)
+ * in the 20 monomials of MONO. */
+static void fivept_system(const double* f1, const double* f2, double N[4][9], double A[10][20]) {
   double Q[5][9];
   for (int i = 0; i < 5; ++i)
     for (int a = 0; a < 3; ++a)
       for (int b = 0; b < 3; ++b) Q[i][a * 3 + b] = f1[3 * i + a] * f2[3 * i + b];
-  double N[4][9];
   nullspace_5x9(Q, N);
   double E[9][4]; /* E_e(x, y, z) = N0_e x + N1_e y + N2_e z + N3_e */
   for (int e = 0; e < 9; ++e)
     for (int c = 0; c < 4; ++c) E[e][c] = N[c][e];
-  double A[10][20];
   /* row 9: det(E) by cofactors of the first row */
   {
     double t1[10], t2[10], c2[10], m[20];
@@ -502,7 +502,11 @@ int orc_fivept_nister(const double* f1 /*5x3*/, const double* f2 /*5x3*/, double
         for (int k = 0; k < 20; ++k) r[k] -= m[k];
       }
   }
-  /* Gauss-Jordan with partial pivoting on the first 10 columns */
+}
+
+/* Gauss-Jordan with partial pivoting on the first 10 columns of the 10x20
+ * system: A = [I | C] on success, 0 on a zero pivot. */
+static int gj_10x20(double A[10][20]) {
   for (int k = 0; k < 10; ++k) {
     int p = k;
     for (int i = k + 1; i < 10; ++i)
@@ -519,6 +523,15 @@ int orc_fivept_nister(const double* f1 /*5x3*/, const double* f2 /*5x3*/, double
       for (int c = 0; c < 20; ++c) A[i][c] -= f * A[k][c];
     }
   }
+  return 1;
+}
+
+/* Essential matrices E (row-major, unit Frobenius norm) with f1^T E f2 = 0 for
+ * the five bearing pairs; returns their number (<= 10). */
+int orc_fivept_nister(const double* f1 /*5x3*/, const double* f2 /*5x3*/, double* Es /*10x9*/) {
+  double N[4][9], A[10][20];
+  fivept_system(f1, f2, N, A);
+  if (!gj_10x20(A)) return 0;
   /* <k> = e - z f, <l> = g - z h, <m> = i - z j (rows 4..9); B(z) = [x-coef, y-coef, 1-coef] */
   double Bp[3][3][5];
   for (int q = 0; q < 3; ++q) {
@@ -586,6 +599,288 @@ int orc_fivept_nister(const double* f1 /*5x3*/, const double* f2 /*5x3*/, double
   return ns;
 }
 
+/* ---------------------------------------- 5-point (Stewenius 2006) -- */
+/* opengv fivept_stewenius (Stewenius, Engels, Nister, "Recent developments on
+ * direct relative orientation", ISPRS J. 2006), the solver the reference
+ * config selects (ransac_2d2d_algorithm: 0, LcdParams.yaml:73). Restated
+ * procedure:
+ *   - the same 10 cubic constraints in the null-space coordinates (x, y, z)
+ *     as Nister (fivept_system), with the monomials in graded order: the 10
+ *     cubics GORD[0..9] first, then the basis
+ *       b = [x^2, xy, xz, y^2, yz, z^2, x, y, z, 1];
+ *   - Gauss-Jordan on the cubic columns: cubic_i = -sum_j C[i][j] b_j;
+ *   - the action matrix of multiplication by x on b (10x10):
+ *       x*b_i for i < 6 is cubic i -> row -C[i]; x*x = b_0, x*y = b_1,
+ *       x*z = b_2, x*1 = b_6;
+ *   - its eigen-decomposition: each eigenvector is b evaluated at a solution,
+ *     (x, y, z) = (v6, v7, v8) / v9; E = x N0 + y N1 + z N2 + N3;
+ *   - as opengv's CentralRelativePoseSacProblem does with the complex
+ *     essentials of fivept_stewenius, every solution enters RANSAC through the
+ *     real part of its E (a complex-conjugate pair gives one real part; it is
+ *     taken once, from the member with positive imaginary part).
+ * Eigenvalues: Hessenberg reduction by stabilised elimination and the
+ * Francis double-shift QR iteration (EISPACK elmhes / hqr, as published in
+ * Numerical Recipes 11.5-11.6) on the action matrix; eigenvectors: complex
+ * LU with partial pivoting of (M - lambda I), v9 = 1, back substitution.
+ * Eigen's EigenSolver (opengv) reaches the same eigenpairs by a different QR
+ * variant: solution ORDER can differ from opengv [U]; E per solution agrees
+ * to rounding. */
+static const int GORD[20] = {0, 2, 4, 3, 8, 10, 1, 6, 13, 16, 5, 9, 11, 7, 14, 17, 12, 15, 18, 19};
+
+typedef struct {
+  double re, im;
+} cplx;
+static cplx c_mul(cplx a, cplx b) {
+  cplx r = {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+  return r;
+}
+static cplx c_sub(cplx a, cplx b) {
+  cplx r = {a.re - b.re, a.im - b.im};
+  return r;
+}
+static cplx c_div(cplx a, cplx d) { /* Smith's algorithm */
+  cplx r;
+  if (fabs(d.re) >= fabs(d.im)) {
+    const double q = d.im / d.re, den = d.re + d.im * q;
+    r.re = (a.re + a.im * q) / den;
+    r.im = (a.im - a.re * q) / den;
+  } else {
+    const double q = d.re / d.im, den = d.re * q + d.im;
+    r.re = (a.re * q + a.im) / den;
+    r.im = (a.im * q - a.re) / den;
+  }
+  return r;
+}
+static double c_abs1(cplx a) { return fabs(a.re) + fabs(a.im); }
+
+/* Reduction to upper Hessenberg form by elimination with pivoting (elmhes);
+ * the entries below the subdiagonal are cleared. */
+static void hessenberg10(double a[10][10]) {
+  const int n = 10;
+  for (int m = 1; m < n - 1; ++m) {
+    double x = 0.0;
+    int i = m;
+    for (int j = m; j < n; ++j)
+      if (fabs(a[j][m - 1]) > fabs(x)) { x = a[j][m - 1]; i = j; }
+    if (i != m) {
+      for (int j = m - 1; j < n; ++j) { const double t = a[i][j]; a[i][j] = a[m][j]; a[m][j] = t; }
+      for (int j = 0; j < n; ++j) { const double t = a[j][i]; a[j][i] = a[j][m]; a[j][m] = t; }
+    }
+    if (x != 0.0) {
+      for (i = m + 1; i < n; ++i) {
+        double y = a[i][m - 1];
+        if (y != 0.0) {
+          y /= x;
+          a[i][m - 1] = y;
+          for (int j = m; j < n; ++j) a[i][j] -= y * a[m][j];
+          for (int j = 0; j < n; ++j) a[j][m] += y * a[j][i];
+        }
+      }
+    }
+  }
+  for (int i = 2; i < n; ++i)
+    for (int j = 0; j < i - 1; ++j) a[i][j] = 0.0;
+}
+
+/* Eigenvalues of an upper Hessenberg matrix by the shifted QR iteration
+ * (hqr): wr + i wi, a complex pair stored as (-|wi|, +|wi|) at (nn-1, nn).
+ * Returns 0 when an eigenvalue needs more than 30 iterations. */
+static int hqr10(double a[10][10], double wr[10], double wi[10]) {
+  const int n = 10;
+  double anorm = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int j = (i > 0 ? i - 1 : 0); j < n; ++j) anorm += fabs(a[i][j]);
+  int nn = n - 1, l;
+  double t = 0.0, p = 0.0, q = 0.0, r = 0.0, s, w, x, y, z;
+  while (nn >= 0) {
+    int its = 0;
+    do {
+      for (l = nn; l >= 1; --l) {
+        s = fabs(a[l - 1][l - 1]) + fabs(a[l][l]);
+        if (s == 0.0) s = anorm;
+        if (fabs(a[l][l - 1]) + s == s) {
+          a[l][l - 1] = 0.0;
+          break;
+        }
+      }
+      x = a[nn][nn];
+      if (l == nn) { /* one root */
+        wr[nn] = x + t;
+        wi[nn] = 0.0;
+        --nn;
+      } else {
+        y = a[nn - 1][nn - 1];
+        w = a[nn][nn - 1] * a[nn - 1][nn];
+        if (l == nn - 1) { /* two roots */
+          p = 0.5 * (y - x);
+          q = p * p + w;
+          z = sqrt(fabs(q));
+          x += t;
+          if (q >= 0.0) {
+            z = p + (p >= 0.0 ? fabs(z) : -fabs(z));
+            wr[nn - 1] = wr[nn] = x + z;
+            if (z != 0.0) wr[nn] = x - w / z;
+            wi[nn - 1] = wi[nn] = 0.0;
+          } else {
+            wr[nn - 1] = wr[nn] = x + p;
+            wi[nn] = z;
+            wi[nn - 1] = -z;
+          }
+          nn -= 2;
+        } else { /* no root yet: a double-shift QR sweep */
+          if (its == 30) return 0;
+          if (its == 10 || its == 20) { /* exceptional shift */
+            t += x;
+            for (int i = 0; i <= nn; ++i) a[i][i] -= x;
+            s = fabs(a[nn][nn - 1]) + fabs(a[nn - 1][nn - 2]);
+            y = x = 0.75 * s;
+            w = -0.4375 * s * s;
+          }
+          ++its;
+          int m;
+          for (m = nn - 2; m >= l; --m) {
+            z = a[m][m];
+            r = x - z;
+            s = y - z;
+            p = (r * s - w) / a[m + 1][m] + a[m][m + 1];
+            q = a[m + 1][m + 1] - z - r - s;
+            r = a[m + 2][m + 1];
+            s = fabs(p) + fabs(q) + fabs(r);
+            p /= s;
+            q /= s;
+            r /= s;
+            if (m == l) break;
+            const double u = fabs(a[m][m - 1]) * (fabs(q) + fabs(r));
+            const double v = fabs(p) * (fabs(a[m - 1][m - 1]) + fabs(z) + fabs(a[m + 1][m + 1]));
+            if (u + v == v) break;
+          }
+          for (int i = m + 2; i <= nn; ++i) {
+            a[i][i - 2] = 0.0;
+            if (i != m + 2) a[i][i - 3] = 0.0;
+          }
+          for (int k = m; k <= nn - 1; ++k) {
+            if (k != m) {
+              p = a[k][k - 1];
+              q = a[k + 1][k - 1];
+              r = 0.0;
+              if (k != nn - 1) r = a[k + 2][k - 1];
+              if ((x = fabs(p) + fabs(q) + fabs(r)) != 0.0) {
+                p /= x;
+                q /= x;
+                r /= x;
+              }
+            }
+            const double sq = sqrt(p * p + q * q + r * r);
+            if ((s = (p >= 0.0 ? sq : -sq)) != 0.0) {
+              if (k == m) {
+                if (l != m) a[k][k - 1] = -a[k][k - 1];
+              } else {
+                a[k][k - 1] = -s * x;
+              }
+              p += s;
+              x = p / s;
+              y = q / s;
+              z = r / s;
+              q /= p;
+              r /= p;
+              for (int j = k; j <= nn; ++j) {
+                p = a[k][j] + q * a[k + 1][j];
+                if (k != nn - 1) {
+                  p += r * a[k + 2][j];
+                  a[k + 2][j] -= p * z;
+                }
+                a[k + 1][j] -= p * y;
+                a[k][j] -= p * x;
+              }
+              const int mmin = nn < k + 3 ? nn : k + 3;
+              for (int i = l; i <= mmin; ++i) {
+                p = x * a[i][k] + y * a[i][k + 1];
+                if (k != nn - 1) {
+                  p += z * a[i][k + 2];
+                  a[i][k + 2] -= p * r;
+                }
+                a[i][k + 1] -= p * q;
+                a[i][k] -= p;
+              }
+            }
+          }
+        }
+      }
+    } while (nn >= 0 && l < nn - 1);
+  }
+  return 1;
+}
+
+/* Eigenvector of M for the eigenvalue lam normalised to v9 = 1: LU with
+ * partial pivoting (|re| + |im|) of M - lam I over columns 0..8, then back
+ * substitution. Returns 0 on a zero pivot. */
+static int eigvec10(const double M[10][10], cplx lam, cplx v[10]) {
+  cplx B[10][10];
+  for (int i = 0; i < 10; ++i)
+    for (int j = 0; j < 10; ++j) {
+      B[i][j].re = M[i][j];
+      B[i][j].im = 0.0;
+    }
+  for (int i = 0; i < 10; ++i) B[i][i] = c_sub(B[i][i], lam);
+  for (int k = 0; k < 9; ++k) {
+    int p = k;
+    for (int i = k + 1; i < 10; ++i)
+      if (c_abs1(B[i][k]) > c_abs1(B[p][k])) p = i;
+    if (c_abs1(B[p][k]) == 0.0) return 0;
+    if (p != k)
+      for (int j = 0; j < 10; ++j) { const cplx t = B[k][j]; B[k][j] = B[p][j]; B[p][j] = t; }
+    for (int i = k + 1; i < 10; ++i) {
+      const cplx f = c_div(B[i][k], B[k][k]);
+      for (int j = k + 1; j < 10; ++j) B[i][j] = c_sub(B[i][j], c_mul(f, B[k][j]));
+    }
+  }
+  v[9].re = 1.0;
+  v[9].im = 0.0;
+  for (int i = 8; i >= 0; --i) {
+    cplx s = {0.0, 0.0};
+    for (int j = i + 1; j < 10; ++j) s = c_sub(s, c_mul(B[i][j], v[j]));
+    v[i] = c_div(s, B[i][i]);
+  }
+  return 1;
+}
+
+int orc_fivept_stewenius(const double* f1 /*5x3*/, const double* f2 /*5x3*/, double* Es /*10x9*/) {
+  double N[4][9], A0[10][20], A[10][20];
+  fivept_system(f1, f2, N, A0);
+  for (int i = 0; i < 10; ++i)
+    for (int c = 0; c < 20; ++c) A[i][c] = A0[i][GORD[c]];
+  if (!gj_10x20(A)) return 0;
+  double M[10][10];
+  for (int i = 0; i < 10; ++i)
+    for (int j = 0; j < 10; ++j) M[i][j] = (i < 6) ? -A[i][10 + j] : 0.0;
+  M[6][0] = 1.0;
+  M[7][1] = 1.0;
+  M[8][2] = 1.0;
+  M[9][6] = 1.0;
+  double H[10][10], wr[10], wi[10];
+  memcpy(H, M, sizeof(H));
+  hessenberg10(H);
+  if (!hqr10(H, wr, wi)) return 0;
+  int ns = 0;
+  for (int s = 0; s < 10; ++s) {
+    if (wi[s] < 0.0) continue; /* the conjugate of s + 1 */
+    cplx lam = {wr[s], wi[s]}, v[10];
+    if (!eigvec10(M, lam, v)) continue;
+    const double x = v[6].re, y = v[7].re, z = v[8].re;
+    double* Eo = Es + 9 * ns;
+    double nn = 0.0;
+    for (int e = 0; e < 9; ++e) {
+      Eo[e] = x * N[0][e] + y * N[1][e] + z * N[2][e] + N[3][e];
+      nn += Eo[e] * Eo[e];
+    }
+    nn = sqrt(nn);
+    if (!(nn > 0.0) || !isfinite(nn)) continue;
+    for (int e = 0; e < 9; ++e) Eo[e] /= nn;
+    ++ns;
+  }
+  return ns;
+}
+
 /* ----------------------------------------------- opengv-style scoring -- */
 /* error of correspondence (f1, f2) under model (R = R12, t = t12):
  * mid-point triangulation (opengv triangulate2) + bearing errors 1 - cos. */
@@ -610,7 +905,8 @@ static double model_error(const double R[9], const double t[3], const double f1[
 
 /* computeModelCoefficients: 5-point essentials, 4 decompositions each, keep
  * the (R, t) with the smallest summed error over the sample. */
-static int model_from_sample(const double* F1, const double* F2, const int32_t* smp, double R[9], double t[3]) {
+static int model_from_sample(int algo, const double* F1, const double* F2, const int32_t* smp, double R[9],
+                             double t[3]) {
   double f1[15], f2[15];
   for (int i = 0; i < 5; ++i)
     for (int c = 0; c < 3; ++c) {
@@ -618,7 +914,7 @@ static int model_from_sample(const double* F1, const double* F2, const int32_t* 
       f2[3 * i + c] = F2[3 * smp[i] + c];
     }
   double Es[90];
-  const int ne = orc_fivept_nister(f1, f2, Es);
+  const int ne = (algo == KMX_ALGO_NISTER) ? orc_fivept_nister(f1, f2, Es) : orc_fivept_stewenius(f1, f2, Es);
   if (ne == 0) return 0;
   double best = DBL_MAX;
   int found = 0;
@@ -682,7 +978,7 @@ static int ransac_2d2d(const kmx_lcd_params* P, const double* F1, const double* 
     }
     for (int i = 0; i < 5; ++i) smp[i] = sh[i];
     double Rm[9], tm[3];
-    if (!model_from_sample(F1, F2, smp, Rm, tm)) {
+    if (!model_from_sample(P->algorithm_2d2d, F1, F2, smp, Rm, tm)) {
       ++skipped;
       continue;
     }

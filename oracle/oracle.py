@@ -260,9 +260,11 @@ def _lcd_setup(L):
     L.orc_ransac_samples.argtypes = [C.c_uint32, C.c_int, i32, i32, C.POINTER(i32)]
     L.orc_lcd_knn2.argtypes = [C.c_int, f64, C.POINTER(u8), i32, C.POINTER(u8), i32, C.POINTER(i32), C.POINTER(i32)]
     L.orc_fivept_nister.argtypes = [C.POINTER(f64), C.POINTER(f64), C.POINTER(f64)]
+    L.orc_fivept_stewenius.argtypes = [C.POINTER(f64), C.POINTER(f64), C.POINTER(f64)]
     L.orc_lcd_verify_batch.argtypes = [C.POINTER(LcdParams), C.POINTER(LcdBatchDesc), i32, C.POINTER(i32),
                                        C.POINTER(i32), C.POINTER(LcdResult), C.POINTER(u8)]
-    for n in ("orc_mt19937_stream", "orc_ransac_samples", "orc_lcd_knn2", "orc_fivept_nister", "orc_lcd_verify_batch"):
+    for n in ("orc_mt19937_stream", "orc_ransac_samples", "orc_lcd_knn2", "orc_fivept_nister", "orc_fivept_stewenius",
+              "orc_lcd_verify_batch"):
         getattr(L, n).restype = C.c_int
 
 
@@ -290,11 +292,14 @@ def knn2(norm, lowe, q, m):
     return pairs[: k.value].copy()
 
 
-def fivept(f1, f2):
+def fivept(f1, f2, algo=1):
+    """5-point essentials: algo 1 Nister (real roots), 0 Stewenius (every
+    eigen-solution, complex ones by their real part)."""
     L = lib(); _lcd_setup(L)
     f1 = np.ascontiguousarray(f1, dtype=np.float64); f2 = np.ascontiguousarray(f2, dtype=np.float64)
     Es = np.empty((10, 9))
-    n = L.orc_fivept_nister(_f(f1), _f(f2), _f(Es))
+    fn = L.orc_fivept_nister if algo == 1 else L.orc_fivept_stewenius
+    n = fn(_f(f1), _f(f2), _f(Es))
     return Es[:n].reshape(-1, 3, 3)
 
 

@@ -10,7 +10,8 @@ from kmx import abi
 from kmx.lcd import LcdParams, LoopClosureDetector
 from kmx.synth.lcd import make_lcd_pool
 pool = make_lcd_pool(2000, 500, seed=0)
-det = LoopClosureDetector(LcdParams()); det.set_pool(pool)
+algo = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+det = LoopClosureDetector(LcdParams(ransac_2d2d_algorithm=algo)); det.set_pool(pool)
 L = abi.lib()
 fn = L.kmx_lcd_debug_phase_times
 fn.argtypes = [C.POINTER(C.c_ulonglong)]
@@ -25,5 +26,6 @@ tot = sum(buf[i] for i in range(7))
 print(f"hypotheses (first 64 candidates): {hyp}")
 for i, n in enumerate(names):
     print(f"{n:10s} {buf[i] / 100.0 / max(hyp, 1):9.2f} us/hypothesis  {100.0 * buf[i] / max(tot, 1):5.1f} %")
-for i, n in zip(range(7, 11), ["  poly", "  sturm", "  isolate", "  refine"]):
-    print(f"{n:10s} {buf[i] / 100.0 / max(hyp, 1):9.2f} us/hypothesis (within roots)")
+sub = (["  hessenb", "  hqr", "  eigvec", "  decomp"] if algo == 0 else ["  poly", "  sturm", "  isolate", "  refine"])
+for i, n in zip(range(7, 11), sub):
+    print(f"{n:10s} {buf[i] / 100.0 / max(hyp, 1):9.2f} us/hypothesis (within {'models' if algo == 0 else 'roots'})")

@@ -48,13 +48,39 @@ def test_params_to_c_and_yaml(tmp_path):
 
 
 def test_reference_lcdparams_yaml_if_present():
+    """The reference config asks for refine_pose: 1 (stereo refinement, not
+    built): loading it raises; with the refinement switched off it maps onto
+    the verification parameters, Stewenius and EPnP included."""
     f = Path("/root/reference/params/D455/LcdParams.yaml")
     if not f.exists():
         pytest.skip("reference not mounted")
     from kmx.lcd import LcdParams
-    p = LcdParams.from_yaml(str(f))
+    with pytest.raises(ValueError, match="refine_pose"):
+        LcdParams.from_yaml(str(f))
+    p = LcdParams.from_yaml(str(f), refine_pose=0)
     assert (p.lowe_ratio, p.norm, p.ransac_max_iterations, p.ransac_probability) == (0.7, "l1", 500, 0.995)
     assert (p.min_nr_2d2d_inliers, p.min_nr_3d3d_inliers, p.ransac_threshold_2d2d) == (10, 5, 1e-6)
+    assert (p.ransac_2d2d_algorithm, p.ransac_2d3d_algorithm, p.pose_recovery_type) == (0, 3, 0)
+    assert p.to_c().algorithm_2d2d == 0
+
+
+@pytest.mark.parametrize("line,msg", [
+    ("ransac_2d2d_algorithm: 2", "ransac_2d2d_algorithm"),      # SEVENPT
+    ("ransac_2d3d_algorithm: 1", "ransac_2d3d_algorithm"),      # KNEIP
+    ("matcher_type: 1", "matcher_type"),                        # FLANN
+    ("ransac_use_2point_2d2d: 1", "ransac_use_2point_2d2d"),
+    ("optimize_3d3d_pose_from_inliers: 1", "optimize_3d3d"),
+    ("no_such_key: 3", "unknown"),
+])
+def test_lcdparams_yaml_rejects_unbuilt(tmp_path, line, msg):
+    from kmx.lcd import LcdParams
+    y = tmp_path / "LcdParams.yaml"
+    y.write_text("%YAML:1.0\nlowe_ratio: 0.7\n" + line + "\n")
+    with pytest.raises(ValueError, match=msg):
+        LcdParams.from_yaml(str(y))
+    y.write_text("%YAML:1.0\nnfeatures: 700\ngnc_alpha: 0.9\nransac_2d2d_algorithm: 1\nmatcher_type: 5\n")
+    p = LcdParams.from_yaml(str(y))  # out-of-path keys are ignored by name
+    assert (p.ransac_2d2d_algorithm, p.norm) == (1, "hamming")
 
 
 def test_synthetic_generators_are_deterministic():

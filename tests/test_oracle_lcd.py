@@ -110,9 +110,36 @@ def test_fivept_recovers_true_essential():
             assert np.abs(np.einsum("ni,ij,nj->n", f1, E, f2)).max() < 1e-12
 
 
-def test_verify_noise_free_pool():
+@pytest.mark.parametrize("seed", [3, 11])
+def test_fivept_stewenius_contains_every_real_solution(seed):
+    """Stewenius (action-matrix eigen-decomposition) vs Nister (Sturm roots of
+    the degree-10 polynomial) on the same samples: the planted E is among the
+    Stewenius solutions, every Nister root is one of them (independent
+    root-finding methods agree), the count is #real + #complex pairs, and
+    every E (real parts included) satisfies the five epipolar constraints."""
+    rng = np.random.default_rng(seed)
+    for trial in range(60):
+        R = _expm_so3(rng.normal(0, 0.4, (1, 3)))[0]
+        t = rng.normal(size=3)
+        pm = np.c_[rng.uniform(-3, 3, (5, 2)), rng.uniform(2, 15, 5)]
+        pq = pm @ R.T + t
+        f1 = pq / np.linalg.norm(pq, axis=1, keepdims=True)
+        f2 = pm / np.linalg.norm(pm, axis=1, keepdims=True)
+        Es, En = O.fivept(f1, f2, 0), O.fivept(f1, f2, 1)
+        tx = np.array([[0, -t[2], t[1]], [t[2], 0, -t[0]], [-t[1], t[0], 0]])
+        Et = tx @ R
+        Et /= np.linalg.norm(Et)
+        d = lambda A, B: min(np.abs(A - B).max(), np.abs(A + B).max())
+        assert min(d(E, Et) for E in Es) < 1e-10, trial
+        assert all(min(d(E, F) for F in Es) < 1e-5 for E in En), trial
+        assert len(En) + (10 - len(En)) // 2 == len(Es), trial
+        assert np.abs(np.einsum("ni,kij,nj->kn", f1, Es, f2)).max() < 1e-12
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["stewenius", "nister"])
+def test_verify_noise_free_pool(algo):
     pool = make_lcd_pool(12, 200, noise_free=True, seed=4)
-    p = LcdParams().to_c()
+    p = LcdParams(ransac_2d2d_algorithm=algo).to_c()
     res, masks = O.lcd_verify(p, pool)
     for c in range(len(res)):
         r = res[c]
