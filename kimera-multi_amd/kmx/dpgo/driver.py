@@ -80,12 +80,14 @@ def exchange_plan(graph, world: int, rank: int):
 
 class RBCDDriver:
     def __init__(self, params: PGOAgentParameters, graph, *, rank: int = 0, world: int = 1,
-                 device: int = 0, solver=None, exchange_device: str | None = None):
+                 device: int = 0, solver=None, exchange_device: str | None = None, log_dir: str | None = None):
         """`solver` defaults to a BlockSolver on HIP device `device`; any object
         with the same interface can be injected (the CPU gloo tests inject the
         restatement). `exchange_device` is where the collective runs ("cuda"
         for RCCL, "cpu" for gloo). A GPU solver under gloo packs into device
-        buffers and stages them through host copies (N ranks on one GPU)."""
+        buffers and stages them through host copies (N ranks on one GPU).
+        `log_dir`: write dpgo_log_<robot>.csv for the robots of this rank
+        (one row per round in which the robot updated, kmx.io.DpgoIterationLog)."""
         if world > graph.n_robots:
             raise ValueError("need at least one robot block per rank")
         self.params = params
@@ -118,6 +120,10 @@ class RBCDDriver:
         self.exchange_rows = (0, 0)  # (rows sent, rows received) per round
         if world > 1:
             self._setup_exchange()
+        self.logs = {}
+        if log_dir is not None:
+            from ..io import DpgoIterationLog
+            self.logs = {a: DpgoIterationLog(log_dir, a) for a in self.robots}
 
     # ------------------------------------------------------ collectives ---
     def _setup_exchange(self):
@@ -192,8 +198,15 @@ class RBCDDriver:
         Returns per-robot stats (team-indexed) when with_stats."""
         self.exchange_public()
         stats = None
-        if with_stats or self.params.schedule == 0:
-            stats = self.solver.iterate(self.active_mask())
+        if with_stats or self.params.schedule == 0 or self.logs:
+            act = self.active_mask()
+            stats = self.solver.iterate(act)
+            if self.logs:
+                nbytes = self.exchange_rows[1] * 4 * self.params.r * 8
+                for a, log in self.logs.items():
+                    if stats[a]["updated"]:
+                        log.log_iteration(self.round_index, int(act.sum()), int(self.graph.n_poses[a]), nbytes,
+                                          stats[a])
         else:
             self.solver.iterate_async(1, refresh_local=False)
         self.round_index += 1

@@ -8,6 +8,17 @@
   the relative pose T_1_2 maps pose2's frame into pose1's.
 * kimera_distributed_keyframes.csv (lc_result.py:606-615): keyframe_id,
   keyframe_stamp_ns.
+* output_lcd_status.csv / output_lcd_result.csv (the LCD logger files
+  lc_result.py:140-183 reads): one status row per verified candidate
+  (lcd_status, query_id, match_id, mono_inliers, stereo_inliers) and one
+  result row (isLoop, queryKfId, matchKfId, timestamp_query, timestamp_match,
+  x, y, z, qx, qy, qz, qw); LOOP_DETECTED rows and isLoop == 1 rows pair up
+  in order.
+* dpgo_log_<robot>.csv (dpgo_ros createIterationLog / logIteration,
+  drawio:2018, 2136-2142): one row per RBCD round of the robot; the dpgo_ros
+  sources are not vendored, the columns restate its iteration log [U]:
+  robot_id, cluster_id, num_active_robots, iteration, num_poses,
+  bytes_received, iter_success, rel_change.
 * g2o (VERTEX_SE3:QUAT / EDGE_SE3:QUAT with the 6x6 upper-triangular
   information, translation block first) as the pose-graph input format: a
   real graph can replace the synthetic configs (SURVEY.md §8d configs[0]).
@@ -132,6 +143,71 @@ def write_keyframes_csv(path, keyframe_ids, stamps_ns):
         w.writerow(["keyframe_id", "keyframe_stamp_ns"])
         for k, s in zip(keyframe_ids, stamps_ns):
             w.writerow([int(k), int(s)])
+
+
+# ------------------------------------------------------------- LCD logs --
+LCD_STATUS_FIELDS = ["timestamp_kf", "lcd_status", "query_id", "match_id", "mono_inliers", "stereo_inliers"]
+LCD_RESULT_FIELDS = ["timestamp_kf", "isLoop", "queryKfId", "matchKfId", "timestamp_query", "timestamp_match", "x",
+                     "y", "z", "qx", "qy", "qz", "qw"]
+
+
+def lcd_status_name(result: dict, min_2d2d: int = 10) -> str:
+    """LCDStatus of one verification (geometricVerificationNister ->
+    recoverPose, drawio:2589-2598)."""
+    if result["accepted"]:
+        return "LOOP_DETECTED"
+    if result["mono_inliers"] < min_2d2d:
+        return "FAILED_GEOM_VERIFICATION"
+    return "FAILED_POSE_RECOVERY"
+
+
+def write_lcd_logs(status_path, result_path, query_ids, match_ids, results, stamps_ns=None, min_2d2d: int = 10):
+    """output_lcd_status.csv + output_lcd_result.csv from LoopClosureDetector
+    .verify results (T_query_match: p_q = R p_m + t)."""
+    n = len(results)
+    st = np.zeros(n, np.int64) if stamps_ns is None else np.asarray(stamps_ns, np.int64)
+    with open(status_path, "w", newline="") as fs, open(result_path, "w", newline="") as fr:
+        ws, wr = csv.writer(fs), csv.writer(fr)
+        ws.writerow(LCD_STATUS_FIELDS)
+        wr.writerow(LCD_RESULT_FIELDS)
+        for k, r in enumerate(results):
+            q_id, m_id = int(query_ids[k]), int(match_ids[k])
+            ws.writerow([int(st[q_id]) if st.size > q_id else 0, lcd_status_name(r, min_2d2d), q_id, m_id,
+                         int(r["mono_inliers"]), int(r["stereo_inliers"])])
+            T = np.asarray(r["T_query_match"], np.float64)
+            qq = rot_to_quat(T[:9].reshape(3, 3))[0] if r["accepted"] else np.array([0.0, 0.0, 0.0, 1.0])
+            wr.writerow([int(st[q_id]) if st.size > q_id else 0, 1 if r["accepted"] else 0, q_id, m_id,
+                         int(st[q_id]) if st.size > q_id else 0, int(st[m_id]) if st.size > m_id else 0,
+                         *("%.12g" % v for v in T[9:]), *("%.12g" % v for v in qq)])
+
+
+# ------------------------------------------------------------- dpgo log --
+DPGO_LOG_FIELDS = ["robot_id", "cluster_id", "num_active_robots", "iteration", "num_poses", "bytes_received",
+                   "iter_success", "rel_change"]
+
+
+class DpgoIterationLog:
+    """dpgo_log_<robot>.csv writer (one per robot; logIteration appends a row
+    per round in which the robot's stats are known)."""
+
+    def __init__(self, directory, robot_id: int, cluster_id: int = 0):
+        import os
+        self.path = os.path.join(str(directory), f"dpgo_log_{int(robot_id)}.csv")
+        self.robot_id, self.cluster_id = int(robot_id), int(cluster_id)
+        with open(self.path, "w", newline="") as f:
+            csv.writer(f).writerow(DPGO_LOG_FIELDS)
+
+    def log_iteration(self, iteration: int, num_active_robots: int, num_poses: int, bytes_received: int,
+                      stats: dict):
+        with open(self.path, "a", newline="") as f:
+            csv.writer(f).writerow([self.robot_id, self.cluster_id, int(num_active_robots), int(iteration),
+                                    int(num_poses), int(bytes_received), int(bool(stats.get("accepted", 0))),
+                                    "%.12g" % float(stats.get("rel_change", 0.0))])
+
+
+def read_dpgo_log(path):
+    with open(path) as f:
+        return [{k: (float(v) if k == "rel_change" else int(v)) for k, v in row.items()} for row in csv.DictReader(f)]
 
 
 # -------------------------------------------------------------------- g2o --
