@@ -853,7 +853,7 @@ __device__ double pnp_error(const double R[9], const double t[3], const double p
 struct RsParams {
   double thr2d, thr3d, prob;
   int max_iter, min2d, min3d, pmax;
-  int pnp;  // pose_recovery_type 1: k_ransac stops after 2D-2D, k_pnp recovers the pose
+  int pnp;  // PnP or Arun recovery: k_ransac stops after 2D-2D, k_recover recovers the pose
   int prof; // diagnostic phase timers (k_ransac_coop)
   int algo; // KMX_ALGO_*: 5-point minimal solver (k_ransac_coop; k_ransac is Nister only)
 };
@@ -2124,7 +2124,7 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac(const double* bearings,
     if (lane == 0) *R_ = r;
     return;
   }
-  if (P.pnp) {  // k_pnp takes over from the 2D-2D inlier mask
+  if (P.pnp) {  // k_recover takes over from the 2D-2D inlier mask
     if (lane == 0) {
       for (int i = 0; i < 12; ++i) r.T_query_match[i] = 0.0;
       *R_ = r;
@@ -2205,15 +2205,60 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac(const double* bearings,
   }
 }
 
-// PnP pose recovery (pose_recovery_type 1): opengv RANSAC over the
-// AbsolutePoseSacProblem with EPnP (sample size 6) on the 2D-2D inliers whose
-// stereo points are valid — query bearings against match-frame points — one
-// wavefront per candidate, one pass per lane, serial control replayed by lane
-// 0 exactly as in k_ransac.
-__global__ __launch_bounds__(RS_BLOCK) void k_pnp(const double* bearings, const double* points, int N,
-                                                  const int* cq, const int* cm, const int2* pairs, const int* Kin,
-                                                  const short* table, PnpParams P, kmx_lcd_result* res,
-                                                  unsigned char* masks) {
+// Arun 3-point model (oracle arun_model): centroids, H = sum dm dq^T, Kabsch
+// with svd3, t = c_q - R c_m (p_q = R p_m + t).
+__device__ void arun_model(const double* sq, const double* sm, double R[9], double t[3]) {
+  double cq[3] = {0.0, 0.0, 0.0}, cm[3] = {0.0, 0.0, 0.0};
+  for (int i = 0; i < 3; ++i)
+    for (int c = 0; c < 3; ++c) {
+      cq[c] += sq[3 * i + c];
+      cm[c] += sm[3 * i + c];
+    }
+  for (int c = 0; c < 3; ++c) {
+    cq[c] /= 3.0;
+    cm[c] /= 3.0;
+  }
+  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 3; ++i) {
+    double dq[3], dm[3];
+    for (int c = 0; c < 3; ++c) {
+      dq[c] = sq[3 * i + c] - cq[c];
+      dm[c] = sm[3 * i + c] - cm[c];
+    }
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) H[a * 3 + b] += dm[a] * dq[b];
+  }
+  double U[9], sv[3], V[9];
+  svd3(H, U, sv, V);
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  if (det3(R) < 0.0) {
+    for (int a = 0; a < 3; ++a) V[a * 3 + 2] = -V[a * 3 + 2];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  }
+  for (int a = 0; a < 3; ++a) t[a] = cq[a] - (R[a * 3 + 0] * cm[0] + R[a * 3 + 1] * cm[1] + R[a * 3 + 2] * cm[2]);
+}
+__device__ double arun_error(const double R[9], const double t[3], const double pq[3], const double pm[3]) {
+  double d[3];
+  for (int a = 0; a < 3; ++a) d[a] = pq[a] - (R[a * 3 + 0] * pm[0] + R[a * 3 + 1] * pm[1] + R[a * 3 + 2] * pm[2] + t[a]);
+  return sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+}
+
+// Pose recovery after the 2D-2D RANSAC, on its inliers whose stereo points
+// are valid (pair-list order), one wavefront per candidate, one hypothesis
+// per lane, the serial control replayed by lane 0 exactly as in k_ransac:
+//   PNP:  pose_recovery_type 1, opengv AbsolutePoseSacProblem with EPnP
+//         (sample 6): query bearings (A) against match-frame points (B);
+//   !PNP: ransac_use_1point_3d3d 0, PointCloudSacProblem with Arun
+//         (sample 3): query points (A) against match points (B).
+template <bool PNP>
+__global__ __launch_bounds__(RS_BLOCK) void k_recover(const double* bearings, const double* points, int N,
+                                                      const int* cq, const int* cm, const int2* pairs, const int* Kin,
+                                                      const short* table, PnpParams P, kmx_lcd_result* res,
+                                                      unsigned char* masks) {
+  constexpr int S = PNP ? PNP_S : 3;
   extern __shared__ __attribute__((aligned(16))) double sm_d[];
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
@@ -2221,9 +2266,9 @@ __global__ __launch_bounds__(RS_BLOCK) void k_pnp(const double* bearings, const 
   if (R_->mono_inliers < P.min2d) return;
   const int K = Kin[c];
   const int q = cq[c], m = cm[c];
-  double* Fq = sm_d;                  // [n2][3]
-  double* Pw = Fq + 3 * N;            // [n2][3]
-  double* models = Pw + 3 * N;        // [64][12]
+  double* Aq = sm_d;                  // [n2][3]
+  double* Bm = Aq + 3 * N;            // [n2][3]
+  double* models = Bm + 3 * N;        // [64][12]
   double* bestm = models + 64 * 12;   // [12]
   int* okc = reinterpret_cast<int*>(bestm + 12);
   int* cnt = okc + 64;
@@ -2239,9 +2284,10 @@ __global__ __launch_bounds__(RS_BLOCK) void k_pnp(const double* bearings, const 
       const double* a = points + ((size_t)q * N + pr.x) * 3;
       const double* b = points + ((size_t)m * N + pr.y) * 3;
       if (isnan(a[0]) || isnan(a[1]) || isnan(a[2]) || isnan(b[0]) || isnan(b[1]) || isnan(b[2])) continue;
+      const double* av = PNP ? bearings + ((size_t)q * N + pr.x) * 3 : a;
       for (int k = 0; k < 3; ++k) {
-        Fq[3 * n2 + k] = bearings[((size_t)q * N + pr.x) * 3 + k];
-        Pw[3 * n2 + k] = b[k];
+        Aq[3 * n2 + k] = av[k];
+        Bm[3 * n2 + k] = b[k];
       }
       id2[n2++] = j;
     }
@@ -2250,28 +2296,36 @@ __global__ __launch_bounds__(RS_BLOCK) void k_pnp(const double* bearings, const 
   }
   __syncthreads();
   const int n2 = ctrl[3];
+  auto err = [&](const double R[9], const double t[3], int j) {
+    return PNP ? pnp_error(R, t, Bm + 3 * j, Aq + 3 * j) : arun_error(R, t, Aq + 3 * j, Bm + 3 * j);
+  };
   int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
   double kk = 1.0;
   const int max_skip = P.max_iter * 10;
-  if (n2 >= PNP_S) {
-    const short* tab = table + (size_t)(n2 - PNP_S) * P.pmax * PNP_S;
+  if (n2 >= S) {
+    const short* tab = table + (size_t)(n2 - S) * P.pmax * S;
     for (int base = 0;; base += RS_BLOCK) {
       const int p = base + lane;
       int ok = 0, count = 0;
       double Rm[9], tm[3];
       if (p < P.pmax) {
-        double sp[3 * PNP_S], sf[3 * PNP_S];
-        for (int i = 0; i < PNP_S; ++i) {
-          const int id = tab[(size_t)p * PNP_S + i];
+        double sa[3 * S], sb[3 * S];
+        for (int i = 0; i < S; ++i) {
+          const int id = tab[(size_t)p * S + i];
           for (int k = 0; k < 3; ++k) {
-            sp[3 * i + k] = Pw[3 * id + k];
-            sf[3 * i + k] = Fq[3 * id + k];
+            sa[3 * i + k] = Aq[3 * id + k];
+            sb[3 * i + k] = Bm[3 * id + k];
           }
         }
-        ok = epnp6(sp, sf, Rm, tm);
+        if (PNP) {
+          ok = epnp6(sb, sa, Rm, tm);
+        } else {
+          arun_model(sa, sb, Rm, tm);
+          ok = 1;
+        }
         if (ok)
           for (int j = 0; j < n2; ++j)
-            if (pnp_error(Rm, tm, Pw + 3 * j, Fq + 3 * j) < P.thr) ++count;
+            if (err(Rm, tm, j) < P.thr) ++count;
       }
       okc[lane] = ok;
       cnt[lane] = count;
@@ -2290,7 +2344,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_pnp(const double* bearings, const 
             for (int i = 0; i < 12; ++i) bestm[i] = models[l * 12 + i];
             have = 1;
             const double w = (double)cnt[l] / (double)n2;
-            double p_no = 1.0 - pow(w, (double)PNP_S);
+            double p_no = 1.0 - pow(w, (double)S);
             p_no = fmax(DBL_EPSILON, p_no);
             p_no = fmin(1.0 - DBL_EPSILON, p_no);
             kk = log(1.0 - P.prob) / log(p_no);
@@ -2315,21 +2369,30 @@ __global__ __launch_bounds__(RS_BLOCK) void k_pnp(const double* bearings, const 
     for (int i = 0; i < 3; ++i) to[i] = bestm[9 + i];
     for (int j0 = 0; j0 < n2; j0 += RS_BLOCK) {
       const int j = j0 + lane;
-      const bool in = (j < n2) && pnp_error(Ro, to, Pw + 3 * j, Fq + 3 * j) < P.thr;
+      const bool in = (j < n2) && err(Ro, to, j) < P.thr;
       if (in) mask[id2[j]] |= 2;
       np += __popcll(__ballot(in));
     }
   }
   if (lane == 0) {
     kmx_lcd_result r = *R_;
-    r.pnp_inliers = np;
-    if (have_model) {
-      for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b) r.T_query_match[a * 3 + b] = Ro[b * 3 + a];
-      for (int a = 0; a < 3; ++a)
-        r.T_query_match[9 + a] = -(Ro[0 * 3 + a] * to[0] + Ro[1 * 3 + a] * to[1] + Ro[2 * 3 + a] * to[2]);
+    if (PNP) {
+      r.pnp_inliers = np;
+      if (have_model) {  // camera pose in the match frame -> T_query_match
+        for (int a = 0; a < 3; ++a)
+          for (int b = 0; b < 3; ++b) r.T_query_match[a * 3 + b] = Ro[b * 3 + a];
+        for (int a = 0; a < 3; ++a)
+          r.T_query_match[9 + a] = -(Ro[0 * 3 + a] * to[0] + Ro[1 * 3 + a] * to[1] + Ro[2 * 3 + a] * to[2]);
+      }
+      r.accepted = (have_model && np >= P.min_pnp) ? 1 : 0;
+    } else {
+      r.stereo_inliers = np;
+      if (have_model) {
+        for (int i = 0; i < 9; ++i) r.T_query_match[i] = Ro[i];
+        for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = to[i];
+      }
+      r.accepted = (have_model && np >= P.min_pnp) ? 1 : 0;
     }
-    r.accepted = (have_model && np >= P.min_pnp) ? 1 : 0;
     *R_ = r;
   }
 }
@@ -2348,7 +2411,7 @@ struct kmx_lcd {
   double* d_pts = nullptr;
   int* d_nfeat = nullptr;
   short* d_table = nullptr;
-  short* d_table6 = nullptr;  // 6-point samples (PnP), built when pose_recovery_type == 1
+  short* d_table_rec = nullptr;  // samples of the recovery RANSAC (6: PnP, 3: Arun), built when used
   int pmax = 0;
   // candidate buffers
   int cap = 0;
@@ -2368,10 +2431,10 @@ struct kmx_lcd {
 namespace {
 
 void lcd_free_pool(kmx_lcd* h) {
-  void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat, h->d_table, h->d_table6};
+  void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat, h->d_table, h->d_table_rec};
   for (void* x : p)
     if (x) (void)hipFree(x);
-  h->d_desc = nullptr; h->d_bear = h->d_pts = nullptr; h->d_nfeat = nullptr; h->d_table = nullptr; h->d_table6 = nullptr;
+  h->d_desc = nullptr; h->d_bear = h->d_pts = nullptr; h->d_nfeat = nullptr; h->d_table = nullptr; h->d_table_rec = nullptr;
 }
 void lcd_free_cand(kmx_lcd* h) {
   void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask, h->d_fbuf};
@@ -2451,7 +2514,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   rp.min2d = h->P.min_2d2d_inliers;
   rp.min3d = h->P.min_3d3d_inliers;
   rp.pmax = h->pmax;
-  rp.pnp = (h->P.pose_recovery_type == 1) ? 1 : 0;
+  rp.pnp = (h->P.pose_recovery_type == 1 || !h->P.use_1point_3d3d) ? 1 : 0;  // k_recover takes over
   rp.prof = h->prof;
   rp.algo = h->P.algorithm_2d2d;
   {
@@ -2481,17 +2544,19 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
     }
   }
   if (rp.pnp) {
+    const bool pnp = h->P.pose_recovery_type == 1;
     PnpParams pp;
-    pp.thr = h->P.ransac_threshold_2d3d;
+    pp.thr = pnp ? h->P.ransac_threshold_2d3d : h->P.ransac_threshold_3d3d;
     pp.prob = h->P.ransac_probability;
     pp.max_iter = h->P.ransac_max_iterations;
     pp.min2d = h->P.min_2d2d_inliers;
-    pp.min_pnp = h->P.min_2d3d_inliers;
+    pp.min_pnp = pnp ? h->P.min_2d3d_inliers : h->P.min_3d3d_inliers;
     pp.pmax = h->pmax;
     const size_t smem = sizeof(double) * (6 * (size_t)h->N + 64 * 12 + 12) + sizeof(int) * (64 + 64 + 4 + (size_t)h->N);
-    hipLaunchKernelGGL(k_pnp, dim3(n), dim3(RS_BLOCK), smem, h->stream, (const double*)h->d_bear,
+    hipLaunchKernelGGL(pnp ? k_recover<true> : k_recover<false>, dim3(n), dim3(RS_BLOCK), smem, h->stream,
+                       (const double*)h->d_bear,
                        (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
-                       (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table6, pp, h->d_res,
+                       (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table_rec, pp, h->d_res,
                        h->d_mask);
   }
   if (h->timing) KMX_HIP(hipEventRecord(h->ev[2], h->stream));
@@ -2508,7 +2573,7 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
   KMX_CHECK(params->rng_variant == KMX_RNG_GCC9 || params->rng_variant == KMX_RNG_GCC11, KMX_EINVAL,
             "bad rng variant");
   KMX_CHECK(params->ransac_randomize == 0, KMX_EUNSUP, "ransac_randomize = 1 is not reproducible; use 0");
-  KMX_CHECK(params->use_1point_3d3d == 1, KMX_EUNSUP, "only the 1-point (given-rotation) 3D-3D check is built");
+  KMX_CHECK(params->use_1point_3d3d == 0 || params->use_1point_3d3d == 1, KMX_EINVAL, "use_1point_3d3d is 0 or 1");
   KMX_CHECK(params->algorithm_2d2d == KMX_ALGO_STEWENIUS || params->algorithm_2d2d == KMX_ALGO_NISTER, KMX_EUNSUP,
             "ransac_2d2d_algorithm: 0 (Stewenius) and 1 (Nister) are built");
   KMX_CHECK(params->ransac_max_iterations > 0, KMX_EINVAL, "ransac_max_iterations must be > 0");
@@ -2586,10 +2651,10 @@ extern "C" int kmx_lcd_set_frames(kmx_lcd* h, const kmx_lcd_batch_desc* pool) {
   build_table(h->P, h->N, h->pmax, tab);
   KMX_HIP(hipMalloc(&h->d_table, sizeof(short) * tab.size()));
   KMX_HIP(hipMemcpy(h->d_table, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
-  if (h->P.pose_recovery_type == 1) {
-    build_table(h->P, h->N, h->pmax, tab, PNP_S);
-    KMX_HIP(hipMalloc(&h->d_table6, sizeof(short) * tab.size()));
-    KMX_HIP(hipMemcpy(h->d_table6, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
+  if (h->P.pose_recovery_type == 1 || !h->P.use_1point_3d3d) {
+    build_table(h->P, h->N, h->pmax, tab, h->P.pose_recovery_type == 1 ? PNP_S : 3);
+    KMX_HIP(hipMalloc(&h->d_table_rec, sizeof(short) * tab.size()));
+    KMX_HIP(hipMemcpy(h->d_table_rec, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
   }
   return KMX_OK;
   KMX_GUARD_END

@@ -33,7 +33,7 @@ class LcdParams:
     ransac_randomize: int = 0
     ransac_seed: int = 12345
     rng_variant: str = "gcc9"           # libstdc++ of ROS Noetic (SURVEY.md §0 finding 5)
-    ransac_use_1point_3d3d: int = 1
+    ransac_use_1point_3d3d: int = 1     # 1: translation given the 2D-2D rotation; 0: Arun 3-point RANSAC
     # opengv CentralRelativePoseSacProblem::algorithm_t (LcdParams.yaml:73):
     # 0 STEWENIUS (the reference config), 1 NISTER
     ransac_2d2d_algorithm: int = 0
@@ -106,6 +106,8 @@ class LcdParams:
             raise ValueError("ransac_2d3d_algorithm: only 3 (EPnP) is built")
         if self.pose_recovery_type not in (0, 1):
             raise ValueError(f"pose_recovery_type {self.pose_recovery_type}")
+        if self.ransac_use_1point_3d3d not in (0, 1):
+            raise ValueError("ransac_use_1point_3d3d is 0 (Arun 3-point) or 1 (given rotation)")
         if self.rng_variant not in ("gcc9", "gcc11"):
             raise ValueError(f"rng_variant {self.rng_variant!r}")
 

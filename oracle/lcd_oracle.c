@@ -23,9 +23,13 @@
  *   2D-2D RANSAC ........ geometricVerificationNister (drawio:2589-2592):
  *                        opengv sac::Ransac loop (k = log(1-p)/log(1-w^5),
  *                        max_skip = 10 * max_iterations), CentralRelativePose
- *                        problem with the 5-point solver (Nister: 10x20
- *                        Gauss-Jordan -> 3x3 polynomial matrix -> degree-10
- *                        polynomial, real roots by Sturm bisection), models
+ *                        problem with the 5-point solver selected by
+ *                        ransac_2d2d_algorithm (LcdParams.yaml:73): 0
+ *                        Stewenius (the reference config; graded 10x20
+ *                        Gauss-Jordan -> 10x10 action matrix -> eigen-
+ *                        decomposition, orc_fivept_stewenius) or 1 Nister
+ *                        (10x20 Gauss-Jordan -> 3x3 polynomial matrix ->
+ *                        degree-10 polynomial, real roots by Sturm bisection), models
  *                        = the 4 (R, t) decompositions of every essential
  *                        matrix, the one with the smallest error on the sample
  *                        kept; error = (1 - f1.r1) + (1 - f2.r2) after mid-point
@@ -35,7 +39,8 @@
  *                        ransac_use_1point_3d3d = 1 (LcdParams.yaml:58): the
  *                        2D-2D rotation is kept, every stereo correspondence
  *                        votes for t_j = p_q - R p_m, the largest consistent set
- *                        (|t_j - t_i| < 0.3 m, LcdParams.yaml:56) wins.
+ *                        (|t_j - t_i| < 0.3 m, LcdParams.yaml:56) wins; = 0:
+ *                        Arun 3-point RANSAC (ransac_arun).
  *   accept ............. mono >= 10, stereo >= 5 (LcdParams.yaml:51-52).
  */
 #include <float.h>
@@ -1430,6 +1435,109 @@ static int given_rotation_3d3d(const kmx_lcd_params* P, const double R[9], const
   return c;
 }
 
+/* Arun 3-point 3D-3D (ransac_use_1point_3d3d = 0, LcdParams.yaml:58): opengv
+ * sac::Ransac over the PointCloudSacProblem with point_cloud::threept_arun
+ * (Arun, Huang, Blostein 1987), restated: centroids of the 3 sampled pairs,
+ * H = sum (p_m - c_m)(p_q - c_q)^T, H = U S V^T, R = V U^T with V's third
+ * column negated when det R < 0 (Kabsch), t = c_q - R c_m; the model maps
+ * match-frame points to the query frame (p_q = R p_m + t). Error of a pair:
+ * |p_q - (R p_m + t)| (Euclidean, metres) against ransac_threshold_3d3d.
+ * Sampler and stopping rule as the 2D-2D RANSAC with sample size 3, on the
+ * stereo-valid 2D-2D inliers in pair-list order [U: opengv's exact point
+ * cloud error definition; optimize_3d3d_pose_from_inliers = 0, no refit]. */
+static void arun_model(const double* Pq, const double* Pm, const int32_t* smp, double R[9], double t[3]) {
+  double cq[3] = {0.0, 0.0, 0.0}, cm[3] = {0.0, 0.0, 0.0};
+  for (int i = 0; i < 3; ++i)
+    for (int c = 0; c < 3; ++c) {
+      cq[c] += Pq[3 * smp[i] + c];
+      cm[c] += Pm[3 * smp[i] + c];
+    }
+  for (int c = 0; c < 3; ++c) {
+    cq[c] /= 3.0;
+    cm[c] /= 3.0;
+  }
+  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 3; ++i) {
+    double dq[3], dm[3];
+    for (int c = 0; c < 3; ++c) {
+      dq[c] = Pq[3 * smp[i] + c] - cq[c];
+      dm[c] = Pm[3 * smp[i] + c] - cm[c];
+    }
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) H[a * 3 + b] += dm[a] * dq[b];
+  }
+  double U[9], sv[3], V[9];
+  svd3(H, U, sv, V);
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  if (det3(R) < 0.0) {
+    for (int a = 0; a < 3; ++a) V[a * 3 + 2] = -V[a * 3 + 2];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  }
+  for (int a = 0; a < 3; ++a) t[a] = cq[a] - (R[a * 3 + 0] * cm[0] + R[a * 3 + 1] * cm[1] + R[a * 3 + 2] * cm[2]);
+}
+
+static double arun_error(const double R[9], const double t[3], const double pq[3], const double pm[3]) {
+  double d[3];
+  for (int a = 0; a < 3; ++a) d[a] = pq[a] - (R[a * 3 + 0] * pm[0] + R[a * 3 + 1] * pm[1] + R[a * 3 + 2] * pm[2] + t[a]);
+  return sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+}
+
+static int ransac_arun(const kmx_lcd_params* P, const double* Pq, const double* Pm, int K, double R[9], double t[3],
+                       uint8_t* inl, int* n_inl) {
+  *n_inl = 0;
+  const int S = 3;
+  if (K < S) return 0;
+  orc_mt19937 m;
+  mt_seed(&m, P->ransac_seed);
+  int32_t* sh = (int32_t*)malloc(sizeof(int32_t) * K);
+  for (int i = 0; i < K; ++i) sh[i] = i;
+  int iterations = 0, best_cnt = -INT_MAX, have = 0;
+  double k = 1.0;
+  double bR[9], bt[3];
+  while (iterations < k) {
+    for (int i = 0; i < S; ++i) {
+      const int r = uid_draw(&m, P->rng_variant);
+      const int j = i + (int)((size_t)r % (size_t)(K - i));
+      const int32_t tt = sh[i];
+      sh[i] = sh[j];
+      sh[j] = tt;
+    }
+    double Rm[9], tm[3];
+    arun_model(Pq, Pm, sh, Rm, tm);
+    int cnt = 0;
+    for (int j = 0; j < K; ++j)
+      if (arun_error(Rm, tm, Pq + 3 * j, Pm + 3 * j) < P->ransac_threshold_3d3d) ++cnt;
+    if (cnt > best_cnt) {
+      best_cnt = cnt;
+      memcpy(bR, Rm, sizeof(bR));
+      memcpy(bt, tm, sizeof(bt));
+      have = 1;
+      const double w = (double)cnt / (double)K;
+      double p_no = 1.0 - pow(w, (double)S);
+      p_no = fmax(DBL_EPSILON, p_no);
+      p_no = fmin(1.0 - DBL_EPSILON, p_no);
+      k = log(1.0 - P->ransac_probability) / log(p_no);
+    }
+    ++iterations;
+    if (iterations > P->ransac_max_iterations) break;
+  }
+  free(sh);
+  if (!have) return 0;
+  int c = 0;
+  for (int j = 0; j < K; ++j) {
+    const int in = arun_error(bR, bt, Pq + 3 * j, Pm + 3 * j) < P->ransac_threshold_3d3d;
+    inl[j] = (uint8_t)in;
+    c += in;
+  }
+  *n_inl = c;
+  memcpy(R, bR, sizeof(bR));
+  memcpy(t, bt, sizeof(bt));
+  return 1;
+}
+
 /* Full verification of one candidate from a frame pool (same layout as
  * kmx_lcd_batch_desc). masks (optional): [max_feats] bytes per candidate, bit0
  * 2D-2D inlier, bit1 3D-3D inlier, indexed by position in the pair list. */
@@ -1508,6 +1616,33 @@ int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int3
       }
       res->accepted = (okp && np >= P->min_2d3d_inliers) ? 1 : 0;
       free(Fq); free(Pw); free(id2);
+    } else if (!P->use_1point_3d3d) {
+      /* Arun RANSAC over the stereo-valid inliers, in pair-list order */
+      double* Aq = (double*)malloc(sizeof(double) * 3 * (n3 + 1));
+      double* Am = (double*)malloc(sizeof(double) * 3 * (n3 + 1));
+      int32_t* id2 = (int32_t*)malloc(sizeof(int32_t) * (n3 + 1));
+      int n2 = 0;
+      for (int j = 0; j < n3; ++j) {
+        if (!valid[j]) continue;
+        for (int c = 0; c < 3; ++c) {
+          Aq[3 * n2 + c] = Pq[3 * j + c];
+          Am[3 * n2 + c] = Pm[3 * j + c];
+        }
+        id2[n2++] = idx[j];
+      }
+      double Ra[9], ta[3];
+      int na = 0;
+      const int oka = ransac_arun(P, Aq, Am, n2, Ra, ta, in3, &na);
+      res->stereo_inliers = oka ? na : 0;
+      if (oka) {
+        if (mask)
+          for (int j = 0; j < n2; ++j)
+            if (in3[j]) mask[id2[j]] |= 2;
+        for (int i = 0; i < 9; ++i) res->T_query_match[i] = Ra[i];
+        for (int i = 0; i < 3; ++i) res->T_query_match[9 + i] = ta[i];
+      }
+      res->accepted = (oka && na >= P->min_3d3d_inliers) ? 1 : 0;
+      free(Aq); free(Am); free(id2);
     } else {
       double t3[3];
       const int c3 = given_rotation_3d3d(P, R, Pq, Pm, valid, n3, t3, in3);

@@ -23,9 +23,9 @@ OUT = Path(__file__).resolve().parent
 
 DPGO_ROUNDS = 12
 DPGO_GNC_EVERY = 4       # update_weights after rounds 3, 7, 11 (as test_rounds_match_oracle)
-LCD_CASES = [            # (ransac_2d2d_algorithm, rng_variant, norm, pose_recovery_type)
+LCD_CASES = [            # (ransac_2d2d_algorithm, rng_variant, norm, recovery: 0 1-point 3D-3D, 1 PnP, 2 Arun)
     (0, "gcc9", "l1", 0), (1, "gcc9", "l1", 0), (0, "gcc11", "hamming", 0), (1, "gcc11", "hamming", 0),
-    (0, "gcc9", "l1", 1),
+    (0, "gcc9", "l1", 1), (0, "gcc9", "l1", 2),
 ]
 
 
@@ -100,7 +100,8 @@ def pool_from(d):
 def lcd_params(case):
     from kmx.lcd import LcdParams
     algo, variant, norm, rec = case
-    return LcdParams(ransac_2d2d_algorithm=algo, rng_variant=variant, norm=norm, pose_recovery_type=rec)
+    return LcdParams(ransac_2d2d_algorithm=algo, rng_variant=variant, norm=norm, pose_recovery_type=int(rec == 1),
+                     ransac_use_1point_3d3d=int(rec != 2))
 
 
 def run_lcd_oracle(pool, case):

@@ -31,13 +31,16 @@ def test_knn2_matches_oracle(gpu, norm):
 
 
 @pytest.mark.parametrize("algo", [0, 1], ids=["stewenius", "nister"])
-@pytest.mark.parametrize("variant,norm,recovery", [("gcc9", "l1", 0), ("gcc11", "hamming", 0), ("gcc9", "l1", 1)])
+@pytest.mark.parametrize("variant,norm,recovery", [("gcc9", "l1", 0), ("gcc11", "hamming", 0), ("gcc9", "l1", 1),
+                                                   ("gcc11", "l1", 2)])
 def test_verify_bit_exact(gpu, variant, norm, recovery, algo):
-    """recovery 0: 1-point 3D-3D (reference config); 1: EPnP RANSAC (LC4).
+    """recovery 0: 1-point 3D-3D (reference config); 1: EPnP RANSAC (LC4);
+    2: Arun 3-point 3D-3D RANSAC (ransac_use_1point_3d3d 0).
     algo: ransac_2d2d_algorithm (0 Stewenius, the reference config; 1 Nister)."""
     from oracle import oracle as O
     pool = make_lcd_pool(24, 300, seed=3)
-    p = LcdParams(rng_variant=variant, norm=norm, pose_recovery_type=recovery, ransac_2d2d_algorithm=algo)
+    p = LcdParams(rng_variant=variant, norm=norm, pose_recovery_type=int(recovery == 1),
+                  ransac_2d2d_algorithm=algo, ransac_use_1point_3d3d=int(recovery != 2))
     det = LoopClosureDetector(p)
     det.set_pool(pool)
     got, gm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)

@@ -161,6 +161,25 @@ def test_verify_noise_free_pool(algo):
             assert not r.accepted
 
 
+@pytest.mark.parametrize("noise_free", [True, False])
+def test_verify_arun_3d3d(noise_free):
+    """Arun 3-point 3D-3D RANSAC (ransac_use_1point_3d3d: 0): planted pairs
+    accepted with the planted pose (exact without noise, within the point
+    noise otherwise), random pairs rejected."""
+    pool = make_lcd_pool(12, 200, noise_free=noise_free, seed=4)
+    res, masks = O.lcd_verify(LcdParams(ransac_use_1point_3d3d=0).to_c(), pool)
+    for c in range(len(res)):
+        r = res[c]
+        if c % 2 == 0:
+            T = np.array(r.T_query_match[:])
+            assert r.accepted and r.stereo_inliers >= 0.95 * r.mono_inliers
+            assert np.abs(T[:9].reshape(3, 3) - pool.R_qm[c // 2]).max() < (1e-12 if noise_free else 0.02)
+            assert np.abs(T[9:] - pool.t_qm[c // 2]).max() < (1e-12 if noise_free else 0.2)
+            assert int(((masks[c] & 2) > 0).sum()) == r.stereo_inliers
+        else:
+            assert not r.accepted
+
+
 def test_epnp_recovers_camera_pose():
     """EPnP restatement (LC4): noise-free correspondences give the exact camera
     pose (R_wc, t_wc) for 6..40 points."""
