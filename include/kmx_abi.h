@@ -79,7 +79,10 @@ typedef struct kmx_pgo_params {
   double gnc_barc;          /* TLS error threshold c-bar (5.0)                */
   double gnc_mu_init;       /* GNC initial mu (1e-5)                          */
   double gnc_mu_step;       /* mu <- mu * step after each weight update (1.4) */
-  int reserved[8];
+  int acceleration;         /* Nesterov-accelerated RBCD (RBCD++) on/off (0); concurrent
+                               schedule only: every local robot updates every round      */
+  int restart_interval;     /* acceleration restart period in rounds (30)               */
+  int reserved[6];
 } kmx_pgo_params;
 
 /* Per-robot statistics of one RBCD round (what dpgo logs to dpgo_log_*.csv via
@@ -184,6 +187,14 @@ int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats* stats);
  * round (every round republishes the rows it commits): the single-device
  * exchange; otherwise the caller exchanges between rounds. */
 int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local);
+/* Acceleration (kmx_pgo_params.acceleration = 1, concurrent schedule only):
+ * each round first forms the extrapolated point Y = Proj((1 - alpha) X +
+ * alpha V) and sets X := Y (the first of refresh_local / exchange_pack /
+ * iterate in a round does it, so the exchanged and published rows are Y and
+ * the block update starts from Y); after the block updates V = Proj(V +
+ * gamma (X - Y)), and every restart_interval rounds V = X, gamma = 0. Between
+ * rounds X is the accelerated iterate itself; between the exchange and
+ * iterate it holds Y. set_iterate restarts the acceleration (V = X). */
 /* Wait for all work enqueued on the handle's stream. */
 int kmx_pgo_sync(kmx_pgo* h);
 

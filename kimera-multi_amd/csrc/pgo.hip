@@ -1550,6 +1550,60 @@ __global__ void k_traj(const double* X, int n, int R_, const double* anchor, dou
   o[9] = tv[0]; o[10] = tv[1]; o[11] = tv[2];
 }
 
+// Nesterov acceleration (oracle orc_pgo_accel_pre / _post; RBCD++):
+//   mode 0: Y = Proj((1 - c) X + c V) -> Yb, X and the owned public rows
+//   mode 1: V = Proj(V + c (X - Yb))
+//   mode 2: V = X (restart)
+// Proj: polar factor of the pose's r x 3 rotation block, M (M^T M)^(-1/2) from
+// the group's 3 x 3 Gram matrix (gsum in row order) and jacobi3; translation
+// unchanged. One lane per (pose, row), as k_retract.
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_accel(Dev d, double* V, double* Yb, double c, int mode) {
+  const Lane L = lane_map<R>(d);
+  const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+  double x[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0};
+  if (L.valid) {
+    load4(d.X + o, x);
+    if (mode != 2) load4(V + o, v);
+    if (mode == 1) load4(Yb + o, y);
+  }
+  if (mode == 2) {
+    if (L.valid) store4(V + o, x);
+    return;
+  }
+  double m[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m[k] = (mode == 0) ? (1.0 - c) * x[k] + c * v[k] : v[k] + c * (x[k] - y[k]);
+  double G[9], W[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = i; j < 3; ++j) {
+      const double g = gsum<R>(m[i] * m[j], L.base);
+      G[i * 3 + j] = g;
+      G[j * 3 + i] = g;
+    }
+  jacobi3(G, W);
+  double isq[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) isq[k] = 1.0 / sqrt(G[k * 4]);
+  double cc[3], out[4];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) cc[k] = (m[0] * W[0 * 3 + k] + m[1] * W[1 * 3 + k] + m[2] * W[2 * 3 + k]) * isq[k];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) out[j] = cc[0] * W[j * 3 + 0] + cc[1] * W[j * 3 + 1] + cc[2] * W[j * 3 + 2];
+  out[3] = m[3];
+  if (!L.valid) return;
+  if (mode == 0) {
+    store4(Yb + o, out);
+    store4(d.X + o, out);
+    const int s = d.pose_slot[L.pose];
+    if (s >= 0) store4(d.pub + (size_t)s * 4 * R + 4 * L.a, out);
+  } else {
+    store4(V + o, out);
+  }
+}
+
 // Primitive evaluation for parity tests (tiles of one robot), through the same
 // gathers as the round kernels.
 template <int R>
@@ -1680,6 +1734,12 @@ struct kmx_pgo {
   double* d_gpart = nullptr;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
+  // Nesterov acceleration (P.acceleration): momentum V and this round's Y
+  // (allocated only when enabled), gamma and the restart counter on the host
+  double *d_accV = nullptr, *d_accY = nullptr;
+  double acc_gamma = 0.0;
+  int acc_k = 0;
+  bool acc_ready = false, acc_started = false;
 };
 
 namespace {
@@ -1699,7 +1759,7 @@ void free_dev(kmx_pgo* h) {
                   h->d_ctl, h->d_cnt, h->d_tickets, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
-                  h->d_rgroup0, h->d_gtickets, h->d_gpart};
+                  h->d_rgroup0, h->d_gtickets, h->d_gpart, h->d_accV, h->d_accY};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
@@ -1724,6 +1784,7 @@ void free_dev(kmx_pgo* h) {
   h->d_rgroup0 = nullptr;
   h->d_gtickets = nullptr;
   h->d_gpart = nullptr;
+  h->d_accV = h->d_accY = nullptr;
 }
 
 hipEvent_t next_event(kmx_pgo* h) {
@@ -1898,6 +1959,48 @@ void enqueue_round(kmx_pgo* h, const unsigned char* d_active) {
   }
 }
 
+// Acceleration (oracle orc_pgo_accel_pre / _post): gamma' = (1 + sqrt(1 +
+// 4 N^2 gamma^2)) / (2 N), alpha = 1 / (gamma' N), N = team size.
+double accel_gamma_next(const kmx_pgo* h) {
+  const double N = (double)h->n_robots;
+  return (1.0 + std::sqrt(1.0 + 4.0 * N * N * h->acc_gamma * h->acc_gamma)) / (2.0 * N);
+}
+void launch_accel(kmx_pgo* h, double c, int mode) {
+  const dim3 grid(h->ntiles), blk(BLOCK);
+  switch (h->P.r) {
+#define KMX_ACC(RR) \
+  case RR: hipLaunchKernelGGL(k_accel<RR>, grid, blk, 0, h->stream, h->dv, h->d_accV, h->d_accY, c, mode); break;
+    KMX_ACC(3) KMX_ACC(4) KMX_ACC(5) KMX_ACC(6) KMX_ACC(7)
+    default: hipLaunchKernelGGL(k_accel<8>, grid, blk, 0, h->stream, h->dv, h->d_accV, h->d_accY, c, mode); break;
+#undef KMX_ACC
+  }
+}
+// Y for the upcoming round (X := Y, owned public rows := Y); once per round.
+void enqueue_accel_pre(kmx_pgo* h) {
+  if (!h->P.acceleration || h->acc_ready || h->ntiles == 0) return;
+  if (!h->acc_started) {
+    launch_accel(h, 0.0, 2);  // V = X
+    h->acc_started = true;
+  }
+  const double g = accel_gamma_next(h);
+  launch_accel(h, 1.0 / (g * (double)h->n_robots), 0);
+  h->acc_ready = true;
+}
+void enqueue_accel_post(kmx_pgo* h) {
+  if (!h->P.acceleration || !h->acc_ready || h->ntiles == 0) return;
+  const double g = accel_gamma_next(h);
+  const bool restart = h->P.restart_interval > 0 && (h->acc_k + 1) % h->P.restart_interval == 0;
+  launch_accel(h, g, restart ? 2 : 1);
+  h->acc_gamma = restart ? 0.0 : g;
+  h->acc_k = restart ? 0 : h->acc_k + 1;
+  h->acc_ready = false;
+}
+void accel_reset(kmx_pgo* h) {
+  h->acc_gamma = 0.0;
+  h->acc_k = 0;
+  h->acc_ready = h->acc_started = false;
+}
+
 template <int RW>
 void enqueue_apply_weights_t(kmx_pgo* h) {
   if (h->mloc > 0)
@@ -1921,6 +2024,8 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
             "rtr_iterations and tcg_max_iterations must be >= 1");
   KMX_CHECK(params->robust_cost == KMX_COST_L2 || params->robust_cost == KMX_COST_GNC_TLS, KMX_EUNSUP,
             "robust cost must be L2 or GNC_TLS");
+  KMX_CHECK((params->acceleration == 0 || params->acceleration == 1) && params->restart_interval >= 0, KMX_EINVAL,
+            "acceleration is 0 or 1, restart_interval >= 0");
   int ndev = 0;
   KMX_HIP(hipGetDeviceCount(&ndev));
   KMX_CHECK(device >= 0 && device < ndev, KMX_EINVAL, "bad HIP device ordinal");
@@ -1978,6 +2083,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->stream));
   free_dev(h);
+  accel_reset(h);
   const int r = h->P.r, ps = 4 * r;
   h->n_robots = n_robots;
   h->npose.assign(n_poses, n_poses + n_robots);
@@ -2192,6 +2298,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_Pinv, (size_t)std::max(nloc, 1) * 16)) ||
       (rc = dalloc(&h->d_hD, (size_t)std::max(nloc, 1) * 16)) ||
       (rc = dalloc(&h->d_pub, (size_t)std::max<int64_t>(h->npub, 1) * ps)) ||
+      (h->P.acceleration && ((rc = dalloc(&h->d_accV, vec)) || (rc = dalloc(&h->d_accY, vec)))) ||
       (rc = dalloc(&h->d_part, (size_t)h->ntiles * NPART)) || (rc = dalloc(&h->d_ctl, L)) ||
       (rc = dalloc(&h->d_cnt, 1)) || (rc = dalloc(&h->d_tickets, L)) || (rc = dalloc(&h->d_m_robot, L)) ||
       (rc = dalloc(&h->d_n_robot, L)) || (rc = dalloc(&h->d_pub_src, pub_src.size())) ||
@@ -2306,6 +2413,7 @@ extern "C" int kmx_pgo_set_iterate(kmx_pgo* h, int robot, const double* X) {
   KMX_HIP(hipMemcpyAsync(h->d_vec + (size_t)h->loff[l] * ps, X, sizeof(double) * h->npose[robot] * ps,
                          hipMemcpyHostToDevice, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));
+  accel_reset(h);  // a new initial iterate restarts the acceleration (V = X at the next round)
   return KMX_OK;
 }
 
@@ -2366,6 +2474,7 @@ extern "C" int kmx_pgo_exchange_pack(kmx_pgo* h, const int32_t* dev_slots, int64
                 (n_seg == 0 || (dev_seg && dev_out)),
             KMX_EINVAL, "bad argument");
   KMX_HIP(hipSetDevice(h->device));
+  enqueue_accel_pre(h);  // accelerated rounds exchange Y
   const int ps = 4 * h->P.r;
   const long long tot = (long long)n * ps;
   if (tot)
@@ -2413,6 +2522,7 @@ extern "C" int kmx_pgo_exchange_unpack(kmx_pgo* h, const int32_t* dev_slots, int
 extern "C" int kmx_pgo_refresh_local(kmx_pgo* h) {
   KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
   KMX_HIP(hipSetDevice(h->device));
+  enqueue_accel_pre(h);  // accelerated rounds publish Y
   enqueue_publish(h);
   KMX_HIP(hipGetLastError());
   return KMX_OK;
@@ -2448,8 +2558,13 @@ extern "C" int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats
   const int L = (int)h->robots.size();
   std::vector<unsigned char> act(L);
   for (int l = 0; l < L; ++l) act[l] = active[h->robots[l]] ? 1 : 0;
+  if (h->P.acceleration)
+    for (int l = 0; l < L; ++l)
+      KMX_CHECK(act[l], KMX_EUNSUP, "acceleration needs every local robot active (concurrent schedule)");
   KMX_HIP(hipMemcpyAsync(h->d_active, act.data(), L, hipMemcpyHostToDevice, h->stream));
+  enqueue_accel_pre(h);
   enqueue_round(h, h->d_active);
+  enqueue_accel_post(h);
   KMX_HIP(hipGetLastError());
   std::vector<Ctl> ctl(L);
   KMX_HIP(hipMemcpyAsync(ctl.data(), h->d_ctl, sizeof(Ctl) * L, hipMemcpyDeviceToHost, h->stream));
@@ -2488,7 +2603,11 @@ extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local) 
   // every round's k_commit republishes the committed owned rows, so the
   // single-device exchange needs one publish per call
   if (refresh_local && rounds > 0) enqueue_publish(h);
-  for (int i = 0; i < rounds; ++i) enqueue_round(h, h->d_active);
+  for (int i = 0; i < rounds; ++i) {
+    enqueue_accel_pre(h);  // publishes Y itself
+    enqueue_round(h, h->d_active);
+    enqueue_accel_post(h);
+  }
   KMX_HIP(hipGetLastError());
   return KMX_OK;
 }
@@ -2733,6 +2852,7 @@ extern "C" int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_byt
   b += std::max<int64_t>(h->npub, 1) * (ps * 8 + 4) + n * 4;             // public table + maps
   b += (int64_t)h->ntiles * (NPART * 8 + 12) + L * (int64_t)(sizeof(Ctl) + 32);
   b += (int64_t)std::max(h->n_gnc, 1) * 12 + (int64_t)h->scratch_cap * 8;  // GNC lists, scratch in use
+  if (h->P.acceleration) b += 2 * n * ps * 8;                              // V, Y
   if (device_bytes) *device_bytes = b;
   if (record_bytes) *record_bytes = h->rw * 8;
   return KMX_OK;

@@ -50,7 +50,8 @@ class PgoParams(C.Structure):
         ("gradnorm_tol", C.c_double), ("use_preconditioner", C.c_int),
         ("precond_shift", C.c_double), ("robust_cost", C.c_int),
         ("gnc_barc", C.c_double), ("gnc_mu_init", C.c_double),
-        ("gnc_mu_step", C.c_double), ("reserved", C.c_int * 8),
+        ("gnc_mu_step", C.c_double), ("acceleration", C.c_int), ("restart_interval", C.c_int),
+        ("reserved", C.c_int * 6),
     ]
 
 

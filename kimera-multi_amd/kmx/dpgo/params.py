@@ -65,6 +65,8 @@ class PGOAgentParameters:
     schedule: int = 1                      # 0 sequential (dpgo_ros sync), 1 concurrent
     updateRule: int = 0                    # sequential: 0 round-robin, 1 uniform (dpgo_ros update rule)
     randomSeed: int = 0                    # seed of the uniform rule's std::mt19937 (dpgo_ros random_seed)
+    acceleration: bool = False             # Nesterov-accelerated RBCD (dpgo acceleration; concurrent schedule)
+    restartInterval: int = 30              # acceleration restart period in rounds (dpgo restartInterval [U])
 
     def to_c(self) -> PgoParams:
         lo, rc = self.localOptimizationParams, self.robustCostParams
@@ -79,4 +81,6 @@ class PGOAgentParameters:
         p.precond_shift = lo.precond_shift
         p.robust_cost = int(rc.costType)
         p.gnc_barc, p.gnc_mu_init, p.gnc_mu_step = rc.GNCBarc, rc.GNCInitMu, rc.GNCMuStep
+        p.acceleration = 1 if self.acceleration else 0
+        p.restart_interval = int(self.restartInterval)
         return p

@@ -19,7 +19,8 @@
  *         f(X) = 1/2 sum_e w_e (kappa_e ||Y_j - Y_i R_e||^2 + tau_e ||p_j - p_i - Y_i t_e||^2)
  *         over the robot's private and shared edges; neighbour poses fixed.
  *   D4  Stiefel projection, Riemannian Hessian (Weingarten term), QF retraction
- *   D5  RTR outer step + preconditioned Steihaug-Toint tCG (ROPTLIB RTRNewton)
+ *   D5  RTR outer step + preconditioned Steihaug-Toint tCG (ROPTLIB RTRNewton),
+ *       optional Nesterov acceleration with periodic restart (orc_pgo_accel_*)
  *   D6  GNC_TLS weights + mu schedule ......... updateMeasurementWeights (drawio:2215, 2466-2469)
  *   D8  rounding to SE(3) in the anchor frame . getTrajectoryInGlobalFrame / publishTrajectory (drawio:2148)
  *   D9  concurrent / sequential round ......... runOnceSynchronous (drawio:2071, 2478-2481)
@@ -51,6 +52,12 @@ typedef struct {
   double* X;    /* ntot * 4r current iterate */
   double* nbr;  /* ntot * 4r neighbour snapshot (public poses) */
   double mu;
+  /* Nesterov acceleration (P.acceleration): momentum V, the extrapolated
+   * point Y of the current round, gamma, rounds since the last restart, and
+   * whether Y has been formed for the upcoming round */
+  double *V, *Yb;
+  double gamma;
+  int acc_k, acc_ready, acc_started;
 } orc_pgo;
 
 static int PS(const orc_pgo* h) { return 4 * h->P.r; } /* doubles per pose */
@@ -68,7 +75,8 @@ static void free_graph(orc_pgo* h) {
   free(h->r1); free(h->p1); free(h->r2); free(h->p2);
   free(h->Rm); free(h->tv); free(h->kappa); free(h->tau); free(h->w); free(h->fixed);
   if (h->redges) for (int a = 0; a < h->R; ++a) free(h->redges[a]);
-  free(h->redges); free(h->nredges); free(h->X); free(h->nbr);
+  free(h->redges); free(h->nredges); free(h->X); free(h->nbr); free(h->V); free(h->Yb);
+  h->V = h->Yb = NULL;
 }
 
 void orc_pgo_destroy(void* vh) {
@@ -121,12 +129,20 @@ int orc_pgo_set_graph(void* vh, int n_robots, const int32_t* n_poses, int64_t m,
   free(fill);
   h->X = (double*)calloc((size_t)h->ntot * PS(h) + 1, sizeof(double));
   h->nbr = (double*)calloc((size_t)h->ntot * PS(h) + 1, sizeof(double));
+  if (h->P.acceleration) {
+    h->V = (double*)calloc((size_t)h->ntot * PS(h) + 1, sizeof(double));
+    h->Yb = (double*)calloc((size_t)h->ntot * PS(h) + 1, sizeof(double));
+  }
+  h->gamma = 0.0;
+  h->acc_k = h->acc_ready = h->acc_started = 0;
   return 0;
 }
 
 int orc_pgo_set_iterate(void* vh, int a, const double* X) {
   orc_pgo* h = (orc_pgo*)vh;
   memcpy(h->X + h->poff[a] * PS(h), X, sizeof(double) * (size_t)h->npose[a] * PS(h));
+  h->gamma = 0.0; /* a new initial iterate restarts the acceleration */
+  h->acc_k = h->acc_ready = h->acc_started = 0;
   return 0;
 }
 int orc_pgo_get_iterate(void* vh, int a, double* X) {
@@ -492,11 +508,106 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
   free(eta); free(Heta); free(rr); free(z); free(del); free(Hd); free(Xt); free(X0);
 }
 
+/* ------------------------------------------------ Nesterov acceleration -- */
+/* dpgo's accelerated RBCD (RBCD++, Tian et al. T-RO 2021 Alg. 3/4; PGOAgent
+ * updateGamma / updateAlpha / updateY / updateV / restartNesterovAcceleration
+ * [U: dpgo source not vendored]) for the concurrent schedule, N = team size:
+ *   gamma' = (1 + sqrt(1 + 4 N^2 gamma^2)) / (2 N),  alpha = 1 / (gamma' N)
+ *   Y      = Proj((1 - alpha) X + alpha V)        (before the round: the
+ *            public poses and the block update start from Y)
+ *   X'     = block update from Y
+ *   V      = Proj(V + gamma' (X' - Y))
+ * and every restart_interval rounds V = X', gamma = 0 (else gamma = gamma').
+ * Proj: the rotation block to the Stiefel manifold by its polar factor
+ * M (M^T M)^(-1/2) (the SVD's U V^T), translation unchanged. */
+static void jacobi3(double A[9], double V[9]);
+static void proj_stiefel(int r, const double* M, double* out) {
+  double G[9], W[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double s = 0.0;
+      for (int a = 0; a < r; ++a) s += M[4 * a + i] * M[4 * a + j];
+      G[i * 3 + j] = s;
+    }
+  jacobi3(G, W);
+  double isq[3];
+  for (int k = 0; k < 3; ++k) isq[k] = 1.0 / sqrt(G[k * 4]);
+  for (int a = 0; a < r; ++a) {
+    double c[3];
+    for (int k = 0; k < 3; ++k)
+      c[k] = (M[4 * a + 0] * W[0 * 3 + k] + M[4 * a + 1] * W[1 * 3 + k] + M[4 * a + 2] * W[2 * 3 + k]) * isq[k];
+    for (int j = 0; j < 3; ++j) out[4 * a + j] = c[0] * W[j * 3 + 0] + c[1] * W[j * 3 + 1] + c[2] * W[j * 3 + 2];
+    out[4 * a + 3] = M[4 * a + 3];
+  }
+}
+
+static double accel_gamma_next(const orc_pgo* h) {
+  const double N = (double)h->R;
+  return (1.0 + sqrt(1.0 + 4.0 * N * N * h->gamma * h->gamma)) / (2.0 * N);
+}
+
+/* updateGamma / updateAlpha / updateY for the robots in `mask` (NULL: all);
+ * X := Y. A no-op when Y is already formed for this round. */
+int orc_pgo_accel_pre(void* vh, const uint8_t* mask) {
+  orc_pgo* h = (orc_pgo*)vh;
+  if (!h->P.acceleration || h->acc_ready) return 0;
+  const int ps = PS(h), r = h->P.r;
+  if (!h->acc_started) {
+    memcpy(h->V, h->X, sizeof(double) * (size_t)h->ntot * ps);
+    h->acc_started = 1;
+  }
+  const double g = accel_gamma_next(h), alpha = 1.0 / (g * (double)h->R);
+  double M[4 * 8];
+  for (int a = 0; a < h->R; ++a) {
+    if (mask && !mask[a]) continue;
+    for (int64_t i = h->poff[a]; i < h->poff[a + 1]; ++i) {
+      const double* x = h->X + i * ps;
+      const double* v = h->V + i * ps;
+      for (int k = 0; k < ps; ++k) M[k] = (1.0 - alpha) * x[k] + alpha * v[k];
+      proj_stiefel(r, M, h->Yb + i * ps);
+      memcpy(h->X + i * ps, h->Yb + i * ps, sizeof(double) * ps);
+    }
+  }
+  h->acc_ready = 1;
+  return 0;
+}
+
+/* updateV after the block updates, then the periodic restart. */
+int orc_pgo_accel_post(void* vh, const uint8_t* mask) {
+  orc_pgo* h = (orc_pgo*)vh;
+  if (!h->P.acceleration || !h->acc_ready) return 0;
+  const int ps = PS(h), r = h->P.r;
+  const double g = accel_gamma_next(h);
+  const int restart = h->P.restart_interval > 0 && (h->acc_k + 1) % h->P.restart_interval == 0;
+  double M[4 * 8];
+  for (int a = 0; a < h->R; ++a) {
+    if (mask && !mask[a]) continue;
+    for (int64_t i = h->poff[a]; i < h->poff[a + 1]; ++i) {
+      double* v = h->V + i * ps;
+      const double* x = h->X + i * ps;
+      if (restart) {
+        memcpy(v, x, sizeof(double) * ps);
+        continue;
+      }
+      const double* y = h->Yb + i * ps;
+      for (int k = 0; k < ps; ++k) M[k] = v[k] + g * (x[k] - y[k]);
+      proj_stiefel(r, M, v);
+    }
+  }
+  h->gamma = restart ? 0.0 : g;
+  h->acc_k = restart ? 0 : h->acc_k + 1;
+  h->acc_ready = 0;
+  return 0;
+}
+
+double orc_pgo_accel_gamma(void* vh) { return ((orc_pgo*)vh)->gamma; }
+
 /* One RBCD round: neighbour table = iterate at round start (every robot
  * published after its previous iterate), then every active robot updates its
  * block against that table. */
 int orc_pgo_round(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
   orc_pgo* h = (orc_pgo*)vh;
+  orc_pgo_accel_pre(h, active);
   orc_pgo_refresh(h);
   for (int a = 0; a < h->R; ++a) {
     kmx_iter_stats st;
@@ -504,6 +615,7 @@ int orc_pgo_round(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
     if (active[a]) block_update(h, a, &st);
     if (stats) stats[a] = st;
   }
+  orc_pgo_accel_post(h, active);
   return 0;
 }
 
@@ -511,12 +623,14 @@ int orc_pgo_round(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
  * multi-process form, where neighbour rows arrive by exchange. */
 int orc_pgo_round_nbr(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
   orc_pgo* h = (orc_pgo*)vh;
+  orc_pgo_accel_pre(h, active); /* normally already formed before the exchange */
   for (int a = 0; a < h->R; ++a) {
     kmx_iter_stats st;
     memset(&st, 0, sizeof(st));
     if (active[a]) block_update(h, a, &st);
     if (stats) stats[a] = st;
   }
+  orc_pgo_accel_post(h, active);
   return 0;
 }
 
@@ -525,6 +639,7 @@ int orc_pgo_round_nbr(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
  * the all-cores CPU baseline of BASELINE.md §2.4. */
 int orc_pgo_round_mt(void* vh, const uint8_t* active, kmx_iter_stats* stats, int threads) {
   orc_pgo* h = (orc_pgo*)vh;
+  if (h->P.acceleration) return KMX_EUNSUP;
   orc_pgo_refresh(h);
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
   for (int a = 0; a < h->R; ++a) {

@@ -66,6 +66,9 @@ def _setup(L):
         "orc_pgo_update_weights": ([P, pf64], C.c_int),
         "orc_pgo_get_trajectory": ([P, C.c_int, pf64, pf64], C.c_int),
         "orc_pgo_eval": ([P, C.c_int, C.c_int, pf64, pf64, pf64], C.c_int),
+        "orc_pgo_accel_pre": ([P, pu8], C.c_int),
+        "orc_pgo_accel_post": ([P, pu8], C.c_int),
+        "orc_pgo_accel_gamma": ([P], f64),
     }
     for name, (a, r) in sigs.items():
         fn = getattr(L, name)
@@ -167,6 +170,19 @@ class OraclePGO:
         stats = (IterStats * self.n_robots)()
         self.L.orc_pgo_round_nbr(self.h, _u(act), stats)
         return [s.as_dict() for s in stats]
+
+    def accel_pre(self, mask=None):
+        """Form the accelerated extrapolation Y for the next round (X := Y)."""
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self.L.orc_pgo_accel_pre(self.h, None if m is None else _u(m))
+
+    def accel_post(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        self.L.orc_pgo_accel_post(self.h, None if m is None else _u(m))
+
+    @property
+    def accel_gamma(self):
+        return self.L.orc_pgo_accel_gamma(self.h)
 
     def set_nbr_rows(self, robots, poses, X):
         r = np.ascontiguousarray(robots, dtype=np.int32); p = np.ascontiguousarray(poses, dtype=np.int32)

@@ -62,6 +62,7 @@ class OracleBlockSolver:
         return np.frombuffer((C.c_int32 * n).from_address(ptr), dtype=np.int32).copy()
 
     def exchange_pack(self, slots_ptr, n, seg_ptr, n_seg, out_ptr):
+        self.o.accel_pre(self.local)  # accelerated rounds exchange Y
         ps = self._rows()
         seg = self._i32(seg_ptr, n_seg + 1) if n_seg else np.array([0, n], np.int32)
         sl = self._i32(slots_ptr, n) if n else np.zeros(0, np.int32)
@@ -93,6 +94,7 @@ class OracleBlockSolver:
         self.ext = np.array(ext)
 
     def refresh_local(self):
+        self.o.accel_pre(self.local)  # accelerated rounds publish Y
         X = self.o.get_x_rows(self.pub_robot, self.pub_pose)
         own = self.local[self.pub_robot] == 1
         self.o.set_nbr_rows(self.pub_robot[own], self.pub_pose[own], X[own])

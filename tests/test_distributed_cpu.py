@@ -18,9 +18,9 @@ def _graph():
     return make_pose_graph(4, 400, 1000, seed=2)
 
 
-def _params(rel_tol=1e-3):
+def _params(rel_tol=1e-3, accel=False):
     from kmx.dpgo.params import PGOAgentParameters
-    P = PGOAgentParameters(r=5)
+    P = PGOAgentParameters(r=5, acceleration=accel, restartInterval=4)
     P.robustOptInnerIters = 3
     P.robustOptNumWeightUpdates = 3
     P.relChangeTol = rel_tol
@@ -32,13 +32,13 @@ def _x0(g):
     return {a: lift(g.init_R[a], g.init_t[a], Y) for a in range(g.n_robots)}
 
 
-def _worker(rank, world, port, rounds, q, rel_tol):
+def _worker(rank, world, port, rounds, q, rel_tol, accel=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from kmx.dpgo.driver import RBCDDriver
     from tests.mock_solver import OracleBlockSolver
-    g, P = _graph(), _params(rel_tol)
+    g, P = _graph(), _params(rel_tol, accel)
     drv = RBCDDriver(P, g, rank=rank, world=world, solver=OracleBlockSolver(P), exchange_device="cpu")
     drv.initialize(_x0(g))
     for _ in range(rounds):
@@ -65,6 +65,7 @@ def reference_rounds(g, P, rounds):
     sched = GncSchedule.from_params(P)
     relc = np.full(g.n_robots, np.inf)
     for _ in range(rounds):
+        o.accel_pre()  # accelerated rounds: Y first (the GNC decision and the exchange see Y)
         if sched.should_update(relc):
             o.refresh()
             o.update_weights()
@@ -75,14 +76,15 @@ def reference_rounds(g, P, rounds):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,rel_tol", [(2, 1e-3), (3, 1e-3), (2, 30.0)])
-def test_gloo_ranks_match_single_process(world, rel_tol):
+@pytest.mark.parametrize("world,rel_tol,accel", [(2, 1e-3, False), (3, 1e-3, False), (2, 30.0, False),
+                                                (2, 1e-3, True)])
+def test_gloo_ranks_match_single_process(world, rel_tol, accel):
     from oracle.oracle import OraclePGO
     rounds = 9
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, rounds, q, rel_tol), daemon=True)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, rounds, q, rel_tol, accel), daemon=True)
              for r in range(world)]
     for p in procs:
         p.start()
@@ -100,7 +102,7 @@ def test_gloo_ranks_match_single_process(world, rel_tol):
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
     # single-process reference: same rounds, same GNC schedule
-    g, P = _graph(), _params(rel_tol)
+    g, P = _graph(), _params(rel_tol, accel)
     o, sched = reference_rounds(g, P, rounds)
     assert sched.updates >= 2
     assert wu == [sched.updates] * world

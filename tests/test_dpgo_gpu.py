@@ -256,3 +256,45 @@ def test_device_gnc_schedule_matches_host_rule(gpu, rel_tol):
         assert np.abs(s.status() - relc).max() <= 1e-9
     assert sched.updates == P.robustOptNumWeightUpdates or rel_tol < 1
     assert len(fired) >= 3
+
+
+@pytest.mark.parametrize("robust", [False, True])
+def test_accelerated_rounds_match_oracle(gpu, robust):
+    """Nesterov-accelerated RBCD (k_accel: Y before the round, V after it,
+    restart every restartInterval rounds) vs the oracle's orc_pgo_accel_*:
+    tCG counts equal and poses within 1e-6 every round, across two restarts
+    and (robust) two explicit GNC updates."""
+    g, P, X0 = _setup(robust=robust)
+    P.acceleration, P.restartInterval = True, 5
+    s, o = _pair(g, P, X0)
+    for it in range(12):
+        s.refresh_local()
+        sg = s.iterate()
+        so = o.iterate()
+        for a in range(g.n_robots):
+            assert sg[a]["tcg_iterations"] == so[a]["tcg_iterations"], (it, a, sg[a], so[a])
+            d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
+            assert d <= 1e-6, (it, a, d)
+        if robust and it % 4 == 3:
+            s.refresh_local()
+            o.accel_pre()
+            o.refresh()
+            assert s.update_weights() == o.update_weights()
+    assert s.memory()[0] > 0
+
+
+def test_accelerated_async_equals_sync(gpu):
+    g, P, X0 = _setup()
+    P.acceleration, P.restartInterval = True, 4
+    s1, s2 = BlockSolver(P, 0), BlockSolver(P, 0)
+    for s in (s1, s2):
+        s.set_graph_data(g)
+        for a in range(g.n_robots):
+            s.set_iterate(a, X0[a])
+    for _ in range(9):
+        s1.refresh_local()
+        s1.iterate()
+    s2.iterate_async(9, refresh_local=True)
+    s2.sync()
+    for a in range(g.n_robots):
+        assert np.array_equal(s1.get_iterate(a), s2.get_iterate(a))
