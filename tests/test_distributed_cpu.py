@@ -14,7 +14,9 @@ import torch.multiprocessing as mp
 from kmx.synth import lift, lifting_matrix, make_pose_graph
 
 
-def _graph():
+def _graph(big=False):
+    if big:  # configs[3] shape: 8 robot blocks, 100k poses, 500k edges (20 % outliers)
+        return make_pose_graph(8, 100_000, 500_000, seed=0)
     return make_pose_graph(4, 400, 1000, seed=2)
 
 
@@ -32,18 +34,18 @@ def _x0(g):
     return {a: lift(g.init_R[a], g.init_t[a], Y) for a in range(g.n_robots)}
 
 
-def _worker(rank, world, port, rounds, q, rel_tol, accel=False):
+def _worker(rank, world, port, rounds, q, rel_tol, accel=False, big=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from kmx.dpgo.driver import RBCDDriver
     from tests.mock_solver import OracleBlockSolver
-    g, P = _graph(), _params(rel_tol, accel)
+    g, P = _graph(big), _params(rel_tol, accel)
     drv = RBCDDriver(P, g, rank=rank, world=world, solver=OracleBlockSolver(P), exchange_device="cpu")
     drv.initialize(_x0(g))
     for _ in range(rounds):
         drv.step(with_stats=True)
-    q.put((rank, {a: drv.iterate_of(a) for a in drv.robots}, drv.weight_updates))
+    q.put((rank, {a: drv.iterate_of(a) for a in drv.robots}, drv.weight_updates, drv.exchange_rows))
     dist.destroy_process_group()
 
 
@@ -92,7 +94,7 @@ def test_gloo_ranks_match_single_process(world, rel_tol, accel):
     wu = []
     try:
         for _ in procs:
-            rank, X, w = q.get(timeout=240)
+            rank, X, w, _ = q.get(timeout=240)
             got.update(X)
             wu.append(w)
     finally:
@@ -106,6 +108,40 @@ def test_gloo_ranks_match_single_process(world, rel_tol, accel):
     o, sched = reference_rounds(g, P, rounds)
     assert sched.updates >= 2
     assert wu == [sched.updates] * world
+    for a in range(g.n_robots):
+        assert np.array_equal(got[a], o.get_iterate(a)), a
+
+
+@pytest.mark.timeout(600)
+def test_gloo_ws2_configs3_shape():
+    """world_size 2 on the configs[3]-shaped graph (8 blocks, 100k poses, 500k
+    edges, 4 blocks per rank, ~34k public rows each way per round) across a
+    GNC weight update: bitwise equal to the single-process team run."""
+    rounds, world = 6, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, rounds, q, 1e-3, False, True), daemon=True)
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got, wu, rows = {}, [], []
+    try:
+        for _ in procs:
+            rank, X, w, xr = q.get(timeout=500)
+            got.update(X)
+            wu.append(w)
+            rows.append(xr)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    g, P = _graph(True), _params(1e-3)
+    o, sched = reference_rounds(g, P, rounds)
+    assert sched.updates >= 1 and wu == [sched.updates] * world
+    assert all(20_000 < a < 60_000 and 20_000 < b < 60_000 for a, b in rows)
     for a in range(g.n_robots):
         assert np.array_equal(got[a], o.get_iterate(a)), a
 
