@@ -124,7 +124,10 @@ struct Dev {
   const int2* eipos;   // [mloc] record positions (tail, head) of each local edge, -1 if not local
   double *X, *Xt, *g, *r, *z, *eta, *del, *hd, *S, *Pinv, *hD, *pub;
   double* part;        // [ntiles][NPART]
+  double* part_h;      // [ntiles][2] k_hess partials (RM_CONSUMER: read by k_update)
+  double* part_u;      // [ntiles][2] k_update partials (RM_CONSUMER: read by the next k_hess)
   Ctl* ctl;
+  Ctl* ctl2;           // [L] RM_CONSUMER: the state between k_hess and k_update of a tCG step
   Counters* cnt;
   unsigned* tickets;          // [L] per-robot arrival counters (zero between launches)
   const long long* m_robot;   // [L] local-problem edges per robot
@@ -700,7 +703,19 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
 // (write-through partial stores, vmcnt drain, a returning device-scope
 // atomic) keeps its wave and LDS allocated for microseconds after its work,
 // which delays the next generation of workgroups (k_hess runs ~2 per CU slot).
-enum RedMode { RM_LAUNCH = 0, RM_TICKET = 1 };
+// RM_CONSUMER (KMX_RED=2): no reduction launch inside tCG — every workgroup of
+// k_update reduces its robot's k_hess partials itself (and every workgroup of
+// the next k_hess the k_update partials) in k_reduce's exact order and runs the
+// control step on a private copy of the robot's state; the robot's first tile
+// writes the state out, double-buffered (k_hess: ctl -> ctl2, k_update: ctl2 ->
+// ctl), so no workgroup reads a state another one of the same launch writes.
+// Two launches per tCG step instead of four, same results as RM_LAUNCH.
+// Measured on configs[3] (profiles/r02/ab_red): k_hess 41.2 us and k_update
+// 22.7 us against 32.4 + 19.8 us plus two 4.6 us k_reduce launches — the
+// per-workgroup reduction and decision add latency to every workgroup of the
+// latency-bound gather, which outweighs the saved launches (0.87-0.88 vs
+// 0.86 ms per round), so RM_LAUNCH stays the default.
+enum RedMode { RM_LAUNCH = 0, RM_TICKET = 1, RM_CONSUMER = 2 };
 
 template <int KIND, int NV, int RM, typename Store>
 __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const double* vals, char* smem_red,
@@ -713,7 +728,7 @@ __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const d
     if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
   }
   __syncthreads();
-  if constexpr (RM == RM_LAUNCH) {
+  if constexpr (RM == RM_LAUNCH || (RM == RM_CONSUMER && KIND != RED_HESS && KIND != RED_UPDATE)) {
     if (threadIdx.x == 0) {
 #pragma unroll
       for (int s = 0; s < NV; ++s) {
@@ -721,6 +736,20 @@ __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const d
 #pragma unroll
         for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
         d.part[(size_t)L.tile * NPART + s] = t;
+      }
+    }
+    store();
+    return;
+  } else if constexpr (RM == RM_CONSUMER) {  // RED_HESS / RED_UPDATE: 2-wide partials for the consumer launch
+    static_assert(NV <= 2, "consumer partials");
+    if (threadIdx.x == 0) {
+      double* dst = (KIND == RED_HESS ? d.part_h : d.part_u) + (size_t)L.tile * 2;
+#pragma unroll
+      for (int s = 0; s < NV; ++s) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
+        dst[s] = t;
       }
     }
     store();
@@ -820,8 +849,60 @@ __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const d
   }
 }
 
-__device__ void control(const Dev& d, int l, int kind, const double* tot, int R_) {
-  Ctl& c = d.ctl[l];
+// The tCG decisions after the Hess-vec and after the update, shared by
+// control_on and by RM_CONSUMER's workgroups (which evaluate them from the
+// robot's state without a copy of it); contraction off so every call site
+// rounds alike.
+struct HessStep {
+  double alpha, e_Pe_new, coef;
+  int boundary, stop;
+};
+__device__ __forceinline__ HessStep hess_step(double z_r, double e_Pe, double e_Pd, double d_Pd, double Delta,
+                                              double d_Hd) {
+#pragma clang fp contract(off)
+  HessStep h;
+  h.alpha = z_r / d_Hd;
+  h.e_Pe_new = e_Pe + 2.0 * h.alpha * e_Pd + h.alpha * h.alpha * d_Pd;
+  const double D2 = Delta * Delta;
+  h.boundary = (d_Hd <= 0.0 || h.e_Pe_new >= D2) ? 1 : 0;
+  h.stop = d_Hd <= 0.0 ? KMX_TCG_NEGATIVE_CURVATURE : KMX_TCG_EXCEEDED_TR;
+  h.coef = h.boundary ? (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (D2 - e_Pe))) / d_Pd : h.alpha;
+  return h;
+}
+struct UpdStep {
+  int done, stop;
+  double beta;
+};
+__device__ __forceinline__ UpdStep upd_step(int mode, double norm_r0, double z_r, int tcg_iter, double rr,
+                                            double zr_new, const Params& P) {
+#pragma clang fp contract(off)
+  UpdStep u;
+  u.done = 0;
+  u.stop = KMX_TCG_MAX_ITER;
+  u.beta = 0.0;
+  if (mode == MODE_BOUNDARY) {
+    u.done = 1;
+    u.stop = -1;  // keep the boundary reason
+    return u;
+  }
+  const double norm_r = sqrt(rr);
+  const double pw = pow(norm_r0, P.theta);
+  if (norm_r <= norm_r0 * fmin(pw, P.kappa)) {
+    u.done = 1;
+    u.stop = (P.kappa < pw) ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
+  } else if (tcg_iter >= P.tcg_max) {
+    u.done = 1;
+    u.stop = KMX_TCG_MAX_ITER;
+  } else {
+    u.beta = zr_new / z_r;
+  }
+  return u;
+}
+
+// The RTR / tCG scalar logic of robot l after a reduction of `kind`, applied
+// to c. `side`: perform the side effects (team status, counters) — exactly one
+// caller per robot and reduction does.
+__device__ void control_on(Ctl& c, const Dev& d, int l, int kind, const double* tot, int R_, bool side) {
   const Params& P = d.p;
   if (kind == RED_GRAD) {
     const double f = tot[0], gn = sqrt(tot[1]);
@@ -835,8 +916,7 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
       c.tcg_iter = 0;
       c.accepted = 0;
       c.skipped = 1;
-      if (c.rtr_iter == 0) d.relc[l] = 0.0;
-      else d.relc[l] = c.rel_change;
+      if (side) d.relc[l] = (c.rtr_iter == 0) ? 0.0 : c.rel_change;
     } else {
       c.phase = PH_TCG;
       c.tcg_iter = 0;
@@ -847,47 +927,38 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
       c.e_Pe = 0.0;
       c.beta = 0.0;
       c.tcg_stop = KMX_TCG_MAX_ITER;
-      if (c.rtr_iter == 0) {
+      if (side && c.rtr_iter == 0) {
         atomicAdd(&d.cnt->edges_iters, (unsigned long long)d.m_robot[l]);
         atomicAdd(&d.cnt->block_updates, 1ull);
       }
     }
   } else if (kind == RED_HESS) {
     const double d_Hd = tot[0];
-    const double alpha = c.z_r / d_Hd;
-    const double e_Pe_new = c.e_Pe + 2.0 * alpha * c.e_Pd + alpha * alpha * c.d_Pd;
-    const double D2 = c.Delta * c.Delta;
+    const HessStep hs = hess_step(c.z_r, c.e_Pe, c.e_Pd, c.d_Pd, c.Delta, d_Hd);
     c.tcg_iter += 1;
     c.hessvecs += 1;
-    atomicAdd(&d.cnt->hessvecs, 1ull);
-    atomicAdd(&d.cnt->hess_alg_bytes, 128.0 * (double)d.m_robot[l] + 2.0 * 8.0 * R_ * 4.0 * (double)d.n_robot[l]);
-    if (d_Hd <= 0.0 || e_Pe_new >= D2) {
-      const double tau = (-c.e_Pd + sqrt(c.e_Pd * c.e_Pd + c.d_Pd * (D2 - c.e_Pe))) / c.d_Pd;
-      c.coef = tau;
+    if (side) {
+      atomicAdd(&d.cnt->hessvecs, 1ull);
+      atomicAdd(&d.cnt->hess_alg_bytes, 128.0 * (double)d.m_robot[l] + 2.0 * 8.0 * R_ * 4.0 * (double)d.n_robot[l]);
+    }
+    if (hs.boundary) {
+      c.coef = hs.coef;
       c.mode = MODE_BOUNDARY;
-      c.tcg_stop = d_Hd <= 0.0 ? KMX_TCG_NEGATIVE_CURVATURE : KMX_TCG_EXCEEDED_TR;
+      c.tcg_stop = hs.stop;
     } else {
-      c.alpha = alpha;
-      c.coef = alpha;
-      c.e_Pe = e_Pe_new;
+      c.alpha = hs.alpha;
+      c.coef = hs.coef;
+      c.e_Pe = hs.e_Pe_new;
       c.mode = MODE_INTERIOR;
     }
   } else if (kind == RED_UPDATE) {
-    if (c.mode == MODE_BOUNDARY) {
-      c.phase = PH_STEP;
-      return;
-    }
-    const double norm_r = sqrt(tot[0]);
     const double zr_new = tot[1];
-    const double pw = pow(c.norm_r0, P.theta);
-    if (norm_r <= c.norm_r0 * fmin(pw, P.kappa)) {
-      c.tcg_stop = (P.kappa < pw) ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
-      c.phase = PH_STEP;
-    } else if (c.tcg_iter >= P.tcg_max) {
-      c.tcg_stop = KMX_TCG_MAX_ITER;
+    const UpdStep u = upd_step(c.mode, c.norm_r0, c.z_r, c.tcg_iter, tot[0], zr_new, P);
+    if (u.done) {
+      if (u.stop >= 0) c.tcg_stop = u.stop;
       c.phase = PH_STEP;
     } else {
-      const double beta = zr_new / c.z_r;
+      const double beta = u.beta;
       c.e_Pd = beta * (c.e_Pd + c.alpha * c.d_Pd);
       c.d_Pd = zr_new + beta * beta * c.d_Pd;
       c.z_r = zr_new;
@@ -914,16 +985,125 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
     c.rtr_iter += 1;
     c.phase = (c.rtr_iter < P.rtr_iters) ? PH_START : PH_IDLE;
     c.rel_change = sqrt(c.chg_acc / (double)d.n_robot[l]);
-    if (c.phase == PH_IDLE) d.relc[l] = c.rel_change;  // the team status of dpgo's getStatus
+    if (side && c.phase == PH_IDLE) d.relc[l] = c.rel_change;  // the team status of dpgo's getStatus
   }
+}
+__device__ void control(const Dev& d, int l, int kind, const double* tot, int R_) {
+  control_on(d.ctl[l], d, l, kind, tot, R_, true);
 }
 
 // RM_LAUNCH: one workgroup per robot reduces the robot's tile partials in
 // tile order and runs the control logic (after k_update it also reports the
 // robot's tCG progress to the host).
 constexpr int RBLOCK = 256;  // k_reduce: one workgroup per robot (1024 threads measured slower: 6.3 vs 4.6 us)
+static_assert(RBLOCK == BLOCK, "robot_sum runs in k_reduce and in the tCG kernels");
+// Sum of NS partials (row stride `stride`) over tiles [t0, t1) of a robot by
+// the whole workgroup: two tiles per thread in flight (512 tiles, ~24k poses
+// per robot, in one round trip), tile order within a thread, then the wave
+// sums and the 4 waves in order; every thread gets the totals. The one order
+// used by k_reduce and by RM_CONSUMER's tCG kernels. lds: >= NS * 4 doubles.
+template <int NS>
+__device__ __forceinline__ void robot_sum(const double* part, int stride, int t0, int t1, double* lds,
+                                          double tot[NPART]) {
+  constexpr int RW_ = RBLOCK / 64;
+  double v[NPART] = {0.0, 0.0, 0.0, 0.0};
+  for (int tb = t0; tb < t1; tb += 2 * RBLOCK) {
+    double a[2][NS];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = min(tb + (int)threadIdx.x + u * RBLOCK, t1 - 1);
+      if constexpr (NS == 4) {
+        const double2* p2 = reinterpret_cast<const double2*>(part + (size_t)t * stride);
+        const double2 x = p2[0], y = p2[1];
+        a[u][0] = x.x; a[u][1] = x.y; a[u][NS - 2] = y.x; a[u][NS - 1] = y.y;
+      } else {
+        const double2 x = *reinterpret_cast<const double2*>(part + (size_t)t * stride);
+        a[u][0] = x.x;
+        if constexpr (NS > 1) a[u][NS - 1] = x.y;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (tb + (int)threadIdx.x + u * RBLOCK < t1) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) v[k] += a[u][k];
+      }
+  }
+  __syncthreads();  // lds may still be read by an earlier user
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const double w = wave_sum(v[k]);
+    if ((threadIdx.x & 63) == 0) lds[k * RW_ + (threadIdx.x >> 6)] = w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NPART; ++k) {
+    double acc = 0.0;
+    if (k < NS) {
+#pragma unroll
+      for (int w = 0; w < RW_; ++w) acc += lds[k * RW_ + w];
+    }
+    tot[k] = acc;
+  }
+}
+
+// robot_sum in two halves, so the partial loads can be in flight during other
+// work: issue() loads a robot's <= 2 * RBLOCK tiles into registers (larger
+// robots fall back to robot_sum in finish()); finish() adds them in
+// robot_sum's order.
+template <int NS>
+struct RobotSum {
+  double a[2][NS];
+  int t0, t1;
+  __device__ __forceinline__ void issue(const double* part, int stride, int t0_, int t1_) {
+    t0 = t0_;
+    t1 = t1_;
+    if (t1 - t0 > 2 * RBLOCK) return;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = min(t0 + (int)threadIdx.x + u * RBLOCK, t1 - 1);
+      const double2 x = *reinterpret_cast<const double2*>(part + (size_t)t * stride);
+      a[u][0] = x.x;
+      if constexpr (NS > 1) a[u][NS - 1] = x.y;
+    }
+  }
+  __device__ __forceinline__ void finish(const double* part, int stride, double* lds, double tot[NPART]) {
+    static_assert(NS <= 2, "2-wide partials");
+    if (t1 - t0 > 2 * RBLOCK) {
+      robot_sum<NS>(part, stride, t0, t1, lds, tot);
+      return;
+    }
+    constexpr int RW_ = RBLOCK / 64;
+    double v[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) v[k] = 0.0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (t0 + (int)threadIdx.x + u * RBLOCK < t1) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) v[k] += a[u][k];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const double w = wave_sum(v[k]);
+      if ((threadIdx.x & 63) == 0) lds[k * RW_ + (threadIdx.x >> 6)] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NPART; ++k) {
+      double acc = 0.0;
+      if (k < NS) {
+#pragma unroll
+        for (int w = 0; w < RW_; ++w) acc += lds[k * RW_ + w];
+      }
+      tot[k] = acc;
+    }
+  }
+};
+
 __global__ __launch_bounds__(RBLOCK) void k_reduce(Dev d, int kind, int R_, HostStatus* hs, unsigned long long seq,
-                                                  int slot) {
+                                                  int slot, const double* src) {
   constexpr int RW_ = RBLOCK / 64;
   __shared__ double lds[NPART * RW_];
   const int l = blockIdx.x;
@@ -937,40 +1117,12 @@ __global__ __launch_bounds__(RBLOCK) void k_reduce(Dev d, int kind, int R_, Host
     return;
   }
   const int ns = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
-  const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
-  // the robot's tile partials, two per thread in flight (512 tiles, ~24k
-  // poses per robot, in one round trip), in tile order within each thread
-  double v[NPART] = {0.0, 0.0, 0.0, 0.0};
-  for (int tb = t0; tb < t1; tb += 2 * RBLOCK) {
-    double2 a[2], b[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int t = min(tb + (int)threadIdx.x + u * RBLOCK, t1 - 1);
-      const double2* p2 = reinterpret_cast<const double2*>(d.part + (size_t)t * NPART);
-      a[u] = p2[0];
-      b[u] = p2[1];
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      if (tb + (int)threadIdx.x + u * RBLOCK < t1) {
-        v[0] += a[u].x; v[1] += a[u].y; v[2] += b[u].x; v[3] += b[u].y;
-      }
-  }
-#pragma unroll
-  for (int s = 0; s < NPART; ++s) {
-    const double w = wave_sum(v[s]);
-    if ((threadIdx.x & 63) == 0) lds[s * RW_ + (threadIdx.x >> 6)] = w;
-  }
-  __syncthreads();
+  double tot[NPART];
+  if (src) robot_sum<2>(src, 2, d.rtile0[l], d.rtile0[l + 1], lds, tot);  // RM_CONSUMER's 2-wide partials
+  else robot_sum<NPART>(d.part, NPART, d.rtile0[l], d.rtile0[l + 1], lds, tot);
   if (threadIdx.x == 0) {
-    double tot[NPART];
 #pragma unroll
-    for (int s = 0; s < NPART; ++s) {
-      double acc = 0.0;
-#pragma unroll
-      for (int w = 0; w < RW_; ++w) acc += lds[s * RW_ + w];
-      tot[s] = s < ns ? acc : 0.0;
-    }
+    for (int s = 0; s < NPART; ++s) tot[s] = s < ns ? tot[s] : 0.0;
     control(d, l, kind, tot, R_);
     if (kind == RED_HESS && slot >= 0) atomicAdd(d.hv_launch + slot, 1);
     if (hs) post_status(hs, l, seq, d.ctl[l].phase == PH_TCG);
@@ -1025,16 +1177,59 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d) {
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old;
 // partial <delta, Hdelta>.
 template <int R, int RW, int RM>
-__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot) {
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostStatus* hs, unsigned long long seq) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
-  const Ctl& c = d.ctl[L.l];
-  if (c.phase != PH_TCG) return;
-  const bool first = (c.tcg_iter == 0);
-  const double beta = c.beta;
+  int tcg_iter;
+  double beta;
   double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4], S[9];
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-  hinc_gather<R, RW>(d, L, d.z, H, smem);
+  if constexpr (RM == RM_CONSUMER) {
+    // the previous step's k_update partials give this robot's control step
+    // after the update (stop test, beta); it runs on a private copy after the
+    // gather (speculative: a robot whose tCG stops here discards it), so the
+    // partial loads are in flight with the gather's first records. The robot's
+    // first tile writes the state to ctl2 for k_update and reports tCG
+    // progress to the host.
+    __shared__ Ctl cs;
+    __shared__ double rl[NPART * WAVES];
+    const Ctl& c0 = d.ctl[L.l];
+    const bool writer = L.tile == d.rtile0[L.l];
+    if (c0.phase != PH_TCG) {  // uniform: a tile never straddles robots
+      if (writer && threadIdx.x == 0) {
+        d.ctl2[L.l] = c0;
+        if (hs) post_status(hs, L.l, seq, false);
+      }
+      return;
+    }
+    const bool upd = c0.tcg_iter > 0;
+    RobotSum<2> rs;
+    if (upd) rs.issue(d.part_u, 2, d.rtile0[L.l], d.rtile0[L.l + 1]);
+    hinc_gather<R, RW>(d, L, d.z, H, smem);
+    double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+    if (upd) rs.finish(d.part_u, 2, rl, tot);
+    // every thread evaluates the decision; the first tile's thread 0 also
+    // updates the robot's state (on an LDS copy: a private one would live in
+    // scratch) and publishes it
+    UpdStep u{0, 0, 0.0};
+    if (upd) u = upd_step(c0.mode, c0.norm_r0, c0.z_r, c0.tcg_iter, tot[0], tot[1], d.p);
+    if (writer && threadIdx.x == 0) {
+      cs = c0;
+      if (upd) control_on(cs, d, L.l, RED_UPDATE, tot, R, true);
+      d.ctl2[L.l] = cs;
+      if (hs) post_status(hs, L.l, seq, cs.phase == PH_TCG);
+    }
+    if (u.done) return;
+    tcg_iter = c0.tcg_iter;
+    beta = u.beta;
+  } else {
+    const Ctl& c = d.ctl[L.l];
+    if (c.phase != PH_TCG) return;
+    tcg_iter = c.tcg_iter;
+    beta = c.beta;
+    hinc_gather<R, RW>(d, L, d.z, H, smem);
+  }
+  const bool first = (tcg_iter == 0);
   asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
   if (L.valid) {
     load4(d.z + o, zs);
@@ -1079,31 +1274,73 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot) {
 // tCG step, part 2: eta += coef delta, r += coef Hdelta; interior steps also
 // z = precon(r) and partials <r,r>, <z,r>.
 template <int R, int RM>
-__global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq) {
+__global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq, int slot) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
-  const Ctl& c = d.ctl[L.l];
-  if (c.phase != PH_TCG) {  // not in tCG: the robot's first tile reports it
-    if (hs && threadIdx.x == 0 && L.tile == d.rtile0[L.l]) post_status(hs, L.l, seq, false);
-    return;
-  }
-  const bool first = (c.tcg_iter == 1);
-  const double coef = c.coef;
-  const bool interior = (c.mode == MODE_INTERIOR);
+  int tcg_iter, mode;
+  double coef;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-  double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0};
+  double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0},
+         hdl[4] = {0, 0, 0, 0};
+  if constexpr (RM == RM_CONSUMER) {
+    // this step's k_hess partials: the control step after the Hess-vec (alpha
+    // or the boundary tau) on a private copy, with the step's vector loads in
+    // flight; the first tile writes the robot's state back to ctl
+    __shared__ Ctl cs;
+    __shared__ double rl[NPART * WAVES];
+    const Ctl& cq = d.ctl2[L.l];
+    const bool writer = L.tile == d.rtile0[L.l];
+    if (cq.phase != PH_TCG) {
+      if (writer && threadIdx.x == 0) d.ctl[L.l] = cq;
+      return;
+    }
+    const bool first0 = cq.tcg_iter == 0;  // the control step makes it 1
+    RobotSum<1> rs;
+    rs.issue(d.part_h, 2, d.rtile0[L.l], d.rtile0[L.l + 1]);
+    if (L.valid) {
+      load4(d.del + o, dl);
+      load4(d.hd + o, hdl);
+      load4((first0 ? d.g : d.r) + o, rr);
+      if (!first0) load4(d.eta + o, et);
+      load4(d.X + o, y);  // used by the precon of interior steps (boundary steps are rare)
+    }
+    double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+    rs.finish(d.part_h, 2, rl, tot);
+    const HessStep hsx = hess_step(cq.z_r, cq.e_Pe, cq.e_Pd, cq.d_Pd, cq.Delta, tot[0]);
+    if (writer && threadIdx.x == 0) {  // the state update, on an LDS copy
+      cs = cq;
+      control_on(cs, d, L.l, RED_HESS, tot, R, true);
+      d.ctl[L.l] = cs;
+      if (slot >= 0) atomicAdd(d.hv_launch + slot, 1);
+    }
+    tcg_iter = cq.tcg_iter + 1;
+    mode = hsx.boundary ? MODE_BOUNDARY : MODE_INTERIOR;
+    coef = hsx.coef;
+  } else {
+    const Ctl& c = d.ctl[L.l];
+    if (c.phase != PH_TCG) {  // not in tCG: the robot's first tile reports it
+      if (hs && threadIdx.x == 0 && L.tile == d.rtile0[L.l]) post_status(hs, L.l, seq, false);
+      return;
+    }
+    tcg_iter = c.tcg_iter;
+    mode = c.mode;
+    coef = c.coef;
+    if (L.valid) {
+      load4(d.del + o, dl);
+      load4(d.hd + o, hdl);
+      load4((tcg_iter == 1 ? d.g : d.r) + o, rr);  // r_0 = g (k_grad does not store r)
+      if (tcg_iter != 1) load4(d.eta + o, et);
+      if (c.mode == MODE_INTERIOR) load4(d.X + o, y);
+    }
+  }
+  const bool interior = (mode == MODE_INTERIOR);
+  (void)tcg_iter;
   if (L.valid) {
-    double dl[4], hdl[4];
-    load4(d.del + o, dl);
-    load4(d.hd + o, hdl);
-    load4((first ? d.g : d.r) + o, rr);  // r_0 = g (k_grad does not store r)
-    if (!first) load4(d.eta + o, et);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       et[k] += coef * dl[k];
       rr[k] += coef * hdl[k];
     }
-    if (interior) load4(d.X + o, y);
   }
   double vals[2] = {0.0, 0.0}, zr[4] = {0, 0, 0, 0};
   if (interior) {  // uniform per robot
@@ -1701,6 +1938,8 @@ struct kmx_pgo {
   double* d_vec = nullptr;  // X Xt g r z eta del hd
   double *d_S = nullptr, *d_Pinv = nullptr, *d_hD = nullptr, *d_pub = nullptr, *d_part = nullptr;
   Ctl* d_ctl = nullptr;
+  Ctl* d_ctl2 = nullptr;
+  double *d_part_h = nullptr, *d_part_u = nullptr;
   Counters* d_cnt = nullptr;
   unsigned* d_tickets = nullptr;
   long long* d_m_robot = nullptr;
@@ -1724,7 +1963,7 @@ struct kmx_pgo {
   int hstat_cap = 0;
   unsigned long long seq = 0;
   bool poll = true;          // KMX_POLL=0: enqueue every tCG step (finished robots exit at once)
-  int rm = RM_LAUNCH;        // KMX_RED=1: reductions behind tickets in the producing launch (measured slower)
+  int rm = RM_LAUNCH;        // KMX_RED=1: tickets in the producing launch; 2: consumer-side reductions (both measured slower)
   bool poll_timeout = false;
   // timing
   bool timing = false;
@@ -1759,7 +1998,8 @@ void free_dev(kmx_pgo* h) {
                   h->d_ctl, h->d_cnt, h->d_tickets, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
-                  h->d_rgroup0, h->d_gtickets, h->d_gpart, h->d_accV, h->d_accY};
+                  h->d_rgroup0, h->d_gtickets, h->d_gpart, h->d_accV, h->d_accY, h->d_ctl2, h->d_part_h,
+                  h->d_part_u};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
@@ -1785,6 +2025,8 @@ void free_dev(kmx_pgo* h) {
   h->d_gtickets = nullptr;
   h->d_gpart = nullptr;
   h->d_accV = h->d_accY = nullptr;
+  h->d_ctl2 = nullptr;
+  h->d_part_h = h->d_part_u = nullptr;
 }
 
 hipEvent_t next_event(kmx_pgo* h) {
@@ -1894,9 +2136,10 @@ bool wait_running(kmx_pgo* h, unsigned long long seq) {
 template <int R, int RW, int RM>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   const dim3 grid(h->ntiles), blk(BLOCK);
-  auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0, int slot = -1) {
-    if (RM == RM_LAUNCH)
-      hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot);
+  auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0, int slot = -1,
+                 const double* src = nullptr) {
+    if (RM != RM_TICKET)
+      hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot, src);
   };
   enqueue_begin(h, d_active, BEGIN_ROUND);
   for (int it = 0; it < h->P.rtr_iterations; ++it) {
@@ -1914,20 +2157,30 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
         e1 = next_event(h);
         (void)hipEventRecord(e0, h->stream);
       }
-      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot);
-      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
-      red(RED_HESS, nullptr, 0, slot);
       const bool poll = h->poll && h->hstat;
       const unsigned long long seq = poll ? ++h->seq : 0;
       HostStatus* hs = poll ? h->hstat : nullptr;
+      if constexpr (RM == RM_CONSUMER) {
+        // k_hess reports the stop test of the previous step's update
+        hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, hs, seq);
+        if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+        hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, 0ull, slot);
+        if (poll && j > 0 && !wait_running(h, seq)) break;
+        continue;
+      }
+      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, nullptr, 0ull);
+      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+      red(RED_HESS, nullptr, 0, slot);
       hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv,
-                         RM == RM_TICKET ? hs : nullptr, seq);
+                         RM == RM_TICKET ? hs : nullptr, seq, -1);
       red(RED_UPDATE, hs, seq);
       if (poll) {
         if (j > 0 && !wait_running(h, prev)) break;
         prev = seq;
       }
     }
+    // RM_CONSUMER: the last step's update has no k_hess after it
+    if (RM == RM_CONSUMER) red(RED_UPDATE, nullptr, 0, -1, h->dv.part_u);
     hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv);
     hipLaunchKernelGGL((k_cost<R, RW, RM>), grid, blk, SmemC<R>::bytes, h->stream, h->dv);
     red(RED_COST);
@@ -1937,7 +2190,10 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
 
 template <int R>
 void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
-  if (h->rm == RM_TICKET) {
+  if (h->rm == RM_CONSUMER) {
+    if (h->rw == 12) enqueue_round_t<R, 12, RM_CONSUMER>(h, d_active);
+    else enqueue_round_t<R, 16, RM_CONSUMER>(h, d_active);
+  } else if (h->rm == RM_TICKET) {
     if (h->rw == 12) enqueue_round_t<R, 12, RM_TICKET>(h, d_active);
     else enqueue_round_t<R, 16, RM_TICKET>(h, d_active);
   } else {
@@ -2040,7 +2296,10 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   }
   h->own_stream = true;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
-  if (const char* v = std::getenv("KMX_RED")) h->rm = std::atoi(v) ? RM_TICKET : RM_LAUNCH;
+  if (const char* v = std::getenv("KMX_RED")) {
+    const int m = std::atoi(v);
+    h->rm = m == 0 ? RM_LAUNCH : m == 1 ? RM_TICKET : RM_CONSUMER;
+  }
   *out = h;
   return KMX_OK;
   KMX_GUARD_END
@@ -2300,6 +2559,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_pub, (size_t)std::max<int64_t>(h->npub, 1) * ps)) ||
       (h->P.acceleration && ((rc = dalloc(&h->d_accV, vec)) || (rc = dalloc(&h->d_accY, vec)))) ||
       (rc = dalloc(&h->d_part, (size_t)h->ntiles * NPART)) || (rc = dalloc(&h->d_ctl, L)) ||
+      (rc = dalloc(&h->d_ctl2, L)) || (rc = dalloc(&h->d_part_h, (size_t)h->ntiles * 2)) ||
+      (rc = dalloc(&h->d_part_u, (size_t)h->ntiles * 2)) ||
       (rc = dalloc(&h->d_cnt, 1)) || (rc = dalloc(&h->d_tickets, L)) || (rc = dalloc(&h->d_m_robot, L)) ||
       (rc = dalloc(&h->d_n_robot, L)) || (rc = dalloc(&h->d_pub_src, pub_src.size())) ||
       (rc = dalloc(&h->d_own_src, own_src.size())) || (rc = dalloc(&h->d_pose_slot, pose_slot.size())) ||
@@ -2385,6 +2646,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   d.z = h->d_vec + 4 * vec; d.eta = h->d_vec + 5 * vec; d.del = h->d_vec + 6 * vec; d.hd = h->d_vec + 7 * vec;
   d.S = h->d_S; d.Pinv = h->d_Pinv; d.hD = h->d_hD; d.pub = h->d_pub; d.part = h->d_part;
   d.ctl = h->d_ctl; d.cnt = h->d_cnt; d.tickets = h->d_tickets;
+  d.ctl2 = h->d_ctl2; d.part_h = h->d_part_h; d.part_u = h->d_part_u;
   d.m_robot = h->d_m_robot; d.n_robot = h->d_n_robot; d.pose_slot = h->d_pose_slot;
   d.relc = h->d_relc; d.gnc = h->d_gnc; d.gnc_next = h->d_gnc + 1;
   d.gnc_edge = h->d_gnc_edge; d.gnc_ends = h->d_gnc_ends; d.n_gnc = h->n_gnc;
