@@ -1963,6 +1963,11 @@ struct kmx_pgo {
   int hstat_cap = 0;
   unsigned long long seq = 0;
   bool poll = true;          // KMX_POLL=0: enqueue every tCG step (finished robots exit at once)
+  // KMX_QUERY=1: hipStreamQuery before the status spin. Measured: the query
+  // puts a ~5 us bubble before the next tCG step's first kernel (profiles/r02/
+  // ab_query: 0.836 vs 0.863 ms per round; wall = busy without it), and
+  // launches reach the hardware queue without it
+  bool query = false;
   int rm = RM_LAUNCH;        // KMX_RED=1: tickets in the producing launch; 2: consumer-side reductions (both measured slower)
   bool poll_timeout = false;
   // timing
@@ -2115,7 +2120,7 @@ void enqueue_begin(kmx_pgo* h, const unsigned char* d_active, int mode) {
 // the handle to blind enqueueing (every tCG step launched).
 bool wait_running(kmx_pgo* h, unsigned long long seq) {
   volatile HostStatus* hs = h->hstat;
-  (void)hipStreamQuery(h->stream);  // make sure queued work is submitted
+  if (h->query) (void)hipStreamQuery(h->stream);  // KMX_QUERY=1: force submission before spinning
   const auto t0 = std::chrono::steady_clock::now();
   bool running = false;
   for (int l = 0; l < h->dv.L; ++l) {
@@ -2296,6 +2301,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   }
   h->own_stream = true;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
+  if (const char* v = std::getenv("KMX_QUERY")) h->query = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);
     h->rm = m == 0 ? RM_LAUNCH : m == 1 ? RM_TICKET : RM_CONSUMER;
