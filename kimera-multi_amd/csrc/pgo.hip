@@ -1181,7 +1181,7 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
   int tcg_iter;
-  double beta;
+  double beta, pcoef;  // pcoef: the previous step's eta coefficient (alpha or tau)
   double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4], S[9];
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   if constexpr (RM == RM_CONSUMER) {
@@ -1222,11 +1222,13 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
     if (u.done) return;
     tcg_iter = c0.tcg_iter;
     beta = u.beta;
+    pcoef = c0.coef;
   } else {
     const Ctl& c = d.ctl[L.l];
     if (c.phase != PH_TCG) return;
     tcg_iter = c.tcg_iter;
     beta = c.beta;
+    pcoef = c.coef;
     hinc_gather<R, RW>(d, L, d.z, H, smem);
   }
   const bool first = (tcg_iter == 0);
@@ -1244,7 +1246,7 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
   double hz[4];
   group_rhess<R, true>(y, zs, H, S, L.base, hz, reinterpret_cast<double*>(smem));
   double v = 0.0;
-  double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
+  double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0};
   if (L.valid) {
     if (first) {
 #pragma unroll
@@ -1253,10 +1255,12 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
       double dold[4], hold[4];
       load4(d.del + o, dold);
       load4(d.hd + o, hold);
+      if (tcg_iter > 1) load4(d.eta + o, et);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         dl[k] = -zs[k] + beta * dold[k];
         hdl[k] = -hz[k] + beta * hold[k];
+        et[k] += pcoef * dold[k];  // the previous step's eta update, deferred from k_update
       }
     }
     v = dl[0] * hdl[0] + dl[1] * hdl[1] + dl[2] * hdl[2] + dl[3] * hdl[3];
@@ -1267,11 +1271,13 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
     if (L.valid) {
       store4(d.del + o, dl);
       store4(d.hd + o, hdl);
+      if (!first) store4(d.eta + o, et);
     }
   }, po);
 }
 
-// tCG step, part 2: eta += coef delta, r += coef Hdelta; interior steps also
+// tCG step, part 2: r += coef Hdelta (eta += coef delta is deferred to the next
+// k_hess, which reads delta anyway, or to k_retract); interior steps also
 // z = precon(r) and partials <r,r>, <z,r>.
 template <int R, int RM>
 __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq, int slot) {
@@ -1280,8 +1286,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
   int tcg_iter, mode;
   double coef;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-  double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0},
-         hdl[4] = {0, 0, 0, 0};
+  double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
   if constexpr (RM == RM_CONSUMER) {
     // this step's k_hess partials: the control step after the Hess-vec (alpha
     // or the boundary tau) on a private copy, with the step's vector loads in
@@ -1298,10 +1303,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
     RobotSum<1> rs;
     rs.issue(d.part_h, 2, d.rtile0[L.l], d.rtile0[L.l + 1]);
     if (L.valid) {
-      load4(d.del + o, dl);
       load4(d.hd + o, hdl);
       load4((first0 ? d.g : d.r) + o, rr);
-      if (!first0) load4(d.eta + o, et);
       load4(d.X + o, y);  // used by the precon of interior steps (boundary steps are rare)
     }
     double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
@@ -1326,10 +1329,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
     mode = c.mode;
     coef = c.coef;
     if (L.valid) {
-      load4(d.del + o, dl);
       load4(d.hd + o, hdl);
       load4((tcg_iter == 1 ? d.g : d.r) + o, rr);  // r_0 = g (k_grad does not store r)
-      if (tcg_iter != 1) load4(d.eta + o, et);
       if (c.mode == MODE_INTERIOR) load4(d.X + o, y);
     }
   }
@@ -1337,10 +1338,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
   (void)tcg_iter;
   if (L.valid) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      et[k] += coef * dl[k];
-      rr[k] += coef * hdl[k];
-    }
+    for (int k = 0; k < 4; ++k) rr[k] += coef * hdl[k];
   }
   double vals[2] = {0.0, 0.0}, zr[4] = {0, 0, 0, 0};
   if (interior) {  // uniform per robot
@@ -1355,7 +1353,6 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
   po.seq = seq;
   finish_tile<RED_UPDATE, 2, RM>(d, L, vals, smem + SmemU::red_off, R, [&]() {
     if (L.valid) {
-      store4(d.eta + o, et);
       store4(d.r + o, rr);
       if (interior) store4(d.z + o, zr);
     }
@@ -1368,14 +1365,19 @@ template <int R>
 __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
-  if (d.ctl[L.l].phase != PH_STEP) return;
+  const Ctl& c = d.ctl[L.l];
+  if (c.phase != PH_STEP) return;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-  double x[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0}, gg[4] = {0, 0, 0, 0}, rr[4] = {0, 0, 0, 0};
-  if (L.valid) {  // all four rows in flight before the Gram-Schmidt chain
+  double x[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0}, gg[4] = {0, 0, 0, 0}, rr[4] = {0, 0, 0, 0}, dl[4];
+  if (L.valid) {  // all rows in flight before the Gram-Schmidt chain
     load4(d.X + o, x);
-    load4(d.eta + o, et);
+    if (c.tcg_iter > 1) load4(d.eta + o, et);  // eta after the last step's update is eta + coef delta
+    load4(d.del + o, dl);
     load4(d.g + o, gg);
     load4(d.r + o, rr);
+    const double coef = c.coef;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) et[k] += coef * dl[k];
   }
   double xt[4];
   group_retract<R>(x, et, L.base, xt);
