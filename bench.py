@@ -287,8 +287,12 @@ def bow_leg(args, rank, world, barrier_sync):
     return out, cpu
 
 
-def load_traffic():
-    f = ROOT / "profiles" / "hessvec_traffic.json"
+def load_traffic(config="synth100k"):
+    """PMC traffic of k_hess measured for this config (scripts/gpu_pmc_hess.sh ->
+    scripts/hess_traffic.py); None when that config was not profiled."""
+    f = ROOT / "profiles" / f"hessvec_traffic_{config}.json"
+    if not f.exists() and config == "synth100k":
+        f = ROOT / "profiles" / "hessvec_traffic.json"
     if f.exists():
         try:
             return json.loads(f.read_text())
@@ -409,7 +413,7 @@ def main():
     hv_ms, hv_bytes, hv_n = leg["hv"]
     value = edges_iters / el
     achieved = hv_bytes / (hv_ms * 1e-3) if hv_ms > 0 else 0.0
-    traffic = load_traffic()
+    traffic = load_traffic(args.config)
     ps_bytes = 8 * 4 * P.r
     w0 = args.burn_in + args.warmup
     if headline == "weak" and world > 1:

@@ -1,4 +1,4 @@
-# usage: bash scripts/gpu_pmc_hess.sh [tag] — HBM traffic of the dpgo kernels:
+# usage: bash scripts/gpu_pmc_hess.sh [tag] [config] — HBM traffic of the dpgo kernels:
 # separate rocprofv3 --pmc passes (kernel trace only) over `bench.py --profile` (burn-in 40 +
 # 10 rounds, every round evented), so every profiled k_hess dispatch is also counted in the
 # bench JSON of that pass (empty dispatches read ~0 bytes and are not counted as launches).
@@ -6,11 +6,12 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-pmc}
+CFG=${2:-synth100k}
 mkdir -p gpurun_out/$TAG
 i=0
 for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $C -d gpurun_out/$TAG/p$i -o run --output-format csv -- python3 bench.py --steps 10 --warmup 0 --profile --no-cpu --no-lcd > gpurun_out/$TAG/p$i.json 2> gpurun_out/$TAG/p$i.err
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $C -d gpurun_out/$TAG/p$i -o run --output-format csv -- python3 bench.py --config $CFG --burn-in ${BURN:-40} --steps ${STEPS:-10} --warmup 0 --profile --no-cpu --no-lcd > gpurun_out/$TAG/p$i.json 2> gpurun_out/$TAG/p$i.err
   rc=$?; echo "pmc pass $i ($C) rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done
