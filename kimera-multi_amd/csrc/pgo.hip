@@ -1970,7 +1970,15 @@ struct kmx_pgo {
   // ab_query: 0.836 vs 0.863 ms per round; wall = busy without it), and
   // launches reach the hardware queue without it
   bool query = false;
-  int rm = RM_LAUNCH;        // KMX_RED=1: tickets in the producing launch; 2: consumer-side reductions (both measured slower)
+  // reduction mode: set per graph (below) unless KMX_RED forces one (0 launch,
+  // 1 tickets, 2 consumer). Measured (profiles/r02/round_sizes): consumer-side
+  // reductions win on small per-GPU problems, where a round is launch-bound
+  // (12.5k poses 173 vs 196 us, 25k 274 vs 303 us per round), and tie or lose
+  // from 50k poses on, where the added per-workgroup latency of the gather
+  // kernels costs as much as the saved launches
+  int rm = RM_LAUNCH;
+  int rm_forced = -1;
+  static constexpr int RM_CONSUMER_MAX_POSES = 40000;
   bool poll_timeout = false;
   // timing
   bool timing = false;
@@ -2306,7 +2314,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   if (const char* v = std::getenv("KMX_QUERY")) h->query = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);
-    h->rm = m == 0 ? RM_LAUNCH : m == 1 ? RM_TICKET : RM_CONSUMER;
+    h->rm_forced = m == 0 ? RM_LAUNCH : m == 1 ? RM_TICKET : RM_CONSUMER;
   }
   *out = h;
   return KMX_OK;
@@ -2368,6 +2376,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     }
   }
   h->nloc = nloc;
+  h->rm = h->rm_forced >= 0 ? h->rm_forced : (nloc <= kmx_pgo::RM_CONSUMER_MAX_POSES ? RM_CONSUMER : RM_LAUNCH);
   const int L = (int)h->robots.size();
   KMX_CHECK(L > 0, KMX_EINVAL, "no local robot");
   KMX_CHECK(L <= 1024, KMX_EUNSUP, "at most 1024 local robots per handle");
