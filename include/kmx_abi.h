@@ -56,6 +56,10 @@ int kmx_device_count(int* out);
 #define KMX_COST_L2 0
 #define KMX_COST_GNC_TLS 1
 
+/* Local solver of a block update (dpgo ROptParameters::ROptMethod). */
+#define KMX_METHOD_RTR 0 /* Riemannian trust region + truncated CG (the default) */
+#define KMX_METHOD_RGD 1 /* one preconditioned Riemannian gradient step, fixed step size */
+
 /* Block-update schedule across robots (SURVEY.md §0 finding 6). */
 #define KMX_SCHEDULE_SEQUENTIAL 0 /* one executing robot per round (dpgo_ros sync) */
 #define KMX_SCHEDULE_CONCURRENT 1 /* every active robot per round (Jacobi)        */
@@ -82,7 +86,10 @@ typedef struct kmx_pgo_params {
   int acceleration;         /* Nesterov-accelerated RBCD (RBCD++) on/off (0); concurrent
                                schedule only: every local robot updates every round      */
   int restart_interval;     /* acceleration restart period in rounds (30)               */
-  int reserved[6];
+  int method;               /* KMX_METHOD_RTR (0) or KMX_METHOD_RGD (1)                  */
+  int reserved0;
+  double rgd_stepsize;      /* RGD: X <- Retr_X(-s * precon(grad f)) (1e-3)              */
+  int reserved[2];
 } kmx_pgo_params;
 
 /* Per-robot statistics of one RBCD round (what dpgo logs to dpgo_log_*.csv via

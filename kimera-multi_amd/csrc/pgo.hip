@@ -108,6 +108,8 @@ struct Params {
   int tcg_max, rtr_iters, use_precond, robust;
   double kappa, theta, Delta0, Delta_max, accept_rho, gn_tol, shift, barc, mu_step, rel_tol;
   int gnc_on, inner_iters, max_updates, n_ext;
+  int rgd;          // KMX_METHOD_RGD: one preconditioned gradient step per block update
+  double rgd_step;
 };
 
 struct Dev {
@@ -917,6 +919,15 @@ __device__ void control_on(Ctl& c, const Dev& d, int l, int kind, const double* 
       c.accepted = 0;
       c.skipped = 1;
       if (side) d.relc[l] = (c.rtr_iter == 0) ? 0.0 : c.rel_change;
+    } else if (P.rgd) {  // RGD: eta = -s z (z = precon(g), from k_grad), straight to the step
+      c.phase = PH_STEP;
+      c.tcg_iter = 0;
+      c.tcg_stop = KMX_TCG_NONE;
+      c.coef = -P.rgd_step;
+      if (side && c.rtr_iter == 0) {
+        atomicAdd(&d.cnt->edges_iters, (unsigned long long)d.m_robot[l]);
+        atomicAdd(&d.cnt->block_updates, 1ull);
+      }
     } else {
       c.phase = PH_TCG;
       c.tcg_iter = 0;
@@ -964,6 +975,16 @@ __device__ void control_on(Ctl& c, const Dev& d, int l, int kind, const double* 
       c.z_r = zr_new;
       c.beta = beta;
     }
+  } else if (P.rgd) {  // RED_COST after an RGD step: always accepted, one step per block update
+    c.rho = 0.0;
+    c.accepted = 1;
+    c.commit = 1;
+    c.f_final = tot[0];
+    c.chg_acc += tot[3];
+    c.rtr_iter += 1;
+    c.phase = PH_IDLE;
+    c.rel_change = sqrt(c.chg_acc / (double)d.n_robot[l]);
+    if (side) d.relc[l] = c.rel_change;
   } else {  // RED_COST: tot[0] = f(Xt), tot[2] = 2 m(eta), tot[3] = ||Xt - X||^2
     const double ft = tot[0];
     const double model_dec = -0.5 * tot[2];
@@ -1372,7 +1393,7 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
   if (L.valid) {  // all rows in flight before the Gram-Schmidt chain
     load4(d.X + o, x);
     if (c.tcg_iter > 1) load4(d.eta + o, et);  // eta after the last step's update is eta + coef delta
-    load4(d.del + o, dl);
+    load4((d.p.rgd ? d.z : d.del) + o, dl);    // RGD: eta = -s z
     load4(d.g + o, gg);
     load4(d.r + o, rr);
     const double coef = c.coef;
@@ -2089,6 +2110,8 @@ void sync_params(kmx_pgo* h) {
   p.inner_iters = h->gnc_inner_iters;
   p.max_updates = h->gnc_max_updates;
   p.n_ext = h->n_ext;
+  p.rgd = h->P.method == KMX_METHOD_RGD ? 1 : 0;
+  p.rgd_step = h->P.rgd_stepsize;
   h->dv.ext = h->d_ext;
 }
 
@@ -2157,13 +2180,14 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
       hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot, src);
   };
   enqueue_begin(h, d_active, BEGIN_ROUND);
-  for (int it = 0; it < h->P.rtr_iterations; ++it) {
+  const bool rgd = h->P.method == KMX_METHOD_RGD;
+  for (int it = 0; it < (rgd ? 1 : h->P.rtr_iterations); ++it) {
     hipLaunchKernelGGL((k_grad<R, RW, RM>), grid, blk, SmemHG<R>::bytes, h->stream, h->dv);
     red(RED_GRAD);
     // tCG: each step is (k_hess, k_update); with polling, exactly one step
     // stays queued beyond the last one known to be needed
     unsigned long long prev = 0;
-    for (int j = 0; j < h->P.tcg_max_iterations; ++j) {
+    for (int j = 0; j < (rgd ? 0 : h->P.tcg_max_iterations); ++j) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
       int slot = -1;
       if (h->timing && h->ev_used / 2 < (size_t)HV_SLOTS) {
@@ -2195,7 +2219,7 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
       }
     }
     // RM_CONSUMER: the last step's update has no k_hess after it
-    if (RM == RM_CONSUMER) red(RED_UPDATE, nullptr, 0, -1, h->dv.part_u);
+    if (RM == RM_CONSUMER && !rgd) red(RED_UPDATE, nullptr, 0, -1, h->dv.part_u);
     hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv);
     hipLaunchKernelGGL((k_cost<R, RW, RM>), grid, blk, SmemC<R>::bytes, h->stream, h->dv);
     red(RED_COST);
@@ -2297,6 +2321,9 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
             "robust cost must be L2 or GNC_TLS");
   KMX_CHECK((params->acceleration == 0 || params->acceleration == 1) && params->restart_interval >= 0, KMX_EINVAL,
             "acceleration is 0 or 1, restart_interval >= 0");
+  KMX_CHECK(params->method == KMX_METHOD_RTR || params->method == KMX_METHOD_RGD, KMX_EUNSUP,
+            "method must be KMX_METHOD_RTR or KMX_METHOD_RGD");
+  KMX_CHECK(params->method != KMX_METHOD_RGD || params->rgd_stepsize > 0.0, KMX_EINVAL, "rgd_stepsize must be > 0");
   int ndev = 0;
   KMX_HIP(hipGetDeviceCount(&ndev));
   KMX_CHECK(device >= 0 && device < ndev, KMX_EINVAL, "bad HIP device ordinal");

@@ -51,7 +51,7 @@ class PgoParams(C.Structure):
         ("precond_shift", C.c_double), ("robust_cost", C.c_int),
         ("gnc_barc", C.c_double), ("gnc_mu_init", C.c_double),
         ("gnc_mu_step", C.c_double), ("acceleration", C.c_int), ("restart_interval", C.c_int),
-        ("reserved", C.c_int * 6),
+        ("method", C.c_int), ("reserved0", C.c_int), ("rgd_stepsize", C.c_double), ("reserved", C.c_int * 2),
     ]
 
 

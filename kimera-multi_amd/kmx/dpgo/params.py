@@ -36,8 +36,15 @@ class RobustCostParameters:
     GNCInitMu: float = 1e-5
 
 
+class ROptMethod(IntEnum):
+    RTR = 0
+    RGD = 1
+
+
 @dataclass
 class ROptParameters:
+    method: ROptMethod = ROptMethod.RTR     # dpgo ROptParameters::method
+    RGD_stepsize: float = 1e-3              # [U] dpgo default
     RTR_iterations: int = 1
     RTR_tCG_iterations: int = 10
     RTR_initial_radius: float = 100.0
@@ -81,6 +88,8 @@ class PGOAgentParameters:
         p.precond_shift = lo.precond_shift
         p.robust_cost = int(rc.costType)
         p.gnc_barc, p.gnc_mu_init, p.gnc_mu_step = rc.GNCBarc, rc.GNCInitMu, rc.GNCMuStep
+        p.method = int(lo.method)
+        p.rgd_stepsize = float(lo.RGD_stepsize)
         p.acceleration = 1 if self.acceleration else 0
         p.restart_interval = int(self.restartInterval)
         return p

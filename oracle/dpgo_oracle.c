@@ -421,7 +421,32 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
   st->updated = 1;
   st->edges = h->nredges[a];
   double Delta = h->P.rtr_initial_radius;
-  for (int it = 0; it < h->P.rtr_iterations; ++it) {
+  if (h->P.method == KMX_METHOD_RGD) {
+    /* dpgo QuadraticOptimizer::gradientDescent (ROptMethod RGD) [U: dpgo not vendored]:
+     * X <- Retr_X(-s * precon(rgrad)), always accepted; the same gradient-norm skip as RTR */
+    const double f = edge_eval(&b, c.Xb, 1, c.eg);
+    for (int i = 0; i < b.n; ++i) {
+      sym_YtG(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.S + (int64_t)i * 9);
+      proj_pose(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.g + (int64_t)i * b.ps);
+    }
+    const double gn = sqrt(dot(c.g, c.g, N));
+    st->f_init = f;
+    st->gradnorm_init = gn;
+    st->f_final = f;
+    if (gn < h->P.gradnorm_tol) {
+      st->tcg_stop = KMX_TCG_SKIPPED;
+    } else {
+      precon(&b, &c, c.g, z);
+      const double s = h->P.rgd_stepsize;
+      for (int64_t k = 0; k < N; ++k) eta[k] = -s * z[k];
+      for (int i = 0; i < b.n; ++i)
+        retract_pose(b.r, c.Xb + (int64_t)i * b.ps, eta + (int64_t)i * b.ps, Xt + (int64_t)i * b.ps);
+      st->f_final = edge_eval(&b, Xt, 1, c.tmp);
+      memcpy(c.Xb, Xt, sizeof(double) * N);
+      st->accepted = 1;
+    }
+  }
+  for (int it = 0; it < (h->P.method == KMX_METHOD_RGD ? 0 : h->P.rtr_iterations); ++it) {
     double f = edge_eval(&b, c.Xb, 1, c.eg);
     for (int i = 0; i < b.n; ++i) {
       sym_YtG(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.S + (int64_t)i * 9);

@@ -298,3 +298,26 @@ def test_accelerated_async_equals_sync(gpu):
     s2.sync()
     for a in range(g.n_robots):
         assert np.array_equal(s1.get_iterate(a), s2.get_iterate(a))
+
+
+@pytest.mark.parametrize("robust", [False, True])
+def test_rgd_rounds_match_oracle(gpu, robust):
+    """ROptMethod RGD on the device (k_grad -> k_retract with eta = -s z, no tCG
+    launches, always accepted) vs the oracle's gradientDescent restatement."""
+    from kmx.dpgo.params import ROptMethod
+    g, P, X0 = _setup(robust=robust)
+    P.localOptimizationParams.method = ROptMethod.RGD
+    P.localOptimizationParams.RGD_stepsize = 1e-4
+    s, o = _pair(g, P, X0)
+    for it in range(8):
+        s.refresh_local()
+        sg = s.iterate()
+        so = o.iterate()
+        for a in range(g.n_robots):
+            assert (sg[a]["tcg_iterations"], sg[a]["accepted"]) == (so[a]["tcg_iterations"], so[a]["accepted"])
+            assert abs(sg[a]["f_final"] - so[a]["f_final"]) <= 1e-9 * max(1.0, abs(so[a]["f_final"]))
+            d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
+            assert d <= 1e-6, (it, a, d)
+        if robust and it % 4 == 3:
+            s.refresh_local()
+            assert s.update_weights() == o.update_weights()

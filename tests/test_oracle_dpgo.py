@@ -222,3 +222,30 @@ def test_acceleration_schedule_and_speedup():
     _, _, c0, _ = _accel_run(False, 40)
     _, _, c1, _ = _accel_run(True, 40, restart=30)
     assert c1[-1] < c0[-1] and c1[20] < c0[20]
+
+
+def test_rgd_method_descends():
+    """ROptMethod RGD (dpgo QuadraticOptimizer::gradientDescent): one
+    preconditioned Riemannian gradient step of size s per block update, always
+    accepted; the cost decreases monotonically from the odometry start for a
+    small step, no tCG runs, and the iterate stays on the manifold."""
+    from kmx.dpgo.params import ROptMethod
+    g = make_pose_graph(3, 300, 900, outlier_frac=0.0, seed=2)
+    P = PGOAgentParameters(r=5)
+    P.robustCostParams.costType = RobustCostType.L2
+    P.localOptimizationParams.method = ROptMethod.RGD
+    P.localOptimizationParams.RGD_stepsize = 1e-4
+    o = OraclePGO(P.to_c(), g)
+    Y = lifting_matrix(5, seed=1)
+    for a in range(g.n_robots):
+        o.set_iterate(a, lift(g.init_R[a], g.init_t[a], Y))
+    costs = []
+    for _ in range(15):
+        st = o.iterate()
+        assert all(s["tcg_iterations"] == 0 and s["accepted"] == 1 for s in st)
+        assert all(s["f_final"] < s["f_init"] for s in st)
+        costs.append(sum(s["f_final"] for s in st))
+    assert all(b < a for a, b in zip(costs, costs[1:]))
+    for a in range(g.n_robots):
+        X = o.get_iterate(a)[:, :, :3]
+        assert np.abs(np.einsum("nai,naj->nij", X, X) - np.eye(3)).max() < 1e-10
