@@ -717,7 +717,13 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
 // per-workgroup reduction and decision add latency to every workgroup of the
 // latency-bound gather, which outweighs the saved launches (0.87-0.88 vs
 // 0.86 ms per round), so RM_LAUNCH stays the default.
-enum RedMode { RM_LAUNCH = 0, RM_TICKET = 1, RM_CONSUMER = 2 };
+// RM_HALF (KMX_RED=3): k_update consumes the k_hess partials itself and only
+// the update's reduction keeps its k_reduce launch (so no decision adds
+// latency to the gather kernel): k_hess reads ctl, k_update writes ctl2,
+// k_reduce moves ctl2 -> ctl. Measured at configs[3] (profiles/r02/ab_half):
+// 0.814 / 0.839 vs 0.817 / 0.839 ms per round — the saved launch is what
+// k_update's added latency costs; not the default.
+enum RedMode { RM_LAUNCH = 0, RM_TICKET = 1, RM_CONSUMER = 2, RM_HALF = 3 };
 
 template <int KIND, int NV, int RM, typename Store>
 __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const double* vals, char* smem_red,
@@ -730,7 +736,8 @@ __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const d
     if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
   }
   __syncthreads();
-  if constexpr (RM == RM_LAUNCH || (RM == RM_CONSUMER && KIND != RED_HESS && KIND != RED_UPDATE)) {
+  if constexpr (RM == RM_LAUNCH || (RM == RM_CONSUMER && KIND != RED_HESS && KIND != RED_UPDATE) ||
+                (RM == RM_HALF && KIND != RED_HESS)) {
     if (threadIdx.x == 0) {
 #pragma unroll
       for (int s = 0; s < NV; ++s) {
@@ -742,7 +749,7 @@ __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const d
     }
     store();
     return;
-  } else if constexpr (RM == RM_CONSUMER) {  // RED_HESS / RED_UPDATE: 2-wide partials for the consumer launch
+  } else if constexpr (RM == RM_CONSUMER || RM == RM_HALF) {  // 2-wide partials for the consumer launch
     static_assert(NV <= 2, "consumer partials");
     if (threadIdx.x == 0) {
       double* dst = (KIND == RED_HESS ? d.part_h : d.part_u) + (size_t)L.tile * 2;
@@ -1124,11 +1131,12 @@ struct RobotSum {
 };
 
 __global__ __launch_bounds__(RBLOCK) void k_reduce(Dev d, int kind, int R_, HostStatus* hs, unsigned long long seq,
-                                                  int slot, const double* src) {
+                                                  int slot, const double* src, const Ctl* from) {
   constexpr int RW_ = RBLOCK / 64;
   __shared__ double lds[NPART * RW_];
   const int l = blockIdx.x;
-  const int ph = d.ctl[l].phase;
+  const int ph = from ? from[l].phase : d.ctl[l].phase;
+  if (from && threadIdx.x == 0) d.ctl[l] = from[l];  // RM_HALF: the state k_update left in ctl2
   bool act = false;
   if (kind == RED_GRAD) act = ph == PH_START;
   if (kind == RED_HESS || kind == RED_UPDATE) act = ph == PH_TCG;
@@ -1308,16 +1316,19 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
   double coef;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
-  if constexpr (RM == RM_CONSUMER) {
+  if constexpr (RM == RM_CONSUMER || RM == RM_HALF) {
     // this step's k_hess partials: the control step after the Hess-vec (alpha
     // or the boundary tau) on a private copy, with the step's vector loads in
-    // flight; the first tile writes the robot's state back to ctl
+    // flight; the first tile writes the robot's state (RM_CONSUMER: ctl2 ->
+    // ctl; RM_HALF: ctl -> ctl2, which k_reduce moves back)
     __shared__ Ctl cs;
     __shared__ double rl[NPART * WAVES];
-    const Ctl& cq = d.ctl2[L.l];
+    Ctl* const cin = (RM == RM_HALF) ? d.ctl : d.ctl2;
+    Ctl* const cout = (RM == RM_HALF) ? d.ctl2 : d.ctl;
+    const Ctl& cq = cin[L.l];
     const bool writer = L.tile == d.rtile0[L.l];
     if (cq.phase != PH_TCG) {
-      if (writer && threadIdx.x == 0) d.ctl[L.l] = cq;
+      if (writer && threadIdx.x == 0) cout[L.l] = cq;
       return;
     }
     const bool first0 = cq.tcg_iter == 0;  // the control step makes it 1
@@ -1334,7 +1345,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
     if (writer && threadIdx.x == 0) {  // the state update, on an LDS copy
       cs = cq;
       control_on(cs, d, L.l, RED_HESS, tot, R, true);
-      d.ctl[L.l] = cs;
+      cout[L.l] = cs;
       if (slot >= 0) atomicAdd(d.hv_launch + slot, 1);
     }
     tcg_iter = cq.tcg_iter + 1;
@@ -2175,9 +2186,10 @@ template <int R, int RW, int RM>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   const dim3 grid(h->ntiles), blk(BLOCK);
   auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0, int slot = -1,
-                 const double* src = nullptr) {
+                 const double* src = nullptr, const Ctl* from = nullptr) {
     if (RM != RM_TICKET)
-      hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot, src);
+      hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot, src,
+                         from);
   };
   enqueue_begin(h, d_active, BEGIN_ROUND);
   const bool rgd = h->P.method == KMX_METHOD_RGD;
@@ -2209,10 +2221,10 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
       }
       hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, nullptr, 0ull);
       if (slot >= 0) (void)hipEventRecord(e1, h->stream);
-      red(RED_HESS, nullptr, 0, slot);
+      if (RM != RM_HALF) red(RED_HESS, nullptr, 0, slot);
       hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv,
-                         RM == RM_TICKET ? hs : nullptr, seq, -1);
-      red(RED_UPDATE, hs, seq);
+                         RM == RM_TICKET ? hs : nullptr, seq, RM == RM_HALF ? slot : -1);
+      red(RED_UPDATE, hs, seq, -1, nullptr, RM == RM_HALF ? h->dv.ctl2 : nullptr);
       if (poll) {
         if (j > 0 && !wait_running(h, prev)) break;
         prev = seq;
@@ -2232,6 +2244,9 @@ void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
   if (h->rm == RM_CONSUMER) {
     if (h->rw == 12) enqueue_round_t<R, 12, RM_CONSUMER>(h, d_active);
     else enqueue_round_t<R, 16, RM_CONSUMER>(h, d_active);
+  } else if (h->rm == RM_HALF) {
+    if (h->rw == 12) enqueue_round_t<R, 12, RM_HALF>(h, d_active);
+    else enqueue_round_t<R, 16, RM_HALF>(h, d_active);
   } else if (h->rm == RM_TICKET) {
     if (h->rw == 12) enqueue_round_t<R, 12, RM_TICKET>(h, d_active);
     else enqueue_round_t<R, 16, RM_TICKET>(h, d_active);
@@ -2341,7 +2356,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   if (const char* v = std::getenv("KMX_QUERY")) h->query = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);
-    h->rm_forced = m == 0 ? RM_LAUNCH : m == 1 ? RM_TICKET : RM_CONSUMER;
+    h->rm_forced = m == 0 ? RM_LAUNCH : m == 1 ? RM_TICKET : m == 2 ? RM_CONSUMER : RM_HALF;
   }
   *out = h;
   return KMX_OK;
