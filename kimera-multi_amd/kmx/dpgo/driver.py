@@ -28,11 +28,21 @@ per GPU). ROS topics become collectives over RCCL/xGMI:
   UPDATE_WEIGHT         -> decided on the device at the start of each round
                            from the schedule state and the team status
   TERMINATE             -> all_reduce(MAX) of the ranks' largest relative change
+  commands / timeout    -> handle_command applies the dpgo_ros command set on
+                           every rank (TERMINATE, HARD_TERMINATE = reset,
+                           RECOVER, SET_ACTIVE_ROBOTS, UPDATE, UPDATE_WEIGHT,
+                           INITIALIZE, NOOP); check_timeout is the leader's
+                           checkTimeout (kmx.dpgo.command), rank 0's decision
+                           broadcast so every rank applies the same command
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 
+from .command import TimeoutMonitor, TimeoutParameters
+from .messages import Command, CommandType, PGOAgentState
 from .params import PGOAgentParameters
 from .schedule import ExecutingRobot
 from .solver import BlockSolver
@@ -80,14 +90,16 @@ def exchange_plan(graph, world: int, rank: int):
 
 class RBCDDriver:
     def __init__(self, params: PGOAgentParameters, graph, *, rank: int = 0, world: int = 1,
-                 device: int = 0, solver=None, exchange_device: str | None = None, log_dir: str | None = None):
+                 device: int = 0, solver=None, exchange_device: str | None = None, log_dir: str | None = None,
+                 timeout: TimeoutParameters | None = None):
         """`solver` defaults to a BlockSolver on HIP device `device`; any object
         with the same interface can be injected (the CPU gloo tests inject the
         restatement). `exchange_device` is where the collective runs ("cuda"
         for RCCL, "cpu" for gloo). A GPU solver under gloo packs into device
         buffers and stages them through host copies (N ranks on one GPU).
         `log_dir`: write dpgo_log_<robot>.csv for the robots of this rank
-        (one row per round in which the robot updated, kmx.io.DpgoIterationLog)."""
+        (one row per round in which the robot updated, kmx.io.DpgoIterationLog).
+        `timeout`: the checkTimeout parameters (kmx.dpgo.command)."""
         if world > graph.n_robots:
             raise ValueError("need at least one robot block per rank")
         self.params = params
@@ -124,6 +136,13 @@ class RBCDDriver:
         if log_dir is not None:
             from ..io import DpgoIterationLog
             self.logs = {a: DpgoIterationLog(log_dir, a) for a in self.robots}
+        # the command channel's state (dpgo_ros PGOAgentROS; kmx.dpgo.command)
+        self.state = PGOAgentState.WAIT_FOR_INITIALIZATION  # the graph is bound at construction
+        self.instance = 0
+        self.terminated = False
+        self.active_robots = set(range(graph.n_robots))
+        self.monitor = TimeoutMonitor(timeout, now=time.monotonic())
+        self._X0 = None
 
     # ------------------------------------------------------ collectives ---
     def _setup_exchange(self):
@@ -182,23 +201,36 @@ class RBCDDriver:
 
     # ------------------------------------------------------------ rounds ---
     def initialize(self, X_by_robot: dict):
+        self._X0 = {a: np.array(X_by_robot[a], dtype=np.float64) for a in self.robots}
         for a in self.robots:
-            self.solver.set_iterate(a, X_by_robot[a])
+            self.solver.set_iterate(a, self._X0[a])
+        self.state = PGOAgentState.INITIALIZED
+        self.terminated = False
 
     def active_mask(self) -> np.ndarray:
         act = np.zeros(self.graph.n_robots, np.uint8)
         if self.params.schedule == 0:  # sequential: the leader picks one executing robot
-            act[self.executing.next(range(self.graph.n_robots))] = 1
+            act[self.executing.next(sorted(self.active_robots))] = 1
         else:
-            act[:] = 1
+            act[sorted(self.active_robots)] = 1
         return act
+
+    def _all_active(self) -> bool:
+        return len(self.active_robots) == self.graph.n_robots
+
+    def _check_running(self):
+        if self.state != PGOAgentState.INITIALIZED:
+            raise ValueError("round before initialize (or after HARD_TERMINATE)")
+        if self.terminated:
+            raise ValueError("round after TERMINATE")
 
     def step(self, with_stats: bool = True):
         """One synchronous round (its GNC decision runs on the device first).
         Returns per-robot stats (team-indexed) when with_stats."""
+        self._check_running()
         self.exchange_public()
         stats = None
-        if with_stats or self.params.schedule == 0 or self.logs:
+        if with_stats or self.params.schedule == 0 or self.logs or not self._all_active():
             act = self.active_mask()
             stats = self.solver.iterate(act)
             if self.logs:
@@ -215,7 +247,8 @@ class RBCDDriver:
     def run_async(self, rounds: int):
         """Benchmark path: enqueue `rounds` concurrent rounds with no host sync
         (single GPU: one C call; multi-GPU: one all-to-all between rounds)."""
-        if self.world == 1 and self.params.schedule == 1:
+        self._check_running()
+        if self.world == 1 and self.params.schedule == 1 and self._all_active():
             self.solver.iterate_async(rounds, refresh_local=True)
             self.round_index += rounds
             return
@@ -246,7 +279,7 @@ class RBCDDriver:
         at the end); returns the rounds run."""
         limit = self.params.maxNumIters if max_rounds is None else max_rounds
         done = 0
-        while done < limit:
+        while done < limit and not self.terminated:
             k = min(check_every, limit - done)
             self.run_async(k)
             done += k
@@ -256,3 +289,93 @@ class RBCDDriver:
 
     def iterate_of(self, robot: int) -> np.ndarray:
         return self.solver.get_iterate(robot)
+
+    # ---------------------------------------------------------- commands ---
+    def reset(self):
+        """PGOAgent::reset as HARD_TERMINATE runs it (drawio:2433-2436): next
+        instance, iteration number 0, GNC weights / mu / schedule and the team
+        status back to their initial values; the graph stays bound, so the
+        team resumes with INITIALIZE (or initialize(X))."""
+        P, g = self.params, self.graph
+        self.instance += 1
+        self.round_index = 0
+        self.state = PGOAgentState.WAIT_FOR_INITIALIZATION
+        self.terminated = False
+        self.active_robots = set(range(g.n_robots))
+        self.executing = ExecutingRobot(P.updateRule, P.randomSeed)
+        self.solver.set_weights(np.asarray(g.weight, np.float64))
+        self.solver.set_gnc_state({"inner_iter": 0, "updates": 0, "mu": P.robustCostParams.GNCInitMu})
+        self.solver.set_status(np.where(np.asarray(g.n_poses) > 0, np.inf, 0.0))
+
+    def handle_command(self, cmd: Command, now: float | None = None):
+        """commandCallback of dpgo_ros (drawio:2124-2481) on this rank; every
+        rank receives the same command. Returns the stats of an UPDATE round
+        (None otherwise).
+          TERMINATE          stop; the iterate stays readable (drawio:2180)
+          HARD_TERMINATE     reset() (drawio:2433-2436)
+          RECOVER            iteration number := executing_iteration, active
+                             robots := the message's (if it names any), resume
+                             (drawio:2448, 2472-2481)
+          SET_ACTIVE_ROBOTS  the robots that update in later rounds (drawio:2405)
+          UPDATE             one round; executing_robot >= 0 runs that robot
+                             alone (drawio:2369, 2478-2481)
+          UPDATE_WEIGHT      GNC weight update now (drawio:2212-2215)
+          INITIALIZE         re-apply the last initial iterate after a reset
+          REQUEST_POSE_GRAPH the graph was bound at construction: no-op
+          NOOP               refreshes the command clock only (drawio:2402)"""
+        now = time.monotonic() if now is None else float(now)
+        self.monitor.note_command(now)
+        c = CommandType(cmd.command)
+        if c == CommandType.TERMINATE:
+            self.terminated = True
+        elif c == CommandType.HARD_TERMINATE:
+            self.reset()
+        elif c == CommandType.RECOVER:
+            self.round_index = int(cmd.executing_iteration)
+            if cmd.active_robots:
+                self.active_robots = {int(a) for a in cmd.active_robots}
+            self.terminated = False
+        elif c == CommandType.SET_ACTIVE_ROBOTS:
+            act = {int(a) for a in cmd.active_robots}
+            if not act or not act <= set(range(self.graph.n_robots)):
+                raise ValueError(f"SET_ACTIVE_ROBOTS: robots must be a non-empty subset of the team, got {sorted(act)}")
+            self.active_robots = act
+        elif c == CommandType.UPDATE:
+            keep = self.active_robots
+            if cmd.executing_robot >= 0:
+                if cmd.executing_robot not in keep:
+                    raise ValueError(f"UPDATE: robot {cmd.executing_robot} is not active")
+                self.active_robots = {int(cmd.executing_robot)}
+            try:
+                st = self.step(with_stats=True)
+            finally:
+                self.active_robots = keep
+            self.monitor.note_update(now)
+            return st
+        elif c == CommandType.UPDATE_WEIGHT:
+            self._check_running()
+            self.update_weights()
+        elif c == CommandType.INITIALIZE:
+            if self.state != PGOAgentState.INITIALIZED:
+                if self._X0 is None:
+                    raise ValueError("INITIALIZE: no initial iterate; call initialize(X) first")
+                self.initialize(self._X0)
+        return None
+
+    def check_timeout(self, now: float | None = None) -> Command | None:
+        """The leader's checkTimeout (kmx.dpgo.command.TimeoutMonitor): rank 0
+        decides, every rank applies the same HARD_TERMINATE or RECOVER (one
+        broadcast when world > 1). Returns the command applied, or None."""
+        now = time.monotonic() if now is None else float(now)
+        c = self.monitor.check(now, self.state, self.round_index, len(self.active_robots))
+        if self.world > 1:
+            t = self._torch.tensor([-1 if c is None else int(c)], dtype=self._torch.int64,
+                                   device="cuda" if self._xdev == "cuda" else "cpu")
+            self._dist.broadcast(t, src=0)
+            v = int(t.item())
+            c = None if v < 0 else CommandType(v)
+        if c is None:
+            return None
+        cmd = Command(0, c, executing_iteration=self.round_index, active_robots=sorted(self.active_robots))
+        self.handle_command(cmd, now)
+        return cmd

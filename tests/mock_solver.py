@@ -108,8 +108,15 @@ class OracleBlockSolver:
     def gnc_state(self):
         return {"inner_iter": self.gnc.inner, "updates": self.gnc.updates, "mu": self.o.mu}
 
+    def set_gnc_state(self, state):
+        self.gnc.inner, self.gnc.updates = int(state["inner_iter"]), int(state["updates"])
+        self.o.mu = float(state["mu"])
+
     def status(self):
         return self.relc.copy()
+
+    def set_status(self, v):
+        self.relc = np.array(v, dtype=np.float64)
 
     def _round(self, active):
         team = np.concatenate([self.relc[self.local == 1], self.ext])

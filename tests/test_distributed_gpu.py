@@ -97,3 +97,34 @@ def test_two_ranks_one_gpu_match_single_process(gpu, rel_tol):
         assert np.array_equal(w[sel], w1[sel]), rank
     for a in range(g.n_robots):
         assert np.array_equal(got[a], X1[a]), a
+
+
+@pytest.mark.timeout(300)
+def test_commands_on_device(gpu):
+    """HARD_TERMINATE resets the device state (weights, mu, GNC counters,
+    status) so that INITIALIZE + the same rounds reproduce a fresh handle bit
+    for bit; SET_ACTIVE_ROBOTS freezes the inactive blocks on the device."""
+    from kmx.dpgo.driver import RBCDDriver
+    from kmx.dpgo.messages import Command, CommandType
+    g, P = _graph(), _params()
+    drv = RBCDDriver(P, g, device=0)
+    drv.initialize(_x0(g))
+    drv.run(max_rounds=10, check_every=5)
+    assert drv.weight_updates >= 2
+    drv.handle_command(Command(0, CommandType.HARD_TERMINATE))
+    assert drv.weight_updates == 0 and np.all(np.isinf(drv.solver.status()))
+    drv.handle_command(Command(0, CommandType.INITIALIZE))
+    X1, w1 = _run(drv, 9)
+    fresh = RBCDDriver(P, g, device=0)
+    fresh.initialize(_x0(g))
+    X2, w2 = _run(fresh, 9)
+    assert drv.weight_updates == fresh.weight_updates >= 2
+    assert np.array_equal(w1, w2)
+    for a in range(g.n_robots):
+        assert np.array_equal(X1[a], X2[a]), a
+    drv.handle_command(Command(0, CommandType.SET_ACTIVE_ROBOTS, active_robots=[1, 3]))
+    drv.run(max_rounds=4)
+    drv.solver.sync()
+    for a in range(g.n_robots):
+        same = np.array_equal(drv.iterate_of(a), X1[a])
+        assert same == (a in (0, 2)), a
