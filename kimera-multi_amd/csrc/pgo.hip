@@ -333,9 +333,11 @@ __device__ __forceinline__ void group_proj(const double y[4], const double V[4],
 }
 
 // Preconditioner: P_Y(V Pinv_i) (block-Jacobi on Q's 4x4 diagonal blocks).
+// Pre (LDS form only, has_pre): the pose's block, already loaded by the caller.
 template <int R, bool LDS = false>
 __device__ __forceinline__ void group_precon(const Dev& d, int pose, bool valid, const double y[4],
-                                             const double V[4], int base, double out[4], double* scr = nullptr) {
+                                             const double V[4], int base, double out[4], double* scr = nullptr,
+                                             const double* Pre = nullptr, bool has_pre = false) {
   if (!d.p.use_precond) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) out[k] = V[k];
@@ -345,8 +347,13 @@ __device__ __forceinline__ void group_precon(const Dev& d, int pose, bool valid,
   const double* Pp = d.Pinv + 16 * (size_t)pose;
   if constexpr (LDS) {  // 128-VGPR kernels: all of P in flight (pose is valid on every lane)
     double P[16];
+    if (has_pre) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) load4(Pp + 4 * i, P + 4 * i);
+      for (int i = 0; i < 16; ++i) P[i] = Pre[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) load4(Pp + 4 * i, P + 4 * i);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -469,9 +476,14 @@ static_assert(SCR_BYTES <= SmemHG<3>::x_off, "scratch");
 // a public neighbour's row counts as zero). Q's diagonal block D_i (k_precond)
 // is applied once per pose; an incidence contributes only its off-diagonal
 // block applied to the other endpoint's whole r x 4 row.
-template <int R, int RW>
-__device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const double* V, double acc[4],
-                                            char* smem) {
+struct NoPre {
+  __device__ bool operator()() const { return true; }
+};
+// `pre` runs once the first chunk's records are in flight, before any row is
+// gathered (workgroup-uniform; false: leave without gathering).
+template <int R, int RW, typename Pre = NoPre>
+__device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const double* V, double acc[4],
+                                            char* smem, Pre&& pre = Pre{}) {
   using SM = SmemH<R>;
   using RC = Rec<RW>;
   constexpr int CH = SM::CH;
@@ -491,6 +503,7 @@ __device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const d
   double2 q[RC::Q];
   ld(0, q);
   __syncthreads();  // sptr
+  if (!pre()) return false;
   for (int c0 = 0; c0 < n; c0 += CH) {
     Edge E;
     RC::edge(q, E);
@@ -547,6 +560,7 @@ __device__ __forceinline__ void hinc_gather(const Dev& d, const Lane& L, const d
       acc[c] += vs[0] * dr[0] + vs[1] * dr[1] + vs[2] * dr[2] + vs[3] * dr[3];
     }
   }
+  return true;
 }
 
 // Gradient and cost, incidence-parallel. A lane evaluates its whole incidence
@@ -711,7 +725,12 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
 // control step on a private copy of the robot's state; the robot's first tile
 // writes the state out, double-buffered (k_hess: ctl -> ctl2, k_update: ctl2 ->
 // ctl), so no workgroup reads a state another one of the same launch writes.
-// Two launches per tCG step instead of four, same results as RM_LAUNCH.
+// Two launches per tCG step instead of four, same results as RM_LAUNCH; the
+// round's other reductions are folded too (gradient -> first k_hess, last
+// update -> k_retract, trial cost -> k_commit), so a round has no k_reduce
+// launch: 12.5k poses 167.7 -> 161.4 us per round, with the host no longer
+// waiting on a reduction launch between the tCG loop and the retraction
+// (profiles/r02/small_round/3_*).
 // Measured on configs[3] (profiles/r02/ab_red): k_hess 41.2 us and k_update
 // 22.7 us against 32.4 + 19.8 us plus two 4.6 us k_reduce launches — the
 // per-workgroup reduction and decision add latency to every workgroup of the
@@ -1079,6 +1098,7 @@ __device__ __forceinline__ void robot_sum(const double* part, int stride, int t0
 // work: issue() loads a robot's <= 2 * RBLOCK tiles into registers (larger
 // robots fall back to robot_sum in finish()); finish() adds them in
 // robot_sum's order.
+// NS <= 2: 2-wide partials (part_h / part_u); NS = 3, 4: d.part (stride NPART).
 template <int NS>
 struct RobotSum {
   double a[2][NS];
@@ -1090,15 +1110,22 @@ struct RobotSum {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int t = min(t0 + (int)threadIdx.x + u * RBLOCK, t1 - 1);
-      const double2 x = *reinterpret_cast<const double2*>(part + (size_t)t * stride);
+      const double2* p2 = reinterpret_cast<const double2*>(part + (size_t)t * stride);
+      const double2 x = p2[0];
+      if constexpr (NS > 2) {
+        const double2 y = p2[1];
+        a[u][2] = y.x;
+        if constexpr (NS > 3) a[u][3] = y.y;
+      }
       a[u][0] = x.x;
-      if constexpr (NS > 1) a[u][NS - 1] = x.y;
+      if constexpr (NS > 1) a[u][1] = x.y;
     }
   }
   __device__ __forceinline__ void finish(const double* part, int stride, double* lds, double tot[NPART]) {
-    static_assert(NS <= 2, "2-wide partials");
+    static_assert(NS <= NPART, "partials");
     if (t1 - t0 > 2 * RBLOCK) {
-      robot_sum<NS>(part, stride, t0, t1, lds, tot);
+      robot_sum<(NS > 2 ? NPART : NS)>(part, stride, t0, t1, lds, tot);
+      if constexpr (NS == 3) tot[3] = 0.0;
       return;
     }
     constexpr int RW_ = RBLOCK / 64;
@@ -1215,41 +1242,55 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   if constexpr (RM == RM_CONSUMER) {
     // the previous step's k_update partials give this robot's control step
-    // after the update (stop test, beta); it runs on a private copy after the
-    // gather (speculative: a robot whose tCG stops here discards it), so the
-    // partial loads are in flight with the gather's first records. The robot's
+    // after the update (stop test, beta); the partial loads are in flight with
+    // the gather's first records, and the decision comes before the rows are
+    // gathered (a stopped robot's tiles leave without the gather). The robot's
     // first tile writes the state to ctl2 for k_update and reports tCG
     // progress to the host.
     __shared__ Ctl cs;
     __shared__ double rl[NPART * WAVES];
     const Ctl& c0 = d.ctl[L.l];
     const bool writer = L.tile == d.rtile0[L.l];
-    if (c0.phase != PH_TCG) {  // uniform: a tile never straddles robots
+    const int ph0 = c0.phase;  // written by an earlier launch: uniform
+    // PH_START: the first step of the tCG, whose gradient reduction (k_grad's
+    // partials) this launch also consumes in place of a k_reduce launch
+    const bool grad = ph0 == PH_START;
+    if (ph0 != PH_TCG && !grad) {  // uniform: a tile never straddles robots
       if (writer && threadIdx.x == 0) {
         d.ctl2[L.l] = c0;
         if (hs) post_status(hs, L.l, seq, false);
       }
       return;
     }
-    const bool upd = c0.tcg_iter > 0;
+    const bool upd = !grad && c0.tcg_iter > 0;
     RobotSum<2> rs;
+    RobotSum<3> rg;
     if (upd) rs.issue(d.part_u, 2, d.rtile0[L.l], d.rtile0[L.l + 1]);
-    hinc_gather<R, RW>(d, L, d.z, H, smem);
-    double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
-    if (upd) rs.finish(d.part_u, 2, rl, tot);
-    // every thread evaluates the decision; the first tile's thread 0 also
-    // updates the robot's state (on an LDS copy: a private one would live in
-    // scratch) and publishes it
+    if (grad) rg.issue(d.part, NPART, d.rtile0[L.l], d.rtile0[L.l + 1]);
     UpdStep u{0, 0, 0.0};
-    if (upd) u = upd_step(c0.mode, c0.norm_r0, c0.z_r, c0.tcg_iter, tot[0], tot[1], d.p);
-    if (writer && threadIdx.x == 0) {
-      cs = c0;
-      if (upd) control_on(cs, d, L.l, RED_UPDATE, tot, R, true);
-      d.ctl2[L.l] = cs;
-      if (hs) post_status(hs, L.l, seq, cs.phase == PH_TCG);
-    }
-    if (u.done) return;
-    tcg_iter = c0.tcg_iter;
+    // the decision runs while the first chunk's records are in flight and
+    // before any row is gathered: a robot whose tCG stops here (or whose
+    // gradient is below tolerance) skips the gather, and the host sees the
+    // stop at the start of the launch
+    const bool go = hinc_gather<R, RW>(d, L, d.z, H, smem, [&]() {
+      double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+      if (upd) rs.finish(d.part_u, 2, rl, tot);
+      if (grad) rg.finish(d.part, NPART, rl, tot);
+      // every thread evaluates the decision; the first tile's thread 0 also
+      // updates the robot's state (on an LDS copy: a private one would live in
+      // scratch) and publishes it
+      if (upd) u = upd_step(c0.mode, c0.norm_r0, c0.z_r, c0.tcg_iter, tot[0], tot[1], d.p);
+      if (grad) u.done = sqrt(tot[1]) < d.p.gn_tol ? 1 : 0;  // control_on's RED_GRAD test
+      if (writer && threadIdx.x == 0) {
+        cs = c0;
+        if (upd || grad) control_on(cs, d, L.l, grad ? RED_GRAD : RED_UPDATE, tot, R, true);
+        d.ctl2[L.l] = cs;
+        if (hs) post_status(hs, L.l, seq, cs.phase == PH_TCG);
+      }
+      return !u.done;
+    });
+    if (!go) return;
+    tcg_iter = grad ? 0 : c0.tcg_iter;
     beta = u.beta;
     pcoef = c0.coef;
   } else {
@@ -1316,6 +1357,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
   double coef;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
+  double Pm[16];
+  bool pre = false;
   if constexpr (RM == RM_CONSUMER || RM == RM_HALF) {
     // this step's k_hess partials: the control step after the Hess-vec (alpha
     // or the boundary tau) on a private copy, with the step's vector loads in
@@ -1338,6 +1381,11 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
       load4(d.hd + o, hdl);
       load4((first0 ? d.g : d.r) + o, rr);
       load4(d.X + o, y);  // used by the precon of interior steps (boundary steps are rare)
+      if (d.p.use_precond) {  // the preconditioner block too: no load after the decision
+        const double* Pp = d.Pinv + 16 * (size_t)L.pose;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) load4(Pp + 4 * i, Pm + 4 * i);
+      }
     }
     double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
     rs.finish(d.part_h, 2, rl, tot);
@@ -1351,6 +1399,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
     tcg_iter = cq.tcg_iter + 1;
     mode = hsx.boundary ? MODE_BOUNDARY : MODE_INTERIOR;
     coef = hsx.coef;
+    pre = L.valid;
   } else {
     const Ctl& c = d.ctl[L.l];
     if (c.phase != PH_TCG) {  // not in tCG: the robot's first tile reports it
@@ -1374,7 +1423,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
   }
   double vals[2] = {0.0, 0.0}, zr[4] = {0, 0, 0, 0};
   if (interior) {  // uniform per robot
-    group_precon<R, true>(d, L.pose, L.valid, y, rr, L.base, zr, reinterpret_cast<double*>(smem));
+    group_precon<R, true>(d, L.pose, L.valid, y, rr, L.base, zr, reinterpret_cast<double*>(smem),
+                          Pm, pre);
     if (L.valid) {
       vals[0] = rr[0] * rr[0] + rr[1] * rr[1] + rr[2] * rr[2] + rr[3] * rr[3];
       vals[1] = zr[0] * rr[0] + zr[1] * rr[1] + zr[2] * rr[2] + zr[3] * rr[3];
@@ -1393,14 +1443,38 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
 
 // Trial point Xt = R_X(eta); partials: model m(eta) = 1/2 <eta, g + r> (r = g +
 // H eta by the tCG recurrence) and ||Xt - X||^2 (slots 2, 3; k_cost reduces).
+// fold (RM_CONSUMER): a robot still in tCG ran its last step's update with no
+// k_hess after it; its reduction (the 2-wide part_u) and stop decision run
+// here, in place of a k_reduce launch. The robot's first tile writes the
+// decision into ctl in place: it changes only phase and tcg_stop, and a tile
+// that reads the new phase goes straight to the retraction, as the decision
+// says, so every tile acts alike.
 template <int R>
-__global__ __launch_bounds__(BLOCK) void k_retract(Dev d) {
+__global__ __launch_bounds__(BLOCK) void k_retract(Dev d, int fold) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
-  const Ctl& c = d.ctl[L.l];
-  if (c.phase != PH_STEP) return;
+  Ctl& c = d.ctl[L.l];
+  __shared__ int sph;
+  __shared__ double rl[NPART * WAVES];
+  if (threadIdx.x == 0) sph = c.phase;
+  __syncthreads();
+  const int ph = sph;  // one read per workgroup
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   double x[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0}, gg[4] = {0, 0, 0, 0}, rr[4] = {0, 0, 0, 0}, dl[4];
+  if (fold && ph == PH_TCG) {
+    RobotSum<2> rs;
+    rs.issue(d.part_u, 2, d.rtile0[L.l], d.rtile0[L.l + 1]);
+    double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+    rs.finish(d.part_u, 2, rl, tot);
+    const UpdStep u = upd_step(c.mode, c.norm_r0, c.z_r, c.tcg_iter, tot[0], tot[1], d.p);
+    if (!u.done) return;  // (cannot happen: the host stops enqueueing only when no robot is in tCG or at tcg_max)
+    if (threadIdx.x == 0 && L.tile == d.rtile0[L.l]) {
+      if (u.stop >= 0) c.tcg_stop = u.stop;
+      c.phase = PH_STEP;
+    }
+  } else if (ph != PH_STEP) {
+    return;
+  }
   if (L.valid) {  // all rows in flight before the Gram-Schmidt chain
     load4(d.X + o, x);
     if (c.tcg_iter > 1) load4(d.eta + o, et);  // eta after the last step's update is eta + coef delta
@@ -1457,14 +1531,49 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d) {
 // rows of the committed poses are published (the single-device exchange), so
 // the next round — and a GNC weight update before it — sees the new poses.
 // Tile 0 also counts the round for the GNC schedule.
+// fold (RM_CONSUMER, one RTR iteration): the trial-cost reduction and the
+// accept decision run here in place of a k_reduce launch; every tile decides
+// from the robot's totals and f_cur, which the decision does not change. The
+// robot's first tile writes the RTR state, except the phase, which stays
+// PH_STEP (the next round's k_begin resets it), so tiles that read the state
+// after that write still see a robot with a step to decide.
 template <int R>
-__global__ __launch_bounds__(BLOCK) void k_commit(Dev d) {
+__global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold) {
   const Lane L = lane_map<R>(d);
   if (L.tile == 0 && threadIdx.x == 0) {
     d.gnc->inner += 1;
     d.gnc->rounds += 1;
   }
-  if (!d.ctl[L.l].commit || !L.valid) return;
+  bool commit;
+  if (fold) {
+    __shared__ int sph;
+    __shared__ Ctl cs;
+    __shared__ double rl[NPART * WAVES];
+    const Ctl& c = d.ctl[L.l];
+    if (threadIdx.x == 0) sph = c.phase;
+    __syncthreads();
+    if (sph != PH_STEP) return;
+    RobotSum<NPART> rs;
+    rs.issue(d.part, NPART, d.rtile0[L.l], d.rtile0[L.l + 1]);
+    double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+    rs.finish(d.part, NPART, rl, tot);
+    if (d.p.rgd) {
+      commit = true;
+    } else {  // control_on's RED_COST acceptance test
+      const double model_dec = -0.5 * tot[2];
+      const double rho = (model_dec > 0.0) ? (c.f_cur - tot[0]) / model_dec : -1.0;
+      commit = rho > d.p.accept_rho;
+    }
+    if (threadIdx.x == 0 && L.tile == d.rtile0[L.l]) {
+      cs = c;
+      control_on(cs, d, L.l, RED_COST, tot, R, true);
+      cs.phase = PH_STEP;
+      d.ctl[L.l] = cs;
+    }
+  } else {
+    commit = d.ctl[L.l].commit != 0;
+  }
+  if (!commit || !L.valid) return;
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   double v[4];
   load4(d.Xt + o, v);
@@ -2026,6 +2135,13 @@ struct kmx_pgo {
   double acc_gamma = 0.0;
   int acc_k = 0;
   bool acc_ready = false, acc_started = false;
+  // round seams replayed from hipGraphs (launch_seam; KMX_GRAPH=1, off by default):
+  // [SEAM_TAIL], [SEAM_HEAD], [SEAM_TAIL | SEAM_HEAD], each captured with the
+  // handle state in seam_dv / seam_key and rebuilt when that changes
+  bool graphs = false;
+  hipGraphExec_t seam[4] = {nullptr, nullptr, nullptr, nullptr};
+  Dev seam_dv{};
+  long long seam_key[8] = {};
 };
 
 namespace {
@@ -2039,7 +2155,16 @@ int dalloc(T** p, size_t count) {
   return 0;
 }
 
+void drop_seams(kmx_pgo* h) {
+  for (auto& g : h->seam)
+    if (g) {
+      (void)hipGraphExecDestroy(g);
+      g = nullptr;
+    }
+}
+
 void free_dev(kmx_pgo* h) {
+  drop_seams(h);
   void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_rec, h->d_ekappa,
                   h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_hD, h->d_pub, h->d_part,
                   h->d_ctl, h->d_cnt, h->d_tickets, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
@@ -2182,61 +2307,116 @@ bool wait_running(kmx_pgo* h, unsigned long long seq) {
   return running;
 }
 
+template <int R, int RM>
+void red_t(kmx_pgo* h, int kind, HostStatus* hs = nullptr, unsigned long long seq = 0, int slot = -1,
+           const double* src = nullptr, const Ctl* from = nullptr) {
+  if (RM != RM_TICKET)
+    hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot, src, from);
+}
+
+// The three parts of a round: head (round begin, gradient), tCG (host-polled
+// steps), tail (retraction, trial cost, commit). With one RTR iteration the
+// head and tail launches are fixed for the handle, so back-to-back rounds
+// replay them from hipGraphs (launch_seam below).
+// RM_CONSUMER folds the round's other reductions into the kernel after them
+// (no k_reduce launch in a round): the gradient's into the first k_hess, the
+// last tCG update's into k_retract, the trial cost's into k_commit (one RTR
+// iteration). RGD keeps the gradient's launch (no k_hess follows).
+template <int RM>
+bool fold_grad(const kmx_pgo* h) {
+  return RM == RM_CONSUMER && h->P.method != KMX_METHOD_RGD && h->P.tcg_max_iterations > 0;
+}
+template <int RM>
+bool fold_cost(const kmx_pgo* h) {
+  return RM == RM_CONSUMER && (h->P.rtr_iterations == 1 || h->P.method == KMX_METHOD_RGD);
+}
+
+template <int R, int RW, int RM>
+void enqueue_grad_t(kmx_pgo* h) {
+  hipLaunchKernelGGL((k_grad<R, RW, RM>), dim3(h->ntiles), dim3(BLOCK), SmemHG<R>::bytes, h->stream, h->dv);
+  if (!fold_grad<RM>(h)) red_t<R, RM>(h, RED_GRAD);
+}
+
+template <int R, int RW, int RM>
+void enqueue_tcg_t(kmx_pgo* h) {
+  const dim3 grid(h->ntiles), blk(BLOCK);
+  // tCG: each step is (k_hess, k_update); with polling, exactly one step
+  // stays queued beyond the last one known to be needed
+  unsigned long long prev = 0;
+  for (int j = 0; j < h->P.tcg_max_iterations; ++j) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int slot = -1;
+    if (h->timing && h->ev_used / 2 < (size_t)HV_SLOTS) {
+      slot = (int)(h->ev_used / 2);
+      e0 = next_event(h);
+      e1 = next_event(h);
+      (void)hipEventRecord(e0, h->stream);
+    }
+    const bool poll = h->poll && h->hstat;
+    const unsigned long long seq = poll ? ++h->seq : 0;
+    HostStatus* hs = poll ? h->hstat : nullptr;
+    if constexpr (RM == RM_CONSUMER) {
+      // k_hess reports the stop test of the previous step's update
+      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, hs, seq);
+      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+      hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, 0ull, slot);
+      if (poll && j > 0 && !wait_running(h, seq)) break;
+      continue;
+    }
+    hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, nullptr, 0ull);
+    if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+    if (RM != RM_HALF) red_t<R, RM>(h, RED_HESS, nullptr, 0, slot);
+    hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv,
+                       RM == RM_TICKET ? hs : nullptr, seq, RM == RM_HALF ? slot : -1);
+    red_t<R, RM>(h, RED_UPDATE, hs, seq, -1, nullptr, RM == RM_HALF ? h->dv.ctl2 : nullptr);
+    if (poll) {
+      if (j > 0 && !wait_running(h, prev)) break;
+      prev = seq;
+    }
+  }
+}
+
+// after the tCG loop (or the RGD step): trial point and its cost
+template <int R, int RW, int RM>
+void enqueue_trial_t(kmx_pgo* h, bool rgd) {
+  const dim3 grid(h->ntiles), blk(BLOCK);
+  // RM_CONSUMER: the last step's update has no k_hess after it; k_retract
+  // reduces it
+  hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv, RM == RM_CONSUMER && !rgd ? 1 : 0);
+  hipLaunchKernelGGL((k_cost<R, RW, RM>), grid, blk, SmemC<R>::bytes, h->stream, h->dv);
+  if (!fold_cost<RM>(h)) red_t<R, RM>(h, RED_COST);
+}
+
 template <int R, int RW, int RM>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
-  const dim3 grid(h->ntiles), blk(BLOCK);
-  auto red = [&](int kind, HostStatus* hs = nullptr, unsigned long long seq = 0, int slot = -1,
-                 const double* src = nullptr, const Ctl* from = nullptr) {
-    if (RM != RM_TICKET)
-      hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot, src,
-                         from);
-  };
   enqueue_begin(h, d_active, BEGIN_ROUND);
   const bool rgd = h->P.method == KMX_METHOD_RGD;
   for (int it = 0; it < (rgd ? 1 : h->P.rtr_iterations); ++it) {
-    hipLaunchKernelGGL((k_grad<R, RW, RM>), grid, blk, SmemHG<R>::bytes, h->stream, h->dv);
-    red(RED_GRAD);
-    // tCG: each step is (k_hess, k_update); with polling, exactly one step
-    // stays queued beyond the last one known to be needed
-    unsigned long long prev = 0;
-    for (int j = 0; j < (rgd ? 0 : h->P.tcg_max_iterations); ++j) {
-      hipEvent_t e0 = nullptr, e1 = nullptr;
-      int slot = -1;
-      if (h->timing && h->ev_used / 2 < (size_t)HV_SLOTS) {
-        slot = (int)(h->ev_used / 2);
-        e0 = next_event(h);
-        e1 = next_event(h);
-        (void)hipEventRecord(e0, h->stream);
-      }
-      const bool poll = h->poll && h->hstat;
-      const unsigned long long seq = poll ? ++h->seq : 0;
-      HostStatus* hs = poll ? h->hstat : nullptr;
-      if constexpr (RM == RM_CONSUMER) {
-        // k_hess reports the stop test of the previous step's update
-        hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, hs, seq);
-        if (slot >= 0) (void)hipEventRecord(e1, h->stream);
-        hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, 0ull, slot);
-        if (poll && j > 0 && !wait_running(h, seq)) break;
-        continue;
-      }
-      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, nullptr, 0ull);
-      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
-      if (RM != RM_HALF) red(RED_HESS, nullptr, 0, slot);
-      hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv,
-                         RM == RM_TICKET ? hs : nullptr, seq, RM == RM_HALF ? slot : -1);
-      red(RED_UPDATE, hs, seq, -1, nullptr, RM == RM_HALF ? h->dv.ctl2 : nullptr);
-      if (poll) {
-        if (j > 0 && !wait_running(h, prev)) break;
-        prev = seq;
-      }
-    }
-    // RM_CONSUMER: the last step's update has no k_hess after it
-    if (RM == RM_CONSUMER && !rgd) red(RED_UPDATE, nullptr, 0, -1, h->dv.part_u);
-    hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv);
-    hipLaunchKernelGGL((k_cost<R, RW, RM>), grid, blk, SmemC<R>::bytes, h->stream, h->dv);
-    red(RED_COST);
+    enqueue_grad_t<R, RW, RM>(h);
+    if (!rgd) enqueue_tcg_t<R, RW, RM>(h);
+    enqueue_trial_t<R, RW, RM>(h, rgd);
   }
-  hipLaunchKernelGGL((k_commit<R>), grid, blk, 0, h->stream, h->dv);
+  hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0);
+}
+
+// Seam parts (one RTR iteration, RTR method): SEAM_HEAD = round begin +
+// gradient; SEAM_TAIL = trial + commit.
+enum { SEAM_TAIL = 1, SEAM_HEAD = 2 };
+template <int R, int RW, int RM>
+void enqueue_part_t(kmx_pgo* h, int part, const unsigned char* d_active) {
+  switch (part) {
+    case SEAM_HEAD:
+      enqueue_begin(h, d_active, BEGIN_ROUND);
+      enqueue_grad_t<R, RW, RM>(h);
+      break;
+    case SEAM_TAIL:
+      enqueue_trial_t<R, RW, RM>(h, false);
+      hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0);
+      break;
+    default:
+      enqueue_tcg_t<R, RW, RM>(h);
+      break;
+  }
 }
 
 template <int R>
@@ -2254,6 +2434,72 @@ void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
     if (h->rw == 12) enqueue_round_t<R, 12, RM_LAUNCH>(h, d_active);
     else enqueue_round_t<R, 16, RM_LAUNCH>(h, d_active);
   }
+}
+
+template <int R>
+void enqueue_part_r(kmx_pgo* h, int part, const unsigned char* d_active) {
+  if (h->rm == RM_CONSUMER) {
+    if (h->rw == 12) enqueue_part_t<R, 12, RM_CONSUMER>(h, part, d_active);
+    else enqueue_part_t<R, 16, RM_CONSUMER>(h, part, d_active);
+  } else if (h->rm == RM_HALF) {
+    if (h->rw == 12) enqueue_part_t<R, 12, RM_HALF>(h, part, d_active);
+    else enqueue_part_t<R, 16, RM_HALF>(h, part, d_active);
+  } else if (h->rm == RM_TICKET) {
+    if (h->rw == 12) enqueue_part_t<R, 12, RM_TICKET>(h, part, d_active);
+    else enqueue_part_t<R, 16, RM_TICKET>(h, part, d_active);
+  } else {
+    if (h->rw == 12) enqueue_part_t<R, 12, RM_LAUNCH>(h, part, d_active);
+    else enqueue_part_t<R, 16, RM_LAUNCH>(h, part, d_active);
+  }
+}
+// part: SEAM_HEAD, SEAM_TAIL, or 0 (the tCG loop)
+void enqueue_part(kmx_pgo* h, int part, const unsigned char* d_active) {
+  switch (h->P.r) {
+    case 3: enqueue_part_r<3>(h, part, d_active); break;
+    case 4: enqueue_part_r<4>(h, part, d_active); break;
+    case 5: enqueue_part_r<5>(h, part, d_active); break;
+    case 6: enqueue_part_r<6>(h, part, d_active); break;
+    case 7: enqueue_part_r<7>(h, part, d_active); break;
+    default: enqueue_part_r<8>(h, part, d_active); break;
+  }
+}
+
+// The launches between two tCG loops — the trial point, its cost and the
+// commit of one round, then the next round's begin and gradient — depend only
+// on the handle, so back-to-back rounds replay them from a hipGraph: one host
+// call instead of 9-11 launches while the device waits for them (the tCG stop
+// is known only when the last step posts it). Measured on the strong-scaling
+// floor (one 12.5k-pose block): 170.1 vs 167.7 us per round eager — the graph
+// launch moves the host latency to the first tCG step after it
+// (profiles/r02/small_round/2_*), so it is off by default.
+bool seams_usable(const kmx_pgo* h) {
+  return h->graphs && !h->timing && !h->P.acceleration && h->P.rtr_iterations == 1 &&
+         h->P.method != KMX_METHOD_RGD;
+}
+int launch_seam(kmx_pgo* h, int parts) {
+  const long long key[8] = {h->rm, h->rw, h->P.r, h->ntiles, h->n_gnc, h->gnc_on, h->P.robust_cost,
+                            (long long)(uintptr_t)h->d_active};
+  if (std::memcmp(key, h->seam_key, sizeof(key)) != 0 || std::memcmp(&h->dv, &h->seam_dv, sizeof(Dev)) != 0) {
+    drop_seams(h);
+    std::memcpy(h->seam_key, key, sizeof(key));
+    std::memcpy(&h->seam_dv, &h->dv, sizeof(Dev));
+  }
+  if (!h->seam[parts]) {
+    hipGraph_t g = nullptr;
+    KMX_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    if (parts & SEAM_TAIL) enqueue_part(h, SEAM_TAIL, h->d_active);
+    if (parts & SEAM_HEAD) enqueue_part(h, SEAM_HEAD, h->d_active);
+    const hipError_t e = hipStreamEndCapture(h->stream, &g);
+    if (e != hipSuccess) {
+      if (g) (void)hipGraphDestroy(g);
+      KMX_HIP(e);
+    }
+    const hipError_t ei = hipGraphInstantiate(&h->seam[parts], g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    KMX_HIP(ei);
+  }
+  KMX_HIP(hipGraphLaunch(h->seam[parts], h->stream));
+  return KMX_OK;
 }
 
 // One RBCD round for the robots whose d_active flag is set; it starts with
@@ -2353,6 +2599,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   }
   h->own_stream = true;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
+  if (const char* v = std::getenv("KMX_GRAPH")) h->graphs = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_QUERY")) h->query = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);
@@ -2924,10 +3171,18 @@ extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local) 
   // every round's k_commit republishes the committed owned rows, so the
   // single-device exchange needs one publish per call
   if (refresh_local && rounds > 0) enqueue_publish(h);
-  for (int i = 0; i < rounds; ++i) {
-    enqueue_accel_pre(h);  // publishes Y itself
-    enqueue_round(h, h->d_active);
-    enqueue_accel_post(h);
+  if (seams_usable(h) && rounds > 0) {
+    enqueue_part(h, SEAM_HEAD, h->d_active);
+    for (int i = 0; i < rounds; ++i) {
+      enqueue_part(h, 0, h->d_active);  // the tCG loop
+      if (int rc = launch_seam(h, i + 1 < rounds ? SEAM_TAIL | SEAM_HEAD : SEAM_TAIL)) return rc;
+    }
+  } else {
+    for (int i = 0; i < rounds; ++i) {
+      enqueue_accel_pre(h);  // publishes Y itself
+      enqueue_round(h, h->d_active);
+      enqueue_accel_post(h);
+    }
   }
   KMX_HIP(hipGetLastError());
   return KMX_OK;

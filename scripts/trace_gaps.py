@@ -26,3 +26,9 @@ for i in range(len(seq) - 1):
     gap[(nm(seq[i][2]), nm(seq[i + 1][2]))].append((seq[i + 1][0] - seq[i][1]) / 1e3)
 for k, v in sorted(gap.items(), key=lambda kv: -sum(kv[1])):
     print(f"{k[0]:>10s} -> {k[1]:10s} n={len(v):4d} mean gap {sum(v) / len(v):6.2f} us, total/round {sum(v) / 10:7.1f} us")
+
+kt = defaultdict(list)
+for a, b, n in seq:
+    kt[nm(n)].append((b - a) / 1e3)
+for k, v in sorted(kt.items(), key=lambda kv: -sum(kv[1])):
+    print(f"{k:>10s} n/round={len(v) / 10:5.1f} mean {sum(v) / len(v):6.2f} us, total/round {sum(v) / 10:7.1f} us")

@@ -109,15 +109,15 @@ def test_commands_on_device(gpu):
     g, P = _graph(), _params()
     drv = RBCDDriver(P, g, device=0)
     drv.initialize(_x0(g))
-    drv.run(max_rounds=10, check_every=5)
+    drv.run(max_rounds=12, check_every=6)
     assert drv.weight_updates >= 2
     drv.handle_command(Command(0, CommandType.HARD_TERMINATE))
     assert drv.weight_updates == 0 and np.all(np.isinf(drv.solver.status()))
     drv.handle_command(Command(0, CommandType.INITIALIZE))
-    X1, w1 = _run(drv, 9)
+    X1, w1 = _run(drv, 12)
     fresh = RBCDDriver(P, g, device=0)
     fresh.initialize(_x0(g))
-    X2, w2 = _run(fresh, 9)
+    X2, w2 = _run(fresh, 12)
     assert drv.weight_updates == fresh.weight_updates >= 2
     assert np.array_equal(w1, w2)
     for a in range(g.n_robots):
