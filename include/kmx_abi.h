@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KMX_ABI_VERSION 3
+#define KMX_ABI_VERSION 4
 
 /* error codes */
 #define KMX_OK 0
@@ -89,7 +89,11 @@ typedef struct kmx_pgo_params {
   int method;               /* KMX_METHOD_RTR (0) or KMX_METHOD_RGD (1)                  */
   int reserved0;
   double rgd_stepsize;      /* RGD: X <- Retr_X(-s * precon(grad f)) (1e-3)              */
-  int reserved[2];
+  int tile_incidences;      /* incidences per workgroup tile (0: from the handle's local
+                               problem, 180..2 chunks; the tile cut orders the per-robot
+                               reductions, so handles that must agree bit for bit across
+                               placements set the same value)                            */
+  int reserved;
 } kmx_pgo_params;
 
 /* Per-robot statistics of one RBCD round (what dpgo logs to dpgo_log_*.csv via

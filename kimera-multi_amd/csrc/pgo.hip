@@ -1042,6 +1042,7 @@ __device__ void control(const Dev& d, int l, int kind, const double* tot, int R_
 // RM_LAUNCH: one workgroup per robot reduces the robot's tile partials in
 // tile order and runs the control logic (after k_update it also reports the
 // robot's tCG progress to the host).
+constexpr int TILES_TARGET = 736;  // tile count the cut of small problems aims at (set_graph)
 constexpr int RBLOCK = 256;  // k_reduce: one workgroup per robot (1024 threads measured slower: 6.3 vs 4.6 us)
 static_assert(RBLOCK == BLOCK, "robot_sum runs in k_reduce and in the tCG kernels");
 // Sum of NS partials (row stride `stride`) over tiles [t0, t1) of a robot by
@@ -2585,6 +2586,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   KMX_CHECK(params->method == KMX_METHOD_RTR || params->method == KMX_METHOD_RGD, KMX_EUNSUP,
             "method must be KMX_METHOD_RTR or KMX_METHOD_RGD");
   KMX_CHECK(params->method != KMX_METHOD_RGD || params->rgd_stepsize > 0.0, KMX_EINVAL, "rgd_stepsize must be > 0");
+  KMX_CHECK(params->tile_incidences >= 0, KMX_EINVAL, "tile_incidences must be >= 0 (0: automatic)");
   int ndev = 0;
   KMX_HIP(hipGetDeviceCount(&ndev));
   KMX_CHECK(device >= 0 && device < ndev, KMX_EINVAL, "bad HIP device ordinal");
@@ -2816,7 +2818,19 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   // and capped at two chunks of TP * r incidences (two LDS hand-offs in k_hess)
   const int TP = WAVES * (64 / r);
   std::vector<int> tr, tp0, tnp, rt0(L + 1, 0);
-  const int64_t tilecap = 2 * (int64_t)TP * r;
+  // incidences per tile: at most two gather chunks; small problems are cut
+  // finer, to about TILES_TARGET tiles (3 workgroups per CU, one generation),
+  // but not below 180 (3/4 of a chunk). Measured on one 12.5k-pose block
+  // (125k incidences): 160.0 / 156.5 / 154.9 / 152.6 us per round at caps
+  // 480 / 360 / 240 / 180, 207 at 120 (> 1024 tiles: a second generation);
+  // 25k poses: 254.7 at 480, 245.6 at 360, 301 at 240
+  // (profiles/r02/small_round/5_tile_cap.log). kmx_pgo_params.tile_incidences
+  // (the multi-rank driver sets it from the team) or KMX_TILE_CAP override.
+  int64_t inc_all = (int64_t)inc_ptr[nloc] - inc_ptr[0];
+  int64_t tilecap = std::min<int64_t>(2 * (int64_t)TP * r,
+                                      std::max<int64_t>(180, (inc_all + TILES_TARGET - 1) / TILES_TARGET));
+  if (h->P.tile_incidences > 0) tilecap = std::max(16, h->P.tile_incidences);
+  if (const char* v = std::getenv("KMX_TILE_CAP")) tilecap = std::max(16, std::atoi(v));
   for (int l = 0; l < L; ++l) {
     const int n = n_poses[h->robots[l]];
     const int base = h->loff[l];

@@ -17,7 +17,7 @@ import numpy as np
 _LIB_PATH = Path(__file__).resolve().parent / "libkmx.so"
 
 KMX_OK = 0
-ABI_VERSION = 3  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
+ABI_VERSION = 4  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
 KMX_COST_L2 = 0
 KMX_COST_GNC_TLS = 1
 KMX_SCHEDULE_SEQUENTIAL = 0
@@ -51,7 +51,8 @@ class PgoParams(C.Structure):
         ("precond_shift", C.c_double), ("robust_cost", C.c_int),
         ("gnc_barc", C.c_double), ("gnc_mu_init", C.c_double),
         ("gnc_mu_step", C.c_double), ("acceleration", C.c_int), ("restart_interval", C.c_int),
-        ("method", C.c_int), ("reserved0", C.c_int), ("rgd_stepsize", C.c_double), ("reserved", C.c_int * 2),
+        ("method", C.c_int), ("reserved0", C.c_int), ("rgd_stepsize", C.c_double), ("tile_incidences", C.c_int),
+        ("reserved", C.c_int),
     ]
 
 

@@ -88,6 +88,19 @@ def exchange_plan(graph, world: int, rank: int):
             need_slot[rm], np.bincount(owner[rm], minlength=world)[:world])
 
 
+TILES_TARGET = 736  # csrc/pgo.hip: the tile count the cut of small problems aims at
+
+
+def team_tile_incidences(graph, world: int, r: int) -> int:
+    """The tile cut (incidences per workgroup tile) kmx_pgo_set_graph picks
+    automatically for a handle holding 1/world of the team's incidences; the
+    multi-rank driver passes it to every rank, so all ranks cut their robots
+    alike whatever their share (csrc/pgo.hip set_graph)."""
+    tp = 4 * (64 // r)
+    inc = 2 * int(graph.m) // max(world, 1)
+    return min(2 * tp * r, max(180, -(-inc // TILES_TARGET)))
+
+
 class RBCDDriver:
     def __init__(self, params: PGOAgentParameters, graph, *, rank: int = 0, world: int = 1,
                  device: int = 0, solver=None, exchange_device: str | None = None, log_dir: str | None = None,
@@ -110,6 +123,10 @@ class RBCDDriver:
         local = np.zeros(graph.n_robots, np.uint8)
         local[lo:hi] = 1
         self.local = local
+        if solver is None and world > 1 and params.tileIncidences == 0:
+            import dataclasses
+            params = dataclasses.replace(params, tileIncidences=team_tile_incidences(graph, world, params.r))
+            self.params = params
         self.solver = solver if solver is not None else BlockSolver(params, device)
         self.executing = ExecutingRobot(params.updateRule, params.randomSeed)
         self.round_index = 0

@@ -74,6 +74,7 @@ class PGOAgentParameters:
     randomSeed: int = 0                    # seed of the uniform rule's std::mt19937 (dpgo_ros random_seed)
     acceleration: bool = False             # Nesterov-accelerated RBCD (dpgo acceleration; concurrent schedule)
     restartInterval: int = 30              # acceleration restart period in rounds (dpgo restartInterval [U])
+    tileIncidences: int = 0                # kmx: incidences per workgroup tile (0: from the handle's problem)
 
     def to_c(self) -> PgoParams:
         lo, rc = self.localOptimizationParams, self.robustCostParams
@@ -92,4 +93,5 @@ class PGOAgentParameters:
         p.rgd_stepsize = float(lo.RGD_stepsize)
         p.acceleration = 1 if self.acceleration else 0
         p.restart_interval = int(self.restartInterval)
+        p.tile_incidences = int(self.tileIncidences)
         return p

@@ -128,3 +128,25 @@ def test_commands_on_device(gpu):
     for a in range(g.n_robots):
         same = np.array_equal(drv.iterate_of(a), X1[a])
         assert same == (a in (0, 2)), a
+
+
+@pytest.mark.timeout(300)
+def test_tile_cut_rule_matches_handle(gpu):
+    """The driver's team_tile_incidences (what every rank of a multi-rank team
+    is given) reproduces the cut kmx_pgo_set_graph picks on its own for the
+    whole team: passing it explicitly leaves a single-handle run bit for bit
+    unchanged (25k poses, 250k incidences: a cut above the 180 floor)."""
+    import dataclasses
+    from kmx.dpgo.driver import RBCDDriver, team_tile_incidences
+    g = make_pose_graph(2, 25_000, 125_000, seed=7)
+    P = _params()
+    cap = team_tile_incidences(g, 1, P.r)
+    assert 180 < cap < 480
+    out = []
+    for Pk in (P, dataclasses.replace(P, tileIncidences=cap)):
+        drv = RBCDDriver(Pk, g, device=0)
+        drv.initialize(_x0(g))
+        out.append(_run(drv, 6))
+        drv.solver.close()
+    for a in range(g.n_robots):
+        assert np.array_equal(out[0][0][a], out[1][0][a]), a
