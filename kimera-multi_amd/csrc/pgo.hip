@@ -205,27 +205,31 @@ __device__ __forceinline__ int2 unpack_int2(double v) {
   return make_int2((int)(b & 0xffffffffll), (int)(b >> 32));
 }
 
-// RW = 12: compact record (R rows 0-1, t, w kappa, w tau, {other, edge|tail});
-// RW = 16: full record (R, t, w kappa, w tau, {other, edge|tail}, pad).
+// RW = 10: compact record (unit quaternion of R, t, w kappa, w tau,
+// {other, edge|tail}) — 80 B, five 16-B parts; the gathers rebuild R from the
+// quaternion (R R^T = I to rounding, as the preconditioner assumes).
+// RW = 16: full record (R, t, w kappa, w tau, {other, edge|tail}, pad), for
+// measurement rotations off SO(3).
 template <int RW>
 struct Rec {
   static constexpr int Q = RW / 2;        // 16-B parts
-  static constexpr int WK = RW == 12 ? 9 : 12;  // index of w kappa (w tau follows)
+  static constexpr int WK = RW == 10 ? 7 : 12;  // index of w kappa (w tau follows)
   __device__ static __forceinline__ void load(const double* base, size_t k, double2 q[Q]) {
     const double2* q2 = reinterpret_cast<const double2*>(base + (size_t)RW * k);
 #pragma unroll
     for (int i = 0; i < Q; ++i) q[i] = q2[i];
   }
   __device__ static __forceinline__ void edge(const double2 q[Q], Edge& E) {
-    if constexpr (RW == 12) {
-      E.R[0] = q[0].x; E.R[1] = q[0].y; E.R[2] = q[1].x;
-      E.R[3] = q[1].y; E.R[4] = q[2].x; E.R[5] = q[2].y;
-      E.R[6] = E.R[1] * E.R[5] - E.R[2] * E.R[4];
-      E.R[7] = E.R[2] * E.R[3] - E.R[0] * E.R[5];
-      E.R[8] = E.R[0] * E.R[4] - E.R[1] * E.R[3];
-      E.t[0] = q[3].x; E.t[1] = q[3].y; E.t[2] = q[4].x;
-      E.wk = q[4].y;
-      E.wt = q[5].x;
+    if constexpr (RW == 10) {
+      const double w = q[0].x, x = q[0].y, y = q[1].x, z = q[1].y;
+      const double xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
+      const double wx = w * x, wy = w * y, wz = w * z;
+      E.R[0] = 1.0 - 2.0 * (yy + zz); E.R[1] = 2.0 * (xy - wz); E.R[2] = 2.0 * (xz + wy);
+      E.R[3] = 2.0 * (xy + wz); E.R[4] = 1.0 - 2.0 * (xx + zz); E.R[5] = 2.0 * (yz - wx);
+      E.R[6] = 2.0 * (xz - wy); E.R[7] = 2.0 * (yz + wx); E.R[8] = 1.0 - 2.0 * (xx + yy);
+      E.t[0] = q[2].x; E.t[1] = q[2].y; E.t[2] = q[3].x;
+      E.wk = q[3].y;
+      E.wt = q[4].x;
     } else {
       E.R[0] = q[0].x; E.R[1] = q[0].y; E.R[2] = q[1].x; E.R[3] = q[1].y; E.R[4] = q[2].x;
       E.R[5] = q[2].y; E.R[6] = q[3].x; E.R[7] = q[3].y; E.R[8] = q[4].x;
@@ -235,7 +239,7 @@ struct Rec {
     }
   }
   __device__ static __forceinline__ int2 inc(const double2 q[Q]) {
-    return unpack_int2(RW == 12 ? q[5].y : q[7].x);
+    return unpack_int2(RW == 10 ? q[4].y : q[7].x);
   }
 };
 
@@ -1716,7 +1720,7 @@ __global__ void k_precond(Dev d, int gated) {
         for (int i = 0; i < 3; ++i) {
           for (int j = 0; j < 3; ++j) {
             A[i * 4 + j] += wt * tt[i] * tt[j] + (i == j ? wk : 0.0);
-            const double rr = (RW == 12) ? (i == j ? 1.0 : 0.0)
+            const double rr = (RW == 10) ? (i == j ? 1.0 : 0.0)
                                          : E.R[i * 3 + 0] * E.R[j * 3 + 0] + E.R[i * 3 + 1] * E.R[j * 3 + 1] +
                                                E.R[i * 3 + 2] * E.R[j * 3 + 2];
             Dq[i * 4 + j] += wt * tt[i] * tt[j] + wk * rr;
@@ -2063,7 +2067,7 @@ struct kmx_pgo {
   int mloc = 0;
   std::vector<int64_t> loc_edge_gid;
   int ninc = 0;
-  int rw = 12;  // record width (12 compact / 16 full)
+  int rw = 10;  // record width in doubles (10 compact quaternion / 16 full)
   int64_t nshared = 0;
   int n_sh_local = 0, n_gnc = 0, n_osh = 0;
   std::vector<long long> m_robot;
@@ -2146,6 +2150,37 @@ struct kmx_pgo {
 };
 
 namespace {
+
+// Unit quaternion (w, x, y, z) of a rotation matrix (row-major), by the
+// largest of the four diagonal combinations (Shepperd), and back.
+void rot_to_quat(const double* R, double* q) {
+  const double tr = R[0] + R[4] + R[8];
+  double w, x, y, z;
+  if (tr > 0.0) {
+    const double s = 2.0 * std::sqrt(tr + 1.0);
+    w = 0.25 * s; x = (R[7] - R[5]) / s; y = (R[2] - R[6]) / s; z = (R[3] - R[1]) / s;
+  } else if (R[0] > R[4] && R[0] > R[8]) {
+    const double s = 2.0 * std::sqrt(1.0 + R[0] - R[4] - R[8]);
+    w = (R[7] - R[5]) / s; x = 0.25 * s; y = (R[1] + R[3]) / s; z = (R[2] + R[6]) / s;
+  } else if (R[4] > R[8]) {
+    const double s = 2.0 * std::sqrt(1.0 + R[4] - R[0] - R[8]);
+    w = (R[2] - R[6]) / s; x = (R[1] + R[3]) / s; y = 0.25 * s; z = (R[5] + R[7]) / s;
+  } else {
+    const double s = 2.0 * std::sqrt(1.0 + R[8] - R[0] - R[4]);
+    w = (R[3] - R[1]) / s; x = (R[2] + R[6]) / s; y = (R[5] + R[7]) / s; z = 0.25 * s;
+  }
+  const double n = std::sqrt(w * w + x * x + y * y + z * z);
+  q[0] = w / n; q[1] = x / n; q[2] = y / n; q[3] = z / n;
+}
+// the device's Rec<10>::edge expressions
+void quat_to_rot(const double* q, double* R) {
+  const double w = q[0], x = q[1], y = q[2], z = q[3];
+  const double xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
+  const double wx = w * x, wy = w * y, wz = w * z;
+  R[0] = 1.0 - 2.0 * (yy + zz); R[1] = 2.0 * (xy - wz); R[2] = 2.0 * (xz + wy);
+  R[3] = 2.0 * (xy + wz); R[4] = 1.0 - 2.0 * (xx + zz); R[5] = 2.0 * (yz - wx);
+  R[6] = 2.0 * (xz - wy); R[7] = 2.0 * (yz + wx); R[8] = 1.0 - 2.0 * (xx + yy);
+}
 
 template <typename T>
 int dalloc(T** p, size_t count) {
@@ -2267,7 +2302,7 @@ void enqueue_precond_t(kmx_pgo* h, int gated) {
   hipLaunchKernelGGL(k_precond<RW>, dim3(blocks), dim3(128), 0, h->stream, h->dv, gated);
 }
 void enqueue_precond(kmx_pgo* h, int gated) {
-  if (h->rw == 12) enqueue_precond_t<12>(h, gated);
+  if (h->rw == 10) enqueue_precond_t<10>(h, gated);
   else enqueue_precond_t<16>(h, gated);
 }
 
@@ -2278,8 +2313,8 @@ void enqueue_begin(kmx_pgo* h, const unsigned char* d_active, int mode) {
   if (!may_fire) mode |= BEGIN_SOLO;  // no weight update possible: one block, no preconditioner rebuild
   // a capped grid: when the schedule does not fire, the launch costs its dispatch
   const unsigned grid = may_fire ? 1 + (unsigned)std::min(256, std::max(1, (h->n_gnc + 255) / 256)) : 1;
-  if (h->rw == 12)
-    hipLaunchKernelGGL(k_begin<12>, dim3(grid), dim3(256), 0, h->stream, h->dv, d_active, mode, h->P.r);
+  if (h->rw == 10)
+    hipLaunchKernelGGL(k_begin<10>, dim3(grid), dim3(256), 0, h->stream, h->dv, d_active, mode, h->P.r);
   else
     hipLaunchKernelGGL(k_begin<16>, dim3(grid), dim3(256), 0, h->stream, h->dv, d_active, mode, h->P.r);
   if (may_fire) enqueue_precond(h, 1);
@@ -2423,16 +2458,16 @@ void enqueue_part_t(kmx_pgo* h, int part, const unsigned char* d_active) {
 template <int R>
 void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
   if (h->rm == RM_CONSUMER) {
-    if (h->rw == 12) enqueue_round_t<R, 12, RM_CONSUMER>(h, d_active);
+    if (h->rw == 10) enqueue_round_t<R, 10, RM_CONSUMER>(h, d_active);
     else enqueue_round_t<R, 16, RM_CONSUMER>(h, d_active);
   } else if (h->rm == RM_HALF) {
-    if (h->rw == 12) enqueue_round_t<R, 12, RM_HALF>(h, d_active);
+    if (h->rw == 10) enqueue_round_t<R, 10, RM_HALF>(h, d_active);
     else enqueue_round_t<R, 16, RM_HALF>(h, d_active);
   } else if (h->rm == RM_TICKET) {
-    if (h->rw == 12) enqueue_round_t<R, 12, RM_TICKET>(h, d_active);
+    if (h->rw == 10) enqueue_round_t<R, 10, RM_TICKET>(h, d_active);
     else enqueue_round_t<R, 16, RM_TICKET>(h, d_active);
   } else {
-    if (h->rw == 12) enqueue_round_t<R, 12, RM_LAUNCH>(h, d_active);
+    if (h->rw == 10) enqueue_round_t<R, 10, RM_LAUNCH>(h, d_active);
     else enqueue_round_t<R, 16, RM_LAUNCH>(h, d_active);
   }
 }
@@ -2440,16 +2475,16 @@ void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
 template <int R>
 void enqueue_part_r(kmx_pgo* h, int part, const unsigned char* d_active) {
   if (h->rm == RM_CONSUMER) {
-    if (h->rw == 12) enqueue_part_t<R, 12, RM_CONSUMER>(h, part, d_active);
+    if (h->rw == 10) enqueue_part_t<R, 10, RM_CONSUMER>(h, part, d_active);
     else enqueue_part_t<R, 16, RM_CONSUMER>(h, part, d_active);
   } else if (h->rm == RM_HALF) {
-    if (h->rw == 12) enqueue_part_t<R, 12, RM_HALF>(h, part, d_active);
+    if (h->rw == 10) enqueue_part_t<R, 10, RM_HALF>(h, part, d_active);
     else enqueue_part_t<R, 16, RM_HALF>(h, part, d_active);
   } else if (h->rm == RM_TICKET) {
-    if (h->rw == 12) enqueue_part_t<R, 12, RM_TICKET>(h, part, d_active);
+    if (h->rw == 10) enqueue_part_t<R, 10, RM_TICKET>(h, part, d_active);
     else enqueue_part_t<R, 16, RM_TICKET>(h, part, d_active);
   } else {
-    if (h->rw == 12) enqueue_part_t<R, 12, RM_LAUNCH>(h, part, d_active);
+    if (h->rw == 10) enqueue_part_t<R, 10, RM_LAUNCH>(h, part, d_active);
     else enqueue_part_t<R, 16, RM_LAUNCH>(h, part, d_active);
   }
 }
@@ -2564,7 +2599,7 @@ void enqueue_apply_weights_t(kmx_pgo* h) {
     hipLaunchKernelGGL(k_apply_weights<RW>, dim3((h->mloc + 255) / 256), dim3(256), 0, h->stream, h->dv, h->mloc);
 }
 void enqueue_apply_weights(kmx_pgo* h) {
-  if (h->rw == 12) enqueue_apply_weights_t<12>(h);
+  if (h->rw == 10) enqueue_apply_weights_t<10>(h);
   else enqueue_apply_weights_t<16>(h);
   enqueue_precond(h, 0);
 }
@@ -2730,16 +2765,20 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     if (a1 >= 0) { deg[lpose(r1[e], p1[e])]++; h->m_robot[a1]++; }
     if (a2 >= 0) { deg[lpose(r2[e], p2[e])]++; if (r2[e] != r1[e]) h->m_robot[a2]++; }
   }
-  // record width: compact when every local measurement rotation's third row is
-  // row0 x row1 to 1e-12 (the gathers rebuild it), the full rotation otherwise
+  // record width: compact (quaternion) when every local measurement rotation
+  // is rebuilt from its unit quaternion to 1e-12 (a rotation), full otherwise
+  std::vector<double> quat((size_t)std::max(h->mloc, 1) * 4);
   {
     bool ok = true;
     for (int k = 0; k < h->mloc && ok; ++k) {
       const double* Q = R + 9 * ledges[k];
-      const double c0 = Q[1] * Q[5] - Q[2] * Q[4], c1 = Q[2] * Q[3] - Q[0] * Q[5], c2 = Q[0] * Q[4] - Q[1] * Q[3];
-      ok = std::fabs(c0 - Q[6]) <= 1e-12 && std::fabs(c1 - Q[7]) <= 1e-12 && std::fabs(c2 - Q[8]) <= 1e-12;
+      double* qk = &quat[4 * (size_t)k];
+      rot_to_quat(Q, qk);
+      double Rq[9];
+      quat_to_rot(qk, Rq);
+      for (int i = 0; i < 9 && ok; ++i) ok = std::fabs(Rq[i] - Q[i]) <= 1e-12;
     }
-    h->rw = ok ? 12 : 16;
+    h->rw = ok ? 10 : 16;
   }
   const int RW = h->rw;
   std::vector<int> inc_ptr(nloc + 1, 0);
@@ -2748,11 +2787,11 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   std::vector<double> rec((size_t)(h->ninc + 1) * RW, 0.0);  // + one zero pad record
   std::vector<int2> eipos(std::max(h->mloc, 1), make_int2(-1, -1));
   std::vector<int> fill(inc_ptr.begin(), inc_ptr.end() - 1);
-  auto put_rec = [&](int pos, int64_t e, int other, int code) {
+  auto put_rec = [&](int pos, int k, int64_t e, int other, int code) {
     double* c = &rec[(size_t)pos * RW];
-    const double* Q = R + 9 * e;
+    const double* Q = RW == 10 ? &quat[4 * (size_t)k] : R + 9 * e;
     int j = 0;
-    for (int q = 0; q < (RW == 12 ? 6 : 9); ++q) c[j++] = Q[q];
+    for (int q = 0; q < (RW == 10 ? 4 : 9); ++q) c[j++] = Q[q];
     for (int q = 0; q < 3; ++q) c[j++] = t[3 * e + q];
     c[j++] = weight[e] * kappa[e];
     c[j++] = weight[e] * tau[e];
@@ -2766,13 +2805,13 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       const int sp = lpose(r1[e], p1[e]);
       const int other = priv ? lpose(r2[e], p2[e]) : (int)(-1 - slot_of(r2[e], p2[e]));
       eipos[k].x = fill[sp];
-      put_rec(fill[sp]++, e, other, (int)(k | 0x80000000u));
+      put_rec(fill[sp]++, k, e, other, (int)(k | 0x80000000u));
     }
     if (h->local_of[r2[e]] >= 0) {
       const int sp = lpose(r2[e], p2[e]);
       const int other = priv ? lpose(r1[e], p1[e]) : (int)(-1 - slot_of(r1[e], p1[e]));
       eipos[k].y = fill[sp];
-      put_rec(fill[sp]++, e, other, k);
+      put_rec(fill[sp]++, k, e, other, k);
     }
   }
   // GNC: every non-fixed local edge is re-weighted here (a shared loop closure
@@ -3396,8 +3435,8 @@ extern "C" int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, do
   KMX_HIP(hipMemsetAsync(h->d_scratch, 0, sizeof(double) * vec * 2, h->stream));
   if (V) KMX_HIP(hipMemcpyAsync(dV + o, V, sizeof(double) * n * ps, hipMemcpyHostToDevice, h->stream));
 #define KMX_EVAL_LAUNCH(RR)                                                                                      \
-  if (h->rw == 12)                                                                                               \
-    hipLaunchKernelGGL((k_eval<RR, 12>), dim3(h->ntiles), dim3(BLOCK), SmemE<RR>::bytes, h->stream, h->dv, l, mode, \
+  if (h->rw == 10)                                                                                               \
+    hipLaunchKernelGGL((k_eval<RR, 10>), dim3(h->ntiles), dim3(BLOCK), SmemE<RR>::bytes, h->stream, h->dv, l, mode, \
                        (const double*)dV, dO);                                                                   \
   else                                                                                                           \
     hipLaunchKernelGGL((k_eval<RR, 16>), dim3(h->ntiles), dim3(BLOCK), SmemE<RR>::bytes, h->stream, h->dv, l, mode, \
