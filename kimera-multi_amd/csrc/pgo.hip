@@ -193,6 +193,24 @@ __device__ __forceinline__ void store4(double* p, const double v[4]) {
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops but
 // not for its outstanding global loads (__syncthreads waits vmcnt(0), which
 // would drain the next chunk's prefetched records).
+// Symmetric 4x4 blocks (Q's diagonal blocks, the preconditioner) are stored
+// as their upper triangle, row by row: 10 doubles, five 16-B loads.
+constexpr int SYM4 = 10;
+__device__ __forceinline__ void load_sym4(const double* p, double M[16]) {
+  const double2* p2 = reinterpret_cast<const double2*>(p);
+  const double2 a = p2[0], b = p2[1], c = p2[2], e = p2[3], f = p2[4];
+  M[0] = a.x; M[1] = M[4] = a.y; M[2] = M[8] = b.x; M[3] = M[12] = b.y;
+  M[5] = c.x; M[6] = M[9] = c.y; M[7] = M[13] = e.x;
+  M[10] = e.y; M[11] = M[14] = f.x;
+  M[15] = f.y;
+}
+// S = sym(Y^T G_Y) stored as its 6 upper entries
+__device__ __forceinline__ void load_sym3(const double* p, double S[9]) {
+  S[0] = p[0]; S[1] = S[3] = p[1]; S[2] = S[6] = p[2];
+  S[4] = p[3]; S[5] = S[7] = p[4];
+  S[8] = p[5];
+}
+
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ------------------------------------------------------------ edge records --
@@ -348,30 +366,18 @@ __device__ __forceinline__ void group_precon(const Dev& d, int pose, bool valid,
     return;
   }
   double buf[4] = {0.0, 0.0, 0.0, 0.0};
-  const double* Pp = d.Pinv + 16 * (size_t)pose;
-  if constexpr (LDS) {  // 128-VGPR kernels: all of P in flight (pose is valid on every lane)
-    double P[16];
-    if (has_pre) {
+  static_assert(LDS, "the LDS form only");
+  double P[16];
+  if (has_pre) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) P[i] = Pre[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) load4(Pp + 4 * i, P + 4 * i);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * P[k] : buf[k] + V[i] * P[4 * i + k];
-  } else {  // one 4-double row of P at a time (8 VGPRs of P live)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      double Pr[4] = {0.0, 0.0, 0.0, 0.0};
-      if (valid) load4(Pp + 4 * i, Pr);
-      asm volatile("" : "+v"(Pr[0]), "+v"(Pr[1]), "+v"(Pr[2]), "+v"(Pr[3]) : "v"(buf[0]));
-#pragma unroll
-      for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * Pr[k] : buf[k] + V[i] * Pr[k];
-    }
+    for (int i = 0; i < 16; ++i) P[i] = Pre[i];
+  } else {
+    load_sym4(d.Pinv + SYM4 * (size_t)pose, P);  // pose is valid on every lane
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) buf[k] = (i == 0) ? V[0] * P[k] : buf[k] + V[i] * P[4 * i + k];
   group_proj<R, LDS>(y, buf, base, out, scr);
 }
 
@@ -556,13 +562,11 @@ __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const d
   if (L.valid) {
     double vs[4];
     load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
-    const double* Dp = d.hD + 16 * (size_t)L.pose;
+    double D[16];
+    load_sym4(d.hD + SYM4 * (size_t)L.pose, D);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      double dr[4];
-      load4(Dp + 4 * c, dr);
-      acc[c] += vs[0] * dr[0] + vs[1] * dr[1] + vs[2] * dr[2] + vs[3] * dr[3];
-    }
+    for (int c = 0; c < 4; ++c)
+      acc[c] += vs[0] * D[4 * c] + vs[1] * D[4 * c + 1] + vs[2] * D[4 * c + 2] + vs[3] * D[4 * c + 3];
   }
   return true;
 }
@@ -1227,9 +1231,8 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d) {
     store4(d.g + o, gr);  // r = g at the start of tCG: k_update's first step reads g
     store4(d.z + o, zr);
     if (L.a == 0) {
-      double* Sp = d.S + 9 * (size_t)L.pose;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) Sp[i] = S[i];
+      double* Sp = d.S + 6 * (size_t)L.pose;
+      Sp[0] = S[0]; Sp[1] = S[1]; Sp[2] = S[2]; Sp[3] = S[4]; Sp[4] = S[5]; Sp[5] = S[8];
     }
   });
 }
@@ -1311,9 +1314,7 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
   if (L.valid) {
     load4(d.z + o, zs);
     load4(d.X + o, y);
-    const double* Sp = d.S + 9 * (size_t)L.pose;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) S[i] = Sp[i];
+    load_sym3(d.S + 6 * (size_t)L.pose, S);
   } else {
 #pragma unroll
     for (int i = 0; i < 9; ++i) S[i] = 0.0;
@@ -1387,9 +1388,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
       load4((first0 ? d.g : d.r) + o, rr);
       load4(d.X + o, y);  // used by the precon of interior steps (boundary steps are rare)
       if (d.p.use_precond) {  // the preconditioner block too: no load after the decision
-        const double* Pp = d.Pinv + 16 * (size_t)L.pose;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) load4(Pp + 4 * i, Pm + 4 * i);
+        load_sym4(d.Pinv + SYM4 * (size_t)L.pose, Pm);
       }
     }
     double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
@@ -1737,7 +1736,12 @@ __global__ void k_precond(Dev d, int gated) {
         Dq[0] += wk; Dq[5] += wk; Dq[10] += wk; Dq[15] += wt;
       }
     }
-    for (int i = 0; i < 16; ++i) d.hD[16 * (size_t)pose + i] = Dq[i];
+    {
+      double* Dp = d.hD + SYM4 * (size_t)pose;
+      int j = 0;
+      for (int a = 0; a < 4; ++a)
+        for (int b = a; b < 4; ++b) Dp[j++] = Dq[a * 4 + b];
+    }
     for (int j = 0; j < 4; ++j) A[j * 5] += d.p.shift;
     double Lm[16], Li[16];
     for (int i = 0; i < 16; ++i) { Lm[i] = 0.0; Li[i] = 0.0; }
@@ -1757,12 +1761,13 @@ __global__ void k_precond(Dev d, int gated) {
         for (int k = c; k < ii; ++k) s -= Lm[ii * 4 + k] * Li[k * 4 + c];
         Li[ii * 4 + c] = (ii < c) ? 0.0 : s / Lm[ii * 4 + ii];
       }
-    double* Pi = d.Pinv + 16 * (size_t)pose;
+    double* Pi = d.Pinv + SYM4 * (size_t)pose;  // Li^T Li: symmetric (upper triangle)
+    int j = 0;
     for (int x = 0; x < 4; ++x)
-      for (int y = 0; y < 4; ++y) {
+      for (int y = x; y < 4; ++y) {
         double s = 0.0;
         for (int k = 0; k < 4; ++k) s += Li[k * 4 + x] * Li[k * 4 + y];
-        Pi[x * 4 + y] = s;
+        Pi[j++] = s;
       }
   }
 }
@@ -2912,9 +2917,9 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_rec, rec.size())) ||
       (rc = dalloc(&h->d_ekappa, ek_h.size())) || (rc = dalloc(&h->d_etau, et_h.size())) ||
       (rc = dalloc(&h->d_ew, ew_h.size())) || (rc = dalloc(&h->d_eipos, eipos.size())) ||
-      (rc = dalloc(&h->d_vec, vec * 8)) || (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 9)) ||
-      (rc = dalloc(&h->d_Pinv, (size_t)std::max(nloc, 1) * 16)) ||
-      (rc = dalloc(&h->d_hD, (size_t)std::max(nloc, 1) * 16)) ||
+      (rc = dalloc(&h->d_vec, vec * 8)) || (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 6)) ||
+      (rc = dalloc(&h->d_Pinv, (size_t)std::max(nloc, 1) * SYM4)) ||
+      (rc = dalloc(&h->d_hD, (size_t)std::max(nloc, 1) * SYM4)) ||
       (rc = dalloc(&h->d_pub, (size_t)std::max<int64_t>(h->npub, 1) * ps)) ||
       (h->P.acceleration && ((rc = dalloc(&h->d_accV, vec)) || (rc = dalloc(&h->d_accY, vec)))) ||
       (rc = dalloc(&h->d_part, (size_t)h->ntiles * NPART)) || (rc = dalloc(&h->d_ctl, L)) ||
@@ -3477,7 +3482,7 @@ extern "C" int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_byt
   int64_t b = 0;
   b += (int64_t)(h->ninc + 1) * h->rw * 8 + (int64_t)(h->nloc + 1) * 4;  // records, CSR
   b += (int64_t)std::max(h->mloc, 1) * (3 * 8 + 8);                      // kappa, tau, w, positions
-  b += n * ps * 8 * 8 + n * (9 + 16 + 16) * 8;                           // vectors, S, Pinv, D
+  b += n * ps * 8 * 8 + n * (6 + SYM4 + SYM4) * 8;                       // vectors, S, Pinv, D
   b += std::max<int64_t>(h->npub, 1) * (ps * 8 + 4) + n * 4;             // public table + maps
   b += (int64_t)h->ntiles * (NPART * 8 + 12) + L * (int64_t)(sizeof(Ctl) + 32);
   b += (int64_t)std::max(h->n_gnc, 1) * 12 + (int64_t)h->scratch_cap * 8;  // GNC lists, scratch in use
