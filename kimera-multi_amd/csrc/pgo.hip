@@ -1541,10 +1541,14 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d) {
 // robot's first tile writes the RTR state, except the phase, which stays
 // PH_STEP (the next round's k_begin resets it), so tiles that read the state
 // after that write still see a robot with a step to decide.
+// final = 0: between two RTR iterations of one block update — the accepted
+// trial point becomes the iterate the next iteration starts from, but the
+// public rows (the neighbours' snapshot of this round) and the round counters
+// wait for the block update's end.
 template <int R>
-__global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold) {
+__global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
   const Lane L = lane_map<R>(d);
-  if (L.tile == 0 && threadIdx.x == 0) {
+  if (final && L.tile == 0 && threadIdx.x == 0) {
     d.gnc->inner += 1;
     d.gnc->rounds += 1;
   }
@@ -1582,6 +1586,7 @@ __global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold) {
   double v[4];
   load4(d.Xt + o, v);
   store4(d.X + o, v);
+  if (!final) return;
   const int s = d.pose_slot[L.pose];
   if (s >= 0) store4(d.pub + (size_t)s * 4 * R + 4 * L.a, v);
 }
@@ -2432,12 +2437,15 @@ template <int R, int RW, int RM>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   enqueue_begin(h, d_active, BEGIN_ROUND);
   const bool rgd = h->P.method == KMX_METHOD_RGD;
-  for (int it = 0; it < (rgd ? 1 : h->P.rtr_iterations); ++it) {
+  const int iters = rgd ? 1 : h->P.rtr_iterations;
+  for (int it = 0; it < iters; ++it) {
     enqueue_grad_t<R, RW, RM>(h);
     if (!rgd) enqueue_tcg_t<R, RW, RM>(h);
     enqueue_trial_t<R, RW, RM>(h, rgd);
+    if (it + 1 < iters)  // the next RTR iteration starts from the accepted point
+      hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, 0, 0);
   }
-  hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0);
+  hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0, 1);
 }
 
 // Seam parts (one RTR iteration, RTR method): SEAM_HEAD = round begin +
@@ -2452,7 +2460,8 @@ void enqueue_part_t(kmx_pgo* h, int part, const unsigned char* d_active) {
       break;
     case SEAM_TAIL:
       enqueue_trial_t<R, RW, RM>(h, false);
-      hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0);
+      hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0,
+                         1);
       break;
     default:
       enqueue_tcg_t<R, RW, RM>(h);

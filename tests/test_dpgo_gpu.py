@@ -321,3 +321,41 @@ def test_rgd_rounds_match_oracle(gpu, robust):
         if robust and it % 4 == 3:
             s.refresh_local()
             assert s.update_weights() == o.update_weights()
+
+
+@pytest.mark.parametrize("red", ["0", "2"])
+@pytest.mark.parametrize("case", ["rtr2", "tcg1", "tcg3"])
+def test_round_structure_matches_oracle(gpu, monkeypatch, red, case):
+    """Both reduction forms (KMX_RED=0: a k_reduce launch per reduction; 2: the
+    consumer form with every reduction folded into the next kernel) on round
+    structures the default parameters never produce: two RTR iterations per
+    block update (the trial cost is reduced by a launch and the second
+    iteration's gradient folded into its first k_hess), and tCG capped at one /
+    three steps (the last update reduced in k_retract). Synchronous rounds
+    (kmx_pgo_iterate) and the asynchronous form (kmx_pgo_iterate_async) both
+    match the CPU restatement."""
+    monkeypatch.setenv("KMX_RED", red)
+    g, P, X0 = _setup(robust=True, seed=3)
+    lo = P.localOptimizationParams
+    if case == "rtr2":
+        lo.RTR_iterations = 2
+    else:
+        lo.RTR_tCG_iterations = 1 if case == "tcg1" else 3
+    s, o = _pair(g, P, X0)
+    for it in range(6):
+        s.refresh_local()
+        sg = s.iterate()
+        so = o.iterate()
+        for a in range(g.n_robots):
+            assert sg[a]["tcg_iterations"] == so[a]["tcg_iterations"], (it, a, sg[a], so[a])
+            assert sg[a]["accepted"] == so[a]["accepted"], (it, a)
+            d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
+            assert d <= 1e-6, (it, a, d)
+    s.iterate_async(3, refresh_local=True)
+    s.sync()
+    for _ in range(3):
+        o.refresh()
+        o.iterate()
+    for a in range(g.n_robots):
+        d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
+        assert d <= 1e-6, (a, d)
