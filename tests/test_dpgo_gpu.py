@@ -323,11 +323,12 @@ def test_rgd_rounds_match_oracle(gpu, robust):
             assert s.update_weights() == o.update_weights()
 
 
-@pytest.mark.parametrize("red", ["0", "2"])
+@pytest.mark.parametrize("red", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("case", ["rtr2", "tcg1", "tcg3"])
 def test_round_structure_matches_oracle(gpu, monkeypatch, red, case):
-    """Both reduction forms (KMX_RED=0: a k_reduce launch per reduction; 2: the
-    consumer form with every reduction folded into the next kernel) on round
+    """Every reduction form (KMX_RED=0: a k_reduce launch per reduction; 1:
+    tickets in the producing launch; 2: the consumer form with every reduction
+    folded into the next kernel; 3: the Hess-vec's consumed by k_update) on round
     structures the default parameters never produce: two RTR iterations per
     block update (the trial cost is reduced by a launch and the second
     iteration's gradient folded into its first k_hess), and tCG capped at one /
