@@ -360,3 +360,20 @@ def test_round_structure_matches_oracle(gpu, monkeypatch, red, case):
     for a in range(g.n_robots):
         d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
         assert d <= 1e-6, (a, d)
+
+
+def test_large_robot_block_matches_oracle(gpu):
+    """One 12.5k-pose robot block (the per-GPU share of configs[3] at N = 8): the
+    finer tile cut gives it ~700 tiles, more than the 2 x 256 partials the
+    consumer kernels' one-shot robot sums hold, so every folded reduction takes
+    the looped robot_sum path; rounds (GNC on) still match the restatement."""
+    g, P, X0 = _setup(n_robots=1, n=12_500, m=62_500, seed=5)
+    s, o = _pair(g, P, X0)
+    for it in range(4):
+        s.refresh_local()
+        sg = s.iterate()
+        so = o.iterate()
+        assert sg[0]["tcg_iterations"] == so[0]["tcg_iterations"], (it, sg[0], so[0])
+        assert sg[0]["accepted"] == so[0]["accepted"]
+        d = np.linalg.norm((s.get_iterate(0) - o.get_iterate(0)).reshape(-1, 4 * P.r), axis=1).max()
+        assert d <= 1e-6, (it, d)
