@@ -110,6 +110,7 @@ struct Params {
   int gnc_on, inner_iters, max_updates, n_ext;
   int rgd;          // KMX_METHOD_RGD: one preconditioned gradient step per block update
   double rgd_step;
+  int early_stop;   // RM_CONSUMER k_hess: the stop decision before the gather (else after)
 };
 
 struct Dev {
@@ -1166,32 +1167,50 @@ struct RobotSum {
   }
 };
 
+// The robot's state (256 B, into LDS) and its tile partials are loaded
+// together at the start, the control logic runs on the LDS copy and 32 lanes
+// write it back: no global round trip is serialised behind another.
 __global__ __launch_bounds__(RBLOCK) void k_reduce(Dev d, int kind, int R_, HostStatus* hs, unsigned long long seq,
                                                   int slot, const double* src, const Ctl* from) {
   constexpr int RW_ = RBLOCK / 64;
+  constexpr int CW = sizeof(Ctl) / 8;
+  static_assert(CW <= RBLOCK, "Ctl copy");
   __shared__ double lds[NPART * RW_];
+  __shared__ Ctl cs;
   const int l = blockIdx.x;
-  const int ph = from ? from[l].phase : d.ctl[l].phase;
-  if (from && threadIdx.x == 0) d.ctl[l] = from[l];  // RM_HALF: the state k_update left in ctl2
+  const Ctl* cin = from ? from : d.ctl;  // RM_HALF: the state k_update left in ctl2
+  if (threadIdx.x < CW)
+    reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(cin + l)[threadIdx.x];
+  const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
+  double tot[NPART];
+  if (src) {  // RM_CONSUMER's 2-wide partials
+    RobotSum<2> rs;
+    rs.issue(src, 2, t0, t1);
+    rs.finish(src, 2, lds, tot);  // (its barriers also publish cs)
+  } else {
+    RobotSum<NPART> rs;
+    rs.issue(d.part, NPART, t0, t1);
+    rs.finish(d.part, NPART, lds, tot);
+  }
+  const int ph = cs.phase;
   bool act = false;
   if (kind == RED_GRAD) act = ph == PH_START;
   if (kind == RED_HESS || kind == RED_UPDATE) act = ph == PH_TCG;
   if (kind == RED_COST) act = ph == PH_STEP;
-  if (!act) {
-    if (hs && threadIdx.x == 0) post_status(hs, l, seq, false);
-    return;
-  }
-  const int ns = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
-  double tot[NPART];
-  if (src) robot_sum<2>(src, 2, d.rtile0[l], d.rtile0[l + 1], lds, tot);  // RM_CONSUMER's 2-wide partials
-  else robot_sum<NPART>(d.part, NPART, d.rtile0[l], d.rtile0[l + 1], lds, tot);
   if (threadIdx.x == 0) {
+    if (act) {
+      const int ns = kind == RED_GRAD ? 3 : kind == RED_HESS ? 1 : kind == RED_UPDATE ? 2 : 4;
 #pragma unroll
-    for (int s = 0; s < NPART; ++s) tot[s] = s < ns ? tot[s] : 0.0;
-    control(d, l, kind, tot, R_);
-    if (kind == RED_HESS && slot >= 0) atomicAdd(d.hv_launch + slot, 1);
-    if (hs) post_status(hs, l, seq, d.ctl[l].phase == PH_TCG);
+      for (int s = 0; s < NPART; ++s) tot[s] = s < ns ? tot[s] : 0.0;
+      control_on(cs, d, l, kind, tot, R_, true);
+      if (kind == RED_HESS && slot >= 0) atomicAdd(d.hv_launch + slot, 1);
+    }
+    if (hs) post_status(hs, l, seq, act && cs.phase == PH_TCG);
   }
+  if (!act && !from) return;
+  __syncthreads();
+  if (threadIdx.x < CW)
+    reinterpret_cast<double*>(d.ctl + l)[threadIdx.x] = reinterpret_cast<const double*>(&cs)[threadIdx.x];
 }
 
 #define KMX_SMEM extern __shared__ __attribute__((aligned(16))) char smem[]
@@ -1280,7 +1299,7 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
     // before any row is gathered: a robot whose tCG stops here (or whose
     // gradient is below tolerance) skips the gather, and the host sees the
     // stop at the start of the launch
-    const bool go = hinc_gather<R, RW>(d, L, d.z, H, smem, [&]() {
+    auto decide = [&]() {
       double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
       if (upd) rs.finish(d.part_u, 2, rl, tot);
       if (grad) rg.finish(d.part, NPART, rl, tot);
@@ -1296,7 +1315,16 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
         if (hs) post_status(hs, L.l, seq, cs.phase == PH_TCG);
       }
       return !u.done;
-    });
+    };
+    // early (small problems): decide before the gather; otherwise after it,
+    // speculatively, so the robot sums' latency hides behind the gather
+    bool go;
+    if (d.p.early_stop) {
+      go = hinc_gather<R, RW>(d, L, d.z, H, smem, decide);
+    } else {
+      hinc_gather<R, RW>(d, L, d.z, H, smem);
+      go = decide();
+    }
     if (!go) return;
     tcg_iter = grad ? 0 : c0.tcg_iter;
     beta = u.beta;
@@ -2134,6 +2162,7 @@ struct kmx_pgo {
   // kernels costs as much as the saved launches
   int rm = RM_LAUNCH;
   int rm_forced = -1;
+  int early_stop = 1, early_forced = -1;  // KMX_EARLY
   static constexpr int RM_CONSUMER_MAX_POSES = 40000;
   bool poll_timeout = false;
   // timing
@@ -2294,6 +2323,7 @@ void sync_params(kmx_pgo* h) {
   p.n_ext = h->n_ext;
   p.rgd = h->P.method == KMX_METHOD_RGD ? 1 : 0;
   p.rgd_step = h->P.rgd_stepsize;
+  p.early_stop = h->early_stop;
   h->dv.ext = h->d_ext;
 }
 
@@ -2651,6 +2681,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   h->own_stream = true;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_GRAPH")) h->graphs = std::atoi(v) != 0;
+  if (const char* v = std::getenv("KMX_EARLY")) h->early_forced = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("KMX_QUERY")) h->query = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);
@@ -2717,6 +2748,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   }
   h->nloc = nloc;
   h->rm = h->rm_forced >= 0 ? h->rm_forced : (nloc <= kmx_pgo::RM_CONSUMER_MAX_POSES ? RM_CONSUMER : RM_LAUNCH);
+  h->early_stop = h->early_forced >= 0 ? h->early_forced : (nloc <= kmx_pgo::RM_CONSUMER_MAX_POSES ? 1 : 0);
   const int L = (int)h->robots.size();
   KMX_CHECK(L > 0, KMX_EINVAL, "no local robot");
   KMX_CHECK(L <= 1024, KMX_EUNSUP, "at most 1024 local robots per handle");
