@@ -1278,6 +1278,10 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
     __shared__ double rl[NPART * WAVES];
     const Ctl& c0 = d.ctl[L.l];
     const bool writer = L.tile == d.rtile0[L.l];
+    // the writer's working copy of the state, loaded by wave 0 at the start
+    // (its lane 0 reads it after these in-order LDS writes of its own wave)
+    if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))
+      reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(&c0)[threadIdx.x];
     const int ph0 = c0.phase;  // written by an earlier launch: uniform
     // PH_START: the first step of the tCG, whose gradient reduction (k_grad's
     // partials) this launch also consumes in place of a k_reduce launch
@@ -1309,7 +1313,6 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
       if (upd) u = upd_step(c0.mode, c0.norm_r0, c0.z_r, c0.tcg_iter, tot[0], tot[1], d.p);
       if (grad) u.done = sqrt(tot[1]) < d.p.gn_tol ? 1 : 0;  // control_on's RED_GRAD test
       if (writer && threadIdx.x == 0) {
-        cs = c0;
         if (upd || grad) control_on(cs, d, L.l, grad ? RED_GRAD : RED_UPDATE, tot, R, true);
         d.ctl2[L.l] = cs;
         if (hs) post_status(hs, L.l, seq, cs.phase == PH_TCG);
@@ -1404,6 +1407,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
     Ctl* const cout = (RM == RM_HALF) ? d.ctl2 : d.ctl;
     const Ctl& cq = cin[L.l];
     const bool writer = L.tile == d.rtile0[L.l];
+    if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))  // as in k_hess
+      reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(&cq)[threadIdx.x];
     if (cq.phase != PH_TCG) {
       if (writer && threadIdx.x == 0) cout[L.l] = cq;
       return;
@@ -1423,7 +1428,6 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
     rs.finish(d.part_h, 2, rl, tot);
     const HessStep hsx = hess_step(cq.z_r, cq.e_Pe, cq.e_Pd, cq.d_Pd, cq.Delta, tot[0]);
     if (writer && threadIdx.x == 0) {  // the state update, on an LDS copy
-      cs = cq;
       control_on(cs, d, L.l, RED_HESS, tot, R, true);
       cout[L.l] = cs;
       if (slot >= 0) atomicAdd(d.hv_launch + slot, 1);
@@ -1586,6 +1590,9 @@ __global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
     __shared__ Ctl cs;
     __shared__ double rl[NPART * WAVES];
     const Ctl& c = d.ctl[L.l];
+    const bool writer = L.tile == d.rtile0[L.l];
+    if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))  // as in k_hess
+      reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(&c)[threadIdx.x];
     if (threadIdx.x == 0) sph = c.phase;
     __syncthreads();
     if (sph != PH_STEP) return;
@@ -1600,8 +1607,7 @@ __global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
       const double rho = (model_dec > 0.0) ? (c.f_cur - tot[0]) / model_dec : -1.0;
       commit = rho > d.p.accept_rho;
     }
-    if (threadIdx.x == 0 && L.tile == d.rtile0[L.l]) {
-      cs = c;
+    if (threadIdx.x == 0 && writer) {
       control_on(cs, d, L.l, RED_COST, tot, R, true);
       cs.phase = PH_STEP;
       d.ctl[L.l] = cs;
