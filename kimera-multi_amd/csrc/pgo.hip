@@ -2185,13 +2185,6 @@ struct kmx_pgo {
   double acc_gamma = 0.0;
   int acc_k = 0;
   bool acc_ready = false, acc_started = false;
-  // round seams replayed from hipGraphs (launch_seam; KMX_GRAPH=1, off by default):
-  // [SEAM_TAIL], [SEAM_HEAD], [SEAM_TAIL | SEAM_HEAD], each captured with the
-  // handle state in seam_dv / seam_key and rebuilt when that changes
-  bool graphs = false;
-  hipGraphExec_t seam[4] = {nullptr, nullptr, nullptr, nullptr};
-  Dev seam_dv{};
-  long long seam_key[8] = {};
 };
 
 namespace {
@@ -2236,16 +2229,7 @@ int dalloc(T** p, size_t count) {
   return 0;
 }
 
-void drop_seams(kmx_pgo* h) {
-  for (auto& g : h->seam)
-    if (g) {
-      (void)hipGraphExecDestroy(g);
-      g = nullptr;
-    }
-}
-
 void free_dev(kmx_pgo* h) {
-  drop_seams(h);
   void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_rec, h->d_ekappa,
                   h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_hD, h->d_pub, h->d_part,
                   h->d_ctl, h->d_cnt, h->d_tickets, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
@@ -2396,10 +2380,11 @@ void red_t(kmx_pgo* h, int kind, HostStatus* hs = nullptr, unsigned long long se
     hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot, src, from);
 }
 
-// The three parts of a round: head (round begin, gradient), tCG (host-polled
-// steps), tail (retraction, trial cost, commit). With one RTR iteration the
-// head and tail launches are fixed for the handle, so back-to-back rounds
-// replay them from hipGraphs (launch_seam below).
+// The parts of a round: gradient, tCG (host-polled steps), trial point and
+// cost; round begin before and commit after. Replaying the launches between
+// two tCG loops from a hipGraph was measured on one 12.5k-pose block (170.1
+// vs 167.7 us per round eager: the graph launch moves the host latency to the
+// first tCG step after it; profiles/r02/small_round/2_*) and not kept.
 // RM_CONSUMER folds the round's other reductions into the kernel after them
 // (no k_reduce launch in a round): the gradient's into the first k_hess, the
 // last tCG update's into k_retract, the trial cost's into k_commit (one RTR
@@ -2484,27 +2469,6 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0, 1);
 }
 
-// Seam parts (one RTR iteration, RTR method): SEAM_HEAD = round begin +
-// gradient; SEAM_TAIL = trial + commit.
-enum { SEAM_TAIL = 1, SEAM_HEAD = 2 };
-template <int R, int RW, int RM>
-void enqueue_part_t(kmx_pgo* h, int part, const unsigned char* d_active) {
-  switch (part) {
-    case SEAM_HEAD:
-      enqueue_begin(h, d_active, BEGIN_ROUND);
-      enqueue_grad_t<R, RW, RM>(h);
-      break;
-    case SEAM_TAIL:
-      enqueue_trial_t<R, RW, RM>(h, false);
-      hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0,
-                         1);
-      break;
-    default:
-      enqueue_tcg_t<R, RW, RM>(h);
-      break;
-  }
-}
-
 template <int R>
 void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
   if (h->rm == RM_CONSUMER) {
@@ -2520,72 +2484,6 @@ void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
     if (h->rw == 10) enqueue_round_t<R, 10, RM_LAUNCH>(h, d_active);
     else enqueue_round_t<R, 16, RM_LAUNCH>(h, d_active);
   }
-}
-
-template <int R>
-void enqueue_part_r(kmx_pgo* h, int part, const unsigned char* d_active) {
-  if (h->rm == RM_CONSUMER) {
-    if (h->rw == 10) enqueue_part_t<R, 10, RM_CONSUMER>(h, part, d_active);
-    else enqueue_part_t<R, 16, RM_CONSUMER>(h, part, d_active);
-  } else if (h->rm == RM_HALF) {
-    if (h->rw == 10) enqueue_part_t<R, 10, RM_HALF>(h, part, d_active);
-    else enqueue_part_t<R, 16, RM_HALF>(h, part, d_active);
-  } else if (h->rm == RM_TICKET) {
-    if (h->rw == 10) enqueue_part_t<R, 10, RM_TICKET>(h, part, d_active);
-    else enqueue_part_t<R, 16, RM_TICKET>(h, part, d_active);
-  } else {
-    if (h->rw == 10) enqueue_part_t<R, 10, RM_LAUNCH>(h, part, d_active);
-    else enqueue_part_t<R, 16, RM_LAUNCH>(h, part, d_active);
-  }
-}
-// part: SEAM_HEAD, SEAM_TAIL, or 0 (the tCG loop)
-void enqueue_part(kmx_pgo* h, int part, const unsigned char* d_active) {
-  switch (h->P.r) {
-    case 3: enqueue_part_r<3>(h, part, d_active); break;
-    case 4: enqueue_part_r<4>(h, part, d_active); break;
-    case 5: enqueue_part_r<5>(h, part, d_active); break;
-    case 6: enqueue_part_r<6>(h, part, d_active); break;
-    case 7: enqueue_part_r<7>(h, part, d_active); break;
-    default: enqueue_part_r<8>(h, part, d_active); break;
-  }
-}
-
-// The launches between two tCG loops — the trial point, its cost and the
-// commit of one round, then the next round's begin and gradient — depend only
-// on the handle, so back-to-back rounds replay them from a hipGraph: one host
-// call instead of 9-11 launches while the device waits for them (the tCG stop
-// is known only when the last step posts it). Measured on the strong-scaling
-// floor (one 12.5k-pose block): 170.1 vs 167.7 us per round eager — the graph
-// launch moves the host latency to the first tCG step after it
-// (profiles/r02/small_round/2_*), so it is off by default.
-bool seams_usable(const kmx_pgo* h) {
-  return h->graphs && !h->timing && !h->P.acceleration && h->P.rtr_iterations == 1 &&
-         h->P.method != KMX_METHOD_RGD;
-}
-int launch_seam(kmx_pgo* h, int parts) {
-  const long long key[8] = {h->rm, h->rw, h->P.r, h->ntiles, h->n_gnc, h->gnc_on, h->P.robust_cost,
-                            (long long)(uintptr_t)h->d_active};
-  if (std::memcmp(key, h->seam_key, sizeof(key)) != 0 || std::memcmp(&h->dv, &h->seam_dv, sizeof(Dev)) != 0) {
-    drop_seams(h);
-    std::memcpy(h->seam_key, key, sizeof(key));
-    std::memcpy(&h->seam_dv, &h->dv, sizeof(Dev));
-  }
-  if (!h->seam[parts]) {
-    hipGraph_t g = nullptr;
-    KMX_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    if (parts & SEAM_TAIL) enqueue_part(h, SEAM_TAIL, h->d_active);
-    if (parts & SEAM_HEAD) enqueue_part(h, SEAM_HEAD, h->d_active);
-    const hipError_t e = hipStreamEndCapture(h->stream, &g);
-    if (e != hipSuccess) {
-      if (g) (void)hipGraphDestroy(g);
-      KMX_HIP(e);
-    }
-    const hipError_t ei = hipGraphInstantiate(&h->seam[parts], g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    KMX_HIP(ei);
-  }
-  KMX_HIP(hipGraphLaunch(h->seam[parts], h->stream));
-  return KMX_OK;
 }
 
 // One RBCD round for the robots whose d_active flag is set; it starts with
@@ -2686,7 +2584,6 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
   }
   h->own_stream = true;
   if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
-  if (const char* v = std::getenv("KMX_GRAPH")) h->graphs = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_EARLY")) h->early_forced = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("KMX_QUERY")) h->query = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_RED")) {
@@ -3276,18 +3173,10 @@ extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local) 
   // every round's k_commit republishes the committed owned rows, so the
   // single-device exchange needs one publish per call
   if (refresh_local && rounds > 0) enqueue_publish(h);
-  if (seams_usable(h) && rounds > 0) {
-    enqueue_part(h, SEAM_HEAD, h->d_active);
-    for (int i = 0; i < rounds; ++i) {
-      enqueue_part(h, 0, h->d_active);  // the tCG loop
-      if (int rc = launch_seam(h, i + 1 < rounds ? SEAM_TAIL | SEAM_HEAD : SEAM_TAIL)) return rc;
-    }
-  } else {
-    for (int i = 0; i < rounds; ++i) {
-      enqueue_accel_pre(h);  // publishes Y itself
-      enqueue_round(h, h->d_active);
-      enqueue_accel_post(h);
-    }
+  for (int i = 0; i < rounds; ++i) {
+    enqueue_accel_pre(h);  // publishes Y itself
+    enqueue_round(h, h->d_active);
+    enqueue_accel_post(h);
   }
   KMX_HIP(hipGetLastError());
   return KMX_OK;
