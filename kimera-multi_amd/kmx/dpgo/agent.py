@@ -34,7 +34,7 @@ import numpy as np
 from ..synth.pose_graph import PoseGraphData, lift, lifting_matrix
 from .messages import (MeasurementWeights, PGOAgentState, PGOAgentStatus, PoseID, PublicPoses,
                        RelativeSEMeasurement)
-from .params import PGOAgentParameters, RobustCostType
+from .params import PGOAgentParameters
 from .schedule import GncSchedule
 
 

@@ -12,7 +12,6 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from kmx.abi import LcdParams as CParams
 from kmx.lcd.detector import LcdParams
 from kmx.synth.lcd import make_lcd_pool
 from kmx.synth.pose_graph import _expm_so3

@@ -2,7 +2,6 @@
 same pipeline run on the CPU restatement (accepted loop-closure set bit-exact,
 so the team graph and initialisation are identical; final trajectory error
 within 1e-6 m)."""
-import numpy as np
 import pytest
 
 from kmx import pipeline as PL
