@@ -160,6 +160,7 @@ class RBCDDriver:
         self.active_robots = set(range(graph.n_robots))
         self.monitor = TimeoutMonitor(timeout, now=time.monotonic())
         self._X0 = None
+        self._pub_fresh = False  # owned public rows current (see exchange_public)
 
     # ------------------------------------------------------ collectives ---
     def _setup_exchange(self):
@@ -196,7 +197,9 @@ class RBCDDriver:
     def exchange_public(self):
         """publishPublicPoses -> updateNeighborPoses (+ publishStatus) for the
         whole team."""
-        self.solver.refresh_local()  # the owned slots of the table
+        if not (self._pub_fresh and getattr(self.solver, "publishes_on_commit", False)):
+            self.solver.refresh_local()  # the owned slots of the table
+            self._pub_fresh = True
         if self.world == 1:
             return
         s = self.solver
@@ -221,6 +224,7 @@ class RBCDDriver:
         self._X0 = {a: np.array(X_by_robot[a], dtype=np.float64) for a in self.robots}
         for a in self.robots:
             self.solver.set_iterate(a, self._X0[a])
+        self._pub_fresh = False
         self.state = PGOAgentState.INITIALIZED
         self.terminated = False
 

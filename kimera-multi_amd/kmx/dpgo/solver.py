@@ -17,6 +17,10 @@ from .params import PGOAgentParameters
 
 class BlockSolver:
     device_pointers = True  # pack/unpack take HIP device pointers
+    # every round's k_commit republishes the committed owned public rows (and an
+    # accelerated round publishes Y before its exchange), so the table needs an
+    # explicit refresh_local only after set_iterate
+    publishes_on_commit = True
 
     def __init__(self, params: PGOAgentParameters, device: int = 0):
         self.params = params
