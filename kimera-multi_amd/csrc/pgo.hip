@@ -2161,15 +2161,16 @@ struct kmx_pgo {
   // launches reach the hardware queue without it
   bool query = false;
   // reduction mode: set per graph (below) unless KMX_RED forces one (0 launch,
-  // 1 tickets, 2 consumer). Measured (profiles/r02/round_sizes): consumer-side
-  // reductions win on small per-GPU problems, where a round is launch-bound
-  // (12.5k poses 173 vs 196 us, 25k 274 vs 303 us per round), and tie or lose
-  // from 50k poses on, where the added per-workgroup latency of the gather
-  // kernels costs as much as the saved launches
+  // 1 tickets, 2 consumer, 3 half). Measured at the end of round 2
+  // (profiles/r02/small_round/16_*): the consumer form (no reduction launch,
+  // the stop decision before the gather) wins per round at 25k poses (244 vs
+  // 280 us), 37.5k (318 vs 357), 62.5k (530 vs 543) and 75k (583 vs 591), ties
+  // at 50k and 87.5k, and loses at 100k (773 vs 731-738: two and a bit
+  // generations of workgroups, each waiting for its robot's sums)
   int rm = RM_LAUNCH;
   int rm_forced = -1;
   int early_stop = 1, early_forced = -1;  // KMX_EARLY
-  static constexpr int RM_CONSUMER_MAX_POSES = 40000;
+  static constexpr int RM_CONSUMER_MAX_POSES = 80000;
   bool poll_timeout = false;
   // timing
   bool timing = false;

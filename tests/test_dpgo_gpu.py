@@ -377,3 +377,25 @@ def test_large_robot_block_matches_oracle(gpu):
         assert sg[0]["accepted"] == so[0]["accepted"]
         d = np.linalg.norm((s.get_iterate(0) - o.get_iterate(0)).reshape(-1, 4 * P.r), axis=1).max()
         assert d <= 1e-6, (it, d)
+
+
+def test_reduction_forms_agree_bitwise(gpu, monkeypatch):
+    """The consumer kernels reduce every robot's partials in k_reduce's order and
+    take the same decisions, so both forms give the same iterates bit for bit
+    (what keeps a team's result independent of how its ranks' sizes fall on
+    either side of the form's size threshold)."""
+    g, P, X0 = _setup(robust=True, seed=4)
+    out = []
+    for red in ("0", "2"):
+        monkeypatch.setenv("KMX_RED", red)
+        s = BlockSolver(P, 0)
+        s.set_graph_data(g)
+        s.set_gnc_schedule(True, 3, 50, P.relChangeTol)
+        for a in range(g.n_robots):
+            s.set_iterate(a, X0[a])
+        s.iterate_async(9, refresh_local=True)
+        s.sync()
+        out.append([s.get_iterate(a) for a in range(g.n_robots)] + [s.get_weights()])
+        s.close()
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
