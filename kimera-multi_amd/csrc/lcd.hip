@@ -923,7 +923,15 @@ struct CoopWS {
   signed char t11[10][2][2], t21[20][3][2];  // LDS copies of T11 / T21
 };
 
-__device__ __forceinline__ void wsync() { __syncthreads(); }  // the block is one wavefront
+// The block is one wavefront and a wave's LDS operations complete in issue
+// order, so lane-to-lane hand-offs through LDS need only a compiler barrier
+// (the pattern of pgo.hip's group_symYtG), not a workgroup barrier with its
+// memory-count waits.
+__device__ __forceinline__ void wsync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 
 __device__ __forceinline__ double rdlane(double v, int src) {  // src wave-uniform
   const long long b = __double_as_longlong(v);
