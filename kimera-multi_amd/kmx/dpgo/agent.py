@@ -154,7 +154,9 @@ class PGOAgent:
 
     def initialize(self, TInit=None, neighbor_global_poses=None):
         """INITIALIZE: build the local problem and the initial lifted iterate.
-        TInit: dpgo PoseArray (d x (d+1)n) or [n, 3, 4]; default: odometry chain.
+        TInit: dpgo PoseArray (d x (d+1)n) or [n, 3, 4]; default: the odometry
+        chain or, with localInitializationMethod "chordal", the chordal
+        relaxation over the robot's own measurements (kmx.dpgo.init).
         neighbor_global_poses: {(robot, pose): (R, t)} of neighbours already in
         the global frame -> the local trajectory is aligned to it by robust
         single-pose averaging over the shared loop closures (kmx.dpgo.init;
@@ -193,7 +195,14 @@ class PGOAgent:
         self._have_nbr = set()
         self._weights = g.weight.copy()
         if TInit is None:
-            Rs, ts = self._odometry_chain()
+            if self.params.localInitializationMethod == "chordal":
+                from .init import chordal_initialization
+                own = self.odometry + self.private_lcs
+                Rs, ts = chordal_initialization(self.n, [(m.p1, m.p2, m.R, m.t, m.kappa, m.tau, m.weight) for m in own])
+            elif self.params.localInitializationMethod == "odometry":
+                Rs, ts = self._odometry_chain()
+            else:
+                raise ValueError(f"unknown localInitializationMethod {self.params.localInitializationMethod!r}")
         else:
             T = np.asarray(TInit, dtype=np.float64)
             if T.shape == (self.d, (self.d + 1) * self.n):

@@ -116,3 +116,80 @@ def align_to_world(shared_lcs, own_robot, own_R, own_t, nbr_global, **kw):
 def transform_trajectory(R_WA, t_WA, R, t):
     """Express a trajectory given in frame A in the world frame."""
     return np.einsum("ij,njk->nik", R_WA, R), t @ R_WA.T + t_WA
+
+
+def chordal_initialization(n: int, edges, anchor: int = 0):
+    """Local chordal initialisation of one robot's trajectory (SURVEY.md §8
+    row D10; dpgo's local initialisation method Chordal [U: restated from the
+    SE-Sync chordal relaxation it uses]).
+
+    edges: iterable of (i, j, R_ij [3x3], t_ij [3], kappa, tau, weight) for the
+    robot's own measurements (odometry and private loop closures), with
+    R_j = R_i R_ij and t_j = t_i + R_i t_ij. Step 1 minimises
+    sum w kappa |R_j - R_i R_ij|_F^2 over unconstrained 3x3 blocks with
+    R_anchor = I (sparse normal equations), then projects every block to SO(3);
+    step 2 minimises sum w tau |t_j - t_i - R_i t_ij|^2 with t_anchor = 0 for
+    the rotations of step 1. Returns (R [n,3,3], t [n,3])."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    E = list(edges)
+    if n == 1:
+        return np.eye(3)[None], np.zeros((1, 3))
+    free = np.array([k for k in range(n) if k != anchor])
+    col = -np.ones(n, np.int64)
+    col[free] = np.arange(n - 1)
+    # rotations: unknowns are the 3x3 blocks of the free poses, row-major, and
+    # every edge gives R_j - R_i R_ij = 0, i.e. for each row a of R:
+    # R_j[a, :] - R_i[a, :] R_ij = 0 (3 equations per row, same structure per row)
+    # row a of every block is an independent problem with the same matrix:
+    # s (R_j[a, c] - sum_b R_i[a, b] R_ij[b, c]) = 0 for c = 0..2; the anchor's
+    # known row (R_anchor = I) moves to the right-hand side
+    rows, cols, vals, rhs = [], [], [], []
+    r = 0
+    for (i, j, Rij, _t, kap, _tau, w) in E:
+        s = np.sqrt(max(w * kap, 0.0))
+        Rij = np.asarray(Rij, np.float64)
+        for c in range(3):
+            if col[j] >= 0:
+                rows.append(r); cols.append(3 * col[j] + c); vals.append(s)
+            if col[i] >= 0:
+                for b in range(3):
+                    rows.append(r); cols.append(3 * col[i] + b); vals.append(-s * Rij[b, c])
+            rhs.append((c, i, j, s, Rij))
+            r += 1
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(r, 3 * (n - 1)))
+    AtA = (A.T @ A).tocsc()
+    solve = spla.factorized(AtA)
+    Rs = np.zeros((n, 3, 3))
+    Rs[anchor] = np.eye(3)
+    for a in range(3):  # one solve per row of the rotation blocks, same matrix
+        bvec = np.zeros(r)
+        for k, (c, i, j, s, Rij) in enumerate(rhs):
+            v = 0.0
+            if i == anchor:
+                v += s * Rij[a, c]
+            if j == anchor:
+                v -= s * (1.0 if a == c else 0.0)
+            bvec[k] = v
+        x = solve(A.T @ bvec)
+        Rs[free, a, :] = x.reshape(n - 1, 3)
+    for k in free:
+        Rs[k] = project_so3(Rs[k])
+    # translations
+    rows, cols, vals, b = [], [], [], []
+    r = 0
+    for (i, j, Rij, tij, _kap, tau, w) in E:
+        s = np.sqrt(max(w * tau, 0.0))
+        d = Rs[i] @ np.asarray(tij, np.float64)
+        for c in range(3):
+            if col[j] >= 0:
+                rows.append(r); cols.append(3 * col[j] + c); vals.append(s)
+            if col[i] >= 0:
+                rows.append(r); cols.append(3 * col[i] + c); vals.append(-s)
+            b.append(s * d[c])
+            r += 1
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(r, 3 * (n - 1)))
+    x = spla.spsolve((A.T @ A).tocsc(), A.T @ np.asarray(b))
+    ts = np.zeros((n, 3))
+    ts[free] = np.asarray(x).reshape(n - 1, 3)
+    return Rs, ts

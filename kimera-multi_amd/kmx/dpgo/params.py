@@ -75,6 +75,7 @@ class PGOAgentParameters:
     acceleration: bool = False             # Nesterov-accelerated RBCD (dpgo acceleration; concurrent schedule)
     restartInterval: int = 30              # acceleration restart period in rounds (dpgo restartInterval [U])
     tileIncidences: int = 0                # kmx: incidences per workgroup tile (0: from the handle's problem)
+    localInitializationMethod: str = "odometry"  # dpgo local initialisation: "odometry" or "chordal" [U default]
 
     def to_c(self) -> PgoParams:
         lo, rc = self.localOptimizationParams, self.robustCostParams
