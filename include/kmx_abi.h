@@ -130,6 +130,38 @@ int kmx_pgo_destroy(kmx_pgo* h);
 /* Use the caller's HIP stream (e.g. torch.cuda.current_stream().cuda_stream). */
 int kmx_pgo_set_stream(kmx_pgo* h, void* hip_stream);
 
+/* How the host enqueues the tCG steps of a round (dpgo's tCG loop inside
+ * PGOAgent::iterate, drawio:2058-2066; the results are identical in every mode):
+ *   1  polled: after each step the host waits for the device's progress word
+ *      and stops enqueueing once every robot left tCG;
+ *   0  blind: all tcg_max_iterations steps are enqueued; the kernels of a
+ *      finished robot exit at once; the host never waits inside a round;
+ *  -1  adaptive (default): a polled loop that needed nearly tcg_max steps sends
+ *      the next loops blind, then one polled loop measures again.
+ * The environment variable KMX_POLL=0/1 at handle creation forces 0 / 1. */
+int kmx_pgo_set_tcg_poll(kmx_pgo* h, int mode);
+
+/* Native team exchange over RCCL (replaces the ROS topics public_poses +
+ * status of dpgo_ros, drawio:2340-2375, for a team with one process per GPU).
+ * Rank 0 calls kmx_comm_unique_id and hands the KMX_COMM_ID_BYTES bytes to
+ * every rank (any side channel); every rank calls kmx_pgo_comm_init on its
+ * handle after kmx_pgo_set_graph, then kmx_pgo_set_exchange with the slot
+ * lists of kmx_pgo_exchange_pack / _unpack (host arrays: send_slots grouped by
+ * destination rank, recv_slots by source rank, counts[world] each; the own
+ * rank's counts equal). From then on every kmx_pgo_iterate /
+ * kmx_pgo_iterate_async round starts with the exchange on the handle's stream:
+ * gather, one ncclSend / ncclRecv per peer in one group, scatter (rows into the
+ * public table, the peers' status words into the team status). Every rank must
+ * run the same number of rounds. kmx_pgo_set_graph drops the exchange lists. */
+#define KMX_COMM_ID_BYTES 128
+int kmx_comm_unique_id(void* out, int64_t nbytes);
+int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, int rank);
+int kmx_pgo_set_exchange(kmx_pgo* h, const int32_t* send_slots, const int64_t* send_counts,
+                         const int32_t* recv_slots, const int64_t* recv_counts);
+/* One exchange now, outside a round (e.g. before kmx_pgo_update_weights);
+ * every rank must call it the same number of times. */
+int kmx_pgo_exchange(kmx_pgo* h);
+
 /* Replaces the pose-graph intake `PGOAgent::addMeasurement` ->
  * PoseGraph::addOdometry / addPrivateLoopClosure / addSharedLoopClosure
  * (drawio:2142, 2779-2826). Edges are the GLOBAL measurement list of the team:

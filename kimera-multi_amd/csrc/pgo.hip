@@ -29,6 +29,7 @@
 //     robustOptNumWeightUpdates) from device state and re-weights the loop
 //     closures in the same launch.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -1851,38 +1852,38 @@ __device__ __forceinline__ long long seg_offset(const int* seg, int nseg, long l
   while (k + 1 < nseg && seg[k + 1] <= s) ++k;
   return nseg > 0 ? k : 0;
 }
+// The status words ride in the same launch: threads n*ps .. n*ps + nseg - 1
+// write this handle's max relative change after every segment (gather) /
+// read the peers' into ext (scatter). One launch per side of the exchange.
 __global__ void k_gather_slots(const double* X, const int* pub_src, const int* slots, long long n, int npub,
-                               double* out, int ps, const int* seg, int nseg) {
+                               double* out, int ps, const int* seg, int nseg, const double* relc, int L) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long s = i / ps;
-  if (s >= n) return;
+  if (s >= n) {
+    const long long k = i - n * ps;
+    if (k >= nseg) return;
+    double m = 0.0;
+    for (int l = 0; l < L; ++l) m = (relc[l] > m || relc[l] != relc[l]) ? relc[l] : m;
+    out[(long long)seg[k + 1] * ps + k] = m;
+    return;
+  }
   const int q = (int)(i - s * ps);
   const int sl = slots[s];
   const int p = (sl >= 0 && sl < npub) ? pub_src[sl] : -1;
   out[i + seg_offset(seg, nseg, s)] = (p >= 0) ? X[(long long)p * ps + q] : 0.0;
 }
 __global__ void k_scatter_slots(double* pub, const int* slots, long long n, int npub, const double* rows, int ps,
-                                const int* seg, int nseg) {
+                                const int* seg, int nseg, double* ext) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long s = i / ps;
-  if (s >= n) return;
+  if (s >= n) {
+    const long long k = i - n * ps;
+    if (k < nseg) ext[k] = rows[(long long)seg[k + 1] * ps + k];
+    return;
+  }
   const int q = (int)(i - s * ps);
   const int sl = slots[s];
   if (sl >= 0 && sl < npub) pub[(long long)sl * ps + q] = rows[i + seg_offset(seg, nseg, s)];
-}
-// status words: write this handle's max relative change after every segment
-// (pack) / read the peers' into ext (unpack)
-__global__ void k_status_pack(const double* relc, int L, double* out, const int* seg, int nseg, int ps) {
-  const int k = threadIdx.x;
-  if (k >= nseg) return;
-  double m = 0.0;
-  for (int l = 0; l < L; ++l) m = (relc[l] > m || relc[l] != relc[l]) ? relc[l] : m;
-  out[(long long)seg[k + 1] * ps + k] = m;
-}
-__global__ void k_status_unpack(const double* in, double* ext, const int* seg, int nseg, int ps) {
-  const int k = threadIdx.x;
-  if (k >= nseg) return;
-  ext[k] = in[(long long)seg[k + 1] * ps + k];
 }
 
 __global__ void k_pack(const double* X, double* out, const int* src, int first, int count, int ps) {
@@ -2155,6 +2156,29 @@ struct kmx_pgo {
   int hstat_cap = 0;
   unsigned long long seq = 0;
   bool poll = true;          // KMX_POLL=0: enqueue every tCG step (finished robots exit at once)
+  // KMX_POLL unset / kmx_pgo_set_tcg_poll(-1): adaptive. A polled tCG loop
+  // that ran to within BLIND_SLACK steps of the cap sends the next
+  // BLIND_WINDOW loops blind (no host wait: at most BLIND_SLACK empty step
+  // pairs of ~1.5 us each, against the host round trip of every polled step
+  // and the host seam of a multi-rank round); then one polled loop measures
+  // again. Measured on configs[3] (scripts/host_seam.py, round_sizes.py):
+  // blind wins at 100k poses (728 vs 740 us), on the N = 4 / 8 rank handles
+  // (274 vs 284, 197 vs 217 us), loses on a 12.5k block needing ~5 steps
+  // (163 vs 150 us), where the adaptive rule keeps polling.
+  bool poll_auto = true;
+  // native exchange (kmx_pgo_comm_init + kmx_pgo_set_exchange): every round
+  // of iterate / iterate_async starts with gather -> RCCL send/recv with each
+  // peer -> scatter, all on the handle's stream (no cross-stream event, no
+  // host round trip between the exchange and the round)
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0;
+  bool xchg = false, xchg_self_p2p = false;
+  int *d_xs_slots = nullptr, *d_xr_slots = nullptr, *d_xs_seg = nullptr, *d_xr_seg = nullptr;
+  double *d_xsbuf = nullptr, *d_xrbuf = nullptr;
+  long long xn_send = 0, xn_recv = 0;
+  std::vector<long long> xs_cnt, xr_cnt, xs_off, xr_off;  // per peer, in doubles (rows * 4r + 1 status)
+  int blind_left = 0;
+  static constexpr int BLIND_SLACK = 2, BLIND_WINDOW = 8;
   // KMX_QUERY=1: hipStreamQuery before the status spin. Measured: the query
   // puts a ~5 us bubble before the next tCG step's first kernel (profiles/r02/
   // ab_query: 0.836 vs 0.863 ms per round; wall = busy without it), and
@@ -2228,6 +2252,15 @@ int dalloc(T** p, size_t count) {
   hipError_t e = hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * count);
   if (e != hipSuccess) return kmx::fail(KMX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
   return 0;
+}
+
+void free_xchg(kmx_pgo* h) {
+  void* ptrs[] = {h->d_xs_slots, h->d_xr_slots, h->d_xs_seg, h->d_xr_seg, h->d_xsbuf, h->d_xrbuf};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  h->d_xs_slots = h->d_xr_slots = h->d_xs_seg = h->d_xr_seg = nullptr;
+  h->d_xsbuf = h->d_xrbuf = nullptr;
+  h->xchg = false;
 }
 
 void free_dev(kmx_pgo* h) {
@@ -2411,7 +2444,15 @@ void enqueue_tcg_t(kmx_pgo* h) {
   // tCG: each step is (k_hess, k_update); with polling, exactly one step
   // stays queued beyond the last one known to be needed
   unsigned long long prev = 0;
-  for (int j = 0; j < h->P.tcg_max_iterations; ++j) {
+  // this loop polled or blind (see kmx_pgo::poll_auto)
+  bool poll = h->poll && h->hstat;
+  if (poll && h->poll_auto && h->blind_left > 0) {
+    --h->blind_left;
+    poll = false;
+  }
+  const int tmax = h->P.tcg_max_iterations;
+  int steps = tmax;  // steps enqueued by a polled loop
+  for (int j = 0; j < tmax; ++j) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int slot = -1;
     if (h->timing && h->ev_used / 2 < (size_t)HV_SLOTS) {
@@ -2420,7 +2461,7 @@ void enqueue_tcg_t(kmx_pgo* h) {
       e1 = next_event(h);
       (void)hipEventRecord(e0, h->stream);
     }
-    const bool poll = h->poll && h->hstat;
+    poll = poll && h->poll;  // a poll timeout inside wait_running switches to blind
     const unsigned long long seq = poll ? ++h->seq : 0;
     HostStatus* hs = poll ? h->hstat : nullptr;
     if constexpr (RM == RM_CONSUMER) {
@@ -2428,7 +2469,10 @@ void enqueue_tcg_t(kmx_pgo* h) {
       hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, hs, seq);
       if (slot >= 0) (void)hipEventRecord(e1, h->stream);
       hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, 0ull, slot);
-      if (poll && j > 0 && !wait_running(h, seq)) break;
+      if (poll && j > 0 && !wait_running(h, seq)) {
+        steps = j + 1;
+        break;
+      }
       continue;
     }
     hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, nullptr, 0ull);
@@ -2438,10 +2482,14 @@ void enqueue_tcg_t(kmx_pgo* h) {
                        RM == RM_TICKET ? hs : nullptr, seq, RM == RM_HALF ? slot : -1);
     red_t<R, RM>(h, RED_UPDATE, hs, seq, -1, nullptr, RM == RM_HALF ? h->dv.ctl2 : nullptr);
     if (poll) {
-      if (j > 0 && !wait_running(h, prev)) break;
+      if (j > 0 && !wait_running(h, prev)) {
+        steps = j + 1;
+        break;
+      }
       prev = seq;
     }
   }
+  if (poll && h->poll_auto && steps + kmx_pgo::BLIND_SLACK >= tmax) h->blind_left = kmx_pgo::BLIND_WINDOW;
 }
 
 // after the tCG loop (or the RGD step): trial point and its cost
@@ -2584,7 +2632,10 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     return kmx::fail(KMX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
   h->own_stream = true;
-  if (const char* v = std::getenv("KMX_POLL")) h->poll = std::atoi(v) != 0;
+  if (const char* v = std::getenv("KMX_POLL")) {
+    h->poll = std::atoi(v) != 0;
+    h->poll_auto = false;
+  }
   if (const char* v = std::getenv("KMX_EARLY")) h->early_forced = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("KMX_QUERY")) h->query = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_RED")) {
@@ -2601,6 +2652,8 @@ extern "C" int kmx_pgo_destroy(kmx_pgo* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   free_dev(h);
+  free_xchg(h);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   if (h->hstat) (void)hipHostFree(h->hstat);
@@ -2620,6 +2673,15 @@ extern "C" int kmx_pgo_set_stream(kmx_pgo* h, void* s) {
   return KMX_OK;
 }
 
+extern "C" int kmx_pgo_set_tcg_poll(kmx_pgo* h, int mode) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_CHECK(mode >= -1 && mode <= 1, KMX_EINVAL, "mode is -1 (adaptive), 0 (blind) or 1 (polled)");
+  h->poll = mode != 0;
+  h->poll_auto = mode == -1;
+  h->blind_left = 0;
+  return KMX_OK;
+}
+
 extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_poses, const uint8_t* local,
                                  int64_t m, const int32_t* r1, const int32_t* p1, const int32_t* r2,
                                  const int32_t* p2, const double* R, const double* t, const double* kappa,
@@ -2633,6 +2695,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->stream));
   free_dev(h);
+  free_xchg(h);  // the exchange slot lists index this graph's public table
   accel_reset(h);
   const int r = h->P.r, ps = 4 * r;
   h->n_robots = n_robots;
@@ -3047,14 +3110,11 @@ extern "C" int kmx_pgo_exchange_pack(kmx_pgo* h, const int32_t* dev_slots, int64
   KMX_HIP(hipSetDevice(h->device));
   enqueue_accel_pre(h);  // accelerated rounds exchange Y
   const int ps = 4 * h->P.r;
-  const long long tot = (long long)n * ps;
+  const long long tot = (long long)n * ps + n_seg;  // rows, then the status words
   if (tot)
     hipLaunchKernelGGL(k_gather_slots, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
                        h->d_pub_src, (const int*)dev_slots, (long long)n, (int)h->npub, (double*)dev_out, ps,
-                       (const int*)dev_seg, n_seg);
-  if (n_seg)
-    hipLaunchKernelGGL(k_status_pack, dim3(1), dim3(1024), 0, h->stream, (const double*)h->d_relc, h->dv.L,
-                       (double*)dev_out, (const int*)dev_seg, n_seg, ps);
+                       (const int*)dev_seg, n_seg, (const double*)h->d_relc, h->dv.L);
   KMX_HIP(hipGetLastError());
   return KMX_OK;
 }
@@ -3067,27 +3127,156 @@ extern "C" int kmx_pgo_exchange_unpack(kmx_pgo* h, const int32_t* dev_slots, int
             KMX_EINVAL, "bad argument");
   KMX_HIP(hipSetDevice(h->device));
   const int ps = 4 * h->P.r;
-  const long long tot = (long long)n * ps;
+  if (n_seg > h->ext_cap) {
+    KMX_HIP(hipStreamSynchronize(h->stream));
+    if (h->d_ext) (void)hipFree(h->d_ext);
+    h->d_ext = nullptr;
+    h->ext_cap = 0;
+    if (int rc = dalloc(&h->d_ext, n_seg)) return rc;
+    h->ext_cap = n_seg;
+  }
+  const long long tot = (long long)n * ps + n_seg;  // rows, then the status words
   if (tot)
     hipLaunchKernelGGL(k_scatter_slots, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->d_pub,
                        (const int*)dev_slots, (long long)n, (int)h->npub, (const double*)dev_in, ps,
-                       (const int*)dev_seg, n_seg);
-  if (n_seg) {
-    if (n_seg > h->ext_cap) {
-      KMX_HIP(hipStreamSynchronize(h->stream));
-      if (h->d_ext) (void)hipFree(h->d_ext);
-      h->d_ext = nullptr;
-      h->ext_cap = 0;
-      if (int rc = dalloc(&h->d_ext, n_seg)) return rc;
-      h->ext_cap = n_seg;
-    }
-    hipLaunchKernelGGL(k_status_unpack, dim3(1), dim3(1024), 0, h->stream, (const double*)dev_in, h->d_ext,
-                       (const int*)dev_seg, n_seg, ps);
-  }
+                       (const int*)dev_seg, n_seg, h->d_ext);
   h->n_ext = n_seg;
   sync_params(h);
   KMX_HIP(hipGetLastError());
   return KMX_OK;
+}
+
+#define KMX_NCCL(call)                                                                      \
+  do {                                                                                      \
+    const ncclResult_t r_ = (call);                                                         \
+    if (r_ != ncclSuccess) return kmx::fail(KMX_EHIP, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+// publishPublicPoses -> updateNeighborPoses + publishStatus of one round
+// (drawio:2340-2375) over RCCL: the rows every peer needs (+ this handle's
+// status word) are gathered, each peer's segment goes by ncclSend / ncclRecv in
+// one group on the handle's stream, then the received rows land in the public
+// table and the peers' status words in ext. Segment layout as
+// kmx_pgo_exchange_pack / _unpack.
+int enqueue_exchange(kmx_pgo* h) {
+  if (!h->xchg) return KMX_OK;
+  const int ps = 4 * h->P.r, W = h->world;
+  const long long ts = h->xn_send * ps + W, tr = h->xn_recv * ps + W;
+  hipLaunchKernelGGL(k_gather_slots, dim3((unsigned)((ts + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
+                     h->d_pub_src, h->d_xs_slots, h->xn_send, (int)h->npub, h->d_xsbuf, ps, h->d_xs_seg, W,
+                     (const double*)h->d_relc, h->dv.L);
+  KMX_NCCL(ncclGroupStart());
+  for (int q = 0; q < W; ++q) {
+    if (q == h->rank && !h->xchg_self_p2p) continue;
+    KMX_NCCL(ncclSend(h->d_xsbuf + h->xs_off[q], (size_t)h->xs_cnt[q], ncclDouble, q, h->comm, h->stream));
+    KMX_NCCL(ncclRecv(h->d_xrbuf + h->xr_off[q], (size_t)h->xr_cnt[q], ncclDouble, q, h->comm, h->stream));
+  }
+  KMX_NCCL(ncclGroupEnd());
+  if (!h->xchg_self_p2p)  // this handle's own segment (its status word)
+    KMX_HIP(hipMemcpyAsync(h->d_xrbuf + h->xr_off[h->rank], h->d_xsbuf + h->xs_off[h->rank],
+                           sizeof(double) * h->xs_cnt[h->rank], hipMemcpyDeviceToDevice, h->stream));
+  hipLaunchKernelGGL(k_scatter_slots, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, h->stream, h->d_pub,
+                     h->d_xr_slots, h->xn_recv, (int)h->npub, (const double*)h->d_xrbuf, ps, h->d_xr_seg, W,
+                     h->d_ext);
+  if (h->n_ext != W) {
+    h->n_ext = W;
+    sync_params(h);
+  }
+  KMX_HIP(hipGetLastError());
+  return KMX_OK;
+}
+
+extern "C" int kmx_comm_unique_id(void* out, int64_t nbytes) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(out && nbytes >= (int64_t)sizeof(ncclUniqueId), KMX_EINVAL, "need a buffer of KMX_COMM_ID_BYTES");
+  ncclUniqueId id;
+  KMX_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(out, &id, sizeof(id));
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, int rank) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(h && unique_id, KMX_EINVAL, "null argument");
+  KMX_CHECK(world >= 1 && world <= 1024 && rank >= 0 && rank < world, KMX_EINVAL, "bad world / rank");
+  KMX_CHECK(!h->comm, KMX_ESTATE, "communicator already initialised");
+  KMX_HIP(hipSetDevice(h->device));
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof(id));
+  ncclComm_t c = nullptr;
+  KMX_NCCL(ncclCommInitRank(&c, world, id, rank));
+  h->comm = c;
+  h->world = world;
+  h->rank = rank;
+  if (const char* v = std::getenv("KMX_XCHG_SELF_P2P")) h->xchg_self_p2p = std::atoi(v) != 0;
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_set_exchange(kmx_pgo* h, const int32_t* send_slots, const int64_t* send_counts,
+                                    const int32_t* recv_slots, const int64_t* recv_counts) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(h->comm, KMX_ESTATE, "kmx_pgo_comm_init first");
+  KMX_CHECK(send_counts && recv_counts, KMX_EINVAL, "null counts");
+  const int W = h->world, ps = 4 * h->P.r;
+  long long ns = 0, nr = 0;
+  for (int q = 0; q < W; ++q) {
+    KMX_CHECK(send_counts[q] >= 0 && recv_counts[q] >= 0, KMX_EINVAL, "negative count");
+    ns += send_counts[q];
+    nr += recv_counts[q];
+  }
+  KMX_CHECK(send_counts[h->rank] == recv_counts[h->rank], KMX_EINVAL, "own segment: send and receive counts differ");
+  KMX_CHECK((ns == 0 || send_slots) && (nr == 0 || recv_slots), KMX_EINVAL, "null slot list");
+  for (long long i = 0; i < ns; ++i) KMX_CHECK(send_slots[i] >= 0 && send_slots[i] < h->npub, KMX_EINVAL, "send slot out of range");
+  for (long long i = 0; i < nr; ++i) KMX_CHECK(recv_slots[i] >= 0 && recv_slots[i] < h->npub, KMX_EINVAL, "recv slot out of range");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  free_xchg(h);
+  std::vector<int> sseg(W + 1, 0), rseg(W + 1, 0);
+  h->xs_cnt.assign(W, 0); h->xr_cnt.assign(W, 0); h->xs_off.assign(W, 0); h->xr_off.assign(W, 0);
+  for (int q = 0; q < W; ++q) {
+    sseg[q + 1] = sseg[q] + (int)send_counts[q];
+    rseg[q + 1] = rseg[q] + (int)recv_counts[q];
+    h->xs_cnt[q] = send_counts[q] * ps + 1;
+    h->xr_cnt[q] = recv_counts[q] * ps + 1;
+    h->xs_off[q] = (long long)sseg[q] * ps + q;
+    h->xr_off[q] = (long long)rseg[q] * ps + q;
+  }
+  int rc = 0;
+  if ((rc = dalloc(&h->d_xs_slots, ns)) || (rc = dalloc(&h->d_xr_slots, nr)) || (rc = dalloc(&h->d_xs_seg, W + 1)) ||
+      (rc = dalloc(&h->d_xr_seg, W + 1)) || (rc = dalloc(&h->d_xsbuf, ns * ps + W)) ||
+      (rc = dalloc(&h->d_xrbuf, nr * ps + W))) {
+    free_xchg(h);
+    return rc;
+  }
+  if (W > h->ext_cap) {
+    if (h->d_ext) (void)hipFree(h->d_ext);
+    h->d_ext = nullptr;
+    h->ext_cap = 0;
+    if ((rc = dalloc(&h->d_ext, W))) return rc;
+    h->ext_cap = W;
+  }
+  if (ns) KMX_HIP(hipMemcpy(h->d_xs_slots, send_slots, sizeof(int) * ns, hipMemcpyHostToDevice));
+  if (nr) KMX_HIP(hipMemcpy(h->d_xr_slots, recv_slots, sizeof(int) * nr, hipMemcpyHostToDevice));
+  KMX_HIP(hipMemcpy(h->d_xs_seg, sseg.data(), sizeof(int) * (W + 1), hipMemcpyHostToDevice));
+  KMX_HIP(hipMemcpy(h->d_xr_seg, rseg.data(), sizeof(int) * (W + 1), hipMemcpyHostToDevice));
+  h->xn_send = ns;
+  h->xn_recv = nr;
+  h->xchg = true;
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_exchange(kmx_pgo* h) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(h->xchg, KMX_ESTATE, "kmx_pgo_set_exchange first");
+  KMX_HIP(hipSetDevice(h->device));
+  enqueue_accel_pre(h);
+  return enqueue_exchange(h);
+  KMX_GUARD_END
 }
 
 extern "C" int kmx_pgo_refresh_local(kmx_pgo* h) {
@@ -3134,6 +3323,7 @@ extern "C" int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats
       KMX_CHECK(act[l], KMX_EUNSUP, "acceleration needs every local robot active (concurrent schedule)");
   KMX_HIP(hipMemcpyAsync(h->d_active, act.data(), L, hipMemcpyHostToDevice, h->stream));
   enqueue_accel_pre(h);
+  if (int rc = enqueue_exchange(h)) return rc;
   enqueue_round(h, h->d_active);
   enqueue_accel_post(h);
   KMX_HIP(hipGetLastError());
@@ -3176,6 +3366,7 @@ extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local) 
   if (refresh_local && rounds > 0) enqueue_publish(h);
   for (int i = 0; i < rounds; ++i) {
     enqueue_accel_pre(h);  // publishes Y itself
+    if (int rc = enqueue_exchange(h)) return rc;
     enqueue_round(h, h->d_active);
     enqueue_accel_post(h);
   }

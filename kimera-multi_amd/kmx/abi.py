@@ -19,6 +19,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "libkmx.so"
 KMX_OK = 0
 ABI_VERSION = 4  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
 KMX_COST_L2 = 0
+KMX_COMM_ID_BYTES = 128  # include/kmx_abi.h (ncclUniqueId)
 KMX_COST_GNC_TLS = 1
 KMX_SCHEDULE_SEQUENTIAL = 0
 KMX_SCHEDULE_CONCURRENT = 1
@@ -133,6 +134,11 @@ def lib() -> C.CDLL:
         "kmx_pgo_create": ([C.POINTER(PgoParams), C.c_int, C.POINTER(P)], C.c_int),
         "kmx_pgo_destroy": ([P], C.c_int),
         "kmx_pgo_set_stream": ([P, P], C.c_int),
+        "kmx_pgo_set_tcg_poll": ([P, C.c_int], C.c_int),
+        "kmx_comm_unique_id": ([P, i64], C.c_int),
+        "kmx_pgo_comm_init": ([P, P, C.c_int, C.c_int], C.c_int),
+        "kmx_pgo_set_exchange": ([P, pi32, pi64, pi32, pi64], C.c_int),
+        "kmx_pgo_exchange": ([P], C.c_int),
         "kmx_pgo_set_graph": ([P, C.c_int, pi32, pu8, i64, pi32, pi32, pi32, pi32,
                                pf64, pf64, pf64, pf64, pf64, pu8], C.c_int),
         "kmx_pgo_set_iterate": ([P, C.c_int, pf64], C.c_int),

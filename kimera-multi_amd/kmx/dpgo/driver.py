@@ -37,6 +37,7 @@ per GPU). ROS topics become collectives over RCCL/xGMI:
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -132,6 +133,7 @@ class RBCDDriver:
         self.round_index = 0
         self._torch = None
         self._xdev = exchange_device
+        self.native = False  # RCCL exchange inside the solver's rounds (_setup_exchange)
         if world > 1:
             import torch
             import torch.distributed as dist
@@ -182,6 +184,18 @@ class RBCDDriver:
         self._sbuf = torch.zeros(sum(self._send_splits), dtype=torch.float64, device=dev)
         self._rbuf = torch.zeros(sum(self._recv_splits), dtype=torch.float64, device=dev)
         self.exchange_rows = (self._n_send, self._n_recv)
+        # RCCL inside the round (kmx_pgo_comm_init / kmx_pgo_set_exchange): the
+        # exchange runs on the solver's stream, enqueued by the same C call as
+        # the round, so a batch of rounds is one host call with no Python or
+        # cross-stream hop between exchange and round. KMX_NATIVE_XCHG=0 keeps
+        # the torch.distributed all_to_all of exchange_public.
+        self.native = (self._xdev == "cuda" and getattr(self.solver, "native_exchange", False)
+                       and os.environ.get("KMX_NATIVE_XCHG", "1") != "0")
+        if self.native:
+            uid = [self.solver.comm_unique_id() if self.rank == 0 else None]
+            self._dist.broadcast_object_list(uid, src=0)
+            self.solver.comm_init(uid[0], self.world, self.rank)
+            self.solver.set_exchange(send_slots, send_counts, recv_slots, recv_counts)
 
     def _all_to_all(self, out, inp):
         """One all-to-all with per-peer sizes (RCCL directly; a GPU solver under
@@ -194,13 +208,19 @@ class RBCDDriver:
         else:
             self._dist.all_to_all_single(out, inp, self._recv_splits, self._send_splits)
 
-    def exchange_public(self):
-        """publishPublicPoses -> updateNeighborPoses (+ publishStatus) for the
-        whole team."""
+    def _refresh_owned(self):
         if not (self._pub_fresh and getattr(self.solver, "publishes_on_commit", False)):
             self.solver.refresh_local()  # the owned slots of the table
             self._pub_fresh = True
+
+    def exchange_public(self):
+        """publishPublicPoses -> updateNeighborPoses (+ publishStatus) for the
+        whole team."""
+        self._refresh_owned()
         if self.world == 1:
+            return
+        if self.native:  # every round starts with it; this is an extra one (UPDATE_WEIGHT)
+            self.solver.exchange()
             return
         s = self.solver
         s.exchange_pack(self._sslots.data_ptr(), self._n_send, self._sseg.data_ptr(), self.world,
@@ -249,7 +269,10 @@ class RBCDDriver:
         """One synchronous round (its GNC decision runs on the device first).
         Returns per-robot stats (team-indexed) when with_stats."""
         self._check_running()
-        self.exchange_public()
+        if self.native:  # the round starts with the exchange itself
+            self._refresh_owned()
+        else:
+            self.exchange_public()
         stats = None
         if with_stats or self.params.schedule == 0 or self.logs or not self._all_active():
             act = self.active_mask()
@@ -269,7 +292,7 @@ class RBCDDriver:
         """Benchmark path: enqueue `rounds` concurrent rounds with no host sync
         (single GPU: one C call; multi-GPU: one all-to-all between rounds)."""
         self._check_running()
-        if self.world == 1 and self.params.schedule == 1 and self._all_active():
+        if (self.world == 1 or self.native) and self.params.schedule == 1 and self._all_active():
             self.solver.iterate_async(rounds, refresh_local=True)
             self.round_index += rounds
             return

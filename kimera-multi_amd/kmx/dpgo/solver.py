@@ -11,7 +11,7 @@ import ctypes as C
 import numpy as np
 
 from .. import abi
-from ..abi import check, fptr, iptr, u8ptr
+from ..abi import check, fptr, i64ptr, iptr, u8ptr
 from .params import PGOAgentParameters
 
 
@@ -52,6 +52,40 @@ class BlockSolver:
 
     def set_stream(self, hip_stream: int):
         check(self.L.kmx_pgo_set_stream(self.h, C.c_void_p(hip_stream)), "kmx_pgo_set_stream")
+
+    def set_tcg_poll(self, mode: int):
+        """-1 adaptive (default), 0 blind, 1 polled tCG enqueueing
+        (kmx_pgo_set_tcg_poll; identical results in every mode)."""
+        check(self.L.kmx_pgo_set_tcg_poll(self.h, int(mode)), "kmx_pgo_set_tcg_poll")
+
+    # ------------------------------------------------- native exchange ---
+    native_exchange = True  # kmx_pgo_comm_init / kmx_pgo_set_exchange (RCCL inside the round)
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """RCCL unique id (rank 0 creates it; every rank passes it to comm_init)."""
+        buf = C.create_string_buffer(abi.KMX_COMM_ID_BYTES)
+        check(abi.lib().kmx_comm_unique_id(C.cast(buf, C.c_void_p), abi.KMX_COMM_ID_BYTES), "kmx_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, unique_id: bytes, world: int, rank: int):
+        if len(unique_id) != abi.KMX_COMM_ID_BYTES:
+            raise ValueError(f"unique id must be {abi.KMX_COMM_ID_BYTES} bytes")
+        buf = C.create_string_buffer(bytes(unique_id), abi.KMX_COMM_ID_BYTES)
+        check(self.L.kmx_pgo_comm_init(self.h, C.cast(buf, C.c_void_p), int(world), int(rank)), "kmx_pgo_comm_init")
+
+    def set_exchange(self, send_slots, send_counts, recv_slots, recv_counts):
+        """The per-peer slot lists (kmx.dpgo.driver.exchange_plan); from now on
+        every round starts with the RCCL exchange on this handle's stream."""
+        ss = np.ascontiguousarray(send_slots, dtype=np.int32)
+        rs = np.ascontiguousarray(recv_slots, dtype=np.int32)
+        sc = np.ascontiguousarray(send_counts, dtype=np.int64)
+        rc = np.ascontiguousarray(recv_counts, dtype=np.int64)
+        check(self.L.kmx_pgo_set_exchange(self.h, iptr(ss), i64ptr(sc), iptr(rs), i64ptr(rc)), "kmx_pgo_set_exchange")
+
+    def exchange(self):
+        """One native exchange now (kmx_pgo_exchange), outside a round."""
+        check(self.L.kmx_pgo_exchange(self.h), "kmx_pgo_exchange")
 
     # ----------------------------------------------------------- graph ---
     def set_graph(self, n_poses, local, r1, p1, r2, p2, R, t, kappa, tau, weight, fixed):

@@ -150,3 +150,62 @@ def test_tile_cut_rule_matches_handle(gpu):
         drv.solver.close()
     for a in range(g.n_robots):
         assert np.array_equal(out[0][0][a], out[1][0][a]), a
+
+
+@pytest.mark.parametrize("self_p2p", ["0", "1"])
+def test_native_exchange_world1_matches_plain_rounds(gpu, monkeypatch, self_p2p):
+    """The RCCL exchange inside the round (kmx_pgo_comm_init / set_exchange) on a
+    world-1 communicator: the own segment (this handle's status word) is copied,
+    or with KMX_XCHG_SELF_P2P=1 sent to itself by ncclSend / ncclRecv. Rounds,
+    an explicit exchange and a GNC update give the same iterates bit for bit as
+    the handle without a communicator (the multi-peer path is the same group with
+    more peers; the 8-GPU run is the driver's)."""
+    import numpy as np
+    from kmx.dpgo.params import PGOAgentParameters
+    from kmx.dpgo.solver import BlockSolver
+    from kmx.synth import lift, lifting_matrix, make_pose_graph
+    monkeypatch.setenv("KMX_XCHG_SELF_P2P", self_p2p)
+    g = make_pose_graph(2, 400, 1200, seed=2)
+    P = PGOAgentParameters(r=5)
+    Y = lifting_matrix(5, seed=1)
+    out = []
+    for native in (False, True):
+        s = BlockSolver(P, 0)
+        s.set_graph_data(g)
+        s.set_gnc_schedule(True, 3, 50, P.relChangeTol)
+        if native:
+            s.comm_init(BlockSolver.comm_unique_id(), 1, 0)
+            s.set_exchange(np.zeros(0, np.int32), [0], np.zeros(0, np.int32), [0])
+        for a in range(g.n_robots):
+            s.set_iterate(a, lift(g.init_R[a], g.init_t[a], Y))
+        s.iterate_async(5, refresh_local=True)
+        if native:
+            s.exchange()
+        s.update_weights()
+        s.iterate_async(4, refresh_local=False)
+        s.sync()
+        out.append([s.get_iterate(a) for a in range(g.n_robots)] + [s.get_weights()])
+        s.close()
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+
+
+def test_native_exchange_checks(gpu):
+    import numpy as np
+    from kmx import abi
+    from kmx.dpgo.params import PGOAgentParameters
+    from kmx.dpgo.solver import BlockSolver
+    from kmx.synth import make_pose_graph
+    g = make_pose_graph(2, 50, 120, seed=1)
+    s = BlockSolver(PGOAgentParameters(r=5), 0)
+    s.set_graph_data(g)
+    with pytest.raises(abi.KmxError):  # before comm_init
+        s.set_exchange(np.zeros(0, np.int32), [0], np.zeros(0, np.int32), [0])
+    with pytest.raises(abi.KmxError):
+        s.exchange()
+    s.comm_init(BlockSolver.comm_unique_id(), 1, 0)
+    with pytest.raises(abi.KmxError):  # own segment counts differ
+        s.set_exchange(np.zeros(1, np.int32), [1], np.zeros(0, np.int32), [0])
+    with pytest.raises(abi.KmxError):  # slot out of range
+        s.set_exchange(np.array([10**6], np.int32), [1], np.array([0], np.int32), [1])
+    s.close()

@@ -399,3 +399,41 @@ def test_reduction_forms_agree_bitwise(gpu, monkeypatch):
         s.close()
     for a, b in zip(*out):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("red", ["0", "2"])
+def test_tcg_poll_modes_agree_bitwise(gpu, monkeypatch, red):
+    """Polled, blind and adaptive tCG enqueueing (kmx_pgo_set_tcg_poll 1 / 0 /
+    -1) launch the same work that matters: a blind step of a robot that already
+    left tCG exits at once. Iterates, GNC weights and work counters agree bit
+    for bit over rounds that cross GNC updates, in both reduction forms, and
+    the team status a multi-rank exchange carries is the same."""
+    monkeypatch.setenv("KMX_RED", red)
+    monkeypatch.delenv("KMX_POLL", raising=False)
+    g, P, X0 = _setup(robust=True, seed=6)
+    out = []
+    for mode in (1, 0, -1):
+        s = BlockSolver(P, 0)
+        s.set_tcg_poll(mode)
+        s.set_graph_data(g)
+        s.set_gnc_schedule(True, 3, 50, P.relChangeTol)
+        for a in range(g.n_robots):
+            s.set_iterate(a, X0[a])
+        s.read_counters()
+        s.iterate_async(14, refresh_local=True)
+        s.sync()
+        c = s.read_counters()
+        out.append([s.get_iterate(a) for a in range(g.n_robots)] + [s.get_weights(), s.status(),
+                   np.array([c["hessvecs"], c["edges_iters"], c["block_updates"], c["gnc_updates"]])])
+        s.close()
+    for other in out[1:]:
+        for a, b in zip(out[0], other):
+            assert np.array_equal(a, b)
+
+
+def test_tcg_poll_mode_checked(gpu):
+    P = PGOAgentParameters(r=5)
+    s = BlockSolver(P, 0)
+    with pytest.raises(abi.KmxError):
+        s.set_tcg_poll(2)
+    s.close()
