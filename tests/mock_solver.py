@@ -157,3 +157,57 @@ class OracleBlockSolver:
         mu = self.o.update_weights_local(self.local)
         self.gnc.updated()
         return mu
+
+
+class NativeOracleBlockSolver(OracleBlockSolver):
+    """The native-exchange interface of BlockSolver (kmx_pgo_comm_init /
+    set_exchange / exchange: every round of iterate / iterate_async starts with
+    the exchange) on the restatement, with the default torch.distributed group
+    (gloo) standing in for the handle's RCCL communicator. Lets the CPU tests run
+    RBCDDriver's native branch across ranks."""
+    native_exchange = True
+
+    @staticmethod
+    def comm_unique_id():
+        return bytes(range(128))
+
+    def comm_init(self, unique_id, world, rank):
+        assert len(unique_id) == 128
+        self.world, self.rank, self.xchg = world, rank, None
+        self.comm_inits = getattr(self, "comm_inits", 0) + 1
+
+    def set_exchange(self, send_slots, send_counts, recv_slots, recv_counts):
+        sc, rc = np.asarray(send_counts, np.int64), np.asarray(recv_counts, np.int64)
+        assert sc.shape == rc.shape == (self.world,) and sc[self.rank] == rc[self.rank]
+        ss, rs = np.ascontiguousarray(send_slots, np.int32), np.ascontiguousarray(recv_slots, np.int32)
+        sseg = np.concatenate([[0], np.cumsum(sc)]).astype(np.int32)
+        rseg = np.concatenate([[0], np.cumsum(rc)]).astype(np.int32)
+        ps = self._rows()
+        self.xchg = (ss if ss.size else np.zeros(1, np.int32), int(ss.size), sseg,
+                     rs if rs.size else np.zeros(1, np.int32), int(rs.size), rseg,
+                     [int(c) * ps + 1 for c in sc], [int(c) * ps + 1 for c in rc])
+        self.exchanges = 0
+
+    def exchange(self):
+        import torch
+        import torch.distributed as dist
+        ss, ns, sseg, rs, nr, rseg, ssplit, rsplit = self.xchg
+        sbuf, rbuf = np.zeros(sum(ssplit)), np.zeros(sum(rsplit))
+        self.exchange_pack(ss.ctypes.data, ns, sseg.ctypes.data, self.world, sbuf.ctypes.data)
+        out = torch.zeros(rbuf.shape[0], dtype=torch.float64)
+        dist.all_to_all_single(out, torch.from_numpy(sbuf), rsplit, ssplit)
+        rbuf[:] = out.numpy()
+        self.exchange_unpack(rs.ctypes.data, nr, rseg.ctypes.data, self.world, rbuf.ctypes.data)
+        self.exchanges += 1
+
+    def iterate(self, active):
+        self.exchange()
+        return self._round(active)
+
+    def iterate_async(self, rounds, refresh_local=True):
+        self.async_calls = getattr(self, "async_calls", 0) + 1
+        for _ in range(rounds):
+            if refresh_local:
+                self.refresh_local()
+            self.exchange()
+            self._round(self.local)

@@ -181,3 +181,48 @@ def test_exchange_plan_consistent(world):
             seg_recv = recv_q[off_r[k]:off_r[k + 1]]
             assert np.array_equal(seg_sent, seg_recv), (k, q)
             assert np.all(rank_of[keys[seg_sent] >> 32] == k)
+
+
+def _native_worker(rank, world, port, rounds, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kmx.dpgo.driver import RBCDDriver
+    from tests.mock_solver import NativeOracleBlockSolver
+    g, P = _graph(False), _params(1e-3, False)
+    s = NativeOracleBlockSolver(P)
+    drv = RBCDDriver(P, g, rank=rank, world=world, solver=s, exchange_device="cuda")
+    drv.initialize(_x0(g))
+    drv.step(with_stats=True)          # one exchange (the round's own)
+    drv.run_async(rounds - 2)          # one solver call for all its rounds
+    drv.step(with_stats=True)
+    q.put((rank, {a: drv.iterate_of(a) for a in drv.robots}, drv.weight_updates, drv.native, s.comm_inits,
+           s.exchanges, getattr(s, "async_calls", 0)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_native_exchange_branch_matches_single_process():
+    """RBCDDriver's native branch (the exchange inside the solver's rounds, the
+    RCCL path of a GPU team; here the mock solver runs it over gloo): the unique
+    id reaches every rank, each round exchanges exactly once (no extra exchange
+    from step(), run_async is one solver call), and the iterates equal the
+    single-process team run bit for bit."""
+    world, rounds = 2, 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_native_worker, args=(r, world, port, rounds, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    g, P = _graph(False), _params(1e-3, False)
+    o, sched = reference_rounds(g, P, rounds)
+    for rank, X, wu, native, inits, exchanges, async_calls in res:
+        assert native and inits == 1
+        assert exchanges == rounds and async_calls == 1
+        assert wu == sched.updates
+        for a, Xa in X.items():
+            assert np.array_equal(Xa, o.get_iterate(a)), (rank, a)
