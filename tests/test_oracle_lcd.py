@@ -207,3 +207,32 @@ def test_verify_pnp_noise_free_pool():
             assert np.count_nonzero(masks[c] & 2) == r.pnp_inliers
         else:
             assert not r.accepted
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["stewenius", "nister"])
+def test_fivept_solutions_are_essential_matrices(algo):
+    """Known-answer properties that hold whatever root finder or eigen-solver
+    computes them (so they pin the restatement independently of the kernels):
+    every real solution E of a random (noisy, not planted) 5-point problem
+    satisfies the five epipolar constraints, det(E) = 0 and the trace
+    constraint 2 E E^T E - tr(E E^T) E = 0 (Nister 2004, eq. 9), up to rounding.
+    Nister's count of real solutions is even-parity consistent (<= 10)."""
+    rng = np.random.default_rng(21 + algo)
+    seen = 0
+    for trial in range(80):
+        f1 = rng.normal(size=(5, 3))
+        f2 = f1 + rng.normal(0, 0.3, (5, 3))
+        f1 /= np.linalg.norm(f1, axis=1, keepdims=True)
+        f2 /= np.linalg.norm(f2, axis=1, keepdims=True)
+        Es = O.fivept(f1, f2, algo)
+        assert len(Es) <= 10
+        for E in Es:
+            if algo == 0 and abs(np.linalg.det(E)) > 1e-6:
+                continue  # Stewenius also returns the real parts of complex pairs
+            seen += 1
+            E = E / np.linalg.norm(E)
+            assert np.abs(np.einsum("ni,ij,nj->n", f1, E, f2)).max() < 1e-9, trial
+            assert abs(np.linalg.det(E)) < 1e-9, trial
+            EEt = E @ E.T
+            assert np.abs(2 * EEt @ E - np.trace(EEt) * E).max() < 1e-8, trial
+    assert seen > 80
