@@ -1225,10 +1225,97 @@ struct LB {
 
 // Start of an RTR iteration: egrad (gather X with public neighbours), cost,
 // S = sym(Y^T egrad_Y), g = P_Y(egrad), z = precon(g); partials f, |g|^2, <z,g>.
+// The per-pose 4x4 blocks D_i and the preconditioner (k_precond's work, same
+// expressions and order), also used by k_grad's gated prologue.
+template <int RW>
+__device__ __forceinline__ void pose_precond(const Dev& d, int pose) {
+  // A: the preconditioner's blocks (kappa I for the rotation part, as in the
+  // oracle); Dq: Q's exact diagonal block for the Hessian gather, which with
+  // the full records (measurements off SO(3)) carries w kappa R R^T instead
+  double A[16], Dq[16];
+  for (int i = 0; i < 16; ++i) A[i] = Dq[i] = 0.0;
+  for (int k = d.inc_ptr[pose]; k < d.inc_ptr[pose + 1]; ++k) {
+    double2 q[Rec<RW>::Q];
+    Rec<RW>::load(d.rec, (size_t)k, q);
+    Edge E;
+    Rec<RW>::edge(q, E);
+    const bool tail = (Rec<RW>::inc(q).y >> 31) & 1;
+    const double wk = E.wk, wt = E.wt;
+    const double* tt = E.t;
+    if (tail) {
+      for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) {
+          A[i * 4 + j] += wt * tt[i] * tt[j] + (i == j ? wk : 0.0);
+          const double rr = (RW == 10) ? (i == j ? 1.0 : 0.0)
+                                       : E.R[i * 3 + 0] * E.R[j * 3 + 0] + E.R[i * 3 + 1] * E.R[j * 3 + 1] +
+                                             E.R[i * 3 + 2] * E.R[j * 3 + 2];
+          Dq[i * 4 + j] += wt * tt[i] * tt[j] + wk * rr;
+        }
+        A[i * 4 + 3] += wt * tt[i];
+        A[3 * 4 + i] += wt * tt[i];
+        Dq[i * 4 + 3] += wt * tt[i];
+        Dq[3 * 4 + i] += wt * tt[i];
+      }
+      A[15] += wt;
+      Dq[15] += wt;
+    } else {
+      A[0] += wk; A[5] += wk; A[10] += wk; A[15] += wt;
+      Dq[0] += wk; Dq[5] += wk; Dq[10] += wk; Dq[15] += wt;
+    }
+  }
+  {
+    double* Dp = d.hD + SYM4 * (size_t)pose;
+    int j = 0;
+    for (int a = 0; a < 4; ++a)
+      for (int b = a; b < 4; ++b) Dp[j++] = Dq[a * 4 + b];
+  }
+  for (int j = 0; j < 4; ++j) A[j * 5] += d.p.shift;
+  double Lm[16], Li[16];
+  for (int i = 0; i < 16; ++i) { Lm[i] = 0.0; Li[i] = 0.0; }
+  for (int j = 0; j < 4; ++j) {
+    double s = A[j * 4 + j];
+    for (int k = 0; k < j; ++k) s -= Lm[j * 4 + k] * Lm[j * 4 + k];
+    Lm[j * 4 + j] = sqrt(s);
+    for (int ii = j + 1; ii < 4; ++ii) {
+      double t = A[ii * 4 + j];
+      for (int k = 0; k < j; ++k) t -= Lm[ii * 4 + k] * Lm[j * 4 + k];
+      Lm[ii * 4 + j] = t / Lm[j * 4 + j];
+    }
+  }
+  for (int c = 0; c < 4; ++c)
+    for (int ii = 0; ii < 4; ++ii) {
+      double s = (ii == c) ? 1.0 : 0.0;
+      for (int k = c; k < ii; ++k) s -= Lm[ii * 4 + k] * Li[k * 4 + c];
+      Li[ii * 4 + c] = (ii < c) ? 0.0 : s / Lm[ii * 4 + ii];
+    }
+  double* Pi = d.Pinv + SYM4 * (size_t)pose;  // Li^T Li: symmetric (upper triangle)
+  int j = 0;
+  for (int x = 0; x < 4; ++x)
+    for (int y = x; y < 4; ++y) {
+      double s = 0.0;
+      for (int k = 0; k < 4; ++k) s += Li[k * 4 + x] * Li[k * 4 + y];
+      Pi[j++] = s;
+    }
+}
+
+// gated: the first gradient of a round whose begin launch may have re-weighted
+// (the k_precond launch folded in): block 0 commits the GNC state and, when
+// the begin fired, every tile rebuilds D_i and the preconditioner of its own
+// poses (only its own incidence records are read) before the phase test, so
+// idle robots are rebuilt too. The writes are read back by the tile's own
+// lanes after the workgroup barrier (one CU: workgroup-scope visibility).
 template <int R, int RW, int RM>
-__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d) {
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d, int gated) {
   KMX_SMEM;
   const Lane L = lane_map<R>(d);
+  if (gated) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *d.gnc = *d.gnc_next;
+    if (d.gnc_next->fired) {
+      const int np = d.tile_np[L.tile], p0 = d.tile_p0[L.tile];
+      for (int t = threadIdx.x; t < np; t += blockDim.x) pose_precond<RW>(d, p0 + t);
+      __syncthreads();
+    }
+  }
   if (d.ctl[L.l].phase != PH_START) return;
   double y[4] = {0, 0, 0, 0}, G[4], cost = 0.0;
   hinc_grad<R, RW>(d, L, d.X, d.pub, G, &cost, smem);
@@ -1741,75 +1828,8 @@ __global__ void k_precond(Dev d, int gated) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *d.gnc = *d.gnc_next;
     if (!d.gnc_next->fired) return;
   }
-  for (int pose = blockIdx.x * blockDim.x + threadIdx.x; pose < d.nloc; pose += gridDim.x * blockDim.x) {
-    // A: the preconditioner's blocks (kappa I for the rotation part, as in the
-    // oracle); Dq: Q's exact diagonal block for the Hessian gather, which with
-    // the full records (measurements off SO(3)) carries w kappa R R^T instead
-    double A[16], Dq[16];
-    for (int i = 0; i < 16; ++i) A[i] = Dq[i] = 0.0;
-    for (int k = d.inc_ptr[pose]; k < d.inc_ptr[pose + 1]; ++k) {
-      double2 q[Rec<RW>::Q];
-      Rec<RW>::load(d.rec, (size_t)k, q);
-      Edge E;
-      Rec<RW>::edge(q, E);
-      const bool tail = (Rec<RW>::inc(q).y >> 31) & 1;
-      const double wk = E.wk, wt = E.wt;
-      const double* tt = E.t;
-      if (tail) {
-        for (int i = 0; i < 3; ++i) {
-          for (int j = 0; j < 3; ++j) {
-            A[i * 4 + j] += wt * tt[i] * tt[j] + (i == j ? wk : 0.0);
-            const double rr = (RW == 10) ? (i == j ? 1.0 : 0.0)
-                                         : E.R[i * 3 + 0] * E.R[j * 3 + 0] + E.R[i * 3 + 1] * E.R[j * 3 + 1] +
-                                               E.R[i * 3 + 2] * E.R[j * 3 + 2];
-            Dq[i * 4 + j] += wt * tt[i] * tt[j] + wk * rr;
-          }
-          A[i * 4 + 3] += wt * tt[i];
-          A[3 * 4 + i] += wt * tt[i];
-          Dq[i * 4 + 3] += wt * tt[i];
-          Dq[3 * 4 + i] += wt * tt[i];
-        }
-        A[15] += wt;
-        Dq[15] += wt;
-      } else {
-        A[0] += wk; A[5] += wk; A[10] += wk; A[15] += wt;
-        Dq[0] += wk; Dq[5] += wk; Dq[10] += wk; Dq[15] += wt;
-      }
-    }
-    {
-      double* Dp = d.hD + SYM4 * (size_t)pose;
-      int j = 0;
-      for (int a = 0; a < 4; ++a)
-        for (int b = a; b < 4; ++b) Dp[j++] = Dq[a * 4 + b];
-    }
-    for (int j = 0; j < 4; ++j) A[j * 5] += d.p.shift;
-    double Lm[16], Li[16];
-    for (int i = 0; i < 16; ++i) { Lm[i] = 0.0; Li[i] = 0.0; }
-    for (int j = 0; j < 4; ++j) {
-      double s = A[j * 4 + j];
-      for (int k = 0; k < j; ++k) s -= Lm[j * 4 + k] * Lm[j * 4 + k];
-      Lm[j * 4 + j] = sqrt(s);
-      for (int ii = j + 1; ii < 4; ++ii) {
-        double t = A[ii * 4 + j];
-        for (int k = 0; k < j; ++k) t -= Lm[ii * 4 + k] * Lm[j * 4 + k];
-        Lm[ii * 4 + j] = t / Lm[j * 4 + j];
-      }
-    }
-    for (int c = 0; c < 4; ++c)
-      for (int ii = 0; ii < 4; ++ii) {
-        double s = (ii == c) ? 1.0 : 0.0;
-        for (int k = c; k < ii; ++k) s -= Lm[ii * 4 + k] * Li[k * 4 + c];
-        Li[ii * 4 + c] = (ii < c) ? 0.0 : s / Lm[ii * 4 + ii];
-      }
-    double* Pi = d.Pinv + SYM4 * (size_t)pose;  // Li^T Li: symmetric (upper triangle)
-    int j = 0;
-    for (int x = 0; x < 4; ++x)
-      for (int y = x; y < 4; ++y) {
-        double s = 0.0;
-        for (int k = 0; k < 4; ++k) s += Li[k * 4 + x] * Li[k * 4 + y];
-        Pi[j++] = s;
-      }
-  }
+  for (int pose = blockIdx.x * blockDim.x + threadIdx.x; pose < d.nloc; pose += gridDim.x * blockDim.x)
+    pose_precond<RW>(d, pose);
 }
 
 // setMeasurementWeight in bulk: push the per-edge weights into both incidence
@@ -2372,7 +2392,9 @@ void enqueue_precond(kmx_pgo* h, int gated) {
 
 // Round begin (mode BEGIN_ROUND) and/or GNC update, then the gated
 // preconditioner rebuild that commits the GNC state.
-void enqueue_begin(kmx_pgo* h, const unsigned char* d_active, int mode) {
+// Returns whether the gated preconditioner rebuild is left to the next k_grad
+// (defer: the round's first gradient follows this launch directly).
+bool enqueue_begin(kmx_pgo* h, const unsigned char* d_active, int mode, bool defer = false) {
   const bool may_fire = h->P.robust_cost == KMX_COST_GNC_TLS && (h->gnc_on || (mode & BEGIN_FORCE_GNC));
   if (!may_fire) mode |= BEGIN_SOLO;  // no weight update possible: one block, no preconditioner rebuild
   // a capped grid: when the schedule does not fire, the launch costs its dispatch
@@ -2381,7 +2403,8 @@ void enqueue_begin(kmx_pgo* h, const unsigned char* d_active, int mode) {
     hipLaunchKernelGGL(k_begin<10>, dim3(grid), dim3(256), 0, h->stream, h->dv, d_active, mode, h->P.r);
   else
     hipLaunchKernelGGL(k_begin<16>, dim3(grid), dim3(256), 0, h->stream, h->dv, d_active, mode, h->P.r);
-  if (may_fire) enqueue_precond(h, 1);
+  if (may_fire && !defer) enqueue_precond(h, 1);
+  return may_fire && defer;
 }
 
 // Wait until every robot with tiles reported tCG step `seq`; returns whether
@@ -2433,8 +2456,8 @@ bool fold_cost(const kmx_pgo* h) {
 }
 
 template <int R, int RW, int RM>
-void enqueue_grad_t(kmx_pgo* h) {
-  hipLaunchKernelGGL((k_grad<R, RW, RM>), dim3(h->ntiles), dim3(BLOCK), SmemHG<R>::bytes, h->stream, h->dv);
+void enqueue_grad_t(kmx_pgo* h, int gated = 0) {
+  hipLaunchKernelGGL((k_grad<R, RW, RM>), dim3(h->ntiles), dim3(BLOCK), SmemHG<R>::bytes, h->stream, h->dv, gated);
   if (!fold_grad<RM>(h)) red_t<R, RM>(h, RED_GRAD);
 }
 
@@ -2505,11 +2528,12 @@ void enqueue_trial_t(kmx_pgo* h, bool rgd) {
 
 template <int R, int RW, int RM>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
-  enqueue_begin(h, d_active, BEGIN_ROUND);
+  // no tiles: nothing would run the deferred rebuild
+  const bool pend = enqueue_begin(h, d_active, BEGIN_ROUND, h->ntiles > 0);
   const bool rgd = h->P.method == KMX_METHOD_RGD;
   const int iters = rgd ? 1 : h->P.rtr_iterations;
   for (int it = 0; it < iters; ++it) {
-    enqueue_grad_t<R, RW, RM>(h);
+    enqueue_grad_t<R, RW, RM>(h, it == 0 && pend ? 1 : 0);
     if (!rgd) enqueue_tcg_t<R, RW, RM>(h);
     enqueue_trial_t<R, RW, RM>(h, rgd);
     if (it + 1 < iters)  // the next RTR iteration starts from the accepted point
