@@ -20,8 +20,9 @@ Hessian-vector launch: the roofline describes exactly the timed rounds (the
 replay must reproduce their work counters). The CPU baseline restarts the
 restatement from the same snapshot and times the same rounds.
 
-Multi-GPU (one process per GPU, robot blocks dealt to ranks, one all-to-all of
-public poses + status words per round over RCCL):
+Multi-GPU (one process per GPU, robot blocks dealt to ranks; per round the
+public poses + status words go to every peer over RCCL, by default from inside
+the solver's round: kmx_pgo_comm_init / kmx_pgo_set_exchange):
   --scaling strong (default): the fixed configs[3] graph split over the N GPUs
       (north_star's "further scaling at 8 GPUs"); value is the team's rate.
   --scaling weak: every GPU holds a configs[3]-shaped shard (8N robot blocks,
@@ -361,6 +362,7 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
         hv_ms, hv_bytes, hv_n = r["hessvec_ms_total"], r["hessvec_alg_bytes"], r["hessvec_launches"]
         same = all(r[k] == c[k] for k in ("edges_iters", "hessvecs", "block_updates", "gnc_updates"))
     xs, xr = drv.exchange_rows
+    native = bool(drv.native)
     mem = drv.solver.memory()[0]
     tot = _gather(dist, world, [el, float(c["edges_iters"]), float(c["hessvecs"]), float(c["block_updates"]),
                                 float(c["gnc_updates"]), hv_ms, hv_bytes, float(hv_n), float(xs), float(xr),
@@ -370,7 +372,7 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
     return {"el": tot[0], "edges_iters": tot[1], "hessvecs": tot[2], "block_updates": tot[3],
             "gnc_updates": int(tot[4]), "hv": (tot[5], tot[6], int(tot[7])), "xrows": (int(tot[8]), int(tot[9])),
             "mem_max": int(tot[10]), "replay_identical": (tot[11] == world) if replay and snap is not None else None,
-            "snap": snap}
+            "snap": snap, "native": native}
 
 
 def main():
@@ -446,7 +448,10 @@ def main():
             "timed_rounds": [w0, w0 + args.steps] if not args.profile else [0, args.steps],
             "burn_in_rounds": 0 if args.profile else args.burn_in,
             "parallelism": f"robot blocks {g.n_robots} over {world} GPU(s)"
-                           + (", public poses + status by one RCCL all_to_all per round" if world > 1 else ""),
+                           + ((", public poses + status exchanged over RCCL "
+                               + ("(ncclSend/ncclRecv group inside each round, on the solver's stream)"
+                                  if leg["native"] else "(torch.distributed all_to_all_single per round)"))
+                              if world > 1 else ""),
             "exchange_rows_per_round": {"sent_max": leg["xrows"][0], "recv_max": leg["xrows"][1],
                                         "recv_bytes_max": leg["xrows"][1] * ps_bytes},
             "graph_gen_s": round(gen_s, 1),
