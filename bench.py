@@ -448,9 +448,10 @@ def main():
             "timed_rounds": [w0, w0 + args.steps] if not args.profile else [0, args.steps],
             "burn_in_rounds": 0 if args.profile else args.burn_in,
             "parallelism": f"robot blocks {g.n_robots} over {world} GPU(s)"
-                           + ((", public poses + status exchanged over RCCL "
-                               + ("(ncclSend/ncclRecv group inside each round, on the solver's stream)"
-                                  if leg["native"] else "(torch.distributed all_to_all_single per round)"))
+                           + ((", public poses + status exchanged "
+                               + ("over RCCL (ncclSend/ncclRecv group inside each round, on the solver's stream)"
+                                  if leg["native"] else
+                                  f"by torch.distributed all_to_all_single ({dist.get_backend()}) per round"))
                               if world > 1 else ""),
             "exchange_rows_per_round": {"sent_max": leg["xrows"][0], "recv_max": leg["xrows"][1],
                                         "recv_bytes_max": leg["xrows"][1] * ps_bytes},

@@ -235,7 +235,7 @@ __global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int*
                                                             const long long* qptr, const unsigned* qw,
                                                             const double* qv, const int* max_id, int K,
                                                             int* out_n, int* out_id, double* out_score,
-                                                            int* err, int dbg) {
+                                                            int* err) {
   extern __shared__ __attribute__((aligned(16))) char bsm[];
   double* acc = reinterpret_cast<double*>(bsm);                   // [ch]
   double* c_val = acc + LCH;                                        // [LSEL]        \  selection scratch;
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int*
           apply(e3, d3, w3, k3);
         }
       };
-      for (long long b0 = q0; b0 < q1 && !(dbg & 1); b0 += QW) {
+      for (long long b0 = q0; b0 < q1; b0 += QW) {
         const int nw = (int)min((long long)QW, q1 - b0);
         __syncthreads();  // accumulator zeroed / previous batch's weights no longer read
         for (int i = tid; i < nw; i += LW_BLOCK) wq[i] = qv[b0 + i];
@@ -378,7 +378,6 @@ __global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int*
       }
       __syncthreads();
       // ---- this chunk's best min(K, touched) by (acc, id): LDS histogram narrowing
-      if (dbg & 2) continue;  // diagnostic: accumulation only
       if (tid == 0) { s_nt = 0; s_ns = 0; s_done = 0; }
       __syncthreads();
       {
@@ -541,7 +540,6 @@ struct kmx_bow {
   int* d_err = nullptr;
   // LDS-accumulator query (k_bow_query_lds): per-word chunk split points
   bool lds = true;
-  int dbg = 0;  // KMX_BOW_DBG (diagnostic timing only): bit 0 skips accumulation, bit 1 the top-K
   int ch = 0, nch = 0;
   int* d_cptr = nullptr;
   size_t qcap = 0, wcap = 0;
@@ -670,7 +668,6 @@ extern "C" int kmx_bow_set_database(kmx_bow* h, int32_t n_words, int32_t n_entri
   // entries per LDS chunk (tests use small chunks to cover the merge)
   h->lds = true;
   if (const char* v = std::getenv("KMX_BOW_LDS")) h->lds = std::atoi(v) != 0;
-  if (const char* v = std::getenv("KMX_BOW_DBG")) h->dbg = std::atoi(v);
   h->ch = LCH;
   if (const char* v = std::getenv("KMX_BOW_CHUNK")) h->ch = std::max(1, std::min(LCH, std::atoi(v)));
   h->ch = (h->ch + LW_WAVES - 1) / LW_WAVES * LW_WAVES;  // whole sub-ranges, one per wave
@@ -756,7 +753,7 @@ extern "C" int kmx_bow_query_async(kmx_bow* h, int32_t nq, const int64_t* qptr, 
                        (const int*)h->d_cptr, h->nch, h->ch, nq, (const long long*)h->d_qptr,
                        (const unsigned*)h->d_qw, (const double*)h->d_qv,
                        max_id ? (const int*)h->d_maxid : nullptr, max_results, h->d_n, h->d_id, h->d_score,
-                       h->d_err, h->dbg);
+                       h->d_err);
     KMX_HIP(hipGetLastError());
     return KMX_OK;
   }

@@ -2199,11 +2199,8 @@ struct kmx_pgo {
   std::vector<long long> xs_cnt, xr_cnt, xs_off, xr_off;  // per peer, in doubles (rows * 4r + 1 status)
   int blind_left = 0;
   static constexpr int BLIND_SLACK = 2, BLIND_WINDOW = 8;
-  // KMX_QUERY=1: hipStreamQuery before the status spin. Measured: the query
-  // puts a ~5 us bubble before the next tCG step's first kernel (profiles/r02/
-  // ab_query: 0.836 vs 0.863 ms per round; wall = busy without it), and
-  // launches reach the hardware queue without it
-  bool query = false;
+  // (measured and removed: a hipStreamQuery before the status spin put a ~5 us
+  // bubble before the next tCG step's first kernel, profiles/r02/ab_query)
   // reduction mode: set per graph (below) unless KMX_RED forces one (0 launch,
   // 1 tickets, 2 consumer, 3 half). Measured at the end of round 2
   // (profiles/r02/small_round/16_*): the consumer form (no reduction launch,
@@ -2412,7 +2409,6 @@ bool enqueue_begin(kmx_pgo* h, const unsigned char* d_active, int mode, bool def
 // the handle to blind enqueueing (every tCG step launched).
 bool wait_running(kmx_pgo* h, unsigned long long seq) {
   volatile HostStatus* hs = h->hstat;
-  if (h->query) (void)hipStreamQuery(h->stream);  // KMX_QUERY=1: force submission before spinning
   const auto t0 = std::chrono::steady_clock::now();
   bool running = false;
   for (int l = 0; l < h->dv.L; ++l) {
@@ -2661,7 +2657,6 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     h->poll_auto = false;
   }
   if (const char* v = std::getenv("KMX_EARLY")) h->early_forced = std::atoi(v) != 0 ? 1 : 0;
-  if (const char* v = std::getenv("KMX_QUERY")) h->query = std::atoi(v) != 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);
     h->rm_forced = m == 0 ? RM_LAUNCH : m == 1 ? RM_TICKET : m == 2 ? RM_CONSUMER : RM_HALF;
