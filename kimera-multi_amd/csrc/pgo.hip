@@ -1906,6 +1906,38 @@ __global__ void k_scatter_slots(double* pub, const int* slots, long long n, int 
   if (sl >= 0 && sl < npub) pub[(long long)sl * ps + q] = rows[i + seg_offset(seg, nseg, s)];
 }
 
+// The native exchange's gather / scatter (enqueue_exchange): the segment of
+// every row is precomputed (rseg[s], set_exchange), so a thread reads one int
+// instead of walking the segment table; status words as above.
+__global__ void k_xgather(const double* X, const int* pub_src, const int* slots, const int* rseg, long long n,
+                          double* out, int ps, const int* seg, int nseg, const double* relc, int L) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long s = i / ps;
+  if (s >= n) {
+    const long long k = i - n * ps;
+    if (k >= nseg) return;
+    double m = 0.0;
+    for (int l = 0; l < L; ++l) m = (relc[l] > m || relc[l] != relc[l]) ? relc[l] : m;
+    out[(long long)seg[k + 1] * ps + k] = m;
+    return;
+  }
+  const int q = (int)(i - s * ps);
+  const int p = pub_src[slots[s]];
+  out[i + rseg[s]] = (p >= 0) ? X[(long long)p * ps + q] : 0.0;
+}
+__global__ void k_xscatter(double* pub, const int* slots, const int* rseg, long long n, const double* rows, int ps,
+                           const int* seg, int nseg, double* ext) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long s = i / ps;
+  if (s >= n) {
+    const long long k = i - n * ps;
+    if (k < nseg) ext[k] = rows[(long long)seg[k + 1] * ps + k];
+    return;
+  }
+  const int q = (int)(i - s * ps);
+  pub[(long long)slots[s] * ps + q] = rows[i + rseg[s]];
+}
+
 __global__ void k_pack(const double* X, double* out, const int* src, int first, int count, int ps) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long s = i / ps;
@@ -2194,6 +2226,7 @@ struct kmx_pgo {
   int world = 1, rank = 0;
   bool xchg = false, xchg_self_p2p = false;
   int *d_xs_slots = nullptr, *d_xr_slots = nullptr, *d_xs_seg = nullptr, *d_xr_seg = nullptr;
+  int *d_xs_rseg = nullptr, *d_xr_rseg = nullptr;  // segment index of every row
   double *d_xsbuf = nullptr, *d_xrbuf = nullptr;
   long long xn_send = 0, xn_recv = 0;
   std::vector<long long> xs_cnt, xr_cnt, xs_off, xr_off;  // per peer, in doubles (rows * 4r + 1 status)
@@ -2272,10 +2305,11 @@ int dalloc(T** p, size_t count) {
 }
 
 void free_xchg(kmx_pgo* h) {
-  void* ptrs[] = {h->d_xs_slots, h->d_xr_slots, h->d_xs_seg, h->d_xr_seg, h->d_xsbuf, h->d_xrbuf};
+  void* ptrs[] = {h->d_xs_slots, h->d_xr_slots, h->d_xs_seg, h->d_xr_seg, h->d_xs_rseg, h->d_xr_rseg,
+                  h->d_xsbuf, h->d_xrbuf};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
-  h->d_xs_slots = h->d_xr_slots = h->d_xs_seg = h->d_xr_seg = nullptr;
+  h->d_xs_slots = h->d_xr_slots = h->d_xs_seg = h->d_xr_seg = h->d_xs_rseg = h->d_xr_rseg = nullptr;
   h->d_xsbuf = h->d_xrbuf = nullptr;
   h->xchg = false;
 }
@@ -3181,8 +3215,8 @@ int enqueue_exchange(kmx_pgo* h) {
   if (!h->xchg) return KMX_OK;
   const int ps = 4 * h->P.r, W = h->world;
   const long long ts = h->xn_send * ps + W, tr = h->xn_recv * ps + W;
-  hipLaunchKernelGGL(k_gather_slots, dim3((unsigned)((ts + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
-                     h->d_pub_src, h->d_xs_slots, h->xn_send, (int)h->npub, h->d_xsbuf, ps, h->d_xs_seg, W,
+  hipLaunchKernelGGL(k_xgather, dim3((unsigned)((ts + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
+                     h->d_pub_src, h->d_xs_slots, h->d_xs_rseg, h->xn_send, h->d_xsbuf, ps, h->d_xs_seg, W,
                      (const double*)h->d_relc, h->dv.L);
   KMX_NCCL(ncclGroupStart());
   for (int q = 0; q < W; ++q) {
@@ -3194,9 +3228,8 @@ int enqueue_exchange(kmx_pgo* h) {
   if (!h->xchg_self_p2p)  // this handle's own segment (its status word)
     KMX_HIP(hipMemcpyAsync(h->d_xrbuf + h->xr_off[h->rank], h->d_xsbuf + h->xs_off[h->rank],
                            sizeof(double) * h->xs_cnt[h->rank], hipMemcpyDeviceToDevice, h->stream));
-  hipLaunchKernelGGL(k_scatter_slots, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, h->stream, h->d_pub,
-                     h->d_xr_slots, h->xn_recv, (int)h->npub, (const double*)h->d_xrbuf, ps, h->d_xr_seg, W,
-                     h->d_ext);
+  hipLaunchKernelGGL(k_xscatter, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, h->stream, h->d_pub,
+                     h->d_xr_slots, h->d_xr_rseg, h->xn_recv, (const double*)h->d_xrbuf, ps, h->d_xr_seg, W, h->d_ext);
   if (h->n_ext != W) {
     h->n_ext = W;
     sync_params(h);
@@ -3265,6 +3298,7 @@ extern "C" int kmx_pgo_set_exchange(kmx_pgo* h, const int32_t* send_slots, const
   }
   int rc = 0;
   if ((rc = dalloc(&h->d_xs_slots, ns)) || (rc = dalloc(&h->d_xr_slots, nr)) || (rc = dalloc(&h->d_xs_seg, W + 1)) ||
+      (rc = dalloc(&h->d_xs_rseg, ns)) || (rc = dalloc(&h->d_xr_rseg, nr)) ||
       (rc = dalloc(&h->d_xr_seg, W + 1)) || (rc = dalloc(&h->d_xsbuf, ns * ps + W)) ||
       (rc = dalloc(&h->d_xrbuf, nr * ps + W))) {
     free_xchg(h);
@@ -3279,6 +3313,15 @@ extern "C" int kmx_pgo_set_exchange(kmx_pgo* h, const int32_t* send_slots, const
   }
   if (ns) KMX_HIP(hipMemcpy(h->d_xs_slots, send_slots, sizeof(int) * ns, hipMemcpyHostToDevice));
   if (nr) KMX_HIP(hipMemcpy(h->d_xr_slots, recv_slots, sizeof(int) * nr, hipMemcpyHostToDevice));
+  {
+    std::vector<int> srs(std::max<long long>(ns, 1)), rrs(std::max<long long>(nr, 1));
+    for (int q = 0; q < W; ++q) {
+      for (int k = sseg[q]; k < sseg[q + 1]; ++k) srs[k] = q;
+      for (int k = rseg[q]; k < rseg[q + 1]; ++k) rrs[k] = q;
+    }
+    if (ns) KMX_HIP(hipMemcpy(h->d_xs_rseg, srs.data(), sizeof(int) * ns, hipMemcpyHostToDevice));
+    if (nr) KMX_HIP(hipMemcpy(h->d_xr_rseg, rrs.data(), sizeof(int) * nr, hipMemcpyHostToDevice));
+  }
   KMX_HIP(hipMemcpy(h->d_xs_seg, sseg.data(), sizeof(int) * (W + 1), hipMemcpyHostToDevice));
   KMX_HIP(hipMemcpy(h->d_xr_seg, rseg.data(), sizeof(int) * (W + 1), hipMemcpyHostToDevice));
   h->xn_send = ns;
