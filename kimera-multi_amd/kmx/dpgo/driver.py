@@ -192,10 +192,21 @@ class RBCDDriver:
         self.native = (self._xdev == "cuda" and getattr(self.solver, "native_exchange", False)
                        and os.environ.get("KMX_NATIVE_XCHG", "1") != "0")
         if self.native:
-            uid = [self.solver.comm_unique_id() if self.rank == 0 else None]
-            self._dist.broadcast_object_list(uid, src=0)
-            self.solver.comm_init(uid[0], self.world, self.rank)
-            self.solver.set_exchange(send_slots, send_counts, recv_slots, recv_counts)
+            ok = 1
+            try:
+                uid = [self.solver.comm_unique_id() if self.rank == 0 else None]
+                self._dist.broadcast_object_list(uid, src=0)
+                self.solver.comm_init(uid[0], self.world, self.rank)
+            except Exception as e:  # every rank falls back together (one MIN all-reduce)
+                import warnings
+                warnings.warn(f"native RCCL exchange unavailable ({e}); using torch.distributed all_to_all")
+                ok = 0
+            flag = torch.tensor([ok], dtype=torch.int32,
+                                device="cuda" if self._dist.get_backend() == "nccl" else "cpu")
+            self._dist.all_reduce(flag, op=self._dist.ReduceOp.MIN)
+            self.native = bool(flag.item())
+            if self.native:
+                self.solver.set_exchange(send_slots, send_counts, recv_slots, recv_counts)
 
     def _all_to_all(self, out, inp):
         """One all-to-all with per-peer sizes (RCCL directly; a GPU solver under

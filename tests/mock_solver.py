@@ -200,8 +200,12 @@ class NativeOracleBlockSolver(OracleBlockSolver):
         self.exchange_unpack(rs.ctypes.data, nr, rseg.ctypes.data, self.world, rbuf.ctypes.data)
         self.exchanges += 1
 
+    def _native(self):  # the exchange lists are set: every round starts with the exchange
+        if getattr(self, "xchg", None) is not None:
+            self.exchange()
+
     def iterate(self, active):
-        self.exchange()
+        self._native()
         return self._round(active)
 
     def iterate_async(self, rounds, refresh_local=True):
@@ -209,5 +213,5 @@ class NativeOracleBlockSolver(OracleBlockSolver):
         for _ in range(rounds):
             if refresh_local:
                 self.refresh_local()
-            self.exchange()
+            self._native()
             self._round(self.local)
