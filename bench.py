@@ -178,8 +178,35 @@ def cpu_baseline(g, P, snap, steps, seconds, threads_list):
                 break
         el = time.perf_counter() - t0
         out[threads] = {"value": edges_iters / el, "rounds": rounds, "seconds": el, "hessvecs": hv,
-                        "ms_per_step": 1e3 * el / rounds}
+                        "ms_per_step": 1e3 * el / rounds, "edges_iters": edges_iters,
+                        "X": {a: o.get_iterate(a) for a in range(g.n_robots)}}
     return out
+
+
+def gpu_parity(drv, snap, cpu):
+    """Free full-size, steady-state parity check: replay on the GPU, from the
+    same snapshot, exactly the rounds the CPU leg ran, and compare the work
+    counters (Hess-vecs, edges*iters) and every pose with the restatement's
+    (north_star: 1e-6 Frobenius per pose)."""
+    restore(drv, snap)
+    drv.solver.sync()
+    drv.solver.read_counters()
+    drv.run_async(cpu["rounds"])
+    drv.solver.sync()
+    c = drv.solver.read_counters()
+    worst = 0.0
+    for a in drv.robots:
+        d = np.linalg.norm((drv.iterate_of(a) - cpu["X"][a]).reshape(-1, 4 * drv.params.r), axis=1)
+        worst = max(worst, float(d.max()) if d.size else 0.0)
+    ok = int(c["hessvecs"]) == int(cpu["hessvecs"]) and int(c["edges_iters"]) == int(cpu["edges_iters"]) \
+        and worst <= 1e-6
+    if not ok:
+        print(f"bench: GPU vs restatement parity FAILED over {cpu['rounds']} rounds: hessvecs "
+              f"{c['hessvecs']} vs {cpu['hessvecs']}, edges*iters {c['edges_iters']} vs {cpu['edges_iters']}, "
+              f"max pose diff {worst:.3e}", file=sys.stderr, flush=True)
+    return {"parity_checked_rounds": int(cpu["rounds"]), "hessvecs_gpu": int(c["hessvecs"]),
+            "hessvecs_cpu": int(cpu["hessvecs"]), "edges_iters_equal": int(c["edges_iters"]) == int(cpu["edges_iters"]),
+            "max_pose_frobenius_diff": worst, "tolerance": 1e-6, "ok": bool(ok)}
 
 
 # ---------------------------------------------------------------- LCD legs ---
@@ -363,16 +390,19 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
         same = all(r[k] == c[k] for k in ("edges_iters", "hessvecs", "block_updates", "gnc_updates"))
     xs, xr = drv.exchange_rows
     native = bool(drv.native)
+    mode = drv.exchange_mode
     mem = drv.solver.memory()[0]
     tot = _gather(dist, world, [el, float(c["edges_iters"]), float(c["hessvecs"]), float(c["block_updates"]),
                                 float(c["gnc_updates"]), hv_ms, hv_bytes, float(hv_n), float(xs), float(xr),
                                 float(mem), 1.0 if same in (None, True) else 0.0],
                   ["max", "sum", "sum", "sum", "max", "sum", "sum", "sum", "max", "max", "max", "sum"])
-    drv.solver.close()
+    if not want_snapshot:
+        drv.solver.close()
+        drv = None
     return {"el": tot[0], "edges_iters": tot[1], "hessvecs": tot[2], "block_updates": tot[3],
             "gnc_updates": int(tot[4]), "hv": (tot[5], tot[6], int(tot[7])), "xrows": (int(tot[8]), int(tot[9])),
             "mem_max": int(tot[10]), "replay_identical": (tot[11] == world) if replay and snap is not None else None,
-            "snap": snap, "native": native}
+            "snap": snap, "native": native, "exchange": mode, "drv": drv}
 
 
 def main():
@@ -439,6 +469,7 @@ def main():
         "higher_is_better": True,
         "scaling": headline,
         "vs_baseline": None,
+        "exchange": leg["exchange"],
         "dtype": "f64",
         "data": "synthetic (seeded numpy PCG64; Campus bags unavailable offline)",
         "config": {
@@ -475,11 +506,14 @@ def main():
             "peak": PEAK_HBM / 1e9,
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM,
-            # PMC bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section),
-            # measured as a ratio to the algorithmic bytes of the same dispatches
-            # (scripts/gpu_pmc_hess.sh -> profiles/hessvec_traffic.json) and applied to this run's launches
+            # NOT a counter read in this run: the PMC bytes per launch (FETCH_SIZE x2 + WRITE_SIZE,
+            # MI355X_MICROARCH.md HBM section) of a separate rocprofv3 --pmc pass, stored as a ratio to
+            # the algorithmic bytes of the same dispatches (scripts/gpu_pmc_hess.sh ->
+            # profiles/hessvec_traffic_<config>.json) and multiplied by this run's algorithmic bytes
             "traffic": (traffic["traffic_over_alg"] * hv_bytes / max(hv_n, 1)) if traffic else None,
             "traffic_over_alg": traffic["traffic_over_alg"] if traffic else None,
+            "traffic_source": (f"stored PMC ratio from profiles/hessvec_traffic_{args.config}.json "
+                               "(separate rocprofv3 --pmc pass) x this run's algorithmic bytes") if traffic else None,
             "launches": hv_n,
             "measured_over": (f"replay of the timed rounds {w0}..{w0 + args.steps} from their snapshot, HIP events "
                               "around each k_hess launch that ran a Hess-vec") if not args.profile else
@@ -509,12 +543,21 @@ def main():
             os.environ["ORC_LIB"] = lib
         cpu = cpu_baseline(g, P, leg["snap"], args.steps, args.cpu_seconds, (g.n_robots, 1))
         team, one = cpu[g.n_robots], cpu[1]
+        out["parity"] = gpu_parity(leg["drv"], leg["snap"], team)
+        leg["drv"].solver.close()
         out["cpu_baseline"] = {
             "value": team["value"], "unit": "edges*iters/s", "cores": g.n_robots, "kind": "port",
             "sample": f"rounds {w0}..{w0 + team['rounds']} of the timed window (the GPU's snapshot), "
                       f"oracle/dpgo_oracle.c -O3 -march={march}, one OpenMP thread per robot block "
                       f"({g.n_robots}), {team['seconds']:.1f} s",
             "ms_per_step": team["ms_per_step"], "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "cores_note": "one thread per robot block, the reference's execution model: dpgo runs one "
+                          "single-threaded PGOAgent per robot (one process per robot in 1014-example.yaml), so "
+                          "the reference CPU path of this 8-block team uses 8 cores whatever the host has; the "
+                          "restatement's per-block loops sum in a fixed edge order (the frozen fixtures pin it), "
+                          "and no intra-block parallel variant is built",
+            "edge_count_rule": "same as the GPU counter: a block update counts its local edges when its "
+                               "gradient norm passed gradnorm_tol (csrc/pgo.hip control_on RED_GRAD)",
             "single_thread": {"value": one["value"], "cores": 1, "rounds": one["rounds"],
                               "ms_per_step": one["ms_per_step"]},
         }

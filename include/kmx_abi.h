@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KMX_ABI_VERSION 4
+#define KMX_ABI_VERSION 5
 
 /* error codes */
 #define KMX_OK 0
@@ -155,7 +155,13 @@ int kmx_pgo_set_tcg_poll(kmx_pgo* h, int mode);
  * run the same number of rounds. kmx_pgo_set_graph drops the exchange lists. */
 #define KMX_COMM_ID_BYTES 128
 int kmx_comm_unique_id(void* out, int64_t nbytes);
-int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, int rank);
+/* The communicator is created non-blocking: a rank whose peers do not all
+ * arrive within timeout_s seconds aborts it and returns KMX_EHIP, so one
+ * failing rank cannot strand the others in the rendezvous. */
+int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, int rank, double timeout_s);
+/* Drop the communicator and the exchange lists (back to caller-driven
+ * exchanges, e.g. after a failed start-up check on another rank). */
+int kmx_pgo_comm_destroy(kmx_pgo* h);
 int kmx_pgo_set_exchange(kmx_pgo* h, const int32_t* send_slots, const int64_t* send_counts,
                          const int32_t* recv_slots, const int64_t* recv_counts);
 /* One exchange now, outside a round (e.g. before kmx_pgo_update_weights);
@@ -218,6 +224,10 @@ int kmx_pgo_exchange_unpack(kmx_pgo* h, const int32_t* dev_slots, int64_t n, con
                             int n_seg, const void* dev_in);
 int kmx_pgo_set_neighbor_poses(kmx_pgo* h, int64_t count, const int32_t* robot,
                                const int32_t* pose, const double* X);
+/* The installed public table (n_public * 4r doubles) and, when ext != NULL,
+ * the peers' status words of the last exchange (one per per-peer segment):
+ * used to check two exchange paths against each other bit for bit. */
+int kmx_pgo_get_public(kmx_pgo* h, double* table, double* ext);
 
 /* One RBCD round: `PGOAgent::iterate(doOptimization)` of every robot with
  * active[a] != 0 (drawio:2058-2066, 2513), all using the current neighbour
@@ -238,8 +248,20 @@ int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local);
  * gamma (X - Y)), and every restart_interval rounds V = X, gamma = 0. Between
  * rounds X is the accelerated iterate itself; between the exchange and
  * iterate it holds Y. set_iterate restarts the acceleration (V = X). */
-/* Wait for all work enqueued on the handle's stream. */
+/* Wait for all work enqueued on the handle's stream (and report a persistent
+ * round whose grid barrier gave up, see kmx_pgo_set_round_form). */
 int kmx_pgo_sync(kmx_pgo* h);
+/* How a round is executed (results are bit for bit the same either way):
+ *   0  launched: one kernel per phase, the host enqueues the tCG steps;
+ *   1  persistent where it applies (default, also mode -1): one launch per
+ *      round (begin, gradient, tCG steps, trial point, cost, commit between
+ *      grid barriers) when every workgroup tile of the handle can be resident
+ *      at once, one RTR iteration of the RTR method (the per-GPU shard of a
+ *      multi-GPU team). The environment variable KMX_ROUND=0/1 sets it at
+ *      creation. round_form reports the form in use, the device's resident
+ *      capacity for it and the handle's tile count. */
+int kmx_pgo_set_round_form(kmx_pgo* h, int mode);
+int kmx_pgo_round_form(kmx_pgo* h, int* persistent, int* capacity, int* tiles);
 
 /* GNC: `updateMeasurementWeights()` (drawio:2215) for every non-fixed edge with
  * a local endpoint, evaluated at the current iterate and neighbour table, then
@@ -370,7 +392,12 @@ typedef struct kmx_lcd_params {
                                  1 - cos(atan(px / f)) (LcdParams.yaml:57)     */
   int algorithm_2d2d;         /* KMX_ALGO_* 5-point minimal solver
                                  (ransac_2d2d_algorithm, LcdParams.yaml:73)     */
-  int reserved[3];
+  int refine_pose;            /* refine_pose (LcdParams.yaml:14): after an accepted
+                                 3D-3D recovery (pose_recovery_type 0), T is
+                                 re-estimated over all 3D-3D inliers by least
+                                 squares (centroids + Kabsch), the restated form
+                                 of Kimera-VIO's stereo pose refinement [U]     */
+  int reserved[2];
 } kmx_lcd_params;
 
 /* computeMatchedIndices (drawio:2583-2586): k=2 brute-force match of every

@@ -134,7 +134,7 @@ __device__ void sym_eig3(double A[9], double V[9]) {
         const double apq = A[p * 3 + q];
         if (apq == 0.0) continue;
         const double app = A[p * 3 + p], aqq = A[q * 3 + q];
-        // negligible next to both diagonal entries: zero it (Numerical Recipes' jacobi rule)
+        // negligible next to both diagonal entries: zero it (Rutishauser's threshold rule, Handbook for Automatic Computation II/1, 1971)
         const double g = 100.0 * fabs(apq);
         if (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq)) {
           A[p * 3 + q] = 0.0;
@@ -853,6 +853,7 @@ __device__ double pnp_error(const double R[9], const double t[3], const double p
 struct RsParams {
   double thr2d, thr3d, prob;
   int max_iter, min2d, min3d, pmax;
+  int refine;  // refine_pose: least-squares T over the 3D-3D inliers of an accepted recovery (refit_3d3d)
   int pnp;  // PnP or Arun recovery: k_ransac stops after 2D-2D, k_recover recovers the pose
   int prof; // diagnostic phase timers (k_ransac_coop)
   int algo; // KMX_ALGO_*: 5-point minimal solver (k_ransac_coop; k_ransac is Nister only)
@@ -860,7 +861,55 @@ struct RsParams {
 struct PnpParams {
   double thr, prob;
   int max_iter, min2d, min_pnp, pmax;
+  int refine;  // Arun recovery only (refit_3d3d)
 };
+
+// refine_pose (oracle/lcd_oracle.c refit_3d3d, the same operations in the same
+// order): least-squares T over the inlier pairs — centroids of all inliers,
+// H = sum (p_m - c_m)(p_q - c_q)^T, Kabsch R with the reflection fix,
+// t = c_q - R c_m. Serial (one lane); fetch(j, pq, pm) returns whether pair j
+// is an inlier and, if so, its two points. Two passes (centroids, then H).
+template <typename Fetch>
+__device__ void refit_3d3d(int n, Fetch&& fetch, double R[9], double t[3]) {
+  double cq[3] = {0.0, 0.0, 0.0}, cm[3] = {0.0, 0.0, 0.0};
+  int c = 0;
+  for (int j = 0; j < n; ++j) {
+    double pq[3], pm[3];
+    if (!fetch(j, pq, pm)) continue;
+    for (int k = 0; k < 3; ++k) {
+      cq[k] += pq[k];
+      cm[k] += pm[k];
+    }
+    ++c;
+  }
+  for (int k = 0; k < 3; ++k) {
+    cq[k] /= (double)c;
+    cm[k] /= (double)c;
+  }
+  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < n; ++j) {
+    double pq[3], pm[3];
+    if (!fetch(j, pq, pm)) continue;
+    double dq[3], dm[3];
+    for (int k = 0; k < 3; ++k) {
+      dq[k] = pq[k] - cq[k];
+      dm[k] = pm[k] - cm[k];
+    }
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) H[a * 3 + b] += dm[a] * dq[b];
+  }
+  double U[9], sv[3], V[9];
+  svd3(H, U, sv, V);
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  if (det3(R) < 0.0) {
+    for (int a = 0; a < 3; ++a) V[a * 3 + 2] = -V[a * 3 + 2];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  }
+  for (int a = 0; a < 3; ++a) t[a] = cq[a] - (R[a * 3 + 0] * cm[0] + R[a * 3 + 1] * cm[1] + R[a * 3 + 2] * cm[2]);
+}
 
 // Diagnostic phase timers (kmx_lcd_debug_phase_times): cycles per phase summed
 // over the first 64 candidates' hypotheses.
@@ -1432,7 +1481,7 @@ __device__ void coop_decompose(CoopWS& w, int lane, bool ok_root, const double E
 // ------------------------------------------ 5-point (Stewenius 2006) --
 // oracle/lcd_oracle.c orc_fivept_stewenius: action matrix of x on the
 // basis [x^2, xy, xz, y^2, yz, z^2, x, y, z, 1] after the graded
-// Gauss-Jordan, elmhes + hqr eigenvalues, complex eigenvectors, E from the
+// Gauss-Jordan, EISPACK elmhes + hqr eigenvalues, complex eigenvectors, E from the
 // real part of each solution (conjugate pairs once). The Hessenberg
 // reduction and the QR iteration are the oracle's serial code run by lane 0
 // on the LDS copy (data-dependent deflation); the eigenvector solves are
@@ -1457,40 +1506,42 @@ __device__ __forceinline__ cplx_d c_div(cplx_d a, cplx_d d) {
 }
 __device__ __forceinline__ double c_abs1(cplx_d a) { return fabs(a.re) + fabs(a.im); }
 
-// elmhes on w.H: the pivot search and the multipliers are formed from
-// broadcast LDS reads in the serial order; each row / column update is one
-// lane per element (the serial loop's element operations, same order of
-// the dependent steps).
+// EISPACK ELMHES (Smith et al., EISPACK Guide, 1976; netlib eispack/elmhes.f;
+// oracle/lcd_oracle.c hessenberg10) on w.H, cooperatively: the pivot search
+// and the multipliers are formed from broadcast LDS reads in the serial order;
+// each row / column update is one lane per element (the serial loop's element
+// operations, same order of the dependent steps).
 __device__ void coop_hessenberg(CoopWS& w, int lane) {
   double (*a)[10] = w.H;
-  const int n = 10;
-  for (int m = 1; m < n - 1; ++m) {
+  const int n = 10, la = n - 2;
+  for (int m = 1; m <= la; ++m) {
+    const int mm1 = m - 1;
     double x = 0.0;
-    int i = m;
+    int piv = m;
     for (int j = m; j < n; ++j) {
-      const double v = a[j][m - 1];
-      if (fabs(v) > fabs(x)) { x = v; i = j; }
+      const double v = a[j][mm1];
+      if (fabs(v) <= fabs(x)) continue;
+      x = v;
+      piv = j;
     }
     wsync();
-    if (i != m) {
-      if (lane >= m - 1 && lane < n) { const double t = a[i][lane]; a[i][lane] = a[m][lane]; a[m][lane] = t; }
+    if (piv != m) {  // interchange rows and columns piv, m
+      if (lane >= mm1 && lane < n) { const double y = a[piv][lane]; a[piv][lane] = a[m][lane]; a[m][lane] = y; }
       wsync();
-      if (lane < n) { const double t = a[lane][i]; a[lane][i] = a[lane][m]; a[lane][m] = t; }
+      if (lane < n) { const double y = a[lane][piv]; a[lane][piv] = a[lane][m]; a[lane][m] = y; }
       wsync();
     }
-    if (x != 0.0) {
-      for (i = m + 1; i < n; ++i) {
-        double y = a[i][m - 1];
-        if (y != 0.0) {  // uniform
-          y /= x;
-          wsync();
-          if (lane == 0) a[i][m - 1] = y;
-          if (lane >= m && lane < n) a[i][lane] -= y * a[m][lane];
-          wsync();
-          if (lane < n) a[lane][m] += y * a[lane][i];
-          wsync();
-        }
-      }
+    if (x == 0.0) continue;
+    for (int i = m + 1; i < n; ++i) {
+      double y = a[i][mm1];
+      if (y == 0.0) continue;  // uniform
+      y = y / x;
+      wsync();
+      if (lane == 0) a[i][mm1] = y;
+      if (lane >= m && lane < n) a[i][lane] = a[i][lane] - y * a[m][lane];
+      wsync();
+      if (lane < n) a[lane][m] = a[lane][m] + y * a[lane][i];
+      wsync();
     }
   }
   if (lane >= 2 && lane < n)
@@ -1498,161 +1549,169 @@ __device__ void coop_hessenberg(CoopWS& w, int lane) {
   wsync();
 }
 
-// hqr on w.H with every lane running the scalar control on broadcast reads;
-// the deflation search and the bulge-start search evaluate all candidates
-// at once (lane per candidate; the serial loop's pick = the highest index
-// whose test holds), the Householder row and column updates are one lane per
-// row / column. Eigenvalues to w.wr / w.wi; returns 0 after 30 iterations.
+// EISPACK HQR (netlib eispack/hqr.f; oracle/lcd_oracle.c hqr10, the same
+// loops and names) on w.H with every lane running the scalar control on
+// broadcast reads: the search for a negligible subdiagonal and the search for
+// the sweep's start row m evaluate all candidates at once (lane per candidate;
+// the serial loop's pick = the highest index whose test holds), the row and
+// column modifications of the double QR step are one lane per column / row.
+// Eigenvalues to w.wr / w.wi (a complex pair: wi(na) = +, wi(en) = -);
+// returns 0 when the 30 n sweeps (itn) run out.
 __device__ int coop_hqr(CoopWS& w, int lane) {
-  double (*a)[10] = w.H;
+  double (*h)[10] = w.H;
   const int n = 10;
-  double anorm = 0.0;
-  for (int i = 0; i < n; ++i)
-    for (int j = (i > 0 ? i - 1 : 0); j < n; ++j) anorm += fabs(a[i][j]);
-  int nn = n - 1, l;
-  double t = 0.0, p = 0.0, q = 0.0, r = 0.0, s, wv, x, y, z;
-  while (nn >= 0) {
+  double norm = 0.0;
+  for (int i = 0, k = 0; i < n; k = i, ++i)
+    for (int j = k; j < n; ++j) norm += fabs(h[i][j]);
+  int en = n - 1, itn = 30 * n;
+  double t = 0.0;
+  while (en >= 0) {
     int its = 0;
-    do {
-      bool hit = false;
-      if (lane >= 1 && lane <= nn) {
-        double ss = fabs(a[lane - 1][lane - 1]) + fabs(a[lane][lane]);
-        if (ss == 0.0) ss = anorm;
-        hit = fabs(a[lane][lane - 1]) + ss == ss;
+    const int na = en - 1, enm2 = na - 1;
+    for (;;) {
+      bool hit = false;  // single small subdiagonal element: h(l,l-1), l = en .. 1
+      if (lane >= 1 && lane <= en) {
+        double s = fabs(h[lane - 1][lane - 1]) + fabs(h[lane][lane]);
+        if (s == 0.0) s = norm;
+        const double tst1 = s, tst2 = tst1 + fabs(h[lane][lane - 1]);
+        hit = tst2 == tst1;
       }
       const unsigned long long hm = __ballot(hit);
-      l = hm ? 63 - __clzll(hm) : 0;
-      wsync();
-      if (hm && lane == 0) a[l][l - 1] = 0.0;
-      wsync();
-      x = a[nn][nn];
-      if (l == nn) {
-        if (lane == 0) { w.wr[nn] = x + t; w.wi[nn] = 0.0; }
-        --nn;
-      } else {
-        y = a[nn - 1][nn - 1];
-        wv = a[nn][nn - 1] * a[nn - 1][nn];
-        if (l == nn - 1) {
-          p = 0.5 * (y - x);
-          q = p * p + wv;
-          z = sqrt(fabs(q));
-          x += t;
-          if (lane == 0) {
-            if (q >= 0.0) {
-              z = p + (p >= 0.0 ? fabs(z) : -fabs(z));
-              w.wr[nn - 1] = w.wr[nn] = x + z;
-              if (z != 0.0) w.wr[nn] = x - wv / z;
-              w.wi[nn - 1] = w.wi[nn] = 0.0;
-            } else {
-              w.wr[nn - 1] = w.wr[nn] = x + p;
-              w.wi[nn] = z;
-              w.wi[nn - 1] = -z;
-            }
-          }
-          nn -= 2;
-        } else {
-          if (its == 30) return 0;
-          if (its == 10 || its == 20) {
-            t += x;
-            wsync();
-            if (lane <= nn) a[lane][lane] -= x;
-            wsync();
-            s = fabs(a[nn][nn - 1]) + fabs(a[nn - 1][nn - 2]);
-            y = x = 0.75 * s;
-            wv = -0.4375 * s * s;
-          }
-          ++its;
-          // bulge start: the largest m in [l, nn-2] with m == l or a small
-          // subdiagonal product (lane per m)
-          bool stop = false;
-          double pm = 0.0, qm = 0.0, rm = 0.0;
-          if (lane >= l && lane <= nn - 2) {
-            const int m = lane;
-            const double zz = a[m][m];
-            double rr = x - zz;
-            double ss = y - zz;
-            pm = (rr * ss - wv) / a[m + 1][m] + a[m][m + 1];
-            qm = a[m + 1][m + 1] - zz - rr - ss;
-            rm = a[m + 2][m + 1];
-            ss = fabs(pm) + fabs(qm) + fabs(rm);
-            pm /= ss;
-            qm /= ss;
-            rm /= ss;
-            if (m == l) {
-              stop = true;
-            } else {
-              const double u = fabs(a[m][m - 1]) * (fabs(qm) + fabs(rm));
-              const double v = fabs(pm) * (fabs(a[m - 1][m - 1]) + fabs(zz) + fabs(a[m + 1][m + 1]));
-              stop = u + v == v;
-            }
-          }
-          const unsigned long long sm = __ballot(stop);
-          const int m = 63 - __clzll(sm);  // lane l always stops
-          p = rdlane(pm, m);
-          q = rdlane(qm, m);
-          r = rdlane(rm, m);
-          wsync();
-          if (lane >= m + 2 && lane <= nn) {
-            a[lane][lane - 2] = 0.0;
-            if (lane != m + 2) a[lane][lane - 3] = 0.0;
-          }
-          wsync();
-          for (int k = m; k <= nn - 1; ++k) {
-            if (k != m) {
-              p = a[k][k - 1];
-              q = a[k + 1][k - 1];
-              r = 0.0;
-              if (k != nn - 1) r = a[k + 2][k - 1];
-              if ((x = fabs(p) + fabs(q) + fabs(r)) != 0.0) {
-                p /= x;
-                q /= x;
-                r /= x;
-              }
-            }
-            const double sq = sqrt(p * p + q * q + r * r);
-            if ((s = (p >= 0.0 ? sq : -sq)) != 0.0) {
-              wsync();
-              if (lane == 0) {
-                if (k == m) {
-                  if (l != m) a[k][k - 1] = -a[k][k - 1];
-                } else {
-                  a[k][k - 1] = -s * x;
-                }
-              }
-              p += s;
-              x = p / s;
-              y = q / s;
-              z = r / s;
-              q /= p;
-              r /= p;
-              if (lane >= k && lane <= nn) {
-                const int j = lane;
-                double pp = a[k][j] + q * a[k + 1][j];
-                if (k != nn - 1) {
-                  pp += r * a[k + 2][j];
-                  a[k + 2][j] -= pp * z;
-                }
-                a[k + 1][j] -= pp * y;
-                a[k][j] -= pp * x;
-              }
-              wsync();
-              const int mmin = nn < k + 3 ? nn : k + 3;
-              if (lane >= l && lane <= mmin) {
-                const int i = lane;
-                double pp = x * a[i][k] + y * a[i][k + 1];
-                if (k != nn - 1) {
-                  pp += z * a[i][k + 2];
-                  a[i][k + 2] -= pp * r;
-                }
-                a[i][k + 1] -= pp * q;
-                a[i][k] -= pp;
-              }
-              wsync();
-            }
+      const int l = hm ? 63 - __clzll(hm) : 0;
+      double x = h[en][en];
+      if (l == en) {  // one root
+        if (lane == 0) { w.wr[en] = x + t; w.wi[en] = 0.0; }
+        en = na;
+        break;
+      }
+      double y = h[na][na], wv = h[en][na] * h[na][en];
+      if (l == na) {  // two roots
+        const double p = (y - x) / 2.0, q = p * p + wv;
+        double zz = sqrt(fabs(q));
+        x = x + t;
+        if (lane == 0) {
+          if (q >= 0.0) {
+            zz = p + (p >= 0.0 ? fabs(zz) : -fabs(zz));
+            w.wr[na] = x + zz;
+            w.wr[en] = w.wr[na];
+            if (zz != 0.0) w.wr[en] = x - wv / zz;
+            w.wi[na] = 0.0;
+            w.wi[en] = 0.0;
+          } else {
+            w.wr[na] = x + p;
+            w.wr[en] = x + p;
+            w.wi[na] = zz;
+            w.wi[en] = -zz;
           }
         }
+        en = enm2;
+        break;
       }
-    } while (nn >= 0 && l < nn - 1);
+      if (itn == 0) return 0;
+      if (its == 10 || its == 20) {  // exceptional shift
+        t = t + x;
+        wsync();
+        if (lane <= en) h[lane][lane] = h[lane][lane] - x;
+        wsync();
+        const double s = fabs(h[en][na]) + fabs(h[na][enm2]);
+        x = 0.75 * s;
+        y = x;
+        wv = -0.4375 * s * s;
+      }
+      ++its;
+      --itn;
+      // the sweep's start: the largest m in [l, enm2] with m == l or two
+      // consecutive small subdiagonal elements (lane per m)
+      bool stop = false;
+      double pm = 0.0, qm = 0.0, rm = 0.0;
+      if (lane >= l && lane <= enm2) {
+        const int m = lane;
+        const double zz = h[m][m];
+        rm = x - zz;
+        double s = y - zz;
+        pm = (rm * s - wv) / h[m + 1][m] + h[m][m + 1];
+        qm = h[m + 1][m + 1] - zz - rm - s;
+        rm = h[m + 2][m + 1];
+        s = fabs(pm) + fabs(qm) + fabs(rm);
+        pm = pm / s;
+        qm = qm / s;
+        rm = rm / s;
+        if (m == l) {
+          stop = true;
+        } else {
+          const double tst1 = fabs(pm) * (fabs(h[m - 1][m - 1]) + fabs(zz) + fabs(h[m + 1][m + 1]));
+          const double tst2 = tst1 + fabs(h[m][m - 1]) * (fabs(qm) + fabs(rm));
+          stop = tst2 == tst1;
+        }
+      }
+      const unsigned long long sm = __ballot(stop);
+      const int m = 63 - __clzll(sm);  // lane l always stops
+      double p = rdlane(pm, m), q = rdlane(qm, m), r = rdlane(rm, m), zz;
+      wsync();
+      if (lane >= m + 2 && lane <= en) {
+        h[lane][lane - 2] = 0.0;
+        if (lane != m + 2) h[lane][lane - 3] = 0.0;
+      }
+      wsync();
+      for (int k = m; k <= na; ++k) {  // double QR step on rows l..en, columns m..en
+        const bool notlas = k != na;
+        if (k != m) {
+          p = h[k][k - 1];
+          q = h[k + 1][k - 1];
+          r = 0.0;
+          if (notlas) r = h[k + 2][k - 1];
+          x = fabs(p) + fabs(q) + fabs(r);
+          if (x == 0.0) continue;  // uniform
+          p = p / x;
+          q = q / x;
+          r = r / x;
+        }
+        const double sq = sqrt(p * p + q * q + r * r), s = p >= 0.0 ? sq : -sq;
+        wsync();
+        if (lane == 0) {
+          if (k == m) {
+            if (l != m) h[k][k - 1] = -h[k][k - 1];
+          } else {
+            h[k][k - 1] = -s * x;
+          }
+        }
+        p = p + s;
+        x = p / s;
+        y = q / s;
+        zz = r / s;
+        q = q / p;
+        r = r / p;
+        if (lane >= k && lane <= en) {  // row modification, column j = lane
+          const int j = lane;
+          if (notlas) {
+            const double pp = h[k][j] + q * h[k + 1][j] + r * h[k + 2][j];
+            h[k][j] = h[k][j] - pp * x;
+            h[k + 1][j] = h[k + 1][j] - pp * y;
+            h[k + 2][j] = h[k + 2][j] - pp * zz;
+          } else {
+            const double pp = h[k][j] + q * h[k + 1][j];
+            h[k][j] = h[k][j] - pp * x;
+            h[k + 1][j] = h[k + 1][j] - pp * y;
+          }
+        }
+        wsync();
+        const int jmax = en < k + 3 ? en : k + 3;
+        if (lane >= l && lane <= jmax) {  // column modification, row i = lane
+          const int i = lane;
+          if (notlas) {
+            const double pp = x * h[i][k] + y * h[i][k + 1] + zz * h[i][k + 2];
+            h[i][k] = h[i][k] - pp;
+            h[i][k + 1] = h[i][k + 1] - pp * q;
+            h[i][k + 2] = h[i][k + 2] - pp * r;
+          } else {
+            const double pp = x * h[i][k] + y * h[i][k + 1];
+            h[i][k] = h[i][k] - pp;
+            h[i][k + 1] = h[i][k + 1] - pp * q;
+          }
+        }
+        wsync();
+      }
+    }
   }
   wsync();
   return 1;
@@ -2006,6 +2065,22 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
       for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = s[i] / (double)cc;
       r.stereo_inliers = cc;
       r.accepted = (cc >= P.min3d) ? 1 : 0;
+      if (r.accepted && P.refine) {  // the inliers again: valid and within thr3d of the best translation
+        refit_3d3d(
+            n3,
+            [&](int j, double* pq, double* pm) {
+              if (!valid[j]) return false;
+              const double dx = T[3 * j] - T[3 * best], dy = T[3 * j + 1] - T[3 * best + 1],
+                           dz = T[3 * j + 2] - T[3 * best + 2];
+              if (!(dx * dx + dy * dy + dz * dz < thr2)) return false;
+              const int2 pr = pl[idx[j]];
+              const double* a = points + ((size_t)q * N + pr.x) * 3;
+              const double* b = points + ((size_t)m * N + pr.y) * 3;
+              for (int k = 0; k < 3; ++k) { pq[k] = a[k]; pm[k] = b[k]; }
+              return true;
+            },
+            r.T_query_match, r.T_query_match + 9);
+      }
     } else {
       for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = 0.0;
     }
@@ -2206,6 +2281,22 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac(const double* bearings,
       for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = s[i] / (double)cc;
       r.stereo_inliers = cc;
       r.accepted = (cc >= P.min3d) ? 1 : 0;
+      if (r.accepted && P.refine) {  // the inliers again: valid and within thr3d of the best translation
+        refit_3d3d(
+            n3,
+            [&](int j, double* pq, double* pm) {
+              if (!valid[j]) return false;
+              const double dx = T[3 * j] - T[3 * best], dy = T[3 * j + 1] - T[3 * best + 1],
+                           dz = T[3 * j + 2] - T[3 * best + 2];
+              if (!(dx * dx + dy * dy + dz * dz < thr2)) return false;
+              const int2 pr = pl[idx[j]];
+              const double* a = points + ((size_t)q * N + pr.x) * 3;
+              const double* b = points + ((size_t)m * N + pr.y) * 3;
+              for (int k = 0; k < 3; ++k) { pq[k] = a[k]; pm[k] = b[k]; }
+              return true;
+            },
+            r.T_query_match, r.T_query_match + 9);
+      }
     } else {
       for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = 0.0;
     }
@@ -2400,6 +2491,15 @@ __global__ __launch_bounds__(RS_BLOCK) void k_recover(const double* bearings, co
         for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = to[i];
       }
       r.accepted = (have_model && np >= P.min_pnp) ? 1 : 0;
+      if (r.accepted && P.refine)
+        refit_3d3d(
+            n2,
+            [&](int j, double* pq, double* pm) {
+              if (!(err(Ro, to, j) < P.thr)) return false;
+              for (int k = 0; k < 3; ++k) { pq[k] = Aq[3 * j + k]; pm[k] = Bm[3 * j + k]; }
+              return true;
+            },
+            r.T_query_match, r.T_query_match + 9);
     }
     *R_ = r;
   }
@@ -2525,6 +2625,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   rp.pnp = (h->P.pose_recovery_type == 1 || !h->P.use_1point_3d3d) ? 1 : 0;  // k_recover takes over
   rp.prof = h->prof;
   rp.algo = h->P.algorithm_2d2d;
+  rp.refine = h->P.refine_pose && h->P.pose_recovery_type == 0 ? 1 : 0;
   {
     // KMX_RS_LB: minimum waves per SIMD for k_ransac (diagnostic; 1 = the
     // compiler's choice, 256 VGPRs)
@@ -2559,6 +2660,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
     pp.max_iter = h->P.ransac_max_iterations;
     pp.min2d = h->P.min_2d2d_inliers;
     pp.min_pnp = pnp ? h->P.min_2d3d_inliers : h->P.min_3d3d_inliers;
+    pp.refine = !pnp && h->P.refine_pose ? 1 : 0;
     pp.pmax = h->pmax;
     const size_t smem = sizeof(double) * (6 * (size_t)h->N + 64 * 12 + 12) + sizeof(int) * (64 + 64 + 4 + (size_t)h->N);
     hipLaunchKernelGGL(pnp ? k_recover<true> : k_recover<false>, dim3(n), dim3(RS_BLOCK), smem, h->stream,

@@ -86,6 +86,19 @@ struct Gnc {
   double pad[3];
 };
 
+// Field-wise copies of the schedule state (a struct assignment between global
+// pointers is lowered through a scratch temporary, which would give the
+// persistent round a scratch allocation).
+__device__ __forceinline__ Gnc load_gnc(const Gnc* p) {
+  Gnc s;
+  s.inner = p->inner; s.updates = p->updates; s.fired = p->fired; s.rounds = p->rounds;
+  s.mu = p->mu; s.pad[0] = s.pad[1] = s.pad[2] = 0.0;
+  return s;
+}
+__device__ __forceinline__ void store_gnc(Gnc* p, const Gnc& s) {
+  p->inner = s.inner; p->updates = s.updates; p->fired = s.fired; p->rounds = s.rounds; p->mu = s.mu;
+}
+
 // Host-visible tCG progress of one robot, written after every tCG step by the
 // last-arriving tile of the robot's k_update (or its first tile when it is
 // not in tCG) into host-mapped memory as ONE 64-bit word (seq << 1 |
@@ -98,12 +111,6 @@ struct HostStatus {
 __device__ __forceinline__ void post_status(HostStatus* hs, int l, unsigned long long seq, bool running) {
   __hip_atomic_store(&hs[l].word, (seq << 1) | (running ? 1ull : 0ull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// Per-launch instrumentation passed to the tCG kernels.
-struct Post {
-  HostStatus* hs = nullptr;     // k_update: progress words (nullptr: no polling)
-  unsigned long long seq = 0;
-  int slot = -1;                // k_hess with timing on: event-pair index
-};
 
 struct Params {
   int tcg_max, rtr_iters, use_precond, robust;
@@ -133,7 +140,6 @@ struct Dev {
   Ctl* ctl;
   Ctl* ctl2;           // [L] RM_CONSUMER: the state between k_hess and k_update of a tCG step
   Counters* cnt;
-  unsigned* tickets;          // [L] per-robot arrival counters (zero between launches)
   const long long* m_robot;   // [L] local-problem edges per robot
   const int* n_robot;         // [L] poses per robot
   const int* pose_slot;       // [nloc] owned public-table slot of a pose, or -1
@@ -145,12 +151,24 @@ struct Dev {
   const int2* gnc_ends;       // [n_gnc] endpoints: >= 0 local pose, < 0 public slot -1-x
   int n_gnc;
   int* hv_launch;             // [HV_SLOTS] robots that ran a Hess-vec in timed launch k
-  const int* rgroup0;         // [L+1] first ticket group of each robot (GS tiles per group)
-  unsigned* gtickets;         // [groups] group arrival counters (zero between launches)
-  double* gpart;              // [groups][NPART] group partial sums
+  struct GridBar* bar;        // persistent round: grid-barrier words (k_round)
   Params p;
 };
-constexpr int GS = 16;  // tiles per ticket group
+
+// Grid barrier of the persistent round kernel (k_round): XCD-grouped arrival
+// counters (group = blockIdx % 8: the blocks the dispatcher deals to one XCD;
+// speed only, never correctness), a top counter and a generation word, each
+// on a 256-B line of its own. Every word is monotonic across launches (no
+// reset per launch: the launch reads the generation at its start), `alive`
+// counts the robots still in tCG, `err` is the bounded spins' give-up word.
+struct GridBar {
+  unsigned cnt[8][64];
+  unsigned top[64];
+  unsigned gen[64];
+  unsigned alive[64];
+  unsigned err[64];
+  unsigned census[64];
+};
 constexpr int HV_SLOTS = 1 << 16;
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -710,53 +728,35 @@ __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, co
   return cost;
 }
 
-// -------------------------------------------- fused per-robot reductions --
-// Each tile of robot l reduces its NV values over the workgroup, stores them
-// write-through (sc1) and takes a ticket on robot l's counter; the tile that
-// draws the last ticket reduces robot l's partials in tile order
-// (deterministic, the same thread-strided + wave + workgroup order everywhere)
-// and runs the RTR / tCG scalar logic. Hand-off form: MI355X_MICROARCH.md
-// "Valid forms", table row 1 (sc1 stores, one agent-scope add per workgroup
-// after its vmcnt wait, the last adder told by the returned value, sc1 loads).
-__device__ void control(const Dev& d, int l, int kind, const double* tot, int R_);
-
-// Reduction modes. RM_LAUNCH (default): the tile stores its partials and
-// k_reduce, a one-workgroup-per-robot launch, reduces them and runs the
-// control logic. RM_TICKET (KMX_RED=1): the reduction runs in the producing
-// launch behind two-level agent-scope tickets (below). Measured on configs[3]
-// (steady-state window, profiles/r02): k_hess 47.5 us with tickets vs 39.9 us
-// plus a 4.7 us k_reduce without, k_update +11 us — each workgroup's ticket
-// (write-through partial stores, vmcnt drain, a returning device-scope
-// atomic) keeps its wave and LDS allocated for microseconds after its work,
-// which delays the next generation of workgroups (k_hess runs ~2 per CU slot).
-// RM_CONSUMER (KMX_RED=2): no reduction launch inside tCG — every workgroup of
-// k_update reduces its robot's k_hess partials itself (and every workgroup of
-// the next k_hess the k_update partials) in k_reduce's exact order and runs the
-// control step on a private copy of the robot's state; the robot's first tile
-// writes the state out, double-buffered (k_hess: ctl -> ctl2, k_update: ctl2 ->
-// ctl), so no workgroup reads a state another one of the same launch writes.
-// Two launches per tCG step instead of four, same results as RM_LAUNCH; the
-// round's other reductions are folded too (gradient -> first k_hess, last
-// update -> k_retract, trial cost -> k_commit), so a round has no k_reduce
-// launch: 12.5k poses 167.7 -> 161.4 us per round, with the host no longer
-// waiting on a reduction launch between the tCG loop and the retraction
-// (profiles/r02/small_round/3_*).
-// Measured on configs[3] (profiles/r02/ab_red): k_hess 41.2 us and k_update
-// 22.7 us against 32.4 + 19.8 us plus two 4.6 us k_reduce launches — the
-// per-workgroup reduction and decision add latency to every workgroup of the
-// latency-bound gather, which outweighs the saved launches (0.87-0.88 vs
-// 0.86 ms per round), so RM_LAUNCH stays the default.
-// RM_HALF (KMX_RED=3): k_update consumes the k_hess partials itself and only
-// the update's reduction keeps its k_reduce launch (so no decision adds
-// latency to the gather kernel): k_hess reads ctl, k_update writes ctl2,
-// k_reduce moves ctl2 -> ctl. Measured at configs[3] (profiles/r02/ab_half):
-// 0.814 / 0.839 vs 0.817 / 0.839 ms per round — the saved launch is what
-// k_update's added latency costs; not the default.
-enum RedMode { RM_LAUNCH = 0, RM_TICKET = 1, RM_CONSUMER = 2, RM_HALF = 3 };
+// -------------------------------------------------- per-robot reductions --
+// Each tile reduces its NV values over the workgroup (wave sums, then the 4
+// waves in order) and stores them as the tile's partials; the robot's sums are
+// taken in tile order by whoever consumes them (robot_sum's fixed order):
+// RM_LAUNCH: k_reduce, a one-workgroup-per-robot launch after the producing
+// kernel, which then runs the RTR / tCG control logic; RM_CONSUMER: no
+// reduction launch inside tCG — every workgroup of k_update reduces its robot's
+// k_hess partials itself (and every workgroup of the next k_hess the k_update
+// partials) in the same order and runs the control step on a private copy of
+// the robot's state; the robot's first tile writes the state out,
+// double-buffered (k_hess: ctl -> ctl2, k_update: ctl2 -> ctl), so no
+// workgroup reads a state another one of the same launch writes. The round's
+// other reductions are folded too (gradient -> first k_hess, last update ->
+// k_retract, trial cost -> k_commit), so a consumer-form round has no k_reduce
+// launch (12.5k poses 167.7 -> 161.4 us per round, profiles/r02/small_round/3_*).
+// Measured on configs[3] (profiles/r02/ab_red): at 100k poses the consumer
+// form loses (k_hess 41.2 us and k_update 22.7 us against 32.4 + 19.8 us plus
+// two 4.6 us k_reduce launches: each workgroup of the latency-bound gather
+// waits for its robot's sums), so RM_LAUNCH stays the form above 80k poses per
+// GPU. Two more forms were measured and removed in round 3: agent-scope
+// tickets in the producing launch (k_hess 47.5 vs 39.9 us: the ticket keeps
+// each workgroup resident for microseconds after its work) and a half form
+// with only the update's k_reduce kept (0.814 / 0.839 vs 0.817 / 0.839 ms per
+// round: no gain).
+enum RedMode { RM_LAUNCH = 0, RM_CONSUMER = 2 };
 
 template <int KIND, int NV, int RM, typename Store>
 __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const double* vals, char* smem_red,
-                                            int R_, Store&& store, const Post& po = Post{}) {
+                                            Store&& store) {
   double* lds = reinterpret_cast<double*>(smem_red);
   static_assert(NV <= NPART && WAVES == 4, "reduction area");
 #pragma unroll
@@ -765,126 +765,19 @@ __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const d
     if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
   }
   __syncthreads();
-  if constexpr (RM == RM_LAUNCH || (RM == RM_CONSUMER && KIND != RED_HESS && KIND != RED_UPDATE) ||
-                (RM == RM_HALF && KIND != RED_HESS)) {
-    if (threadIdx.x == 0) {
-#pragma unroll
-      for (int s = 0; s < NV; ++s) {
-        double t = 0.0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
-        d.part[(size_t)L.tile * NPART + s] = t;
-      }
-    }
-    store();
-    return;
-  } else if constexpr (RM == RM_CONSUMER || RM == RM_HALF) {  // 2-wide partials for the consumer launch
-    static_assert(NV <= 2, "consumer partials");
-    if (threadIdx.x == 0) {
-      double* dst = (KIND == RED_HESS ? d.part_h : d.part_u) + (size_t)L.tile * 2;
-#pragma unroll
-      for (int s = 0; s < NV; ++s) {
-        double t = 0.0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
-        dst[s] = t;
-      }
-    }
-    store();
-    return;
-  }
-  // Waves 1..3 store their rows and leave; wave 0 publishes the tile's partials
-  // (lane 0: sc1 stores, vmcnt wait, one agent-scope ticket), so the ticket's
-  // round trip holds one wave, not the workgroup, and no row store is queued
-  // ahead of the partials.
-  if (L.w != 0) {
-    store();
-    return;
-  }
-  // Two-level ticket: tiles arrive on their group's counter (GS consecutive
-  // tiles of the robot); the last tile of a group sums the group's partials and
-  // arrives on the robot's counter; the last group sums the group partials and
-  // runs the control logic. Sums run in tile order within a group and in group
-  // order across groups (deterministic); no counter sees more than GS + the
-  // robot's group count arrivals, where one counter per robot serialised ~260.
-  const int t0 = d.rtile0[L.l], t1 = d.rtile0[L.l + 1];
-  const int gl = (L.tile - t0) / GS, g = d.rgroup0[L.l] + gl;
-  const int gsz = min(GS, t1 - t0 - gl * GS);
-  unsigned ticket = 0;
-  if (L.ln == 0) {
+  constexpr bool two = RM == RM_CONSUMER && (KIND == RED_HESS || KIND == RED_UPDATE);
+  static_assert(!two || NV <= 2, "consumer partials");
+  if (threadIdx.x == 0) {  // 2-wide partials for the consumer launch, else NPART-wide for k_reduce
+    double* dst = two ? (KIND == RED_HESS ? d.part_h : d.part_u) + (size_t)L.tile * 2 : d.part + (size_t)L.tile * NPART;
 #pragma unroll
     for (int s = 0; s < NV; ++s) {
       double t = 0.0;
 #pragma unroll
       for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
-      __hip_atomic_store(d.part + (size_t)L.tile * NPART + s, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dst[s] = t;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ticket = __hip_atomic_fetch_add(d.gtickets + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  ticket = __shfl(ticket, 0, 64);
   store();
-  if (ticket != (unsigned)(gsz - 1)) return;
-  constexpr int NS = (KIND == RED_COST) ? 4 : NV;  // k_cost also sums k_retract's slots 2, 3
-  static_assert(NPART == 4 && GS <= 64, "group layout");
-  // consumer form "ticket -> acquire -> s_waitcnt -> plain loads"
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  double gs[NPART] = {0.0, 0.0, 0.0, 0.0};
-  {
-    double2 a = make_double2(0.0, 0.0), b = make_double2(0.0, 0.0);
-    if (L.ln < gsz) {
-      const double2* p2 = reinterpret_cast<const double2*>(d.part + (size_t)(t0 + gl * GS + L.ln) * NPART);
-      a = p2[0];
-      b = p2[1];
-    }
-    for (int k = 0; k < gsz; ++k) {
-      gs[0] += __shfl(a.x, k, 64); gs[1] += __shfl(a.y, k, 64);
-      gs[2] += __shfl(b.x, k, 64); gs[3] += __shfl(b.y, k, 64);
-    }
-  }
-  unsigned top = 0;
-  if (L.ln == 0) {
-    double2* gp = reinterpret_cast<double2*>(d.gpart + (size_t)g * NPART);
-    __hip_atomic_store(&gp->x, gs[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&gp->y, gs[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&gp[1].x, gs[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&gp[1].y, gs[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(d.gtickets + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    top = __hip_atomic_fetch_add(d.tickets + L.l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  top = __shfl(top, 0, 64);
-  const int g0 = d.rgroup0[L.l], ng = d.rgroup0[L.l + 1] - g0;
-  if (top != (unsigned)(ng - 1)) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
-  for (int c = 0; c < ng; c += 64) {
-    const int n = min(64, ng - c);
-    double2 a = make_double2(0.0, 0.0), b = make_double2(0.0, 0.0);
-    if (L.ln < n) {
-      const double2* p2 = reinterpret_cast<const double2*>(d.gpart + (size_t)(g0 + c + L.ln) * NPART);
-      a = p2[0];
-      b = p2[1];
-    }
-    for (int k = 0; k < n; ++k) {
-      tot[0] += __shfl(a.x, k, 64); tot[1] += __shfl(a.y, k, 64);
-      tot[2] += __shfl(b.x, k, 64); tot[3] += __shfl(b.y, k, 64);
-    }
-  }
-#pragma unroll
-  for (int s = NS; s < NPART; ++s) tot[s] = 0.0;
-  if (L.ln == 0) {
-    control(d, L.l, KIND, tot, R_);
-    if constexpr (KIND == RED_HESS) {
-      if (po.slot >= 0) atomicAdd(d.hv_launch + po.slot, 1);
-    }
-    if constexpr (KIND == RED_UPDATE) {
-      if (po.hs) post_status(po.hs, L.l, po.seq, d.ctl[L.l].phase == PH_TCG);
-    }
-    __hip_atomic_store(d.tickets + L.l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 // The tCG decisions after the Hess-vec and after the update, shared by
@@ -940,7 +833,8 @@ __device__ __forceinline__ UpdStep upd_step(int mode, double norm_r0, double z_r
 // The RTR / tCG scalar logic of robot l after a reduction of `kind`, applied
 // to c. `side`: perform the side effects (team status, counters) — exactly one
 // caller per robot and reduction does.
-__device__ void control_on(Ctl& c, const Dev& d, int l, int kind, const double* tot, int R_, bool side) {
+__device__ __forceinline__ void control_core(Ctl& c, const Dev& d, int l, int kind, const double* tot, int R_,
+                                             bool side) {
   const Params& P = d.p;
   if (kind == RED_GRAD) {
     const double f = tot[0], gn = sqrt(tot[1]);
@@ -1045,9 +939,19 @@ __device__ void control_on(Ctl& c, const Dev& d, int l, int kind, const double* 
     if (side && c.phase == PH_IDLE) d.relc[l] = c.rel_change;  // the team status of dpgo's getStatus
   }
 }
-__device__ void control(const Dev& d, int l, int kind, const double* tot, int R_) {
-  control_on(d.ctl[l], d, l, kind, tot, R_, true);
+// Out of line in the launched kernels (inlined, it costs the 128-VGPR gather
+// kernels spills); inlined in the persistent round (INL), whose Dev is a local
+// copy that must not have its address taken.
+__device__ void control_on(Ctl& c, const Dev& d, int l, int kind, const double* tot, int R_, bool side) {
+  control_core(c, d, l, kind, tot, R_, side);
 }
+template <bool INL>
+__device__ __forceinline__ void control_sel(Ctl& c, const Dev& d, int l, int kind, const double* tot, int R_,
+                                            bool side) {
+  if constexpr (INL) control_core(c, d, l, kind, tot, R_, side);
+  else control_on(c, d, l, kind, tot, R_, side);
+}
+
 
 // RM_LAUNCH: one workgroup per robot reduces the robot's tile partials in
 // tile order and runs the control logic (after k_update it also reports the
@@ -1172,16 +1076,15 @@ struct RobotSum {
 // together at the start, the control logic runs on the LDS copy and 32 lanes
 // write it back: no global round trip is serialised behind another.
 __global__ __launch_bounds__(RBLOCK) void k_reduce(Dev d, int kind, int R_, HostStatus* hs, unsigned long long seq,
-                                                  int slot, const double* src, const Ctl* from) {
+                                                  int slot, const double* src) {
   constexpr int RW_ = RBLOCK / 64;
   constexpr int CW = sizeof(Ctl) / 8;
   static_assert(CW <= RBLOCK, "Ctl copy");
   __shared__ double lds[NPART * RW_];
   __shared__ Ctl cs;
   const int l = blockIdx.x;
-  const Ctl* cin = from ? from : d.ctl;  // RM_HALF: the state k_update left in ctl2
   if (threadIdx.x < CW)
-    reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(cin + l)[threadIdx.x];
+    reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(d.ctl + l)[threadIdx.x];
   const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
   double tot[NPART];
   if (src) {  // RM_CONSUMER's 2-wide partials
@@ -1208,7 +1111,7 @@ __global__ __launch_bounds__(RBLOCK) void k_reduce(Dev d, int kind, int R_, Host
     }
     if (hs) post_status(hs, l, seq, act && cs.phase == PH_TCG);
   }
-  if (!act && !from) return;
+  if (!act) return;
   __syncthreads();
   if (threadIdx.x < CW)
     reinterpret_cast<double*>(d.ctl + l)[threadIdx.x] = reinterpret_cast<const double*>(&cs)[threadIdx.x];
@@ -1305,11 +1208,10 @@ __device__ __forceinline__ void pose_precond(const Dev& d, int pose) {
 // idle robots are rebuilt too. The writes are read back by the tile's own
 // lanes after the workgroup barrier (one CU: workgroup-scope visibility).
 template <int R, int RW, int RM>
-__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d, int gated) {
-  KMX_SMEM;
+__device__ __forceinline__ void body_grad(const Dev& d, int gated, char* smem) {
   const Lane L = lane_map<R>(d);
   if (gated) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *d.gnc = *d.gnc_next;
+    if (blockIdx.x == 0 && threadIdx.x == 0) store_gnc(d.gnc, load_gnc(d.gnc_next));
     if (d.gnc_next->fired) {
       const int np = d.tile_np[L.tile], p0 = d.tile_p0[L.tile];
       for (int t = threadIdx.x; t < np; t += blockDim.x) pose_precond<RW>(d, p0 + t);
@@ -1332,7 +1234,7 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d, int gated) {
     vals[1] = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2] + gr[3] * gr[3];
     vals[2] = zr[0] * gr[0] + zr[1] * gr[1] + zr[2] * gr[2] + zr[3] * gr[3];
   }
-  finish_tile<RED_GRAD, 3, RM>(d, L, vals, smem + SmemHG<R>::red_off, R, [&]() {
+  finish_tile<RED_GRAD, 3, RM>(d, L, vals, smem + SmemHG<R>::red_off, [&]() {
     if (!L.valid) return;
     const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
     store4(d.g + o, gr);  // r = g at the start of tCG: k_update's first step reads g
@@ -1347,9 +1249,11 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d, int gated) {
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old;
 // partial <delta, Hdelta>.
-template <int R, int RW, int RM>
-__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostStatus* hs, unsigned long long seq) {
-  KMX_SMEM;
+// alive (persistent round only): the robot's first tile counts the robots whose
+// tCG continues with this step (the round kernel's exit test).
+template <int R, int RW, int RM, bool INL = false>
+__device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs, unsigned long long seq, char* smem,
+                                          unsigned* alive = nullptr) {
   const Lane L = lane_map<R>(d);
   int tcg_iter;
   double beta, pcoef;  // pcoef: the previous step's eta coefficient (alpha or tau)
@@ -1401,9 +1305,10 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
       if (upd) u = upd_step(c0.mode, c0.norm_r0, c0.z_r, c0.tcg_iter, tot[0], tot[1], d.p);
       if (grad) u.done = sqrt(tot[1]) < d.p.gn_tol ? 1 : 0;  // control_on's RED_GRAD test
       if (writer && threadIdx.x == 0) {
-        if (upd || grad) control_on(cs, d, L.l, grad ? RED_GRAD : RED_UPDATE, tot, R, true);
+        if (upd || grad) control_sel<INL>(cs, d, L.l, grad ? RED_GRAD : RED_UPDATE, tot, R, true);
         d.ctl2[L.l] = cs;
         if (hs) post_status(hs, L.l, seq, cs.phase == PH_TCG);
+        if (alive && !u.done) __hip_atomic_fetch_add(alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return !u.done;
     };
@@ -1460,23 +1365,21 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostS
     }
     v = dl[0] * hdl[0] + dl[1] * hdl[1] + dl[2] * hdl[2] + dl[3] * hdl[3];
   }
-  Post po;
-  po.slot = slot;
-  finish_tile<RED_HESS, 1, RM>(d, L, &v, smem + SmemH<R>::red_off, R, [&]() {
+  finish_tile<RED_HESS, 1, RM>(d, L, &v, smem + SmemH<R>::red_off, [&]() {
     if (L.valid) {
       store4(d.del + o, dl);
       store4(d.hd + o, hdl);
       if (!first) store4(d.eta + o, et);
     }
-  }, po);
+  });
 }
 
 // tCG step, part 2: r += coef Hdelta (eta += coef delta is deferred to the next
 // k_hess, which reads delta anyway, or to k_retract); interior steps also
 // z = precon(r) and partials <r,r>, <z,r>.
-template <int R, int RM>
-__global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq, int slot) {
-  KMX_SMEM;
+template <int R, int RM, bool INL = false>
+__device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsigned long long seq, int slot,
+                                            char* smem) {
   const Lane L = lane_map<R>(d);
   int tcg_iter, mode;
   double coef;
@@ -1484,15 +1387,14 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
   double rr[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
   double Pm[16];
   bool pre = false;
-  if constexpr (RM == RM_CONSUMER || RM == RM_HALF) {
+  if constexpr (RM == RM_CONSUMER) {
     // this step's k_hess partials: the control step after the Hess-vec (alpha
     // or the boundary tau) on a private copy, with the step's vector loads in
-    // flight; the first tile writes the robot's state (RM_CONSUMER: ctl2 ->
-    // ctl; RM_HALF: ctl -> ctl2, which k_reduce moves back)
+    // flight; the first tile writes the robot's state (ctl2 -> ctl)
     __shared__ Ctl cs;
     __shared__ double rl[NPART * WAVES];
-    Ctl* const cin = (RM == RM_HALF) ? d.ctl : d.ctl2;
-    Ctl* const cout = (RM == RM_HALF) ? d.ctl2 : d.ctl;
+    Ctl* const cin = d.ctl2;
+    Ctl* const cout = d.ctl;
     const Ctl& cq = cin[L.l];
     const bool writer = L.tile == d.rtile0[L.l];
     if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))  // as in k_hess
@@ -1516,7 +1418,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
     rs.finish(d.part_h, 2, rl, tot);
     const HessStep hsx = hess_step(cq.z_r, cq.e_Pe, cq.e_Pd, cq.d_Pd, cq.Delta, tot[0]);
     if (writer && threadIdx.x == 0) {  // the state update, on an LDS copy
-      control_on(cs, d, L.l, RED_HESS, tot, R, true);
+      control_sel<INL>(cs, d, L.l, RED_HESS, tot, R, true);
       cout[L.l] = cs;
       if (slot >= 0) atomicAdd(d.hv_launch + slot, 1);
     }
@@ -1554,15 +1456,12 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
       vals[1] = zr[0] * rr[0] + zr[1] * rr[1] + zr[2] * rr[2] + zr[3] * rr[3];
     }
   }
-  Post po;
-  po.hs = hs;
-  po.seq = seq;
-  finish_tile<RED_UPDATE, 2, RM>(d, L, vals, smem + SmemU::red_off, R, [&]() {
+  finish_tile<RED_UPDATE, 2, RM>(d, L, vals, smem + SmemU::red_off, [&]() {
     if (L.valid) {
       store4(d.r + o, rr);
       if (interior) store4(d.z + o, zr);
     }
-  }, po);
+  });
 }
 
 // Trial point Xt = R_X(eta); partials: model m(eta) = 1/2 <eta, g + r> (r = g +
@@ -1574,8 +1473,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
 // that reads the new phase goes straight to the retraction, as the decision
 // says, so every tile acts alike.
 template <int R>
-__global__ __launch_bounds__(BLOCK) void k_retract(Dev d, int fold) {
-  KMX_SMEM;
+__device__ __forceinline__ void body_retract(const Dev& d, int fold, char* smem) {
   const Lane L = lane_map<R>(d);
   Ctl& c = d.ctl[L.l];
   __shared__ int sph;
@@ -1643,12 +1541,11 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d, int fold) {
 }
 
 template <int R, int RW, int RM>
-__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d) {
-  KMX_SMEM;
+__device__ __forceinline__ void body_cost(const Dev& d, char* smem) {
   const Lane L = lane_map<R>(d);
   if (d.ctl[L.l].phase != PH_STEP) return;
   double cost = inc_owner_cost<R, RW>(d, L, d.Xt, d.pub, smem);
-  finish_tile<RED_COST, 1, RM>(d, L, &cost, smem + SmemC<R>::red_off, R, []() {});
+  finish_tile<RED_COST, 1, RM>(d, L, &cost, smem + SmemC<R>::red_off, []() {});
 }
 
 // End of a round: X <- Xt where the step was accepted, and the owned public
@@ -1665,8 +1562,8 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d) {
 // trial point becomes the iterate the next iteration starts from, but the
 // public rows (the neighbours' snapshot of this round) and the round counters
 // wait for the block update's end.
-template <int R>
-__global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
+template <int R, bool INL = false>
+__device__ __forceinline__ void body_commit(const Dev& d, int fold, int final) {
   const Lane L = lane_map<R>(d);
   if (final && L.tile == 0 && threadIdx.x == 0) {
     d.gnc->inner += 1;
@@ -1696,7 +1593,7 @@ __global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
       commit = rho > d.p.accept_rho;
     }
     if (threadIdx.x == 0 && writer) {
-      control_on(cs, d, L.l, RED_COST, tot, R, true);
+      control_sel<INL>(cs, d, L.l, RED_COST, tot, R, true);
       cs.phase = PH_STEP;
       d.ctl[L.l] = cs;
     }
@@ -1711,6 +1608,38 @@ __global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
   if (!final) return;
   const int s = d.pose_slot[L.pose];
   if (s >= 0) store4(d.pub + (size_t)s * 4 * R + 4 * L.a, v);
+}
+
+// The launched form: one kernel per phase of the round (the persistent round
+// kernel k_round below runs the same bodies between grid barriers).
+template <int R, int RW, int RM>
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d, int gated) {
+  KMX_SMEM;
+  body_grad<R, RW, RM>(d, gated, smem);
+}
+template <int R, int RW, int RM>
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostStatus* hs, unsigned long long seq) {
+  KMX_SMEM;
+  body_hess<R, RW, RM>(d, slot, hs, seq, smem);
+}
+template <int R, int RM>
+__global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq, int slot) {
+  KMX_SMEM;
+  body_update<R, RM>(d, hs, seq, slot, smem);
+}
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_retract(Dev d, int fold) {
+  KMX_SMEM;
+  body_retract<R>(d, fold, smem);
+}
+template <int R, int RW, int RM>
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d) {
+  KMX_SMEM;
+  body_cost<R, RW, RM>(d, smem);
+}
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
+  body_commit<R>(d, fold, final);
 }
 
 // ------------------------------------------------- round begin + GNC-TLS ---
@@ -1800,15 +1729,15 @@ __global__ void k_begin(Dev d, const unsigned char* active, int mode, int R_) {
     if (mode & BEGIN_ROUND)
       for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
     if (threadIdx.x == 0) {
-      Gnc s = *d.gnc;
+      Gnc s = load_gnc(d.gnc);
       s.fired = fire ? 1 : 0;
       if (fire) {
         s.inner = 0;
         s.updates += 1;
         s.mu = mu * d.p.mu_step;
       }
-      *d.gnc_next = s;
-      if (mode & BEGIN_SOLO) *d.gnc = s;  // one-block launch: no reader of the state is left
+      store_gnc(d.gnc_next, s);
+      if (mode & BEGIN_SOLO) store_gnc(d.gnc, s);  // one-block launch: no reader of the state is left
       if (fire) atomicAdd(&d.cnt->gnc_updates, 1ull);
     }
     return;
@@ -1818,6 +1747,171 @@ __global__ void k_begin(Dev d, const unsigned char* active, int mode, int R_) {
     gnc_edge<RW>(d, i, R_, mu);
 }
 
+// ------------------------------------------------------ persistent round ---
+// One launch per RBCD round for problems whose tiles fit the GPU at once (the
+// per-GPU shard of a multi-GPU team): the launched form's phase bodies in the
+// same order — begin (+ GNC), gradient, tCG steps (Hess-vec, update), trial
+// point, trial cost, commit — separated by grid barriers instead of kernel
+// boundaries, with one workgroup per tile exactly as the launched form, so
+// every sum is taken in the same order and the results are bit for bit the
+// launched form's (RM_CONSUMER, one RTR iteration; tests/test_round_kernel_gpu.py).
+// The host no longer enqueues or polls tCG steps: after each Hess-vec phase the
+// robots whose tCG continues are counted, and the loop ends once a Hess-vec
+// phase counted none (the launched form's polled exit).
+
+// Hand-off (MI355X_MICROARCH.md "Valid forms", producer / consumer bullets):
+// every wave drains its stores, a workgroup barrier, lane 0 releases at agent
+// scope and arrives; the last arriver of a group releases again and arrives on
+// the top counter, whose last arriver stores the generation; lane 0 polls the
+// generation relaxed (bounded: ~2 s, then the give-up word and a false
+// return), acquires at agent scope, drains, and the workgroup barrier opens.
+constexpr unsigned long long BAR_TIMEOUT_TICKS = 200000000ull;  // 2 s of the 100 MHz wall clock
+__device__ __forceinline__ bool grid_sync(GridBar* b, unsigned target) {
+  __shared__ int ok;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nb = gridDim.x, g = blockIdx.x & 7u;
+    const unsigned G = nb < 8u ? nb : 8u;
+    const unsigned ng = (nb - g + 7u) / 8u;  // blocks in this group
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // every counter starts at 0 with the graph and every launch of the handle
+    // has the same grid, so barrier number `target` (the generation it opens)
+    // is complete at exactly ng * target group / G * target top arrivals
+    // (mod 2^32 on both sides)
+    const unsigned old = __hip_atomic_fetch_add(&b->cnt[g][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1u == ng * target) {  // the group's last arrival
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(&b->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1u == G * target) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&b->gen[0], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    int good = 1;
+    const unsigned long long t0 = wall_clock64();
+    while ((int)(__hip_atomic_load(&b->gen[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > BAR_TIMEOUT_TICKS) {
+        __hip_atomic_store(&b->err[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        good = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ok = good;
+  }
+  __syncthreads();
+  return ok != 0;
+}
+
+// The round-begin phase (k_begin with BEGIN_ROUND) spread over the round's
+// workgroups: the GNC decision is taken by every workgroup from the same
+// state; block 0 resets the robots' state and writes the schedule state; all
+// workgroups re-weight the loop closures grid-stride (one edge per thread,
+// order-free).
+template <int RW>
+__device__ __forceinline__ void body_begin(const Dev& d, const unsigned char* active, bool may_fire, int R_) {
+  const bool fire = may_fire && d.p.robust && gnc_should_update(d);
+  if (blockIdx.x == 0) {
+    for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
+    if (threadIdx.x == 0) {
+      Gnc s = load_gnc(d.gnc);
+      s.fired = fire ? 1 : 0;
+      if (fire) {
+        s.inner = 0;
+        s.updates += 1;
+        s.mu = s.mu * d.p.mu_step;
+      }
+      store_gnc(d.gnc_next, s);
+      if (!may_fire) store_gnc(d.gnc, s);  // no reader of the state is left (k_begin's BEGIN_SOLO)
+      if (fire) atomicAdd(&d.cnt->gnc_updates, 1ull);
+    }
+  }
+  if (!fire) return;
+  const double mu = d.gnc->mu;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n_gnc; i += gridDim.x * blockDim.x) gnc_edge<RW>(d, i, R_, mu);
+}
+
+template <int R>
+struct SmemRound {  // the largest phase's dynamic LDS
+  static constexpr int a = SmemHG<R>::bytes > SmemH<R>::bytes ? SmemHG<R>::bytes : SmemH<R>::bytes;
+  static constexpr int b = SmemC<R>::bytes > SmemU::bytes ? SmemC<R>::bytes : SmemU::bytes;
+  static constexpr int bytes = a > b ? a : b;
+};
+
+// 2 waves per SIMD (2 workgroups per CU, 256 VGPRs): with every phase inlined
+// in one loop the register demand exceeds the launched kernels' (3 waves per
+// SIMD spilled 16-25 VGPRs to scratch, and scratch limits how many workgroups
+// stay resident), so the round takes the cut of at most 2 tiles per CU.
+template <int R>
+struct LBR {
+  static constexpr int w = 2;
+};
+template <int R, int RW>
+__global__ __launch_bounds__(BLOCK, LBR<R>::w) void k_round(Dev d, const unsigned char* active, int may_fire,
+                                                           int census) {
+  GridBar* b = d.bar;
+  const int tcg_max = d.p.tcg_max;
+  if (census) {  // residency check of this very kernel and grid (census word zeroed before the launch)
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(&b->census[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long t0 = wall_clock64();
+      while (__hip_atomic_load(&b->census[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > 2000000ull) {  // 20 ms: not every workgroup is resident
+          __hip_atomic_store(&b->err[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    return;
+  }
+  KMX_SMEM;
+  __shared__ unsigned sh_gen, sh_alive[2];
+  if (threadIdx.x == 0) sh_gen = __hip_atomic_load(&b->gen[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  unsigned gen = sh_gen;
+#define KMX_SYNC()                          \
+  do {                                      \
+    if (!grid_sync(b, ++gen)) return;       \
+  } while (0)
+  // the alive count after a barrier (alternating slots: no barrier needed
+  // between one read and the next write of the broadcast word)
+#define KMX_ALIVE(k, out)                                                                              \
+  do {                                                                                                 \
+    if (threadIdx.x == 0) sh_alive[k] = __hip_atomic_load(&b->alive[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    __syncthreads();                                                                                   \
+    out = sh_alive[k];                                                                                 \
+  } while (0)
+  body_begin<RW>(d, active, may_fire != 0, R);
+  KMX_SYNC();
+  body_grad<R, RW, RM_CONSUMER>(d, may_fire, smem);
+  KMX_SYNC();
+  unsigned a_prev, a;
+  KMX_ALIVE(0, a_prev);
+  for (int j = 0; j < tcg_max; ++j) {
+    body_hess<R, RW, RM_CONSUMER, true>(d, -1, nullptr, 0ull, smem, &b->alive[0]);
+    KMX_SYNC();
+    KMX_ALIVE((j + 1) & 1, a);  // the robots whose tCG ran this step
+    body_update<R, RM_CONSUMER, true>(d, nullptr, 0ull, -1, smem);
+    KMX_SYNC();
+    if (a == a_prev) break;  // no robot continued: the update only carried the states over
+    a_prev = a;
+  }
+  body_retract<R>(d, 1, smem);
+  KMX_SYNC();
+  body_cost<R, RW, RM_CONSUMER>(d, smem);
+  KMX_SYNC();
+  body_commit<R, true>(d, 1, 1);
+#undef KMX_SYNC
+#undef KMX_ALIVE
+}
+
 // 4x4 diagonal blocks D_i of Q per pose (hD, for the Hessian gather) and the
 // inverse preconditioner blocks (D_i + shift I)^-1 by Cholesky; same
 // accumulation order and expressions as oracle build_precond. `gated`: only
@@ -1825,7 +1919,7 @@ __global__ void k_begin(Dev d, const unsigned char* active, int mode, int R_) {
 template <int RW>
 __global__ void k_precond(Dev d, int gated) {
   if (gated) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *d.gnc = *d.gnc_next;
+    if (blockIdx.x == 0 && threadIdx.x == 0) store_gnc(d.gnc, load_gnc(d.gnc_next));
     if (!d.gnc_next->fired) return;
   }
   for (int pose = blockIdx.x * blockDim.x + threadIdx.x; pose < d.nloc; pose += gridDim.x * blockDim.x)
@@ -2186,7 +2280,6 @@ struct kmx_pgo {
   Ctl* d_ctl2 = nullptr;
   double *d_part_h = nullptr, *d_part_u = nullptr;
   Counters* d_cnt = nullptr;
-  unsigned* d_tickets = nullptr;
   long long* d_m_robot = nullptr;
   int* d_n_robot = nullptr;
   int* d_pub_src = nullptr;    // slot -> local pose (-1 if not local)
@@ -2235,7 +2328,7 @@ struct kmx_pgo {
   // (measured and removed: a hipStreamQuery before the status spin put a ~5 us
   // bubble before the next tCG step's first kernel, profiles/r02/ab_query)
   // reduction mode: set per graph (below) unless KMX_RED forces one (0 launch,
-  // 1 tickets, 2 consumer, 3 half). Measured at the end of round 2
+  // 2 consumer). Measured at the end of round 2
   // (profiles/r02/small_round/16_*): the consumer form (no reduction launch,
   // the stop decision before the gather) wins per round at 25k poses (244 vs
   // 280 us), 37.5k (318 vs 357), 62.5k (530 vs 543) and 75k (583 vs 591), ties
@@ -2249,11 +2342,15 @@ struct kmx_pgo {
   // timing
   bool timing = false;
   int* d_hv_launch = nullptr;
-  int* d_rgroup0 = nullptr;
-  unsigned* d_gtickets = nullptr;
-  double* d_gpart = nullptr;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
+  // persistent round (k_round): one launch per round when the problem's tiles
+  // all fit the GPU at once; KMX_ROUND=0 keeps the launched form, 1 (default)
+  // uses k_round wherever it applies
+  GridBar* d_bar = nullptr;
+  bool persistent = false;
+  int round_forced = -1;
+  int round_capacity = 0;  // resident workgroups of k_round on this device
   // Nesterov acceleration (P.acceleration): momentum V and this round's Y
   // (allocated only when enabled), gamma and the restart counter on the host
   double *d_accV = nullptr, *d_accY = nullptr;
@@ -2317,11 +2414,11 @@ void free_xchg(kmx_pgo* h) {
 void free_dev(kmx_pgo* h) {
   void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_rec, h->d_ekappa,
                   h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_hD, h->d_pub, h->d_part,
-                  h->d_ctl, h->d_cnt, h->d_tickets, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
+                  h->d_ctl, h->d_cnt, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
-                  h->d_rgroup0, h->d_gtickets, h->d_gpart, h->d_accV, h->d_accY, h->d_ctl2, h->d_part_h,
-                  h->d_part_u};
+                  h->d_accV, h->d_accY, h->d_ctl2, h->d_part_h,
+                  h->d_part_u, h->d_bar};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
@@ -2330,7 +2427,6 @@ void free_dev(kmx_pgo* h) {
   h->d_vec = h->d_S = h->d_Pinv = h->d_hD = h->d_pub = h->d_part = nullptr;
   h->d_ctl = nullptr;
   h->d_cnt = nullptr;
-  h->d_tickets = nullptr;
   h->d_m_robot = nullptr;
   h->d_n_robot = h->d_pub_src = h->d_own_src = h->d_pose_slot = h->d_gnc_edge = nullptr;
   h->d_gnc_ends = nullptr;
@@ -2343,12 +2439,11 @@ void free_dev(kmx_pgo* h) {
   h->d_scratch = nullptr;
   h->scratch_cap = 0;
   h->d_hv_launch = nullptr;
-  h->d_rgroup0 = nullptr;
-  h->d_gtickets = nullptr;
-  h->d_gpart = nullptr;
   h->d_accV = h->d_accY = nullptr;
   h->d_ctl2 = nullptr;
   h->d_part_h = h->d_part_u = nullptr;
+  h->d_bar = nullptr;
+  h->persistent = false;
 }
 
 hipEvent_t next_event(kmx_pgo* h) {
@@ -2462,9 +2557,8 @@ bool wait_running(kmx_pgo* h, unsigned long long seq) {
 
 template <int R, int RM>
 void red_t(kmx_pgo* h, int kind, HostStatus* hs = nullptr, unsigned long long seq = 0, int slot = -1,
-           const double* src = nullptr, const Ctl* from = nullptr) {
-  if (RM != RM_TICKET)
-    hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot, src, from);
+           const double* src = nullptr) {
+  hipLaunchKernelGGL(k_reduce, dim3(h->dv.L), dim3(RBLOCK), 0, h->stream, h->dv, kind, R, hs, seq, slot, src);
 }
 
 // The parts of a round: gradient, tCG (host-polled steps), trial point and
@@ -2530,10 +2624,9 @@ void enqueue_tcg_t(kmx_pgo* h) {
     }
     hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, nullptr, 0ull);
     if (slot >= 0) (void)hipEventRecord(e1, h->stream);
-    if (RM != RM_HALF) red_t<R, RM>(h, RED_HESS, nullptr, 0, slot);
-    hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv,
-                       RM == RM_TICKET ? hs : nullptr, seq, RM == RM_HALF ? slot : -1);
-    red_t<R, RM>(h, RED_UPDATE, hs, seq, -1, nullptr, RM == RM_HALF ? h->dv.ctl2 : nullptr);
+    red_t<R, RM>(h, RED_HESS, nullptr, 0, slot);
+    hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, seq, -1);
+    red_t<R, RM>(h, RED_UPDATE, hs, seq, -1, nullptr);
     if (poll) {
       if (j > 0 && !wait_running(h, prev)) {
         steps = j + 1;
@@ -2572,17 +2665,50 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0, 1);
 }
 
+// The persistent round: the same phases as enqueue_round_t<R, RW, RM_CONSUMER>
+// in one launch (k_round).
+template <int R, int RW>
+void enqueue_round_persistent(kmx_pgo* h, const unsigned char* d_active) {
+  const int may_fire = h->P.robust_cost == KMX_COST_GNC_TLS && h->gnc_on ? 1 : 0;
+  hipLaunchKernelGGL((k_round<R, RW>), dim3(h->ntiles), dim3(BLOCK), SmemRound<R>::bytes, h->stream, h->dv, d_active,
+                     may_fire, 0);
+}
+
+// Census launch of k_round with the handle's grid: every workgroup arrives
+// and waits (20 ms at most) until all have; true when all were resident.
+template <int R, int RW>
+bool round_census_t(kmx_pgo* h) {
+  if (hipMemsetAsync(h->d_bar, 0, sizeof(GridBar), h->stream) != hipSuccess) return false;
+  hipLaunchKernelGGL((k_round<R, RW>), dim3(h->ntiles), dim3(BLOCK), SmemRound<R>::bytes, h->stream, h->dv,
+                     h->d_active, 0, 1);
+  unsigned err = 1;
+  if (hipGetLastError() != hipSuccess) return false;
+  if (hipMemcpyAsync(&err, &h->d_bar->err[0], sizeof(unsigned), hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+    return false;
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return false;
+  (void)hipMemsetAsync(h->d_bar, 0, sizeof(GridBar), h->stream);
+  (void)hipStreamSynchronize(h->stream);
+  return err == 0;
+}
+
+template <int R, int RW>
+int round_capacity_t(int device) {
+  int nb = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_round<R, RW>, BLOCK, SmemRound<R>::bytes) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  return nb * cus;
+}
+
 template <int R>
 void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
+  if (h->persistent) {
+    if (h->rw == 10) enqueue_round_persistent<R, 10>(h, d_active);
+    else enqueue_round_persistent<R, 16>(h, d_active);
+    return;
+  }
   if (h->rm == RM_CONSUMER) {
     if (h->rw == 10) enqueue_round_t<R, 10, RM_CONSUMER>(h, d_active);
     else enqueue_round_t<R, 16, RM_CONSUMER>(h, d_active);
-  } else if (h->rm == RM_HALF) {
-    if (h->rw == 10) enqueue_round_t<R, 10, RM_HALF>(h, d_active);
-    else enqueue_round_t<R, 16, RM_HALF>(h, d_active);
-  } else if (h->rm == RM_TICKET) {
-    if (h->rw == 10) enqueue_round_t<R, 10, RM_TICKET>(h, d_active);
-    else enqueue_round_t<R, 16, RM_TICKET>(h, d_active);
   } else {
     if (h->rw == 10) enqueue_round_t<R, 10, RM_LAUNCH>(h, d_active);
     else enqueue_round_t<R, 16, RM_LAUNCH>(h, d_active);
@@ -2600,6 +2726,52 @@ void enqueue_round(kmx_pgo* h, const unsigned char* d_active) {
     case 7: enqueue_round_r<7>(h, d_active); break;
     default: enqueue_round_r<8>(h, d_active); break;
   }
+}
+
+int round_capacity(const kmx_pgo* h) {
+  const bool full = h->rw == 16;
+  switch (h->P.r) {
+#define KMX_CAP(RR) \
+  case RR: return full ? round_capacity_t<RR, 16>(h->device) : round_capacity_t<RR, 10>(h->device);
+    KMX_CAP(3) KMX_CAP(4) KMX_CAP(5) KMX_CAP(6) KMX_CAP(7)
+    default: return full ? round_capacity_t<8, 16>(h->device) : round_capacity_t<8, 10>(h->device);
+#undef KMX_CAP
+  }
+}
+
+bool round_census(kmx_pgo* h) {
+  const bool full = h->rw == 16;
+  switch (h->P.r) {
+#define KMX_CEN(RR) \
+  case RR: return full ? round_census_t<RR, 16>(h) : round_census_t<RR, 10>(h);
+    KMX_CEN(3) KMX_CEN(4) KMX_CEN(5) KMX_CEN(6) KMX_CEN(7)
+    default: return full ? round_census_t<8, 16>(h) : round_census_t<8, 10>(h);
+#undef KMX_CEN
+  }
+}
+
+// k_round applies to the RM_CONSUMER form with one RTR iteration of the RTR
+// method (round_form_possible) when every tile is resident at once: within the
+// occupancy API's capacity, and confirmed by a census launch of the kernel on
+// the handle's grid.
+bool round_form_possible(const kmx_pgo* h) {
+  return h->round_forced != 0 && h->rm == RM_CONSUMER && h->P.rtr_iterations == 1 && h->P.method == KMX_METHOD_RTR;
+}
+void choose_round_form(kmx_pgo* h) {
+  h->round_capacity = round_capacity(h);
+  const bool fits = h->ntiles >= 1 && h->ntiles <= h->round_capacity;
+  h->persistent = round_form_possible(h) && fits && round_census(h);
+}
+
+// A bounded barrier spin of k_round gave up (a workgroup was not resident or
+// the device stalled): report it and re-zero the barrier words.
+int check_round(kmx_pgo* h) {
+  if (!h->persistent || !h->d_bar) return KMX_OK;
+  unsigned err = 0;
+  KMX_HIP(hipMemcpy(&err, &h->d_bar->err[0], sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (!err) return KMX_OK;
+  KMX_HIP(hipMemset(h->d_bar, 0, sizeof(GridBar)));
+  return kmx::fail(KMX_EHIP, "k_round: a grid barrier timed out (results of the last rounds are invalid)");
 }
 
 // Acceleration (oracle orc_pgo_accel_pre / _post): gamma' = (1 + sqrt(1 +
@@ -2691,9 +2863,10 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     h->poll_auto = false;
   }
   if (const char* v = std::getenv("KMX_EARLY")) h->early_forced = std::atoi(v) != 0 ? 1 : 0;
+  if (const char* v = std::getenv("KMX_ROUND")) h->round_forced = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);
-    h->rm_forced = m == 0 ? RM_LAUNCH : m == 1 ? RM_TICKET : m == 2 ? RM_CONSUMER : RM_HALF;
+    h->rm_forced = m == 0 ? RM_LAUNCH : m == 2 ? RM_CONSUMER : -1;  // 1 and 3 (tickets, half) were removed
   }
   *out = h;
   return KMX_OK;
@@ -2706,7 +2879,7 @@ extern "C" int kmx_pgo_destroy(kmx_pgo* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   free_dev(h);
   free_xchg(h);
-  if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->comm) (void)ncclCommAbort(h->comm);  // non-blocking communicator: no finalize handshake at teardown
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   if (h->hstat) (void)hipHostFree(h->hstat);
@@ -2934,6 +3107,14 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   int64_t inc_all = (int64_t)inc_ptr[nloc] - inc_ptr[0];
   int64_t tilecap = std::min<int64_t>(2 * (int64_t)TP * r,
                                       std::max<int64_t>(180, (inc_all + TILES_TARGET - 1) / TILES_TARGET));
+  // a problem the persistent round can hold (every tile resident) is cut
+  // coarser, to ~90 % of the round kernel's resident capacity (k_round,
+  // kmx.dpgo.driver.team_tile_incidences mirrors this rule)
+  h->round_capacity = round_capacity(h);
+  if (round_form_possible(h) && h->round_capacity > 0) {
+    const int64_t cp = (inc_all * 10 + 9 * (int64_t)h->round_capacity - 1) / (9 * (int64_t)h->round_capacity);
+    if (cp <= 2 * (int64_t)TP * r) tilecap = std::max(tilecap, cp);
+  }
   if (h->P.tile_incidences > 0) tilecap = std::max(16, h->P.tile_incidences);
   if (const char* v = std::getenv("KMX_TILE_CAP")) tilecap = std::max(16, std::atoi(v));
   for (int l = 0; l < L; ++l) {
@@ -2967,9 +3148,6 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   for (int64_t k = 0; k < h->n_owned; ++k) own_src[k] = pub_src[h->first_owned + k];
   std::vector<int> nrob(L);
   for (int l = 0; l < L; ++l) nrob[l] = n_poses[h->robots[l]];
-  std::vector<int> rgroup0(L + 1, 0);  // ticket groups of GS tiles per robot
-  for (int l = 0; l < L; ++l) rgroup0[l + 1] = rgroup0[l] + (rt0[l + 1] - rt0[l] + GS - 1) / GS;
-  const int ngroups = std::max(rgroup0[L], 1);
   // device
   int rc;
   const size_t vec = (size_t)std::max(nloc, 1) * ps;
@@ -2986,7 +3164,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_part, (size_t)h->ntiles * NPART)) || (rc = dalloc(&h->d_ctl, L)) ||
       (rc = dalloc(&h->d_ctl2, L)) || (rc = dalloc(&h->d_part_h, (size_t)h->ntiles * 2)) ||
       (rc = dalloc(&h->d_part_u, (size_t)h->ntiles * 2)) ||
-      (rc = dalloc(&h->d_cnt, 1)) || (rc = dalloc(&h->d_tickets, L)) || (rc = dalloc(&h->d_m_robot, L)) ||
+      (rc = dalloc(&h->d_cnt, 1)) || (rc = dalloc(&h->d_m_robot, L)) ||
       (rc = dalloc(&h->d_n_robot, L)) || (rc = dalloc(&h->d_pub_src, pub_src.size())) ||
       (rc = dalloc(&h->d_own_src, own_src.size())) || (rc = dalloc(&h->d_pose_slot, pose_slot.size())) ||
       (rc = dalloc(&h->d_gnc_edge, std::max(h->n_gnc, 1))) || (rc = dalloc(&h->d_gnc_ends, std::max(h->n_gnc, 1))) ||
@@ -2994,8 +3172,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_sh_idx, std::max(h->n_sh_local, 1))) || (rc = dalloc(&h->d_active, L)) ||
       (rc = dalloc(&h->d_osh_edge, std::max(h->n_osh, 1))) || (rc = dalloc(&h->d_osh_idx, std::max(h->n_osh, 1))) ||
       (rc = dalloc(&h->d_relc, L)) || (rc = dalloc(&h->d_gnc, 2)) || (rc = dalloc(&h->d_ext, 64)) ||
-      (rc = dalloc(&h->d_hv_launch, HV_SLOTS)) || (rc = dalloc(&h->d_rgroup0, L + 1)) ||
-      (rc = dalloc(&h->d_gtickets, ngroups)) || (rc = dalloc(&h->d_gpart, (size_t)ngroups * NPART))) {
+      (rc = dalloc(&h->d_hv_launch, HV_SLOTS)) ||
+      (rc = dalloc(&h->d_bar, 1))) {
     free_dev(h);
     return rc;
   }
@@ -3017,11 +3195,9 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(hipMemsetAsync(h->d_pub, 0, sizeof(double) * std::max<int64_t>(h->npub, 1) * ps, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_ctl, 0, sizeof(Ctl) * L, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_cnt, 0, sizeof(Counters), h->stream));
-  KMX_HIP(hipMemsetAsync(h->d_tickets, 0, sizeof(unsigned) * L, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_ext, 0, sizeof(double) * 64, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_hv_launch, 0, sizeof(int) * HV_SLOTS, h->stream));
-  KMX_HIP(hipMemsetAsync(h->d_gtickets, 0, sizeof(unsigned) * ngroups, h->stream));
-  KMX_HIP(up(h->d_rgroup0, rgroup0.data(), sizeof(int) * (L + 1)));
+  KMX_HIP(hipMemsetAsync(h->d_bar, 0, sizeof(GridBar), h->stream));
   if (L > h->hstat_cap) {  // host-mapped per-robot tCG progress
     if (h->hstat) (void)hipHostFree(h->hstat);
     h->hstat = nullptr;
@@ -3070,15 +3246,16 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
   d.z = h->d_vec + 4 * vec; d.eta = h->d_vec + 5 * vec; d.del = h->d_vec + 6 * vec; d.hd = h->d_vec + 7 * vec;
   d.S = h->d_S; d.Pinv = h->d_Pinv; d.hD = h->d_hD; d.pub = h->d_pub; d.part = h->d_part;
-  d.ctl = h->d_ctl; d.cnt = h->d_cnt; d.tickets = h->d_tickets;
+  d.ctl = h->d_ctl; d.cnt = h->d_cnt;
   d.ctl2 = h->d_ctl2; d.part_h = h->d_part_h; d.part_u = h->d_part_u;
   d.m_robot = h->d_m_robot; d.n_robot = h->d_n_robot; d.pose_slot = h->d_pose_slot;
   d.relc = h->d_relc; d.gnc = h->d_gnc; d.gnc_next = h->d_gnc + 1;
   d.gnc_edge = h->d_gnc_edge; d.gnc_ends = h->d_gnc_ends; d.n_gnc = h->n_gnc;
   d.hv_launch = h->d_hv_launch;
-  d.rgroup0 = h->d_rgroup0; d.gtickets = h->d_gtickets; d.gpart = h->d_gpart;
+  d.bar = h->d_bar;
   h->n_ext = 0;
   sync_params(h);
+  choose_round_form(h);
   enqueue_precond(h, 0);
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipStreamSynchronize(h->stream));
@@ -3205,6 +3382,19 @@ extern "C" int kmx_pgo_exchange_unpack(kmx_pgo* h, const int32_t* dev_slots, int
     if (r_ != ncclSuccess) return kmx::fail(KMX_EHIP, std::string(#call) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
+// A call on a non-blocking communicator may return ncclInProgress: wait for
+// it to settle (bounded), then report its final status.
+int nccl_settle(kmx_pgo* h, ncclResult_t r, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+      return kmx::fail(KMX_EHIP, std::string(what) + ": still in progress after 60 s");
+    if (ncclCommGetAsyncError(h->comm, &r) != ncclSuccess) r = ncclSystemError;
+  }
+  if (r != ncclSuccess) return kmx::fail(KMX_EHIP, std::string(what) + ": " + ncclGetErrorString(r));
+  return KMX_OK;
+}
+
 // publishPublicPoses -> updateNeighborPoses + publishStatus of one round
 // (drawio:2340-2375) over RCCL: the rows every peer needs (+ this handle's
 // status word) are gathered, each peer's segment goes by ncclSend / ncclRecv in
@@ -3224,7 +3414,9 @@ int enqueue_exchange(kmx_pgo* h) {
     KMX_NCCL(ncclSend(h->d_xsbuf + h->xs_off[q], (size_t)h->xs_cnt[q], ncclDouble, q, h->comm, h->stream));
     KMX_NCCL(ncclRecv(h->d_xrbuf + h->xr_off[q], (size_t)h->xr_cnt[q], ncclDouble, q, h->comm, h->stream));
   }
-  KMX_NCCL(ncclGroupEnd());
+  // the communicator is non-blocking (kmx_pgo_comm_init): the group may still
+  // be enqueueing when ncclGroupEnd returns
+  if (int rc = nccl_settle(h, ncclGroupEnd(), "ncclGroupEnd")) return rc;
   if (!h->xchg_self_p2p)  // this handle's own segment (its status word)
     KMX_HIP(hipMemcpyAsync(h->d_xrbuf + h->xr_off[h->rank], h->d_xsbuf + h->xs_off[h->rank],
                            sizeof(double) * h->xs_cnt[h->rank], hipMemcpyDeviceToDevice, h->stream));
@@ -3248,20 +3440,68 @@ extern "C" int kmx_comm_unique_id(void* out, int64_t nbytes) {
   KMX_GUARD_END
 }
 
-extern "C" int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, int rank) {
+// Non-blocking communicator creation with a deadline: a rank whose peers never
+// arrive (one of them failed before ncclCommInitRank) aborts its half-built
+// communicator and returns an error instead of blocking in the rendezvous.
+extern "C" int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, int rank, double timeout_s) {
   KMX_GUARD_BEGIN
   KMX_CHECK(h && unique_id, KMX_EINVAL, "null argument");
   KMX_CHECK(world >= 1 && world <= 1024 && rank >= 0 && rank < world, KMX_EINVAL, "bad world / rank");
+  KMX_CHECK(timeout_s > 0.0, KMX_EINVAL, "timeout_s must be > 0");
   KMX_CHECK(!h->comm, KMX_ESTATE, "communicator already initialised");
   KMX_HIP(hipSetDevice(h->device));
   ncclUniqueId id;
   std::memcpy(&id, unique_id, sizeof(id));
   ncclComm_t c = nullptr;
-  KMX_NCCL(ncclCommInitRank(&c, world, id, rank));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&c, world, id, rank, &cfg);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+      if (c) (void)ncclCommAbort(c);
+      return kmx::fail(KMX_EHIP, "ncclCommInitRankConfig: no rendezvous within the timeout (a peer failed?)");
+    }
+    if (ncclCommGetAsyncError(c, &r) != ncclSuccess) r = ncclSystemError;
+  }
+  if (r != ncclSuccess) {
+    if (c) (void)ncclCommAbort(c);
+    return kmx::fail(KMX_EHIP, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  }
   h->comm = c;
   h->world = world;
   h->rank = rank;
   if (const char* v = std::getenv("KMX_XCHG_SELF_P2P")) h->xchg_self_p2p = std::atoi(v) != 0;
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_pgo_comm_destroy(kmx_pgo* h) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  free_xchg(h);
+  if (h->comm) (void)ncclCommAbort(h->comm);
+  h->comm = nullptr;
+  h->world = 1;
+  h->rank = 0;
+  if (h->n_ext) {  // the peers' statuses came with the exchange
+    h->n_ext = 0;
+    sync_params(h);
+  }
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_get_public(kmx_pgo* h, double* table, double* ext) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  KMX_CHECK(table || h->npub == 0, KMX_EINVAL, "null table");
+  KMX_HIP(hipSetDevice(h->device));
+  if (h->npub)
+    KMX_HIP(hipMemcpyAsync(table, h->d_pub, sizeof(double) * h->npub * 4 * h->P.r, hipMemcpyDeviceToHost, h->stream));
+  if (ext && h->n_ext)
+    KMX_HIP(hipMemcpyAsync(ext, h->d_ext, sizeof(double) * h->n_ext, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -3392,6 +3632,7 @@ extern "C" int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats
   std::vector<Ctl> ctl(L);
   KMX_HIP(hipMemcpyAsync(ctl.data(), h->d_ctl, sizeof(Ctl) * L, hipMemcpyDeviceToHost, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));
+  if (int rc = check_round(h)) return rc;
   // restore the all-active mask used by iterate_async
   std::vector<unsigned char> ones(L, 1);
   KMX_HIP(hipMemcpyAsync(h->d_active, ones.data(), L, hipMemcpyHostToDevice, h->stream));
@@ -3440,6 +3681,24 @@ extern "C" int kmx_pgo_sync(kmx_pgo* h) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->stream));
+  return check_round(h);
+}
+
+extern "C" int kmx_pgo_round_form(kmx_pgo* h, int* persistent, int* capacity, int* tiles) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  if (persistent) *persistent = h->persistent ? 1 : 0;
+  if (capacity) *capacity = h->round_capacity;
+  if (tiles) *tiles = h->ntiles;
+  return KMX_OK;
+}
+
+extern "C" int kmx_pgo_set_round_form(kmx_pgo* h, int mode) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_CHECK(mode >= -1 && mode <= 1, KMX_EINVAL, "mode is -1 (automatic), 0 (launched) or 1 (persistent where it applies)");
+  KMX_HIP(hipSetDevice(h->device));
+  if (h->stream) KMX_HIP(hipStreamSynchronize(h->stream));
+  h->round_forced = mode == -1 ? -1 : mode;
+  if (ready(h)) choose_round_form(h);
   return KMX_OK;
 }
 

@@ -17,7 +17,7 @@ import numpy as np
 _LIB_PATH = Path(__file__).resolve().parent / "libkmx.so"
 
 KMX_OK = 0
-ABI_VERSION = 4  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
+ABI_VERSION = 5  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
 KMX_COST_L2 = 0
 KMX_COMM_ID_BYTES = 128  # include/kmx_abi.h (ncclUniqueId)
 KMX_COST_GNC_TLS = 1
@@ -98,7 +98,8 @@ class LcdParams(C.Structure):
         ("ransac_probability", C.c_double), ("ransac_randomize", C.c_int),
         ("ransac_seed", C.c_uint32), ("rng_variant", C.c_int),
         ("use_1point_3d3d", C.c_int), ("pose_recovery_type", C.c_int), ("min_2d3d_inliers", C.c_int),
-        ("ransac_threshold_2d3d", C.c_double), ("algorithm_2d2d", C.c_int), ("reserved", C.c_int * 3),
+        ("ransac_threshold_2d3d", C.c_double), ("algorithm_2d2d", C.c_int), ("refine_pose", C.c_int),
+        ("reserved", C.c_int * 2),
     ]
 
 
@@ -136,7 +137,9 @@ def lib() -> C.CDLL:
         "kmx_pgo_set_stream": ([P, P], C.c_int),
         "kmx_pgo_set_tcg_poll": ([P, C.c_int], C.c_int),
         "kmx_comm_unique_id": ([P, i64], C.c_int),
-        "kmx_pgo_comm_init": ([P, P, C.c_int, C.c_int], C.c_int),
+        "kmx_pgo_comm_init": ([P, P, C.c_int, C.c_int, f64], C.c_int),
+        "kmx_pgo_comm_destroy": ([P], C.c_int),
+        "kmx_pgo_get_public": ([P, pf64, pf64], C.c_int),
         "kmx_pgo_set_exchange": ([P, pi32, pi64, pi32, pi64], C.c_int),
         "kmx_pgo_exchange": ([P], C.c_int),
         "kmx_pgo_set_graph": ([P, C.c_int, pi32, pu8, i64, pi32, pi32, pi32, pi32,
@@ -155,6 +158,8 @@ def lib() -> C.CDLL:
         "kmx_pgo_iterate": ([P, pu8, C.POINTER(IterStats)], C.c_int),
         "kmx_pgo_iterate_async": ([P, C.c_int, C.c_int], C.c_int),
         "kmx_pgo_sync": ([P], C.c_int),
+        "kmx_pgo_set_round_form": ([P, C.c_int], C.c_int),
+        "kmx_pgo_round_form": ([P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
         "kmx_pgo_update_weights": ([P, pf64], C.c_int),
         "kmx_pgo_get_mu": ([P, pf64], C.c_int),
         "kmx_pgo_set_mu": ([P, f64], C.c_int),

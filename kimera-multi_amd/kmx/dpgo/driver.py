@@ -90,16 +90,31 @@ def exchange_plan(graph, world: int, rank: int):
 
 
 TILES_TARGET = 736  # csrc/pgo.hip: the tile count the cut of small problems aims at
+ROUND_CAPACITY = 512  # csrc/pgo.hip k_round: resident workgroups on an MI355X (2 per CU x 256 CUs)
+CONSUMER_MAX_POSES = 80_000  # csrc/pgo.hip RM_CONSUMER_MAX_POSES
 
 
-def team_tile_incidences(graph, world: int, r: int) -> int:
+def team_tile_incidences(graph, world: int, r: int, params: PGOAgentParameters | None = None) -> int:
     """The tile cut (incidences per workgroup tile) kmx_pgo_set_graph picks
     automatically for a handle holding 1/world of the team's incidences; the
     multi-rank driver passes it to every rank, so all ranks cut their robots
-    alike whatever their share (csrc/pgo.hip set_graph)."""
+    alike whatever their share (csrc/pgo.hip set_graph): about TILES_TARGET
+    tiles between 180 incidences and two gather chunks, and — where the
+    persistent round applies (one RTR iteration of RTR, a consumer-form
+    problem, KMX_ROUND not 0) — coarse enough for ~90 % of the round kernel's
+    resident capacity when that stays within two chunks."""
     tp = 4 * (64 // r)
     inc = 2 * int(graph.m) // max(world, 1)
-    return min(2 * tp * r, max(180, -(-inc // TILES_TARGET)))
+    cap = min(2 * tp * r, max(180, -(-inc // TILES_TARGET)))
+    lo = params.localOptimizationParams if params is not None else None
+    persistent = (os.environ.get("KMX_ROUND", "1") != "0"
+                  and (lo is None or (lo.RTR_iterations == 1 and int(lo.method) == 0))
+                  and int(graph.n_total) // max(world, 1) <= CONSUMER_MAX_POSES)
+    if persistent:
+        cp = -(-inc * 10 // (9 * ROUND_CAPACITY))
+        if cp <= 2 * tp * r:
+            cap = max(cap, cp)
+    return cap
 
 
 class RBCDDriver:
@@ -126,14 +141,16 @@ class RBCDDriver:
         self.local = local
         if solver is None and world > 1 and params.tileIncidences == 0:
             import dataclasses
-            params = dataclasses.replace(params, tileIncidences=team_tile_incidences(graph, world, params.r))
+            params = dataclasses.replace(params, tileIncidences=team_tile_incidences(graph, world, params.r, params))
             self.params = params
         self.solver = solver if solver is not None else BlockSolver(params, device)
         self.executing = ExecutingRobot(params.updateRule, params.randomSeed)
         self.round_index = 0
         self._torch = None
         self._xdev = exchange_device
-        self.native = False  # RCCL exchange inside the solver's rounds (_setup_exchange)
+        self.native = False  # RCCL exchange inside the solver's rounds (_setup_native)
+        self._native_verified = True
+        self.exchange_mode = "none (one rank)" if world == 1 else ""
         if world > 1:
             import torch
             import torch.distributed as dist
@@ -189,24 +206,92 @@ class RBCDDriver:
         # the round, so a batch of rounds is one host call with no Python or
         # cross-stream hop between exchange and round. KMX_NATIVE_XCHG=0 keeps
         # the torch.distributed all_to_all of exchange_public.
-        self.native = (self._xdev == "cuda" and getattr(self.solver, "native_exchange", False)
-                       and os.environ.get("KMX_NATIVE_XCHG", "1") != "0")
-        if self.native:
-            ok = 1
+        self._plan = (send_slots, send_counts, recv_slots, recv_counts)
+        self.native = self._setup_native()
+        self._native_verified = not self.native
+
+    def _agree(self, ok: bool) -> bool:
+        """True on every rank iff ok on every rank (one MIN all-reduce)."""
+        t = self._torch.tensor([1 if ok else 0], dtype=self._torch.int32,
+                               device="cuda" if self._dist.get_backend() == "nccl" else "cpu")
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def _setup_native(self) -> bool:
+        """The in-round RCCL exchange, set up in steps every rank passes
+        together, so a failure on one rank never leaves its peers waiting in a
+        collective or a rendezvous:
+          1. local checks (solver capable, backend nccl, not disabled); rank 0
+             creates the unique id; the id slot is broadcast ALWAYS (None when
+             rank 0 failed), then one MIN all-reduce agrees on going ahead;
+          2. every rank creates its communicator non-blocking with a deadline
+             (kmx_pgo_comm_init), then one MIN all-reduce agrees on success;
+             on any failure every rank drops its communicator;
+          3. at the first round the native exchange is checked bit for bit
+             against the torch.distributed all_to_all (_verify_native).
+        self.exchange_mode says which exchange runs and why."""
+        self.exchange_mode = "torch.distributed all_to_all_single"
+        capable = (self._xdev == "cuda" and bool(getattr(self.solver, "native_exchange", False))
+                   and os.environ.get("KMX_NATIVE_XCHG", "1") != "0")
+        uid = None
+        if self.rank == 0 and capable:
             try:
-                uid = [self.solver.comm_unique_id() if self.rank == 0 else None]
-                self._dist.broadcast_object_list(uid, src=0)
-                self.solver.comm_init(uid[0], self.world, self.rank)
-            except Exception as e:  # every rank falls back together (one MIN all-reduce)
-                import warnings
-                warnings.warn(f"native RCCL exchange unavailable ({e}); using torch.distributed all_to_all")
-                ok = 0
-            flag = torch.tensor([ok], dtype=torch.int32,
-                                device="cuda" if self._dist.get_backend() == "nccl" else "cpu")
-            self._dist.all_reduce(flag, op=self._dist.ReduceOp.MIN)
-            self.native = bool(flag.item())
-            if self.native:
-                self.solver.set_exchange(send_slots, send_counts, recv_slots, recv_counts)
+                uid = self.solver.comm_unique_id()
+            except Exception as e:  # noqa: BLE001 - reported, then every rank falls back
+                self._native_error = f"rank 0 unique id: {e}"
+        box = [uid]
+        self._dist.broadcast_object_list(box, src=0)  # always, so every rank stays in step
+        if not self._agree(capable and box[0] is not None):
+            if capable:
+                self.exchange_mode += " (fallback: the RCCL exchange could not start on every rank)"
+            return False
+        ok = True
+        try:
+            self.solver.comm_init(box[0], self.world, self.rank,
+                                  float(os.environ.get("KMX_COMM_TIMEOUT", "120")))
+        except Exception as e:  # noqa: BLE001
+            import warnings
+            warnings.warn(f"native RCCL exchange unavailable on rank {self.rank} ({e})")
+            ok = False
+        if not self._agree(ok):
+            if ok:
+                self.solver.comm_destroy()
+            self.exchange_mode += " (fallback: a rank could not create its RCCL communicator)"
+            return False
+        self.solver.set_exchange(*self._plan)
+        self.exchange_mode = "RCCL ncclSend/ncclRecv group inside each round (solver stream)"
+        return True
+
+    def _torch_exchange(self):
+        s = self.solver
+        s.exchange_pack(self._sslots.data_ptr(), self._n_send, self._sseg.data_ptr(), self.world,
+                        self._sbuf.data_ptr())
+        self._all_to_all(self._rbuf, self._sbuf)
+        s.exchange_unpack(self._rslots.data_ptr(), self._n_recv, self._rseg.data_ptr(), self.world,
+                          self._rbuf.data_ptr())
+
+    def _verify_native(self):
+        """First round only: the in-round RCCL exchange and the torch.distributed
+        all_to_all must install the same public table and peer statuses bit for
+        bit; otherwise every rank drops the native exchange (exchange_mode says
+        so). KMX_REQUIRE_NATIVE=1 makes a mismatch or fallback an error."""
+        if self._native_verified:
+            return
+        self._native_verified = True
+        s = self.solver
+        s.exchange()
+        tab_n, ext_n = s.get_public(self.world)
+        self._torch_exchange()
+        tab_t, ext_t = s.get_public(self.world)
+        same = np.array_equal(tab_n, tab_t) and np.array_equal(ext_n, ext_t)
+        if self._agree(same):
+            self.exchange_mode += ", checked bitwise against all_to_all at the first round"
+            return
+        s.comm_destroy()
+        self.native = False
+        self.exchange_mode = "torch.distributed all_to_all_single (fallback: the RCCL exchange differed from it)"
+        if os.environ.get("KMX_REQUIRE_NATIVE", "0") == "1":
+            raise RuntimeError(self.exchange_mode)
 
     def _all_to_all(self, out, inp):
         """One all-to-all with per-peer sizes (RCCL directly; a GPU solver under
@@ -231,14 +316,11 @@ class RBCDDriver:
         if self.world == 1:
             return
         if self.native:  # every round starts with it; this is an extra one (UPDATE_WEIGHT)
-            self.solver.exchange()
-            return
-        s = self.solver
-        s.exchange_pack(self._sslots.data_ptr(), self._n_send, self._sseg.data_ptr(), self.world,
-                        self._sbuf.data_ptr())
-        self._all_to_all(self._rbuf, self._sbuf)
-        s.exchange_unpack(self._rslots.data_ptr(), self._n_recv, self._rseg.data_ptr(), self.world,
-                          self._rbuf.data_ptr())
+            self._verify_native()
+            if self.native:
+                self.solver.exchange()
+                return
+        self._torch_exchange()
 
     def update_weights(self) -> float:
         """An explicit UPDATE_WEIGHT (outside the schedule): fresh neighbour rows,
@@ -282,7 +364,8 @@ class RBCDDriver:
         self._check_running()
         if self.native:  # the round starts with the exchange itself
             self._refresh_owned()
-        else:
+            self._verify_native()
+        if not self.native:
             self.exchange_public()
         stats = None
         if with_stats or self.params.schedule == 0 or self.logs or not self._all_active():
@@ -303,6 +386,9 @@ class RBCDDriver:
         """Benchmark path: enqueue `rounds` concurrent rounds with no host sync
         (single GPU: one C call; multi-GPU: one all-to-all between rounds)."""
         self._check_running()
+        if self.native:
+            self._refresh_owned()
+            self._verify_native()
         if (self.world == 1 or self.native) and self.params.schedule == 1 and self._all_active():
             self.solver.iterate_async(rounds, refresh_local=True)
             self.round_index += rounds
@@ -322,12 +408,49 @@ class RBCDDriver:
         self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX)
         return float(t.item())
 
+    def _team_sum(self, vals):
+        if self.world == 1:
+            return [float(v) for v in vals]
+        t = self._torch.tensor([float(v) for v in vals], dtype=self._torch.float64,
+                               device="cuda" if self._xdev == "cuda" else "cpu")
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM)
+        return [float(v) for v in t.cpu().tolist()]
+
+    def converged_weight_ratio(self) -> float:
+        """Fraction of the team's loop closures (non-fixed measurements) whose
+        GNC weight has converged to 0 or 1 (dpgo's robust-optimisation
+        convergence statistic [U: dpgo not vendored; |w| or |1 - w| <= 1e-8]).
+        Each measurement is counted once, on the rank owning its lower robot
+        id (drawio:2198). One all_reduce(SUM) when world > 1."""
+        g = self.graph
+        own = self.local[np.minimum(g.r1, g.r2)] == 1
+        lc = own & (np.asarray(g.fixed) == 0)
+        n = int(lc.sum())
+        conv = 0
+        if n:
+            w = np.asarray(self.solver.get_weights(), np.float64)[lc]
+            conv = int(((np.abs(w) <= 1e-8) | (np.abs(1.0 - w) <= 1e-8)).sum())
+        conv_t, n_t = self._team_sum([conv, n])
+        return 1.0 if n_t == 0 else conv_t / n_t
+
     def should_terminate(self) -> bool:
         """shouldTerminate (drawio:2027-2030): maxNumIters rounds ran, or every
-        agent's relative change is below relChangeTol."""
-        if self.round_index >= self.params.maxNumIters:
+        agent's relative change is below relChangeTol — and, for a robust cost,
+        GNC is done: robustOptNumWeightUpdates weight updates ran, or at least
+        robustOptMinConvergenceRatio of the loop-closure weights converged to
+        0 / 1 (dpgo keeps iterating while GNC still moves the weights; an
+        agent converged on the current weights is exactly what fires the next
+        update, drawio:2466-2469)."""
+        P = self.params
+        if self.round_index >= P.maxNumIters:
             return True
-        return self.team_max_rel_change() < self.params.relChangeTol
+        if not self.team_max_rel_change() < P.relChangeTol:
+            return False
+        if int(P.robustCostParams.costType) == 0:  # L2
+            return True
+        if self.weight_updates >= P.robustOptNumWeightUpdates:
+            return True
+        return self.converged_weight_ratio() >= P.robustOptMinConvergenceRatio
 
     def run(self, max_rounds: int | None = None, check_every: int = 10) -> int:
         """Rounds until shouldTerminate (checked every `check_every` rounds and
@@ -386,15 +509,15 @@ class RBCDDriver:
         elif c == CommandType.HARD_TERMINATE:
             self.reset()
         elif c == CommandType.RECOVER:
-            self.round_index = int(cmd.executing_iteration)
+            # the leader's iteration number (check_timeout sends rank 0's), so
+            # ranks whose counters drifted resume in step; its robot list is
+            # validated as SET_ACTIVE_ROBOTS's
             if cmd.active_robots:
-                self.active_robots = {int(a) for a in cmd.active_robots}
+                self.active_robots = self._valid_robots(cmd.active_robots, "RECOVER")
+            self.round_index = int(cmd.executing_iteration)
             self.terminated = False
         elif c == CommandType.SET_ACTIVE_ROBOTS:
-            act = {int(a) for a in cmd.active_robots}
-            if not act or not act <= set(range(self.graph.n_robots)):
-                raise ValueError(f"SET_ACTIVE_ROBOTS: robots must be a non-empty subset of the team, got {sorted(act)}")
-            self.active_robots = act
+            self.active_robots = self._valid_robots(cmd.active_robots, "SET_ACTIVE_ROBOTS")
         elif c == CommandType.UPDATE:
             keep = self.active_robots
             if cmd.executing_robot >= 0:
@@ -417,20 +540,27 @@ class RBCDDriver:
                 self.initialize(self._X0)
         return None
 
+    def _valid_robots(self, robots, what: str) -> set:
+        act = {int(a) for a in robots}
+        if not act or not act <= set(range(self.graph.n_robots)):
+            raise ValueError(f"{what}: robots must be a non-empty subset of the team, got {sorted(act)}")
+        return act
+
     def check_timeout(self, now: float | None = None) -> Command | None:
         """The leader's checkTimeout (kmx.dpgo.command.TimeoutMonitor): rank 0
         decides, every rank applies the same HARD_TERMINATE or RECOVER (one
         broadcast when world > 1). Returns the command applied, or None."""
         now = time.monotonic() if now is None else float(now)
         c = self.monitor.check(now, self.state, self.round_index, len(self.active_robots))
-        if self.world > 1:
-            t = self._torch.tensor([-1 if c is None else int(c)], dtype=self._torch.int64,
+        it = self.round_index
+        if self.world > 1:  # the leader's decision and iteration number reach every rank
+            t = self._torch.tensor([-1 if c is None else int(c), it], dtype=self._torch.int64,
                                    device="cuda" if self._xdev == "cuda" else "cpu")
             self._dist.broadcast(t, src=0)
-            v = int(t.item())
+            v, it = (int(x) for x in t.cpu().tolist())
             c = None if v < 0 else CommandType(v)
         if c is None:
             return None
-        cmd = Command(0, c, executing_iteration=self.round_index, active_robots=sorted(self.active_robots))
+        cmd = Command(0, c, executing_iteration=it, active_robots=sorted(self.active_robots))
         self.handle_command(cmd, now)
         return cmd

@@ -68,11 +68,26 @@ class BlockSolver:
         check(abi.lib().kmx_comm_unique_id(C.cast(buf, C.c_void_p), abi.KMX_COMM_ID_BYTES), "kmx_comm_unique_id")
         return buf.raw
 
-    def comm_init(self, unique_id: bytes, world: int, rank: int):
+    def comm_init(self, unique_id: bytes, world: int, rank: int, timeout_s: float = 120.0):
+        """Non-blocking communicator creation with a deadline (a rank whose
+        peers never arrive gets KmxError instead of hanging)."""
         if len(unique_id) != abi.KMX_COMM_ID_BYTES:
             raise ValueError(f"unique id must be {abi.KMX_COMM_ID_BYTES} bytes")
         buf = C.create_string_buffer(bytes(unique_id), abi.KMX_COMM_ID_BYTES)
-        check(self.L.kmx_pgo_comm_init(self.h, C.cast(buf, C.c_void_p), int(world), int(rank)), "kmx_pgo_comm_init")
+        check(self.L.kmx_pgo_comm_init(self.h, C.cast(buf, C.c_void_p), int(world), int(rank), float(timeout_s)),
+              "kmx_pgo_comm_init")
+
+    def comm_destroy(self):
+        """Drop the communicator and the in-round exchange."""
+        check(self.L.kmx_pgo_comm_destroy(self.h), "kmx_pgo_comm_destroy")
+
+    def get_public(self, n_ext: int = 0):
+        """(public table [n_public, r, 4], the last exchange's peer status words)."""
+        n_pub = self.public_count()[0]
+        tab = np.zeros((max(n_pub, 1), self.r, 4))
+        ext = np.zeros(max(n_ext, 1))
+        check(self.L.kmx_pgo_get_public(self.h, fptr(tab), fptr(ext) if n_ext else None), "kmx_pgo_get_public")
+        return tab[:n_pub], ext[:n_ext]
 
     def set_exchange(self, send_slots, send_counts, recv_slots, recv_counts):
         """The per-peer slot lists (kmx.dpgo.driver.exchange_plan); from now on
@@ -177,6 +192,15 @@ class BlockSolver:
 
     def sync(self):
         check(self.L.kmx_pgo_sync(self.h), "kmx_pgo_sync")
+
+    def set_round_form(self, mode: int):
+        """0 launched, 1 persistent where it applies, -1 automatic (kmx_pgo_set_round_form)."""
+        check(self.L.kmx_pgo_set_round_form(self.h, int(mode)), "kmx_pgo_set_round_form")
+
+    def round_form(self) -> dict:
+        p, c, t = C.c_int(), C.c_int(), C.c_int()
+        check(self.L.kmx_pgo_round_form(self.h, C.byref(p), C.byref(c), C.byref(t)), "kmx_pgo_round_form")
+        return {"persistent": bool(p.value), "capacity": c.value, "tiles": t.value}
 
     # ------------------------------------------------------------- GNC ---
     def set_gnc_schedule(self, enabled: bool, inner_iters: int = 20, max_updates: int = 2**31 - 1,

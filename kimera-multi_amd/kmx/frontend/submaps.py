@@ -177,3 +177,29 @@ def measurements_from_pose_graph(g: PoseGraph) -> list[RelativeSEMeasurement]:
         out.append(RelativeSEMeasurement(e.robot_from, e.robot_to, e.key_from, e.key_to, 3, np.asarray(e.R),
                                          np.asarray(e.t), kappa, tau, e.type == ODOM, 1.0))
     return out
+
+
+def graph_data(measurements, n_poses=None):
+    """dpgo measurements (e.g. measurements_from_pose_graph of a
+    request_pose_graph reply) -> the team graph kmx_pgo_set_graph takes
+    (PoseGraphData; pose counts from the largest pose index per robot unless
+    given)."""
+    from ..synth.pose_graph import PoseGraphData
+    ms = list(measurements)
+    if not ms:
+        raise ValueError("no measurements")
+    nr = max(max(m.r1, m.r2) for m in ms) + 1 if n_poses is None else len(n_poses)
+    npose = np.zeros(nr, np.int32)
+    if n_poses is not None:
+        npose[:] = np.asarray(n_poses, np.int32)
+    for m in ms:
+        npose[m.r1] = max(npose[m.r1], m.p1 + 1)
+        npose[m.r2] = max(npose[m.r2], m.p2 + 1)
+    f = lambda key, dt: np.array([getattr(m, key) for m in ms], dtype=dt)
+    return PoseGraphData(
+        n_robots=nr, n_poses=npose, r1=f("r1", np.int32), p1=f("p1", np.int32), r2=f("r2", np.int32),
+        p2=f("p2", np.int32), R=np.array([np.asarray(m.R, np.float64) for m in ms]).reshape(-1, 3, 3),
+        t=np.array([np.asarray(m.t, np.float64) for m in ms]).reshape(-1, 3), kappa=f("kappa", np.float64),
+        tau=f("tau", np.float64), weight=f("weight", np.float64), fixed=f("fixedWeight", np.uint8),
+        outlier=np.zeros(len(ms), bool))
+

@@ -55,6 +55,9 @@ class LcdParams:
     max_intraisland_gap: int = 3
     max_nrFrames_between_islands: int = 3
     max_nrFrames_between_queries: int = 2
+    # stereo pose refinement after an accepted 3D-3D recovery (LcdParams.yaml:14):
+    # least-squares T over the 3D-3D inliers (include/kmx_abi.h refine_pose) [U]
+    refine_pose: int = 1
 
     @classmethod
     def from_yaml(cls, path: str, **overrides) -> "LcdParams":
@@ -110,6 +113,11 @@ class LcdParams:
             raise ValueError("ransac_use_1point_3d3d is 0 (Arun 3-point) or 1 (given rotation)")
         if self.rng_variant not in ("gcc9", "gcc11"):
             raise ValueError(f"rng_variant {self.rng_variant!r}")
+        if self.refine_pose not in (0, 1):
+            raise ValueError(f"refine_pose {self.refine_pose}")
+        if self.refine_pose and self.pose_recovery_type == 1:
+            raise ValueError("refine_pose: 1 with pose_recovery_type 1 (PnP) is not built (refinement follows the "
+                             "3D-3D recovery); set refine_pose 0")
 
     def to_c(self) -> abi.LcdParams:
         self.validate()
@@ -127,6 +135,7 @@ class LcdParams:
         c.rng_variant = abi.KMX_RNG_GCC11 if self.rng_variant == "gcc11" else abi.KMX_RNG_GCC9
         c.use_1point_3d3d = int(self.ransac_use_1point_3d3d)
         c.algorithm_2d2d = int(self.ransac_2d2d_algorithm)
+        c.refine_pose = int(self.refine_pose)
         c.pose_recovery_type = int(self.pose_recovery_type)
         c.min_2d3d_inliers = int(self.min_nr_2d3d_inliers)
         c.ransac_threshold_2d3d = 1.0 - np.cos(np.arctan(float(self.ransac_threshold_2d3d) / float(self.focal_length)))
@@ -148,7 +157,7 @@ _YAML_FIELDS = (
 _MATCHER_NORM = {3: "l1", 4: "hamming", 5: "hamming"}
 # switches of verification stages: yaml key -> (built values, field or None)
 _YAML_SELECTORS = {
-    "refine_pose": ({0}, None),                       # stereo pose refinement (LcdParams.yaml:14)
+    "refine_pose": ({0, 1}, "refine_pose"),           # stereo pose refinement (LcdParams.yaml:14)
     "ransac_use_2point_2d2d": ({0}, None),            # 2-point 2D-2D given rotation (:59)
     "optimize_2d2d_pose_from_inliers": ({0}, None),   # nonlinear refits (:67-69)
     "optimize_3d3d_pose_from_inliers": ({0}, None),

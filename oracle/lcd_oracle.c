@@ -178,7 +178,7 @@ static void sym_eig3(double A[9], double V[9]) {
         const double apq = A[p * 3 + q];
         if (apq == 0.0) continue;
         const double app = A[p * 3 + p], aqq = A[q * 3 + q];
-        /* negligible next to both diagonal entries: zero it (Numerical Recipes' jacobi rule) */
+        /* negligible next to both diagonal entries: zero it (Rutishauser's threshold rule, Handbook for Automatic Computation II/1, 1971) */
         const double g = 100.0 * fabs(apq);
         if (fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq)) {
           A[p * 3 + q] = 0.0;
@@ -624,8 +624,8 @@ int orc_fivept_nister(const double* f1 /*5x3*/, const double* f2 /*5x3*/, double
  *     real part of its E (a complex-conjugate pair gives one real part; it is
  *     taken once, from the member with positive imaginary part).
  * Eigenvalues: Hessenberg reduction by stabilised elimination and the
- * Francis double-shift QR iteration (EISPACK elmhes / hqr, as published in
- * Numerical Recipes 11.5-11.6) on the action matrix; eigenvectors: complex
+ * Francis double-shift QR iteration (EISPACK elmhes / hqr, restated from the
+ * public-domain EISPACK Fortran below) on the action matrix; eigenvectors: complex
  * LU with partial pivoting of (M - lambda I), v9 = 1, back substitution.
  * Eigen's EigenSolver (opengv) reaches the same eigenpairs by a different QR
  * variant: solution ORDER can differ from opengv [U]; E per solution agrees
@@ -658,160 +658,186 @@ static cplx c_div(cplx a, cplx d) { /* Smith's algorithm */
 }
 static double c_abs1(cplx a) { return fabs(a.re) + fabs(a.im); }
 
-/* Reduction to upper Hessenberg form by elimination with pivoting (elmhes);
- * the entries below the subdiagonal are cleared. */
+/* Reduction to upper Hessenberg form by stabilised elementary similarity
+ * transformations: EISPACK ELMHES (B. T. Smith et al., "Matrix Eigensystem
+ * Routines - EISPACK Guide", Springer LNCS 6, 1976; public domain, netlib
+ * eispack/elmhes.f) with low = 1, igh = n, 0-based. For each column mm1 = m-1
+ * the pivot is the first largest |a(j,mm1)|, j >= m; rows and columns m and the
+ * pivot are interchanged; the multipliers y = a(i,mm1)/x are applied to row i
+ * (columns m..n) and column m (rows 1..igh). The multipliers EISPACK leaves
+ * below the subdiagonal are cleared here (hqr never reads them). */
 static void hessenberg10(double a[10][10]) {
-  const int n = 10;
-  for (int m = 1; m < n - 1; ++m) {
+  const int n = 10, la = n - 2;
+  for (int m = 1; m <= la; ++m) {
+    const int mm1 = m - 1;
     double x = 0.0;
-    int i = m;
-    for (int j = m; j < n; ++j)
-      if (fabs(a[j][m - 1]) > fabs(x)) { x = a[j][m - 1]; i = j; }
-    if (i != m) {
-      for (int j = m - 1; j < n; ++j) { const double t = a[i][j]; a[i][j] = a[m][j]; a[m][j] = t; }
-      for (int j = 0; j < n; ++j) { const double t = a[j][i]; a[j][i] = a[j][m]; a[j][m] = t; }
+    int piv = m;
+    for (int j = m; j < n; ++j) {
+      if (fabs(a[j][mm1]) <= fabs(x)) continue;
+      x = a[j][mm1];
+      piv = j;
     }
-    if (x != 0.0) {
-      for (i = m + 1; i < n; ++i) {
-        double y = a[i][m - 1];
-        if (y != 0.0) {
-          y /= x;
-          a[i][m - 1] = y;
-          for (int j = m; j < n; ++j) a[i][j] -= y * a[m][j];
-          for (int j = 0; j < n; ++j) a[j][m] += y * a[j][i];
-        }
-      }
+    if (piv != m) {  /* interchange rows and columns piv, m */
+      for (int j = mm1; j < n; ++j) { const double y = a[piv][j]; a[piv][j] = a[m][j]; a[m][j] = y; }
+      for (int j = 0; j < n; ++j) { const double y = a[j][piv]; a[j][piv] = a[j][m]; a[j][m] = y; }
+    }
+    if (x == 0.0) continue;
+    for (int i = m + 1; i < n; ++i) {
+      double y = a[i][mm1];
+      if (y == 0.0) continue;
+      y = y / x;
+      a[i][mm1] = y;
+      for (int j = m; j < n; ++j) a[i][j] = a[i][j] - y * a[m][j];
+      for (int j = 0; j < n; ++j) a[j][m] = a[j][m] + y * a[j][i];
     }
   }
   for (int i = 2; i < n; ++i)
     for (int j = 0; j < i - 1; ++j) a[i][j] = 0.0;
 }
 
-/* Eigenvalues of an upper Hessenberg matrix by the shifted QR iteration
- * (hqr): wr + i wi, a complex pair stored as (-|wi|, +|wi|) at (nn-1, nn).
- * Returns 0 when an eigenvalue needs more than 30 iterations. */
-static int hqr10(double a[10][10], double wr[10], double wi[10]) {
+/* Eigenvalues of an upper Hessenberg matrix by the double-shift QR method:
+ * EISPACK HQR (same source as elmhes above; netlib eispack/hqr.f) with
+ * low = 1, igh = n, 0-based, its GOTO structure as loops: en is the last row
+ * of the active block, na = en - 1, enm2 = na - 1; l is found by the backward
+ * search for a negligible subdiagonal h(l,l-1) (tst2 == tst1); one root
+ * (l = en) or two (l = na) deflate; otherwise a double-shift QR sweep with
+ * the ad hoc shifts at its = 10 and 20, starting at the row m found by the
+ * two-small-subdiagonals test. A complex pair is stored as EISPACK does,
+ * wi(na) = +zz, wi(en) = -zz. At most 30 n sweeps in all (itn); returns 0 when
+ * they run out (EISPACK ierr = en). */
+static int hqr10(double h[10][10], double wr[10], double wi[10]) {
   const int n = 10;
-  double anorm = 0.0;
-  for (int i = 0; i < n; ++i)
-    for (int j = (i > 0 ? i - 1 : 0); j < n; ++j) anorm += fabs(a[i][j]);
-  int nn = n - 1, l;
-  double t = 0.0, p = 0.0, q = 0.0, r = 0.0, s, w, x, y, z;
-  while (nn >= 0) {
+  double norm = 0.0;
+  for (int i = 0, k = 0; i < n; k = i, ++i)  /* the norm of the Hessenberg part, row by row */
+    for (int j = k; j < n; ++j) norm += fabs(h[i][j]);
+  int en = n - 1, itn = 30 * n;
+  double t = 0.0;
+  while (en >= 0) {  /* label 60: search for the next eigenvalues */
     int its = 0;
-    do {
-      for (l = nn; l >= 1; --l) {
-        s = fabs(a[l - 1][l - 1]) + fabs(a[l][l]);
-        if (s == 0.0) s = anorm;
-        if (fabs(a[l][l - 1]) + s == s) {
-          a[l][l - 1] = 0.0;
-          break;
+    const int na = en - 1, enm2 = na - 1;
+    for (;;) {
+      int l;
+      for (l = en; l > 0; --l) {  /* label 70: single small subdiagonal element */
+        double s = fabs(h[l - 1][l - 1]) + fabs(h[l][l]);
+        if (s == 0.0) s = norm;
+        const double tst1 = s, tst2 = tst1 + fabs(h[l][l - 1]);
+        if (tst2 == tst1) break;
+      }
+      double x = h[en][en];  /* label 100: form shift */
+      if (l == en) {  /* label 270: one root */
+        wr[en] = x + t;
+        wi[en] = 0.0;
+        en = na;
+        break;
+      }
+      double y = h[na][na], w = h[en][na] * h[na][en];
+      if (l == na) {  /* label 280: two roots */
+        const double p = (y - x) / 2.0, q = p * p + w;
+        double zz = sqrt(fabs(q));
+        x = x + t;
+        if (q >= 0.0) {  /* real pair */
+          zz = p + (p >= 0.0 ? fabs(zz) : -fabs(zz));
+          wr[na] = x + zz;
+          wr[en] = wr[na];
+          if (zz != 0.0) wr[en] = x - w / zz;
+          wi[na] = 0.0;
+          wi[en] = 0.0;
+        } else {  /* complex pair */
+          wr[na] = x + p;
+          wr[en] = x + p;
+          wi[na] = zz;
+          wi[en] = -zz;
+        }
+        en = enm2;
+        break;
+      }
+      if (itn == 0) return 0;  /* label 1000 */
+      if (its == 10 || its == 20) {  /* form exceptional shift */
+        t = t + x;
+        for (int i = 0; i <= en; ++i) h[i][i] = h[i][i] - x;
+        const double s = fabs(h[en][na]) + fabs(h[na][enm2]);
+        x = 0.75 * s;
+        y = x;
+        w = -0.4375 * s * s;
+      }
+      ++its;  /* label 130 */
+      --itn;
+      double p = 0.0, q = 0.0, r = 0.0, zz;
+      int m;
+      for (m = enm2; m >= l; --m) {  /* label 140: two consecutive small subdiagonal elements */
+        zz = h[m][m];
+        r = x - zz;
+        double s = y - zz;
+        p = (r * s - w) / h[m + 1][m] + h[m][m + 1];
+        q = h[m + 1][m + 1] - zz - r - s;
+        r = h[m + 2][m + 1];
+        s = fabs(p) + fabs(q) + fabs(r);
+        p = p / s;
+        q = q / s;
+        r = r / s;
+        if (m == l) break;
+        const double tst1 = fabs(p) * (fabs(h[m - 1][m - 1]) + fabs(zz) + fabs(h[m + 1][m + 1]));
+        const double tst2 = tst1 + fabs(h[m][m - 1]) * (fabs(q) + fabs(r));
+        if (tst2 == tst1) break;
+      }
+      for (int i = m + 2; i <= en; ++i) {  /* label 150 */
+        h[i][i - 2] = 0.0;
+        if (i != m + 2) h[i][i - 3] = 0.0;
+      }
+      for (int k = m; k <= na; ++k) {  /* double QR step on rows l..en, columns m..en */
+        const int notlas = k != na;
+        if (k != m) {
+          p = h[k][k - 1];
+          q = h[k + 1][k - 1];
+          r = 0.0;
+          if (notlas) r = h[k + 2][k - 1];
+          x = fabs(p) + fabs(q) + fabs(r);
+          if (x == 0.0) continue;
+          p = p / x;
+          q = q / x;
+          r = r / x;
+        }
+        const double sq = sqrt(p * p + q * q + r * r), s = p >= 0.0 ? sq : -sq;  /* label 170: dsign */
+        if (k == m) {
+          if (l != m) h[k][k - 1] = -h[k][k - 1];  /* label 180 */
+        } else {
+          h[k][k - 1] = -s * x;
+        }
+        p = p + s;  /* label 190 */
+        x = p / s;
+        y = q / s;
+        zz = r / s;
+        q = q / p;
+        r = r / p;
+        if (notlas) {  /* label 225 */
+          for (int j = k; j <= en; ++j) {  /* row modification */
+            p = h[k][j] + q * h[k + 1][j] + r * h[k + 2][j];
+            h[k][j] = h[k][j] - p * x;
+            h[k + 1][j] = h[k + 1][j] - p * y;
+            h[k + 2][j] = h[k + 2][j] - p * zz;
+          }
+          const int jmax = en < k + 3 ? en : k + 3;
+          for (int i = l; i <= jmax; ++i) {  /* column modification */
+            p = x * h[i][k] + y * h[i][k + 1] + zz * h[i][k + 2];
+            h[i][k] = h[i][k] - p;
+            h[i][k + 1] = h[i][k + 1] - p * q;
+            h[i][k + 2] = h[i][k + 2] - p * r;
+          }
+        } else {
+          for (int j = k; j <= en; ++j) {
+            p = h[k][j] + q * h[k + 1][j];
+            h[k][j] = h[k][j] - p * x;
+            h[k + 1][j] = h[k + 1][j] - p * y;
+          }
+          const int jmax = en < k + 3 ? en : k + 3;
+          for (int i = l; i <= jmax; ++i) {
+            p = x * h[i][k] + y * h[i][k + 1];
+            h[i][k] = h[i][k] - p;
+            h[i][k + 1] = h[i][k + 1] - p * q;
+          }
         }
       }
-      x = a[nn][nn];
-      if (l == nn) { /* one root */
-        wr[nn] = x + t;
-        wi[nn] = 0.0;
-        --nn;
-      } else {
-        y = a[nn - 1][nn - 1];
-        w = a[nn][nn - 1] * a[nn - 1][nn];
-        if (l == nn - 1) { /* two roots */
-          p = 0.5 * (y - x);
-          q = p * p + w;
-          z = sqrt(fabs(q));
-          x += t;
-          if (q >= 0.0) {
-            z = p + (p >= 0.0 ? fabs(z) : -fabs(z));
-            wr[nn - 1] = wr[nn] = x + z;
-            if (z != 0.0) wr[nn] = x - w / z;
-            wi[nn - 1] = wi[nn] = 0.0;
-          } else {
-            wr[nn - 1] = wr[nn] = x + p;
-            wi[nn] = z;
-            wi[nn - 1] = -z;
-          }
-          nn -= 2;
-        } else { /* no root yet: a double-shift QR sweep */
-          if (its == 30) return 0;
-          if (its == 10 || its == 20) { /* exceptional shift */
-            t += x;
-            for (int i = 0; i <= nn; ++i) a[i][i] -= x;
-            s = fabs(a[nn][nn - 1]) + fabs(a[nn - 1][nn - 2]);
-            y = x = 0.75 * s;
-            w = -0.4375 * s * s;
-          }
-          ++its;
-          int m;
-          for (m = nn - 2; m >= l; --m) {
-            z = a[m][m];
-            r = x - z;
-            s = y - z;
-            p = (r * s - w) / a[m + 1][m] + a[m][m + 1];
-            q = a[m + 1][m + 1] - z - r - s;
-            r = a[m + 2][m + 1];
-            s = fabs(p) + fabs(q) + fabs(r);
-            p /= s;
-            q /= s;
-            r /= s;
-            if (m == l) break;
-            const double u = fabs(a[m][m - 1]) * (fabs(q) + fabs(r));
-            const double v = fabs(p) * (fabs(a[m - 1][m - 1]) + fabs(z) + fabs(a[m + 1][m + 1]));
-            if (u + v == v) break;
-          }
-          for (int i = m + 2; i <= nn; ++i) {
-            a[i][i - 2] = 0.0;
-            if (i != m + 2) a[i][i - 3] = 0.0;
-          }
-          for (int k = m; k <= nn - 1; ++k) {
-            if (k != m) {
-              p = a[k][k - 1];
-              q = a[k + 1][k - 1];
-              r = 0.0;
-              if (k != nn - 1) r = a[k + 2][k - 1];
-              if ((x = fabs(p) + fabs(q) + fabs(r)) != 0.0) {
-                p /= x;
-                q /= x;
-                r /= x;
-              }
-            }
-            const double sq = sqrt(p * p + q * q + r * r);
-            if ((s = (p >= 0.0 ? sq : -sq)) != 0.0) {
-              if (k == m) {
-                if (l != m) a[k][k - 1] = -a[k][k - 1];
-              } else {
-                a[k][k - 1] = -s * x;
-              }
-              p += s;
-              x = p / s;
-              y = q / s;
-              z = r / s;
-              q /= p;
-              r /= p;
-              for (int j = k; j <= nn; ++j) {
-                p = a[k][j] + q * a[k + 1][j];
-                if (k != nn - 1) {
-                  p += r * a[k + 2][j];
-                  a[k + 2][j] -= p * z;
-                }
-                a[k + 1][j] -= p * y;
-                a[k][j] -= p * x;
-              }
-              const int mmin = nn < k + 3 ? nn : k + 3;
-              for (int i = l; i <= mmin; ++i) {
-                p = x * a[i][k] + y * a[i][k + 1];
-                if (k != nn - 1) {
-                  p += z * a[i][k + 2];
-                  a[i][k + 2] -= p * r;
-                }
-                a[i][k + 1] -= p * q;
-                a[i][k] -= p;
-              }
-            }
-          }
-        }
-      }
-    } while (nn >= 0 && l < nn - 1);
+    }
   }
   return 1;
 }
@@ -1479,6 +1505,56 @@ static void arun_model(const double* Pq, const double* Pm, const int32_t* smp, d
   for (int a = 0; a < 3; ++a) t[a] = cq[a] - (R[a * 3 + 0] * cm[0] + R[a * 3 + 1] * cm[1] + R[a * 3 + 2] * cm[2]);
 }
 
+/* refine_pose: 1 (LcdParams.yaml:14). Kimera-VIO's LoopClosureDetector
+ * refinePoses re-estimates T_query_match after an accepted recovery by a small
+ * GTSAM optimisation over the stereo landmarks of the inlier matches, with the
+ * match pose fixed by a prior [U: Kimera-VIO is not vendored; restated from
+ * its published description]. In this pool's data model a stereo observation
+ * is the 3D point itself; with isotropic unit noise on both frames'
+ * observations the optimal landmark is the midpoint, and the problem reduces
+ * to least squares over the inlier pairs, min_{R,t} sum |p_q - (R p_m + t)|^2:
+ * closed form (centroids over ALL inliers, H = sum (p_m - c_m)(p_q - c_q)^T,
+ * Kabsch R with the reflection fix, t = c_q - R c_m), i.e. arun_model over
+ * the whole inlier set. in[j] selects the inlier pairs of Pq / Pm (j < n). */
+static void refit_3d3d(int n, const double* Pq, const double* Pm, const uint8_t* in, double R[9], double t[3]) {
+  double cq[3] = {0.0, 0.0, 0.0}, cm[3] = {0.0, 0.0, 0.0};
+  int c = 0;
+  for (int j = 0; j < n; ++j) {
+    if (!in[j]) continue;
+    for (int k = 0; k < 3; ++k) {
+      cq[k] += Pq[3 * j + k];
+      cm[k] += Pm[3 * j + k];
+    }
+    ++c;
+  }
+  for (int k = 0; k < 3; ++k) {
+    cq[k] /= (double)c;
+    cm[k] /= (double)c;
+  }
+  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < n; ++j) {
+    if (!in[j]) continue;
+    double dq[3], dm[3];
+    for (int k = 0; k < 3; ++k) {
+      dq[k] = Pq[3 * j + k] - cq[k];
+      dm[k] = Pm[3 * j + k] - cm[k];
+    }
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) H[a * 3 + b] += dm[a] * dq[b];
+  }
+  double U[9], sv[3], V[9];
+  svd3(H, U, sv, V);
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  if (det3(R) < 0.0) {
+    for (int a = 0; a < 3; ++a) V[a * 3 + 2] = -V[a * 3 + 2];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  }
+  for (int a = 0; a < 3; ++a) t[a] = cq[a] - (R[a * 3 + 0] * cm[0] + R[a * 3 + 1] * cm[1] + R[a * 3 + 2] * cm[2]);
+}
+
 static double arun_error(const double R[9], const double t[3], const double pq[3], const double pm[3]) {
   double d[3];
   for (int a = 0; a < 3; ++a) d[a] = pq[a] - (R[a * 3 + 0] * pm[0] + R[a * 3 + 1] * pm[1] + R[a * 3 + 2] * pm[2] + t[a]);
@@ -1642,6 +1718,7 @@ int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int3
         for (int i = 0; i < 3; ++i) res->T_query_match[9 + i] = ta[i];
       }
       res->accepted = (oka && na >= P->min_3d3d_inliers) ? 1 : 0;
+      if (res->accepted && P->refine_pose) refit_3d3d(n2, Aq, Am, in3, res->T_query_match, res->T_query_match + 9);
       free(Aq); free(Am); free(id2);
     } else {
       double t3[3];
@@ -1653,6 +1730,7 @@ int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int3
       for (int i = 0; i < 9; ++i) res->T_query_match[i] = R[i];
       for (int i = 0; i < 3; ++i) res->T_query_match[9 + i] = t3[i];
       res->accepted = (c3 >= P->min_3d3d_inliers) ? 1 : 0;
+      if (res->accepted && P->refine_pose) refit_3d3d(n3, Pq, Pm, in3, res->T_query_match, res->T_query_match + 9);
     }
     free(Pq); free(Pm); free(valid); free(idx); free(in3);
   } else if (ok) {

@@ -97,20 +97,39 @@ def pool_from(d):
                    true_idx=np.zeros((0, 0, 2), np.int32))
 
 
-def lcd_params(case):
+LCD_REFINE_CASES = [     # refine_pose 1 (LcdParams.yaml:14) on the 3D-3D recoveries: lcd_refine.npz
+    (0, "gcc9", "l1", 0), (1, "gcc11", "hamming", 0), (0, "gcc9", "l1", 2),
+]
+
+
+def lcd_params(case, refine=0):
     from kmx.lcd import LcdParams
     algo, variant, norm, rec = case
     return LcdParams(ransac_2d2d_algorithm=algo, rng_variant=variant, norm=norm, pose_recovery_type=int(rec == 1),
-                     ransac_use_1point_3d3d=int(rec != 2))
+                     ransac_use_1point_3d3d=int(rec != 2), refine_pose=refine)
 
 
-def run_lcd_oracle(pool, case):
+def run_lcd_oracle(pool, case, refine=0):
     from oracle import oracle as O
-    res, masks = O.lcd_verify(lcd_params(case).to_c(), pool)
+    res, masks = O.lcd_verify(lcd_params(case, refine).to_c(), pool)
     ints = np.array([[r.n_matches, r.mono_inliers, r.stereo_inliers, r.pnp_inliers, r.accepted, r.iterations_2d2d]
                      for r in res], np.int32)
     T = np.array([list(r.T_query_match[:]) for r in res], np.float64)
     return ints, T, masks
+
+
+def make_refine():
+    """lcd_refine.npz: the refine_pose cases on the same pool (added with the
+    refinement; the earlier fixtures are not regenerated)."""
+    pool = lcd_inputs()
+    arrs = {}
+    for k, case in enumerate(LCD_REFINE_CASES):
+        ints, T, masks = run_lcd_oracle(pool, case, refine=1)
+        arrs[f"ints_{k}"], arrs[f"T_{k}"], arrs[f"masks_{k}"] = ints, T, masks
+    np.savez_compressed(OUT / "lcd_refine.npz",
+                        cases=np.array([[a, v == "gcc11", n == "hamming", r] for a, v, n, r in LCD_REFINE_CASES],
+                                       np.int32), **arrs)
+    print("lcd_refine.npz", (OUT / "lcd_refine.npz").stat().st_size, "bytes")
 
 
 def main():
@@ -133,4 +152,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--refine"]:
+        make_refine()
+    else:
+        main()

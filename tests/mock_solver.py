@@ -91,13 +91,24 @@ class OracleBlockSolver:
                 ext.append(buf[b * ps + k])
         if n:
             self.o.set_nbr_rows(self.pub_robot[sl], self.pub_pose[sl], rows.reshape(n, self.r, 4))
+            self._table()[sl] = rows.reshape(n, self.r, 4)
         self.ext = np.array(ext)
+
+    def _table(self):
+        if getattr(self, "pubtab", None) is None:
+            self.pubtab = np.zeros((self.pub_robot.shape[0], self.r, 4))
+        return self.pubtab
+
+    def get_public(self, n_ext=0):
+        """The neighbour table as installed by refresh_local / exchange_unpack."""
+        return self._table().copy(), np.array(self.ext[:n_ext], dtype=np.float64)
 
     def refresh_local(self):
         self.o.accel_pre(self.local)  # accelerated rounds publish Y
         X = self.o.get_x_rows(self.pub_robot, self.pub_pose)
         own = self.local[self.pub_robot] == 1
         self.o.set_nbr_rows(self.pub_robot[own], self.pub_pose[own], X[own])
+        self._table()[own] = X[own]
 
     # --------------------------------------------------------- rounds ---
     def set_gnc_schedule(self, enabled, inner_iters=20, max_updates=2**31 - 1, rel_change_tol=1e-3):
@@ -171,10 +182,14 @@ class NativeOracleBlockSolver(OracleBlockSolver):
     def comm_unique_id():
         return bytes(range(128))
 
-    def comm_init(self, unique_id, world, rank):
-        assert len(unique_id) == 128
+    def comm_init(self, unique_id, world, rank, timeout_s=120.0):
+        assert len(unique_id) == 128 and timeout_s > 0
         self.world, self.rank, self.xchg = world, rank, None
         self.comm_inits = getattr(self, "comm_inits", 0) + 1
+
+    def comm_destroy(self):
+        self.xchg = None
+        self.comm_destroys = getattr(self, "comm_destroys", 0) + 1
 
     def set_exchange(self, send_slots, send_counts, recv_slots, recv_counts):
         sc, rc = np.asarray(send_counts, np.int64), np.asarray(recv_counts, np.int64)
@@ -188,6 +203,8 @@ class NativeOracleBlockSolver(OracleBlockSolver):
                      [int(c) * ps + 1 for c in sc], [int(c) * ps + 1 for c in rc])
         self.exchanges = 0
 
+    corrupt = False  # a faulty transport for the start-up check's test
+
     def exchange(self):
         import torch
         import torch.distributed as dist
@@ -197,6 +214,8 @@ class NativeOracleBlockSolver(OracleBlockSolver):
         out = torch.zeros(rbuf.shape[0], dtype=torch.float64)
         dist.all_to_all_single(out, torch.from_numpy(sbuf), rsplit, ssplit)
         rbuf[:] = out.numpy()
+        if self.corrupt and rbuf.size:
+            rbuf[0] += 1e-12
         self.exchange_unpack(rs.ctypes.data, nr, rseg.ctypes.data, self.world, rbuf.ctypes.data)
         self.exchanges += 1
 

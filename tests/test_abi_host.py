@@ -48,16 +48,17 @@ def test_params_to_c_and_yaml(tmp_path):
 
 
 def test_reference_lcdparams_yaml_if_present():
-    """The reference config asks for refine_pose: 1 (stereo refinement, not
-    built): loading it raises; with the refinement switched off it maps onto
-    the verification parameters, Stewenius and EPnP included."""
+    """The reference config loads unmodified (refine_pose: 1 included) and
+    maps onto the verification parameters, Stewenius and EPnP included; the
+    refinement with PnP recovery is the one combination not built."""
     f = Path("/root/reference/params/D455/LcdParams.yaml")
     if not f.exists():
         pytest.skip("reference not mounted")
     from kmx.lcd import LcdParams
+    p = LcdParams.from_yaml(str(f))
+    assert p.refine_pose == 1 and p.to_c().refine_pose == 1
     with pytest.raises(ValueError, match="refine_pose"):
-        LcdParams.from_yaml(str(f))
-    p = LcdParams.from_yaml(str(f), refine_pose=0)
+        LcdParams.from_yaml(str(f), pose_recovery_type=1)
     assert (p.lowe_ratio, p.norm, p.ransac_max_iterations, p.ransac_probability) == (0.7, "l1", 500, 0.995)
     assert (p.min_nr_2d2d_inliers, p.min_nr_3d3d_inliers, p.ransac_threshold_2d2d) == (10, 5, 1e-6)
     assert (p.ransac_2d2d_algorithm, p.ransac_2d3d_algorithm, p.pose_recovery_type) == (0, 3, 0)

@@ -183,7 +183,7 @@ def test_exchange_plan_consistent(world):
             assert np.all(rank_of[keys[seg_sent] >> 32] == k)
 
 
-def _native_worker(rank, world, port, rounds, q, fail_rank=-1):
+def _native_worker(rank, world, port, rounds, q, fail_rank=-1, corrupt_rank=-1):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -192,16 +192,18 @@ def _native_worker(rank, world, port, rounds, q, fail_rank=-1):
     g, P = _graph(False), _params(1e-3, False)
     s = NativeOracleBlockSolver(P)
     if rank == fail_rank:  # this rank's communicator cannot be created
-        def fail(*a):
+        def fail(*a, **k):
             raise RuntimeError("no RCCL")
         s.comm_init = fail
+    s.corrupt = rank == corrupt_rank  # this rank's transport delivers a wrong bit
     drv = RBCDDriver(P, g, rank=rank, world=world, solver=s, exchange_device="cuda")
     drv.initialize(_x0(g))
     drv.step(with_stats=True)          # one exchange (the round's own)
     drv.run_async(rounds - 2)          # one solver call for all its rounds
     drv.step(with_stats=True)
     q.put((rank, {a: drv.iterate_of(a) for a in drv.robots}, drv.weight_updates, drv.native,
-           getattr(s, "comm_inits", 0), getattr(s, "exchanges", 0), getattr(s, "async_calls", 0)))
+           getattr(s, "comm_inits", 0), getattr(s, "exchanges", 0), getattr(s, "async_calls", 0),
+           drv.exchange_mode, getattr(s, "comm_destroys", 0)))
     dist.destroy_process_group()
 
 
@@ -224,9 +226,10 @@ def test_native_exchange_branch_matches_single_process():
         p.join(timeout=60)
     g, P = _graph(False), _params(1e-3, False)
     o, sched = reference_rounds(g, P, rounds)
-    for rank, X, wu, native, inits, exchanges, async_calls in res:
-        assert native and inits == 1
-        assert exchanges == rounds and async_calls == 1
+    for rank, X, wu, native, inits, exchanges, async_calls, mode, destroys in res:
+        assert native and inits == 1 and destroys == 0
+        assert exchanges == rounds + 1 and async_calls == 1  # + the first round's start-up check
+        assert "checked bitwise" in mode
         assert wu == sched.updates
         for a, Xa in X.items():
             assert np.array_equal(Xa, o.get_iterate(a)), (rank, a)
@@ -249,7 +252,34 @@ def test_native_exchange_falls_back_together():
         p.join(timeout=60)
     g, P = _graph(False), _params(1e-3, False)
     o, _ = reference_rounds(g, P, rounds)
-    for rank, X, wu, native, inits, exchanges, async_calls in res:
+    for rank, X, wu, native, inits, exchanges, async_calls, mode, destroys in res:
         assert not native and exchanges == 0
+        assert "fallback" in mode and destroys == (1 if rank == 0 else 0)
+        for a, Xa in X.items():
+            assert np.array_equal(Xa, o.get_iterate(a)), (rank, a)
+
+
+@pytest.mark.timeout(300)
+def test_native_exchange_checked_at_first_round():
+    """One rank's in-round transport delivers a wrong bit: the first round's
+    check (native exchange vs the torch.distributed all_to_all, public table
+    and status words compared bitwise) fails there, every rank drops the
+    native exchange together, and the team still matches the single-process
+    run bit for bit."""
+    world, rounds = 2, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_native_worker, args=(r, world, port, rounds, q, -1, 1)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    g, P = _graph(False), _params(1e-3, False)
+    o, _ = reference_rounds(g, P, rounds)
+    for rank, X, wu, native, inits, exchanges, async_calls, mode, destroys in res:
+        assert not native and inits == 1 and destroys == 1 and exchanges == 1
+        assert "differed" in mode
         for a, Xa in X.items():
             assert np.array_equal(Xa, o.get_iterate(a)), (rank, a)

@@ -48,3 +48,30 @@ def test_pose_graph_message_round_trip():
         assert (a.r1, a.p1, a.r2, a.p2, a.fixedWeight) == (b.r1, b.p1, b.r2, b.p2, b.fixedWeight)
         assert abs(a.kappa - b.kappa) < 1e-9 * a.kappa and abs(a.tau - b.tau) < 1e-9 * a.tau
         assert np.array_equal(a.R, b.R) and np.array_equal(a.t, b.t)
+
+
+def test_submap_team_init_and_rounds_on_restatement():
+    """f1 -> f4 -> dpgo on the CPU restatement: the submap graph built from
+    keyframe odometry and keyframe loop closures (through the PoseGraph
+    message), robot 1 aligned to robot 0's frame by robust averaging over the
+    shared submap loop closures (exact odometry: the planted frame change is
+    recovered to rounding, the outlier closures rejected), then RBCD + GNC
+    rounds lower the team cost."""
+    from kmx.dpgo.driver import RBCDDriver
+    from kmx.dpgo.params import PGOAgentParameters
+    from tests.mock_solver import OracleBlockSolver
+    from tests.submap_team import planted_alignment, submap_team
+    g, atlases, sg, X0, align = submap_team(noise_free=True)
+    assert sg.n_robots == 2 and all(1 < at.n_submaps < len(at.kf_submap) for at in atlases)
+    assert int((sg.r1 != sg.r2).sum()) > 20
+    R_WA, t_WA, w = align[1]
+    Rp, tp = planted_alignment(g, 1)
+    assert np.abs(R_WA - Rp).max() < 1e-9 and np.abs(t_WA - tp).max() < 1e-8
+    assert 0 < w.sum() < len(w)  # outlier loop closures rejected
+    P = PGOAgentParameters(r=5)
+    drv = RBCDDriver(P, sg, solver=OracleBlockSolver(P))
+    drv.initialize(X0)
+    st0 = drv.step(with_stats=True)
+    for _ in range(15):
+        st = drv.step(with_stats=True)
+    assert sum(s["f_final"] for s in st) < sum(s["f_init"] for s in st0)

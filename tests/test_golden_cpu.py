@@ -60,3 +60,46 @@ def test_generator_inputs_unchanged():
     l = np.load(GOLD / "lcd_small.npz")
     pool = MG.lcd_inputs()
     assert np.array_equal(pool.desc, l["desc"]) and np.array_equal(pool.bearings, l["bearings"])
+
+
+@pytest.mark.parametrize("k", range(len(MG.LCD_REFINE_CASES)))
+def test_lcd_refine_fixture_reproduced(k):
+    d = np.load(GOLD / "lcd_small.npz")
+    r = np.load(GOLD / "lcd_refine.npz")
+    pool = MG.pool_from(d)
+    case = MG.LCD_REFINE_CASES[k]
+    assert r["cases"][k].tolist() == [case[0], case[1] == "gcc11", case[2] == "hamming", case[3]]
+    ints, T, masks = MG.run_lcd_oracle(pool, case, refine=1)
+    assert np.array_equal(ints, r[f"ints_{k}"])
+    assert np.array_equal(masks, r[f"masks_{k}"])
+    _close(T, r[f"T_{k}"])
+    # the refinement moves only the pose: counts and masks are the unrefined run's
+    k0 = MG.LCD_CASES.index(case)
+    assert np.array_equal(ints, d[f"ints_{k0}"]) and np.array_equal(masks, d[f"masks_{k0}"])
+
+
+def test_refine_pose_delta_on_planted_pool():
+    """The delta refine_pose makes on this pool (measured
+    and documented). Its restated form — least squares over all 3D-3D
+    inliers — fits the rotation to the 0.05 m-noise stereo points, where the
+    unrefined 1-point result keeps the 2D-2D rotation from near-exact bearings
+    and averages the translation: on 20 planted candidates the mean
+    translation error is 0.0149 m unrefined vs 0.0158 m refined, rotation
+    1.11e-3 vs 1.17e-3 (max |dR|). Both stay at the stereo noise level; the
+    refinement's real form (stereo reprojection factors, pixel noise) is not
+    restatable from this data model [U]."""
+    from kmx.synth.lcd import make_lcd_pool
+    from oracle import oracle as O
+    pool = make_lcd_pool(40, 300, seed=11)
+    errs = {}
+    for refine in (0, 1):
+        res, _ = O.lcd_verify(MG.lcd_params((0, "gcc9", "l1", 0), refine).to_c(), pool, masks=False)
+        e = []
+        for c in range(0, len(res), 2):  # planted candidates
+            assert res[c].accepted
+            T = np.array(res[c].T_query_match[:])
+            e.append(np.linalg.norm(T[9:] - pool.t_qm[c // 2]))
+        errs[refine] = np.array(e)
+    assert errs[0].size == errs[1].size == 20
+    assert errs[0].mean() < 0.03 and errs[1].mean() < 0.03
+    assert abs(errs[1].mean() - errs[0].mean()) < 0.005

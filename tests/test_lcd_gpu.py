@@ -40,7 +40,8 @@ def test_verify_bit_exact(gpu, variant, norm, recovery, algo):
     from oracle import oracle as O
     pool = make_lcd_pool(24, 300, seed=3)
     p = LcdParams(rng_variant=variant, norm=norm, pose_recovery_type=int(recovery == 1),
-                  ransac_2d2d_algorithm=algo, ransac_use_1point_3d3d=int(recovery != 2))
+                  ransac_2d2d_algorithm=algo, ransac_use_1point_3d3d=int(recovery != 2),
+                  refine_pose=int(recovery != 1))  # the 3D-3D recoveries with the reference's refinement
     det = LoopClosureDetector(p)
     det.set_pool(pool)
     got, gm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)

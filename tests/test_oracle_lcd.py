@@ -195,7 +195,7 @@ def test_epnp_recovers_camera_pose():
 
 def test_verify_pnp_noise_free_pool():
     pool = make_lcd_pool(12, 200, noise_free=True, seed=4)
-    p = LcdParams(pose_recovery_type=1).to_c()
+    p = LcdParams(pose_recovery_type=1, refine_pose=0).to_c()
     res, masks = O.lcd_verify(p, pool)
     for c in range(len(res)):
         r = res[c]

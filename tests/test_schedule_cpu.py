@@ -120,3 +120,30 @@ def test_team_termination_over_gloo():
                 p.kill()
     assert out[0][0] == out[1][0] == expect
     assert out[0][1] == out[1][1] == tm[expect - 1]
+
+
+def test_gnc_run_does_not_stop_before_gnc_is_done():
+    """Robust cost: the team's relative change can fall below relChangeTol
+    while GNC weight updates are still pending (that convergence is what fires
+    the next update, drawio:2466-2469). run() keeps going until
+    robustOptNumWeightUpdates updates ran, unless robustOptMinConvergenceRatio
+    of the loop-closure weights already sit at 0 / 1."""
+    from kmx.dpgo.driver import RBCDDriver
+    from kmx.dpgo.params import RobustCostType
+    from tests.mock_solver import OracleBlockSolver
+    g, P, X0 = _problem()
+    P.robustCostParams.costType = RobustCostType.GNC_TLS
+    P.relChangeTol = 1e9              # every block update counts as converged
+    P.robustOptInnerIters = 3
+    P.robustOptNumWeightUpdates = 3
+    P.robustOptMinConvergenceRatio = 1.01  # unreachable: only the update count ends GNC
+    drv = RBCDDriver(P, g, solver=OracleBlockSolver(P))
+    drv.initialize(X0)
+    # round 1 (no status yet: no update), rounds 2-4 each fire ("all converged")
+    assert drv.run(max_rounds=50, check_every=1) == 4
+    assert drv.weight_updates == 3
+    P.robustOptMinConvergenceRatio = 0.0  # GNC counts as done at once: the L2 rule
+    drv2 = RBCDDriver(P, g, solver=OracleBlockSolver(P))
+    drv2.initialize(X0)
+    assert drv2.run(max_rounds=50, check_every=1) == 1
+    assert 0.0 <= drv2.converged_weight_ratio() <= 1.0
