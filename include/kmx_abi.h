@@ -248,20 +248,8 @@ int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local);
  * gamma (X - Y)), and every restart_interval rounds V = X, gamma = 0. Between
  * rounds X is the accelerated iterate itself; between the exchange and
  * iterate it holds Y. set_iterate restarts the acceleration (V = X). */
-/* Wait for all work enqueued on the handle's stream (and report a persistent
- * round whose grid barrier gave up, see kmx_pgo_set_round_form). */
+/* Wait for all work enqueued on the handle's stream. */
 int kmx_pgo_sync(kmx_pgo* h);
-/* How a round is executed (results are bit for bit the same either way):
- *   0  launched: one kernel per phase, the host enqueues the tCG steps;
- *   1  persistent where it applies (default, also mode -1): one launch per
- *      round (begin, gradient, tCG steps, trial point, cost, commit between
- *      grid barriers) when every workgroup tile of the handle can be resident
- *      at once, one RTR iteration of the RTR method (the per-GPU shard of a
- *      multi-GPU team). The environment variable KMX_ROUND=0/1 sets it at
- *      creation. round_form reports the form in use, the device's resident
- *      capacity for it and the handle's tile count. */
-int kmx_pgo_set_round_form(kmx_pgo* h, int mode);
-int kmx_pgo_round_form(kmx_pgo* h, int* persistent, int* capacity, int* tiles);
 
 /* GNC: `updateMeasurementWeights()` (drawio:2215) for every non-fixed edge with
  * a local endpoint, evaluated at the current iterate and neighbour table, then

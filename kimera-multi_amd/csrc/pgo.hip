@@ -87,8 +87,7 @@ struct Gnc {
 };
 
 // Field-wise copies of the schedule state (a struct assignment between global
-// pointers is lowered through a scratch temporary, which would give the
-// persistent round a scratch allocation).
+// pointers is lowered through a scratch temporary).
 __device__ __forceinline__ Gnc load_gnc(const Gnc* p) {
   Gnc s;
   s.inner = p->inner; s.updates = p->updates; s.fired = p->fired; s.rounds = p->rounds;
@@ -151,24 +150,9 @@ struct Dev {
   const int2* gnc_ends;       // [n_gnc] endpoints: >= 0 local pose, < 0 public slot -1-x
   int n_gnc;
   int* hv_launch;             // [HV_SLOTS] robots that ran a Hess-vec in timed launch k
-  struct GridBar* bar;        // persistent round: grid-barrier words (k_round)
   Params p;
 };
 
-// Grid barrier of the persistent round kernel (k_round): XCD-grouped arrival
-// counters (group = blockIdx % 8: the blocks the dispatcher deals to one XCD;
-// speed only, never correctness), a top counter and a generation word, each
-// on a 256-B line of its own. Every word is monotonic across launches (no
-// reset per launch: the launch reads the generation at its start), `alive`
-// counts the robots still in tCG, `err` is the bounded spins' give-up word.
-struct GridBar {
-  unsigned cnt[8][64];
-  unsigned top[64];
-  unsigned gen[64];
-  unsigned alive[64];
-  unsigned err[64];
-  unsigned census[64];
-};
 constexpr int HV_SLOTS = 1 << 16;
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -939,19 +923,10 @@ __device__ __forceinline__ void control_core(Ctl& c, const Dev& d, int l, int ki
     if (side && c.phase == PH_IDLE) d.relc[l] = c.rel_change;  // the team status of dpgo's getStatus
   }
 }
-// Out of line in the launched kernels (inlined, it costs the 128-VGPR gather
-// kernels spills); inlined in the persistent round (INL), whose Dev is a local
-// copy that must not have its address taken.
+// Out of line: inlined, it costs the 128-VGPR gather kernels spills.
 __device__ void control_on(Ctl& c, const Dev& d, int l, int kind, const double* tot, int R_, bool side) {
   control_core(c, d, l, kind, tot, R_, side);
 }
-template <bool INL>
-__device__ __forceinline__ void control_sel(Ctl& c, const Dev& d, int l, int kind, const double* tot, int R_,
-                                            bool side) {
-  if constexpr (INL) control_core(c, d, l, kind, tot, R_, side);
-  else control_on(c, d, l, kind, tot, R_, side);
-}
-
 
 // RM_LAUNCH: one workgroup per robot reduces the robot's tile partials in
 // tile order and runs the control logic (after k_update it also reports the
@@ -1249,11 +1224,8 @@ __device__ __forceinline__ void body_grad(const Dev& d, int gated, char* smem) {
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old;
 // partial <delta, Hdelta>.
-// alive (persistent round only): the robot's first tile counts the robots whose
-// tCG continues with this step (the round kernel's exit test).
-template <int R, int RW, int RM, bool INL = false>
-__device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs, unsigned long long seq, char* smem,
-                                          unsigned* alive = nullptr) {
+template <int R, int RW, int RM>
+__device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs, unsigned long long seq, char* smem) {
   const Lane L = lane_map<R>(d);
   int tcg_iter;
   double beta, pcoef;  // pcoef: the previous step's eta coefficient (alpha or tau)
@@ -1305,10 +1277,9 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
       if (upd) u = upd_step(c0.mode, c0.norm_r0, c0.z_r, c0.tcg_iter, tot[0], tot[1], d.p);
       if (grad) u.done = sqrt(tot[1]) < d.p.gn_tol ? 1 : 0;  // control_on's RED_GRAD test
       if (writer && threadIdx.x == 0) {
-        if (upd || grad) control_sel<INL>(cs, d, L.l, grad ? RED_GRAD : RED_UPDATE, tot, R, true);
+        if (upd || grad) control_on(cs, d, L.l, grad ? RED_GRAD : RED_UPDATE, tot, R, true);
         d.ctl2[L.l] = cs;
         if (hs) post_status(hs, L.l, seq, cs.phase == PH_TCG);
-        if (alive && !u.done) __hip_atomic_fetch_add(alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return !u.done;
     };
@@ -1377,7 +1348,7 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
 // tCG step, part 2: r += coef Hdelta (eta += coef delta is deferred to the next
 // k_hess, which reads delta anyway, or to k_retract); interior steps also
 // z = precon(r) and partials <r,r>, <z,r>.
-template <int R, int RM, bool INL = false>
+template <int R, int RM>
 __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsigned long long seq, int slot,
                                             char* smem) {
   const Lane L = lane_map<R>(d);
@@ -1418,7 +1389,7 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
     rs.finish(d.part_h, 2, rl, tot);
     const HessStep hsx = hess_step(cq.z_r, cq.e_Pe, cq.e_Pd, cq.d_Pd, cq.Delta, tot[0]);
     if (writer && threadIdx.x == 0) {  // the state update, on an LDS copy
-      control_sel<INL>(cs, d, L.l, RED_HESS, tot, R, true);
+      control_on(cs, d, L.l, RED_HESS, tot, R, true);
       cout[L.l] = cs;
       if (slot >= 0) atomicAdd(d.hv_launch + slot, 1);
     }
@@ -1562,7 +1533,7 @@ __device__ __forceinline__ void body_cost(const Dev& d, char* smem) {
 // trial point becomes the iterate the next iteration starts from, but the
 // public rows (the neighbours' snapshot of this round) and the round counters
 // wait for the block update's end.
-template <int R, bool INL = false>
+template <int R>
 __device__ __forceinline__ void body_commit(const Dev& d, int fold, int final) {
   const Lane L = lane_map<R>(d);
   if (final && L.tile == 0 && threadIdx.x == 0) {
@@ -1593,7 +1564,7 @@ __device__ __forceinline__ void body_commit(const Dev& d, int fold, int final) {
       commit = rho > d.p.accept_rho;
     }
     if (threadIdx.x == 0 && writer) {
-      control_sel<INL>(cs, d, L.l, RED_COST, tot, R, true);
+      control_on(cs, d, L.l, RED_COST, tot, R, true);
       cs.phase = PH_STEP;
       d.ctl[L.l] = cs;
     }
@@ -1610,8 +1581,7 @@ __device__ __forceinline__ void body_commit(const Dev& d, int fold, int final) {
   if (s >= 0) store4(d.pub + (size_t)s * 4 * R + 4 * L.a, v);
 }
 
-// The launched form: one kernel per phase of the round (the persistent round
-// kernel k_round below runs the same bodies between grid barriers).
+// One kernel per phase of the round.
 template <int R, int RW, int RM>
 __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d, int gated) {
   KMX_SMEM;
@@ -1745,171 +1715,6 @@ __global__ void k_begin(Dev d, const unsigned char* active, int mode, int R_) {
   if (!fire) return;
   for (int i = (blockIdx.x - 1) * blockDim.x + threadIdx.x; i < d.n_gnc; i += (gridDim.x - 1) * blockDim.x)
     gnc_edge<RW>(d, i, R_, mu);
-}
-
-// ------------------------------------------------------ persistent round ---
-// One launch per RBCD round for problems whose tiles fit the GPU at once (the
-// per-GPU shard of a multi-GPU team): the launched form's phase bodies in the
-// same order — begin (+ GNC), gradient, tCG steps (Hess-vec, update), trial
-// point, trial cost, commit — separated by grid barriers instead of kernel
-// boundaries, with one workgroup per tile exactly as the launched form, so
-// every sum is taken in the same order and the results are bit for bit the
-// launched form's (RM_CONSUMER, one RTR iteration; tests/test_round_kernel_gpu.py).
-// The host no longer enqueues or polls tCG steps: after each Hess-vec phase the
-// robots whose tCG continues are counted, and the loop ends once a Hess-vec
-// phase counted none (the launched form's polled exit).
-
-// Hand-off (MI355X_MICROARCH.md "Valid forms", producer / consumer bullets):
-// every wave drains its stores, a workgroup barrier, lane 0 releases at agent
-// scope and arrives; the last arriver of a group releases again and arrives on
-// the top counter, whose last arriver stores the generation; lane 0 polls the
-// generation relaxed (bounded: ~2 s, then the give-up word and a false
-// return), acquires at agent scope, drains, and the workgroup barrier opens.
-constexpr unsigned long long BAR_TIMEOUT_TICKS = 200000000ull;  // 2 s of the 100 MHz wall clock
-__device__ __forceinline__ bool grid_sync(GridBar* b, unsigned target) {
-  __shared__ int ok;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned nb = gridDim.x, g = blockIdx.x & 7u;
-    const unsigned G = nb < 8u ? nb : 8u;
-    const unsigned ng = (nb - g + 7u) / 8u;  // blocks in this group
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // every counter starts at 0 with the graph and every launch of the handle
-    // has the same grid, so barrier number `target` (the generation it opens)
-    // is complete at exactly ng * target group / G * target top arrivals
-    // (mod 2^32 on both sides)
-    const unsigned old = __hip_atomic_fetch_add(&b->cnt[g][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1u == ng * target) {  // the group's last arrival
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned t = __hip_atomic_fetch_add(&b->top[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1u == G * target) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&b->gen[0], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    int good = 1;
-    const unsigned long long t0 = wall_clock64();
-    while ((int)(__hip_atomic_load(&b->gen[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > BAR_TIMEOUT_TICKS) {
-        __hip_atomic_store(&b->err[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        good = 0;
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ok = good;
-  }
-  __syncthreads();
-  return ok != 0;
-}
-
-// The round-begin phase (k_begin with BEGIN_ROUND) spread over the round's
-// workgroups: the GNC decision is taken by every workgroup from the same
-// state; block 0 resets the robots' state and writes the schedule state; all
-// workgroups re-weight the loop closures grid-stride (one edge per thread,
-// order-free).
-template <int RW>
-__device__ __forceinline__ void body_begin(const Dev& d, const unsigned char* active, bool may_fire, int R_) {
-  const bool fire = may_fire && d.p.robust && gnc_should_update(d);
-  if (blockIdx.x == 0) {
-    for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
-    if (threadIdx.x == 0) {
-      Gnc s = load_gnc(d.gnc);
-      s.fired = fire ? 1 : 0;
-      if (fire) {
-        s.inner = 0;
-        s.updates += 1;
-        s.mu = s.mu * d.p.mu_step;
-      }
-      store_gnc(d.gnc_next, s);
-      if (!may_fire) store_gnc(d.gnc, s);  // no reader of the state is left (k_begin's BEGIN_SOLO)
-      if (fire) atomicAdd(&d.cnt->gnc_updates, 1ull);
-    }
-  }
-  if (!fire) return;
-  const double mu = d.gnc->mu;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n_gnc; i += gridDim.x * blockDim.x) gnc_edge<RW>(d, i, R_, mu);
-}
-
-template <int R>
-struct SmemRound {  // the largest phase's dynamic LDS
-  static constexpr int a = SmemHG<R>::bytes > SmemH<R>::bytes ? SmemHG<R>::bytes : SmemH<R>::bytes;
-  static constexpr int b = SmemC<R>::bytes > SmemU::bytes ? SmemC<R>::bytes : SmemU::bytes;
-  static constexpr int bytes = a > b ? a : b;
-};
-
-// 2 waves per SIMD (2 workgroups per CU, 256 VGPRs): with every phase inlined
-// in one loop the register demand exceeds the launched kernels' (3 waves per
-// SIMD spilled 16-25 VGPRs to scratch, and scratch limits how many workgroups
-// stay resident), so the round takes the cut of at most 2 tiles per CU.
-template <int R>
-struct LBR {
-  static constexpr int w = 2;
-};
-template <int R, int RW>
-__global__ __launch_bounds__(BLOCK, LBR<R>::w) void k_round(Dev d, const unsigned char* active, int may_fire,
-                                                           int census) {
-  GridBar* b = d.bar;
-  const int tcg_max = d.p.tcg_max;
-  if (census) {  // residency check of this very kernel and grid (census word zeroed before the launch)
-    if (threadIdx.x == 0) {
-      __hip_atomic_fetch_add(&b->census[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long t0 = wall_clock64();
-      while (__hip_atomic_load(&b->census[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
-        __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > 2000000ull) {  // 20 ms: not every workgroup is resident
-          __hip_atomic_store(&b->err[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    return;
-  }
-  KMX_SMEM;
-  __shared__ unsigned sh_gen, sh_alive[2];
-  if (threadIdx.x == 0) sh_gen = __hip_atomic_load(&b->gen[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  unsigned gen = sh_gen;
-#define KMX_SYNC()                          \
-  do {                                      \
-    if (!grid_sync(b, ++gen)) return;       \
-  } while (0)
-  // the alive count after a barrier (alternating slots: no barrier needed
-  // between one read and the next write of the broadcast word)
-#define KMX_ALIVE(k, out)                                                                              \
-  do {                                                                                                 \
-    if (threadIdx.x == 0) sh_alive[k] = __hip_atomic_load(&b->alive[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
-    __syncthreads();                                                                                   \
-    out = sh_alive[k];                                                                                 \
-  } while (0)
-  body_begin<RW>(d, active, may_fire != 0, R);
-  KMX_SYNC();
-  body_grad<R, RW, RM_CONSUMER>(d, may_fire, smem);
-  KMX_SYNC();
-  unsigned a_prev, a;
-  KMX_ALIVE(0, a_prev);
-  for (int j = 0; j < tcg_max; ++j) {
-    body_hess<R, RW, RM_CONSUMER, true>(d, -1, nullptr, 0ull, smem, &b->alive[0]);
-    KMX_SYNC();
-    KMX_ALIVE((j + 1) & 1, a);  // the robots whose tCG ran this step
-    body_update<R, RM_CONSUMER, true>(d, nullptr, 0ull, -1, smem);
-    KMX_SYNC();
-    if (a == a_prev) break;  // no robot continued: the update only carried the states over
-    a_prev = a;
-  }
-  body_retract<R>(d, 1, smem);
-  KMX_SYNC();
-  body_cost<R, RW, RM_CONSUMER>(d, smem);
-  KMX_SYNC();
-  body_commit<R, true>(d, 1, 1);
-#undef KMX_SYNC
-#undef KMX_ALIVE
 }
 
 // 4x4 diagonal blocks D_i of Q per pose (hD, for the Hessian gather) and the
@@ -2344,13 +2149,6 @@ struct kmx_pgo {
   int* d_hv_launch = nullptr;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
-  // persistent round (k_round): one launch per round when the problem's tiles
-  // all fit the GPU at once; KMX_ROUND=0 keeps the launched form, 1 (default)
-  // uses k_round wherever it applies
-  GridBar* d_bar = nullptr;
-  bool persistent = false;
-  int round_forced = -1;
-  int round_capacity = 0;  // resident workgroups of k_round on this device
   // Nesterov acceleration (P.acceleration): momentum V and this round's Y
   // (allocated only when enabled), gamma and the restart counter on the host
   double *d_accV = nullptr, *d_accY = nullptr;
@@ -2418,7 +2216,7 @@ void free_dev(kmx_pgo* h) {
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
                   h->d_accV, h->d_accY, h->d_ctl2, h->d_part_h,
-                  h->d_part_u, h->d_bar};
+                  h->d_part_u};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
@@ -2442,8 +2240,6 @@ void free_dev(kmx_pgo* h) {
   h->d_accV = h->d_accY = nullptr;
   h->d_ctl2 = nullptr;
   h->d_part_h = h->d_part_u = nullptr;
-  h->d_bar = nullptr;
-  h->persistent = false;
 }
 
 hipEvent_t next_event(kmx_pgo* h) {
@@ -2665,47 +2461,8 @@ void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
   hipLaunchKernelGGL((k_commit<R>), dim3(h->ntiles), dim3(BLOCK), 0, h->stream, h->dv, fold_cost<RM>(h) ? 1 : 0, 1);
 }
 
-// The persistent round: the same phases as enqueue_round_t<R, RW, RM_CONSUMER>
-// in one launch (k_round).
-template <int R, int RW>
-void enqueue_round_persistent(kmx_pgo* h, const unsigned char* d_active) {
-  const int may_fire = h->P.robust_cost == KMX_COST_GNC_TLS && h->gnc_on ? 1 : 0;
-  hipLaunchKernelGGL((k_round<R, RW>), dim3(h->ntiles), dim3(BLOCK), SmemRound<R>::bytes, h->stream, h->dv, d_active,
-                     may_fire, 0);
-}
-
-// Census launch of k_round with the handle's grid: every workgroup arrives
-// and waits (20 ms at most) until all have; true when all were resident.
-template <int R, int RW>
-bool round_census_t(kmx_pgo* h) {
-  if (hipMemsetAsync(h->d_bar, 0, sizeof(GridBar), h->stream) != hipSuccess) return false;
-  hipLaunchKernelGGL((k_round<R, RW>), dim3(h->ntiles), dim3(BLOCK), SmemRound<R>::bytes, h->stream, h->dv,
-                     h->d_active, 0, 1);
-  unsigned err = 1;
-  if (hipGetLastError() != hipSuccess) return false;
-  if (hipMemcpyAsync(&err, &h->d_bar->err[0], sizeof(unsigned), hipMemcpyDeviceToHost, h->stream) != hipSuccess)
-    return false;
-  if (hipStreamSynchronize(h->stream) != hipSuccess) return false;
-  (void)hipMemsetAsync(h->d_bar, 0, sizeof(GridBar), h->stream);
-  (void)hipStreamSynchronize(h->stream);
-  return err == 0;
-}
-
-template <int R, int RW>
-int round_capacity_t(int device) {
-  int nb = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_round<R, RW>, BLOCK, SmemRound<R>::bytes) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
-  return nb * cus;
-}
-
 template <int R>
 void enqueue_round_r(kmx_pgo* h, const unsigned char* d_active) {
-  if (h->persistent) {
-    if (h->rw == 10) enqueue_round_persistent<R, 10>(h, d_active);
-    else enqueue_round_persistent<R, 16>(h, d_active);
-    return;
-  }
   if (h->rm == RM_CONSUMER) {
     if (h->rw == 10) enqueue_round_t<R, 10, RM_CONSUMER>(h, d_active);
     else enqueue_round_t<R, 16, RM_CONSUMER>(h, d_active);
@@ -2726,52 +2483,6 @@ void enqueue_round(kmx_pgo* h, const unsigned char* d_active) {
     case 7: enqueue_round_r<7>(h, d_active); break;
     default: enqueue_round_r<8>(h, d_active); break;
   }
-}
-
-int round_capacity(const kmx_pgo* h) {
-  const bool full = h->rw == 16;
-  switch (h->P.r) {
-#define KMX_CAP(RR) \
-  case RR: return full ? round_capacity_t<RR, 16>(h->device) : round_capacity_t<RR, 10>(h->device);
-    KMX_CAP(3) KMX_CAP(4) KMX_CAP(5) KMX_CAP(6) KMX_CAP(7)
-    default: return full ? round_capacity_t<8, 16>(h->device) : round_capacity_t<8, 10>(h->device);
-#undef KMX_CAP
-  }
-}
-
-bool round_census(kmx_pgo* h) {
-  const bool full = h->rw == 16;
-  switch (h->P.r) {
-#define KMX_CEN(RR) \
-  case RR: return full ? round_census_t<RR, 16>(h) : round_census_t<RR, 10>(h);
-    KMX_CEN(3) KMX_CEN(4) KMX_CEN(5) KMX_CEN(6) KMX_CEN(7)
-    default: return full ? round_census_t<8, 16>(h) : round_census_t<8, 10>(h);
-#undef KMX_CEN
-  }
-}
-
-// k_round applies to the RM_CONSUMER form with one RTR iteration of the RTR
-// method (round_form_possible) when every tile is resident at once: within the
-// occupancy API's capacity, and confirmed by a census launch of the kernel on
-// the handle's grid.
-bool round_form_possible(const kmx_pgo* h) {
-  return h->round_forced != 0 && h->rm == RM_CONSUMER && h->P.rtr_iterations == 1 && h->P.method == KMX_METHOD_RTR;
-}
-void choose_round_form(kmx_pgo* h) {
-  h->round_capacity = round_capacity(h);
-  const bool fits = h->ntiles >= 1 && h->ntiles <= h->round_capacity;
-  h->persistent = round_form_possible(h) && fits && round_census(h);
-}
-
-// A bounded barrier spin of k_round gave up (a workgroup was not resident or
-// the device stalled): report it and re-zero the barrier words.
-int check_round(kmx_pgo* h) {
-  if (!h->persistent || !h->d_bar) return KMX_OK;
-  unsigned err = 0;
-  KMX_HIP(hipMemcpy(&err, &h->d_bar->err[0], sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (!err) return KMX_OK;
-  KMX_HIP(hipMemset(h->d_bar, 0, sizeof(GridBar)));
-  return kmx::fail(KMX_EHIP, "k_round: a grid barrier timed out (results of the last rounds are invalid)");
 }
 
 // Acceleration (oracle orc_pgo_accel_pre / _post): gamma' = (1 + sqrt(1 +
@@ -2863,7 +2574,6 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     h->poll_auto = false;
   }
   if (const char* v = std::getenv("KMX_EARLY")) h->early_forced = std::atoi(v) != 0 ? 1 : 0;
-  if (const char* v = std::getenv("KMX_ROUND")) h->round_forced = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);
     h->rm_forced = m == 0 ? RM_LAUNCH : m == 2 ? RM_CONSUMER : -1;  // 1 and 3 (tickets, half) were removed
@@ -3107,14 +2817,6 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   int64_t inc_all = (int64_t)inc_ptr[nloc] - inc_ptr[0];
   int64_t tilecap = std::min<int64_t>(2 * (int64_t)TP * r,
                                       std::max<int64_t>(180, (inc_all + TILES_TARGET - 1) / TILES_TARGET));
-  // a problem the persistent round can hold (every tile resident) is cut
-  // coarser, to ~90 % of the round kernel's resident capacity (k_round,
-  // kmx.dpgo.driver.team_tile_incidences mirrors this rule)
-  h->round_capacity = round_capacity(h);
-  if (round_form_possible(h) && h->round_capacity > 0) {
-    const int64_t cp = (inc_all * 10 + 9 * (int64_t)h->round_capacity - 1) / (9 * (int64_t)h->round_capacity);
-    if (cp <= 2 * (int64_t)TP * r) tilecap = std::max(tilecap, cp);
-  }
   if (h->P.tile_incidences > 0) tilecap = std::max(16, h->P.tile_incidences);
   if (const char* v = std::getenv("KMX_TILE_CAP")) tilecap = std::max(16, std::atoi(v));
   for (int l = 0; l < L; ++l) {
@@ -3172,8 +2874,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_sh_idx, std::max(h->n_sh_local, 1))) || (rc = dalloc(&h->d_active, L)) ||
       (rc = dalloc(&h->d_osh_edge, std::max(h->n_osh, 1))) || (rc = dalloc(&h->d_osh_idx, std::max(h->n_osh, 1))) ||
       (rc = dalloc(&h->d_relc, L)) || (rc = dalloc(&h->d_gnc, 2)) || (rc = dalloc(&h->d_ext, 64)) ||
-      (rc = dalloc(&h->d_hv_launch, HV_SLOTS)) ||
-      (rc = dalloc(&h->d_bar, 1))) {
+      (rc = dalloc(&h->d_hv_launch, HV_SLOTS))) {
     free_dev(h);
     return rc;
   }
@@ -3197,7 +2898,6 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(hipMemsetAsync(h->d_cnt, 0, sizeof(Counters), h->stream));
   KMX_HIP(hipMemsetAsync(h->d_ext, 0, sizeof(double) * 64, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_hv_launch, 0, sizeof(int) * HV_SLOTS, h->stream));
-  KMX_HIP(hipMemsetAsync(h->d_bar, 0, sizeof(GridBar), h->stream));
   if (L > h->hstat_cap) {  // host-mapped per-robot tCG progress
     if (h->hstat) (void)hipHostFree(h->hstat);
     h->hstat = nullptr;
@@ -3252,10 +2952,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   d.relc = h->d_relc; d.gnc = h->d_gnc; d.gnc_next = h->d_gnc + 1;
   d.gnc_edge = h->d_gnc_edge; d.gnc_ends = h->d_gnc_ends; d.n_gnc = h->n_gnc;
   d.hv_launch = h->d_hv_launch;
-  d.bar = h->d_bar;
   h->n_ext = 0;
   sync_params(h);
-  choose_round_form(h);
   enqueue_precond(h, 0);
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipStreamSynchronize(h->stream));
@@ -3632,7 +3330,6 @@ extern "C" int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats
   std::vector<Ctl> ctl(L);
   KMX_HIP(hipMemcpyAsync(ctl.data(), h->d_ctl, sizeof(Ctl) * L, hipMemcpyDeviceToHost, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  if (int rc = check_round(h)) return rc;
   // restore the all-active mask used by iterate_async
   std::vector<unsigned char> ones(L, 1);
   KMX_HIP(hipMemcpyAsync(h->d_active, ones.data(), L, hipMemcpyHostToDevice, h->stream));
@@ -3681,24 +3378,6 @@ extern "C" int kmx_pgo_sync(kmx_pgo* h) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  return check_round(h);
-}
-
-extern "C" int kmx_pgo_round_form(kmx_pgo* h, int* persistent, int* capacity, int* tiles) {
-  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
-  if (persistent) *persistent = h->persistent ? 1 : 0;
-  if (capacity) *capacity = h->round_capacity;
-  if (tiles) *tiles = h->ntiles;
-  return KMX_OK;
-}
-
-extern "C" int kmx_pgo_set_round_form(kmx_pgo* h, int mode) {
-  KMX_CHECK(h, KMX_EINVAL, "null handle");
-  KMX_CHECK(mode >= -1 && mode <= 1, KMX_EINVAL, "mode is -1 (automatic), 0 (launched) or 1 (persistent where it applies)");
-  KMX_HIP(hipSetDevice(h->device));
-  if (h->stream) KMX_HIP(hipStreamSynchronize(h->stream));
-  h->round_forced = mode == -1 ? -1 : mode;
-  if (ready(h)) choose_round_form(h);
   return KMX_OK;
 }
 

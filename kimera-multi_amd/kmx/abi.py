@@ -158,8 +158,6 @@ def lib() -> C.CDLL:
         "kmx_pgo_iterate": ([P, pu8, C.POINTER(IterStats)], C.c_int),
         "kmx_pgo_iterate_async": ([P, C.c_int, C.c_int], C.c_int),
         "kmx_pgo_sync": ([P], C.c_int),
-        "kmx_pgo_set_round_form": ([P, C.c_int], C.c_int),
-        "kmx_pgo_round_form": ([P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
         "kmx_pgo_update_weights": ([P, pf64], C.c_int),
         "kmx_pgo_get_mu": ([P, pf64], C.c_int),
         "kmx_pgo_set_mu": ([P, f64], C.c_int),

@@ -90,31 +90,16 @@ def exchange_plan(graph, world: int, rank: int):
 
 
 TILES_TARGET = 736  # csrc/pgo.hip: the tile count the cut of small problems aims at
-ROUND_CAPACITY = 512  # csrc/pgo.hip k_round: resident workgroups on an MI355X (2 per CU x 256 CUs)
-CONSUMER_MAX_POSES = 80_000  # csrc/pgo.hip RM_CONSUMER_MAX_POSES
 
 
-def team_tile_incidences(graph, world: int, r: int, params: PGOAgentParameters | None = None) -> int:
+def team_tile_incidences(graph, world: int, r: int) -> int:
     """The tile cut (incidences per workgroup tile) kmx_pgo_set_graph picks
     automatically for a handle holding 1/world of the team's incidences; the
     multi-rank driver passes it to every rank, so all ranks cut their robots
-    alike whatever their share (csrc/pgo.hip set_graph): about TILES_TARGET
-    tiles between 180 incidences and two gather chunks, and — where the
-    persistent round applies (one RTR iteration of RTR, a consumer-form
-    problem, KMX_ROUND not 0) — coarse enough for ~90 % of the round kernel's
-    resident capacity when that stays within two chunks."""
+    alike whatever their share (csrc/pgo.hip set_graph)."""
     tp = 4 * (64 // r)
     inc = 2 * int(graph.m) // max(world, 1)
-    cap = min(2 * tp * r, max(180, -(-inc // TILES_TARGET)))
-    lo = params.localOptimizationParams if params is not None else None
-    persistent = (os.environ.get("KMX_ROUND", "1") != "0"
-                  and (lo is None or (lo.RTR_iterations == 1 and int(lo.method) == 0))
-                  and int(graph.n_total) // max(world, 1) <= CONSUMER_MAX_POSES)
-    if persistent:
-        cp = -(-inc * 10 // (9 * ROUND_CAPACITY))
-        if cp <= 2 * tp * r:
-            cap = max(cap, cp)
-    return cap
+    return min(2 * tp * r, max(180, -(-inc // TILES_TARGET)))
 
 
 class RBCDDriver:
@@ -141,7 +126,7 @@ class RBCDDriver:
         self.local = local
         if solver is None and world > 1 and params.tileIncidences == 0:
             import dataclasses
-            params = dataclasses.replace(params, tileIncidences=team_tile_incidences(graph, world, params.r, params))
+            params = dataclasses.replace(params, tileIncidences=team_tile_incidences(graph, world, params.r))
             self.params = params
         self.solver = solver if solver is not None else BlockSolver(params, device)
         self.executing = ExecutingRobot(params.updateRule, params.randomSeed)

@@ -193,15 +193,6 @@ class BlockSolver:
     def sync(self):
         check(self.L.kmx_pgo_sync(self.h), "kmx_pgo_sync")
 
-    def set_round_form(self, mode: int):
-        """0 launched, 1 persistent where it applies, -1 automatic (kmx_pgo_set_round_form)."""
-        check(self.L.kmx_pgo_set_round_form(self.h, int(mode)), "kmx_pgo_set_round_form")
-
-    def round_form(self) -> dict:
-        p, c, t = C.c_int(), C.c_int(), C.c_int()
-        check(self.L.kmx_pgo_round_form(self.h, C.byref(p), C.byref(c), C.byref(t)), "kmx_pgo_round_form")
-        return {"persistent": bool(p.value), "capacity": c.value, "tiles": t.value}
-
     # ------------------------------------------------------------- GNC ---
     def set_gnc_schedule(self, enabled: bool, inner_iters: int = 20, max_updates: int = 2**31 - 1,
                          rel_change_tol: float = 1e-3):

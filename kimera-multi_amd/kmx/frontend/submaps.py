@@ -92,10 +92,15 @@ class SubmapAtlas:
 
     @staticmethod
     def submap_loop_closure(atlas_a: "SubmapAtlas", kf_a: int, atlas_b: "SubmapAtlas", kf_b: int, R_ab, t_ab,
-                            kappa: float, tau: float) -> RelativeSEMeasurement:
-        """Keyframe loop closure T_ka_kb -> submap edge T_Sa_Sb."""
+                            kappa: float, tau: float) -> RelativeSEMeasurement | None:
+        """Keyframe loop closure T_ka_kb -> submap edge T_Sa_Sb; None when both
+        keyframes lie in the same submap of one robot (a self-loop carries no
+        constraint between submap poses, and kmx_pgo_set_graph rejects it) [U:
+        Kimera-Distributed's own handling is not vendored]."""
         sa, (Ra, ta) = atlas_a.keyframe_in_submap(kf_a)
         sb, (Rb, tb) = atlas_b.keyframe_in_submap(kf_b)
+        if atlas_a.robot == atlas_b.robot and sa == sb:
+            return None
         R, t = _mul(*_mul(Ra, ta, np.asarray(R_ab, np.float64), np.asarray(t_ab, np.float64)), *_inv(Rb, tb))
         return RelativeSEMeasurement(atlas_a.robot, atlas_b.robot, sa, sb, 3, R, t, kappa, tau, False, 1.0)
 

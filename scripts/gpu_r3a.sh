@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 T=${1:-r3a}
 mkdir -p gpurun_out/$T
-timeout -k 10 700 python -u -m pytest tests -x -q --timeout 600 --timeout-method thread -m gpu --deselect tests/test_parity_long_gpu.py --deselect tests/test_round_kernel_gpu.py > gpurun_out/$T/pytest_gpu.log 2>&1 || { echo "gpu suite failed"; tail -30 gpurun_out/$T/pytest_gpu.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests -x -q --timeout 600 --timeout-method thread -m gpu --deselect tests/test_parity_long_gpu.py > gpurun_out/$T/pytest_gpu.log 2>&1 || { echo "gpu suite failed"; tail -30 gpurun_out/$T/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/$T/pytest_gpu.log
 timeout -k 10 400 python -u bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || { echo "bench failed"; tail -20 gpurun_out/$T/bench.err; exit 1; }
 T=$T python - <<'PY'

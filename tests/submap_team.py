@@ -31,8 +31,10 @@ def submap_team(seed=5, n_robots=2, n_kf=1600, m=2600, noise_free=False):
     for at in atlases:
         ms += at.odometry_edges(1e4, 1e2)
     for e in np.nonzero(g.fixed == 0)[0]:
-        ms.append(SubmapAtlas.submap_loop_closure(atlases[g.r1[e]], int(g.p1[e]), atlases[g.r2[e]], int(g.p2[e]),
-                                                  g.R[e], g.t[e], float(g.kappa[e]), float(g.tau[e])))
+        m_ = SubmapAtlas.submap_loop_closure(atlases[g.r1[e]], int(g.p1[e]), atlases[g.r2[e]], int(g.p2[e]),
+                                             g.R[e], g.t[e], float(g.kappa[e]), float(g.tau[e]))
+        if m_ is not None:  # both keyframes in one submap: no submap edge
+            ms.append(m_)
     # what dpgo receives: the request_pose_graph reply (pose_graph_tools message)
     ms = measurements_from_pose_graph(pose_graph_from_measurements(ms))
     sg = graph_data(ms, [at.n_submaps for at in atlases])

@@ -174,13 +174,12 @@ def test_gloo_leader_timeout_decision():
 def test_team_tile_incidences_rule():
     """The cut the multi-rank driver hands every rank (csrc/pgo.hip set_graph's
     automatic rule for 1/world of the team's incidences): about 736 tiles,
-    between 180 incidences and two 240-incidence chunks (r = 5), coarser
-    where the persistent round holds the whole shard."""
+    between 180 incidences and two 240-incidence chunks (r = 5)."""
     from kmx.dpgo.driver import team_tile_incidences
     from kmx.synth import make_pose_graph
     g = make_pose_graph(8, 100_000, 500_000, seed=0)  # 1M incidences
     assert team_tile_incidences(g, 1, 5) == 480       # capped at two chunks
     assert team_tile_incidences(g, 2, 5) == 480
     assert team_tile_incidences(g, 4, 5) == 340       # ceil(250000 / 736)
-    assert team_tile_incidences(g, 8, 5) == 272       # the persistent round: ceil(125000 / (0.9 x 512))
+    assert team_tile_incidences(g, 8, 5) == 180       # not below 180
     assert team_tile_incidences(g, 1, 3) == 2 * 4 * 21 * 3  # r = 3: tiles of 84 poses

@@ -323,20 +323,18 @@ def test_rgd_rounds_match_oracle(gpu, robust):
             assert s.update_weights() == o.update_weights()
 
 
-@pytest.mark.parametrize("red,form", [("0", 0), ("2", 0), ("2", 1)])
+@pytest.mark.parametrize("red", ["0", "2"])
 @pytest.mark.parametrize("case", ["rtr2", "tcg1", "tcg3"])
-def test_round_structure_matches_oracle(gpu, monkeypatch, red, form, case):
-    """Every reduction form (KMX_RED=0: a k_reduce launch per reduction; 2: the
-    consumer form with every reduction folded into the next kernel, launched or
-    as the persistent round k_round where it applies) on round structures the
-    default parameters never produce: two RTR iterations per
+def test_round_structure_matches_oracle(gpu, monkeypatch, red, case):
+    """Both reduction forms (KMX_RED=0: a k_reduce launch per reduction; 2: the
+    consumer form with every reduction folded into the next kernel) on round
+    structures the default parameters never produce: two RTR iterations per
     block update (the trial cost is reduced by a launch and the second
     iteration's gradient folded into its first k_hess), and tCG capped at one /
     three steps (the last update reduced in k_retract). Synchronous rounds
     (kmx_pgo_iterate) and the asynchronous form (kmx_pgo_iterate_async) both
     match the CPU restatement."""
     monkeypatch.setenv("KMX_RED", red)
-    monkeypatch.setenv("KMX_ROUND", str(form))
     g, P, X0 = _setup(robust=True, seed=3)
     lo = P.localOptimizationParams
     if case == "rtr2":
@@ -387,7 +385,6 @@ def test_reduction_forms_agree_bitwise(gpu, monkeypatch):
     either side of the form's size threshold)."""
     g, P, X0 = _setup(robust=True, seed=4)
     out = []
-    monkeypatch.setenv("KMX_ROUND", "0")  # the launched consumer form (k_round: test_round_kernel_gpu.py)
     for red in ("0", "2"):
         monkeypatch.setenv("KMX_RED", red)
         s = BlockSolver(P, 0)
