@@ -31,6 +31,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -948,9 +949,8 @@ struct CoopWS {
       double st_lo[16], st_hi[16];
       int st_vl[16], st_vh[16], st_d[16];
     };
-    struct {                  // Stewenius: action matrix, its Hessenberg form, eigen-solutions
+    struct {                  // Stewenius: action matrix, its eigenvalues, eigen-solutions
       double M[10][10];
-      double H[10][10];
       double wr[10], wi[10];
       double Es[10][9];
     };
@@ -1483,8 +1483,8 @@ __device__ void coop_decompose(CoopWS& w, int lane, bool ok_root, const double E
 // basis [x^2, xy, xz, y^2, yz, z^2, x, y, z, 1] after the graded
 // Gauss-Jordan, EISPACK elmhes + hqr eigenvalues, complex eigenvectors, E from the
 // real part of each solution (conjugate pairs once). The Hessenberg
-// reduction and the QR iteration are the oracle's serial code run by lane 0
-// on the LDS copy (data-dependent deflation); the eigenvector solves are
+// reduction and the QR iteration run on several hypotheses' matrices at once
+// (grp_hessenberg / grp_hqr below); the eigenvector solves are
 // column-per-lane complex LUs with the same per-element operations.
 struct cplx_d {
   double re, im;
@@ -1505,218 +1505,6 @@ __device__ __forceinline__ cplx_d c_div(cplx_d a, cplx_d d) {
   return r;
 }
 __device__ __forceinline__ double c_abs1(cplx_d a) { return fabs(a.re) + fabs(a.im); }
-
-// EISPACK ELMHES (Smith et al., EISPACK Guide, 1976; netlib eispack/elmhes.f;
-// oracle/lcd_oracle.c hessenberg10) on w.H, cooperatively: the pivot search
-// and the multipliers are formed from broadcast LDS reads in the serial order;
-// each row / column update is one lane per element (the serial loop's element
-// operations, same order of the dependent steps).
-__device__ void coop_hessenberg(CoopWS& w, int lane) {
-  double (*a)[10] = w.H;
-  const int n = 10, la = n - 2;
-  for (int m = 1; m <= la; ++m) {
-    const int mm1 = m - 1;
-    double x = 0.0;
-    int piv = m;
-    for (int j = m; j < n; ++j) {
-      const double v = a[j][mm1];
-      if (fabs(v) <= fabs(x)) continue;
-      x = v;
-      piv = j;
-    }
-    wsync();
-    if (piv != m) {  // interchange rows and columns piv, m
-      if (lane >= mm1 && lane < n) { const double y = a[piv][lane]; a[piv][lane] = a[m][lane]; a[m][lane] = y; }
-      wsync();
-      if (lane < n) { const double y = a[lane][piv]; a[lane][piv] = a[lane][m]; a[lane][m] = y; }
-      wsync();
-    }
-    if (x == 0.0) continue;
-    for (int i = m + 1; i < n; ++i) {
-      double y = a[i][mm1];
-      if (y == 0.0) continue;  // uniform
-      y = y / x;
-      wsync();
-      if (lane == 0) a[i][mm1] = y;
-      if (lane >= m && lane < n) a[i][lane] = a[i][lane] - y * a[m][lane];
-      wsync();
-      if (lane < n) a[lane][m] = a[lane][m] + y * a[lane][i];
-      wsync();
-    }
-  }
-  if (lane >= 2 && lane < n)
-    for (int j = 0; j < lane - 1; ++j) a[lane][j] = 0.0;
-  wsync();
-}
-
-// EISPACK HQR (netlib eispack/hqr.f; oracle/lcd_oracle.c hqr10, the same
-// loops and names) on w.H with every lane running the scalar control on
-// broadcast reads: the search for a negligible subdiagonal and the search for
-// the sweep's start row m evaluate all candidates at once (lane per candidate;
-// the serial loop's pick = the highest index whose test holds), the row and
-// column modifications of the double QR step are one lane per column / row.
-// Eigenvalues to w.wr / w.wi (a complex pair: wi(na) = +, wi(en) = -);
-// returns 0 when the 30 n sweeps (itn) run out.
-__device__ int coop_hqr(CoopWS& w, int lane) {
-  double (*h)[10] = w.H;
-  const int n = 10;
-  double norm = 0.0;
-  for (int i = 0, k = 0; i < n; k = i, ++i)
-    for (int j = k; j < n; ++j) norm += fabs(h[i][j]);
-  int en = n - 1, itn = 30 * n;
-  double t = 0.0;
-  while (en >= 0) {
-    int its = 0;
-    const int na = en - 1, enm2 = na - 1;
-    for (;;) {
-      bool hit = false;  // single small subdiagonal element: h(l,l-1), l = en .. 1
-      if (lane >= 1 && lane <= en) {
-        double s = fabs(h[lane - 1][lane - 1]) + fabs(h[lane][lane]);
-        if (s == 0.0) s = norm;
-        const double tst1 = s, tst2 = tst1 + fabs(h[lane][lane - 1]);
-        hit = tst2 == tst1;
-      }
-      const unsigned long long hm = __ballot(hit);
-      const int l = hm ? 63 - __clzll(hm) : 0;
-      double x = h[en][en];
-      if (l == en) {  // one root
-        if (lane == 0) { w.wr[en] = x + t; w.wi[en] = 0.0; }
-        en = na;
-        break;
-      }
-      double y = h[na][na], wv = h[en][na] * h[na][en];
-      if (l == na) {  // two roots
-        const double p = (y - x) / 2.0, q = p * p + wv;
-        double zz = sqrt(fabs(q));
-        x = x + t;
-        if (lane == 0) {
-          if (q >= 0.0) {
-            zz = p + (p >= 0.0 ? fabs(zz) : -fabs(zz));
-            w.wr[na] = x + zz;
-            w.wr[en] = w.wr[na];
-            if (zz != 0.0) w.wr[en] = x - wv / zz;
-            w.wi[na] = 0.0;
-            w.wi[en] = 0.0;
-          } else {
-            w.wr[na] = x + p;
-            w.wr[en] = x + p;
-            w.wi[na] = zz;
-            w.wi[en] = -zz;
-          }
-        }
-        en = enm2;
-        break;
-      }
-      if (itn == 0) return 0;
-      if (its == 10 || its == 20) {  // exceptional shift
-        t = t + x;
-        wsync();
-        if (lane <= en) h[lane][lane] = h[lane][lane] - x;
-        wsync();
-        const double s = fabs(h[en][na]) + fabs(h[na][enm2]);
-        x = 0.75 * s;
-        y = x;
-        wv = -0.4375 * s * s;
-      }
-      ++its;
-      --itn;
-      // the sweep's start: the largest m in [l, enm2] with m == l or two
-      // consecutive small subdiagonal elements (lane per m)
-      bool stop = false;
-      double pm = 0.0, qm = 0.0, rm = 0.0;
-      if (lane >= l && lane <= enm2) {
-        const int m = lane;
-        const double zz = h[m][m];
-        rm = x - zz;
-        double s = y - zz;
-        pm = (rm * s - wv) / h[m + 1][m] + h[m][m + 1];
-        qm = h[m + 1][m + 1] - zz - rm - s;
-        rm = h[m + 2][m + 1];
-        s = fabs(pm) + fabs(qm) + fabs(rm);
-        pm = pm / s;
-        qm = qm / s;
-        rm = rm / s;
-        if (m == l) {
-          stop = true;
-        } else {
-          const double tst1 = fabs(pm) * (fabs(h[m - 1][m - 1]) + fabs(zz) + fabs(h[m + 1][m + 1]));
-          const double tst2 = tst1 + fabs(h[m][m - 1]) * (fabs(qm) + fabs(rm));
-          stop = tst2 == tst1;
-        }
-      }
-      const unsigned long long sm = __ballot(stop);
-      const int m = 63 - __clzll(sm);  // lane l always stops
-      double p = rdlane(pm, m), q = rdlane(qm, m), r = rdlane(rm, m), zz;
-      wsync();
-      if (lane >= m + 2 && lane <= en) {
-        h[lane][lane - 2] = 0.0;
-        if (lane != m + 2) h[lane][lane - 3] = 0.0;
-      }
-      wsync();
-      for (int k = m; k <= na; ++k) {  // double QR step on rows l..en, columns m..en
-        const bool notlas = k != na;
-        if (k != m) {
-          p = h[k][k - 1];
-          q = h[k + 1][k - 1];
-          r = 0.0;
-          if (notlas) r = h[k + 2][k - 1];
-          x = fabs(p) + fabs(q) + fabs(r);
-          if (x == 0.0) continue;  // uniform
-          p = p / x;
-          q = q / x;
-          r = r / x;
-        }
-        const double sq = sqrt(p * p + q * q + r * r), s = p >= 0.0 ? sq : -sq;
-        wsync();
-        if (lane == 0) {
-          if (k == m) {
-            if (l != m) h[k][k - 1] = -h[k][k - 1];
-          } else {
-            h[k][k - 1] = -s * x;
-          }
-        }
-        p = p + s;
-        x = p / s;
-        y = q / s;
-        zz = r / s;
-        q = q / p;
-        r = r / p;
-        if (lane >= k && lane <= en) {  // row modification, column j = lane
-          const int j = lane;
-          if (notlas) {
-            const double pp = h[k][j] + q * h[k + 1][j] + r * h[k + 2][j];
-            h[k][j] = h[k][j] - pp * x;
-            h[k + 1][j] = h[k + 1][j] - pp * y;
-            h[k + 2][j] = h[k + 2][j] - pp * zz;
-          } else {
-            const double pp = h[k][j] + q * h[k + 1][j];
-            h[k][j] = h[k][j] - pp * x;
-            h[k + 1][j] = h[k + 1][j] - pp * y;
-          }
-        }
-        wsync();
-        const int jmax = en < k + 3 ? en : k + 3;
-        if (lane >= l && lane <= jmax) {  // column modification, row i = lane
-          const int i = lane;
-          if (notlas) {
-            const double pp = x * h[i][k] + y * h[i][k + 1] + zz * h[i][k + 2];
-            h[i][k] = h[i][k] - pp;
-            h[i][k + 1] = h[i][k + 1] - pp * q;
-            h[i][k + 2] = h[i][k + 2] - pp * r;
-          } else {
-            const double pp = x * h[i][k] + y * h[i][k + 1];
-            h[i][k] = h[i][k] - pp;
-            h[i][k + 1] = h[i][k + 1] - pp * q;
-          }
-        }
-        wsync();
-      }
-    }
-  }
-  wsync();
-  return 1;
-}
-
 
 // Eigenvectors of w.M, normalised to v9 = 1, for up to 6 eigenvalues at
 // once: lanes 10g..10g+9 solve eigenvalue g of the pass, lane 10g+c holding
@@ -1778,21 +1566,288 @@ __device__ int coop_eigvec6(const CoopWS& w, int lane, cplx_d lam, double xyz[3]
   return ok;
 }
 
-// After coop_gj(graded): w.A = [I | C] in graded order. Essentials -> coop_decompose.
-__device__ void coop_stewenius(CoopWS& w, int lane, bool prof) {
-  unsigned long long t_prev = prof ? wall_clock64() : 0;
-  for (int t = lane; t < 100; t += RS_BLOCK) {
-    const int i = t / 10, j = t % 10;
-    double v = (i < 6) ? -w.A[i][10 + j] : 0.0;
-    if ((i == 6 && j == 0) || (i == 7 && j == 1) || (i == 8 && j == 2) || (i == 9 && j == 6)) v = 1.0;
-    w.M[i][j] = v;
-    w.H[i][j] = v;
+// ------------------------------------- batched Stewenius eigenvalues ---
+// k_ransac_coop<STEW = true> takes a candidate's hypotheses SG at a time in
+// the serial loop's order: the null space, system and Gauss-Jordan of each
+// (cooperative, 64 lanes), then the Hessenberg reduction and the QR iteration
+// of the SG action matrices together, one group of GL lanes per matrix, then
+// the rest of each hypothesis (eigenvectors, decomposition, scoring) one at a
+// time with the serial loop's stopping rule, so hypotheses past the stop are
+// computed but never scored. The eigenvalue stage is a chain of scalar steps
+// (the elimination and QR pivots, ~8 divisions and a square root per QR
+// step) that every lane of the cooperative form repeats; in groups each
+// instruction advances SG matrices (the per-element operations and their
+// order are the serial code's: bit-identical results). Counters behind the
+// choice: profiles/r03/lcd/.
+constexpr int SG = 4, GL = 16;
+static_assert(SG * GL <= RS_BLOCK && GL >= 10, "groups");
+struct StewBatch {
+  double H[SG][10][10];
+  double C6[SG][6][10];  // rows 0-5 of each action matrix
+  double N[SG][4][9];    // each hypothesis's null space
+  double wr[SG][10], wi[SG][10];
+  int ok[SG];            // Gauss-Jordan and QR iteration succeeded
+};
+
+// The highest group-local lane whose pred holds (-1: none).
+__device__ __forceinline__ int grp_top(bool pred, int g) {
+  const unsigned long long b = __ballot(pred);
+  const unsigned long long gm = (b >> (GL * g)) & ((1ull << GL) - 1ull);
+  return gm ? 63 - __clzll(gm) : -1;
+}
+__device__ __forceinline__ double grp_bcast(double v, int g, int src) { return __shfl(v, g * GL + src, 64); }
+
+// EISPACK ELMHES (Smith et al., EISPACK Guide, 1976; netlib eispack/elmhes.f;
+// oracle/lcd_oracle.c hessenberg10) on sb.H[g] for every group g that is `on`:
+// the pivot search and the multipliers are formed by the group's lanes from
+// LDS reads in the serial order; each row / column update is one lane per
+// element (the serial loop's element operations, same order of the dependent
+// steps).
+__device__ void grp_hessenberg(StewBatch& sb, int lane, bool on) {
+  const int g = lane / GL, gl = lane - g * GL;
+  double (*a)[10] = sb.H[g < SG ? g : 0];
+  const int n = 10, la = n - 2;
+  for (int m = 1; m <= la; ++m) {
+    const int mm1 = m - 1;
+    double x = 0.0;
+    int piv = m;
+    for (int j = m; j < n; ++j) {
+      const double v = a[j][mm1];
+      if (fabs(v) <= fabs(x)) continue;
+      x = v;
+      piv = j;
+    }
+    wsync();
+    const bool sw = on && piv != m;
+    if (sw && gl >= mm1 && gl < n) { const double y = a[piv][gl]; a[piv][gl] = a[m][gl]; a[m][gl] = y; }
+    wsync();
+    if (sw && gl < n) { const double y = a[gl][piv]; a[gl][piv] = a[gl][m]; a[gl][m] = y; }
+    wsync();
+    const bool go = on && x != 0.0;
+    for (int i = m + 1; i < n; ++i) {
+      double y = a[i][mm1];
+      const bool gy = go && y != 0.0;
+      if (gy) y = y / x;
+      wsync();
+      if (gy && gl == 0) a[i][mm1] = y;
+      if (gy && gl >= m && gl < n) a[i][gl] = a[i][gl] - y * a[m][gl];
+      wsync();
+      if (gy && gl < n) a[gl][m] = a[gl][m] + y * a[gl][i];
+      wsync();
+    }
   }
+  if (on && gl >= 2 && gl < n)
+    for (int j = 0; j < gl - 1; ++j) a[gl][j] = 0.0;
   wsync();
-  coop_hessenberg(w, lane);
-  KMX_PT(7);
-  const int ok_eig = coop_hqr(w, lane);
-  KMX_PT(8);
+}
+
+// EISPACK HQR (netlib eispack/hqr.f; oracle/lcd_oracle.c hqr10, the same
+// loops and names) per group: each group's state (en, its, itn, t) advances
+// one step per pass — deflation of one or two roots, or one double QR sweep —
+// and the pass repeats while any group is working. The search for a
+// negligible subdiagonal and the search for the sweep's start row m evaluate
+// all candidates at once (lane per candidate; the serial loop's pick = the
+// highest index whose test holds), the row and column modifications of the
+// double QR step are one lane per column / row. Eigenvalues to sb.wr / sb.wi
+// (a complex pair: wi(na) = +, wi(en) = -); sb.ok[g] = 0 when the group's
+// 30 n sweeps ran out.
+__device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
+  const int g = lane / GL, gl = lane - g * GL;
+  double (*h)[10] = sb.H[g < SG ? g : 0];
+  const int n = 10;
+  double norm = 0.0;
+  for (int i = 0, k = 0; i < n; k = i, ++i)
+    for (int j = k; j < n; ++j) norm += fabs(h[i][j]);
+  int en = on ? n - 1 : -1, itn = 30 * n, its = 0;
+  bool fail = false;
+  double t = 0.0;
+  while (__ballot(en >= 0 && !fail)) {
+    const bool act = en >= 0 && !fail;
+    const int na = en - 1, enm2 = na - 1;
+    bool hit = false;  // single small subdiagonal element: h(l,l-1), l = en .. 1
+    if (act && gl >= 1 && gl <= en) {
+      double s = fabs(h[gl - 1][gl - 1]) + fabs(h[gl][gl]);
+      if (s == 0.0) s = norm;
+      const double tst1 = s, tst2 = tst1 + fabs(h[gl][gl - 1]);
+      hit = tst2 == tst1;
+    }
+    int l = grp_top(hit, g);
+    if (l < 0) l = 0;
+    bool sweep = false;
+    double x = 0.0, y = 0.0, wv = 0.0;
+    if (act) {
+      x = h[en][en];
+      if (l == en) {  // one root
+        if (gl == 0) { sb.wr[g][en] = x + t; sb.wi[g][en] = 0.0; }
+        en = na;
+        its = 0;
+      } else {
+        y = h[na][na];
+        wv = h[en][na] * h[na][en];
+        if (l == na) {  // two roots
+          const double p = (y - x) / 2.0, q = p * p + wv;
+          double zz = sqrt(fabs(q));
+          x = x + t;
+          if (gl == 0) {
+            if (q >= 0.0) {
+              zz = p + (p >= 0.0 ? fabs(zz) : -fabs(zz));
+              sb.wr[g][na] = x + zz;
+              sb.wr[g][en] = sb.wr[g][na];
+              if (zz != 0.0) sb.wr[g][en] = x - wv / zz;
+              sb.wi[g][na] = 0.0;
+              sb.wi[g][en] = 0.0;
+            } else {
+              sb.wr[g][na] = x + p;
+              sb.wr[g][en] = x + p;
+              sb.wi[g][na] = zz;
+              sb.wi[g][en] = -zz;
+            }
+          }
+          en = enm2;
+          its = 0;
+        } else if (itn == 0) {
+          fail = true;
+        } else {
+          sweep = true;
+        }
+      }
+    }
+    const bool exc = sweep && (its == 10 || its == 20);  // exceptional shift
+    if (exc) t = t + x;
+    wsync();
+    if (exc && gl <= en) h[gl][gl] = h[gl][gl] - x;
+    wsync();
+    if (exc) {
+      const double s = fabs(h[en][na]) + fabs(h[na][enm2]);
+      x = 0.75 * s;
+      y = x;
+      wv = -0.4375 * s * s;
+    }
+    if (sweep) {
+      ++its;
+      --itn;
+    }
+    // the sweep's start: the largest m in [l, enm2] with m == l or two
+    // consecutive small subdiagonal elements (lane per m)
+    bool stop = false;
+    double pm = 0.0, qm = 0.0, rm = 0.0;
+    if (sweep && gl >= l && gl <= enm2) {
+      const int m = gl;
+      const double zz = h[m][m];
+      rm = x - zz;
+      double s = y - zz;
+      pm = (rm * s - wv) / h[m + 1][m] + h[m][m + 1];
+      qm = h[m + 1][m + 1] - zz - rm - s;
+      rm = h[m + 2][m + 1];
+      s = fabs(pm) + fabs(qm) + fabs(rm);
+      pm = pm / s;
+      qm = qm / s;
+      rm = rm / s;
+      if (m == l) {
+        stop = true;
+      } else {
+        const double tst1 = fabs(pm) * (fabs(h[m - 1][m - 1]) + fabs(zz) + fabs(h[m + 1][m + 1]));
+        const double tst2 = tst1 + fabs(h[m][m - 1]) * (fabs(qm) + fabs(rm));
+        stop = tst2 == tst1;
+      }
+    }
+    int m = grp_top(stop, g);  // lane l always stops
+    if (m < 0) m = 0;
+    double p = grp_bcast(pm, g, m), q = grp_bcast(qm, g, m), r = grp_bcast(rm, g, m), zz = 0.0;
+    wsync();
+    if (sweep && gl >= m + 2 && gl <= en) {
+      h[gl][gl - 2] = 0.0;
+      if (gl != m + 2) h[gl][gl - 3] = 0.0;
+    }
+    wsync();
+    for (int kk = 0; __ballot(sweep && m + kk <= na); ++kk) {  // double QR step on rows l..en, columns m..en
+      const int k = m + kk;
+      bool go = sweep && k <= na;
+      const bool notlas = k != na;
+      if (go && k != m) {
+        p = h[k][k - 1];
+        q = h[k + 1][k - 1];
+        r = 0.0;
+        if (notlas) r = h[k + 2][k - 1];
+        x = fabs(p) + fabs(q) + fabs(r);
+        if (x == 0.0) {
+          go = false;
+        } else {
+          p = p / x;
+          q = q / x;
+          r = r / x;
+        }
+      }
+      double s = 0.0;
+      if (go) {
+        const double sq = sqrt(p * p + q * q + r * r);
+        s = p >= 0.0 ? sq : -sq;
+      }
+      wsync();
+      if (go && gl == 0) {
+        if (k == m) {
+          if (l != m) h[k][k - 1] = -h[k][k - 1];
+        } else {
+          h[k][k - 1] = -s * x;
+        }
+      }
+      if (go) {
+        p = p + s;
+        x = p / s;
+        y = q / s;
+        zz = r / s;
+        q = q / p;
+        r = r / p;
+      }
+      if (go && gl >= k && gl <= en) {  // row modification, column j = gl
+        const int j = gl;
+        if (notlas) {
+          const double pp = h[k][j] + q * h[k + 1][j] + r * h[k + 2][j];
+          h[k][j] = h[k][j] - pp * x;
+          h[k + 1][j] = h[k + 1][j] - pp * y;
+          h[k + 2][j] = h[k + 2][j] - pp * zz;
+        } else {
+          const double pp = h[k][j] + q * h[k + 1][j];
+          h[k][j] = h[k][j] - pp * x;
+          h[k + 1][j] = h[k + 1][j] - pp * y;
+        }
+      }
+      wsync();
+      const int jmax = en < k + 3 ? en : k + 3;
+      if (go && gl >= l && gl <= jmax) {  // column modification, row i = gl
+        const int i = gl;
+        if (notlas) {
+          const double pp = x * h[i][k] + y * h[i][k + 1] + zz * h[i][k + 2];
+          h[i][k] = h[i][k] - pp;
+          h[i][k + 1] = h[i][k + 1] - pp * q;
+          h[i][k + 2] = h[i][k + 2] - pp * r;
+        } else {
+          const double pp = x * h[i][k] + y * h[i][k + 1];
+          h[i][k] = h[i][k] - pp;
+          h[i][k + 1] = h[i][k + 1] - pp * q;
+        }
+      }
+      wsync();
+    }
+  }
+  if (on && fail && gl == 0) sb.ok[g] = 0;
+  wsync();
+}
+
+// Entry (i, j) of the action matrix of x after coop_gj(graded) (w.A = [I | C]
+// in graded order): rows 0-5 are -C, rows 6-9 unit entries (oracle
+// orc_fivept_stewenius).
+__device__ __forceinline__ double action_entry(const double (*C6)[10], int i, int j) {
+  double v = (i < 6) ? C6[i][j] : 0.0;
+  if ((i == 6 && j == 0) || (i == 7 && j == 1) || (i == 8 && j == 2) || (i == 9 && j == 6)) v = 1.0;
+  return v;
+}
+
+// The Stewenius solutions from the action matrix w.M, its eigenvalues w.wr /
+// w.wi (ok_eig = 0: hqr ran out of sweeps, no solution) and the null space
+// w.N: eigenvectors, essentials, then coop_decompose.
+__device__ void stew_tail(CoopWS& w, int lane, int ok_eig, bool prof) {
+  unsigned long long t_prev = prof ? wall_clock64() : 0;
   // solutions in eigenvalue order, a conjugate pair once (wi >= 0)
   unsigned solm = 0;  // bit s: eigenvalue s starts a solution
   if (ok_eig)
@@ -1842,9 +1897,9 @@ __device__ void coop_stewenius(CoopWS& w, int lane, bool prof) {
   KMX_PT(10);
 }
 
-// One hypothesis: sample -> models (w.ok, w.mR, w.mt).
-__device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const double* F2, const short* smp,
-                                int algo, bool prof) {
+// The sample's bearings, the null space and the 10x20 system (both solvers).
+__device__ __forceinline__ void coop_prepare(CoopWS& w, int lane, const double* F1, const double* F2, const short* smp,
+                                             bool prof) {
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   if (lane < 15) {
     const int i = lane / 3, c = lane % 3;
@@ -1857,18 +1912,19 @@ __device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const doubl
   KMX_PT(1);
   coop_system(w, lane);
   KMX_PT(2);
-  const bool stew = algo == KMX_ALGO_STEWENIUS;
-  if (!coop_gj(w, lane, stew)) {
+}
+
+// One Nister hypothesis: sample -> models (w.ok, w.mR, w.mt).
+__device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const double* F2, const short* smp,
+                                                bool prof) {
+  coop_prepare(w, lane, F1, F2, smp, prof);
+  unsigned long long t_prev = prof ? wall_clock64() : 0;
+  if (!coop_gj(w, lane, false)) {
     if (lane == 0) w.ok = 0;
     wsync();
     return;
   }
   KMX_PT(3);
-  if (stew) {
-    coop_stewenius(w, lane, prof);
-    KMX_PT(5);
-    return;
-  }
   coop_roots(w, lane, prof);
   KMX_PT(4);
   if (w.nr == 0) {
@@ -1880,13 +1936,61 @@ __device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const doubl
   KMX_PT(5);
 }
 
-template <int LB>
+// Stewenius: the hypotheses p0 .. p0 + nb - 1 up to their action matrices,
+// stashed in sb (one at a time, 64 lanes), then their eigenvalues together.
+__device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, int lane, const double* F1, const double* F2, const short* tab,
+                           int p0, int nb, bool prof) {
+  for (int b = 0; b < nb; ++b) {
+    coop_prepare(w, lane, F1, F2, tab + (size_t)(p0 + b) * 5, prof);
+    const int okg = coop_gj(w, lane, true);
+    if (okg) {
+      for (int t = lane; t < 100; t += RS_BLOCK) {
+        const int i = t / 10, j = t % 10;
+        if (i < 6) sb.C6[b][i][j] = -w.A[i][10 + j];
+        sb.H[b][i][j] = (i < 6) ? -w.A[i][10 + j] : action_entry(sb.C6[b], i, j);
+      }
+      for (int t = lane; t < 36; t += RS_BLOCK) (&sb.N[b][0][0])[t] = (&w.N[0][0])[t];
+    }
+    if (lane == 0) sb.ok[b] = okg;
+    wsync();
+  }
+  unsigned long long t_prev = prof ? wall_clock64() : 0;
+  const int g = lane / GL;
+  const bool on = g < nb && sb.ok[g];
+  grp_hessenberg(sb, lane, on);
+  KMX_PT(7);
+  grp_hqr(sb, lane, on);
+  KMX_PT(8);
+}
+
+// Hypothesis b of the batch -> model (w.ok, w.mR, w.mt): the sample's
+// bearings (the decomposition's sample error), the action matrix, null space
+// and eigenvalues back into the workspace, then stew_tail.
+__device__ __forceinline__ void stew_model(CoopWS& w, const StewBatch& sb, int lane, const double* F1, const double* F2,
+                           const short* smp, int b, bool prof) {
+  if (lane < 15) {
+    const int i = lane / 3, c = lane % 3;
+    w.f1[lane] = F1[3 * smp[i] + c];
+    w.f2[lane] = F2[3 * smp[i] + c];
+  }
+  for (int t = lane; t < 100; t += RS_BLOCK) w.M[t / 10][t % 10] = action_entry(sb.C6[b], t / 10, t % 10);
+  for (int t = lane; t < 36; t += RS_BLOCK) (&w.N[0][0])[t] = (&sb.N[b][0][0])[t];
+  if (lane < 10) {
+    w.wr[lane] = sb.wr[b][lane];
+    w.wi[lane] = sb.wi[b][lane];
+  }
+  wsync();
+  stew_tail(w, lane, 1, prof);
+}
+
+template <int LB, bool STEW>
 __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bearings, const double* points, int N,
                                                           const int* cq, const int* cm, const int2* pairs,
                                                           const int* Kin, const short* table, RsParams P,
                                                           kmx_lcd_result* res, unsigned char* masks,
                                                           double* fbuf) {
   __shared__ CoopWS w;
+  __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;  // Stewenius: the batch
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
   const int K = Kin[c];
@@ -1921,16 +2025,17 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
   double kk = 1.0;
   const int max_skip = P.max_iter * 10;
   const short* tab = table + (size_t)(K - 5) * P.pmax * 5;
-  for (int p = 0; p < P.pmax; ++p) {
-    if (!(iterations < kk && skipped < max_skip)) break;  // uniform
-    const bool prof = (c < 64) && P.prof;
+  const bool prof = (c < 64) && P.prof;
+  bool done = false;
+  // the serial loop's bookkeeping of one hypothesis's model (w.ok, w.mR, w.mt):
+  // a failed solve counts as skipped; otherwise its inliers, the best model and
+  // the adaptive iteration bound, and the iteration count
+  auto account = [&]() {
     unsigned long long t_prev = prof ? wall_clock64() : 0;
-    coop_hypothesis(w, lane, F1, F2, tab + (size_t)p * 5, P.algo, prof);
-    if (prof && lane == 0) t_prev = wall_clock64();
     if (!w.ok) {
       ++skipped;
       wsync();
-      continue;
+      return;
     }
     double Rm[9], tm[3];
     for (int i = 0; i < 9; ++i) Rm[i] = w.mR[i];
@@ -1957,7 +2062,36 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
     }
     ++iterations;
     wsync();
-    if (iterations > P.max_iter) break;
+    if (iterations > P.max_iter) done = true;
+  };
+  if constexpr (STEW) {
+    // SG hypotheses' eigenvalues at a time, then each hypothesis in order under
+    // the serial loop's tests (a batch may run past the stop: those are never
+    // scored, so the results are the one-at-a-time loop's)
+    for (int p0 = 0; p0 < P.pmax && !done; p0 += SG) {
+      if (!(iterations < kk && skipped < max_skip)) break;  // uniform
+      const int nb = min(SG, P.pmax - p0);
+      stew_batch(w, sb, lane, F1, F2, tab, p0, nb, prof);
+      for (int b = 0; b < nb && !done; ++b) {
+        if (!(iterations < kk && skipped < max_skip)) {
+          done = true;
+          break;
+        }
+        if (!sb.ok[b]) {  // no action matrix or no eigenvalues: the solve failed
+          ++skipped;
+          wsync();
+          continue;
+        }
+        stew_model(w, sb, lane, F1, F2, tab + (size_t)(p0 + b) * 5, b, prof);
+        account();
+      }
+    }
+  } else {
+    for (int p = 0; p < P.pmax && !done; ++p) {
+      if (!(iterations < kk && skipped < max_skip)) break;  // uniform
+      coop_hypothesis(w, lane, F1, F2, tab + (size_t)p * 5, prof);
+      account();
+    }
   }
   if (!have) {
     if (lane == 0) {
@@ -2638,8 +2772,15 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
         const char* v = std::getenv("KMX_COOP_LB");
         return v ? std::atoi(v) : 4;
       }();
-      auto kc = (clb >= 8) ? k_ransac_coop<8> : (clb >= 6) ? k_ransac_coop<6> : (clb >= 5) ? k_ransac_coop<5>
-                                                                                             : k_ransac_coop<4>;
+      const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
+      // Stewenius: the batch's LDS (11.6 KB per wave) admits 13 waves per CU, so
+      // 3 waves per SIMD and their 168 VGPRs (no spills in the eigenvector
+      // solves) unless KMX_COOP_LB asks for more
+      auto kc = stew ? ((clb >= 8) ? k_ransac_coop<8, true> : (clb >= 6) ? k_ransac_coop<6, true>
+                        : (clb >= 5) ? k_ransac_coop<5, true> : (clb == 4 && std::getenv("KMX_COOP_LB"))
+                        ? k_ransac_coop<4, true> : k_ransac_coop<3, true>)
+                     : ((clb >= 8) ? k_ransac_coop<8, false> : (clb >= 6) ? k_ransac_coop<6, false>
+                        : (clb >= 5) ? k_ransac_coop<5, false> : k_ransac_coop<4, false>);
       hipLaunchKernelGGL(kc, dim3(n), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
                          (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
                          (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,

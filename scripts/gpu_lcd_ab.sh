@@ -1,11 +1,15 @@
-# LCD verification throughput, current library vs ab_libs/libkmx_prev.so (per solver)
+# A/B of LCD variants: in-tree build under KMX_COOP_LB settings vs alt/libkmx_old.so
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-T=${1:-lcd_ab}; shift
+T=${1:-lcdab}
 mkdir -p gpurun_out/$T
-for rep in 1 2; do for lib in cur prev; do for a in 0 1; do
-  if [ $lib = prev ]; then export KMX_LIB=ab_libs/libkmx_prev.so; else unset KMX_LIB; fi
-  timeout -k 10 300 python bench.py --steps 2 --warmup 1 --burn-in 0 --no-cpu --no-replay --lcd-algo $a > gpurun_out/$T/$lib$a.json 2> gpurun_out/$T/$lib$a.err || { tail gpurun_out/$T/$lib$a.err; exit 1; }
-  python -c "import json; d=json.load(open('gpurun_out/$T/$lib$a.json'))['lcd']; print('$lib algo $a', round(d['value']), round(d['ms_per_step'],2))" | tee -a gpurun_out/$T/ab.log
-done; done; done
+run() {  # name, env...
+  local name=$1; shift
+  env "$@" timeout -k 10 200 python -u scripts/lcd_timing.py 20000 > gpurun_out/$T/timing_$name.log 2>&1; echo "timing $name rc=$?"; grep verify_async gpurun_out/$T/timing_$name.log | tail -1
+}
+run lb3 KMX_DUMMY=1
+run lb4 KMX_COOP_LB=4
+run lb5 KMX_COOP_LB=5
+run old KMX_LIB=$PWD/alt/libkmx_old.so
+timeout -k 10 120 python -u scripts/lcd_phases.py 0 > gpurun_out/$T/phases_lb3.log 2>&1; echo "phases rc=$?"; cat gpurun_out/$T/phases_lb3.log
