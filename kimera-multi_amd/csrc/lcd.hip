@@ -1579,15 +1579,23 @@ __device__ int coop_eigvec6(const CoopWS& w, int lane, cplx_d lam, double xyz[3]
 // instruction advances SG matrices (the per-element operations and their
 // order are the serial code's: bit-identical results). Counters behind the
 // choice: profiles/r03/lcd/.
-constexpr int SG = 4, GL = 16;
+#ifndef KMX_SG
+#define KMX_SG 6
+#endif
+constexpr int SG = KMX_SG, GL = SG <= 4 ? 16 : 10;
 static_assert(SG * GL <= RS_BLOCK && GL >= 10, "groups");
+// LDS: the matrices the groups work on and their eigenvalues; rows 0-5 of each
+// action matrix and each null space (needed again by the eigenvector and
+// essential-matrix steps) wait in the candidate's global scratch (STASH
+// doubles per candidate after its compact bearings), so the batch costs 5.8
+// KB of LDS per wave at SG = 6
 struct StewBatch {
   double H[SG][10][10];
-  double C6[SG][6][10];  // rows 0-5 of each action matrix
-  double N[SG][4][9];    // each hypothesis's null space
   double wr[SG][10], wi[SG][10];
   int ok[SG];            // Gauss-Jordan and QR iteration succeeded
 };
+constexpr int STASH_H = 96;  // per hypothesis: C6 (rows 0-5 of M, 60) + N (36)
+constexpr int STASH = SG * STASH_H;
 
 // The highest group-local lane whose pred holds (-1: none).
 __device__ __forceinline__ int grp_top(bool pred, int g) {
@@ -1837,8 +1845,8 @@ __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
 // Entry (i, j) of the action matrix of x after coop_gj(graded) (w.A = [I | C]
 // in graded order): rows 0-5 are -C, rows 6-9 unit entries (oracle
 // orc_fivept_stewenius).
-__device__ __forceinline__ double action_entry(const double (*C6)[10], int i, int j) {
-  double v = (i < 6) ? C6[i][j] : 0.0;
+__device__ __forceinline__ double action_entry(const double* C6, int i, int j) {
+  double v = (i < 6) ? C6[i * 10 + j] : 0.0;
   if ((i == 6 && j == 0) || (i == 7 && j == 1) || (i == 8 && j == 2) || (i == 9 && j == 6)) v = 1.0;
   return v;
 }
@@ -1938,22 +1946,25 @@ __device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const doubl
 
 // Stewenius: the hypotheses p0 .. p0 + nb - 1 up to their action matrices,
 // stashed in sb (one at a time, 64 lanes), then their eigenvalues together.
-__device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, int lane, const double* F1, const double* F2, const short* tab,
-                           int p0, int nb, bool prof) {
+__device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* stash, int lane, const double* F1,
+                                           const double* F2, const short* tab, int p0, int nb, bool prof) {
   for (int b = 0; b < nb; ++b) {
     coop_prepare(w, lane, F1, F2, tab + (size_t)(p0 + b) * 5, prof);
     const int okg = coop_gj(w, lane, true);
     if (okg) {
+      double* st = stash + b * STASH_H;
       for (int t = lane; t < 100; t += RS_BLOCK) {
         const int i = t / 10, j = t % 10;
-        if (i < 6) sb.C6[b][i][j] = -w.A[i][10 + j];
-        sb.H[b][i][j] = (i < 6) ? -w.A[i][10 + j] : action_entry(sb.C6[b], i, j);
+        const double v = (i < 6) ? -w.A[i][10 + j] : action_entry(nullptr, i, j);
+        if (i < 6) st[t] = v;
+        sb.H[b][i][j] = v;
       }
-      for (int t = lane; t < 36; t += RS_BLOCK) (&sb.N[b][0][0])[t] = (&w.N[0][0])[t];
+      if (lane < 36) st[60 + lane] = (&w.N[0][0])[lane];
     }
     if (lane == 0) sb.ok[b] = okg;
     wsync();
   }
+  __threadfence_block();  // the stash is read back by this wave (stew_model)
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   const int g = lane / GL;
   const bool on = g < nb && sb.ok[g];
@@ -1966,15 +1977,16 @@ __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, int lane, c
 // Hypothesis b of the batch -> model (w.ok, w.mR, w.mt): the sample's
 // bearings (the decomposition's sample error), the action matrix, null space
 // and eigenvalues back into the workspace, then stew_tail.
-__device__ __forceinline__ void stew_model(CoopWS& w, const StewBatch& sb, int lane, const double* F1, const double* F2,
-                           const short* smp, int b, bool prof) {
+__device__ __forceinline__ void stew_model(CoopWS& w, const StewBatch& sb, const double* stash, int lane,
+                                           const double* F1, const double* F2, const short* smp, int b, bool prof) {
   if (lane < 15) {
     const int i = lane / 3, c = lane % 3;
     w.f1[lane] = F1[3 * smp[i] + c];
     w.f2[lane] = F2[3 * smp[i] + c];
   }
-  for (int t = lane; t < 100; t += RS_BLOCK) w.M[t / 10][t % 10] = action_entry(sb.C6[b], t / 10, t % 10);
-  for (int t = lane; t < 36; t += RS_BLOCK) (&w.N[0][0])[t] = (&sb.N[b][0][0])[t];
+  const double* st = stash + b * STASH_H;
+  for (int t = lane; t < 100; t += RS_BLOCK) w.M[t / 10][t % 10] = action_entry(st, t / 10, t % 10);
+  if (lane < 36) (&w.N[0][0])[lane] = st[60 + lane];
   if (lane < 10) {
     w.wr[lane] = sb.wr[b][lane];
     w.wi[lane] = sb.wi[b][lane];
@@ -2007,7 +2019,8 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
     return;
   }
   // compact bearings of the match pairs (global scratch, L1/L2 resident)
-  double* F1 = fbuf + (size_t)c * 6 * N;
+  double* F1 = fbuf + (size_t)c * (6 * N + STASH);
+  double* stash = F1 + 6 * N;  // Stewenius: the batch's action matrices and null spaces
   double* F2 = F1 + 3 * N;
   const int2* pl = pairs + (size_t)c * N;
   for (int j = lane; j < K; j += RS_BLOCK) {
@@ -2071,7 +2084,7 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
     for (int p0 = 0; p0 < P.pmax && !done; p0 += SG) {
       if (!(iterations < kk && skipped < max_skip)) break;  // uniform
       const int nb = min(SG, P.pmax - p0);
-      stew_batch(w, sb, lane, F1, F2, tab, p0, nb, prof);
+      stew_batch(w, sb, stash, lane, F1, F2, tab, p0, nb, prof);
       for (int b = 0; b < nb && !done; ++b) {
         if (!(iterations < kk && skipped < max_skip)) {
           done = true;
@@ -2082,7 +2095,7 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
           wsync();
           continue;
         }
-        stew_model(w, sb, lane, F1, F2, tab + (size_t)(p0 + b) * 5, b, prof);
+        stew_model(w, sb, stash, lane, F1, F2, tab + (size_t)(p0 + b) * 5, b, prof);
         account();
       }
     }
@@ -2661,7 +2674,7 @@ struct kmx_lcd {
   int2* d_pairs = nullptr;
   kmx_lcd_result* d_res = nullptr;
   unsigned char* d_mask = nullptr;
-  double* d_fbuf = nullptr;  // [cap][2][N][3] compact match bearings (k_ransac_coop)
+  double* d_fbuf = nullptr;  // [cap][6 N + STASH] compact match bearings + Stewenius stash (k_ransac_coop)
   int ransac = 1;            // KMX_RANSAC: 1 cooperative (default), 0 lane-per-hypothesis
   int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
   // kmx_lcd_enable_timing: events around the kNN2 and the RANSAC launches
@@ -2724,7 +2737,7 @@ int ensure_cap(kmx_lcd* h, int n) {
       hipMalloc(&h->d_pairs, sizeof(int2) * (size_t)cap * h->N) != hipSuccess ||
       hipMalloc(&h->d_res, sizeof(kmx_lcd_result) * cap) != hipSuccess ||
       hipMalloc(&h->d_mask, (size_t)cap * h->N) != hipSuccess ||
-      hipMalloc(&h->d_fbuf, sizeof(double) * 6 * (size_t)cap * h->N) != hipSuccess) {
+      hipMalloc(&h->d_fbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * cap) != hipSuccess) {
     lcd_free_cand(h);
     return kmx::fail(KMX_ENOMEM, "candidate buffers");
   }
