@@ -949,11 +949,6 @@ struct CoopWS {
       double st_lo[16], st_hi[16];
       int st_vl[16], st_vh[16], st_d[16];
     };
-    struct {                  // Stewenius: action matrix, its eigenvalues, eigen-solutions
-      double M[10][10];
-      double wr[10], wi[10];
-      double Es[10][9];
-    };
   };
   union {
     struct {                  // system + elimination
@@ -1506,18 +1501,19 @@ __device__ __forceinline__ cplx_d c_div(cplx_d a, cplx_d d) {
 }
 __device__ __forceinline__ double c_abs1(cplx_d a) { return fabs(a.re) + fabs(a.im); }
 
-// Eigenvectors of w.M, normalised to v9 = 1, for up to 6 eigenvalues at
-// once: lanes 10g..10g+9 solve eigenvalue g of the pass, lane 10g+c holding
-// column c of M - lam I (eigvec10's LU with partial pivoting, per element
-// the same operations; the column broadcasts are group shuffles). Returns
-// this group's (v6, v7, v8) real parts; ok = 0 on a zero pivot.
+// Eigenvectors normalised to v9 = 1 for up to 6 eigenvalues at once: lanes
+// 10g..10g+9 solve the eigenvalue of group g, lane 10g+c holding column c of
+// M - lam I (mcol = column c of its group's M; eigvec10's LU with partial
+// pivoting, per element the same operations; the column broadcasts are group
+// shuffles). Returns this group's (v6, v7, v8) real parts; ok = 0 on a zero
+// pivot.
 __device__ __forceinline__ cplx_d shfl_c(cplx_d v, int src) { return {__shfl(v.re, src, 64), __shfl(v.im, src, 64)}; }
-__device__ int coop_eigvec6(const CoopWS& w, int lane, cplx_d lam, double xyz[3]) {
+__device__ __forceinline__ int eigvec_col(const double mcol[10], int lane, cplx_d lam, double xyz[3]) {
   const int g0 = (lane / 10) * 10, c = lane - g0 < 10 ? lane - g0 : 9;
   cplx_d b[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    b[i].re = w.M[i][c];
+    b[i].re = mcol[i];
     b[i].im = 0.0;
   }
 #pragma unroll
@@ -1589,13 +1585,18 @@ static_assert(SG * GL <= RS_BLOCK && GL >= 10, "groups");
 // essential-matrix steps) wait in the candidate's global scratch (STASH
 // doubles per candidate after its compact bearings), so the batch costs 5.8
 // KB of LDS per wave at SG = 6
+constexpr int MAXP = SG * 10;  // solutions of one batch
 struct StewBatch {
   double H[SG][10][10];
   double wr[SG][10], wi[SG][10];
-  int ok[SG];            // Gauss-Jordan and QR iteration succeeded
+  double mR[SG][9], mt[SG][3];  // each hypothesis's model
+  double f1[SG][15], f2[SG][15];  // each hypothesis's sample bearings
+  int ok[SG];                   // Gauss-Jordan and QR iteration succeeded
+  int mok[SG];                  // a model was found
+  unsigned char pb[MAXP], ps[MAXP];  // the batch's solutions: hypothesis, eigenvalue
 };
 constexpr int STASH_H = 96;  // per hypothesis: C6 (rows 0-5 of M, 60) + N (36)
-constexpr int STASH = SG * STASH_H;
+constexpr int STASH = SG * STASH_H + MAXP * 9;  // + the batch's essentials
 
 // The highest group-local lane whose pred holds (-1: none).
 __device__ __forceinline__ int grp_top(bool pred, int g) {
@@ -1851,29 +1852,47 @@ __device__ __forceinline__ double action_entry(const double* C6, int i, int j) {
   return v;
 }
 
-// The Stewenius solutions from the action matrix w.M, its eigenvalues w.wr /
-// w.wi (ok_eig = 0: hqr ran out of sweeps, no solution) and the null space
-// w.N: eigenvectors, essentials, then coop_decompose.
-__device__ void stew_tail(CoopWS& w, int lane, int ok_eig, bool prof) {
+// The models of a batch after grp_hqr (orc_fivept_stewenius + model_from_sample
+// for each hypothesis b < nb, all at once): the solutions of every hypothesis
+// whose eigenvalues exist (eigenvalue order, a conjugate pair once) are listed
+// in (b, solution) order; their eigenvectors six at a time (eigvec_col, the
+// column of the hypothesis's action matrix rebuilt from the stash) and
+// essentials (stash, STASH_E); then one lane per essential decomposes it and
+// scores its 4 (R, t) candidates on its hypothesis's sample in candidate
+// order; each hypothesis takes the first minimum in (essential, candidate)
+// order, as coop_decompose does for one. sb.mok[b] = 0: no model.
+__device__ __forceinline__ void stew_models(StewBatch& sb, double* stash, int lane, const double* F1, const double* F2,
+                                            const short* tab, int p0, int nb, bool prof) {
   unsigned long long t_prev = prof ? wall_clock64() : 0;
-  // solutions in eigenvalue order, a conjugate pair once (wi >= 0)
-  unsigned solm = 0;  // bit s: eigenvalue s starts a solution
-  if (ok_eig)
-    for (int s = 0; s < 10; ++s)
-      if (!(w.wi[s] < 0.0)) solm |= 1u << s;
-  const int ns = __popc(solm);
-  unsigned okm = 0;  // bit s: solution s gave an essential (Es[s])
-  for (int b0 = 0; b0 < ns; b0 += 6) {
-    const int g = lane / 10, sidx = b0 + g;
-    const bool act = g < 6 && sidx < ns;
-    unsigned mm = solm;  // eigenvalue of solution sidx: the sidx-th set bit
-    for (int k = 0; k < sidx && k < 10; ++k) mm &= mm - 1;
-    const int si = act ? __ffs(mm) - 1 : 0;
+  int np;
+  {  // solution list
+    const int b = lane / 10, s = lane - 10 * b;
+    const bool sol = lane < 10 * nb && sb.ok[b < SG ? b : 0] && !(sb.wi[b < SG ? b : 0][s] < 0.0);
+    const unsigned long long m = __ballot(sol);
+    if (sol) {
+      const int k = __popcll(m & ((1ull << lane) - 1ull));
+      sb.pb[k] = (unsigned char)b;
+      sb.ps[k] = (unsigned char)s;
+    }
+    np = __popcll(m);
+  }
+  wsync();
+  double* Es = stash + SG * STASH_H;
+  unsigned long long pok = 0;  // bit k: solution k gave an essential
+  for (int q0 = 0; q0 < np; q0 += 6) {
+    const int g = lane / 10, g0 = g * 10, c = lane - g0, pi = q0 + g;
+    const bool act = g < 6 && pi < np;
+    const int b = act ? sb.pb[pi] : 0, si = act ? sb.ps[pi] : 0;
+    const double* st = stash + b * STASH_H;
+    const int cc = c < 10 ? c : 9;
+    double mcol[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) mcol[i] = action_entry(st, i, cc);
     double xyz[3] = {0.0, 0.0, 0.0};
-    const int okv = coop_eigvec6(w, lane, cplx_d{act ? w.wr[si] : 0.0, act ? w.wi[si] : 0.0}, xyz);
+    const int okv = eigvec_col(mcol, lane, cplx_d{act ? sb.wr[b][si] : 0.0, act ? sb.wi[b][si] : 0.0}, xyz);
     // lane 10g + e (e < 9): entry e of E; the norm over the group's 9 entries in order
-    const int g0 = g * 10, c = lane - g0;
-    const double e = (c < 9) ? xyz[0] * w.N[0][c] + xyz[1] * w.N[1][c] + xyz[2] * w.N[2][c] + w.N[3][c] : 0.0;
+    const double* Nb = st + 60;
+    const double e = (c < 9) ? xyz[0] * Nb[c] + xyz[1] * Nb[9 + c] + xyz[2] * Nb[18 + c] + Nb[27 + c] : 0.0;
     double nn = 0.0;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
@@ -1882,26 +1901,68 @@ __device__ void stew_tail(CoopWS& w, int lane, int ok_eig, bool prof) {
     }
     nn = sqrt(nn);
     const bool good = act && okv && nn > 0.0 && isfinite(nn);
-    if (good && c < 9) w.Es[sidx][c] = e / nn;
+    if (good && c < 9) Es[pi * 9 + c] = e / nn;
     const unsigned long long gm = __ballot(good && c == 0);
 #pragma unroll
     for (int gg = 0; gg < 6; ++gg)
-      if ((gm >> (10 * gg)) & 1ull) okm |= 1u << (b0 + gg);
+      if ((gm >> (10 * gg)) & 1ull) pok |= 1ull << (q0 + gg);
   }
+  __threadfence_block();  // Es is read back by other lanes of this wave
   wsync();
   KMX_PT(9);
-  // compact in solution order (orc_fivept_stewenius's ns counter)
-  const int ne = __popc(okm);
-  double Eo[9];
-  const bool ok = lane < ne;
-  if (ok) {
-    unsigned mm = okm;
-    for (int k = 0; k < lane; ++k) mm &= mm - 1;
-    const int src = __ffs(mm) - 1;
-    for (int i = 0; i < 9; ++i) Eo[i] = w.Es[src][i];
+  // lane per essential: decomposition and its best candidate on the sample
+  const bool eact = lane < np && ((pok >> lane) & 1ull);
+  const int eb = eact ? sb.pb[lane] : 0;
+  bool valid = false;
+  double best = DBL_MAX, bR[9], bt[3];
+  if (eact) {
+    double Eo[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Eo[i] = Es[lane * 9 + i];
+    double U[9], sv[3], V[9];
+    svd3(Eo, U, sv, V);
+    double Ra[9], Rb[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        const double uw0 = U[i * 3 + 1], uw1 = -U[i * 3 + 0], uw2 = U[i * 3 + 2];
+        Ra[i * 3 + j] = uw0 * V[j * 3 + 0] + uw1 * V[j * 3 + 1] + uw2 * V[j * 3 + 2];
+        const double uv0 = -U[i * 3 + 1], uv1 = U[i * 3 + 0], uv2 = U[i * 3 + 2];
+        Rb[i * 3 + j] = uv0 * V[j * 3 + 0] + uv1 * V[j * 3 + 1] + uv2 * V[j * 3 + 2];
+      }
+    const bool na = det3(Ra) < 0.0, nbn = det3(Rb) < 0.0;
+    for (int i = 0; i < 9; ++i) {
+      Ra[i] = na ? -Ra[i] : Ra[i];
+      Rb[i] = nbn ? -Rb[i] : Rb[i];
+    }
+    const double* f1 = sb.f1[eb];
+    const double* f2 = sb.f2[eb];
+    for (int cand = 0; cand < 4; ++cand) {
+      double R[9], t[3];
+      for (int i = 0; i < 9; ++i) R[i] = (cand >> 1) ? Rb[i] : Ra[i];
+      const double sg = (cand & 1) ? -1.0 : 1.0;
+      for (int i = 0; i < 3; ++i) t[i] = sg * U[i * 3 + 2];
+      double err = 0.0;
+      for (int i = 0; i < 5; ++i) err += model_error(R, t, f1 + 3 * i, f2 + 3 * i);
+      if (err < DBL_MAX && (!valid || err < best)) {
+        valid = true;
+        best = err;
+        for (int i = 0; i < 9; ++i) bR[i] = R[i];
+        for (int i = 0; i < 3; ++i) bt[i] = t[i];
+      }
+    }
+  }
+  for (int b = 0; b < nb; ++b) {  // each hypothesis: the first minimum over its essentials
+    const bool inb = valid && eb == b;
+    double mn = inb ? best : DBL_MAX;
+    for (int off = 32; off > 0; off >>= 1) mn = fmin(mn, __shfl_xor(mn, off, 64));
+    const unsigned long long wm = __ballot(inb && best == mn);
+    if (lane == 0) sb.mok[b] = wm ? 1 : 0;
+    if (wm && lane == __ffsll((long long)wm) - 1) {
+      for (int i = 0; i < 9; ++i) sb.mR[b][i] = bR[i];
+      for (int i = 0; i < 3; ++i) sb.mt[b][i] = bt[i];
+    }
   }
   wsync();
-  coop_decompose(w, lane, ok, Eo);
   KMX_PT(10);
 }
 
@@ -1961,10 +2022,14 @@ __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* sta
       }
       if (lane < 36) st[60 + lane] = (&w.N[0][0])[lane];
     }
+    if (lane < 15) {
+      sb.f1[b][lane] = w.f1[lane];
+      sb.f2[b][lane] = w.f2[lane];
+    }
     if (lane == 0) sb.ok[b] = okg;
     wsync();
   }
-  __threadfence_block();  // the stash is read back by this wave (stew_model)
+  __threadfence_block();  // the stash is read back by this wave (stew_models)
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   const int g = lane / GL;
   const bool on = g < nb && sb.ok[g];
@@ -1972,27 +2037,6 @@ __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* sta
   KMX_PT(7);
   grp_hqr(sb, lane, on);
   KMX_PT(8);
-}
-
-// Hypothesis b of the batch -> model (w.ok, w.mR, w.mt): the sample's
-// bearings (the decomposition's sample error), the action matrix, null space
-// and eigenvalues back into the workspace, then stew_tail.
-__device__ __forceinline__ void stew_model(CoopWS& w, const StewBatch& sb, const double* stash, int lane,
-                                           const double* F1, const double* F2, const short* smp, int b, bool prof) {
-  if (lane < 15) {
-    const int i = lane / 3, c = lane % 3;
-    w.f1[lane] = F1[3 * smp[i] + c];
-    w.f2[lane] = F2[3 * smp[i] + c];
-  }
-  const double* st = stash + b * STASH_H;
-  for (int t = lane; t < 100; t += RS_BLOCK) w.M[t / 10][t % 10] = action_entry(st, t / 10, t % 10);
-  if (lane < 36) (&w.N[0][0])[lane] = st[60 + lane];
-  if (lane < 10) {
-    w.wr[lane] = sb.wr[b][lane];
-    w.wi[lane] = sb.wi[b][lane];
-  }
-  wsync();
-  stew_tail(w, lane, 1, prof);
 }
 
 template <int LB, bool STEW>
@@ -2043,16 +2087,16 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
   // the serial loop's bookkeeping of one hypothesis's model (w.ok, w.mR, w.mt):
   // a failed solve counts as skipped; otherwise its inliers, the best model and
   // the adaptive iteration bound, and the iteration count
-  auto account = [&]() {
+  auto account = [&](bool ok, const double* mR, const double* mt) {
     unsigned long long t_prev = prof ? wall_clock64() : 0;
-    if (!w.ok) {
+    if (!ok) {
       ++skipped;
       wsync();
       return;
     }
     double Rm[9], tm[3];
-    for (int i = 0; i < 9; ++i) Rm[i] = w.mR[i];
-    for (int i = 0; i < 3; ++i) tm[i] = w.mt[i];
+    for (int i = 0; i < 9; ++i) Rm[i] = mR[i];
+    for (int i = 0; i < 3; ++i) tm[i] = mt[i];
     int cnt = 0;
     for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
       const int j = j0 + lane;
@@ -2085,25 +2129,20 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
       if (!(iterations < kk && skipped < max_skip)) break;  // uniform
       const int nb = min(SG, P.pmax - p0);
       stew_batch(w, sb, stash, lane, F1, F2, tab, p0, nb, prof);
+      stew_models(sb, stash, lane, F1, F2, tab, p0, nb, prof);
       for (int b = 0; b < nb && !done; ++b) {
         if (!(iterations < kk && skipped < max_skip)) {
           done = true;
           break;
         }
-        if (!sb.ok[b]) {  // no action matrix or no eigenvalues: the solve failed
-          ++skipped;
-          wsync();
-          continue;
-        }
-        stew_model(w, sb, stash, lane, F1, F2, tab + (size_t)(p0 + b) * 5, b, prof);
-        account();
+        account(sb.mok[b] != 0, sb.mR[b], sb.mt[b]);
       }
     }
   } else {
     for (int p = 0; p < P.pmax && !done; ++p) {
       if (!(iterations < kk && skipped < max_skip)) break;  // uniform
       coop_hypothesis(w, lane, F1, F2, tab + (size_t)p * 5, prof);
-      account();
+      account(w.ok != 0, w.mR, w.mt);
     }
   }
   if (!have) {
