@@ -1540,9 +1540,16 @@ __device__ __forceinline__ int eigvec_col(const double mcol[10], int lane, cplx_
       if (i == p) { b[i] = bk; col[i] = ck; }
     b[k] = bp;
     col[k] = cp;
+    // the multiplier of row i, col[i] / col[k], is formed once, by lane g0 + i,
+    // and broadcast (the same division, so the same bits in every lane)
+    cplx_d cm = col[k];
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i)
+      if (i == c) cm = col[i];
+    const cplx_d fm = c_div(cm, col[k]);
 #pragma unroll
     for (int i = k + 1; i < 10; ++i) {
-      const cplx_d f = c_div(col[i], col[k]);
+      const cplx_d f = shfl_c(fm, g0 + i);
       if (c > k) b[i] = c_sub(b[i], c_mul(f, b[k]));
     }
   }
