@@ -1788,10 +1788,11 @@ __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
         x = fabs(p) + fabs(q) + fabs(r);
         if (x == 0.0) {
           go = false;
-        } else {
-          p = p / x;
-          q = q / x;
-          r = r / x;
+        } else {  // p / x, q / x, r / x: one quotient per lane 0-2 of the group, broadcast
+          const double quo = (gl == 0 ? p : gl == 1 ? q : r) / x;
+          p = grp_bcast(quo, g, 0);
+          q = grp_bcast(quo, g, 1);
+          r = grp_bcast(quo, g, 2);
         }
       }
       double s = 0.0;
@@ -1807,13 +1808,14 @@ __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
           h[k][k - 1] = -s * x;
         }
       }
-      if (go) {
+      if (go) {  // p / s, q / s, r / s, q / p, r / p: lanes 0-4 of the group, broadcast
         p = p + s;
-        x = p / s;
-        y = q / s;
-        zz = r / s;
-        q = q / p;
-        r = r / p;
+        const double quo = (gl == 0 ? p : gl == 1 || gl == 3 ? q : r) / (gl < 3 ? s : p);
+        x = grp_bcast(quo, g, 0);
+        y = grp_bcast(quo, g, 1);
+        zz = grp_bcast(quo, g, 2);
+        q = grp_bcast(quo, g, 3);
+        r = grp_bcast(quo, g, 4);
       }
       if (go && gl >= k && gl <= en) {  // row modification, column j = gl
         const int j = gl;
