@@ -57,3 +57,33 @@ def test_verify_bit_exact(gpu, variant, norm, recovery, algo):
     # planted loop closures are found, random pairs rejected
     acc = np.array([g["accepted"] for g in got])
     assert acc[0::2].all() and not acc[1::2].any()
+
+
+@pytest.mark.parametrize("max_iter,true_frac,false_frac", [(1, 0.5, 0.2), (7, 0.25, 0.5), (40, 0.25, 0.4),
+                                                           (500, 0.3, 0.4)])
+def test_stewenius_batches_stop_like_the_serial_loop(gpu, max_iter, true_frac, false_frac):
+    """k_ransac_coop computes Stewenius hypotheses six at a time and scores
+    them in order under the serial loop's tests (iterations < k, skipped <
+    max_skip, iterations > max_iter): iteration caps that end a batch part
+    way, and low inlier ratios (long runs, adaptive k shrinking mid-batch),
+    give the one-at-a-time restatement's iteration counts, inlier sets and
+    poses bit for bit."""
+    from oracle import oracle as O
+    pool = make_lcd_pool(24, 300, true_frac=true_frac, false_frac=false_frac, seed=9)
+    p = LcdParams(ransac_2d2d_algorithm=0, ransac_max_iterations=max_iter)
+    det = LoopClosureDetector(p)
+    det.set_pool(pool)
+    got, gm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    ref, rm = O.lcd_verify(p.to_c(), pool)
+    its = []
+    for i in range(len(got)):
+        r, g = ref[i], got[i]
+        assert (g["n_matches"], g["mono_inliers"], g["stereo_inliers"], g["accepted"], g["iterations_2d2d"]) == \
+            (r.n_matches, r.mono_inliers, r.stereo_inliers, bool(r.accepted), r.iterations_2d2d), i
+        assert np.array_equal(g["T_query_match"], np.array(r.T_query_match[:])), i
+        its.append(r.iterations_2d2d)
+    assert np.array_equal(gm, rm)
+    its = np.array(its[0::2])
+    assert its.max() <= max_iter + 1
+    if max_iter == 500:  # the adaptive bound ends the runs (345 .. 486 iterations), inside batches of six
+        assert its.max() < max_iter and (its % 6 != 0).any()
