@@ -42,11 +42,6 @@ constexpr int KNN_BLOCK = 256;
 constexpr int RS_BLOCK = 64;          // one wavefront per candidate
 constexpr int MAX_FEATS = 1024;
 
-__constant__ int MUL11[4][4] = {{0, 1, 2, 6}, {1, 3, 4, 7}, {2, 4, 5, 8}, {6, 7, 8, 9}};
-__constant__ int MUL21[10][4] = {{0, 2, 4, 5},    {2, 3, 8, 9},    {4, 8, 10, 11},  {3, 1, 6, 7},
-                                 {8, 6, 13, 14},  {10, 13, 16, 17}, {5, 9, 11, 12}, {9, 7, 14, 15},
-                                 {11, 14, 17, 18}, {12, 15, 18, 19}};
-
 // ------------------------------------------------------------------ knn2 --
 __global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const int* nfeat, int N,
                                                     const int* cq, const int* cm, int norm, double lowe,
@@ -198,96 +193,13 @@ __device__ void svd3(const double E[9], double U[9], double s[3], double V[9]) {
     for (int r = 0; r < 3; ++r) U[r * 3 + c] = u[c][r];
 }
 
-// ------------------------------------------------ 5-point (Nister 2004) --
-__device__ void mul11(const double* a, const double* b, double* out) {
-  for (int k = 0; k < 10; ++k) out[k] = 0.0;
-  for (int i = 0; i < 4; ++i)
-    for (int j = 0; j < 4; ++j) out[MUL11[i][j]] += a[i] * b[j];
-}
-__device__ void mul21(const double* a, const double* b, double* out) {
-  for (int k = 0; k < 20; ++k) out[k] = 0.0;
-  for (int i = 0; i < 10; ++i)
-    for (int j = 0; j < 4; ++j) out[MUL21[i][j]] += a[i] * b[j];
-}
-
-__device__ void nullspace_5x9(const double Q[5][9], double N[4][9]) {
-  double A[9][5];
-  for (int i = 0; i < 9; ++i)
-    for (int j = 0; j < 5; ++j) A[i][j] = Q[j][i];
-  double vs[5][9];
-  for (int k = 0; k < 5; ++k) {
-    double nx = 0.0;
-    for (int i = k; i < 9; ++i) nx += A[i][k] * A[i][k];
-    nx = sqrt(nx);
-    const double alpha = (A[k][k] >= 0.0) ? -nx : nx;
-    double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = k; i < 9; ++i) v[i] = A[i][k];
-    v[k] -= alpha;
-    double nv = 0.0;
-    for (int i = k; i < 9; ++i) nv += v[i] * v[i];
-    nv = sqrt(nv);
-    for (int i = 0; i < 9; ++i) vs[k][i] = (nv > 0.0 && i >= k) ? v[i] / nv : 0.0;
-    for (int j = k; j < 5; ++j) {
-      double d = 0.0;
-      for (int i = k; i < 9; ++i) d += vs[k][i] * A[i][j];
-      for (int i = k; i < 9; ++i) A[i][j] -= 2.0 * vs[k][i] * d;
-    }
-  }
-  for (int c = 0; c < 4; ++c) {
-    double x[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    x[5 + c] = 1.0;
-    for (int k = 4; k >= 0; --k) {
-      double d = 0.0;
-      for (int i = k; i < 9; ++i) d += vs[k][i] * x[i];
-      for (int i = k; i < 9; ++i) x[i] -= 2.0 * vs[k][i] * d;
-    }
-    for (int i = 0; i < 9; ++i) N[c][i] = x[i];
-  }
-}
-
 __device__ double poly_eval(const double* c, int deg, double z) {
   double v = c[deg];
   for (int i = deg - 1; i >= 0; --i) v = v * z + c[i];
   return v;
 }
 
-__device__ int sign_changes(const double S[11][11], const int* sd, int ns, double z) {
-  int ch = 0;
-  double prev = 0.0;
-  for (int s = 0; s < ns; ++s) {
-    const double v = poly_eval(S[s], sd[s], z);
-    if (v != 0.0) {
-      if (prev != 0.0 && ((v < 0.0) != (prev < 0.0))) ++ch;
-      prev = v;
-    }
-  }
-  return ch;
-}
-
 constexpr int RR_SPLIT = 64, RR_DEPTH = 12;
-
-// Safeguarded Newton on an isolating interval (oracle refine_root).
-__device__ double refine_root(const double* c, int deg, double a, double b) {
-  double dc[10];
-  for (int i = 0; i < deg; ++i) dc[i] = (double)(i + 1) * c[i + 1];
-  double fa = poly_eval(c, deg, a);
-  double x = 0.5 * (a + b);
-  for (int it = 0; it < 60; ++it) {
-    const double fx = poly_eval(c, deg, x);
-    if (fx == 0.0) return x;
-    if ((fx < 0.0) == (fa < 0.0)) { a = x; fa = fx; }
-    else b = x;
-    const double dfx = poly_eval(dc, deg - 1, x);
-    double xn = (dfx != 0.0) ? x - fx / dfx : 0.5 * (a + b);
-    if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;  // converged (before the safeguard)
-    if (!(xn > a && xn < b)) {
-      xn = 0.5 * (a + b);
-      if (fabs(xn - x) <= 1e-15 * fmax(1.0, fabs(x))) return xn;
-    }
-    x = xn;
-  }
-  return x;
-}
 
 // Fujiwara root bound with power-of-two terms (oracle/lcd_oracle.c root_bound)
 __device__ __forceinline__ int root_bound_term(double ai, int m) {  // INT_MIN: none
@@ -295,211 +207,9 @@ __device__ __forceinline__ int root_bound_term(double ai, int m) {  // INT_MIN: 
   const int x = ilogb(ai) + 1;
   return x >= 0 ? (x + m - 1) / m : -((-x) / m);
 }
-__device__ double root_bound(const double* a, int deg) {
-  int kmax = INT_MIN, fin = 1;
-  double cauchy = 0.0;
-  for (int i = 0; i < deg; ++i) {
-    cauchy = fmax(cauchy, fabs(a[i]));
-    if (!isfinite(a[i])) fin = 0;
-    kmax = max(kmax, root_bound_term(a[i], deg - i));
-  }
-  if (!fin) return cauchy + 1.0;
-  if (kmax == INT_MIN) return 1.0;
-  return ldexp(1.0, kmax + 1);
-}
 
-__device__ int real_roots(const double* coef, int deg_in, double* roots) {
-  int deg = deg_in;
-  while (deg > 0 && coef[deg] == 0.0) --deg;
-  if (deg <= 0) return 0;
-  double S[11][11];
-  int sd[11];
-  for (int i = 0; i <= deg; ++i) S[0][i] = coef[i] / coef[deg];
-  sd[0] = deg;
-  for (int i = 0; i < deg; ++i) S[1][i] = (double)(i + 1) * S[0][i + 1];
-  sd[1] = deg - 1;
-  int ns = 2;
-  while (sd[ns - 1] > 0 && ns < 11) {
-    double r[11];
-    const int da = sd[ns - 2], db = sd[ns - 1];
-    for (int i = 0; i <= da; ++i) r[i] = S[ns - 2][i];
-    for (int k = da - db; k >= 0; --k) {
-      const double f = r[k + db] / S[ns - 1][db];
-      for (int i = 0; i <= db; ++i) r[k + i] -= f * S[ns - 1][i];
-    }
-    int dr = db - 1;
-    double mx = 0.0;
-    for (int i = 0; i <= da; ++i) mx = fmax(mx, fabs(S[ns - 2][i]));
-    while (dr >= 0 && fabs(r[dr]) <= 1e-14 * mx) --dr;
-    if (dr < 0) break;
-    for (int i = 0; i <= dr; ++i) S[ns][i] = -r[i];
-    sd[ns] = dr;
-    ++ns;
-  }
-  const double bound = root_bound(S[0], deg);
-  // 64-ary isolation / refinement, the oracle's sequence of points
-  // (oracle/lcd_oracle.c real_roots); k_ransac_coop evaluates a level's 63
-  // points in one wavefront. At most deg intervals with roots are alive.
-  double st_lo[16], st_hi[16];
-  int st_vl[16], st_vh[16], st_d[16];
-  int sp = 0, nr = 0;
-  const int vlo = sign_changes(S, sd, ns, -bound);
-  const int vhi = sign_changes(S, sd, ns, bound);
-  st_lo[sp] = -bound; st_hi[sp] = bound; st_vl[sp] = vlo; st_vh[sp] = vhi; st_d[sp] = 0; ++sp;
-  while (sp > 0) {
-    --sp;
-    const double lo = st_lo[sp], hi = st_hi[sp];
-    const int vl = st_vl[sp], vh = st_vh[sp], dep = st_d[sp];
-    const int cnt = vl - vh;
-    if (cnt <= 0) continue;
-    if (cnt == 1 || dep >= RR_DEPTH) {
-      if (nr < 10) roots[nr++] = refine_root(S[0], deg, lo, hi);
-      continue;
-    }
-    const double w = (hi - lo) / RR_SPLIT;
-    int vprev = vh;
-    double xprev = hi;
-    for (int j = RR_SPLIT - 1; j >= 0; --j) {
-      const double xj = (j == 0) ? lo : lo + (double)j * w;
-      const int vj = (j == 0) ? vl : sign_changes(S, sd, ns, xj);
-      if (vj - vprev > 0 && sp < 16) {
-        st_lo[sp] = xj; st_hi[sp] = xprev; st_vl[sp] = vj; st_vh[sp] = vprev; st_d[sp] = dep + 1; ++sp;
-      }
-      vprev = vj;
-      xprev = xj;
-    }
-  }
-  for (int a = 0; a < nr; ++a)
-    for (int b = 0; b + 1 < nr - a; ++b)
-      if (roots[b] > roots[b + 1]) { const double t = roots[b]; roots[b] = roots[b + 1]; roots[b + 1] = t; }
-  return nr;
-}
-
-__device__ void pmul(const double* a, int da, const double* b, int db, double* out) {
-  for (int i = 0; i <= da + db; ++i) out[i] = 0.0;
-  for (int i = 0; i <= da; ++i)
-    for (int j = 0; j <= db; ++j) out[i + j] += a[i] * b[j];
-}
-
-__device__ int fivept_nister(const double* f1, const double* f2, double* Es) {
-  double Q[5][9];
-  for (int i = 0; i < 5; ++i)
-    for (int a = 0; a < 3; ++a)
-      for (int b = 0; b < 3; ++b) Q[i][a * 3 + b] = f1[3 * i + a] * f2[3 * i + b];
-  double N[4][9];
-  nullspace_5x9(Q, N);
-  double E[9][4];
-  for (int e = 0; e < 9; ++e)
-    for (int c = 0; c < 4; ++c) E[e][c] = N[c][e];
-  double A[10][20];
-  {
-    double t1[10], t2[10], c2[10], m[20];
-    for (int k = 0; k < 20; ++k) A[9][k] = 0.0;
-    mul11(E[4], E[8], t1); mul11(E[5], E[7], t2);
-    for (int k = 0; k < 10; ++k) c2[k] = t1[k] - t2[k];
-    mul21(c2, E[0], m);
-    for (int k = 0; k < 20; ++k) A[9][k] += m[k];
-    mul11(E[3], E[8], t1); mul11(E[5], E[6], t2);
-    for (int k = 0; k < 10; ++k) c2[k] = t1[k] - t2[k];
-    mul21(c2, E[1], m);
-    for (int k = 0; k < 20; ++k) A[9][k] -= m[k];
-    mul11(E[3], E[7], t1); mul11(E[4], E[6], t2);
-    for (int k = 0; k < 10; ++k) c2[k] = t1[k] - t2[k];
-    mul21(c2, E[2], m);
-    for (int k = 0; k < 20; ++k) A[9][k] += m[k];
-  }
-  {
-    double EEt[9][10], tr[10], t[10], m[20];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        for (int k = 0; k < 10; ++k) EEt[i * 3 + j][k] = 0.0;
-        for (int l = 0; l < 3; ++l) {
-          mul11(E[i * 3 + l], E[j * 3 + l], t);
-          for (int k = 0; k < 10; ++k) EEt[i * 3 + j][k] += t[k];
-        }
-      }
-    for (int k = 0; k < 10; ++k) tr[k] = EEt[0][k] + EEt[4][k] + EEt[8][k];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        double* r = A[i * 3 + j];
-        for (int k = 0; k < 20; ++k) r[k] = 0.0;
-        for (int l = 0; l < 3; ++l) {
-          mul21(EEt[i * 3 + l], E[l * 3 + j], m);
-          for (int k = 0; k < 20; ++k) r[k] += 2.0 * m[k];
-        }
-        mul21(tr, E[i * 3 + j], m);
-        for (int k = 0; k < 20; ++k) r[k] -= m[k];
-      }
-  }
-  for (int k = 0; k < 10; ++k) {
-    int p = k;
-    for (int i = k + 1; i < 10; ++i)
-      if (fabs(A[i][k]) > fabs(A[p][k])) p = i;
-    if (A[p][k] == 0.0) return 0;
-    if (p != k)
-      for (int c = 0; c < 20; ++c) { const double t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t; }
-    const double inv = 1.0 / A[k][k];
-    for (int c = 0; c < 20; ++c) A[k][c] *= inv;
-    for (int i = 0; i < 10; ++i) {
-      if (i == k) continue;
-      const double f = A[i][k];
-      if (f == 0.0) continue;
-      for (int c = 0; c < 20; ++c) A[i][c] -= f * A[k][c];
-    }
-  }
-  double Bp[3][3][5];
-  for (int q = 0; q < 3; ++q) {
-    const double* e = &A[4 + 2 * q][10];
-    const double* f = &A[5 + 2 * q][10];
-    double* px = Bp[q][0];
-    double* py = Bp[q][1];
-    double* pc = Bp[q][2];
-    px[0] = e[2]; px[1] = e[1] - f[2]; px[2] = e[0] - f[1]; px[3] = -f[0]; px[4] = 0.0;
-    py[0] = e[5]; py[1] = e[4] - f[5]; py[2] = e[3] - f[4]; py[3] = -f[3]; py[4] = 0.0;
-    pc[0] = e[9]; pc[1] = e[8] - f[9]; pc[2] = e[7] - f[8]; pc[3] = e[6] - f[7]; pc[4] = -f[6];
-  }
-  double n[11];
-  {
-    double c1[8], c2[8], c3[8], t1[8], t2[8];
-    pmul(Bp[1][1], 3, Bp[2][2], 4, t1); pmul(Bp[1][2], 4, Bp[2][1], 3, t2);
-    for (int i = 0; i < 8; ++i) c1[i] = t1[i] - t2[i];
-    pmul(Bp[1][0], 3, Bp[2][2], 4, t1); pmul(Bp[1][2], 4, Bp[2][0], 3, t2);
-    for (int i = 0; i < 8; ++i) c2[i] = t1[i] - t2[i];
-    pmul(Bp[1][0], 3, Bp[2][1], 3, t1); pmul(Bp[1][1], 3, Bp[2][0], 3, t2);
-    for (int i = 0; i < 7; ++i) c3[i] = t1[i] - t2[i];
-    c3[7] = 0.0;
-    double u1[11], u2[11], u3[11];
-    pmul(Bp[0][0], 3, c1, 7, u1);
-    pmul(Bp[0][1], 3, c2, 7, u2);
-    pmul(Bp[0][2], 4, c3, 6, u3);
-    for (int i = 0; i < 11; ++i) n[i] = u1[i] - u2[i] + u3[i];
-  }
-  double roots[10];
-  const int nr = real_roots(n, 10, roots);
-  int ns = 0;
-  for (int ri = 0; ri < nr; ++ri) {
-    const double z = roots[ri];
-    double row[3][3];
-    for (int q = 0; q < 3; ++q)
-      for (int c = 0; c < 3; ++c) row[q][c] = poly_eval(Bp[q][c], c == 2 ? 4 : 3, z);
-    double v[3];
-    cross3(row[0], row[1], v);
-    if (v[2] == 0.0) continue;
-    const double x = v[0] / v[2], y = v[1] / v[2];
-    double* Eo = Es + 9 * ns;
-    double nn = 0.0;
-    for (int e = 0; e < 9; ++e) {
-      Eo[e] = x * N[0][e] + y * N[1][e] + z * N[2][e] + N[3][e];
-      nn += Eo[e] * Eo[e];
-    }
-    nn = sqrt(nn);
-    if (!(nn > 0.0)) continue;
-    for (int e = 0; e < 9; ++e) Eo[e] /= nn;
-    ++ns;
-  }
-  return ns;
-}
-
+// 2D-2D sample error of a model (oracle/lcd_oracle.c model_error): the point
+// triangulated from both bearings, 1 - cos to it in each frame, summed.
 __device__ double model_error(const double R[9], const double t[3], const double f1[3], const double f2[3]) {
   double f2u[3];
   for (int i = 0; i < 3; ++i) f2u[i] = R[i * 3 + 0] * f2[0] + R[i * 3 + 1] * f2[1] + R[i * 3 + 2] * f2[2];
@@ -519,52 +229,6 @@ __device__ double model_error(const double R[9], const double t[3], const double
   return e1 + e2;
 }
 
-__device__ int model_from_sample(const double* F1, const double* F2, const int* smp, double R[9], double t[3]) {
-  double f1[15], f2[15];
-  for (int i = 0; i < 5; ++i)
-    for (int c = 0; c < 3; ++c) {
-      f1[3 * i + c] = F1[3 * smp[i] + c];
-      f2[3 * i + c] = F2[3 * smp[i] + c];
-    }
-  double Es[90];
-  const int ne = fivept_nister(f1, f2, Es);
-  if (ne == 0) return 0;
-  double best = DBL_MAX;
-  int found = 0;
-  for (int e = 0; e < ne; ++e) {
-    double U[9], s[3], V[9];
-    svd3(Es + 9 * e, U, s, V);
-    double Ra[9], Rb[9];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        const double uw0 = U[i * 3 + 1], uw1 = -U[i * 3 + 0], uw2 = U[i * 3 + 2];
-        Ra[i * 3 + j] = uw0 * V[j * 3 + 0] + uw1 * V[j * 3 + 1] + uw2 * V[j * 3 + 2];
-        const double uv0 = -U[i * 3 + 1], uv1 = U[i * 3 + 0], uv2 = U[i * 3 + 2];
-        Rb[i * 3 + j] = uv0 * V[j * 3 + 0] + uv1 * V[j * 3 + 1] + uv2 * V[j * 3 + 2];
-      }
-    if (det3(Ra) < 0.0)
-      for (int i = 0; i < 9; ++i) Ra[i] = -Ra[i];
-    if (det3(Rb) < 0.0)
-      for (int i = 0; i < 9; ++i) Rb[i] = -Rb[i];
-    const double tu[3] = {U[0 * 3 + 2], U[1 * 3 + 2], U[2 * 3 + 2]};
-    for (int cand = 0; cand < 4; ++cand) {
-      const double* Rc = (cand < 2) ? Ra : Rb;
-      const double sg = (cand & 1) ? -1.0 : 1.0;
-      const double tc[3] = {sg * tu[0], sg * tu[1], sg * tu[2]};
-      double err = 0.0;
-      for (int i = 0; i < 5; ++i) err += model_error(Rc, tc, f1 + 3 * i, f2 + 3 * i);
-      if (err < best) {
-        best = err;
-        for (int i = 0; i < 9; ++i) R[i] = Rc[i];
-        for (int i = 0; i < 3; ++i) t[i] = tc[i];
-        found = 1;
-      }
-    }
-  }
-  return found;
-}
-
-// ---------------------------------------------------------- RANSAC kernel --
 // ------------------------------------------------------------- EPnP ------
 // Port of oracle/lcd_oracle.c orc_epnp for the RANSAC minimal sample (n = 6):
 // same operations in the same order, so models are bit-identical.
@@ -2283,221 +1947,6 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
   }
 }
 
-template <int LB>
-__global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac(const double* bearings, const double* points, int N,
-                                                     const int* cq, const int* cm, const int2* pairs,
-                                                     const int* Kin, const short* table, RsParams P,
-                                                     kmx_lcd_result* res, unsigned char* masks) {
-  extern __shared__ __attribute__((aligned(16))) double sm_d[];
-  const int c = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int K = Kin[c];
-  const int q = cq[c], m = cm[c];
-  double* F1 = sm_d;                  // [K][3]
-  double* F2 = F1 + 3 * N;            // [K][3]
-  double* models = F2 + 3 * N;        // [64][12]
-  double* bestm = models + 64 * 12;   // [12]
-  int* okc = reinterpret_cast<int*>(bestm + 12);  // [64] ok flags, [64] counts, ctrl[4]
-  int* cnt = okc + 64;
-  int* ctrl = cnt + 64;
-  unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
-  kmx_lcd_result* R_ = res + c;
-  for (int j = lane; j < N && mask; j += RS_BLOCK) mask[j] = 0;
-  if (K < 5) {
-    if (lane == 0) {
-      kmx_lcd_result r = {};
-      r.n_matches = K;
-      *R_ = r;
-    }
-    return;
-  }
-  const int2* pl = pairs + (size_t)c * N;
-  for (int j = lane; j < K; j += RS_BLOCK) {
-    const int2 pr = pl[j];
-    for (int k = 0; k < 3; ++k) {
-      F1[3 * j + k] = bearings[((size_t)q * N + pr.x) * 3 + k];
-      F2[3 * j + k] = bearings[((size_t)m * N + pr.y) * 3 + k];
-    }
-  }
-  __syncthreads();
-  // serial-loop state (lane 0)
-  int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
-  double kk = 1.0;
-  const int max_skip = P.max_iter * 10;
-  const short* tab = table + (size_t)(K - 5) * P.pmax * 5;
-  for (int base = 0;; base += RS_BLOCK) {
-    const int p = base + lane;
-    int ok = 0, count = 0;
-    double Rm[9], tm[3];
-    if (p < P.pmax) {
-      int smp[5];
-      for (int i = 0; i < 5; ++i) smp[i] = tab[(size_t)p * 5 + i];
-      ok = model_from_sample(F1, F2, smp, Rm, tm);
-      if (ok)
-        for (int j = 0; j < K; ++j)
-          if (model_error(Rm, tm, F1 + 3 * j, F2 + 3 * j) < P.thr2d) ++count;
-    }
-    okc[lane] = ok;
-    cnt[lane] = count;
-    if (ok) {
-      for (int i = 0; i < 9; ++i) models[lane * 12 + i] = Rm[i];
-      for (int i = 0; i < 3; ++i) models[lane * 12 + 9 + i] = tm[i];
-    }
-    __syncthreads();
-    if (lane == 0) {
-      int done = 0;
-      for (int l = 0; l < RS_BLOCK; ++l) {
-        if (!(iterations < kk && skipped < max_skip) || base + l >= P.pmax) { done = 1; break; }
-        if (!okc[l]) { ++skipped; continue; }
-        if (cnt[l] > best_cnt) {
-          best_cnt = cnt[l];
-          for (int i = 0; i < 12; ++i) bestm[i] = models[l * 12 + i];
-          have = 1;
-          const double w = (double)cnt[l] / (double)K;
-          double p_no = 1.0 - pow(w, 5.0);
-          p_no = fmax(DBL_EPSILON, p_no);
-          p_no = fmin(1.0 - DBL_EPSILON, p_no);
-          kk = log(1.0 - P.prob) / log(p_no);
-        }
-        ++iterations;
-        if (iterations > P.max_iter) { done = 1; break; }
-      }
-      if (!done && base + RS_BLOCK >= P.pmax) done = 1;
-      ctrl[0] = done;
-      ctrl[1] = have;
-      ctrl[2] = iterations;
-    }
-    __syncthreads();
-    if (ctrl[0]) break;
-  }
-  const int have_model = ctrl[1];
-  const int iters = ctrl[2];
-  if (!have_model) {
-    if (lane == 0) {
-      kmx_lcd_result r = {};
-      r.n_matches = K;
-      r.iterations_2d2d = iters;
-      *R_ = r;
-    }
-    return;
-  }
-  double Rb[9], tb[3];
-  for (int i = 0; i < 9; ++i) Rb[i] = bestm[i];
-  for (int i = 0; i < 3; ++i) tb[i] = bestm[9 + i];
-  // final inlier set of the best model; compact stereo points of inliers
-  int n_in = 0;
-  for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
-    const int j = j0 + lane;
-    const bool in = (j < K) && model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d;
-    if (j < K && mask) mask[j] = in ? 1 : 0;
-    n_in += __popcll(__ballot(in));
-  }
-  kmx_lcd_result r = {};
-  r.n_matches = K;
-  r.mono_inliers = n_in;
-  r.iterations_2d2d = iters;
-  for (int i = 0; i < 9; ++i) r.T_query_match[i] = Rb[i];
-  for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = tb[i];
-  if (n_in < P.min2d) {
-    if (lane == 0) *R_ = r;
-    return;
-  }
-  if (P.pnp) {  // k_recover takes over from the 2D-2D inlier mask
-    if (lane == 0) {
-      for (int i = 0; i < 12; ++i) r.T_query_match[i] = 0.0;
-      *R_ = r;
-    }
-    return;
-  }
-  // 3D-3D given rotation: T_j = p_q - R p_m over the 2D-2D inliers in pair order
-  __syncthreads();
-  double* T = F2;  // reuse: [n3][3] translations
-  unsigned char* valid = reinterpret_cast<unsigned char*>(models);  // [N] bytes
-  int* idx = reinterpret_cast<int*>(F1);  // [n3] pair positions (F1 no longer needed)
-  if (lane == 0) {
-    int n3 = 0;
-    for (int j = 0; j < K; ++j) {
-      // recompute the inlier predicate identically (lane 0 walks the pair list)
-      if (!(model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d)) continue;
-      idx[n3++] = j;  // safe: idx[n3] overwrites F1 words of entries < j only
-    }
-    ctrl[3] = n3;
-  }
-  __syncthreads();
-  const int n3 = ctrl[3];
-  for (int k = lane; k < n3; k += RS_BLOCK) {
-    const int j = idx[k];
-    const int2 pr = pl[j];
-    const double* a = points + ((size_t)q * N + pr.x) * 3;
-    const double* b = points + ((size_t)m * N + pr.y) * 3;
-    const bool v = !(isnan(a[0]) || isnan(a[1]) || isnan(a[2]) || isnan(b[0]) || isnan(b[1]) || isnan(b[2]));
-    valid[k] = v ? 1 : 0;
-    for (int i = 0; i < 3; ++i) T[3 * k + i] = a[i] - (Rb[i * 3 + 0] * b[0] + Rb[i * 3 + 1] * b[1] + Rb[i * 3 + 2] * b[2]);
-  }
-  __syncthreads();
-  const double thr2 = P.thr3d * P.thr3d;
-  int my_best = -1, my_cnt = 0;
-  for (int i = lane; i < n3; i += RS_BLOCK) {
-    if (!valid[i]) continue;
-    int cc = 0;
-    for (int j = 0; j < n3; ++j) {
-      if (!valid[j]) continue;
-      const double dx = T[3 * j] - T[3 * i], dy = T[3 * j + 1] - T[3 * i + 1], dz = T[3 * j + 2] - T[3 * i + 2];
-      if (dx * dx + dy * dy + dz * dz < thr2) ++cc;
-    }
-    if (cc > my_cnt) { my_cnt = cc; my_best = i; }
-  }
-  // wave reduction: max count, then smallest index
-  for (int off = 32; off > 0; off >>= 1) {
-    const int oc = __shfl_xor(my_cnt, off, 64);
-    const int ob = __shfl_xor(my_best, off, 64);
-    if (oc > my_cnt || (oc == my_cnt && ob >= 0 && (my_best < 0 || ob < my_best))) {
-      my_cnt = oc;
-      my_best = ob;
-    }
-  }
-  if (lane == 0) {
-    const int best = my_best;
-    if (best >= 0) {
-      int cc = 0;
-      double s[3] = {0.0, 0.0, 0.0};
-      for (int j = 0; j < n3; ++j) {
-        int in = 0;
-        if (valid[j]) {
-          const double dx = T[3 * j] - T[3 * best], dy = T[3 * j + 1] - T[3 * best + 1], dz = T[3 * j + 2] - T[3 * best + 2];
-          in = dx * dx + dy * dy + dz * dz < thr2;
-        }
-        if (in) {
-          for (int i = 0; i < 3; ++i) s[i] += T[3 * j + i];
-          ++cc;
-          if (mask) mask[idx[j]] |= 2;
-        }
-      }
-      for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = s[i] / (double)cc;
-      r.stereo_inliers = cc;
-      r.accepted = (cc >= P.min3d) ? 1 : 0;
-      if (r.accepted && P.refine) {  // the inliers again: valid and within thr3d of the best translation
-        refit_3d3d(
-            n3,
-            [&](int j, double* pq, double* pm) {
-              if (!valid[j]) return false;
-              const double dx = T[3 * j] - T[3 * best], dy = T[3 * j + 1] - T[3 * best + 1],
-                           dz = T[3 * j + 2] - T[3 * best + 2];
-              if (!(dx * dx + dy * dy + dz * dz < thr2)) return false;
-              const int2 pr = pl[idx[j]];
-              const double* a = points + ((size_t)q * N + pr.x) * 3;
-              const double* b = points + ((size_t)m * N + pr.y) * 3;
-              for (int k = 0; k < 3; ++k) { pq[k] = a[k]; pm[k] = b[k]; }
-              return true;
-            },
-            r.T_query_match, r.T_query_match + 9);
-      }
-    } else {
-      for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = 0.0;
-    }
-    *R_ = r;
-  }
-}
 
 // Arun 3-point model (oracle arun_model): centroids, H = sum dm dq^T, Kabsch
 // with svd3, t = c_q - R c_m (p_q = R p_m + t).
@@ -2723,7 +2172,6 @@ struct kmx_lcd {
   kmx_lcd_result* d_res = nullptr;
   unsigned char* d_mask = nullptr;
   double* d_fbuf = nullptr;  // [cap][6 N + STASH] compact match bearings + Stewenius stash (k_ransac_coop)
-  int ransac = 1;            // KMX_RANSAC: 1 cooperative (default), 0 lane-per-hypothesis
   int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
   // kmx_lcd_enable_timing: events around the kNN2 and the RANSAC launches
   bool timing = false;
@@ -2793,7 +2241,6 @@ int ensure_cap(kmx_lcd* h, int n) {
   return 0;
 }
 
-size_t ransac_smem(int N) { return sizeof(double) * (6 * (size_t)N + 64 * 12 + 12) + sizeof(int) * (64 + 64 + 4); }
 
 int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   if (n == 0) return 0;
@@ -2822,37 +2269,23 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   rp.algo = h->P.algorithm_2d2d;
   rp.refine = h->P.refine_pose && h->P.pose_recovery_type == 0 ? 1 : 0;
   {
-    // KMX_RS_LB: minimum waves per SIMD for k_ransac (diagnostic; 1 = the
-    // compiler's choice, 256 VGPRs)
-    static const int lb = [] {
-      const char* v = std::getenv("KMX_RS_LB");
-      return v ? std::atoi(v) : 1;
+    // KMX_COOP_LB: minimum waves per SIMD (register-budget A/B). Stewenius: the
+    // batch's LDS (12.6 KB per wave) admits 12 waves per CU, so 3 waves per SIMD
+    // and their 168 VGPRs; Nister: 4 waves per SIMD
+    static const int clb = [] {
+      const char* v = std::getenv("KMX_COOP_LB");
+      return v ? std::atoi(v) : 0;
     }();
-    if (h->ransac == 1 || rp.algo != KMX_ALGO_NISTER) {
-      static const int clb = [] {
-        const char* v = std::getenv("KMX_COOP_LB");
-        return v ? std::atoi(v) : 4;
-      }();
-      const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
-      // Stewenius: the batch's LDS (11.6 KB per wave) admits 13 waves per CU, so
-      // 3 waves per SIMD and their 168 VGPRs (no spills in the eigenvector
-      // solves) unless KMX_COOP_LB asks for more
-      auto kc = stew ? ((clb >= 8) ? k_ransac_coop<8, true> : (clb >= 6) ? k_ransac_coop<6, true>
-                        : (clb >= 5) ? k_ransac_coop<5, true> : (clb == 4 && std::getenv("KMX_COOP_LB"))
-                        ? k_ransac_coop<4, true> : k_ransac_coop<3, true>)
-                     : ((clb >= 8) ? k_ransac_coop<8, false> : (clb >= 6) ? k_ransac_coop<6, false>
-                        : (clb >= 5) ? k_ransac_coop<5, false> : k_ransac_coop<4, false>);
-      hipLaunchKernelGGL(kc, dim3(n), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
-                         (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
-                         (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
-                         (want_masks || rp.pnp) ? h->d_mask : nullptr, h->d_fbuf);
-    } else {
-      auto k = (lb >= 4) ? k_ransac<4> : (lb >= 2) ? k_ransac<2> : k_ransac<1>;
-      hipLaunchKernelGGL(k, dim3(n), dim3(RS_BLOCK), ransac_smem(h->N), h->stream, (const double*)h->d_bear,
-                         (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
-                         (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
-                         (want_masks || rp.pnp) ? h->d_mask : nullptr);
-    }
+    const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
+    auto kc = stew ? ((clb >= 8) ? k_ransac_coop<8, true> : (clb >= 6) ? k_ransac_coop<6, true>
+                      : (clb >= 5) ? k_ransac_coop<5, true> : (clb == 4) ? k_ransac_coop<4, true>
+                      : k_ransac_coop<3, true>)
+                   : ((clb >= 8) ? k_ransac_coop<8, false> : (clb >= 6) ? k_ransac_coop<6, false>
+                      : (clb >= 5) ? k_ransac_coop<5, false> : k_ransac_coop<4, false>);
+    hipLaunchKernelGGL(kc, dim3(n), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
+                       (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
+                       (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
+                       (want_masks || rp.pnp) ? h->d_mask : nullptr, h->d_fbuf);
   }
   if (rp.pnp) {
     const bool pnp = h->P.pose_recovery_type == 1;
@@ -2901,7 +2334,6 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
     return kmx::fail(KMX_EHIP, "hipStreamCreate");
   }
   h->own_stream = true;
-  if (const char* v = std::getenv("KMX_RANSAC")) h->ransac = std::atoi(v) ? 1 : 0;
   if (const char* v = std::getenv("KMX_RS_PROF")) h->prof = std::atoi(v) ? 1 : 0;
   *out = h;
   return KMX_OK;
