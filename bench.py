@@ -142,17 +142,18 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(g, P, snap, steps, seconds, threads_list):
+def cpu_baseline(g, P, snap, steps, seconds, variants):
     """The C restatement (oracle/, -march=native) on this host from the
     snapshot of the timed window's first round: the same rounds as the GPU's
     timed window (GNC by the host mirror of the schedule), bounded by
-    `seconds` per variant. threads = one per robot block (dpgo runs one agent
-    per process) and 1."""
+    `seconds` per variant. variants: (threads, inner) — one thread per robot
+    block (dpgo runs one agent per process), 1, and the all-cores form (blocks
+    x `inner` threads inside each block update; equal to rounding only)."""
     from kmx.dpgo.schedule import GncSchedule
     sys.path.insert(0, str(ROOT))
     from oracle.oracle import OraclePGO
     out = {}
-    for threads in threads_list:
+    for threads, inner in variants:
         o = OraclePGO(P.to_c(), g)
         for a, X in snap["X"].items():
             o.set_iterate(a, X)
@@ -168,7 +169,7 @@ def cpu_baseline(g, P, snap, steps, seconds, threads_list):
                 o.refresh()
                 o.update_weights()
                 sched.updated()
-            st = o.iterate(threads=threads)
+            st = o.iterate(threads=threads, inner=inner)
             sched.round_done()
             relc = np.array([s["rel_change"] if s["updated"] else relc[a] for a, s in enumerate(st)])
             edges_iters += sum(s["edges"] for s in st if s["updated"] and s["tcg_stop"] != "skipped")
@@ -177,7 +178,7 @@ def cpu_baseline(g, P, snap, steps, seconds, threads_list):
             if time.perf_counter() - t0 >= seconds:
                 break
         el = time.perf_counter() - t0
-        out[threads] = {"value": edges_iters / el, "rounds": rounds, "seconds": el, "hessvecs": hv,
+        out[(threads, inner)] = {"value": edges_iters / el, "rounds": rounds, "seconds": el, "hessvecs": hv,
                         "ms_per_step": 1e3 * el / rounds, "edges_iters": edges_iters,
                         "X": {a: o.get_iterate(a) for a in range(g.n_robots)}}
     return out
@@ -576,8 +577,13 @@ def main():
         lib, march = _native_oracle()
         if lib:
             os.environ["ORC_LIB"] = lib
-        cpu = cpu_baseline(g, P, leg["snap"], args.steps, args.cpu_seconds, (g.n_robots, 1))
-        team, one = cpu[g.n_robots], cpu[1]
+        # the host share for the all-cores form: OMP_NUM_THREADS where set (the
+        # GPU box sets it to the job's CPU share), else the affinity mask
+        share = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+        inner = max(1, share // g.n_robots)
+        variants = [(g.n_robots, 1), (1, 1)] + ([(g.n_robots, inner)] if inner > 1 else [])
+        cpu = cpu_baseline(g, P, leg["snap"], args.steps, args.cpu_seconds, variants)
+        team, one = cpu[(g.n_robots, 1)], cpu[(1, 1)]
         out["parity"] = gpu_parity(leg["drv"], leg["snap"], team)
         leg["drv"].solver.close()
         out["cpu_baseline"] = {
@@ -589,13 +595,21 @@ def main():
             "cores_note": "one thread per robot block, the reference's execution model: dpgo runs one "
                           "single-threaded PGOAgent per robot (one process per robot in 1014-example.yaml), so "
                           "the reference CPU path of this 8-block team uses 8 cores whatever the host has; the "
-                          "restatement's per-block loops sum in a fixed edge order (the frozen fixtures pin it), "
-                          "and no intra-block parallel variant is built",
+                          "restatement's per-block loops sum in a fixed edge order (the frozen fixtures pin it); "
+                          "all_cores adds threads inside each block update on the job's CPU share",
             "edge_count_rule": "same as the GPU counter: a block update counts its local edges when its "
                                "gradient norm passed gradnorm_tol (csrc/pgo.hip control_on RED_GRAD)",
             "single_thread": {"value": one["value"], "cores": 1, "rounds": one["rounds"],
                               "ms_per_step": one["ms_per_step"]},
         }
+        if inner > 1:
+            ac = cpu[(g.n_robots, inner)]
+            out["cpu_baseline"]["all_cores"] = {
+                "value": ac["value"], "cores": g.n_robots * inner, "share": share, "rounds": ac["rounds"],
+                "ms_per_step": ac["ms_per_step"],
+                "form": f"{g.n_robots} blocks x {inner} threads inside each block update (oracle "
+                        "orc_pgo_round_mt2: edge terms gathered per pose, per-pose loops and dot products "
+                        "split; equal to the serial restatement to rounding)"}
     if not args.no_lcd and not args.profile:
         lcd, lcd_cpu = lcd_leg(args, rank, world, barrier)
         n_local, lel = _gather(dist, world, [float(lcd["n_local"] * lcd["steps"]), lcd["elapsed"]], ["sum", "max"])

@@ -33,6 +33,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <omp.h>
+
 #include "../include/kmx_abi.h"
 
 #define D 3
@@ -58,6 +60,13 @@ typedef struct {
   double *V, *Yb;
   double gamma;
   int acc_k, acc_ready, acc_started;
+  /* all-cores timing variant (orc_pgo_round_mt2): per robot, each local pose's
+   * incidences (edge id << 1 | is_head), built on first use */
+  int64_t** inc_ptr;
+  int64_t** inc_e;
+  /* per robot: the block update's work vectors, kept between rounds (12 of
+   * n*4r doubles + S, Pinv), so a round does not page in fresh allocations */
+  double** work;
 } orc_pgo;
 
 static int PS(const orc_pgo* h) { return 4 * h->P.r; } /* doubles per pose */
@@ -77,6 +86,14 @@ static void free_graph(orc_pgo* h) {
   if (h->redges) for (int a = 0; a < h->R; ++a) free(h->redges[a]);
   free(h->redges); free(h->nredges); free(h->X); free(h->nbr); free(h->V); free(h->Yb);
   h->V = h->Yb = NULL;
+  if (h->inc_ptr)
+    for (int a = 0; a < h->R; ++a) { free(h->inc_ptr[a]); free(h->inc_e[a]); }
+  free(h->inc_ptr); free(h->inc_e);
+  h->inc_ptr = h->inc_e = NULL;
+  if (h->work)
+    for (int a = 0; a < h->R; ++a) free(h->work[a]);
+  free(h->work);
+  h->work = NULL;
 }
 
 void orc_pgo_destroy(void* vh) {
@@ -135,6 +152,7 @@ int orc_pgo_set_graph(void* vh, int n_robots, const int32_t* n_poses, int64_t m,
   }
   h->gamma = 0.0;
   h->acc_k = h->acc_ready = h->acc_started = 0;
+  h->work = (double**)calloc(n_robots, sizeof(double*));
   return 0;
 }
 
@@ -191,6 +209,7 @@ typedef struct {
   int r;
   int ps;      /* 4r */
   int64_t off; /* global offset */
+  int inner;   /* threads inside the block update (1: the serial restatement) */
 } blk;
 
 static double dot(const double* x, const double* y, int64_t k) {
@@ -247,6 +266,98 @@ static double edge_eval(const blk* b, const double* V, int use_nbr, double* out)
   return cost;
 }
 
+/* ---- all-cores timing variant (orc_pgo_round_mt2, bench.py's cpu_baseline
+ * "all_cores"): the same block update with its O(m) and O(n) loops spread over
+ * b->inner threads — edge_eval in gather form (each pose sums its incidences),
+ * per-pose loops split, dot products by OpenMP reductions. The summation
+ * order differs from the serial restatement (results agree to rounding), so it
+ * is a timing leg only: parity is always checked against the serial form. */
+static void build_incidences(orc_pgo* h) {
+  if (h->inc_ptr) return;
+  h->inc_ptr = (int64_t**)calloc(h->R, sizeof(int64_t*));
+  h->inc_e = (int64_t**)calloc(h->R, sizeof(int64_t*));
+  for (int a = 0; a < h->R; ++a) {
+    const int n = h->npose[a];
+    int64_t* ip = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+    for (int64_t k = 0; k < h->nredges[a]; ++k) {
+      const int64_t e = h->redges[a][k];
+      if (h->r1[e] == a) ip[h->p1[e] + 1]++;
+      if (h->r2[e] == a) ip[h->p2[e] + 1]++;
+    }
+    for (int i = 0; i < n; ++i) ip[i + 1] += ip[i];
+    int64_t* ie = (int64_t*)malloc(sizeof(int64_t) * ((size_t)ip[n] + 1));
+    int64_t* fill = (int64_t*)malloc(sizeof(int64_t) * ((size_t)n + 1));
+    memcpy(fill, ip, sizeof(int64_t) * (size_t)n);
+    for (int64_t k = 0; k < h->nredges[a]; ++k) {
+      const int64_t e = h->redges[a][k];
+      if (h->r1[e] == a) ie[fill[h->p1[e]]++] = e << 1;
+      if (h->r2[e] == a) ie[fill[h->p2[e]]++] = (e << 1) | 1;
+    }
+    free(fill);
+    h->inc_ptr[a] = ip;
+    h->inc_e[a] = ie;
+  }
+}
+
+static double edge_eval_par(const blk* b, const double* V, int use_nbr, double* out) {
+  orc_pgo* h = b->h;
+  const int r = b->r, ps = b->ps, ra = b->a;
+  const int64_t* ip = h->inc_ptr[ra];
+  const int64_t* ie = h->inc_e[ra];
+  double cost = 0.0;
+#pragma omp parallel for num_threads(b->inner) schedule(static) reduction(+ : cost)
+  for (int i = 0; i < b->n; ++i) {
+    double acc[4 * 8];
+    const double zero[4 * 8] = {0};
+    memset(acc, 0, sizeof(acc));
+    for (int64_t q = ip[i]; q < ip[i + 1]; ++q) {
+      const int64_t e = ie[q] >> 1;
+      const int head = (int)(ie[q] & 1);
+      const int ti = (h->r1[e] == ra), hi = (h->r2[e] == ra);
+      const double* Vi = ti ? V + (int64_t)h->p1[e] * ps
+                            : (use_nbr ? h->nbr + (h->poff[h->r1[e]] + h->p1[e]) * ps : zero);
+      const double* Vj = hi ? V + (int64_t)h->p2[e] * ps
+                            : (use_nbr ? h->nbr + (h->poff[h->r2[e]] + h->p2[e]) * ps : zero);
+      const double* Rt = h->Rm + 9 * e;
+      const double* tt = h->tv + 3 * e;
+      const double wk = h->w[e] * h->kappa[e], wt = h->w[e] * h->tau[e];
+      const int owner = head ? !ti : 1;  /* each edge's cost once: at its tail if local, else its head */
+      for (int a = 0; a < r; ++a) {
+        const double* yi = Vi + 4 * a;
+        const double* yj = Vj + 4 * a;
+        double ER[3], Et;
+        for (int c = 0; c < 3; ++c)
+          ER[c] = yj[c] - (yi[0] * Rt[0 * 3 + c] + yi[1] * Rt[1 * 3 + c] + yi[2] * Rt[2 * 3 + c]);
+        Et = yj[3] - yi[3] - (yi[0] * tt[0] + yi[1] * tt[1] + yi[2] * tt[2]);
+        if (owner) cost += 0.5 * (wk * (ER[0] * ER[0] + ER[1] * ER[1] + ER[2] * ER[2]) + wt * Et * Et);
+        double* o = acc + 4 * a;
+        if (head) {
+          o[0] += wk * ER[0]; o[1] += wk * ER[1]; o[2] += wk * ER[2];
+          o[3] += wt * Et;
+        } else {
+          for (int c = 0; c < 3; ++c)
+            o[c] -= wk * (ER[0] * Rt[c * 3 + 0] + ER[1] * Rt[c * 3 + 1] + ER[2] * Rt[c * 3 + 2]) + wt * Et * tt[c];
+          o[3] -= wt * Et;
+        }
+      }
+    }
+    memcpy(out + (int64_t)i * ps, acc, sizeof(double) * (size_t)ps);
+  }
+  return cost;
+}
+
+static double EVAL(const blk* b, const double* V, int use_nbr, double* out) {
+  return b->inner > 1 ? edge_eval_par(b, V, use_nbr, out) : edge_eval(b, V, use_nbr, out);
+}
+
+static double pdot(const blk* b, const double* x, const double* y, int64_t k) {
+  if (b->inner <= 1) return dot(x, y, k);
+  double s = 0.0;
+#pragma omp parallel for num_threads(b->inner) schedule(static) reduction(+ : s)
+  for (int64_t i = 0; i < k; ++i) s += x[i] * y[i];
+  return s;
+}
+
 /* per pose: S = sym(Y^T G_Y) (3x3) */
 static void sym_YtG(int r, const double* X, const double* G, double* S) {
   double M[9];
@@ -275,7 +386,30 @@ static void proj_pose(int r, const double* X, const double* V, double* out) {
 static void build_precond(const blk* b, double* Pinv /* n*16 */) {
   orc_pgo* h = b->h;
   double* Dm = (double*)calloc((size_t)b->n * 16, sizeof(double));
-  for (int64_t k = 0; k < h->nredges[b->a]; ++k) {
+  if (b->inner > 1) {  /* gather: each pose sums its incidences in redges order, as the scatter does */
+    const int64_t* ip = h->inc_ptr[b->a];
+    const int64_t* ie = h->inc_e[b->a];
+#pragma omp parallel for num_threads(b->inner) schedule(static)
+    for (int i = 0; i < b->n; ++i) {
+      double* M = Dm + (int64_t)i * 16;
+      for (int64_t q = ip[i]; q < ip[i + 1]; ++q) {
+        const int64_t e = ie[q] >> 1;
+        const double wk = h->w[e] * h->kappa[e], wt = h->w[e] * h->tau[e];
+        const double* tt = h->tv + 3 * e;
+        if (!(ie[q] & 1)) {
+          for (int ii = 0; ii < 3; ++ii) {
+            for (int j = 0; j < 3; ++j) M[ii * 4 + j] += wt * tt[ii] * tt[j] + (ii == j ? wk : 0.0);
+            M[ii * 4 + 3] += wt * tt[ii];
+            M[3 * 4 + ii] += wt * tt[ii];
+          }
+          M[15] += wt;
+        } else {
+          M[0] += wk; M[5] += wk; M[10] += wk; M[15] += wt;
+        }
+      }
+    }
+  }
+  for (int64_t k = 0; k < (b->inner > 1 ? 0 : h->nredges[b->a]); ++k) {
     const int64_t e = h->redges[b->a][k];
     const double wk = h->w[e] * h->kappa[e], wt = h->w[e] * h->tau[e];
     const double* tt = h->tv + 3 * e;
@@ -293,6 +427,7 @@ static void build_precond(const blk* b, double* Pinv /* n*16 */) {
       M[0] += wk; M[5] += wk; M[10] += wk; M[15] += wt;
     }
   }
+#pragma omp parallel for num_threads(b->inner) schedule(static) if (b->inner > 1)
   for (int i = 0; i < b->n; ++i) {
     double A[16], L[16] = {0}, Li[16] = {0};
     memcpy(A, Dm + (int64_t)i * 16, sizeof(A));
@@ -338,10 +473,11 @@ typedef struct {
 } ctx;
 
 static void rhess(const blk* b, const ctx* c, const double* V, double* out) {
-  edge_eval(b, V, 0, c->tmp); /* Euclidean Hess-vec Q V */
+  EVAL(b, V, 0, c->tmp); /* Euclidean Hess-vec Q V */
   const int r = b->r, ps = b->ps;
-  double buf[32];
+#pragma omp parallel for num_threads(b->inner) schedule(static) if (b->inner > 1)
   for (int i = 0; i < b->n; ++i) {
+    double buf[32];
     const double* Xi = c->Xb + (int64_t)i * ps;
     const double* Vi = V + (int64_t)i * ps;
     const double* Hi = c->tmp + (int64_t)i * ps;
@@ -361,8 +497,9 @@ static void precon(const blk* b, const ctx* c, const double* V, double* out) {
     memcpy(out, V, sizeof(double) * (size_t)b->n * ps);
     return;
   }
-  double buf[32];
+#pragma omp parallel for num_threads(b->inner) schedule(static) if (b->inner > 1)
   for (int i = 0; i < b->n; ++i) {
+    double buf[32];
     const double* Vi = V + (int64_t)i * ps;
     const double* P = c->Pinv + (int64_t)i * 16;
     for (int a = 0; a < r; ++a)
@@ -396,24 +533,29 @@ static void retract_pose(int r, const double* X, const double* V, double* out) {
 }
 
 /* --------------------------------------------------------- block update -- */
-static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
-  blk b = {h, a, h->npose[a], h->P.r, PS(h), h->poff[a]};
+static void block_update(orc_pgo* h, int a, kmx_iter_stats* st, int inner) {
+  blk b = {h, a, h->npose[a], h->P.r, PS(h), h->poff[a], inner};
   const int64_t N = (int64_t)b.n * b.ps;
   ctx c;
   c.Xb = h->X + b.off * b.ps;
-  c.eg = (double*)malloc(sizeof(double) * N + 8);
-  c.g = (double*)malloc(sizeof(double) * N + 8);
-  c.S = (double*)malloc(sizeof(double) * (size_t)b.n * 9 + 8);
-  c.Pinv = (double*)malloc(sizeof(double) * (size_t)b.n * 16 + 8);
-  c.tmp = (double*)malloc(sizeof(double) * N + 8);
-  double* eta = (double*)malloc(sizeof(double) * N + 8);
-  double* Heta = (double*)malloc(sizeof(double) * N + 8);
-  double* rr = (double*)malloc(sizeof(double) * N + 8);
-  double* z = (double*)malloc(sizeof(double) * N + 8);
-  double* del = (double*)malloc(sizeof(double) * N + 8);
-  double* Hd = (double*)malloc(sizeof(double) * N + 8);
-  double* Xt = (double*)malloc(sizeof(double) * N + 8);
-  double* X0 = (double*)malloc(sizeof(double) * N + 8);
+  /* work vectors: 12 of N doubles, S (n*9) and Pinv (n*16), one allocation per
+   * robot kept across rounds (h->work; robots write only their own) */
+  const int64_t NP = N + 1;
+  double* wk_ = h->work[a];
+  if (!wk_) wk_ = h->work[a] = (double*)malloc(sizeof(double) * (size_t)(12 * NP + (int64_t)b.n * 25 + 2));
+  c.eg = wk_;
+  c.g = wk_ + NP;
+  c.tmp = wk_ + 2 * NP;
+  double* eta = wk_ + 3 * NP;
+  double* Heta = wk_ + 4 * NP;
+  double* rr = wk_ + 5 * NP;
+  double* z = wk_ + 6 * NP;
+  double* del = wk_ + 7 * NP;
+  double* Hd = wk_ + 8 * NP;
+  double* Xt = wk_ + 9 * NP;
+  double* X0 = wk_ + 10 * NP;
+  c.S = wk_ + 12 * NP;
+  c.Pinv = c.S + (int64_t)b.n * 9 + 1;
   memcpy(X0, c.Xb, sizeof(double) * N);
   build_precond(&b, c.Pinv);
 
@@ -424,12 +566,13 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
   if (h->P.method == KMX_METHOD_RGD) {
     /* dpgo QuadraticOptimizer::gradientDescent (ROptMethod RGD) [U: dpgo not vendored]:
      * X <- Retr_X(-s * precon(rgrad)), always accepted; the same gradient-norm skip as RTR */
-    const double f = edge_eval(&b, c.Xb, 1, c.eg);
+    const double f = EVAL(&b, c.Xb, 1, c.eg);
+#pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
     for (int i = 0; i < b.n; ++i) {
       sym_YtG(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.S + (int64_t)i * 9);
       proj_pose(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.g + (int64_t)i * b.ps);
     }
-    const double gn = sqrt(dot(c.g, c.g, N));
+    const double gn = sqrt(pdot(&b, c.g, c.g, N));
     st->f_init = f;
     st->gradnorm_init = gn;
     st->f_final = f;
@@ -438,21 +581,24 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
     } else {
       precon(&b, &c, c.g, z);
       const double s = h->P.rgd_stepsize;
+#pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
       for (int64_t k = 0; k < N; ++k) eta[k] = -s * z[k];
+#pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
       for (int i = 0; i < b.n; ++i)
         retract_pose(b.r, c.Xb + (int64_t)i * b.ps, eta + (int64_t)i * b.ps, Xt + (int64_t)i * b.ps);
-      st->f_final = edge_eval(&b, Xt, 1, c.tmp);
+      st->f_final = EVAL(&b, Xt, 1, c.tmp);
       memcpy(c.Xb, Xt, sizeof(double) * N);
       st->accepted = 1;
     }
   }
   for (int it = 0; it < (h->P.method == KMX_METHOD_RGD ? 0 : h->P.rtr_iterations); ++it) {
-    double f = edge_eval(&b, c.Xb, 1, c.eg);
+    double f = EVAL(&b, c.Xb, 1, c.eg);
+#pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
     for (int i = 0; i < b.n; ++i) {
       sym_YtG(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.S + (int64_t)i * 9);
       proj_pose(b.r, c.Xb + (int64_t)i * b.ps, c.eg + (int64_t)i * b.ps, c.g + (int64_t)i * b.ps);
     }
-    const double gn = sqrt(dot(c.g, c.g, N));
+    const double gn = sqrt(pdot(&b, c.g, c.g, N));
     if (it == 0) { st->f_init = f; st->gradnorm_init = gn; }
     st->f_final = f;
     if (gn < h->P.gradnorm_tol) {
@@ -466,31 +612,34 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
     memset(Heta, 0, sizeof(double) * N);
     memcpy(rr, c.g, sizeof(double) * N);
     double e_Pe = 0.0, e_Pd = 0.0;
-    const double norm_r0 = sqrt(dot(rr, rr, N));
+    const double norm_r0 = sqrt(pdot(&b, rr, rr, N));
     precon(&b, &c, rr, z);
-    double z_r = dot(z, rr, N);
+    double z_r = pdot(&b, z, rr, N);
     double d_Pd = z_r;
+#pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
     for (int64_t k = 0; k < N; ++k) del[k] = -z[k];
     int stop = KMX_TCG_MAX_ITER, j;
     for (j = 1; j <= h->P.tcg_max_iterations; ++j) {
       rhess(&b, &c, del, Hd);
       st->hessvecs++;
-      const double d_Hd = dot(del, Hd, N);
+      const double d_Hd = pdot(&b, del, Hd, N);
       const double alpha = z_r / d_Hd;
       const double e_Pe_new = e_Pe + 2.0 * alpha * e_Pd + alpha * alpha * d_Pd;
       if (d_Hd <= 0.0 || e_Pe_new >= Delta * Delta) {
         const double tau = (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (Delta * Delta - e_Pe))) / d_Pd;
+#pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
         for (int64_t k = 0; k < N; ++k) { eta[k] += tau * del[k]; Heta[k] += tau * Hd[k]; }
         stop = d_Hd <= 0.0 ? KMX_TCG_NEGATIVE_CURVATURE : KMX_TCG_EXCEEDED_TR;
         break;
       }
       e_Pe = e_Pe_new;
+#pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
       for (int64_t k = 0; k < N; ++k) {
         eta[k] += alpha * del[k];
         Heta[k] += alpha * Hd[k];
         rr[k] += alpha * Hd[k];
       }
-      const double norm_r = sqrt(dot(rr, rr, N));
+      const double norm_r = sqrt(pdot(&b, rr, rr, N));
       if (norm_r <= norm_r0 * fmin(pow(norm_r0, h->P.tcg_theta), h->P.tcg_kappa)) {
         stop = (h->P.tcg_kappa < pow(norm_r0, h->P.tcg_theta)) ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
         break;
@@ -498,8 +647,9 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
       if (j == h->P.tcg_max_iterations) break;
       precon(&b, &c, rr, z);
       const double zold_rold = z_r;
-      z_r = dot(z, rr, N);
+      z_r = pdot(&b, z, rr, N);
       const double beta = z_r / zold_rold;
+#pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
       for (int64_t k = 0; k < N; ++k) del[k] = -z[k] + beta * del[k];
       e_Pd = beta * (e_Pd + alpha * d_Pd);
       d_Pd = z_r + beta * beta * d_Pd;
@@ -507,10 +657,11 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
     st->tcg_iterations = j > h->P.tcg_max_iterations ? h->P.tcg_max_iterations : j;
     st->tcg_stop = stop;
     /* ---- trial point, model decrease, acceptance ---- */
+#pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
     for (int i = 0; i < b.n; ++i)
       retract_pose(b.r, c.Xb + (int64_t)i * b.ps, eta + (int64_t)i * b.ps, Xt + (int64_t)i * b.ps);
-    const double ft = edge_eval(&b, Xt, 1, c.tmp);
-    const double model_dec = -(dot(eta, c.g, N) + 0.5 * dot(eta, Heta, N));
+    const double ft = EVAL(&b, Xt, 1, c.tmp);
+    const double model_dec = -(pdot(&b, eta, c.g, N) + 0.5 * pdot(&b, eta, Heta, N));
     const double rho = (model_dec > 0.0) ? (f - ft) / model_dec : -1.0;
     const int boundary = (stop == KMX_TCG_NEGATIVE_CURVATURE || stop == KMX_TCG_EXCEEDED_TR);
     if (!(rho >= 0.25)) Delta *= 0.25;
@@ -529,8 +680,6 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st) {
   double ch = 0.0;
   for (int64_t k = 0; k < N; ++k) { const double dd = c.Xb[k] - X0[k]; ch += dd * dd; }
   st->rel_change = sqrt(ch / (double)b.n);
-  free(c.eg); free(c.g); free(c.S); free(c.Pinv); free(c.tmp);
-  free(eta); free(Heta); free(rr); free(z); free(del); free(Hd); free(Xt); free(X0);
 }
 
 /* ------------------------------------------------ Nesterov acceleration -- */
@@ -637,7 +786,7 @@ int orc_pgo_round(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
   for (int a = 0; a < h->R; ++a) {
     kmx_iter_stats st;
     memset(&st, 0, sizeof(st));
-    if (active[a]) block_update(h, a, &st);
+    if (active[a]) block_update(h, a, &st, 1);
     if (stats) stats[a] = st;
   }
   orc_pgo_accel_post(h, active);
@@ -652,7 +801,7 @@ int orc_pgo_round_nbr(void* vh, const uint8_t* active, kmx_iter_stats* stats) {
   for (int a = 0; a < h->R; ++a) {
     kmx_iter_stats st;
     memset(&st, 0, sizeof(st));
-    if (active[a]) block_update(h, a, &st);
+    if (active[a]) block_update(h, a, &st, 1);
     if (stats) stats[a] = st;
   }
   orc_pgo_accel_post(h, active);
@@ -670,7 +819,26 @@ int orc_pgo_round_mt(void* vh, const uint8_t* active, kmx_iter_stats* stats, int
   for (int a = 0; a < h->R; ++a) {
     kmx_iter_stats st;
     memset(&st, 0, sizeof(st));
-    if (active[a]) block_update(h, a, &st);
+    if (active[a]) block_update(h, a, &st, 1);
+    if (stats) stats[a] = st;
+  }
+  return 0;
+}
+
+/* The all-cores timing variant: blocks over `outer` threads, each block update
+ * over `inner` more (nested), e.g. 8 blocks x 2 on a 16-core share. Results
+ * agree with orc_pgo_round to rounding, not bit for bit (see edge_eval_par). */
+int orc_pgo_round_mt2(void* vh, const uint8_t* active, kmx_iter_stats* stats, int outer, int inner) {
+  orc_pgo* h = (orc_pgo*)vh;
+  if (h->P.acceleration) return KMX_EUNSUP;
+  build_incidences(h);
+  omp_set_max_active_levels(2);
+  orc_pgo_refresh(h);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(outer)
+  for (int a = 0; a < h->R; ++a) {
+    kmx_iter_stats st;
+    memset(&st, 0, sizeof(st));
+    if (active[a]) block_update(h, a, &st, inner);
     if (stats) stats[a] = st;
   }
   return 0;
@@ -841,7 +1009,7 @@ int orc_pgo_get_trajectory(void* vh, int a, const double* anchor, double* out) {
 /* ------------------------------------------------ primitive evaluation -- */
 int orc_pgo_eval(void* vh, int a, int mode, const double* V, double* out, double* scalar) {
   orc_pgo* h = (orc_pgo*)vh;
-  blk b = {h, a, h->npose[a], h->P.r, PS(h), h->poff[a]};
+  blk b = {h, a, h->npose[a], h->P.r, PS(h), h->poff[a], 1};
   const int64_t N = (int64_t)b.n * b.ps;
   ctx c;
   c.Xb = h->X + b.off * b.ps;

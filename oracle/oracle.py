@@ -58,6 +58,7 @@ def _setup(L):
         "orc_pgo_local_edges": ([P, C.c_int], i64),
         "orc_pgo_round": ([P, pu8, C.POINTER(IterStats)], C.c_int),
         "orc_pgo_round_mt": ([P, pu8, C.POINTER(IterStats), C.c_int], C.c_int),
+        "orc_pgo_round_mt2": ([P, pu8, C.POINTER(IterStats), C.c_int, C.c_int], C.c_int),
         "orc_pgo_round_nbr": ([P, pu8, C.POINTER(IterStats)], C.c_int),
         "orc_pgo_update_weights_owned": ([P, pu8, pf64], C.c_int),
         "orc_pgo_update_weights_local": ([P, pu8, pf64], C.c_int),
@@ -153,11 +154,16 @@ class OraclePGO:
     def refresh(self):
         self.L.orc_pgo_refresh(self.h)
 
-    def iterate(self, active=None, threads=1):
+    def iterate(self, active=None, threads=1, inner=1):
+        """threads: robot blocks over OpenMP threads (results identical to the
+        serial round); inner > 1: each block update over `inner` more threads,
+        the all-cores timing variant (results equal to rounding only)."""
         from kmx.abi import IterStats
         act = np.ones(self.n_robots, np.uint8) if active is None else np.ascontiguousarray(active, dtype=np.uint8)
         stats = (IterStats * self.n_robots)()
-        if threads > 1:
+        if inner > 1:
+            self.L.orc_pgo_round_mt2(self.h, _u(act), stats, max(threads, 1), inner)
+        elif threads > 1:
             self.L.orc_pgo_round_mt(self.h, _u(act), stats, threads)
         else:
             self.L.orc_pgo_round(self.h, _u(act), stats)

@@ -249,3 +249,28 @@ def test_rgd_method_descends():
     for a in range(g.n_robots):
         X = o.get_iterate(a)[:, :, :3]
         assert np.abs(np.einsum("nai,naj->nij", X, X) - np.eye(3)).max() < 1e-10
+
+
+def test_all_cores_variant_agrees_with_serial_round():
+    """orc_pgo_round_mt2 (bench.py's all-cores CPU baseline: blocks over outer
+    threads, each block update over inner threads, edge terms gathered per pose)
+    follows the serial restatement to rounding: equal tCG counts and acceptance,
+    poses within 1e-9 over 10 rounds."""
+    from oracle.oracle import OraclePGO
+    from kmx.dpgo.params import PGOAgentParameters
+    from kmx.synth import lift, lifting_matrix, make_pose_graph
+    g = make_pose_graph(4, 4000, 16000, outlier_frac=0.2, seed=2)
+    P = PGOAgentParameters(r=5)
+    Y = lifting_matrix(5, seed=1)
+    a_, b_ = OraclePGO(P.to_c(), g), OraclePGO(P.to_c(), g)
+    for a in range(g.n_robots):
+        X0 = lift(g.init_R[a], g.init_t[a], Y)
+        a_.set_iterate(a, X0)
+        b_.set_iterate(a, X0)
+    for it in range(10):
+        sa = a_.iterate()
+        sb = b_.iterate(threads=2, inner=2)
+        for r in range(g.n_robots):
+            assert sa[r]["tcg_iterations"] == sb[r]["tcg_iterations"] and sa[r]["accepted"] == sb[r]["accepted"]
+            d = np.abs(a_.get_iterate(r) - b_.get_iterate(r)).max()
+            assert d <= 1e-9, (it, r, d)
