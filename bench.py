@@ -595,8 +595,11 @@ def main():
             "cores_note": "one thread per robot block, the reference's execution model: dpgo runs one "
                           "single-threaded PGOAgent per robot (one process per robot in 1014-example.yaml), so "
                           "the reference CPU path of this 8-block team uses 8 cores whatever the host has; the "
-                          "restatement's per-block loops sum in a fixed edge order (the frozen fixtures pin it); "
-                          "all_cores adds threads inside each block update on the job's CPU share",
+                          "restatement's per-block loops sum in a fixed edge order (the frozen fixtures pin it). "
+                          "all_cores spends the job's whole CPU share by adding threads inside each block update; "
+                          "it is slower than one thread per block (its gather form evaluates every edge at both "
+                          "endpoints, and the per-block loops are too short for nested teams), so the "
+                          "one-thread-per-block figure is the fastest CPU number this restatement has",
             "edge_count_rule": "same as the GPU counter: a block update counts its local edges when its "
                                "gradient norm passed gradnorm_tol (csrc/pgo.hip control_on RED_GRAD)",
             "single_thread": {"value": one["value"], "cores": 1, "rounds": one["rounds"],

@@ -834,7 +834,7 @@ int orc_pgo_round_mt2(void* vh, const uint8_t* active, kmx_iter_stats* stats, in
   build_incidences(h);
   omp_set_max_active_levels(2);
   orc_pgo_refresh(h);
-#pragma omp parallel for schedule(dynamic, 1) num_threads(outer)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(outer) if (outer > 1)
   for (int a = 0; a < h->R; ++a) {
     kmx_iter_stats st;
     memset(&st, 0, sizeof(st));
