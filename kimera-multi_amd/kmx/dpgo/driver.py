@@ -264,11 +264,15 @@ class RBCDDriver:
             return
         self._native_verified = True
         s = self.solver
-        s.exchange()
-        tab_n, ext_n = s.get_public(self.world)
+        try:  # an error here must still reach the agreement below on every rank
+            s.exchange()
+            tab_n, ext_n = s.get_public(self.world)
+        except Exception as e:  # noqa: BLE001 - reported through exchange_mode
+            tab_n = ext_n = None
+            self._native_error = f"first native exchange: {e}"
         self._torch_exchange()
         tab_t, ext_t = s.get_public(self.world)
-        same = np.array_equal(tab_n, tab_t) and np.array_equal(ext_n, ext_t)
+        same = tab_n is not None and np.array_equal(tab_n, tab_t) and np.array_equal(ext_n, ext_t)
         if self._agree(same):
             self.exchange_mode += ", checked bitwise against all_to_all at the first round"
             return
