@@ -87,3 +87,36 @@ def test_stewenius_batches_stop_like_the_serial_loop(gpu, max_iter, true_frac, f
     assert its.max() <= max_iter + 1
     if max_iter == 500:  # the adaptive bound ends the runs (345 .. 486 iterations), inside batches of six
         assert its.max() < max_iter and (its % 6 != 0).any()
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["stewenius", "nister"])
+@pytest.mark.parametrize("max_iter", [50, 500])
+@pytest.mark.parametrize("frames", ["match", "both"])
+def test_degenerate_samples_skip_like_the_serial_loop(gpu, algo, max_iter, frames):
+    """Every bearing of one candidate's match frame (and, with "both", of its
+    query frame) points the same way. "both": no sample gives a solvable
+    5-point system, every hypothesis counts as skipped and the loop ends at
+    max_skip = 10 x max_iter with no model (Stewenius: six skipped hypotheses
+    per batch, each checked against the serial stopping rule); "match": the
+    solvers return degenerate models the loop scores and rejects. The other
+    candidates are unaffected. Bit for bit against the restatement."""
+    from oracle import oracle as O
+    pool = make_lcd_pool(4, 120, seed=5)
+    pool.bearings[int(pool.cand_match[0]), :, :] = np.array([0.0, 0.0, 1.0])
+    if frames == "both":
+        pool.bearings[int(pool.cand_query[0]), :, :] = np.array([0.0, 1.0, 0.0])
+    p = LcdParams(ransac_2d2d_algorithm=algo, ransac_max_iterations=max_iter)
+    det = LoopClosureDetector(p)
+    det.set_pool(pool)
+    got, gm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    ref, rm = O.lcd_verify(p.to_c(), pool)
+    for i in range(len(got)):
+        r, g = ref[i], got[i]
+        assert (g["n_matches"], g["mono_inliers"], g["stereo_inliers"], g["accepted"], g["iterations_2d2d"]) == \
+            (r.n_matches, r.mono_inliers, r.stereo_inliers, bool(r.accepted), r.iterations_2d2d), i
+        assert np.array_equal(g["T_query_match"], np.array(r.T_query_match[:])), i
+    assert np.array_equal(gm, rm)
+    assert got[0]["n_matches"] >= 5 and not got[0]["accepted"]
+    if frames == "both":
+        assert got[0]["iterations_2d2d"] == 0
+    assert got[2]["accepted"]
