@@ -120,11 +120,18 @@ struct Params {
   int early_stop;   // RM_CONSUMER k_hess: the stop decision before the gather (else after)
 };
 
+// One tile's description, read by a single 16-B scalar load at the start of
+// every tile kernel: its robot, its first pose, its incidence range start
+// inc_ptr[p0] and, packed, its pose count np (< 256) and incidence count
+// n = inc_ptr[p0 + np] - inc_ptr[p0] (np | n << 8), so the record loads do not
+// wait for an inc_ptr lookup.
+struct alignas(16) TileDesc {
+  int robot, p0, k0, np_n;
+};
+
 struct Dev {
   int ntiles, L, nloc, npub;
-  const int* tile_robot;
-  const int* tile_p0;
-  const int* tile_np;
+  const TileDesc* tile;
   const int* rtile0;   // [L+1]
   const int* inc_ptr;  // [nloc+1]
   double* rec;         // [ninc + 1][RW] incidence records in CSR order (+ one zero pad record)
@@ -421,6 +428,7 @@ __device__ __forceinline__ void group_retract(const double x[4], const double v[
 // ------------------------------------------------------------- lane map ----
 struct Lane {
   int tile, l, w, ln, pw, a, base, pose;
+  int p0, np, k0, n;  // the tile's poses and incidences (TileDesc)
   bool valid;
 };
 template <int R>
@@ -435,15 +443,20 @@ __device__ __forceinline__ Lane lane_map(const Dev& d) {
     const int q = nwg >> 3, rr = nwg & 7, x = b & 7;
     L.tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
   }
-  L.l = d.tile_robot[L.tile];
+  const TileDesc t = d.tile[L.tile];
+  L.l = t.robot;
+  L.p0 = t.p0;
+  L.np = t.np_n & 0xff;
+  L.k0 = t.k0;
+  L.n = t.np_n >> 8;
   L.w = threadIdx.x >> 6;
   L.ln = threadIdx.x & 63;
   L.pw = L.ln / R;
   L.a = L.ln - L.pw * R;
   L.base = L.pw * R;
   const int local = L.w * PPW + L.pw;
-  L.valid = (L.pw < PPW) && (local < d.tile_np[L.tile]);
-  L.pose = d.tile_p0[L.tile] + (L.valid ? local : 0);
+  L.valid = (L.pw < PPW) && (local < L.np);
+  L.pose = L.p0 + (L.valid ? local : 0);
   if (L.base + R > 64) L.base = 64 - R;  // idle tail lanes shuffle within range
   return L;
 }
@@ -495,7 +508,11 @@ struct NoPre {
 };
 // `pre` runs once the first chunk's records are in flight, before any row is
 // gathered (workgroup-uniform; false: leave without gathering).
-template <int R, int RW, typename Pre = NoPre>
+// REC_FIRST: the first chunk's records are issued before the tile's CSR
+// offsets, so the two loads overlap (the consumer form keeps the offsets
+// first: its decision in `pre` is a call, and the records live across it
+// would spill)
+template <int R, int RW, bool REC_FIRST = false, typename Pre = NoPre>
 __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const double* V, double acc[4],
                                             char* smem, Pre&& pre = Pre{}) {
   using SM = SmemH<R>;
@@ -504,10 +521,7 @@ __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const d
   double* Cs = reinterpret_cast<double*>(smem + SM::c_off);
   int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
   const int tid = threadIdx.x;
-  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
-  const int K0 = d.inc_ptr[p0];
-  const int n = d.inc_ptr[p0 + np] - K0;
-  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
+  const int p0 = L.p0, np = L.np, K0 = L.k0, n = L.n;
   const int pl = L.pose - p0;
   const int lt = min(tid, CH - 1);
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
@@ -515,7 +529,9 @@ __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const d
   // at the end of the array inside it)
   auto ld = [&](int c0, double2* q) { RC::load(d.rec, (size_t)(K0 + max(min(c0 + lt, n - 1), 0)), q); };
   double2 q[RC::Q];
-  ld(0, q);
+  if constexpr (REC_FIRST) ld(0, q);
+  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
+  if constexpr (!REC_FIRST) ld(0, q);
   __syncthreads();  // sptr
   if (!pre()) return false;
   for (int c0 = 0; c0 < n; c0 += CH) {
@@ -591,21 +607,19 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
   double2* xs = reinterpret_cast<double2*>(smem + SM::x_off);
   int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
   const int tid = threadIdx.x;
-  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
-  const int K0 = d.inc_ptr[p0];
-  const int n = d.inc_ptr[p0 + np] - K0;
-  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
-  {
-    const double2* v2 = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
-    for (int i = tid; i < np * 2 * R; i += BLOCK) xs[i] = v2[i];
-  }
+  const int p0 = L.p0, np = L.np, K0 = L.k0, n = L.n;
   const int pl = L.pose - p0;
   const int lt = min(tid, CH - 1);
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
   double csum = 0.0;
   auto ld = [&](int c0, double2* q) { RC::load(d.rec, (size_t)(K0 + max(min(c0 + lt, n - 1), 0)), q); };
   double2 q[RC::Q];
-  ld(0, q);
+  ld(0, q);  // in flight with the CSR offsets and the tile's rows
+  if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
+  {
+    const double2* v2 = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
+    for (int i = tid; i < np * 2 * R; i += BLOCK) xs[i] = v2[i];
+  }
   __syncthreads();  // sptr, xs
   for (int c0 = 0; c0 < n; c0 += CH) {
     const int k = max(min(c0 + lt, n - 1), 0);
@@ -668,9 +682,7 @@ __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, co
   int* sptr = reinterpret_cast<int*>(smem + SM::ptr_off);
   double2* xs = reinterpret_cast<double2*>(smem + SM::x_off);
   const int tid = threadIdx.x;
-  const int p0 = d.tile_p0[L.tile], np = d.tile_np[L.tile];
-  const int K0 = d.inc_ptr[p0];
-  const int n = d.inc_ptr[p0 + np] - K0;
+  const int p0 = L.p0, np = L.np, K0 = L.k0, n = L.n;
   if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
   {
     const double2* v2 = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
@@ -1188,7 +1200,7 @@ __device__ __forceinline__ void body_grad(const Dev& d, int gated, char* smem) {
   if (gated) {
     if (blockIdx.x == 0 && threadIdx.x == 0) store_gnc(d.gnc, load_gnc(d.gnc_next));
     if (d.gnc_next->fired) {
-      const int np = d.tile_np[L.tile], p0 = d.tile_p0[L.tile];
+      const int np = L.np, p0 = L.p0;
       for (int t = threadIdx.x; t < np; t += blockDim.x) pose_precond<RW>(d, p0 + t);
       __syncthreads();
     }
@@ -1297,12 +1309,13 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
     beta = u.beta;
     pcoef = c0.coef;
   } else {
+    // the phase test runs once the first chunk's records are in flight (a
+    // robot out of tCG leaves before any row is gathered)
     const Ctl& c = d.ctl[L.l];
-    if (c.phase != PH_TCG) return;
+    if (!hinc_gather<R, RW, true>(d, L, d.z, H, smem, [&]() { return c.phase == PH_TCG; })) return;
     tcg_iter = c.tcg_iter;
     beta = c.beta;
     pcoef = c.coef;
-    hinc_gather<R, RW>(d, L, d.z, H, smem);
   }
   const bool first = (tcg_iter == 0);
   asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
@@ -2074,7 +2087,8 @@ struct kmx_pgo {
   double gnc_rel_tol = 1e-3;
   // device
   Dev dv{};
-  int *d_tile_robot = nullptr, *d_tile_p0 = nullptr, *d_tile_np = nullptr, *d_rtile0 = nullptr;
+  TileDesc* d_tile = nullptr;
+  int* d_rtile0 = nullptr;
   int* d_inc_ptr = nullptr;
   double* d_rec = nullptr;
   double *d_ekappa = nullptr, *d_etau = nullptr, *d_ew = nullptr;
@@ -2210,7 +2224,7 @@ void free_xchg(kmx_pgo* h) {
 }
 
 void free_dev(kmx_pgo* h) {
-  void* ptrs[] = {h->d_tile_robot, h->d_tile_p0, h->d_tile_np, h->d_rtile0, h->d_inc_ptr, h->d_rec, h->d_ekappa,
+  void* ptrs[] = {h->d_tile, h->d_rtile0, h->d_inc_ptr, h->d_rec, h->d_ekappa,
                   h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_hD, h->d_pub, h->d_part,
                   h->d_ctl, h->d_cnt, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
@@ -2219,7 +2233,8 @@ void free_dev(kmx_pgo* h) {
                   h->d_part_u};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  h->d_tile_robot = h->d_tile_p0 = h->d_tile_np = h->d_rtile0 = h->d_inc_ptr = nullptr;
+  h->d_tile = nullptr;
+  h->d_rtile0 = h->d_inc_ptr = nullptr;
   h->d_rec = h->d_ekappa = h->d_etau = h->d_ew = nullptr;
   h->d_eipos = nullptr;
   h->d_vec = h->d_S = h->d_Pinv = h->d_hD = h->d_pub = h->d_part = nullptr;
@@ -2853,8 +2868,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   // device
   int rc;
   const size_t vec = (size_t)std::max(nloc, 1) * ps;
-  if ((rc = dalloc(&h->d_tile_robot, h->ntiles)) || (rc = dalloc(&h->d_tile_p0, h->ntiles)) ||
-      (rc = dalloc(&h->d_tile_np, h->ntiles)) || (rc = dalloc(&h->d_rtile0, L + 1)) ||
+  if ((rc = dalloc(&h->d_tile, h->ntiles)) || (rc = dalloc(&h->d_rtile0, L + 1)) ||
       (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_rec, rec.size())) ||
       (rc = dalloc(&h->d_ekappa, ek_h.size())) || (rc = dalloc(&h->d_etau, et_h.size())) ||
       (rc = dalloc(&h->d_ew, ew_h.size())) || (rc = dalloc(&h->d_eipos, eipos.size())) ||
@@ -2882,9 +2896,17 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   auto up = [&](void* dst, const void* src, size_t bytes) {
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream);
   };
-  KMX_HIP(up(h->d_tile_robot, tr.data(), sizeof(int) * tr.size()));
-  KMX_HIP(up(h->d_tile_p0, tp0.data(), sizeof(int) * tp0.size()));
-  KMX_HIP(up(h->d_tile_np, tnp.data(), sizeof(int) * tnp.size()));
+  std::vector<TileDesc> tdesc(h->ntiles);
+  for (int t = 0; t < h->ntiles; ++t) {
+    TileDesc& td = tdesc[t];
+    td.robot = tr[t];
+    td.p0 = tp0[t];
+    td.k0 = inc_ptr[tp0[t]];
+    const int ninc = inc_ptr[tp0[t] + tnp[t]] - td.k0;
+    KMX_CHECK(tnp[t] < 256 && ninc < (1 << 23), KMX_EINVAL, "tile too large");
+    td.np_n = tnp[t] | (ninc << 8);
+  }
+  KMX_HIP(up(h->d_tile, tdesc.data(), sizeof(TileDesc) * tdesc.size()));
   KMX_HIP(up(h->d_rtile0, rt0.data(), sizeof(int) * rt0.size()));
   KMX_HIP(up(h->d_inc_ptr, inc_ptr.data(), sizeof(int) * inc_ptr.size()));
   KMX_HIP(up(h->d_rec, rec.data(), sizeof(double) * rec.size()));
@@ -2940,7 +2962,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   Dev& d = h->dv;
   d = Dev{};
   d.ntiles = h->ntiles; d.L = L; d.nloc = nloc; d.npub = (int)h->npub;
-  d.tile_robot = h->d_tile_robot; d.tile_p0 = h->d_tile_p0; d.tile_np = h->d_tile_np; d.rtile0 = h->d_rtile0;
+  d.tile = h->d_tile; d.rtile0 = h->d_rtile0;
   d.inc_ptr = h->d_inc_ptr; d.rec = h->d_rec;
   d.ekappa = h->d_ekappa; d.etau = h->d_etau; d.ew = h->d_ew; d.eipos = h->d_eipos;
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
