@@ -139,7 +139,17 @@ struct Dev {
   double* etau;
   double* ew;          // GNC weight
   const int2* eipos;   // [mloc] record positions (tail, head) of each local edge, -1 if not local
-  double *X, *Xt, *g, *r, *z, *eta, *del, *hd, *S, *Pinv, *hD, *pub;
+  double *X, *Xt, *g, *r, *z, *hd, *S, *Pinv, *hD, *pub;
+  // tCG search directions: delta_k lives in dh + (k % dhn) * vec for the whole
+  // block update, so eta = sum_k coef_k delta_k is formed once, in k_retract,
+  // in the serial order (no eta read / write per Hess-vec). With tcg_max >
+  // dhn, k_hess folds the dhn oldest directions into eta before a buffer is
+  // reused (same order of additions).
+  double* dh;          // [dhn][vec]
+  double* eta;         // [vec] folded directions (tcg_max > dhn only)
+  double* coefh;       // [L][tcg_max] the eta coefficient (alpha or tau) of each step
+  long long vec;       // doubles per vector
+  int dhn;
   double* part;        // [ntiles][NPART]
   double* part_h;      // [ntiles][2] k_hess partials (RM_CONSUMER: read by k_update)
   double* part_u;      // [ntiles][2] k_update partials (RM_CONSUMER: read by the next k_hess)
@@ -161,6 +171,7 @@ struct Dev {
 };
 
 constexpr int HV_SLOTS = 1 << 16;
+constexpr int DHMAX = 10;  // tCG directions kept per block update (Dev::dh; dpgo's default tcg_max)
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -872,6 +883,7 @@ __device__ __forceinline__ void control_core(Ctl& c, const Dev& d, int l, int ki
   } else if (kind == RED_HESS) {
     const double d_Hd = tot[0];
     const HessStep hs = hess_step(c.z_r, c.e_Pe, c.e_Pd, c.d_Pd, c.Delta, d_Hd);
+    if (side) d.coefh[(size_t)l * P.tcg_max + min(c.tcg_iter, P.tcg_max - 1)] = hs.coef;  // delta_k's eta coefficient
     c.tcg_iter += 1;
     c.hessvecs += 1;
     if (side) {
@@ -1235,12 +1247,12 @@ __device__ __forceinline__ void body_grad(const Dev& d, int gated, char* smem) {
 
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old;
-// partial <delta, Hdelta>.
+// partial <delta, Hdelta>. delta_k is kept for k_retract's eta (Dev::dh).
 template <int R, int RW, int RM>
 __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs, unsigned long long seq, char* smem) {
   const Lane L = lane_map<R>(d);
   int tcg_iter;
-  double beta, pcoef;  // pcoef: the previous step's eta coefficient (alpha or tau)
+  double beta;
   double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4], S[9];
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   if constexpr (RM == RM_CONSUMER) {
@@ -1307,7 +1319,6 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
     if (!go) return;
     tcg_iter = grad ? 0 : c0.tcg_iter;
     beta = u.beta;
-    pcoef = c0.coef;
   } else {
     // the phase test runs once the first chunk's records are in flight (a
     // robot out of tCG leaves before any row is gathered)
@@ -1315,7 +1326,6 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
     if (!hinc_gather<R, RW, true>(d, L, d.z, H, smem, [&]() { return c.phase == PH_TCG; })) return;
     tcg_iter = c.tcg_iter;
     beta = c.beta;
-    pcoef = c.coef;
   }
   const bool first = (tcg_iter == 0);
   asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
@@ -1330,37 +1340,49 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
   double hz[4];
   group_rhess<R, true>(y, zs, H, S, L.base, hz, reinterpret_cast<double*>(smem));
   double v = 0.0;
-  double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0};
+  double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
+  const int dhn = d.dhn;
   if (L.valid) {
     if (first) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) { dl[k] = -zs[k]; hdl[k] = -hz[k]; }
     } else {
       double dold[4], hold[4];
-      load4(d.del + o, dold);
+      load4(d.dh + (size_t)((tcg_iter - 1) % dhn) * d.vec + o, dold);
       load4(d.hd + o, hold);
-      if (tcg_iter > 1) load4(d.eta + o, et);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         dl[k] = -zs[k] + beta * dold[k];
         hdl[k] = -hz[k] + beta * hold[k];
-        et[k] += pcoef * dold[k];  // the previous step's eta update, deferred from k_update
+      }
+      if (tcg_iter >= dhn && tcg_iter % dhn == 0) {
+        // tcg_max > dhn only: delta_k goes into the oldest direction's buffer,
+        // so the dhn directions k - dhn .. k - 1 join eta first, in step order
+        double et[4] = {0, 0, 0, 0};
+        if (tcg_iter > dhn) load4(d.eta + o, et);
+        const double* ch = d.coefh + (size_t)L.l * d.p.tcg_max;
+        for (int j = tcg_iter - dhn; j < tcg_iter; ++j) {
+          double dj[4];
+          load4(d.dh + (size_t)(j % dhn) * d.vec + o, dj);
+          const double cj = ch[j];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) et[k] += cj * dj[k];
+        }
+        store4(d.eta + o, et);
       }
     }
     v = dl[0] * hdl[0] + dl[1] * hdl[1] + dl[2] * hdl[2] + dl[3] * hdl[3];
   }
   finish_tile<RED_HESS, 1, RM>(d, L, &v, smem + SmemH<R>::red_off, [&]() {
     if (L.valid) {
-      store4(d.del + o, dl);
+      store4(d.dh + (size_t)(tcg_iter % dhn) * d.vec + o, dl);
       store4(d.hd + o, hdl);
-      if (!first) store4(d.eta + o, et);
     }
   });
 }
 
-// tCG step, part 2: r += coef Hdelta (eta += coef delta is deferred to the next
-// k_hess, which reads delta anyway, or to k_retract); interior steps also
-// z = precon(r) and partials <r,r>, <z,r>.
+// tCG step, part 2: r += coef Hdelta (eta = sum coef_k delta_k is formed in
+// k_retract); interior steps also z = precon(r) and partials <r,r>, <z,r>.
 template <int R, int RM>
 __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsigned long long seq, int slot,
                                             char* smem) {
@@ -1483,13 +1505,32 @@ __device__ __forceinline__ void body_retract(const Dev& d, int fold, char* smem)
   }
   if (L.valid) {  // all rows in flight before the Gram-Schmidt chain
     load4(d.X + o, x);
-    if (c.tcg_iter > 1) load4(d.eta + o, et);  // eta after the last step's update is eta + coef delta
-    load4((d.p.rgd ? d.z : d.del) + o, dl);    // RGD: eta = -s z
     load4(d.g + o, gg);
     load4(d.r + o, rr);
-    const double coef = c.coef;
+    if (d.p.rgd) {  // RGD: eta = -s z
+      load4(d.z + o, dl);
+      const double coef = c.coef;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) et[k] += coef * dl[k];
+      for (int k = 0; k < 4; ++k) et[k] += coef * dl[k];
+    } else {
+      // eta = sum_k coef_k delta_k over the T steps, in step order; the first
+      // F directions were folded into d.eta by k_hess (tcg_max > dhn only)
+      const int T = c.tcg_iter, dhn = d.dhn;
+      const int F = T > 0 ? (T - 1) / dhn * dhn : 0;
+      if (F > 0) load4(d.eta + o, et);
+      double dd[DHMAX][4];
+#pragma unroll
+      for (int i = 0; i < DHMAX; ++i)
+        if (F + i < T) load4(d.dh + (size_t)i * d.vec + o, dd[i]);
+      const double* ch = d.coefh + (size_t)L.l * d.p.tcg_max;
+#pragma unroll
+      for (int i = 0; i < DHMAX; ++i)
+        if (F + i < T) {
+          const double cj = ch[F + i];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) et[k] += cj * dd[i][k];
+        }
+    }
   }
   double xt[4];
   group_retract<R>(x, et, L.base, xt);
@@ -2093,7 +2134,8 @@ struct kmx_pgo {
   double* d_rec = nullptr;
   double *d_ekappa = nullptr, *d_etau = nullptr, *d_ew = nullptr;
   int2* d_eipos = nullptr;
-  double* d_vec = nullptr;  // X Xt g r z eta del hd
+  double* d_vec = nullptr;  // X Xt g r z hd eta, then the dhn tCG directions (nvec())
+  double* d_coefh = nullptr;  // [L][tcg_max]
   double *d_S = nullptr, *d_Pinv = nullptr, *d_hD = nullptr, *d_pub = nullptr, *d_part = nullptr;
   Ctl* d_ctl = nullptr;
   Ctl* d_ctl2 = nullptr;
@@ -2230,7 +2272,7 @@ void free_dev(kmx_pgo* h) {
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
                   h->d_accV, h->d_accY, h->d_ctl2, h->d_part_h,
-                  h->d_part_u};
+                  h->d_part_u, h->d_coefh};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile = nullptr;
@@ -2254,6 +2296,7 @@ void free_dev(kmx_pgo* h) {
   h->d_hv_launch = nullptr;
   h->d_accV = h->d_accY = nullptr;
   h->d_ctl2 = nullptr;
+  h->d_coefh = nullptr;
   h->d_part_h = h->d_part_u = nullptr;
 }
 
@@ -2267,6 +2310,10 @@ hipEvent_t next_event(kmx_pgo* h) {
 }
 
 bool ready(kmx_pgo* h) { return h && h->d_vec != nullptr; }
+
+// Vectors of d_vec: X Xt g r z hd eta + the tCG directions kept for k_retract.
+int dh_count(const kmx_pgo* h) { return std::max(1, std::min(h->P.tcg_max_iterations, DHMAX)); }
+size_t nvec(const kmx_pgo* h) { return 7 + (size_t)dh_count(h); }
 
 // Scratch of the diagnostic / output entry points (not resident with the graph).
 int ensure_scratch(kmx_pgo* h, size_t doubles) {
@@ -2872,7 +2919,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_rec, rec.size())) ||
       (rc = dalloc(&h->d_ekappa, ek_h.size())) || (rc = dalloc(&h->d_etau, et_h.size())) ||
       (rc = dalloc(&h->d_ew, ew_h.size())) || (rc = dalloc(&h->d_eipos, eipos.size())) ||
-      (rc = dalloc(&h->d_vec, vec * 8)) || (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 6)) ||
+      (rc = dalloc(&h->d_vec, vec * nvec(h))) || (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 6)) ||
       (rc = dalloc(&h->d_Pinv, (size_t)std::max(nloc, 1) * SYM4)) ||
       (rc = dalloc(&h->d_hD, (size_t)std::max(nloc, 1) * SYM4)) ||
       (rc = dalloc(&h->d_pub, (size_t)std::max<int64_t>(h->npub, 1) * ps)) ||
@@ -2888,7 +2935,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_sh_idx, std::max(h->n_sh_local, 1))) || (rc = dalloc(&h->d_active, L)) ||
       (rc = dalloc(&h->d_osh_edge, std::max(h->n_osh, 1))) || (rc = dalloc(&h->d_osh_idx, std::max(h->n_osh, 1))) ||
       (rc = dalloc(&h->d_relc, L)) || (rc = dalloc(&h->d_gnc, 2)) || (rc = dalloc(&h->d_ext, 64)) ||
-      (rc = dalloc(&h->d_hv_launch, HV_SLOTS))) {
+      (rc = dalloc(&h->d_hv_launch, HV_SLOTS)) ||
+      (rc = dalloc(&h->d_coefh, (size_t)L * std::max(h->P.tcg_max_iterations, 1)))) {
     free_dev(h);
     return rc;
   }
@@ -2914,7 +2962,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(up(h->d_etau, et_h.data(), sizeof(double) * et_h.size()));
   KMX_HIP(up(h->d_ew, ew_h.data(), sizeof(double) * ew_h.size()));
   KMX_HIP(up(h->d_eipos, eipos.data(), sizeof(int2) * eipos.size()));
-  KMX_HIP(hipMemsetAsync(h->d_vec, 0, sizeof(double) * vec * 8, h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_vec, 0, sizeof(double) * vec * nvec(h), h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_coefh, 0, sizeof(double) * L * std::max(h->P.tcg_max_iterations, 1), h->stream));
   KMX_HIP(hipMemsetAsync(h->d_pub, 0, sizeof(double) * std::max<int64_t>(h->npub, 1) * ps, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_ctl, 0, sizeof(Ctl) * L, h->stream));
   KMX_HIP(hipMemsetAsync(h->d_cnt, 0, sizeof(Counters), h->stream));
@@ -2966,7 +3015,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   d.inc_ptr = h->d_inc_ptr; d.rec = h->d_rec;
   d.ekappa = h->d_ekappa; d.etau = h->d_etau; d.ew = h->d_ew; d.eipos = h->d_eipos;
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
-  d.z = h->d_vec + 4 * vec; d.eta = h->d_vec + 5 * vec; d.del = h->d_vec + 6 * vec; d.hd = h->d_vec + 7 * vec;
+  d.z = h->d_vec + 4 * vec; d.hd = h->d_vec + 5 * vec; d.eta = h->d_vec + 6 * vec; d.dh = h->d_vec + 7 * vec;
+  d.coefh = h->d_coefh; d.vec = (long long)vec; d.dhn = dh_count(h);
   d.S = h->d_S; d.Pinv = h->d_Pinv; d.hD = h->d_hD; d.pub = h->d_pub; d.part = h->d_part;
   d.ctl = h->d_ctl; d.cnt = h->d_cnt;
   d.ctl2 = h->d_ctl2; d.part_h = h->d_part_h; d.part_u = h->d_part_u;
@@ -3632,7 +3682,8 @@ extern "C" int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_byt
   int64_t b = 0;
   b += (int64_t)(h->ninc + 1) * h->rw * 8 + (int64_t)(h->nloc + 1) * 4;  // records, CSR
   b += (int64_t)std::max(h->mloc, 1) * (3 * 8 + 8);                      // kappa, tau, w, positions
-  b += n * ps * 8 * 8 + n * (6 + SYM4 + SYM4) * 8;                       // vectors, S, Pinv, D
+  b += n * ps * 8 * (int64_t)nvec(h) + n * (6 + SYM4 + SYM4) * 8;       // vectors, S, Pinv, D
+  b += L * 8 * (int64_t)std::max(h->P.tcg_max_iterations, 1);            // tCG coefficients
   b += std::max<int64_t>(h->npub, 1) * (ps * 8 + 4) + n * 4;             // public table + maps
   b += (int64_t)h->ntiles * (NPART * 8 + 12) + L * (int64_t)(sizeof(Ctl) + 32);
   b += (int64_t)std::max(h->n_gnc, 1) * 12 + (int64_t)h->scratch_cap * 8;  // GNC lists, scratch in use

@@ -361,6 +361,35 @@ def test_round_structure_matches_oracle(gpu, monkeypatch, red, case):
         assert d <= 1e-6, (a, d)
 
 
+@pytest.mark.parametrize("red", ["0", "2"])
+def test_long_tcg_folds_directions(gpu, monkeypatch, red):
+    """tCG longer than the directions the handle keeps (DHMAX = 10): k_hess folds
+    the oldest ten directions into eta before their buffers are reused (steps 10
+    and 20 of a 25-step cap) and k_retract adds the rest, in step order; the
+    rounds match the restatement, whose eta is one running sum."""
+    monkeypatch.setenv("KMX_RED", red)
+    # no outliers, start near the optimum: positive curvature, so tCG stops on
+    # its residual test (kappa 1e-8) rather than at the trust-region boundary
+    g, P, X0 = _setup(robust=False, seed=4, perturb=0.01, outlier=0.0)
+    lo = P.localOptimizationParams
+    lo.RTR_tCG_iterations = 25
+    lo.tCG_kappa = 1e-8  # long inner solves: the residual test needs many steps
+    lo.RTR_initial_radius, lo.RTR_max_radius = 1e4, 1e6
+    s, o = _pair(g, P, X0)
+    longest = 0
+    for it in range(8):
+        s.refresh_local()
+        sg = s.iterate()
+        so = o.iterate()
+        for a in range(g.n_robots):
+            assert sg[a]["tcg_iterations"] == so[a]["tcg_iterations"], (it, a, sg[a], so[a])
+            assert sg[a]["accepted"] == so[a]["accepted"], (it, a)
+            longest = max(longest, sg[a]["tcg_iterations"])
+            d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
+            assert d <= 1e-6, (it, a, d)
+    assert longest > 10, longest  # the fold ran
+
+
 def test_large_robot_block_matches_oracle(gpu):
     """One 12.5k-pose robot block (the per-GPU share of configs[3] at N = 8): the
     finer tile cut gives it ~700 tiles, more than the 2 x 256 partials the
