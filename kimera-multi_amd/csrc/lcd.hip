@@ -579,6 +579,21 @@ __device__ void refit_3d3d(int n, Fetch&& fetch, double R[9], double t[3]) {
 // Diagnostic phase timers (kmx_lcd_debug_phase_times): cycles per phase summed
 // over the first 64 candidates' hypotheses.
 __device__ unsigned long long g_phase[16];
+// KMX_RS_PROF=2 (diagnostic): each candidate's wave start / end (wall clock,
+// 100 MHz) for the first STAMPS candidates of a launch: loaded latency and
+// resident waves over time (scripts/lcd_stamps.py)
+constexpr int STAMPS = 1 << 16;
+__device__ unsigned long long g_stamp[2 * STAMPS];
+struct WaveStamp {
+  int c;
+  bool on;
+  __device__ WaveStamp(int c_, bool on_) : c(c_), on(on_ && c_ < STAMPS) {
+    if (on && threadIdx.x == 0) g_stamp[2 * c] = wall_clock64();
+  }
+  __device__ ~WaveStamp() {
+    if (on && threadIdx.x == 0) g_stamp[2 * c + 1] = wall_clock64();
+  }
+};
 #define KMX_PT(i)                                                              \
   do {                                                                         \
     if (prof && lane == 0) {                                                   \
@@ -641,6 +656,26 @@ __device__ __forceinline__ void wsync() {
   asm volatile("" ::: "memory");
 }
 
+// The lane index as an opaque value at the start of each phase: the phases'
+// lane-derived indices and LDS addresses are then formed where they are used
+// instead of being hoisted out of the hypothesis loop by the compiler, where
+// dozens of them stayed live across every phase (168 VGPRs + 596 B of scratch
+// per lane, and the scratch-backed waves capped the resident waves).
+__device__ __forceinline__ int fresh_lane(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
+}
+
+// Candidate of workgroup b: blocks b and b + 8 run on the same XCD (the XCDs
+// take workgroups round robin, statically), so XCD x is given one contiguous
+// range of the candidates instead of every eighth one — a list whose costly
+// candidates fall on a stride (the synthetic pools alternate true / false
+// pairs: every true one went to the even XCDs) no longer leaves XCDs idle.
+__device__ __forceinline__ int xcd_candidate(int b, int nwg) {
+  const int q = nwg >> 3, rr = nwg & 7, x = b & 7;
+  return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
+}
+
 __device__ __forceinline__ double rdlane(double v, int src) {  // src wave-uniform
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)b, src);
@@ -657,6 +692,7 @@ __device__ __forceinline__ double wave_fmax(double v) {  // exact in any order
 // formed from readlane broadcasts in the serial order, each d_j from a
 // 9-term gather of column j. Then the 4 back-substitutions (lanes 0-3).
 __device__ void coop_nullspace(CoopWS& w, int lane) {
+  lane = fresh_lane(lane);
   const int li = lane % 9, lj = lane / 9;  // lanes >= 45 carry a dummy column
   double a = (lane < 45) ? w.f1[3 * lj + li / 3] * w.f2[3 * lj + li % 3] : 0.0;
 #pragma unroll
@@ -747,6 +783,7 @@ __device__ __forceinline__ double mul21_e(const double* a, const CoopWS& w, int 
 }
 
 __device__ void coop_system(CoopWS& w, int lane) {
+  lane = fresh_lane(lane);
   // EEt[ij][k] = sum_l mul11(E[i*3+l], E[j*3+l])[k] (l = 0, 1, 2 in order); c2 for row 9:
   // c2_q = mul11(E_a, E_b) - mul11(E_c, E_d), (a, b, c, d) = (4,8,5,7), (3,8,5,6), (3,7,4,6)
   for (int t = lane; t < 90 + 30; t += RS_BLOCK) {
@@ -790,6 +827,7 @@ __device__ void coop_system(CoopWS& w, int lane) {
 // graded: the columns are first permuted to Stewenius' graded order GORD.
 __constant__ signed char GORD_D[20] = {0, 2, 4, 3, 8, 10, 1, 6, 13, 16, 5, 9, 11, 7, 14, 17, 12, 15, 18, 19};
 __device__ int coop_gj(CoopWS& w, int lane, bool graded) {
+  lane = fresh_lane(lane);
   const int cl = lane < 20 ? lane : 19;  // lanes >= 20 shadow column 19, never store
   const int src = graded ? GORD_D[cl] : cl;
   double a[10];
@@ -915,6 +953,7 @@ __device__ double refine_root_reg(const double c[11], double a, double b) {
 // then the 64-ary isolation with one point per lane and one lane per root.
 // Leaves w.nr roots in ascending order in w.roots.
 __device__ void coop_roots(CoopWS& w, int lane, bool prof) {
+  lane = fresh_lane(lane);
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   if (lane < 45) {  // Bp[q][c][i]
     const int q = lane / 15, c = (lane / 5) % 3, i = lane % 5;
@@ -1058,6 +1097,7 @@ __device__ void coop_decompose(CoopWS& w, int lane, bool ok_root, const double E
 
 // Essential matrices from the roots (lane per root), then coop_decompose.
 __device__ void coop_models(CoopWS& w, int lane) {
+  lane = fresh_lane(lane);
   const int nr = w.nr;
   int ok_root = 0;
   double Eo[9];
@@ -1089,6 +1129,7 @@ __device__ void coop_models(CoopWS& w, int lane) {
 // the 4 decompositions scored on the sample; the first minimum in (E, cand)
 // order wins, as in model_from_sample. Result in w.mR / w.mt, w.ok.
 __device__ void coop_decompose(CoopWS& w, int lane, bool ok_root, const double Eo[9]) {
+  lane = fresh_lane(lane);
   const unsigned long long m = __ballot(ok_root);
   const int slot = __popcll(m & ((1ull << lane) - 1ull));
   const int ne = __popcll(m);
@@ -1173,6 +1214,7 @@ __device__ __forceinline__ double c_abs1(cplx_d a) { return fabs(a.re) + fabs(a.
 // pivot.
 __device__ __forceinline__ cplx_d shfl_c(cplx_d v, int src) { return {__shfl(v.re, src, 64), __shfl(v.im, src, 64)}; }
 __device__ __forceinline__ int eigvec_col(const double mcol[10], int lane, cplx_d lam, double xyz[3]) {
+  lane = fresh_lane(lane);
   const int g0 = (lane / 10) * 10, c = lane - g0 < 10 ? lane - g0 : 9;
   cplx_d b[10];
 #pragma unroll
@@ -1284,6 +1326,7 @@ __device__ __forceinline__ double grp_bcast(double v, int g, int src) { return _
 // element (the serial loop's element operations, same order of the dependent
 // steps).
 __device__ void grp_hessenberg(StewBatch& sb, int lane, bool on) {
+  lane = fresh_lane(lane);
   const int g = lane / GL, gl = lane - g * GL;
   double (*a)[10] = sb.H[g < SG ? g : 0];
   const int n = 10, la = n - 2;
@@ -1332,6 +1375,7 @@ __device__ void grp_hessenberg(StewBatch& sb, int lane, bool on) {
 // (a complex pair: wi(na) = +, wi(en) = -); sb.ok[g] = 0 when the group's
 // 30 n sweeps ran out.
 __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
+  lane = fresh_lane(lane);
   const int g = lane / GL, gl = lane - g * GL;
   double (*h)[10] = sb.H[g < SG ? g : 0];
   const int n = 10;
@@ -1536,6 +1580,7 @@ __device__ __forceinline__ double action_entry(const double* C6, int i, int j) {
 // order, as coop_decompose does for one. sb.mok[b] = 0: no model.
 __device__ __forceinline__ void stew_models(StewBatch& sb, double* stash, int lane, const double* F1, const double* F2,
                                             const short* tab, int p0, int nb, bool prof) {
+  lane = fresh_lane(lane);
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   int np;
   {  // solution list
@@ -1594,33 +1639,34 @@ __device__ __forceinline__ void stew_models(StewBatch& sb, double* stash, int la
     for (int i = 0; i < 9; ++i) Eo[i] = Es[lane * 9 + i];
     double U[9], sv[3], V[9];
     svd3(Eo, U, sv, V);
-    double Ra[9], Rb[9];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        const double uw0 = U[i * 3 + 1], uw1 = -U[i * 3 + 0], uw2 = U[i * 3 + 2];
-        Ra[i * 3 + j] = uw0 * V[j * 3 + 0] + uw1 * V[j * 3 + 1] + uw2 * V[j * 3 + 2];
-        const double uv0 = -U[i * 3 + 1], uv1 = U[i * 3 + 0], uv2 = U[i * 3 + 2];
-        Rb[i * 3 + j] = uv0 * V[j * 3 + 0] + uv1 * V[j * 3 + 1] + uv2 * V[j * 3 + 2];
-      }
-    const bool na = det3(Ra) < 0.0, nbn = det3(Rb) < 0.0;
-    for (int i = 0; i < 9; ++i) {
-      Ra[i] = na ? -Ra[i] : Ra[i];
-      Rb[i] = nbn ? -Rb[i] : Rb[i];
-    }
     const double* f1 = sb.f1[eb];
     const double* f2 = sb.f2[eb];
-    for (int cand = 0; cand < 4; ++cand) {
-      double R[9], t[3];
-      for (int i = 0; i < 9; ++i) R[i] = (cand >> 1) ? Rb[i] : Ra[i];
-      const double sg = (cand & 1) ? -1.0 : 1.0;
-      for (int i = 0; i < 3; ++i) t[i] = sg * U[i * 3 + 2];
-      double err = 0.0;
-      for (int i = 0; i < 5; ++i) err += model_error(R, t, f1 + 3 * i, f2 + 3 * i);
-      if (err < DBL_MAX && (!valid || err < best)) {
-        valid = true;
-        best = err;
-        for (int i = 0; i < 9; ++i) bR[i] = R[i];
-        for (int i = 0; i < 3; ++i) bt[i] = t[i];
+    // the two rotations one after the other (Ra: candidates 0, 1; Rb: 2, 3),
+    // so only one is live: Ra = (U1, -U0, U2) V^T, Rb = (-U1, U0, U2) V^T
+    // (the negations are exact: the same bits as forming both at once)
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      double Rh[9];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+          const double u0 = h ? -U[i * 3 + 1] : U[i * 3 + 1], u1 = h ? U[i * 3 + 0] : -U[i * 3 + 0],
+                       u2 = U[i * 3 + 2];
+          Rh[i * 3 + j] = u0 * V[j * 3 + 0] + u1 * V[j * 3 + 1] + u2 * V[j * 3 + 2];
+        }
+      const bool neg = det3(Rh) < 0.0;
+      for (int i = 0; i < 9; ++i) Rh[i] = neg ? -Rh[i] : Rh[i];
+      for (int cs = 0; cs < 2; ++cs) {
+        double t[3];
+        const double sg = cs ? -1.0 : 1.0;
+        for (int i = 0; i < 3; ++i) t[i] = sg * U[i * 3 + 2];
+        double err = 0.0;
+        for (int i = 0; i < 5; ++i) err += model_error(Rh, t, f1 + 3 * i, f2 + 3 * i);
+        if (err < DBL_MAX && (!valid || err < best)) {
+          valid = true;
+          best = err;
+          for (int i = 0; i < 9; ++i) bR[i] = Rh[i];
+          for (int i = 0; i < 3; ++i) bt[i] = t[i];
+        }
       }
     }
   }
@@ -1720,8 +1766,9 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
                                                           double* fbuf) {
   __shared__ CoopWS w;
   __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;  // Stewenius: the batch
-  const int c = blockIdx.x;
+  const int c = xcd_candidate(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
+  const WaveStamp stamp(c, P.prof == 2);
   const int K = Kin[c];
   const int q = cq[c], m = cm[c];
   unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
@@ -1755,7 +1802,7 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
   double kk = 1.0;
   const int max_skip = P.max_iter * 10;
   const short* tab = table + (size_t)(K - 5) * P.pmax * 5;
-  const bool prof = (c < 64) && P.prof;
+  const bool prof = (c < 64) && P.prof == 1;
   bool done = false;
   // the serial loop's bookkeeping of one hypothesis's model (w.ok, w.mR, w.mt):
   // a failed solve counts as skipped; otherwise its inliers, the best model and
@@ -2003,7 +2050,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_recover(const double* bearings, co
                                                       unsigned char* masks) {
   constexpr int S = PNP ? PNP_S : 3;
   extern __shared__ __attribute__((aligned(16))) double sm_d[];
-  const int c = blockIdx.x;
+  const int c = xcd_candidate(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
   kmx_lcd_result* R_ = res + c;
   if (R_->mono_inliers < P.min2d) return;
@@ -2279,7 +2326,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
     const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
     auto kc = stew ? ((clb >= 8) ? k_ransac_coop<8, true> : (clb >= 6) ? k_ransac_coop<6, true>
                       : (clb >= 5) ? k_ransac_coop<5, true> : (clb == 4) ? k_ransac_coop<4, true>
-                      : k_ransac_coop<3, true>)
+                      : (clb == 2) ? k_ransac_coop<2, true> : k_ransac_coop<3, true>)
                    : ((clb >= 8) ? k_ransac_coop<8, false> : (clb >= 6) ? k_ransac_coop<6, false>
                       : (clb >= 5) ? k_ransac_coop<5, false> : k_ransac_coop<4, false>);
     hipLaunchKernelGGL(kc, dim3(n), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
@@ -2334,7 +2381,7 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
     return kmx::fail(KMX_EHIP, "hipStreamCreate");
   }
   h->own_stream = true;
-  if (const char* v = std::getenv("KMX_RS_PROF")) h->prof = std::atoi(v) ? 1 : 0;
+  if (const char* v = std::getenv("KMX_RS_PROF")) h->prof = std::atoi(v);
   *out = h;
   return KMX_OK;
   KMX_GUARD_END
@@ -2521,6 +2568,14 @@ extern "C" int kmx_lcd_knn2(int norm, double lowe_ratio, const uint8_t* q, int32
   *k = K;
   return KMX_OK;
   KMX_GUARD_END
+}
+
+// Diagnostic (KMX_RS_PROF=2): the per-candidate wave start / end stamps of the
+// last launch, n <= 65536 pairs.
+extern "C" int kmx_lcd_debug_wave_stamps(unsigned long long* out, int n) {
+  n = std::max(0, std::min(n, STAMPS));
+  KMX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(unsigned long long) * 2 * n));
+  return KMX_OK;
 }
 
 // Diagnostic: read (and reset) the k_ransac_coop phase timers (wall-clock ticks).

@@ -140,11 +140,11 @@ struct Dev {
   double* ew;          // GNC weight
   const int2* eipos;   // [mloc] record positions (tail, head) of each local edge, -1 if not local
   double *X, *Xt, *g, *r, *z, *hd, *S, *Pinv, *hD, *pub;
-  // tCG search directions: delta_k lives in dh + (k % dhn) * vec for the whole
-  // block update, so eta = sum_k coef_k delta_k is formed once, in k_retract,
-  // in the serial order (no eta read / write per Hess-vec). With tcg_max >
-  // dhn, k_hess folds the dhn oldest directions into eta before a buffer is
-  // reused (same order of additions).
+  // tCG search directions: delta_k lives in dh + (k % dhn) * vec, so eta =
+  // sum_k coef_k delta_k is not updated at every Hess-vec: k_hess folds the
+  // dhn oldest directions into eta before their buffer is reused (every dhn
+  // steps) and k_retract adds the rest, in step order (the additions of the
+  // serial eta += coef delta, same bits).
   double* dh;          // [dhn][vec]
   double* eta;         // [vec] folded directions (tcg_max > dhn only)
   double* coefh;       // [L][tcg_max] the eta coefficient (alpha or tau) of each step
@@ -171,7 +171,15 @@ struct Dev {
 };
 
 constexpr int HV_SLOTS = 1 << 16;
-constexpr int DHMAX = 10;  // tCG directions kept per block update (Dev::dh; dpgo's default tcg_max)
+// tCG directions kept (Dev::dh). Same-box A/B at configs[3] (profiles/r03/dhist/):
+// all ten (eta formed only in k_retract) gives the fastest k_hess (38.2 vs
+// 40.5 us) but k_retract then reads up to ten vectors, and the round is 1.7 %
+// slower; two (eta folded at every second step) keeps the round at the
+// one-buffer form's time or better with half its eta traffic in k_hess.
+#ifndef KMX_DHMAX
+#define KMX_DHMAX 2
+#endif
+constexpr int DHMAX = KMX_DHMAX;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -1363,7 +1371,12 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
         const double* ch = d.coefh + (size_t)L.l * d.p.tcg_max;
         for (int j = tcg_iter - dhn; j < tcg_iter; ++j) {
           double dj[4];
-          load4(d.dh + (size_t)(j % dhn) * d.vec + o, dj);
+          if (j + 1 < tcg_iter) {
+            load4(d.dh + (size_t)(j % dhn) * d.vec + o, dj);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dj[k] = dold[k];
+          }
           const double cj = ch[j];
 #pragma unroll
           for (int k = 0; k < 4; ++k) et[k] += cj * dj[k];

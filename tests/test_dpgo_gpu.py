@@ -363,10 +363,10 @@ def test_round_structure_matches_oracle(gpu, monkeypatch, red, case):
 
 @pytest.mark.parametrize("red", ["0", "2"])
 def test_long_tcg_folds_directions(gpu, monkeypatch, red):
-    """tCG longer than the directions the handle keeps (DHMAX = 10): k_hess folds
-    the oldest ten directions into eta before their buffers are reused (steps 10
-    and 20 of a 25-step cap) and k_retract adds the rest, in step order; the
-    rounds match the restatement, whose eta is one running sum."""
+    """Long tCG (25-step cap, residual test at kappa 1e-8): k_hess folds the kept
+    directions (DHMAX, pgo.hip) into eta before their buffers are reused, at
+    every DHMAX-th step, and k_retract adds the rest, in step order; the rounds
+    match the restatement, whose eta is one running sum."""
     monkeypatch.setenv("KMX_RED", red)
     # no outliers, start near the optimum: positive curvature, so tCG stops on
     # its residual test (kappa 1e-8) rather than at the trust-region boundary
