@@ -40,6 +40,7 @@ namespace {
 
 constexpr int KNN_BLOCK = 256;
 constexpr int RS_BLOCK = 64;          // one wavefront per candidate
+constexpr int RS_MAX_SLOTS = 8192;    // k_ransac_coop waves per launch at most (256 CUs x 32 waves)
 constexpr int MAX_FEATS = 1024;
 
 // ------------------------------------------------------------------ knn2 --
@@ -1758,16 +1759,14 @@ __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* sta
   KMX_PT(8);
 }
 
-template <int LB, bool STEW>
-__global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bearings, const double* points, int N,
-                                                          const int* cq, const int* cm, const int2* pairs,
-                                                          const int* Kin, const short* table, RsParams P,
-                                                          kmx_lcd_result* res, unsigned char* masks,
-                                                          double* fbuf) {
-  __shared__ CoopWS w;
-  __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;  // Stewenius: the batch
-  const int c = xcd_candidate(blockIdx.x, gridDim.x);
-  const int lane = threadIdx.x;
+// One candidate's 2D-2D RANSAC and 3D-3D recovery by the calling wave; F1 is
+// the wave's global scratch (6 N + STASH doubles).
+template <bool STEW, typename SB>
+__device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, double* F1, const double* bearings,
+                                                 const double* points, int N, const int* cq, const int* cm,
+                                                 const int2* pairs, const int* Kin, const short* table,
+                                                 const RsParams& P, kmx_lcd_result* res, unsigned char* masks) {
+  const int lane = fresh_lane(threadIdx.x);
   const WaveStamp stamp(c, P.prof == 2);
   const int K = Kin[c];
   const int q = cq[c], m = cm[c];
@@ -1783,7 +1782,6 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
     return;
   }
   // compact bearings of the match pairs (global scratch, L1/L2 resident)
-  double* F1 = fbuf + (size_t)c * (6 * N + STASH);
   double* stash = F1 + 6 * N;  // Stewenius: the batch's action matrices and null spaces
   double* F2 = F1 + 3 * N;
   const int2* pl = pairs + (size_t)c * N;
@@ -1994,6 +1992,35 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
   }
 }
 
+
+// k_ransac_coop: a work queue over the candidates. The launch holds as many
+// one-wave workgroups as are resident at once; each wave takes the next
+// candidate from a counter until none is left (every wave reaches the exit
+// test). The candidates' costs differ by orders of magnitude (no RANSAC below
+// 5 matches; ~30 hypotheses for a true loop closure; up to max_iter), so a
+// static candidate -> workgroup map leaves slots idle: with the synthetic
+// pools' alternating true / false pairs the statically dispatched form kept
+// only half of the 12 waves per CU busy (profiles/r03/lcd/occupancy/). The
+// scratch is per wave (blockIdx), reused from candidate to candidate.
+template <int LB, bool STEW>
+__global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bearings, const double* points, int N,
+                                                          const int* cq, const int* cm, const int2* pairs,
+                                                          const int* Kin, const short* table, RsParams P,
+                                                          kmx_lcd_result* res, unsigned char* masks,
+                                                          double* fbuf, int n, int* next) {
+  __shared__ CoopWS w;
+  __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;  // Stewenius: the batch
+  double* F1 = fbuf + (size_t)blockIdx.x * (6 * N + STASH);
+  for (;;) {
+    int c = 0;
+    if (threadIdx.x == 0) c = atomicAdd(next, 1);
+    c = __shfl(c, 0, 64);
+    if (c >= n) break;
+    ransac_candidate<STEW>(c, w, sb, F1, bearings, points, N, cq, cm, pairs, Kin, table, P, res, masks);
+    __threadfence_block();
+    wsync();
+  }
+}
 
 // Arun 3-point model (oracle arun_model): centroids, H = sum dm dq^T, Kabsch
 // with svd3, t = c_q - R c_m (p_q = R p_m + t).
@@ -2218,7 +2245,8 @@ struct kmx_lcd {
   int2* d_pairs = nullptr;
   kmx_lcd_result* d_res = nullptr;
   unsigned char* d_mask = nullptr;
-  double* d_fbuf = nullptr;  // [cap][6 N + STASH] compact match bearings + Stewenius stash (k_ransac_coop)
+  double* d_fbuf = nullptr;  // [slots][6 N + STASH] compact match bearings + Stewenius stash, per k_ransac_coop wave
+  int* d_next = nullptr;     // k_ransac_coop's work-queue counter
   int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
   // kmx_lcd_enable_timing: events around the kNN2 and the RANSAC launches
   bool timing = false;
@@ -2235,11 +2263,12 @@ void lcd_free_pool(kmx_lcd* h) {
   h->d_desc = nullptr; h->d_bear = h->d_pts = nullptr; h->d_nfeat = nullptr; h->d_table = nullptr; h->d_table_rec = nullptr;
 }
 void lcd_free_cand(kmx_lcd* h) {
-  void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask, h->d_fbuf};
+  void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask, h->d_fbuf, h->d_next};
   for (void* x : p)
     if (x) (void)hipFree(x);
   h->d_cq = h->d_cm = h->d_K = nullptr; h->d_pairs = nullptr; h->d_res = nullptr; h->d_mask = nullptr;
   h->d_fbuf = nullptr;
+  h->d_next = nullptr;
   h->cap = 0;
 }
 
@@ -2280,7 +2309,8 @@ int ensure_cap(kmx_lcd* h, int n) {
       hipMalloc(&h->d_pairs, sizeof(int2) * (size_t)cap * h->N) != hipSuccess ||
       hipMalloc(&h->d_res, sizeof(kmx_lcd_result) * cap) != hipSuccess ||
       hipMalloc(&h->d_mask, (size_t)cap * h->N) != hipSuccess ||
-      hipMalloc(&h->d_fbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * cap) != hipSuccess) {
+      hipMalloc(&h->d_fbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::min(cap, RS_MAX_SLOTS)) != hipSuccess ||
+      hipMalloc(&h->d_next, sizeof(int)) != hipSuccess) {
     lcd_free_cand(h);
     return kmx::fail(KMX_ENOMEM, "candidate buffers");
   }
@@ -2324,15 +2354,19 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
       return v ? std::atoi(v) : 0;
     }();
     const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
-    auto kc = stew ? ((clb >= 8) ? k_ransac_coop<8, true> : (clb >= 6) ? k_ransac_coop<6, true>
-                      : (clb >= 5) ? k_ransac_coop<5, true> : (clb == 4) ? k_ransac_coop<4, true>
-                      : (clb == 2) ? k_ransac_coop<2, true> : k_ransac_coop<3, true>)
-                   : ((clb >= 8) ? k_ransac_coop<8, false> : (clb >= 6) ? k_ransac_coop<6, false>
-                      : (clb >= 5) ? k_ransac_coop<5, false> : k_ransac_coop<4, false>);
-    hipLaunchKernelGGL(kc, dim3(n), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
+    auto kc = stew ? ((clb == 2) ? k_ransac_coop<2, true> : k_ransac_coop<3, true>)
+                   : ((clb == 3) ? k_ransac_coop<3, false> : k_ransac_coop<4, false>);
+    // one wave per resident slot (<= RS_MAX_SLOTS: the scratch is sized for it)
+    int per_cu = 0, dev = 0, cus = 0;
+    KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kc, RS_BLOCK, 0));
+    KMX_HIP(hipGetDevice(&dev));
+    KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int slots = std::max(1, std::min({n, std::max(per_cu, 1) * cus, RS_MAX_SLOTS, h->cap}));
+    KMX_HIP(hipMemsetAsync(h->d_next, 0, sizeof(int), h->stream));
+    hipLaunchKernelGGL(kc, dim3(slots), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
                        (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
                        (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
-                       (want_masks || rp.pnp) ? h->d_mask : nullptr, h->d_fbuf);
+                       (want_masks || rp.pnp) ? h->d_mask : nullptr, h->d_fbuf, n, h->d_next);
   }
   if (rp.pnp) {
     const bool pnp = h->P.pose_recovery_type == 1;
