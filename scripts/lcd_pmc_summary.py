@@ -1,7 +1,11 @@
 """Summarise the k_ransac_coop PMC passes of scripts/gpu_lcd_pmc3.sh (run
 over scripts/lcd_timing.py N: one warm-up launch of 64 candidates, then 4
 launches of N) into the per-candidate counts bench.py's LCD roofline uses.
-usage: lcd_pmc_summary.py PMC_DIR OUT_JSON"""
+usage: lcd_pmc_summary.py PMC_DIR OUT_JSON [N]
+N (the candidates per timed launch, scripts/lcd_timing.py's argument): the
+work-queue k_ransac_coop's grid is its resident waves, not its candidates,
+so the candidates counted are N per timed launch; without N the grid rule of
+the one-workgroup-per-candidate kernel is used."""
 import csv, glob, json, os, sys
 from collections import defaultdict
 
@@ -23,7 +27,7 @@ grids = []
 for r in csv.DictReader(open(glob.glob(os.path.join(d, "p1", "run_counter_collection.csv"))[0])):
     if "k_ransac_coop" in r["Kernel_Name"] and int(r["Grid_Size"]) >= 64 * 1000 and r["Counter_Name"] == "SQ_WAVES":
         grids.append(int(r["Grid_Size"]) // 64)
-cand = sum(grids)
+cand = len(grids) * int(sys.argv[3]) if len(sys.argv) > 3 else sum(grids)
 kern = [float(r["TotalDurationNs"]) for r in csv.DictReader(open(os.path.join(d, "stats", "run_kernel_stats.csv")))
         if "k_ransac_coop" in r["Name"]]
 f64 = {k: vals[k] for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
