@@ -60,35 +60,60 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const 
   const int per = (nq + KNN_BLOCK - 1) / KNN_BLOCK;
   const int i0 = threadIdx.x * per, i1 = min(nq, i0 + per);
   int found = 0;
-  int bestj[8];  // per <= 4 for N <= 1024
-  bool pass[8];
-  for (int u = 0; u < 8; ++u) { bestj[u] = -1; pass[u] = false; }
+  int bestj[4];  // per <= 4 for N <= MAX_FEATS
+  bool pass[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) { bestj[u] = -1; pass[u] = false; }
+  // The two nearest neighbours as ordered keys (distance << 10 | match index;
+  // distance <= 32 x 255 < 2^13, index < 1024): the smallest key is the first
+  // match at the smallest distance and the second smallest carries the second
+  // distance (a repeat of the first included) — the serial scan's d0 / j0 / d1
+  // with its strict tests — in three min / max operations per pair. Each match
+  // descriptor read from LDS serves two of the thread's queries.
+  auto dist = [&](const uint32_t a[8], const uint32_t b[8]) -> uint32_t {
+    uint32_t d = 0;
+    if (norm == KMX_NORM_HAMMING) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) d += __popc(a[w] ^ b[w]);
+    } else {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) d = __builtin_amdgcn_sad_u8(a[w], b[w], d);
+    }
+    return d;
+  };
   if (nm >= 2) {
-    for (int i = i0, u = 0; i < i1; ++i, ++u) {
-      uint32_t a[8];
 #pragma unroll
-      for (int w = 0; w < 8; ++w) a[w] = dq[(size_t)i * 8 + w];
-      int d0 = INT_MAX, d1 = INT_MAX, j0 = -1;
-      for (int j = 0; j < nm; ++j) {
-        const uint32_t* b = sdesc + j * 8;
-        int d = 0;
-        if (norm == KMX_NORM_HAMMING) {
+    for (int pp = 0; pp < 2; ++pp) {  // per <= 4: at most two pairs, unrolled (static register indices)
+      const int i = i0 + 2 * pp, u = 2 * pp;
+      if (i >= i1) break;
+      const bool two = i + 1 < i1;
+      uint32_t a0[8], a1[8];
 #pragma unroll
-          for (int w = 0; w < 8; ++w) d += __popc(a[w] ^ b[w]);
-        } else {
-          uint32_t acc = 0;
-#pragma unroll
-          for (int w = 0; w < 8; ++w) acc = __builtin_amdgcn_sad_u8(a[w], b[w], acc);
-          d = (int)acc;
-        }
-        if (d < d1) {
-          if (d < d0) { d1 = d0; d0 = d; j0 = j; }
-          else d1 = d;
-        }
+      for (int w = 0; w < 8; ++w) {
+        a0[w] = dq[(size_t)i * 8 + w];
+        a1[w] = two ? dq[(size_t)(i + 1) * 8 + w] : a0[w];
       }
-      bestj[u] = j0;
-      pass[u] = (double)(float)d0 < lowe * (double)(float)d1;
-      found += pass[u] ? 1 : 0;
+      uint32_t k00 = 0xffffffffu, k01 = 0xffffffffu, k10 = 0xffffffffu, k11 = 0xffffffffu;
+      for (int j = 0; j < nm; ++j) {
+        const uint4* b4 = reinterpret_cast<const uint4*>(sdesc + j * 8);
+        const uint4 x = b4[0], y = b4[1];
+        const uint32_t b[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        const uint32_t ka = (dist(a0, b) << 10) | (uint32_t)j, kb = (dist(a1, b) << 10) | (uint32_t)j;
+        const uint32_t ta = max(k00, ka), tb = max(k10, kb);
+        k00 = min(k00, ka);
+        k01 = min(k01, ta);
+        k10 = min(k10, kb);
+        k11 = min(k11, tb);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        const uint32_t k0 = h ? k10 : k00, k1 = h ? k11 : k01;
+        const int d0 = (int)(k0 >> 10), d1 = (int)(k1 >> 10);
+        bestj[u + h] = (int)(k0 & 1023u);
+        pass[u + h] = (double)(float)d0 < lowe * (double)(float)d1;
+        found += pass[u + h] ? 1 : 0;
+      }
     }
   }
   // exclusive prefix sum of per-thread counts (query order = thread order)
@@ -106,8 +131,9 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const 
   __syncthreads();
   int pos = scnt[threadIdx.x];
   int2* out = pairs + (size_t)c * N;
-  for (int i = i0, u = 0; i < i1; ++i, ++u)
-    if (pass[u]) out[pos++] = make_int2(i, bestj[u]);
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (i0 + u < i1 && pass[u]) out[pos++] = make_int2(i0 + u, bestj[u]);
   if (threadIdx.x == 0) Kout[c] = scnt[KNN_BLOCK];
 }
 
