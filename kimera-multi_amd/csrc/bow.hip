@@ -79,11 +79,22 @@ __device__ __forceinline__ void find_bin(const int* hist, int need, int* wsum, i
   }
 }
 
+// The workgroup's next query (workgroup-uniform): one atomic per query on a
+// counter the launch starts at 0, so a workgroup that drew short posting lists
+// takes more queries instead of every workgroup taking every gridDim-th one.
+__device__ __forceinline__ int next_query(int* next, int nq) {
+  __shared__ int s_q;
+  __syncthreads();  // the previous query's readers of s_q are done
+  if (threadIdx.x == 0) s_q = atomicAdd(next, 1);
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(min(s_q, nq));  // uniform: keep it in a scalar register
+}
+
 __global__ __launch_bounds__(BOW_BLOCK) void k_bow_query(BowDb db, int nq, const long long* qptr,
                                                          const unsigned* qw, const double* qv,
                                                          const int* max_id, int K, double* acc_all,
                                                          int* touched_all, int* out_n, int* out_id,
-                                                         double* out_score, int* err) {
+                                                         double* out_score, int* err, int* next) {
   __shared__ int s_nt, s_ns, s_b, s_cb, s_done;
   __shared__ int s_wsum[BOW_BLOCK / 64];
   __shared__ int hist[NBINS];
@@ -92,7 +103,9 @@ __global__ __launch_bounds__(BOW_BLOCK) void k_bow_query(BowDb db, int nq, const
   const int tid = threadIdx.x;
   double* acc = acc_all + (size_t)blockIdx.x * db.n_entries;
   int* touched = touched_all + (size_t)blockIdx.x * db.n_entries;
-  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+  for (;;) {  // a work queue: the next query from a counter (queries differ in postings by 10x)
+    const int q = next_query(next, nq);
+    if (q >= nq) break;
     const int mid = max_id ? max_id[q] : -1;
     if (tid == 0) s_nt = 0;
     __syncthreads();
@@ -235,7 +248,7 @@ __global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int*
                                                             const long long* qptr, const unsigned* qw,
                                                             const double* qv, const int* max_id, int K,
                                                             int* out_n, int* out_id, double* out_score,
-                                                            int* err) {
+                                                            int* err, int* next) {
   extern __shared__ __attribute__((aligned(16))) char bsm[];
   double* acc = reinterpret_cast<double*>(bsm);                   // [ch]
   double* c_val = acc + LCH;                                        // [LSEL]        \  selection scratch;
@@ -252,7 +265,9 @@ __global__ __launch_bounds__(LW_BLOCK) void k_bow_query_lds(BowDb db, const int*
   __shared__ int s_wsum[LW_WAVES];
   const int tid = threadIdx.x, v = tid >> 6, lane = tid & 63;
   const int nsub = nch * LW_WAVES, sch = ch / LW_WAVES;
-  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+  for (;;) {  // a work queue: the next query from a counter (queries differ in postings by 10x)
+    const int q = next_query(next, nq);
+    if (q >= nq) break;
     const int mid = max_id ? max_id[q] : -1;
     const int lim = (mid < 0) ? db.n_entries : min(mid, db.n_entries);  // entries < lim are eligible
     const long long q0 = qptr[q], q1 = qptr[q + 1];
@@ -600,7 +615,7 @@ extern "C" int kmx_bow_create(int device, kmx_bow** out) {
     return kmx::fail(KMX_EHIP, "hipStreamCreate failed");
   }
   h->own_stream = true;
-  if (hipMalloc(reinterpret_cast<void**>(&h->d_err), sizeof(int)) != hipSuccess) {
+  if (hipMalloc(reinterpret_cast<void**>(&h->d_err), 2 * sizeof(int)) != hipSuccess) {
     (void)hipStreamDestroy(h->stream);
     delete h;
     return kmx::fail(KMX_ENOMEM, "hipMalloc failed");
@@ -745,7 +760,7 @@ extern "C" int kmx_bow_query_async(kmx_bow* h, int32_t nq, const int64_t* qptr, 
   for (int q = 0; q < nq; ++q) KMX_CHECK(qptr[q + 1] >= qptr[q], KMX_EINVAL, "qptr not monotone");
   if (int rc = bow_upload_queries(h, nq, qptr, words, weights, max_id, max_results)) return rc;
   if (nq == 0) return KMX_OK;
-  KMX_HIP(hipMemsetAsync(h->d_err, 0, sizeof(int), h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_err, 0, 2 * sizeof(int), h->stream));  // error flag, query counter
   BowDb db{h->d_ptr, h->d_ent, h->d_wt, h->n_words, h->n_entries};
   const int grid = std::min(nq, h->n_wg);
   if (h->lds) {
@@ -753,14 +768,14 @@ extern "C" int kmx_bow_query_async(kmx_bow* h, int32_t nq, const int64_t* qptr, 
                        (const int*)h->d_cptr, h->nch, h->ch, nq, (const long long*)h->d_qptr,
                        (const unsigned*)h->d_qw, (const double*)h->d_qv,
                        max_id ? (const int*)h->d_maxid : nullptr, max_results, h->d_n, h->d_id, h->d_score,
-                       h->d_err);
+                       h->d_err, h->d_err + 1);
     KMX_HIP(hipGetLastError());
     return KMX_OK;
   }
   hipLaunchKernelGGL(k_bow_query, dim3(grid), dim3(BOW_BLOCK), 0, h->stream, db, nq,
                      (const long long*)h->d_qptr, (const unsigned*)h->d_qw, (const double*)h->d_qv,
                      max_id ? (const int*)h->d_maxid : nullptr, max_results, h->d_acc, h->d_touched, h->d_n,
-                     h->d_id, h->d_score, h->d_err);
+                     h->d_id, h->d_score, h->d_err, h->d_err + 1);
   KMX_HIP(hipGetLastError());
   return KMX_OK;
   KMX_GUARD_END
