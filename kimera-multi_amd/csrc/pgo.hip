@@ -63,7 +63,9 @@ struct Ctl {
   double f_final, norm_r0, z_r, e_Pe;
   double e_Pd, d_Pd, alpha, beta;
   double coef, rho, chg_acc, rel_change;
-  double pad2[10];  // 256 B: one robot's record never shares a line with the next
+  double r_stop;    // tCG residual stop: ||r_0|| min(||r_0||^theta, kappa), formed once per tCG
+  int lin_stop, pad3;  // kappa < ||r_0||^theta: a stop at r_stop is KMX_TCG_LINEAR
+  double pad2[8];   // 256 B: one robot's record never shares a line with the next
 };
 static_assert(sizeof(Ctl) == 256, "Ctl is 256 B");
 
@@ -819,7 +821,7 @@ struct UpdStep {
   int done, stop;
   double beta;
 };
-__device__ __forceinline__ UpdStep upd_step(int mode, double norm_r0, double z_r, int tcg_iter, double rr,
+__device__ __forceinline__ UpdStep upd_step(int mode, double r_stop, int lin_stop, double z_r, int tcg_iter, double rr,
                                             double zr_new, const Params& P) {
 #pragma clang fp contract(off)
   UpdStep u;
@@ -832,10 +834,9 @@ __device__ __forceinline__ UpdStep upd_step(int mode, double norm_r0, double z_r
     return u;
   }
   const double norm_r = sqrt(rr);
-  const double pw = pow(norm_r0, P.theta);
-  if (norm_r <= norm_r0 * fmin(pw, P.kappa)) {
+  if (norm_r <= r_stop) {
     u.done = 1;
-    u.stop = (P.kappa < pw) ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
+    u.stop = lin_stop ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
   } else if (tcg_iter >= P.tcg_max) {
     u.done = 1;
     u.stop = KMX_TCG_MAX_ITER;
@@ -877,6 +878,11 @@ __device__ __forceinline__ void control_core(Ctl& c, const Dev& d, int l, int ki
       c.phase = PH_TCG;
       c.tcg_iter = 0;
       c.norm_r0 = gn;
+      {  // the residual stop of this tCG (upd_step), formed once instead of at every step
+        const double pw = pow(gn, P.theta);
+        c.r_stop = gn * fmin(pw, P.kappa);
+        c.lin_stop = (P.kappa < pw) ? 1 : 0;
+      }
       c.z_r = tot[2];
       c.d_Pd = tot[2];
       c.e_Pd = 0.0;
@@ -910,7 +916,7 @@ __device__ __forceinline__ void control_core(Ctl& c, const Dev& d, int l, int ki
     }
   } else if (kind == RED_UPDATE) {
     const double zr_new = tot[1];
-    const UpdStep u = upd_step(c.mode, c.norm_r0, c.z_r, c.tcg_iter, tot[0], zr_new, P);
+    const UpdStep u = upd_step(c.mode, c.r_stop, c.lin_stop, c.z_r, c.tcg_iter, tot[0], zr_new, P);
     if (u.done) {
       if (u.stop >= 0) c.tcg_stop = u.stop;
       c.phase = PH_STEP;
@@ -1306,7 +1312,7 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
       // every thread evaluates the decision; the first tile's thread 0 also
       // updates the robot's state (on an LDS copy: a private one would live in
       // scratch) and publishes it
-      if (upd) u = upd_step(c0.mode, c0.norm_r0, c0.z_r, c0.tcg_iter, tot[0], tot[1], d.p);
+      if (upd) u = upd_step(c0.mode, c0.r_stop, c0.lin_stop, c0.z_r, c0.tcg_iter, tot[0], tot[1], d.p);
       if (grad) u.done = sqrt(tot[1]) < d.p.gn_tol ? 1 : 0;  // control_on's RED_GRAD test
       if (writer && threadIdx.x == 0) {
         if (upd || grad) control_on(cs, d, L.l, grad ? RED_GRAD : RED_UPDATE, tot, R, true);
@@ -1507,7 +1513,7 @@ __device__ __forceinline__ void body_retract(const Dev& d, int fold, char* smem)
     rs.issue(d.part_u, 2, d.rtile0[L.l], d.rtile0[L.l + 1]);
     double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
     rs.finish(d.part_u, 2, rl, tot);
-    const UpdStep u = upd_step(c.mode, c.norm_r0, c.z_r, c.tcg_iter, tot[0], tot[1], d.p);
+    const UpdStep u = upd_step(c.mode, c.r_stop, c.lin_stop, c.z_r, c.tcg_iter, tot[0], tot[1], d.p);
     if (!u.done) return;  // (cannot happen: the host stops enqueueing only when no robot is in tCG or at tcg_max)
     if (threadIdx.x == 0 && L.tile == d.rtile0[L.l]) {
       if (u.stop >= 0) c.tcg_stop = u.stop;
