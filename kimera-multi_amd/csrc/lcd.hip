@@ -1869,9 +1869,20 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
     // SG hypotheses' eigenvalues at a time, then each hypothesis in order under
     // the serial loop's tests (a batch may run past the stop: those are never
     // scored, so the results are the one-at-a-time loop's)
-    for (int p0 = 0; p0 < P.pmax && !done; p0 += SG) {
+    int nb = SG;
+    for (int p0 = 0; p0 < P.pmax && !done; p0 += nb) {
       if (!(iterations < kk && skipped < max_skip)) break;  // uniform
-      const int nb = min(SG, P.pmax - p0);
+      // once a model exists, the serial loop scores at most ceil(kk) -
+      // iterations more hypotheses (kk only falls), plus any that fail to give
+      // a model (a later batch takes those): a batch no longer computes the
+      // hypotheses past that bound (up to SG - 1 of them in a candidate's last
+      // batch)
+      int want = SG;
+      if (have) {
+        const double rem = ceil(kk) - (double)iterations;
+        want = rem < 1.0 ? 1 : (rem < (double)SG ? (int)rem : SG);
+      }
+      nb = min(want, P.pmax - p0);
       stew_batch(w, sb, stash, lane, F1, F2, tab, p0, nb, prof);
       stew_models(sb, stash, lane, F1, F2, tab, p0, nb, prof);
       for (int b = 0; b < nb && !done; ++b) {
