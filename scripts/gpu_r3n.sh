@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 T=${1:-r3n}
 mkdir -p gpurun_out/$T
-timeout -k 10 300 python -u -m pytest tests/test_lcd_gpu.py tests/test_configs_gpu.py tests/test_pipeline_gpu.py -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/$T/pytest_lcd.log 2>&1; rc=$?; echo "lcd tests rc=$rc"; tail -3 gpurun_out/$T/pytest_lcd.log
+timeout -k 10 300 python -u -m pytest tests/test_lcd_gpu.py tests/test_configs_gpu.py tests/test_pipeline_gpu.py tests/test_outputs_gpu.py -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/$T/pytest_lcd.log 2>&1; rc=$?; echo "lcd tests rc=$rc"; tail -3 gpurun_out/$T/pytest_lcd.log
 [ $rc -ne 0 ] && exit 1
 for k in 1 2; do
   for v in intree prev; do
