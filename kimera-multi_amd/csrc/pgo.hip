@@ -7,17 +7,20 @@
 //     same launches (batched RBCD). Workgroup tiles never straddle robots, so
 //     every reduction is per robot and its RTR / tCG scalars live on the device
 //     in one Ctl record per robot.
-//   * No scalar reaches the host inside a round, and no reduction has a launch
-//     of its own: each tile publishes its partial sums and takes a ticket on its
-//     robot's counter; the tile that draws the last ticket reduces the robot's
-//     partials in tile order (deterministic) and runs the control logic. The
-//     tCG loop is a fixed launch sequence of tcg_max (Hess-vec, update) pairs;
-//     a robot whose tCG has stopped exits at its first instruction, so the host
-//     never waits on the device (no polling).
-//   * Edge data: one 96-B compact record per incidence in CSR order (R rows
-//     0-1, t, w kappa, w tau, {other, edge | tail << 31}; row 2 = row0 x row1 for
-//     measurements in SO(3)), or a 128-B record with the full rotation when some
-//     measurement is not a rotation to 1e-12. The gathers are incidence-parallel:
+//   * No scalar reaches the host inside a round. Each tile publishes its
+//     partial sums; a robot's partials are reduced in tile order
+//     (deterministic) either by a one-workgroup-per-robot k_reduce launch
+//     (large problems) or by every workgroup of the next kernel, which needs
+//     the decision anyway (the consumer form, small problems: no reduction
+//     launch at all). The host only reads one progress word per robot to stop
+//     enqueueing tCG steps (polled, blind or adaptive, kmx_pgo_set_tcg_poll).
+//   * tCG in the linearity form: Hz by gather, delta = -z + beta delta_old,
+//     Hdelta = -Hz + beta Hdelta_old; eta = sum coef_k delta_k is folded from
+//     two kept directions every second step and finished in k_retract.
+//   * Edge data: one 80-B compact record per incidence in CSR order (unit
+//     quaternion of R, t, w kappa, w tau, {other, edge | tail << 31}), or a
+//     128-B record with the full rotation when some measurement is not a
+//     rotation to 1e-12. The gathers are incidence-parallel:
 //     one lane per incidence evaluates its block against the neighbour's whole
 //     r x 4 row and parks the r contribution rows in LDS; the (pose, row) lanes
 //     then add their pose's contributions in CSR (= increasing edge id) order.
@@ -101,8 +104,8 @@ __device__ __forceinline__ void store_gnc(Gnc* p, const Gnc& s) {
 }
 
 // Host-visible tCG progress of one robot, written after every tCG step by the
-// last-arriving tile of the robot's k_update (or its first tile when it is
-// not in tCG) into host-mapped memory as ONE 64-bit word (seq << 1 |
+// robot's update reduction (k_reduce, or the robot's first tile of the
+// consumer-form k_hess) into host-mapped memory as ONE 64-bit word (seq << 1 |
 // still-in-tCG): a single relaxed system-scope store, no release fence, so no
 // L2 writeback. The host keeps one tCG step queued beyond the last one known
 // to be needed and stops enqueueing once no robot is in tCG.
