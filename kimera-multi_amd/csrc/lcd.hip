@@ -5,20 +5,20 @@
 // Design (DESIGN.md "LCD"):
 //   * k_knn2: one workgroup per candidate. The match frame's descriptors sit in
 //     LDS (32 B each, read as broadcast); each lane owns a contiguous run of
-//     query descriptors, computes L1 (v_sad_u8 on 4-byte words) or Hamming
-//     (xor + popcount) to every match descriptor, keeps the two smallest
-//     (distance, index) pairs with OpenCV's strict-'<' insertion, applies Lowe,
-//     and the workgroup compacts the pairs in query order with a prefix sum.
-//   * k_ransac: one wavefront per candidate, one RANSAC pass (hypothesis) per
-//     lane: 64 consecutive passes of the opengv loop are evaluated at once
-//     (5-point solve + scoring of all K correspondences held in LDS), then lane
-//     0 replays the serial loop control (skips, best model, adaptive k,
-//     max-iteration stop) over the batch in pass order, so the accepted model
-//     and inlier set are the serial loop's. Samples come from a host-built
-//     table of the opengv sampler (std::mt19937, seed 12345, GCC-9 or GCC-11
-//     uniform_int_distribution) indexed by K.
-//   * 3D-3D (1-point given rotation) voting on the 2D-2D inliers in the same
-//     wavefront.
+//     query descriptors (two per LDS read), computes L1 (v_sad_u8 on 4-byte
+//     words) or Hamming (xor + popcount) to every match descriptor, keeps the
+//     two nearest as ordered keys (distance << 10 | index: OpenCV's strict-'<'
+//     insertion), applies Lowe, and the workgroup compacts the pairs in query
+//     order with a prefix sum.
+//   * k_ransac_coop: a work queue of one-wave workgroups (one per resident
+//     slot), each taking the next candidate from a counter; per candidate the
+//     opengv RANSAC loop in its serial order with all 64 lanes cooperating on
+//     each 5-point solve (Stewenius: six hypotheses' eigenvalue stages at once,
+//     groups of 10 lanes), then the 1-point 3D-3D voting on the 2D-2D inliers.
+//     Samples come from a host-built table of the opengv sampler (std::mt19937,
+//     seed 12345, GCC-9 or GCC-11 uniform_int_distribution) indexed by K.
+//   * k_recover: EPnP or Arun 3-point RANSAC on the 2D-2D inliers (lane per
+//     hypothesis, lane 0 replays the serial control).
 // The solver code is a line-by-line port of oracle/lcd_oracle.c and this file
 // is compiled with -ffp-contract=off, so the inlier sets are bit-exact.
 #include <hip/hip_runtime.h>
