@@ -1336,7 +1336,9 @@ struct StewBatch {
   unsigned char pb[MAXP], ps[MAXP];  // the batch's solutions: hypothesis, eigenvalue
 };
 constexpr int STASH_H = 96;  // per hypothesis: C6 (rows 0-5 of M, 60) + N (36)
-constexpr int STASH = SG * STASH_H + MAXP * 9;  // + the batch's essentials
+constexpr int GJW = 3;       // hypotheses per batched Gauss-Jordan (groups of 20 lanes)
+// + the batch's essentials, + GJW staged 10 x 20 systems
+constexpr int STASH = SG * STASH_H + MAXP * 9 + GJW * 200;
 
 // The highest group-local lane whose pred holds (-1: none).
 __device__ __forceinline__ int grp_top(bool pred, int g) {
@@ -1753,26 +1755,95 @@ __device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const doubl
 
 // Stewenius: the hypotheses p0 .. p0 + nb - 1 up to their action matrices,
 // stashed in sb (one at a time, 64 lanes), then their eigenvalues together.
+// coop_gj for GJW systems at once: group g (lanes 20g .. 20g + 19) eliminates
+// the system staged at A (row-major 10 x 20) with lane 20g + c holding graded
+// column c, the column-k broadcasts a group shuffle; per element the
+// operations of coop_gj in its order (the same bits). Returns the group's
+// success (0: a zero pivot; the group's later values are then unused).
+__device__ __forceinline__ int grp_gj(const double* A, int cl, int g0, double a[10]) {
+  const int src = GORD_D[cl];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) a[i] = A[i * 20 + src];
+  int ok = 1;
+  for (int k = 0; k < 10; ++k) {
+    double col[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) col[i] = __shfl(a[i], g0 + k, 64);
+    int p = k;
+    double pv = 0.0, pa = -1.0, ck = 0.0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      if (i == k) { ck = col[i]; pv = ck; pa = fabs(ck); }
+      else if (i > k && fabs(col[i]) > pa) { p = i; pv = col[i]; pa = fabs(col[i]); }
+    }
+    if (pv == 0.0) ok = 0;
+    const double inv = 1.0 / pv;
+    double ak = 0.0, ap = 0.0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      ak = (i == k) ? a[i] : ak;
+      ap = (i == p) ? a[i] : ap;
+    }
+    const double rk = ap * inv;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      if (i == k) {
+        a[i] = rk;
+      } else {
+        double ai = (i == p) ? ak : a[i];
+        const double f = (i == p) ? ck : col[i];
+        if (f != 0.0) ai -= f * rk;
+        a[i] = ai;
+      }
+    }
+  }
+  return ok;
+}
+
+// Stewenius: the hypotheses p0 .. p0 + nb - 1 up to their action matrices
+// (null space and system one at a time, 64 lanes; Gauss-Jordan GJW at a time
+// from systems staged in the wave's scratch), stashed in sb, then their
+// eigenvalues together.
 __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* stash, int lane, const double* F1,
                                            const double* F2, const short* tab, int p0, int nb, bool prof) {
-  for (int b = 0; b < nb; ++b) {
-    coop_prepare(w, lane, F1, F2, tab + (size_t)(p0 + b) * 5, prof);
-    const int okg = coop_gj(w, lane, true);
-    if (okg) {
+  double* Ab = stash + SG * STASH_H + MAXP * 9;
+  for (int b0 = 0; b0 < nb; b0 += GJW) {
+    const int nw = min(GJW, nb - b0);
+    for (int u = 0; u < nw; ++u) {
+      const int b = b0 + u;
+      coop_prepare(w, lane, F1, F2, tab + (size_t)(p0 + b) * 5, prof);
+      double* A = Ab + u * 200;
+      for (int t = lane; t < 200; t += RS_BLOCK) A[t] = (&w.A[0][0])[t];
       double* st = stash + b * STASH_H;
-      for (int t = lane; t < 100; t += RS_BLOCK) {
-        const int i = t / 10, j = t % 10;
-        const double v = (i < 6) ? -w.A[i][10 + j] : action_entry(nullptr, i, j);
-        if (i < 6) st[t] = v;
-        sb.H[b][i][j] = v;
-      }
       if (lane < 36) st[60 + lane] = (&w.N[0][0])[lane];
+      if (lane < 15) {
+        sb.f1[b][lane] = w.f1[lane];
+        sb.f2[b][lane] = w.f2[lane];
+      }
+      __threadfence_block();  // the staged system is read by other lanes of this wave
+      wsync();
     }
-    if (lane < 15) {
-      sb.f1[b][lane] = w.f1[lane];
-      sb.f2[b][lane] = w.f2[lane];
+    const int gg = lane / 20, g = gg < nw ? gg : 0, cl = lane - gg * 20 < 20 ? lane - gg * 20 : 19;
+    const bool gact = gg < nw;
+    double a[10];
+    const int okg = grp_gj(Ab + g * 200, cl, g * 20, a);
+    if (gact && okg) {
+      const int b = b0 + gg;
+      double* st = stash + b * STASH_H;
+      if (cl >= 10) {  // rows 0-5 of the action matrix: -C from columns 10-19
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const double v = -a[i];
+          st[i * 10 + (cl - 10)] = v;
+          sb.H[b][i][cl - 10] = v;
+        }
+      } else {  // rows 6-9: unit entries
+#pragma unroll
+        for (int i = 6; i < 10; ++i) sb.H[b][i][cl] = action_entry(nullptr, i, cl);
+      }
     }
-    if (lane == 0) sb.ok[b] = okg;
+    if (gact && cl == 0 && lane - gg * 20 == 0) sb.ok[b0 + gg] = okg;
+    __threadfence_block();
     wsync();
   }
   __threadfence_block();  // the stash is read back by this wave (stew_models)
