@@ -290,6 +290,9 @@ def lcd_leg(args, rank, world, barrier_sync):
                              "frac": (lane_ops / (tk["knn_ms"] * 1e-3)) / PEAK_VALU_OPS if tk["knn_ms"] > 0 else 0.0,
                              "algorithmic": f"{pair_evals:.3e} descriptor pairs x 8 v_sad_u8 lane-ops (32 B each)",
                              "knn_ms": tk["knn_ms"]}}
+    out["stream"] = stream_leg(det, pool, cq, cm, args)
+    out["hamming"] = hamming_leg(args, pool, cq, cm, barrier_sync)
+    det.close()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, str(ROOT))
@@ -305,6 +308,80 @@ def lcd_leg(args, rank, world, barrier_sync):
                "sample": f"first {n} candidates of configs[2] (half planted), oracle/lcd_oracle.c, 1 thread, "
                          f"{done:.1f} s"}
     return out, cpu
+
+
+def stream_leg(det, pool, cq, cm, args):
+    """The streaming boundary on the resident configs[2] pool (VERDICT r3
+    item 1): (a) addVLCFrame cost — 1,000 frames appended one call each
+    (kmx_lcd_add_frames: host-to-device copy of the frame, the pool grows by
+    capacity doubling; the first append doubles the 50k-frame pool with one
+    device-to-device copy, included); (b) geometricVerificationNister +
+    recoverPose on caller-supplied correspondences (kmx_lcd_verify_matches,
+    both stages, no kNN2) over the step's candidates with the kNN2 pairs as
+    input — host CSR upload included, as a caller would pay it."""
+    n_add = 1000
+    src = np.arange(n_add) % pool.n_frames
+    ts = []
+    t0 = time.perf_counter()
+    for f in src:
+        a = time.perf_counter()
+        det.add_frames(pool.n_feats[f:f + 1], pool.desc[f:f + 1], pool.bearings[f:f + 1], pool.points[f:f + 1])
+        ts.append(time.perf_counter() - a)
+    el = time.perf_counter() - t0
+    ts = np.array(ts) * 1e6
+    info = det.pool_info()
+    out = {"frames_added": n_add, "us_per_frame": el * 1e6 / n_add, "us_per_frame_median": float(np.median(ts)),
+           "us_first_append": float(ts[0]), "bytes_per_frame": int(pool.max_feats * (32 + 48 + 48) + 4),
+           "pool_after": info,
+           "note": "one kmx_lcd_add_frames call per frame from pageable host memory; the first call doubles the "
+                   "resident pool (device-to-device copy)"}
+    pairs, k = det.match(cq, cm)
+    corr = [(pairs[i, :k[i], 0], pairs[i, :k[i], 1]) for i in range(len(cq))]
+    det.verify_matches(cq[:64], cm[:64], corr[:64])  # warmup
+    a = time.perf_counter()
+    res, _ = det.verify_matches(cq, cm, corr, stages=3)
+    el2 = time.perf_counter() - a
+    out["verify_matches"] = {"metric": "LC candidates verified/sec (caller-supplied correspondences, both stages)",
+                             "value": len(cq) / el2, "n": int(len(cq)), "elapsed": el2,
+                             "pairs": int(k.sum()), "accepted": int(sum(r["accepted"] for r in res))}
+    return out
+
+
+def hamming_leg(args, pool, cq, cm, barrier_sync):
+    """configs[2] with the Hamming matcher north_star names (BruteForce-Hamming
+    over 256 bits, `norm: hamming`), same pool and candidates as the L1 leg
+    (the reference build's matcher, kimera_multi_lcd.patch:33-35)."""
+    from kmx.lcd import LcdParams, LoopClosureDetector
+    det = LoopClosureDetector(LcdParams(ransac_2d2d_algorithm=args.lcd_algo, norm="hamming"),
+                              device=int(os.environ.get("KMX_BENCH_DEVICE", "0")))
+    det.set_pool(pool)
+    det.verify_async(cq, cm)
+    det.sync()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.lcd_steps):
+        det.verify_async(cq, cm)
+    det.sync()
+    barrier_sync()
+    el = time.perf_counter() - t0
+    det.enable_timing(True)
+    det.verify_async(cq, cm)
+    det.sync()
+    tk = det.read_timing()
+    res, _ = det.verify(cq[:256], cm[:256])
+    det.close()
+    nf = pool.n_feats.astype(np.int64)
+    pair_evals = float((nf[cq] * nf[cm]).sum())
+    lane_ops = pair_evals * 16  # 8 words per pair, v_xor_b32 + v_bcnt_u32_b32 (accumulating) each
+    return {"metric": "LC candidates verified/sec (Hamming matcher)", "unit": "candidates/s", "elapsed": el, "steps": args.lcd_steps,
+            "accepted_frac_first256": sum(r["accepted"] for r in res) / max(len(res), 1),
+            "ransac_ms": tk["ransac_ms"], "knn_ms": tk["knn_ms"],
+            "knn2_roofline": {"kernel": "k_knn2 (kNN2 + Lowe, Hamming)", "bound": "valu", "unit": "lane-op/s",
+                              "achieved": lane_ops / (tk["knn_ms"] * 1e-3) if tk["knn_ms"] > 0 else 0.0,
+                              "peak": PEAK_VALU_OPS,
+                              "frac": (lane_ops / (tk["knn_ms"] * 1e-3)) / PEAK_VALU_OPS if tk["knn_ms"] > 0 else 0.0,
+                              "algorithmic": f"{pair_evals:.3e} descriptor pairs x (8 v_xor_b32 + 8 v_bcnt_u32_b32) "
+                                             "lane-ops (256 bits each)"}}
 
 
 def bow_leg(args, rank, world, barrier_sync):
@@ -381,6 +458,27 @@ def _gather(dist, world, vals, ops):
     return [float(a[:, i].max() if op == "max" else a[:, i].sum()) for i, op in enumerate(ops)]
 
 
+def _runtime():
+    """Which librccl / libamdhip64 serve libkmx in this process (torch bundles
+    copies of the same SONAME; load order decides), with versions."""
+    try:
+        from kmx import abi
+        return abi.runtime_info()
+    except Exception as e:  # noqa: BLE001 - reported, never fatal to the measurement
+        return {"error": str(e)}
+
+
+def _gather_each(dist, world, vals):
+    """Every rank's scalars, in rank order (a list of lists)."""
+    if dist is None:
+        return [list(vals)]
+    import torch
+    t = torch.tensor(vals, dtype=torch.float64, device=_coll_device(dist))
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [p.cpu().tolist() for p in parts]
+
+
 def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, replay=True, want_snapshot=False):
     """Burn-in + warmup, snapshot, time `steps` rounds (max over ranks), then
     replay the same rounds from the snapshot with HIP events around every
@@ -394,6 +492,7 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
         barrier()
 
     hv_ms, hv_bytes, hv_n, same, snap = 0.0, 0.0, 0, None, None
+    el_local = None
     if args.profile:  # every round evented and counted (the rocprofv3 / PMC passes divide by these)
         drv.solver.read_counters()
         drv.solver.enable_timing(True)
@@ -411,7 +510,9 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
         sync()
         t0 = time.perf_counter()
         drv.run_async(steps)
-        sync()
+        drv.solver.sync()
+        el_local = time.perf_counter() - t0  # this rank's own rounds, before waiting for its peers
+        barrier()
         el = time.perf_counter() - t0
         c = drv.solver.read_counters()
     if snap is not None and replay:
@@ -432,10 +533,13 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
                                 float(c["gnc_updates"]), hv_ms, hv_bytes, float(hv_n), float(xs), float(xr),
                                 float(mem), 1.0 if same in (None, True) else 0.0],
                   ["max", "sum", "sum", "sum", "max", "sum", "sum", "sum", "max", "max", "max", "sum"])
+    per_rank = _gather_each(dist, world, [el_local if el_local is not None else el, float(c["edges_iters"])])
     if not want_snapshot:
         drv.solver.close()
         drv = None
-    return {"el": tot[0], "edges_iters": tot[1], "hessvecs": tot[2], "block_updates": tot[3],
+    return {"per_rank": [{"rank": r, "ms_per_step": 1e3 * v[0] / steps, "edges_iters": int(v[1])}
+                         for r, v in enumerate(per_rank)],
+            "el": tot[0], "edges_iters": tot[1], "hessvecs": tot[2], "block_updates": tot[3],
             "gnc_updates": int(tot[4]), "hv": (tot[5], tot[6], int(tot[7])), "xrows": (int(tot[8]), int(tot[9])),
             "mem_max": int(tot[10]), "replay_identical": (tot[11] == world) if replay and snap is not None else None,
             "snap": snap, "native": native, "exchange": mode, "drv": drv}
@@ -506,6 +610,8 @@ def main():
         "scaling": headline,
         "vs_baseline": None,
         "exchange": leg["exchange"],
+        "per_rank": leg["per_rank"],
+        "runtime": _runtime(),
         "dtype": "f64",
         "data": "synthetic (seeded numpy PCG64; Campus bags unavailable offline)",
         "config": {
@@ -620,6 +726,11 @@ def main():
         lcd["unit"] = "candidates/s"
         lcd["ms_per_step"] = 1e3 * lel / lcd["steps"]
         del lcd["elapsed"]
+        hm = lcd["hamming"]
+        n_h, hel = _gather(dist, world, [float(lcd["n_local"] * hm["steps"]), hm["elapsed"]], ["sum", "max"])
+        hm["value"] = n_h / hel
+        hm["ms_per_step"] = 1e3 * hel / hm["steps"]
+        del hm["elapsed"]
         if lcd_cpu:
             lcd["cpu_baseline"] = lcd_cpu
         bow, bow_cpu = bow_leg(args, rank, world, barrier)

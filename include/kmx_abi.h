@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KMX_ABI_VERSION 5
+#define KMX_ABI_VERSION 6
 
 /* error codes */
 #define KMX_OK 0
@@ -41,6 +41,7 @@ extern "C" {
 #define KMX_ESTATE (-3)   /* call out of order (e.g. iterate before set_graph) */
 #define KMX_ENOMEM (-4)
 #define KMX_EUNSUP (-5)   /* unsupported parameter value (e.g. relaxation rank) */
+#define KMX_ETIMEOUT (-6) /* a bounded wait expired (kmx_pgo_sync_timeout)       */
 
 const char* kmx_last_error(void);
 int kmx_abi_version(void);
@@ -155,6 +156,10 @@ int kmx_pgo_set_tcg_poll(kmx_pgo* h, int mode);
  * run the same number of rounds. kmx_pgo_set_graph drops the exchange lists. */
 #define KMX_COMM_ID_BYTES 128
 int kmx_comm_unique_id(void* out, int64_t nbytes);
+/* JSON text: the shared objects libkmx's RCCL and HIP calls resolve to in this
+ * process (dladdr of ncclSend / hipMalloc), ncclGetVersion, the RCCL header
+ * version kmx was built with, hipRuntimeGetVersion / hipDriverGetVersion. */
+int kmx_runtime_info(char* out, int64_t nbytes);
 /* The communicator is created non-blocking: a rank whose peers do not all
  * arrive within timeout_s seconds aborts it and returns KMX_EHIP, so one
  * failing rank cannot strand the others in the rendezvous. */
@@ -250,6 +255,10 @@ int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local);
  * iterate it holds Y. set_iterate restarts the acceleration (V = X). */
 /* Wait for all work enqueued on the handle's stream. */
 int kmx_pgo_sync(kmx_pgo* h);
+/* As kmx_pgo_sync with a deadline: KMX_ETIMEOUT when the stream has not
+ * drained after timeout_s (a round's exchange waiting on a peer that failed);
+ * kmx_pgo_comm_destroy then aborts the communicator, which releases it. */
+int kmx_pgo_sync_timeout(kmx_pgo* h, double timeout_s);
 
 /* GNC: `updateMeasurementWeights()` (drawio:2215) for every non-fixed edge with
  * a local endpoint, evaluated at the current iterate and neighbour table, then
@@ -385,8 +394,21 @@ typedef struct kmx_lcd_params {
                                  re-estimated over all 3D-3D inliers by least
                                  squares (centroids + Kabsch), the restated form
                                  of Kimera-VIO's stereo pose refinement [U]     */
-  int reserved[2];
+  int rng_stream;             /* LC5, the OpenGV fork's "thread_local" sampler
+                                 (README.md:35-36): 0 = every RANSAC problem
+                                 seeds its own std::mt19937 with ransac_seed
+                                 (opengv's SampleConsensusProblem constructor;
+                                 the default); 1 = one engine per verification
+                                 thread, seeded once, that every problem
+                                 continues in candidate order (2D-2D, then the
+                                 Arun / EPnP recovery). Mode 1 is an ordered,
+                                 candidate-serial GPU path. */
+  int reserved[1];
 } kmx_lcd_params;
+
+/* Stages of kmx_lcd_verify_matches. */
+#define KMX_LCD_STAGE_2D2D 1    /* geometricVerificationNister (drawio:2589-2592) */
+#define KMX_LCD_STAGE_RECOVER 2 /* recoverPose (drawio:2595-2598)                 */
 
 /* computeMatchedIndices (drawio:2583-2586): k=2 brute-force match of every
  * query descriptor against the match frame + Lowe ratio. desc are 32-byte ORB
@@ -424,8 +446,21 @@ typedef struct kmx_lcd kmx_lcd;
 int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd** out);
 int kmx_lcd_destroy(kmx_lcd* h);
 int kmx_lcd_set_stream(kmx_lcd* h, void* hip_stream);
-/* Upload the frame pool (host arrays) to the device; kept until replaced. */
+/* Upload the frame pool (host arrays) to the device; kept until replaced.
+ * Replaces every resident frame (a whole-pool reload); frames that arrive one
+ * at a time go through kmx_lcd_add_frames. */
 int kmx_lcd_set_frames(kmx_lcd* h, const kmx_lcd_batch_desc* pool);
+/* LoopClosureDetector::addVLCFrame (drawio:2601; Kimera-Distributed adds each
+ * VLC frame as it arrives, drawio:441-505): append n frames (max_feats must
+ * equal the pool's, or set it on an empty handle). Resident frames are never
+ * re-uploaded: the device pool grows by capacity doubling (one device-to-
+ * device copy per doubling), the sampler table is kept (it depends only on
+ * the parameters and max_feats). *first_id = id of the first appended frame. */
+int kmx_lcd_add_frames(kmx_lcd* h, int32_t n, int32_t max_feats, const int32_t* n_feats,
+                       const uint8_t* desc, const double* bearings, const double* points,
+                       int32_t* first_id);
+/* Frames resident (added or set) and the device capacity in frames. */
+int kmx_lcd_pool_info(kmx_lcd* h, int32_t* n_frames, int32_t* capacity, int32_t* max_feats);
 /* Verify n_cand candidates against the resident pool. results: n_cand records.
  * inlier masks (optional, may be NULL): [n_cand][max_feats] bytes, bit0 = 2D-2D
  * inlier, bit1 = 3D-3D inlier, indexed by match index (position in the pair
@@ -438,6 +473,30 @@ int kmx_lcd_verify(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
 int kmx_lcd_verify_async(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
                          const int32_t* cand_match);
 int kmx_lcd_sync(kmx_lcd* h);
+/* computeMatchedIndices (drawio:2583-2586) on resident frames, batched: for
+ * candidate i the kNN2 + Lowe pairs of frames cand_query[i] / cand_match[i]
+ * in query order, pairs_out[i][k] = (i_query, i_match) for k < k_out[i]
+ * (pairs_out: [n_cand][max_feats][2]). */
+int kmx_lcd_match(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query, const int32_t* cand_match,
+                  int32_t* pairs_out, int32_t* k_out);
+/* geometricVerificationNister and / or recoverPose (drawio:2589-2598) on
+ * caller-supplied correspondences, batched over candidates, no kNN2: the
+ * pairs of candidate i are (i_query[k], i_match[k]) for k in
+ * [mptr[i], mptr[i+1]) (feature indices of frames cand_query[i] /
+ * cand_match[i]; at most max_feats pairs per candidate). stages: a mask of
+ * KMX_LCD_STAGE_*.
+ *   - without KMX_LCD_STAGE_2D2D every pair is a 2D-2D inlier (the
+ *     correspondences are geometricVerificationNister's inliers) and, for the
+ *     1-point 3D-3D recovery, the rotation is T_prior[i] (R row-major, t;
+ *     [n][12]; required then, otherwise may be NULL);
+ *   - without KMX_LCD_STAGE_RECOVER, accepted = mono_inliers >= min_2d2d and
+ *     T_query_match = the 2D-2D pose (unit-norm t).
+ * results / inlier_masks as kmx_lcd_verify, masks indexed by pair position. */
+int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
+                           const int32_t* cand_match, const int64_t* mptr,
+                           const int32_t* i_query, const int32_t* i_match, int stages,
+                           const double* T_prior, kmx_lcd_result* results,
+                           uint8_t* inlier_masks);
 /* Instrumentation: when enabled, every verification brackets its kNN2 launch
  * and its RANSAC launches with HIP events; read_timing synchronises and
  * returns the device times (ms) of the last evented verification. */

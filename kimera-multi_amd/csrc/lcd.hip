@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <thread>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -549,11 +550,18 @@ struct RsParams {
   int pnp;  // PnP or Arun recovery: k_ransac stops after 2D-2D, k_recover recovers the pose
   int prof; // diagnostic phase timers (k_ransac_coop)
   int algo; // KMX_ALGO_*: 5-point minimal solver (k_ransac_coop; k_ransac is Nister only)
+  int stages;       // KMX_LCD_STAGE_* (kmx_lcd_verify: both)
+  int tab_fixed;    // ordered sampler (rng_stream 1): `table` is this candidate's own row
+  const double* prior;  // [n][12] 2D-2D pose of the 1-point recovery without the 2D-2D stage
+  int* hyps;        // ordered sampler: passes the serial loop drew (iterations + skipped) per candidate
+  int* nrec;        // ordered sampler: size of the recovery problem (stereo-valid 2D-2D inliers)
 };
 struct PnpParams {
   double thr, prob;
   int max_iter, min2d, min_pnp, pmax;
-  int refine;  // Arun recovery only (refit_3d3d)
+  int refine;     // Arun recovery only (refit_3d3d)
+  int tab_fixed;  // as RsParams
+  int* hyps;      // as RsParams
 };
 
 // refine_pose (oracle/lcd_oracle.c refit_3d3d, the same operations in the same
@@ -1870,7 +1878,9 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
   unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
   kmx_lcd_result* R_ = res + c;
   for (int j = lane; j < N && mask; j += RS_BLOCK) mask[j] = 0;
-  if (K < 5) {
+  const bool st2d = (P.stages & KMX_LCD_STAGE_2D2D) != 0;
+  if (K < 5 && st2d) {
+    if (P.hyps && lane == 0) P.hyps[c] = 0;
     if (lane == 0) {
       kmx_lcd_result r = {};
       r.n_matches = K;
@@ -1896,9 +1906,9 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
   int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
   double kk = 1.0;
   const int max_skip = P.max_iter * 10;
-  const short* tab = table + (size_t)(K - 5) * P.pmax * 5;
+  const short* tab = P.tab_fixed ? table : table + (size_t)(K - 5) * P.pmax * 5;
   const bool prof = (c < 64) && P.prof == 1;
-  bool done = false;
+  bool done = !st2d;  // without the 2D-2D stage every pair is an inlier of the caller's pose
   // the serial loop's bookkeeping of one hypothesis's model (w.ok, w.mR, w.mt):
   // a failed solve counts as skipped; otherwise its inliers, the best model and
   // the adaptive iteration bound, and the iteration count
@@ -1936,7 +1946,8 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
     wsync();
     if (iterations > P.max_iter) done = true;
   };
-  if constexpr (STEW) {
+  if (!st2d) {
+  } else if constexpr (STEW) {
     // SG hypotheses' eigenvalues at a time, then each hypothesis in order under
     // the serial loop's tests (a batch may run past the stop: those are never
     // scored, so the results are the one-at-a-time loop's)
@@ -1971,7 +1982,8 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
       account(w.ok != 0, w.mR, w.mt);
     }
   }
-  if (!have) {
+  if (P.hyps && lane == 0) P.hyps[c] = iterations + skipped;
+  if (!have && st2d) {
     if (lane == 0) {
       kmx_lcd_result r = {};
       r.n_matches = K;
@@ -1981,12 +1993,18 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
     return;
   }
   double Rb[9], tb[3];
-  for (int i = 0; i < 9; ++i) Rb[i] = w.bestm[i];
-  for (int i = 0; i < 3; ++i) tb[i] = w.bestm[9 + i];
+  if (st2d) {
+    for (int i = 0; i < 9; ++i) Rb[i] = w.bestm[i];
+    for (int i = 0; i < 3; ++i) tb[i] = w.bestm[9 + i];
+  } else {  // the caller's 2D-2D pose (only the 1-point recovery reads it)
+    for (int i = 0; i < 12; ++i) (i < 9 ? Rb[i] : tb[i - 9]) = P.prior ? P.prior[(size_t)c * 12 + i] : (i % 4 == 0 && i < 9 ? 1.0 : 0.0);
+  }
+  // a pair's 2D-2D inlier test: the best model's, or every pair without the stage
+  auto inl2d = [&](int j) { return (j < K) && (!st2d || model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d); };
   int n_in = 0;
   for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
     const int j = j0 + lane;
-    const bool in = (j < K) && model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d;
+    const bool in = inl2d(j);
     if (j < K && mask) mask[j] = in ? 1 : 0;
     n_in += __popcll(__ballot(in));
   }
@@ -1996,11 +2014,31 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
   r.iterations_2d2d = iterations;
   for (int i = 0; i < 9; ++i) r.T_query_match[i] = Rb[i];
   for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = tb[i];
-  if (n_in < P.min2d) {
+  if (st2d && n_in < P.min2d) {
+    if (lane == 0) *R_ = r;
+    return;
+  }
+  if (!(P.stages & KMX_LCD_STAGE_RECOVER)) {  // geometricVerificationNister alone
+    r.accepted = 1;
     if (lane == 0) *R_ = r;
     return;
   }
   if (P.pnp) {
+    if (P.nrec) {  // ordered sampler: the host sizes the recovery's sample row
+      int n2 = 0;
+      for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
+        const int j = j0 + lane;
+        bool v = inl2d(j);
+        if (v) {
+          const int2 pr = pl[j];
+          const double* a = points + ((size_t)q * N + pr.x) * 3;
+          const double* b = points + ((size_t)m * N + pr.y) * 3;
+          v = !(isnan(a[0]) || isnan(a[1]) || isnan(a[2]) || isnan(b[0]) || isnan(b[1]) || isnan(b[2]));
+        }
+        n2 += __popcll(__ballot(v));
+      }
+      if (lane == 0) P.nrec[c] = n2;
+    }
     if (lane == 0) {
       for (int i = 0; i < 12; ++i) r.T_query_match[i] = 0.0;
       *R_ = r;
@@ -2015,7 +2053,7 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
   int n3 = 0;
   for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {  // compact inlier positions in pair order
     const int j = j0 + lane;
-    const bool in = (j < K) && model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d;
+    const bool in = inl2d(j);
     const unsigned long long bm = __ballot(in);
     const int pos = n3 + __popcll(bm & ((1ull << lane) - 1ull));
     if (in) reinterpret_cast<int*>(F1)[pos] = j;  // F1 rows < j0 + 64 are no longer read
@@ -2188,7 +2226,10 @@ __global__ __launch_bounds__(RS_BLOCK) void k_recover(const double* bearings, co
   const int c = xcd_candidate(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
   kmx_lcd_result* R_ = res + c;
-  if (R_->mono_inliers < P.min2d) return;
+  if (R_->mono_inliers < P.min2d) {
+    if (P.hyps && lane == 0) P.hyps[c] = 0;
+    return;
+  }
   const int K = Kin[c];
   const int q = cq[c], m = cm[c];
   double* Aq = sm_d;                  // [n2][3]
@@ -2228,7 +2269,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_recover(const double* bearings, co
   double kk = 1.0;
   const int max_skip = P.max_iter * 10;
   if (n2 >= S) {
-    const short* tab = table + (size_t)(n2 - S) * P.pmax * S;
+    const short* tab = P.tab_fixed ? table : table + (size_t)(n2 - S) * P.pmax * S;
     for (int base = 0;; base += RS_BLOCK) {
       const int p = base + lane;
       int ok = 0, count = 0;
@@ -2286,6 +2327,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_recover(const double* bearings, co
     }
   }
   __syncthreads();
+  if (P.hyps && lane == 0) P.hyps[c] = iterations + skipped;
   const int have_model = ctrl[1];
   int np = 0;
   double Ro[9], to[3];
@@ -2339,13 +2381,18 @@ struct kmx_lcd {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  int F = 0, N = 0;
+  // frame pool: F resident frames of N feature slots, device capacity capF frames
+  int F = 0, N = 0, capF = 0;
+  std::vector<int> h_nfeat;  // host copy of the feature counts (argument checks)
   uint32_t* d_desc = nullptr;
   double* d_bear = nullptr;
   double* d_pts = nullptr;
   int* d_nfeat = nullptr;
+  // sampler tables, built for rows K in [S, table_N] (they depend only on the
+  // parameters and N, so frames can be added without rebuilding them)
   short* d_table = nullptr;
   short* d_table_rec = nullptr;  // samples of the recovery RANSAC (6: PnP, 3: Arun), built when used
+  int table_N = 0;
   int pmax = 0;
   // candidate buffers
   int cap = 0;
@@ -2355,6 +2402,16 @@ struct kmx_lcd {
   unsigned char* d_mask = nullptr;
   double* d_fbuf = nullptr;  // [slots][6 N + STASH] compact match bearings + Stewenius stash, per k_ransac_coop wave
   int* d_next = nullptr;     // k_ransac_coop's work-queue counter
+  // caller-supplied correspondences (kmx_lcd_verify_matches): CSR staging
+  size_t pair_cap = 0;
+  int64_t* d_mptr = nullptr;
+  int *d_iq = nullptr, *d_im = nullptr;
+  double* d_prior = nullptr;
+  // ordered sampler (rng_stream 1): the verification thread's engine, one
+  // candidate's sample row, the passes each problem drew, recovery sizes
+  std::mt19937 stream_rng;
+  short* d_row = nullptr;
+  int *d_hyps = nullptr, *d_nrec = nullptr;
   int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
   // kmx_lcd_enable_timing: events around the kNN2 and the RANSAC launches
   bool timing = false;
@@ -2364,48 +2421,107 @@ struct kmx_lcd {
 
 namespace {
 
-void lcd_free_pool(kmx_lcd* h) {
-  void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat, h->d_table, h->d_table_rec};
+void lcd_free_frames(kmx_lcd* h) {
+  void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat};
   for (void* x : p)
     if (x) (void)hipFree(x);
-  h->d_desc = nullptr; h->d_bear = h->d_pts = nullptr; h->d_nfeat = nullptr; h->d_table = nullptr; h->d_table_rec = nullptr;
+  h->d_desc = nullptr; h->d_bear = h->d_pts = nullptr; h->d_nfeat = nullptr;
+  h->F = h->capF = 0;
+  h->h_nfeat.clear();
+}
+void lcd_free_tables(kmx_lcd* h) {
+  if (h->d_table) (void)hipFree(h->d_table);
+  if (h->d_table_rec) (void)hipFree(h->d_table_rec);
+  h->d_table = h->d_table_rec = nullptr;
+  h->table_N = 0;
 }
 void lcd_free_cand(kmx_lcd* h) {
-  void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask, h->d_fbuf, h->d_next};
+  void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask, h->d_fbuf, h->d_next, h->d_hyps, h->d_nrec,
+               h->d_prior};
   for (void* x : p)
     if (x) (void)hipFree(x);
   h->d_cq = h->d_cm = h->d_K = nullptr; h->d_pairs = nullptr; h->d_res = nullptr; h->d_mask = nullptr;
   h->d_fbuf = nullptr;
-  h->d_next = nullptr;
+  h->d_next = h->d_hyps = h->d_nrec = nullptr;
+  h->d_prior = nullptr;
   h->cap = 0;
 }
+void lcd_free_pairs(kmx_lcd* h) {
+  void* p[] = {h->d_mptr, h->d_iq, h->d_im, h->d_row};
+  for (void* x : p)
+    if (x) (void)hipFree(x);
+  h->d_mptr = nullptr; h->d_iq = h->d_im = nullptr; h->d_row = nullptr;
+  h->pair_cap = 0;
+}
 
-// opengv sampler table: for every K in [5, N], the 5 indices drawn by each of
-// the first pmax passes (std::mt19937 seeded per problem; drawIndexSample swap
-// shuffle over a persistent index vector; GCC-9 or GCC-11 uniform_int).
-void build_table(const kmx_lcd_params& P, int N, int pmax, std::vector<short>& tab, int S = 5) {
-  tab.assign((size_t)std::max(N - S + 1, 1) * pmax * S, 0);
-  std::vector<int> sh;
-  for (int K = S; K <= N; ++K) {
-    std::mt19937 rng(P.ransac_seed);
-    sh.resize(K);
-    for (int i = 0; i < K; ++i) sh[i] = i;
-    short* out = tab.data() + (size_t)(K - S) * pmax * S;
-    for (int p = 0; p < pmax; ++p) {
-      for (int i = 0; i < S; ++i) {
-        uint32_t x;
-        if (P.rng_variant == KMX_RNG_GCC11) {
-          x = (uint32_t)rng() >> 1;
-        } else {
-          do x = (uint32_t)rng();
-          while (x >= 0x80000000u);
-        }
-        const int j = i + (int)((size_t)x % (size_t)(K - i));
-        std::swap(sh[i], sh[j]);
-      }
-      for (int i = 0; i < S; ++i) out[p * S + i] = (short)sh[i];
-    }
+// One pass of opengv's drawIndexSample: S swaps of the persistent shuffle over
+// the problem's K indices, each by std::uniform_int_distribution<int>(0,
+// INT_MAX) over std::mt19937 (GCC-9 rejection or GCC-11 x >> 1).
+inline int sampler_draw(std::mt19937& rng, int variant) {
+  uint32_t x;
+  if (variant == KMX_RNG_GCC11) {
+    x = (uint32_t)rng() >> 1;
+  } else {
+    do x = (uint32_t)rng();
+    while (x >= 0x80000000u);
   }
+  return (int)x;
+}
+void sample_row(std::mt19937& rng, int variant, int K, int pmax, int S, short* out) {
+  std::vector<int> sh(K);
+  for (int i = 0; i < K; ++i) sh[i] = i;
+  for (int p = 0; p < pmax; ++p) {
+    for (int i = 0; i < S; ++i) {
+      const int j = i + (int)((size_t)sampler_draw(rng, variant) % (size_t)(K - i));
+      std::swap(sh[i], sh[j]);
+    }
+    for (int i = 0; i < S; ++i) out[(size_t)p * S + i] = (short)sh[i];
+  }
+}
+
+// opengv sampler table: for every K in [S, N], the S indices drawn by each of
+// the first pmax passes (std::mt19937 seeded per problem). Rows are
+// independent, so they are built on a few host threads.
+void build_table(const kmx_lcd_params& P, int N, int pmax, std::vector<short>& tab, int S = 5) {
+  const int rows = std::max(N - S + 1, 1);
+  tab.assign((size_t)rows * pmax * S, 0);
+  const int nt = std::max(1, std::min(8, rows / 32));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (int K = S + t; K <= N; K += nt) {
+        std::mt19937 rng(P.ransac_seed);
+        sample_row(rng, P.rng_variant, K, pmax, S, tab.data() + (size_t)(K - S) * pmax * S);
+      }
+    });
+  for (auto& x : th) x.join();
+}
+
+bool rec_sampled(const kmx_lcd_params& P) { return P.pose_recovery_type == 1 || !P.use_1point_3d3d; }
+int rec_S(const kmx_lcd_params& P) { return P.pose_recovery_type == 1 ? PNP_S : 3; }
+
+// Sampler tables for the pool's N (kept across set_frames / add_frames with the
+// same N). The ordered sampler draws its rows per candidate instead.
+int ensure_tables(kmx_lcd* h) {
+  // every pass the serial loop can reach: (max_iter + 1) iterations + 10 * max_iter skips
+  h->pmax = h->P.ransac_max_iterations + 1 + 10 * h->P.ransac_max_iterations;
+  if (h->P.rng_stream) {
+    if (!h->d_row) KMX_HIP(hipMalloc(&h->d_row, sizeof(short) * (size_t)h->pmax * PNP_S));
+    return 0;
+  }
+  if (h->table_N == h->N && h->d_table) return 0;
+  lcd_free_tables(h);
+  std::vector<short> tab;
+  build_table(h->P, h->N, h->pmax, tab);
+  KMX_HIP(hipMalloc(&h->d_table, sizeof(short) * tab.size()));
+  KMX_HIP(hipMemcpy(h->d_table, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
+  if (rec_sampled(h->P)) {
+    build_table(h->P, h->N, h->pmax, tab, rec_S(h->P));
+    KMX_HIP(hipMalloc(&h->d_table_rec, sizeof(short) * tab.size()));
+    KMX_HIP(hipMemcpy(h->d_table_rec, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
+  }
+  h->table_N = h->N;
+  return 0;
 }
 
 int ensure_cap(kmx_lcd* h, int n) {
@@ -2418,7 +2534,9 @@ int ensure_cap(kmx_lcd* h, int n) {
       hipMalloc(&h->d_res, sizeof(kmx_lcd_result) * cap) != hipSuccess ||
       hipMalloc(&h->d_mask, (size_t)cap * h->N) != hipSuccess ||
       hipMalloc(&h->d_fbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::min(cap, RS_MAX_SLOTS)) != hipSuccess ||
-      hipMalloc(&h->d_next, sizeof(int)) != hipSuccess) {
+      hipMalloc(&h->d_next, sizeof(int)) != hipSuccess || hipMalloc(&h->d_hyps, sizeof(int) * cap) != hipSuccess ||
+      hipMalloc(&h->d_nrec, sizeof(int) * cap) != hipSuccess ||
+      hipMalloc(&h->d_prior, sizeof(double) * 12 * (size_t)cap) != hipSuccess) {
     lcd_free_cand(h);
     return kmx::fail(KMX_ENOMEM, "candidate buffers");
   }
@@ -2426,6 +2544,156 @@ int ensure_cap(kmx_lcd* h, int n) {
   return 0;
 }
 
+// CSR correspondences -> the per-candidate pair rows of k_ransac_coop
+// (pairs[c][k], K[c]); one workgroup per candidate.
+__global__ __launch_bounds__(256) void k_scatter_pairs(const int64_t* mptr, const int* iq, const int* im, int N,
+                                                       int2* pairs, int* Kout) {
+  const int c = blockIdx.x;
+  const int64_t b = mptr[c];
+  const int K = (int)(mptr[c + 1] - b);
+  for (int k = threadIdx.x; k < K; k += blockDim.x) pairs[(size_t)c * N + k] = make_int2(iq[b + k], im[b + k]);
+  if (threadIdx.x == 0) Kout[c] = K;
+}
+
+RsParams rs_params(const kmx_lcd* h, int stages) {
+  RsParams rp{};
+  rp.thr2d = h->P.ransac_threshold_2d2d;
+  rp.thr3d = h->P.ransac_threshold_3d3d;
+  rp.prob = h->P.ransac_probability;
+  rp.max_iter = h->P.ransac_max_iterations;
+  rp.min2d = h->P.min_2d2d_inliers;
+  rp.min3d = h->P.min_3d3d_inliers;
+  rp.pmax = h->pmax;
+  rp.pnp = rec_sampled(h->P) ? 1 : 0;  // k_recover takes over
+  rp.prof = h->prof;
+  rp.algo = h->P.algorithm_2d2d;
+  rp.refine = h->P.refine_pose && h->P.pose_recovery_type == 0 ? 1 : 0;
+  rp.stages = stages;
+  rp.prior = h->d_prior;
+  return rp;
+}
+PnpParams pnp_params(const kmx_lcd* h, int stages) {
+  const bool pnp = h->P.pose_recovery_type == 1;
+  PnpParams pp{};
+  pp.thr = pnp ? h->P.ransac_threshold_2d3d : h->P.ransac_threshold_3d3d;
+  pp.prob = h->P.ransac_probability;
+  pp.max_iter = h->P.ransac_max_iterations;
+  // without the 2D-2D stage the caller's pairs are the inliers: recover whatever K is
+  pp.min2d = (stages & KMX_LCD_STAGE_2D2D) ? h->P.min_2d2d_inliers : 0;
+  pp.min_pnp = pnp ? h->P.min_2d3d_inliers : h->P.min_3d3d_inliers;
+  pp.refine = !pnp && h->P.refine_pose ? 1 : 0;
+  pp.pmax = h->pmax;
+  return pp;
+}
+
+// k_ransac_coop over candidates [0, n) of the (offset) candidate arrays.
+int launch_ransac(kmx_lcd* h, int n, const RsParams& rp, const short* table, int c0, bool masks) {
+  // KMX_COOP_LB: minimum waves per SIMD (register-budget A/B). Stewenius: the
+  // batch's LDS (12.6 KB per wave) admits 12 waves per CU, so 3 waves per SIMD
+  // and their 168 VGPRs; Nister: 4 waves per SIMD
+  static const int clb = [] {
+    const char* v = std::getenv("KMX_COOP_LB");
+    return v ? std::atoi(v) : 0;
+  }();
+  const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
+  auto kc = stew ? ((clb == 2) ? k_ransac_coop<2, true> : k_ransac_coop<3, true>)
+                 : ((clb == 3) ? k_ransac_coop<3, false> : k_ransac_coop<4, false>);
+  // one wave per resident slot (<= RS_MAX_SLOTS: the scratch is sized for it)
+  int per_cu = 0, dev = 0, cus = 0;
+  KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kc, RS_BLOCK, 0));
+  KMX_HIP(hipGetDevice(&dev));
+  KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int slots = std::max(1, std::min({n, std::max(per_cu, 1) * cus, RS_MAX_SLOTS, h->cap}));
+  KMX_HIP(hipMemsetAsync(h->d_next, 0, sizeof(int), h->stream));
+  RsParams p = rp;
+  if (p.prior) p.prior += (size_t)c0 * 12;
+  if (p.hyps) p.hyps += c0;
+  if (p.nrec) p.nrec += c0;
+  hipLaunchKernelGGL(kc, dim3(slots), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
+                     (const double*)h->d_pts, h->N, (const int*)h->d_cq + c0, (const int*)h->d_cm + c0,
+                     (const int2*)h->d_pairs + (size_t)c0 * h->N, (const int*)h->d_K + c0, table, p, h->d_res + c0,
+                     masks ? h->d_mask + (size_t)c0 * h->N : nullptr, h->d_fbuf, n, h->d_next);
+  return 0;
+}
+int launch_recover(kmx_lcd* h, int n, const PnpParams& pp, const short* table, int c0) {
+  const bool pnp = h->P.pose_recovery_type == 1;
+  const size_t smem = sizeof(double) * (6 * (size_t)h->N + 64 * 12 + 12) + sizeof(int) * (64 + 64 + 4 + (size_t)h->N);
+  PnpParams p = pp;
+  if (p.hyps) p.hyps += c0;
+  hipLaunchKernelGGL(pnp ? k_recover<true> : k_recover<false>, dim3(n), dim3(RS_BLOCK), smem, h->stream,
+                     (const double*)h->d_bear, (const double*)h->d_pts, h->N, (const int*)h->d_cq + c0,
+                     (const int*)h->d_cm + c0, (const int2*)h->d_pairs + (size_t)c0 * h->N, (const int*)h->d_K + c0,
+                     table, p, h->d_res + c0, h->d_mask + (size_t)c0 * h->N);
+  return 0;
+}
+
+// The ordered sampler (rng_stream 1): candidates one after the other, each
+// RANSAC problem drawing from the handle's engine where the previous problem
+// left it — a chain through every candidate (the k-th problem's first sample
+// depends on how many passes problem k-1 drew, known only when it ends), so
+// this path is serial by construction: per problem the host draws the
+// problem's sample row from a copy of the engine, the kernel runs that one
+// problem, and the engine then advances by the passes the serial loop drew.
+int verify_ordered(kmx_lcd* h, int n, int stages, bool masks) {
+  std::vector<int> K(n);
+  KMX_HIP(hipMemcpyAsync(K.data(), h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  RsParams rp = rs_params(h, stages);
+  rp.tab_fixed = 1;
+  rp.hyps = h->d_hyps;
+  rp.nrec = rec_sampled(h->P) ? h->d_nrec : nullptr;
+  PnpParams pp = pnp_params(h, stages);
+  pp.tab_fixed = 1;
+  pp.hyps = h->d_hyps;
+  const int v = h->P.rng_variant;
+  std::vector<short> row((size_t)h->pmax * PNP_S);
+  auto advance = [&](int passes, int S) {
+    for (long i = 0; i < (long)passes * S; ++i) (void)sampler_draw(h->stream_rng, v);
+  };
+  for (int c = 0; c < n; ++c) {
+    const bool st2d = (stages & KMX_LCD_STAGE_2D2D) != 0;
+    if (st2d && K[c] >= 5) {
+      std::mt19937 probe = h->stream_rng;
+      sample_row(probe, v, K[c], h->pmax, 5, row.data());
+      KMX_HIP(hipMemcpyAsync(h->d_row, row.data(), sizeof(short) * (size_t)h->pmax * 5, hipMemcpyHostToDevice,
+                             h->stream));
+    }
+    if (int rc = launch_ransac(h, 1, rp, h->d_row, c, masks || rp.pnp)) return rc;
+    int got[2] = {0, 0};
+    KMX_HIP(hipMemcpyAsync(&got[0], h->d_hyps + c, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    if (rp.nrec) KMX_HIP(hipMemcpyAsync(&got[1], h->d_nrec + c, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    KMX_HIP(hipStreamSynchronize(h->stream));
+    if (st2d && K[c] >= 5) advance(got[0], 5);
+    if (!rp.pnp || !(stages & KMX_LCD_STAGE_RECOVER)) continue;
+    kmx_lcd_result r{};
+    KMX_HIP(hipMemcpyAsync(&r, h->d_res + c, sizeof(r), hipMemcpyDeviceToHost, h->stream));
+    KMX_HIP(hipStreamSynchronize(h->stream));
+    if (r.mono_inliers < pp.min2d) continue;
+    const int S = rec_S(h->P), n2 = got[1];
+    if (n2 >= S) {
+      std::mt19937 probe = h->stream_rng;
+      sample_row(probe, v, n2, h->pmax, S, row.data());
+      KMX_HIP(hipMemcpyAsync(h->d_row, row.data(), sizeof(short) * (size_t)h->pmax * S, hipMemcpyHostToDevice,
+                             h->stream));
+    }
+    if (int rc = launch_recover(h, 1, pp, h->d_row, c)) return rc;
+    int hy = 0;
+    KMX_HIP(hipMemcpyAsync(&hy, h->d_hyps + c, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    KMX_HIP(hipStreamSynchronize(h->stream));
+    if (n2 >= S) advance(hy, S);
+  }
+  return 0;
+}
+
+// Everything after the pair rows d_pairs / d_K exist: RANSAC, then recovery.
+int enqueue_ransac(kmx_lcd* h, int n, int stages, bool want_masks) {
+  if (h->P.rng_stream) return verify_ordered(h, n, stages, want_masks);
+  const RsParams rp = rs_params(h, stages);
+  if (int rc = launch_ransac(h, n, rp, h->d_table, 0, want_masks || rp.pnp)) return rc;
+  if (rp.pnp && (stages & KMX_LCD_STAGE_RECOVER))
+    if (int rc = launch_recover(h, n, pnp_params(h, stages), h->d_table_rec, 0)) return rc;
+  return 0;
+}
 
 int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   if (n == 0) return 0;
@@ -2441,60 +2709,57 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
                      (const int*)h->d_nfeat, h->N, (const int*)h->d_cq, (const int*)h->d_cm, h->P.norm,
                      h->P.lowe_ratio, h->d_pairs, h->d_K);
   if (h->timing) KMX_HIP(hipEventRecord(h->ev[1], h->stream));
-  RsParams rp;
-  rp.thr2d = h->P.ransac_threshold_2d2d;
-  rp.thr3d = h->P.ransac_threshold_3d3d;
-  rp.prob = h->P.ransac_probability;
-  rp.max_iter = h->P.ransac_max_iterations;
-  rp.min2d = h->P.min_2d2d_inliers;
-  rp.min3d = h->P.min_3d3d_inliers;
-  rp.pmax = h->pmax;
-  rp.pnp = (h->P.pose_recovery_type == 1 || !h->P.use_1point_3d3d) ? 1 : 0;  // k_recover takes over
-  rp.prof = h->prof;
-  rp.algo = h->P.algorithm_2d2d;
-  rp.refine = h->P.refine_pose && h->P.pose_recovery_type == 0 ? 1 : 0;
-  {
-    // KMX_COOP_LB: minimum waves per SIMD (register-budget A/B). Stewenius: the
-    // batch's LDS (12.6 KB per wave) admits 12 waves per CU, so 3 waves per SIMD
-    // and their 168 VGPRs; Nister: 4 waves per SIMD
-    static const int clb = [] {
-      const char* v = std::getenv("KMX_COOP_LB");
-      return v ? std::atoi(v) : 0;
-    }();
-    const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
-    auto kc = stew ? ((clb == 2) ? k_ransac_coop<2, true> : k_ransac_coop<3, true>)
-                   : ((clb == 3) ? k_ransac_coop<3, false> : k_ransac_coop<4, false>);
-    // one wave per resident slot (<= RS_MAX_SLOTS: the scratch is sized for it)
-    int per_cu = 0, dev = 0, cus = 0;
-    KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kc, RS_BLOCK, 0));
-    KMX_HIP(hipGetDevice(&dev));
-    KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const int slots = std::max(1, std::min({n, std::max(per_cu, 1) * cus, RS_MAX_SLOTS, h->cap}));
-    KMX_HIP(hipMemsetAsync(h->d_next, 0, sizeof(int), h->stream));
-    hipLaunchKernelGGL(kc, dim3(slots), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
-                       (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
-                       (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp, h->d_res,
-                       (want_masks || rp.pnp) ? h->d_mask : nullptr, h->d_fbuf, n, h->d_next);
-  }
-  if (rp.pnp) {
-    const bool pnp = h->P.pose_recovery_type == 1;
-    PnpParams pp;
-    pp.thr = pnp ? h->P.ransac_threshold_2d3d : h->P.ransac_threshold_3d3d;
-    pp.prob = h->P.ransac_probability;
-    pp.max_iter = h->P.ransac_max_iterations;
-    pp.min2d = h->P.min_2d2d_inliers;
-    pp.min_pnp = pnp ? h->P.min_2d3d_inliers : h->P.min_3d3d_inliers;
-    pp.refine = !pnp && h->P.refine_pose ? 1 : 0;
-    pp.pmax = h->pmax;
-    const size_t smem = sizeof(double) * (6 * (size_t)h->N + 64 * 12 + 12) + sizeof(int) * (64 + 64 + 4 + (size_t)h->N);
-    hipLaunchKernelGGL(pnp ? k_recover<true> : k_recover<false>, dim3(n), dim3(RS_BLOCK), smem, h->stream,
-                       (const double*)h->d_bear,
-                       (const double*)h->d_pts, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
-                       (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table_rec, pp, h->d_res,
-                       h->d_mask);
-  }
+  if (int rc = enqueue_ransac(h, n, KMX_LCD_STAGE_2D2D | KMX_LCD_STAGE_RECOVER, want_masks)) return rc;
   if (h->timing) KMX_HIP(hipEventRecord(h->ev[2], h->stream));
   KMX_HIP(hipGetLastError());
+  return 0;
+}
+
+// Device pool of at least `need` frames of N slots: capacity doubling, the
+// resident frames copied device to device (never re-uploaded).
+int grow_pool(kmx_lcd* h, int need) {
+  if (need <= h->capF) return 0;
+  const int cap = std::max({need, 2 * h->capF, 64});
+  const size_t FN = (size_t)cap * h->N, old = (size_t)h->F * h->N;
+  uint32_t* desc = nullptr;
+  double *bear = nullptr, *pts = nullptr;
+  int* nf = nullptr;
+  if (hipMalloc(&desc, FN * 32) != hipSuccess || hipMalloc(&bear, FN * 3 * sizeof(double)) != hipSuccess ||
+      hipMalloc(&pts, FN * 3 * sizeof(double)) != hipSuccess || hipMalloc(&nf, sizeof(int) * cap) != hipSuccess) {
+    for (void* x : {(void*)desc, (void*)bear, (void*)pts, (void*)nf})
+      if (x) (void)hipFree(x);
+    return kmx::fail(KMX_ENOMEM, "frame pool");
+  }
+  if (h->F) {
+    KMX_HIP(hipMemcpyAsync(desc, h->d_desc, old * 32, hipMemcpyDeviceToDevice, h->stream));
+    KMX_HIP(hipMemcpyAsync(bear, h->d_bear, old * 3 * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    KMX_HIP(hipMemcpyAsync(pts, h->d_pts, old * 3 * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    KMX_HIP(hipMemcpyAsync(nf, h->d_nfeat, sizeof(int) * h->F, hipMemcpyDeviceToDevice, h->stream));
+    KMX_HIP(hipStreamSynchronize(h->stream));
+  }
+  for (void* x : {(void*)h->d_desc, (void*)h->d_bear, (void*)h->d_pts, (void*)h->d_nfeat})
+    if (x) (void)hipFree(x);
+  h->d_desc = desc;
+  h->d_bear = bear;
+  h->d_pts = pts;
+  h->d_nfeat = nf;
+  h->capF = cap;
+  return 0;
+}
+
+// Frames [F, F + n) from host arrays (desc [n][N][32], bearings / points
+// [n][N][3]); the caller has grown the pool.
+int upload_frames(kmx_lcd* h, int n, const int32_t* n_feats, const uint8_t* desc, const double* bearings,
+                  const double* points) {
+  const size_t at = (size_t)h->F * h->N, FN = (size_t)n * h->N;
+  KMX_HIP(hipMemcpyAsync(reinterpret_cast<uint8_t*>(h->d_desc) + at * 32, desc, FN * 32, hipMemcpyHostToDevice,
+                         h->stream));
+  KMX_HIP(hipMemcpyAsync(h->d_bear + at * 3, bearings, FN * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipMemcpyAsync(h->d_pts + at * 3, points, FN * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipMemcpyAsync(h->d_nfeat + h->F, n_feats, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));  // the host arrays may go away after return
+  h->h_nfeat.insert(h->h_nfeat.end(), n_feats, n_feats + n);
+  h->F += n;
   return 0;
 }
 
@@ -2511,6 +2776,7 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
   KMX_CHECK(params->algorithm_2d2d == KMX_ALGO_STEWENIUS || params->algorithm_2d2d == KMX_ALGO_NISTER, KMX_EUNSUP,
             "ransac_2d2d_algorithm: 0 (Stewenius) and 1 (Nister) are built");
   KMX_CHECK(params->ransac_max_iterations > 0, KMX_EINVAL, "ransac_max_iterations must be > 0");
+  KMX_CHECK(params->rng_stream == 0 || params->rng_stream == 1, KMX_EINVAL, "rng_stream is 0 or 1");
   int ndev = 0;
   KMX_HIP(hipGetDeviceCount(&ndev));
   KMX_CHECK(device >= 0 && device < ndev, KMX_EINVAL, "bad HIP device ordinal");
@@ -2518,6 +2784,7 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
   kmx_lcd* h = new kmx_lcd();
   h->P = *params;
   h->device = device;
+  h->stream_rng.seed(params->ransac_seed);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return kmx::fail(KMX_EHIP, "hipStreamCreate");
@@ -2533,8 +2800,10 @@ extern "C" int kmx_lcd_destroy(kmx_lcd* h) {
   if (!h) return KMX_OK;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  lcd_free_pool(h);
+  lcd_free_frames(h);
+  lcd_free_tables(h);
   lcd_free_cand(h);
+  lcd_free_pairs(h);
   if (h->ev_ok)
     for (auto e : h->ev) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -2543,6 +2812,7 @@ extern "C" int kmx_lcd_destroy(kmx_lcd* h) {
 }
 
 extern "C" int kmx_lcd_set_stream(kmx_lcd* h, void* s) {
+  KMX_GUARD_BEGIN
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
   if (h->own_stream && h->stream) {
@@ -2552,6 +2822,7 @@ extern "C" int kmx_lcd_set_stream(kmx_lcd* h, void* s) {
   h->own_stream = false;
   h->stream = reinterpret_cast<hipStream_t>(s);
   return KMX_OK;
+  KMX_GUARD_END
 }
 
 extern "C" int kmx_lcd_set_frames(kmx_lcd* h, const kmx_lcd_batch_desc* pool) {
@@ -2564,37 +2835,51 @@ extern "C" int kmx_lcd_set_frames(kmx_lcd* h, const kmx_lcd_batch_desc* pool) {
     KMX_CHECK(pool->n_feats[f] >= 0 && pool->n_feats[f] <= pool->max_feats, KMX_EINVAL, "bad n_feats");
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  const bool regrow = pool->max_feats != h->N;
-  lcd_free_pool(h);
-  if (regrow) lcd_free_cand(h);
-  h->F = pool->n_frames;
+  if (pool->max_feats != h->N) lcd_free_cand(h);
+  lcd_free_frames(h);
   h->N = pool->max_feats;
-  const size_t FN = (size_t)h->F * h->N;
-  KMX_HIP(hipMalloc(&h->d_desc, FN * 32));
-  KMX_HIP(hipMalloc(&h->d_bear, FN * 3 * sizeof(double)));
-  KMX_HIP(hipMalloc(&h->d_pts, FN * 3 * sizeof(double)));
-  KMX_HIP(hipMalloc(&h->d_nfeat, sizeof(int) * h->F));
-  KMX_HIP(hipMemcpy(h->d_desc, pool->desc, FN * 32, hipMemcpyHostToDevice));
-  KMX_HIP(hipMemcpy(h->d_bear, pool->bearings, FN * 3 * sizeof(double), hipMemcpyHostToDevice));
-  KMX_HIP(hipMemcpy(h->d_pts, pool->points, FN * 3 * sizeof(double), hipMemcpyHostToDevice));
-  KMX_HIP(hipMemcpy(h->d_nfeat, pool->n_feats, sizeof(int) * h->F, hipMemcpyHostToDevice));
-  // every pass the serial loop can reach: (max_iter + 1) iterations + 10 * max_iter skips
-  h->pmax = h->P.ransac_max_iterations + 1 + 10 * h->P.ransac_max_iterations;
-  std::vector<short> tab;
-  build_table(h->P, h->N, h->pmax, tab);
-  KMX_HIP(hipMalloc(&h->d_table, sizeof(short) * tab.size()));
-  KMX_HIP(hipMemcpy(h->d_table, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
-  if (h->P.pose_recovery_type == 1 || !h->P.use_1point_3d3d) {
-    build_table(h->P, h->N, h->pmax, tab, h->P.pose_recovery_type == 1 ? PNP_S : 3);
-    KMX_HIP(hipMalloc(&h->d_table_rec, sizeof(short) * tab.size()));
-    KMX_HIP(hipMemcpy(h->d_table_rec, tab.data(), sizeof(short) * tab.size(), hipMemcpyHostToDevice));
-  }
-  return KMX_OK;
+  if (int rc = grow_pool(h, pool->n_frames)) return rc;
+  if (int rc = upload_frames(h, pool->n_frames, pool->n_feats, pool->desc, pool->bearings, pool->points)) return rc;
+  return ensure_tables(h);
   KMX_GUARD_END
 }
 
+extern "C" int kmx_lcd_add_frames(kmx_lcd* h, int32_t n, int32_t max_feats, const int32_t* n_feats,
+                                  const uint8_t* desc, const double* bearings, const double* points,
+                                  int32_t* first_id) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_CHECK(n >= 0 && (n == 0 || (n_feats && desc && bearings && points)), KMX_EINVAL, "null frame array");
+  KMX_CHECK(max_feats >= 5 && max_feats <= MAX_FEATS, KMX_EINVAL, "need 5 <= max_feats <= 1024");
+  KMX_CHECK(h->F == 0 || max_feats == h->N, KMX_EINVAL, "max_feats differs from the resident pool's");
+  for (int f = 0; f < n; ++f)
+    KMX_CHECK(n_feats[f] >= 0 && n_feats[f] <= max_feats, KMX_EINVAL, "bad n_feats");
+  KMX_CHECK((int64_t)h->F + n <= INT32_MAX, KMX_EINVAL, "frame ids exceed int32");
+  KMX_HIP(hipSetDevice(h->device));
+  if (h->F == 0 && max_feats != h->N) {
+    KMX_HIP(hipStreamSynchronize(h->stream));
+    lcd_free_cand(h);
+    lcd_free_frames(h);
+    h->N = max_feats;
+  }
+  if (first_id) *first_id = h->F;
+  if (n == 0) return ensure_tables(h);
+  if (int rc = grow_pool(h, h->F + n)) return rc;
+  if (int rc = upload_frames(h, n, n_feats, desc, bearings, points)) return rc;
+  return ensure_tables(h);
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_lcd_pool_info(kmx_lcd* h, int32_t* n_frames, int32_t* capacity, int32_t* max_feats) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  if (n_frames) *n_frames = h->F;
+  if (capacity) *capacity = h->capF;
+  if (max_feats) *max_feats = h->N;
+  return KMX_OK;
+}
+
 static int check_cands(kmx_lcd* h, int32_t n, const int32_t* cq, const int32_t* cm) {
-  KMX_CHECK(h && h->d_desc, KMX_ESTATE, "set_frames first");
+  KMX_CHECK(h && h->d_desc && h->F > 0, KMX_ESTATE, "no frames: set_frames or add_frames first");
   KMX_CHECK(n >= 0 && (n == 0 || (cq && cm)), KMX_EINVAL, "bad candidate arrays");
   for (int i = 0; i < n; ++i)
     KMX_CHECK(cq[i] >= 0 && cq[i] < h->F && cm[i] >= 0 && cm[i] < h->F, KMX_EINVAL, "candidate frame id out of range");
@@ -2628,6 +2913,90 @@ extern "C" int kmx_lcd_verify_async(kmx_lcd* h, int32_t n, const int32_t* cq, co
   KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));  // host arrays may go away after return
   return enqueue_verify(h, n, false);
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_lcd_match(kmx_lcd* h, int32_t n, const int32_t* cq, const int32_t* cm, int32_t* pairs_out,
+                             int32_t* k_out) {
+  KMX_GUARD_BEGIN
+  if (int rc = check_cands(h, n, cq, cm)) return rc;
+  KMX_CHECK(n == 0 || (pairs_out && k_out), KMX_EINVAL, "null output");
+  if (n == 0) return KMX_OK;
+  KMX_HIP(hipSetDevice(h->device));
+  if (int rc = ensure_cap(h, n)) return rc;
+  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1), h->stream,
+                     (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, (const int*)h->d_cq,
+                     (const int*)h->d_cm, h->P.norm, h->P.lowe_ratio, h->d_pairs, h->d_K);
+  KMX_HIP(hipGetLastError());
+  KMX_HIP(hipMemcpyAsync(pairs_out, h->d_pairs, sizeof(int2) * (size_t)n * h->N, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipMemcpyAsync(k_out, h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
+extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, const int32_t* cm,
+                                      const int64_t* mptr, const int32_t* iq, const int32_t* im, int stages,
+                                      const double* T_prior, kmx_lcd_result* results, uint8_t* inlier_masks) {
+  KMX_GUARD_BEGIN
+  if (int rc = check_cands(h, n, cq, cm)) return rc;
+  KMX_CHECK(results || n == 0, KMX_EINVAL, "null results");
+  KMX_CHECK(stages >= 1 && stages <= 3, KMX_EINVAL, "stages: a non-empty mask of KMX_LCD_STAGE_*");
+  KMX_CHECK(n == 0 || mptr, KMX_EINVAL, "null mptr");
+  const bool need_prior = !(stages & KMX_LCD_STAGE_2D2D) && (stages & KMX_LCD_STAGE_RECOVER) &&
+                          h->P.pose_recovery_type == 0 && h->P.use_1point_3d3d;
+  KMX_CHECK(!need_prior || T_prior, KMX_EINVAL,
+            "the 1-point 3D-3D recovery without the 2D-2D stage needs T_prior (the 2D-2D rotation)");
+  if (n == 0) return KMX_OK;
+  const int64_t base = mptr[0];
+  KMX_CHECK(base >= 0, KMX_EINVAL, "mptr[0] < 0");
+  for (int i = 0; i < n; ++i) {
+    const int64_t K = mptr[i + 1] - mptr[i];
+    KMX_CHECK(K >= 0 && K <= h->N, KMX_EINVAL, "a candidate has more pairs than max_feats (or mptr decreases)");
+    const int nq = h->h_nfeat[cq[i]], nm = h->h_nfeat[cm[i]];
+    for (int64_t k = mptr[i]; k < mptr[i + 1]; ++k)
+      KMX_CHECK(iq[k] >= 0 && iq[k] < nq && im[k] >= 0 && im[k] < nm, KMX_EINVAL,
+                "correspondence index outside its frame's features");
+  }
+  const size_t total = (size_t)(mptr[n] - base);
+  KMX_HIP(hipSetDevice(h->device));
+  if (int rc = ensure_cap(h, n)) return rc;
+  if (total > h->pair_cap || !h->d_mptr) {
+    if (h->d_iq) (void)hipFree(h->d_iq);
+    if (h->d_im) (void)hipFree(h->d_im);
+    h->d_iq = h->d_im = nullptr;
+    h->pair_cap = 0;
+    const size_t pc = std::max<size_t>(total, 4096);
+    KMX_HIP(hipMalloc(&h->d_iq, sizeof(int) * pc));
+    KMX_HIP(hipMalloc(&h->d_im, sizeof(int) * pc));
+    h->pair_cap = pc;
+  }
+  if (h->d_mptr) (void)hipFree(h->d_mptr);
+  h->d_mptr = nullptr;
+  KMX_HIP(hipMalloc(&h->d_mptr, sizeof(int64_t) * (n + 1)));
+  std::vector<int64_t> mp(mptr, mptr + n + 1);
+  for (auto& x : mp) x -= base;
+  KMX_HIP(hipMemcpyAsync(h->d_mptr, mp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, h->stream));
+  if (total) {
+    KMX_HIP(hipMemcpyAsync(h->d_iq, iq + base, sizeof(int) * total, hipMemcpyHostToDevice, h->stream));
+    KMX_HIP(hipMemcpyAsync(h->d_im, im + base, sizeof(int) * total, hipMemcpyHostToDevice, h->stream));
+  }
+  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  if (T_prior)
+    KMX_HIP(hipMemcpyAsync(h->d_prior, T_prior, sizeof(double) * 12 * (size_t)n, hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(k_scatter_pairs, dim3(n), dim3(256), 0, h->stream, (const int64_t*)h->d_mptr,
+                     (const int*)h->d_iq, (const int*)h->d_im, h->N, h->d_pairs, h->d_K);
+  KMX_HIP(hipGetLastError());
+  if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr)) return rc;
+  KMX_HIP(hipGetLastError());
+  KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, h->stream));
+  if (inlier_masks)
+    KMX_HIP(hipMemcpyAsync(inlier_masks, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  return KMX_OK;
   KMX_GUARD_END
 }
 

@@ -33,9 +33,11 @@
 //     closures in the same launch.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -2934,6 +2936,18 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   for (int64_t k = 0; k < h->n_owned; ++k) own_src[k] = pub_src[h->first_owned + k];
   std::vector<int> nrob(L);
   for (int l = 0; l < L; ++l) nrob[l] = n_poses[h->robots[l]];
+  // tile descriptors: validated before any device allocation, so a rejected
+  // graph leaves the handle without buffers (ready() false)
+  std::vector<TileDesc> tdesc(h->ntiles);
+  for (int t = 0; t < h->ntiles; ++t) {
+    TileDesc& td = tdesc[t];
+    td.robot = tr[t];
+    td.p0 = tp0[t];
+    td.k0 = inc_ptr[tp0[t]];
+    const int ninc = inc_ptr[tp0[t] + tnp[t]] - td.k0;
+    KMX_CHECK(tnp[t] < 256 && ninc < (1 << 23), KMX_EINVAL, "tile too large");
+    td.np_n = tnp[t] | (ninc << 8);
+  }
   // device
   int rc;
   const size_t vec = (size_t)std::max(nloc, 1) * ps;
@@ -2966,16 +2980,6 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   auto up = [&](void* dst, const void* src, size_t bytes) {
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream);
   };
-  std::vector<TileDesc> tdesc(h->ntiles);
-  for (int t = 0; t < h->ntiles; ++t) {
-    TileDesc& td = tdesc[t];
-    td.robot = tr[t];
-    td.p0 = tp0[t];
-    td.k0 = inc_ptr[tp0[t]];
-    const int ninc = inc_ptr[tp0[t] + tnp[t]] - td.k0;
-    KMX_CHECK(tnp[t] < 256 && ninc < (1 << 23), KMX_EINVAL, "tile too large");
-    td.np_n = tnp[t] | (ninc << 8);
-  }
   KMX_HIP(up(h->d_tile, tdesc.data(), sizeof(TileDesc) * tdesc.size()));
   KMX_HIP(up(h->d_rtile0, rt0.data(), sizeof(int) * rt0.size()));
   KMX_HIP(up(h->d_inc_ptr, inc_ptr.data(), sizeof(int) * inc_ptr.size()));
@@ -3181,6 +3185,7 @@ int nccl_settle(kmx_pgo* h, ncclResult_t r, const char* what) {
   while (r == ncclInProgress) {
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
       return kmx::fail(KMX_EHIP, std::string(what) + ": still in progress after 60 s");
+    std::this_thread::yield();
     if (ncclCommGetAsyncError(h->comm, &r) != ncclSuccess) r = ncclSystemError;
   }
   if (r != ncclSuccess) return kmx::fail(KMX_EHIP, std::string(what) + ": " + ncclGetErrorString(r));
@@ -3222,6 +3227,29 @@ int enqueue_exchange(kmx_pgo* h) {
   return KMX_OK;
 }
 
+// Which RCCL / HIP runtime libkmx's own calls resolve to in this process
+// (torch bundles a librccl.so.1 of the same SONAME: whichever was loaded first
+// serves both), their versions and the RCCL headers kmx was built against.
+extern "C" int kmx_runtime_info(char* out, int64_t nbytes) {
+  KMX_GUARD_BEGIN
+  KMX_CHECK(out && nbytes > 0, KMX_EINVAL, "null buffer");
+  Dl_info di{}, dh{};
+  const char* rp = dladdr(reinterpret_cast<void*>(&ncclSend), &di) && di.dli_fname ? di.dli_fname : "?";
+  const char* hp = dladdr(reinterpret_cast<void*>(static_cast<hipError_t (*)(void**, size_t)>(&hipMalloc)), &dh) && dh.dli_fname ? dh.dli_fname : "?";
+  int rv = 0, hv = 0, dv = 0;
+  (void)ncclGetVersion(&rv);
+  (void)hipRuntimeGetVersion(&hv);
+  (void)hipDriverGetVersion(&dv);
+  const std::string js = std::string("{\"rccl_path\": \"") + rp + "\", \"rccl_version\": " + std::to_string(rv) +
+                         ", \"rccl_header_version\": " + std::to_string(NCCL_VERSION_CODE) + ", \"hip_path\": \"" + hp +
+                         "\", \"hip_runtime_version\": " + std::to_string(hv) + ", \"hip_driver_version\": " +
+                         std::to_string(dv) + "}";
+  KMX_CHECK((int64_t)js.size() < nbytes, KMX_EINVAL, "buffer too small");
+  std::memcpy(out, js.c_str(), js.size() + 1);
+  return KMX_OK;
+  KMX_GUARD_END
+}
+
 extern "C" int kmx_comm_unique_id(void* out, int64_t nbytes) {
   KMX_GUARD_BEGIN
   KMX_CHECK(out && nbytes >= (int64_t)sizeof(ncclUniqueId), KMX_EINVAL, "need a buffer of KMX_COMM_ID_BYTES");
@@ -3254,6 +3282,7 @@ extern "C" int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, i
       if (c) (void)ncclCommAbort(c);
       return kmx::fail(KMX_EHIP, "ncclCommInitRankConfig: no rendezvous within the timeout (a peer failed?)");
     }
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
     if (ncclCommGetAsyncError(c, &r) != ncclSuccess) r = ncclSystemError;
   }
   if (r != ncclSuccess) {
@@ -3268,13 +3297,17 @@ extern "C" int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, i
   KMX_GUARD_END
 }
 
+// Abort first: a round whose exchange waits on a peer that never posts its
+// half (the peer failed) only leaves the stream once the communicator is
+// aborted; then the stream drains and the exchange buffers can go.
 extern "C" int kmx_pgo_comm_destroy(kmx_pgo* h) {
+  KMX_GUARD_BEGIN
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
-  KMX_HIP(hipStreamSynchronize(h->stream));
-  free_xchg(h);
   if (h->comm) (void)ncclCommAbort(h->comm);
   h->comm = nullptr;
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  free_xchg(h);
   h->world = 1;
   h->rank = 0;
   if (h->n_ext) {  // the peers' statuses came with the exchange
@@ -3282,6 +3315,24 @@ extern "C" int kmx_pgo_comm_destroy(kmx_pgo* h) {
     sync_params(h);
   }
   return KMX_OK;
+  KMX_GUARD_END
+}
+
+// The handle's stream drained within timeout_s (polled), or KMX_ETIMEOUT: a
+// bounded wait for a round whose exchange depends on peers.
+extern "C" int kmx_pgo_sync_timeout(kmx_pgo* h, double timeout_s) {
+  KMX_CHECK(h, KMX_EINVAL, "null handle");
+  KMX_CHECK(timeout_s > 0.0, KMX_EINVAL, "timeout_s must be > 0");
+  KMX_HIP(hipSetDevice(h->device));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(h->stream);
+    if (e == hipSuccess) return KMX_OK;
+    if (e != hipErrorNotReady) return kmx::fail(KMX_EHIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+      return kmx::fail(KMX_ETIMEOUT, "the stream did not drain within the timeout (an exchange peer is missing?)");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
 }
 
 extern "C" int kmx_pgo_get_public(kmx_pgo* h, double* table, double* ext) {

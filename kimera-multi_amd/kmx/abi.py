@@ -17,7 +17,8 @@ import numpy as np
 _LIB_PATH = Path(__file__).resolve().parent / "libkmx.so"
 
 KMX_OK = 0
-ABI_VERSION = 5  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
+KMX_ETIMEOUT = -6
+ABI_VERSION = 6  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
 KMX_COST_L2 = 0
 KMX_COMM_ID_BYTES = 128  # include/kmx_abi.h (ncclUniqueId)
 KMX_COST_GNC_TLS = 1
@@ -33,6 +34,8 @@ KMX_NORM_L1 = 0
 KMX_NORM_HAMMING = 1
 KMX_RNG_GCC9 = 0
 KMX_RNG_GCC11 = 1
+KMX_LCD_STAGE_2D2D = 1
+KMX_LCD_STAGE_RECOVER = 2
 
 TCG_STOP_NAMES = {0: "none", 1: "negative_curvature", 2: "exceeded_trust_region",
                   3: "linear", 4: "superlinear", 5: "max_iterations", 6: "skipped"}
@@ -99,7 +102,7 @@ class LcdParams(C.Structure):
         ("ransac_seed", C.c_uint32), ("rng_variant", C.c_int),
         ("use_1point_3d3d", C.c_int), ("pose_recovery_type", C.c_int), ("min_2d3d_inliers", C.c_int),
         ("ransac_threshold_2d3d", C.c_double), ("algorithm_2d2d", C.c_int), ("refine_pose", C.c_int),
-        ("reserved", C.c_int * 2),
+        ("rng_stream", C.c_int), ("reserved", C.c_int * 1),
     ]
 
 
@@ -137,6 +140,7 @@ def lib() -> C.CDLL:
         "kmx_pgo_set_stream": ([P, P], C.c_int),
         "kmx_pgo_set_tcg_poll": ([P, C.c_int], C.c_int),
         "kmx_comm_unique_id": ([P, i64], C.c_int),
+        "kmx_runtime_info": ([C.c_char_p, i64], C.c_int),
         "kmx_pgo_comm_init": ([P, P, C.c_int, C.c_int, f64], C.c_int),
         "kmx_pgo_comm_destroy": ([P], C.c_int),
         "kmx_pgo_get_public": ([P, pf64, pf64], C.c_int),
@@ -158,6 +162,7 @@ def lib() -> C.CDLL:
         "kmx_pgo_iterate": ([P, pu8, C.POINTER(IterStats)], C.c_int),
         "kmx_pgo_iterate_async": ([P, C.c_int, C.c_int], C.c_int),
         "kmx_pgo_sync": ([P], C.c_int),
+        "kmx_pgo_sync_timeout": ([P, f64], C.c_int),
         "kmx_pgo_update_weights": ([P, pf64], C.c_int),
         "kmx_pgo_get_mu": ([P, pf64], C.c_int),
         "kmx_pgo_set_mu": ([P, f64], C.c_int),
@@ -185,8 +190,13 @@ def lib() -> C.CDLL:
         "kmx_lcd_destroy": ([P], C.c_int),
         "kmx_lcd_set_stream": ([P, P], C.c_int),
         "kmx_lcd_set_frames": ([P, P], C.c_int),
+        "kmx_lcd_add_frames": ([P, i32, i32, pi32, pu8, pf64, pf64, pi32], C.c_int),
+        "kmx_lcd_pool_info": ([P, pi32, pi32, pi32], C.c_int),
+        "kmx_lcd_match": ([P, i32, pi32, pi32, pi32, pi32], C.c_int),
         "kmx_lcd_verify": ([P, i32, pi32, pi32, C.POINTER(LcdResult), pu8], C.c_int),
         "kmx_lcd_verify_async": ([P, i32, pi32, pi32], C.c_int),
+        "kmx_lcd_verify_matches": ([P, i32, pi32, pi32, pi64, pi32, pi32, C.c_int, pf64,
+                                    C.POINTER(LcdResult), pu8], C.c_int),
         "kmx_lcd_sync": ([P], C.c_int),
         "kmx_lcd_enable_timing": ([P, C.c_int], C.c_int),
         "kmx_lcd_read_timing": ([P, pf64, pf64], C.c_int),
@@ -199,25 +209,10 @@ def lib() -> C.CDLL:
         "kmx_bow_sync": ([P], C.c_int),
         "kmx_bow_score_pairs": ([P, i32, pi64, pu32, pf64, pi64, pu32, pf64, pf64], C.c_int),
     })
-    optional = {
-        "kmx_lcd_knn2": ([C.c_int, C.c_double, pu8, i32, pu8, i32, pi32, pi32], C.c_int),
-        "kmx_lcd_create": ([C.POINTER(LcdParams), C.c_int, C.POINTER(P)], C.c_int),
-        "kmx_lcd_destroy": ([P], C.c_int),
-        "kmx_lcd_set_stream": ([P, P], C.c_int),
-        "kmx_lcd_set_frames": ([P, P], C.c_int),
-        "kmx_lcd_verify": ([P, i32, pi32, pi32, C.POINTER(LcdResult), pu8], C.c_int),
-        "kmx_lcd_verify_async": ([P, i32, pi32, pi32], C.c_int),
-        "kmx_lcd_sync": ([P], C.c_int),
-    }
     for name, (argt, rest) in sig.items():
         fn = getattr(L, name)
         fn.argtypes = argt
         fn.restype = rest
-    for name, (argt, rest) in optional.items():
-        if hasattr(L, name):
-            fn = getattr(L, name)
-            fn.argtypes = argt
-            fn.restype = rest
     if L.kmx_abi_version() != ABI_VERSION:
         raise KmxError(f"{path} implements ABI {L.kmx_abi_version()}, this binding needs {ABI_VERSION}: rebuild it")
     _lib = L
@@ -259,3 +254,32 @@ def u32ptr(a: np.ndarray):
 def u8ptr(a: np.ndarray):
     assert a.dtype == np.uint8 and a.flags.c_contiguous
     return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def runtime_info() -> dict:
+    """Where libkmx's RCCL / HIP calls resolve in this process, with versions
+    (kmx_runtime_info), plus every librccl / libamdhip64 mapped into the
+    process (/proc/self/maps): torch ships a librccl.so.1 of the same SONAME,
+    so which copy serves kmx depends on load order."""
+    import json
+    buf = C.create_string_buffer(4096)
+    check(lib().kmx_runtime_info(buf, 4096), "kmx_runtime_info")
+    info = json.loads(buf.value.decode())
+    mapped = {"librccl": set(), "libamdhip64": set()}
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 6:
+                    path = parts[-1]
+                    for k in mapped:
+                        if f"/{k}" in path:
+                            mapped[k].add(os.path.realpath(path))
+    except OSError:
+        pass
+    info["mapped_rccl"] = sorted(mapped["librccl"])
+    info["mapped_hip"] = sorted(mapped["libamdhip64"])
+    info["rccl_path_real"] = os.path.realpath(info["rccl_path"]) if info["rccl_path"] != "?" else "?"
+    info["single_rccl"] = len(info["mapped_rccl"]) <= 1 and (
+        not info["mapped_rccl"] or info["rccl_path_real"] in info["mapped_rccl"])
+    return info

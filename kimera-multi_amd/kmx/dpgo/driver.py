@@ -245,6 +245,19 @@ class RBCDDriver:
             return False
         self.solver.set_exchange(*self._plan)
         self.exchange_mode = "RCCL ncclSend/ncclRecv group inside each round (solver stream)"
+        info = getattr(self.solver, "runtime_info", None)
+        if info is not None:
+            # torch bundles a librccl of the same SONAME as the one kmx links: one
+            # copy must serve both, or kmx's communicator runs on a different RCCL
+            # (and HIP runtime) than torch's process group
+            ri = info()
+            self.runtime = ri
+            self.exchange_mode += f" [kmx RCCL {ri.get('rccl_version')} at {ri.get('rccl_path_real')}]"
+            if not ri.get("single_rccl", True):
+                self.exchange_mode += f" (WARNING: {len(ri.get('mapped_rccl', []))} RCCL copies mapped)"
+                if os.environ.get("KMX_REQUIRE_NATIVE", "0") == "1":
+                    raise RuntimeError("KMX_REQUIRE_NATIVE=1: libkmx's RCCL symbols resolve to "
+                                       f"{ri.get('rccl_path_real')} but the process maps {ri.get('mapped_rccl')}")
         return True
 
     def _torch_exchange(self):
@@ -264,21 +277,40 @@ class RBCDDriver:
             return
         self._native_verified = True
         s = self.solver
+        alive = True
+        # Bounded: a rank whose exchange raises after its peers have posted
+        # their ncclSend / ncclRecv leaves those peers waiting on the stream;
+        # they wait at most KMX_XCHG_TIMEOUT s (kmx_pgo_sync_timeout), then
+        # abort their communicator (kmx_pgo_comm_destroy), which releases the
+        # stream, and every rank reaches the agreement below.
+        deadline = float(os.environ.get("KMX_XCHG_TIMEOUT", "60"))
         try:  # an error here must still reach the agreement below on every rank
             s.exchange()
+            if hasattr(s, "sync_timeout") and not s.sync_timeout(deadline):
+                raise TimeoutError(f"the first native exchange did not complete within {deadline:g} s")
             tab_n, ext_n = s.get_public(self.world)
         except Exception as e:  # noqa: BLE001 - reported through exchange_mode
             tab_n = ext_n = None
-            self._native_error = f"first native exchange: {e}"
+            self._native_error = f"first native exchange on rank {self.rank}: {type(e).__name__}: {e}"
+            s.comm_destroy()  # abort: the stream drains even if a peer's half never comes
+            alive = False
         self._torch_exchange()
         tab_t, ext_t = s.get_public(self.world)
         same = tab_n is not None and np.array_equal(tab_n, tab_t) and np.array_equal(ext_n, ext_t)
         if self._agree(same):
             self.exchange_mode += ", checked bitwise against all_to_all at the first round"
             return
-        s.comm_destroy()
+        errs = [None] * self.world
+        self._dist.all_gather_object(errs, getattr(self, "_native_error", None))
+        if alive:
+            s.comm_destroy()
         self.native = False
-        self.exchange_mode = "torch.distributed all_to_all_single (fallback: the RCCL exchange differed from it)"
+        failed = [e for e in errs if e]
+        if failed:  # an exception (a timeout included) is not a bitwise mismatch: say which
+            self.exchange_mode = ("torch.distributed all_to_all_single (fallback: the RCCL exchange failed: "
+                                  + "; ".join(failed) + ")")
+        else:
+            self.exchange_mode = "torch.distributed all_to_all_single (fallback: the RCCL exchange differed from it)"
         if os.environ.get("KMX_REQUIRE_NATIVE", "0") == "1":
             raise RuntimeError(self.exchange_mode)
 

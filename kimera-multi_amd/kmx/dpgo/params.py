@@ -68,6 +68,12 @@ class PGOAgentParameters:
     relChangeTol: float = 1e-3
     robustOptInnerIters: int = 20          # rounds between GNC weight updates
     robustOptNumWeightUpdates: int = 50    # after this many updates weights freeze
+    # shouldTerminate's "GNC done" gate (RBCDDriver.should_terminate) [U: a
+    # restated substitute for dpgo's rule, which is not vendored; drawio:2030
+    # shows only iteration_number() > maxNumIters]: a robust run stops on
+    # relChangeTol only once this fraction of the loop-closure weights sits
+    # within 1e-8 of 0 or 1 (team-wide) or robustOptNumWeightUpdates ran.
+    # 0 restores the plain relChangeTol / maxNumIters stop.
     robustOptMinConvergenceRatio: float = 0.8
     schedule: int = 1                      # 0 sequential (dpgo_ros sync), 1 concurrent
     updateRule: int = 0                    # sequential: 0 round-robin, 1 uniform (dpgo_ros update rule)

@@ -77,6 +77,11 @@ class BlockSolver:
         check(self.L.kmx_pgo_comm_init(self.h, C.cast(buf, C.c_void_p), int(world), int(rank), float(timeout_s)),
               "kmx_pgo_comm_init")
 
+    @staticmethod
+    def runtime_info() -> dict:
+        """abi.runtime_info(): the RCCL / HIP libraries serving libkmx."""
+        return abi.runtime_info()
+
     def comm_destroy(self):
         """Drop the communicator and the in-round exchange."""
         check(self.L.kmx_pgo_comm_destroy(self.h), "kmx_pgo_comm_destroy")
@@ -192,6 +197,15 @@ class BlockSolver:
 
     def sync(self):
         check(self.L.kmx_pgo_sync(self.h), "kmx_pgo_sync")
+
+    def sync_timeout(self, timeout_s: float) -> bool:
+        """kmx_pgo_sync with a deadline: False when the stream has not drained
+        after timeout_s (kmx_pgo_comm_destroy then aborts the exchange)."""
+        rc = self.L.kmx_pgo_sync_timeout(self.h, float(timeout_s))
+        if rc == abi.KMX_ETIMEOUT:
+            return False
+        check(rc, "kmx_pgo_sync_timeout")
+        return True
 
     # ------------------------------------------------------------- GNC ---
     def set_gnc_schedule(self, enabled: bool, inner_iters: int = 20, max_updates: int = 2**31 - 1,

@@ -1,2 +1,2 @@
-from .detector import LcdParams, LoopClosureDetector  # noqa: F401
+from .detector import LcdParams, LoopClosureDetector, VLCFrame  # noqa: F401
 from .bow import BowDatabase, BowDetector  # noqa: F401

@@ -55,9 +55,23 @@ class LcdParams:
     max_intraisland_gap: int = 3
     max_nrFrames_between_islands: int = 3
     max_nrFrames_between_queries: int = 2
-    # stereo pose refinement after an accepted 3D-3D recovery (LcdParams.yaml:14):
-    # least-squares T over the 3D-3D inliers (include/kmx_abi.h refine_pose) [U]
+    # stereo pose refinement after an accepted 3D-3D recovery (LcdParams.yaml:14,
+    # the reference config): least-squares T over the 3D-3D inliers
+    # (include/kmx_abi.h refine_pose), a restated substitute for Kimera-VIO's
+    # GTSAM stereo refinement [U, parity unpinned]. Results it touched carry
+    # "pose_refined": True. Measured on 20 planted candidates it is not more
+    # accurate than the unrefined pose (translation error 0.0158 vs 0.0149 m,
+    # rotation 1.17e-3 vs 1.11e-3; tests/test_golden_cpu.py
+    # test_refine_pose_delta_on_planted_pool); 0 keeps the recovered pose.
     refine_pose: int = 1
+    # ORB keypoints per frame (LcdParams.yaml:19): the feature-slot stride of
+    # the frame pool that addVLCFrame fills
+    nfeatures: int = 700
+    # LC5 sampler reading (include/kmx_abi.h rng_stream): 0 every RANSAC
+    # problem seeds its own engine (opengv's constructor, the default); 1 the
+    # fork's thread_local engine continued from problem to problem (ordered,
+    # candidate-serial path)
+    rng_stream: int = 0
 
     @classmethod
     def from_yaml(cls, path: str, **overrides) -> "LcdParams":
@@ -113,6 +127,10 @@ class LcdParams:
             raise ValueError("ransac_use_1point_3d3d is 0 (Arun 3-point) or 1 (given rotation)")
         if self.rng_variant not in ("gcc9", "gcc11"):
             raise ValueError(f"rng_variant {self.rng_variant!r}")
+        if self.rng_stream not in (0, 1):
+            raise ValueError(f"rng_stream {self.rng_stream}")
+        if not 5 <= int(self.nfeatures) <= 1024:
+            raise ValueError(f"nfeatures {self.nfeatures}: the frame pool holds 5..1024 features per frame")
         if self.refine_pose not in (0, 1):
             raise ValueError(f"refine_pose {self.refine_pose}")
         if self.refine_pose and self.pose_recovery_type == 1:
@@ -136,6 +154,7 @@ class LcdParams:
         c.use_1point_3d3d = int(self.ransac_use_1point_3d3d)
         c.algorithm_2d2d = int(self.ransac_2d2d_algorithm)
         c.refine_pose = int(self.refine_pose)
+        c.rng_stream = int(self.rng_stream)
         c.pose_recovery_type = int(self.pose_recovery_type)
         c.min_2d3d_inliers = int(self.min_nr_2d3d_inliers)
         c.ransac_threshold_2d3d = 1.0 - np.cos(np.arctan(float(self.ransac_threshold_2d3d) / float(self.focal_length)))
@@ -153,7 +172,7 @@ _YAML_FIELDS = (
     "ransac_2d2d_algorithm", "ransac_2d3d_algorithm",
     "use_nss", "alpha", "min_temporal_matches", "recent_frames_window", "max_db_results",
     "min_nss_factor", "min_matches_per_island", "max_intraisland_gap",
-    "max_nrFrames_between_islands", "max_nrFrames_between_queries")
+    "max_nrFrames_between_islands", "max_nrFrames_between_queries", "nfeatures")
 _MATCHER_NORM = {3: "l1", 4: "hamming", 5: "hamming"}
 # switches of verification stages: yaml key -> (built values, field or None)
 _YAML_SELECTORS = {
@@ -166,10 +185,26 @@ _YAML_SELECTORS = {
 # keys of stages outside the verification hot path (SURVEY.md §8 out of scope):
 # ORB extraction (:19-27), the PGO back end (:29-37), the stereo tracker (:48)
 _YAML_IGNORED = frozenset((
-    "nfeatures", "scale_factor", "nlevels", "edge_threshold", "first_level", "WTA_K", "score_type_id",
+    "scale_factor", "nlevels", "edge_threshold", "first_level", "WTA_K", "score_type_id",
     "patch_sze", "fast_threshold", "betweenRotationPrecision", "betweenTranslationPrecision",
     "odom_rot_threshold", "odom_trans_threshold", "pcm_rot_threshold", "pcm_trans_threshold", "gnc_alpha",
     "max_lc_cached_before_optimize", "disparity_threshold"))
+
+
+@dataclass
+class VLCFrame:
+    """The visual-loop-closure frame Kimera-Distributed exchanges and hands to
+    LoopClosureDetector::addVLCFrame (drawio:2601; pose_graph_tools VLCFrame,
+    drawio:441-505), reduced to what verification reads [U field names:
+    Kimera-Multi-LCD is not vendored]: its (robot_id, pose_id) vertex, the ORB
+    descriptors [n, 32] uint8, the unit bearing vectors ("versors") [n, 3]
+    and the stereo keypoints [n, 3] (NaN where a keypoint has no stereo
+    depth)."""
+    robot_id: int
+    pose_id: int
+    descriptors: np.ndarray
+    versors: np.ndarray
+    keypoints: np.ndarray
 
 
 class _BatchDesc(C.Structure):
@@ -194,6 +229,8 @@ class LoopClosureDetector:
         check(L.kmx_lcd_create(C.byref(self._c), device, C.byref(h)), "kmx_lcd_create")
         self.h, self.L = h, L
         self.max_feats = 0
+        self.n_frames = 0
+        self._vertex = {}  # (robot_id, pose_id) -> frame id in the pool
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
@@ -226,9 +263,148 @@ class LoopClosureDetector:
         d.points = pt.ctypes.data_as(C.POINTER(C.c_double))
         check(self.L.kmx_lcd_set_frames(self.h, C.byref(d)), "kmx_lcd_set_frames")
         self.max_feats = N
+        self.n_frames = F
+        self._vertex = {}
 
     def set_pool(self, pool):
         self.set_frames(pool.n_feats, pool.desc, pool.bearings, pool.points)
+
+    # ------------------------------------------------ streaming frame pool --
+    def add_frames(self, n_feats, desc, bearings, points) -> int:
+        """Append frames to the resident pool (kmx_lcd_add_frames: capacity
+        doubling on the device, resident frames never re-uploaded, the sampler
+        table kept). Arrays as set_frames; the stride N must equal the pool's
+        (on an empty detector it sets it). Returns the first new frame id."""
+        nf = np.ascontiguousarray(n_feats, dtype=np.int32)
+        de = np.ascontiguousarray(desc, dtype=np.uint8)
+        be = np.ascontiguousarray(bearings, dtype=np.float64)
+        pt = np.ascontiguousarray(points, dtype=np.float64)
+        F, N = de.shape[0], de.shape[1]
+        if de.shape != (F, N, 32) or be.shape != (F, N, 3) or pt.shape != (F, N, 3) or nf.shape != (F,):
+            raise ValueError("frame shapes must be desc [F,N,32], bearings/points [F,N,3], n_feats [F]")
+        first = C.c_int32()
+        check(self.L.kmx_lcd_add_frames(self.h, F, N, abi.iptr(nf), abi.u8ptr(de), abi.fptr(be), abi.fptr(pt),
+                                        C.byref(first)), "kmx_lcd_add_frames")
+        self.max_feats = N
+        self.n_frames = first.value + F
+        return first.value
+
+    def pool_info(self) -> dict:
+        f, cap, n = C.c_int32(), C.c_int32(), C.c_int32()
+        check(self.L.kmx_lcd_pool_info(self.h, C.byref(f), C.byref(cap), C.byref(n)), "kmx_lcd_pool_info")
+        return {"n_frames": f.value, "capacity": cap.value, "max_feats": n.value}
+
+    def addVLCFrame(self, frame: VLCFrame) -> int:
+        """LoopClosureDetector::addVLCFrame (drawio:2601): the frame joins the
+        device pool (padded to the pool's feature stride, `nfeatures` of
+        LcdParams on an empty detector) and its (robot_id, pose_id) vertex
+        maps to the returned frame id."""
+        N = self.max_feats or int(self.params.nfeatures)
+        d = np.asarray(frame.descriptors, np.uint8)
+        n = d.shape[0]
+        if n > N:
+            raise ValueError(f"frame has {n} features, the pool's stride is {N}")
+        de = np.zeros((1, N, 32), np.uint8)
+        be = np.zeros((1, N, 3))
+        pt = np.full((1, N, 3), np.nan)
+        de[0, :n] = d
+        be[0, :n] = np.asarray(frame.versors, np.float64)
+        pt[0, :n] = np.asarray(frame.keypoints, np.float64)
+        fid = self.add_frames(np.array([n], np.int32), de, be, pt)
+        self._vertex[(int(frame.robot_id), int(frame.pose_id))] = fid
+        return fid
+
+    def frame_id(self, vertex) -> int:
+        """Pool id of a vertex: an int frame id, or a (robot_id, pose_id) added
+        by addVLCFrame."""
+        if isinstance(vertex, (tuple, list)):
+            return self._vertex[(int(vertex[0]), int(vertex[1]))]
+        return int(vertex)
+
+    # ------------------------------------------- reference-shaped single calls --
+    def computeMatchedIndices(self, vertex_query, vertex_match):
+        """LoopClosureDetector::computeMatchedIndices (drawio:2583-2586) on two
+        resident frames: (i_query, i_match) int32 arrays in query order."""
+        pairs, k = self.match([self.frame_id(vertex_query)], [self.frame_id(vertex_match)])
+        return pairs[0, : k[0], 0].copy(), pairs[0, : k[0], 1].copy()
+
+    def geometricVerificationNister(self, vertex_query, vertex_match, i_query, i_match):
+        """geometricVerificationNister (drawio:2589-2592): the 2D-2D RANSAC on
+        the given correspondences. Returns (ok, i_query_inliers,
+        i_match_inliers, T_query_match 4x4 with unit-norm t); ok = at least
+        min_nr_2d2d_inliers inliers. The inlier lists are what the reference
+        writes back into i_query / i_match."""
+        iq = np.ascontiguousarray(i_query, np.int32)
+        im = np.ascontiguousarray(i_match, np.int32)
+        out, masks = self.verify_matches([self.frame_id(vertex_query)], [self.frame_id(vertex_match)], [(iq, im)],
+                                         stages=abi.KMX_LCD_STAGE_2D2D, with_masks=True)
+        keep = (masks[0, : iq.shape[0]] & 1).astype(bool)
+        return out[0]["accepted"], iq[keep], im[keep], _T4(out[0]["T_query_match"])
+
+    def recoverPose(self, vertex_query, vertex_match, i_query, i_match, T_query_match_mono=None):
+        """recoverPose (drawio:2595-2598) on geometricVerificationNister's
+        inliers: the 3D-3D recovery (1-point given the 2D-2D rotation of
+        T_query_match_mono, or Arun) or EPnP, per LcdParams. Returns (ok,
+        T_query_match 4x4, inlier mask over the given pairs)."""
+        iq = np.ascontiguousarray(i_query, np.int32)
+        im = np.ascontiguousarray(i_match, np.int32)
+        prior = None
+        if T_query_match_mono is not None:
+            T = np.asarray(T_query_match_mono, np.float64)
+            prior = np.concatenate([T[:3, :3].reshape(9), T[:3, 3]])[None]
+        out, masks = self.verify_matches([self.frame_id(vertex_query)], [self.frame_id(vertex_match)], [(iq, im)],
+                                         stages=abi.KMX_LCD_STAGE_RECOVER, T_prior=prior, with_masks=True)
+        return out[0]["accepted"], _T4(out[0]["T_query_match"]), (masks[0, : iq.shape[0]] & 2).astype(bool)
+
+    # --------------------------------------------------------------- batched --
+    def match(self, cand_query, cand_match):
+        """Batched computeMatchedIndices on resident frames (kmx_lcd_match):
+        pairs [n, max_feats, 2] int32 and k [n]."""
+        cq = np.ascontiguousarray(cand_query, dtype=np.int32)
+        cm = np.ascontiguousarray(cand_match, dtype=np.int32)
+        n = cq.shape[0]
+        pairs = np.zeros((max(n, 1), max(self.max_feats, 1), 2), np.int32)
+        k = np.zeros(max(n, 1), np.int32)
+        check(self.L.kmx_lcd_match(self.h, n, abi.iptr(cq), abi.iptr(cm), abi.iptr(pairs), abi.iptr(k)),
+              "kmx_lcd_match")
+        return pairs[:n], k[:n]
+
+    def verify_matches(self, cand_query, cand_match, correspondences, stages: int = 3, T_prior=None,
+                       with_masks: bool = False):
+        """geometricVerificationNister and / or recoverPose on caller-supplied
+        correspondences (kmx_lcd_verify_matches), batched: correspondences[i] =
+        (i_query, i_match) of candidate i; stages a mask of
+        abi.KMX_LCD_STAGE_2D2D / _RECOVER; T_prior [n, 12] (R row-major, t) is
+        the rotation source of the 1-point recovery without the 2D-2D stage.
+        Returns (results, masks) as verify, masks indexed by pair position."""
+        cq = np.ascontiguousarray(cand_query, dtype=np.int32)
+        cm = np.ascontiguousarray(cand_match, dtype=np.int32)
+        n = cq.shape[0]
+        if len(correspondences) != n:
+            raise ValueError("one (i_query, i_match) pair list per candidate")
+        lens = [len(np.asarray(a)) for a, _ in correspondences]
+        for (a, b), k in zip(correspondences, lens):
+            if len(np.asarray(b)) != k:
+                raise ValueError("i_query and i_match differ in length")
+        mptr = np.zeros(n + 1, np.int64)
+        mptr[1:] = np.cumsum(lens)
+        iq = np.ascontiguousarray(np.concatenate([np.asarray(a, np.int32) for a, _ in correspondences])
+                                  if n else np.zeros(0, np.int32), np.int32)
+        im = np.ascontiguousarray(np.concatenate([np.asarray(b, np.int32) for _, b in correspondences])
+                                  if n else np.zeros(0, np.int32), np.int32)
+        if iq.size == 0:
+            iq = np.zeros(1, np.int32)
+            im = np.zeros(1, np.int32)
+        pr = None
+        if T_prior is not None:
+            pr = np.ascontiguousarray(T_prior, np.float64).reshape(n, 12)
+        res = (abi.LcdResult * max(n, 1))()
+        masks = np.zeros((max(n, 1), max(self.max_feats, 1)), np.uint8) if with_masks else None
+        check(self.L.kmx_lcd_verify_matches(self.h, n, abi.iptr(cq), abi.iptr(cm), abi.i64ptr(mptr), abi.iptr(iq),
+                                            abi.iptr(im), int(stages), abi.fptr(pr) if pr is not None else None,
+                                            res, abi.u8ptr(masks) if with_masks else None),
+              "kmx_lcd_verify_matches")
+        return _results(res, n, self._refines(stages)), (masks[:n] if with_masks else None)
 
     def verify(self, cand_query, cand_match, with_masks: bool = False):
         """Verify candidates; returns (list of result dicts, masks or None).
@@ -243,14 +419,11 @@ class LoopClosureDetector:
                                     cm.ctypes.data_as(C.POINTER(C.c_int32)), res,
                                     masks.ctypes.data_as(C.POINTER(C.c_uint8)) if with_masks else None),
               "kmx_lcd_verify")
-        out = []
-        for i in range(n):
-            r = res[i]
-            out.append({"n_matches": r.n_matches, "mono_inliers": r.mono_inliers,
-                        "stereo_inliers": r.stereo_inliers, "pnp_inliers": r.pnp_inliers,
-                        "accepted": bool(r.accepted),
-                        "iterations_2d2d": r.iterations_2d2d, "T_query_match": np.array(r.T_query_match[:])})
-        return out, masks
+        return _results(res, n, self._refines(3)), masks
+
+    def _refines(self, stages: int) -> bool:
+        p = self.params
+        return bool(p.refine_pose) and p.pose_recovery_type == 0 and bool(stages & abi.KMX_LCD_STAGE_RECOVER)
 
     def verify_async(self, cand_query, cand_match):
         cq = np.ascontiguousarray(cand_query, dtype=np.int32)
@@ -284,3 +457,24 @@ class LoopClosureDetector:
                                      pairs.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(k)),
               "kmx_lcd_knn2")
         return pairs[: k.value, 0].copy(), pairs[: k.value, 1].copy()
+
+
+def _results(res, n: int, refines: bool = False) -> list:
+    """Result records; pose_refined marks an accepted 3D-3D pose that went
+    through the restated refine_pose refit (a substitute, parity unpinned)."""
+    out = []
+    for i in range(n):
+        r = res[i]
+        out.append({"n_matches": r.n_matches, "mono_inliers": r.mono_inliers,
+                    "stereo_inliers": r.stereo_inliers, "pnp_inliers": r.pnp_inliers,
+                    "accepted": bool(r.accepted),
+                    "iterations_2d2d": r.iterations_2d2d, "T_query_match": np.array(r.T_query_match[:]),
+                    "pose_refined": bool(refines and r.accepted)})
+    return out
+
+
+def _T4(t12) -> np.ndarray:
+    T = np.eye(4)
+    T[:3, :3] = np.asarray(t12[:9]).reshape(3, 3)
+    T[:3, 3] = t12[9:12]
+    return T

@@ -241,7 +241,8 @@ def ate_rmse(g: PoseGraphData, traj: dict, *, anchor_robot: int = 0) -> float:
 
 
 def run_pipeline(g0: PoseGraphData, stream: LcStream, params, lcd_params, *, rank: int = 0, world: int = 1,
-                 device: int = 0, rounds: int = 100, verifier=None, solver=None, exchange_device=None) -> dict:
+                 device: int = 0, rounds: int = 100, verifier=None, solver=None, exchange_device=None,
+                 return_trajectory: bool = False) -> dict:
     """One team run: LCD verification of this rank's candidates (query robot
     in the rank's robot range) -> all_gather of the accepted loop closures ->
     team graph -> global initialisation -> `rounds` concurrent RBCD rounds
@@ -311,6 +312,8 @@ def run_pipeline(g0: PoseGraphData, stream: LcStream, params, lcd_params, *, ran
     w = drv.solver.get_weights() if hasattr(drv.solver, "get_weights") else None
     out["dpgo"] = {"rounds": rounds, "seconds": t_pgo, "edges_iters_per_s": ei / max(t_pgo, 1e-12),
                    "ate_m": ate_rmse(g, mine)}
+    if return_trajectory:  # the team's rounded trajectories (identical on every rank)
+        out["trajectory"] = mine
     if w is not None and world == 1:
         lc = g.fixed == 0
         out["dpgo"]["gnc_weight_mean_inlier_lc"] = float(w[lc & ~g.outlier].mean()) if (lc & ~g.outlier).any() else None

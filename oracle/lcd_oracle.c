@@ -91,6 +91,19 @@ static int uid_draw(orc_mt19937* m, int variant) {
   return (int)x;
 }
 
+/* The engine a RANSAC problem draws from (LC5, README.md:35-36). rng_stream 0:
+ * every SampleConsensusProblem seeds its own engine with ransac_seed (opengv's
+ * constructor: rng_alg_.seed(12345u), and std::bind copies the engine into the
+ * problem's generator, so a problem never advances anyone else's engine);
+ * rng_stream 1: the fork's thread_local engine read as ONE engine per
+ * verification thread that every problem continues, seeded once when the
+ * thread starts (the caller passes it as `stream`). */
+static orc_mt19937* problem_rng(const kmx_lcd_params* P, orc_mt19937* local, orc_mt19937* stream) {
+  if (stream) return stream;
+  mt_seed(local, P->ransac_seed);
+  return local;
+}
+
 int orc_mt19937_stream(uint32_t seed, int variant, int32_t n, int32_t* out) {
   orc_mt19937 m;
   mt_seed(&m, seed);
@@ -986,12 +999,12 @@ static int model_from_sample(int algo, const double* F1, const double* F2, const
 
 /* opengv sac::Ransac::computeModel over the pair list; returns 1 on success. */
 static int ransac_2d2d(const kmx_lcd_params* P, const double* F1, const double* F2, int K, double R[9], double t[3],
-                       uint8_t* inl, int* n_inl, int* iters_out) {
+                       uint8_t* inl, int* n_inl, int* iters_out, orc_mt19937* stream) {
   *n_inl = 0;
   *iters_out = 0;
   if (K < 5) return 0;
-  orc_mt19937 m;
-  mt_seed(&m, P->ransac_seed);
+  orc_mt19937 m0;
+  orc_mt19937* m = problem_rng(P, &m0, stream);
   int32_t* sh = (int32_t*)malloc(sizeof(int32_t) * K);
   for (int i = 0; i < K; ++i) sh[i] = i;
   int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
@@ -1001,7 +1014,7 @@ static int ransac_2d2d(const kmx_lcd_params* P, const double* F1, const double* 
   while (iterations < k && skipped < max_skip) {
     int32_t smp[5];
     for (int i = 0; i < 5; ++i) {
-      const int r = uid_draw(&m, P->rng_variant);
+      const int r = uid_draw(m, P->rng_variant);
       const int j = i + (int)((size_t)r % (size_t)(K - i));
       const int32_t tt = sh[i];
       sh[i] = sh[j];
@@ -1359,12 +1372,12 @@ static double pnp_error(const double R[9], const double t[3], const double p[3],
 
 /* opengv sac::Ransac over the AbsolutePoseSacProblem (sample size 6, EPnP). */
 static int ransac_pnp(const kmx_lcd_params* P, const double* Fq, const double* Pm, int K, double R[9], double t[3],
-                      uint8_t* inl, int* n_inl) {
+                      uint8_t* inl, int* n_inl, orc_mt19937* stream) {
   *n_inl = 0;
   const int S = 6;
   if (K < S) return 0;
-  orc_mt19937 m;
-  mt_seed(&m, P->ransac_seed);
+  orc_mt19937 m0;
+  orc_mt19937* m = problem_rng(P, &m0, stream);
   int32_t* sh = (int32_t*)malloc(sizeof(int32_t) * K);
   for (int i = 0; i < K; ++i) sh[i] = i;
   int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
@@ -1374,7 +1387,7 @@ static int ransac_pnp(const kmx_lcd_params* P, const double* Fq, const double* P
   while (iterations < k && skipped < max_skip) {
     double sp[18], sf[18];
     for (int i = 0; i < S; ++i) {
-      const int r = uid_draw(&m, P->rng_variant);
+      const int r = uid_draw(m, P->rng_variant);
       const int j = i + (int)((size_t)r % (size_t)(K - i));
       const int32_t tt = sh[i];
       sh[i] = sh[j];
@@ -1562,12 +1575,12 @@ static double arun_error(const double R[9], const double t[3], const double pq[3
 }
 
 static int ransac_arun(const kmx_lcd_params* P, const double* Pq, const double* Pm, int K, double R[9], double t[3],
-                       uint8_t* inl, int* n_inl) {
+                       uint8_t* inl, int* n_inl, orc_mt19937* stream) {
   *n_inl = 0;
   const int S = 3;
   if (K < S) return 0;
-  orc_mt19937 m;
-  mt_seed(&m, P->ransac_seed);
+  orc_mt19937 m0;
+  orc_mt19937* m = problem_rng(P, &m0, stream);
   int32_t* sh = (int32_t*)malloc(sizeof(int32_t) * K);
   for (int i = 0; i < K; ++i) sh[i] = i;
   int iterations = 0, best_cnt = -INT_MAX, have = 0;
@@ -1575,7 +1588,7 @@ static int ransac_arun(const kmx_lcd_params* P, const double* Pq, const double* 
   double bR[9], bt[3];
   while (iterations < k) {
     for (int i = 0; i < S; ++i) {
-      const int r = uid_draw(&m, P->rng_variant);
+      const int r = uid_draw(m, P->rng_variant);
       const int j = i + (int)((size_t)r % (size_t)(K - i));
       const int32_t tt = sh[i];
       sh[i] = sh[j];
@@ -1614,18 +1627,24 @@ static int ransac_arun(const kmx_lcd_params* P, const double* Pq, const double* 
   return 1;
 }
 
-/* Full verification of one candidate from a frame pool (same layout as
- * kmx_lcd_batch_desc). masks (optional): [max_feats] bytes per candidate, bit0
- * 2D-2D inlier, bit1 3D-3D inlier, indexed by position in the pair list. */
-int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int32_t q, int32_t mfr,
-                   kmx_lcd_result* res, uint8_t* mask) {
+/* Verification of one candidate on a given correspondence list (pairs[2j] =
+ * query feature, pairs[2j+1] = match feature, j < K): geometricVerificationNister
+ * (KMX_LCD_STAGE_2D2D, drawio:2589-2592) then recoverPose (KMX_LCD_STAGE_RECOVER,
+ * drawio:2595-2598), the two calls Kimera-Distributed's verifyLoopSpin makes on
+ * computeMatchedIndices' output (drawio:2638-2657).
+ *   - without the 2D-2D stage every pair counts as a 2D-2D inlier (the caller
+ *     passes geometricVerificationNister's inliers to recoverPose) and the
+ *     rotation of the 1-point 3D-3D recovery is T_prior's (the caller's
+ *     2D-2D pose); recovery then runs whatever K is;
+ *   - without the recovery stage, accepted = the 2D-2D model exists and has
+ *     >= min_2d2d_inliers (geometricVerificationNister's bool), T = its pose.
+ * masks (optional): [max_feats] bytes, bit0 2D-2D inlier, bit1 3D-3D / 2D-3D
+ * inlier, indexed by position in the pair list. */
+static void verify_pairs(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int32_t q, int32_t mfr, int K,
+                         const int32_t* pairs, int stages, const double* T_prior, orc_mt19937* stream,
+                         kmx_lcd_result* res, uint8_t* mask) {
   memset(res, 0, sizeof(*res));
   const int F = pool->max_feats;
-  const int nq = pool->n_feats[q], nm = pool->n_feats[mfr];
-  int32_t* pairs = (int32_t*)malloc(sizeof(int32_t) * 2 * (nq + 1));
-  int32_t K = 0;
-  orc_lcd_knn2(P->norm, (double)P->lowe_ratio, pool->desc + (size_t)q * F * 32, nq,
-               pool->desc + (size_t)mfr * F * 32, nm, pairs, &K);
   res->n_matches = K;
   if (mask) memset(mask, 0, (size_t)F);
   double* F1 = (double*)malloc(sizeof(double) * 3 * (K + 1));
@@ -1636,14 +1655,27 @@ int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int3
       F2[3 * j + c] = pool->bearings[((size_t)mfr * F + pairs[2 * j + 1]) * 3 + c];
     }
   uint8_t* inl = (uint8_t*)calloc((size_t)K + 1, 1);
-  double R[9], t[3];
-  int n_inl = 0, iters = 0;
-  const int ok = ransac_2d2d(P, F1, F2, K, R, t, inl, &n_inl, &iters);
-  res->iterations_2d2d = iters;
-  res->mono_inliers = ok ? n_inl : 0;
+  double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, t[3] = {0, 0, 0};
+  int n_inl = 0, iters = 0, ok = 0, gate = 0;
+  if (stages & KMX_LCD_STAGE_2D2D) {
+    ok = ransac_2d2d(P, F1, F2, K, R, t, inl, &n_inl, &iters, stream);
+    res->iterations_2d2d = iters;
+    res->mono_inliers = ok ? n_inl : 0;
+    gate = ok && n_inl >= P->min_2d2d_inliers;
+  } else {
+    for (int j = 0; j < K; ++j) inl[j] = 1;
+    n_inl = K;
+    ok = 1;
+    gate = 1;
+    res->mono_inliers = K;
+    if (T_prior) {
+      memcpy(R, T_prior, sizeof(R));
+      memcpy(t, T_prior + 9, sizeof(t));
+    }
+  }
   if (ok && mask)
     for (int j = 0; j < K; ++j) mask[j] = inl[j];
-  if (ok && n_inl >= P->min_2d2d_inliers) {
+  if (gate && (stages & KMX_LCD_STAGE_RECOVER)) {
     /* stereo points of the 2D-2D inliers, in pair-list order */
     double* Pq = (double*)malloc(sizeof(double) * 3 * (K + 1));
     double* Pm = (double*)malloc(sizeof(double) * 3 * (K + 1));
@@ -1678,7 +1710,7 @@ int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int3
       }
       double Ro[9], to[3];
       int np = 0;
-      const int okp = ransac_pnp(P, Fq, Pw, n2, Ro, to, in3, &np);
+      const int okp = ransac_pnp(P, Fq, Pw, n2, Ro, to, in3, &np, stream);
       res->pnp_inliers = okp ? np : 0;
       if (okp) {
         if (mask)
@@ -1708,7 +1740,7 @@ int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int3
       }
       double Ra[9], ta[3];
       int na = 0;
-      const int oka = ransac_arun(P, Aq, Am, n2, Ra, ta, in3, &na);
+      const int oka = ransac_arun(P, Aq, Am, n2, Ra, ta, in3, &na, stream);
       res->stereo_inliers = oka ? na : 0;
       if (oka) {
         if (mask)
@@ -1733,17 +1765,72 @@ int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int3
       if (res->accepted && P->refine_pose) refit_3d3d(n3, Pq, Pm, in3, res->T_query_match, res->T_query_match + 9);
     }
     free(Pq); free(Pm); free(valid); free(idx); free(in3);
-  } else if (ok) {
+  } else if (ok && (stages & KMX_LCD_STAGE_2D2D)) {
     for (int i = 0; i < 9; ++i) res->T_query_match[i] = R[i];
     for (int i = 0; i < 3; ++i) res->T_query_match[9 + i] = t[i];
+    if (!(stages & KMX_LCD_STAGE_RECOVER)) res->accepted = gate;
   }
-  free(pairs); free(F1); free(F2); free(inl);
+  free(F1); free(F2); free(inl);
+}
+
+/* Full verification of one candidate from a frame pool (same layout as
+ * kmx_lcd_batch_desc): computeMatchedIndices (knn2 + Lowe), then both stages.
+ * `stream`: the verification thread's engine when rng_stream = 1 (NULL:
+ * every problem seeds its own). */
+static void verify_one(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int32_t q, int32_t mfr,
+                       orc_mt19937* stream, kmx_lcd_result* res, uint8_t* mask) {
+  const int F = pool->max_feats;
+  const int nq = pool->n_feats[q], nm = pool->n_feats[mfr];
+  int32_t* pairs = (int32_t*)malloc(sizeof(int32_t) * 2 * (nq + 1));
+  int32_t K = 0;
+  orc_lcd_knn2(P->norm, (double)P->lowe_ratio, pool->desc + (size_t)q * F * 32, nq,
+               pool->desc + (size_t)mfr * F * 32, nm, pairs, &K);
+  verify_pairs(P, pool, q, mfr, K, pairs, KMX_LCD_STAGE_2D2D | KMX_LCD_STAGE_RECOVER, NULL, stream, res, mask);
+  free(pairs);
+}
+
+int orc_lcd_verify(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int32_t q, int32_t mfr,
+                   kmx_lcd_result* res, uint8_t* mask) {
+  orc_mt19937 s;
+  if (P->rng_stream) mt_seed(&s, P->ransac_seed);
+  verify_one(P, pool, q, mfr, P->rng_stream ? &s : NULL, res, mask);
   return 0;
 }
 
+/* Candidates in order, as Kimera-Distributed's single verification thread
+ * takes them off its queue (drawio:246, 405); with rng_stream = 1 the thread's
+ * engine is seeded once at the start of the batch and continues from problem
+ * to problem (2D-2D, then the Arun / EPnP recovery). */
 int orc_lcd_verify_batch(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int32_t n,
                          const int32_t* cq, const int32_t* cm, kmx_lcd_result* res, uint8_t* masks) {
+  orc_mt19937 s;
+  if (P->rng_stream) mt_seed(&s, P->ransac_seed);
   for (int i = 0; i < n; ++i)
-    orc_lcd_verify(P, pool, cq[i], cm[i], res + i, masks ? masks + (size_t)i * pool->max_feats : NULL);
+    verify_one(P, pool, cq[i], cm[i], P->rng_stream ? &s : NULL, res + i,
+               masks ? masks + (size_t)i * pool->max_feats : NULL);
+  return 0;
+}
+
+/* geometricVerificationNister / recoverPose on caller-supplied correspondences
+ * (kmx_lcd_verify_matches): candidate i's pairs are
+ * (i_query[k], i_match[k]) for k in [mptr[i], mptr[i+1]); T_prior [n][12]
+ * (R row-major, t) is read only without the 2D-2D stage. */
+int orc_lcd_verify_pairs_batch(const kmx_lcd_params* P, const kmx_lcd_batch_desc* pool, int32_t n,
+                               const int32_t* cq, const int32_t* cm, const int64_t* mptr, const int32_t* i_query,
+                               const int32_t* i_match, int stages, const double* T_prior, kmx_lcd_result* res,
+                               uint8_t* masks) {
+  orc_mt19937 s;
+  if (P->rng_stream) mt_seed(&s, P->ransac_seed);
+  for (int i = 0; i < n; ++i) {
+    const int K = (int)(mptr[i + 1] - mptr[i]);
+    int32_t* pairs = (int32_t*)malloc(sizeof(int32_t) * 2 * (K + 1));
+    for (int k = 0; k < K; ++k) {
+      pairs[2 * k] = i_query[mptr[i] + k];
+      pairs[2 * k + 1] = i_match[mptr[i] + k];
+    }
+    verify_pairs(P, pool, cq[i], cm[i], K, pairs, stages, T_prior ? T_prior + 12 * (size_t)i : NULL,
+                 P->rng_stream ? &s : NULL, res + i, masks ? masks + (size_t)i * pool->max_feats : NULL);
+    free(pairs);
+  }
   return 0;
 }

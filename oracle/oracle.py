@@ -285,8 +285,11 @@ def _lcd_setup(L):
     L.orc_fivept_stewenius.argtypes = [C.POINTER(f64), C.POINTER(f64), C.POINTER(f64)]
     L.orc_lcd_verify_batch.argtypes = [C.POINTER(LcdParams), C.POINTER(LcdBatchDesc), i32, C.POINTER(i32),
                                        C.POINTER(i32), C.POINTER(LcdResult), C.POINTER(u8)]
+    L.orc_lcd_verify_pairs_batch.argtypes = [C.POINTER(LcdParams), C.POINTER(LcdBatchDesc), i32, C.POINTER(i32),
+                                             C.POINTER(i32), C.POINTER(C.c_int64), C.POINTER(i32), C.POINTER(i32),
+                                             C.c_int, C.POINTER(f64), C.POINTER(LcdResult), C.POINTER(u8)]
     for n in ("orc_mt19937_stream", "orc_ransac_samples", "orc_lcd_knn2", "orc_fivept_nister", "orc_fivept_stewenius",
-              "orc_lcd_verify_batch"):
+              "orc_lcd_verify_batch", "orc_lcd_verify_pairs_batch"):
         getattr(L, n).restype = C.c_int
 
 
@@ -351,6 +354,29 @@ def lcd_verify(params, pool, cand_query=None, cand_match=None, masks=True):
     L.orc_lcd_verify_batch(C.byref(params), C.byref(d), cq.shape[0], _i(cq), _i(cm), res,
                            _u(mk) if masks else None)
     return res, mk
+
+
+def lcd_verify_pairs(params, pool, cand_query, cand_match, correspondences, stages=3, T_prior=None, masks=True):
+    """geometricVerificationNister / recoverPose restated on caller-supplied
+    correspondences (oracle/lcd_oracle.c orc_lcd_verify_pairs_batch)."""
+    from kmx.abi import LcdResult
+    L = lib(); _lcd_setup(L)
+    cq = np.ascontiguousarray(cand_query, dtype=np.int32)
+    cm = np.ascontiguousarray(cand_match, dtype=np.int32)
+    n = cq.shape[0]
+    lens = [len(a) for a, _ in correspondences]
+    mptr = np.zeros(n + 1, np.int64)
+    mptr[1:] = np.cumsum(lens)
+    iq = np.ascontiguousarray(np.concatenate([np.asarray(a, np.int32) for a, _ in correspondences] + [np.zeros(1, np.int32)]))
+    im = np.ascontiguousarray(np.concatenate([np.asarray(b, np.int32) for _, b in correspondences] + [np.zeros(1, np.int32)]))
+    pr = None if T_prior is None else np.ascontiguousarray(T_prior, np.float64).reshape(n, 12)
+    d = batch_desc(pool)
+    res = (LcdResult * max(n, 1))()
+    mk = np.zeros((max(n, 1), pool.max_feats), np.uint8) if masks else None
+    L.orc_lcd_verify_pairs_batch(C.byref(params), C.byref(d), n, _i(cq), _i(cm),
+                                 mptr.ctypes.data_as(C.POINTER(C.c_int64)), _i(iq), _i(im), int(stages),
+                                 _f(pr) if pr is not None else None, res, _u(mk) if masks else None)
+    return res, (mk[:n] if masks else None)
 
 
 # ------------------------------------------------------------------ BoW ----

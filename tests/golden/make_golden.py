@@ -102,16 +102,16 @@ LCD_REFINE_CASES = [     # refine_pose 1 (LcdParams.yaml:14) on the 3D-3D recove
 ]
 
 
-def lcd_params(case, refine=0):
+def lcd_params(case, refine=0, stream=0):
     from kmx.lcd import LcdParams
     algo, variant, norm, rec = case
     return LcdParams(ransac_2d2d_algorithm=algo, rng_variant=variant, norm=norm, pose_recovery_type=int(rec == 1),
-                     ransac_use_1point_3d3d=int(rec != 2), refine_pose=refine)
+                     ransac_use_1point_3d3d=int(rec != 2), refine_pose=refine, rng_stream=stream)
 
 
-def run_lcd_oracle(pool, case, refine=0):
+def run_lcd_oracle(pool, case, refine=0, stream=0):
     from oracle import oracle as O
-    res, masks = O.lcd_verify(lcd_params(case, refine).to_c(), pool)
+    res, masks = O.lcd_verify(lcd_params(case, refine, stream).to_c(), pool)
     ints = np.array([[r.n_matches, r.mono_inliers, r.stereo_inliers, r.pnp_inliers, r.accepted, r.iterations_2d2d]
                      for r in res], np.int32)
     T = np.array([list(r.T_query_match[:]) for r in res], np.float64)
@@ -130,6 +130,22 @@ def make_refine():
                         cases=np.array([[a, v == "gcc11", n == "hamming", r] for a, v, n, r in LCD_REFINE_CASES],
                                        np.int32), **arrs)
     print("lcd_refine.npz", (OUT / "lcd_refine.npz").stat().st_size, "bytes")
+
+
+def make_stream():
+    """lcd_stream.npz: every LCD case under the other LC5 reading (rng_stream
+    1, the fork's thread_local engine continued across problems; README.md:35-36)
+    on the same pool (added in round 4; the earlier fixtures are not
+    regenerated)."""
+    pool = lcd_inputs()
+    arrs = {}
+    for k, case in enumerate(LCD_CASES):
+        ints, T, masks = run_lcd_oracle(pool, case, stream=1)
+        arrs[f"ints_{k}"], arrs[f"T_{k}"], arrs[f"masks_{k}"] = ints, T, masks
+    np.savez_compressed(OUT / "lcd_stream.npz",
+                        cases=np.array([[a, v == "gcc11", n == "hamming", r] for a, v, n, r in LCD_CASES], np.int32),
+                        **arrs)
+    print("lcd_stream.npz", (OUT / "lcd_stream.npz").stat().st_size, "bytes")
 
 
 def main():
@@ -154,5 +170,7 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["--refine"]:
         make_refine()
+    elif sys.argv[1:] == ["--stream"]:
+        make_stream()
     else:
         main()

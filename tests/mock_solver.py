@@ -7,6 +7,8 @@ oracle/); the schedule is kmx.dpgo.schedule.GncSchedule, the host mirror of
 the device rule in csrc/pgo.hip."""
 import ctypes as C
 
+import os
+
 import numpy as np
 
 from kmx.dpgo.schedule import GncSchedule
@@ -186,9 +188,20 @@ class NativeOracleBlockSolver(OracleBlockSolver):
         assert len(unique_id) == 128 and timeout_s > 0
         self.world, self.rank, self.xchg = world, rank, None
         self.comm_inits = getattr(self, "comm_inits", 0) + 1
+        # KMX_MOCK_STORE: a posted (asynchronous) transport like ncclSend /
+        # ncclRecv on the solver stream — exchange() posts this rank's segments
+        # and returns, sync_timeout() waits for the peers' with a deadline
+        path = os.environ.get("KMX_MOCK_STORE")
+        self._store = None
+        if path:
+            import torch.distributed as dist
+            self._store = dist.FileStore(path, world)
+            self._pending = None
+            self._nx = 0
 
     def comm_destroy(self):
         self.xchg = None
+        self._pending = None
         self.comm_destroys = getattr(self, "comm_destroys", 0) + 1
 
     def set_exchange(self, send_slots, send_counts, recv_slots, recv_counts):
@@ -205,12 +218,24 @@ class NativeOracleBlockSolver(OracleBlockSolver):
 
     corrupt = False  # a faulty transport for the start-up check's test
 
+    raise_in_exchange = False  # this rank's exchange raises before posting (its peers have posted theirs)
+
     def exchange(self):
         import torch
         import torch.distributed as dist
         ss, ns, sseg, rs, nr, rseg, ssplit, rsplit = self.xchg
         sbuf, rbuf = np.zeros(sum(ssplit)), np.zeros(sum(rsplit))
         self.exchange_pack(ss.ctypes.data, ns, sseg.ctypes.data, self.world, sbuf.ctypes.data)
+        if self.raise_in_exchange:
+            raise RuntimeError("ncclSend: unhandled system error (injected)")
+        if getattr(self, "_store", None) is not None:
+            so = np.concatenate([[0], np.cumsum(ssplit)]).astype(np.int64)
+            for q in range(self.world):
+                self._store.set(f"x{self._nx}/{self.rank}->{q}", sbuf[so[q]:so[q + 1]].tobytes())
+            self._pending = (rbuf, rsplit, self._nx)
+            self._nx += 1
+            self.exchanges += 1
+            return
         out = torch.zeros(rbuf.shape[0], dtype=torch.float64)
         dist.all_to_all_single(out, torch.from_numpy(sbuf), rsplit, ssplit)
         rbuf[:] = out.numpy()
@@ -219,9 +244,32 @@ class NativeOracleBlockSolver(OracleBlockSolver):
         self.exchange_unpack(rs.ctypes.data, nr, rseg.ctypes.data, self.world, rbuf.ctypes.data)
         self.exchanges += 1
 
+    def sync_timeout(self, timeout_s):
+        """Wait (bounded) for the posted exchange's incoming segments; False on
+        a timeout, as kmx_pgo_sync_timeout."""
+        import datetime
+        if getattr(self, "_pending", None) is None:
+            return True
+        rbuf, rsplit, k = self._pending
+        keys = [f"x{k}/{q}->{self.rank}" for q in range(self.world)]
+        try:
+            self._store.wait(keys, datetime.timedelta(seconds=timeout_s))
+        except Exception:  # noqa: BLE001 - the store's timeout error
+            return False
+        ro = np.concatenate([[0], np.cumsum(rsplit)]).astype(np.int64)
+        for q in range(self.world):
+            rbuf[ro[q]:ro[q + 1]] = np.frombuffer(self._store.get(keys[q]), np.float64)
+        if self.corrupt and rbuf.size:
+            rbuf[0] += 1e-12
+        ss, ns, sseg, rs, nr, rseg, _, _ = self.xchg
+        self.exchange_unpack(rs.ctypes.data, nr, rseg.ctypes.data, self.world, rbuf.ctypes.data)
+        self._pending = None
+        return True
+
     def _native(self):  # the exchange lists are set: every round starts with the exchange
         if getattr(self, "xchg", None) is not None:
             self.exchange()
+            assert self.sync_timeout(120.0)
 
     def iterate(self, active):
         self._native()

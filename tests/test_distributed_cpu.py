@@ -183,9 +183,11 @@ def test_exchange_plan_consistent(world):
             assert np.all(rank_of[keys[seg_sent] >> 32] == k)
 
 
-def _native_worker(rank, world, port, rounds, q, fail_rank=-1, corrupt_rank=-1):
+def _native_worker(rank, world, port, rounds, q, fail_rank=-1, corrupt_rank=-1, raise_rank=-1, store=None):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if store:
+        os.environ.update(KMX_MOCK_STORE=store, KMX_XCHG_TIMEOUT="5")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from kmx.dpgo.driver import RBCDDriver
     from tests.mock_solver import NativeOracleBlockSolver
@@ -196,6 +198,7 @@ def _native_worker(rank, world, port, rounds, q, fail_rank=-1, corrupt_rank=-1):
             raise RuntimeError("no RCCL")
         s.comm_init = fail
     s.corrupt = rank == corrupt_rank  # this rank's transport delivers a wrong bit
+    s.raise_in_exchange = rank == raise_rank  # this rank's first exchange raises after its peers posted
     drv = RBCDDriver(P, g, rank=rank, world=world, solver=s, exchange_device="cuda")
     drv.initialize(_x0(g))
     drv.step(with_stats=True)          # one exchange (the round's own)
@@ -281,5 +284,36 @@ def test_native_exchange_checked_at_first_round():
     for rank, X, wu, native, inits, exchanges, async_calls, mode, destroys in res:
         assert not native and inits == 1 and destroys == 1 and exchanges == 1
         assert "differed" in mode
+        for a, Xa in X.items():
+            assert np.array_equal(Xa, o.get_iterate(a)), (rank, a)
+
+
+@pytest.mark.timeout(300)
+def test_native_exchange_raise_after_peers_posted(tmp_path):
+    """one rank's first native exchange raises after its
+    peer has posted its half (a posted, asynchronous transport as ncclSend /
+    ncclRecv on the stream). The peer's wait is bounded (sync_timeout,
+    KMX_XCHG_TIMEOUT), both ranks reach the agreement, drop the native
+    exchange together, exchange_mode reports the exception (not a bitwise
+    mismatch), and the team still matches the single-process run bit for
+    bit."""
+    world, rounds = 2, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    store = str(tmp_path / "xchg_store")
+    ps = [ctx.Process(target=_native_worker, args=(r, world, port, rounds, q, -1, -1, 1, store))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    g, P = _graph(False), _params(1e-3, False)
+    o, _ = reference_rounds(g, P, rounds)
+    for rank, X, wu, native, inits, exchanges, async_calls, mode, destroys in res:
+        assert not native and inits == 1 and destroys == 1
+        assert "failed" in mode and "rank 1" in mode and "injected" in mode and "differed" not in mode
+        assert exchanges == (1 if rank == 0 else 0)  # rank 0 posted; rank 1 raised first
         for a, Xa in X.items():
             assert np.array_equal(Xa, o.get_iterate(a)), (rank, a)

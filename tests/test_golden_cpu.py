@@ -78,6 +78,43 @@ def test_lcd_refine_fixture_reproduced(k):
     assert np.array_equal(ints, d[f"ints_{k0}"]) and np.array_equal(masks, d[f"masks_{k0}"])
 
 
+@pytest.mark.parametrize("k", range(len(MG.LCD_CASES)))
+def test_lcd_stream_fixture_reproduced(k):
+    """LC5's other reading (rng_stream 1: one engine per verification thread,
+    continued from problem to problem) is frozen too; its first 2D-2D problem
+    equals the per-problem reseed's (both start from the seed), and a later
+    drawing candidate differs (the flag selects a different sampler)."""
+    d = np.load(GOLD / "lcd_small.npz")
+    s = np.load(GOLD / "lcd_stream.npz")
+    pool = MG.pool_from(d)
+    case = MG.LCD_CASES[k]
+    assert s["cases"][k].tolist() == [case[0], case[1] == "gcc11", case[2] == "hamming", case[3]]
+    ints, T, masks = MG.run_lcd_oracle(pool, case, stream=1)
+    assert np.array_equal(ints, s[f"ints_{k}"])
+    assert np.array_equal(masks, s[f"masks_{k}"])
+    _close(T, s[f"T_{k}"])
+    assert np.array_equal(ints[0, [0, 1, 5]], d[f"ints_{k}"][0, [0, 1, 5]])  # the first 2D-2D problem
+    assert not (np.array_equal(ints, d[f"ints_{k}"]) and np.array_equal(T, d[f"T_{k}"]))
+
+
+def test_verify_pairs_on_knn_pairs_is_verify():
+    """orc_lcd_verify_pairs_batch with both stages on computeMatchedIndices'
+    pairs is orc_lcd_verify (the fused path), for every case."""
+    from oracle import oracle as O
+    d = np.load(GOLD / "lcd_small.npz")
+    pool = MG.pool_from(d)
+    corr = []
+    for q, m in zip(pool.cand_query, pool.cand_match):
+        pr = O.knn2(0, 0.7, pool.desc[q, :pool.n_feats[q]], pool.desc[m, :pool.n_feats[m]])
+        corr.append((pr[:, 0], pr[:, 1]))
+    case = MG.LCD_CASES[0]
+    res, masks = O.lcd_verify_pairs(MG.lcd_params(case).to_c(), pool, pool.cand_query, pool.cand_match, corr)
+    assert np.array_equal(masks, d["masks_0"])
+    ints = np.array([[r.n_matches, r.mono_inliers, r.stereo_inliers, r.pnp_inliers, r.accepted, r.iterations_2d2d]
+                     for r in res], np.int32)
+    assert np.array_equal(ints, d["ints_0"])
+
+
 def test_refine_pose_delta_on_planted_pool():
     """The delta refine_pose makes on this pool (measured
     and documented). Its restated form — least squares over all 3D-3D

@@ -77,3 +77,21 @@ def test_lcd_refine_gpu_matches_fixture(gpu, k):
     assert np.array_equal(ints, r[f"ints_{k}"])
     assert np.array_equal(gm, r[f"masks_{k}"])
     assert np.array_equal(np.array([x["T_query_match"] for x in got]), r[f"T_{k}"])
+
+
+@pytest.mark.parametrize("k", range(len(MG.LCD_CASES)))
+def test_lcd_stream_gpu_matches_fixture(gpu, k):
+    """rng_stream 1 (the ordered, candidate-serial sampler) against the frozen
+    restatement output of the persistent-engine reading, bit for bit."""
+    from kmx.lcd import LoopClosureDetector
+    d = np.load(GOLD / "lcd_small.npz")
+    r = np.load(GOLD / "lcd_stream.npz")
+    pool = MG.pool_from(d)
+    det = LoopClosureDetector(MG.lcd_params(MG.LCD_CASES[k], stream=1))
+    det.set_pool(pool)
+    got, gm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    ints = np.array([[x["n_matches"], x["mono_inliers"], x["stereo_inliers"], x["pnp_inliers"], int(x["accepted"]),
+                      x["iterations_2d2d"]] for x in got], np.int32)
+    assert np.array_equal(ints, r[f"ints_{k}"])
+    assert np.array_equal(gm, r[f"masks_{k}"])
+    assert np.array_equal(np.array([x["T_query_match"] for x in got]), r[f"T_{k}"])

@@ -3,7 +3,12 @@ loop-closure stream plants ground-truth relative poses, the distributed
 initialisation recovers the team from exact loop closures, and a tiny team
 run (oracle LCD + oracle RBCD) accepts exactly the planted loop closures and
 lowers the trajectory error."""
+import multiprocessing as mp
+import os
+import socket
+
 import numpy as np
+import pytest
 
 from kmx import pipeline as PL
 from kmx.synth import make_pose_graph
@@ -72,3 +77,65 @@ def test_run_pipeline_oracle():
                           solver=OracleBlockSolver(P))
     assert out["lcd"]["accepted"] == out["lcd"]["true_positives"] == 60
     assert out["dpgo"]["ate_m"] < out["init"]["ate_m"]
+
+
+def _pipe_inputs():
+    from kmx.dpgo.params import PGOAgentParameters
+    g0 = make_pose_graph(3, 1500, 6000, f_inter=0.0, outlier_scope="robot", seed=4)
+    st = PL.make_lc_stream(g0, 40, 20, n_feats=160, seed=2)
+    P = PGOAgentParameters(r=5)
+    P.robustOptInnerIters = 5
+    P.schedule = 1
+    return g0, st, P
+
+
+def _pipe_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kmx.lcd import LcdParams
+    from tests.mock_solver import OracleBlockSolver
+    g0, st, P = _pipe_inputs()
+    out = PL.run_pipeline(g0, st, P, LcdParams(), rank=rank, world=world, rounds=12, verifier=_oracle_verifier(st),
+                          solver=OracleBlockSolver(P), exchange_device="cpu", return_trajectory=True)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_run_pipeline_world2_equals_world1():
+    """configs[4]'s multi-rank branch: per-rank
+    verification of the candidates whose query robot the rank owns,
+    all_gather_object of the accepted loop closures, then RBCD over two gloo
+    ranks — the same accepted set, initial error and final trajectories (bit
+    for bit) as the single-process run."""
+    from kmx.lcd import LcdParams
+    from tests.mock_solver import OracleBlockSolver
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, 2, port, q), daemon=True) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(q.get(timeout=240) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    g0, st, P = _pipe_inputs()
+    ref = PL.run_pipeline(g0, st, P, LcdParams(), rounds=12, verifier=_oracle_verifier(st),
+                          solver=OracleBlockSolver(P), return_trajectory=True)
+    assert ref["lcd"]["accepted"] == ref["lcd"]["true_positives"] == 40
+    for rank, out in got.items():
+        for k in ("verified", "accepted", "true_positives"):
+            assert out["lcd"][k] == ref["lcd"][k], (rank, k)
+        assert out["init"]["ate_m"] == ref["init"]["ate_m"]
+        assert out["init"]["shared_loop_closures"] == ref["init"]["shared_loop_closures"]
+        assert out["dpgo"]["ate_m"] == ref["dpgo"]["ate_m"]
+        for a, (R, t) in ref["trajectory"].items():
+            assert np.array_equal(out["trajectory"][a][0], R) and np.array_equal(out["trajectory"][a][1], t), (rank, a)
