@@ -2588,16 +2588,11 @@ PnpParams pnp_params(const kmx_lcd* h, int stages) {
 
 // k_ransac_coop over candidates [0, n) of the (offset) candidate arrays.
 int launch_ransac(kmx_lcd* h, int n, const RsParams& rp, const short* table, int c0, bool masks) {
-  // KMX_COOP_LB: minimum waves per SIMD (register-budget A/B). Stewenius: the
-  // batch's LDS (12.6 KB per wave) admits 12 waves per CU, so 3 waves per SIMD
-  // and their 168 VGPRs; Nister: 4 waves per SIMD
-  static const int clb = [] {
-    const char* v = std::getenv("KMX_COOP_LB");
-    return v ? std::atoi(v) : 0;
-  }();
+  // minimum waves per SIMD: Stewenius 3 (the batch's LDS, 12.6 KB per wave,
+  // admits 12 waves per CU; 168 VGPRs), Nister 4 — the measured best register
+  // budgets (the other budgets lost their A/B and were removed)
   const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
-  auto kc = stew ? ((clb == 2) ? k_ransac_coop<2, true> : k_ransac_coop<3, true>)
-                 : ((clb == 3) ? k_ransac_coop<3, false> : k_ransac_coop<4, false>);
+  auto kc = stew ? k_ransac_coop<3, true> : k_ransac_coop<4, false>;
   // one wave per resident slot (<= RS_MAX_SLOTS: the scratch is sized for it)
   int per_cu = 0, dev = 0, cus = 0;
   KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kc, RS_BLOCK, 0));

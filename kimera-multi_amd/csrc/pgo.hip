@@ -2185,8 +2185,8 @@ struct kmx_pgo {
   HostStatus* hstat = nullptr;
   int hstat_cap = 0;
   unsigned long long seq = 0;
-  bool poll = true;          // KMX_POLL=0: enqueue every tCG step (finished robots exit at once)
-  // KMX_POLL unset / kmx_pgo_set_tcg_poll(-1): adaptive. A polled tCG loop
+  bool poll = true;          // kmx_pgo_set_tcg_poll(0): enqueue every tCG step (finished robots exit at once)
+  // kmx_pgo_set_tcg_poll(-1) (the default): adaptive. A polled tCG loop
   // that ran to within BLIND_SLACK steps of the cap sends the next
   // BLIND_WINDOW loops blind (no host wait: at most BLIND_SLACK empty step
   // pairs of ~1.5 us each, against the host round trip of every polled step
@@ -2655,10 +2655,6 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     return kmx::fail(KMX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
   h->own_stream = true;
-  if (const char* v = std::getenv("KMX_POLL")) {
-    h->poll = std::atoi(v) != 0;
-    h->poll_auto = false;
-  }
   if (const char* v = std::getenv("KMX_EARLY")) h->early_forced = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);

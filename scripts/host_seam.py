@@ -14,8 +14,8 @@ table (rows gathered once) and times rounds under:
          world-1 communicator, the segment sent to self by ncclSend / ncclRecv:
          min(sent, received) rows, so the rows are the rank's own, not its
          peers' — timing only), all rounds from one iterate_async call
-Run under KMX_POLL=1 (host-polled tCG) and KMX_POLL=0 (tCG steps enqueued
-blind; the kernels exit early once every robot stopped).
+The handle's tCG enqueueing is the default adaptive mode
+(kmx_pgo_set_tcg_poll(-1)).
 usage: python scripts/host_seam.py N [rounds]
 """
 import os
@@ -79,7 +79,7 @@ wire_in = torch.zeros(n_recv * ps + N, dtype=torch.float64, device=dev)
 wire_out = torch.zeros_like(wire_in)
 print(f"N={N}: rank 0 holds robots {lo}..{hi - 1}, {int(g.n_poses[lo:hi].sum())} poses; "
       f"sends {n_send} rows, receives {n_recv} rows ({n_recv * ps * 8 / 1e6:.2f} MB) per round; "
-      f"KMX_POLL={os.environ.get('KMX_POLL', '1')}", flush=True)
+      "adaptive tCG enqueueing", flush=True)
 
 for mode in ("batch", "seam", "native"):
     s = make()

@@ -437,7 +437,6 @@ def test_tcg_poll_modes_agree_bitwise(gpu, monkeypatch, red):
     for bit over rounds that cross GNC updates, in both reduction forms, and
     the team status a multi-rank exchange carries is the same."""
     monkeypatch.setenv("KMX_RED", red)
-    monkeypatch.delenv("KMX_POLL", raising=False)
     g, P, X0 = _setup(robust=True, seed=6)
     out = []
     for mode in (1, 0, -1):
