@@ -1310,6 +1310,64 @@ __device__ __forceinline__ int eigvec_col(const double mcol[10], int lane, cplx_
   return ok;
 }
 
+// eigvec_col for a real eigenvalue (lam.im == 0): the complex LU's operations
+// with every imaginary part zero, in real arithmetic — the same real parts
+// bit for bit (x - 0 * y = x, |re| + 0 = |re|, Smith's quotient by (d, 0) is
+// re / d; lcd.hip is built without contraction), at half the shuffles and a
+// quarter of the arithmetic.
+__device__ __forceinline__ int eigvec_col_real(const double mcol[10], int lane, double lam, double xyz[3]) {
+  lane = fresh_lane(lane);
+  const int g0 = (lane / 10) * 10, c = lane - g0 < 10 ? lane - g0 : 9;
+  double b[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) b[i] = (i == c) ? mcol[i] - lam : mcol[i];
+  int ok = 1;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    double col[10];
+#pragma unroll
+    for (int i = k; i < 10; ++i) col[i] = __shfl(b[i], g0 + k, 64);
+    int p = k;
+    double pa = fabs(col[k]);
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i)
+      if (fabs(col[i]) > pa) { p = i; pa = fabs(col[i]); }
+    if (pa == 0.0) ok = 0;
+    double bk = b[k], bp = b[k], ck = col[k], cp = col[k];
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i)
+      if (i == p) { bp = b[i]; cp = col[i]; }
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i)
+      if (i == p) { b[i] = bk; col[i] = ck; }
+    b[k] = bp;
+    col[k] = cp;
+    double cm = col[k];
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i)
+      if (i == c) cm = col[i];
+    const double fm = cm / col[k];
+#pragma unroll
+    for (int i = k + 1; i < 10; ++i) {
+      const double f = __shfl(fm, g0 + i, 64);
+      if (c > k) b[i] = b[i] - f * b[k];
+    }
+  }
+  double v[10];
+  v[9] = 1.0;
+#pragma unroll
+  for (int i = 8; i >= 0; --i) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = i + 1; j < 10; ++j) s = s - __shfl(b[i], g0 + j, 64) * v[j];
+    v[i] = s / __shfl(b[i], g0 + i, 64);
+  }
+  xyz[0] = v[6];
+  xyz[1] = v[7];
+  xyz[2] = v[8];
+  return ok;
+}
+
 // ------------------------------------- batched Stewenius eigenvalues ---
 // k_ransac_coop<STEW = true> takes a candidate's hypotheses SG at a time in
 // the serial loop's order: the null space, system and Gauss-Jordan of each
@@ -1342,6 +1400,7 @@ struct StewBatch {
   int ok[SG];                   // Gauss-Jordan and QR iteration succeeded
   int mok[SG];                  // a model was found
   unsigned char pb[MAXP], ps[MAXP];  // the batch's solutions: hypothesis, eigenvalue
+  unsigned char qo[MAXP];            // solution indices in eigenvector order (real first)
 };
 constexpr int STASH_H = 96;  // per hypothesis: C6 (rows 0-5 of M, 60) + N (36)
 constexpr int GJW = 3;       // hypotheses per batched Gauss-Jordan (groups of 20 lanes)
@@ -1620,23 +1679,36 @@ __device__ __forceinline__ void stew_models(StewBatch& sb, double* stash, int la
   lane = fresh_lane(lane);
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   int np;
+  int nre;  // the real solutions come first in the eigenvector order (sb.qo)
   {  // solution list
     const int b = lane / 10, s = lane - 10 * b;
     const bool sol = lane < 10 * nb && sb.ok[b < SG ? b : 0] && !(sb.wi[b < SG ? b : 0][s] < 0.0);
-    const unsigned long long m = __ballot(sol);
+    const bool re = sol && sb.wi[b < SG ? b : 0][s] == 0.0;
+    const unsigned long long m = __ballot(sol), mr = __ballot(re);
     if (sol) {
       const int k = __popcll(m & ((1ull << lane) - 1ull));
       sb.pb[k] = (unsigned char)b;
       sb.ps[k] = (unsigned char)s;
+      // eigenvector order: real solutions first (real LU), then the complex ones
+      const int o = re ? __popcll(mr & ((1ull << lane) - 1ull))
+                       : __popcll(mr) + __popcll((m & ~mr) & ((1ull << lane) - 1ull));
+      sb.qo[o] = (unsigned char)k;
     }
     np = __popcll(m);
+    nre = __popcll(mr);
   }
   wsync();
   double* Es = stash + SG * STASH_H;
   unsigned long long pok = 0;  // bit k: solution k gave an essential
-  for (int q0 = 0; q0 < np; q0 += 6) {
-    const int g = lane / 10, g0 = g * 10, c = lane - g0, pi = q0 + g;
-    const bool act = g < 6 && pi < np;
+  // six solutions at a time in eigenvector order: batches [0, nre) real, then
+  // [nre, np) complex (a batch never mixes them; results land at the solution's
+  // list index, so the order they are computed in changes nothing)
+  for (int q0 = 0; q0 < np;) {
+    const bool real = q0 < nre;
+    const int qend = real ? nre : np, qn = min(6, qend - q0);
+    const int g = lane / 10, g0 = g * 10, c = lane - g0;
+    const bool act = g < qn;
+    const int pi = act ? sb.qo[q0 + g] : 0;
     const int b = act ? sb.pb[pi] : 0, si = act ? sb.ps[pi] : 0;
     const double* st = stash + b * STASH_H;
     const int cc = c < 10 ? c : 9;
@@ -1644,7 +1716,8 @@ __device__ __forceinline__ void stew_models(StewBatch& sb, double* stash, int la
 #pragma unroll
     for (int i = 0; i < 10; ++i) mcol[i] = action_entry(st, i, cc);
     double xyz[3] = {0.0, 0.0, 0.0};
-    const int okv = eigvec_col(mcol, lane, cplx_d{act ? sb.wr[b][si] : 0.0, act ? sb.wi[b][si] : 0.0}, xyz);
+    const int okv = real ? eigvec_col_real(mcol, lane, act ? sb.wr[b][si] : 0.0, xyz)
+                         : eigvec_col(mcol, lane, cplx_d{act ? sb.wr[b][si] : 0.0, act ? sb.wi[b][si] : 0.0}, xyz);
     // lane 10g + e (e < 9): entry e of E; the norm over the group's 9 entries in order
     const double* Nb = st + 60;
     const double e = (c < 9) ? xyz[0] * Nb[c] + xyz[1] * Nb[9 + c] + xyz[2] * Nb[18 + c] + Nb[27 + c] : 0.0;
@@ -1660,7 +1733,8 @@ __device__ __forceinline__ void stew_models(StewBatch& sb, double* stash, int la
     const unsigned long long gm = __ballot(good && c == 0);
 #pragma unroll
     for (int gg = 0; gg < 6; ++gg)
-      if ((gm >> (10 * gg)) & 1ull) pok |= 1ull << (q0 + gg);
+      if ((gm >> (10 * gg)) & 1ull) pok |= 1ull << sb.qo[q0 + gg];
+    q0 += qn;
   }
   __threadfence_block();  // Es is read back by other lanes of this wave
   wsync();

@@ -48,6 +48,13 @@
 
 #include "common.h"
 
+// KMX_HESS_PROBE (diagnostic builds only, scripts/gpu_hess_probe.sh): bits
+// remove one k_hess stream each so its PMC traffic can be attributed; the
+// results of such a build are wrong by design. 0 in the product build.
+#ifndef KMX_HESS_PROBE
+#define KMX_HESS_PROBE 0
+#endif
+
 namespace {
 
 constexpr int WAVES = 4;
@@ -568,8 +575,14 @@ __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const d
     const bool tail = (in.y >> 31) & 1;
     const double2* b2 = reinterpret_cast<const double2*>(V + (size_t)max(o, 0) * 4 * R);
     double2 vr[2 * R];
+#if KMX_HESS_PROBE & 1  // traffic attribution build: no neighbour rows
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) vr[i] = make_double2(1e-3 * i, 1e-3);
+    (void)b2;
+#else
 #pragma unroll
     for (int i = 0; i < 2 * R; ++i) vr[i] = b2[i];
+#endif
     if (tid < CH && c0 + tid < n) {
       const double wk = (o >= 0) ? E.wk : 0.0, wt = (o >= 0) ? E.wt : 0.0;
 #pragma unroll
@@ -607,9 +620,14 @@ __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const d
   }
   if (L.valid) {
     double vs[4];
-    load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
     double D[16];
+#if KMX_HESS_PROBE & 2  // traffic attribution build: no own-row / diagonal-block loads
+    for (int c = 0; c < 4; ++c) vs[c] = 1e-3 * c;
+    for (int c = 0; c < 16; ++c) D[c] = (c % 5 == 0) ? 1.0 : 0.0;
+#else
+    load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
     load_sym4(d.hD + SYM4 * (size_t)L.pose, D);
+#endif
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       acc[c] += vs[0] * D[4 * c] + vs[1] * D[4 * c + 1] + vs[2] * D[4 * c + 2] + vs[3] * D[4 * c + 3];
@@ -1349,9 +1367,14 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
   const bool first = (tcg_iter == 0);
   asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
   if (L.valid) {
+#if KMX_HESS_PROBE & 2
+    for (int k = 0; k < 4; ++k) { zs[k] = 1e-3 * k; y[k] = (k == L.a) ? 1.0 : 0.0; }
+    for (int k = 0; k < 9; ++k) S[k] = (k % 4 == 0) ? 1.0 : 0.0;
+#else
     load4(d.z + o, zs);
     load4(d.X + o, y);
     load_sym3(d.S + 6 * (size_t)L.pose, S);
+#endif
   } else {
 #pragma unroll
     for (int i = 0; i < 9; ++i) S[i] = 0.0;
@@ -1362,7 +1385,7 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
   double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
   const int dhn = d.dhn;
   if (L.valid) {
-    if (first) {
+    if (first || (KMX_HESS_PROBE & 4)) {  // (probe 4: no delta_old / Hdelta_old traffic)
 #pragma unroll
       for (int k = 0; k < 4; ++k) { dl[k] = -zs[k]; hdl[k] = -hz[k]; }
     } else {
@@ -1398,7 +1421,7 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
     v = dl[0] * hdl[0] + dl[1] * hdl[1] + dl[2] * hdl[2] + dl[3] * hdl[3];
   }
   finish_tile<RED_HESS, 1, RM>(d, L, &v, smem + SmemH<R>::red_off, [&]() {
-    if (L.valid) {
+    if (L.valid && !(KMX_HESS_PROBE & 8)) {  // (probe 8: no stores)
       store4(d.dh + (size_t)(tcg_iter % dhn) * d.vec + o, dl);
       store4(d.hd + o, hdl);
     }

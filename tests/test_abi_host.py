@@ -19,6 +19,20 @@ def test_library_exports_every_header_symbol():
     assert L.kmx_abi_version() == abi.ABI_VERSION
 
 
+def test_runtime_info_names_the_rccl_serving_kmx():
+    """which librccl / libamdhip64 libkmx's own calls resolve
+    to (dladdr inside the library), their versions, and every copy mapped into
+    the process — torch bundles a librccl of the same SONAME, so two copies can
+    end up mapped when kmx is loaded first."""
+    from kmx import abi
+    ri = abi.runtime_info()
+    assert ri["rccl_path"].endswith((".so", ".so.1")) or "librccl" in ri["rccl_path"]
+    assert ri["rccl_version"] >= 20000 and ri["rccl_header_version"] >= 20000
+    assert "libamdhip64" in ri["hip_path"] and ri["hip_runtime_version"] > 0
+    assert ri["rccl_path_real"] in ri["mapped_rccl"]
+    assert ri["single_rccl"] == (len(ri["mapped_rccl"]) == 1)
+
+
 def test_no_cpu_fallback_without_gpu():
     from kmx import abi
     if abi.device_count() > 0:
