@@ -2227,7 +2227,7 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
                                                           const int* cq, const int* cm, const int2* pairs,
                                                           const int* Kin, const short* table, RsParams P,
                                                           kmx_lcd_result* res, unsigned char* masks,
-                                                          double* fbuf, int n, int* next) {
+                                                          double* fbuf, int n, int* next, const int* order) {
   __shared__ CoopWS w;
   __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;  // Stewenius: the batch
   double* F1 = fbuf + (size_t)blockIdx.x * (6 * N + STASH);
@@ -2236,6 +2236,7 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
     if (threadIdx.x == 0) c = atomicAdd(next, 1);
     c = __shfl(c, 0, 64);
     if (c >= n) break;
+    if (order) c = order[c];  // the queue in the given order (longest first)
     ransac_candidate<STEW>(c, w, sb, F1, bearings, points, N, cq, cm, pairs, Kin, table, P, res, masks);
     __threadfence_block();
     wsync();
@@ -2468,8 +2469,20 @@ struct kmx_lcd {
   short* d_table_rec = nullptr;  // samples of the recovery RANSAC (6: PnP, 3: Arun), built when used
   int table_N = 0;
   int pmax = 0;
-  // candidate buffers
-  int cap = 0;
+  // candidate buffers: two slots, used by alternate calls, so one call's kNN2
+  // (on kstream) can run while the previous call's RANSAC drains (stream);
+  // d_cq .. d_order below point into the current slot
+  int cap = 0, cur = 0;
+  struct Slot {
+    int *cq = nullptr, *cm = nullptr, *K = nullptr, *hyps = nullptr, *nrec = nullptr, *order = nullptr;
+    int2* pairs = nullptr;
+    kmx_lcd_result* res = nullptr;
+    unsigned char* mask = nullptr;
+    double* prior = nullptr;
+  } slot[2];
+  hipStream_t kstream = nullptr;  // kNN2 of kmx_lcd_verify / _async
+  hipEvent_t ev_knn[2] = {nullptr, nullptr}, ev_rs[2] = {nullptr, nullptr};
+  bool ev_rs_set[2] = {false, false};
   int *d_cq = nullptr, *d_cm = nullptr, *d_K = nullptr;
   int2* d_pairs = nullptr;
   kmx_lcd_result* d_res = nullptr;
@@ -2486,6 +2499,7 @@ struct kmx_lcd {
   std::mt19937 stream_rng;
   short* d_row = nullptr;
   int *d_hyps = nullptr, *d_nrec = nullptr;
+  int* d_order = nullptr;  // k_order's queue order (KMX_LCD_ORDER)
   int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
   // kmx_lcd_enable_timing: events around the kNN2 and the RANSAC launches
   bool timing = false;
@@ -2510,15 +2524,30 @@ void lcd_free_tables(kmx_lcd* h) {
   h->table_N = 0;
 }
 void lcd_free_cand(kmx_lcd* h) {
-  void* p[] = {h->d_cq, h->d_cm, h->d_K, h->d_pairs, h->d_res, h->d_mask, h->d_fbuf, h->d_next, h->d_hyps, h->d_nrec,
-               h->d_prior};
-  for (void* x : p)
-    if (x) (void)hipFree(x);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);  // in-flight calls may still use the buffers
+  if (h->kstream) (void)hipStreamSynchronize(h->kstream);
+  for (auto& sl : h->slot) {
+    void* p[] = {sl.cq, sl.cm, sl.K, sl.hyps, sl.nrec, sl.order, sl.pairs, sl.res, sl.mask, sl.prior};
+    for (void* x : p)
+      if (x) (void)hipFree(x);
+    sl = kmx_lcd::Slot{};
+  }
+  if (h->d_fbuf) (void)hipFree(h->d_fbuf);
+  if (h->d_next) (void)hipFree(h->d_next);
   h->d_cq = h->d_cm = h->d_K = nullptr; h->d_pairs = nullptr; h->d_res = nullptr; h->d_mask = nullptr;
   h->d_fbuf = nullptr;
   h->d_next = h->d_hyps = h->d_nrec = nullptr;
   h->d_prior = nullptr;
+  h->d_order = nullptr;
+  h->ev_rs_set[0] = h->ev_rs_set[1] = false;
   h->cap = 0;
+}
+// The next call's slot: its buffers become d_cq .. d_order.
+void use_next_slot(kmx_lcd* h) {
+  h->cur ^= 1;
+  const kmx_lcd::Slot& sl = h->slot[h->cur];
+  h->d_cq = sl.cq; h->d_cm = sl.cm; h->d_K = sl.K; h->d_hyps = sl.hyps; h->d_nrec = sl.nrec; h->d_order = sl.order;
+  h->d_pairs = sl.pairs; h->d_res = sl.res; h->d_mask = sl.mask; h->d_prior = sl.prior;
 }
 void lcd_free_pairs(kmx_lcd* h) {
   void* p[] = {h->d_mptr, h->d_iq, h->d_im, h->d_row};
@@ -2598,23 +2627,30 @@ int ensure_tables(kmx_lcd* h) {
   return 0;
 }
 
+// Candidate buffers for n candidates in both slots, then the next call's slot.
 int ensure_cap(kmx_lcd* h, int n) {
-  if (n <= h->cap) return 0;
-  lcd_free_cand(h);
-  const int cap = std::max(n, 1024);
-  if (hipMalloc(&h->d_cq, sizeof(int) * cap) != hipSuccess || hipMalloc(&h->d_cm, sizeof(int) * cap) != hipSuccess ||
-      hipMalloc(&h->d_K, sizeof(int) * cap) != hipSuccess ||
-      hipMalloc(&h->d_pairs, sizeof(int2) * (size_t)cap * h->N) != hipSuccess ||
-      hipMalloc(&h->d_res, sizeof(kmx_lcd_result) * cap) != hipSuccess ||
-      hipMalloc(&h->d_mask, (size_t)cap * h->N) != hipSuccess ||
-      hipMalloc(&h->d_fbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::min(cap, RS_MAX_SLOTS)) != hipSuccess ||
-      hipMalloc(&h->d_next, sizeof(int)) != hipSuccess || hipMalloc(&h->d_hyps, sizeof(int) * cap) != hipSuccess ||
-      hipMalloc(&h->d_nrec, sizeof(int) * cap) != hipSuccess ||
-      hipMalloc(&h->d_prior, sizeof(double) * 12 * (size_t)cap) != hipSuccess) {
+  if (n > h->cap) {
     lcd_free_cand(h);
-    return kmx::fail(KMX_ENOMEM, "candidate buffers");
+    const int cap = std::max(n, 1024);
+    bool ok = hipMalloc(&h->d_fbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::min(cap, RS_MAX_SLOTS)) ==
+                  hipSuccess &&
+              hipMalloc(&h->d_next, sizeof(int)) == hipSuccess;
+    for (auto& sl : h->slot)
+      ok = ok && hipMalloc(&sl.cq, sizeof(int) * cap) == hipSuccess && hipMalloc(&sl.cm, sizeof(int) * cap) == hipSuccess &&
+           hipMalloc(&sl.K, sizeof(int) * cap) == hipSuccess &&
+           hipMalloc(&sl.pairs, sizeof(int2) * (size_t)cap * h->N) == hipSuccess &&
+           hipMalloc(&sl.res, sizeof(kmx_lcd_result) * cap) == hipSuccess &&
+           hipMalloc(&sl.mask, (size_t)cap * h->N) == hipSuccess && hipMalloc(&sl.hyps, sizeof(int) * cap) == hipSuccess &&
+           hipMalloc(&sl.nrec, sizeof(int) * cap) == hipSuccess &&
+           hipMalloc(&sl.prior, sizeof(double) * 12 * (size_t)cap) == hipSuccess &&
+           hipMalloc(&sl.order, sizeof(int) * cap) == hipSuccess;
+    if (!ok) {
+      lcd_free_cand(h);
+      return kmx::fail(KMX_ENOMEM, "candidate buffers");
+    }
+    h->cap = cap;
   }
-  h->cap = cap;
+  use_next_slot(h);
   return 0;
 }
 
@@ -2660,6 +2696,27 @@ PnpParams pnp_params(const kmx_lcd* h, int stages) {
   return pp;
 }
 
+// The work queue's order: candidates by match count K, largest first (a
+// counting sort in one workgroup; ties in any order — each candidate's result
+// does not depend on when it is taken). KMX_LCD_ORDER=1 (A/B).
+__global__ __launch_bounds__(1024) void k_order(const int* K, int n, int N, int* order) {
+  __shared__ int hist[MAX_FEATS + 1];
+  for (int k = threadIdx.x; k <= N; k += blockDim.x) hist[k] = 0;
+  __syncthreads();
+  for (int c = threadIdx.x; c < n; c += blockDim.x) atomicAdd(&hist[min(max(K[c], 0), N)], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // start of each K's range, largest K first
+    int acc = 0;
+    for (int k = N; k >= 0; --k) {
+      const int v = hist[k];
+      hist[k] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < n; c += blockDim.x) order[atomicAdd(&hist[min(max(K[c], 0), N)], 1)] = c;
+}
+
 // k_ransac_coop over candidates [0, n) of the (offset) candidate arrays.
 int launch_ransac(kmx_lcd* h, int n, const RsParams& rp, const short* table, int c0, bool masks) {
   // minimum waves per SIMD: Stewenius 3 (the batch's LDS, 12.6 KB per wave,
@@ -2678,10 +2735,17 @@ int launch_ransac(kmx_lcd* h, int n, const RsParams& rp, const short* table, int
   if (p.prior) p.prior += (size_t)c0 * 12;
   if (p.hyps) p.hyps += c0;
   if (p.nrec) p.nrec += c0;
+  const char* ov = std::getenv("KMX_LCD_ORDER");
+  const bool longest_first = ov && std::atoi(ov) == 1;
+  const int* order = nullptr;
+  if (longest_first && n > 1 && c0 == 0) {
+    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, h->stream, (const int*)h->d_K, n, h->N, h->d_order);
+    order = h->d_order;
+  }
   hipLaunchKernelGGL(kc, dim3(slots), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
                      (const double*)h->d_pts, h->N, (const int*)h->d_cq + c0, (const int*)h->d_cm + c0,
                      (const int2*)h->d_pairs + (size_t)c0 * h->N, (const int*)h->d_K + c0, table, p, h->d_res + c0,
-                     masks ? h->d_mask + (size_t)c0 * h->N : nullptr, h->d_fbuf, n, h->d_next);
+                     masks ? h->d_mask + (size_t)c0 * h->N : nullptr, h->d_fbuf, n, h->d_next, order);
   return 0;
 }
 int launch_recover(kmx_lcd* h, int n, const PnpParams& pp, const short* table, int c0) {
@@ -2764,23 +2828,48 @@ int enqueue_ransac(kmx_lcd* h, int n, int stages, bool want_masks) {
   return 0;
 }
 
+// The side stream may write the current slot once the last RANSAC that read it
+// (two calls back) is done; the candidate uploads then go on it.
+int slot_upload(kmx_lcd* h, int n, const int32_t* cq, const int32_t* cm) {
+  const int s = h->cur;
+  if (h->ev_rs_set[s]) KMX_HIP(hipStreamWaitEvent(h->kstream, h->ev_rs[s], 0));
+  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->kstream));
+  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->kstream));
+  return 0;
+}
+// kNN2 of the current slot on the side stream, the RANSAC on the handle's
+// stream behind it: a call's kNN2 runs in the previous call's RANSAC tail
+// (the work-queue RANSAC holds every wave slot until its queue drains, so the
+// kNN2 workgroups start as its last waves leave), off the critical path.
 int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   if (n == 0) return 0;
+  const int s = h->cur;
   const size_t knn_smem = (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1);
   if (h->timing) {
     if (!h->ev_ok) {
       for (auto& e : h->ev) KMX_HIP(hipEventCreate(&e));
       h->ev_ok = true;
     }
-    KMX_HIP(hipEventRecord(h->ev[0], h->stream));
+    KMX_HIP(hipEventRecord(h->ev[0], h->kstream));
   }
-  hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), knn_smem, h->stream, (const uint32_t*)h->d_desc,
+  hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), knn_smem, h->kstream, (const uint32_t*)h->d_desc,
                      (const int*)h->d_nfeat, h->N, (const int*)h->d_cq, (const int*)h->d_cm, h->P.norm,
                      h->P.lowe_ratio, h->d_pairs, h->d_K);
-  if (h->timing) KMX_HIP(hipEventRecord(h->ev[1], h->stream));
+  if (h->timing) KMX_HIP(hipEventRecord(h->ev[1], h->kstream));
+  KMX_HIP(hipEventRecord(h->ev_knn[s], h->kstream));
+  KMX_HIP(hipStreamWaitEvent(h->stream, h->ev_knn[s], 0));
   if (int rc = enqueue_ransac(h, n, KMX_LCD_STAGE_2D2D | KMX_LCD_STAGE_RECOVER, want_masks)) return rc;
   if (h->timing) KMX_HIP(hipEventRecord(h->ev[2], h->stream));
+  KMX_HIP(hipEventRecord(h->ev_rs[s], h->stream));
+  h->ev_rs_set[s] = true;
   KMX_HIP(hipGetLastError());
+  return 0;
+}
+// Calls that work on the current slot from the handle's stream only (match,
+// verify_matches): they end with its RANSAC-done event too.
+int mark_slot(kmx_lcd* h) {
+  KMX_HIP(hipEventRecord(h->ev_rs[h->cur], h->stream));
+  h->ev_rs_set[h->cur] = true;
   return 0;
 }
 
@@ -2859,6 +2948,14 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
     return kmx::fail(KMX_EHIP, "hipStreamCreate");
   }
   h->own_stream = true;
+  bool ok = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; i < 2 && ok; ++i)
+    ok = hipEventCreateWithFlags(&h->ev_knn[i], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&h->ev_rs[i], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    kmx_lcd_destroy(h);
+    return kmx::fail(KMX_EHIP, "hipStreamCreate / hipEventCreate");
+  }
   if (const char* v = std::getenv("KMX_RS_PROF")) h->prof = std::atoi(v);
   *out = h;
   return KMX_OK;
@@ -2869,12 +2966,18 @@ extern "C" int kmx_lcd_destroy(kmx_lcd* h) {
   if (!h) return KMX_OK;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->kstream) (void)hipStreamSynchronize(h->kstream);
   lcd_free_frames(h);
   lcd_free_tables(h);
   lcd_free_cand(h);
   lcd_free_pairs(h);
   if (h->ev_ok)
     for (auto e : h->ev) (void)hipEventDestroy(e);
+  for (int i = 0; i < 2; ++i) {
+    if (h->ev_knn[i]) (void)hipEventDestroy(h->ev_knn[i]);
+    if (h->ev_rs[i]) (void)hipEventDestroy(h->ev_rs[i]);
+  }
+  if (h->kstream) (void)hipStreamDestroy(h->kstream);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return KMX_OK;
@@ -2884,10 +2987,9 @@ extern "C" int kmx_lcd_set_stream(kmx_lcd* h, void* s) {
   KMX_GUARD_BEGIN
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
-  if (h->own_stream && h->stream) {
-    KMX_HIP(hipStreamSynchronize(h->stream));
-    KMX_HIP(hipStreamDestroy(h->stream));
-  }
+  if (h->kstream) KMX_HIP(hipStreamSynchronize(h->kstream));
+  if (h->stream) KMX_HIP(hipStreamSynchronize(h->stream));
+  if (h->own_stream && h->stream) KMX_HIP(hipStreamDestroy(h->stream));
   h->own_stream = false;
   h->stream = reinterpret_cast<hipStream_t>(s);
   return KMX_OK;
@@ -2962,8 +3064,7 @@ extern "C" int kmx_lcd_verify(kmx_lcd* h, int32_t n, const int32_t* cq, const in
   KMX_CHECK(results || n == 0, KMX_EINVAL, "null results");
   KMX_HIP(hipSetDevice(h->device));
   if (int rc = ensure_cap(h, n)) return rc;
-  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
-  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  if (int rc = slot_upload(h, n, cq, cm)) return rc;
   if (int rc = enqueue_verify(h, n, inlier_masks != nullptr)) return rc;
   if (n) KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, h->stream));
   if (n && inlier_masks)
@@ -2978,9 +3079,8 @@ extern "C" int kmx_lcd_verify_async(kmx_lcd* h, int32_t n, const int32_t* cq, co
   if (int rc = check_cands(h, n, cq, cm)) return rc;
   KMX_HIP(hipSetDevice(h->device));
   if (int rc = ensure_cap(h, n)) return rc;
-  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
-  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
-  KMX_HIP(hipStreamSynchronize(h->stream));  // host arrays may go away after return
+  if (int rc = slot_upload(h, n, cq, cm)) return rc;
+  KMX_HIP(hipStreamSynchronize(h->kstream));  // host arrays may go away after return
   return enqueue_verify(h, n, false);
   KMX_GUARD_END
 }
@@ -3001,6 +3101,7 @@ extern "C" int kmx_lcd_match(kmx_lcd* h, int32_t n, const int32_t* cq, const int
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipMemcpyAsync(pairs_out, h->d_pairs, sizeof(int2) * (size_t)n * h->N, hipMemcpyDeviceToHost, h->stream));
   KMX_HIP(hipMemcpyAsync(k_out, h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
+  if (int rc = mark_slot(h)) return rc;
   KMX_HIP(hipStreamSynchronize(h->stream));
   return KMX_OK;
   KMX_GUARD_END
@@ -3064,6 +3165,7 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
   KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, h->stream));
   if (inlier_masks)
     KMX_HIP(hipMemcpyAsync(inlier_masks, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, h->stream));
+  if (int rc = mark_slot(h)) return rc;
   KMX_HIP(hipStreamSynchronize(h->stream));
   return KMX_OK;
   KMX_GUARD_END
@@ -3079,6 +3181,7 @@ extern "C" int kmx_lcd_read_timing(kmx_lcd* h, double* knn_ms, double* ransac_ms
   KMX_CHECK(h && knn_ms && ransac_ms, KMX_EINVAL, "null argument");
   KMX_CHECK(h->ev_ok, KMX_ESTATE, "no evented verification yet (kmx_lcd_enable_timing)");
   KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->kstream));
   KMX_HIP(hipStreamSynchronize(h->stream));
   float a = 0.f, b = 0.f;
   KMX_HIP(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
@@ -3091,6 +3194,7 @@ extern "C" int kmx_lcd_read_timing(kmx_lcd* h, double* knn_ms, double* ransac_ms
 extern "C" int kmx_lcd_sync(kmx_lcd* h) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
+  KMX_HIP(hipStreamSynchronize(h->kstream));
   KMX_HIP(hipStreamSynchronize(h->stream));
   return KMX_OK;
 }

@@ -8,6 +8,7 @@
 #   bench:ARGS   python bench.py ARGS (commas = spaces)-> TAG/bench_<n>.json
 #   prof         rocprofv3 --kernel-trace --stats of the default bench -> TAG/prof/
 #   py:SCRIPT    python SCRIPT (commas = spaces)       -> TAG/py_<n>.log
+#   env:VAR=VAL:ARGS  bench.py ARGS under VAR=VAL       -> TAG/bench_<n>.json
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -39,6 +40,11 @@ for step in "$@"; do
       timeout -k 10 600 python bench.py ${args//,/ } > "$O/bench_$n.json" 2> "$O/bench_$n.err" \
         || { echo "bench $args failed"; tail -20 "$O/bench_$n.err"; exit 1; }
       python scripts/bench_summary.py "$O/bench_$n.json" ;;
+    env:*)  # env:VAR=VAL:bench-args (commas = spaces): bench.py under one environment setting
+      rest=${step#env:}; kv=${rest%%:*}; args=${rest#*:}
+      env "$kv" timeout -k 10 600 python bench.py ${args//,/ } > "$O/bench_$n.json" 2> "$O/bench_$n.err" \
+        || { echo "bench $kv $args failed"; tail -20 "$O/bench_$n.err"; exit 1; }
+      echo -n "$kv: "; python scripts/bench_summary.py "$O/bench_$n.json" ;;
     prof)
       mkdir -p "$O/prof"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py \

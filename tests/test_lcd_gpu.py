@@ -120,3 +120,21 @@ def test_degenerate_samples_skip_like_the_serial_loop(gpu, algo, max_iter, frame
     if frames == "both":
         assert got[0]["iterations_2d2d"] == 0
     assert got[2]["accepted"]
+
+
+@pytest.mark.parametrize("algo", [0, 1], ids=["stewenius", "nister"])
+def test_longest_first_queue_is_bit_exact(gpu, monkeypatch, algo):
+    """KMX_LCD_ORDER=1: the RANSAC work queue takes candidates by match count,
+    largest first (k_order); each candidate's result is independent of when
+    it is taken, so results and masks equal the index-order queue's."""
+    pool = make_lcd_pool(40, 300, seed=17)
+    p = LcdParams(ransac_2d2d_algorithm=algo)
+    det = LoopClosureDetector(p)
+    det.set_pool(pool)
+    monkeypatch.delenv("KMX_LCD_ORDER", raising=False)
+    a, am = det.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    monkeypatch.setenv("KMX_LCD_ORDER", "1")
+    b, bm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    assert np.array_equal(am, bm)
+    for x, y in zip(a, b):
+        assert all(np.array_equal(x[k], y[k]) for k in x)
