@@ -243,6 +243,13 @@ def ransac_roofline(algo, n_cand, tk):
                                 "wave instruction, 2 per FMA, whatever the exec mask)",
                 "fp64_share_of_valu_insts": d["fractions"]["fp64_share_of_valu_insts"],
                 "valu_active_over_wave_cycles": d["fractions"]["valu_active_over_wave_cycles"]})
+    lanes = d.get("lanes") or {}
+    if lanes.get("valu_thread_util") is not None:
+        # exec-mask aware: the share of lanes active in the VALU's active cycles
+        # (SQ_THREAD_CYCLES_VALU / 64 SQ_ACTIVE_INST_VALU) applied to the issued figure
+        u = lanes["valu_thread_util"]
+        out.update({"valu_thread_util": u, "achieved_useful": ach * u, "frac_useful": ach * u / PEAK_FP64,
+                    "useful_rule": "issued fp64 lane-flops x VALU thread utilisation (stored PMC ratio)"})
     return out
 
 

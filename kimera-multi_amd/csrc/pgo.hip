@@ -39,6 +39,7 @@
 #include <chrono>
 #include <thread>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -2951,6 +2952,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   h->rt0_h = rt0;
   h->ntiles = (int)tr.size();
   KMX_CHECK(h->ntiles > 0, KMX_EINVAL, "no local poses");
+  if (std::getenv("KMX_TILE_CAP"))  // A/B sweeps (scripts/gpu_tile_sweep.sh) log the cut they ran
+    std::fprintf(stderr, "kmx: %d tiles at %lld incidences per tile (cap)\n", h->ntiles, (long long)tilecap);
   std::vector<int> own_src(std::max<int64_t>(h->n_owned, 1), 0);
   for (int64_t k = 0; k < h->n_owned; ++k) own_src[k] = pub_src[h->first_owned + k];
   std::vector<int> nrob(L);

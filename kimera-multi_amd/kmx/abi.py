@@ -209,11 +209,17 @@ def lib() -> C.CDLL:
         "kmx_bow_sync": ([P], C.c_int),
         "kmx_bow_score_pairs": ([P, i32, pi64, pu32, pf64, pi64, pu32, pf64, pf64], C.c_int),
     })
+    # KMX_AB_OLDLIB=1 (same-box A/B against an earlier build given by KMX_LIB
+    # only): entry points the older library lacks are skipped and its ABI
+    # version is accepted; the calls an A/B makes must exist in both
+    old_ok = os.environ.get("KMX_AB_OLDLIB") == "1" and "KMX_LIB" in os.environ
     for name, (argt, rest) in sig.items():
+        if old_ok and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.argtypes = argt
         fn.restype = rest
-    if L.kmx_abi_version() != ABI_VERSION:
+    if L.kmx_abi_version() != ABI_VERSION and not old_ok:
         raise KmxError(f"{path} implements ABI {L.kmx_abi_version()}, this binding needs {ABI_VERSION}: rebuild it")
     _lib = L
     return L

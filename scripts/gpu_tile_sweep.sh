@@ -11,6 +11,7 @@ for cap in "$@"; do
   if [ "$cap" = default ]; then unset KMX_TILE_CAP; else export KMX_TILE_CAP=$cap; fi
   timeout -k 10 300 python bench.py --no-cpu --no-lcd --steps 200 > gpurun_out/$T/cap_$cap.json 2> gpurun_out/$T/cap_$cap.err \
     || { echo "cap $cap failed"; tail -5 gpurun_out/$T/cap_$cap.err; exit 1; }
+  grep -h "tiles at" gpurun_out/$T/cap_$cap.err | head -1 | tee -a gpurun_out/$T/summary.txt
   python3 - "$T" "$cap" <<'PY' | tee -a gpurun_out/$T/summary.txt
 import json, sys
 t, cap = sys.argv[1], sys.argv[2]

@@ -46,6 +46,17 @@ res = {
         "salu_insts": vals["SQ_INSTS_SALU"] / cand,
         "vmem_rd_insts": vals["SQ_INSTS_VMEM_RD"] / cand,
     },
+    # exec-mask-aware: SQ_THREAD_CYCLES_VALU counts active
+    # lanes per VALU cycle; over 64 x SQ_ACTIVE_INST_VALU it is the share of
+    # lanes doing work in the VALU's active cycles. SQ_INSTS_VALU_FLOPS_FP64
+    # is the hardware's own fp64 FLOP count (compared with the issued figure
+    # above: equal means it ignores the exec mask, lower means it counts lanes)
+    "lanes": {
+        "valu_thread_util": vals["SQ_THREAD_CYCLES_VALU"] / max(64.0 * vals["SQ_ACTIVE_INST_VALU"], 1.0)
+        if "SQ_THREAD_CYCLES_VALU" in vals else None,
+        "fp64_flops_counter_per_candidate": (vals["SQ_INSTS_VALU_FLOPS_FP64"] + vals.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0))
+        / cand if "SQ_INSTS_VALU_FLOPS_FP64" in vals else None,
+    },
     "fractions": {
         "fp64_share_of_valu_insts": sum(f64.values()) / max(vals["SQ_INSTS_VALU"], 1.0),
         "valu_active_over_wave_cycles": vals["SQ_ACTIVE_INST_VALU"] / max(vals["SQ_WAVE_CYCLES"], 1.0),
@@ -60,4 +71,6 @@ res = {
             "78.6 TFLOP/s fp64 vector peak (a stored PMC ratio, labelled as such in the JSON)",
 }
 json.dump(res, open(out, "w"), indent=1)
-print(json.dumps({k: res[k] for k in ("candidates_counted", "per_candidate", "fractions")}, indent=1))
+if res["lanes"]["valu_thread_util"] is not None:
+    res["per_candidate"]["fp64_useful_flops"] = res["per_candidate"]["fp64_issued_flops"] * res["lanes"]["valu_thread_util"]
+print(json.dumps({k: res[k] for k in ("candidates_counted", "per_candidate", "lanes", "fractions")}, indent=1))

@@ -20,3 +20,11 @@ for rep in range(2):
           f"{np.mean([r['iterations_2d2d'] for r in res[1::2]]):.1f} (false), mean K "
           f"{np.mean([r['n_matches'] for r in res[0::2]]):.0f} / {np.mean([r['n_matches'] for r in res[1::2]]):.0f}",
           flush=True)
+# back-to-back calls (the bench's LCD steps): a call's kNN2 can fill the
+# previous call's RANSAC tail
+t = time.time()
+for _ in range(4):
+    det.verify_async(pool.cand_query, pool.cand_match)
+det.sync()
+el4 = time.time() - t
+print(f"back-to-back x4: {4 * n / el4:.0f} cand/s ({el4 * 1e3 / 4:.1f} ms per call)", flush=True)

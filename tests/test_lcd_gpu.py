@@ -138,3 +138,27 @@ def test_longest_first_queue_is_bit_exact(gpu, monkeypatch, algo):
     assert np.array_equal(am, bm)
     for x, y in zip(a, b):
         assert all(np.array_equal(x[k], y[k]) for k in x)
+
+
+def test_back_to_back_calls_overlap_safely(gpu):
+    """Alternate calls use two candidate slots and a call's kNN2 runs on a side
+    stream while the previous call's RANSAC drains: back-to-back async calls,
+    a call that grows the buffers while another is in flight, and the
+    synchronous results after them equal a fresh detector's."""
+    pool = make_lcd_pool(64, 200, seed=23)
+    p = LcdParams()
+    ref = LoopClosureDetector(p)
+    ref.set_pool(pool)
+    want, wm = ref.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    det = LoopClosureDetector(p)
+    det.set_pool(pool)
+    rng = np.random.default_rng(0)
+    for _ in range(3):
+        sel = rng.permutation(pool.cand_query.shape[0])[:20]
+        det.verify_async(pool.cand_query[sel], pool.cand_match[sel])
+    det.verify_async(np.tile(pool.cand_query, 40), np.tile(pool.cand_match, 40))  # > 1024: regrows in flight
+    got, gm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    det.sync()
+    assert np.array_equal(gm, wm)
+    for g, w in zip(got, want):
+        assert all(np.array_equal(g[k], w[k]) for k in g)
