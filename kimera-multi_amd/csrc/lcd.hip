@@ -2510,6 +2510,8 @@ struct kmx_lcd {
 namespace {
 
 void lcd_free_frames(kmx_lcd* h) {
+  if (h->stream) (void)hipStreamSynchronize(h->stream);  // a verification in flight may read the pool
+  if (h->kstream) (void)hipStreamSynchronize(h->kstream);
   void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat};
   for (void* x : p)
     if (x) (void)hipFree(x);
@@ -2888,6 +2890,7 @@ int grow_pool(kmx_lcd* h, int need) {
       if (x) (void)hipFree(x);
     return kmx::fail(KMX_ENOMEM, "frame pool");
   }
+  KMX_HIP(hipStreamSynchronize(h->kstream));  // a kNN2 in flight may read the old pool
   if (h->F) {
     KMX_HIP(hipMemcpyAsync(desc, h->d_desc, old * 32, hipMemcpyDeviceToDevice, h->stream));
     KMX_HIP(hipMemcpyAsync(bear, h->d_bear, old * 3 * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
