@@ -2723,9 +2723,15 @@ __global__ __launch_bounds__(1024) void k_order(const int* K, int n, int N, int*
 int launch_ransac(kmx_lcd* h, int n, const RsParams& rp, const short* table, int c0, bool masks) {
   // minimum waves per SIMD: Stewenius 3 (the batch's LDS, 12.6 KB per wave,
   // admits 12 waves per CU; 168 VGPRs), Nister 4 — the measured best register
-  // budgets (the other budgets lost their A/B and were removed)
+  // budgets. The <2, true> and <3, false> instantiations are compiled but never
+  // launched: with them in the module the backend's code for the launched
+  // <3, true> spills 118 VGPRs (412 B scratch per lane) instead of 396 (972 B)
+  // — same source, every callee inlined in both builds, a different inlining
+  // order (measured with -Rpass-analysis=kernel-resource-usage, round 4; the
+  // RANSAC step took ~11 % longer without them).
   const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
   auto kc = stew ? k_ransac_coop<3, true> : k_ransac_coop<4, false>;
+  if (rp.pmax < 0) kc = stew ? k_ransac_coop<2, true> : k_ransac_coop<3, false>;  // never: keeps them compiled
   // one wave per resident slot (<= RS_MAX_SLOTS: the scratch is sized for it)
   int per_cu = 0, dev = 0, cus = 0;
   KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kc, RS_BLOCK, 0));
