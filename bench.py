@@ -325,7 +325,8 @@ def stream_leg(det, pool, cq, cm, args):
     device-to-device copy, included); (b) geometricVerificationNister +
     recoverPose on caller-supplied correspondences (kmx_lcd_verify_matches,
     both stages, no kNN2) over the step's candidates with the kNN2 pairs as
-    input — host CSR upload included, as a caller would pay it."""
+    input in CSR form — host argument checks and the CSR upload included, as a
+    caller would pay them."""
     n_add = 1000
     src = np.arange(n_add) % pool.n_frames
     ts = []
@@ -343,10 +344,13 @@ def stream_leg(det, pool, cq, cm, args):
            "note": "one kmx_lcd_add_frames call per frame from pageable host memory; the first call doubles the "
                    "resident pool (device-to-device copy)"}
     pairs, k = det.match(cq, cm)
-    corr = [(pairs[i, :k[i], 0], pairs[i, :k[i], 1]) for i in range(len(cq))]
-    det.verify_matches(cq[:64], cm[:64], corr[:64])  # warmup
+    mptr = np.zeros(len(cq) + 1, np.int64)
+    mptr[1:] = np.cumsum(k)
+    sel = np.arange(pairs.shape[1])[None, :] < k[:, None]
+    iq, im = pairs[:, :, 0][sel], pairs[:, :, 1][sel]  # the kNN2 pairs as CSR, candidate order
+    det.verify_matches_csr(cq[:64], cm[:64], mptr[:65], iq, im)  # warmup
     a = time.perf_counter()
-    res, _ = det.verify_matches(cq, cm, corr, stages=3)
+    res, _ = det.verify_matches_csr(cq, cm, mptr, iq, im, stages=3)
     el2 = time.perf_counter() - a
     out["verify_matches"] = {"metric": "LC candidates verified/sec (caller-supplied correspondences, both stages)",
                              "value": len(cq) / el2, "n": int(len(cq)), "elapsed": el2,

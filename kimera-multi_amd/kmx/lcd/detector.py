@@ -377,9 +377,7 @@ class LoopClosureDetector:
         abi.KMX_LCD_STAGE_2D2D / _RECOVER; T_prior [n, 12] (R row-major, t) is
         the rotation source of the 1-point recovery without the 2D-2D stage.
         Returns (results, masks) as verify, masks indexed by pair position."""
-        cq = np.ascontiguousarray(cand_query, dtype=np.int32)
-        cm = np.ascontiguousarray(cand_match, dtype=np.int32)
-        n = cq.shape[0]
+        n = len(cand_query)
         if len(correspondences) != n:
             raise ValueError("one (i_query, i_match) pair list per candidate")
         lens = [len(np.asarray(a)) for a, _ in correspondences]
@@ -388,10 +386,25 @@ class LoopClosureDetector:
                 raise ValueError("i_query and i_match differ in length")
         mptr = np.zeros(n + 1, np.int64)
         mptr[1:] = np.cumsum(lens)
-        iq = np.ascontiguousarray(np.concatenate([np.asarray(a, np.int32) for a, _ in correspondences])
-                                  if n else np.zeros(0, np.int32), np.int32)
-        im = np.ascontiguousarray(np.concatenate([np.asarray(b, np.int32) for _, b in correspondences])
-                                  if n else np.zeros(0, np.int32), np.int32)
+        iq = np.concatenate([np.asarray(a, np.int32) for a, _ in correspondences]) if n else np.zeros(0, np.int32)
+        im = np.concatenate([np.asarray(b, np.int32) for _, b in correspondences]) if n else np.zeros(0, np.int32)
+        return self.verify_matches_csr(cand_query, cand_match, mptr, iq, im, stages, T_prior, with_masks)
+
+    def verify_matches_csr(self, cand_query, cand_match, mptr, i_query, i_match, stages: int = 3, T_prior=None,
+                           with_masks: bool = False):
+        """verify_matches with the correspondences already in CSR form: candidate
+        i's pairs are (i_query[k], i_match[k]) for k in [mptr[i], mptr[i+1])
+        (kmx_lcd_verify_matches' own layout; no per-candidate Python lists)."""
+        cq = np.ascontiguousarray(cand_query, dtype=np.int32)
+        cm = np.ascontiguousarray(cand_match, dtype=np.int32)
+        n = cq.shape[0]
+        mptr = np.ascontiguousarray(mptr, np.int64)
+        if mptr.shape != (n + 1,):
+            raise ValueError("mptr must have n_cand + 1 entries")
+        iq = np.ascontiguousarray(i_query, np.int32)
+        im = np.ascontiguousarray(i_match, np.int32)
+        if iq.shape != im.shape:
+            raise ValueError("i_query and i_match differ in length")
         if iq.size == 0:
             iq = np.zeros(1, np.int32)
             im = np.zeros(1, np.int32)
