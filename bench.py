@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--no-lcd", action="store_true")
     ap.add_argument("--no-replay", action="store_true", help="skip the evented replay (roofline)")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3: timed rounds only")
+    ap.add_argument("--tcg-form", choices=["standard", "onesync"], default="standard",
+                    help="tCG form (kmx_pgo_params.tcg_form): ROPTLIB's, or the opt-in one-sync form")
     ap.add_argument("--lcd-frames", type=int, default=50_000)
     ap.add_argument("--lcd-steps", type=int, default=3)
     ap.add_argument("--lcd-algo", type=int, default=0,
@@ -583,6 +585,7 @@ def main():
             torch.cuda.synchronize()
 
     P = params()
+    P.localOptimizationParams.tCG_form = args.tcg_form
     headline = args.scaling if world > 1 else "strong"
     t_gen = time.perf_counter()
     g, X0 = make_workload(args.config, world, headline)
@@ -628,7 +631,7 @@ def main():
         "config": {
             "workload": workload,
             "robots": g.n_robots, "poses": g.n_total, "edges": g.m, "r": P.r,
-            "rtr_iterations": 1, "tcg_max": 10, "schedule": "concurrent",
+            "rtr_iterations": 1, "tcg_max": 10, "schedule": "concurrent", "tcg_form": args.tcg_form,
             "timed_rounds": [w0, w0 + args.steps] if not args.profile else [0, args.steps],
             "burn_in_rounds": 0 if args.profile else args.burn_in,
             "parallelism": f"robot blocks {g.n_robots} over {world} GPU(s)"
@@ -653,7 +656,8 @@ def main():
     out["work"]["edges_hessvecs_per_s"] = value * out["work"]["hessvecs_per_block_update"]
     if hv_n:
         out["roofline"] = {
-            "kernel": "k_hess (tCG Hessian-vector product)",
+            "kernel": ("k_hess (tCG Hessian-vector product)" if args.tcg_form == "standard" else
+                       "k_step (one-sync tCG step: update + Hessian-vector product)"),
             "bound": "hbm",
             "achieved": achieved / 1e9,
             "peak": PEAK_HBM / 1e9,

@@ -88,7 +88,11 @@ typedef struct kmx_pgo_params {
                                schedule only: every local robot updates every round      */
   int restart_interval;     /* acceleration restart period in rounds (30)               */
   int method;               /* KMX_METHOD_RTR (0) or KMX_METHOD_RGD (1)                  */
-  int reserved0;
+  int tcg_form;             /* KMX_TCG_FORM_STANDARD (0): ROPTLIB's tCG, two dependent
+                               reductions per step; KMX_TCG_FORM_ONESYNC (1): opt-in, one
+                               reduction and one kernel per step, the
+                               neighbours' new direction formed from gathered z, M^-1 H delta
+                               and delta; parity with the standard form at convergence only */
   double rgd_stepsize;      /* RGD: X <- Retr_X(-s * precon(grad f)) (1e-3)              */
   int tile_incidences;      /* incidences per workgroup tile (0: from the handle's local
                                problem, 180..2 chunks; the tile cut orders the per-robot
@@ -113,6 +117,9 @@ typedef struct kmx_iter_stats {
   int64_t edges;        /* edges in the block's local problem (metric unit)    */
   int64_t hessvecs;     /* Hessian-vector products evaluated                   */
 } kmx_iter_stats;
+
+#define KMX_TCG_FORM_STANDARD 0
+#define KMX_TCG_FORM_ONESYNC 1
 
 #define KMX_TCG_NONE 0
 #define KMX_TCG_NEGATIVE_CURVATURE 1
@@ -259,6 +266,13 @@ int kmx_pgo_sync(kmx_pgo* h);
  * drained after timeout_s (a round's exchange waiting on a peer that failed);
  * kmx_pgo_comm_destroy then aborts the communicator, which releases it. */
 int kmx_pgo_sync_timeout(kmx_pgo* h, double timeout_s);
+
+/* Diagnostic (no reference counterpart): the phase stamps of the one-sync tCG
+ * kernel in a KMX_STEP_STAMPS build (`make -C kimera-multi_amd/csrc stamps`):
+ * per tile 16 words — 7 wall-clock stamps (100 MHz; pgo.hip body_step), -,
+ * poses, incidences, block index, first tile of its robot — of the last launch
+ * that formed step 2. KMX_EUNSUP otherwise. */
+int kmx_pgo_debug_step_stamps(uint64_t* out, int64_t n);
 
 /* GNC: `updateMeasurementWeights()` (drawio:2215) for every non-fixed edge with
  * a local endpoint, evaluated at the current iterate and neighbour table, then

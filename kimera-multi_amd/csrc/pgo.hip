@@ -135,13 +135,16 @@ struct Params {
   int early_stop;   // RM_CONSUMER k_hess: the stop decision before the gather (else after)
 };
 
-// One tile's description, read by a single 16-B scalar load at the start of
+// One tile's description, read by a single 32-B scalar load at the start of
 // every tile kernel: its robot, its first pose, its incidence range start
 // inc_ptr[p0] and, packed, its pose count np (< 256) and incidence count
 // n = inc_ptr[p0 + np] - inc_ptr[p0] (np | n << 8), so the record loads do not
-// wait for an inc_ptr lookup.
+// wait for an inc_ptr lookup; and its robot's tile range, so the consumer
+// kernels' robot sums do not wait for an rtile0 lookup.
 struct alignas(16) TileDesc {
   int robot, p0, k0, np_n;
+  int rt0, rt1;  // the robot's tile range: the consumer kernels' robot sums start from it
+  int pad0, pad1;
 };
 
 struct Dev {
@@ -183,6 +186,11 @@ struct Dev {
   int n_gnc;
   int* hv_launch;             // [HV_SLOTS] robots that ran a Hess-vec in timed launch k
   Params p;
+  // one-sync tCG (P.tcg_form, body_step): H z_k, and w_k = precon(H delta_k)
+  // double-buffered by step parity (the gathered vector), and the step's
+  // 8-wide partials
+  double *hz, *w0, *w1;
+  double* part_f;             // [ntiles][8]
 };
 
 constexpr int HV_SLOTS = 1 << 16;
@@ -196,10 +204,31 @@ constexpr int HV_SLOTS = 1 << 16;
 #endif
 constexpr int DHMAX = KMX_DHMAX;
 
+// Wave sum by DPP lane moves inside each row of 16 (xor 1, xor 2 by
+// quad_perm, then the half-row and row mirrors: every lane of a row holds the
+// row's sum, bitwise alike since each step adds the same two values), then
+// the four row sums read out as scalars and added in a fixed order: the same
+// value in every lane. (A shuffle butterfly costs 12 LDS permutes per sum: the
+// one-sync k_step's 15 sums took ~4 us of its decision and epilogue.)
+template <int CTRL>
+__device__ __forceinline__ double dpp_row(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ double read_lane(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  v += dpp_row<0xb1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_row<0x4e>(v);   // quad_perm [2,3,0,1]
+  v += dpp_row<0x141>(v);  // row_half_mirror
+  v += dpp_row<0x140>(v);  // row_mirror
+  return (read_lane(v, 0) + read_lane(v, 16)) + (read_lane(v, 32) + read_lane(v, 48));
 }
 
 // Sum over all BLOCK threads in fixed order; every thread gets the result.
@@ -463,6 +492,7 @@ __device__ __forceinline__ void group_retract(const double x[4], const double v[
 struct Lane {
   int tile, l, w, ln, pw, a, base, pose;
   int p0, np, k0, n;  // the tile's poses and incidences (TileDesc)
+  int rt0, rt1;       // the robot's tiles
   bool valid;
 };
 template <int R>
@@ -483,6 +513,8 @@ __device__ __forceinline__ Lane lane_map(const Dev& d) {
   L.np = t.np_n & 0xff;
   L.k0 = t.k0;
   L.n = t.np_n >> 8;
+  L.rt0 = t.rt0;
+  L.rt1 = t.rt1;
   L.w = threadIdx.x >> 6;
   L.ln = threadIdx.x & 63;
   L.pw = L.ln / R;
@@ -546,9 +578,11 @@ struct NoPre {
 // offsets, so the two loads overlap (the consumer form keeps the offsets
 // first: its decision in `pre` is a call, and the records live across it
 // would spill)
-template <int R, int RW, bool REC_FIRST = false, typename Pre = NoPre>
-__device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const double* V, double acc[4],
-                                            char* smem, Pre&& pre = Pre{}) {
+// DIAG = false: the caller applies the diagonal block itself (k_step, whose
+// epilogue loads the own row and D_i with the rest of its rows in one batch).
+template <int R, int RW, bool REC_FIRST, typename Src, typename Pre, bool DIAG = true>
+__device__ __forceinline__ bool hinc_gather_src(const Dev& d, const Lane& L, Src& src, double acc[4], char* smem,
+                                                Pre&& pre) {
   using SM = SmemH<R>;
   using RC = Rec<RW>;
   constexpr int CH = SM::CH;
@@ -574,16 +608,8 @@ __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const d
     const int2 in = RC::inc(q);
     const int o = in.x;
     const bool tail = (in.y >> 31) & 1;
-    const double2* b2 = reinterpret_cast<const double2*>(V + (size_t)max(o, 0) * 4 * R);
     double2 vr[2 * R];
-#if KMX_HESS_PROBE & 1  // traffic attribution build: no neighbour rows
-#pragma unroll
-    for (int i = 0; i < 2 * R; ++i) vr[i] = make_double2(1e-3 * i, 1e-3);
-    (void)b2;
-#else
-#pragma unroll
-    for (int i = 0; i < 2 * R; ++i) vr[i] = b2[i];
-#endif
+    src.nbr(o, vr);
     if (tid < CH && c0 + tid < n) {
       const double wk = (o >= 0) ? E.wk : 0.0, wt = (o >= 0) ? E.wt : 0.0;
 #pragma unroll
@@ -619,14 +645,13 @@ __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const d
     }
     lds_barrier();
   }
-  if (L.valid) {
+  if (DIAG && L.valid) {
     double vs[4];
     double D[16];
-#if KMX_HESS_PROBE & 2  // traffic attribution build: no own-row / diagonal-block loads
-    for (int c = 0; c < 4; ++c) vs[c] = 1e-3 * c;
+    src.own(L.pose, L.a, vs);
+#if KMX_HESS_PROBE & 2  // traffic attribution build: no diagonal-block loads
     for (int c = 0; c < 16; ++c) D[c] = (c % 5 == 0) ? 1.0 : 0.0;
 #else
-    load4(V + (size_t)L.pose * 4 * R + 4 * L.a, vs);
     load_sym4(d.hD + SYM4 * (size_t)L.pose, D);
 #endif
 #pragma unroll
@@ -634,6 +659,39 @@ __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const d
       acc[c] += vs[0] * D[4 * c] + vs[1] * D[4 * c + 1] + vs[2] * D[4 * c + 2] + vs[3] * D[4 * c + 3];
   }
   return true;
+}
+
+// Where the gathered rows come from: a stored vector (the rows of the
+// traffic-attribution builds replaced by constants).
+template <int R>
+struct PlainRows {
+  const double* V;
+  // the other endpoint's whole r x 4 row (o < 0, a public neighbour: any row; its weight is zeroed)
+  __device__ __forceinline__ void nbr(int o, double2 vr[2 * R]) const {
+    const double2* b2 = reinterpret_cast<const double2*>(V + (size_t)max(o, 0) * 4 * R);
+#if KMX_HESS_PROBE & 1  // traffic attribution build: no neighbour rows
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) vr[i] = make_double2(1e-3 * i, 1e-3);
+    (void)b2;
+#else
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) vr[i] = b2[i];
+#endif
+  }
+  // row a of the lane's own pose
+  __device__ __forceinline__ void own(int pose, int a, double vs[4]) {
+#if KMX_HESS_PROBE & 2  // traffic attribution build: no own-row loads
+    for (int c = 0; c < 4; ++c) vs[c] = 1e-3 * c;
+#else
+    load4(V + (size_t)pose * 4 * R + 4 * a, vs);
+#endif
+  }
+};
+template <int R, int RW, bool REC_FIRST = false, typename Pre = NoPre>
+__device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const double* V, double acc[4],
+                                            char* smem, Pre&& pre = Pre{}) {
+  PlainRows<R> src{V};
+  return hinc_gather_src<R, RW, REC_FIRST>(d, L, src, acc, smem, pre);
 }
 
 // Gradient and cost, incidence-parallel. A lane evaluates its whole incidence
@@ -1047,20 +1105,21 @@ __device__ __forceinline__ void robot_sum(const double* part, int stride, int t0
 }
 
 // robot_sum in two halves, so the partial loads can be in flight during other
-// work: issue() loads a robot's <= 2 * RBLOCK tiles into registers (larger
+// work: issue() loads a robot's <= U * RBLOCK tiles into registers (larger
 // robots fall back to robot_sum in finish()); finish() adds them in
-// robot_sum's order.
+// robot_sum's order (a thread's tiles in tile order, then the wave sums and
+// the waves in order: the same sums for any U).
 // NS <= 2: 2-wide partials (part_h / part_u); NS = 3, 4: d.part (stride NPART).
-template <int NS>
+template <int NS, int U = 2>
 struct RobotSum {
-  double a[2][NS];
+  double a[U][NS];
   int t0, t1;
   __device__ __forceinline__ void issue(const double* part, int stride, int t0_, int t1_) {
     t0 = t0_;
     t1 = t1_;
-    if (t1 - t0 > 2 * RBLOCK) return;
+    if (t1 - t0 > U * RBLOCK) return;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int t = min(t0 + (int)threadIdx.x + u * RBLOCK, t1 - 1);
       const double2* p2 = reinterpret_cast<const double2*>(part + (size_t)t * stride);
       const double2 x = p2[0];
@@ -1075,7 +1134,7 @@ struct RobotSum {
   }
   __device__ __forceinline__ void finish(const double* part, int stride, double* lds, double tot[NPART]) {
     static_assert(NS <= NPART, "partials");
-    if (t1 - t0 > 2 * RBLOCK) {
+    if (t1 - t0 > U * RBLOCK) {
       robot_sum<(NS > 2 ? NPART : NS)>(part, stride, t0, t1, lds, tot);
       if constexpr (NS == 3) tot[3] = 0.0;
       return;
@@ -1085,7 +1144,7 @@ struct RobotSum {
 #pragma unroll
     for (int k = 0; k < NS; ++k) v[k] = 0.0;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < U; ++u)
       if (t0 + (int)threadIdx.x + u * RBLOCK < t1) {
 #pragma unroll
         for (int k = 0; k < NS; ++k) v[k] += a[u][k];
@@ -1303,7 +1362,7 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
     __shared__ Ctl cs;
     __shared__ double rl[NPART * WAVES];
     const Ctl& c0 = d.ctl[L.l];
-    const bool writer = L.tile == d.rtile0[L.l];
+    const bool writer = L.tile == L.rt0;
     // the writer's working copy of the state, loaded by wave 0 at the start
     // (its lane 0 reads it after these in-order LDS writes of its own wave)
     if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))
@@ -1320,10 +1379,10 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
       return;
     }
     const bool upd = !grad && c0.tcg_iter > 0;
-    RobotSum<2> rs;
+    RobotSum<2> rs;  // (four tiles per thread here: spills at 128 VGPRs)
     RobotSum<3> rg;
-    if (upd) rs.issue(d.part_u, 2, d.rtile0[L.l], d.rtile0[L.l + 1]);
-    if (grad) rg.issue(d.part, NPART, d.rtile0[L.l], d.rtile0[L.l + 1]);
+    if (upd) rs.issue(d.part_u, 2, L.rt0, L.rt1);
+    if (grad) rg.issue(d.part, NPART, L.rt0, L.rt1);
     UpdStep u{0, 0, 0.0};
     // the decision runs while the first chunk's records are in flight and
     // before any row is gathered: a robot whose tCG stops here (or whose
@@ -1450,7 +1509,7 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
     Ctl* const cin = d.ctl2;
     Ctl* const cout = d.ctl;
     const Ctl& cq = cin[L.l];
-    const bool writer = L.tile == d.rtile0[L.l];
+    const bool writer = L.tile == L.rt0;
     if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))  // as in k_hess
       reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(&cq)[threadIdx.x];
     if (cq.phase != PH_TCG) {
@@ -1458,8 +1517,8 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
       return;
     }
     const bool first0 = cq.tcg_iter == 0;  // the control step makes it 1
-    RobotSum<1> rs;
-    rs.issue(d.part_h, 2, d.rtile0[L.l], d.rtile0[L.l + 1]);
+    RobotSum<1, 4> rs;
+    rs.issue(d.part_h, 2, L.rt0, L.rt1);
     if (L.valid) {
       load4(d.hd + o, hdl);
       load4((first0 ? d.g : d.r) + o, rr);
@@ -1483,7 +1542,7 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
   } else {
     const Ctl& c = d.ctl[L.l];
     if (c.phase != PH_TCG) {  // not in tCG: the robot's first tile reports it
-      if (hs && threadIdx.x == 0 && L.tile == d.rtile0[L.l]) post_status(hs, L.l, seq, false);
+      if (hs && threadIdx.x == 0 && L.tile == L.rt0) post_status(hs, L.l, seq, false);
       return;
     }
     tcg_iter = c.tcg_iter;
@@ -1518,6 +1577,334 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
   });
 }
 
+// ------------------------------------------------ one-sync tCG (opt-in) ---
+// P.tcg_form = KMX_TCG_FORM_ONESYNC: one kernel per tCG step (k_step), so a
+// step has one grid-wide dependency instead of two (k_hess -> k_update ->
+// k_hess). Launch j applies step j-1's decision and forms step j:
+//  1. every workgroup reduces the robot's 8-wide partials of launch j-1
+//     (RobotSum8, tile order) and evaluates the decisions on them:
+//     alpha (or the boundary tau) from <delta,H delta> and <r,z>, then the
+//     stop test and beta from <r',r'> and <r',z'> formed by the recurrences
+//       <r',r'> = <r,r> + 2 alpha <r,Hd> + alpha^2 <Hd,Hd>
+//       <r',z'> = <r,z> + alpha (<r,w> + <Hd,z>) + alpha^2 <Hd,w>
+//     (w = precon(H delta), precon linear); <r,z> and <r,r> are reduced from
+//     the recurred vectors at every step, so the scalar recurrences are one
+//     step deep. The robot's first tile writes the state (cin -> cout,
+//     alternating buffers) and the host status;
+//  2. the gather applies the Hessian to w (step 0: to z_0) — one row per
+//     incidence, as k_hess — and the owner forms, by linearity,
+//       z' = z + alpha w,        Hz' = Hz + alpha Hw,
+//       delta' = -z' + beta delta,  H delta' = -Hz' + beta H delta,
+//       r' = r + coef H delta,   w' = precon(H delta')
+//     (fused multiply-adds, as the restatement), and the 7 partials.
+// A robot whose tCG stops in step 1 only updates r (k_retract's model). Only
+// w is read across tiles, so only w is double-buffered (by step parity); the
+// kept directions are d.dh as in the standard form.
+// Restated by oracle/dpgo_oracle.c tcg_onesync (same recurrences); parity
+// with the standard form at convergence only.
+__device__ __forceinline__ void onesync_scalars(double al, const double* tot, double* rrn, double* zrn) {
+#pragma clang fp contract(off)
+  *rrn = fmax(tot[2] + 2.0 * al * tot[5] + al * al * tot[6], 0.0);
+  *zrn = tot[1] + al * tot[3] + al * al * tot[4];
+}
+
+// RobotSum for the one-sync step's 8-wide partials (d.part_f), same order as
+// robot_sum: U tiles per thread in one round trip (1024 tiles, the 736-tile
+// cut of a 12.5k-pose block included), tile order within a thread, then the
+// wave sums and the waves in order; larger robots loop.
+template <int U>
+struct RobotSum8 {
+  double a[U][8];
+  int t0, t1;
+  __device__ __forceinline__ void load(const double* part, int tb) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = min(tb + (int)threadIdx.x + u * RBLOCK, t1 - 1);
+      const double2* p2 = reinterpret_cast<const double2*>(part + (size_t)t * 8);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double2 x = p2[k];
+        a[u][2 * k] = x.x;
+        a[u][2 * k + 1] = x.y;
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(const double* part, int t0_, int t1_) {
+    t0 = t0_;
+    t1 = t1_;
+    if (t1 - t0 <= U * RBLOCK) load(part, t0);
+  }
+  __device__ __forceinline__ void finish(const double* part, double* lds, double tot[8]) {
+    constexpr int RW_ = RBLOCK / 64;
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = 0.0;
+    for (int tb = t0; tb < t1; tb += U * RBLOCK) {
+      if (t1 - t0 > U * RBLOCK) load(part, tb);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (tb + (int)threadIdx.x + u * RBLOCK < t1) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += a[u][k];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const double w = wave_sum(v[k]);
+      if ((threadIdx.x & 63) == 0) lds[k * RW_ + (threadIdx.x >> 6)] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      double acc = 0.0;
+#pragma unroll
+      for (int w = 0; w < RW_; ++w) acc += lds[k * RW_ + w];
+      tot[k] = acc;
+    }
+  }
+};
+
+template <int R>
+struct SmemF {  // k_step: the Hessian gather's layout with an 8-wide reduction area
+  static constexpr int red_off = SmemH<R>::red_off;
+  static constexpr int bytes = red_off + 8 * 8 * WAVES + 16;
+};
+
+__device__ __forceinline__ double dot4(const double a[4], const double b[4]) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+}
+
+// KMX_STEP_STAMPS builds (diagnostic, `make stamps`): thread 0 of every
+// workgroup of the k_step launches that form step 2 records the wall clock
+// (100 MHz) at entry, once the robot sums' loads are issued, once they (and
+// the first records) have landed, after the decision, after the gather loop,
+// after the Hessian's own-row part and at exit (kmx_pgo_debug_step_stamps;
+// scripts/step_stamps.py).
+#ifdef KMX_STEP_STAMPS
+constexpr int STEP_STAMP_TILES = 8192;
+__device__ unsigned long long g_step_stamp[16 * STEP_STAMP_TILES];
+#define KMX_SS(i) \
+  do { if (threadIdx.x == 0) ss_[i] = wall_clock64(); } while (0)
+#else
+#define KMX_SS(i) do {} while (0)
+#endif
+
+template <int R, int RW>
+__device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cout, int slot, HostStatus* hs,
+                                          unsigned long long seq, char* smem) {
+#ifdef KMX_STEP_STAMPS
+  unsigned long long ss_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  KMX_SS(0);
+  const Lane L = lane_map<R>(d);
+  const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+  __shared__ Ctl cs;
+  __shared__ double rl[8 * WAVES];
+  const Ctl& c0 = cin[L.l];
+  const bool writer = L.tile == L.rt0;
+  if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))  // as in k_hess
+    reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(&c0)[threadIdx.x];
+  const int ph0 = c0.phase;
+  if (ph0 != PH_TCG && ph0 != PH_START) {
+    if (writer && threadIdx.x == 0) {
+      cout[L.l] = c0;
+      if (hs) post_status(hs, L.l, seq, false);
+    }
+    return;
+  }
+  const bool grad = ph0 == PH_START;  // the tCG's first step: k_grad's partials give the start
+  const int k = grad ? -1 : c0.tcg_iter;  // the step whose partials this launch consumes
+  const int t0 = L.rt0, t1 = L.rt1;
+  RobotSum<3> rg;
+  RobotSum8<4> rf;
+  if (grad) rg.issue(d.part, NPART, t0, t1);
+  else rf.issue(d.part_f, t0, t1);
+  double coef = 0.0, al = 0.0, be = 0.0;
+  KMX_SS(1);
+  auto decide = [&]() -> bool {
+    bool go;
+    KMX_SS(2);
+    if (grad) {
+      double tot[NPART];
+      rg.finish(d.part, NPART, rl, tot);
+      go = !(sqrt(tot[1]) < d.p.gn_tol);  // control_on's RED_GRAD test
+      if (writer && threadIdx.x == 0) control_on(cs, d, L.l, RED_GRAD, tot, R, true);
+    } else {
+      double tot[8];
+      rf.finish(d.part_f, rl, tot);
+      const double zr = tot[1];
+      const HessStep hx = hess_step(zr, c0.e_Pe, c0.e_Pd, c0.d_Pd, c0.Delta, tot[0]);
+      double rrn, zrn;
+      onesync_scalars(hx.alpha, tot, &rrn, &zrn);
+      const UpdStep u = upd_step(hx.boundary ? MODE_BOUNDARY : MODE_INTERIOR, c0.r_stop, c0.lin_stop, zr, k + 1,
+                                 rrn, zrn, d.p);
+      coef = hx.coef;
+      al = hx.alpha;
+      be = u.beta;
+      go = !u.done;
+      if (writer && threadIdx.x == 0) {  // the standard form's two control steps, on the LDS copy
+        cs.z_r = zr;
+        double th[NPART] = {tot[0], 0.0, 0.0, 0.0};
+        control_on(cs, d, L.l, RED_HESS, th, R, true);
+        double tu[NPART] = {rrn, zrn, 0.0, 0.0};
+        control_on(cs, d, L.l, RED_UPDATE, tu, R, true);
+      }
+    }
+    if (writer && threadIdx.x == 0) {
+      cout[L.l] = cs;
+      if (hs) post_status(hs, L.l, seq, cs.phase == PH_TCG);
+      if (go && slot >= 0) atomicAdd(d.hv_launch + slot, 1);
+    }
+    KMX_SS(3);
+    return go;
+  };
+  const int dhn = d.dhn;
+  const double* V = grad ? d.z : ((k & 1) ? d.w1 : d.w0);  // the vector the Hessian is applied to
+  double H[4];
+  PlainRows<R> src{V};
+  const bool go = hinc_gather_src<R, RW, false, PlainRows<R>, decltype(decide)&, false>(d, L, src, H, smem, decide);
+  if (!grad && !go) {  // the robot's tCG ends here: the last step's residual (k_retract's model)
+    if (L.valid) {
+      double rr[4], hd[4];
+      load4(d.r + o, rr);
+      load4(d.hd + o, hd);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) rr[c] = fma(coef, hd[c], rr[c]);
+      store4(d.r + o, rr);
+    }
+    return;
+  }
+  if (!go) return;
+  const int kn = k + 1;  // the step this launch forms
+  KMX_SS(4);
+  asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
+  // every row the epilogue needs, in one batch (one round trip after the gather)
+  // delta_kn goes into the oldest direction's buffer: directions kn - dhn ..
+  // kn - 1 join eta first, in step order (the standard form's fold; the
+  // newest coefficient is this launch's own decision). dhn = 2 (the
+  // default): the older direction and eta load with the rest
+  const bool fold = !grad && kn >= dhn && kn % dhn == 0;
+  const bool fold2 = fold && dhn == 2;
+  double dprev[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0};
+  const double cprev = fold2 ? d.coefh[(size_t)L.l * d.p.tcg_max + kn - 2] : 0.0;
+  double y[4] = {0, 0, 0, 0}, S[9], v[4] = {0, 0, 0, 0}, D[16], Pm[16];
+  double rn[4] = {0, 0, 0, 0}, hold[4] = {0, 0, 0, 0}, zo[4] = {0, 0, 0, 0}, hzo[4] = {0, 0, 0, 0},
+         dold[4] = {0, 0, 0, 0};
+  if (L.valid) {
+    load4(V + o, v);
+    load_sym4(d.hD + SYM4 * (size_t)L.pose, D);
+    load4(d.X + o, y);
+    load_sym3(d.S + 6 * (size_t)L.pose, S);
+    if (d.p.use_precond) load_sym4(d.Pinv + SYM4 * (size_t)L.pose, Pm);
+    if (grad) {
+      load4(d.g + o, rn);  // r_0 = g
+    } else {
+      load4(d.r + o, rn);
+      load4(d.hd + o, hold);
+      load4(d.z + o, zo);
+      load4(d.hz + o, hzo);
+      load4(d.dh + (size_t)(k % dhn) * d.vec + o, dold);
+      if (fold2) {  // the direction folded with dold (below), and eta
+        load4(d.dh + (size_t)(kn % dhn) * d.vec + o, dprev);
+        if (kn > dhn) load4(d.eta + o, et);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)  // the diagonal block (hinc_gather's DIAG term, same expression)
+      H[c] += v[0] * D[4 * c] + v[1] * D[4 * c + 1] + v[2] * D[4 * c + 2] + v[3] * D[4 * c + 3];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) S[i] = 0.0;
+  }
+  double* scr = reinterpret_cast<double*>(smem);  // the chunk buffer is free after the gather
+  double hv[4];
+  group_rhess<R, true>(y, v, H, S, L.base, hv, scr);  // Riemannian Hess of z_0 or w_k
+  KMX_SS(5);
+  double zn[4], hzn[4], dl[4], hdl[4];
+  if (grad) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      zn[c] = v[c];
+      hzn[c] = hv[c];
+      dl[c] = -v[c];
+      hdl[c] = -hv[c];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      rn[c] = fma(coef, hold[c], rn[c]);
+      zn[c] = fma(al, v[c], zo[c]);
+      hzn[c] = fma(al, hv[c], hzo[c]);
+      dl[c] = fma(be, dold[c], -zn[c]);
+      hdl[c] = fma(be, hold[c], -hzn[c]);
+    }
+  }
+  double wn[4];
+  group_precon<R, true>(d, L.pose, L.valid, y, hdl, L.base, wn, scr, Pm, L.valid);
+  if (fold2 && L.valid) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) et[c] += cprev * dprev[c];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) et[c] += coef * dold[c];
+    store4(d.eta + o, et);
+  } else if (fold && L.valid) {  // other KMX_DHMAX builds
+    if (kn > dhn) load4(d.eta + o, et);
+    const double* ch = d.coefh + (size_t)L.l * d.p.tcg_max;
+    for (int j = kn - dhn; j < kn; ++j) {
+      double dj[4];
+      load4(d.dh + (size_t)(j % dhn) * d.vec + o, dj);
+      const double cj = (j == kn - 1) ? coef : ch[j];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) et[c] += cj * dj[c];
+    }
+    store4(d.eta + o, et);
+  }
+  double pv[7] = {0, 0, 0, 0, 0, 0, 0};
+  if (L.valid) {
+    pv[0] = dot4(dl, hdl);
+    pv[1] = dot4(rn, zn);
+    pv[2] = dot4(rn, rn);
+    pv[3] = dot4(rn, wn) + dot4(hdl, zn);
+    pv[4] = dot4(hdl, wn);
+    pv[5] = dot4(rn, hdl);
+    pv[6] = dot4(hdl, hdl);
+  }
+  double* lds = reinterpret_cast<double*>(smem + SmemF<R>::red_off);
+#pragma unroll
+  for (int s2 = 0; s2 < 7; ++s2) {
+    const double w = wave_sum(pv[s2]);
+    if ((threadIdx.x & 63) == 0) lds[s2 * WAVES + (threadIdx.x >> 6)] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    double t = 0.0;
+    if (threadIdx.x < 7) {
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) t += lds[threadIdx.x * WAVES + w];
+    }
+    d.part_f[(size_t)L.tile * 8 + threadIdx.x] = t;
+  }
+  if (L.valid) {
+    store4(d.dh + (size_t)(kn % dhn) * d.vec + o, dl);
+    store4(d.hd + o, hdl);
+    store4(d.hz + o, hzn);
+    if (!grad) store4(d.z + o, zn);
+    store4(((kn & 1) ? d.w1 : d.w0) + o, wn);
+    store4(d.r + o, rn);
+  }
+#ifdef KMX_STEP_STAMPS
+  KMX_SS(6);
+  if (kn == 2 && threadIdx.x == 0 && L.tile < STEP_STAMP_TILES) {
+    for (int i = 0; i < 7; ++i) g_step_stamp[(size_t)L.tile * 16 + i] = ss_[i];
+    g_step_stamp[(size_t)L.tile * 16 + 8] = (unsigned long long)L.np;
+    g_step_stamp[(size_t)L.tile * 16 + 9] = (unsigned long long)L.n;
+    g_step_stamp[(size_t)L.tile * 16 + 10] = (unsigned long long)blockIdx.x;
+    g_step_stamp[(size_t)L.tile * 16 + 11] = (unsigned long long)(L.tile == L.rt0);
+  }
+#endif
+}
+
 // Trial point Xt = R_X(eta); partials: model m(eta) = 1/2 <eta, g + r> (r = g +
 // H eta by the tCG recurrence) and ||Xt - X||^2 (slots 2, 3; k_cost reduces).
 // fold (RM_CONSUMER): a robot still in tCG ran its last step's update with no
@@ -1526,27 +1913,33 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
 // decision into ctl in place: it changes only phase and tcg_stop, and a tile
 // that reads the new phase goes straight to the retraction, as the decision
 // says, so every tile acts alike.
+// src: where the tCG left the robot's state — d.ctl, or d.ctl2 after an odd
+// number of one-sync steps; the robot's first tile copies it to d.ctl, which
+// the launches after this one read.
 template <int R>
-__device__ __forceinline__ void body_retract(const Dev& d, int fold, char* smem) {
+__device__ __forceinline__ void body_retract(const Dev& d, int fold, const Ctl* src, char* smem) {
   const Lane L = lane_map<R>(d);
-  Ctl& c = d.ctl[L.l];
+  const Ctl& c = src[L.l];
   __shared__ int sph;
   __shared__ double rl[NPART * WAVES];
-  if (threadIdx.x == 0) sph = c.phase;
+  if (threadIdx.x == 0) {
+    sph = c.phase;
+    if (src != d.ctl && L.tile == L.rt0) d.ctl[L.l] = c;
+  }
   __syncthreads();
   const int ph = sph;  // one read per workgroup
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   double x[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0}, gg[4] = {0, 0, 0, 0}, rr[4] = {0, 0, 0, 0}, dl[4];
   if (fold && ph == PH_TCG) {
     RobotSum<2> rs;
-    rs.issue(d.part_u, 2, d.rtile0[L.l], d.rtile0[L.l + 1]);
+    rs.issue(d.part_u, 2, L.rt0, L.rt1);
     double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
     rs.finish(d.part_u, 2, rl, tot);
     const UpdStep u = upd_step(c.mode, c.r_stop, c.lin_stop, c.z_r, c.tcg_iter, tot[0], tot[1], d.p);
     if (!u.done) return;  // (cannot happen: the host stops enqueueing only when no robot is in tCG or at tcg_max)
-    if (threadIdx.x == 0 && L.tile == d.rtile0[L.l]) {
-      if (u.stop >= 0) c.tcg_stop = u.stop;
-      c.phase = PH_STEP;
+    if (threadIdx.x == 0 && L.tile == L.rt0) {  // (fold: src is d.ctl)
+      if (u.stop >= 0) d.ctl[L.l].tcg_stop = u.stop;
+      d.ctl[L.l].phase = PH_STEP;
     }
   } else if (ph != PH_STEP) {
     return;
@@ -1648,14 +2041,14 @@ __device__ __forceinline__ void body_commit(const Dev& d, int fold, int final) {
     __shared__ Ctl cs;
     __shared__ double rl[NPART * WAVES];
     const Ctl& c = d.ctl[L.l];
-    const bool writer = L.tile == d.rtile0[L.l];
+    const bool writer = L.tile == L.rt0;
     if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))  // as in k_hess
       reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(&c)[threadIdx.x];
     if (threadIdx.x == 0) sph = c.phase;
     __syncthreads();
     if (sph != PH_STEP) return;
     RobotSum<NPART> rs;
-    rs.issue(d.part, NPART, d.rtile0[L.l], d.rtile0[L.l + 1]);
+    rs.issue(d.part, NPART, L.rt0, L.rt1);
     double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
     rs.finish(d.part, NPART, rl, tot);
     if (d.p.rgd) {
@@ -1699,10 +2092,18 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
   KMX_SMEM;
   body_update<R, RM>(d, hs, seq, slot, smem);
 }
-template <int R>
-__global__ __launch_bounds__(BLOCK) void k_retract(Dev d, int fold) {
+// 3 waves per SIMD at r <= 5: the 736-tile cut of a small shard is resident
+// in one generation (256 CUs x 3), without the spills of a 128-VGPR bound
+template <int R, int RW>
+__global__ __launch_bounds__(BLOCK, (R <= 5 ? 3 : 2)) void k_step(Dev d, const Ctl* cin, Ctl* cout, int slot, HostStatus* hs,
+                                                unsigned long long seq) {
   KMX_SMEM;
-  body_retract<R>(d, fold, smem);
+  body_step<R, RW>(d, cin, cout, slot, hs, seq, smem);
+}
+template <int R>
+__global__ __launch_bounds__(BLOCK) void k_retract(Dev d, int fold, const Ctl* src) {
+  KMX_SMEM;
+  body_retract<R>(d, fold, src, smem);
 }
 template <int R, int RW, int RM>
 __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d) {
@@ -2184,6 +2585,8 @@ struct kmx_pgo {
   int2* d_eipos = nullptr;
   double* d_vec = nullptr;  // X Xt g r z hd eta, then the dhn tCG directions (nvec())
   double* d_coefh = nullptr;  // [L][tcg_max]
+  double* d_part_f = nullptr;  // [ntiles][8] one-sync tCG partials (P.tcg_form)
+  int ctl_par = 0;             // one-sync tCG: the state after the last tCG loop is in ctl2 (odd step count)
   double *d_S = nullptr, *d_Pinv = nullptr, *d_hD = nullptr, *d_pub = nullptr, *d_part = nullptr;
   Ctl* d_ctl = nullptr;
   Ctl* d_ctl2 = nullptr;
@@ -2320,7 +2723,7 @@ void free_dev(kmx_pgo* h) {
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
                   h->d_accV, h->d_accY, h->d_ctl2, h->d_part_h,
-                  h->d_part_u, h->d_coefh};
+                  h->d_part_u, h->d_coefh, h->d_part_f};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile = nullptr;
@@ -2346,6 +2749,7 @@ void free_dev(kmx_pgo* h) {
   h->d_ctl2 = nullptr;
   h->d_coefh = nullptr;
   h->d_part_h = h->d_part_u = nullptr;
+  h->d_part_f = nullptr;
 }
 
 hipEvent_t next_event(kmx_pgo* h) {
@@ -2359,9 +2763,13 @@ hipEvent_t next_event(kmx_pgo* h) {
 
 bool ready(kmx_pgo* h) { return h && h->d_vec != nullptr; }
 
-// Vectors of d_vec: X Xt g r z hd eta + the tCG directions kept for k_retract.
-int dh_count(const kmx_pgo* h) { return std::max(1, std::min(h->P.tcg_max_iterations, DHMAX)); }
-size_t nvec(const kmx_pgo* h) { return 7 + (size_t)dh_count(h); }
+// Vectors of d_vec: X Xt g r z hd eta + the tCG directions kept for k_retract
+// (+ Hz, w_0, w_1 for the one-sync tCG, which needs two directions).
+bool onesync(const kmx_pgo* h) { return h->P.tcg_form == KMX_TCG_FORM_ONESYNC && h->P.method == KMX_METHOD_RTR; }
+int dh_count(const kmx_pgo* h) {
+  return std::max(onesync(h) ? 2 : 1, std::min(h->P.tcg_max_iterations, DHMAX));
+}
+size_t nvec(const kmx_pgo* h) { return 7 + (size_t)dh_count(h) + (onesync(h) ? 3 : 0); }
 
 // Scratch of the diagnostic / output entry points (not resident with the graph).
 int ensure_scratch(kmx_pgo* h, size_t doubles) {
@@ -2505,6 +2913,40 @@ void enqueue_tcg_t(kmx_pgo* h) {
   }
   const int tmax = h->P.tcg_max_iterations;
   int steps = tmax;  // steps enqueued by a polled loop
+  if constexpr (RM == RM_CONSUMER) {
+    if (onesync(h)) {
+      // one k_step per step: launch j applies step j-1's decision (which it
+      // reports at its start) and runs Hess-vec j; launch tmax only decides.
+      // A polled loop waits for launch j's report while launch j still
+      // gathers, so the next launch is queued before the GPU runs dry.
+      int J = tmax + 1;
+      for (int j = 0; j <= tmax; ++j) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        int slot = -1;
+        if (h->timing && h->ev_used / 2 < (size_t)HV_SLOTS) {
+          slot = (int)(h->ev_used / 2);
+          e0 = next_event(h);
+          e1 = next_event(h);
+          (void)hipEventRecord(e0, h->stream);
+        }
+        poll = poll && h->poll;
+        const unsigned long long seq = poll ? ++h->seq : 0;
+        HostStatus* hs = poll ? h->hstat : nullptr;
+        const Ctl* cin = (j & 1) ? h->d_ctl2 : h->d_ctl;
+        Ctl* cout = (j & 1) ? h->d_ctl : h->d_ctl2;
+        hipLaunchKernelGGL((k_step<R, RW>), grid, blk, SmemF<R>::bytes, h->stream, h->dv, cin, cout, slot, hs, seq);
+        if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+        if (poll && j > 0 && !wait_running(h, seq)) {
+          J = j + 1;
+          break;
+        }
+      }
+      h->ctl_par = J & 1;
+      steps = J - 1;
+      if (poll && h->poll_auto && steps + kmx_pgo::BLIND_SLACK >= tmax) h->blind_left = kmx_pgo::BLIND_WINDOW;
+      return;
+    }
+  }
   for (int j = 0; j < tmax; ++j) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int slot = -1;
@@ -2550,7 +2992,10 @@ void enqueue_trial_t(kmx_pgo* h, bool rgd) {
   const dim3 grid(h->ntiles), blk(BLOCK);
   // RM_CONSUMER: the last step's update has no k_hess after it; k_retract
   // reduces it
-  hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv, RM == RM_CONSUMER && !rgd ? 1 : 0);
+  const bool os = RM == RM_CONSUMER && !rgd && onesync(h);  // no update left to fold: k_step decided it
+  const Ctl* src = os && h->ctl_par ? h->d_ctl2 : h->d_ctl;
+  hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv, RM == RM_CONSUMER && !rgd && !os ? 1 : 0,
+                     src);
   hipLaunchKernelGGL((k_cost<R, RW, RM>), grid, blk, SmemC<R>::bytes, h->stream, h->dv);
   if (!fold_cost<RM>(h)) red_t<R, RM>(h, RED_COST);
 }
@@ -2664,6 +3109,8 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
             "acceleration is 0 or 1, restart_interval >= 0");
   KMX_CHECK(params->method == KMX_METHOD_RTR || params->method == KMX_METHOD_RGD, KMX_EUNSUP,
             "method must be KMX_METHOD_RTR or KMX_METHOD_RGD");
+  KMX_CHECK(params->tcg_form == KMX_TCG_FORM_STANDARD || params->tcg_form == KMX_TCG_FORM_ONESYNC, KMX_EINVAL,
+            "tcg_form must be KMX_TCG_FORM_STANDARD or KMX_TCG_FORM_ONESYNC");
   KMX_CHECK(params->method != KMX_METHOD_RGD || params->rgd_stepsize > 0.0, KMX_EINVAL, "rgd_stepsize must be > 0");
   KMX_CHECK(params->tile_incidences >= 0, KMX_EINVAL, "tile_incidences must be >= 0 (0: automatic)");
   int ndev = 0;
@@ -2757,6 +3204,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   }
   h->nloc = nloc;
   h->rm = h->rm_forced >= 0 ? h->rm_forced : (nloc <= kmx_pgo::RM_CONSUMER_MAX_POSES ? RM_CONSUMER : RM_LAUNCH);
+  if (onesync(h)) h->rm = RM_CONSUMER;  // its decisions are taken by every workgroup
   h->early_stop = h->early_forced >= 0 ? h->early_forced : (nloc <= kmx_pgo::RM_CONSUMER_MAX_POSES ? 1 : 0);
   const int L = (int)h->robots.size();
   KMX_CHECK(L > 0, KMX_EINVAL, "no local robot");
@@ -2969,6 +3417,9 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     const int ninc = inc_ptr[tp0[t] + tnp[t]] - td.k0;
     KMX_CHECK(tnp[t] < 256 && ninc < (1 << 23), KMX_EINVAL, "tile too large");
     td.np_n = tnp[t] | (ninc << 8);
+    td.rt0 = rt0[tr[t]];
+    td.rt1 = rt0[tr[t] + 1];
+    td.pad0 = td.pad1 = 0;
   }
   // device
   int rc;
@@ -2994,7 +3445,8 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_osh_edge, std::max(h->n_osh, 1))) || (rc = dalloc(&h->d_osh_idx, std::max(h->n_osh, 1))) ||
       (rc = dalloc(&h->d_relc, L)) || (rc = dalloc(&h->d_gnc, 2)) || (rc = dalloc(&h->d_ext, 64)) ||
       (rc = dalloc(&h->d_hv_launch, HV_SLOTS)) ||
-      (rc = dalloc(&h->d_coefh, (size_t)L * std::max(h->P.tcg_max_iterations, 1)))) {
+      (rc = dalloc(&h->d_coefh, (size_t)L * std::max(h->P.tcg_max_iterations, 1))) ||
+      (onesync(h) && (rc = dalloc(&h->d_part_f, (size_t)h->ntiles * 8)))) {
     free_dev(h);
     return rc;
   }
@@ -3072,6 +3524,11 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   d.relc = h->d_relc; d.gnc = h->d_gnc; d.gnc_next = h->d_gnc + 1;
   d.gnc_edge = h->d_gnc_edge; d.gnc_ends = h->d_gnc_ends; d.n_gnc = h->n_gnc;
   d.hv_launch = h->d_hv_launch;
+  if (onesync(h)) {
+    const size_t v0 = 7 + (size_t)dh_count(h);
+    d.hz = h->d_vec + v0 * vec; d.w0 = h->d_vec + (v0 + 1) * vec; d.w1 = h->d_vec + (v0 + 2) * vec;
+    d.part_f = h->d_part_f;
+  }
   h->n_ext = 0;
   sync_params(h);
   enqueue_precond(h, 0);
@@ -3780,7 +4237,7 @@ extern "C" int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_byt
   b += n * ps * 8 * (int64_t)nvec(h) + n * (6 + SYM4 + SYM4) * 8;       // vectors, S, Pinv, D
   b += L * 8 * (int64_t)std::max(h->P.tcg_max_iterations, 1);            // tCG coefficients
   b += std::max<int64_t>(h->npub, 1) * (ps * 8 + 4) + n * 4;             // public table + maps
-  b += (int64_t)h->ntiles * (NPART * 8 + 12) + L * (int64_t)(sizeof(Ctl) + 32);
+  b += (int64_t)h->ntiles * (NPART * 8 + 12 + (onesync(h) ? 64 : 0)) + L * (int64_t)(sizeof(Ctl) + 32);
   b += (int64_t)std::max(h->n_gnc, 1) * 12 + (int64_t)h->scratch_cap * 8;  // GNC lists, scratch in use
   if (h->P.acceleration) b += 2 * n * ps * 8;                              // V, Y
   if (device_bytes) *device_bytes = b;
@@ -3825,4 +4282,22 @@ extern "C" int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out) {
   h->ev_used = 0;
   KMX_HIP(hipMemset(h->d_cnt, 0, sizeof(Counters)));
   return KMX_OK;
+}
+
+// Diagnostic: the k_step phase stamps of a KMX_STEP_STAMPS build (16 words per
+// tile: 7 wall-clock stamps, -, poses, incidences, block index, writer);
+// KMX_EUNSUP in the product build.
+extern "C" int kmx_pgo_debug_step_stamps(uint64_t* out, int64_t n) {
+  KMX_GUARD_BEGIN
+#ifdef KMX_STEP_STAMPS
+  KMX_CHECK(out && n >= 0, KMX_EINVAL, "null buffer");
+  const int64_t m = std::min<int64_t>(n, 16 * (int64_t)STEP_STAMP_TILES);
+  KMX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_stamp), sizeof(uint64_t) * m, 0, hipMemcpyDeviceToHost));
+  return KMX_OK;
+#else
+  (void)out;
+  (void)n;
+  return kmx::fail(KMX_EUNSUP, "not a KMX_STEP_STAMPS build");
+#endif
+  KMX_GUARD_END
 }

@@ -55,7 +55,7 @@ class PgoParams(C.Structure):
         ("precond_shift", C.c_double), ("robust_cost", C.c_int),
         ("gnc_barc", C.c_double), ("gnc_mu_init", C.c_double),
         ("gnc_mu_step", C.c_double), ("acceleration", C.c_int), ("restart_interval", C.c_int),
-        ("method", C.c_int), ("reserved0", C.c_int), ("rgd_stepsize", C.c_double), ("tile_incidences", C.c_int),
+        ("method", C.c_int), ("tcg_form", C.c_int), ("rgd_stepsize", C.c_double), ("tile_incidences", C.c_int),
         ("reserved", C.c_int),
     ]
 
@@ -163,6 +163,7 @@ def lib() -> C.CDLL:
         "kmx_pgo_iterate_async": ([P, C.c_int, C.c_int], C.c_int),
         "kmx_pgo_sync": ([P], C.c_int),
         "kmx_pgo_sync_timeout": ([P, f64], C.c_int),
+        "kmx_pgo_debug_step_stamps": ([P, i64], C.c_int),
         "kmx_pgo_update_weights": ([P, pf64], C.c_int),
         "kmx_pgo_get_mu": ([P, pf64], C.c_int),
         "kmx_pgo_set_mu": ([P, f64], C.c_int),

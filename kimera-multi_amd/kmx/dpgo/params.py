@@ -55,6 +55,9 @@ class ROptParameters:
     gradnorm_tol: float = 1e-2
     use_preconditioner: bool = True
     precond_shift: float = 1e-1
+    # kmx opt-in: "standard" (ROPTLIB's tCG) or "onesync" (one reduction and one
+    # kernel per tCG step, KMX_TCG_FORM_ONESYNC; parity at convergence only)
+    tCG_form: str = "standard"
 
 
 @dataclass
@@ -101,4 +104,8 @@ class PGOAgentParameters:
         p.acceleration = 1 if self.acceleration else 0
         p.restart_interval = int(self.restartInterval)
         p.tile_incidences = int(self.tileIncidences)
+        forms = {"standard": 0, "onesync": 1}
+        if lo.tCG_form not in forms:
+            raise ValueError(f"tCG_form must be one of {sorted(forms)}, got {lo.tCG_form!r}")
+        p.tcg_form = forms[lo.tCG_form]
         return p

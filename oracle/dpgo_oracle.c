@@ -532,6 +532,88 @@ static void retract_pose(int r, const double* X, const double* V, double* out) {
   }
 }
 
+/* ------------------------------------------------- one-sync tCG (opt-in) -- */
+/* KMX_TCG_FORM_ONESYNC: the same Steihaug-Toint iteration with every scalar of
+ * step k+1 formed from ONE reduction after step k, so the GPU runs one kernel
+ * (one grid-wide dependency) per step (pgo.hip body_step, DESIGN.md §5
+ * "one-sync tCG"). With w = precon(H delta) (precon and H linear):
+ *   r' = r + alpha H delta,   z' = z + alpha w,   Hz' = Hz + alpha Hw,
+ *   delta' = -z' + beta delta,   H delta' = -Hz' + beta H delta
+ *   <r',r'> = <r,r> + 2 alpha <r,H delta> + alpha^2 <H delta,H delta>
+ *   <r',z'> = <r,z> + alpha (<r,w> + <H delta,z>) + alpha^2 <H delta,w>
+ * so the Hessian is applied to w (step 0: to z_0; one gathered row per
+ * incidence, as in the standard form's linearity H delta = -Hz + beta H
+ * delta_old), and the reduction after step k carries <delta,H delta>, <r,z>,
+ * <r,r>, <r,w> + <H delta,z>, <H delta,w>, <r,H delta>, <H delta,H delta>;
+ * <r,z> and <r,r> are taken from the recurred vectors at every step (residual
+ * replacement for the scalars), so the scalar recurrences are one step deep.
+ * Pipelined CG in the sense of Ghysels & Vanroose (Parallel Computing 40,
+ * 2014) and Chronopoulos & Gear (J. Comput. Appl. Math. 25, 1989), inside the
+ * trust-region tests of ROPTLIB's tCG (the standard loop in block_update).
+ * The vector recurrences are fused multiply-adds, as on the GPU. Parity with
+ * the standard form is at convergence only; against the GPU's
+ * same form, per round within rounding.
+ * Hz and Hw use the work vectors the tCG does not touch (the trial point's
+ * and the Euclidean gradient's). */
+static int tcg_onesync(const blk* b, const ctx* c, double Delta, double norm_r0, double d_Pd, double* rr, double* z,
+                       double* del, double* Hd, double* w, double* Hz, double* Hw, double* eta, double* Heta,
+                       kmx_iter_stats* st, int* stop_out) {
+  const orc_pgo* h = b->h;
+  const int64_t N = (int64_t)b->n * b->ps;
+  const double r_stop = norm_r0 * fmin(pow(norm_r0, h->P.tcg_theta), h->P.tcg_kappa);
+  const int lin = (h->P.tcg_kappa < pow(norm_r0, h->P.tcg_theta)) ? 1 : 0;
+  double e_Pe = 0.0, e_Pd = 0.0;
+  int stop = KMX_TCG_MAX_ITER, j;
+  rhess(b, c, z, Hz); /* step 0: delta_0 = -z_0, H delta_0 = -H z_0 */
+  for (int64_t k = 0; k < N; ++k) Hd[k] = -Hz[k];
+  precon(b, c, Hd, w);
+  for (j = 1; j <= h->P.tcg_max_iterations; ++j) {
+    st->hessvecs++;
+    /* the step's one reduction */
+    const double d_Hd = pdot(b, del, Hd, N), zr = pdot(b, rr, z, N), rr2 = pdot(b, rr, rr, N);
+    const double s1 = pdot(b, rr, w, N) + pdot(b, Hd, z, N), s2 = pdot(b, Hd, w, N);
+    const double s3 = pdot(b, rr, Hd, N), s4 = pdot(b, Hd, Hd, N);
+    const double alpha = zr / d_Hd;
+    const double e_Pe_new = e_Pe + 2.0 * alpha * e_Pd + alpha * alpha * d_Pd;
+    if (d_Hd <= 0.0 || e_Pe_new >= Delta * Delta) {
+      const double tau = (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (Delta * Delta - e_Pe))) / d_Pd;
+      for (int64_t k = 0; k < N; ++k) { eta[k] += tau * del[k]; Heta[k] += tau * Hd[k]; rr[k] = fma(tau, Hd[k], rr[k]); }
+      stop = d_Hd <= 0.0 ? KMX_TCG_NEGATIVE_CURVATURE : KMX_TCG_EXCEEDED_TR;
+      break;
+    }
+    e_Pe = e_Pe_new;
+    for (int64_t k = 0; k < N; ++k) {
+      eta[k] += alpha * del[k];
+      Heta[k] += alpha * Hd[k];
+    }
+    const double rr_new = fmax(rr2 + 2.0 * alpha * s3 + alpha * alpha * s4, 0.0);
+    const double zr_new = zr + alpha * s1 + alpha * alpha * s2;
+    if (sqrt(rr_new) <= r_stop) {
+      for (int64_t k = 0; k < N; ++k) rr[k] = fma(alpha, Hd[k], rr[k]);
+      stop = lin ? KMX_TCG_LINEAR : KMX_TCG_SUPERLINEAR;
+      break;
+    }
+    if (j == h->P.tcg_max_iterations) {
+      for (int64_t k = 0; k < N; ++k) rr[k] = fma(alpha, Hd[k], rr[k]);
+      break;
+    }
+    const double beta = zr_new / zr;
+    rhess(b, c, w, Hw);
+    for (int64_t k = 0; k < N; ++k) {
+      rr[k] = fma(alpha, Hd[k], rr[k]);
+      z[k] = fma(alpha, w[k], z[k]);
+      Hz[k] = fma(alpha, Hw[k], Hz[k]);
+      del[k] = fma(beta, del[k], -z[k]);
+      Hd[k] = fma(beta, Hd[k], -Hz[k]);
+    }
+    precon(b, c, Hd, w);
+    e_Pd = beta * (e_Pd + alpha * d_Pd);
+    d_Pd = zr_new + beta * beta * d_Pd;
+  }
+  *stop_out = stop;
+  return j;
+}
+
 /* --------------------------------------------------------- block update -- */
 static void block_update(orc_pgo* h, int a, kmx_iter_stats* st, int inner) {
   blk b = {h, a, h->npose[a], h->P.r, PS(h), h->poff[a], inner};
@@ -619,6 +701,9 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st, int inner) {
 #pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
     for (int64_t k = 0; k < N; ++k) del[k] = -z[k];
     int stop = KMX_TCG_MAX_ITER, j;
+    if (h->P.tcg_form == KMX_TCG_FORM_ONESYNC) {
+      j = tcg_onesync(&b, &c, Delta, norm_r0, d_Pd, rr, z, del, Hd, wk_ + 11 * NP, Xt, c.eg, eta, Heta, st, &stop);
+    } else
     for (j = 1; j <= h->P.tcg_max_iterations; ++j) {
       rhess(&b, &c, del, Hd);
       st->hessvecs++;

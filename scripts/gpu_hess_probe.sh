@@ -3,7 +3,8 @@
 # drop one stream (1 neighbour rows, 2 own rows + D_i, 4 delta_old / Hdelta_old,
 # 8 the delta / Hdelta stores, 15 all: records + CSR only), built beforehand by
 # `make -C kimera-multi_amd/csrc probe PROBE=n` into alt/.
-# usage: bash scripts/gpu_hess_probe.sh TAG [variants...]
+# usage: [BURN=40] bash scripts/gpu_hess_probe.sh TAG [variants...]  (BURN: rounds before the window;
+# 10 = first tCG steps, 40 = the bench steady-state window with delta_old / Hdelta_old in play)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -17,7 +18,7 @@ for v in $V; do
   i=0
   for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
     i=$((i+1))
-    KMX_LIB=$lib timeout -k 10 240 rocprofv3 --kernel-trace --pmc $C -d $O/p$i -o run --output-format csv -- python3 bench.py --burn-in 10 --steps 10 --warmup 0 --profile --no-cpu --no-lcd > $O/p$i.json 2> $O/p$i.err
+    KMX_LIB=$lib timeout -k 10 240 rocprofv3 --kernel-trace --pmc $C -d $O/p$i -o run --output-format csv -- python3 bench.py --burn-in ${BURN:-40} --steps 10 --warmup 0 --profile --no-cpu --no-lcd > $O/p$i.json 2> $O/p$i.err
     rc=$?; echo "variant $v pass $i ($C) rc=$rc"
     [ $rc -ne 0 ] && { tail -5 $O/p$i.err; exit $rc; }
   done

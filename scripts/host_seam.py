@@ -16,7 +16,7 @@ table (rows gathered once) and times rounds under:
          peers' — timing only), all rounds from one iterate_async call
 The handle's tCG enqueueing is the default adaptive mode
 (kmx_pgo_set_tcg_poll(-1)).
-usage: python scripts/host_seam.py N [rounds]
+usage: python scripts/host_seam.py N [rounds] [standard|onesync]  (the tCG form)
 """
 import os
 import sys
@@ -45,6 +45,7 @@ dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cu
 
 g = config("synth100k", seed=0)
 P = bench.params()
+P.localOptimizationParams.tCG_form = sys.argv[3] if len(sys.argv) > 3 else "standard"
 P = dataclasses.replace(P, tileIncidences=team_tile_incidences(g, N, P.r))
 Y = lifting_matrix(5, seed=1)
 lo, hi = robot_ranges(g.n_robots, N)[0]
@@ -79,7 +80,7 @@ wire_in = torch.zeros(n_recv * ps + N, dtype=torch.float64, device=dev)
 wire_out = torch.zeros_like(wire_in)
 print(f"N={N}: rank 0 holds robots {lo}..{hi - 1}, {int(g.n_poses[lo:hi].sum())} poses; "
       f"sends {n_send} rows, receives {n_recv} rows ({n_recv * ps * 8 / 1e6:.2f} MB) per round; "
-      "adaptive tCG enqueueing", flush=True)
+      f"adaptive tCG enqueueing, {P.localOptimizationParams.tCG_form} tCG", flush=True)
 
 for mode in ("batch", "seam", "native"):
     s = make()

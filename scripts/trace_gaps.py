@@ -14,7 +14,7 @@ print(f"wall {(s1 - s0) / 10e3:.1f} us/round, busy {busy / 10e3:.1f} us/round, k
 
 
 def nm(n):
-    for k in ("k_hess", "k_update", "k_reduce", "k_grad", "k_cost", "k_retract", "k_commit", "k_begin", "k_precond",
+    for k in ("k_step", "k_hess", "k_update", "k_reduce", "k_grad", "k_cost", "k_retract", "k_commit", "k_begin", "k_precond",
               "k_publish", "k_accel"):
         if k in n:
             return k

@@ -274,3 +274,40 @@ def test_all_cores_variant_agrees_with_serial_round():
             assert sa[r]["tcg_iterations"] == sb[r]["tcg_iterations"] and sa[r]["accepted"] == sb[r]["accepted"]
             d = np.abs(a_.get_iterate(r) - b_.get_iterate(r)).max()
             assert d <= 1e-9, (it, r, d)
+
+
+def test_onesync_tcg_form_tracks_standard_form():
+    """The one-sync tCG restatement (tcg_onesync, KMX_TCG_FORM_ONESYNC): the
+    same Steihaug-Toint decisions from one reduction per step. In exact
+    arithmetic it is the standard iteration; in floating point the two stay
+    within rounding over a run to relChangeTol: equal Hess-vec counts per
+    round here, the same round count to converge, costs within 1e-9."""
+    runs = {}
+    for form in ("standard", "onesync"):
+        g, P, o, X = _problem(seed=2, robots=3, n=300, m=900)
+        P.localOptimizationParams.tCG_form = form
+        o = OraclePGO(P.to_c(), g)
+        for a in range(g.n_robots):
+            o.set_iterate(a, X[a])
+        o.refresh()
+        hist = []
+        for it in range(200):
+            st = o.iterate()
+            hist.append((max(s["rel_change"] for s in st), [s["hessvecs"] for s in st],
+                         sum(s["f_final"] for s in st)))
+            if it % 10 == 9:
+                o.refresh()
+                o.update_weights()
+        runs[form] = hist
+    conv = {f: next(i for i, x in enumerate(h) if x[0] < 1e-3) for f, h in runs.items()}
+    assert conv["onesync"] == conv["standard"], conv
+    for a, b in zip(runs["standard"], runs["onesync"]):
+        assert a[1] == b[1]
+        assert abs(a[2] - b[2]) <= 1e-9 * abs(a[2])
+
+
+def test_tcg_form_is_checked():
+    P = PGOAgentParameters(r=5)
+    P.localOptimizationParams.tCG_form = "pipelined"
+    with pytest.raises(ValueError):
+        P.to_c()
