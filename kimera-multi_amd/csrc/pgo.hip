@@ -1346,7 +1346,8 @@ __device__ __forceinline__ void body_grad(const Dev& d, int gated, char* smem) {
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old;
 // partial <delta, Hdelta>. delta_k is kept for k_retract's eta (Dev::dh).
 template <int R, int RW, int RM>
-__device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs, unsigned long long seq, char* smem) {
+__device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int slot, HostStatus* hs,
+                                          unsigned long long seq, char* smem) {
   const Lane L = lane_map<R>(d);
   int tcg_iter;
   double beta;
@@ -1367,22 +1368,25 @@ __device__ __forceinline__ void body_hess(const Dev& d, int slot, HostStatus* hs
     // (its lane 0 reads it after these in-order LDS writes of its own wave)
     if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))
       reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(&c0)[threadIdx.x];
+    // first (the host's launch 0 of a tCG loop): a robot in it is at
+    // PH_START, the first step of the tCG, whose gradient reduction (k_grad's
+    // partials) this launch also consumes in place of a k_reduce launch; later
+    // launches find it in PH_TCG. The robot sums' loads go out before the
+    // state arrives.
+    const bool grad = first_launch != 0;
+    const bool upd = !grad;
+    RobotSum<2> rs;  // (four tiles per thread here: spills at 128 VGPRs)
+    RobotSum<3> rg;
+    if (upd) rs.issue(d.part_u, 2, L.rt0, L.rt1);
+    if (grad) rg.issue(d.part, NPART, L.rt0, L.rt1);
     const int ph0 = c0.phase;  // written by an earlier launch: uniform
-    // PH_START: the first step of the tCG, whose gradient reduction (k_grad's
-    // partials) this launch also consumes in place of a k_reduce launch
-    const bool grad = ph0 == PH_START;
-    if (ph0 != PH_TCG && !grad) {  // uniform: a tile never straddles robots
+    if (ph0 != (grad ? PH_START : PH_TCG)) {  // uniform: a tile never straddles robots
       if (writer && threadIdx.x == 0) {
         d.ctl2[L.l] = c0;
         if (hs) post_status(hs, L.l, seq, false);
       }
       return;
     }
-    const bool upd = !grad && c0.tcg_iter > 0;
-    RobotSum<2> rs;  // (four tiles per thread here: spills at 128 VGPRs)
-    RobotSum<3> rg;
-    if (upd) rs.issue(d.part_u, 2, L.rt0, L.rt1);
-    if (grad) rg.issue(d.part, NPART, L.rt0, L.rt1);
     UpdStep u{0, 0, 0.0};
     // the decision runs while the first chunk's records are in flight and
     // before any row is gathered: a robot whose tCG stops here (or whose
@@ -1691,8 +1695,8 @@ __device__ unsigned long long g_step_stamp[16 * STEP_STAMP_TILES];
 #endif
 
 template <int R, int RW>
-__device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cout, int slot, HostStatus* hs,
-                                          unsigned long long seq, char* smem) {
+__device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cout, int first, int slot,
+                                          HostStatus* hs, unsigned long long seq, char* smem) {
 #ifdef KMX_STEP_STAMPS
   unsigned long long ss_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1705,21 +1709,24 @@ __device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cou
   const bool writer = L.tile == L.rt0;
   if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))  // as in k_hess
     reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(&c0)[threadIdx.x];
+  // first (the host's launch 0 of a tCG loop): a robot in it is at PH_START
+  // and the launch consumes k_grad's partials, else it is in PH_TCG; the
+  // robot sums' loads go out before the state arrives
+  const bool grad = first != 0;
+  const int t0 = L.rt0, t1 = L.rt1;
+  RobotSum<3> rg;
+  RobotSum8<4> rf;
+  if (grad) rg.issue(d.part, NPART, t0, t1);
+  else rf.issue(d.part_f, t0, t1);
   const int ph0 = c0.phase;
-  if (ph0 != PH_TCG && ph0 != PH_START) {
+  if (ph0 != (grad ? PH_START : PH_TCG)) {
     if (writer && threadIdx.x == 0) {
       cout[L.l] = c0;
       if (hs) post_status(hs, L.l, seq, false);
     }
     return;
   }
-  const bool grad = ph0 == PH_START;  // the tCG's first step: k_grad's partials give the start
   const int k = grad ? -1 : c0.tcg_iter;  // the step whose partials this launch consumes
-  const int t0 = L.rt0, t1 = L.rt1;
-  RobotSum<3> rg;
-  RobotSum8<4> rf;
-  if (grad) rg.issue(d.part, NPART, t0, t1);
-  else rf.issue(d.part_f, t0, t1);
   double coef = 0.0, al = 0.0, be = 0.0;
   KMX_SS(1);
   auto decide = [&]() -> bool {
@@ -2083,9 +2090,10 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d, int gated) {
   body_grad<R, RW, RM>(d, gated, smem);
 }
 template <int R, int RW, int RM>
-__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int slot, HostStatus* hs, unsigned long long seq) {
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int first, int slot, HostStatus* hs,
+                                                          unsigned long long seq) {
   KMX_SMEM;
-  body_hess<R, RW, RM>(d, slot, hs, seq, smem);
+  body_hess<R, RW, RM>(d, first, slot, hs, seq, smem);
 }
 template <int R, int RM>
 __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq, int slot) {
@@ -2095,10 +2103,10 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
 // 3 waves per SIMD at r <= 5: the 736-tile cut of a small shard is resident
 // in one generation (256 CUs x 3), without the spills of a 128-VGPR bound
 template <int R, int RW>
-__global__ __launch_bounds__(BLOCK, (R <= 5 ? 3 : 2)) void k_step(Dev d, const Ctl* cin, Ctl* cout, int slot, HostStatus* hs,
-                                                unsigned long long seq) {
+__global__ __launch_bounds__(BLOCK, (R <= 5 ? 3 : 2)) void k_step(Dev d, const Ctl* cin, Ctl* cout, int first, int slot,
+                                                                  HostStatus* hs, unsigned long long seq) {
   KMX_SMEM;
-  body_step<R, RW>(d, cin, cout, slot, hs, seq, smem);
+  body_step<R, RW>(d, cin, cout, first, slot, hs, seq, smem);
 }
 template <int R>
 __global__ __launch_bounds__(BLOCK) void k_retract(Dev d, int fold, const Ctl* src) {
@@ -2934,7 +2942,8 @@ void enqueue_tcg_t(kmx_pgo* h) {
         HostStatus* hs = poll ? h->hstat : nullptr;
         const Ctl* cin = (j & 1) ? h->d_ctl2 : h->d_ctl;
         Ctl* cout = (j & 1) ? h->d_ctl : h->d_ctl2;
-        hipLaunchKernelGGL((k_step<R, RW>), grid, blk, SmemF<R>::bytes, h->stream, h->dv, cin, cout, slot, hs, seq);
+        hipLaunchKernelGGL((k_step<R, RW>), grid, blk, SmemF<R>::bytes, h->stream, h->dv, cin, cout, j == 0 ? 1 : 0,
+                           slot, hs, seq);
         if (slot >= 0) (void)hipEventRecord(e1, h->stream);
         if (poll && j > 0 && !wait_running(h, seq)) {
           J = j + 1;
@@ -2961,7 +2970,8 @@ void enqueue_tcg_t(kmx_pgo* h) {
     HostStatus* hs = poll ? h->hstat : nullptr;
     if constexpr (RM == RM_CONSUMER) {
       // k_hess reports the stop test of the previous step's update
-      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, hs, seq);
+      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot, hs,
+                         seq);
       if (slot >= 0) (void)hipEventRecord(e1, h->stream);
       hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, 0ull, slot);
       if (poll && j > 0 && !wait_running(h, seq)) {
@@ -2970,7 +2980,8 @@ void enqueue_tcg_t(kmx_pgo* h) {
       }
       continue;
     }
-    hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, slot, nullptr, 0ull);
+    hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot, nullptr,
+                       0ull);
     if (slot >= 0) (void)hipEventRecord(e1, h->stream);
     red_t<R, RM>(h, RED_HESS, nullptr, 0, slot);
     hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, seq, -1);
