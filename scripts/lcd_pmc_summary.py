@@ -1,11 +1,15 @@
 """Summarise the k_ransac_coop PMC passes of scripts/gpu_lcd_pmc3.sh (run
 over scripts/lcd_timing.py N: one warm-up launch of 64 candidates, then 4
 launches of N) into the per-candidate counts bench.py's LCD roofline uses.
-usage: lcd_pmc_summary.py PMC_DIR OUT_JSON [N]
+usage: lcd_pmc_summary.py PMC_DIR OUT_JSON [N] [LAUNCHES]
 N (the candidates per timed launch, scripts/lcd_timing.py's argument): the
 work-queue k_ransac_coop's grid is its resident waves, not its candidates,
 so the candidates counted are N per timed launch; without N the grid rule of
-the one-workgroup-per-candidate kernel is used."""
+the one-workgroup-per-candidate kernel is used. LAUNCHES (default 4): only
+the first LAUNCHES timed dispatches of each pass count — lcd_timing.py's
+single calls; its back-to-back calls run the next call's kNN2 on a side
+stream concurrently, and the SQ counters of a dispatch then include the
+kNN2 kernel's instructions."""
 import csv, glob, json, os, sys
 from collections import defaultdict
 
@@ -13,20 +17,26 @@ d, out = sys.argv[1], sys.argv[2]
 vals = defaultdict(float)
 disp = set()
 cand = 0
-for p in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
-    seen = set()
-    for r in csv.DictReader(open(p)):
-        if "k_ransac_coop" not in r["Kernel_Name"] or int(r["Grid_Size"]) < 64 * 1000:
-            continue  # the timed launches only (not the 64-candidate warm-up)
-        vals[r["Counter_Name"]] += float(r["Counter_Value"])
-        if r["Dispatch_Id"] not in seen:
-            seen.add(r["Dispatch_Id"])
-    disp |= {len(seen)}
+LAUNCHES = int(sys.argv[4]) if len(sys.argv) > 4 else 4
+for p in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")),
+                key=lambda x: int(os.path.basename(os.path.dirname(x))[1:])):
+    rows = [r for r in csv.DictReader(open(p))
+            if "k_ransac_coop" in r["Kernel_Name"] and int(r["Grid_Size"]) >= 64 * 1000]  # timed launches only
+    keep = sorted({int(r["Dispatch_Id"]) for r in rows})[:LAUNCHES]
+    here = defaultdict(float)
+    for r in rows:
+        if int(r["Dispatch_Id"]) in keep:
+            here[r["Counter_Name"]] += float(r["Counter_Value"])
+    for k, v in here.items():  # a counter collected in two passes counts once (its first pass)
+        if k not in vals:
+            vals[k] = v
+    disp |= {len(keep)}
 # candidates per pass: grid / 64 per launch, 4 launches
 grids = []
 for r in csv.DictReader(open(glob.glob(os.path.join(d, "p1", "run_counter_collection.csv"))[0])):
     if "k_ransac_coop" in r["Kernel_Name"] and int(r["Grid_Size"]) >= 64 * 1000 and r["Counter_Name"] == "SQ_WAVES":
         grids.append(int(r["Grid_Size"]) // 64)
+grids = grids[:LAUNCHES]
 cand = len(grids) * int(sys.argv[3]) if len(sys.argv) > 3 else sum(grids)
 kern = [float(r["TotalDurationNs"]) for r in csv.DictReader(open(os.path.join(d, "stats", "run_kernel_stats.csv")))
         if "k_ransac_coop" in r["Name"]]
