@@ -47,7 +47,7 @@ for step in "$@"; do
       echo -n "$kv: "; python scripts/bench_summary.py "$O/bench_$n.json" ;;
     prof)
       mkdir -p "$O/prof"
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 bench.py \
         > "$O/prof/bench.json" 2> "$O/prof/rocprof.err" || { echo "prof failed"; tail -20 "$O/prof/rocprof.err"; exit 1; }
       find "$O/prof" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$O/kernel_stats.csv"
       head -12 "$O/kernel_stats.csv" | cut -c1-160 ;;
