@@ -1414,6 +1414,22 @@ __device__ __forceinline__ int grp_top(bool pred, int g) {
   return gm ? 63 - __clzll(gm) : -1;
 }
 __device__ __forceinline__ double grp_bcast(double v, int g, int src) { return __shfl(v, g * GL + src, 64); }
+// A broadcast from a fixed group lane: with 16-lane groups (SG <= 4) one DPP
+// row_newbcast move per 32-bit half (each group is a DPP row), else a shuffle.
+// Measured (profiles/r04/lcd/sg4_dpp/): SG = 4 with DPP broadcasts 1.05-1.07e6
+// candidates/s back to back, with shuffles 1.04-1.05e6, SG = 6 (the default,
+// shuffles) 1.18e6: six matrices per pass outweigh the cheaper broadcasts.
+template <int SRC>
+__device__ __forceinline__ double grp_bcast_c(double v, int g) {
+  if constexpr (GL == 16) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x150 + SRC, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x150 + SRC, 0xf, 0xf, false);
+    (void)g;
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+  }
+  return __shfl(v, g * GL + SRC, 64);
+}
 
 // EISPACK ELMHES (Smith et al., EISPACK Guide, 1976; netlib eispack/elmhes.f;
 // oracle/lcd_oracle.c hessenberg10) on sb.H[g] for every group g that is `on`:
@@ -1594,9 +1610,9 @@ __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
           go = false;
         } else {  // p / x, q / x, r / x: one quotient per lane 0-2 of the group, broadcast
           const double quo = (gl == 0 ? p : gl == 1 ? q : r) / x;
-          p = grp_bcast(quo, g, 0);
-          q = grp_bcast(quo, g, 1);
-          r = grp_bcast(quo, g, 2);
+          p = grp_bcast_c<0>(quo, g);
+          q = grp_bcast_c<1>(quo, g);
+          r = grp_bcast_c<2>(quo, g);
         }
       }
       double s = 0.0;
@@ -1615,11 +1631,11 @@ __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
       if (go) {  // p / s, q / s, r / s, q / p, r / p: lanes 0-4 of the group, broadcast
         p = p + s;
         const double quo = (gl == 0 ? p : gl == 1 || gl == 3 ? q : r) / (gl < 3 ? s : p);
-        x = grp_bcast(quo, g, 0);
-        y = grp_bcast(quo, g, 1);
-        zz = grp_bcast(quo, g, 2);
-        q = grp_bcast(quo, g, 3);
-        r = grp_bcast(quo, g, 4);
+        x = grp_bcast_c<0>(quo, g);
+        y = grp_bcast_c<1>(quo, g);
+        zz = grp_bcast_c<2>(quo, g);
+        q = grp_bcast_c<3>(quo, g);
+        r = grp_bcast_c<4>(quo, g);
       }
       if (go && gl >= k && gl <= en) {  // row modification, column j = gl
         const int j = gl;

@@ -19,12 +19,13 @@ def _graph():
     return make_pose_graph(4, 2000, 5000, seed=3)
 
 
-def _params(rel_tol=1e-3):
+def _params(rel_tol=1e-3, form="standard"):
     from kmx.dpgo.params import PGOAgentParameters
     P = PGOAgentParameters(r=5)
     P.robustOptInnerIters = 4
     P.relChangeTol = rel_tol
     P.schedule = 1
+    P.localOptimizationParams.tCG_form = form
     return P
 
 
@@ -40,14 +41,14 @@ def _run(drv, rounds):
     return {a: drv.iterate_of(a) for a in drv.robots}, drv.solver.get_weights()
 
 
-def _worker(rank, world, port, rounds, q, rel_tol):
+def _worker(rank, world, port, rounds, q, rel_tol, form="standard"):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from kmx.dpgo.driver import RBCDDriver
-    g, P = _graph(), _params(rel_tol)
+    g, P = _graph(), _params(rel_tol, form)
     drv = RBCDDriver(P, g, rank=rank, world=world, device=0, exchange_device="cpu")
     drv.initialize(_x0(g))
     X, w = _run(drv, rounds)
@@ -65,11 +66,13 @@ def _free_port():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("rel_tol", [1e-3, 30.0])
-def test_two_ranks_one_gpu_match_single_process(gpu, rel_tol):
+@pytest.mark.parametrize("rel_tol,form", [(1e-3, "standard"), (30.0, "standard"), (1e-3, "onesync")])
+def test_two_ranks_one_gpu_match_single_process(gpu, rel_tol, form):
+    """(onesync: the opt-in one-sync tCG keeps the same placement independence:
+    its 8-wide robot sums are ordered like the standard form's.)"""
     from kmx.dpgo.driver import RBCDDriver
     rounds = 11
-    g, P = _graph(), _params(rel_tol)
+    g, P = _graph(), _params(rel_tol, form)
     drv = RBCDDriver(P, g, device=0)
     drv.initialize(_x0(g))
     X1, w1 = _run(drv, rounds)
@@ -77,7 +80,7 @@ def test_two_ranks_one_gpu_match_single_process(gpu, rel_tol):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q, rel_tol), daemon=True) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, rounds, q, rel_tol, form), daemon=True) for r in range(2)]
     for p in procs:
         p.start()
     results = []

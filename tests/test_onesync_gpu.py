@@ -123,6 +123,33 @@ def test_onesync_large_robot_block(gpu):
         s.close()
 
 
+@pytest.mark.parametrize("robust", [False, True])
+def test_onesync_accelerated_rounds_match_oracle(gpu, robust):
+    """Nesterov-accelerated RBCD with the one-sync tCG: the extrapolated point
+    the round starts from and the momentum update around it are the standard
+    form's; the rounds match the restatement's same form across two restarts."""
+    g, P, X0 = _setup(robust=robust)
+    _onesync(P)
+    P.acceleration, P.restartInterval = True, 5
+    s, o = _pair(g, P, X0)
+    try:
+        for it in range(12):
+            s.refresh_local()
+            sg = s.iterate()
+            so = o.iterate()
+            for a in range(g.n_robots):
+                assert sg[a]["tcg_iterations"] == so[a]["tcg_iterations"], (it, a, sg[a], so[a])
+                d = np.linalg.norm((s.get_iterate(a) - o.get_iterate(a)).reshape(-1, 4 * P.r), axis=1).max()
+                assert d <= 1e-6, (it, a, d)
+            if robust and it % 4 == 3:
+                s.refresh_local()
+                o.accel_pre()
+                o.refresh()
+                assert s.update_weights() == o.update_weights()
+    finally:
+        s.close()
+
+
 def test_onesync_poll_modes_agree_bitwise(gpu):
     g, P, X0 = _setup(robust=True, seed=6)
     _onesync(P)
@@ -198,6 +225,7 @@ def test_onesync_configs1_converged(gpu):
     try:
         assert n_std < 1500 and n_os < 1500, (n_std, n_os)
         assert abs(n_os - n_std) <= 0.1 * n_std, (n_os, n_std)
+        print(f"configs[1] rounds to converge: standard {n_std}, one-sync {n_os}")
         from tests.test_parity_long_gpu import _trajectories_agree
         _trajectories_agree(s, o, g, Y, P.r)
     finally:
