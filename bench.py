@@ -69,7 +69,9 @@ def parse():
     ap.add_argument("--tcg-form", choices=["standard", "onesync"], default="standard",
                     help="tCG form (kmx_pgo_params.tcg_form): ROPTLIB's, or the opt-in one-sync form")
     ap.add_argument("--lcd-frames", type=int, default=50_000)
-    ap.add_argument("--lcd-steps", type=int, default=3)
+    ap.add_argument("--lcd-steps", type=int, default=8,
+                    help="back-to-back LCD verification calls timed (a call's kNN2 overlaps the previous call's "
+                         "RANSAC tail on the detector's second candidate slot, as in a stream of queries)")
     ap.add_argument("--lcd-algo", type=int, default=0,
                     help="ransac_2d2d_algorithm: 0 Stewenius (the reference config, LcdParams.yaml:73), 1 Nister")
     return ap.parse_args()
