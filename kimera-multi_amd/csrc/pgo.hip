@@ -1581,6 +1581,68 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
   });
 }
 
+// eta = sum_k coef_k delta_k over a tCG's T directions, in step order (the
+// first F were folded into d.eta by the Hess-vec launches), added to et. LAST:
+// the coefficient of direction T - 1 is clast (a k_step that ends the tCG
+// decided it in the same launch whose writer stores it to coefh).
+template <bool LAST>
+__device__ __forceinline__ void eta_rows(const Dev& d, int l, size_t o, int T, double clast, double et[4]) {
+  const int dhn = d.dhn;
+  const int F = T > 0 ? (T - 1) / dhn * dhn : 0;
+  if (F > 0) load4(d.eta + o, et);
+  double dd[DHMAX][4];
+#pragma unroll
+  for (int i = 0; i < DHMAX; ++i)
+    if (F + i < T) load4(d.dh + (size_t)i * d.vec + o, dd[i]);
+  const double* ch = d.coefh + (size_t)l * d.p.tcg_max;
+#pragma unroll
+  for (int i = 0; i < DHMAX; ++i)
+    if (F + i < T) {
+      const double cj = (LAST && F + i == T - 1) ? clast : ch[F + i];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) et[k] += cj * dd[i][k];
+    }
+}
+
+// The trial point Xt = R_X(eta) of the lane's row, and the tile's partials
+// m(eta) = 1/2 <eta, g + r> (as 2 m) and ||Xt - X||^2 into d.part slots 2, 3
+// (k_cost adds the cost in slot 0). Every lane of the workgroup calls it.
+template <int R>
+__device__ __forceinline__ void trial_rows(const Dev& d, const Lane& L, size_t o, const double x[4],
+                                           const double gg[4], const double rr[4], const double et[4], char* smem) {
+  double xt[4];
+  group_retract<R>(x, et, L.base, xt);
+  double vals[2] = {0.0, 0.0};
+  if (L.valid) {
+    store4(d.Xt + o, xt);
+    double m = 0.0, ch = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      m += et[k] * (gg[k] + rr[k]);
+      const double dd = xt[k] - x[k];
+      ch += dd * dd;
+    }
+    vals[0] = m;
+    vals[1] = ch;
+  }
+  double* lds = reinterpret_cast<double*>(smem);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const double w = wave_sum(vals[s]);
+    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      double t = 0.0;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
+      d.part[(size_t)L.tile * NPART + 2 + s] = t;
+    }
+  }
+}
+
 // ------------------------------------------------ one-sync tCG (opt-in) ---
 // P.tcg_form = KMX_TCG_FORM_ONESYNC: one kernel per tCG step (k_step), so a
 // step has one grid-wide dependency instead of two (k_hess -> k_update ->
@@ -1771,15 +1833,23 @@ __device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cou
   double H[4];
   PlainRows<R> src{V};
   const bool go = hinc_gather_src<R, RW, false, PlainRows<R>, decltype(decide)&, false>(d, L, src, H, smem, decide);
-  if (!grad && !go) {  // the robot's tCG ends here: the last step's residual (k_retract's model)
+  if (!grad && !go) {
+    // the robot's tCG ends here: the last step's residual, then (no k_retract
+    // in this form) the trial point of its rows and the model partials, with
+    // this launch's coefficient for the last direction
+    double x[4] = {0, 0, 0, 0}, gg[4] = {0, 0, 0, 0}, rr[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0};
     if (L.valid) {
-      double rr[4], hd[4];
+      double hd[4];
       load4(d.r + o, rr);
       load4(d.hd + o, hd);
+      load4(d.X + o, x);
+      load4(d.g + o, gg);
 #pragma unroll
       for (int c = 0; c < 4; ++c) rr[c] = fma(coef, hd[c], rr[c]);
       store4(d.r + o, rr);
+      eta_rows<true>(d, L.l, o, k + 1, coef, et);
     }
+    trial_rows<R>(d, L, o, x, gg, rr, et, smem);
     return;
   }
   if (!go) return;
@@ -1961,62 +2031,21 @@ __device__ __forceinline__ void body_retract(const Dev& d, int fold, const Ctl* 
 #pragma unroll
       for (int k = 0; k < 4; ++k) et[k] += coef * dl[k];
     } else {
-      // eta = sum_k coef_k delta_k over the T steps, in step order; the first
-      // F directions were folded into d.eta by k_hess (tcg_max > dhn only)
-      const int T = c.tcg_iter, dhn = d.dhn;
-      const int F = T > 0 ? (T - 1) / dhn * dhn : 0;
-      if (F > 0) load4(d.eta + o, et);
-      double dd[DHMAX][4];
-#pragma unroll
-      for (int i = 0; i < DHMAX; ++i)
-        if (F + i < T) load4(d.dh + (size_t)i * d.vec + o, dd[i]);
-      const double* ch = d.coefh + (size_t)L.l * d.p.tcg_max;
-#pragma unroll
-      for (int i = 0; i < DHMAX; ++i)
-        if (F + i < T) {
-          const double cj = ch[F + i];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) et[k] += cj * dd[i][k];
-        }
+      eta_rows<false>(d, L.l, o, c.tcg_iter, 0.0, et);
     }
   }
-  double xt[4];
-  group_retract<R>(x, et, L.base, xt);
-  double vals[2] = {0.0, 0.0};
-  if (L.valid) {
-    store4(d.Xt + o, xt);
-    double m = 0.0, ch = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      m += et[k] * (gg[k] + rr[k]);
-      const double dd = xt[k] - x[k];
-      ch += dd * dd;
-    }
-    vals[0] = m;
-    vals[1] = ch;
-  }
-  double* lds = reinterpret_cast<double*>(smem);
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const double w = wave_sum(vals[s]);
-    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      double t = 0.0;
-#pragma unroll
-      for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
-      d.part[(size_t)L.tile * NPART + 2 + s] = t;
-    }
-  }
+  trial_rows<R>(d, L, o, x, gg, rr, et, smem);
 }
 
+// src: as k_retract's (the one-sync form has no k_retract: its k_step
+// retracts a robot's rows in the launch that ends its tCG, so k_cost carries
+// the state over to d.ctl).
 template <int R, int RW, int RM>
-__device__ __forceinline__ void body_cost(const Dev& d, char* smem) {
+__device__ __forceinline__ void body_cost(const Dev& d, const Ctl* src, char* smem) {
   const Lane L = lane_map<R>(d);
-  if (d.ctl[L.l].phase != PH_STEP) return;
+  const Ctl& c = src[L.l];
+  if (src != d.ctl && threadIdx.x == 0 && L.tile == L.rt0) d.ctl[L.l] = c;
+  if (c.phase != PH_STEP) return;
   double cost = inc_owner_cost<R, RW>(d, L, d.Xt, d.pub, smem);
   finish_tile<RED_COST, 1, RM>(d, L, &cost, smem + SmemC<R>::red_off, []() {});
 }
@@ -2114,9 +2143,9 @@ __global__ __launch_bounds__(BLOCK) void k_retract(Dev d, int fold, const Ctl* s
   body_retract<R>(d, fold, src, smem);
 }
 template <int R, int RW, int RM>
-__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d) {
+__global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d, const Ctl* src) {
   KMX_SMEM;
-  body_cost<R, RW, RM>(d, smem);
+  body_cost<R, RW, RM>(d, src, smem);
 }
 template <int R>
 __global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
@@ -3003,11 +3032,15 @@ void enqueue_trial_t(kmx_pgo* h, bool rgd) {
   const dim3 grid(h->ntiles), blk(BLOCK);
   // RM_CONSUMER: the last step's update has no k_hess after it; k_retract
   // reduces it
-  const bool os = RM == RM_CONSUMER && !rgd && onesync(h);  // no update left to fold: k_step decided it
+  // one-sync form: each k_step that ended a robot's tCG also formed its trial
+  // point, so there is no k_retract; k_cost takes the state from where the
+  // tCG left it
+  const bool os = RM == RM_CONSUMER && !rgd && onesync(h);
   const Ctl* src = os && h->ctl_par ? h->d_ctl2 : h->d_ctl;
-  hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv, RM == RM_CONSUMER && !rgd && !os ? 1 : 0,
-                     src);
-  hipLaunchKernelGGL((k_cost<R, RW, RM>), grid, blk, SmemC<R>::bytes, h->stream, h->dv);
+  if (!os)
+    hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv, RM == RM_CONSUMER && !rgd ? 1 : 0,
+                       (const Ctl*)h->d_ctl);
+  hipLaunchKernelGGL((k_cost<R, RW, RM>), grid, blk, SmemC<R>::bytes, h->stream, h->dv, src);
   if (!fold_cost<RM>(h)) red_t<R, RM>(h, RED_COST);
 }
 

@@ -390,12 +390,16 @@ def test_long_tcg_folds_directions(gpu, monkeypatch, red):
     assert longest > 10, longest  # the fold ran
 
 
-def test_large_robot_block_matches_oracle(gpu):
+@pytest.mark.parametrize("tile_incidences", [0, 60])
+def test_large_robot_block_matches_oracle(gpu, tile_incidences):
     """One 12.5k-pose robot block (the per-GPU share of configs[3] at N = 8): the
     finer tile cut gives it ~700 tiles, more than the 2 x 256 partials the
-    consumer kernels' one-shot robot sums hold, so every folded reduction takes
-    the looped robot_sum path; rounds (GNC on) still match the restatement."""
+    consumer k_hess's one-shot robot sums hold, so its folded reductions take
+    the looped robot_sum path (k_update's four-tile-per-thread sum holds them);
+    with 60 incidences per tile (~2,100 tiles) every consumer sum loops. Rounds
+    (GNC on) still match the restatement."""
     g, P, X0 = _setup(n_robots=1, n=12_500, m=62_500, seed=5)
+    P.tileIncidences = tile_incidences
     s, o = _pair(g, P, X0)
     for it in range(4):
         s.refresh_local()

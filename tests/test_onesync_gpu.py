@@ -105,11 +105,14 @@ def test_onesync_long_tcg_folds_directions(gpu):
         s.close()
 
 
-def test_onesync_large_robot_block(gpu):
-    """One 12.5k-pose block (~700 tiles): every k_step reduces the robot's
-    8-wide partials over more tiles than one pass of RobotSum8 holds."""
+@pytest.mark.parametrize("tile_incidences", [0, 60])
+def test_onesync_large_robot_block(gpu, tile_incidences):
+    """One 12.5k-pose block: ~700 tiles with the automatic cut (one pass of
+    RobotSum8, four tiles per thread), ~2,100 with 60 incidences per tile (more
+    than the 1,024 one pass holds: the looped path)."""
     g, P, X0 = _setup(n_robots=1, n=12_500, m=62_500, seed=5)
     _onesync(P)
+    P.tileIncidences = tile_incidences
     s, o = _pair(g, P, X0)
     try:
         for it in range(4):
