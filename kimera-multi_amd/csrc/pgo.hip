@@ -71,7 +71,7 @@ enum RedKind { RED_GRAD = 0, RED_HESS = 1, RED_UPDATE = 2, RED_COST = 3 };
 struct Ctl {
   int phase, rtr_iter, tcg_iter, tcg_stop;
   int mode, accepted, commit, updated;
-  int hessvecs, skipped, pad0, pad1;
+  int hessvecs, skipped, retracted, pad1;  // retracted: the consumer k_update formed the trial point
   double Delta, f_init, gn_init, f_cur;
   double f_final, norm_r0, z_r, e_Pe;
   double e_Pd, d_Pd, alpha, beta;
@@ -1039,6 +1039,7 @@ __device__ __forceinline__ void control_core(Ctl& c, const Dev& d, int l, int ki
     }
     c.rtr_iter += 1;
     c.phase = (c.rtr_iter < P.rtr_iters) ? PH_START : PH_IDLE;
+    c.retracted = 0;
     c.rel_change = sqrt(c.chg_acc / (double)d.n_robot[l]);
     if (side && c.phase == PH_IDLE) d.relc[l] = c.rel_change;  // the team status of dpgo's getStatus
   }
@@ -1342,6 +1343,68 @@ __device__ __forceinline__ void body_grad(const Dev& d, int gated, char* smem) {
   });
 }
 
+// eta = sum_k coef_k delta_k over a tCG's T directions, in step order (the
+// first F were folded into d.eta by the Hess-vec launches), added to et. LAST:
+// the coefficient of direction T - 1 is clast (a k_step that ends the tCG
+// decided it in the same launch whose writer stores it to coefh).
+template <bool LAST>
+__device__ __forceinline__ void eta_rows(const Dev& d, int l, size_t o, int T, double clast, double et[4]) {
+  const int dhn = d.dhn;
+  const int F = T > 0 ? (T - 1) / dhn * dhn : 0;
+  if (F > 0) load4(d.eta + o, et);
+  double dd[DHMAX][4];
+#pragma unroll
+  for (int i = 0; i < DHMAX; ++i)
+    if (F + i < T) load4(d.dh + (size_t)i * d.vec + o, dd[i]);
+  const double* ch = d.coefh + (size_t)l * d.p.tcg_max;
+#pragma unroll
+  for (int i = 0; i < DHMAX; ++i)
+    if (F + i < T) {
+      const double cj = (LAST && F + i == T - 1) ? clast : ch[F + i];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) et[k] += cj * dd[i][k];
+    }
+}
+
+// The trial point Xt = R_X(eta) of the lane's row, and the tile's partials
+// m(eta) = 1/2 <eta, g + r> (as 2 m) and ||Xt - X||^2 into d.part slots 2, 3
+// (k_cost adds the cost in slot 0). Every lane of the workgroup calls it.
+template <int R>
+__device__ __forceinline__ void trial_rows(const Dev& d, const Lane& L, size_t o, const double x[4],
+                                           const double gg[4], const double rr[4], const double et[4], char* smem) {
+  double xt[4];
+  group_retract<R>(x, et, L.base, xt);
+  double vals[2] = {0.0, 0.0};
+  if (L.valid) {
+    store4(d.Xt + o, xt);
+    double m = 0.0, ch = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      m += et[k] * (gg[k] + rr[k]);
+      const double dd = xt[k] - x[k];
+      ch += dd * dd;
+    }
+    vals[0] = m;
+    vals[1] = ch;
+  }
+  double* lds = reinterpret_cast<double*>(smem);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const double w = wave_sum(vals[s]);
+    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      double t = 0.0;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
+      d.part[(size_t)L.tile * NPART + 2 + s] = t;
+    }
+  }
+}
+
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old;
 // partial <delta, Hdelta>. delta_k is kept for k_retract's eta (Dev::dh).
@@ -1517,6 +1580,27 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
     if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))  // as in k_hess
       reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(&cq)[threadIdx.x];
     if (cq.phase != PH_TCG) {
+      if (cq.phase == PH_STEP && !cq.retracted) {
+        // this step's k_hess ended the robot's tCG at its stop test: the trial
+        // point and the model partials here (k_retract's arithmetic; every
+        // coefficient was decided by an earlier launch), so a round whose
+        // robots all stop this way needs no k_retract (the host skips it, or
+        // launches it with fold = 2 for the robots still in tCG at the cap)
+        const size_t o2 = (size_t)L.pose * 4 * R + 4 * L.a;
+        double x[4] = {0, 0, 0, 0}, gg[4] = {0, 0, 0, 0}, rr2[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0};
+        if (L.valid) {
+          load4(d.X + o2, x);
+          load4(d.g + o2, gg);
+          load4(d.r + o2, rr2);
+          eta_rows<false>(d, L.l, o2, cq.tcg_iter, 0.0, et);
+        }
+        trial_rows<R>(d, L, o2, x, gg, rr2, et, smem);
+        if (writer && threadIdx.x == 0) {
+          cout[L.l] = cq;
+          cout[L.l].retracted = 1;
+        }
+        return;
+      }
       if (writer && threadIdx.x == 0) cout[L.l] = cq;
       return;
     }
@@ -1579,68 +1663,6 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
       if (interior) store4(d.z + o, zr);
     }
   });
-}
-
-// eta = sum_k coef_k delta_k over a tCG's T directions, in step order (the
-// first F were folded into d.eta by the Hess-vec launches), added to et. LAST:
-// the coefficient of direction T - 1 is clast (a k_step that ends the tCG
-// decided it in the same launch whose writer stores it to coefh).
-template <bool LAST>
-__device__ __forceinline__ void eta_rows(const Dev& d, int l, size_t o, int T, double clast, double et[4]) {
-  const int dhn = d.dhn;
-  const int F = T > 0 ? (T - 1) / dhn * dhn : 0;
-  if (F > 0) load4(d.eta + o, et);
-  double dd[DHMAX][4];
-#pragma unroll
-  for (int i = 0; i < DHMAX; ++i)
-    if (F + i < T) load4(d.dh + (size_t)i * d.vec + o, dd[i]);
-  const double* ch = d.coefh + (size_t)l * d.p.tcg_max;
-#pragma unroll
-  for (int i = 0; i < DHMAX; ++i)
-    if (F + i < T) {
-      const double cj = (LAST && F + i == T - 1) ? clast : ch[F + i];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) et[k] += cj * dd[i][k];
-    }
-}
-
-// The trial point Xt = R_X(eta) of the lane's row, and the tile's partials
-// m(eta) = 1/2 <eta, g + r> (as 2 m) and ||Xt - X||^2 into d.part slots 2, 3
-// (k_cost adds the cost in slot 0). Every lane of the workgroup calls it.
-template <int R>
-__device__ __forceinline__ void trial_rows(const Dev& d, const Lane& L, size_t o, const double x[4],
-                                           const double gg[4], const double rr[4], const double et[4], char* smem) {
-  double xt[4];
-  group_retract<R>(x, et, L.base, xt);
-  double vals[2] = {0.0, 0.0};
-  if (L.valid) {
-    store4(d.Xt + o, xt);
-    double m = 0.0, ch = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      m += et[k] * (gg[k] + rr[k]);
-      const double dd = xt[k] - x[k];
-      ch += dd * dd;
-    }
-    vals[0] = m;
-    vals[1] = ch;
-  }
-  double* lds = reinterpret_cast<double*>(smem);
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const double w = wave_sum(vals[s]);
-    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      double t = 0.0;
-#pragma unroll
-      for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
-      d.part[(size_t)L.tile * NPART + 2 + s] = t;
-    }
-  }
 }
 
 // ------------------------------------------------ one-sync tCG (opt-in) ---
@@ -2007,7 +2029,7 @@ __device__ __forceinline__ void body_retract(const Dev& d, int fold, const Ctl* 
   const int ph = sph;  // one read per workgroup
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   double x[4] = {0, 0, 0, 0}, et[4] = {0, 0, 0, 0}, gg[4] = {0, 0, 0, 0}, rr[4] = {0, 0, 0, 0}, dl[4];
-  if (fold && ph == PH_TCG) {
+  if (fold && ph == PH_TCG) {  // fold 2: a robot at PH_STEP may already be retracted (k_update)
     RobotSum<2> rs;
     rs.issue(d.part_u, 2, L.rt0, L.rt1);
     double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
@@ -2018,7 +2040,7 @@ __device__ __forceinline__ void body_retract(const Dev& d, int fold, const Ctl* 
       if (u.stop >= 0) d.ctl[L.l].tcg_stop = u.stop;
       d.ctl[L.l].phase = PH_STEP;
     }
-  } else if (ph != PH_STEP) {
+  } else if (ph != PH_STEP || (fold == 2 && c.retracted)) {
     return;
   }
   if (L.valid) {  // all rows in flight before the Gram-Schmidt chain
@@ -2624,6 +2646,7 @@ struct kmx_pgo {
   double* d_coefh = nullptr;  // [L][tcg_max]
   double* d_part_f = nullptr;  // [ntiles][8] one-sync tCG partials (P.tcg_form)
   int ctl_par = 0;             // one-sync tCG: the state after the last tCG loop is in ctl2 (odd step count)
+  bool tcg_stopped = false;    // consumer tCG loop saw every robot stop (each was retracted by its k_update)
   double *d_S = nullptr, *d_Pinv = nullptr, *d_hD = nullptr, *d_pub = nullptr, *d_part = nullptr;
   Ctl* d_ctl = nullptr;
   Ctl* d_ctl2 = nullptr;
@@ -2950,6 +2973,7 @@ void enqueue_tcg_t(kmx_pgo* h) {
   }
   const int tmax = h->P.tcg_max_iterations;
   int steps = tmax;  // steps enqueued by a polled loop
+  h->tcg_stopped = false;
   if constexpr (RM == RM_CONSUMER) {
     if (onesync(h)) {
       // one k_step per step: launch j applies step j-1's decision (which it
@@ -3005,6 +3029,7 @@ void enqueue_tcg_t(kmx_pgo* h) {
       hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, 0ull, slot);
       if (poll && j > 0 && !wait_running(h, seq)) {
         steps = j + 1;
+        h->tcg_stopped = true;
         break;
       }
       continue;
@@ -3037,9 +3062,13 @@ void enqueue_trial_t(kmx_pgo* h, bool rgd) {
   // tCG left it
   const bool os = RM == RM_CONSUMER && !rgd && onesync(h);
   const Ctl* src = os && h->ctl_par ? h->d_ctl2 : h->d_ctl;
-  if (!os)
-    hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv, RM == RM_CONSUMER && !rgd ? 1 : 0,
-                       (const Ctl*)h->d_ctl);
+  // consumer form: the k_update after the k_hess that stopped a robot formed
+  // its trial point; k_retract (fold 2) decides and retracts the robots still
+  // in tCG at the cap, and is not needed when the polled loop saw every robot
+  // stop
+  const bool cons = RM == RM_CONSUMER && !rgd;
+  if (!os && !(cons && h->tcg_stopped))
+    hipLaunchKernelGGL((k_retract<R>), grid, blk, SmemU::bytes, h->stream, h->dv, cons ? 2 : 0, (const Ctl*)h->d_ctl);
   hipLaunchKernelGGL((k_cost<R, RW, RM>), grid, blk, SmemC<R>::bytes, h->stream, h->dv, src);
   if (!fold_cost<RM>(h)) red_t<R, RM>(h, RED_COST);
 }
