@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--no-lcd", action="store_true")
     ap.add_argument("--no-replay", action="store_true", help="skip the evented replay (roofline)")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3: timed rounds only")
+    ap.add_argument("--tile-incidences", type=int, default=0,
+                    help="incidences per workgroup tile (kmx_pgo_params.tile_incidences; 0: automatic)")
     ap.add_argument("--tcg-form", choices=["standard", "onesync"], default="standard",
                     help="tCG form (kmx_pgo_params.tcg_form): ROPTLIB's, or the opt-in one-sync form")
     ap.add_argument("--lcd-frames", type=int, default=50_000)
@@ -588,6 +590,7 @@ def main():
 
     P = params()
     P.localOptimizationParams.tCG_form = args.tcg_form
+    P.tileIncidences = args.tile_incidences
     headline = args.scaling if world > 1 else "strong"
     t_gen = time.perf_counter()
     g, X0 = make_workload(args.config, world, headline)

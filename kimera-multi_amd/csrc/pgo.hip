@@ -2708,7 +2708,7 @@ struct kmx_pgo {
   // generations of workgroups, each waiting for its robot's sums)
   int rm = RM_LAUNCH;
   int rm_forced = -1;
-  int early_stop = 1, early_forced = -1;  // KMX_EARLY
+  int early_stop = 1;
   static constexpr int RM_CONSUMER_MAX_POSES = 80000;
   bool poll_timeout = false;
   // timing
@@ -3199,7 +3199,6 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     return kmx::fail(KMX_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
   h->own_stream = true;
-  if (const char* v = std::getenv("KMX_EARLY")) h->early_forced = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("KMX_RED")) {
     const int m = std::atoi(v);
     h->rm_forced = m == 0 ? RM_LAUNCH : m == 2 ? RM_CONSUMER : -1;  // 1 and 3 (tickets, half) were removed
@@ -3278,7 +3277,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   h->nloc = nloc;
   h->rm = h->rm_forced >= 0 ? h->rm_forced : (nloc <= kmx_pgo::RM_CONSUMER_MAX_POSES ? RM_CONSUMER : RM_LAUNCH);
   if (onesync(h)) h->rm = RM_CONSUMER;  // its decisions are taken by every workgroup
-  h->early_stop = h->early_forced >= 0 ? h->early_forced : (nloc <= kmx_pgo::RM_CONSUMER_MAX_POSES ? 1 : 0);
+  h->early_stop = nloc <= kmx_pgo::RM_CONSUMER_MAX_POSES ? 1 : 0;  // decide before the gather on small problems
   const int L = (int)h->robots.size();
   KMX_CHECK(L > 0, KMX_EINVAL, "no local robot");
   KMX_CHECK(L <= 1024, KMX_EUNSUP, "at most 1024 local robots per handle");
@@ -3440,12 +3439,12 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   // 480 / 360 / 240 / 180, 207 at 120 (> 1024 tiles: a second generation);
   // 25k poses: 254.7 at 480, 245.6 at 360, 301 at 240
   // (profiles/r02/small_round/5_tile_cap.log). kmx_pgo_params.tile_incidences
-  // (the multi-rank driver sets it from the team) or KMX_TILE_CAP override.
+  // overrides it (the multi-rank driver sets it from the team; bench.py
+  // --tile-incidences for sweeps).
   int64_t inc_all = (int64_t)inc_ptr[nloc] - inc_ptr[0];
   int64_t tilecap = std::min<int64_t>(2 * (int64_t)TP * r,
                                       std::max<int64_t>(180, (inc_all + TILES_TARGET - 1) / TILES_TARGET));
   if (h->P.tile_incidences > 0) tilecap = std::max(16, h->P.tile_incidences);
-  if (const char* v = std::getenv("KMX_TILE_CAP")) tilecap = std::max(16, std::atoi(v));
   for (int l = 0; l < L; ++l) {
     const int n = n_poses[h->robots[l]];
     const int base = h->loff[l];
@@ -3473,8 +3472,6 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   h->rt0_h = rt0;
   h->ntiles = (int)tr.size();
   KMX_CHECK(h->ntiles > 0, KMX_EINVAL, "no local poses");
-  if (std::getenv("KMX_TILE_CAP"))  // A/B sweeps (scripts/gpu_tile_sweep.sh) log the cut they ran
-    std::fprintf(stderr, "kmx: %d tiles at %lld incidences per tile (cap)\n", h->ntiles, (long long)tilecap);
   std::vector<int> own_src(std::max<int64_t>(h->n_owned, 1), 0);
   for (int64_t k = 0; k < h->n_owned; ++k) own_src[k] = pub_src[h->first_owned + k];
   std::vector<int> nrob(L);

@@ -1,5 +1,5 @@
-# Round time and k_hess roofline against the tile cut (KMX_TILE_CAP: incidences
-# per workgroup tile; the default cut gives 2,084 tiles at configs[3], i.e. two
+# Round time and k_hess roofline against the tile cut (bench.py --tile-incidences:
+# incidences per workgroup tile; the default cut gives 2,084 tiles at configs[3], i.e. two
 # generations of the 1,024 resident k_hess workgroups plus 36 tiles).
 # usage: bash scripts/gpu_tile_sweep.sh TAG cap...
 set -o pipefail
@@ -8,10 +8,9 @@ export TMPDIR=/tmp
 T=${1:-tiles}; shift
 mkdir -p gpurun_out/$T
 for cap in "$@"; do
-  if [ "$cap" = default ]; then unset KMX_TILE_CAP; else export KMX_TILE_CAP=$cap; fi
-  timeout -k 10 300 python bench.py --no-cpu --no-lcd --steps 200 > gpurun_out/$T/cap_$cap.json 2> gpurun_out/$T/cap_$cap.err \
+  if [ "$cap" = default ]; then ti=0; else ti=$cap; fi
+  timeout -k 10 300 python bench.py --no-cpu --no-lcd --steps 200 --tile-incidences $ti > gpurun_out/$T/cap_$cap.json 2> gpurun_out/$T/cap_$cap.err \
     || { echo "cap $cap failed"; tail -5 gpurun_out/$T/cap_$cap.err; exit 1; }
-  grep -h "tiles at" gpurun_out/$T/cap_$cap.err | head -1 | tee -a gpurun_out/$T/summary.txt
   python3 - "$T" "$cap" <<'PY' | tee -a gpurun_out/$T/summary.txt
 import json, sys
 t, cap = sys.argv[1], sys.argv[2]
