@@ -45,10 +45,21 @@ constexpr int RS_MAX_SLOTS = 8192;    // k_ransac_coop waves per launch at most 
 constexpr int MAX_FEATS = 1024;
 
 // ------------------------------------------------------------------ knn2 --
-__global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const int* nfeat, int N,
-                                                    const int* cq, const int* cm, int norm, double lowe,
-                                                    int2* pairs, int* Kout) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t sm_u32[];
+// The two-nearest update of ordered keys k0 <= k1 with a new key: k1' is the
+// median of (k0, key, k1) (one v_med3_u32 in place of a max and a min), k0'
+// the minimum. Same keys, same result as the min / max form.
+__device__ __forceinline__ void two_nearest(uint32_t& k0, uint32_t& k1, uint32_t key) {
+  uint32_t m;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m) : "v"(k0), "v"(key), "v"(k1));
+  k1 = m;
+  k0 = min(k0, key);
+}
+
+// The norm is a template parameter so the inner loop carries no branch on it
+// (the runtime form evaluated the test twice per match descriptor).
+template <bool HAMMING>
+__device__ __forceinline__ void knn2_body(const uint32_t* desc, const int* nfeat, int N, const int* cq, const int* cm,
+                                          double lowe, int2* pairs, int* Kout, uint32_t* sm_u32) {
   uint32_t* sdesc = sm_u32;                    // [nm][8]
   int* scnt = reinterpret_cast<int*>(sm_u32 + (size_t)N * 8);  // [KNN_BLOCK + 1]
   const int c = blockIdx.x;
@@ -69,11 +80,11 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const 
   // distance <= 32 x 255 < 2^13, index < 1024): the smallest key is the first
   // match at the smallest distance and the second smallest carries the second
   // distance (a repeat of the first included) — the serial scan's d0 / j0 / d1
-  // with its strict tests — in three min / max operations per pair. Each match
-  // descriptor read from LDS serves two of the thread's queries.
+  // with its strict tests — in two operations per pair (two_nearest). Each
+  // match descriptor read from LDS serves two of the thread's queries.
   auto dist = [&](const uint32_t a[8], const uint32_t b[8]) -> uint32_t {
     uint32_t d = 0;
-    if (norm == KMX_NORM_HAMMING) {
+    if constexpr (HAMMING) {
 #pragma unroll
       for (int w = 0; w < 8; ++w) d += __popc(a[w] ^ b[w]);
     } else {
@@ -99,12 +110,8 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const 
         const uint4* b4 = reinterpret_cast<const uint4*>(sdesc + j * 8);
         const uint4 x = b4[0], y = b4[1];
         const uint32_t b[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-        const uint32_t ka = (dist(a0, b) << 10) | (uint32_t)j, kb = (dist(a1, b) << 10) | (uint32_t)j;
-        const uint32_t ta = max(k00, ka), tb = max(k10, kb);
-        k00 = min(k00, ka);
-        k01 = min(k01, ta);
-        k10 = min(k10, kb);
-        k11 = min(k11, tb);
+        two_nearest(k00, k01, (dist(a0, b) << 10) | (uint32_t)j);
+        two_nearest(k10, k11, (dist(a1, b) << 10) | (uint32_t)j);
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -136,6 +143,14 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const 
   for (int u = 0; u < 4; ++u)
     if (i0 + u < i1 && pass[u]) out[pos++] = make_int2(i0 + u, bestj[u]);
   if (threadIdx.x == 0) Kout[c] = scnt[KNN_BLOCK];
+}
+
+__global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const int* nfeat, int N,
+                                                    const int* cq, const int* cm, int norm, double lowe,
+                                                    int2* pairs, int* Kout) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm_u32[];
+  if (norm == KMX_NORM_HAMMING) knn2_body<true>(desc, nfeat, N, cq, cm, lowe, pairs, Kout, sm_u32);
+  else knn2_body<false>(desc, nfeat, N, cq, cm, lowe, pairs, Kout, sm_u32);
 }
 
 // --------------------------------------------------- small linear algebra --
