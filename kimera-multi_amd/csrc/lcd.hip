@@ -2504,13 +2504,23 @@ struct kmx_lcd {
   // (on kstream) can run while the previous call's RANSAC drains (stream);
   // d_cq .. d_order below point into the current slot
   int cap = 0, cur = 0;
+  // Each slot's RANSAC runs on its own stream (slot 0: the handle's stream,
+  // slot 1: rsx) with its own work-queue counter and per-wave scratch, so the
+  // next call's RANSAC takes the CUs the previous call's drains (its last
+  // candidates, finishing alone) leave idle.
   struct Slot {
     int *cq = nullptr, *cm = nullptr, *K = nullptr, *hyps = nullptr, *nrec = nullptr, *order = nullptr;
     int2* pairs = nullptr;
     kmx_lcd_result* res = nullptr;
     unsigned char* mask = nullptr;
     double* prior = nullptr;
+    double* fbuf = nullptr;
+    int* next = nullptr;
   } slot[2];
+  hipStream_t rsx = nullptr;      // slot 1's RANSAC stream
+  bool rs_conc = true;            // KMX_LCD_RSX=0: both slots on the handle's stream (A/B switch)
+  bool rs_on = false;             // this call's slot runs on rsx
+  int cus = 0;
   hipStream_t kstream = nullptr;  // kNN2 of kmx_lcd_verify / _async
   hipEvent_t ev_knn[2] = {nullptr, nullptr}, ev_rs[2] = {nullptr, nullptr};
   bool ev_rs_set[2] = {false, false};
@@ -2542,6 +2552,7 @@ namespace {
 
 void lcd_free_frames(kmx_lcd* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);  // a verification in flight may read the pool
+  if (h->rsx) (void)hipStreamSynchronize(h->rsx);
   if (h->kstream) (void)hipStreamSynchronize(h->kstream);
   void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat};
   for (void* x : p)
@@ -2558,15 +2569,14 @@ void lcd_free_tables(kmx_lcd* h) {
 }
 void lcd_free_cand(kmx_lcd* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);  // in-flight calls may still use the buffers
+  if (h->rsx) (void)hipStreamSynchronize(h->rsx);
   if (h->kstream) (void)hipStreamSynchronize(h->kstream);
   for (auto& sl : h->slot) {
-    void* p[] = {sl.cq, sl.cm, sl.K, sl.hyps, sl.nrec, sl.order, sl.pairs, sl.res, sl.mask, sl.prior};
+    void* p[] = {sl.cq, sl.cm, sl.K, sl.hyps, sl.nrec, sl.order, sl.pairs, sl.res, sl.mask, sl.prior, sl.fbuf, sl.next};
     for (void* x : p)
       if (x) (void)hipFree(x);
     sl = kmx_lcd::Slot{};
   }
-  if (h->d_fbuf) (void)hipFree(h->d_fbuf);
-  if (h->d_next) (void)hipFree(h->d_next);
   h->d_cq = h->d_cm = h->d_K = nullptr; h->d_pairs = nullptr; h->d_res = nullptr; h->d_mask = nullptr;
   h->d_fbuf = nullptr;
   h->d_next = h->d_hyps = h->d_nrec = nullptr;
@@ -2581,6 +2591,21 @@ void use_next_slot(kmx_lcd* h) {
   const kmx_lcd::Slot& sl = h->slot[h->cur];
   h->d_cq = sl.cq; h->d_cm = sl.cm; h->d_K = sl.K; h->d_hyps = sl.hyps; h->d_nrec = sl.nrec; h->d_order = sl.order;
   h->d_pairs = sl.pairs; h->d_res = sl.res; h->d_mask = sl.mask; h->d_prior = sl.prior;
+  h->d_fbuf = sl.fbuf; h->d_next = sl.next;
+}
+// The current slot's RANSAC stream: everything a call does on its slot's
+// buffers after the kNN2 runs there.
+// Slot 1 goes on rsx for calls of fewer than 96 candidates per CU (8 per
+// resident RANSAC wave): there the previous call's drain is a large part of a
+// call and the kNN2 alone does not fill it (2k candidates: 6.5 -> 3.8 ms per
+// back-to-back call, 20k: 16.9 -> 15.1 ms); at configs[2]'s 50k the kNN2
+// already fills it and the overlap cost 1.6 % (profiles/r04/lcd/two_stream).
+hipStream_t rs_stream(const kmx_lcd* h) { return h->rs_on ? h->rsx : h->stream; }
+// The current slot's last work may be on the other stream (the choice is per
+// call): calls that write the slot's buffers from rs_stream wait for it.
+int rs_wait_slot(kmx_lcd* h) {
+  if (h->ev_rs_set[h->cur]) KMX_HIP(hipStreamWaitEvent(rs_stream(h), h->ev_rs[h->cur], 0));
+  return 0;
 }
 void lcd_free_pairs(kmx_lcd* h) {
   void* p[] = {h->d_mptr, h->d_iq, h->d_im, h->d_row};
@@ -2665,11 +2690,13 @@ int ensure_cap(kmx_lcd* h, int n) {
   if (n > h->cap) {
     lcd_free_cand(h);
     const int cap = std::max(n, 1024);
-    bool ok = hipMalloc(&h->d_fbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::min(cap, RS_MAX_SLOTS)) ==
-                  hipSuccess &&
-              hipMalloc(&h->d_next, sizeof(int)) == hipSuccess;
+    bool ok = true;
     for (auto& sl : h->slot)
-      ok = ok && hipMalloc(&sl.cq, sizeof(int) * cap) == hipSuccess && hipMalloc(&sl.cm, sizeof(int) * cap) == hipSuccess &&
+      ok = ok &&
+           hipMalloc(&sl.fbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::min(cap, RS_MAX_SLOTS)) ==
+               hipSuccess &&
+           hipMalloc(&sl.next, sizeof(int)) == hipSuccess &&
+           hipMalloc(&sl.cq, sizeof(int) * cap) == hipSuccess && hipMalloc(&sl.cm, sizeof(int) * cap) == hipSuccess &&
            hipMalloc(&sl.K, sizeof(int) * cap) == hipSuccess &&
            hipMalloc(&sl.pairs, sizeof(int2) * (size_t)cap * h->N) == hipSuccess &&
            hipMalloc(&sl.res, sizeof(kmx_lcd_result) * cap) == hipSuccess &&
@@ -2684,6 +2711,8 @@ int ensure_cap(kmx_lcd* h, int n) {
     h->cap = cap;
   }
   use_next_slot(h);
+  if (!h->cus) KMX_HIP(hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device));
+  h->rs_on = h->cur == 1 && h->rs_conc && (int64_t)n < 96LL * h->cus;
   return 0;
 }
 
@@ -2769,7 +2798,7 @@ int launch_ransac(kmx_lcd* h, int n, const RsParams& rp, const short* table, int
   KMX_HIP(hipGetDevice(&dev));
   KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int slots = std::max(1, std::min({n, std::max(per_cu, 1) * cus, RS_MAX_SLOTS, h->cap}));
-  KMX_HIP(hipMemsetAsync(h->d_next, 0, sizeof(int), h->stream));
+  KMX_HIP(hipMemsetAsync(h->d_next, 0, sizeof(int), rs_stream(h)));
   RsParams p = rp;
   if (p.prior) p.prior += (size_t)c0 * 12;
   if (p.hyps) p.hyps += c0;
@@ -2778,10 +2807,10 @@ int launch_ransac(kmx_lcd* h, int n, const RsParams& rp, const short* table, int
   const bool longest_first = ov && std::atoi(ov) == 1;
   const int* order = nullptr;
   if (longest_first && n > 1 && c0 == 0) {
-    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, h->stream, (const int*)h->d_K, n, h->N, h->d_order);
+    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, rs_stream(h), (const int*)h->d_K, n, h->N, h->d_order);
     order = h->d_order;
   }
-  hipLaunchKernelGGL(kc, dim3(slots), dim3(RS_BLOCK), 0, h->stream, (const double*)h->d_bear,
+  hipLaunchKernelGGL(kc, dim3(slots), dim3(RS_BLOCK), 0, rs_stream(h), (const double*)h->d_bear,
                      (const double*)h->d_pts, h->N, (const int*)h->d_cq + c0, (const int*)h->d_cm + c0,
                      (const int2*)h->d_pairs + (size_t)c0 * h->N, (const int*)h->d_K + c0, table, p, h->d_res + c0,
                      masks ? h->d_mask + (size_t)c0 * h->N : nullptr, h->d_fbuf, n, h->d_next, order);
@@ -2792,7 +2821,7 @@ int launch_recover(kmx_lcd* h, int n, const PnpParams& pp, const short* table, i
   const size_t smem = sizeof(double) * (6 * (size_t)h->N + 64 * 12 + 12) + sizeof(int) * (64 + 64 + 4 + (size_t)h->N);
   PnpParams p = pp;
   if (p.hyps) p.hyps += c0;
-  hipLaunchKernelGGL(pnp ? k_recover<true> : k_recover<false>, dim3(n), dim3(RS_BLOCK), smem, h->stream,
+  hipLaunchKernelGGL(pnp ? k_recover<true> : k_recover<false>, dim3(n), dim3(RS_BLOCK), smem, rs_stream(h),
                      (const double*)h->d_bear, (const double*)h->d_pts, h->N, (const int*)h->d_cq + c0,
                      (const int*)h->d_cm + c0, (const int2*)h->d_pairs + (size_t)c0 * h->N, (const int*)h->d_K + c0,
                      table, p, h->d_res + c0, h->d_mask + (size_t)c0 * h->N);
@@ -2808,8 +2837,8 @@ int launch_recover(kmx_lcd* h, int n, const PnpParams& pp, const short* table, i
 // problem, and the engine then advances by the passes the serial loop drew.
 int verify_ordered(kmx_lcd* h, int n, int stages, bool masks) {
   std::vector<int> K(n);
-  KMX_HIP(hipMemcpyAsync(K.data(), h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
-  KMX_HIP(hipStreamSynchronize(h->stream));
+  KMX_HIP(hipMemcpyAsync(K.data(), h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, rs_stream(h)));
+  KMX_HIP(hipStreamSynchronize(rs_stream(h)));
   RsParams rp = rs_params(h, stages);
   rp.tab_fixed = 1;
   rp.hyps = h->d_hyps;
@@ -2828,30 +2857,30 @@ int verify_ordered(kmx_lcd* h, int n, int stages, bool masks) {
       std::mt19937 probe = h->stream_rng;
       sample_row(probe, v, K[c], h->pmax, 5, row.data());
       KMX_HIP(hipMemcpyAsync(h->d_row, row.data(), sizeof(short) * (size_t)h->pmax * 5, hipMemcpyHostToDevice,
-                             h->stream));
+                             rs_stream(h)));
     }
     if (int rc = launch_ransac(h, 1, rp, h->d_row, c, masks || rp.pnp)) return rc;
     int got[2] = {0, 0};
-    KMX_HIP(hipMemcpyAsync(&got[0], h->d_hyps + c, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-    if (rp.nrec) KMX_HIP(hipMemcpyAsync(&got[1], h->d_nrec + c, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-    KMX_HIP(hipStreamSynchronize(h->stream));
+    KMX_HIP(hipMemcpyAsync(&got[0], h->d_hyps + c, sizeof(int), hipMemcpyDeviceToHost, rs_stream(h)));
+    if (rp.nrec) KMX_HIP(hipMemcpyAsync(&got[1], h->d_nrec + c, sizeof(int), hipMemcpyDeviceToHost, rs_stream(h)));
+    KMX_HIP(hipStreamSynchronize(rs_stream(h)));
     if (st2d && K[c] >= 5) advance(got[0], 5);
     if (!rp.pnp || !(stages & KMX_LCD_STAGE_RECOVER)) continue;
     kmx_lcd_result r{};
-    KMX_HIP(hipMemcpyAsync(&r, h->d_res + c, sizeof(r), hipMemcpyDeviceToHost, h->stream));
-    KMX_HIP(hipStreamSynchronize(h->stream));
+    KMX_HIP(hipMemcpyAsync(&r, h->d_res + c, sizeof(r), hipMemcpyDeviceToHost, rs_stream(h)));
+    KMX_HIP(hipStreamSynchronize(rs_stream(h)));
     if (r.mono_inliers < pp.min2d) continue;
     const int S = rec_S(h->P), n2 = got[1];
     if (n2 >= S) {
       std::mt19937 probe = h->stream_rng;
       sample_row(probe, v, n2, h->pmax, S, row.data());
       KMX_HIP(hipMemcpyAsync(h->d_row, row.data(), sizeof(short) * (size_t)h->pmax * S, hipMemcpyHostToDevice,
-                             h->stream));
+                             rs_stream(h)));
     }
     if (int rc = launch_recover(h, 1, pp, h->d_row, c)) return rc;
     int hy = 0;
-    KMX_HIP(hipMemcpyAsync(&hy, h->d_hyps + c, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-    KMX_HIP(hipStreamSynchronize(h->stream));
+    KMX_HIP(hipMemcpyAsync(&hy, h->d_hyps + c, sizeof(int), hipMemcpyDeviceToHost, rs_stream(h)));
+    KMX_HIP(hipStreamSynchronize(rs_stream(h)));
     if (n2 >= S) advance(hy, S);
   }
   return 0;
@@ -2896,10 +2925,10 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
                      h->P.lowe_ratio, h->d_pairs, h->d_K);
   if (h->timing) KMX_HIP(hipEventRecord(h->ev[1], h->kstream));
   KMX_HIP(hipEventRecord(h->ev_knn[s], h->kstream));
-  KMX_HIP(hipStreamWaitEvent(h->stream, h->ev_knn[s], 0));
+  KMX_HIP(hipStreamWaitEvent(rs_stream(h), h->ev_knn[s], 0));
   if (int rc = enqueue_ransac(h, n, KMX_LCD_STAGE_2D2D | KMX_LCD_STAGE_RECOVER, want_masks)) return rc;
-  if (h->timing) KMX_HIP(hipEventRecord(h->ev[2], h->stream));
-  KMX_HIP(hipEventRecord(h->ev_rs[s], h->stream));
+  if (h->timing) KMX_HIP(hipEventRecord(h->ev[2], rs_stream(h)));
+  KMX_HIP(hipEventRecord(h->ev_rs[s], rs_stream(h)));
   h->ev_rs_set[s] = true;
   KMX_HIP(hipGetLastError());
   return 0;
@@ -2907,7 +2936,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
 // Calls that work on the current slot from the handle's stream only (match,
 // verify_matches): they end with its RANSAC-done event too.
 int mark_slot(kmx_lcd* h) {
-  KMX_HIP(hipEventRecord(h->ev_rs[h->cur], h->stream));
+  KMX_HIP(hipEventRecord(h->ev_rs[h->cur], rs_stream(h)));
   h->ev_rs_set[h->cur] = true;
   return 0;
 }
@@ -2928,6 +2957,7 @@ int grow_pool(kmx_lcd* h, int need) {
     return kmx::fail(KMX_ENOMEM, "frame pool");
   }
   KMX_HIP(hipStreamSynchronize(h->kstream));  // a kNN2 in flight may read the old pool
+  KMX_HIP(hipStreamSynchronize(h->rsx));      // and slot 1's RANSAC (slot 0's is on h->stream, below)
   if (h->F) {
     KMX_HIP(hipMemcpyAsync(desc, h->d_desc, old * 32, hipMemcpyDeviceToDevice, h->stream));
     KMX_HIP(hipMemcpyAsync(bear, h->d_bear, old * 3 * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
@@ -2988,7 +3018,9 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
     return kmx::fail(KMX_EHIP, "hipStreamCreate");
   }
   h->own_stream = true;
-  bool ok = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking) == hipSuccess;
+  if (const char* e = std::getenv("KMX_LCD_RSX")) h->rs_conc = std::atoi(e) != 0;
+  bool ok = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&h->rsx, hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; i < 2 && ok; ++i)
     ok = hipEventCreateWithFlags(&h->ev_knn[i], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&h->ev_rs[i], hipEventDisableTiming) == hipSuccess;
@@ -3006,6 +3038,7 @@ extern "C" int kmx_lcd_destroy(kmx_lcd* h) {
   if (!h) return KMX_OK;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->rsx) (void)hipStreamSynchronize(h->rsx);
   if (h->kstream) (void)hipStreamSynchronize(h->kstream);
   lcd_free_frames(h);
   lcd_free_tables(h);
@@ -3018,6 +3051,7 @@ extern "C" int kmx_lcd_destroy(kmx_lcd* h) {
     if (h->ev_rs[i]) (void)hipEventDestroy(h->ev_rs[i]);
   }
   if (h->kstream) (void)hipStreamDestroy(h->kstream);
+  if (h->rsx) (void)hipStreamDestroy(h->rsx);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return KMX_OK;
@@ -3028,6 +3062,7 @@ extern "C" int kmx_lcd_set_stream(kmx_lcd* h, void* s) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
   if (h->kstream) KMX_HIP(hipStreamSynchronize(h->kstream));
+  if (h->rsx) KMX_HIP(hipStreamSynchronize(h->rsx));
   if (h->stream) KMX_HIP(hipStreamSynchronize(h->stream));
   if (h->own_stream && h->stream) KMX_HIP(hipStreamDestroy(h->stream));
   h->own_stream = false;
@@ -3106,10 +3141,10 @@ extern "C" int kmx_lcd_verify(kmx_lcd* h, int32_t n, const int32_t* cq, const in
   if (int rc = ensure_cap(h, n)) return rc;
   if (int rc = slot_upload(h, n, cq, cm)) return rc;
   if (int rc = enqueue_verify(h, n, inlier_masks != nullptr)) return rc;
-  if (n) KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, h->stream));
+  if (n) KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
   if (n && inlier_masks)
-    KMX_HIP(hipMemcpyAsync(inlier_masks, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, h->stream));
-  KMX_HIP(hipStreamSynchronize(h->stream));
+    KMX_HIP(hipMemcpyAsync(inlier_masks, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
+  KMX_HIP(hipStreamSynchronize(rs_stream(h)));
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -3133,16 +3168,17 @@ extern "C" int kmx_lcd_match(kmx_lcd* h, int32_t n, const int32_t* cq, const int
   if (n == 0) return KMX_OK;
   KMX_HIP(hipSetDevice(h->device));
   if (int rc = ensure_cap(h, n)) return rc;
-  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
-  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
-  hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1), h->stream,
+  if (int rc = rs_wait_slot(h)) return rc;
+  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
+  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
+  hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1), rs_stream(h),
                      (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, (const int*)h->d_cq,
                      (const int*)h->d_cm, h->P.norm, h->P.lowe_ratio, h->d_pairs, h->d_K);
   KMX_HIP(hipGetLastError());
-  KMX_HIP(hipMemcpyAsync(pairs_out, h->d_pairs, sizeof(int2) * (size_t)n * h->N, hipMemcpyDeviceToHost, h->stream));
-  KMX_HIP(hipMemcpyAsync(k_out, h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipMemcpyAsync(pairs_out, h->d_pairs, sizeof(int2) * (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
+  KMX_HIP(hipMemcpyAsync(k_out, h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, rs_stream(h)));
   if (int rc = mark_slot(h)) return rc;
-  KMX_HIP(hipStreamSynchronize(h->stream));
+  KMX_HIP(hipStreamSynchronize(rs_stream(h)));
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -3173,6 +3209,7 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
   const size_t total = (size_t)(mptr[n] - base);
   KMX_HIP(hipSetDevice(h->device));
   if (int rc = ensure_cap(h, n)) return rc;
+  if (int rc = rs_wait_slot(h)) return rc;
   if (total > h->pair_cap || !h->d_mptr) {
     if (h->d_iq) (void)hipFree(h->d_iq);
     if (h->d_im) (void)hipFree(h->d_im);
@@ -3188,25 +3225,25 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
   KMX_HIP(hipMalloc(&h->d_mptr, sizeof(int64_t) * (n + 1)));
   std::vector<int64_t> mp(mptr, mptr + n + 1);
   for (auto& x : mp) x -= base;
-  KMX_HIP(hipMemcpyAsync(h->d_mptr, mp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipMemcpyAsync(h->d_mptr, mp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, rs_stream(h)));
   if (total) {
-    KMX_HIP(hipMemcpyAsync(h->d_iq, iq + base, sizeof(int) * total, hipMemcpyHostToDevice, h->stream));
-    KMX_HIP(hipMemcpyAsync(h->d_im, im + base, sizeof(int) * total, hipMemcpyHostToDevice, h->stream));
+    KMX_HIP(hipMemcpyAsync(h->d_iq, iq + base, sizeof(int) * total, hipMemcpyHostToDevice, rs_stream(h)));
+    KMX_HIP(hipMemcpyAsync(h->d_im, im + base, sizeof(int) * total, hipMemcpyHostToDevice, rs_stream(h)));
   }
-  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
-  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
+  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
   if (T_prior)
-    KMX_HIP(hipMemcpyAsync(h->d_prior, T_prior, sizeof(double) * 12 * (size_t)n, hipMemcpyHostToDevice, h->stream));
-  hipLaunchKernelGGL(k_scatter_pairs, dim3(n), dim3(256), 0, h->stream, (const int64_t*)h->d_mptr,
+    KMX_HIP(hipMemcpyAsync(h->d_prior, T_prior, sizeof(double) * 12 * (size_t)n, hipMemcpyHostToDevice, rs_stream(h)));
+  hipLaunchKernelGGL(k_scatter_pairs, dim3(n), dim3(256), 0, rs_stream(h), (const int64_t*)h->d_mptr,
                      (const int*)h->d_iq, (const int*)h->d_im, h->N, h->d_pairs, h->d_K);
   KMX_HIP(hipGetLastError());
   if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr)) return rc;
   KMX_HIP(hipGetLastError());
-  KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, h->stream));
+  KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
   if (inlier_masks)
-    KMX_HIP(hipMemcpyAsync(inlier_masks, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, h->stream));
+    KMX_HIP(hipMemcpyAsync(inlier_masks, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
   if (int rc = mark_slot(h)) return rc;
-  KMX_HIP(hipStreamSynchronize(h->stream));
+  KMX_HIP(hipStreamSynchronize(rs_stream(h)));
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -3223,6 +3260,7 @@ extern "C" int kmx_lcd_read_timing(kmx_lcd* h, double* knn_ms, double* ransac_ms
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->kstream));
   KMX_HIP(hipStreamSynchronize(h->stream));
+  KMX_HIP(hipStreamSynchronize(h->rsx));
   float a = 0.f, b = 0.f;
   KMX_HIP(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
   KMX_HIP(hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
@@ -3236,6 +3274,7 @@ extern "C" int kmx_lcd_sync(kmx_lcd* h) {
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->kstream));
   KMX_HIP(hipStreamSynchronize(h->stream));
+  KMX_HIP(hipStreamSynchronize(h->rsx));
   return KMX_OK;
 }
 

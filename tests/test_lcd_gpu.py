@@ -162,3 +162,40 @@ def test_back_to_back_calls_overlap_safely(gpu):
     assert np.array_equal(gm, wm)
     for g, w in zip(got, want):
         assert all(np.array_equal(g[k], w[k]) for k in g)
+
+
+@pytest.mark.parametrize("env", ["1", "0"], ids=["rsx", "one_stream"])
+def test_concurrent_slots_mixed_sizes(gpu, monkeypatch, env):
+    """Slot 1's RANSAC runs on its own stream for calls under 96 candidates per
+    CU (lcd.hip rs_stream), so which stream a slot last used changes from call
+    to call: async calls on either side of that size, then match and
+    verify_matches (which write the slot from its stream) and a synchronous
+    verify; every result equals a fresh detector's. KMX_LCD_RSX=0 keeps both
+    slots on the handle's stream."""
+    monkeypatch.setenv("KMX_LCD_RSX", env)
+    pool = make_lcd_pool(64, 200, seed=29)
+    p = LcdParams()
+    ref = LoopClosureDetector(p)
+    ref.set_pool(pool)
+    want, wm = ref.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    wp, wk = ref.match(pool.cand_query, pool.cand_match)
+    corr = [(wp[i, :wk[i], 0], wp[i, :wk[i], 1]) for i in range(len(wk))]
+    wv, wvm = ref.verify_matches(pool.cand_query, pool.cand_match, corr, with_masks=True)
+    det = LoopClosureDetector(p)
+    det.set_pool(pool)
+    big = -(-(96 * 256 + 1) // pool.cand_query.shape[0])  # above the cut on a 256-CU part
+    for reps in (1, big, 2, big, 1):
+        det.verify_async(np.tile(pool.cand_query, reps), np.tile(pool.cand_match, reps))
+        gp, gk = det.match(pool.cand_query, pool.cand_match)
+        assert np.array_equal(gk, wk) and np.array_equal(gp, wp)
+    det.verify_async(np.tile(pool.cand_query, big), np.tile(pool.cand_match, big))
+    gv, gvm = det.verify_matches(pool.cand_query, pool.cand_match, corr, with_masks=True)
+    assert np.array_equal(gvm, wvm)
+    for g, w in zip(gv, wv):
+        assert all(np.array_equal(g[k], w[k]) for k in g)
+    det.verify_async(pool.cand_query, pool.cand_match)
+    got, gm = det.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    det.sync()
+    assert np.array_equal(gm, wm)
+    for g, w in zip(got, want):
+        assert all(np.array_equal(g[k], w[k]) for k in g)
