@@ -43,6 +43,7 @@ constexpr int KNN_BLOCK = 256;
 constexpr int RS_BLOCK = 64;          // one wavefront per candidate
 constexpr int RS_MAX_SLOTS = 8192;    // k_ransac_coop waves per launch at most (256 CUs x 32 waves)
 constexpr int MAX_FEATS = 1024;
+constexpr int LCD_SLOTS = 4;          // candidate slots: calls in flight at once (kmx_lcd_verify_async)
 
 // ------------------------------------------------------------------ knn2 --
 // The two-nearest update of ordered keys k0 <= k1 with a new key: k1' is the
@@ -2500,14 +2501,14 @@ struct kmx_lcd {
   short* d_table_rec = nullptr;  // samples of the recovery RANSAC (6: PnP, 3: Arun), built when used
   int table_N = 0;
   int pmax = 0;
-  // candidate buffers: two slots, used by alternate calls, so one call's kNN2
-  // (on kstream) can run while the previous call's RANSAC drains (stream);
+  // candidate buffers: LCD_SLOTS slots, used by successive calls in turn, so
+  // a call's kNN2 (on kstream) can run while earlier calls' RANSACs drain;
   // d_cq .. d_order below point into the current slot
   int cap = 0, cur = 0;
-  // Each slot's RANSAC runs on its own stream (slot 0: the handle's stream,
-  // slot 1: rsx) with its own work-queue counter and per-wave scratch, so the
-  // next call's RANSAC takes the CUs the previous call's drains (its last
-  // candidates, finishing alone) leave idle.
+  // Each slot's RANSAC can run on its own stream (slot 0: the handle's
+  // stream, slot s > 0: rsx[s]) with its own work-queue counter and per-wave
+  // scratch, so the next calls' RANSACs take the CUs the previous call's
+  // drain (its last candidates, finishing alone) leaves idle.
   struct Slot {
     int *cq = nullptr, *cm = nullptr, *K = nullptr, *hyps = nullptr, *nrec = nullptr, *order = nullptr;
     int2* pairs = nullptr;
@@ -2516,14 +2517,15 @@ struct kmx_lcd {
     double* prior = nullptr;
     double* fbuf = nullptr;
     int* next = nullptr;
-  } slot[2];
-  hipStream_t rsx = nullptr;      // slot 1's RANSAC stream
-  bool rs_conc = true;            // KMX_LCD_RSX=0: both slots on the handle's stream (A/B switch)
-  bool rs_on = false;             // this call's slot runs on rsx
+  } slot[LCD_SLOTS];
+  hipStream_t rsx[LCD_SLOTS] = {};  // rsx[s]: slot s's RANSAC stream (s > 0)
+  bool rs_conc = true;              // KMX_LCD_RSX=0: every slot on the handle's stream (A/B switch)
+  bool rs_small = false;            // this call runs its slots' RANSACs concurrently (the size cut)
+  bool rs_on = false;               // this call's slot runs on rsx[cur]
   int cus = 0;
   hipStream_t kstream = nullptr;  // kNN2 of kmx_lcd_verify / _async
-  hipEvent_t ev_knn[2] = {nullptr, nullptr}, ev_rs[2] = {nullptr, nullptr};
-  bool ev_rs_set[2] = {false, false};
+  hipEvent_t ev_knn[LCD_SLOTS] = {}, ev_rs[LCD_SLOTS] = {};
+  bool ev_rs_set[LCD_SLOTS] = {};
   int *d_cq = nullptr, *d_cm = nullptr, *d_K = nullptr;
   int2* d_pairs = nullptr;
   kmx_lcd_result* d_res = nullptr;
@@ -2550,9 +2552,13 @@ struct kmx_lcd {
 
 namespace {
 
+void sync_rsx(kmx_lcd* h) {
+  for (hipStream_t x : h->rsx)
+    if (x) (void)hipStreamSynchronize(x);
+}
 void lcd_free_frames(kmx_lcd* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);  // a verification in flight may read the pool
-  if (h->rsx) (void)hipStreamSynchronize(h->rsx);
+  sync_rsx(h);
   if (h->kstream) (void)hipStreamSynchronize(h->kstream);
   void* p[] = {h->d_desc, h->d_bear, h->d_pts, h->d_nfeat};
   for (void* x : p)
@@ -2569,7 +2575,7 @@ void lcd_free_tables(kmx_lcd* h) {
 }
 void lcd_free_cand(kmx_lcd* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);  // in-flight calls may still use the buffers
-  if (h->rsx) (void)hipStreamSynchronize(h->rsx);
+  sync_rsx(h);
   if (h->kstream) (void)hipStreamSynchronize(h->kstream);
   for (auto& sl : h->slot) {
     void* p[] = {sl.cq, sl.cm, sl.K, sl.hyps, sl.nrec, sl.order, sl.pairs, sl.res, sl.mask, sl.prior, sl.fbuf, sl.next};
@@ -2582,12 +2588,12 @@ void lcd_free_cand(kmx_lcd* h) {
   h->d_next = h->d_hyps = h->d_nrec = nullptr;
   h->d_prior = nullptr;
   h->d_order = nullptr;
-  h->ev_rs_set[0] = h->ev_rs_set[1] = false;
+  for (bool& e : h->ev_rs_set) e = false;
   h->cap = 0;
 }
 // The next call's slot: its buffers become d_cq .. d_order.
 void use_next_slot(kmx_lcd* h) {
-  h->cur ^= 1;
+  h->cur = (h->cur + 1) % LCD_SLOTS;
   const kmx_lcd::Slot& sl = h->slot[h->cur];
   h->d_cq = sl.cq; h->d_cm = sl.cm; h->d_K = sl.K; h->d_hyps = sl.hyps; h->d_nrec = sl.nrec; h->d_order = sl.order;
   h->d_pairs = sl.pairs; h->d_res = sl.res; h->d_mask = sl.mask; h->d_prior = sl.prior;
@@ -2595,13 +2601,16 @@ void use_next_slot(kmx_lcd* h) {
 }
 // The current slot's RANSAC stream: everything a call does on its slot's
 // buffers after the kNN2 runs there.
-// Slot 1 goes on rsx for calls of fewer than 96 candidates per CU (8 per
-// resident RANSAC wave): there the previous call's drain is a large part of a
-// call and the kNN2 alone does not fill it (2k candidates: 6.5 -> 3.8 ms per
-// back-to-back call, 20k: 16.9 -> 15.1 ms); at configs[2]'s 50k the kNN2
-// already fills it and the overlap cost 1.6 % (profiles/r04/lcd/two_stream).
-hipStream_t rs_stream(const kmx_lcd* h) { return h->rs_on ? h->rsx : h->stream; }
-// The current slot's last work may be on the other stream (the choice is per
+// Slots s > 0 go on rsx[s] for calls of fewer than 96 candidates per CU (8
+// per resident RANSAC wave): there the previous call's drain is a large part
+// of a call and the kNN2 alone does not fill it (2k candidates, two slots:
+// 6.5 -> 3.8 ms per back-to-back call, 20k: 16.9 -> 15.1 ms); at configs[2]'s
+// 50k the kNN2 already fills it and the overlap cost 1.6 %
+// (profiles/r04/lcd/two_stream). A larger call's kNN2 also waits for the
+// RANSAC two calls back, as with two slots: run further ahead, the kNN2s took
+// CUs from the RANSAC (four slots without it: 50k steps up to 3 % slower).
+hipStream_t rs_stream(const kmx_lcd* h) { return h->rs_on ? h->rsx[h->cur] : h->stream; }
+// The current slot's last work may be on another stream (the choice is per
 // call): calls that write the slot's buffers from rs_stream wait for it.
 int rs_wait_slot(kmx_lcd* h) {
   if (h->ev_rs_set[h->cur]) KMX_HIP(hipStreamWaitEvent(rs_stream(h), h->ev_rs[h->cur], 0));
@@ -2712,7 +2721,8 @@ int ensure_cap(kmx_lcd* h, int n) {
   }
   use_next_slot(h);
   if (!h->cus) KMX_HIP(hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device));
-  h->rs_on = h->cur == 1 && h->rs_conc && (int64_t)n < 96LL * h->cus;
+  h->rs_small = h->rs_conc && (int64_t)n < 96LL * h->cus;
+  h->rs_on = h->cur != 0 && h->rs_small;
   return 0;
 }
 
@@ -2897,10 +2907,11 @@ int enqueue_ransac(kmx_lcd* h, int n, int stages, bool want_masks) {
 }
 
 // The side stream may write the current slot once the last RANSAC that read it
-// (two calls back) is done; the candidate uploads then go on it.
+// (LCD_SLOTS calls back) is done; the candidate uploads then go on it.
 int slot_upload(kmx_lcd* h, int n, const int32_t* cq, const int32_t* cm) {
-  const int s = h->cur;
+  const int s = h->cur, s2 = (s + LCD_SLOTS - 2) % LCD_SLOTS;
   if (h->ev_rs_set[s]) KMX_HIP(hipStreamWaitEvent(h->kstream, h->ev_rs[s], 0));
+  if (!h->rs_small && h->ev_rs_set[s2]) KMX_HIP(hipStreamWaitEvent(h->kstream, h->ev_rs[s2], 0));
   KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, h->kstream));
   KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->kstream));
   return 0;
@@ -2957,7 +2968,8 @@ int grow_pool(kmx_lcd* h, int need) {
     return kmx::fail(KMX_ENOMEM, "frame pool");
   }
   KMX_HIP(hipStreamSynchronize(h->kstream));  // a kNN2 in flight may read the old pool
-  KMX_HIP(hipStreamSynchronize(h->rsx));      // and slot 1's RANSAC (slot 0's is on h->stream, below)
+  for (hipStream_t x : h->rsx)  // and the slots' RANSACs (slot 0's is on h->stream, below)
+    if (x) KMX_HIP(hipStreamSynchronize(x));
   if (h->F) {
     KMX_HIP(hipMemcpyAsync(desc, h->d_desc, old * 32, hipMemcpyDeviceToDevice, h->stream));
     KMX_HIP(hipMemcpyAsync(bear, h->d_bear, old * 3 * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
@@ -3019,9 +3031,9 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
   }
   h->own_stream = true;
   if (const char* e = std::getenv("KMX_LCD_RSX")) h->rs_conc = std::atoi(e) != 0;
-  bool ok = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&h->rsx, hipStreamNonBlocking) == hipSuccess;
-  for (int i = 0; i < 2 && ok; ++i)
+  bool ok = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 1; i < LCD_SLOTS && ok; ++i) ok = hipStreamCreateWithFlags(&h->rsx[i], hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; i < LCD_SLOTS && ok; ++i)
     ok = hipEventCreateWithFlags(&h->ev_knn[i], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&h->ev_rs[i], hipEventDisableTiming) == hipSuccess;
   if (!ok) {
@@ -3038,7 +3050,7 @@ extern "C" int kmx_lcd_destroy(kmx_lcd* h) {
   if (!h) return KMX_OK;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->rsx) (void)hipStreamSynchronize(h->rsx);
+  sync_rsx(h);
   if (h->kstream) (void)hipStreamSynchronize(h->kstream);
   lcd_free_frames(h);
   lcd_free_tables(h);
@@ -3046,12 +3058,13 @@ extern "C" int kmx_lcd_destroy(kmx_lcd* h) {
   lcd_free_pairs(h);
   if (h->ev_ok)
     for (auto e : h->ev) (void)hipEventDestroy(e);
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < LCD_SLOTS; ++i) {
     if (h->ev_knn[i]) (void)hipEventDestroy(h->ev_knn[i]);
     if (h->ev_rs[i]) (void)hipEventDestroy(h->ev_rs[i]);
   }
   if (h->kstream) (void)hipStreamDestroy(h->kstream);
-  if (h->rsx) (void)hipStreamDestroy(h->rsx);
+  for (hipStream_t x : h->rsx)
+    if (x) (void)hipStreamDestroy(x);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return KMX_OK;
@@ -3062,7 +3075,8 @@ extern "C" int kmx_lcd_set_stream(kmx_lcd* h, void* s) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
   if (h->kstream) KMX_HIP(hipStreamSynchronize(h->kstream));
-  if (h->rsx) KMX_HIP(hipStreamSynchronize(h->rsx));
+  for (hipStream_t x : h->rsx)
+    if (x) KMX_HIP(hipStreamSynchronize(x));
   if (h->stream) KMX_HIP(hipStreamSynchronize(h->stream));
   if (h->own_stream && h->stream) KMX_HIP(hipStreamDestroy(h->stream));
   h->own_stream = false;
@@ -3260,7 +3274,8 @@ extern "C" int kmx_lcd_read_timing(kmx_lcd* h, double* knn_ms, double* ransac_ms
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->kstream));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  KMX_HIP(hipStreamSynchronize(h->rsx));
+  for (hipStream_t x : h->rsx)
+    if (x) KMX_HIP(hipStreamSynchronize(x));
   float a = 0.f, b = 0.f;
   KMX_HIP(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
   KMX_HIP(hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
@@ -3274,7 +3289,8 @@ extern "C" int kmx_lcd_sync(kmx_lcd* h) {
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->kstream));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  KMX_HIP(hipStreamSynchronize(h->rsx));
+  for (hipStream_t x : h->rsx)
+    if (x) KMX_HIP(hipStreamSynchronize(x));
   return KMX_OK;
 }
 

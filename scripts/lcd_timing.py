@@ -28,3 +28,10 @@ for _ in range(4):
 det.sync()
 el4 = time.time() - t
 print(f"back-to-back x4: {4 * n / el4:.0f} cand/s ({el4 * 1e3 / 4:.1f} ms per call)", flush=True)
+# a longer stream of calls (the detector keeps several calls in flight)
+t = time.time()
+for _ in range(16):
+    det.verify_async(pool.cand_query, pool.cand_match)
+det.sync()
+el16 = time.time() - t
+print(f"back-to-back x16: {16 * n / el16:.0f} cand/s ({el16 * 1e3 / 16:.1f} ms per call)", flush=True)

@@ -141,7 +141,7 @@ def test_longest_first_queue_is_bit_exact(gpu, monkeypatch, algo):
 
 
 def test_back_to_back_calls_overlap_safely(gpu):
-    """Alternate calls use two candidate slots and a call's kNN2 runs on a side
+    """Successive calls use the detector's candidate slots in turn and a call's kNN2 runs on a side
     stream while the previous call's RANSAC drains: back-to-back async calls,
     a call that grows the buffers while another is in flight, and the
     synchronous results after them equal a fresh detector's."""
@@ -166,12 +166,12 @@ def test_back_to_back_calls_overlap_safely(gpu):
 
 @pytest.mark.parametrize("env", ["1", "0"], ids=["rsx", "one_stream"])
 def test_concurrent_slots_mixed_sizes(gpu, monkeypatch, env):
-    """Slot 1's RANSAC runs on its own stream for calls under 96 candidates per
-    CU (lcd.hip rs_stream), so which stream a slot last used changes from call
-    to call: async calls on either side of that size, then match and
+    """Slots 1-3's RANSACs run on their own streams for calls under 96
+    candidates per CU (lcd.hip rs_stream), so which stream a slot last used
+    changes from call to call: async calls on either side of that size, then match and
     verify_matches (which write the slot from its stream) and a synchronous
-    verify; every result equals a fresh detector's. KMX_LCD_RSX=0 keeps both
-    slots on the handle's stream."""
+    verify; every result equals a fresh detector's. KMX_LCD_RSX=0 keeps every
+    slot on the handle's stream."""
     monkeypatch.setenv("KMX_LCD_RSX", env)
     pool = make_lcd_pool(64, 200, seed=29)
     p = LcdParams()
