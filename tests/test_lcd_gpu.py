@@ -142,9 +142,10 @@ def test_longest_first_queue_is_bit_exact(gpu, monkeypatch, algo):
 
 def test_back_to_back_calls_overlap_safely(gpu):
     """Successive calls use the detector's candidate slots in turn and a
-    call's kNN2 runs on a side stream while the previous call's RANSAC drains: back-to-back async calls,
-    a call that grows the buffers while another is in flight, and the
-    synchronous results after them equal a fresh detector's."""
+    call's kNN2 runs on a side stream while the previous call's RANSAC
+    drains: back-to-back async calls, a call that grows the buffers while
+    another is in flight, and the synchronous results after them equal a
+    fresh detector's."""
     pool = make_lcd_pool(64, 200, seed=23)
     p = LcdParams()
     ref = LoopClosureDetector(p)
