@@ -483,7 +483,11 @@ int kmx_lcd_verify(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
                    const int32_t* cand_match, kmx_lcd_result* results,
                    uint8_t* inlier_masks);
 /* Enqueue verification of candidates already resident on the device without
- * host synchronisation (benchmark path). */
+ * host synchronisation (benchmark / streaming path). Up to four calls are in
+ * flight (candidate slots used in turn; a fifth waits for the first); calls
+ * under 96 candidates per CU run their RANSACs concurrently. Results are not
+ * returned: kmx_lcd_sync waits for every call (the synchronous entry points
+ * return results). */
 int kmx_lcd_verify_async(kmx_lcd* h, int32_t n_cand, const int32_t* cand_query,
                          const int32_t* cand_match);
 int kmx_lcd_sync(kmx_lcd* h);
