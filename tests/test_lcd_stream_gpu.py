@@ -68,6 +68,39 @@ def test_frames_added_one_at_a_time_match_whole_pool(gpu):
                           np.zeros((1, 200, 3)))
 
 
+def test_frames_added_while_calls_are_in_flight(gpu):
+    """The streaming pattern: a frame arrives, the candidates among the frames
+    so far are verified asynchronously, the next frame arrives. Appends that
+    double the pool (device-to-device copy, old pool freed) run while up to
+    four small calls' RANSACs read it from their own streams; the synchronous
+    results at the end, and of a call made between appends, equal the
+    whole-pool path's bit for bit."""
+    pool = make_lcd_pool(200, 120, seed=31)
+    p = LcdParams()
+    whole = LoopClosureDetector(p)
+    whole.set_pool(pool)
+    ref, rm = whole.verify(pool.cand_query, pool.cand_match, with_masks=True)
+    stream = LoopClosureDetector(p)
+    cq, cm = pool.cand_query, pool.cand_match
+    mid = None
+    for f in range(pool.n_frames):
+        stream.add_frames(pool.n_feats[f:f + 1], pool.desc[f:f + 1], pool.bearings[f:f + 1], pool.points[f:f + 1])
+        ready = np.flatnonzero(np.maximum(cq, cm) <= f)
+        if len(ready):
+            stream.verify_async(cq[ready], cm[ready])
+        if f == 120:
+            mid = (ready, stream.verify(cq[ready], cm[ready], with_masks=True))
+    stream.sync()
+    ready, (g1, m1) = mid
+    assert np.array_equal(m1, rm[ready][:, :m1.shape[1]])
+    for i, g in zip(ready, g1):
+        assert all(np.array_equal(g[k], ref[i][k]) for k in g), i
+    got, gm = stream.verify(cq, cm, with_masks=True)
+    assert np.array_equal(gm, rm)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert all(np.array_equal(g[k], r[k]) for k in g), i
+
+
 def test_add_vlc_frame_vertices(gpu):
     """addVLCFrame keys frames by (robot_id, pose_id) and pads them to the
     pool stride (LcdParams nfeatures); computeMatchedIndices on vertices is
