@@ -762,15 +762,16 @@ __device__ void coop_nullspace(CoopWS& w, int lane) {
 #pragma unroll
     for (int i = k; i < 9; ++i) nv += v[i] * v[i];
     nv = sqrt(nv);
+    // the reflector's entries: lane i < 9 divides entry i (one quotient per
+    // lane instead of nine per lane), then every lane reads them back
+    double mine = 0.0;
+#pragma unroll
+    for (int i = k; i < 9; ++i) mine = (lane == i) ? v[i] : mine;
+    mine = (nv > 0.0 && lane >= k && lane < 9) ? mine / nv : 0.0;
     double vs[9];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) vs[i] = (nv > 0.0 && i >= k) ? v[i] / nv : 0.0;
-    if (lane < 9) {
-      double x = 0.0;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) x = (lane == i) ? vs[i] : x;
-      w.vs[k][lane] = x;
-    }
+    for (int i = 0; i < 9; ++i) vs[i] = i >= k ? rdlane(mine, i) : 0.0;
+    if (lane < 9) w.vs[k][lane] = mine;
     // d_j = sum_{i >= k} vs[i] A[i][j] over this lane's column j
     double d = 0.0;
 #pragma unroll
