@@ -1830,13 +1830,13 @@ __device__ __forceinline__ void stew_models(StewBatch& sb, double* stash, int la
 }
 
 // The sample's bearings, the null space and the 10x20 system (both solvers).
-__device__ __forceinline__ void coop_prepare(CoopWS& w, int lane, const double* F1, const double* F2, const short* smp,
-                                             bool prof) {
+__device__ __forceinline__ void coop_prepare(CoopWS& w, int lane, const double* F1, const double* F2, int N,
+                                             const short* smp, bool prof) {
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   if (lane < 15) {
     const int i = lane / 3, c = lane % 3;
-    w.f1[lane] = F1[3 * smp[i] + c];
-    w.f2[lane] = F2[3 * smp[i] + c];
+    w.f1[lane] = F1[(size_t)c * N + smp[i]];
+    w.f2[lane] = F2[(size_t)c * N + smp[i]];
   }
   wsync();
   KMX_PT(0);
@@ -1847,9 +1847,9 @@ __device__ __forceinline__ void coop_prepare(CoopWS& w, int lane, const double* 
 }
 
 // One Nister hypothesis: sample -> models (w.ok, w.mR, w.mt).
-__device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const double* F2, const short* smp,
-                                                bool prof) {
-  coop_prepare(w, lane, F1, F2, smp, prof);
+__device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const double* F2, int N,
+                                                const short* smp, bool prof) {
+  coop_prepare(w, lane, F1, F2, N, smp, prof);
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   if (!coop_gj(w, lane, false)) {
     if (lane == 0) w.ok = 0;
@@ -1920,13 +1920,13 @@ __device__ __forceinline__ int grp_gj(const double* A, int cl, int g0, double a[
 // from systems staged in the wave's scratch), stashed in sb, then their
 // eigenvalues together.
 __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* stash, int lane, const double* F1,
-                                           const double* F2, const short* tab, int p0, int nb, bool prof) {
+                                           const double* F2, int N, const short* tab, int p0, int nb, bool prof) {
   double* Ab = stash + SG * STASH_H + MAXP * 9;
   for (int b0 = 0; b0 < nb; b0 += GJW) {
     const int nw = min(GJW, nb - b0);
     for (int u = 0; u < nw; ++u) {
       const int b = b0 + u;
-      coop_prepare(w, lane, F1, F2, tab + (size_t)(p0 + b) * 5, prof);
+      coop_prepare(w, lane, F1, F2, N, tab + (size_t)(p0 + b) * 5, prof);
       double* A = Ab + u * 200;
       for (int t = lane; t < 200; t += RS_BLOCK) A[t] = (&w.A[0][0])[t];
       double* st = stash + b * STASH_H;
@@ -1995,17 +1995,23 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
     }
     return;
   }
-  // compact bearings of the match pairs (global scratch, L1/L2 resident)
+  // compact bearings of the match pairs (global scratch, L1/L2 resident), one
+  // component per row of N (F1[k][j]): the scoring loops' loads are coalesced
   double* stash = F1 + 6 * N;  // Stewenius: the batch's action matrices and null spaces
   double* F2 = F1 + 3 * N;
   const int2* pl = pairs + (size_t)c * N;
   for (int j = lane; j < K; j += RS_BLOCK) {
     const int2 pr = pl[j];
     for (int k = 0; k < 3; ++k) {
-      F1[3 * j + k] = bearings[((size_t)q * N + pr.x) * 3 + k];
-      F2[3 * j + k] = bearings[((size_t)m * N + pr.y) * 3 + k];
+      F1[(size_t)k * N + j] = bearings[((size_t)q * N + pr.x) * 3 + k];
+      F2[(size_t)k * N + j] = bearings[((size_t)m * N + pr.y) * 3 + k];
     }
   }
+  // pair j's error under the model (R, t)
+  auto pair_error = [&](const double* R, const double* t, int j) {
+    const double a[3] = {F1[j], F1[N + j], F1[2 * N + j]}, b[3] = {F2[j], F2[N + j], F2[2 * N + j]};
+    return model_error(R, t, a, b);
+  };
   for (int t = lane; t < 40; t += RS_BLOCK) (&w.t11[0][0][0])[t] = (&T11[0][0][0])[t];
   for (int t = lane; t < 120; t += RS_BLOCK) (&w.t21[0][0][0])[t] = (&T21[0][0][0])[t];
   __threadfence_block();
@@ -2032,7 +2038,7 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
     int cnt = 0;
     for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
       const int j = j0 + lane;
-      const bool in = (j < K) && model_error(Rm, tm, F1 + 3 * j, F2 + 3 * j) < P.thr2d;
+      const bool in = (j < K) && pair_error(Rm, tm, j) < P.thr2d;
       cnt += __popcll(__ballot(in));
     }
     KMX_PT(6);
@@ -2072,7 +2078,7 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
         want = rem < 1.0 ? 1 : (rem < (double)SG ? (int)rem : SG);
       }
       nb = min(want, P.pmax - p0);
-      stew_batch(w, sb, stash, lane, F1, F2, tab, p0, nb, prof);
+      stew_batch(w, sb, stash, lane, F1, F2, N, tab, p0, nb, prof);
       stew_models(sb, stash, lane, F1, F2, tab, p0, nb, prof);
       for (int b = 0; b < nb && !done; ++b) {
         if (!(iterations < kk && skipped < max_skip)) {
@@ -2085,7 +2091,7 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
   } else {
     for (int p = 0; p < P.pmax && !done; ++p) {
       if (!(iterations < kk && skipped < max_skip)) break;  // uniform
-      coop_hypothesis(w, lane, F1, F2, tab + (size_t)p * 5, prof);
+      coop_hypothesis(w, lane, F1, F2, N, tab + (size_t)p * 5, prof);
       account(w.ok != 0, w.mR, w.mt);
     }
   }
@@ -2107,7 +2113,7 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
     for (int i = 0; i < 12; ++i) (i < 9 ? Rb[i] : tb[i - 9]) = P.prior ? P.prior[(size_t)c * 12 + i] : (i % 4 == 0 && i < 9 ? 1.0 : 0.0);
   }
   // a pair's 2D-2D inlier test: the best model's, or every pair without the stage
-  auto inl2d = [&](int j) { return (j < K) && (!st2d || model_error(Rb, tb, F1 + 3 * j, F2 + 3 * j) < P.thr2d); };
+  auto inl2d = [&](int j) { return (j < K) && (!st2d || pair_error(Rb, tb, j) < P.thr2d); };
   int n_in = 0;
   for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
     const int j = j0 + lane;
