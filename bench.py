@@ -238,12 +238,13 @@ def ransac_roofline(algo, n_cand, tk):
     d = json.load(open(f))
     per = d["per_candidate"]
     ach = per["fp64_issued_flops"] * n_cand / (tk["ransac_ms"] * 1e-3)
-    # every wave64 VALU instruction holds its SIMD for 4 cycles (16 lanes per
-    # cycle): the share of the chip's VALU issue capacity this step used
-    valu_issue = per["valu_insts"] * n_cand * 4.0 / (tk["ransac_ms"] * 1e-3) / (1024 * 2.4e9)
+    # gfx950 issues a wave64 VALU instruction over 2 SIMD cycles (SIMD-32,
+    # MI355X_MICROARCH.md "Wave scheduling"; the same rate the 78.6 TF fp64
+    # peak assumes): the share of the chip's VALU issue capacity this step used
+    valu_issue = per["valu_insts"] * n_cand * 2.0 / (tk["ransac_ms"] * 1e-3) / (1024 * 2.4e9)
     out.update({"achieved": ach, "frac": ach / PEAK_FP64, "valu_issue_frac": valu_issue,
                 "valu_issue_rule": f"{per['valu_insts']:.4g} VALU wave-instructions per candidate (stored PMC ratio) "
-                                   "x 4 SIMD cycles each / (1024 SIMDs x 2.4 GHz)",
+                                   "x 2 SIMD cycles each (SIMD-32) / (1024 SIMDs x 2.4 GHz)",
                 "flops_source": "stored PMC ratio (profiles/lcd_fp64_stewenius.json): "
                                 f"{per['fp64_issued_flops']:.4g} issued fp64 lane-flops per candidate (64 lanes per "
                                 "wave instruction, 2 per FMA, whatever the exec mask)",

@@ -190,7 +190,8 @@ struct Dev {
   // double-buffered by step parity (the gathered vector), and the step's
   // 8-wide partials
   double *hz, *w0, *w1;
-  double* part_f;             // [ntiles][8]
+  double* part_f;             // [2][ntiles][8], by step parity (a launch reads step k's
+                              // partials of every tile of its robot while its own tile writes step k+1's)
 };
 
 constexpr int HV_SLOTS = 1 << 16;
@@ -1685,9 +1686,10 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
 //       delta' = -z' + beta delta,  H delta' = -Hz' + beta H delta,
 //       r' = r + coef H delta,   w' = precon(H delta')
 //     (fused multiply-adds, as the restatement), and the 7 partials.
-// A robot whose tCG stops in step 1 only updates r (k_retract's model). Only
-// w is read across tiles, so only w is double-buffered (by step parity); the
-// kept directions are d.dh as in the standard form.
+// A robot whose tCG stops in step 1 only updates r (k_retract's model). What
+// a launch reads across tiles — w and the robot's 8-wide partials — is
+// double-buffered by step parity (launch j reads step j-1's and writes step
+// j's); the kept directions are d.dh as in the standard form.
 // Restated by oracle/dpgo_oracle.c tcg_onesync (same recurrences); parity
 // with the standard form at convergence only.
 __device__ __forceinline__ void onesync_scalars(double al, const double* tot, double* rrn, double* zrn) {
@@ -1779,7 +1781,7 @@ __device__ unsigned long long g_step_stamp[16 * STEP_STAMP_TILES];
 #endif
 
 template <int R, int RW>
-__device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cout, int first, int slot,
+__device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cout, int jl, int slot,
                                           HostStatus* hs, unsigned long long seq, char* smem) {
 #ifdef KMX_STEP_STAMPS
   unsigned long long ss_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1796,12 +1798,17 @@ __device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cou
   // first (the host's launch 0 of a tCG loop): a robot in it is at PH_START
   // and the launch consumes k_grad's partials, else it is in PH_TCG; the
   // robot sums' loads go out before the state arrives
-  const bool grad = first != 0;
+  const bool grad = jl == 0;
   const int t0 = L.rt0, t1 = L.rt1;
   RobotSum<3> rg;
   RobotSum8<4> rf;
   if (grad) rg.issue(d.part, NPART, t0, t1);
-  else rf.issue(d.part_f, t0, t1);
+  // launch jl consumes step jl - 1's partials (buffer (jl - 1) & 1) and
+  // writes step jl's into the other buffer, so no tile of the robot can
+  // overwrite a partial another tile of the same launch has yet to read (a
+  // robot in tCG at launch jl is at tcg_iter jl - 1)
+  const double* pf_in = d.part_f + (size_t)(((jl + 1) & 1) * d.ntiles) * 8;
+  if (!grad) rf.issue(pf_in, t0, t1);
   const int ph0 = c0.phase;
   if (ph0 != (grad ? PH_START : PH_TCG)) {
     if (writer && threadIdx.x == 0) {
@@ -1823,7 +1830,7 @@ __device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cou
       if (writer && threadIdx.x == 0) control_on(cs, d, L.l, RED_GRAD, tot, R, true);
     } else {
       double tot[8];
-      rf.finish(d.part_f, rl, tot);
+      rf.finish(pf_in, rl, tot);
       const double zr = tot[1];
       const HessStep hx = hess_step(zr, c0.e_Pe, c0.e_Pd, c0.d_Pd, c0.Delta, tot[0]);
       double rrn, zrn;
@@ -1982,7 +1989,7 @@ __device__ __forceinline__ void body_step(const Dev& d, const Ctl* cin, Ctl* cou
 #pragma unroll
       for (int w = 0; w < WAVES; ++w) t += lds[threadIdx.x * WAVES + w];
     }
-    d.part_f[(size_t)L.tile * 8 + threadIdx.x] = t;
+    d.part_f[((size_t)(kn & 1) * d.ntiles + L.tile) * 8 + threadIdx.x] = t;
   }
   if (L.valid) {
     store4(d.dh + (size_t)(kn % dhn) * d.vec + o, dl);
@@ -2154,10 +2161,10 @@ __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigne
 // 3 waves per SIMD at r <= 5: the 736-tile cut of a small shard is resident
 // in one generation (256 CUs x 3), without the spills of a 128-VGPR bound
 template <int R, int RW>
-__global__ __launch_bounds__(BLOCK, (R <= 5 ? 3 : 2)) void k_step(Dev d, const Ctl* cin, Ctl* cout, int first, int slot,
+__global__ __launch_bounds__(BLOCK, (R <= 5 ? 3 : 2)) void k_step(Dev d, const Ctl* cin, Ctl* cout, int jl, int slot,
                                                                   HostStatus* hs, unsigned long long seq) {
   KMX_SMEM;
-  body_step<R, RW>(d, cin, cout, first, slot, hs, seq, smem);
+  body_step<R, RW>(d, cin, cout, jl, slot, hs, seq, smem);
 }
 template <int R>
 __global__ __launch_bounds__(BLOCK) void k_retract(Dev d, int fold, const Ctl* src) {
@@ -2995,7 +3002,7 @@ void enqueue_tcg_t(kmx_pgo* h) {
         HostStatus* hs = poll ? h->hstat : nullptr;
         const Ctl* cin = (j & 1) ? h->d_ctl2 : h->d_ctl;
         Ctl* cout = (j & 1) ? h->d_ctl : h->d_ctl2;
-        hipLaunchKernelGGL((k_step<R, RW>), grid, blk, SmemF<R>::bytes, h->stream, h->dv, cin, cout, j == 0 ? 1 : 0,
+        hipLaunchKernelGGL((k_step<R, RW>), grid, blk, SmemF<R>::bytes, h->stream, h->dv, cin, cout, j,
                            slot, hs, seq);
         if (slot >= 0) (void)hipEventRecord(e1, h->stream);
         if (poll && j > 0 && !wait_running(h, seq)) {
@@ -3516,7 +3523,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_relc, L)) || (rc = dalloc(&h->d_gnc, 2)) || (rc = dalloc(&h->d_ext, 64)) ||
       (rc = dalloc(&h->d_hv_launch, HV_SLOTS)) ||
       (rc = dalloc(&h->d_coefh, (size_t)L * std::max(h->P.tcg_max_iterations, 1))) ||
-      (onesync(h) && (rc = dalloc(&h->d_part_f, (size_t)h->ntiles * 8)))) {
+      (onesync(h) && (rc = dalloc(&h->d_part_f, (size_t)h->ntiles * 16)))) {
     free_dev(h);
     return rc;
   }

@@ -210,17 +210,13 @@ def lib() -> C.CDLL:
         "kmx_bow_sync": ([P], C.c_int),
         "kmx_bow_score_pairs": ([P, i32, pi64, pu32, pf64, pi64, pu32, pf64, pf64], C.c_int),
     })
-    # KMX_AB_OLDLIB=1 (same-box A/B against an earlier build given by KMX_LIB
-    # only): entry points the older library lacks are skipped and its ABI
-    # version is accepted; the calls an A/B makes must exist in both
-    old_ok = os.environ.get("KMX_AB_OLDLIB") == "1" and "KMX_LIB" in os.environ
     for name, (argt, rest) in sig.items():
-        if old_ok and not hasattr(L, name):
-            continue
+        if not hasattr(L, name):
+            raise KmxError(f"{path} lacks the entry point {name}: rebuild it")
         fn = getattr(L, name)
         fn.argtypes = argt
         fn.restype = rest
-    if L.kmx_abi_version() != ABI_VERSION and not old_ok:
+    if L.kmx_abi_version() != ABI_VERSION:
         raise KmxError(f"{path} implements ABI {L.kmx_abi_version()}, this binding needs {ABI_VERSION}: rebuild it")
     _lib = L
     return L
@@ -272,7 +268,11 @@ def runtime_info() -> dict:
     buf = C.create_string_buffer(4096)
     check(lib().kmx_runtime_info(buf, 4096), "kmx_runtime_info")
     info = json.loads(buf.value.decode())
+    import re
     mapped = {"librccl": set(), "libamdhip64": set()}
+    # the core libraries only, by basename (librccl.so, librccl.so.1, ...): an
+    # RCCL plugin such as librccl-net.so is not a second copy of RCCL
+    core = {k: re.compile(rf"^{k}\.so(\.\d+)*$") for k in mapped}
     try:
         with open("/proc/self/maps") as f:
             for line in f:
@@ -280,7 +280,7 @@ def runtime_info() -> dict:
                 if len(parts) >= 6:
                     path = parts[-1]
                     for k in mapped:
-                        if f"/{k}" in path:
+                        if core[k].match(os.path.basename(path)):
                             mapped[k].add(os.path.realpath(path))
     except OSError:
         pass

@@ -240,12 +240,13 @@ class RBCDDriver:
             ok = False
         if not self._agree(ok):
             if ok:
-                self.solver.comm_destroy()
+                self._destroy_comm()
             self.exchange_mode += " (fallback: a rank could not create its RCCL communicator)"
             return False
         self.solver.set_exchange(*self._plan)
         self.exchange_mode = "RCCL ncclSend/ncclRecv group inside each round (solver stream)"
         info = getattr(self.solver, "runtime_info", None)
+        refuse = None
         if info is not None:
             # torch bundles a librccl of the same SONAME as the one kmx links: one
             # copy must serve both, or kmx's communicator runs on a different RCCL
@@ -256,9 +257,25 @@ class RBCDDriver:
             if not ri.get("single_rccl", True):
                 self.exchange_mode += f" (WARNING: {len(ri.get('mapped_rccl', []))} RCCL copies mapped)"
                 if os.environ.get("KMX_REQUIRE_NATIVE", "0") == "1":
-                    raise RuntimeError("KMX_REQUIRE_NATIVE=1: libkmx's RCCL symbols resolve to "
-                                       f"{ri.get('rccl_path_real')} but the process maps {ri.get('mapped_rccl')}")
+                    refuse = ("KMX_REQUIRE_NATIVE=1: libkmx's RCCL symbols resolve to "
+                              f"{ri.get('rccl_path_real')} but the process maps {ri.get('mapped_rccl')}")
+        # the refusal is agreed, so every rank raises together (a per-rank raise
+        # would leave the peers waiting in their first exchange)
+        if not self._agree(refuse is None):
+            self._destroy_comm()
+            raise RuntimeError(refuse or "KMX_REQUIRE_NATIVE=1: a peer rank maps more than one RCCL copy")
         return True
+
+    def _destroy_comm(self):
+        """Abort the native communicator; an error from it (a stream already in
+        error, a timeout) is recorded, never raised, so the caller still reaches
+        the agreement its peers wait in."""
+        try:
+            self.solver.comm_destroy()
+        except Exception as e:  # noqa: BLE001 - reported through exchange_mode
+            prev = getattr(self, "_native_error", None)
+            msg = f"comm_destroy on rank {self.rank}: {type(e).__name__}: {e}"
+            self._native_error = f"{prev}; {msg}" if prev else msg
 
     def _torch_exchange(self):
         s = self.solver
@@ -292,7 +309,7 @@ class RBCDDriver:
         except Exception as e:  # noqa: BLE001 - reported through exchange_mode
             tab_n = ext_n = None
             self._native_error = f"first native exchange on rank {self.rank}: {type(e).__name__}: {e}"
-            s.comm_destroy()  # abort: the stream drains even if a peer's half never comes
+            self._destroy_comm()  # abort: the stream drains even if a peer's half never comes
             alive = False
         self._torch_exchange()
         tab_t, ext_t = s.get_public(self.world)
@@ -303,7 +320,7 @@ class RBCDDriver:
         errs = [None] * self.world
         self._dist.all_gather_object(errs, getattr(self, "_native_error", None))
         if alive:
-            s.comm_destroy()
+            self._destroy_comm()
         self.native = False
         failed = [e for e in errs if e]
         if failed:  # an exception (a timeout included) is not a bitwise mismatch: say which

@@ -43,7 +43,11 @@ class LcdParams:
     pose_recovery_type: int = 0
     min_nr_2d3d_inliers: int = 20
     ransac_threshold_2d3d: float = 1.0   # pixels
-    focal_length: float = 380.0          # px, converts the 2D-3D threshold to (1 - cos) [U: D455 intrinsics]
+    # px: converts the 2D-3D threshold to (1 - cos), as Kimera-VIO's LCD does
+    # with the left camera's fu. The default is the D455 left camera's fu
+    # (params/D455/LeftCameraParams.yaml:18, intrinsics[0]); from_yaml(...,
+    # camera_yaml=...) reads it from a camera file
+    focal_length: float = 377.229220831
     # BoW detection (LcdParams.yaml:3-12)
     use_nss: int = 1
     alpha: float = 0.4
@@ -74,10 +78,12 @@ class LcdParams:
     rng_stream: int = 0
 
     @classmethod
-    def from_yaml(cls, path: str, **overrides) -> "LcdParams":
+    def from_yaml(cls, path: str, camera_yaml: str | None = None, **overrides) -> "LcdParams":
         """Read an OpenCV-FileStorage LcdParams.yaml (the %YAML:1.0 header is
-        skipped). `overrides` replace yaml keys (by yaml name) or dataclass
-        fields before validation. Every key is accounted for: verification
+        skipped). `camera_yaml`: a Kimera camera file (LeftCameraParams.yaml)
+        whose `intrinsics` fu sets focal_length (the PnP threshold's pixel to
+        angle conversion). `overrides` replace yaml keys (by yaml name) or
+        dataclass fields before validation. Every key is accounted for: verification
         and BoW keys map onto fields, keys of stages outside the hot path
         (ORB extraction, the PGO back end, the tracker) are ignored by name,
         and anything else, or a value that selects an algorithm this build
@@ -87,6 +93,8 @@ class LcdParams:
         if text.startswith("%YAML"):
             text = text.split("\n", 1)[1] if "\n" in text else ""
         y = dict(yaml.safe_load(text) or {})
+        if camera_yaml is not None:
+            y["focal_length"] = camera_focal_length(camera_yaml)
         y.update(overrides)
         p = cls()
         for k, v in y.items():
@@ -163,6 +171,24 @@ class LcdParams:
 
 ALGO_STEWENIUS = 0
 ALGO_NISTER = 1
+
+
+def camera_focal_length(path: str) -> float:
+    """fu of a Kimera camera file (`intrinsics: [fu, fv, cu, cv]`,
+    params/D455/LeftCameraParams.yaml:18), the focal length Kimera-VIO's LCD
+    converts the PnP pixel threshold with."""
+    import yaml
+    text = open(path).read()
+    if text.startswith("%YAML"):
+        text = text.split("\n", 1)[1] if "\n" in text else ""
+    y = yaml.safe_load(text) or {}
+    intr = y.get("intrinsics")
+    if not isinstance(intr, (list, tuple)) or len(intr) < 1:
+        raise ValueError(f"{path}: no `intrinsics: [fu, fv, cu, cv]`")
+    fu = float(intr[0])
+    if not fu > 0.0:
+        raise ValueError(f"{path}: fu = {fu}")
+    return fu
 
 # yaml keys that are dataclass fields of the same name
 _YAML_FIELDS = (

@@ -105,8 +105,11 @@ LCD_REFINE_CASES = [     # refine_pose 1 (LcdParams.yaml:14) on the 3D-3D recove
 def lcd_params(case, refine=0, stream=0):
     from kmx.lcd import LcdParams
     algo, variant, norm, rec = case
+    # focal_length 380: the value the frozen PnP fixtures were generated with
+    # (before the default became the D455 fu, 377.229); it only sets the 2D-3D
+    # inlier threshold, so the fixtures stay valid vectors for that parameter
     return LcdParams(ransac_2d2d_algorithm=algo, rng_variant=variant, norm=norm, pose_recovery_type=int(rec == 1),
-                     ransac_use_1point_3d3d=int(rec != 2), refine_pose=refine, rng_stream=stream)
+                     ransac_use_1point_3d3d=int(rec != 2), refine_pose=refine, rng_stream=stream, focal_length=380.0)
 
 
 def run_lcd_oracle(pool, case, refine=0, stream=0):

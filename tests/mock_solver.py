@@ -199,10 +199,14 @@ class NativeOracleBlockSolver(OracleBlockSolver):
             self._pending = None
             self._nx = 0
 
+    raise_in_destroy = False  # the abort itself fails (a stream already in error)
+
     def comm_destroy(self):
         self.xchg = None
         self._pending = None
         self.comm_destroys = getattr(self, "comm_destroys", 0) + 1
+        if self.raise_in_destroy:
+            raise RuntimeError("hipStreamSynchronize: an illegal memory access (injected in comm_destroy)")
 
     def set_exchange(self, send_slots, send_counts, recv_slots, recv_counts):
         sc, rc = np.asarray(send_counts, np.int64), np.asarray(recv_counts, np.int64)

@@ -79,6 +79,30 @@ def test_reference_lcdparams_yaml_if_present():
     assert p.to_c().algorithm_2d2d == 0
 
 
+def test_focal_length_from_camera_file(tmp_path):
+    """The PnP threshold's focal length is the camera file's fu (Kimera-VIO's
+    LCD converts the pixel threshold with the left camera's intrinsics[0]);
+    the default is the D455 left camera's fu (LeftCameraParams.yaml:18)."""
+    import numpy as np
+    from kmx.lcd import LcdParams
+    from kmx.lcd.detector import camera_focal_length
+    assert LcdParams().focal_length == 377.229220831
+    cam = tmp_path / "LeftCameraParams.yaml"
+    cam.write_text("%YAML:1.0\ncamera_id: left_cam\nintrinsics: [400.5, 401.0, 320.0, 240.0]  # [fu, fv, cu, cv]\n")
+    y = tmp_path / "LcdParams.yaml"
+    y.write_text("%YAML:1.0\nransac_threshold_2d3d: 2\n")
+    p = LcdParams.from_yaml(str(y), camera_yaml=str(cam))
+    assert p.focal_length == 400.5
+    assert p.to_c().ransac_threshold_2d3d == 1.0 - np.cos(np.arctan(2.0 / 400.5))
+    bad = tmp_path / "bad.yaml"
+    bad.write_text("%YAML:1.0\ncamera_id: x\n")
+    with pytest.raises(ValueError, match="intrinsics"):
+        camera_focal_length(str(bad))
+    ref = Path("/root/reference/params/D455/LeftCameraParams.yaml")
+    if ref.exists():
+        assert camera_focal_length(str(ref)) == LcdParams().focal_length
+
+
 @pytest.mark.parametrize("line,msg", [
     ("ransac_2d2d_algorithm: 2", "ransac_2d2d_algorithm"),      # SEVENPT
     ("ransac_2d3d_algorithm: 1", "ransac_2d3d_algorithm"),      # KNEIP

@@ -183,7 +183,8 @@ def test_exchange_plan_consistent(world):
             assert np.all(rank_of[keys[seg_sent] >> 32] == k)
 
 
-def _native_worker(rank, world, port, rounds, q, fail_rank=-1, corrupt_rank=-1, raise_rank=-1, store=None):
+def _native_worker(rank, world, port, rounds, q, fail_rank=-1, corrupt_rank=-1, raise_rank=-1, store=None,
+                   destroy_raises=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if store:
@@ -199,6 +200,7 @@ def _native_worker(rank, world, port, rounds, q, fail_rank=-1, corrupt_rank=-1, 
         s.comm_init = fail
     s.corrupt = rank == corrupt_rank  # this rank's transport delivers a wrong bit
     s.raise_in_exchange = rank == raise_rank  # this rank's first exchange raises after its peers posted
+    s.raise_in_destroy = destroy_raises and rank == raise_rank  # and then its abort raises too
     drv = RBCDDriver(P, g, rank=rank, world=world, solver=s, exchange_device="cuda")
     drv.initialize(_x0(g))
     drv.step(with_stats=True)          # one exchange (the round's own)
@@ -289,7 +291,8 @@ def test_native_exchange_checked_at_first_round():
 
 
 @pytest.mark.timeout(300)
-def test_native_exchange_raise_after_peers_posted(tmp_path):
+@pytest.mark.parametrize("destroy_raises", [False, True], ids=["abort_ok", "abort_raises"])
+def test_native_exchange_raise_after_peers_posted(tmp_path, destroy_raises):
     """one rank's first native exchange raises after its
     peer has posted its half (a posted, asynchronous transport as ncclSend /
     ncclRecv on the stream). The peer's wait is bounded (sync_timeout,
@@ -302,7 +305,7 @@ def test_native_exchange_raise_after_peers_posted(tmp_path):
     q = ctx.Queue()
     port = _free_port()
     store = str(tmp_path / "xchg_store")
-    ps = [ctx.Process(target=_native_worker, args=(r, world, port, rounds, q, -1, -1, 1, store))
+    ps = [ctx.Process(target=_native_worker, args=(r, world, port, rounds, q, -1, -1, 1, store, destroy_raises))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -314,6 +317,8 @@ def test_native_exchange_raise_after_peers_posted(tmp_path):
     for rank, X, wu, native, inits, exchanges, async_calls, mode, destroys in res:
         assert not native and inits == 1 and destroys == 1
         assert "failed" in mode and "rank 1" in mode and "injected" in mode and "differed" not in mode
+        # an abort that raises is reported, and the peers still agree
+        assert ("comm_destroy on rank 1" in mode) == destroy_raises
         assert exchanges == (1 if rank == 0 else 0)  # rank 0 posted; rank 1 raised first
         for a, Xa in X.items():
             assert np.array_equal(Xa, o.get_iterate(a)), (rank, a)

@@ -126,6 +126,35 @@ def test_onesync_large_robot_block(gpu, tile_incidences):
         s.close()
 
 
+@pytest.mark.parametrize("tile_incidences", [24, 40])
+def test_onesync_partials_double_buffered(gpu, tile_incidences):
+    """a k_step launch reads step k's 8-wide partials of
+    every tile of its robot while each tile writes step k + 1's; with the
+    partials in one buffer, a tile dispatched after a same-robot tile finished
+    read the new partial. Cut so fine that a robot's tiles span several
+    generations of resident workgroups (~3,000-5,000 tiles for one 12.5k-pose
+    block, against 768 resident at 3 per CU), every round must still match the
+    restatement's one-sync form: the same tCG count and stop reason, and every
+    lifted pose within 1e-9 (the per-round drift of a correct run is ~1e-12; a
+    torn robot sum changes alpha / beta in some tiles only)."""
+    g, P, X0 = _setup(n_robots=1, n=12_500, m=62_500, seed=7)
+    _onesync(P)
+    P.tileIncidences = tile_incidences
+    s, o = _pair(g, P, X0)
+    try:
+        for it in range(5):
+            s.refresh_local()
+            sg = s.iterate()
+            so = o.iterate()
+            assert sg[0]["tcg_iterations"] == so[0]["tcg_iterations"], (it, sg[0], so[0])
+            assert sg[0]["tcg_stop"] == so[0]["tcg_stop"], (it, sg[0], so[0])
+            assert sg[0]["accepted"] == so[0]["accepted"], it
+            d = np.linalg.norm((s.get_iterate(0) - o.get_iterate(0)).reshape(-1, 4 * P.r), axis=1).max()
+            assert d <= 1e-9, (it, d)
+    finally:
+        s.close()
+
+
 @pytest.mark.parametrize("robust", [False, True])
 def test_onesync_accelerated_rounds_match_oracle(gpu, robust):
     """Nesterov-accelerated RBCD with the one-sync tCG: the extrapolated point
