@@ -190,6 +190,7 @@ struct Dev {
   // double-buffered by step parity (the gathered vector), and the step's
   // 8-wide partials
   double *hz, *w0, *w1;
+  unsigned* gbar;             // resident round: grid-barrier words (zeroed by k_begin), or null
   double* part_f;             // [2][ntiles][8], by step parity (a launch reads step k's
                               // partials of every tile of its robot while its own tile writes step k+1's)
 };
@@ -1112,7 +1113,21 @@ __device__ __forceinline__ void robot_sum(const double* part, int stride, int t0
 // robot_sum's order (a thread's tiles in tile order, then the wave sums and
 // the waves in order: the same sums for any U).
 // NS <= 2: 2-wide partials (part_h / part_u); NS = 3, 4: d.part (stride NPART).
-template <int NS, int U = 2>
+// A tile partial pair: plain, or (SC, the resident round: partials another
+// workgroup of the same launch wrote through) two 8-B agent-scope loads (sc1).
+template <bool SC>
+__device__ __forceinline__ double2 ldpart(const double* p) {
+  if constexpr (SC) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(const_cast<double*>(p));
+    const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_double2(__longlong_as_double((long long)a), __longlong_as_double((long long)b));
+  } else {
+    return *reinterpret_cast<const double2*>(p);
+  }
+}
+
+template <int NS, int U = 2, bool SC = false>
 struct RobotSum {
   double a[U][NS];
   int t0, t1;
@@ -1123,10 +1138,10 @@ struct RobotSum {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = min(t0 + (int)threadIdx.x + u * RBLOCK, t1 - 1);
-      const double2* p2 = reinterpret_cast<const double2*>(part + (size_t)t * stride);
-      const double2 x = p2[0];
+      const double* pt = part + (size_t)t * stride;
+      const double2 x = ldpart<SC>(pt);
       if constexpr (NS > 2) {
-        const double2 y = p2[1];
+        const double2 y = ldpart<SC>(pt + 2);
         a[u][2] = y.x;
         if constexpr (NS > 3) a[u][3] = y.y;
       }
@@ -1136,7 +1151,7 @@ struct RobotSum {
   }
   __device__ __forceinline__ void finish(const double* part, int stride, double* lds, double tot[NPART]) {
     static_assert(NS <= NPART, "partials");
-    if (t1 - t0 > U * RBLOCK) {
+    if (!SC && t1 - t0 > U * RBLOCK) {  // (SC: the host caps a robot's tiles at U * RBLOCK)
       robot_sum<(NS > 2 ? NPART : NS)>(part, stride, t0, t1, lds, tot);
       if constexpr (NS == 3) tot[3] = 0.0;
       return;
@@ -1702,7 +1717,7 @@ __device__ __forceinline__ void onesync_scalars(double al, const double* tot, do
 // robot_sum: U tiles per thread in one round trip (1024 tiles, the 736-tile
 // cut of a 12.5k-pose block included), tile order within a thread, then the
 // wave sums and the waves in order; larger robots loop.
-template <int U>
+template <int U, bool SC = false>
 struct RobotSum8 {
   double a[U][8];
   int t0, t1;
@@ -1710,10 +1725,9 @@ struct RobotSum8 {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = min(tb + (int)threadIdx.x + u * RBLOCK, t1 - 1);
-      const double2* p2 = reinterpret_cast<const double2*>(part + (size_t)t * 8);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const double2 x = p2[k];
+        const double2 x = ldpart<SC>(part + (size_t)t * 8 + 2 * k);
         a[u][2 * k] = x.x;
         a[u][2 * k + 1] = x.y;
       }
@@ -2181,6 +2195,477 @@ __global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
   body_commit<R>(d, fold, final);
 }
 
+// ================================================ resident one-sync round ===
+// tcg_form KMX_TCG_FORM_RESIDENT (SURVEY.md §7
+// step 4, §8e): the whole block update of a small shard in ONE launch per
+// round — gradient, every one-sync tCG step, the trial point, its cost, the
+// accept decision and the commit — with one grid barrier where the launched
+// form (k_grad, k_step x J, k_cost, k_commit) has a kernel boundary. What it
+// removes per step is the launch's own latency chain (profiles/r04: ~17 us of
+// dependent steps per k_step at 12.5k poses, 4.4 us of it loading the tile's
+// own rows): each workgroup holds its tile's rows of y, g, r, z, Hz, delta,
+// H delta, w and eta in registers and its poses' D_i, M^-1 and S blocks in LDS
+// for the whole round, so a step reads only what crosses workgroups: the
+// robot's 8-wide partials and the neighbours' rows of w.
+// Arithmetic: body_step's and the oracle's tcg_onesync, expression for
+// expression (fused multiply-adds included), the robot sums in RobotSum8's
+// order, so a resident round equals the launched one-sync round on the same
+// tile cut bit for bit (tests/test_resident_gpu.py).
+// Hand-offs inside the launch (MI355X_MICROARCH.md "Valid forms", row 1):
+// every byte another workgroup reads in this launch — z, w, Xt rows and the
+// tile partials — is stored write-through (sc1 16-B buffer stores, 8-B agent
+// atomics) and loaded sc1; every storing wave drains (s_waitcnt vmcnt(0))
+// before the workgroup barrier behind which one lane arrives. Data written by
+// earlier launches (X, the public table, records, D_i, M^-1) are read plainly.
+// Grid barrier: per-group arrival counters (group = block % 8, one XCD under
+// round-robin placement: speed only), the group's last arriver (told by its
+// add's return) adds to the top counter, whose last arriver publishes the
+// barrier's generation; one lane per workgroup polls it (sc1, s_sleep).
+// Counters are monotonic within the launch and zeroed by k_begin before each
+// round. Every spin is bounded (KMX_RES_SPIN ticks of the 100 MHz clock): a
+// workgroup that gives up writes the host-mapped fail word and leaves; the
+// host turns it into an error at the next sync. All workgroups must be
+// resident: set_graph checks the occupancy query and runs a census launch.
+constexpr int GB_STRIDE = 32;                // one 128-B line per word
+constexpr int GB_CNT = 0, GB_TOP = 8, GB_GEN = 9, GB_CONT = 10;
+constexpr int GB_WORDS = 12 * GB_STRIDE;
+constexpr unsigned long long KMX_RES_SPIN = 200000000ull;  // 2 s
+
+__device__ __forceinline__ unsigned gb_load(unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One grid barrier (index b within the launch). `cont`: this workgroup's robot
+// formed a tCG step whose partials the next step consumes; *any: some
+// workgroup arrived with cont. Returns false when the wait gave up.
+__device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, bool* any, unsigned* fail, int* sflag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned e = b + 1;
+    unsigned* cw = gb + (GB_CONT + (b & 1)) * GB_STRIDE;
+    if (cont) {
+      __hip_atomic_store(cw, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned n = gridDim.x, G = n < 8 ? n : 8, g = blockIdx.x & 7, ng = (n - g + 7) / 8;
+    const unsigned old = __hip_atomic_fetch_add(gb + (GB_CNT + g) * GB_STRIDE, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == ng * e) {
+      const unsigned o2 = __hip_atomic_fetch_add(gb + GB_TOP * GB_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (o2 + 1 == G * e) __hip_atomic_store(gb + GB_GEN * GB_STRIDE, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    int ok = 1;
+    const unsigned long long t0 = wall_clock64();
+    while (gb_load(gb + GB_GEN * GB_STRIDE) < e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > KMX_RES_SPIN) {
+        ok = 0;
+        __hip_atomic_store(fail, 1u + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    *sflag = ok ? (1 | (gb_load(cw) == e ? 2 : 0)) : 0;
+  }
+  __syncthreads();
+  const int f = *sflag;
+  *any = (f & 2) != 0;
+  return (f & 1) != 0;
+}
+
+// write-through row I/O: 16-B buffer loads / stores with the sc1 bit (aux 16)
+// through a descriptor built from a kernel-argument base (wave-uniform)
+typedef unsigned kmx_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const double* base, long long doubles) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, (int)(doubles * 8), 0x00020000);
+}
+__device__ __forceinline__ double2 wt_ld2(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  const kmx_u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+  return __builtin_bit_cast(double2, v);
+}
+__device__ __forceinline__ void wt_st4(__amdgpu_buffer_rsrc_t rs, unsigned off, const double v[4]) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kmx_u4, make_double2(v[0], v[1])), rs, off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kmx_u4, make_double2(v[2], v[3])), rs, off + 16, 0, 16);
+}
+__device__ __forceinline__ void wt_st1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the gathered rows of a vector another workgroup of this launch wrote
+template <int R>
+struct WtRows {
+  __amdgpu_buffer_rsrc_t rs;
+  __device__ __forceinline__ void nbr(int o, double2 vr[2 * R]) const {
+    const unsigned b = (unsigned)max(o, 0) * (unsigned)(32 * R);
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) vr[i] = wt_ld2(rs, b + 16u * i);
+  }
+  __device__ __forceinline__ void own(int, int, double*) {}  // (DIAG = false: the caller's registers)
+};
+
+// the tile's partials, written through (the robot sums read them sc1)
+template <int NV>
+__device__ __forceinline__ void wt_tile_partials(const double* vals, double* dst, double* lds) {
+#pragma unroll
+  for (int s = 0; s < NV; ++s) {
+    const double w = wave_sum(vals[s]);
+    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) t += lds[threadIdx.x * WAVES + w];
+    wt_st1(dst + threadIdx.x, t);
+  }
+}
+
+template <int R>
+struct SmemRes {  // the gathers' layouts at 0 (the largest of k_grad's, k_step's, k_cost's), then per pose D, M^-1, S
+  static constexpr int TP = WAVES * (64 / R);
+  static constexpr int a0 = SmemHG<R>::bytes > SmemF<R>::bytes ? SmemHG<R>::bytes : SmemF<R>::bytes;
+  static constexpr int a1 = a0 > SmemC<R>::bytes ? a0 : SmemC<R>::bytes;
+  static constexpr int d_off = (a1 + 15) / 16 * 16;  // double[TP][16]
+  static constexpr int p_off = d_off + TP * 16 * 8;  // double[TP][16]
+  static constexpr int s_off = p_off + TP * 16 * 8;  // double[TP][9]
+  static constexpr int g_off = s_off + TP * 9 * 8;   // double[TP][R][4]: g, then the trial point
+  static constexpr int red_off = g_off + TP * R * 32; // double[8 * WAVES]
+  static constexpr int bytes = red_off + 8 * 8 * WAVES;
+};
+
+// Scalar decisions of one tCG step, taken by thread 0 on the workgroup's copy
+// of its robot's state and broadcast through LDS.
+struct ResStep {
+  double coef, al, be;
+  int go;
+};
+// the round's static LDS besides the Ctl copy: 48 B, so the statics stay a
+// multiple of 16 B and the dynamic area 16-B aligned (Guideline 17)
+struct alignas(16) ResShared {
+  ResStep st;
+  int flag, pad[3];
+};
+
+template <int R, int RW>
+__device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned* fail, int census, char* smem) {
+  using SM = SmemRes<R>;
+  __shared__ Ctl cs;
+  __shared__ ResShared rsh;
+  ResStep& rst = rsh.st;
+  int& sflag = rsh.flag;
+  unsigned b = 0;
+  bool any;
+  if (census) {  // residency check: every workgroup must reach one barrier
+    (void)grid_sync(gb, 0, false, &any, fail, &sflag);
+    return;
+  }
+  const Lane L = lane_map<R>(d);
+  const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
+  const unsigned ob = (unsigned)o * 8u;  // byte offset of the lane's row
+  const int pl = L.pose - L.p0;
+  const bool writer = L.tile == L.rt0;
+  double* Dl = reinterpret_cast<double*>(smem + SM::d_off);
+  double* Pl = reinterpret_cast<double*>(smem + SM::p_off);
+  double* Sl = reinterpret_cast<double*>(smem + SM::s_off);
+  double* gx = reinterpret_cast<double*>(smem + SM::g_off) + 4 * (pl * R + L.a);  // this lane's row of g / Xt
+  double* red = reinterpret_cast<double*>(smem + SM::red_off);
+  double* rl = red;  // robot sums' scratch (8 x WAVES), used after the tile partials are out
+  double* scr = reinterpret_cast<double*>(smem);  // group-op scratch (the chunk area, between gathers)
+  const __amdgpu_buffer_rsrc_t rz = wt_rsrc(d.z, d.vec), rw0 = wt_rsrc(d.w0, d.vec), rw1 = wt_rsrc(d.w1, d.vec),
+                               rxt = wt_rsrc(d.Xt, d.vec);
+  // the robot's state (k_begin's), one copy per workgroup; GNC state commit
+  if (threadIdx.x < (int)(sizeof(Ctl) / 8))
+    reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(d.ctl + L.l)[threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 0) store_gnc(d.gnc, load_gnc(d.gnc_next));
+  if (d.gnc_next->fired) {  // k_begin re-weighted: this tile's D_i and M^-1 (k_grad's gated prologue)
+    for (int t = threadIdx.x; t < L.np; t += blockDim.x) pose_precond<RW>(d, L.p0 + t);
+  }
+  __syncthreads();
+  // per-pose blocks into LDS (the tile's own poses, rebuilt above by this workgroup or by an earlier launch)
+  for (int i = threadIdx.x; i < L.np * 2; i += blockDim.x) {
+    const int p = i >> 1;
+    double M[16];
+    load_sym4((i & 1 ? d.Pinv : d.hD) + SYM4 * (size_t)(L.p0 + p), M);
+    double* dst = (i & 1 ? Pl : Dl) + 16 * p;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[k] = M[k];
+  }
+  const int ph0 = cs.phase;  // (read before any barrier of this launch: every thread sees k_begin's value)
+  // -------- gradient (body_grad's arithmetic; X and the public table are the round's start) --------
+  double y[4] = {0, 0, 0, 0}, rn[4] = {0, 0, 0, 0}, zn[4] = {0, 0, 0, 0};
+  const bool grad = ph0 == PH_START;
+  if (grad) {
+    double G[4], cost = 0.0;
+    hinc_grad<R, RW>(d, L, d.X, d.pub, G, &cost, smem);
+    if (L.valid) load4(d.X + o, y);
+    double S[9], gr[4];
+    group_symYtG<R, true>(y, G, L.base, S, scr);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) gr[c] = G[c] - (y[0] * S[0 * 3 + c] + y[1] * S[1 * 3 + c] + y[2] * S[2 * 3 + c]);
+    gr[3] = G[3];
+    // S as k_grad stores it (6 entries) and k_step reads it back (load_sym3)
+    if (L.valid && L.a == 0) {
+      double* Sp = Sl + 9 * pl;
+      Sp[0] = S[0]; Sp[1] = S[1]; Sp[2] = S[2]; Sp[3] = S[4]; Sp[4] = S[5]; Sp[5] = S[8];
+    }
+    double Pm[16];
+    if (L.valid) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) Pm[k] = Pl[16 * pl + k];
+    }
+    group_precon<R, true>(d, L.pose, L.valid, y, gr, L.base, zn, scr, Pm, L.valid);
+    double vals[3] = {cost, 0.0, 0.0};
+    if (L.valid) {
+      vals[1] = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2] + gr[3] * gr[3];
+      vals[2] = zn[0] * gr[0] + zn[1] * gr[1] + zn[2] * gr[2] + zn[3] * gr[3];
+      wt_st4(rz, ob, zn);  // z_0: step 0 gathers it
+#pragma unroll
+      for (int c = 0; c < 4; ++c) gx[c] = gr[c];  // g waits in LDS for the model decrease
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) rn[c] = gr[c];  // r_0 = g
+    wt_tile_partials<3>(vals, d.part + (size_t)L.tile * NPART, red);
+  }
+  // -------- tCG, one barrier per step (body_step's arithmetic) --------
+  double hzn[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0}, wn[4] = {0, 0, 0, 0},
+         et[4] = {0, 0, 0, 0};
+  bool formed = grad;   // this workgroup's robot formed the step the next barrier's consumers need
+  bool trial = false;   // its tCG ended this round: the trial point is in LDS (gx) and published
+  int k = -1;           // the step whose partials the next decision consumes
+  for (int jl = 0;; ++jl) {
+    bool go = false;
+    double coef = 0.0, al = 0.0, be = 0.0;
+    auto decide = [&]() -> bool {
+      if (!grid_sync(gb, b++, formed, &any, fail, &sflag)) return false;
+      if (!any) return false;
+      if (!formed) return false;  // not in tCG (skipped, idle, or stopped earlier)
+      double tot[8];
+      if (jl == 0) {
+        RobotSum<3, 2, true> rg;
+        rg.issue(d.part, NPART, L.rt0, L.rt1);
+        double t4[NPART];
+        rg.finish(d.part, NPART, rl, t4);
+        if (threadIdx.x == 0) {
+          control_core(cs, d, L.l, RED_GRAD, t4, R, writer);
+          rst.go = cs.phase == PH_TCG;
+          rst.coef = rst.al = rst.be = 0.0;
+        }
+      } else {
+        RobotSum8<2, true> rf;  // (<= 512 tiles per robot: RobotSum8<4>'s order in one pass)
+        const double* pf_in = d.part_f + (size_t)((k & 1) * d.ntiles) * 8;
+        rf.issue(pf_in, L.rt0, L.rt1);
+        rf.finish(pf_in, rl, tot);
+        if (threadIdx.x == 0) {
+          const double zr = tot[1];
+          const HessStep hx = hess_step(zr, cs.e_Pe, cs.e_Pd, cs.d_Pd, cs.Delta, tot[0]);
+          double rrn, zrn;
+          onesync_scalars(hx.alpha, tot, &rrn, &zrn);
+          const UpdStep u = upd_step(hx.boundary ? MODE_BOUNDARY : MODE_INTERIOR, cs.r_stop, cs.lin_stop, zr, k + 1,
+                                     rrn, zrn, d.p);
+          rst.coef = hx.coef;
+          rst.al = hx.alpha;
+          rst.be = u.beta;
+          rst.go = !u.done;
+          cs.z_r = zr;
+          double th[NPART] = {tot[0], 0.0, 0.0, 0.0};
+          control_core(cs, d, L.l, RED_HESS, th, R, writer);
+          double tu[NPART] = {rrn, zrn, 0.0, 0.0};
+          control_core(cs, d, L.l, RED_UPDATE, tu, R, writer);
+        }
+      }
+      __syncthreads();
+      go = rst.go != 0;
+      coef = rst.coef;
+      al = rst.al;
+      be = rst.be;
+      return go;
+    };
+    double H[4];
+    WtRows<R> src{jl == 0 ? rz : ((k & 1) ? rw1 : rw0)};
+    hinc_gather_src<R, RW, false, WtRows<R>, decltype(decide)&, false>(d, L, src, H, smem, decide);
+    if (sflag == 0) return;  // a barrier gave up (the fail word is set)
+    if (!any) break;
+    if (formed && !go && jl > 0) {
+      // the robot's tCG ends here: the last residual, eta's last direction
+      // (this decision's coefficient), the trial point and the model partials
+#pragma unroll
+      for (int c = 0; c < 4; ++c) rn[c] = fma(coef, hdl[c], rn[c]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) et[c] += coef * dl[c];
+      double xt[4];
+      group_retract<R>(y, et, L.base, xt);
+      double vals[2] = {0.0, 0.0};
+      if (L.valid) {
+        wt_st4(rxt, ob, xt);
+        double m = 0.0, ch = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          m += et[c] * (gx[c] + rn[c]);
+          const double dd = xt[c] - y[c];
+          ch += dd * dd;
+        }
+        vals[0] = m;
+        vals[1] = ch;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) gx[c] = xt[c];  // the trial cost's own row (and the commit's)
+      }
+      wt_tile_partials<2>(vals, d.part + (size_t)L.tile * NPART + 2, red);
+      trial = true;
+    }
+    formed = go;
+    if (!go) continue;
+    const int kn = k + 1;  // the step this pass forms
+    double v[4], S[9];
+    if (jl == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = zn[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = wn[c];
+    }
+    if (L.valid) {
+      const double* Dp = Dl + 16 * pl;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)  // the diagonal block (hinc_gather's DIAG term, same expression)
+        H[c] += v[0] * Dp[4 * c] + v[1] * Dp[4 * c + 1] + v[2] * Dp[4 * c + 2] + v[3] * Dp[4 * c + 3];
+      load_sym3(Sl + 9 * pl, S);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) S[i] = 0.0;
+    }
+    __syncthreads();  // the chunk area (group-op scratch) is free: every wave left the gather's last LDS read
+    double hv[4];
+    group_rhess<R, true>(y, v, H, S, L.base, hv, scr);
+    if (jl == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        hzn[c] = hv[c];
+        dl[c] = -v[c];
+        hdl[c] = -hv[c];
+      }
+    } else {
+      // eta += coef_k delta_k (the serial order of the folds), then the step's recurrences
+#pragma unroll
+      for (int c = 0; c < 4; ++c) et[c] += coef * dl[c];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double hold = hdl[c], dold = dl[c];
+        rn[c] = fma(coef, hold, rn[c]);
+        zn[c] = fma(al, v[c], zn[c]);
+        hzn[c] = fma(al, hv[c], hzn[c]);
+        dl[c] = fma(be, dold, -zn[c]);
+        hdl[c] = fma(be, hold, -hzn[c]);
+      }
+    }
+    double Pm[16];
+    if (L.valid) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) Pm[i] = Pl[16 * pl + i];
+    }
+    group_precon<R, true>(d, L.pose, L.valid, y, hdl, L.base, wn, scr, Pm, L.valid);
+    double pv[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (L.valid) {
+      pv[0] = dot4(dl, hdl);
+      pv[1] = dot4(rn, zn);
+      pv[2] = dot4(rn, rn);
+      pv[3] = dot4(rn, wn) + dot4(hdl, zn);
+      pv[4] = dot4(hdl, wn);
+      pv[5] = dot4(rn, hdl);
+      pv[6] = dot4(hdl, hdl);
+      wt_st4((kn & 1) ? rw1 : rw0, ob, wn);
+    }
+    wt_tile_partials<7>(pv, d.part_f + ((size_t)(kn & 1) * d.ntiles + L.tile) * 8, red);
+    k = kn;
+  }
+  // -------- trial cost, accept, commit (body_cost + body_commit's fold) --------
+  if (trial) {  // uniform per robot: the owner incidences' cost of the trial point
+    using SC = SmemC<R>;
+    int* sptr = reinterpret_cast<int*>(smem + SC::ptr_off);
+    const double2* xs = reinterpret_cast<const double2*>(smem + SM::g_off);  // the tile's trial rows
+    const int tid = threadIdx.x, np = L.np, K0 = L.k0, n = L.n;
+    __syncthreads();
+    if (tid <= np) sptr[tid] = d.inc_ptr[L.p0 + tid] - K0;
+    __syncthreads();
+    double cost = 0.0;
+    using RC = Rec<RW>;
+    for (int kk = tid; kk < n; kk += BLOCK) {
+      double2 q[RC::Q];
+      RC::load(d.rec, (size_t)(K0 + kk), q);
+      const int2 in = RC::inc(q);
+      const int ot = in.x;
+      const bool tail = (in.y >> 31) & 1;
+      if (ot >= 0 && !tail) continue;
+      int lo = 0, hi = np;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (sptr[mid] <= kk) lo = mid;
+        else hi = mid;
+      }
+      const double2* s2 = xs + lo * 2 * R;
+      double2 vs2[2 * R], vo2[2 * R];
+      if (ot >= 0) {
+        const unsigned bo = (unsigned)ot * (unsigned)(32 * R);
+#pragma unroll
+        for (int i = 0; i < 2 * R; ++i) vo2[i] = wt_ld2(rxt, bo + 16u * i);
+      } else {
+        const double2* o2 = reinterpret_cast<const double2*>(d.pub + (size_t)(-1 - ot) * 4 * R);
+#pragma unroll
+        for (int i = 0; i < 2 * R; ++i) vo2[i] = o2[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 2 * R; ++i) vs2[i] = s2[i];
+      Edge E;
+      RC::edge(q, E);
+      double c = 0.0;
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        const double vs[4] = {vs2[2 * a].x, vs2[2 * a].y, vs2[2 * a + 1].x, vs2[2 * a + 1].y};
+        const double vo[4] = {vo2[2 * a].x, vo2[2 * a].y, vo2[2 * a + 1].x, vo2[2 * a + 1].y};
+        double dummy[4] = {0.0, 0.0, 0.0, 0.0};
+        c += incidence_row(E, tail, vs, vo, dummy);
+      }
+      cost += c;
+    }
+    wt_tile_partials<1>(&cost, d.part + (size_t)L.tile * NPART, red);
+  }
+  if (!grid_sync(gb, b++, false, &any, fail, &sflag)) return;
+  bool commit = false;
+  if (trial) {
+    RobotSum<NPART, 2, true> rs;
+    rs.issue(d.part, NPART, L.rt0, L.rt1);
+    double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+    rs.finish(d.part, NPART, rl, tot);
+    {  // control_on's RED_COST acceptance test (body_commit's fold)
+      const double model_dec = -0.5 * tot[2];
+      const double rho = (model_dec > 0.0) ? (cs.f_cur - tot[0]) / model_dec : -1.0;
+      commit = rho > d.p.accept_rho;
+    }
+    if (threadIdx.x == 0) {
+      control_core(cs, d, L.l, RED_COST, tot, R, writer);
+      cs.phase = PH_STEP;
+    }
+  }
+  __syncthreads();
+  if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))
+    reinterpret_cast<double*>(d.ctl + L.l)[threadIdx.x] = reinterpret_cast<const double*>(&cs)[threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    d.gnc->inner += 1;
+    d.gnc->rounds += 1;
+  }
+  if (!commit || !L.valid) return;
+  double xt[4] = {gx[0], gx[1], gx[2], gx[3]};
+  store4(d.X + o, xt);
+  const int s = d.pose_slot[L.pose];
+  if (s >= 0) store4(d.pub + (size_t)s * 4 * R + 4 * L.a, xt);
+}
+
+template <int R, int RW>
+__global__ __launch_bounds__(BLOCK, 2) void k_round(Dev d, unsigned* gb, unsigned* fail, int census) {
+  KMX_SMEM;
+  body_round<R, RW>(d, gb, fail, census, smem);
+}
+
 // ------------------------------------------------- round begin + GNC-TLS ---
 // shouldUpdateMeasurementWeights (drawio:2466-2469): never for L2 or once
 // robustOptNumWeightUpdates updates were made; otherwise when more than
@@ -2265,6 +2750,8 @@ __global__ void k_begin(Dev d, const unsigned char* active, int mode, int R_) {
   const bool fire = d.p.robust && ((mode & BEGIN_FORCE_GNC) ? true : gnc_should_update(d));
   const double mu = d.gnc->mu;
   if (blockIdx.x == 0) {
+    if (d.gbar)  // the resident round's barrier counters start every round at zero
+      for (int i = threadIdx.x; i < GB_WORDS; i += blockDim.x) d.gbar[i] = 0u;
     if (mode & BEGIN_ROUND)
       for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
     if (threadIdx.x == 0) {
@@ -2726,6 +3213,13 @@ struct kmx_pgo {
   // Nesterov acceleration (P.acceleration): momentum V and this round's Y
   // (allocated only when enabled), gamma and the restart counter on the host
   double *d_accV = nullptr, *d_accY = nullptr;
+  // KMX_TCG_FORM_RESIDENT: one persistent launch per round (k_round) when every
+  // tile fits resident (decided at set_graph: occupancy query + census launch)
+  bool res_on = false;
+  int res_cap = 0;             // workgroups of k_round resident on the device
+  std::string res_reason = "tcg_form is not KMX_TCG_FORM_RESIDENT";
+  unsigned* d_gbar = nullptr;  // grid-barrier words (GB_WORDS)
+  unsigned* h_fail = nullptr;  // host-mapped: nonzero when a barrier wait gave up (1 + its index)
   double acc_gamma = 0.0;
   int acc_k = 0;
   bool acc_ready = false, acc_started = false;
@@ -2790,7 +3284,7 @@ void free_dev(kmx_pgo* h) {
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
                   h->d_accV, h->d_accY, h->d_ctl2, h->d_part_h,
-                  h->d_part_u, h->d_coefh, h->d_part_f};
+                  h->d_part_u, h->d_coefh, h->d_part_f, h->d_gbar};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile = nullptr;
@@ -2817,6 +3311,8 @@ void free_dev(kmx_pgo* h) {
   h->d_coefh = nullptr;
   h->d_part_h = h->d_part_u = nullptr;
   h->d_part_f = nullptr;
+  h->d_gbar = nullptr;
+  h->res_on = false;
 }
 
 hipEvent_t next_event(kmx_pgo* h) {
@@ -2832,7 +3328,10 @@ bool ready(kmx_pgo* h) { return h && h->d_vec != nullptr; }
 
 // Vectors of d_vec: X Xt g r z hd eta + the tCG directions kept for k_retract
 // (+ Hz, w_0, w_1 for the one-sync tCG, which needs two directions).
-bool onesync(const kmx_pgo* h) { return h->P.tcg_form == KMX_TCG_FORM_ONESYNC && h->P.method == KMX_METHOD_RTR; }
+bool onesync(const kmx_pgo* h) {
+  return (h->P.tcg_form == KMX_TCG_FORM_ONESYNC || h->P.tcg_form == KMX_TCG_FORM_RESIDENT) &&
+         h->P.method == KMX_METHOD_RTR;
+}
 int dh_count(const kmx_pgo* h) {
   return std::max(onesync(h) ? 2 : 1, std::min(h->P.tcg_max_iterations, DHMAX));
 }
@@ -3080,8 +3579,88 @@ void enqueue_trial_t(kmx_pgo* h, bool rgd) {
   if (!fold_cost<RM>(h)) red_t<R, RM>(h, RED_COST);
 }
 
+// KMX_TCG_FORM_RESIDENT: the round begin (GNC decision and re-weighting; the
+// preconditioner rebuild is left to k_round), then the whole block update.
+template <int R, int RW>
+void enqueue_resident_t(kmx_pgo* h, const unsigned char* d_active) {
+  (void)enqueue_begin(h, d_active, BEGIN_ROUND, true);
+  hipLaunchKernelGGL((k_round<R, RW>), dim3(h->ntiles), dim3(BLOCK), SmemRes<R>::bytes, h->stream, h->dv, h->d_gbar,
+                     h->h_fail, 0);
+}
+
+// Whether the resident round can run on this handle: RTR with one RTR
+// iteration, every robot's tiles within one pass of the robot sums, and every
+// tile resident at once — the occupancy query's workgroups per CU times the
+// CUs, then a census launch in which every workgroup must reach one grid
+// barrier (a workgroup that does not fit would leave the others spinning until
+// the bounded wait gives up: MI355X_MICROARCH.md "Residency").
+template <int R, int RW>
+int resident_setup_t(kmx_pgo* h) {
+  h->res_on = false;
+  if (h->P.method != KMX_METHOD_RTR) { h->res_reason = "RGD method"; return 0; }
+  if (h->P.rtr_iterations != 1) { h->res_reason = "rtr_iterations != 1"; return 0; }
+  for (size_t l = 0; l + 1 < h->rt0_h.size(); ++l)
+    if (h->rt0_h[l + 1] - h->rt0_h[l] > 2 * RBLOCK) {
+      h->res_reason = "a robot has more than 512 tiles";
+      return 0;
+    }
+  int nb = 0, cus = 0;
+  KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_round<R, RW>, BLOCK, SmemRes<R>::bytes));
+  KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+  h->res_cap = nb * cus;
+  if (h->ntiles > h->res_cap) {
+    h->res_reason = std::to_string(h->ntiles) + " tiles > " + std::to_string(h->res_cap) + " resident workgroups (" +
+                    std::to_string(nb) + " per CU)";
+    return 0;
+  }
+  if (!h->d_gbar)
+    if (int rc = dalloc(&h->d_gbar, GB_WORDS)) return rc;
+  if (!h->h_fail) {
+    KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_fail), sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+  }
+  *h->h_fail = 0;
+  KMX_HIP(hipMemsetAsync(h->d_gbar, 0, sizeof(unsigned) * GB_WORDS, h->stream));
+  hipLaunchKernelGGL((k_round<R, RW>), dim3(h->ntiles), dim3(BLOCK), SmemRes<R>::bytes, h->stream, h->dv, h->d_gbar,
+                     h->h_fail, 1);
+  KMX_HIP(hipGetLastError());
+  KMX_HIP(hipStreamSynchronize(h->stream));
+  if (__atomic_load_n(h->h_fail, __ATOMIC_ACQUIRE) != 0) {
+    *h->h_fail = 0;
+    h->res_reason = "census: the " + std::to_string(h->ntiles) + " workgroups were not all resident";
+    return 0;
+  }
+  h->dv.gbar = h->d_gbar;
+  h->res_on = true;
+  h->res_reason = "";
+  return 0;
+}
+template <int R>
+int resident_setup_r(kmx_pgo* h) {
+  return h->rw == 10 ? resident_setup_t<R, 10>(h) : resident_setup_t<R, 16>(h);
+}
+int resident_setup(kmx_pgo* h) {
+  h->dv.gbar = nullptr;
+  h->res_on = false;
+  if (h->P.tcg_form != KMX_TCG_FORM_RESIDENT) {
+    h->res_reason = "tcg_form is not KMX_TCG_FORM_RESIDENT";
+    return 0;
+  }
+  switch (h->P.r) {
+    case 3: return resident_setup_r<3>(h);
+    case 4: return resident_setup_r<4>(h);
+    case 5: return resident_setup_r<5>(h);
+    case 6: return resident_setup_r<6>(h);
+    case 7: return resident_setup_r<7>(h);
+    default: return resident_setup_r<8>(h);
+  }
+}
+
 template <int R, int RW, int RM>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
+  if (h->res_on) {
+    enqueue_resident_t<R, RW>(h, d_active);
+    return;
+  }
   // no tiles: nothing would run the deferred rebuild
   const bool pend = enqueue_begin(h, d_active, BEGIN_ROUND, h->ntiles > 0);
   const bool rgd = h->P.method == KMX_METHOD_RGD;
@@ -3189,8 +3768,9 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
             "acceleration is 0 or 1, restart_interval >= 0");
   KMX_CHECK(params->method == KMX_METHOD_RTR || params->method == KMX_METHOD_RGD, KMX_EUNSUP,
             "method must be KMX_METHOD_RTR or KMX_METHOD_RGD");
-  KMX_CHECK(params->tcg_form == KMX_TCG_FORM_STANDARD || params->tcg_form == KMX_TCG_FORM_ONESYNC, KMX_EINVAL,
-            "tcg_form must be KMX_TCG_FORM_STANDARD or KMX_TCG_FORM_ONESYNC");
+  KMX_CHECK(params->tcg_form == KMX_TCG_FORM_STANDARD || params->tcg_form == KMX_TCG_FORM_ONESYNC ||
+                params->tcg_form == KMX_TCG_FORM_RESIDENT,
+            KMX_EINVAL, "tcg_form must be KMX_TCG_FORM_STANDARD, _ONESYNC or _RESIDENT");
   KMX_CHECK(params->method != KMX_METHOD_RGD || params->rgd_stepsize > 0.0, KMX_EINVAL, "rgd_stepsize must be > 0");
   KMX_CHECK(params->tile_incidences >= 0, KMX_EINVAL, "tile_incidences must be >= 0 (0: automatic)");
   int ndev = 0;
@@ -3225,6 +3805,7 @@ extern "C" int kmx_pgo_destroy(kmx_pgo* h) {
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   if (h->hstat) (void)hipHostFree(h->hstat);
+  if (h->h_fail) (void)hipHostFree(h->h_fail);
   delete h;
   return KMX_OK;
 }
@@ -3451,6 +4032,9 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   int64_t inc_all = (int64_t)inc_ptr[nloc] - inc_ptr[0];
   int64_t tilecap = std::min<int64_t>(2 * (int64_t)TP * r,
                                       std::max<int64_t>(180, (inc_all + TILES_TARGET - 1) / TILES_TARGET));
+  // the resident round keeps one tile per workgroup for the whole round: full
+  // 48-pose tiles (two chunks), so the cut needs the fewest resident workgroups
+  if (h->P.tcg_form == KMX_TCG_FORM_RESIDENT) tilecap = 2 * (int64_t)TP * r;
   if (h->P.tile_incidences > 0) tilecap = std::max(16, h->P.tile_incidences);
   for (int l = 0; l < L; ++l) {
     const int n = n_poses[h->robots[l]];
@@ -3611,6 +4195,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   enqueue_precond(h, 0);
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipStreamSynchronize(h->stream));
+  if (int rc2 = resident_setup(h)) return rc2;
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -3876,6 +4461,7 @@ extern "C" int kmx_pgo_comm_destroy(kmx_pgo* h) {
 
 // The handle's stream drained within timeout_s (polled), or KMX_ETIMEOUT: a
 // bounded wait for a round whose exchange depends on peers.
+static int check_resident_fail(kmx_pgo* h);
 extern "C" int kmx_pgo_sync_timeout(kmx_pgo* h, double timeout_s) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_CHECK(timeout_s > 0.0, KMX_EINVAL, "timeout_s must be > 0");
@@ -3883,7 +4469,7 @@ extern "C" int kmx_pgo_sync_timeout(kmx_pgo* h, double timeout_s) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipStreamQuery(h->stream);
-    if (e == hipSuccess) return KMX_OK;
+    if (e == hipSuccess) return check_resident_fail(h);
     if (e != hipErrorNotReady) return kmx::fail(KMX_EHIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
     if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
       return kmx::fail(KMX_ETIMEOUT, "the stream did not drain within the timeout (an exchange peer is missing?)");
@@ -4035,6 +4621,7 @@ extern "C" int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats
   std::vector<unsigned char> ones(L, 1);
   KMX_HIP(hipMemcpyAsync(h->d_active, ones.data(), L, hipMemcpyHostToDevice, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));
+  if (int rc = check_resident_fail(h)) return rc;
   if (stats) {
     for (int a = 0; a < h->n_robots; ++a) std::memset(&stats[a], 0, sizeof(kmx_iter_stats));
     for (int l = 0; l < L; ++l) {
@@ -4075,10 +4662,36 @@ extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local) 
   return KMX_OK;
 }
 
+// After a synchronisation: a resident round whose grid barrier gave up (a
+// workgroup not resident, or a fault that stopped a workgroup) left the round
+// incomplete; report it once.
+static int check_resident_fail(kmx_pgo* h) {
+  if (!h->h_fail) return KMX_OK;
+  const unsigned f = __atomic_load_n(h->h_fail, __ATOMIC_ACQUIRE);
+  if (f == 0) return KMX_OK;
+  *h->h_fail = 0;
+  return kmx::fail(KMX_EHIP, "resident round: grid barrier " + std::to_string(f - 1) +
+                                 " gave up waiting (the round is incomplete)");
+}
+
 extern "C" int kmx_pgo_sync(kmx_pgo* h) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->stream));
+  return check_resident_fail(h);
+}
+
+extern "C" int kmx_pgo_resident_info(kmx_pgo* h, int* resident, int* ntiles, int* capacity, char* reason,
+                                     int64_t nbytes) {
+  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
+  if (resident) *resident = h->res_on ? 1 : 0;
+  if (ntiles) *ntiles = h->ntiles;
+  if (capacity) *capacity = h->res_cap;
+  if (reason && nbytes > 0) {
+    const size_t n = std::min<size_t>((size_t)nbytes - 1, h->res_reason.size());
+    std::memcpy(reason, h->res_reason.data(), n);
+    reason[n] = 0;
+  }
   return KMX_OK;
 }
 

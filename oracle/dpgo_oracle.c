@@ -701,7 +701,7 @@ static void block_update(orc_pgo* h, int a, kmx_iter_stats* st, int inner) {
 #pragma omp parallel for num_threads(b.inner) schedule(static) if (b.inner > 1)
     for (int64_t k = 0; k < N; ++k) del[k] = -z[k];
     int stop = KMX_TCG_MAX_ITER, j;
-    if (h->P.tcg_form == KMX_TCG_FORM_ONESYNC) {
+    if (h->P.tcg_form != KMX_TCG_FORM_STANDARD) { /* ONESYNC, and RESIDENT (same arithmetic) */
       j = tcg_onesync(&b, &c, Delta, norm_r0, d_Pd, rr, z, del, Hd, wk_ + 11 * NP, Xt, c.eg, eta, Heta, st, &stop);
     } else
     for (j = 1; j <= h->P.tcg_max_iterations; ++j) {
