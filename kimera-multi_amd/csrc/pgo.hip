@@ -530,34 +530,36 @@ __device__ __forceinline__ Lane lane_map(const Dev& d) {
 }
 
 // --------------------------------------------------------------- gathers ---
-// LDS layouts. A tile holds TP = WAVES * (64 / R) poses; its incidences are one
-// contiguous CSR range walked in chunks of CH incidences (one lane each).
-template <int R>
+// LDS layouts. A tile holds TP = W * (64 / R) poses (W waves per workgroup:
+// WAVES for the launched kernels, 4 or 5 for the resident round); its
+// incidences are one contiguous CSR range walked in chunks of CH incidences
+// (one lane each).
+template <int R, int W = WAVES>
 struct SmemH {  // Hessian gather (k_hess, eval EHESS)
-  static constexpr int TP = WAVES * (64 / R);
-  static constexpr int CH = TP * R;                                       // <= BLOCK
+  static constexpr int TP = W * (64 / R);
+  static constexpr int CH = TP * R;                                       // <= 64 W
   static constexpr int c_off = 0;                                         // double[CH][R][4]
   static constexpr int ptr_off = CH * R * 32;                             // int[TP + 1]
   static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
-  static constexpr int bytes = red_off + RED_BYTES;
+  static constexpr int bytes = red_off + 8 * NPART * W + 16;
 };
-template <int R>
+template <int R, int W = WAVES>
 struct SmemHG {  // gradient / cost gathers: a chunk buffer plus the tile's own rows
-  static constexpr int TP = WAVES * (64 / R);
+  static constexpr int TP = W * (64 / R);
   static constexpr int CH = 240;                                          // incidences per chunk
   static constexpr int c_off = 0;                                         // double[CH][R][4]
   static constexpr int x_off = CH * R * 32;                               // double[TP][R][4]
   static constexpr int ptr_off = x_off + TP * R * 32;                     // int[TP + 1]
   static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
-  static constexpr int bytes = red_off + RED_BYTES;
+  static constexpr int bytes = red_off + 8 * NPART * W + 16;
 };
-template <int R>
+template <int R, int W = WAVES>
 struct SmemC {  // trial cost: own rows + CSR pointers only
-  static constexpr int TP = WAVES * (64 / R);
+  static constexpr int TP = W * (64 / R);
   static constexpr int x_off = 0;
   static constexpr int ptr_off = TP * R * 32;
   static constexpr int red_off = ptr_off + ((TP + 1) * 4 + 15) / 16 * 16;
-  static constexpr int bytes = red_off + RED_BYTES;
+  static constexpr int bytes = red_off + 8 * NPART * W + 16;
 };
 constexpr int SCR_BYTES = BLOCK * 6 * 8;  // group_symYtG<R, true> scratch
 struct SmemU {                            // element-wise kernels: scratch + reduction
@@ -582,10 +584,10 @@ struct NoPre {
 // would spill)
 // DIAG = false: the caller applies the diagonal block itself (k_step, whose
 // epilogue loads the own row and D_i with the rest of its rows in one batch).
-template <int R, int RW, bool REC_FIRST, typename Src, typename Pre, bool DIAG = true>
+template <int R, int RW, bool REC_FIRST, typename Src, typename Pre, bool DIAG = true, int W = WAVES>
 __device__ __forceinline__ bool hinc_gather_src(const Dev& d, const Lane& L, Src& src, double acc[4], char* smem,
                                                 Pre&& pre) {
-  using SM = SmemH<R>;
+  using SM = SmemH<R, W>;
   using RC = Rec<RW>;
   constexpr int CH = SM::CH;
   double* Cs = reinterpret_cast<double*>(smem + SM::c_off);
@@ -702,10 +704,10 @@ __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const d
 // rows (owning pose found by a binary search of the tile CSR), and adds the
 // incidence's cost share (1/2 per endpoint of a local edge; all of a shared
 // edge). The pose sums run in CSR order.
-template <int R, int RW>
+template <int R, int RW, int W = WAVES>
 __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const double* V, const double* pub,
                                           double acc[4], double* cost, char* smem) {
-  using SM = SmemHG<R>;
+  using SM = SmemHG<R, W>;
   using RC = Rec<RW>;
   constexpr int CH = SM::CH;
   double* Cs = reinterpret_cast<double*>(smem + SM::c_off);
@@ -723,7 +725,7 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
   if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
   {
     const double2* v2 = reinterpret_cast<const double2*>(V + (size_t)p0 * 4 * R);
-    for (int i = tid; i < np * 2 * R; i += BLOCK) xs[i] = v2[i];
+    for (int i = tid; i < np * 2 * R; i += 64 * W) xs[i] = v2[i];
   }
   __syncthreads();  // sptr, xs
   for (int c0 = 0; c0 < n; c0 += CH) {
@@ -1162,7 +1164,7 @@ struct RobotSum {
     for (int k = 0; k < NS; ++k) v[k] = 0.0;
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (t0 + (int)threadIdx.x + u * RBLOCK < t1) {
+      if (t0 + (int)threadIdx.x + u * RBLOCK < t1 && threadIdx.x < RBLOCK) {
 #pragma unroll
         for (int k = 0; k < NS; ++k) v[k] += a[u][k];
       }
@@ -1170,7 +1172,7 @@ struct RobotSum {
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
       const double w = wave_sum(v[k]);
-      if ((threadIdx.x & 63) == 0) lds[k * RW_ + (threadIdx.x >> 6)] = w;
+      if ((threadIdx.x & 63) == 0 && threadIdx.x < RBLOCK) lds[k * RW_ + (threadIdx.x >> 6)] = w;
     }
     __syncthreads();
 #pragma unroll
@@ -1747,7 +1749,7 @@ struct RobotSum8 {
       if (t1 - t0 > U * RBLOCK) load(part, tb);
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (tb + (int)threadIdx.x + u * RBLOCK < t1) {
+        if (tb + (int)threadIdx.x + u * RBLOCK < t1 && threadIdx.x < RBLOCK) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] += a[u][k];
         }
@@ -1756,7 +1758,7 @@ struct RobotSum8 {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const double w = wave_sum(v[k]);
-      if ((threadIdx.x & 63) == 0) lds[k * RW_ + (threadIdx.x >> 6)] = w;
+      if ((threadIdx.x & 63) == 0 && threadIdx.x < RBLOCK) lds[k * RW_ + (threadIdx.x >> 6)] = w;
     }
     __syncthreads();
 #pragma unroll
@@ -1769,10 +1771,10 @@ struct RobotSum8 {
   }
 };
 
-template <int R>
+template <int R, int W = WAVES>
 struct SmemF {  // k_step: the Hessian gather's layout with an 8-wide reduction area
-  static constexpr int red_off = SmemH<R>::red_off;
-  static constexpr int bytes = red_off + 8 * 8 * WAVES + 16;
+  static constexpr int red_off = SmemH<R, W>::red_off;
+  static constexpr int bytes = red_off + 8 * 8 * W + 16;
 };
 
 __device__ __forceinline__ double dot4(const double a[4], const double b[4]) {
@@ -2305,34 +2307,53 @@ struct WtRows {
 };
 
 // the tile's partials, written through (the robot sums read them sc1)
-template <int NV>
+template <int NV, int W>
 __device__ __forceinline__ void wt_tile_partials(const double* vals, double* dst, double* lds) {
 #pragma unroll
   for (int s = 0; s < NV; ++s) {
     const double w = wave_sum(vals[s]);
-    if ((threadIdx.x & 63) == 0) lds[s * WAVES + (threadIdx.x >> 6)] = w;
+    if ((threadIdx.x & 63) == 0) lds[s * W + (threadIdx.x >> 6)] = w;
   }
   __syncthreads();
   if (threadIdx.x < NV) {
     double t = 0.0;
 #pragma unroll
-    for (int w = 0; w < WAVES; ++w) t += lds[threadIdx.x * WAVES + w];
+    for (int w = 0; w < W; ++w) t += lds[threadIdx.x * W + w];
     wt_st1(dst + threadIdx.x, t);
   }
 }
 
-template <int R>
+template <int R, int W>
 struct SmemRes {  // the gathers' layouts at 0 (the largest of k_grad's, k_step's, k_cost's), then per pose D, M^-1, S
-  static constexpr int TP = WAVES * (64 / R);
-  static constexpr int a0 = SmemHG<R>::bytes > SmemF<R>::bytes ? SmemHG<R>::bytes : SmemF<R>::bytes;
-  static constexpr int a1 = a0 > SmemC<R>::bytes ? a0 : SmemC<R>::bytes;
+  static constexpr int TP = W * (64 / R);
+  static constexpr int a0 = SmemHG<R, W>::bytes > SmemF<R, W>::bytes ? SmemHG<R, W>::bytes : SmemF<R, W>::bytes;
+  static constexpr int a1 = a0 > SmemC<R, W>::bytes ? a0 : SmemC<R, W>::bytes;
   static constexpr int d_off = (a1 + 15) / 16 * 16;  // double[TP][16]
   static constexpr int p_off = d_off + TP * 16 * 8;  // double[TP][16]
   static constexpr int s_off = p_off + TP * 16 * 8;  // double[TP][9]
   static constexpr int g_off = s_off + TP * 9 * 8;   // double[TP][R][4]: g, then the trial point
-  static constexpr int red_off = g_off + TP * R * 32; // double[8 * WAVES]
-  static constexpr int bytes = red_off + 8 * 8 * WAVES;
+  static constexpr int red_off = g_off + TP * R * 32; // double[8 * W]
+  static constexpr int bytes = red_off + 8 * 8 * W;
+  static_assert(64 * W * 6 * 8 <= SmemH<R, W>::ptr_off, "group-op scratch inside the chunk area");
 };
+
+// KMX_RES_STAMPS builds (diagnostic, `make res_stamps`): thread 0 of every
+// workgroup records the wall clock (100 MHz) at the phases of the last round
+// (kmx_pgo_debug_step_stamps; scripts/res_stamps.py): 0 entry, 1 prologue, 2
+// gradient; per tCG pass jl < 17 at 4 + 5 jl: barrier arrival, release,
+// decision, gather, step end; 90 cost start, 91 cost end, 92 final release,
+// 93 exit; 94 tile poses, 95 tile incidences.
+#ifdef KMX_RES_STAMPS
+constexpr int RES_STAMP_TILES = 2048;
+__device__ unsigned long long g_res_stamp[96 * RES_STAMP_TILES];
+#define KMX_RS(i)                                                                                  \
+  do {                                                                                             \
+    const int i_ = (i);                                                                            \
+    if (threadIdx.x == 0 && L.tile < RES_STAMP_TILES && i_ < 96) g_res_stamp[L.tile * 96 + i_] = wall_clock64(); \
+  } while (0)
+#else
+#define KMX_RS(i) do {} while (0)
+#endif
 
 // Scalar decisions of one tCG step, taken by thread 0 on the workgroup's copy
 // of its robot's state and broadcast through LDS.
@@ -2347,9 +2368,9 @@ struct alignas(16) ResShared {
   int flag, pad[3];
 };
 
-template <int R, int RW>
+template <int R, int RW, int W>
 __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned* fail, int census, char* smem) {
-  using SM = SmemRes<R>;
+  using SM = SmemRes<R, W>;
   __shared__ Ctl cs;
   __shared__ ResShared rsh;
   ResStep& rst = rsh.st;
@@ -2361,6 +2382,13 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     return;
   }
   const Lane L = lane_map<R>(d);
+  KMX_RS(0);
+#ifdef KMX_RES_STAMPS
+  if (threadIdx.x == 0 && L.tile < RES_STAMP_TILES) {
+    g_res_stamp[L.tile * 96 + 94] = L.np;
+    g_res_stamp[L.tile * 96 + 95] = L.n;
+  }
+#endif
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   const unsigned ob = (unsigned)o * 8u;  // byte offset of the lane's row
   const int pl = L.pose - L.p0;
@@ -2392,12 +2420,13 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     for (int k = 0; k < 16; ++k) dst[k] = M[k];
   }
   const int ph0 = cs.phase;  // (read before any barrier of this launch: every thread sees k_begin's value)
+  KMX_RS(1);
   // -------- gradient (body_grad's arithmetic; X and the public table are the round's start) --------
   double y[4] = {0, 0, 0, 0}, rn[4] = {0, 0, 0, 0}, zn[4] = {0, 0, 0, 0};
   const bool grad = ph0 == PH_START;
   if (grad) {
     double G[4], cost = 0.0;
-    hinc_grad<R, RW>(d, L, d.X, d.pub, G, &cost, smem);
+    hinc_grad<R, RW, W>(d, L, d.X, d.pub, G, &cost, smem);
     if (L.valid) load4(d.X + o, y);
     double S[9], gr[4];
     group_symYtG<R, true>(y, G, L.base, S, scr);
@@ -2425,8 +2454,9 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) rn[c] = gr[c];  // r_0 = g
-    wt_tile_partials<3>(vals, d.part + (size_t)L.tile * NPART, red);
+    wt_tile_partials<3, W>(vals, d.part + (size_t)L.tile * NPART, red);
   }
+  KMX_RS(2);
   // -------- tCG, one barrier per step (body_step's arithmetic) --------
   double hzn[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0}, wn[4] = {0, 0, 0, 0},
          et[4] = {0, 0, 0, 0};
@@ -2437,7 +2467,9 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     bool go = false;
     double coef = 0.0, al = 0.0, be = 0.0;
     auto decide = [&]() -> bool {
+      KMX_RS(4 + 5 * jl);
       if (!grid_sync(gb, b++, formed, &any, fail, &sflag)) return false;
+      KMX_RS(5 + 5 * jl);
       if (!any) return false;
       if (!formed) return false;  // not in tCG (skipped, idle, or stopped earlier)
       double tot[8];
@@ -2479,12 +2511,14 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
       coef = rst.coef;
       al = rst.al;
       be = rst.be;
+      KMX_RS(6 + 5 * jl);
       return go;
     };
     double H[4];
     WtRows<R> src{jl == 0 ? rz : ((k & 1) ? rw1 : rw0)};
-    hinc_gather_src<R, RW, false, WtRows<R>, decltype(decide)&, false>(d, L, src, H, smem, decide);
+    hinc_gather_src<R, RW, false, WtRows<R>, decltype(decide)&, false, W>(d, L, src, H, smem, decide);
     if (sflag == 0) return;  // a barrier gave up (the fail word is set)
+    KMX_RS(7 + 5 * jl);
     if (!any) break;
     if (formed && !go && jl > 0) {
       // the robot's tCG ends here: the last residual, eta's last direction
@@ -2510,7 +2544,7 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
 #pragma unroll
         for (int c = 0; c < 4; ++c) gx[c] = xt[c];  // the trial cost's own row (and the commit's)
       }
-      wt_tile_partials<2>(vals, d.part + (size_t)L.tile * NPART + 2, red);
+      wt_tile_partials<2, W>(vals, d.part + (size_t)L.tile * NPART + 2, red);
       trial = true;
     }
     formed = go;
@@ -2575,12 +2609,14 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
       pv[6] = dot4(hdl, hdl);
       wt_st4((kn & 1) ? rw1 : rw0, ob, wn);
     }
-    wt_tile_partials<7>(pv, d.part_f + ((size_t)(kn & 1) * d.ntiles + L.tile) * 8, red);
+    wt_tile_partials<7, W>(pv, d.part_f + ((size_t)(kn & 1) * d.ntiles + L.tile) * 8, red);
+    KMX_RS(8 + 5 * jl);
     k = kn;
   }
   // -------- trial cost, accept, commit (body_cost + body_commit's fold) --------
+  KMX_RS(90);
   if (trial) {  // uniform per robot: the owner incidences' cost of the trial point
-    using SC = SmemC<R>;
+    using SC = SmemC<R, W>;
     int* sptr = reinterpret_cast<int*>(smem + SC::ptr_off);
     const double2* xs = reinterpret_cast<const double2*>(smem + SM::g_off);  // the tile's trial rows
     const int tid = threadIdx.x, np = L.np, K0 = L.k0, n = L.n;
@@ -2589,7 +2625,7 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     __syncthreads();
     double cost = 0.0;
     using RC = Rec<RW>;
-    for (int kk = tid; kk < n; kk += BLOCK) {
+    for (int kk = tid; kk < n; kk += 64 * W) {
       double2 q[RC::Q];
       RC::load(d.rec, (size_t)(K0 + kk), q);
       const int2 in = RC::inc(q);
@@ -2627,9 +2663,11 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
       }
       cost += c;
     }
-    wt_tile_partials<1>(&cost, d.part + (size_t)L.tile * NPART, red);
+    wt_tile_partials<1, W>(&cost, d.part + (size_t)L.tile * NPART, red);
   }
+  KMX_RS(91);
   if (!grid_sync(gb, b++, false, &any, fail, &sflag)) return;
+  KMX_RS(92);
   bool commit = false;
   if (trial) {
     RobotSum<NPART, 2, true> rs;
@@ -2653,6 +2691,7 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     d.gnc->inner += 1;
     d.gnc->rounds += 1;
   }
+  KMX_RS(93);
   if (!commit || !L.valid) return;
   double xt[4] = {gx[0], gx[1], gx[2], gx[3]};
   store4(d.X + o, xt);
@@ -2660,10 +2699,15 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
   if (s >= 0) store4(d.pub + (size_t)s * 4 * R + 4 * L.a, xt);
 }
 
-template <int R, int RW>
-__global__ __launch_bounds__(BLOCK, 2) void k_round(Dev d, unsigned* gb, unsigned* fail, int census) {
+// W = 4: up to two workgroups per CU (2 waves per SIMD); W = 5 (r = 5 only):
+// 60-pose tiles, one workgroup per CU (a SIMD hosts two of its waves), so a
+// 12.5k-pose shard needs fewer workgroups than the device has CUs and no CU
+// runs two tiles (a CU with two took ~10 us more per tCG step than one with
+// one: the barrier waits for it; profiles/r05/resident/)
+template <int R, int RW, int W>
+__global__ __launch_bounds__(64 * W, 2) void k_round(Dev d, unsigned* gb, unsigned* fail, int census) {
   KMX_SMEM;
-  body_round<R, RW>(d, gb, fail, census, smem);
+  body_round<R, RW, W>(d, gb, fail, census, smem);
 }
 
 // ------------------------------------------------- round begin + GNC-TLS ---
@@ -3216,6 +3260,7 @@ struct kmx_pgo {
   // KMX_TCG_FORM_RESIDENT: one persistent launch per round (k_round) when every
   // tile fits resident (decided at set_graph: occupancy query + census launch)
   bool res_on = false;
+  int res_w = 4;               // waves per workgroup of the resident round (the tile cut's)
   int res_cap = 0;             // workgroups of k_round resident on the device
   std::string res_reason = "tcg_form is not KMX_TCG_FORM_RESIDENT";
   unsigned* d_gbar = nullptr;  // grid-barrier words (GB_WORDS)
@@ -3581,11 +3626,22 @@ void enqueue_trial_t(kmx_pgo* h, bool rgd) {
 
 // KMX_TCG_FORM_RESIDENT: the round begin (GNC decision and re-weighting; the
 // preconditioner rebuild is left to k_round), then the whole block update.
+template <int R, int RW, int W>
+void launch_round(kmx_pgo* h, int census) {
+  hipLaunchKernelGGL((k_round<R, RW, W>), dim3(h->ntiles), dim3(64 * W), (SmemRes<R, W>::bytes), h->stream, h->dv,
+                     h->d_gbar, h->h_fail, census);
+}
+template <int R, int RW>
+void launch_round_w(kmx_pgo* h, int census) {
+  if constexpr (R == 5) {
+    if (h->res_w == 5) return launch_round<R, RW, 5>(h, census);
+  }
+  launch_round<R, RW, 4>(h, census);
+}
 template <int R, int RW>
 void enqueue_resident_t(kmx_pgo* h, const unsigned char* d_active) {
   (void)enqueue_begin(h, d_active, BEGIN_ROUND, true);
-  hipLaunchKernelGGL((k_round<R, RW>), dim3(h->ntiles), dim3(BLOCK), SmemRes<R>::bytes, h->stream, h->dv, h->d_gbar,
-                     h->h_fail, 0);
+  launch_round_w<R, RW>(h, 0);
 }
 
 // Whether the resident round can run on this handle: RTR with one RTR
@@ -3605,7 +3661,22 @@ int resident_setup_t(kmx_pgo* h) {
       return 0;
     }
   int nb = 0, cus = 0;
-  KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_round<R, RW>, BLOCK, SmemRes<R>::bytes));
+  if constexpr (R == 5) {
+    if (h->res_w == 5) {
+      if (SmemRes<R, 5>::bytes > 65536)
+        KMX_HIP(hipFuncSetAttribute((const void*)k_round<R, RW, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    SmemRes<R, 5>::bytes));
+      KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_round<R, RW, 5>, 64 * 5,
+                                                           SmemRes<R, 5>::bytes));
+    }
+  }
+  if (h->res_w != 5) {
+    if (SmemRes<R, 4>::bytes > 65536)
+      KMX_HIP(hipFuncSetAttribute((const void*)k_round<R, RW, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  SmemRes<R, 4>::bytes));
+    KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_round<R, RW, 4>, 64 * 4,
+                                                         SmemRes<R, 4>::bytes));
+  }
   KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
   h->res_cap = nb * cus;
   if (h->ntiles > h->res_cap) {
@@ -3620,8 +3691,7 @@ int resident_setup_t(kmx_pgo* h) {
   }
   *h->h_fail = 0;
   KMX_HIP(hipMemsetAsync(h->d_gbar, 0, sizeof(unsigned) * GB_WORDS, h->stream));
-  hipLaunchKernelGGL((k_round<R, RW>), dim3(h->ntiles), dim3(BLOCK), SmemRes<R>::bytes, h->stream, h->dv, h->d_gbar,
-                     h->h_fail, 1);
+  launch_round_w<R, RW>(h, 1);
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipStreamSynchronize(h->stream));
   if (__atomic_load_n(h->h_fail, __ATOMIC_ACQUIRE) != 0) {
@@ -4018,7 +4088,6 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   // workgroup's gather walks about the same number of incidences (a tile closes
   // when the next pose would take it past 1.05 x the robot's mean per full tile)
   // and capped at two chunks of TP * r incidences (two LDS hand-offs in k_hess)
-  const int TP = WAVES * (64 / r);
   std::vector<int> tr, tp0, tnp, rt0(L + 1, 0);
   // incidences per tile: at most two gather chunks; small problems are cut
   // finer, to about TILES_TARGET tiles (3 workgroups per CU, one generation),
@@ -4030,33 +4099,56 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   // overrides it (the multi-rank driver sets it from the team; bench.py
   // --tile-incidences for sweeps).
   int64_t inc_all = (int64_t)inc_ptr[nloc] - inc_ptr[0];
-  int64_t tilecap = std::min<int64_t>(2 * (int64_t)TP * r,
-                                      std::max<int64_t>(180, (inc_all + TILES_TARGET - 1) / TILES_TARGET));
-  // the resident round keeps one tile per workgroup for the whole round: full
-  // 48-pose tiles (two chunks), so the cut needs the fewest resident workgroups
-  if (h->P.tcg_form == KMX_TCG_FORM_RESIDENT) tilecap = 2 * (int64_t)TP * r;
-  if (h->P.tile_incidences > 0) tilecap = std::max(16, h->P.tile_incidences);
-  for (int l = 0; l < L; ++l) {
-    const int n = n_poses[h->robots[l]];
-    const int base = h->loff[l];
-    rt0[l] = (int)tr.size();
-    const int64_t inc_l = (int64_t)inc_ptr[base + n] - inc_ptr[base];
-    const int64_t full = std::max<int64_t>(1, (n + TP - 1) / TP);
-    const int64_t cap = std::min(tilecap, std::max<int64_t>(1, (inc_l * 21 / 20 + full - 1) / full));
-    int p0 = 0;
-    while (p0 < n) {
-      int np = 0;
-      int64_t cum = 0;
-      while (p0 + np < n && np < TP) {
-        const int64_t dg = inc_ptr[base + p0 + np + 1] - inc_ptr[base + p0 + np];
-        if (np > 0 && cum + dg > cap) break;
-        cum += dg;
-        ++np;
+  auto cut = [&](int TP, int64_t tilecap) {
+    tr.clear(); tp0.clear(); tnp.clear();
+    for (int l = 0; l < L; ++l) {
+      const int n = n_poses[h->robots[l]];
+      const int base = h->loff[l];
+      rt0[l] = (int)tr.size();
+      const int64_t inc_l = (int64_t)inc_ptr[base + n] - inc_ptr[base];
+      const int64_t full = std::max<int64_t>(1, (n + TP - 1) / TP);
+      const int64_t cap = std::min(tilecap, std::max<int64_t>(1, (inc_l * 21 / 20 + full - 1) / full));
+      int p0 = 0;
+      while (p0 < n) {
+        int np = 0;
+        int64_t cum = 0;
+        while (p0 + np < n && np < TP) {
+          const int64_t dg = inc_ptr[base + p0 + np + 1] - inc_ptr[base + p0 + np];
+          if (np > 0 && cum + dg > cap) break;
+          cum += dg;
+          ++np;
+        }
+        tr.push_back(l);
+        tp0.push_back(base + p0);
+        tnp.push_back(np);
+        p0 += np;
       }
-      tr.push_back(l);
-      tp0.push_back(base + p0);
-      tnp.push_back(np);
-      p0 += np;
+    }
+  };
+  h->res_w = WAVES;
+  {
+    const int TP = WAVES * (64 / r);
+    int64_t tilecap = std::min<int64_t>(2 * (int64_t)TP * r,
+                                        std::max<int64_t>(180, (inc_all + TILES_TARGET - 1) / TILES_TARGET));
+    // the resident round keeps one tile per workgroup for the whole round: full
+    // tiles (two chunks), so the cut needs the fewest resident workgroups
+    if (h->P.tcg_form == KMX_TCG_FORM_RESIDENT) tilecap = 2 * (int64_t)TP * r;
+    if (h->P.tile_incidences > 0) tilecap = std::max(16, h->P.tile_incidences);
+    cut(TP, tilecap);
+    int cus = 0;
+    KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+    if (h->P.tcg_form == KMX_TCG_FORM_RESIDENT && r == 5 && (int)tr.size() > cus) {
+      // more 48-pose tiles than CUs: 5-wave workgroups of 60 poses, one per
+      // CU, when that cut fits (k_round W = 5)
+      const int TP5 = 5 * (64 / r);
+      const int64_t cap5 = h->P.tile_incidences > 0 ? std::max(16, h->P.tile_incidences) : 2 * (int64_t)TP5 * r;
+      std::vector<int> tr4 = tr, tp04 = tp0, tnp4 = tnp, rt04 = rt0;
+      cut(TP5, cap5);
+      if ((int)tr.size() <= cus) {
+        h->res_w = 5;
+      } else {
+        tr = tr4; tp0 = tp04; tnp = tnp4; rt0 = rt04;
+      }
     }
   }
   rt0[L] = (int)tr.size();
@@ -4979,6 +5071,12 @@ extern "C" int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out) {
 // KMX_EUNSUP in the product build.
 extern "C" int kmx_pgo_debug_step_stamps(uint64_t* out, int64_t n) {
   KMX_GUARD_BEGIN
+#ifdef KMX_RES_STAMPS
+  KMX_CHECK(out && n >= 0, KMX_EINVAL, "null buffer");
+  const int64_t m = std::min<int64_t>(n, 96 * (int64_t)RES_STAMP_TILES);
+  KMX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_stamp), sizeof(uint64_t) * m, 0, hipMemcpyDeviceToHost));
+  return KMX_OK;
+#endif
 #ifdef KMX_STEP_STAMPS
   KMX_CHECK(out && n >= 0, KMX_EINVAL, "null buffer");
   const int64_t m = std::min<int64_t>(n, 16 * (int64_t)STEP_STAMP_TILES);

@@ -2,7 +2,7 @@
 # k_hess launch for the product build and for KMX_HESS_PROBE builds that each
 # drop one stream (1 neighbour rows, 2 own rows + D_i, 4 delta_old / Hdelta_old,
 # 8 the delta / Hdelta stores, 15 all: records + CSR only), built beforehand by
-# `make -C kimera-multi_amd/csrc probe PROBE=n` into alt/.
+# `make -C kimera-multi_amd/csrc probe PROBE=n` into diag/.
 # usage: [BURN=40] bash scripts/gpu_hess_probe.sh TAG [variants...]  (BURN: rounds before the window;
 # 10 = first tCG steps, 40 = the bench steady-state window with delta_old / Hdelta_old in play)
 set -o pipefail
@@ -12,7 +12,7 @@ T=${1:-hprobe}; shift
 V=${@:-0 1 2 4 8 15}
 mkdir -p gpurun_out/$T
 for v in $V; do
-  if [ "$v" = 0 ]; then lib=$PWD/kimera-multi_amd/kmx/libkmx.so; else lib=$PWD/alt/libkmx_hp$v.so; fi
+  if [ "$v" = 0 ]; then lib=$PWD/kimera-multi_amd/kmx/libkmx.so; else lib=$PWD/diag/libkmx_hp$v.so; fi
   O=gpurun_out/$T/v$v
   mkdir -p $O
   i=0

@@ -16,7 +16,7 @@ table (rows gathered once) and times rounds under:
          peers' — timing only), all rounds from one iterate_async call
 The handle's tCG enqueueing is the default adaptive mode
 (kmx_pgo_set_tcg_poll(-1)).
-usage: python scripts/host_seam.py N [rounds] [standard|onesync]  (the tCG form)
+usage: python scripts/host_seam.py N [rounds] [standard|onesync|resident]  (the tCG form)
 """
 import os
 import sys
@@ -46,7 +46,7 @@ dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cu
 g = config("synth100k", seed=0)
 P = bench.params()
 P.localOptimizationParams.tCG_form = sys.argv[3] if len(sys.argv) > 3 else "standard"
-P = dataclasses.replace(P, tileIncidences=team_tile_incidences(g, N, P.r))
+P = dataclasses.replace(P, tileIncidences=team_tile_incidences(g, N, P.r, P.localOptimizationParams.tCG_form))
 Y = lifting_matrix(5, seed=1)
 lo, hi = robot_ranges(g.n_robots, N)[0]
 local = np.zeros(g.n_robots, np.uint8)
@@ -78,6 +78,10 @@ sbuf = torch.zeros(n_send * ps + N, dtype=torch.float64, device=dev)
 rbuf = torch.zeros(n_recv * ps + N, dtype=torch.float64, device=dev)
 wire_in = torch.zeros(n_recv * ps + N, dtype=torch.float64, device=dev)
 wire_out = torch.zeros_like(wire_in)
+if P.localOptimizationParams.tCG_form == "resident":
+    _s = make()
+    print("resident:", _s.resident_info(), flush=True)
+    _s.close()
 print(f"N={N}: rank 0 holds robots {lo}..{hi - 1}, {int(g.n_poses[lo:hi].sum())} poses; "
       f"sends {n_send} rows, receives {n_recv} rows ({n_recv * ps * 8 / 1e6:.2f} MB) per round; "
       f"adaptive tCG enqueueing, {P.localOptimizationParams.tCG_form} tCG", flush=True)

@@ -1,6 +1,6 @@
 """Phase timeline of one one-sync tCG launch (k_step) on a 12.5k-pose block,
 from a KMX_STEP_STAMPS build (`make -C kimera-multi_amd/csrc stamps`, run with
-KMX_LIB=alt/libkmx_ss.so): per workgroup the wall clock (100 MHz) at entry,
+KMX_LIB=diag/libkmx_ss.so): per workgroup the wall clock (100 MHz) at entry,
 after the decision, after the gather loop, after the Hessian's own part and at
 exit of the last launch that formed step 2. Prints, relative to the earliest
 entry, the spread of each stamp over the workgroups and the per-phase
