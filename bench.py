@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--lcd-steps", type=int, default=8,
                     help="back-to-back LCD verification calls timed (a call's kNN2 overlaps the previous call's "
                          "RANSAC tail on the detector's second candidate slot, as in a stream of queries)")
+    ap.add_argument("--lcd-hard", type=int, default=4096,
+                    help="candidates of the hard LCD leg (look-alikes that pass Lowe and fail geometry; 0 = skip)")
     ap.add_argument("--lcd-algo", type=int, default=0,
                     help="ransac_2d2d_algorithm: 0 Stewenius (the reference config, LcdParams.yaml:73), 1 Nister")
     return ap.parse_args()
@@ -307,6 +309,10 @@ def lcd_leg(args, rank, world, barrier_sync):
     out["stream"] = stream_leg(det, pool, cq, cm, args)
     out["hamming"] = hamming_leg(args, pool, cq, cm, barrier_sync)
     det.close()
+    if args.lcd_hard > 0:
+        out["hard"], hard_pool = hard_leg(args, params, rank, world, barrier_sync)
+        if rank == 0 and world == 1:
+            out["single"] = single_leg(args, params, pool, hard_pool)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, str(ROOT))
@@ -322,6 +328,112 @@ def lcd_leg(args, rank, world, barrier_sync):
                "sample": f"first {n} candidates of configs[2] (half planted), oracle/lcd_oracle.c, 1 thread, "
                          f"{done:.1f} s"}
     return out, cpu
+
+
+def hard_leg(args, params, rank, world, barrier_sync):
+    """The expensive case of a real BoW candidate stream (VERDICT r4 items 3 /
+    weak 5): false candidates whose frames share look-alike descriptors (150
+    of 500 features: the match frame's descriptor with 5 % of its bits
+    flipped, unrelated geometry). They pass Lowe and fail geometry, so every
+    one runs the 2D-2D RANSAC to its 500-iteration cap (LcdParams.yaml:64-65).
+    Same solver, parameters and batching as the configs[2] leg; the 1-thread C
+    restatement on a bounded sample of the same candidates beside it."""
+    from kmx.lcd import LcdParams, LoopClosureDetector
+    from kmx.synth.lcd import make_lcd_pool
+    C_ = args.lcd_hard
+    pool = make_lcd_pool(2 * C_, 500, true_frac=0.0, false_frac=0.3, seed=3)
+    det = LoopClosureDetector(params, device=int(os.environ.get("KMX_BENCH_DEVICE", "0")))
+    det.set_pool(pool)
+    cq = pool.cand_query[0::2][rank::world].copy()  # (2k, 2k + 1): the look-alike pairs
+    cm = pool.cand_match[0::2][rank::world].copy()
+    det.verify_async(cq, cm)
+    det.sync()
+    barrier_sync()
+    steps = 2
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        det.verify_async(cq, cm)
+    det.sync()
+    barrier_sync()
+    el = time.perf_counter() - t0
+    det.enable_timing(True)
+    det.verify_async(cq, cm)
+    det.sync()
+    tk = det.read_timing()
+    res, _ = det.verify(cq[:512], cm[:512])
+    det.close()
+    its = np.array([r["iterations_2d2d"] for r in res])
+    nm = np.array([r["n_matches"] for r in res])
+    out = {"metric": "LC candidates verified/sec (hard: look-alikes that fail geometry)", "unit": "candidates/s",
+           "value": steps * len(cq) / el * world, "n_local": int(len(cq)), "steps": steps, "elapsed": el,
+           "ransac_ms": tk["ransac_ms"], "knn_ms": tk["knn_ms"],
+           "first512": {"accepted": int(sum(r["accepted"] for r in res)), "iterations_2d2d_mean": float(its.mean()),
+                        "iterations_2d2d_min": int(its.min()), "matches_after_lowe_mean": float(nm.mean())},
+           "workload": f"{len(cq)} candidates of {2 * C_} synthetic frames x 500 ORB features: 150 look-alike "
+                       "descriptors per pair (5 % of bits flipped), no true correspondence; "
+                       + ("Stewenius" if args.lcd_algo == 0 else "Nister") + " RANSAC, reference parameters"}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, str(ROOT))
+        from oracle import oracle as O
+        p = params.to_c()
+        n, t0c, done = 0, time.perf_counter(), 0.0
+        while done < args.cpu_seconds * 0.25 and n < len(cq):
+            O.lcd_verify(p, pool, cand_query=cq[n:n + 8], cand_match=cm[n:n + 8], masks=False)
+            n += 8
+            done = time.perf_counter() - t0c
+        out["cpu_baseline"] = {"value": n / done, "unit": "candidates/s", "cores": 1, "kind": "port",
+                               "sample": f"first {n} hard candidates, oracle/lcd_oracle.c, 1 thread, {done:.1f} s"}
+        out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+    return out, pool
+
+
+def single_leg(args, params, pool, hard_pool):
+    """Call-for-call latency: the reference verifies ONE
+    candidate per call on its verification thread (verifyLoopSpin ->
+    computeMatchedIndices -> geometricVerificationNister -> recoverPose,
+    drawio:2638-2657; INTEGRATION.md section 2 binds exactly that). Here the
+    same three calls per candidate through the Python mirror (kmx_lcd_match,
+    kmx_lcd_verify_matches STAGE_2D2D, then STAGE_RECOVER on its inliers),
+    host argument handling and the device round trips included, for planted
+    loop closures of configs[2] and for hard candidates; the 1-thread C
+    restatement's time for the same candidates (one lcd_verify call each)
+    beside it."""
+    from kmx.lcd import LoopClosureDetector
+    sys.path.insert(0, str(ROOT))
+    from oracle import oracle as O
+    out = {}
+    for name, pl, idx in (("planted", pool, np.arange(0, 64, 2)), ("hard", hard_pool, np.arange(0, 16, 2))):
+        det = LoopClosureDetector(params, device=int(os.environ.get("KMX_BENCH_DEVICE", "0")))
+        det.set_pool(pl)
+        q, m = pl.cand_query[idx], pl.cand_match[idx]
+        lat, acc = [], 0
+        for rep in range(2):  # the first pass warms the call path up
+            lat = []
+            for a, b in zip(q, m):
+                t0 = time.perf_counter()
+                iq, im = det.computeMatchedIndices(int(a), int(b))
+                ok, iq2, im2, T = det.geometricVerificationNister(int(a), int(b), iq, im)
+                if ok:
+                    ok2, T2, _ = det.recoverPose(int(a), int(b), iq2, im2, T)
+                    acc += int(ok2) if rep else 0
+                lat.append(time.perf_counter() - t0)
+        det.close()
+        cpu = []
+        if not args.no_cpu:
+            p = params.to_c()
+            for a, b in zip(q, m):
+                t0 = time.perf_counter()
+                O.lcd_verify(p, pl, cand_query=np.array([a], np.int32), cand_match=np.array([b], np.int32),
+                             masks=False)
+                cpu.append(time.perf_counter() - t0)
+        lat = np.array(lat) * 1e3
+        out[name] = {"candidates": int(len(q)), "accepted": acc, "gpu_ms_median": float(np.median(lat)),
+                     "gpu_ms_max": float(lat.max()),
+                     "cpu_ms_median": float(np.median(cpu) * 1e3) if cpu else None,
+                     "gpu_over_cpu_latency": (float(np.median(lat)) / (np.median(cpu) * 1e3)) if cpu else None}
+    out["note"] = ("one candidate per call chain (computeMatchedIndices, geometricVerificationNister, recoverPose), "
+                   "as the reference's verification thread; one wave runs one candidate's RANSAC (k_ransac_coop)")
+    return out
 
 
 def stream_leg(det, pool, cq, cm, args):
