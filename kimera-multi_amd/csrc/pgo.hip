@@ -2240,7 +2240,11 @@ __device__ __forceinline__ unsigned gb_load(unsigned* p) {
 // One grid barrier (index b within the launch). `cont`: this workgroup's robot
 // formed a tCG step whose partials the next step consumes; *any: some
 // workgroup arrived with cont. Returns false when the wait gave up.
-__device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, bool* any, unsigned* fail, int* sflag) {
+// `during`: work of thread 0 between its arrival and its poll (it must not
+// touch anything another workgroup reads after this barrier)
+template <typename F>
+__device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, bool* any, unsigned* fail, int* sflag,
+                                          F&& during) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -2257,6 +2261,7 @@ __device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, b
       const unsigned o2 = __hip_atomic_fetch_add(gb + GB_TOP * GB_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (o2 + 1 == G * e) __hip_atomic_store(gb + GB_GEN * GB_STRIDE, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    during();
     int ok = 1;
     const unsigned long long t0 = wall_clock64();
     while (gb_load(gb + GB_GEN * GB_STRIDE) < e) {
@@ -2273,6 +2278,9 @@ __device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, b
   const int f = *sflag;
   *any = (f & 2) != 0;
   return (f & 1) != 0;
+}
+__device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, bool* any, unsigned* fail, int* sflag) {
+  return grid_sync(gb, b, cont, any, fail, sflag, []() {});
 }
 
 // write-through row I/O: 16-B buffer loads / stores with the sc1 bit (aux 16)
@@ -2332,9 +2340,27 @@ struct SmemRes {  // the gathers' layouts at 0 (the largest of k_grad's, k_step'
   static constexpr int p_off = d_off + TP * 16 * 8;  // double[TP][16]
   static constexpr int s_off = p_off + TP * 16 * 8;  // double[TP][9]
   static constexpr int g_off = s_off + TP * 9 * 8;   // double[TP][R][4]: g, then the trial point
-  static constexpr int red_off = g_off + TP * R * 32; // double[8 * W]
-  static constexpr int bytes = red_off + 8 * 8 * W;
+  static constexpr int CH = SmemH<R, W>::CH;          // a resident tile holds at most two chunks
+  template <int RW>
+  static constexpr int rec_off = g_off + TP * R * 32;  // double[2 CH][RW]: the tile's incidence records
+  template <int RW>
+  static constexpr int sp_off = rec_off<RW> + 2 * CH * RW * 8;  // int[TP + 1]: the tile's CSR offsets
+  template <int RW>
+  static constexpr int red_off = sp_off<RW> + ((TP + 1) * 4 + 15) / 16 * 16;  // double[8 * W]
+  template <int RW>
+  static constexpr int base_bytes = red_off<RW> + 8 * 8 * W;
+  // Hz and eta: in LDS when they fit (two fewer register-resident vectors for
+  // the 5-wave form, whose SIMDs host two waves: 256 VGPRs), else in registers
+  template <int RW>
+  static constexpr bool lv = W > 4 && base_bytes<RW> + 2 * TP * R * 32 + 304 <= 160 * 1024;
+  template <int RW>
+  static constexpr int hz_off = base_bytes<RW>;  // double[TP][R][4] (lv)
+  template <int RW>
+  static constexpr int et_off = hz_off<RW> + TP * R * 32;  // double[TP][R][4] (lv)
+  template <int RW>
+  static constexpr int bytes = base_bytes<RW> + (lv<RW> ? 2 * TP * R * 32 : 0);
   static_assert(64 * W * 6 * 8 <= SmemH<R, W>::ptr_off, "group-op scratch inside the chunk area");
+  static_assert(bytes<16> + 304 <= 160 * 1024, "one resident workgroup per CU");
 };
 
 // KMX_RES_STAMPS builds (diagnostic, `make res_stamps`): thread 0 of every
@@ -2368,6 +2394,79 @@ struct alignas(16) ResShared {
   int flag, pad[3];
 };
 
+// The resident round's Hessian gather (hinc_gather_src's arithmetic, sums and
+// order): the tile's records and CSR offsets are in LDS for the whole round,
+// so both chunks' neighbour rows are requested right after the decision — one
+// dependent round trip per tCG step instead of record -> row per chunk.
+// acc = the off-diagonal part of (Q V) for the lane's row; false: pre() said
+// the robot does not step (nothing gathered).
+template <int R, int RW, int W, typename Pre>
+__device__ __forceinline__ bool res_gather(const Lane& L, const double* recs, const int* sptr, const WtRows<R>& src,
+                                           double acc[4], double* Cs, Pre&& pre) {
+  using RC = Rec<RW>;
+  constexpr int CH = SmemH<R, W>::CH;
+  constexpr int OI = RW == 10 ? 9 : 14;  // the {other, edge | tail} word of a record
+  const int tid = threadIdx.x, n = L.n, pl = L.pose - L.p0;
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+  if (!pre()) return false;
+  const int lt = min(tid, CH - 1);
+  auto other = [&](int k) { return unpack_int2(recs[(size_t)RW * max(min(k, n - 1), 0) + OI]).x; };
+  double2 v0[2 * R], v1[2 * R];
+  const bool two = n > CH;  // uniform
+  src.nbr(other(lt), v0);
+  if (two) src.nbr(other(CH + lt), v1);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (c == 1 && !two) break;
+    const int k = c * CH + lt;
+    double2 q[RC::Q];
+    {
+      const double2* p2 = reinterpret_cast<const double2*>(recs + (size_t)RW * max(min(k, n - 1), 0));
+#pragma unroll
+      for (int i = 0; i < RC::Q; ++i) q[i] = p2[i];
+    }
+    Edge E;
+    RC::edge(q, E);
+    const int2 in = RC::inc(q);
+    const int o = in.x;
+    const bool tail = (in.y >> 31) & 1;
+    const double2* vr = c == 0 ? v0 : v1;
+    if (tid < CH && k < n) {
+      const double wk = (o >= 0) ? E.wk : 0.0, wt = (o >= 0) ? E.wt : 0.0;
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        const double x0 = vr[2 * a].x, x1 = vr[2 * a].y, x2 = vr[2 * a + 1].x, x3 = vr[2 * a + 1].y;
+        double h[4];
+        if (tail) {
+#pragma unroll
+          for (int cc = 0; cc < 3; ++cc)
+            h[cc] = -(wk * (x0 * E.R[cc * 3 + 0] + x1 * E.R[cc * 3 + 1] + x2 * E.R[cc * 3 + 2]) + wt * x3 * E.t[cc]);
+          h[3] = -(wt * x3);
+        } else {
+#pragma unroll
+          for (int cc = 0; cc < 3; ++cc)
+            h[cc] = -(wk * (x0 * E.R[0 * 3 + cc] + x1 * E.R[1 * 3 + cc] + x2 * E.R[2 * 3 + cc]));
+          h[3] = -(wt * (x3 + (x0 * E.t[0] + x1 * E.t[1] + x2 * E.t[2])));
+        }
+        store4(Cs + (tid * R + a) * 4, h);
+      }
+    }
+    lds_barrier();
+    if (L.valid) {
+      const int c0 = c * CH;
+      const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
+#pragma unroll 4
+      for (int j = j0; j < j1; ++j) {
+        double h[4];
+        load4(Cs + (j * R + L.a) * 4, h);
+        acc[0] += h[0]; acc[1] += h[1]; acc[2] += h[2]; acc[3] += h[3];
+      }
+    }
+    lds_barrier();
+  }
+  return true;
+}
+
 template <int R, int RW, int W>
 __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned* fail, int census, char* smem) {
   using SM = SmemRes<R, W>;
@@ -2397,7 +2496,9 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
   double* Pl = reinterpret_cast<double*>(smem + SM::p_off);
   double* Sl = reinterpret_cast<double*>(smem + SM::s_off);
   double* gx = reinterpret_cast<double*>(smem + SM::g_off) + 4 * (pl * R + L.a);  // this lane's row of g / Xt
-  double* red = reinterpret_cast<double*>(smem + SM::red_off);
+  double* recs = reinterpret_cast<double*>(smem + SM::template rec_off<RW>);
+  int* sptr = reinterpret_cast<int*>(smem + SM::template sp_off<RW>);
+  double* red = reinterpret_cast<double*>(smem + SM::template red_off<RW>);
   double* rl = red;  // robot sums' scratch (8 x WAVES), used after the tile partials are out
   double* scr = reinterpret_cast<double*>(smem);  // group-op scratch (the chunk area, between gathers)
   const __amdgpu_buffer_rsrc_t rz = wt_rsrc(d.z, d.vec), rw0 = wt_rsrc(d.w0, d.vec), rw1 = wt_rsrc(d.w1, d.vec),
@@ -2418,6 +2519,14 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     double* dst = (i & 1 ? Pl : Dl) + 16 * p;
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[k] = M[k];
+  }
+  // the tile's records and CSR offsets, for every tCG step's gather (the host
+  // keeps a resident tile within two chunks)
+  {
+    const double2* src2 = reinterpret_cast<const double2*>(d.rec + (size_t)RW * L.k0);
+    double2* dst2 = reinterpret_cast<double2*>(recs);
+    for (int i = threadIdx.x; i < L.n * (RW / 2); i += blockDim.x) dst2[i] = src2[i];
+    if (threadIdx.x <= L.np) sptr[threadIdx.x] = d.inc_ptr[L.p0 + threadIdx.x] - L.k0;
   }
   const int ph0 = cs.phase;  // (read before any barrier of this launch: every thread sees k_begin's value)
   KMX_RS(1);
@@ -2458,65 +2567,83 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
   }
   KMX_RS(2);
   // -------- tCG, one barrier per step (body_step's arithmetic) --------
-  double hzn[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0}, wn[4] = {0, 0, 0, 0},
-         et[4] = {0, 0, 0, 0};
+  constexpr bool LV = SM::template lv<RW>;
+  double* hzl = reinterpret_cast<double*>(smem + SM::template hz_off<RW>) + 4 * (pl * R + L.a);
+  double* etl = reinterpret_cast<double*>(smem + SM::template et_off<RW>) + 4 * (pl * R + L.a);
+  double hzr[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0}, wn[4] = {0, 0, 0, 0},
+         etr[4] = {0, 0, 0, 0};
+  if constexpr (LV) {  // eta starts at 0
+    if (L.valid) store4(etl, etr);
+  }
   bool formed = grad;   // this workgroup's robot formed the step the next barrier's consumers need
   bool trial = false;   // its tCG ended this round: the trial point is in LDS (gx) and published
   int k = -1;           // the step whose partials the next decision consumes
+  // Every thread takes the step's decision from the robot sums and the
+  // state's copy (as k_step's workgroups do); thread 0 applies the same
+  // control steps to the copy (control_core: counters, coefh, team status
+  // through the robot's first tile) between its arrival at the next barrier
+  // and its poll, off the critical path.
+  int pend = 0;         // thread 0: 1 a gradient, 2 a tCG step's control update waits for the next barrier
+  double pq[4] = {0.0, 0.0, 0.0, 0.0};
+  auto apply_pending = [&]() {
+    if (pend == 1) {
+      double t4[NPART] = {pq[0], pq[1], pq[2], 0.0};
+      control_core(cs, d, L.l, RED_GRAD, t4, R, writer);
+    } else if (pend == 2) {
+      cs.z_r = pq[1];
+      double th[NPART] = {pq[0], 0.0, 0.0, 0.0};
+      control_core(cs, d, L.l, RED_HESS, th, R, writer);
+      double tu[NPART] = {pq[2], pq[3], 0.0, 0.0};
+      control_core(cs, d, L.l, RED_UPDATE, tu, R, writer);
+    }
+    pend = 0;
+  };
   for (int jl = 0;; ++jl) {
     bool go = false;
     double coef = 0.0, al = 0.0, be = 0.0;
     auto decide = [&]() -> bool {
       KMX_RS(4 + 5 * jl);
-      if (!grid_sync(gb, b++, formed, &any, fail, &sflag)) return false;
+      if (!grid_sync(gb, b++, formed, &any, fail, &sflag, apply_pending)) return false;
       KMX_RS(5 + 5 * jl);
       if (!any) return false;
       if (!formed) return false;  // not in tCG (skipped, idle, or stopped earlier)
-      double tot[8];
       if (jl == 0) {
         RobotSum<3, 2, true> rg;
         rg.issue(d.part, NPART, L.rt0, L.rt1);
         double t4[NPART];
         rg.finish(d.part, NPART, rl, t4);
+        go = !(sqrt(t4[1]) < d.p.gn_tol);  // control_core's RED_GRAD test (RTR: the tCG starts)
         if (threadIdx.x == 0) {
-          control_core(cs, d, L.l, RED_GRAD, t4, R, writer);
-          rst.go = cs.phase == PH_TCG;
-          rst.coef = rst.al = rst.be = 0.0;
+          pend = 1;
+          pq[0] = t4[0]; pq[1] = t4[1]; pq[2] = t4[2];
         }
       } else {
+        double tot[8];
         RobotSum8<2, true> rf;  // (<= 512 tiles per robot: RobotSum8<4>'s order in one pass)
         const double* pf_in = d.part_f + (size_t)((k & 1) * d.ntiles) * 8;
         rf.issue(pf_in, L.rt0, L.rt1);
         rf.finish(pf_in, rl, tot);
+        const double zr = tot[1];
+        const HessStep hx = hess_step(zr, cs.e_Pe, cs.e_Pd, cs.d_Pd, cs.Delta, tot[0]);
+        double rrn, zrn;
+        onesync_scalars(hx.alpha, tot, &rrn, &zrn);
+        const UpdStep u = upd_step(hx.boundary ? MODE_BOUNDARY : MODE_INTERIOR, cs.r_stop, cs.lin_stop, zr, k + 1,
+                                   rrn, zrn, d.p);
+        coef = hx.coef;
+        al = hx.alpha;
+        be = u.beta;
+        go = !u.done;
         if (threadIdx.x == 0) {
-          const double zr = tot[1];
-          const HessStep hx = hess_step(zr, cs.e_Pe, cs.e_Pd, cs.d_Pd, cs.Delta, tot[0]);
-          double rrn, zrn;
-          onesync_scalars(hx.alpha, tot, &rrn, &zrn);
-          const UpdStep u = upd_step(hx.boundary ? MODE_BOUNDARY : MODE_INTERIOR, cs.r_stop, cs.lin_stop, zr, k + 1,
-                                     rrn, zrn, d.p);
-          rst.coef = hx.coef;
-          rst.al = hx.alpha;
-          rst.be = u.beta;
-          rst.go = !u.done;
-          cs.z_r = zr;
-          double th[NPART] = {tot[0], 0.0, 0.0, 0.0};
-          control_core(cs, d, L.l, RED_HESS, th, R, writer);
-          double tu[NPART] = {rrn, zrn, 0.0, 0.0};
-          control_core(cs, d, L.l, RED_UPDATE, tu, R, writer);
+          pend = 2;
+          pq[0] = tot[0]; pq[1] = zr; pq[2] = rrn; pq[3] = zrn;
         }
       }
-      __syncthreads();
-      go = rst.go != 0;
-      coef = rst.coef;
-      al = rst.al;
-      be = rst.be;
       KMX_RS(6 + 5 * jl);
       return go;
     };
     double H[4];
     WtRows<R> src{jl == 0 ? rz : ((k & 1) ? rw1 : rw0)};
-    hinc_gather_src<R, RW, false, WtRows<R>, decltype(decide)&, false, W>(d, L, src, H, smem, decide);
+    res_gather<R, RW, W>(L, recs, sptr, src, H, reinterpret_cast<double*>(smem), decide);
     if (sflag == 0) return;  // a barrier gave up (the fail word is set)
     KMX_RS(7 + 5 * jl);
     if (!any) break;
@@ -2525,6 +2652,10 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
       // (this decision's coefficient), the trial point and the model partials
 #pragma unroll
       for (int c = 0; c < 4; ++c) rn[c] = fma(coef, hdl[c], rn[c]);
+      double et[4] = {etr[0], etr[1], etr[2], etr[3]};
+      if constexpr (LV) {
+        if (L.valid) load4(etl, et);
+      }
 #pragma unroll
       for (int c = 0; c < 4; ++c) et[c] += coef * dl[c];
       double xt[4];
@@ -2574,12 +2705,22 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     if (jl == 0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        hzn[c] = hv[c];
+        hzr[c] = hv[c];
         dl[c] = -v[c];
         hdl[c] = -hv[c];
       }
+      if constexpr (LV) {
+        if (L.valid) store4(hzl, hzr);
+      }
     } else {
       // eta += coef_k delta_k (the serial order of the folds), then the step's recurrences
+      double et[4] = {etr[0], etr[1], etr[2], etr[3]}, hzn[4] = {hzr[0], hzr[1], hzr[2], hzr[3]};
+      if constexpr (LV) {
+        if (L.valid) {
+          load4(etl, et);
+          load4(hzl, hzn);
+        }
+      }
 #pragma unroll
       for (int c = 0; c < 4; ++c) et[c] += coef * dl[c];
 #pragma unroll
@@ -2590,6 +2731,18 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
         hzn[c] = fma(al, hv[c], hzn[c]);
         dl[c] = fma(be, dold, -zn[c]);
         hdl[c] = fma(be, hold, -hzn[c]);
+      }
+      if constexpr (LV) {
+        if (L.valid) {
+          store4(etl, et);
+          store4(hzl, hzn);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          etr[c] = et[c];
+          hzr[c] = hzn[c];
+        }
       }
     }
     double Pm[16];
@@ -2705,7 +2858,7 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
 // runs two tiles (a CU with two took ~10 us more per tCG step than one with
 // one: the barrier waits for it; profiles/r05/resident/)
 template <int R, int RW, int W>
-__global__ __launch_bounds__(64 * W, 2) void k_round(Dev d, unsigned* gb, unsigned* fail, int census) {
+__global__ __launch_bounds__(64 * W, W > 4 ? 2 : 1) void k_round(Dev d, unsigned* gb, unsigned* fail, int census) {
   KMX_SMEM;
   body_round<R, RW, W>(d, gb, fail, census, smem);
 }
@@ -3261,6 +3414,7 @@ struct kmx_pgo {
   // tile fits resident (decided at set_graph: occupancy query + census launch)
   bool res_on = false;
   int res_w = 4;               // waves per workgroup of the resident round (the tile cut's)
+  int max_tile_inc = 0;        // incidences of the largest tile
   int res_cap = 0;             // workgroups of k_round resident on the device
   std::string res_reason = "tcg_form is not KMX_TCG_FORM_RESIDENT";
   unsigned* d_gbar = nullptr;  // grid-barrier words (GB_WORDS)
@@ -3628,7 +3782,7 @@ void enqueue_trial_t(kmx_pgo* h, bool rgd) {
 // preconditioner rebuild is left to k_round), then the whole block update.
 template <int R, int RW, int W>
 void launch_round(kmx_pgo* h, int census) {
-  hipLaunchKernelGGL((k_round<R, RW, W>), dim3(h->ntiles), dim3(64 * W), (SmemRes<R, W>::bytes), h->stream, h->dv,
+  hipLaunchKernelGGL((k_round<R, RW, W>), dim3(h->ntiles), dim3(64 * W), (SmemRes<R, W>::template bytes<RW>), h->stream, h->dv,
                      h->d_gbar, h->h_fail, census);
 }
 template <int R, int RW>
@@ -3655,6 +3809,11 @@ int resident_setup_t(kmx_pgo* h) {
   h->res_on = false;
   if (h->P.method != KMX_METHOD_RTR) { h->res_reason = "RGD method"; return 0; }
   if (h->P.rtr_iterations != 1) { h->res_reason = "rtr_iterations != 1"; return 0; }
+  if (h->max_tile_inc > 2 * h->res_w * (64 / R) * R) {
+    h->res_reason = "a tile holds more than two gather chunks (tile_incidences " +
+                    std::to_string(h->P.tile_incidences) + ")";
+    return 0;
+  }
   for (size_t l = 0; l + 1 < h->rt0_h.size(); ++l)
     if (h->rt0_h[l + 1] - h->rt0_h[l] > 2 * RBLOCK) {
       h->res_reason = "a robot has more than 512 tiles";
@@ -3663,19 +3822,19 @@ int resident_setup_t(kmx_pgo* h) {
   int nb = 0, cus = 0;
   if constexpr (R == 5) {
     if (h->res_w == 5) {
-      if (SmemRes<R, 5>::bytes > 65536)
+      if (SmemRes<R, 5>::template bytes<RW> > 65536)
         KMX_HIP(hipFuncSetAttribute((const void*)k_round<R, RW, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    SmemRes<R, 5>::bytes));
+                                    SmemRes<R, 5>::template bytes<RW>));
       KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_round<R, RW, 5>, 64 * 5,
-                                                           SmemRes<R, 5>::bytes));
+                                                           SmemRes<R, 5>::template bytes<RW>));
     }
   }
   if (h->res_w != 5) {
-    if (SmemRes<R, 4>::bytes > 65536)
+    if (SmemRes<R, 4>::template bytes<RW> > 65536)
       KMX_HIP(hipFuncSetAttribute((const void*)k_round<R, RW, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  SmemRes<R, 4>::bytes));
+                                  SmemRes<R, 4>::template bytes<RW>));
     KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_round<R, RW, 4>, 64 * 4,
-                                                         SmemRes<R, 4>::bytes));
+                                                         SmemRes<R, 4>::template bytes<RW>));
   }
   KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
   h->res_cap = nb * cus;
@@ -4126,6 +4285,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     }
   };
   h->res_w = WAVES;
+  h->max_tile_inc = 0;
   {
     const int TP = WAVES * (64 / r);
     int64_t tilecap = std::min<int64_t>(2 * (int64_t)TP * r,
@@ -4169,6 +4329,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     td.k0 = inc_ptr[tp0[t]];
     const int ninc = inc_ptr[tp0[t] + tnp[t]] - td.k0;
     KMX_CHECK(tnp[t] < 256 && ninc < (1 << 23), KMX_EINVAL, "tile too large");
+    h->max_tile_inc = std::max(h->max_tile_inc, ninc);
     td.np_n = tnp[t] | (ninc << 8);
     td.rt0 = rt0[tr[t]];
     td.rt1 = rt0[tr[t] + 1];
