@@ -47,6 +47,10 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "kimera-multi_amd"))
 
 PEAK_HBM = 8.0e12      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# tCG form "auto": the resident round (one persistent launch per round) for
+# shards up to this many poses per GPU, ROPTLIB's launched tCG above (the
+# resident round needs one 60-pose tile per CU at r = 5: 256 x 60 = 15,360)
+RESIDENT_MAX_POSES = 15_000
 PEAK_VALU_OPS = 78.6e12  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
 
 
@@ -68,8 +72,10 @@ def parse():
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3: timed rounds only")
     ap.add_argument("--tile-incidences", type=int, default=0,
                     help="incidences per workgroup tile (kmx_pgo_params.tile_incidences; 0: automatic)")
-    ap.add_argument("--tcg-form", choices=["standard", "onesync"], default="standard",
-                    help="tCG form (kmx_pgo_params.tcg_form): ROPTLIB's, or the opt-in one-sync form")
+    ap.add_argument("--tcg-form", choices=["auto", "standard", "onesync", "resident"], default="auto",
+                    help="tCG form (kmx_pgo_params.tcg_form): ROPTLIB's, the one-sync form launched per step, or "
+                         "the one-sync form as one persistent launch per round; auto = resident for shards of "
+                         f"<= {RESIDENT_MAX_POSES} poses per GPU (the strong-scaling ranks), else standard")
     ap.add_argument("--lcd-frames", type=int, default=50_000)
     ap.add_argument("--lcd-steps", type=int, default=8,
                     help="back-to-back LCD verification calls timed (a call's kNN2 overlaps the previous call's "
@@ -656,6 +662,7 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
         hv_ms, hv_bytes, hv_n = r["hessvec_ms_total"], r["hessvec_alg_bytes"], r["hessvec_launches"]
         same = all(r[k] == c[k] for k in ("edges_iters", "hessvecs", "block_updates", "gnc_updates"))
     xs, xr = drv.exchange_rows
+    res_info = drv.solver.resident_info() if P.localOptimizationParams.tCG_form == "resident" else None
     native = bool(drv.native)
     mode = drv.exchange_mode
     mem = drv.solver.memory()[0]
@@ -672,7 +679,7 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
             "el": tot[0], "edges_iters": tot[1], "hessvecs": tot[2], "block_updates": tot[3],
             "gnc_updates": int(tot[4]), "hv": (tot[5], tot[6], int(tot[7])), "xrows": (int(tot[8]), int(tot[9])),
             "mem_max": int(tot[10]), "replay_identical": (tot[11] == world) if replay and snap is not None else None,
-            "snap": snap, "native": native, "exchange": mode, "drv": drv}
+            "snap": snap, "native": native, "exchange": mode, "drv": drv, "resident": res_info}
 
 
 def main():
@@ -702,12 +709,14 @@ def main():
             torch.cuda.synchronize()
 
     P = params()
-    P.localOptimizationParams.tCG_form = args.tcg_form
     P.tileIncidences = args.tile_incidences
     headline = args.scaling if world > 1 else "strong"
     t_gen = time.perf_counter()
     g, X0 = make_workload(args.config, world, headline)
     gen_s = time.perf_counter() - t_gen
+    if args.tcg_form == "auto":
+        args.tcg_form = "resident" if g.n_total / world <= RESIDENT_MAX_POSES else "standard"
+    P.localOptimizationParams.tCG_form = args.tcg_form
     want_cpu = rank == 0 and world == 1 and not args.no_cpu and not args.profile
     leg = dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, args.steps, barrier,
                    replay=not args.no_replay and not args.profile, want_snapshot=want_cpu)
@@ -760,6 +769,7 @@ def main():
                               if world > 1 else ""),
             "exchange_rows_per_round": {"sent_max": leg["xrows"][0], "recv_max": leg["xrows"][1],
                                         "recv_bytes_max": leg["xrows"][1] * ps_bytes},
+            "resident_round": leg["resident"],
             "graph_gen_s": round(gen_s, 1),
             "device_bytes_per_gpu": leg["mem_max"],
         },

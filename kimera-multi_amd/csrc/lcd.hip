@@ -1971,131 +1971,19 @@ __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* sta
   KMX_PT(8);
 }
 
-// One candidate's 2D-2D RANSAC and 3D-3D recovery by the calling wave; F1 is
-// the wave's global scratch (6 N + STASH doubles).
-template <bool STEW, typename SB>
-__device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, double* F1, const double* bearings,
-                                                 const double* points, int N, const int* cq, const int* cm,
-                                                 const int2* pairs, const int* Kin, const short* table,
-                                                 const RsParams& P, kmx_lcd_result* res, unsigned char* masks) {
-  const int lane = fresh_lane(threadIdx.x);
-  const WaveStamp stamp(c, P.prof == 2);
-  const int K = Kin[c];
-  const int q = cq[c], m = cm[c];
-  unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
-  kmx_lcd_result* R_ = res + c;
-  for (int j = lane; j < N && mask; j += RS_BLOCK) mask[j] = 0;
+// The candidate's result after its RANSAC loop (shared by the work-queue
+// kernel and the spread form's k_rs_finish): the best model's inliers (and
+// mask), then the 1-point 3D-3D recovery (and refine_pose), or the hand-over
+// to k_recover. w.bestm holds the best model when `have`.
+__device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double* F2, const double* points, int N,
+                                            int q, int m, const int2* pl, int K, const RsParams& P,
+                                            kmx_lcd_result* R_, unsigned char* mask, int have, int iterations,
+                                            int lane) {
   const bool st2d = (P.stages & KMX_LCD_STAGE_2D2D) != 0;
-  if (K < 5 && st2d) {
-    if (P.hyps && lane == 0) P.hyps[c] = 0;
-    if (lane == 0) {
-      kmx_lcd_result r = {};
-      r.n_matches = K;
-      *R_ = r;
-    }
-    return;
-  }
-  // compact bearings of the match pairs (global scratch, L1/L2 resident), one
-  // component per row of N (F1[k][j]): the scoring loops' loads are coalesced
-  double* stash = F1 + 6 * N;  // Stewenius: the batch's action matrices and null spaces
-  double* F2 = F1 + 3 * N;
-  const int2* pl = pairs + (size_t)c * N;
-  for (int j = lane; j < K; j += RS_BLOCK) {
-    const int2 pr = pl[j];
-    for (int k = 0; k < 3; ++k) {
-      F1[(size_t)k * N + j] = bearings[((size_t)q * N + pr.x) * 3 + k];
-      F2[(size_t)k * N + j] = bearings[((size_t)m * N + pr.y) * 3 + k];
-    }
-  }
-  // pair j's error under the model (R, t)
   auto pair_error = [&](const double* R, const double* t, int j) {
     const double a[3] = {F1[j], F1[N + j], F1[2 * N + j]}, b[3] = {F2[j], F2[N + j], F2[2 * N + j]};
     return model_error(R, t, a, b);
   };
-  for (int t = lane; t < 40; t += RS_BLOCK) (&w.t11[0][0][0])[t] = (&T11[0][0][0])[t];
-  for (int t = lane; t < 120; t += RS_BLOCK) (&w.t21[0][0][0])[t] = (&T21[0][0][0])[t];
-  __threadfence_block();
-  wsync();
-  int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
-  double kk = 1.0;
-  const int max_skip = P.max_iter * 10;
-  const short* tab = P.tab_fixed ? table : table + (size_t)(K - 5) * P.pmax * 5;
-  const bool prof = (c < 64) && P.prof == 1;
-  bool done = !st2d;  // without the 2D-2D stage every pair is an inlier of the caller's pose
-  // the serial loop's bookkeeping of one hypothesis's model (w.ok, w.mR, w.mt):
-  // a failed solve counts as skipped; otherwise its inliers, the best model and
-  // the adaptive iteration bound, and the iteration count
-  auto account = [&](bool ok, const double* mR, const double* mt) {
-    unsigned long long t_prev = prof ? wall_clock64() : 0;
-    if (!ok) {
-      ++skipped;
-      wsync();
-      return;
-    }
-    double Rm[9], tm[3];
-    for (int i = 0; i < 9; ++i) Rm[i] = mR[i];
-    for (int i = 0; i < 3; ++i) tm[i] = mt[i];
-    int cnt = 0;
-    for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
-      const int j = j0 + lane;
-      const bool in = (j < K) && pair_error(Rm, tm, j) < P.thr2d;
-      cnt += __popcll(__ballot(in));
-    }
-    KMX_PT(6);
-    if (cnt > best_cnt) {
-      best_cnt = cnt;
-      if (lane == 0) {
-        for (int i = 0; i < 9; ++i) w.bestm[i] = Rm[i];
-        for (int i = 0; i < 3; ++i) w.bestm[9 + i] = tm[i];
-      }
-      have = 1;
-      const double wr = (double)cnt / (double)K;
-      double p_no = 1.0 - pow(wr, 5.0);
-      p_no = fmax(DBL_EPSILON, p_no);
-      p_no = fmin(1.0 - DBL_EPSILON, p_no);
-      kk = log(1.0 - P.prob) / log(p_no);
-    }
-    ++iterations;
-    wsync();
-    if (iterations > P.max_iter) done = true;
-  };
-  if (!st2d) {
-  } else if constexpr (STEW) {
-    // SG hypotheses' eigenvalues at a time, then each hypothesis in order under
-    // the serial loop's tests (a batch may run past the stop: those are never
-    // scored, so the results are the one-at-a-time loop's)
-    int nb = SG;
-    for (int p0 = 0; p0 < P.pmax && !done; p0 += nb) {
-      if (!(iterations < kk && skipped < max_skip)) break;  // uniform
-      // once a model exists, the serial loop scores at most ceil(kk) -
-      // iterations more hypotheses (kk only falls), plus any that fail to give
-      // a model (a later batch takes those): a batch no longer computes the
-      // hypotheses past that bound (up to SG - 1 of them in a candidate's last
-      // batch)
-      int want = SG;
-      if (have) {
-        const double rem = ceil(kk) - (double)iterations;
-        want = rem < 1.0 ? 1 : (rem < (double)SG ? (int)rem : SG);
-      }
-      nb = min(want, P.pmax - p0);
-      stew_batch(w, sb, stash, lane, F1, F2, N, tab, p0, nb, prof);
-      stew_models(sb, stash, lane, F1, F2, tab, p0, nb, prof);
-      for (int b = 0; b < nb && !done; ++b) {
-        if (!(iterations < kk && skipped < max_skip)) {
-          done = true;
-          break;
-        }
-        account(sb.mok[b] != 0, sb.mR[b], sb.mt[b]);
-      }
-    }
-  } else {
-    for (int p = 0; p < P.pmax && !done; ++p) {
-      if (!(iterations < kk && skipped < max_skip)) break;  // uniform
-      coop_hypothesis(w, lane, F1, F2, N, tab + (size_t)p * 5, prof);
-      account(w.ok != 0, w.mR, w.mt);
-    }
-  }
-  if (P.hyps && lane == 0) P.hyps[c] = iterations + skipped;
   if (!have && st2d) {
     if (lane == 0) {
       kmx_lcd_result r = {};
@@ -2250,6 +2138,134 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
     *R_ = r;
   }
 }
+// One candidate's 2D-2D RANSAC and 3D-3D recovery by the calling wave; F1 is
+// the wave's global scratch (6 N + STASH doubles).
+template <bool STEW, typename SB>
+__device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, double* F1, const double* bearings,
+                                                 const double* points, int N, const int* cq, const int* cm,
+                                                 const int2* pairs, const int* Kin, const short* table,
+                                                 const RsParams& P, kmx_lcd_result* res, unsigned char* masks) {
+  const int lane = fresh_lane(threadIdx.x);
+  const WaveStamp stamp(c, P.prof == 2);
+  const int K = Kin[c];
+  const int q = cq[c], m = cm[c];
+  unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
+  kmx_lcd_result* R_ = res + c;
+  for (int j = lane; j < N && mask; j += RS_BLOCK) mask[j] = 0;
+  const bool st2d = (P.stages & KMX_LCD_STAGE_2D2D) != 0;
+  if (K < 5 && st2d) {
+    if (P.hyps && lane == 0) P.hyps[c] = 0;
+    if (lane == 0) {
+      kmx_lcd_result r = {};
+      r.n_matches = K;
+      *R_ = r;
+    }
+    return;
+  }
+  // compact bearings of the match pairs (global scratch, L1/L2 resident), one
+  // component per row of N (F1[k][j]): the scoring loops' loads are coalesced
+  double* stash = F1 + 6 * N;  // Stewenius: the batch's action matrices and null spaces
+  double* F2 = F1 + 3 * N;
+  const int2* pl = pairs + (size_t)c * N;
+  for (int j = lane; j < K; j += RS_BLOCK) {
+    const int2 pr = pl[j];
+    for (int k = 0; k < 3; ++k) {
+      F1[(size_t)k * N + j] = bearings[((size_t)q * N + pr.x) * 3 + k];
+      F2[(size_t)k * N + j] = bearings[((size_t)m * N + pr.y) * 3 + k];
+    }
+  }
+  // pair j's error under the model (R, t)
+  auto pair_error = [&](const double* R, const double* t, int j) {
+    const double a[3] = {F1[j], F1[N + j], F1[2 * N + j]}, b[3] = {F2[j], F2[N + j], F2[2 * N + j]};
+    return model_error(R, t, a, b);
+  };
+  for (int t = lane; t < 40; t += RS_BLOCK) (&w.t11[0][0][0])[t] = (&T11[0][0][0])[t];
+  for (int t = lane; t < 120; t += RS_BLOCK) (&w.t21[0][0][0])[t] = (&T21[0][0][0])[t];
+  __threadfence_block();
+  wsync();
+  int iterations = 0, skipped = 0, best_cnt = -INT_MAX, have = 0;
+  double kk = 1.0;
+  const int max_skip = P.max_iter * 10;
+  const short* tab = P.tab_fixed ? table : table + (size_t)(K - 5) * P.pmax * 5;
+  const bool prof = (c < 64) && P.prof == 1;
+  bool done = !st2d;  // without the 2D-2D stage every pair is an inlier of the caller's pose
+  // the serial loop's bookkeeping of one hypothesis's model (w.ok, w.mR, w.mt):
+  // a failed solve counts as skipped; otherwise its inliers, the best model and
+  // the adaptive iteration bound, and the iteration count
+  auto account = [&](bool ok, const double* mR, const double* mt) {
+    unsigned long long t_prev = prof ? wall_clock64() : 0;
+    if (!ok) {
+      ++skipped;
+      wsync();
+      return;
+    }
+    double Rm[9], tm[3];
+    for (int i = 0; i < 9; ++i) Rm[i] = mR[i];
+    for (int i = 0; i < 3; ++i) tm[i] = mt[i];
+    int cnt = 0;
+    for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {
+      const int j = j0 + lane;
+      const bool in = (j < K) && pair_error(Rm, tm, j) < P.thr2d;
+      cnt += __popcll(__ballot(in));
+    }
+    KMX_PT(6);
+    if (cnt > best_cnt) {
+      best_cnt = cnt;
+      if (lane == 0) {
+        for (int i = 0; i < 9; ++i) w.bestm[i] = Rm[i];
+        for (int i = 0; i < 3; ++i) w.bestm[9 + i] = tm[i];
+      }
+      have = 1;
+      const double wr = (double)cnt / (double)K;
+      double p_no = 1.0 - pow(wr, 5.0);
+      p_no = fmax(DBL_EPSILON, p_no);
+      p_no = fmin(1.0 - DBL_EPSILON, p_no);
+      kk = log(1.0 - P.prob) / log(p_no);
+    }
+    ++iterations;
+    wsync();
+    if (iterations > P.max_iter) done = true;
+  };
+  if (!st2d) {
+  } else if constexpr (STEW) {
+    // SG hypotheses' eigenvalues at a time, then each hypothesis in order under
+    // the serial loop's tests (a batch may run past the stop: those are never
+    // scored, so the results are the one-at-a-time loop's)
+    int nb = SG;
+    for (int p0 = 0; p0 < P.pmax && !done; p0 += nb) {
+      if (!(iterations < kk && skipped < max_skip)) break;  // uniform
+      // once a model exists, the serial loop scores at most ceil(kk) -
+      // iterations more hypotheses (kk only falls), plus any that fail to give
+      // a model (a later batch takes those): a batch no longer computes the
+      // hypotheses past that bound (up to SG - 1 of them in a candidate's last
+      // batch)
+      int want = SG;
+      if (have) {
+        const double rem = ceil(kk) - (double)iterations;
+        want = rem < 1.0 ? 1 : (rem < (double)SG ? (int)rem : SG);
+      }
+      nb = min(want, P.pmax - p0);
+      stew_batch(w, sb, stash, lane, F1, F2, N, tab, p0, nb, prof);
+      stew_models(sb, stash, lane, F1, F2, tab, p0, nb, prof);
+      for (int b = 0; b < nb && !done; ++b) {
+        if (!(iterations < kk && skipped < max_skip)) {
+          done = true;
+          break;
+        }
+        account(sb.mok[b] != 0, sb.mR[b], sb.mt[b]);
+      }
+    }
+  } else {
+    for (int p = 0; p < P.pmax && !done; ++p) {
+      if (!(iterations < kk && skipped < max_skip)) break;  // uniform
+      coop_hypothesis(w, lane, F1, F2, N, tab + (size_t)p * 5, prof);
+      account(w.ok != 0, w.mR, w.mt);
+    }
+  }
+  if (P.hyps && lane == 0) P.hyps[c] = iterations + skipped;
+  ransac_tail(c, w, F1, F2, points, N, q, m, pl, K, P, R_, mask, have, iterations, lane);
+}
+
 
 
 // k_ransac_coop: a work queue over the candidates. The launch holds as many
@@ -2280,6 +2296,210 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
     __threadfence_block();
     wsync();
   }
+}
+
+// ------------------------------------------------- spread form (small calls) --
+// A call of a few candidates (the reference's verification thread checks ONE
+// candidate per call: verifyLoopSpin -> geometricVerificationNister,
+// drawio:2638-2657) would leave one wave working through up to max_iter
+// hypotheses while the rest of the device idles (a look-alike candidate that
+// fails geometry runs all 500 iterations: ~20 ms on one wave against ~10 ms
+// for one CPU thread). The hypotheses of one candidate do not depend on each
+// other — each pass p takes its sample from the sampler table row and gives a
+// model (or none) and that model's inlier count — only the serial loop's
+// control does (the iteration bound kk from the best count so far, the skip
+// count, the stop). So the spread form
+//   1. computes a range of hypotheses of every candidate on many waves at once
+//      (k_rs_hyps: SG per wave for Stewenius, as one batch of the work-queue
+//      kernel; per hypothesis the same operations, so the same bits), scoring
+//      each model over the candidate's pairs;
+//   2. replays the serial loop's control over them in order (k_rs_replay: the
+//      `account` arithmetic of ransac_candidate, one thread per candidate),
+//      stopping where the serial loop stops;
+//   3. computes the next range only for candidates whose replay ran past the
+//      computed ones (ranges grow: 66, then 444, then 1500 ... passes);
+//   4. finishes each candidate from the replayed state (k_rs_finish: the best
+//      model's inliers and the 3D-3D recovery, ransac_tail).
+// Results are the serial loop's bit for bit (tests/test_lcd_spread_gpu.py);
+// hypotheses past a candidate's stop inside a range are computed and never
+// counted. Used by the synchronous calls for n <= spread_max candidates
+// (KMX_LCD_SPREAD, default 8; 0 turns it off).
+struct HypOut {
+  double m[12];  // R (row-major), t
+  int ok, cnt;   // a model was found; its inliers among the candidate's pairs
+};
+struct RsState {  // the serial loop's control between passes
+  double kk;
+  double best[12];
+  int iterations, skipped, best_cnt, have, done, p_next;
+};
+constexpr int SPREAD_PER_NISTER = 2;  // Nister hypotheses per wave (one at a time)
+
+__global__ void k_rs_init(RsState* st, int n, int stages) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  RsState s;
+  s.kk = 1.0;
+  for (int i = 0; i < 12; ++i) s.best[i] = 0.0;
+  s.iterations = s.skipped = s.have = s.p_next = 0;
+  s.best_cnt = -INT_MAX;
+  s.done = (stages & KMX_LCD_STAGE_2D2D) ? 0 : 1;
+  st[c] = s;
+}
+
+// The candidate's compact bearings (ransac_candidate's layout) and the LDS
+// constant tables, by the calling wave.
+__device__ __forceinline__ void rs_compact(CoopWS& w, double* F1, const double* bearings, int N, int q, int m,
+                                           const int2* pl, int K, int lane) {
+  double* F2 = F1 + 3 * N;
+  for (int j = lane; j < K; j += RS_BLOCK) {
+    const int2 pr = pl[j];
+    for (int k = 0; k < 3; ++k) {
+      F1[(size_t)k * N + j] = bearings[((size_t)q * N + pr.x) * 3 + k];
+      F2[(size_t)k * N + j] = bearings[((size_t)m * N + pr.y) * 3 + k];
+    }
+  }
+  for (int t = lane; t < 40; t += RS_BLOCK) (&w.t11[0][0][0])[t] = (&T11[0][0][0])[t];
+  for (int t = lane; t < 120; t += RS_BLOCK) (&w.t21[0][0][0])[t] = (&T21[0][0][0])[t];
+  __threadfence_block();
+  wsync();
+}
+
+// Hypotheses [pa, pb) of every candidate still running: wave b works on
+// candidate b / G, hypotheses pa + (b % G) * per ... (+ per).
+template <bool STEW>
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, int N, const int* cq, const int* cm,
+                                                      const int2* pairs, const int* Kin, const short* table,
+                                                      RsParams P, const RsState* st, HypOut* hout, int pa, int pb,
+                                                      int G, double* fbuf) {
+  __shared__ CoopWS w;
+  __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;
+  const int c = blockIdx.x / G, g = blockIdx.x % G;
+  const int lane = fresh_lane(threadIdx.x);
+  const int K = Kin[c];
+  if (K < 5 || st[c].done) return;
+  constexpr int per = STEW ? SG : SPREAD_PER_NISTER;
+  const int p_lo = pa + g * per, p_hi = min(min(p_lo + per, pb), P.pmax);
+  if (p_lo >= p_hi) return;
+  double* F1 = fbuf + (size_t)blockIdx.x * (6 * N + STASH);
+  double* F2 = F1 + 3 * N;
+  double* stash = F1 + 6 * N;
+  rs_compact(w, F1, bearings, N, cq[c], cm[c], pairs + (size_t)c * N, K, lane);
+  const short* tab = table + (size_t)(K - 5) * P.pmax * 5;
+  HypOut* ho = hout + (size_t)c * P.pmax;
+  auto emit = [&](int p, bool ok, const double* mR, const double* mt) {
+    int cnt = 0;
+    if (ok) {
+      double Rm[9], tm[3];
+      for (int i = 0; i < 9; ++i) Rm[i] = mR[i];
+      for (int i = 0; i < 3; ++i) tm[i] = mt[i];
+      for (int j0 = 0; j0 < K; j0 += RS_BLOCK) {  // account()'s count, the same expression
+        const int j = j0 + lane;
+        bool in = false;
+        if (j < K) {
+          const double a[3] = {F1[j], F1[N + j], F1[2 * N + j]}, b[3] = {F2[j], F2[N + j], F2[2 * N + j]};
+          in = model_error(Rm, tm, a, b) < P.thr2d;
+        }
+        cnt += __popcll(__ballot(in));
+      }
+      if (lane < 12) ho[p].m[lane] = lane < 9 ? Rm[lane] : tm[lane - 9];
+    }
+    if (lane == 0) {
+      ho[p].ok = ok ? 1 : 0;
+      ho[p].cnt = cnt;
+    }
+    wsync();
+  };
+  if constexpr (STEW) {
+    const int nb = p_hi - p_lo;
+    stew_batch(w, sb, stash, lane, F1, F2, N, tab, p_lo, nb, false);
+    stew_models(sb, stash, lane, F1, F2, tab, p_lo, nb, false);
+    for (int b = 0; b < nb; ++b) emit(p_lo + b, sb.mok[b] != 0, sb.mR[b], sb.mt[b]);
+  } else {
+    for (int p = p_lo; p < p_hi; ++p) {
+      coop_hypothesis(w, lane, F1, F2, N, tab + (size_t)p * 5, false);
+      emit(p, w.ok != 0, w.mR, w.mt);
+    }
+  }
+}
+
+// The serial loop's control (ransac_candidate: the stop test, then account)
+// over the computed hypotheses [p_next, pb), one thread per candidate.
+__global__ void k_rs_replay(const int* Kin, RsParams P, RsState* st, const HypOut* hout, int pb, int n,
+                            unsigned* more) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  RsState s = st[c];
+  if (s.done) return;
+  const int K = Kin[c];
+  if (K < 5) {
+    s.done = 1;
+    st[c] = s;
+    return;
+  }
+  const int max_skip = P.max_iter * 10;
+  const HypOut* ho = hout + (size_t)c * P.pmax;
+  for (;;) {
+    if (s.p_next >= P.pmax || !(s.iterations < s.kk && s.skipped < max_skip)) {
+      s.done = 1;
+      break;
+    }
+    if (s.p_next >= pb) break;  // past the computed hypotheses: the next pass
+    const HypOut& h = ho[s.p_next++];
+    if (!h.ok) {
+      ++s.skipped;
+      continue;
+    }
+    if (h.cnt > s.best_cnt) {
+      s.best_cnt = h.cnt;
+      for (int i = 0; i < 12; ++i) s.best[i] = h.m[i];
+      s.have = 1;
+      const double wr = (double)h.cnt / (double)K;
+      double p_no = 1.0 - pow(wr, 5.0);
+      p_no = fmax(DBL_EPSILON, p_no);
+      p_no = fmin(1.0 - DBL_EPSILON, p_no);
+      s.kk = log(1.0 - P.prob) / log(p_no);
+    }
+    ++s.iterations;
+    if (s.iterations > P.max_iter) {
+      s.done = 1;
+      break;
+    }
+  }
+  st[c] = s;
+  if (!s.done) atomicOr(more, 1u);
+}
+
+// Each candidate's result from its replayed loop (one wave per candidate).
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_finish(const double* bearings, const double* points, int N,
+                                                        const int* cq, const int* cm, const int2* pairs,
+                                                        const int* Kin, RsParams P, const RsState* st,
+                                                        kmx_lcd_result* res, unsigned char* masks, double* fbuf) {
+  __shared__ CoopWS w;
+  const int c = blockIdx.x;
+  const int lane = fresh_lane(threadIdx.x);
+  const int K = Kin[c];
+  const int q = cq[c], m = cm[c];
+  unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
+  kmx_lcd_result* R_ = res + c;
+  for (int j = lane; j < N && mask; j += RS_BLOCK) mask[j] = 0;
+  const bool st2d = (P.stages & KMX_LCD_STAGE_2D2D) != 0;
+  if (K < 5 && st2d) {
+    if (lane == 0) {
+      kmx_lcd_result r = {};
+      r.n_matches = K;
+      *R_ = r;
+    }
+    return;
+  }
+  double* F1 = fbuf + (size_t)blockIdx.x * (6 * N + STASH);
+  const int2* pl = pairs + (size_t)c * N;
+  rs_compact(w, F1, bearings, N, q, m, pl, K, lane);
+  const RsState s = st[c];
+  if (lane < 12) w.bestm[lane] = s.best[lane];
+  __threadfence_block();
+  wsync();
+  ransac_tail(c, w, F1, F1 + 3 * N, points, N, q, m, pl, K, P, R_, mask, s.have, s.iterations, lane);
 }
 
 // Arun 3-point model (oracle arun_model): centroids, H = sum dm dq^T, Kabsch
@@ -2550,6 +2770,13 @@ struct kmx_lcd {
   short* d_row = nullptr;
   int *d_hyps = nullptr, *d_nrec = nullptr;
   int* d_order = nullptr;  // k_order's queue order (KMX_LCD_ORDER)
+  // spread form (synchronous calls of <= spread_max candidates; lcd.hip k_rs_*)
+  int spread_max = 8;
+  int spread_cap = 0;
+  RsState* d_st = nullptr;
+  HypOut* d_hout = nullptr;
+  double* d_sfbuf = nullptr;
+  unsigned* d_more = nullptr;
   int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
   // kmx_lcd_enable_timing: events around the kNN2 and the RANSAC launches
   bool timing = false;
@@ -2597,6 +2824,11 @@ void lcd_free_cand(kmx_lcd* h) {
   h->d_order = nullptr;
   for (bool& e : h->ev_rs_set) e = false;
   h->cap = 0;
+  void* q[] = {h->d_st, h->d_hout, h->d_sfbuf, h->d_more};
+  for (void* x : q)
+    if (x) (void)hipFree(x);
+  h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_more = nullptr;
+  h->spread_cap = 0;
 }
 // The next call's slot: its buffers become d_cq .. d_order.
 void use_next_slot(kmx_lcd* h) {
@@ -2903,9 +3135,67 @@ int verify_ordered(kmx_lcd* h, int n, int stages, bool masks) {
   return 0;
 }
 
+// The spread form (see k_rs_hyps): hypothesis ranges of growing size on many
+// waves, the serial control replayed after each, until every candidate's loop
+// has stopped; then the candidates' results. Synchronous (the host reads
+// whether a candidate needs another range).
+constexpr int SPREAD_WAVES = 1024;  // waves of one k_rs_hyps launch at most
+int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks) {
+  const RsParams rp = rs_params(h, stages);
+  const bool masks = want_masks || rp.pnp;
+  hipStream_t st = rs_stream(h);
+  if (n > h->spread_cap) {
+    void* q[] = {h->d_st, h->d_hout, h->d_sfbuf, h->d_more};
+    KMX_HIP(hipStreamSynchronize(st));
+    for (void* x : q)
+      if (x) (void)hipFree(x);
+    h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_more = nullptr;
+    h->spread_cap = 0;
+    const int cap = std::max(n, h->spread_max);
+    KMX_HIP(hipMalloc(&h->d_st, sizeof(RsState) * cap));
+    KMX_HIP(hipMalloc(&h->d_hout, sizeof(HypOut) * (size_t)cap * h->pmax));
+    KMX_HIP(hipMalloc(&h->d_sfbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::max(SPREAD_WAVES, cap)));
+    KMX_HIP(hipMalloc(&h->d_more, sizeof(unsigned)));
+    h->spread_cap = cap;
+  }
+  const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
+  const int per = stew ? SG : SPREAD_PER_NISTER;
+  hipLaunchKernelGGL(k_rs_init, dim3((n + 63) / 64), dim3(64), 0, st, h->d_st, n, stages);
+  int pa = 0;
+  int range = 66;  // covers a true loop closure's loop (~30 iterations) in one pass
+  while (pa < h->pmax) {
+    int G = (range + per - 1) / per;
+    G = std::max(1, std::min(G, SPREAD_WAVES / n));
+    const int pb = std::min(pa + G * per, h->pmax);
+    KMX_HIP(hipMemsetAsync(h->d_more, 0, sizeof(unsigned), st));
+    hipLaunchKernelGGL(stew ? k_rs_hyps<true> : k_rs_hyps<false>, dim3(n * G), dim3(RS_BLOCK), 0, st,
+                       (const double*)h->d_bear, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
+                       (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp,
+                       (const RsState*)h->d_st, h->d_hout, pa, pb, G, h->d_sfbuf);
+    hipLaunchKernelGGL(k_rs_replay, dim3((n + 63) / 64), dim3(64), 0, st, (const int*)h->d_K, rp, h->d_st,
+                       (const HypOut*)h->d_hout, pb, n, h->d_more);
+    unsigned more = 0;
+    KMX_HIP(hipMemcpyAsync(&more, h->d_more, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    KMX_HIP(hipStreamSynchronize(st));
+    if (!more) break;
+    pa = pb;
+    range = pa < 510 ? 510 - pa : 1500;  // then the rest of a 500-iteration loop, then its skips
+  }
+  hipLaunchKernelGGL(k_rs_finish, dim3(n), dim3(RS_BLOCK), 0, st, (const double*)h->d_bear, (const double*)h->d_pts,
+                     h->N, (const int*)h->d_cq, (const int*)h->d_cm, (const int2*)h->d_pairs, (const int*)h->d_K, rp,
+                     (const RsState*)h->d_st, h->d_res, masks ? h->d_mask : nullptr, h->d_sfbuf);
+  if (rp.pnp && (stages & KMX_LCD_STAGE_RECOVER))
+    if (int rc = launch_recover(h, n, pnp_params(h, stages), h->d_table_rec, 0)) return rc;
+  KMX_HIP(hipGetLastError());
+  return 0;
+}
+
 // Everything after the pair rows d_pairs / d_K exist: RANSAC, then recovery.
-int enqueue_ransac(kmx_lcd* h, int n, int stages, bool want_masks) {
+// sync_ok: the caller synchronises on the results (kmx_lcd_verify,
+// kmx_lcd_verify_matches), so a small call may take the spread form.
+int enqueue_ransac(kmx_lcd* h, int n, int stages, bool want_masks, bool sync_ok = false) {
   if (h->P.rng_stream) return verify_ordered(h, n, stages, want_masks);
+  if (sync_ok && n > 0 && n <= h->spread_max) return ransac_spread(h, n, stages, want_masks);
   const RsParams rp = rs_params(h, stages);
   if (int rc = launch_ransac(h, n, rp, h->d_table, 0, want_masks || rp.pnp)) return rc;
   if (rp.pnp && (stages & KMX_LCD_STAGE_RECOVER))
@@ -2927,7 +3217,7 @@ int slot_upload(kmx_lcd* h, int n, const int32_t* cq, const int32_t* cm) {
 // stream behind it: a call's kNN2 runs in the previous call's RANSAC tail
 // (the work-queue RANSAC holds every wave slot until its queue drains, so the
 // kNN2 workgroups start as its last waves leave), off the critical path.
-int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
+int enqueue_verify(kmx_lcd* h, int n, bool want_masks, bool sync_ok = false) {
   if (n == 0) return 0;
   const int s = h->cur;
   const size_t knn_smem = (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1);
@@ -2944,7 +3234,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks) {
   if (h->timing) KMX_HIP(hipEventRecord(h->ev[1], h->kstream));
   KMX_HIP(hipEventRecord(h->ev_knn[s], h->kstream));
   KMX_HIP(hipStreamWaitEvent(rs_stream(h), h->ev_knn[s], 0));
-  if (int rc = enqueue_ransac(h, n, KMX_LCD_STAGE_2D2D | KMX_LCD_STAGE_RECOVER, want_masks)) return rc;
+  if (int rc = enqueue_ransac(h, n, KMX_LCD_STAGE_2D2D | KMX_LCD_STAGE_RECOVER, want_masks, sync_ok)) return rc;
   if (h->timing) KMX_HIP(hipEventRecord(h->ev[2], rs_stream(h)));
   KMX_HIP(hipEventRecord(h->ev_rs[s], rs_stream(h)));
   h->ev_rs_set[s] = true;
@@ -3048,6 +3338,8 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
     return kmx::fail(KMX_EHIP, "hipStreamCreate / hipEventCreate");
   }
   if (const char* v = std::getenv("KMX_RS_PROF")) h->prof = std::atoi(v);
+  // KMX_LCD_SPREAD: the largest synchronous call that takes the spread form (0: never)
+  if (const char* v = std::getenv("KMX_LCD_SPREAD")) h->spread_max = std::max(0, std::atoi(v));
   *out = h;
   return KMX_OK;
   KMX_GUARD_END
@@ -3161,7 +3453,7 @@ extern "C" int kmx_lcd_verify(kmx_lcd* h, int32_t n, const int32_t* cq, const in
   KMX_HIP(hipSetDevice(h->device));
   if (int rc = ensure_cap(h, n)) return rc;
   if (int rc = slot_upload(h, n, cq, cm)) return rc;
-  if (int rc = enqueue_verify(h, n, inlier_masks != nullptr)) return rc;
+  if (int rc = enqueue_verify(h, n, inlier_masks != nullptr, true)) return rc;
   if (n) KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
   if (n && inlier_masks)
     KMX_HIP(hipMemcpyAsync(inlier_masks, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
@@ -3258,7 +3550,7 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
   hipLaunchKernelGGL(k_scatter_pairs, dim3(n), dim3(256), 0, rs_stream(h), (const int64_t*)h->d_mptr,
                      (const int*)h->d_iq, (const int*)h->d_im, h->N, h->d_pairs, h->d_K);
   KMX_HIP(hipGetLastError());
-  if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr)) return rc;
+  if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr, true)) return rc;
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
   if (inlier_masks)

@@ -97,10 +97,13 @@ def team_tile_incidences(graph, world: int, r: int, form: str = "standard") -> i
     automatically for a handle holding 1/world of the team's incidences; the
     multi-rank driver passes it to every rank, so all ranks cut their robots
     alike whatever their share (csrc/pgo.hip set_graph). The resident round
-    (tCG_form "resident") always cuts full tiles of two gather chunks."""
+    (tCG_form "resident") cuts each rank's shard itself (0: automatic): full
+    tiles of two gather chunks, 4- or 5-wave workgroups by what the shard
+    needs to keep one tile per CU, so its summation order (the last bits, not
+    the parity bar) depends on the poses per GPU."""
     tp = 4 * (64 // r)
     if form == "resident":
-        return 2 * tp * r
+        return 0
     inc = 2 * int(graph.m) // max(world, 1)
     return min(2 * tp * r, max(180, -(-inc // TILES_TARGET)))
 
