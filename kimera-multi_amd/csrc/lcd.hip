@@ -2731,7 +2731,7 @@ struct kmx_lcd {
   // candidate buffers: LCD_SLOTS slots, used by successive calls in turn, so
   // a call's kNN2 (on kstream) can run while earlier calls' RANSACs drain;
   // d_cq .. d_order below point into the current slot
-  int cap = 0, cur = 0;
+  int cap = 0, cur = 0;  // cap: the current slot's capacity
   // Each slot's RANSAC can run on its own stream (slot 0: the handle's
   // stream, slot s > 0: rsx[s]) with its own work-queue counter and per-wave
   // scratch, so the next calls' RANSACs take the CUs the previous call's
@@ -2744,6 +2744,7 @@ struct kmx_lcd {
     double* prior = nullptr;
     double* fbuf = nullptr;
     int* next = nullptr;
+    int cap = 0;  // candidates the slot's buffers hold (0: not allocated yet)
   } slot[LCD_SLOTS];
   hipStream_t rsx[LCD_SLOTS] = {};  // rsx[s]: slot s's RANSAC stream (s > 0)
   bool rs_conc = true;              // KMX_LCD_RSX=0: every slot on the handle's stream (A/B switch)
@@ -2762,6 +2763,7 @@ struct kmx_lcd {
   // caller-supplied correspondences (kmx_lcd_verify_matches): CSR staging
   size_t pair_cap = 0;
   int64_t* d_mptr = nullptr;
+  int mptr_cap = 0;
   int *d_iq = nullptr, *d_im = nullptr;
   double* d_prior = nullptr;
   // ordered sampler (rng_stream 1): the verification thread's engine, one
@@ -2837,6 +2839,7 @@ void use_next_slot(kmx_lcd* h) {
   h->d_cq = sl.cq; h->d_cm = sl.cm; h->d_K = sl.K; h->d_hyps = sl.hyps; h->d_nrec = sl.nrec; h->d_order = sl.order;
   h->d_pairs = sl.pairs; h->d_res = sl.res; h->d_mask = sl.mask; h->d_prior = sl.prior;
   h->d_fbuf = sl.fbuf; h->d_next = sl.next;
+  h->cap = sl.cap;
 }
 // The current slot's RANSAC stream: everything a call does on its slot's
 // buffers after the kNN2 runs there.
@@ -2860,6 +2863,7 @@ void lcd_free_pairs(kmx_lcd* h) {
   for (void* x : p)
     if (x) (void)hipFree(x);
   h->d_mptr = nullptr; h->d_iq = h->d_im = nullptr; h->d_row = nullptr;
+  h->mptr_cap = 0;
   h->pair_cap = 0;
 }
 
@@ -2933,14 +2937,33 @@ int ensure_tables(kmx_lcd* h) {
   return 0;
 }
 
-// Candidate buffers for n candidates in both slots, then the next call's slot.
-int ensure_cap(kmx_lcd* h, int n) {
-  if (n > h->cap) {
-    lcd_free_cand(h);
+// True while an earlier call may still run on some slot (an async call's
+// RANSAC or kNN2 not yet complete).
+bool slots_busy(kmx_lcd* h) {
+  for (int s = 0; s < LCD_SLOTS; ++s)
+    if (h->ev_rs_set[s] && hipEventQuery(h->ev_rs[s]) != hipSuccess) return true;
+  return h->kstream && hipStreamQuery(h->kstream) != hipSuccess;
+}
+// The call's slot, with buffers for n candidates. Slots are allocated (and
+// grown) one at a time, when a call first lands on them: a synchronous call
+// with nothing in flight takes slot 0, so callers that never overlap calls
+// hold one slot's buffers, not LCD_SLOTS; async calls rotate through all.
+int ensure_cap(kmx_lcd* h, int n, bool async) {
+  if (!async && !slots_busy(h)) h->cur = LCD_SLOTS - 1;  // use_next_slot -> slot 0
+  use_next_slot(h);
+  kmx_lcd::Slot& sl = h->slot[h->cur];
+  if (n > sl.cap) {
+    // the slot's last call may still be in flight on any stream
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    sync_rsx(h);
+    if (h->kstream) (void)hipStreamSynchronize(h->kstream);
+    void* p[] = {sl.cq, sl.cm, sl.K, sl.hyps, sl.nrec, sl.order, sl.pairs, sl.res, sl.mask, sl.prior, sl.fbuf, sl.next};
+    for (void* x : p)
+      if (x) (void)hipFree(x);
+    sl = kmx_lcd::Slot{};
+    h->ev_rs_set[h->cur] = false;
     const int cap = std::max(n, 1024);
-    bool ok = true;
-    for (auto& sl : h->slot)
-      ok = ok &&
+    bool ok =
            hipMalloc(&sl.fbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::min(cap, RS_MAX_SLOTS)) ==
                hipSuccess &&
            hipMalloc(&sl.next, sizeof(int)) == hipSuccess &&
@@ -2956,9 +2979,10 @@ int ensure_cap(kmx_lcd* h, int n) {
       lcd_free_cand(h);
       return kmx::fail(KMX_ENOMEM, "candidate buffers");
     }
-    h->cap = cap;
+    sl.cap = cap;
+    h->cur = (h->cur + LCD_SLOTS - 1) % LCD_SLOTS;
+    use_next_slot(h);  // re-point d_cq .. d_order at the new buffers
   }
-  use_next_slot(h);
   if (!h->cus) KMX_HIP(hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device));
   h->rs_small = h->rs_conc && (int64_t)n < 96LL * h->cus;
   h->rs_on = h->cur != 0 && h->rs_small;
@@ -3451,7 +3475,7 @@ extern "C" int kmx_lcd_verify(kmx_lcd* h, int32_t n, const int32_t* cq, const in
   if (int rc = check_cands(h, n, cq, cm)) return rc;
   KMX_CHECK(results || n == 0, KMX_EINVAL, "null results");
   KMX_HIP(hipSetDevice(h->device));
-  if (int rc = ensure_cap(h, n)) return rc;
+  if (int rc = ensure_cap(h, n, false)) return rc;
   if (int rc = slot_upload(h, n, cq, cm)) return rc;
   if (int rc = enqueue_verify(h, n, inlier_masks != nullptr, true)) return rc;
   if (n) KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
@@ -3466,7 +3490,7 @@ extern "C" int kmx_lcd_verify_async(kmx_lcd* h, int32_t n, const int32_t* cq, co
   KMX_GUARD_BEGIN
   if (int rc = check_cands(h, n, cq, cm)) return rc;
   KMX_HIP(hipSetDevice(h->device));
-  if (int rc = ensure_cap(h, n)) return rc;
+  if (int rc = ensure_cap(h, n, true)) return rc;
   if (int rc = slot_upload(h, n, cq, cm)) return rc;
   KMX_HIP(hipStreamSynchronize(h->kstream));  // host arrays may go away after return
   return enqueue_verify(h, n, false);
@@ -3480,7 +3504,7 @@ extern "C" int kmx_lcd_match(kmx_lcd* h, int32_t n, const int32_t* cq, const int
   KMX_CHECK(n == 0 || (pairs_out && k_out), KMX_EINVAL, "null output");
   if (n == 0) return KMX_OK;
   KMX_HIP(hipSetDevice(h->device));
-  if (int rc = ensure_cap(h, n)) return rc;
+  if (int rc = ensure_cap(h, n, false)) return rc;
   if (int rc = rs_wait_slot(h)) return rc;
   KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
   KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
@@ -3511,6 +3535,7 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
   if (n == 0) return KMX_OK;
   const int64_t base = mptr[0];
   KMX_CHECK(base >= 0, KMX_EINVAL, "mptr[0] < 0");
+  KMX_CHECK(mptr[n] == base || (iq && im), KMX_EINVAL, "null i_query / i_match with correspondences in mptr");
   for (int i = 0; i < n; ++i) {
     const int64_t K = mptr[i + 1] - mptr[i];
     KMX_CHECK(K >= 0 && K <= h->N, KMX_EINVAL, "a candidate has more pairs than max_feats (or mptr decreases)");
@@ -3521,9 +3546,9 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
   }
   const size_t total = (size_t)(mptr[n] - base);
   KMX_HIP(hipSetDevice(h->device));
-  if (int rc = ensure_cap(h, n)) return rc;
+  if (int rc = ensure_cap(h, n, false)) return rc;
   if (int rc = rs_wait_slot(h)) return rc;
-  if (total > h->pair_cap || !h->d_mptr) {
+  if (total > h->pair_cap || !h->d_iq) {
     if (h->d_iq) (void)hipFree(h->d_iq);
     if (h->d_im) (void)hipFree(h->d_im);
     h->d_iq = h->d_im = nullptr;
@@ -3533,9 +3558,14 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
     KMX_HIP(hipMalloc(&h->d_im, sizeof(int) * pc));
     h->pair_cap = pc;
   }
-  if (h->d_mptr) (void)hipFree(h->d_mptr);
-  h->d_mptr = nullptr;
-  KMX_HIP(hipMalloc(&h->d_mptr, sizeof(int64_t) * (n + 1)));
+  if (n + 1 > h->mptr_cap) {  // grow-only: a hipFree here would wait for calls in flight on other slots
+    if (h->d_mptr) (void)hipFree(h->d_mptr);
+    h->d_mptr = nullptr;
+    h->mptr_cap = 0;
+    const int mc = std::max(n + 1, 1024);
+    KMX_HIP(hipMalloc(&h->d_mptr, sizeof(int64_t) * mc));
+    h->mptr_cap = mc;
+  }
   std::vector<int64_t> mp(mptr, mptr + n + 1);
   for (auto& x : mp) x -= base;
   KMX_HIP(hipMemcpyAsync(h->d_mptr, mp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, rs_stream(h)));
