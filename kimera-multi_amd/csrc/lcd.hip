@@ -2335,8 +2335,9 @@ struct RsState {  // the serial loop's control between passes
 };
 constexpr int SPREAD_PER_NISTER = 2;  // Nister hypotheses per wave (one at a time)
 
-__global__ void k_rs_init(RsState* st, int n, int stages) {
+__global__ void k_rs_init(RsState* st, int n, int stages, unsigned* more, int nmore) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < nmore) more[c] = 0u;  // the ranges' flags (k_rs_replay)
   if (c >= n) return;
   RsState s;
   s.kk = 1.0;
@@ -2760,12 +2761,7 @@ struct kmx_lcd {
   unsigned char* d_mask = nullptr;
   double* d_fbuf = nullptr;  // [slots][6 N + STASH] compact match bearings + Stewenius stash, per k_ransac_coop wave
   int* d_next = nullptr;     // k_ransac_coop's work-queue counter
-  // caller-supplied correspondences (kmx_lcd_verify_matches): CSR staging
-  size_t pair_cap = 0;
-  int64_t* d_mptr = nullptr;
-  int mptr_cap = 0;
-  int *d_iq = nullptr, *d_im = nullptr;
-  double* d_prior = nullptr;
+  double* d_prior = nullptr;  // the current slot's T_prior rows (kmx_lcd_verify_matches)
   // ordered sampler (rng_stream 1): the verification thread's engine, one
   // candidate's sample row, the passes each problem drew, recovery sizes
   std::mt19937 stream_rng;
@@ -2778,7 +2774,16 @@ struct kmx_lcd {
   RsState* d_st = nullptr;
   HypOut* d_hout = nullptr;
   double* d_sfbuf = nullptr;
-  unsigned* d_more = nullptr;
+  unsigned* d_more = nullptr;  // [more_cap] one word per range: some candidate needs the next range
+  int more_cap = 0;
+  unsigned* h_more = nullptr;  // pinned copy of the word just read
+  // pinned staging of the synchronous one-candidate calls (kmx_lcd_match,
+  // kmx_lcd_verify_matches): every input in one host-to-device copy, every
+  // output through pinned memory (a pageable copy is a blocking staged copy
+  // each; the call-for-call chain made five to seven of them per call)
+  size_t io_cap = 0;
+  char* h_io = nullptr;  // pinned host
+  char* d_io = nullptr;
   int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
   // kmx_lcd_enable_timing: events around the kNN2 and the RANSAC launches
   bool timing = false;
@@ -2829,9 +2834,28 @@ void lcd_free_cand(kmx_lcd* h) {
   void* q[] = {h->d_st, h->d_hout, h->d_sfbuf, h->d_more};
   for (void* x : q)
     if (x) (void)hipFree(x);
-  h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_more = nullptr;
+  if (h->h_more) (void)hipHostFree(h->h_more);
+  h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_more = nullptr; h->h_more = nullptr;
   h->spread_cap = 0;
+  h->more_cap = 0;
 }
+// Pinned host + device staging of at least `bytes` (grow-only; the callers
+// are synchronous, so the previous call's copies have completed).
+int io_reserve(kmx_lcd* h, size_t bytes) {
+  if (bytes <= h->io_cap) return 0;
+  if (h->stream) KMX_HIP(hipStreamSynchronize(h->stream));
+  sync_rsx(h);
+  if (h->h_io) (void)hipHostFree(h->h_io);
+  if (h->d_io) (void)hipFree(h->d_io);
+  h->h_io = nullptr; h->d_io = nullptr;
+  h->io_cap = 0;
+  const size_t cap = std::max<size_t>(bytes, 256 * 1024);
+  KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_io), cap, hipHostMallocDefault));
+  KMX_HIP(hipMalloc(reinterpret_cast<void**>(&h->d_io), cap));
+  h->io_cap = cap;
+  return 0;
+}
+inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 // The next call's slot: its buffers become d_cq .. d_order.
 void use_next_slot(kmx_lcd* h) {
   h->cur = (h->cur + 1) % LCD_SLOTS;
@@ -2859,12 +2883,14 @@ int rs_wait_slot(kmx_lcd* h) {
   return 0;
 }
 void lcd_free_pairs(kmx_lcd* h) {
-  void* p[] = {h->d_mptr, h->d_iq, h->d_im, h->d_row};
+  void* p[] = {h->d_row};
   for (void* x : p)
     if (x) (void)hipFree(x);
-  h->d_mptr = nullptr; h->d_iq = h->d_im = nullptr; h->d_row = nullptr;
-  h->mptr_cap = 0;
-  h->pair_cap = 0;
+  h->d_row = nullptr;
+  if (h->h_io) (void)hipHostFree(h->h_io);
+  if (h->d_io) (void)hipFree(h->d_io);
+  h->h_io = nullptr; h->d_io = nullptr;
+  h->io_cap = 0;
 }
 
 // One pass of opengv's drawIndexSample: S swaps of the persistent shuffle over
@@ -2990,14 +3016,21 @@ int ensure_cap(kmx_lcd* h, int n, bool async) {
 }
 
 // CSR correspondences -> the per-candidate pair rows of k_ransac_coop
-// (pairs[c][k], K[c]); one workgroup per candidate.
+// (pairs[c][k], K[c]); one workgroup per candidate, which also moves the
+// candidate's frame ids (and its prior) from the staging block to the slot.
 __global__ __launch_bounds__(256) void k_scatter_pairs(const int64_t* mptr, const int* iq, const int* im, int N,
-                                                       int2* pairs, int* Kout) {
+                                                       int2* pairs, int* Kout, const int* cq_in, const int* cm_in,
+                                                       const double* prior_in, int* cq, int* cm, double* prior) {
   const int c = blockIdx.x;
   const int64_t b = mptr[c];
   const int K = (int)(mptr[c + 1] - b);
   for (int k = threadIdx.x; k < K; k += blockDim.x) pairs[(size_t)c * N + k] = make_int2(iq[b + k], im[b + k]);
-  if (threadIdx.x == 0) Kout[c] = K;
+  if (threadIdx.x == 0) {
+    Kout[c] = K;
+    cq[c] = cq_in[c];
+    cm[c] = cm_in[c];
+  }
+  if (prior_in && threadIdx.x < 12) prior[12 * (size_t)c + threadIdx.x] = prior_in[12 * (size_t)c + threadIdx.x];
 }
 
 RsParams rs_params(const kmx_lcd* h, int stages) {
@@ -3169,39 +3202,47 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks) {
   const bool masks = want_masks || rp.pnp;
   hipStream_t st = rs_stream(h);
   if (n > h->spread_cap) {
-    void* q[] = {h->d_st, h->d_hout, h->d_sfbuf, h->d_more};
+    void* q[] = {h->d_st, h->d_hout, h->d_sfbuf};
     KMX_HIP(hipStreamSynchronize(st));
     for (void* x : q)
       if (x) (void)hipFree(x);
-    h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_more = nullptr;
+    h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr;
     h->spread_cap = 0;
     const int cap = std::max(n, h->spread_max);
     KMX_HIP(hipMalloc(&h->d_st, sizeof(RsState) * cap));
     KMX_HIP(hipMalloc(&h->d_hout, sizeof(HypOut) * (size_t)cap * h->pmax));
     KMX_HIP(hipMalloc(&h->d_sfbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::max(SPREAD_WAVES, cap)));
-    KMX_HIP(hipMalloc(&h->d_more, sizeof(unsigned)));
     h->spread_cap = cap;
   }
+  if (h->pmax + 1 > h->more_cap) {  // every range advances by >= 1 pass: at most pmax ranges
+    KMX_HIP(hipStreamSynchronize(st));
+    if (h->d_more) (void)hipFree(h->d_more);
+    h->d_more = nullptr;
+    h->more_cap = 0;
+    KMX_HIP(hipMalloc(&h->d_more, sizeof(unsigned) * (h->pmax + 1)));
+    h->more_cap = h->pmax + 1;
+  }
+  if (!h->h_more)
+    KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_more), sizeof(unsigned), hipHostMallocDefault));
   const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
   const int per = stew ? SG : SPREAD_PER_NISTER;
-  hipLaunchKernelGGL(k_rs_init, dim3((n + 63) / 64), dim3(64), 0, st, h->d_st, n, stages);
+  hipLaunchKernelGGL(k_rs_init, dim3((std::max(n, h->more_cap) + 63) / 64), dim3(64), 0, st, h->d_st, n, stages,
+                     h->d_more, h->more_cap);
   int pa = 0;
   int range = 66;  // covers a true loop closure's loop (~30 iterations) in one pass
-  while (pa < h->pmax) {
+  for (int it = 0; pa < h->pmax; ++it) {
     int G = (range + per - 1) / per;
     G = std::max(1, std::min(G, SPREAD_WAVES / n));
     const int pb = std::min(pa + G * per, h->pmax);
-    KMX_HIP(hipMemsetAsync(h->d_more, 0, sizeof(unsigned), st));
     hipLaunchKernelGGL(stew ? k_rs_hyps<true> : k_rs_hyps<false>, dim3(n * G), dim3(RS_BLOCK), 0, st,
                        (const double*)h->d_bear, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
                        (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp,
                        (const RsState*)h->d_st, h->d_hout, pa, pb, G, h->d_sfbuf);
     hipLaunchKernelGGL(k_rs_replay, dim3((n + 63) / 64), dim3(64), 0, st, (const int*)h->d_K, rp, h->d_st,
-                       (const HypOut*)h->d_hout, pb, n, h->d_more);
-    unsigned more = 0;
-    KMX_HIP(hipMemcpyAsync(&more, h->d_more, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+                       (const HypOut*)h->d_hout, pb, n, h->d_more + it);
+    KMX_HIP(hipMemcpyAsync(h->h_more, h->d_more + it, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     KMX_HIP(hipStreamSynchronize(st));
-    if (!more) break;
+    if (!*h->h_more) break;
     pa = pb;
     range = pa < 510 ? 510 - pa : 1500;  // then the rest of a 500-iteration loop, then its skips
   }
@@ -3506,16 +3547,22 @@ extern "C" int kmx_lcd_match(kmx_lcd* h, int32_t n, const int32_t* cq, const int
   KMX_HIP(hipSetDevice(h->device));
   if (int rc = ensure_cap(h, n, false)) return rc;
   if (int rc = rs_wait_slot(h)) return rc;
-  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
-  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
+  // pinned staging: [cq][cm] in, [pairs][K] out
+  const size_t pb = sizeof(int2) * (size_t)n * h->N, kin = al16(sizeof(int) * n);
+  if (int rc = io_reserve(h, std::max(2 * kin, pb + kin))) return rc;
+  std::memcpy(h->h_io, cq, sizeof(int) * n);
+  std::memcpy(h->h_io + kin, cm, sizeof(int) * n);
+  KMX_HIP(hipMemcpyAsync(h->d_io, h->h_io, 2 * kin, hipMemcpyHostToDevice, rs_stream(h)));
   hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1), rs_stream(h),
-                     (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, (const int*)h->d_cq,
-                     (const int*)h->d_cm, h->P.norm, h->P.lowe_ratio, h->d_pairs, h->d_K);
+                     (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, (const int*)h->d_io,
+                     (const int*)(h->d_io + kin), h->P.norm, h->P.lowe_ratio, h->d_pairs, h->d_K);
   KMX_HIP(hipGetLastError());
-  KMX_HIP(hipMemcpyAsync(pairs_out, h->d_pairs, sizeof(int2) * (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
-  KMX_HIP(hipMemcpyAsync(k_out, h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, rs_stream(h)));
+  KMX_HIP(hipMemcpyAsync(h->h_io, h->d_pairs, pb, hipMemcpyDeviceToHost, rs_stream(h)));
+  KMX_HIP(hipMemcpyAsync(h->h_io + pb, h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, rs_stream(h)));
   if (int rc = mark_slot(h)) return rc;
   KMX_HIP(hipStreamSynchronize(rs_stream(h)));
+  std::memcpy(pairs_out, h->h_io, pb);
+  std::memcpy(k_out, h->h_io + pb, sizeof(int) * n);
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -3548,45 +3595,40 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
   KMX_HIP(hipSetDevice(h->device));
   if (int rc = ensure_cap(h, n, false)) return rc;
   if (int rc = rs_wait_slot(h)) return rc;
-  if (total > h->pair_cap || !h->d_iq) {
-    if (h->d_iq) (void)hipFree(h->d_iq);
-    if (h->d_im) (void)hipFree(h->d_im);
-    h->d_iq = h->d_im = nullptr;
-    h->pair_cap = 0;
-    const size_t pc = std::max<size_t>(total, 4096);
-    KMX_HIP(hipMalloc(&h->d_iq, sizeof(int) * pc));
-    KMX_HIP(hipMalloc(&h->d_im, sizeof(int) * pc));
-    h->pair_cap = pc;
+  // every input in one pinned block and one host-to-device copy:
+  // [mptr - base][cq][cm][i_query][i_match][T_prior]; k_scatter_pairs moves
+  // the candidates' ids and priors into the slot's buffers
+  const size_t o_cq = al16(sizeof(int64_t) * (n + 1)), o_cm = o_cq + al16(sizeof(int) * n),
+               o_iq = o_cm + al16(sizeof(int) * n), o_im = o_iq + al16(sizeof(int) * total),
+               o_pr = o_im + al16(sizeof(int) * total), in_bytes = o_pr + (T_prior ? sizeof(double) * 12 * n : 0);
+  const size_t rb = al16(sizeof(kmx_lcd_result) * n), out_bytes = rb + (inlier_masks ? (size_t)n * h->N : 0);
+  if (int rc = io_reserve(h, std::max(in_bytes, out_bytes))) return rc;
+  {
+    int64_t* mp = reinterpret_cast<int64_t*>(h->h_io);
+    for (int i = 0; i <= n; ++i) mp[i] = mptr[i] - base;
+    std::memcpy(h->h_io + o_cq, cq, sizeof(int) * n);
+    std::memcpy(h->h_io + o_cm, cm, sizeof(int) * n);
+    if (total) {
+      std::memcpy(h->h_io + o_iq, iq + base, sizeof(int) * total);
+      std::memcpy(h->h_io + o_im, im + base, sizeof(int) * total);
+    }
+    if (T_prior) std::memcpy(h->h_io + o_pr, T_prior, sizeof(double) * 12 * n);
   }
-  if (n + 1 > h->mptr_cap) {  // grow-only: a hipFree here would wait for calls in flight on other slots
-    if (h->d_mptr) (void)hipFree(h->d_mptr);
-    h->d_mptr = nullptr;
-    h->mptr_cap = 0;
-    const int mc = std::max(n + 1, 1024);
-    KMX_HIP(hipMalloc(&h->d_mptr, sizeof(int64_t) * mc));
-    h->mptr_cap = mc;
-  }
-  std::vector<int64_t> mp(mptr, mptr + n + 1);
-  for (auto& x : mp) x -= base;
-  KMX_HIP(hipMemcpyAsync(h->d_mptr, mp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, rs_stream(h)));
-  if (total) {
-    KMX_HIP(hipMemcpyAsync(h->d_iq, iq + base, sizeof(int) * total, hipMemcpyHostToDevice, rs_stream(h)));
-    KMX_HIP(hipMemcpyAsync(h->d_im, im + base, sizeof(int) * total, hipMemcpyHostToDevice, rs_stream(h)));
-  }
-  KMX_HIP(hipMemcpyAsync(h->d_cq, cq, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
-  KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, rs_stream(h)));
-  if (T_prior)
-    KMX_HIP(hipMemcpyAsync(h->d_prior, T_prior, sizeof(double) * 12 * (size_t)n, hipMemcpyHostToDevice, rs_stream(h)));
-  hipLaunchKernelGGL(k_scatter_pairs, dim3(n), dim3(256), 0, rs_stream(h), (const int64_t*)h->d_mptr,
-                     (const int*)h->d_iq, (const int*)h->d_im, h->N, h->d_pairs, h->d_K);
+  KMX_HIP(hipMemcpyAsync(h->d_io, h->h_io, in_bytes, hipMemcpyHostToDevice, rs_stream(h)));
+  hipLaunchKernelGGL(k_scatter_pairs, dim3(n), dim3(256), 0, rs_stream(h), (const int64_t*)h->d_io,
+                     (const int*)(h->d_io + o_iq), (const int*)(h->d_io + o_im), h->N, h->d_pairs, h->d_K,
+                     (const int*)(h->d_io + o_cq), (const int*)(h->d_io + o_cm),
+                     T_prior ? (const double*)(h->d_io + o_pr) : nullptr, h->d_cq, h->d_cm, h->d_prior);
   KMX_HIP(hipGetLastError());
   if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr, true)) return rc;
   KMX_HIP(hipGetLastError());
-  KMX_HIP(hipMemcpyAsync(results, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
+  KMX_HIP(hipMemcpyAsync(h->h_io, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
   if (inlier_masks)
-    KMX_HIP(hipMemcpyAsync(inlier_masks, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
+    KMX_HIP(hipMemcpyAsync(h->h_io + rb, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
   if (int rc = mark_slot(h)) return rc;
   KMX_HIP(hipStreamSynchronize(rs_stream(h)));
+  std::memcpy(results, h->h_io, sizeof(kmx_lcd_result) * n);
+  if (inlier_masks) std::memcpy(inlier_masks, h->h_io + rb, (size_t)n * h->N);
   return KMX_OK;
   KMX_GUARD_END
 }

@@ -1115,17 +1115,20 @@ __device__ __forceinline__ void robot_sum(const double* part, int stride, int t0
 // robot_sum's order (a thread's tiles in tile order, then the wave sums and
 // the waves in order: the same sums for any U).
 // NS <= 2: 2-wide partials (part_h / part_u); NS = 3, 4: d.part (stride NPART).
-// A tile partial pair: plain, or (SC, the resident round: partials another
-// workgroup of the same launch wrote through) two 8-B agent-scope loads (sc1).
+// A tile partial pair part[i], part[i + 1] (i even): plain, or (SC, the
+// resident round: partials another workgroup of the same launch wrote
+// through) one 16-B sc1 buffer load through a descriptor of the
+// (workgroup-uniform) array base — the replicated-counter hand-off takes 4- or
+// 16-B sc1 loads (MI355X_MICROARCH.md "Valid forms").
+typedef unsigned kmx_u4 __attribute__((ext_vector_type(4)));
 template <bool SC>
-__device__ __forceinline__ double2 ldpart(const double* p) {
+__device__ __forceinline__ double2 ldpart(const double* part, size_t i) {
   if constexpr (SC) {
-    unsigned long long* q = reinterpret_cast<unsigned long long*>(const_cast<double*>(p));
-    const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_double2(__longlong_as_double((long long)a), __longlong_as_double((long long)b));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(part), 0, 0x7ffffff0, 0x00020000);
+    const kmx_u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(i * 8), 0, 16);
+    return __builtin_bit_cast(double2, v);
   } else {
-    return *reinterpret_cast<const double2*>(p);
+    return *reinterpret_cast<const double2*>(part + i);
   }
 }
 
@@ -1140,10 +1143,10 @@ struct RobotSum {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = min(t0 + (int)threadIdx.x + u * RBLOCK, t1 - 1);
-      const double* pt = part + (size_t)t * stride;
-      const double2 x = ldpart<SC>(pt);
+      const size_t pt = (size_t)t * stride;
+      const double2 x = ldpart<SC>(part, pt);
       if constexpr (NS > 2) {
-        const double2 y = ldpart<SC>(pt + 2);
+        const double2 y = ldpart<SC>(part, pt + 2);
         a[u][2] = y.x;
         if constexpr (NS > 3) a[u][3] = y.y;
       }
@@ -1426,6 +1429,12 @@ __device__ __forceinline__ void trial_rows(const Dev& d, const Lane& L, size_t o
 // tCG step, part 1 (the dominant kernel): Hz = Hess(z) by gather; then by
 // linearity delta = -z + beta delta_old, Hdelta = -Hz + beta Hdelta_old;
 // partial <delta, Hdelta>. delta_k is kept for k_retract's eta (Dev::dh).
+// Hz and Hdelta are kept BEFORE the tangent projection (Hz^ = H z - z S;
+// the Riemannian H delta = P_Y(H delta^)): projection is linear, so the
+// recurrence holds for the unprojected rows, and <delta, Hdelta^> equals
+// <delta, P_Y(Hdelta^)> for a tangent delta (Y^T delta skew, Y sym(.) S
+// symmetric). k_update, which loads Y anyway, projects; this kernel then
+// reads no X row (16 MB per launch at configs[3]: VERDICT r4 item 2).
 template <int R, int RW, int RM>
 __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int slot, HostStatus* hs,
                                           unsigned long long seq, char* smem) {
@@ -1513,19 +1522,21 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
   asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
   if (L.valid) {
 #if KMX_HESS_PROBE & 2
-    for (int k = 0; k < 4; ++k) { zs[k] = 1e-3 * k; y[k] = (k == L.a) ? 1.0 : 0.0; }
+    for (int k = 0; k < 4; ++k) zs[k] = 1e-3 * k;
     for (int k = 0; k < 9; ++k) S[k] = (k % 4 == 0) ? 1.0 : 0.0;
 #else
     load4(d.z + o, zs);
-    load4(d.X + o, y);
     load_sym3(d.S + 6 * (size_t)L.pose, S);
 #endif
   } else {
 #pragma unroll
     for (int i = 0; i < 9; ++i) S[i] = 0.0;
   }
-  double hz[4];
-  group_rhess<R, true>(y, zs, H, S, L.base, hz, reinterpret_cast<double*>(smem));
+  double hz[4];  // H z - z S (group_rhess before its projection)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) hz[k] = H[k] - (zs[0] * S[0 * 3 + k] + zs[1] * S[1 * 3 + k] + zs[2] * S[2 * 3 + k]);
+  hz[3] = H[3];
+  (void)y;
   double v = 0.0;
   double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
   const int dhn = d.dhn;
@@ -1628,7 +1639,7 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
     if (L.valid) {
       load4(d.hd + o, hdl);
       load4((first0 ? d.g : d.r) + o, rr);
-      load4(d.X + o, y);  // used by the precon of interior steps (boundary steps are rare)
+      load4(d.X + o, y);  // the projection of H delta, and the precon of interior steps
       if (d.p.use_precond) {  // the preconditioner block too: no load after the decision
         load_sym4(d.Pinv + SYM4 * (size_t)L.pose, Pm);
       }
@@ -1657,14 +1668,18 @@ __device__ __forceinline__ void body_update(const Dev& d, HostStatus* hs, unsign
     if (L.valid) {
       load4(d.hd + o, hdl);
       load4((tcg_iter == 1 ? d.g : d.r) + o, rr);  // r_0 = g (k_grad does not store r)
-      if (c.mode == MODE_INTERIOR) load4(d.X + o, y);
+      load4(d.X + o, y);  // the projection of H delta (and the precon of interior steps)
     }
   }
   const bool interior = (mode == MODE_INTERIOR);
   (void)tcg_iter;
-  if (L.valid) {
+  {  // H delta = P_Y(H delta^) (k_hess keeps it unprojected); every lane of the group takes part
+    double hp[4];
+    group_proj<R, true>(y, hdl, L.base, hp, reinterpret_cast<double*>(smem));
+    if (L.valid) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) rr[k] += coef * hdl[k];
+      for (int k = 0; k < 4; ++k) rr[k] += coef * hp[k];
+    }
   }
   double vals[2] = {0.0, 0.0}, zr[4] = {0, 0, 0, 0};
   if (interior) {  // uniform per robot
@@ -1729,7 +1744,7 @@ struct RobotSum8 {
       const int t = min(tb + (int)threadIdx.x + u * RBLOCK, t1 - 1);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const double2 x = ldpart<SC>(part + (size_t)t * 8 + 2 * k);
+        const double2 x = ldpart<SC>(part, (size_t)t * 8 + 2 * k);
         a[u][2 * k] = x.x;
         a[u][2 * k + 1] = x.y;
       }
@@ -2219,19 +2234,34 @@ __global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
 // atomics) and loaded sc1; every storing wave drains (s_waitcnt vmcnt(0))
 // before the workgroup barrier behind which one lane arrives. Data written by
 // earlier launches (X, the public table, records, D_i, M^-1) are read plainly.
-// Grid barrier: per-group arrival counters (group = block % 8, one XCD under
-// round-robin placement: speed only), the group's last arriver (told by its
-// add's return) adds to the top counter, whose last arriver publishes the
-// barrier's generation; one lane per workgroup polls it (sc1, s_sleep).
-// Counters are monotonic within the launch and zeroed by k_begin before each
+// Grid barrier (MI355X_MICROARCH.md "Valid forms", the replicated-counter
+// row): every barrier b of the launch has its own counter, kept in GB_REP = 8
+// replicas on lines of their own. A workgroup arrives, after every wave's
+// write-through stores have drained and a workgroup barrier, with ONE wave
+// instruction whose 8 lanes add to the 8 replicas (no-return agent atomics):
+// 1 per arrival, + 0x10000 when it formed a tCG step the next step consumes.
+// One lane per workgroup polls the replica of its XCD (block % 8 under
+// round-robin placement: speed only) with sc1 loads until the count reaches
+// the grid; the high half then says whether any workgroup formed a step. The
+// chain from the last arrival is one atomic landing and one poll (the
+// two-level counter tree with a separate continue word, round 5's first form,
+// was four dependent round trips: 7-9 us per tCG step after the step's
+// stores, profiles/r05/resident/). Counters are zeroed by k_begin before each
 // round. Every spin is bounded (KMX_RES_SPIN ticks of the 100 MHz clock): a
 // workgroup that gives up writes the host-mapped fail word and leaves; the
 // host turns it into an error at the next sync. All workgroups must be
 // resident: set_graph checks the occupancy query and runs a census launch.
 constexpr int GB_STRIDE = 32;                // one 128-B line per word
-constexpr int GB_CNT = 0, GB_TOP = 8, GB_GEN = 9, GB_CONT = 10;
-constexpr int GB_WORDS = 12 * GB_STRIDE;
+constexpr int GB_REP = 8;                    // replicas per barrier counter
+constexpr int GB_BMAX = 64;                  // barriers per launch (tcg_max + 3 <= GB_BMAX: resident_setup)
+constexpr int GB_WORDS = GB_BMAX * GB_REP * GB_STRIDE;
 constexpr unsigned long long KMX_RES_SPIN = 200000000ull;  // 2 s
+
+#ifdef KMX_RES_STAMPS
+constexpr int RES_STAMP_TILES = 2048;
+constexpr int RES_STAMPS = 128;  // per tile: 0..95 the phases (body_round), 96 + 2 b / 97 + 2 b barrier b < 16
+__device__ unsigned long long g_res_stamp[RES_STAMPS * RES_STAMP_TILES];
+#endif
 
 __device__ __forceinline__ unsigned gb_load(unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2247,32 +2277,40 @@ __device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, b
                                           F&& during) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned e = b + 1;
-    unsigned* cw = gb + (GB_CONT + (b & 1)) * GB_STRIDE;
-    if (cont) {
-      __hip_atomic_store(cw, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const unsigned n = gridDim.x, G = n < 8 ? n : 8, g = blockIdx.x & 7, ng = (n - g + 7) / 8;
-    const unsigned old = __hip_atomic_fetch_add(gb + (GB_CNT + g) * GB_STRIDE, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == ng * e) {
-      const unsigned o2 = __hip_atomic_fetch_add(gb + GB_TOP * GB_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (o2 + 1 == G * e) __hip_atomic_store(gb + GB_GEN * GB_STRIDE, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    during();
-    int ok = 1;
-    const unsigned long long t0 = wall_clock64();
-    while (gb_load(gb + GB_GEN * GB_STRIDE) < e) {
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > KMX_RES_SPIN) {
-        ok = 0;
-        __hip_atomic_store(fail, 1u + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
+#ifdef KMX_RES_STAMPS
+  const unsigned long long ts0 = wall_clock64();
+#endif
+  if (threadIdx.x < 64) {
+    const int ln = threadIdx.x;
+    if (b < GB_BMAX && ln < GB_REP)  // one instruction, 8 lanes, one replica each
+      (void)__hip_atomic_fetch_add(gb + (b * GB_REP + ln) * GB_STRIDE, cont ? 0x10001u : 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    if (ln == 0) {
+      during();
+      int ok = b < GB_BMAX;
+      unsigned v = 0;
+      if (ok) {
+        unsigned* pw = gb + (b * GB_REP + (blockIdx.x & (GB_REP - 1))) * GB_STRIDE;
+        const unsigned n = gridDim.x;
+        const unsigned long long t0 = wall_clock64();
+        while (((v = gb_load(pw)) & 0xffffu) < n) {
+          __builtin_amdgcn_s_sleep(1);
+          if (wall_clock64() - t0 > KMX_RES_SPIN) {
+            ok = 0;
+            break;
+          }
+        }
       }
+      if (!ok) __hip_atomic_store(fail, 1u + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      *sflag = ok ? (1 | ((v >> 16) ? 2 : 0)) : 0;
+#ifdef KMX_RES_STAMPS
+      const int tl = blockIdx.x;  // (stamps by launch block; res_stamps.py maps them)
+      if (tl < RES_STAMP_TILES && b < 16) {
+        g_res_stamp[tl * RES_STAMPS + 96 + 2 * b] = ts0;
+        g_res_stamp[tl * RES_STAMPS + 97 + 2 * b] = wall_clock64();
+      }
+#endif
     }
-    *sflag = ok ? (1 | (gb_load(cw) == e ? 2 : 0)) : 0;
   }
   __syncthreads();
   const int f = *sflag;
@@ -2285,7 +2323,6 @@ __device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, b
 
 // write-through row I/O: 16-B buffer loads / stores with the sc1 bit (aux 16)
 // through a descriptor built from a kernel-argument base (wave-uniform)
-typedef unsigned kmx_u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const double* base, long long doubles) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, (int)(doubles * 8), 0x00020000);
 }
@@ -2370,12 +2407,11 @@ struct SmemRes {  // the gathers' layouts at 0 (the largest of k_grad's, k_step'
 // decision, gather, step end; 90 cost start, 91 cost end, 92 final release,
 // 93 exit; 94 tile poses, 95 tile incidences.
 #ifdef KMX_RES_STAMPS
-constexpr int RES_STAMP_TILES = 2048;
-__device__ unsigned long long g_res_stamp[96 * RES_STAMP_TILES];
 #define KMX_RS(i)                                                                                  \
   do {                                                                                             \
     const int i_ = (i);                                                                            \
-    if (threadIdx.x == 0 && L.tile < RES_STAMP_TILES && i_ < 96) g_res_stamp[L.tile * 96 + i_] = wall_clock64(); \
+    if (threadIdx.x == 0 && blockIdx.x < RES_STAMP_TILES && i_ < 96)                               \
+      g_res_stamp[blockIdx.x * RES_STAMPS + i_] = wall_clock64();                                  \
   } while (0)
 #else
 #define KMX_RS(i) do {} while (0)
@@ -2398,23 +2434,35 @@ struct alignas(16) ResShared {
 // order): the tile's records and CSR offsets are in LDS for the whole round,
 // so both chunks' neighbour rows are requested right after the decision — one
 // dependent round trip per tCG step instead of record -> row per chunk.
-// acc = the off-diagonal part of (Q V) for the lane's row; false: pre() said
-// the robot does not step (nothing gathered).
-template <int R, int RW, int W, typename Pre>
+// acc = the off-diagonal part of (Q V) for the lane's row; false: sync() or
+// pre() said the robot does not step (nothing gathered). sync() is the step's
+// grid barrier (it also issues the robot sums' loads), pre() waits for the
+// sums and takes the decision. EARLY: the neighbour rows are requested between
+// the two, so the decision's latency hides behind the rows' (a robot that
+// stops at the decision has loaded its rows for nothing) — where the
+// registers allow it: the 4-wave form (one wave per SIMD); the 5-wave form
+// (two waves on one SIMD, 256 VGPRs) spilled 70 -> 247 VGPRs with it.
+template <int R, int RW, int W, bool EARLY, typename Sync, typename Pre>
 __device__ __forceinline__ bool res_gather(const Lane& L, const double* recs, const int* sptr, const WtRows<R>& src,
-                                           double acc[4], double* Cs, Pre&& pre) {
+                                           double acc[4], double* Cs, Sync&& sync, Pre&& pre) {
   using RC = Rec<RW>;
   constexpr int CH = SmemH<R, W>::CH;
   constexpr int OI = RW == 10 ? 9 : 14;  // the {other, edge | tail} word of a record
   const int tid = threadIdx.x, n = L.n, pl = L.pose - L.p0;
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  if (!pre()) return false;
+  if (!sync()) return false;
+  if constexpr (!EARLY) {
+    if (!pre()) return false;
+  }
   const int lt = min(tid, CH - 1);
   auto other = [&](int k) { return unpack_int2(recs[(size_t)RW * max(min(k, n - 1), 0) + OI]).x; };
   double2 v0[2 * R], v1[2 * R];
   const bool two = n > CH;  // uniform
   src.nbr(other(lt), v0);
   if (two) src.nbr(other(CH + lt), v1);
+  if constexpr (EARLY) {
+    if (!pre()) return false;
+  }
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     if (c == 1 && !two) break;
@@ -2483,9 +2531,9 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
   const Lane L = lane_map<R>(d);
   KMX_RS(0);
 #ifdef KMX_RES_STAMPS
-  if (threadIdx.x == 0 && L.tile < RES_STAMP_TILES) {
-    g_res_stamp[L.tile * 96 + 94] = L.np;
-    g_res_stamp[L.tile * 96 + 95] = L.n;
+  if (threadIdx.x == 0 && blockIdx.x < RES_STAMP_TILES) {
+    g_res_stamp[blockIdx.x * RES_STAMPS + 94] = L.np;
+    g_res_stamp[blockIdx.x * RES_STAMPS + 95] = L.n;
   }
 #endif
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
@@ -2601,15 +2649,28 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
   for (int jl = 0;; ++jl) {
     bool go = false;
     double coef = 0.0, al = 0.0, be = 0.0;
-    auto decide = [&]() -> bool {
+    RobotSum<3, 2, true> rg;  // (<= 512 tiles per robot: one pass)
+    RobotSum8<2, true> rf;
+    const double* pf_in = d.part_f + (size_t)((k & 1) * d.ntiles) * 8;
+    constexpr bool EARLY = W == 4;  // res_gather: the rows requested before the decision
+    auto sync = [&]() -> bool {
       KMX_RS(4 + 5 * jl);
       if (!grid_sync(gb, b++, formed, &any, fail, &sflag, apply_pending)) return false;
       KMX_RS(5 + 5 * jl);
       if (!any) return false;
       if (!formed) return false;  // not in tCG (skipped, idle, or stopped earlier)
+      if constexpr (EARLY) {
+        if (jl == 0) rg.issue(d.part, NPART, L.rt0, L.rt1);
+        else rf.issue(pf_in, L.rt0, L.rt1);
+      }
+      return true;
+    };
+    auto decide = [&]() -> bool {
+      if constexpr (!EARLY) {
+        if (jl == 0) rg.issue(d.part, NPART, L.rt0, L.rt1);
+        else rf.issue(pf_in, L.rt0, L.rt1);
+      }
       if (jl == 0) {
-        RobotSum<3, 2, true> rg;
-        rg.issue(d.part, NPART, L.rt0, L.rt1);
         double t4[NPART];
         rg.finish(d.part, NPART, rl, t4);
         go = !(sqrt(t4[1]) < d.p.gn_tol);  // control_core's RED_GRAD test (RTR: the tCG starts)
@@ -2619,9 +2680,6 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
         }
       } else {
         double tot[8];
-        RobotSum8<2, true> rf;  // (<= 512 tiles per robot: RobotSum8<4>'s order in one pass)
-        const double* pf_in = d.part_f + (size_t)((k & 1) * d.ntiles) * 8;
-        rf.issue(pf_in, L.rt0, L.rt1);
         rf.finish(pf_in, rl, tot);
         const double zr = tot[1];
         const HessStep hx = hess_step(zr, cs.e_Pe, cs.e_Pd, cs.d_Pd, cs.Delta, tot[0]);
@@ -2643,7 +2701,7 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     };
     double H[4];
     WtRows<R> src{jl == 0 ? rz : ((k & 1) ? rw1 : rw0)};
-    res_gather<R, RW, W>(L, recs, sptr, src, H, reinterpret_cast<double*>(smem), decide);
+    res_gather<R, RW, W, EARLY>(L, recs, sptr, src, H, reinterpret_cast<double*>(smem), sync, decide);
     if (sflag == 0) return;  // a barrier gave up (the fail word is set)
     KMX_RS(7 + 5 * jl);
     if (!any) break;
@@ -2947,8 +3005,8 @@ __global__ void k_begin(Dev d, const unsigned char* active, int mode, int R_) {
   const bool fire = d.p.robust && ((mode & BEGIN_FORCE_GNC) ? true : gnc_should_update(d));
   const double mu = d.gnc->mu;
   if (blockIdx.x == 0) {
-    if (d.gbar)  // the resident round's barrier counters start every round at zero
-      for (int i = threadIdx.x; i < GB_WORDS; i += blockDim.x) d.gbar[i] = 0u;
+    if (d.gbar)  // the resident round's barrier counters start every round at zero (word 0 of each line)
+      for (int i = threadIdx.x; i < GB_BMAX * GB_REP; i += blockDim.x) d.gbar[i * GB_STRIDE] = 0u;
     if (mode & BEGIN_ROUND)
       for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
     if (threadIdx.x == 0) {
@@ -3809,6 +3867,10 @@ int resident_setup_t(kmx_pgo* h) {
   h->res_on = false;
   if (h->P.method != KMX_METHOD_RTR) { h->res_reason = "RGD method"; return 0; }
   if (h->P.rtr_iterations != 1) { h->res_reason = "rtr_iterations != 1"; return 0; }
+  if (h->P.tcg_max_iterations + 3 > GB_BMAX) {  // a barrier per tCG pass, the gradient's and the cost's
+    h->res_reason = "tcg_max_iterations > " + std::to_string(GB_BMAX - 3);
+    return 0;
+  }
   if (h->max_tile_inc > 2 * h->res_w * (64 / R) * R) {
     h->res_reason = "a tile holds more than two gather chunks (tile_incidences " +
                     std::to_string(h->P.tile_incidences) + ")";
@@ -5234,7 +5296,7 @@ extern "C" int kmx_pgo_debug_step_stamps(uint64_t* out, int64_t n) {
   KMX_GUARD_BEGIN
 #ifdef KMX_RES_STAMPS
   KMX_CHECK(out && n >= 0, KMX_EINVAL, "null buffer");
-  const int64_t m = std::min<int64_t>(n, 96 * (int64_t)RES_STAMP_TILES);
+  const int64_t m = std::min<int64_t>(n, RES_STAMPS * (int64_t)RES_STAMP_TILES);
   KMX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_stamp), sizeof(uint64_t) * m, 0, hipMemcpyDeviceToHost));
   return KMX_OK;
 #endif

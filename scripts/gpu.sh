@@ -2,7 +2,7 @@
 # Usage (from gpurun):  bash scripts/gpu.sh TAG STEP [STEP ...]
 # Steps, each under its own time limit, stopping at the first failure:
 #   tests        pytest -m gpu (whole suite)          -> TAG/pytest_gpu.log
-#   tests:EXPR   pytest -m gpu -k EXPR                 -> TAG/pytest_k.log
+#   tests:EXPR   pytest -m gpu -k EXPR (commas = spaces) -> TAG/pytest_k<n>.log
 #   smoke        __graft_entry__.smoke()               -> TAG/smoke.log
 #   bench        python bench.py (defaults)            -> TAG/default.json
 #   bench:ARGS   python bench.py ARGS (commas = spaces)-> TAG/bench_<n>.json
@@ -24,7 +24,8 @@ for step in "$@"; do
         > "$O/pytest_gpu.log" 2>&1 || { echo "gpu suite failed"; tail -40 "$O/pytest_gpu.log"; exit 1; }
       tail -2 "$O/pytest_gpu.log" ;;
     tests:*)
-      timeout -k 10 900 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "${step#tests:}" \
+      kx=${step#tests:}
+      timeout -k 10 900 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu -k "${kx//,/ }" \
         > "$O/pytest_k$n.log" 2>&1 || { echo "gpu tests failed"; tail -40 "$O/pytest_k$n.log"; exit 1; }
       tail -2 "$O/pytest_k$n.log" ;;
     smoke)

@@ -44,13 +44,14 @@ for a in range(lo, hi):
 print("resident:", s.resident_info())
 s.iterate_async(rounds, refresh_local=True)
 s.sync()
-n = 96 * 2048
+n = 128 * 2048
 buf = np.zeros(n, np.uint64)
 abi.check(s.L.kmx_pgo_debug_step_stamps(buf.ctypes.data_as(C.c_void_p), n), "stamps")
-st = buf.reshape(-1, 96).astype(np.int64)
+st = buf.reshape(-1, 128).astype(np.int64)
 st = st[st[:, 0] > 0]
 t0 = st[:, 0].min()
-T = np.where(st[:, :94] > 0, (st[:, :94] - t0) * 0.01, np.nan)  # us
+T = np.where(st > 0, (st - t0) * 0.01, np.nan)  # us
+T[:, 94:96] = np.nan
 print(f"{len(st)} workgroups; poses/tile median {np.median(st[:, 94]):.0f}, incidences/tile median "
       f"{np.median(st[:, 95]):.0f} (max {st[:, 95].max()})")
 def med(i):
@@ -70,6 +71,12 @@ for jl in range(17):
     body = np.nanmedian(T[:, b + 4] - T[:, b + 3])
     print(f"  pass {jl:2d}: {row}")
     print(f"           wait {wait:6.2f}  decide {dec:6.2f}  gather {gat:6.2f}  body {body:6.2f} us (medians)")
+    if jl < 16 and not np.all(st[:, 96 + 2 * jl] == 0):
+        drn = np.nanmedian(T[:, 96 + 2 * jl] - T[:, b])
+        last = np.nanmax(T[:, 96 + 2 * jl])
+        mt = np.nanmedian(T[:, 97 + 2 * jl])
+        print(f"           barrier: drain {drn:6.2f}, last drained arrival {last:7.2f}, poll matched {mt:7.2f} "
+              f"(+{mt - last:5.2f} after the last arrival)")
 for i, nm in [(90, "cost start"), (91, "cost end"), (92, "final release"), (93, "exit")]:
     print(f"  {nm:13s} median {med(i)[0]:7.2f}  max {med(i)[1]:7.2f} us")
 s.close()
