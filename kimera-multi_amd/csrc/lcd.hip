@@ -733,6 +733,63 @@ __device__ __forceinline__ double rdlane(double v, int src) {  // src wave-unifo
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// refit_3d3d by the whole wave (every lane gets the result): the same sums in
+// the same order — the lanes fetch a block of 64 pairs at once, then every
+// lane adds the block's inliers in pair order from readlane broadcasts — so
+// the result is the serial form's bit for bit, without its chain of
+// dependent global loads on one lane (the call-for-call recoverPose spent
+// most of its time there). fetch(j, pq, pm): lane-local, pair j < n.
+template <typename Fetch>
+__device__ void refit_3d3d_wave(int n, int lane, Fetch&& fetch, double R[9], double t[3]) {
+  double cq[3] = {0.0, 0.0, 0.0}, cm[3] = {0.0, 0.0, 0.0};
+  int c = 0;
+  for (int j0 = 0; j0 < n; j0 += 64) {
+    double pq[3] = {0.0, 0.0, 0.0}, pm[3] = {0.0, 0.0, 0.0};
+    const bool in = j0 + lane < n && fetch(j0 + lane, pq, pm);
+    unsigned long long bm = __ballot(in);
+    c += __popcll(bm);
+    while (bm) {
+      const int jj = __builtin_ctzll(bm);
+      bm &= bm - 1;
+      for (int k = 0; k < 3; ++k) {
+        cq[k] += rdlane(pq[k], jj);
+        cm[k] += rdlane(pm[k], jj);
+      }
+    }
+  }
+  for (int k = 0; k < 3; ++k) {
+    cq[k] /= (double)c;
+    cm[k] /= (double)c;
+  }
+  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j0 = 0; j0 < n; j0 += 64) {
+    double pq[3] = {0.0, 0.0, 0.0}, pm[3] = {0.0, 0.0, 0.0};
+    const bool in = j0 + lane < n && fetch(j0 + lane, pq, pm);
+    unsigned long long bm = __ballot(in);
+    while (bm) {
+      const int jj = __builtin_ctzll(bm);
+      bm &= bm - 1;
+      double dq[3], dm[3];
+      for (int k = 0; k < 3; ++k) {
+        dq[k] = rdlane(pq[k], jj) - cq[k];
+        dm[k] = rdlane(pm[k], jj) - cm[k];
+      }
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) H[a * 3 + b] += dm[a] * dq[b];
+    }
+  }
+  double U[9], sv[3], V[9];
+  svd3(H, U, sv, V);
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  if (det3(R) < 0.0) {
+    for (int a = 0; a < 3; ++a) V[a * 3 + 2] = -V[a * 3 + 2];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+  }
+  for (int a = 0; a < 3; ++a) t[a] = cq[a] - (R[a * 3 + 0] * cm[0] + R[a * 3 + 1] * cm[1] + R[a * 3 + 2] * cm[2]);
+}
 __device__ __forceinline__ double wave_fmax(double v) {  // exact in any order
   for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
   return v;
@@ -1975,6 +2032,7 @@ __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* sta
 // kernel and the spread form's k_rs_finish): the best model's inliers (and
 // mask), then the 1-point 3D-3D recovery (and refine_pose), or the hand-over
 // to k_recover. w.bestm holds the best model when `have`.
+template <bool WAVE>
 __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double* F2, const double* points, int N,
                                             int q, int m, const int2* pl, int K, const RsParams& P,
                                             kmx_lcd_result* R_, unsigned char* mask, int have, int iterations,
@@ -2076,6 +2134,7 @@ __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double
   }
   __threadfence_block();
   wsync();
+  if constexpr (!WAVE) {  // one lane's serial loops (the work-queue kernel: other waves fill the CU meanwhile)
   const double thr2 = P.thr3d * P.thr3d;
   int my_best = -1, my_cnt = 0;
   for (int i = lane; i < n3; i += RS_BLOCK) {
@@ -2137,7 +2196,103 @@ __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double
     }
     *R_ = r;
   }
+  } else {  // the same sums by the whole wave (the spread form's latency path: k_rs_finish)
+  // (KMX_RS_PROF=3, diagnostic: g_phase[11..13] = count, final pass, refit; [14] n3, [15] calls)
+  const bool prof = P.prof == 3;
+  unsigned long long t_prev = prof ? wall_clock64() : 0;
+  if (prof && lane == 0) {
+    atomicAdd(&g_phase[15], 1ull);
+    atomicAdd(&g_phase[14], (unsigned long long)n3);
+  }
+  const double thr2 = P.thr3d * P.thr3d;
+  // the largest consistent set: lane i counts the valid j within thr3d of T_i,
+  // the block of T_j broadcast by readlane (uniform j: no per-lane loads in
+  // the inner loop); counts are integers, so their order does not matter
+  int my_best = -1, my_cnt = 0;
+  for (int i0 = 0; i0 < n3; i0 += RS_BLOCK) {
+    const int i = i0 + lane;
+    double ti[3] = {0.0, 0.0, 0.0};
+    const bool vi = i < n3 && valid[i];
+    if (i < n3)
+      for (int k = 0; k < 3; ++k) ti[k] = T[3 * i + k];
+    int cc = 0;
+    for (int j0 = 0; j0 < n3; j0 += RS_BLOCK) {
+      const int j = j0 + lane;
+      double tj[3] = {0.0, 0.0, 0.0};
+      const bool vj = j < n3 && valid[j];
+      if (j < n3)
+        for (int k = 0; k < 3; ++k) tj[k] = T[3 * j + k];
+      unsigned long long vm = __ballot(vj);
+      while (vm) {
+        const int jj = __builtin_ctzll(vm);
+        vm &= vm - 1;
+        const double dx = rdlane(tj[0], jj) - ti[0], dy = rdlane(tj[1], jj) - ti[1], dz = rdlane(tj[2], jj) - ti[2];
+        if (dx * dx + dy * dy + dz * dz < thr2) ++cc;
+      }
+    }
+    if (vi && cc > my_cnt) { my_cnt = cc; my_best = i; }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const int oc = __shfl_xor(my_cnt, off, 64);
+    const int ob = __shfl_xor(my_best, off, 64);
+    if (oc > my_cnt || (oc == my_cnt && ob >= 0 && (my_best < 0 || ob < my_best))) {
+      my_cnt = oc;
+      my_best = ob;
+    }
+  }
+  const int best = my_best;  // the same in every lane
+  KMX_PT(11);
+  if (best >= 0) {
+    // the inliers of the best translation: in pair order, the sum of their
+    // T_j (added from readlane broadcasts in j order, the serial sum's order)
+    const double tb[3] = {T[3 * best], T[3 * best + 1], T[3 * best + 2]};
+    auto within = [&](int j, double tj[3]) {
+      for (int k = 0; k < 3; ++k) tj[k] = T[3 * j + k];
+      if (!valid[j]) return false;
+      const double dx = tj[0] - tb[0], dy = tj[1] - tb[1], dz = tj[2] - tb[2];
+      return dx * dx + dy * dy + dz * dz < thr2;
+    };
+    int cc = 0;
+    double s3[3] = {0.0, 0.0, 0.0};
+    for (int j0 = 0; j0 < n3; j0 += RS_BLOCK) {
+      const int j = j0 + lane;
+      double tj[3] = {0.0, 0.0, 0.0};
+      const bool in = j < n3 && within(j, tj);
+      if (j < n3 && mask) mask[idx[j]] = in ? 3 : 1;  // idx lists 2D-2D inliers (mask 1): | 2
+      unsigned long long im = __ballot(in);
+      cc += __popcll(im);
+      while (im) {
+        const int jj = __builtin_ctzll(im);
+        im &= im - 1;
+        for (int k = 0; k < 3; ++k) s3[k] += rdlane(tj[k], jj);
+      }
+    }
+    for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = s3[i] / (double)cc;
+    r.stereo_inliers = cc;
+    r.accepted = (cc >= P.min3d) ? 1 : 0;
+    KMX_PT(12);
+    if (r.accepted && P.refine) {  // the inliers again: valid and within thr3d of the best translation
+      refit_3d3d_wave(
+          n3, lane,
+          [&](int j, double* pq, double* pm) {
+            double tj[3];
+            if (!within(j, tj)) return false;
+            const int2 pr = pl[idx[j]];
+            const double* a = points + ((size_t)q * N + pr.x) * 3;
+            const double* b = points + ((size_t)m * N + pr.y) * 3;
+            for (int k = 0; k < 3; ++k) { pq[k] = a[k]; pm[k] = b[k]; }
+            return true;
+          },
+          r.T_query_match, r.T_query_match + 9);
+      KMX_PT(13);
+    }
+  } else {
+    for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = 0.0;
+  }
+  if (lane == 0) *R_ = r;
+  }
 }
+
 // One candidate's 2D-2D RANSAC and 3D-3D recovery by the calling wave; F1 is
 // the wave's global scratch (6 N + STASH doubles).
 template <bool STEW, typename SB>
@@ -2263,7 +2418,7 @@ __device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, doubl
     }
   }
   if (P.hyps && lane == 0) P.hyps[c] = iterations + skipped;
-  ransac_tail(c, w, F1, F2, points, N, q, m, pl, K, P, R_, mask, have, iterations, lane);
+  ransac_tail<false>(c, w, F1, F2, points, N, q, m, pl, K, P, R_, mask, have, iterations, lane);
 }
 
 
@@ -2372,14 +2527,13 @@ template <bool STEW>
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, int N, const int* cq, const int* cm,
                                                       const int2* pairs, const int* Kin, const short* table,
                                                       RsParams P, const RsState* st, HypOut* hout, int pa, int pb,
-                                                      int G, double* fbuf) {
+                                                      int G, int per, double* fbuf) {
   __shared__ CoopWS w;
   __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;
   const int c = blockIdx.x / G, g = blockIdx.x % G;
   const int lane = fresh_lane(threadIdx.x);
   const int K = Kin[c];
   if (K < 5 || st[c].done) return;
-  constexpr int per = STEW ? SG : SPREAD_PER_NISTER;
   const int p_lo = pa + g * per, p_hi = min(min(p_lo + per, pb), P.pmax);
   if (p_lo >= p_hi) return;
   double* F1 = fbuf + (size_t)blockIdx.x * (6 * N + STASH);
@@ -2425,50 +2579,83 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, in
 }
 
 // The serial loop's control (ransac_candidate: the stop test, then account)
-// over the computed hypotheses [p_next, pb), one thread per candidate.
-__global__ void k_rs_replay(const int* Kin, RsParams P, RsState* st, const HypOut* hout, int pb, int n,
-                            unsigned* more) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// over the computed hypotheses [p_next, pb), one wave per candidate: the
+// lanes load 64 hypotheses' (ok, count) at once and every lane runs the
+// control over them in order from readlane broadcasts (the same operations
+// on the same values as one thread: the same state), so the serial chain has
+// no dependent global load per hypothesis (one thread per candidate spent
+// ~0.3 us per hypothesis waiting for it: 136 us for a 444-hypothesis range).
+// The best model's 12 values are copied once, after the scan.
+__global__ __launch_bounds__(64) void k_rs_replay(const int* Kin, RsParams P, RsState* st, const HypOut* hout,
+                                                  int pb, int n, unsigned* more) {
+  const int c = blockIdx.x, lane = threadIdx.x;
   if (c >= n) return;
-  RsState s = st[c];
-  if (s.done) return;
+  RsState* sp = st + c;
+  if (sp->done) return;
   const int K = Kin[c];
   if (K < 5) {
-    s.done = 1;
-    st[c] = s;
+    if (lane == 0) sp->done = 1;
     return;
   }
+  // the control state in scalars (wave-uniform)
+  double kk = sp->kk;
+  int iterations = sp->iterations, skipped = sp->skipped, best_cnt = sp->best_cnt, have = sp->have;
+  int p_next = sp->p_next, done = 0;
   const int max_skip = P.max_iter * 10;
   const HypOut* ho = hout + (size_t)c * P.pmax;
-  for (;;) {
-    if (s.p_next >= P.pmax || !(s.iterations < s.kk && s.skipped < max_skip)) {
-      s.done = 1;
-      break;
+  int bestp = -1;  // the hypothesis whose model becomes the best
+  for (bool run = true; run;) {
+    const int p0 = p_next, p = p0 + lane;
+    int okl = 0, cntl = 0;
+    if (p < pb && p < P.pmax) {
+      okl = ho[p].ok;
+      cntl = ho[p].cnt;
     }
-    if (s.p_next >= pb) break;  // past the computed hypotheses: the next pass
-    const HypOut& h = ho[s.p_next++];
-    if (!h.ok) {
-      ++s.skipped;
-      continue;
-    }
-    if (h.cnt > s.best_cnt) {
-      s.best_cnt = h.cnt;
-      for (int i = 0; i < 12; ++i) s.best[i] = h.m[i];
-      s.have = 1;
-      const double wr = (double)h.cnt / (double)K;
-      double p_no = 1.0 - pow(wr, 5.0);
-      p_no = fmax(DBL_EPSILON, p_no);
-      p_no = fmin(1.0 - DBL_EPSILON, p_no);
-      s.kk = log(1.0 - P.prob) / log(p_no);
-    }
-    ++s.iterations;
-    if (s.iterations > P.max_iter) {
-      s.done = 1;
-      break;
+    for (int jj = 0; jj < 64; ++jj) {
+      if (p_next >= P.pmax || !(iterations < kk && skipped < max_skip)) {
+        done = 1;
+        run = false;
+        break;
+      }
+      if (p_next >= pb) {  // past the computed hypotheses: the next pass
+        run = false;
+        break;
+      }
+      const int ok = __builtin_amdgcn_readlane(okl, jj), cnt = __builtin_amdgcn_readlane(cntl, jj);
+      ++p_next;
+      if (!ok) {
+        ++skipped;
+        continue;
+      }
+      if (cnt > best_cnt) {
+        best_cnt = cnt;
+        bestp = p0 + jj;
+        have = 1;
+        const double wr = (double)cnt / (double)K;
+        double p_no = 1.0 - pow(wr, 5.0);
+        p_no = fmax(DBL_EPSILON, p_no);
+        p_no = fmin(1.0 - DBL_EPSILON, p_no);
+        kk = log(1.0 - P.prob) / log(p_no);
+      }
+      ++iterations;
+      if (iterations > P.max_iter) {
+        done = 1;
+        run = false;
+        break;
+      }
     }
   }
-  st[c] = s;
-  if (!s.done) atomicOr(more, 1u);
+  if (lane < 12 && bestp >= 0) sp->best[lane] = ho[bestp].m[lane];
+  if (lane == 0) {
+    sp->kk = kk;
+    sp->iterations = iterations;
+    sp->skipped = skipped;
+    sp->best_cnt = best_cnt;
+    sp->have = have;
+    sp->p_next = p_next;
+    sp->done = done;
+    if (!done) atomicOr(more, 1u);
+  }
 }
 
 // Each candidate's result from its replayed loop (one wave per candidate).
@@ -2500,7 +2687,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_finish(const double* bearings, 
   if (lane < 12) w.bestm[lane] = s.best[lane];
   __threadfence_block();
   wsync();
-  ransac_tail(c, w, F1, F1 + 3 * N, points, N, q, m, pl, K, P, R_, mask, s.have, s.iterations, lane);
+  ransac_tail<true>(c, w, F1, F1 + 3 * N, points, N, q, m, pl, K, P, R_, mask, s.have, s.iterations, lane);
 }
 
 // Arun 3-point model (oracle arun_model): centroids, H = sum dm dq^T, Kabsch
@@ -3225,20 +3412,24 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks) {
   if (!h->h_more)
     KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_more), sizeof(unsigned), hipHostMallocDefault));
   const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
-  const int per = stew ? SG : SPREAD_PER_NISTER;
+  const int per_max = stew ? SG : SPREAD_PER_NISTER;
   hipLaunchKernelGGL(k_rs_init, dim3((std::max(n, h->more_cap) + 63) / 64), dim3(64), 0, st, h->d_st, n, stages,
                      h->d_more, h->more_cap);
   int pa = 0;
   int range = 66;  // covers a true loop closure's loop (~30 iterations) in one pass
-  for (int it = 0; pa < h->pmax; ++it) {
+  for (int it = 0; pa < h->pmax && (stages & KMX_LCD_STAGE_2D2D); ++it) {  // (recovery alone: no hypotheses)
+    // hypotheses per wave: as few as the launch's waves allow (one wave
+    // works through its hypotheses one after another; the batch of SG
+    // Stewenius hypotheses per wave only pays where waves are short)
+    const int per = std::max(1, std::min(per_max, (int)(((int64_t)n * range + SPREAD_WAVES - 1) / SPREAD_WAVES)));
     int G = (range + per - 1) / per;
     G = std::max(1, std::min(G, SPREAD_WAVES / n));
     const int pb = std::min(pa + G * per, h->pmax);
     hipLaunchKernelGGL(stew ? k_rs_hyps<true> : k_rs_hyps<false>, dim3(n * G), dim3(RS_BLOCK), 0, st,
                        (const double*)h->d_bear, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
                        (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp,
-                       (const RsState*)h->d_st, h->d_hout, pa, pb, G, h->d_sfbuf);
-    hipLaunchKernelGGL(k_rs_replay, dim3((n + 63) / 64), dim3(64), 0, st, (const int*)h->d_K, rp, h->d_st,
+                       (const RsState*)h->d_st, h->d_hout, pa, pb, G, per, h->d_sfbuf);
+    hipLaunchKernelGGL(k_rs_replay, dim3(n), dim3(64), 0, st, (const int*)h->d_K, rp, h->d_st,
                        (const HypOut*)h->d_hout, pb, n, h->d_more + it);
     KMX_HIP(hipMemcpyAsync(h->h_more, h->d_more + it, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     KMX_HIP(hipStreamSynchronize(st));

@@ -2666,13 +2666,15 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
       return true;
     };
     auto decide = [&]() -> bool {
-      if constexpr (!EARLY) {
-        if (jl == 0) rg.issue(d.part, NPART, L.rt0, L.rt1);
-        else rf.issue(pf_in, L.rt0, L.rt1);
-      }
       if (jl == 0) {
         double t4[NPART];
-        rg.finish(d.part, NPART, rl, t4);
+        if constexpr (EARLY) {
+          rg.finish(d.part, NPART, rl, t4);
+        } else {  // (the sums' registers scoped to this branch: the 5-wave form's VGPR budget)
+          RobotSum<3, 2, true> rg2;
+          rg2.issue(d.part, NPART, L.rt0, L.rt1);
+          rg2.finish(d.part, NPART, rl, t4);
+        }
         go = !(sqrt(t4[1]) < d.p.gn_tol);  // control_core's RED_GRAD test (RTR: the tCG starts)
         if (threadIdx.x == 0) {
           pend = 1;
@@ -2680,7 +2682,13 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
         }
       } else {
         double tot[8];
-        rf.finish(pf_in, rl, tot);
+        if constexpr (EARLY) {
+          rf.finish(pf_in, rl, tot);
+        } else {
+          RobotSum8<2, true> rf2;
+          rf2.issue(pf_in, L.rt0, L.rt1);
+          rf2.finish(pf_in, rl, tot);
+        }
         const double zr = tot[1];
         const HessStep hx = hess_step(zr, cs.e_Pe, cs.e_Pd, cs.d_Pd, cs.Delta, tot[0]);
         double rrn, zrn;

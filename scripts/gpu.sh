@@ -7,6 +7,7 @@
 #   bench        python bench.py (defaults)            -> TAG/default.json
 #   bench:ARGS   python bench.py ARGS (commas = spaces)-> TAG/bench_<n>.json
 #   prof         rocprofv3 --kernel-trace --stats of the default bench -> TAG/prof/
+#   prof:ARGS    the same of bench.py ARGS (commas = spaces) -> TAG/prof_<n>/
 #   py:SCRIPT    python SCRIPT (commas = spaces)       -> TAG/py_<n>.log
 #   env:VAR=VAL:ARGS  bench.py ARGS under VAR=VAL       -> TAG/bench_<n>.json
 set -o pipefail
@@ -52,6 +53,13 @@ for step in "$@"; do
         > "$O/prof/bench.json" 2> "$O/prof/rocprof.err" || { echo "prof failed"; tail -20 "$O/prof/rocprof.err"; exit 1; }
       find "$O/prof" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$O/kernel_stats.csv"
       head -12 "$O/kernel_stats.csv" | cut -c1-160 ;;
+    prof:*)
+      args=${step#prof:}
+      mkdir -p "$O/prof_$n"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_$n" -o run --output-format csv -- python3 bench.py ${args//,/ } \
+        > "$O/prof_$n/bench.json" 2> "$O/prof_$n/rocprof.err" || { echo "prof $args failed"; tail -20 "$O/prof_$n/rocprof.err"; exit 1; }
+      find "$O/prof_$n" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$O/kernel_stats_$n.csv"
+      head -12 "$O/kernel_stats_$n.csv" | cut -c1-160 ;;
     py:*)
       args=${step#py:}
       timeout -k 10 600 python -u ${args//,/ } > "$O/py_$n.log" 2>&1 \

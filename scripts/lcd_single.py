@@ -41,3 +41,13 @@ for rep in range(3):
     print(f"pass {rep}: match {med[0]:.3f} ms, 2d2d {med[1]:.3f} ms, recover {med[2]:.3f} ms, "
           f"chain {np.median(t.sum(1)) * 1e3:.3f} ms")
 det.close()
+if os.environ.get("KMX_RS_PROF") == "3":  # the recovery tail's phase timers (lcd.hip ransac_tail<true>)
+    import ctypes as C
+    from kmx import abi
+    fn = abi.lib().kmx_lcd_debug_phase_times
+    fn.argtypes = [C.POINTER(C.c_ulonglong)]
+    buf = (C.c_ulonglong * 16)()
+    fn(buf)
+    calls = max(buf[15], 1)
+    print(f"recovery tail: {buf[15]} calls, n3 mean {buf[14] / calls:.1f}; per call: count {buf[11] / 100 / calls:.1f} us, "
+          f"final pass {buf[12] / 100 / calls:.1f} us, refit {buf[13] / 100 / calls:.1f} us")
