@@ -47,10 +47,13 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "kimera-multi_amd"))
 
 PEAK_HBM = 8.0e12      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-# tCG form "auto": the resident round (one persistent launch per round) for
-# shards up to this many poses per GPU, ROPTLIB's launched tCG above (the
-# resident round needs one 60-pose tile per CU at r = 5: 256 x 60 = 15,360)
-RESIDENT_MAX_POSES = 15_000
+# tCG form "auto": ROPTLIB's launched tCG at every shard size. The resident
+# round (one persistent launch per round; it fits shards up to 256 x 60 =
+# 15,360 poses at r = 5) measured level with it at the configs[3] N = 8 shard,
+# not faster (same box: 170.9 vs 169.4 us per round, 203.7 vs 198.3 with the
+# in-round exchange), so it stays opt-in
+# (--tcg-form resident); set this to 15_000 to pick it for small shards
+RESIDENT_MAX_POSES = 0
 PEAK_VALU_OPS = 78.6e12  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
 
 
@@ -75,7 +78,7 @@ def parse():
     ap.add_argument("--tcg-form", choices=["auto", "standard", "onesync", "resident"], default="auto",
                     help="tCG form (kmx_pgo_params.tcg_form): ROPTLIB's, the one-sync form launched per step, or "
                          "the one-sync form as one persistent launch per round; auto = resident for shards of "
-                         f"<= {RESIDENT_MAX_POSES} poses per GPU (the strong-scaling ranks), else standard")
+                         f"<= {RESIDENT_MAX_POSES} poses per GPU (0: never), else standard")
     ap.add_argument("--lcd-frames", type=int, default=50_000)
     ap.add_argument("--lcd-steps", type=int, default=8,
                     help="back-to-back LCD verification calls timed (a call's kNN2 overlaps the previous call's "

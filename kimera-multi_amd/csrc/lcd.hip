@@ -733,63 +733,6 @@ __device__ __forceinline__ double rdlane(double v, int src) {  // src wave-unifo
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-// refit_3d3d by the whole wave (every lane gets the result): the same sums in
-// the same order — the lanes fetch a block of 64 pairs at once, then every
-// lane adds the block's inliers in pair order from readlane broadcasts — so
-// the result is the serial form's bit for bit, without its chain of
-// dependent global loads on one lane (the call-for-call recoverPose spent
-// most of its time there). fetch(j, pq, pm): lane-local, pair j < n.
-template <typename Fetch>
-__device__ void refit_3d3d_wave(int n, int lane, Fetch&& fetch, double R[9], double t[3]) {
-  double cq[3] = {0.0, 0.0, 0.0}, cm[3] = {0.0, 0.0, 0.0};
-  int c = 0;
-  for (int j0 = 0; j0 < n; j0 += 64) {
-    double pq[3] = {0.0, 0.0, 0.0}, pm[3] = {0.0, 0.0, 0.0};
-    const bool in = j0 + lane < n && fetch(j0 + lane, pq, pm);
-    unsigned long long bm = __ballot(in);
-    c += __popcll(bm);
-    while (bm) {
-      const int jj = __builtin_ctzll(bm);
-      bm &= bm - 1;
-      for (int k = 0; k < 3; ++k) {
-        cq[k] += rdlane(pq[k], jj);
-        cm[k] += rdlane(pm[k], jj);
-      }
-    }
-  }
-  for (int k = 0; k < 3; ++k) {
-    cq[k] /= (double)c;
-    cm[k] /= (double)c;
-  }
-  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int j0 = 0; j0 < n; j0 += 64) {
-    double pq[3] = {0.0, 0.0, 0.0}, pm[3] = {0.0, 0.0, 0.0};
-    const bool in = j0 + lane < n && fetch(j0 + lane, pq, pm);
-    unsigned long long bm = __ballot(in);
-    while (bm) {
-      const int jj = __builtin_ctzll(bm);
-      bm &= bm - 1;
-      double dq[3], dm[3];
-      for (int k = 0; k < 3; ++k) {
-        dq[k] = rdlane(pq[k], jj) - cq[k];
-        dm[k] = rdlane(pm[k], jj) - cm[k];
-      }
-      for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b) H[a * 3 + b] += dm[a] * dq[b];
-    }
-  }
-  double U[9], sv[3], V[9];
-  svd3(H, U, sv, V);
-  for (int a = 0; a < 3; ++a)
-    for (int b = 0; b < 3; ++b) R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
-  if (det3(R) < 0.0) {
-    for (int a = 0; a < 3; ++a) V[a * 3 + 2] = -V[a * 3 + 2];
-    for (int a = 0; a < 3; ++a)
-      for (int b = 0; b < 3; ++b)
-        R[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
-  }
-  for (int a = 0; a < 3; ++a) t[a] = cq[a] - (R[a * 3 + 0] * cm[0] + R[a * 3 + 1] * cm[1] + R[a * 3 + 2] * cm[2]);
-}
 __device__ __forceinline__ double wave_fmax(double v) {  // exact in any order
   for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
   return v;
@@ -2032,11 +1975,14 @@ __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* sta
 // kernel and the spread form's k_rs_finish): the best model's inliers (and
 // mask), then the 1-point 3D-3D recovery (and refine_pose), or the hand-over
 // to k_recover. w.bestm holds the best model when `have`.
+// WAVE: the 1-point recovery's loops by the whole wave with its data staged
+// in `lds` (tail_lds_doubles(N) doubles; k_rs_finish's dynamic LDS).
+__host__ __device__ constexpr size_t tail_lds_doubles(int N) { return 3 * ((size_t)N + 4) + ((size_t)N + 15) / 8 + 6 * (size_t)N; }
 template <bool WAVE>
 __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double* F2, const double* points, int N,
                                             int q, int m, const int2* pl, int K, const RsParams& P,
                                             kmx_lcd_result* R_, unsigned char* mask, int have, int iterations,
-                                            int lane) {
+                                            int lane, double* lds = nullptr) {
   const bool st2d = (P.stages & KMX_LCD_STAGE_2D2D) != 0;
   auto pair_error = [&](const double* R, const double* t, int j) {
     const double a[3] = {F1[j], F1[N + j], F1[2 * N + j]}, b[3] = {F2[j], F2[N + j], F2[2 * N + j]};
@@ -2205,31 +2151,46 @@ __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double
     atomicAdd(&g_phase[14], (unsigned long long)n3);
   }
   const double thr2 = P.thr3d * P.thr3d;
+  // T and valid staged in LDS (each lane copies the entries it wrote), then
   // the largest consistent set: lane i counts the valid j within thr3d of T_i,
-  // the block of T_j broadcast by readlane (uniform j: no per-lane loads in
-  // the inner loop); counts are integers, so their order does not matter
+  // every lane reading T_j at the same LDS address (a broadcast), four j per
+  // pass with independent chains (one wave alone on its SIMD: latency, not
+  // issue, bounds the loop); counts are integers, so their order does not
+  // matter
+  double* Tl = lds;                                                              // [N + 4][3]
+  unsigned char* vl = reinterpret_cast<unsigned char*>(lds + 3 * ((size_t)N + 4));  // [N + 4]
+  double* Pc = lds + 3 * ((size_t)N + 4) + ((size_t)N + 15) / 8;                 // [N][6]: compacted inliers
+  for (int k = lane; k < n3; k += RS_BLOCK) {
+    for (int i = 0; i < 3; ++i) Tl[3 * k + i] = T[3 * k + i];
+    vl[k] = valid[k];
+  }
+  for (int k = n3 + lane; k < ((n3 + 3) & ~3); k += RS_BLOCK) {  // the last quad's padding
+    for (int i = 0; i < 3; ++i) Tl[3 * k + i] = 0.0;
+    vl[k] = 0;
+  }
+  wsync();
   int my_best = -1, my_cnt = 0;
   for (int i0 = 0; i0 < n3; i0 += RS_BLOCK) {
     const int i = i0 + lane;
     double ti[3] = {0.0, 0.0, 0.0};
-    const bool vi = i < n3 && valid[i];
+    const bool vi = i < n3 && vl[i];
     if (i < n3)
-      for (int k = 0; k < 3; ++k) ti[k] = T[3 * i + k];
-    int cc = 0;
-    for (int j0 = 0; j0 < n3; j0 += RS_BLOCK) {
-      const int j = j0 + lane;
-      double tj[3] = {0.0, 0.0, 0.0};
-      const bool vj = j < n3 && valid[j];
-      if (j < n3)
-        for (int k = 0; k < 3; ++k) tj[k] = T[3 * j + k];
-      unsigned long long vm = __ballot(vj);
-      while (vm) {
-        const int jj = __builtin_ctzll(vm);
-        vm &= vm - 1;
-        const double dx = rdlane(tj[0], jj) - ti[0], dy = rdlane(tj[1], jj) - ti[1], dz = rdlane(tj[2], jj) - ti[2];
-        if (dx * dx + dy * dy + dz * dz < thr2) ++cc;
+      for (int k = 0; k < 3; ++k) ti[k] = Tl[3 * i + k];
+    int c4[4] = {0, 0, 0, 0};
+    for (int j = 0; j < n3; j += 4) {  // (entries n3 .. n3 + 3 are invalid padding)
+      const unsigned v4 = *reinterpret_cast<const unsigned*>(vl + j);
+      // branch-free (a valid-byte test as a branch serialised the four chains)
+      double d2[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double* t = Tl + 3 * (j + u);
+        const double dx = t[0] - ti[0], dy = t[1] - ti[1], dz = t[2] - ti[2];
+        d2[u] = dx * dx + dy * dy + dz * dz;
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) c4[u] += (int)((v4 >> (8 * u)) & 1u) & (d2[u] < thr2 ? 1 : 0);
     }
+    const int cc = (c4[0] + c4[1]) + (c4[2] + c4[3]);
     if (vi && cc > my_cnt) { my_cnt = cc; my_best = i; }
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -2243,47 +2204,92 @@ __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double
   const int best = my_best;  // the same in every lane
   KMX_PT(11);
   if (best >= 0) {
-    // the inliers of the best translation: in pair order, the sum of their
-    // T_j (added from readlane broadcasts in j order, the serial sum's order)
-    const double tb[3] = {T[3 * best], T[3 * best + 1], T[3 * best + 2]};
-    auto within = [&](int j, double tj[3]) {
-      for (int k = 0; k < 3; ++k) tj[k] = T[3 * j + k];
-      if (!valid[j]) return false;
-      const double dx = tj[0] - tb[0], dy = tj[1] - tb[1], dz = tj[2] - tb[2];
-      return dx * dx + dy * dy + dz * dz < thr2;
-    };
+    // the inliers of the best translation, compacted in pair order into Pc
+    // (T_j, and with refine_pose their two points) by ballot prefix sums; the
+    // ordered sums then run over contiguous LDS (every lane the same adds in
+    // the serial order, four loads ahead)
+    const double tb[3] = {Tl[3 * best], Tl[3 * best + 1], Tl[3 * best + 2]};
+    const bool refine = P.refine != 0;
     int cc = 0;
-    double s3[3] = {0.0, 0.0, 0.0};
     for (int j0 = 0; j0 < n3; j0 += RS_BLOCK) {
       const int j = j0 + lane;
+      bool in = false;
       double tj[3] = {0.0, 0.0, 0.0};
-      const bool in = j < n3 && within(j, tj);
+      if (j < n3 && vl[j]) {
+        for (int k = 0; k < 3; ++k) tj[k] = Tl[3 * j + k];
+        const double dx = tj[0] - tb[0], dy = tj[1] - tb[1], dz = tj[2] - tb[2];
+        in = dx * dx + dy * dy + dz * dz < thr2;
+      }
       if (j < n3 && mask) mask[idx[j]] = in ? 3 : 1;  // idx lists 2D-2D inliers (mask 1): | 2
-      unsigned long long im = __ballot(in);
+      const unsigned long long im = __ballot(in);
+      if (in) {
+        const int pos = cc + __popcll(im & ((1ull << lane) - 1ull));
+        double* o = Pc + 6 * (size_t)pos;
+        if (refine) {
+          const int2 pr = pl[idx[j]];
+          const double* a = points + ((size_t)q * N + pr.x) * 3;
+          const double* b = points + ((size_t)m * N + pr.y) * 3;
+          for (int k = 0; k < 3; ++k) {
+            o[k] = a[k];
+            o[3 + k] = b[k];
+          }
+        } else {
+          for (int k = 0; k < 3; ++k) o[k] = tj[k];
+        }
+      }
       cc += __popcll(im);
-      while (im) {
-        const int jj = __builtin_ctzll(im);
-        im &= im - 1;
-        for (int k = 0; k < 3; ++k) s3[k] += rdlane(tj[k], jj);
+    }
+    wsync();
+    double s3[3] = {0.0, 0.0, 0.0};
+    if (!refine) {
+      for (int k = 0; k < cc; ++k)
+        for (int i = 0; i < 3; ++i) s3[i] += Pc[6 * k + i];
+    } else {  // T_j = p_q - R p_m again from the staged points (the expression T was formed by)
+      for (int k = 0; k < cc; ++k) {
+        const double* a = Pc + 6 * k;
+        const double* b = a + 3;
+        for (int i = 0; i < 3; ++i) s3[i] += a[i] - (Rb[i * 3 + 0] * b[0] + Rb[i * 3 + 1] * b[1] + Rb[i * 3 + 2] * b[2]);
       }
     }
     for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = s3[i] / (double)cc;
     r.stereo_inliers = cc;
     r.accepted = (cc >= P.min3d) ? 1 : 0;
     KMX_PT(12);
-    if (r.accepted && P.refine) {  // the inliers again: valid and within thr3d of the best translation
-      refit_3d3d_wave(
-          n3, lane,
-          [&](int j, double* pq, double* pm) {
-            double tj[3];
-            if (!within(j, tj)) return false;
-            const int2 pr = pl[idx[j]];
-            const double* a = points + ((size_t)q * N + pr.x) * 3;
-            const double* b = points + ((size_t)m * N + pr.y) * 3;
-            for (int k = 0; k < 3; ++k) { pq[k] = a[k]; pm[k] = b[k]; }
-            return true;
-          },
-          r.T_query_match, r.T_query_match + 9);
+    if (r.accepted && refine) {  // refit_3d3d's sums over the same inliers, in its order
+      double cq3[3] = {0.0, 0.0, 0.0}, cm3[3] = {0.0, 0.0, 0.0};
+      for (int k = 0; k < cc; ++k)
+        for (int i = 0; i < 3; ++i) {
+          cq3[i] += Pc[6 * k + i];
+          cm3[i] += Pc[6 * k + 3 + i];
+        }
+      for (int i = 0; i < 3; ++i) {
+        cq3[i] /= (double)cc;
+        cm3[i] /= (double)cc;
+      }
+      double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (int k = 0; k < cc; ++k) {
+        double dq[3], dm[3];
+        for (int i = 0; i < 3; ++i) {
+          dq[i] = Pc[6 * k + i] - cq3[i];
+          dm[i] = Pc[6 * k + 3 + i] - cm3[i];
+        }
+        for (int a = 0; a < 3; ++a)
+          for (int b = 0; b < 3; ++b) H[a * 3 + b] += dm[a] * dq[b];
+      }
+      double U[9], sv[3], V[9], Rr[9];
+      svd3(H, U, sv, V);
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b)
+          Rr[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+      if (det3(Rr) < 0.0) {
+        for (int a = 0; a < 3; ++a) V[a * 3 + 2] = -V[a * 3 + 2];
+        for (int a = 0; a < 3; ++a)
+          for (int b = 0; b < 3; ++b)
+            Rr[a * 3 + b] = V[a * 3 + 0] * U[b * 3 + 0] + V[a * 3 + 1] * U[b * 3 + 1] + V[a * 3 + 2] * U[b * 3 + 2];
+      }
+      for (int a = 0; a < 9; ++a) r.T_query_match[a] = Rr[a];
+      for (int a = 0; a < 3; ++a)
+        r.T_query_match[9 + a] = cq3[a] - (Rr[a * 3 + 0] * cm3[0] + Rr[a * 3 + 1] * cm3[1] + Rr[a * 3 + 2] * cm3[2]);
       KMX_PT(13);
     }
   } else {
@@ -2539,7 +2545,14 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, in
   double* F1 = fbuf + (size_t)blockIdx.x * (6 * N + STASH);
   double* F2 = F1 + 3 * N;
   double* stash = F1 + 6 * N;
+  // KMX_RS_PROF=1 (diagnostic): the solver's phase timers as in k_ransac_coop,
+  // plus g_phase[11] the wave's whole time, [12] the compaction, [13] the
+  // scoring, [15] waves (scripts/lcd_single.py)
+  const bool prof = P.prof == 1;
+  const unsigned long long t_wave = prof ? wall_clock64() : 0;
+  unsigned long long t_prev = t_wave;
   rs_compact(w, F1, bearings, N, cq[c], cm[c], pairs + (size_t)c * N, K, lane);
+  KMX_PT(12);
   const short* tab = table + (size_t)(K - 5) * P.pmax * 5;
   HypOut* ho = hout + (size_t)c * P.pmax;
   auto emit = [&](int p, bool ok, const double* mR, const double* mt) {
@@ -2567,14 +2580,21 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, in
   };
   if constexpr (STEW) {
     const int nb = p_hi - p_lo;
-    stew_batch(w, sb, stash, lane, F1, F2, N, tab, p_lo, nb, false);
-    stew_models(sb, stash, lane, F1, F2, tab, p_lo, nb, false);
+    stew_batch(w, sb, stash, lane, F1, F2, N, tab, p_lo, nb, prof);
+    stew_models(sb, stash, lane, F1, F2, tab, p_lo, nb, prof);
+    if (prof && lane == 0) t_prev = wall_clock64();
     for (int b = 0; b < nb; ++b) emit(p_lo + b, sb.mok[b] != 0, sb.mR[b], sb.mt[b]);
   } else {
     for (int p = p_lo; p < p_hi; ++p) {
-      coop_hypothesis(w, lane, F1, F2, N, tab + (size_t)p * 5, false);
+      coop_hypothesis(w, lane, F1, F2, N, tab + (size_t)p * 5, prof);
+      if (prof && lane == 0) t_prev = wall_clock64();
       emit(p, w.ok != 0, w.mR, w.mt);
     }
+  }
+  KMX_PT(13);
+  if (prof && lane == 0) {
+    atomicAdd(&g_phase[11], wall_clock64() - t_wave);
+    atomicAdd(&g_phase[15], 1ull);
   }
 }
 
@@ -2664,6 +2684,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_finish(const double* bearings, 
                                                         const int* Kin, RsParams P, const RsState* st,
                                                         kmx_lcd_result* res, unsigned char* masks, double* fbuf) {
   __shared__ CoopWS w;
+  extern __shared__ double tail_lds[];  // tail_lds_doubles(N)
   const int c = blockIdx.x;
   const int lane = fresh_lane(threadIdx.x);
   const int K = Kin[c];
@@ -2687,7 +2708,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_finish(const double* bearings, 
   if (lane < 12) w.bestm[lane] = s.best[lane];
   __threadfence_block();
   wsync();
-  ransac_tail<true>(c, w, F1, F1 + 3 * N, points, N, q, m, pl, K, P, R_, mask, s.have, s.iterations, lane);
+  ransac_tail<true>(c, w, F1, F1 + 3 * N, points, N, q, m, pl, K, P, R_, mask, s.have, s.iterations, lane, tail_lds);
 }
 
 // Arun 3-point model (oracle arun_model): centroids, H = sum dm dq^T, Kabsch
@@ -3437,7 +3458,11 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks) {
     pa = pb;
     range = pa < 510 ? 510 - pa : 1500;  // then the rest of a 500-iteration loop, then its skips
   }
-  hipLaunchKernelGGL(k_rs_finish, dim3(n), dim3(RS_BLOCK), 0, st, (const double*)h->d_bear, (const double*)h->d_pts,
+  const size_t tail_bytes = sizeof(double) * tail_lds_doubles(h->N);
+  if (tail_bytes > 65536)  // (max_feats near 1024: up to 75 KB with the 4.7 KB static workspace)
+    KMX_HIP(hipFuncSetAttribute((const void*)k_rs_finish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tail_bytes));
+  hipLaunchKernelGGL(k_rs_finish, dim3(n), dim3(RS_BLOCK), tail_bytes, st,
+                     (const double*)h->d_bear, (const double*)h->d_pts,
                      h->N, (const int*)h->d_cq, (const int*)h->d_cm, (const int2*)h->d_pairs, (const int*)h->d_K, rp,
                      (const RsState*)h->d_st, h->d_res, masks ? h->d_mask : nullptr, h->d_sfbuf);
   if (rp.pnp && (stages & KMX_LCD_STAGE_RECOVER))

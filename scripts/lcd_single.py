@@ -51,3 +51,15 @@ if os.environ.get("KMX_RS_PROF") == "3":  # the recovery tail's phase timers (lc
     calls = max(buf[15], 1)
     print(f"recovery tail: {buf[15]} calls, n3 mean {buf[14] / calls:.1f}; per call: count {buf[11] / 100 / calls:.1f} us, "
           f"final pass {buf[12] / 100 / calls:.1f} us, refit {buf[13] / 100 / calls:.1f} us")
+if os.environ.get("KMX_RS_PROF") == "1":  # the spread form's hypothesis waves (lcd.hip k_rs_hyps)
+    import ctypes as C
+    from kmx import abi
+    fn = abi.lib().kmx_lcd_debug_phase_times
+    fn.argtypes = [C.POINTER(C.c_ulonglong)]
+    buf = (C.c_ulonglong * 16)()
+    fn(buf)
+    w = max(buf[15], 1)
+    names = {0: "sample", 1: "nullspace", 2: "system", 7: "hessenberg", 8: "hqr", 9: "eigvec", 10: "decomp",
+             12: "compaction", 13: "scoring", 11: "whole wave"}
+    print(f"{buf[15]} hypothesis waves; per wave (us): " +
+          ", ".join(f"{n} {buf[i] / 100 / w:.1f}" for i, n in names.items()))

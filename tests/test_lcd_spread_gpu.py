@@ -122,3 +122,32 @@ def test_spread_call_chain_equals_batched(gpu, monkeypatch):
     finally:
         d1.close()
         dq.close()
+
+
+@pytest.mark.parametrize("refine", [0, 1], ids=["keep", "refine"])
+def test_spread_max_feats_1024_and_refine_off(gpu, monkeypatch, refine):
+    """One candidate per call at max_feats = 1024 (the 1-point recovery's
+    staging then needs 75 KB of LDS: the launch raises the dynamic limit) and
+    ragged frames, with refine_pose on and off (the recovery sums T_j itself,
+    or re-forms it from the staged points): bit-exact against the
+    restatement."""
+    from oracle import oracle as O
+    pool = make_lcd_pool(20, 1024, seed=6)
+    pool.n_feats = np.array([1024, 1024, 0, 300, 4, 300, 5, 300, 9, 9, 10, 300, 300, 0, 700, 700, 1, 1, 64, 1024],
+                            np.int32)
+    cq = np.array([0, 2, 3, 4, 6, 8, 10, 12, 14, 16, 18, 19, 5, 7, 0], np.int32)
+    cm = np.array([1, 3, 2, 5, 7, 9, 11, 13, 15, 17, 19, 18, 5, 3, 19], np.int32)
+    p = LcdParams(refine_pose=refine)
+    d = _det(p, pool, 8, monkeypatch)
+    try:
+        ref, rm = O.lcd_verify(p.to_c(), pool, cand_query=cq, cand_match=cm)
+        for i in range(cq.shape[0]):
+            g, gm = d.verify(cq[i:i + 1], cm[i:i + 1], with_masks=True)
+            r = ref[i]
+            assert tuple(g[0][k] for k in FIELDS) == tuple(getattr(r, k) for k in FIELDS), i
+            assert g[0]["accepted"] == bool(r.accepted), i
+            assert np.array_equal(g[0]["T_query_match"], np.array(r.T_query_match[:]), equal_nan=True), i
+            assert np.array_equal(gm[0], rm[i]), i
+        assert ref[0].accepted  # the planted pair at max_feats = 1024 went through the recovery
+    finally:
+        d.close()
