@@ -3437,7 +3437,11 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks) {
   hipLaunchKernelGGL(k_rs_init, dim3((std::max(n, h->more_cap) + 63) / 64), dim3(64), 0, st, h->d_st, n, stages,
                      h->d_more, h->more_cap);
   int pa = 0;
-  int range = 66;  // covers a true loop closure's loop (~30 iterations) in one pass
+  // the first range: a true loop closure's loop (~30 iterations) in one pass;
+  // where the launch has the waves for it (one or two candidates), a whole
+  // 500-iteration loop (510) at once — one hypothesis per wave costs the
+  // same latency, and a look-alike then needs one range, not two
+  int range = (int64_t)n * 510 <= SPREAD_WAVES ? 510 : 66;
   for (int it = 0; pa < h->pmax && (stages & KMX_LCD_STAGE_2D2D); ++it) {  // (recovery alone: no hypotheses)
     // hypotheses per wave: as few as the launch's waves allow (one wave
     // works through its hypotheses one after another; the batch of SG
