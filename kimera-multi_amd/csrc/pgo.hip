@@ -191,6 +191,14 @@ struct Dev {
   // 8-wide partials
   double *hz, *w0, *w1;
   unsigned* gbar;             // resident round: grid-barrier words (zeroed by k_begin), or null
+  // RM_LAUNCH with fused reducers (fuse_red): the tCG launches carry L extra
+  // workgroups, one per robot, that reduce the robot's tile partials as soon
+  // as its tiles have posted them (in place of a k_reduce launch). red_cnt:
+  // [L] arrival counters (128-B apart, reset by their reducer); fail: the
+  // host-mapped word a reducer whose wait gave up writes
+  int fuse_red;
+  unsigned* red_cnt;
+  unsigned* fail;
   double* part_f;             // [2][ntiles][8], by step parity (a launch reads step k's
                               // partials of every tile of its robot while its own tile writes step k+1's)
 };
@@ -505,7 +513,7 @@ __device__ __forceinline__ Lane lane_map(const Dev& d) {
   // blocks b and b + 8 share an XCD, so each XCD gets one contiguous range of
   // tiles — about one robot block, whose rows then stay in that XCD's L2.
   {
-    const int nwg = gridDim.x, b = blockIdx.x;
+    const int nwg = d.ntiles, b = blockIdx.x;  // (the tile blocks: fused reducers come after them)
     const int q = nwg >> 3, rr = nwg & 7, x = b & 7;
     L.tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
   }
@@ -857,6 +865,11 @@ __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, co
 // round: no gain).
 enum RedMode { RM_LAUNCH = 0, RM_CONSUMER = 2 };
 
+constexpr int RC_STRIDE = 32;  // Dev::red_cnt: one 128-B line per robot
+__device__ __forceinline__ void wt_st1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <int KIND, int NV, int RM, typename Store>
 __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const double* vals, char* smem_red,
                                             Store&& store) {
@@ -870,14 +883,24 @@ __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const d
   __syncthreads();
   constexpr bool two = RM == RM_CONSUMER && (KIND == RED_HESS || KIND == RED_UPDATE);
   static_assert(!two || NV <= 2, "consumer partials");
+  constexpr bool fusable = RM == RM_LAUNCH && (KIND == RED_HESS || KIND == RED_UPDATE);
   if (threadIdx.x == 0) {  // 2-wide partials for the consumer launch, else NPART-wide for k_reduce
     double* dst = two ? (KIND == RED_HESS ? d.part_h : d.part_u) + (size_t)L.tile * 2 : d.part + (size_t)L.tile * NPART;
+    const bool fused = fusable && d.fuse_red;
 #pragma unroll
     for (int s = 0; s < NV; ++s) {
       double t = 0.0;
 #pragma unroll
       for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
-      dst[s] = t;
+      if (fused) {
+        wt_st1(dst + s, t);  // write-through: the robot's reducer in this launch reads it sc1
+      } else {
+        dst[s] = t;
+      }
+    }
+    if (fused) {  // drained, then one arrival on the robot's counter (MI355X_MICROARCH.md "Valid forms", row 1)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      (void)__hip_atomic_fetch_add(d.red_cnt + (size_t)L.l * RC_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   store();
@@ -2178,14 +2201,90 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d, int gated) {
   KMX_SMEM;
   body_grad<R, RW, RM>(d, gated, smem);
 }
+// A fused reducer (Dev::fuse_red, RM_LAUNCH): k_reduce's work inside the
+// launch that produces the partials, by workgroup ntiles + l of it. Every tile
+// of robot l posts its partials write-through, drains them and adds one to the
+// robot's counter; the reducer (dispatched after every tile workgroup, so no
+// tile waits for it) polls the counter sc1 until all t1 - t0 tiles have posted,
+// then sums them in k_reduce's order (RobotSum, 16-B sc1 loads) and runs the
+// same control step. A robot not in the launch's phase posts nothing and its
+// reducer does not wait. What the launch's boundary then carries to the next
+// kernel is only the robot's state, as after a k_reduce launch — without that
+// launch's own ramp and dependency.
+constexpr unsigned long long KMX_RED_SPIN = 200000000ull;  // 2 s of the 100 MHz clock
+__device__ __forceinline__ void red_fused(const Dev& d, int kind, int l, int R_, HostStatus* hs,
+                                          unsigned long long seq, int slot) {
+  constexpr int RW_ = RBLOCK / 64;
+  constexpr int CW = sizeof(Ctl) / 8;
+  __shared__ double lds[NPART * RW_];
+  __shared__ Ctl cs;
+  __shared__ int ok_s;
+  if (threadIdx.x < CW)
+    reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(d.ctl + l)[threadIdx.x];
+  __syncthreads();
+  const int ph = cs.phase;
+  const bool act = (kind == RED_HESS || kind == RED_UPDATE) && ph == PH_TCG;
+  const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
+  double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
+  if (act) {
+    if (threadIdx.x == 0) {
+      unsigned* c = d.red_cnt + (size_t)l * RC_STRIDE;
+      const unsigned n = (unsigned)(t1 - t0);
+      int ok = 1;
+      const unsigned long long ts = wall_clock64();
+      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - ts > KMX_RED_SPIN) {
+          ok = 0;
+          __hip_atomic_store(d.fail, 0x10000u + (unsigned)kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's count starts at 0
+      ok_s = ok;
+    }
+    __syncthreads();
+    if (!ok_s) return;
+    RobotSum<NPART, 2, true> rs;  // (<= 512 tiles per robot: the host checks)
+    rs.issue(d.part, NPART, t0, t1);
+    rs.finish(d.part, NPART, lds, tot);
+  }
+  if (threadIdx.x == 0) {
+    if (act) {
+      const int ns = kind == RED_HESS ? 1 : 2;
+#pragma unroll
+      for (int s = 0; s < NPART; ++s) tot[s] = s < ns ? tot[s] : 0.0;
+      control_on(cs, d, l, kind, tot, R_, true);
+      if (kind == RED_HESS && slot >= 0) atomicAdd(d.hv_launch + slot, 1);
+    }
+    if (hs) post_status(hs, l, seq, act && cs.phase == PH_TCG);
+  }
+  if (!act) return;
+  __syncthreads();
+  if (threadIdx.x < CW)
+    reinterpret_cast<double*>(d.ctl + l)[threadIdx.x] = reinterpret_cast<const double*>(&cs)[threadIdx.x];
+}
+
 template <int R, int RW, int RM>
 __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int first, int slot, HostStatus* hs,
                                                           unsigned long long seq) {
+  if constexpr (RM == RM_LAUNCH) {
+    if ((int)blockIdx.x >= d.ntiles) {
+      red_fused(d, RED_HESS, (int)blockIdx.x - d.ntiles, R, hs, seq, slot);
+      return;
+    }
+  }
   KMX_SMEM;
   body_hess<R, RW, RM>(d, first, slot, hs, seq, smem);
 }
 template <int R, int RM>
 __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq, int slot) {
+  if constexpr (RM == RM_LAUNCH) {
+    if ((int)blockIdx.x >= d.ntiles) {
+      red_fused(d, RED_UPDATE, (int)blockIdx.x - d.ntiles, R, hs, seq, slot);
+      return;
+    }
+  }
   KMX_SMEM;
   body_update<R, RM>(d, hs, seq, slot, smem);
 }
@@ -2334,11 +2433,6 @@ __device__ __forceinline__ void wt_st4(__amdgpu_buffer_rsrc_t rs, unsigned off, 
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kmx_u4, make_double2(v[0], v[1])), rs, off, 0, 16);
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kmx_u4, make_double2(v[2], v[3])), rs, off + 16, 0, 16);
 }
-__device__ __forceinline__ void wt_st1(double* p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // the gathered rows of a vector another workgroup of this launch wrote
 template <int R>
 struct WtRows {
@@ -3485,6 +3579,9 @@ struct kmx_pgo {
   std::string res_reason = "tcg_form is not KMX_TCG_FORM_RESIDENT";
   unsigned* d_gbar = nullptr;  // grid-barrier words (GB_WORDS)
   unsigned* h_fail = nullptr;  // host-mapped: nonzero when a barrier wait gave up (1 + its index)
+  bool fuse_red = false;       // RM_LAUNCH tCG launches carry their reducers (Dev::fuse_red; KMX_FUSE_RED=0: off)
+  bool fuse_forced_off = false;
+  unsigned* d_red_cnt = nullptr;
   double acc_gamma = 0.0;
   int acc_k = 0;
   bool acc_ready = false, acc_started = false;
@@ -3549,7 +3646,7 @@ void free_dev(kmx_pgo* h) {
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
                   h->d_accV, h->d_accY, h->d_ctl2, h->d_part_h,
-                  h->d_part_u, h->d_coefh, h->d_part_f, h->d_gbar};
+                  h->d_part_u, h->d_coefh, h->d_part_f, h->d_gbar, h->d_red_cnt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile = nullptr;
@@ -3577,6 +3674,7 @@ void free_dev(kmx_pgo* h) {
   h->d_part_h = h->d_part_u = nullptr;
   h->d_part_f = nullptr;
   h->d_gbar = nullptr;
+  h->d_red_cnt = nullptr;
   h->res_on = false;
 }
 
@@ -3805,12 +3903,20 @@ void enqueue_tcg_t(kmx_pgo* h) {
       }
       continue;
     }
-    hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot, nullptr,
-                       0ull);
-    if (slot >= 0) (void)hipEventRecord(e1, h->stream);
-    red_t<R, RM>(h, RED_HESS, nullptr, 0, slot);
-    hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, seq, -1);
-    red_t<R, RM>(h, RED_UPDATE, hs, seq, -1, nullptr);
+    if (h->fuse_red) {  // each launch carries its robots' reducers (red_fused)
+      const dim3 gr(h->ntiles + h->dv.L);
+      hipLaunchKernelGGL((k_hess<R, RW, RM>), gr, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
+                         nullptr, 0ull);
+      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+      hipLaunchKernelGGL((k_update<R, RM>), gr, blk, SmemU::bytes, h->stream, h->dv, hs, seq, -1);
+    } else {
+      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
+                         nullptr, 0ull);
+      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+      red_t<R, RM>(h, RED_HESS, nullptr, 0, slot);
+      hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, seq, -1);
+      red_t<R, RM>(h, RED_UPDATE, hs, seq, -1, nullptr);
+    }
     if (poll) {
       if (j > 0 && !wait_running(h, prev)) {
         steps = j + 1;
@@ -4513,6 +4619,27 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     d.hz = h->d_vec + v0 * vec; d.w0 = h->d_vec + (v0 + 1) * vec; d.w1 = h->d_vec + (v0 + 2) * vec;
     d.part_f = h->d_part_f;
   }
+  // fused reducers (RM_LAUNCH tCG launches; every robot's tiles within one
+  // RobotSum pass). KMX_FUSE_RED=0: separate k_reduce launches (A/B switch)
+  h->fuse_red = false;
+  if (h->rm == RM_LAUNCH && !h->fuse_forced_off) {
+    bool fits = true;
+    for (size_t l = 0; l + 1 < h->rt0_h.size(); ++l) fits = fits && h->rt0_h[l + 1] - h->rt0_h[l] <= 2 * RBLOCK;
+    if (fits) {
+      if (!h->d_red_cnt)
+        if (int rc = dalloc(&h->d_red_cnt, (size_t)1024 * RC_STRIDE)) return rc;
+      KMX_HIP(hipMemsetAsync(h->d_red_cnt, 0, sizeof(unsigned) * 1024 * RC_STRIDE, h->stream));
+      if (!h->h_fail) {
+        KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_fail), sizeof(unsigned),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        *h->h_fail = 0;
+      }
+      h->fuse_red = true;
+    }
+  }
+  d.fuse_red = h->fuse_red ? 1 : 0;
+  d.red_cnt = h->d_red_cnt;
+  d.fail = h->h_fail;
   h->n_ext = 0;
   sync_params(h);
   enqueue_precond(h, 0);
@@ -4757,6 +4884,7 @@ extern "C" int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, i
   h->world = world;
   h->rank = rank;
   if (const char* v = std::getenv("KMX_XCHG_SELF_P2P")) h->xchg_self_p2p = std::atoi(v) != 0;
+  if (const char* v = std::getenv("KMX_FUSE_RED")) h->fuse_forced_off = std::atoi(v) == 0;
   return KMX_OK;
   KMX_GUARD_END
 }
