@@ -738,21 +738,23 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
   __syncthreads();  // sptr, xs
   for (int c0 = 0; c0 < n; c0 += CH) {
     const int k = max(min(c0 + lt, n - 1), 0);
+    // the other endpoint's row first (it needs only the record), so its
+    // latency runs under the owning pose's search
+    const int2 in = RC::inc(q);
+    const int o = in.x;
+    const bool tail = (in.y >> 31) & 1;
+    const double2* o2 =
+        reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
+    double2 vo2[2 * R];
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) vo2[i] = o2[i];
     int lo = 0, hi = np;  // owning pose: sptr[lo] <= k < sptr[lo + 1]
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
       if (sptr[mid] <= k) lo = mid;
       else hi = mid;
     }
-    const int2 in = RC::inc(q);
-    const int o = in.x;
-    const bool tail = (in.y >> 31) & 1;
     const double2* s2 = xs + lo * 2 * R;
-    const double2* o2 =
-        reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
-    double2 vo2[2 * R];
-#pragma unroll
-    for (int i = 0; i < 2 * R; ++i) vo2[i] = o2[i];
     Edge E;
     RC::edge(q, E);
     if (tid < CH && c0 + tid < n) {
@@ -812,6 +814,12 @@ __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, co
     const int o = in.x;
     const bool tail = (in.y >> 31) & 1;
     if (o >= 0 && !tail) continue;  // the head of a local edge: its tail counts it
+    // the other endpoint's row first: its latency runs under the owning pose's search
+    const double2* o2 =
+        reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
+    double2 vs2[2 * R], vo2[2 * R];
+#pragma unroll
+    for (int i = 0; i < 2 * R; ++i) vo2[i] = o2[i];
     int lo = 0, hi = np;
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -819,11 +827,8 @@ __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, co
       else hi = mid;
     }
     const double2* s2 = xs + lo * 2 * R;
-    const double2* o2 =
-        reinterpret_cast<const double2*>((o >= 0) ? V + (size_t)o * 4 * R : pub + (size_t)(-1 - o) * 4 * R);
-    double2 vs2[2 * R], vo2[2 * R];
 #pragma unroll
-    for (int i = 0; i < 2 * R; ++i) { vs2[i] = s2[i]; vo2[i] = o2[i]; }
+    for (int i = 0; i < 2 * R; ++i) vs2[i] = s2[i];
     Edge E;
     RC::edge(q, E);
     double c = 0.0;
@@ -3579,8 +3584,9 @@ struct kmx_pgo {
   std::string res_reason = "tcg_form is not KMX_TCG_FORM_RESIDENT";
   unsigned* d_gbar = nullptr;  // grid-barrier words (GB_WORDS)
   unsigned* h_fail = nullptr;  // host-mapped: nonzero when a barrier wait gave up (1 + its index)
-  bool fuse_red = false;       // RM_LAUNCH tCG launches carry their reducers (Dev::fuse_red; KMX_FUSE_RED=0: off)
-  bool fuse_forced_off = false;
+  bool fuse_red = false;       // RM_LAUNCH tCG launches carry their reducers (Dev::fuse_red; KMX_FUSE_RED=1: on)
+  bool fuse_forced_off = true;  // opt-in: level with the k_reduce launches at 100k (8.72-8.75e8 vs 8.70e8, one box)
+                                // while each launch then holds the reduction's ~3 us tail (profiles/r05/fused_red/)
   unsigned* d_red_cnt = nullptr;
   double acc_gamma = 0.0;
   int acc_k = 0;
@@ -4620,7 +4626,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     d.part_f = h->d_part_f;
   }
   // fused reducers (RM_LAUNCH tCG launches; every robot's tiles within one
-  // RobotSum pass). KMX_FUSE_RED=0: separate k_reduce launches (A/B switch)
+  // RobotSum pass). Opt-in, KMX_FUSE_RED=1 (A/B switch)
   h->fuse_red = false;
   if (h->rm == RM_LAUNCH && !h->fuse_forced_off) {
     bool fits = true;
