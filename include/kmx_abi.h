@@ -127,8 +127,9 @@ typedef struct kmx_iter_stats {
  * launch per round: each workgroup keeps its tile's rows in registers and LDS
  * for the round, and the one reduction per tCG step crosses workgroups through
  * a grid barrier (write-through stores, no kernel boundary). For small shards
- * (the strong-scaling regime: the tiles must all be resident, about 24k poses
- * per GPU at r = 5) with rtr_iterations 1 and RTR; otherwise the handle runs
+ * (the strong-scaling regime: the tiles must all be resident, one workgroup
+ * per CU: about 15k poses per GPU at r = 5) with rtr_iterations 1 and RTR and
+ * tcg_max_iterations <= 61; otherwise the handle runs
  * the launched one-sync form (1) on the same tile cut, with the same results
  * bit for bit (kmx_pgo_resident_info says which ran and why). */
 #define KMX_TCG_FORM_RESIDENT 2
