@@ -806,9 +806,11 @@ def main():
                                "(separate rocprofv3 --pmc pass) x this run's algorithmic bytes") if traffic else None,
             "launches": hv_n,
             "measured_over": (f"replay of the timed rounds {w0}..{w0 + args.steps} from their snapshot, HIP events "
-                              "around each k_hess launch that ran a Hess-vec") if not args.profile else
-                             f"rounds 0..{args.steps} (profile run), HIP events around each k_hess launch that ran "
+                              "of each k_hess launch that ran a Hess-vec") if not args.profile else
+                             f"rounds 0..{args.steps} (profile run), HIP events of each k_hess launch that ran "
                              "a Hess-vec",
+            "event_form": "hipExtLaunchKernelGGL start / stop events: the dispatch's own timestamps (no event "
+                          "packets between launches)",
             "replay_identical": leg["replay_identical"],
             "avg_launch_us": 1e3 * hv_ms / max(hv_n, 1),
             "hess_ms_per_round": hv_ms / nr,

@@ -32,6 +32,7 @@
 //     robustOptNumWeightUpdates) from device state and re-weights the loop
 //     closures in the same launch.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
 
@@ -158,6 +159,9 @@ struct Dev {
   double* ew;          // GNC weight
   const int2* eipos;   // [mloc] record positions (tail, head) of each local edge, -1 if not local
   double *X, *Xt, *g, *r, *z, *hd, *S, *Pinv, *hD, *pub;
+  // D_i - S_i (S embedded in the rotation block; SYM4 per pose), written by
+  // k_grad: k_hess applies it in place of D_i and S (48 B per pose per launch)
+  double* hDS;
   // tCG search directions: delta_k lives in dh + (k % dhn) * vec, so eta =
   // sum_k coef_k delta_k is not updated at every Hess-vec: k_hess folds the
   // dhn oldest directions into eta before their buffer is reused (every dhn
@@ -592,7 +596,9 @@ struct NoPre {
 // would spill)
 // DIAG = false: the caller applies the diagonal block itself (k_step, whose
 // epilogue loads the own row and D_i with the rest of its rows in one batch).
-template <int R, int RW, bool REC_FIRST, typename Src, typename Pre, bool DIAG = true, int W = WAVES>
+// DS: the diagonal block applied is D_i - S_i (hDS, k_hess: the tangent
+// correction -V S folded into it) instead of D_i.
+template <int R, int RW, bool REC_FIRST, typename Src, typename Pre, bool DIAG = true, int W = WAVES, bool DS = false>
 __device__ __forceinline__ bool hinc_gather_src(const Dev& d, const Lane& L, Src& src, double acc[4], char* smem,
                                                 Pre&& pre) {
   using SM = SmemH<R, W>;
@@ -664,7 +670,7 @@ __device__ __forceinline__ bool hinc_gather_src(const Dev& d, const Lane& L, Src
 #if KMX_HESS_PROBE & 2  // traffic attribution build: no diagonal-block loads
     for (int c = 0; c < 16; ++c) D[c] = (c % 5 == 0) ? 1.0 : 0.0;
 #else
-    load_sym4(d.hD + SYM4 * (size_t)L.pose, D);
+    load_sym4((DS ? d.hDS : d.hD) + SYM4 * (size_t)L.pose, D);
 #endif
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -699,11 +705,11 @@ struct PlainRows {
 #endif
   }
 };
-template <int R, int RW, bool REC_FIRST = false, typename Pre = NoPre>
+template <int R, int RW, bool REC_FIRST = false, bool DS = false, typename Pre = NoPre>
 __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const double* V, double acc[4],
                                             char* smem, Pre&& pre = Pre{}) {
   PlainRows<R> src{V};
-  return hinc_gather_src<R, RW, REC_FIRST>(d, L, src, acc, smem, pre);
+  return hinc_gather_src<R, RW, REC_FIRST, PlainRows<R>, Pre&, true, WAVES, DS>(d, L, src, acc, smem, pre);
 }
 
 // Gradient and cost, incidence-parallel. A lane evaluates its whole incidence
@@ -1368,6 +1374,19 @@ __device__ __forceinline__ void body_grad(const Dev& d, int gated, char* smem) {
   double y[4] = {0, 0, 0, 0}, G[4], cost = 0.0;
   hinc_grad<R, RW>(d, L, d.X, d.pub, G, &cost, smem);
   if (L.valid) load4(d.X + (size_t)L.pose * 4 * R + 4 * L.a, y);
+  // D_i - S_i for k_hess: the pose's D_i (five 16-B parts; a gated re-weight's
+  // rebuild above is this workgroup's own writes) is loaded here, spread over its
+  // lanes (parts a and a + r), so its latency runs under the group operations
+  constexpr int NDP = R >= 5 ? 1 : 2;
+  double2 dpart[NDP];
+  {
+    const double2* Dp2 = reinterpret_cast<const double2*>(d.hD + SYM4 * (size_t)L.pose);
+#pragma unroll
+    for (int u = 0; u < NDP; ++u) {
+      const int i = L.a + u * R;
+      dpart[u] = (L.valid && i < 5) ? Dp2[i] : make_double2(0.0, 0.0);
+    }
+  }
   double S[9], gr[4], zr[4];
   double* scr = reinterpret_cast<double*>(smem);  // the chunk buffer is free after the gather's last barrier
   group_symYtG<R, true>(y, G, L.base, S, scr);
@@ -1388,6 +1407,17 @@ __device__ __forceinline__ void body_grad(const Dev& d, int gated, char* smem) {
     if (L.a == 0) {
       double* Sp = d.S + 6 * (size_t)L.pose;
       Sp[0] = S[0]; Sp[1] = S[1]; Sp[2] = S[2]; Sp[3] = S[4]; Sp[4] = S[5]; Sp[5] = S[8];
+    }
+    // part i holds SYM4 entries 2i, 2i + 1: (00, 01), (02, 03), (11, 12), (13, 22), (23, 33)
+    double2* Fp2 = reinterpret_cast<double2*>(d.hDS + SYM4 * (size_t)L.pose);
+#pragma unroll
+    for (int u = 0; u < NDP; ++u) {
+      const int i = L.a + u * R;
+      if (i < 5) {
+        const double sx = i == 0 ? S[0] : i == 1 ? S[2] : i == 2 ? S[4] : 0.0;
+        const double sy = i == 0 ? S[1] : i == 2 ? S[5] : i == 3 ? S[8] : 0.0;
+        Fp2[i] = make_double2(dpart[u].x - sx, dpart[u].y - sy);
+      }
     }
   });
 }
@@ -1469,7 +1499,7 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
   const Lane L = lane_map<R>(d);
   int tcg_iter;
   double beta;
-  double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4], S[9];
+  double y[4] = {0, 0, 0, 0}, zs[4] = {0, 0, 0, 0}, H[4];
   const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
   if constexpr (RM == RM_CONSUMER) {
     // the previous step's k_update partials give this robot's control step
@@ -1530,9 +1560,9 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     // speculatively, so the robot sums' latency hides behind the gather
     bool go;
     if (d.p.early_stop) {
-      go = hinc_gather<R, RW>(d, L, d.z, H, smem, decide);
+      go = hinc_gather<R, RW, false, true>(d, L, d.z, H, smem, decide);
     } else {
-      hinc_gather<R, RW>(d, L, d.z, H, smem);
+      hinc_gather<R, RW, false, true>(d, L, d.z, H, smem);
       go = decide();
     }
     if (!go) return;
@@ -1542,7 +1572,7 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     // the phase test runs once the first chunk's records are in flight (a
     // robot out of tCG leaves before any row is gathered)
     const Ctl& c = d.ctl[L.l];
-    if (!hinc_gather<R, RW, true>(d, L, d.z, H, smem, [&]() { return c.phase == PH_TCG; })) return;
+    if (!hinc_gather<R, RW, true, true>(d, L, d.z, H, smem, [&]() { return c.phase == PH_TCG; })) return;
     tcg_iter = c.tcg_iter;
     beta = c.beta;
   }
@@ -1551,19 +1581,13 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
   if (L.valid) {
 #if KMX_HESS_PROBE & 2
     for (int k = 0; k < 4; ++k) zs[k] = 1e-3 * k;
-    for (int k = 0; k < 9; ++k) S[k] = (k % 4 == 0) ? 1.0 : 0.0;
 #else
     load4(d.z + o, zs);
-    load_sym3(d.S + 6 * (size_t)L.pose, S);
 #endif
-  } else {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) S[i] = 0.0;
   }
-  double hz[4];  // H z - z S (group_rhess before its projection)
+  double hz[4];  // H z - z S (group_rhess before its projection): the gather applied D_i - S_i
 #pragma unroll
-  for (int k = 0; k < 3; ++k) hz[k] = H[k] - (zs[0] * S[0 * 3 + k] + zs[1] * S[1 * 3 + k] + zs[2] * S[2 * 3 + k]);
-  hz[3] = H[3];
+  for (int k = 0; k < 4; ++k) hz[k] = H[k];
   (void)y;
   double v = 0.0;
   double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
@@ -3503,7 +3527,7 @@ struct kmx_pgo {
   double* d_part_f = nullptr;  // [ntiles][8] one-sync tCG partials (P.tcg_form)
   int ctl_par = 0;             // one-sync tCG: the state after the last tCG loop is in ctl2 (odd step count)
   bool tcg_stopped = false;    // consumer tCG loop saw every robot stop (each was retracted by its k_update)
-  double *d_S = nullptr, *d_Pinv = nullptr, *d_hD = nullptr, *d_pub = nullptr, *d_part = nullptr;
+  double *d_S = nullptr, *d_Pinv = nullptr, *d_hD = nullptr, *d_hDS = nullptr, *d_pub = nullptr, *d_part = nullptr;
   Ctl* d_ctl = nullptr;
   Ctl* d_ctl2 = nullptr;
   double *d_part_h = nullptr, *d_part_u = nullptr;
@@ -3647,7 +3671,7 @@ void free_xchg(kmx_pgo* h) {
 
 void free_dev(kmx_pgo* h) {
   void* ptrs[] = {h->d_tile, h->d_rtile0, h->d_inc_ptr, h->d_rec, h->d_ekappa,
-                  h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_hD, h->d_pub, h->d_part,
+                  h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_hD, h->d_hDS, h->d_pub, h->d_part,
                   h->d_ctl, h->d_cnt, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
@@ -3659,7 +3683,7 @@ void free_dev(kmx_pgo* h) {
   h->d_rtile0 = h->d_inc_ptr = nullptr;
   h->d_rec = h->d_ekappa = h->d_etau = h->d_ew = nullptr;
   h->d_eipos = nullptr;
-  h->d_vec = h->d_S = h->d_Pinv = h->d_hD = h->d_pub = h->d_part = nullptr;
+  h->d_vec = h->d_S = h->d_Pinv = h->d_hD = h->d_hDS = h->d_pub = h->d_part = nullptr;
   h->d_ctl = nullptr;
   h->d_cnt = nullptr;
   h->d_m_robot = nullptr;
@@ -3863,16 +3887,18 @@ void enqueue_tcg_t(kmx_pgo* h) {
           slot = (int)(h->ev_used / 2);
           e0 = next_event(h);
           e1 = next_event(h);
-          (void)hipEventRecord(e0, h->stream);
         }
         poll = poll && h->poll;
         const unsigned long long seq = poll ? ++h->seq : 0;
         HostStatus* hs = poll ? h->hstat : nullptr;
         const Ctl* cin = (j & 1) ? h->d_ctl2 : h->d_ctl;
         Ctl* cout = (j & 1) ? h->d_ctl : h->d_ctl2;
-        hipLaunchKernelGGL((k_step<R, RW>), grid, blk, SmemF<R>::bytes, h->stream, h->dv, cin, cout, j,
-                           slot, hs, seq);
-        if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+        if (slot >= 0)  // the events take the dispatch's own start / end timestamps
+          hipExtLaunchKernelGGL((k_step<R, RW>), grid, blk, SmemF<R>::bytes, h->stream, e0, e1, 0u, h->dv, cin,
+                                cout, j, slot, hs, seq);
+        else
+          hipLaunchKernelGGL((k_step<R, RW>), grid, blk, SmemF<R>::bytes, h->stream, h->dv, cin, cout, j,
+                             slot, hs, seq);
         if (poll && j > 0 && !wait_running(h, seq)) {
           J = j + 1;
           break;
@@ -3891,16 +3917,18 @@ void enqueue_tcg_t(kmx_pgo* h) {
       slot = (int)(h->ev_used / 2);
       e0 = next_event(h);
       e1 = next_event(h);
-      (void)hipEventRecord(e0, h->stream);
     }
     poll = poll && h->poll;  // a poll timeout inside wait_running switches to blind
     const unsigned long long seq = poll ? ++h->seq : 0;
     HostStatus* hs = poll ? h->hstat : nullptr;
     if constexpr (RM == RM_CONSUMER) {
       // k_hess reports the stop test of the previous step's update
-      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot, hs,
-                         seq);
-      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+      if (slot >= 0)  // the events take the dispatch's own start / end timestamps
+        hipExtLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, e0, e1, 0u, h->dv,
+                              j == 0 ? 1 : 0, slot, hs, seq);
+      else
+        hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
+                           hs, seq);
       hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, 0ull, slot);
       if (poll && j > 0 && !wait_running(h, seq)) {
         steps = j + 1;
@@ -3911,14 +3939,20 @@ void enqueue_tcg_t(kmx_pgo* h) {
     }
     if (h->fuse_red) {  // each launch carries its robots' reducers (red_fused)
       const dim3 gr(h->ntiles + h->dv.L);
-      hipLaunchKernelGGL((k_hess<R, RW, RM>), gr, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
-                         nullptr, 0ull);
-      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+      if (slot >= 0)
+        hipExtLaunchKernelGGL((k_hess<R, RW, RM>), gr, blk, SmemH<R>::bytes, h->stream, e0, e1, 0u, h->dv,
+                              j == 0 ? 1 : 0, slot, (HostStatus*)nullptr, 0ull);
+      else
+        hipLaunchKernelGGL((k_hess<R, RW, RM>), gr, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
+                           nullptr, 0ull);
       hipLaunchKernelGGL((k_update<R, RM>), gr, blk, SmemU::bytes, h->stream, h->dv, hs, seq, -1);
     } else {
-      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
-                         nullptr, 0ull);
-      if (slot >= 0) (void)hipEventRecord(e1, h->stream);
+      if (slot >= 0)
+        hipExtLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, e0, e1, 0u, h->dv,
+                              j == 0 ? 1 : 0, slot, (HostStatus*)nullptr, 0ull);
+      else
+        hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
+                           nullptr, 0ull);
       red_t<R, RM>(h, RED_HESS, nullptr, 0, slot);
       hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, seq, -1);
       red_t<R, RM>(h, RED_UPDATE, hs, seq, -1, nullptr);
@@ -4527,6 +4561,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       (rc = dalloc(&h->d_vec, vec * nvec(h))) || (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 6)) ||
       (rc = dalloc(&h->d_Pinv, (size_t)std::max(nloc, 1) * SYM4)) ||
       (rc = dalloc(&h->d_hD, (size_t)std::max(nloc, 1) * SYM4)) ||
+      (rc = dalloc(&h->d_hDS, (size_t)std::max(nloc, 1) * SYM4)) ||
       (rc = dalloc(&h->d_pub, (size_t)std::max<int64_t>(h->npub, 1) * ps)) ||
       (h->P.acceleration && ((rc = dalloc(&h->d_accV, vec)) || (rc = dalloc(&h->d_accY, vec)))) ||
       (rc = dalloc(&h->d_part, (size_t)h->ntiles * NPART)) || (rc = dalloc(&h->d_ctl, L)) ||
@@ -4613,7 +4648,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
   d.z = h->d_vec + 4 * vec; d.hd = h->d_vec + 5 * vec; d.eta = h->d_vec + 6 * vec; d.dh = h->d_vec + 7 * vec;
   d.coefh = h->d_coefh; d.vec = (long long)vec; d.dhn = dh_count(h);
-  d.S = h->d_S; d.Pinv = h->d_Pinv; d.hD = h->d_hD; d.pub = h->d_pub; d.part = h->d_part;
+  d.S = h->d_S; d.Pinv = h->d_Pinv; d.hD = h->d_hD; d.hDS = h->d_hDS; d.pub = h->d_pub; d.part = h->d_part;
   d.ctl = h->d_ctl; d.cnt = h->d_cnt;
   d.ctl2 = h->d_ctl2; d.part_h = h->d_part_h; d.part_u = h->d_part_u;
   d.m_robot = h->d_m_robot; d.n_robot = h->d_n_robot; d.pose_slot = h->d_pose_slot;
