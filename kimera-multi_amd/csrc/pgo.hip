@@ -153,7 +153,8 @@ struct Dev {
   const TileDesc* tile;
   const int* rtile0;   // [L+1]
   const int* inc_ptr;  // [nloc+1]
-  double* rec;         // [ninc + 1][RW] incidence records in CSR order (+ one zero pad record)
+  double* rec;         // [ninc + 1][Rec<RW>::GS] incidence records in CSR order (+ one zero pad record)
+  const int* rec_o;    // [ninc + 1] compact records: the other endpoint of each incidence
   double* ekappa;      // [mloc] per local edge
   double* etau;
   double* ew;          // GNC weight
@@ -311,19 +312,44 @@ __device__ __forceinline__ int2 unpack_int2(double v) {
   return make_int2((int)(b & 0xffffffffll), (int)(b >> 32));
 }
 
-// RW = 10: compact record (unit quaternion of R, t, w kappa, w tau,
-// {other, edge|tail}) — 80 B, five 16-B parts; the gathers rebuild R from the
-// quaternion (R R^T = I to rounding, as the preconditioner assumes).
+// RW = 10: compact record (unit quaternion of R, t, w kappa, +-w tau) — 72 B
+// in HBM (GS = 9 doubles), the sign bit of w tau is the tail flag (w tau >= 0;
+// a zero weight is +-0.0), the other endpoint in Dev::rec_o (4 B): 76 B per
+// incidence. In registers (and the resident round's LDS copy) it is the
+// 10-word form (..., w tau, {other, tail << 31}), five 16-B parts; the gathers
+// rebuild R from the quaternion (R R^T = I to rounding, as the preconditioner
+// assumes).
 // RW = 16: full record (R, t, w kappa, w tau, {other, edge|tail}, pad), for
 // measurement rotations off SO(3).
+struct alignas(8) DPair {  // two doubles at 8-B alignment (a 72-B record's parts)
+  double x, y;
+};
 template <int RW>
 struct Rec {
-  static constexpr int Q = RW / 2;        // 16-B parts
+  static constexpr int Q = RW / 2;        // 16-B parts in registers
+  static constexpr int GS = RW == 10 ? 9 : 16;  // doubles per record in HBM
   static constexpr int WK = RW == 10 ? 7 : 12;  // index of w kappa (w tau follows)
-  __device__ static __forceinline__ void load(const double* base, size_t k, double2 q[Q]) {
-    const double2* q2 = reinterpret_cast<const double2*>(base + (size_t)RW * k);
+  __device__ static __forceinline__ void load(const Dev& d, size_t k, double2 q[Q]) {
+    if constexpr (RW == 10) {
+      const double* p = d.rec + (size_t)GS * k;
+      const DPair* p2 = reinterpret_cast<const DPair*>(p);
 #pragma unroll
-    for (int i = 0; i < Q; ++i) q[i] = q2[i];
+      for (int i = 0; i < 4; ++i) {
+        const DPair v = p2[i];
+        q[i] = make_double2(v.x, v.y);
+      }
+      const double wt = p[8];
+      const long long bits = (long long)(unsigned)d.rec_o[k] | (std::signbit(wt) ? (1ll << 63) : 0ll);
+      q[4] = make_double2(std::fabs(wt), __longlong_as_double(bits));
+    } else {
+      const double2* q2 = reinterpret_cast<const double2*>(d.rec + (size_t)GS * k);
+#pragma unroll
+      for (int i = 0; i < Q; ++i) q[i] = q2[i];
+    }
+  }
+  // the stored w tau of an incidence (compact: its sign is the tail flag)
+  __device__ static __forceinline__ double wt_word(double wt, bool tail) {
+    return (RW == 10 && tail) ? -wt : wt;
   }
   __device__ static __forceinline__ void edge(const double2 q[Q], Edge& E) {
     if constexpr (RW == 10) {
@@ -613,7 +639,7 @@ __device__ __forceinline__ bool hinc_gather_src(const Dev& d, const Lane& L, Src
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
   // clamped, unconditional record loads (the pad record keeps an empty tile
   // at the end of the array inside it)
-  auto ld = [&](int c0, double2* q) { RC::load(d.rec, (size_t)(K0 + max(min(c0 + lt, n - 1), 0)), q); };
+  auto ld = [&](int c0, double2* q) { RC::load(d, (size_t)(K0 + max(min(c0 + lt, n - 1), 0)), q); };
   double2 q[RC::Q];
   if constexpr (REC_FIRST) ld(0, q);
   if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
@@ -733,7 +759,7 @@ __device__ __forceinline__ void hinc_grad(const Dev& d, const Lane& L, const dou
   const int lt = min(tid, CH - 1);
   acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
   double csum = 0.0;
-  auto ld = [&](int c0, double2* q) { RC::load(d.rec, (size_t)(K0 + max(min(c0 + lt, n - 1), 0)), q); };
+  auto ld = [&](int c0, double2* q) { RC::load(d, (size_t)(K0 + max(min(c0 + lt, n - 1), 0)), q); };
   double2 q[RC::Q];
   ld(0, q);  // in flight with the CSR offsets and the tile's rows
   if (tid <= np) sptr[tid] = d.inc_ptr[p0 + tid] - K0;
@@ -815,7 +841,7 @@ __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, co
   double cost = 0.0;
   for (int k = tid; k < n; k += BLOCK) {
     double2 q[RC::Q];
-    RC::load(d.rec, (size_t)(K0 + k), q);
+    RC::load(d, (size_t)(K0 + k), q);
     const int2 in = RC::inc(q);
     const int o = in.x;
     const bool tail = (in.y >> 31) & 1;
@@ -1291,7 +1317,7 @@ __device__ __forceinline__ void pose_precond(const Dev& d, int pose) {
   for (int i = 0; i < 16; ++i) A[i] = Dq[i] = 0.0;
   for (int k = d.inc_ptr[pose]; k < d.inc_ptr[pose + 1]; ++k) {
     double2 q[Rec<RW>::Q];
-    Rec<RW>::load(d.rec, (size_t)k, q);
+    Rec<RW>::load(d, (size_t)k, q);
     Edge E;
     Rec<RW>::edge(q, E);
     const bool tail = (Rec<RW>::inc(q).y >> 31) & 1;
@@ -2643,7 +2669,6 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
   using SM = SmemRes<R, W>;
   __shared__ Ctl cs;
   __shared__ ResShared rsh;
-  ResStep& rst = rsh.st;
   int& sflag = rsh.flag;
   unsigned b = 0;
   bool any;
@@ -2694,9 +2719,13 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
   // the tile's records and CSR offsets, for every tCG step's gather (the host
   // keeps a resident tile within two chunks)
   {
-    const double2* src2 = reinterpret_cast<const double2*>(d.rec + (size_t)RW * L.k0);
-    double2* dst2 = reinterpret_cast<double2*>(recs);
-    for (int i = threadIdx.x; i < L.n * (RW / 2); i += blockDim.x) dst2[i] = src2[i];
+    double2* dst2 = reinterpret_cast<double2*>(recs);  // the register form, 16-B parts
+    for (int i = threadIdx.x; i < L.n; i += blockDim.x) {
+      double2 q[Rec<RW>::Q];
+      Rec<RW>::load(d, (size_t)(L.k0 + i), q);
+#pragma unroll
+      for (int j = 0; j < Rec<RW>::Q; ++j) dst2[(size_t)i * Rec<RW>::Q + j] = q[j];
+    }
     if (threadIdx.x <= L.np) sptr[threadIdx.x] = d.inc_ptr[L.p0 + threadIdx.x] - L.k0;
   }
   const int ph0 = cs.phase;  // (read before any barrier of this launch: every thread sees k_begin's value)
@@ -2969,7 +2998,7 @@ __device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned*
     using RC = Rec<RW>;
     for (int kk = tid; kk < n; kk += 64 * W) {
       double2 q[RC::Q];
-      RC::load(d.rec, (size_t)(K0 + kk), q);
+      RC::load(d, (size_t)(K0 + kk), q);
       const int2 in = RC::inc(q);
       const int ot = in.x;
       const bool tail = (in.y >> 31) & 1;
@@ -3084,7 +3113,7 @@ __device__ __forceinline__ void gnc_edge(const Dev& d, int i, int R_, double mu)
   const double* Xj = en.y >= 0 ? d.X + (size_t)en.y * ps : d.pub + (size_t)(-1 - en.y) * ps;
   const int2 ip = d.eipos[e];
   double2 q[Rec<RW>::Q];
-  Rec<RW>::load(d.rec, (size_t)(ip.x >= 0 ? ip.x : ip.y), q);
+  Rec<RW>::load(d, (size_t)(ip.x >= 0 ? ip.x : ip.y), q);
   Edge E;
   Rec<RW>::edge(q, E);
   double sR = 0.0, sT = 0.0;
@@ -3109,8 +3138,9 @@ __device__ __forceinline__ void gnc_edge(const Dev& d, int i, int R_, double mu)
   d.ew[e] = w;
   const double wk = w * d.ekappa[e], wt = w * d.etau[e];
   constexpr int WK = Rec<RW>::WK;
-  if (ip.x >= 0) { d.rec[(size_t)RW * ip.x + WK] = wk; d.rec[(size_t)RW * ip.x + WK + 1] = wt; }
-  if (ip.y >= 0) { d.rec[(size_t)RW * ip.y + WK] = wk; d.rec[(size_t)RW * ip.y + WK + 1] = wt; }
+  constexpr int GS = Rec<RW>::GS;  // ip.x: the tail's record, ip.y: the head's
+  if (ip.x >= 0) { d.rec[(size_t)GS * ip.x + WK] = wk; d.rec[(size_t)GS * ip.x + WK + 1] = Rec<RW>::wt_word(wt, true); }
+  if (ip.y >= 0) { d.rec[(size_t)GS * ip.y + WK] = wk; d.rec[(size_t)GS * ip.y + WK + 1] = Rec<RW>::wt_word(wt, false); }
 }
 
 __device__ __forceinline__ void begin_robot(const Dev& d, const unsigned char* active, int l) {
@@ -3183,8 +3213,9 @@ __global__ void k_apply_weights(Dev d, int mloc) {
   const double wk = w * d.ekappa[e], wt = w * d.etau[e];
   const int2 ip = d.eipos[e];
   constexpr int WK = Rec<RW>::WK;
-  if (ip.x >= 0) { d.rec[(size_t)RW * ip.x + WK] = wk; d.rec[(size_t)RW * ip.x + WK + 1] = wt; }
-  if (ip.y >= 0) { d.rec[(size_t)RW * ip.y + WK] = wk; d.rec[(size_t)RW * ip.y + WK + 1] = wt; }
+  constexpr int GS = Rec<RW>::GS;  // ip.x: the tail's record, ip.y: the head's
+  if (ip.x >= 0) { d.rec[(size_t)GS * ip.x + WK] = wk; d.rec[(size_t)GS * ip.x + WK + 1] = Rec<RW>::wt_word(wt, true); }
+  if (ip.y >= 0) { d.rec[(size_t)GS * ip.y + WK] = wk; d.rec[(size_t)GS * ip.y + WK + 1] = Rec<RW>::wt_word(wt, false); }
 }
 
 // ------------------------------------------------------- public exchange ---
@@ -3520,6 +3551,7 @@ struct kmx_pgo {
   int* d_rtile0 = nullptr;
   int* d_inc_ptr = nullptr;
   double* d_rec = nullptr;
+  int* d_rec_o = nullptr;
   double *d_ekappa = nullptr, *d_etau = nullptr, *d_ew = nullptr;
   int2* d_eipos = nullptr;
   double* d_vec = nullptr;  // X Xt g r z hd eta, then the dhn tCG directions (nvec())
@@ -3670,7 +3702,7 @@ void free_xchg(kmx_pgo* h) {
 }
 
 void free_dev(kmx_pgo* h) {
-  void* ptrs[] = {h->d_tile, h->d_rtile0, h->d_inc_ptr, h->d_rec, h->d_ekappa,
+  void* ptrs[] = {h->d_tile, h->d_rtile0, h->d_inc_ptr, h->d_rec, h->d_rec_o, h->d_ekappa,
                   h->d_etau, h->d_ew, h->d_eipos, h->d_vec, h->d_S, h->d_Pinv, h->d_hD, h->d_hDS, h->d_pub, h->d_part,
                   h->d_ctl, h->d_cnt, h->d_m_robot, h->d_n_robot, h->d_pub_src, h->d_own_src,
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
@@ -3682,6 +3714,7 @@ void free_dev(kmx_pgo* h) {
   h->d_tile = nullptr;
   h->d_rtile0 = h->d_inc_ptr = nullptr;
   h->d_rec = h->d_ekappa = h->d_etau = h->d_ew = nullptr;
+  h->d_rec_o = nullptr;
   h->d_eipos = nullptr;
   h->d_vec = h->d_S = h->d_Pinv = h->d_hD = h->d_hDS = h->d_pub = h->d_part = nullptr;
   h->d_ctl = nullptr;
@@ -4392,19 +4425,27 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   std::vector<int> inc_ptr(nloc + 1, 0);
   for (int i = 0; i < nloc; ++i) inc_ptr[i + 1] = inc_ptr[i] + deg[i];
   h->ninc = inc_ptr[nloc];
-  std::vector<double> rec((size_t)(h->ninc + 1) * RW, 0.0);  // + one zero pad record
+  const int GS = RW == 10 ? 9 : 16;  // Rec<RW>::GS
+  std::vector<double> rec((size_t)(h->ninc + 1) * GS, 0.0);  // + one zero pad record
+  std::vector<int> rec_o(RW == 10 ? h->ninc + 1 : 1, 0);
   std::vector<int2> eipos(std::max(h->mloc, 1), make_int2(-1, -1));
   std::vector<int> fill(inc_ptr.begin(), inc_ptr.end() - 1);
   auto put_rec = [&](int pos, int k, int64_t e, int other, int code) {
-    double* c = &rec[(size_t)pos * RW];
+    double* c = &rec[(size_t)pos * GS];
     const double* Q = RW == 10 ? &quat[4 * (size_t)k] : R + 9 * e;
     int j = 0;
     for (int q = 0; q < (RW == 10 ? 4 : 9); ++q) c[j++] = Q[q];
     for (int q = 0; q < 3; ++q) c[j++] = t[3 * e + q];
     c[j++] = weight[e] * kappa[e];
-    c[j++] = weight[e] * tau[e];
-    const long long bits = (long long)(unsigned)other | ((long long)code << 32);
-    std::memcpy(&c[j], &bits, 8);
+    const double wt = weight[e] * tau[e];
+    if (RW == 10) {  // compact: the tail flag in w tau's sign bit, the other endpoint apart
+      c[j++] = (code & 0x80000000) ? -wt : wt;
+      rec_o[pos] = other;
+    } else {
+      c[j++] = wt;
+      const long long bits = (long long)(unsigned)other | ((long long)code << 32);
+      std::memcpy(&c[j], &bits, 8);
+    }
   };
   for (int k = 0; k < h->mloc; ++k) {  // increasing global edge id per pose
     const int64_t e = ledges[k];
@@ -4555,7 +4596,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   int rc;
   const size_t vec = (size_t)std::max(nloc, 1) * ps;
   if ((rc = dalloc(&h->d_tile, h->ntiles)) || (rc = dalloc(&h->d_rtile0, L + 1)) ||
-      (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_rec, rec.size())) ||
+      (rc = dalloc(&h->d_inc_ptr, nloc + 1)) || (rc = dalloc(&h->d_rec, rec.size())) || (rc = dalloc(&h->d_rec_o, rec_o.size())) ||
       (rc = dalloc(&h->d_ekappa, ek_h.size())) || (rc = dalloc(&h->d_etau, et_h.size())) ||
       (rc = dalloc(&h->d_ew, ew_h.size())) || (rc = dalloc(&h->d_eipos, eipos.size())) ||
       (rc = dalloc(&h->d_vec, vec * nvec(h))) || (rc = dalloc(&h->d_S, (size_t)std::max(nloc, 1) * 6)) ||
@@ -4589,6 +4630,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   KMX_HIP(up(h->d_rtile0, rt0.data(), sizeof(int) * rt0.size()));
   KMX_HIP(up(h->d_inc_ptr, inc_ptr.data(), sizeof(int) * inc_ptr.size()));
   KMX_HIP(up(h->d_rec, rec.data(), sizeof(double) * rec.size()));
+  KMX_HIP(up(h->d_rec_o, rec_o.data(), sizeof(int) * rec_o.size()));
   KMX_HIP(up(h->d_ekappa, ek_h.data(), sizeof(double) * ek_h.size()));
   KMX_HIP(up(h->d_etau, et_h.data(), sizeof(double) * et_h.size()));
   KMX_HIP(up(h->d_ew, ew_h.data(), sizeof(double) * ew_h.size()));
@@ -4643,7 +4685,7 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   d = Dev{};
   d.ntiles = h->ntiles; d.L = L; d.nloc = nloc; d.npub = (int)h->npub;
   d.tile = h->d_tile; d.rtile0 = h->d_rtile0;
-  d.inc_ptr = h->d_inc_ptr; d.rec = h->d_rec;
+  d.inc_ptr = h->d_inc_ptr; d.rec = h->d_rec; d.rec_o = h->d_rec_o;
   d.ekappa = h->d_ekappa; d.etau = h->d_etau; d.ew = h->d_ew; d.eipos = h->d_eipos;
   d.X = h->d_vec; d.Xt = h->d_vec + vec; d.g = h->d_vec + 2 * vec; d.r = h->d_vec + 3 * vec;
   d.z = h->d_vec + 4 * vec; d.hd = h->d_vec + 5 * vec; d.eta = h->d_vec + 6 * vec; d.dh = h->d_vec + 7 * vec;
@@ -5414,7 +5456,8 @@ extern "C" int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_byt
   KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
   const int64_t L = (int64_t)h->robots.size(), n = std::max(h->nloc, 1), ps = 4 * h->P.r;
   int64_t b = 0;
-  b += (int64_t)(h->ninc + 1) * h->rw * 8 + (int64_t)(h->nloc + 1) * 4;  // records, CSR
+  const int rb = h->rw == 10 ? 9 * 8 + 4 : 128;  // bytes per incidence record (compact: 72 + the 4-B other endpoint)
+  b += (int64_t)(h->ninc + 1) * rb + (int64_t)(h->nloc + 1) * 4;         // records, CSR
   b += (int64_t)std::max(h->mloc, 1) * (3 * 8 + 8);                      // kappa, tau, w, positions
   b += n * ps * 8 * (int64_t)nvec(h) + n * (6 + SYM4 + SYM4) * 8;       // vectors, S, Pinv, D
   b += L * 8 * (int64_t)std::max(h->P.tcg_max_iterations, 1);            // tCG coefficients
@@ -5423,7 +5466,7 @@ extern "C" int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_byt
   b += (int64_t)std::max(h->n_gnc, 1) * 12 + (int64_t)h->scratch_cap * 8;  // GNC lists, scratch in use
   if (h->P.acceleration) b += 2 * n * ps * 8;                              // V, Y
   if (device_bytes) *device_bytes = b;
-  if (record_bytes) *record_bytes = h->rw * 8;
+  if (record_bytes) *record_bytes = rb;
   return KMX_OK;
 }
 
