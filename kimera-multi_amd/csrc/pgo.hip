@@ -622,9 +622,7 @@ struct NoPre {
 // would spill)
 // DIAG = false: the caller applies the diagonal block itself (k_step, whose
 // epilogue loads the own row and D_i with the rest of its rows in one batch).
-// DS: the diagonal block applied is D_i - S_i (hDS, k_hess: the tangent
-// correction -V S folded into it) instead of D_i.
-template <int R, int RW, bool REC_FIRST, typename Src, typename Pre, bool DIAG = true, int W = WAVES, bool DS = false>
+template <int R, int RW, bool REC_FIRST, typename Src, typename Pre, bool DIAG = true, int W = WAVES>
 __device__ __forceinline__ bool hinc_gather_src(const Dev& d, const Lane& L, Src& src, double acc[4], char* smem,
                                                 Pre&& pre) {
   using SM = SmemH<R, W>;
@@ -696,7 +694,7 @@ __device__ __forceinline__ bool hinc_gather_src(const Dev& d, const Lane& L, Src
 #if KMX_HESS_PROBE & 2  // traffic attribution build: no diagonal-block loads
     for (int c = 0; c < 16; ++c) D[c] = (c % 5 == 0) ? 1.0 : 0.0;
 #else
-    load_sym4((DS ? d.hDS : d.hD) + SYM4 * (size_t)L.pose, D);
+    load_sym4(d.hD + SYM4 * (size_t)L.pose, D);
 #endif
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -731,11 +729,11 @@ struct PlainRows {
 #endif
   }
 };
-template <int R, int RW, bool REC_FIRST = false, bool DS = false, typename Pre = NoPre>
+template <int R, int RW, bool REC_FIRST = false, bool DIAG = true, typename Pre = NoPre>
 __device__ __forceinline__ bool hinc_gather(const Dev& d, const Lane& L, const double* V, double acc[4],
                                             char* smem, Pre&& pre = Pre{}) {
   PlainRows<R> src{V};
-  return hinc_gather_src<R, RW, REC_FIRST, PlainRows<R>, Pre&, true, WAVES, DS>(d, L, src, acc, smem, pre);
+  return hinc_gather_src<R, RW, REC_FIRST, PlainRows<R>, Pre&, DIAG, WAVES>(d, L, src, acc, smem, pre);
 }
 
 // Gradient and cost, incidence-parallel. A lane evaluates its whole incidence
@@ -1586,9 +1584,9 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     // speculatively, so the robot sums' latency hides behind the gather
     bool go;
     if (d.p.early_stop) {
-      go = hinc_gather<R, RW, false, true>(d, L, d.z, H, smem, decide);
+      go = hinc_gather<R, RW, false, false>(d, L, d.z, H, smem, decide);
     } else {
-      hinc_gather<R, RW, false, true>(d, L, d.z, H, smem);
+      hinc_gather<R, RW, false, false>(d, L, d.z, H, smem);
       go = decide();
     }
     if (!go) return;
@@ -1598,34 +1596,45 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     // the phase test runs once the first chunk's records are in flight (a
     // robot out of tCG leaves before any row is gathered)
     const Ctl& c = d.ctl[L.l];
-    if (!hinc_gather<R, RW, true, true>(d, L, d.z, H, smem, [&]() { return c.phase == PH_TCG; })) return;
+    if (!hinc_gather<R, RW, true, false>(d, L, d.z, H, smem, [&]() { return c.phase == PH_TCG; })) return;
     tcg_iter = c.tcg_iter;
     beta = c.beta;
   }
-  const bool first = (tcg_iter == 0);
+  const bool first = (tcg_iter == 0) || (KMX_HESS_PROBE & 4);  // (probe 4: no delta_old / Hdelta_old traffic)
   asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
+  // every row the epilogue needs in one batch, one round trip after the gather:
+  // the own z row, D_i - S_i (the diagonal block with the tangent correction
+  // -z S folded in), delta_old and H delta_old
+  const int dhn = d.dhn;
+  double dold[4] = {0, 0, 0, 0}, hold[4] = {0, 0, 0, 0};
   if (L.valid) {
-#if KMX_HESS_PROBE & 2
+    double Dg[16];
+#if KMX_HESS_PROBE & 2  // traffic attribution build: no own-row / diagonal-block loads
     for (int k = 0; k < 4; ++k) zs[k] = 1e-3 * k;
+    for (int c = 0; c < 16; ++c) Dg[c] = (c % 5 == 0) ? 1.0 : 0.0;
 #else
     load4(d.z + o, zs);
+    load_sym4(d.hDS + SYM4 * (size_t)L.pose, Dg);
 #endif
+    if (!first) {
+      load4(d.dh + (size_t)((tcg_iter - 1) % dhn) * d.vec + o, dold);
+      load4(d.hd + o, hold);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)  // (hinc_gather_src's DIAG term, same expression)
+      H[c] += zs[0] * Dg[4 * c] + zs[1] * Dg[4 * c + 1] + zs[2] * Dg[4 * c + 2] + zs[3] * Dg[4 * c + 3];
   }
-  double hz[4];  // H z - z S (group_rhess before its projection): the gather applied D_i - S_i
+  double hz[4];  // H z - z S (group_rhess before its projection)
 #pragma unroll
   for (int k = 0; k < 4; ++k) hz[k] = H[k];
   (void)y;
   double v = 0.0;
   double dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0};
-  const int dhn = d.dhn;
   if (L.valid) {
-    if (first || (KMX_HESS_PROBE & 4)) {  // (probe 4: no delta_old / Hdelta_old traffic)
+    if (first) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) { dl[k] = -zs[k]; hdl[k] = -hz[k]; }
     } else {
-      double dold[4], hold[4];
-      load4(d.dh + (size_t)((tcg_iter - 1) % dhn) * d.vec + o, dold);
-      load4(d.hd + o, hold);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         dl[k] = -zs[k] + beta * dold[k];
