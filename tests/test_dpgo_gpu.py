@@ -77,6 +77,40 @@ def test_primitives_match_oracle(gpu, r, records):
             assert abs(gs - os_) <= 1e-10 * max(1.0, abs(os_)), (mode, gs, os_)
 
 
+@pytest.mark.parametrize("records", ["compact", "full"])
+def test_zero_weights_keep_incidence_direction(gpu, records):
+    """The compact record keeps the tail flag in w tau's sign bit (a zero weight
+    is -0.0 on the tail's record): edges set to weight exactly 0 and back to 1
+    through kmx_pgo_set_weights (k_apply_weights rewrites both records), with the
+    Hessian, gradient and whole rounds against the restatement after each change."""
+    g, P, X0 = _setup(robust=False)
+    if records == "full":
+        _full_records(g)
+    s, o = _pair(g, P, X0)
+    rng = np.random.default_rng(5)
+    w = np.ones(g.m)
+    w[rng.random(g.m) < 0.4] = 0.0  # tails and heads of private and shared edges alike
+    for wv in (w, np.ones(g.m), w):
+        s.set_weights(wv)
+        o.set_weights(wv)
+        s.refresh_local()
+        o.refresh()
+        for a in range(g.n_robots):
+            V = rng.standard_normal(X0[a].shape)
+            for mode in (abi.KMX_EVAL_COST_EGRAD, abi.KMX_EVAL_EHESS):
+                Vin = s.get_iterate(a) if mode == abi.KMX_EVAL_COST_EGRAD else V
+                gout, _ = s.eval(a, mode, Vin)
+                oout, _ = o.eval(a, mode, Vin)
+                assert np.abs(gout - oout).max() <= 1e-12 * max(1.0, np.abs(oout).max()), (records, mode)
+        sg, so = s.iterate(), o.iterate()
+        for a in range(g.n_robots):
+            assert sg[a]["tcg_iterations"] == so[a]["tcg_iterations"], (a, sg[a], so[a])
+            d = np.abs(s.get_iterate(a) - o.get_iterate(a)).max()
+            assert d <= 1e-6, (a, d)
+        assert np.array_equal(s.get_weights(), o.get_weights())
+    s.close()
+
+
 @pytest.mark.parametrize("robust,records", [(False, "compact"), (True, "compact"), (True, "full")])
 def test_rounds_match_oracle(gpu, robust, records):
     """compact: 76-B records (SO(3) input, rotation rebuilt from its quaternion); full: the
