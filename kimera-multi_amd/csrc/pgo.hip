@@ -5468,7 +5468,7 @@ extern "C" int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_byt
   const int rb = h->rw == 10 ? 9 * 8 + 4 : 128;  // bytes per incidence record (compact: 72 + the 4-B other endpoint)
   b += (int64_t)(h->ninc + 1) * rb + (int64_t)(h->nloc + 1) * 4;         // records, CSR
   b += (int64_t)std::max(h->mloc, 1) * (3 * 8 + 8);                      // kappa, tau, w, positions
-  b += n * ps * 8 * (int64_t)nvec(h) + n * (6 + SYM4 + SYM4) * 8;       // vectors, S, Pinv, D
+  b += n * ps * 8 * (int64_t)nvec(h) + n * (6 + 3 * SYM4) * 8;         // vectors, S, Pinv, D, D - S
   b += L * 8 * (int64_t)std::max(h->P.tcg_max_iterations, 1);            // tCG coefficients
   b += std::max<int64_t>(h->npub, 1) * (ps * 8 + 4) + n * 4;             // public table + maps
   b += (int64_t)h->ntiles * (NPART * 8 + 12 + (onesync(h) ? 64 : 0)) + L * (int64_t)(sizeof(Ctl) + 32);
