@@ -15,7 +15,7 @@ table (rows gathered once) and times rounds under:
          min(sent, received) rows, so the rows are the rank's own, not its
          peers' — timing only), all rounds from one iterate_async call
 The handle's tCG enqueueing is the default adaptive mode
-(kmx_pgo_set_tcg_poll(-1)).
+(kmx_pgo_set_tcg_poll(-1)); KMX_SEAM_POLL=0 / 1 sets blind / polled.
 usage: python scripts/host_seam.py N [rounds] [standard|onesync|resident]  (the tCG form)
 """
 import os
@@ -59,6 +59,8 @@ dev = torch.device("cuda", 0)
 def make():
     s = BlockSolver(P, 0)
     s.set_stream(torch.cuda.current_stream().cuda_stream)
+    if os.environ.get("KMX_SEAM_POLL"):  # tCG enqueue mode: -1 adaptive (default), 0 blind, 1 polled
+        s.set_tcg_poll(int(os.environ["KMX_SEAM_POLL"]))
     s.set_graph_data(g, local)
     s.set_gnc_schedule(True, P.robustOptInnerIters, P.robustOptNumWeightUpdates, P.relChangeTol)
     for a in range(lo, hi):
