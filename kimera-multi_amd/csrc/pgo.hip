@@ -1595,10 +1595,13 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
   } else {
     // the phase test runs once the first chunk's records are in flight (a
     // robot out of tCG leaves before any row is gathered)
+    // the robot's state (written by an earlier launch) loads with the first
+    // records, not after the gather's first barrier
     const Ctl& c = d.ctl[L.l];
-    if (!hinc_gather<R, RW, true, false>(d, L, d.z, H, smem, [&]() { return c.phase == PH_TCG; })) return;
+    const int ph = c.phase;
     tcg_iter = c.tcg_iter;
     beta = c.beta;
+    if (!hinc_gather<R, RW, true, false>(d, L, d.z, H, smem, [&]() { return ph == PH_TCG; })) return;
   }
   const bool first = (tcg_iter == 0) || (KMX_HESS_PROBE & 4);  // (probe 4: no delta_old / Hdelta_old traffic)
   asm volatile("" ::: "memory");  // keep the epilogue loads below the gather loop (VGPR pressure)
