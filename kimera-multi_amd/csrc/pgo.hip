@@ -1552,11 +1552,17 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     if (upd) rs.issue(d.part_u, 2, L.rt0, L.rt1);
     if (grad) rg.issue(d.part, NPART, L.rt0, L.rt1);
     const int ph0 = c0.phase;  // written by an earlier launch: uniform
-    if (ph0 != (grad ? PH_START : PH_TCG)) {  // uniform: a tile never straddles robots
+    const bool active = ph0 == (grad ? PH_START : PH_TCG);  // uniform: a tile never straddles robots
+    auto idle = [&]() {
       if (writer && threadIdx.x == 0) {
         d.ctl2[L.l] = c0;
         if (hs) post_status(hs, L.l, seq, false);
       }
+    };
+    // early (below): the phase test waits in the decision, so the first
+    // records load with the state instead of after it
+    if (!active && !d.p.early_stop) {
+      idle();
       return;
     }
     UpdStep u{0, 0, 0.0};
@@ -1565,6 +1571,10 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     // gradient is below tolerance) skips the gather, and the host sees the
     // stop at the start of the launch
     auto decide = [&]() {
+      if (!active) {
+        idle();
+        return false;
+      }
       double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
       if (upd) rs.finish(d.part_u, 2, rl, tot);
       if (grad) rg.finish(d.part, NPART, rl, tot);
@@ -1594,9 +1604,9 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     beta = u.beta;
   } else {
     // the phase test runs once the first chunk's records are in flight (a
-    // robot out of tCG leaves before any row is gathered)
-    // the robot's state (written by an earlier launch) loads with the first
-    // records, not after the gather's first barrier
+    // robot out of tCG leaves before any row is gathered); the robot's state
+    // (written by an earlier launch) loads with those records, not after the
+    // gather's first barrier
     const Ctl& c = d.ctl[L.l];
     const int ph = c.phase;
     tcg_iter = c.tcg_iter;
