@@ -47,13 +47,6 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "kimera-multi_amd"))
 
 PEAK_HBM = 8.0e12      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-# tCG form "auto": ROPTLIB's launched tCG at every shard size. The resident
-# round (one persistent launch per round; it fits shards up to 256 x 60 =
-# 15,360 poses at r = 5) measured level with it at the configs[3] N = 8 shard,
-# not faster (same box: 170.9 vs 169.4 us per round, 203.7 vs 198.3 with the
-# in-round exchange), so it stays opt-in
-# (--tcg-form resident); set this to 15_000 to pick it for small shards
-RESIDENT_MAX_POSES = 0
 PEAK_VALU_OPS = 78.6e12  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
 
 
@@ -75,10 +68,9 @@ def parse():
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3: timed rounds only")
     ap.add_argument("--tile-incidences", type=int, default=0,
                     help="incidences per workgroup tile (kmx_pgo_params.tile_incidences; 0: automatic)")
-    ap.add_argument("--tcg-form", choices=["auto", "standard", "onesync", "resident"], default="auto",
-                    help="tCG form (kmx_pgo_params.tcg_form): ROPTLIB's, the one-sync form launched per step, or "
-                         "the one-sync form as one persistent launch per round; auto = resident for shards of "
-                         f"<= {RESIDENT_MAX_POSES} poses per GPU (0: never), else standard")
+    ap.add_argument("--tcg-form", choices=["auto", "standard", "onesync"], default="auto",
+                    help="tCG form (kmx_pgo_params.tcg_form): ROPTLIB's, or the one-sync form launched per step "
+                         "(opt-in); auto = standard at every shard size (DESIGN.md section 10)")
     ap.add_argument("--lcd-frames", type=int, default=50_000)
     ap.add_argument("--lcd-steps", type=int, default=8,
                     help="back-to-back LCD verification calls timed (a call's kNN2 overlaps the previous call's "
@@ -667,7 +659,6 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
         hv_ms, hv_bytes, hv_n = r["hessvec_ms_total"], r["hessvec_alg_bytes"], r["hessvec_launches"]
         same = all(r[k] == c[k] for k in ("edges_iters", "hessvecs", "block_updates", "gnc_updates"))
     xs, xr = drv.exchange_rows
-    res_info = drv.solver.resident_info() if P.localOptimizationParams.tCG_form == "resident" else None
     native = bool(drv.native)
     mode = drv.exchange_mode
     mem = drv.solver.memory()[0]
@@ -684,7 +675,7 @@ def dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, steps, barrier, repl
             "el": tot[0], "edges_iters": tot[1], "hessvecs": tot[2], "block_updates": tot[3],
             "gnc_updates": int(tot[4]), "hv": (tot[5], tot[6], int(tot[7])), "xrows": (int(tot[8]), int(tot[9])),
             "mem_max": int(tot[10]), "replay_identical": (tot[11] == world) if replay and snap is not None else None,
-            "snap": snap, "native": native, "exchange": mode, "drv": drv, "resident": res_info}
+            "snap": snap, "native": native, "exchange": mode, "drv": drv}
 
 
 def main():
@@ -720,7 +711,7 @@ def main():
     g, X0 = make_workload(args.config, world, headline)
     gen_s = time.perf_counter() - t_gen
     if args.tcg_form == "auto":
-        args.tcg_form = "resident" if g.n_total / world <= RESIDENT_MAX_POSES else "standard"
+        args.tcg_form = "standard"
     P.localOptimizationParams.tCG_form = args.tcg_form
     want_cpu = rank == 0 and world == 1 and not args.no_cpu and not args.profile
     leg = dpgo_leg(g, X0, P, args, rank, world, local_rank, dist, args.steps, barrier,
@@ -774,7 +765,6 @@ def main():
                               if world > 1 else ""),
             "exchange_rows_per_round": {"sent_max": leg["xrows"][0], "recv_max": leg["xrows"][1],
                                         "recv_bytes_max": leg["xrows"][1] * ps_bytes},
-            "resident_round": leg["resident"],
             "graph_gen_s": round(gen_s, 1),
             "device_bytes_per_gpu": leg["mem_max"],
         },

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KMX_ABI_VERSION 7
+#define KMX_ABI_VERSION 8
 
 /* error codes */
 #define KMX_OK 0
@@ -92,9 +92,9 @@ typedef struct kmx_pgo_params {
                                reductions per step; KMX_TCG_FORM_ONESYNC (1): opt-in, one
                                reduction and one kernel per step, the
                                neighbours' new direction formed from gathered z, M^-1 H delta
-                               and delta; parity with the standard form at convergence only;
-                               KMX_TCG_FORM_RESIDENT (2): the one-sync arithmetic, one
-                               persistent launch per round (small shards; see below)      */
+                               and delta; parity with the standard form at convergence only
+                               (2, ABI 7's persistent resident round, was removed in ABI 8:
+                               level with these forms)              */
   double rgd_stepsize;      /* RGD: X <- Retr_X(-s * precon(grad f)) (1e-3)              */
   int tile_incidences;      /* incidences per workgroup tile (0: from the handle's local
                                problem, 180..2 chunks; the tile cut orders the per-robot
@@ -122,17 +122,6 @@ typedef struct kmx_iter_stats {
 
 #define KMX_TCG_FORM_STANDARD 0
 #define KMX_TCG_FORM_ONESYNC 1
-/* The one-sync tCG's arithmetic with the whole block update (gradient, every
- * tCG step, trial point, trial cost, accept and commit) in ONE persistent
- * launch per round: each workgroup keeps its tile's rows in registers and LDS
- * for the round, and the one reduction per tCG step crosses workgroups through
- * a grid barrier (write-through stores, no kernel boundary). For small shards
- * (the strong-scaling regime: the tiles must all be resident, one workgroup
- * per CU: about 15k poses per GPU at r = 5) with rtr_iterations 1 and RTR and
- * tcg_max_iterations <= 61; otherwise the handle runs
- * the launched one-sync form (1) on the same tile cut, with the same results
- * bit for bit (kmx_pgo_resident_info says which ran and why). */
-#define KMX_TCG_FORM_RESIDENT 2
 
 #define KMX_TCG_NONE 0
 #define KMX_TCG_NEGATIVE_CURVATURE 1
@@ -286,14 +275,6 @@ int kmx_pgo_sync_timeout(kmx_pgo* h, double timeout_s);
  * poses, incidences, block index, first tile of its robot — of the last launch
  * that formed step 2. KMX_EUNSUP otherwise. */
 int kmx_pgo_debug_step_stamps(uint64_t* out, int64_t n);
-
-/* KMX_TCG_FORM_RESIDENT: whether the handle runs its rounds as one persistent
- * launch (*resident = 1) or as the launched one-sync form (0), the tiles of the
- * cut (*ntiles) against the workgroups the device keeps resident for that
- * kernel (*capacity), and in `reason` (nbytes incl. the terminating NUL) why
- * not when it does not. Decided at set_graph (occupancy query + a one-time
- * census launch that checks every workgroup is co-resident). */
-int kmx_pgo_resident_info(kmx_pgo* h, int* resident, int* ntiles, int* capacity, char* reason, int64_t nbytes);
 
 /* GNC: `updateMeasurementWeights()` (drawio:2215) for every non-fixed edge with
  * a local endpoint, evaluated at the current iterate and neighbour table, then

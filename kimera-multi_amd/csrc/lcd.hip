@@ -29,6 +29,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <random>
 #include <thread>
 #include <string>
@@ -152,6 +153,109 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const 
   extern __shared__ __attribute__((aligned(16))) uint32_t sm_u32[];
   if (norm == KMX_NORM_HAMMING) knn2_body<true>(desc, nfeat, N, cq, cm, lowe, pairs, Kout, sm_u32);
   else knn2_body<false>(desc, nfeat, N, cq, cm, lowe, pairs, Kout, sm_u32);
+}
+
+// kNN2 of a small synchronous call (the reference's verification thread
+// matches ONE candidate per call: computeMatchedIndices, drawio:2583-2586).
+// k_knn2 gives a candidate one workgroup, whose 4 waves scan every match
+// descriptor for their queries (~65 us on one CU at N = 500). Here a
+// candidate's queries are split over S = ceil(N / 64) workgroups of 64
+// queries, and each query's match set over the workgroup's 4 waves: wave w
+// keeps the two nearest keys of its quarter, and the four pairs are merged.
+// A key is (distance << 10 | match index), unique per match, so the two
+// smallest keys of the union are the serial scan's (d0, j0, d1) whatever
+// the quarter boundaries. The last workgroup of a candidate to finish (an
+// agent-scope counter; its writers fence first) compacts the per-query
+// results in query order into k_knn2's pair rows: the same rows, the same K.
+constexpr int KS_Q = 64;  // queries per workgroup of k_knn2s
+template <bool HAMMING>
+__global__ __launch_bounds__(KNN_BLOCK) void k_knn2s(const uint32_t* desc, const int* nfeat, int N, const int* cq,
+                                                     const int* cm, double lowe, int2* pairs, int* Kout, int* qbest,
+                                                     unsigned* cnt, int S) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm_u32[];
+  uint32_t* sdesc = sm_u32;                                        // [nm][8]
+  uint32_t* mk = sm_u32 + (size_t)N * 8;                           // [4][KS_Q][2] the quarters' keys
+  int* scnt = reinterpret_cast<int*>(mk + 4 * KS_Q * 2);           // [KNN_BLOCK + 1]
+  __shared__ int last;
+  const int c = blockIdx.x / S, s = blockIdx.x - c * S;
+  const int q = cq[c], m = cm[c];
+  const int nq = nfeat[q], nm = nfeat[m];
+  const int tid = threadIdx.x, ql = tid & (KS_Q - 1), part = tid >> 6;
+  const int qi = s * KS_Q + ql;
+  int* qb = qbest + (size_t)c * N;
+  if (s * KS_Q < nq && nm >= 2) {
+    const uint32_t* dm = desc + (size_t)m * N * 8;
+    for (int i = tid; i < nm * 8; i += KNN_BLOCK) sdesc[i] = dm[i];
+    __syncthreads();
+    uint32_t k0 = 0xffffffffu, k1 = 0xffffffffu;
+    if (qi < nq) {
+      uint32_t a[8];
+      const uint32_t* dq = desc + ((size_t)q * N + qi) * 8;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) a[w] = dq[w];
+      const int j0 = part * nm / 4, j1 = (part + 1) * nm / 4;
+      for (int j = j0; j < j1; ++j) {
+        const uint4* b4 = reinterpret_cast<const uint4*>(sdesc + j * 8);
+        const uint4 x = b4[0], y = b4[1];
+        const uint32_t b[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        uint32_t d = 0;
+        if constexpr (HAMMING) {
+#pragma unroll
+          for (int w = 0; w < 8; ++w) d += __popc(a[w] ^ b[w]);
+        } else {
+#pragma unroll
+          for (int w = 0; w < 8; ++w) d = __builtin_amdgcn_sad_u8(a[w], b[w], d);
+        }
+        two_nearest(k0, k1, (d << 10) | (uint32_t)j);
+      }
+    }
+    mk[(part * KS_Q + ql) * 2] = k0;
+    mk[(part * KS_Q + ql) * 2 + 1] = k1;
+    __syncthreads();
+    if (part == 0 && qi < nq) {
+#pragma unroll
+      for (int p = 1; p < 4; ++p) {
+        two_nearest(k0, k1, mk[(p * KS_Q + ql) * 2]);
+        two_nearest(k0, k1, mk[(p * KS_Q + ql) * 2 + 1]);
+      }
+      const int d0 = (int)(k0 >> 10), d1 = (int)(k1 >> 10);
+      const bool pass = (double)(float)d0 < lowe * (double)(float)d1;
+      qb[qi] = pass ? (int)(k0 & 1023u) : -1;
+    }
+  } else if (part == 0 && qi < nq) {
+    qb[qi] = -1;  // fewer than two match features: no pair (k_knn2's nm >= 2 test)
+  }
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(cnt + c, 1u) == (unsigned)(S - 1);
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // compaction in query order (k_knn2's per-thread ranges and prefix sum)
+  const int per = (nq + KNN_BLOCK - 1) / KNN_BLOCK;
+  const int i0 = tid * per, i1 = min(nq, i0 + per);
+  int found = 0;
+  for (int i = i0; i < i1; ++i) found += __hip_atomic_load(qb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 0;
+  scnt[tid] = found;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int t = 0; t < KNN_BLOCK; ++t) {
+      const int v = scnt[t];
+      scnt[t] = acc;
+      acc += v;
+    }
+    scnt[KNN_BLOCK] = acc;
+    cnt[c] = 0u;  // the next call's count starts at zero
+  }
+  __syncthreads();
+  int pos = scnt[tid];
+  int2* out = pairs + (size_t)c * N;
+  for (int i = i0; i < i1; ++i) {
+    const int j = __hip_atomic_load(qb + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (j >= 0) out[pos++] = make_int2(i, j);
+  }
+  if (tid == 0) Kout[c] = scnt[KNN_BLOCK];
 }
 
 // --------------------------------------------------- small linear algebra --
@@ -696,6 +800,23 @@ struct CoopWS {
   int nr, ok;
   signed char t11[10][2][2], t21[20][3][2];  // LDS copies of T11 / T21
 };
+// The Stewenius kernels' workspace: what the null space, the system and the
+// recovery tail use (coop_system writes the 10 x 20 system straight into the
+// wave's global stash, where the batched Gauss-Jordan reads it, and the
+// Sturm / model areas are Nister's), 2.2 KB against CoopWS's 4.7 KB, so that
+// with the batch (StewBatch) a wave stays below 10 KB of LDS: four waves per
+// SIMD fit in the CU's 160 KB.
+struct CoopWSS {
+  double f1[15], f2[15];
+  double N[4][9];
+  double vs[5][9];
+  double c2[3][10];
+  double EEt[9][10];
+  double tr[10];
+  double bestm[12];
+  int ok;
+  signed char t11[10][2][2], t21[20][3][2];
+};
 
 // The block is one wavefront and a wave's LDS operations complete in issue
 // order, so lane-to-lane hand-offs through LDS need only a compiler barrier
@@ -742,7 +863,8 @@ __device__ __forceinline__ double wave_fmax(double v) {  // exact in any order
 // (column j in 9 consecutive lanes); the column norms and the reflector are
 // formed from readlane broadcasts in the serial order, each d_j from a
 // 9-term gather of column j. Then the 4 back-substitutions (lanes 0-3).
-__device__ void coop_nullspace(CoopWS& w, int lane) {
+template <typename WS>
+__device__ void coop_nullspace(WS& w, int lane) {
   lane = fresh_lane(lane);
   const int li = lane % 9, lj = lane / 9;  // lanes >= 45 carry a dummy column
   double a = (lane < 45) ? w.f1[3 * lj + li / 3] * w.f2[3 * lj + li % 3] : 0.0;
@@ -815,7 +937,8 @@ __constant__ signed char T21[20][3][2] = {
     {{8, 3}, {9, 2}, {-1, -1}},   {{9, 3}, {-1, -1}, {-1, -1}}};
 // Coefficient k of mul11(E_ea, E_eb) / mul21(a, E_eb), E_e[c] = N[c][e]:
 // the terms of the serial loop in its (i, j) order (LDS copies of T11 / T21).
-__device__ __forceinline__ double mul11_e(const CoopWS& w, int ea, int eb, int k) {
+template <typename WS>
+__device__ __forceinline__ double mul11_e(const WS& w, int ea, int eb, int k) {
   double s = 0.0;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -824,7 +947,8 @@ __device__ __forceinline__ double mul11_e(const CoopWS& w, int ea, int eb, int k
   }
   return s;
 }
-__device__ __forceinline__ double mul21_e(const double* a, const CoopWS& w, int eb, int k) {
+template <typename WS>
+__device__ __forceinline__ double mul21_e(const double* a, const WS& w, int eb, int k) {
   double s = 0.0;
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
@@ -834,7 +958,10 @@ __device__ __forceinline__ double mul21_e(const double* a, const CoopWS& w, int 
   return s;
 }
 
-__device__ void coop_system(CoopWS& w, int lane) {
+// The system goes to A (row-major 10 x 20): w.A for Nister, the wave's global
+// stash for the batched Stewenius Gauss-Jordan.
+template <typename WS>
+__device__ void coop_system(WS& w, int lane, double* A) {
   lane = fresh_lane(lane);
   // EEt[ij][k] = sum_l mul11(E[i*3+l], E[j*3+l])[k] (l = 0, 1, 2 in order); c2 for row 9:
   // c2_q = mul11(E_a, E_b) - mul11(E_c, E_d), (a, b, c, d) = (4,8,5,7), (3,8,5,6), (3,7,4,6)
@@ -866,7 +993,7 @@ __device__ void coop_system(CoopWS& w, int lane) {
       r -= mul21_e(w.c2[1], w, 1, k);
       r += mul21_e(w.c2[2], w, 2, k);
     }
-    w.A[row][k] = r;
+    A[row * 20 + k] = r;
   }
   wsync();
 }
@@ -1503,9 +1630,21 @@ __device__ void grp_hessenberg(StewBatch& sb, int lane, bool on) {
 // double QR step are one lane per column / row. Eigenvalues to sb.wr / sb.wi
 // (a complex pair: wi(na) = +, wi(en) = -); sb.ok[g] = 0 when the group's
 // 30 n sweeps ran out.
+// ONE: only group 0 works (a batch of one hypothesis: the spread form's lone
+// waves): the broadcasts are readlanes of group 0's lanes (scalar, no LDS
+// round trip) and every search reads group 0's ballot bits, so the source
+// lanes are wave-uniform; the other groups' lanes compute nothing that is
+// kept. The same operations on the same values: the same bits.
+template <bool ONE, int SRC>
+__device__ __forceinline__ double hq_bc(double v, int g) {
+  if constexpr (ONE) return rdlane(v, SRC);
+  else return grp_bcast_c<SRC>(v, g);
+}
+template <bool ONE = false>
 __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
   lane = fresh_lane(lane);
   const int g = lane / GL, gl = lane - g * GL;
+  const int gs = ONE ? 0 : g;  // the group whose ballot bits a search reads
   double (*h)[10] = sb.H[g < SG ? g : 0];
   const int n = 10;
   double norm = 0.0;
@@ -1524,7 +1663,7 @@ __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
       const double tst1 = s, tst2 = tst1 + fabs(h[gl][gl - 1]);
       hit = tst2 == tst1;
     }
-    int l = grp_top(hit, g);
+    int l = grp_top(hit, gs);
     if (l < 0) l = 0;
     bool sweep = false;
     double x = 0.0, y = 0.0, wv = 0.0;
@@ -1604,9 +1743,18 @@ __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
         stop = tst2 == tst1;
       }
     }
-    int m = grp_top(stop, g);  // lane l always stops
+    int m = grp_top(stop, gs);  // lane l always stops
     if (m < 0) m = 0;
-    double p = grp_bcast(pm, g, m), q = grp_bcast(qm, g, m), r = grp_bcast(rm, g, m), zz = 0.0;
+    double p, q, r, zz = 0.0;
+    if constexpr (ONE) {
+      p = rdlane(pm, m);
+      q = rdlane(qm, m);
+      r = rdlane(rm, m);
+    } else {
+      p = grp_bcast(pm, g, m);
+      q = grp_bcast(qm, g, m);
+      r = grp_bcast(rm, g, m);
+    }
     wsync();
     if (sweep && gl >= m + 2 && gl <= en) {
       h[gl][gl - 2] = 0.0;
@@ -1627,9 +1775,9 @@ __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
           go = false;
         } else {  // p / x, q / x, r / x: one quotient per lane 0-2 of the group, broadcast
           const double quo = (gl == 0 ? p : gl == 1 ? q : r) / x;
-          p = grp_bcast_c<0>(quo, g);
-          q = grp_bcast_c<1>(quo, g);
-          r = grp_bcast_c<2>(quo, g);
+          p = hq_bc<ONE, 0>(quo, g);
+          q = hq_bc<ONE, 1>(quo, g);
+          r = hq_bc<ONE, 2>(quo, g);
         }
       }
       double s = 0.0;
@@ -1648,11 +1796,11 @@ __device__ void grp_hqr(StewBatch& sb, int lane, bool on) {
       if (go) {  // p / s, q / s, r / s, q / p, r / p: lanes 0-4 of the group, broadcast
         p = p + s;
         const double quo = (gl == 0 ? p : gl == 1 || gl == 3 ? q : r) / (gl < 3 ? s : p);
-        x = grp_bcast_c<0>(quo, g);
-        y = grp_bcast_c<1>(quo, g);
-        zz = grp_bcast_c<2>(quo, g);
-        q = grp_bcast_c<3>(quo, g);
-        r = grp_bcast_c<4>(quo, g);
+        x = hq_bc<ONE, 0>(quo, g);
+        y = hq_bc<ONE, 1>(quo, g);
+        zz = hq_bc<ONE, 2>(quo, g);
+        q = hq_bc<ONE, 3>(quo, g);
+        r = hq_bc<ONE, 4>(quo, g);
       }
       if (go && gl >= k && gl <= en) {  // row modification, column j = gl
         const int j = gl;
@@ -1830,8 +1978,9 @@ __device__ __forceinline__ void stew_models(StewBatch& sb, double* stash, int la
 }
 
 // The sample's bearings, the null space and the 10x20 system (both solvers).
-__device__ __forceinline__ void coop_prepare(CoopWS& w, int lane, const double* F1, const double* F2, int N,
-                                             const short* smp, bool prof) {
+template <typename WS>
+__device__ __forceinline__ void coop_prepare(WS& w, int lane, const double* F1, const double* F2, int N,
+                                             const short* smp, bool prof, double* A) {
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   if (lane < 15) {
     const int i = lane / 3, c = lane % 3;
@@ -1842,14 +1991,14 @@ __device__ __forceinline__ void coop_prepare(CoopWS& w, int lane, const double* 
   KMX_PT(0);
   coop_nullspace(w, lane);
   KMX_PT(1);
-  coop_system(w, lane);
+  coop_system(w, lane, A);
   KMX_PT(2);
 }
 
 // One Nister hypothesis: sample -> models (w.ok, w.mR, w.mt).
 __device__ __forceinline__ void coop_hypothesis(CoopWS& w, int lane, const double* F1, const double* F2, int N,
                                                 const short* smp, bool prof) {
-  coop_prepare(w, lane, F1, F2, N, smp, prof);
+  coop_prepare(w, lane, F1, F2, N, smp, prof, &w.A[0][0]);
   unsigned long long t_prev = prof ? wall_clock64() : 0;
   if (!coop_gj(w, lane, false)) {
     if (lane == 0) w.ok = 0;
@@ -1919,16 +2068,15 @@ __device__ __forceinline__ int grp_gj(const double* A, int cl, int g0, double a[
 // (null space and system one at a time, 64 lanes; Gauss-Jordan GJW at a time
 // from systems staged in the wave's scratch), stashed in sb, then their
 // eigenvalues together.
-__device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* stash, int lane, const double* F1,
+template <bool ALLOW_ONE = false, typename WS>
+__device__ __forceinline__ void stew_batch(WS& w, StewBatch& sb, double* stash, int lane, const double* F1,
                                            const double* F2, int N, const short* tab, int p0, int nb, bool prof) {
   double* Ab = stash + SG * STASH_H + MAXP * 9;
   for (int b0 = 0; b0 < nb; b0 += GJW) {
     const int nw = min(GJW, nb - b0);
     for (int u = 0; u < nw; ++u) {
       const int b = b0 + u;
-      coop_prepare(w, lane, F1, F2, N, tab + (size_t)(p0 + b) * 5, prof);
-      double* A = Ab + u * 200;
-      for (int t = lane; t < 200; t += RS_BLOCK) A[t] = (&w.A[0][0])[t];
+      coop_prepare(w, lane, F1, F2, N, tab + (size_t)(p0 + b) * 5, prof, Ab + u * 200);
       double* st = stash + b * STASH_H;
       if (lane < 36) st[60 + lane] = (&w.N[0][0])[lane];
       if (lane < 15) {
@@ -1967,7 +2115,8 @@ __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* sta
   const bool on = g < nb && sb.ok[g];
   grp_hessenberg(sb, lane, on);
   KMX_PT(7);
-  grp_hqr(sb, lane, on);
+  if (ALLOW_ONE && nb == 1) grp_hqr<true>(sb, lane, on);
+  else grp_hqr<false>(sb, lane, on);
   KMX_PT(8);
 }
 
@@ -1978,11 +2127,14 @@ __device__ __forceinline__ void stew_batch(CoopWS& w, StewBatch& sb, double* sta
 // WAVE: the 1-point recovery's loops by the whole wave with its data staged
 // in `lds` (tail_lds_doubles(N) doubles; k_rs_finish's dynamic LDS).
 __host__ __device__ constexpr size_t tail_lds_doubles(int N) { return 3 * ((size_t)N + 4) + ((size_t)N + 15) / 8 + 6 * (size_t)N; }
-template <bool WAVE>
-__device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double* F2, const double* points, int N,
+struct NoCount {  // the work-queue kernel: no multi-wave count
+  __device__ int operator()(const double*, const unsigned char*, int, double) const { return -1; }
+};
+template <bool WAVE, typename WS, typename Count = NoCount>
+__device__ __forceinline__ void ransac_tail(int c, WS& w, double* F1, double* F2, const double* points, int N,
                                             int q, int m, const int2* pl, int K, const RsParams& P,
                                             kmx_lcd_result* R_, unsigned char* mask, int have, int iterations,
-                                            int lane, double* lds = nullptr) {
+                                            int lane, double* lds = nullptr, Count&& count_best = Count{}) {
   const bool st2d = (P.stages & KMX_LCD_STAGE_2D2D) != 0;
   auto pair_error = [&](const double* R, const double* t, int j) {
     const double a[3] = {F1[j], F1[N + j], F1[2 * N + j]}, b[3] = {F2[j], F2[N + j], F2[2 * N + j]};
@@ -2152,11 +2304,9 @@ __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double
   }
   const double thr2 = P.thr3d * P.thr3d;
   // T and valid staged in LDS (each lane copies the entries it wrote), then
-  // the largest consistent set: lane i counts the valid j within thr3d of T_i,
-  // every lane reading T_j at the same LDS address (a broadcast), four j per
-  // pass with independent chains (one wave alone on its SIMD: latency, not
-  // issue, bounds the loop); counts are integers, so their order does not
-  // matter
+  // the largest consistent set (count_best: every wave of k_rs_finish's
+  // workgroup counts a block of i against a range of j; the ties and the
+  // first maximum as below)
   double* Tl = lds;                                                              // [N + 4][3]
   unsigned char* vl = reinterpret_cast<unsigned char*>(lds + 3 * ((size_t)N + 4));  // [N + 4]
   double* Pc = lds + 3 * ((size_t)N + 4) + ((size_t)N + 15) / 8;                 // [N][6]: compacted inliers
@@ -2169,39 +2319,7 @@ __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double
     vl[k] = 0;
   }
   wsync();
-  int my_best = -1, my_cnt = 0;
-  for (int i0 = 0; i0 < n3; i0 += RS_BLOCK) {
-    const int i = i0 + lane;
-    double ti[3] = {0.0, 0.0, 0.0};
-    const bool vi = i < n3 && vl[i];
-    if (i < n3)
-      for (int k = 0; k < 3; ++k) ti[k] = Tl[3 * i + k];
-    int c4[4] = {0, 0, 0, 0};
-    for (int j = 0; j < n3; j += 4) {  // (entries n3 .. n3 + 3 are invalid padding)
-      const unsigned v4 = *reinterpret_cast<const unsigned*>(vl + j);
-      // branch-free (a valid-byte test as a branch serialised the four chains)
-      double d2[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const double* t = Tl + 3 * (j + u);
-        const double dx = t[0] - ti[0], dy = t[1] - ti[1], dz = t[2] - ti[2];
-        d2[u] = dx * dx + dy * dy + dz * dz;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) c4[u] += (int)((v4 >> (8 * u)) & 1u) & (d2[u] < thr2 ? 1 : 0);
-    }
-    const int cc = (c4[0] + c4[1]) + (c4[2] + c4[3]);
-    if (vi && cc > my_cnt) { my_cnt = cc; my_best = i; }
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    const int oc = __shfl_xor(my_cnt, off, 64);
-    const int ob = __shfl_xor(my_best, off, 64);
-    if (oc > my_cnt || (oc == my_cnt && ob >= 0 && (my_best < 0 || ob < my_best))) {
-      my_cnt = oc;
-      my_best = ob;
-    }
-  }
-  const int best = my_best;  // the same in every lane
+  const int best = count_best(Tl, vl, n3, thr2);  // the same in every lane
   KMX_PT(11);
   if (best >= 0) {
     // the inliers of the best translation, compacted in pair order into Pc
@@ -2240,41 +2358,84 @@ __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double
       cc += __popcll(im);
     }
     wsync();
+    // Each ordered sum below is one lane's serial chain (the serial loop's
+    // adds in its order, so the same bits), the chains on different lanes,
+    // and each lane's operands loaded eight inliers ahead of its adds (LDS
+    // loads were one latency per inlier on the chain); the results reach every
+    // lane by readlane.
+    constexpr int AH = 8;
     double s3[3] = {0.0, 0.0, 0.0};
-    if (!refine) {
-      for (int k = 0; k < cc; ++k)
-        for (int i = 0; i < 3; ++i) s3[i] += Pc[6 * k + i];
-    } else {  // T_j = p_q - R p_m again from the staged points (the expression T was formed by)
-      for (int k = 0; k < cc; ++k) {
-        const double* a = Pc + 6 * k;
-        const double* b = a + 3;
-        for (int i = 0; i < 3; ++i) s3[i] += a[i] - (Rb[i * 3 + 0] * b[0] + Rb[i * 3 + 1] * b[1] + Rb[i * 3 + 2] * b[2]);
+    {
+      const int i = lane < 3 ? lane : 0;
+      double acc = 0.0;
+      for (int k0 = 0; k0 < cc; k0 += AH) {
+        double v[AH];
+        const int kn = min(AH, cc - k0);
+        if (!refine) {
+#pragma unroll
+          for (int u = 0; u < AH; ++u) v[u] = u < kn ? Pc[6 * (k0 + u) + i] : 0.0;
+        } else {  // T_j = p_q - R p_m again from the staged points (the expression T was formed by)
+#pragma unroll
+          for (int u = 0; u < AH; ++u) {
+            const double* a = Pc + 6 * (k0 + (u < kn ? u : 0));
+            const double* b = a + 3;
+            v[u] = a[i] - (Rb[i * 3 + 0] * b[0] + Rb[i * 3 + 1] * b[1] + Rb[i * 3 + 2] * b[2]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < AH; ++u)
+          if (u < kn) acc += v[u];
       }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) s3[c] = rdlane(acc, c);
     }
     for (int i = 0; i < 3; ++i) r.T_query_match[9 + i] = s3[i] / (double)cc;
     r.stereo_inliers = cc;
     r.accepted = (cc >= P.min3d) ? 1 : 0;
     KMX_PT(12);
     if (r.accepted && refine) {  // refit_3d3d's sums over the same inliers, in its order
-      double cq3[3] = {0.0, 0.0, 0.0}, cm3[3] = {0.0, 0.0, 0.0};
-      for (int k = 0; k < cc; ++k)
-        for (int i = 0; i < 3; ++i) {
-          cq3[i] += Pc[6 * k + i];
-          cm3[i] += Pc[6 * k + 3 + i];
+      // centroids: lane c < 6 sums coordinate c of the staged (p_q, p_m) pairs
+      double cq3[3], cm3[3];
+      {
+        const int c = lane < 6 ? lane : 0;
+        double acc = 0.0;
+        for (int k0 = 0; k0 < cc; k0 += AH) {
+          double v[AH];
+          const int kn = min(AH, cc - k0);
+#pragma unroll
+          for (int u = 0; u < AH; ++u) v[u] = u < kn ? Pc[6 * (k0 + u) + c] : 0.0;
+#pragma unroll
+          for (int u = 0; u < AH; ++u)
+            if (u < kn) acc += v[u];
         }
-      for (int i = 0; i < 3; ++i) {
-        cq3[i] /= (double)cc;
-        cm3[i] /= (double)cc;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          cq3[i] = rdlane(acc, i) / (double)cc;
+          cm3[i] = rdlane(acc, 3 + i) / (double)cc;
+        }
       }
-      double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      for (int k = 0; k < cc; ++k) {
-        double dq[3], dm[3];
-        for (int i = 0; i < 3; ++i) {
-          dq[i] = Pc[6 * k + i] - cq3[i];
-          dm[i] = Pc[6 * k + 3 + i] - cm3[i];
+      // H[a][b] = sum dm[a] dq[b]: lane 3a + b < 9 its entry's chain
+      double H[9];
+      {
+        const int e = lane < 9 ? lane : 0, a = e / 3, b = e - 3 * a;
+        const double ca = a == 0 ? cm3[0] : (a == 1 ? cm3[1] : cm3[2]);
+        const double cb = b == 0 ? cq3[0] : (b == 1 ? cq3[1] : cq3[2]);
+        double acc = 0.0;
+        for (int k0 = 0; k0 < cc; k0 += AH) {
+          double vm[AH], vq[AH];
+          const int kn = min(AH, cc - k0);
+#pragma unroll
+          for (int u = 0; u < AH; ++u) {
+            const int k = k0 + (u < kn ? u : 0);
+            vq[u] = Pc[6 * k + b];
+            vm[u] = Pc[6 * k + 3 + a];
+          }
+#pragma unroll
+          for (int u = 0; u < AH; ++u)
+            if (u < kn) acc += (vm[u] - ca) * (vq[u] - cb);
         }
-        for (int a = 0; a < 3; ++a)
-          for (int b = 0; b < 3; ++b) H[a * 3 + b] += dm[a] * dq[b];
+#pragma unroll
+        for (int x = 0; x < 9; ++x) H[x] = rdlane(acc, x);
       }
       double U[9], sv[3], V[9], Rr[9];
       svd3(H, U, sv, V);
@@ -2301,8 +2462,8 @@ __device__ __forceinline__ void ransac_tail(int c, CoopWS& w, double* F1, double
 
 // One candidate's 2D-2D RANSAC and 3D-3D recovery by the calling wave; F1 is
 // the wave's global scratch (6 N + STASH doubles).
-template <bool STEW, typename SB>
-__device__ __forceinline__ void ransac_candidate(int c, CoopWS& w, SB& sb, double* F1, const double* bearings,
+template <bool STEW, typename WS, typename SB>
+__device__ __forceinline__ void ransac_candidate(int c, WS& w, SB& sb, double* F1, const double* bearings,
                                                  const double* points, int N, const int* cq, const int* cm,
                                                  const int2* pairs, const int* Kin, const short* table,
                                                  const RsParams& P, kmx_lcd_result* res, unsigned char* masks) {
@@ -2444,7 +2605,7 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
                                                           const int* Kin, const short* table, RsParams P,
                                                           kmx_lcd_result* res, unsigned char* masks,
                                                           double* fbuf, int n, int* next, const int* order) {
-  __shared__ CoopWS w;
+  __shared__ typename std::conditional<STEW, CoopWSS, CoopWS>::type w;
   __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;  // Stewenius: the batch
   double* F1 = fbuf + (size_t)blockIdx.x * (6 * N + STASH);
   for (;;) {
@@ -2511,7 +2672,8 @@ __global__ void k_rs_init(RsState* st, int n, int stages, unsigned* more, int nm
 
 // The candidate's compact bearings (ransac_candidate's layout) and the LDS
 // constant tables, by the calling wave.
-__device__ __forceinline__ void rs_compact(CoopWS& w, double* F1, const double* bearings, int N, int q, int m,
+template <typename WS>
+__device__ __forceinline__ void rs_compact(WS& w, double* F1, const double* bearings, int N, int q, int m,
                                            const int2* pl, int K, int lane) {
   double* F2 = F1 + 3 * N;
   for (int j = lane; j < K; j += RS_BLOCK) {
@@ -2534,7 +2696,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, in
                                                       const int2* pairs, const int* Kin, const short* table,
                                                       RsParams P, const RsState* st, HypOut* hout, int pa, int pb,
                                                       int G, int per, double* fbuf) {
-  __shared__ CoopWS w;
+  __shared__ typename std::conditional<STEW, CoopWSS, CoopWS>::type w;
   __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;
   const int c = blockIdx.x / G, g = blockIdx.x % G;
   const int lane = fresh_lane(threadIdx.x);
@@ -2580,7 +2742,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, in
   };
   if constexpr (STEW) {
     const int nb = p_hi - p_lo;
-    stew_batch(w, sb, stash, lane, F1, F2, N, tab, p_lo, nb, prof);
+    stew_batch<true>(w, sb, stash, lane, F1, F2, N, tab, p_lo, nb, prof);
     stew_models(sb, stash, lane, F1, F2, tab, p_lo, nb, prof);
     if (prof && lane == 0) t_prev = wall_clock64();
     for (int b = 0; b < nb; ++b) emit(p_lo + b, sb.mok[b] != 0, sb.mR[b], sb.mt[b]);
@@ -2678,37 +2840,123 @@ __global__ __launch_bounds__(64) void k_rs_replay(const int* Kin, RsParams P, Rs
   }
 }
 
-// Each candidate's result from its replayed loop (one wave per candidate).
-__global__ __launch_bounds__(RS_BLOCK) void k_rs_finish(const double* bearings, const double* points, int N,
-                                                        const int* cq, const int* cm, const int2* pairs,
-                                                        const int* Kin, RsParams P, const RsState* st,
-                                                        kmx_lcd_result* res, unsigned char* masks, double* fbuf) {
-  __shared__ CoopWS w;
-  extern __shared__ double tail_lds[];  // tail_lds_doubles(N)
-  const int c = blockIdx.x;
-  const int lane = fresh_lane(threadIdx.x);
-  const int K = Kin[c];
-  const int q = cq[c], m = cm[c];
-  unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
-  kmx_lcd_result* R_ = res + c;
-  for (int j = lane; j < N && mask; j += RS_BLOCK) mask[j] = 0;
-  const bool st2d = (P.stages & KMX_LCD_STAGE_2D2D) != 0;
-  if (K < 5 && st2d) {
-    if (lane == 0) {
-      kmx_lcd_result r = {};
-      r.n_matches = K;
-      *R_ = r;
+// Each candidate's result from its replayed loop: one workgroup of RS_FIN
+// waves per candidate. Wave 0 runs ransac_tail<true>; the 1-point
+// recovery's largest consistent set — n3^2 distance tests over the 2D-2D
+// inliers, the tail's longest loop on a lone wave — is counted by every wave:
+// wave v takes the 64 inliers i of block v % n_ib against the j of range
+// v / n_ib, adds its integer counts into LDS (any order: the same counts), and
+// wave 0 then takes the first maximum over the valid i (the serial loop's
+// pick). Waves 1.. wait at the first barrier and leave when wave 0 reached no
+// count (`fin_go` < 0: no model, too few inliers, no recovery stage, PnP).
+// `skip` (the speculative finish of a spread call): the range's `more` word;
+// set, the candidates are not done and the workgroup leaves at once.
+constexpr int RS_FIN = 8;
+__device__ __forceinline__ void fin_count(const double* Tl, const unsigned char* vl, int n3, double thr2, int* cnt,
+                                          int wave, int lane) {
+  const int n_ib = (n3 + RS_BLOCK - 1) / RS_BLOCK;
+  if (n_ib == 0) return;
+  const int n_jc = max(1, RS_FIN / n_ib);
+  const int ib = wave % n_ib, jc = wave / n_ib;
+  if (jc >= n_jc) return;
+  const int n3p = (n3 + 3) & ~3;  // entries n3 .. n3 + 3 are invalid padding
+  const int jlen = (((n3p + n_jc - 1) / n_jc) + 3) & ~3;
+  const int j0 = jc * jlen, j1 = min(n3p, j0 + jlen);
+  const int i = ib * RS_BLOCK + lane;
+  double ti[3] = {0.0, 0.0, 0.0};
+  if (i < n3)
+    for (int k = 0; k < 3; ++k) ti[k] = Tl[3 * i + k];
+  int c4[4] = {0, 0, 0, 0};
+  for (int j = j0; j < j1; j += 4) {
+    const unsigned v4 = *reinterpret_cast<const unsigned*>(vl + j);
+    // branch-free (a valid-byte test as a branch serialised the four chains)
+    double d2[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double* t = Tl + 3 * (j + u);
+      const double dx = t[0] - ti[0], dy = t[1] - ti[1], dz = t[2] - ti[2];
+      d2[u] = dx * dx + dy * dy + dz * dz;
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c4[u] += (int)((v4 >> (8 * u)) & 1u) & (d2[u] < thr2 ? 1 : 0);
+  }
+  if (i < n3 && j0 < j1) atomicAdd(cnt + i, (c4[0] + c4[1]) + (c4[2] + c4[3]));
+}
+__global__ __launch_bounds__(RS_BLOCK * RS_FIN) void k_rs_finish(const double* bearings, const double* points, int N,
+                                                                 const int* cq, const int* cm, const int2* pairs,
+                                                                 const int* Kin, RsParams P, const RsState* st,
+                                                                 kmx_lcd_result* res, unsigned char* masks,
+                                                                 double* fbuf, const unsigned* skip) {
+  __shared__ CoopWS w;
+  __shared__ int fin_go;
+  __shared__ int cnt[MAX_FEATS];
+  extern __shared__ double tail_lds[];  // tail_lds_doubles(N)
+  if (skip && *skip) return;  // (uniform over the launch)
+  const int wave = threadIdx.x / RS_BLOCK;
+  const int lane = fresh_lane(threadIdx.x % RS_BLOCK);
+  if (wave > 0) {
+    __syncthreads();  // A: wave 0 staged T (fin_go = n3) or reached no count (-1)
+    const int n3 = fin_go;
+    if (n3 < 0) return;
+    const double* Tl = tail_lds;
+    const unsigned char* vl = reinterpret_cast<const unsigned char*>(tail_lds + 3 * ((size_t)N + 4));
+    fin_count(Tl, vl, n3, P.thr3d * P.thr3d, cnt, wave, lane);
+    __syncthreads();  // B
     return;
   }
-  double* F1 = fbuf + (size_t)blockIdx.x * (6 * N + STASH);
-  const int2* pl = pairs + (size_t)c * N;
-  rs_compact(w, F1, bearings, N, q, m, pl, K, lane);
-  const RsState s = st[c];
-  if (lane < 12) w.bestm[lane] = s.best[lane];
-  __threadfence_block();
-  wsync();
-  ransac_tail<true>(c, w, F1, F1 + 3 * N, points, N, q, m, pl, K, P, R_, mask, s.have, s.iterations, lane, tail_lds);
+  bool met = false;
+  auto count_best = [&](const double* Tl, const unsigned char* vl, int n3, double thr2) -> int {
+    met = true;
+    for (int k = lane; k < n3; k += RS_BLOCK) cnt[k] = 0;
+    if (lane == 0) fin_go = n3;
+    __syncthreads();  // A
+    fin_count(Tl, vl, n3, thr2, cnt, 0, lane);
+    __syncthreads();  // B
+    int my_best = -1, my_cnt = 0;
+    for (int i = lane; i < n3; i += RS_BLOCK) {
+      const int cc = cnt[i];
+      if (vl[i] && cc > my_cnt) { my_cnt = cc; my_best = i; }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const int oc = __shfl_xor(my_cnt, off, 64);
+      const int ob = __shfl_xor(my_best, off, 64);
+      if (oc > my_cnt || (oc == my_cnt && ob >= 0 && (my_best < 0 || ob < my_best))) {
+        my_cnt = oc;
+        my_best = ob;
+      }
+    }
+    return my_best;
+  };
+  [&]() {
+    const int c = blockIdx.x;
+    const int K = Kin[c];
+    const int q = cq[c], m = cm[c];
+    unsigned char* mask = masks ? masks + (size_t)c * N : nullptr;
+    kmx_lcd_result* R_ = res + c;
+    for (int j = lane; j < N && mask; j += RS_BLOCK) mask[j] = 0;
+    const bool st2d = (P.stages & KMX_LCD_STAGE_2D2D) != 0;
+    if (K < 5 && st2d) {
+      if (lane == 0) {
+        kmx_lcd_result r = {};
+        r.n_matches = K;
+        *R_ = r;
+      }
+      return;
+    }
+    double* F1 = fbuf + (size_t)blockIdx.x * (6 * N + STASH);
+    const int2* pl = pairs + (size_t)c * N;
+    rs_compact(w, F1, bearings, N, q, m, pl, K, lane);
+    const RsState s = st[c];
+    if (lane < 12) w.bestm[lane] = s.best[lane];
+    __threadfence_block();
+    wsync();
+    ransac_tail<true>(c, w, F1, F1 + 3 * N, points, N, q, m, pl, K, P, R_, mask, s.have, s.iterations, lane, tail_lds,
+                      count_best);
+  }();
+  if (!met) {
+    if (lane == 0) fin_go = -1;
+    __syncthreads();  // A for the waves that wait to count
+  }
 }
 
 // Arun 3-point model (oracle arun_model): centroids, H = sum dm dq^T, Kabsch
@@ -2985,6 +3233,12 @@ struct kmx_lcd {
   unsigned* d_more = nullptr;  // [more_cap] one word per range: some candidate needs the next range
   int more_cap = 0;
   unsigned* h_more = nullptr;  // pinned copy of the word just read
+  // k_knn2s (synchronous calls of <= KS_MAX candidates): per-query results and
+  // the per-candidate arrival counters (zero between calls; KMX_LCD_KSPLIT=0: off)
+  bool knn_split = true;
+  int* d_kqb = nullptr;
+  unsigned* d_kcnt = nullptr;
+  int kqb_N = 0;
   // pinned staging of the synchronous one-candidate calls (kmx_lcd_match,
   // kmx_lcd_verify_matches): every input in one host-to-device copy, every
   // output through pinned memory (a pageable copy is a blocking staged copy
@@ -3039,11 +3293,12 @@ void lcd_free_cand(kmx_lcd* h) {
   h->d_order = nullptr;
   for (bool& e : h->ev_rs_set) e = false;
   h->cap = 0;
-  void* q[] = {h->d_st, h->d_hout, h->d_sfbuf, h->d_more};
+  void* q[] = {h->d_st, h->d_hout, h->d_sfbuf, h->d_more, h->d_kqb, h->d_kcnt};
   for (void* x : q)
     if (x) (void)hipFree(x);
   if (h->h_more) (void)hipHostFree(h->h_more);
   h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_more = nullptr; h->h_more = nullptr;
+  h->d_kqb = nullptr; h->d_kcnt = nullptr; h->kqb_N = 0;
   h->spread_cap = 0;
   h->more_cap = 0;
 }
@@ -3403,9 +3658,15 @@ int verify_ordered(kmx_lcd* h, int n, int stages, bool masks) {
 // The spread form (see k_rs_hyps): hypothesis ranges of growing size on many
 // waves, the serial control replayed after each, until every candidate's loop
 // has stopped; then the candidates' results. Synchronous (the host reads
-// whether a candidate needs another range).
+// whether a candidate needs another range). With `copy_out` (the caller's
+// result copies) the finish is enqueued speculatively behind the first
+// range, gated on the device by the range's `more` word, with the copies
+// after it: a call whose candidates all stop inside the first range (a true
+// loop closure: ~30 of 66 or 510 hypotheses) then costs one host round trip
+// instead of two, and *copied says the results are on their way.
 constexpr int SPREAD_WAVES = 1024;  // waves of one k_rs_hyps launch at most
-int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks) {
+int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::function<int()>* copy_out = nullptr,
+                  bool* copied = nullptr) {
   const RsParams rp = rs_params(h, stages);
   const bool masks = want_masks || rp.pnp;
   hipStream_t st = rs_stream(h);
@@ -3442,6 +3703,17 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks) {
   // 500-iteration loop (510) at once — one hypothesis per wave costs the
   // same latency, and a look-alike then needs one range, not two
   int range = (int64_t)n * 510 <= SPREAD_WAVES ? 510 : 66;
+  const size_t tail_bytes = sizeof(double) * tail_lds_doubles(h->N);
+  if (tail_bytes > 65536 - 16384)  // (max_feats near 1024: 75 KB, + 8.8 KB static: workspace, counts)
+    KMX_HIP(hipFuncSetAttribute((const void*)k_rs_finish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tail_bytes));
+  auto finish = [&](const unsigned* skip) {
+    hipLaunchKernelGGL(k_rs_finish, dim3(n), dim3(RS_BLOCK * RS_FIN), tail_bytes, st,
+                       (const double*)h->d_bear, (const double*)h->d_pts,
+                       h->N, (const int*)h->d_cq, (const int*)h->d_cm, (const int2*)h->d_pairs, (const int*)h->d_K, rp,
+                       (const RsState*)h->d_st, h->d_res, masks ? h->d_mask : nullptr, h->d_sfbuf, skip);
+  };
+  const bool spec = copy_out && copied && !rp.pnp;
+  if (copied) *copied = false;
   for (int it = 0; pa < h->pmax && (stages & KMX_LCD_STAGE_2D2D); ++it) {  // (recovery alone: no hypotheses)
     // hypotheses per wave: as few as the launch's waves allow (one wave
     // works through its hypotheses one after another; the batch of SG
@@ -3456,19 +3728,24 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks) {
                        (const RsState*)h->d_st, h->d_hout, pa, pb, G, per, h->d_sfbuf);
     hipLaunchKernelGGL(k_rs_replay, dim3(n), dim3(64), 0, st, (const int*)h->d_K, rp, h->d_st,
                        (const HypOut*)h->d_hout, pb, n, h->d_more + it);
+    if (spec && it == 0) {
+      finish(h->d_more);
+      if (int rc = (*copy_out)()) return rc;
+    }
     KMX_HIP(hipMemcpyAsync(h->h_more, h->d_more + it, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     KMX_HIP(hipStreamSynchronize(st));
-    if (!*h->h_more) break;
+    if (!*h->h_more) {
+      if (spec && it == 0) {
+        *copied = true;
+        KMX_HIP(hipGetLastError());
+        return 0;
+      }
+      break;
+    }
     pa = pb;
     range = pa < 510 ? 510 - pa : 1500;  // then the rest of a 500-iteration loop, then its skips
   }
-  const size_t tail_bytes = sizeof(double) * tail_lds_doubles(h->N);
-  if (tail_bytes > 65536)  // (max_feats near 1024: up to 75 KB with the 4.7 KB static workspace)
-    KMX_HIP(hipFuncSetAttribute((const void*)k_rs_finish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tail_bytes));
-  hipLaunchKernelGGL(k_rs_finish, dim3(n), dim3(RS_BLOCK), tail_bytes, st,
-                     (const double*)h->d_bear, (const double*)h->d_pts,
-                     h->N, (const int*)h->d_cq, (const int*)h->d_cm, (const int2*)h->d_pairs, (const int*)h->d_K, rp,
-                     (const RsState*)h->d_st, h->d_res, masks ? h->d_mask : nullptr, h->d_sfbuf);
+  finish(nullptr);
   if (rp.pnp && (stages & KMX_LCD_STAGE_RECOVER))
     if (int rc = launch_recover(h, n, pnp_params(h, stages), h->d_table_rec, 0)) return rc;
   KMX_HIP(hipGetLastError());
@@ -3478,9 +3755,11 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks) {
 // Everything after the pair rows d_pairs / d_K exist: RANSAC, then recovery.
 // sync_ok: the caller synchronises on the results (kmx_lcd_verify,
 // kmx_lcd_verify_matches), so a small call may take the spread form.
-int enqueue_ransac(kmx_lcd* h, int n, int stages, bool want_masks, bool sync_ok = false) {
+int enqueue_ransac(kmx_lcd* h, int n, int stages, bool want_masks, bool sync_ok = false,
+                   const std::function<int()>* copy_out = nullptr, bool* copied = nullptr) {
+  if (copied) *copied = false;
   if (h->P.rng_stream) return verify_ordered(h, n, stages, want_masks);
-  if (sync_ok && n > 0 && n <= h->spread_max) return ransac_spread(h, n, stages, want_masks);
+  if (sync_ok && n > 0 && n <= h->spread_max) return ransac_spread(h, n, stages, want_masks, copy_out, copied);
   const RsParams rp = rs_params(h, stages);
   if (int rc = launch_ransac(h, n, rp, h->d_table, 0, want_masks || rp.pnp)) return rc;
   if (rp.pnp && (stages & KMX_LCD_STAGE_RECOVER))
@@ -3498,6 +3777,36 @@ int slot_upload(kmx_lcd* h, int n, const int32_t* cq, const int32_t* cm) {
   KMX_HIP(hipMemcpyAsync(h->d_cm, cm, sizeof(int) * n, hipMemcpyHostToDevice, h->kstream));
   return 0;
 }
+// The kNN2 of n candidates (ids at dcq / dcm) on stream st: k_knn2, or for a
+// synchronous call of <= KS_MAX candidates the split form k_knn2s (same rows).
+constexpr int KS_MAX = 64;
+int launch_knn2(kmx_lcd* h, int n, const int* dcq, const int* dcm, hipStream_t st, bool sync_call) {
+  if (sync_call && h->knn_split && n <= KS_MAX) {
+    if (h->kqb_N < h->N) {
+      KMX_HIP(hipStreamSynchronize(st));
+      if (h->d_kqb) (void)hipFree(h->d_kqb);
+      h->d_kqb = nullptr;
+      h->kqb_N = 0;
+      KMX_HIP(hipMalloc(&h->d_kqb, sizeof(int) * (size_t)KS_MAX * h->N));
+      h->kqb_N = h->N;
+    }
+    if (!h->d_kcnt) {
+      KMX_HIP(hipMalloc(&h->d_kcnt, sizeof(unsigned) * KS_MAX));
+      KMX_HIP(hipMemsetAsync(h->d_kcnt, 0, sizeof(unsigned) * KS_MAX, st));
+    }
+    const int S = (h->N + KS_Q - 1) / KS_Q;
+    const size_t smem = (size_t)h->N * 32 + sizeof(uint32_t) * 4 * KS_Q * 2 + sizeof(int) * (KNN_BLOCK + 1);
+    hipLaunchKernelGGL(h->P.norm == KMX_NORM_HAMMING ? k_knn2s<true> : k_knn2s<false>, dim3(n * S), dim3(KNN_BLOCK),
+                       smem, st, (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, dcq, dcm,
+                       h->P.lowe_ratio, h->d_pairs, h->d_K, h->d_kqb, h->d_kcnt, S);
+  } else {
+    hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1), st,
+                       (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, dcq, dcm, h->P.norm,
+                       h->P.lowe_ratio, h->d_pairs, h->d_K);
+  }
+  return 0;
+}
+
 // kNN2 of the current slot on the side stream, the RANSAC on the handle's
 // stream behind it: a call's kNN2 runs in the previous call's RANSAC tail
 // (the work-queue RANSAC holds every wave slot until its queue drains, so the
@@ -3505,7 +3814,6 @@ int slot_upload(kmx_lcd* h, int n, const int32_t* cq, const int32_t* cm) {
 int enqueue_verify(kmx_lcd* h, int n, bool want_masks, bool sync_ok = false) {
   if (n == 0) return 0;
   const int s = h->cur;
-  const size_t knn_smem = (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1);
   if (h->timing) {
     if (!h->ev_ok) {
       for (auto& e : h->ev) KMX_HIP(hipEventCreate(&e));
@@ -3513,9 +3821,7 @@ int enqueue_verify(kmx_lcd* h, int n, bool want_masks, bool sync_ok = false) {
     }
     KMX_HIP(hipEventRecord(h->ev[0], h->kstream));
   }
-  hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), knn_smem, h->kstream, (const uint32_t*)h->d_desc,
-                     (const int*)h->d_nfeat, h->N, (const int*)h->d_cq, (const int*)h->d_cm, h->P.norm,
-                     h->P.lowe_ratio, h->d_pairs, h->d_K);
+  if (int rc = launch_knn2(h, n, h->d_cq, h->d_cm, h->kstream, sync_ok)) return rc;
   if (h->timing) KMX_HIP(hipEventRecord(h->ev[1], h->kstream));
   KMX_HIP(hipEventRecord(h->ev_knn[s], h->kstream));
   KMX_HIP(hipStreamWaitEvent(rs_stream(h), h->ev_knn[s], 0));
@@ -3613,6 +3919,7 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
   }
   h->own_stream = true;
   if (const char* e = std::getenv("KMX_LCD_RSX")) h->rs_conc = std::atoi(e) != 0;
+  if (const char* e = std::getenv("KMX_LCD_KSPLIT")) h->knn_split = std::atoi(e) != 0;
   bool ok = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking) == hipSuccess;
   for (int i = 1; i < LCD_SLOTS && ok; ++i) ok = hipStreamCreateWithFlags(&h->rsx[i], hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; i < LCD_SLOTS && ok; ++i)
@@ -3773,9 +4080,7 @@ extern "C" int kmx_lcd_match(kmx_lcd* h, int32_t n, const int32_t* cq, const int
   std::memcpy(h->h_io, cq, sizeof(int) * n);
   std::memcpy(h->h_io + kin, cm, sizeof(int) * n);
   KMX_HIP(hipMemcpyAsync(h->d_io, h->h_io, 2 * kin, hipMemcpyHostToDevice, rs_stream(h)));
-  hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1), rs_stream(h),
-                     (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, (const int*)h->d_io,
-                     (const int*)(h->d_io + kin), h->P.norm, h->P.lowe_ratio, h->d_pairs, h->d_K);
+  if (int rc = launch_knn2(h, n, (const int*)h->d_io, (const int*)(h->d_io + kin), rs_stream(h), true)) return rc;
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipMemcpyAsync(h->h_io, h->d_pairs, pb, hipMemcpyDeviceToHost, rs_stream(h)));
   KMX_HIP(hipMemcpyAsync(h->h_io + pb, h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, rs_stream(h)));
@@ -3840,11 +4145,17 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
                      (const int*)(h->d_io + o_cq), (const int*)(h->d_io + o_cm),
                      T_prior ? (const double*)(h->d_io + o_pr) : nullptr, h->d_cq, h->d_cm, h->d_prior);
   KMX_HIP(hipGetLastError());
-  if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr, true)) return rc;
+  const std::function<int()> copy_out = [&]() -> int {
+    KMX_HIP(hipMemcpyAsync(h->h_io, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
+    if (inlier_masks)
+      KMX_HIP(hipMemcpyAsync(h->h_io + rb, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
+    return 0;
+  };
+  bool copied = false;
+  if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr, true, &copy_out, &copied)) return rc;
   KMX_HIP(hipGetLastError());
-  KMX_HIP(hipMemcpyAsync(h->h_io, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
-  if (inlier_masks)
-    KMX_HIP(hipMemcpyAsync(h->h_io + rb, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
+  if (!copied)
+    if (int rc = copy_out()) return rc;
   if (int rc = mark_slot(h)) return rc;
   KMX_HIP(hipStreamSynchronize(rs_stream(h)));
   std::memcpy(results, h->h_io, sizeof(kmx_lcd_result) * n);

@@ -17,10 +17,12 @@
 //   * tCG in the linearity form: Hz by gather, delta = -z + beta delta_old,
 //     Hdelta = -Hz + beta Hdelta_old; eta = sum coef_k delta_k is folded from
 //     two kept directions every second step and finished in k_retract.
-//   * Edge data: one 80-B compact record per incidence in CSR order (unit
-//     quaternion of R, t, w kappa, w tau, {other, edge | tail << 31}), or a
-//     128-B record with the full rotation when some measurement is not a
-//     rotation to 1e-12. The gathers are incidence-parallel:
+//   * Edge data: one 72-B compact record per incidence in CSR order (unit
+//     quaternion of R, t, w kappa, +-w tau — the sign bit is the tail flag)
+//     plus its other endpoint in a 4-B array (Dev::rec_o), 76 B per incidence
+//     (struct Rec<10>); or a 128-B record with the full rotation when some
+//     measurement is not a rotation to 1e-12 (Rec<16>). The gathers are
+//     incidence-parallel:
 //     one lane per incidence evaluates its block against the neighbour's whole
 //     r x 4 row and parks the r contribution rows in LDS; the (pose, row) lanes
 //     then add their pose's contributions in CSR (= increasing edge id) order.
@@ -195,15 +197,6 @@ struct Dev {
   // double-buffered by step parity (the gathered vector), and the step's
   // 8-wide partials
   double *hz, *w0, *w1;
-  unsigned* gbar;             // resident round: grid-barrier words (zeroed by k_begin), or null
-  // RM_LAUNCH with fused reducers (fuse_red): the tCG launches carry L extra
-  // workgroups, one per robot, that reduce the robot's tile partials as soon
-  // as its tiles have posted them (in place of a k_reduce launch). red_cnt:
-  // [L] arrival counters (128-B apart, reset by their reducer); fail: the
-  // host-mapped word a reducer whose wait gave up writes
-  int fuse_red;
-  unsigned* red_cnt;
-  unsigned* fail;
   double* part_f;             // [2][ntiles][8], by step parity (a launch reads step k's
                               // partials of every tile of its robot while its own tile writes step k+1's)
 };
@@ -315,7 +308,7 @@ __device__ __forceinline__ int2 unpack_int2(double v) {
 // RW = 10: compact record (unit quaternion of R, t, w kappa, +-w tau) — 72 B
 // in HBM (GS = 9 doubles), the sign bit of w tau is the tail flag (w tau >= 0;
 // a zero weight is +-0.0), the other endpoint in Dev::rec_o (4 B): 76 B per
-// incidence. In registers (and the resident round's LDS copy) it is the
+// incidence. In registers it is the
 // 10-word form (..., w tau, {other, tail << 31}), five 16-B parts; the gathers
 // rebuild R from the quaternion (R R^T = I to rounding, as the preconditioner
 // assumes).
@@ -543,7 +536,7 @@ __device__ __forceinline__ Lane lane_map(const Dev& d) {
   // blocks b and b + 8 share an XCD, so each XCD gets one contiguous range of
   // tiles — about one robot block, whose rows then stay in that XCD's L2.
   {
-    const int nwg = d.ntiles, b = blockIdx.x;  // (the tile blocks: fused reducers come after them)
+    const int nwg = d.ntiles, b = blockIdx.x;
     const int q = nwg >> 3, rr = nwg & 7, x = b & 7;
     L.tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
   }
@@ -568,8 +561,8 @@ __device__ __forceinline__ Lane lane_map(const Dev& d) {
 }
 
 // --------------------------------------------------------------- gathers ---
-// LDS layouts. A tile holds TP = W * (64 / R) poses (W waves per workgroup:
-// WAVES for the launched kernels, 4 or 5 for the resident round); its
+// LDS layouts. A tile holds TP = W * (64 / R) poses (W = WAVES waves per
+// workgroup); its
 // incidences are one contiguous CSR range walked in chunks of CH incidences
 // (one lane each).
 template <int R, int W = WAVES>
@@ -900,11 +893,6 @@ __device__ __forceinline__ double inc_owner_cost(const Dev& d, const Lane& L, co
 // round: no gain).
 enum RedMode { RM_LAUNCH = 0, RM_CONSUMER = 2 };
 
-constexpr int RC_STRIDE = 32;  // Dev::red_cnt: one 128-B line per robot
-__device__ __forceinline__ void wt_st1(double* p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 template <int KIND, int NV, int RM, typename Store>
 __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const double* vals, char* smem_red,
                                             Store&& store) {
@@ -918,24 +906,14 @@ __device__ __forceinline__ void finish_tile(const Dev& d, const Lane& L, const d
   __syncthreads();
   constexpr bool two = RM == RM_CONSUMER && (KIND == RED_HESS || KIND == RED_UPDATE);
   static_assert(!two || NV <= 2, "consumer partials");
-  constexpr bool fusable = RM == RM_LAUNCH && (KIND == RED_HESS || KIND == RED_UPDATE);
   if (threadIdx.x == 0) {  // 2-wide partials for the consumer launch, else NPART-wide for k_reduce
     double* dst = two ? (KIND == RED_HESS ? d.part_h : d.part_u) + (size_t)L.tile * 2 : d.part + (size_t)L.tile * NPART;
-    const bool fused = fusable && d.fuse_red;
 #pragma unroll
     for (int s = 0; s < NV; ++s) {
       double t = 0.0;
 #pragma unroll
       for (int w = 0; w < WAVES; ++w) t += lds[s * WAVES + w];
-      if (fused) {
-        wt_st1(dst + s, t);  // write-through: the robot's reducer in this launch reads it sc1
-      } else {
-        dst[s] = t;
-      }
-    }
-    if (fused) {  // drained, then one arrival on the robot's counter (MI355X_MICROARCH.md "Valid forms", row 1)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      (void)__hip_atomic_fetch_add(d.red_cnt + (size_t)L.l * RC_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dst[s] = t;
     }
   }
   store();
@@ -1173,24 +1151,12 @@ __device__ __forceinline__ void robot_sum(const double* part, int stride, int t0
 // robot_sum's order (a thread's tiles in tile order, then the wave sums and
 // the waves in order: the same sums for any U).
 // NS <= 2: 2-wide partials (part_h / part_u); NS = 3, 4: d.part (stride NPART).
-// A tile partial pair part[i], part[i + 1] (i even): plain, or (SC, the
-// resident round: partials another workgroup of the same launch wrote
-// through) one 16-B sc1 buffer load through a descriptor of the
-// (workgroup-uniform) array base — the replicated-counter hand-off takes 4- or
-// 16-B sc1 loads (MI355X_MICROARCH.md "Valid forms").
-typedef unsigned kmx_u4 __attribute__((ext_vector_type(4)));
-template <bool SC>
+// A tile partial pair part[i], part[i + 1] (i even): one 16-B load.
 __device__ __forceinline__ double2 ldpart(const double* part, size_t i) {
-  if constexpr (SC) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(part), 0, 0x7ffffff0, 0x00020000);
-    const kmx_u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(i * 8), 0, 16);
-    return __builtin_bit_cast(double2, v);
-  } else {
-    return *reinterpret_cast<const double2*>(part + i);
-  }
+  return *reinterpret_cast<const double2*>(part + i);
 }
 
-template <int NS, int U = 2, bool SC = false>
+template <int NS, int U = 2>
 struct RobotSum {
   double a[U][NS];
   int t0, t1;
@@ -1202,9 +1168,9 @@ struct RobotSum {
     for (int u = 0; u < U; ++u) {
       const int t = min(t0 + (int)threadIdx.x + u * RBLOCK, t1 - 1);
       const size_t pt = (size_t)t * stride;
-      const double2 x = ldpart<SC>(part, pt);
+      const double2 x = ldpart(part, pt);
       if constexpr (NS > 2) {
-        const double2 y = ldpart<SC>(part, pt + 2);
+        const double2 y = ldpart(part, pt + 2);
         a[u][2] = y.x;
         if constexpr (NS > 3) a[u][3] = y.y;
       }
@@ -1214,7 +1180,7 @@ struct RobotSum {
   }
   __device__ __forceinline__ void finish(const double* part, int stride, double* lds, double tot[NPART]) {
     static_assert(NS <= NPART, "partials");
-    if (!SC && t1 - t0 > U * RBLOCK) {  // (SC: the host caps a robot's tiles at U * RBLOCK)
+    if (t1 - t0 > U * RBLOCK) {
       robot_sum<(NS > 2 ? NPART : NS)>(part, stride, t0, t1, lds, tot);
       if constexpr (NS == 3) tot[3] = 0.0;
       return;
@@ -1545,7 +1511,7 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     // partials) this launch also consumes in place of a k_reduce launch; later
     // launches find it in PH_TCG. The robot sums' loads go out before the
     // state arrives.
-    const bool grad = first_launch != 0;
+    const bool grad = (first_launch & 1) != 0;
     const bool upd = !grad;
     RobotSum<2> rs;  // (four tiles per thread here: spills at 128 VGPRs)
     RobotSum<3> rg;
@@ -1561,7 +1527,10 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     };
     // early (below): the phase test waits in the decision, so the first
     // records load with the state instead of after it
-    if (!active && !d.p.early_stop) {
+    // gated (first_launch & 2, a launch the host expects to find robots
+    // stopped): the phase test before the first records are issued, so a
+    // launch with nothing to do reads its control words and leaves
+    if (!active && (!d.p.early_stop || (first_launch & 2))) {
       idle();
       return;
     }
@@ -1611,6 +1580,9 @@ __device__ __forceinline__ void body_hess(const Dev& d, int first_launch, int sl
     const int ph = c.phase;
     tcg_iter = c.tcg_iter;
     beta = c.beta;
+    // gated (first_launch & 2, see the consumer form): no record is fetched
+    // before the phase test
+    if ((first_launch & 2) && ph != PH_TCG) return;
     if (!hinc_gather<R, RW, true, false>(d, L, d.z, H, smem, [&]() { return ph == PH_TCG; })) return;
   }
   const bool first = (tcg_iter == 0) || (KMX_HESS_PROBE & 4);  // (probe 4: no delta_old / Hdelta_old traffic)
@@ -1834,7 +1806,7 @@ __device__ __forceinline__ void onesync_scalars(double al, const double* tot, do
 // robot_sum: U tiles per thread in one round trip (1024 tiles, the 736-tile
 // cut of a 12.5k-pose block included), tile order within a thread, then the
 // wave sums and the waves in order; larger robots loop.
-template <int U, bool SC = false>
+template <int U>
 struct RobotSum8 {
   double a[U][8];
   int t0, t1;
@@ -1844,7 +1816,7 @@ struct RobotSum8 {
       const int t = min(tb + (int)threadIdx.x + u * RBLOCK, t1 - 1);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const double2 x = ldpart<SC>(part, (size_t)t * 8 + 2 * k);
+        const double2 x = ldpart(part, (size_t)t * 8 + 2 * k);
         a[u][2 * k] = x.x;
         a[u][2 * k + 1] = x.y;
       }
@@ -2278,90 +2250,14 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_grad(Dev d, int gated) {
   KMX_SMEM;
   body_grad<R, RW, RM>(d, gated, smem);
 }
-// A fused reducer (Dev::fuse_red, RM_LAUNCH): k_reduce's work inside the
-// launch that produces the partials, by workgroup ntiles + l of it. Every tile
-// of robot l posts its partials write-through, drains them and adds one to the
-// robot's counter; the reducer (dispatched after every tile workgroup, so no
-// tile waits for it) polls the counter sc1 until all t1 - t0 tiles have posted,
-// then sums them in k_reduce's order (RobotSum, 16-B sc1 loads) and runs the
-// same control step. A robot not in the launch's phase posts nothing and its
-// reducer does not wait. What the launch's boundary then carries to the next
-// kernel is only the robot's state, as after a k_reduce launch — without that
-// launch's own ramp and dependency.
-constexpr unsigned long long KMX_RED_SPIN = 200000000ull;  // 2 s of the 100 MHz clock
-__device__ __forceinline__ void red_fused(const Dev& d, int kind, int l, int R_, HostStatus* hs,
-                                          unsigned long long seq, int slot) {
-  constexpr int RW_ = RBLOCK / 64;
-  constexpr int CW = sizeof(Ctl) / 8;
-  __shared__ double lds[NPART * RW_];
-  __shared__ Ctl cs;
-  __shared__ int ok_s;
-  if (threadIdx.x < CW)
-    reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(d.ctl + l)[threadIdx.x];
-  __syncthreads();
-  const int ph = cs.phase;
-  const bool act = (kind == RED_HESS || kind == RED_UPDATE) && ph == PH_TCG;
-  const int t0 = d.rtile0[l], t1 = d.rtile0[l + 1];
-  double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
-  if (act) {
-    if (threadIdx.x == 0) {
-      unsigned* c = d.red_cnt + (size_t)l * RC_STRIDE;
-      const unsigned n = (unsigned)(t1 - t0);
-      int ok = 1;
-      const unsigned long long ts = wall_clock64();
-      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
-        __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - ts > KMX_RED_SPIN) {
-          ok = 0;
-          __hip_atomic_store(d.fail, 0x10000u + (unsigned)kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's count starts at 0
-      ok_s = ok;
-    }
-    __syncthreads();
-    if (!ok_s) return;
-    RobotSum<NPART, 2, true> rs;  // (<= 512 tiles per robot: the host checks)
-    rs.issue(d.part, NPART, t0, t1);
-    rs.finish(d.part, NPART, lds, tot);
-  }
-  if (threadIdx.x == 0) {
-    if (act) {
-      const int ns = kind == RED_HESS ? 1 : 2;
-#pragma unroll
-      for (int s = 0; s < NPART; ++s) tot[s] = s < ns ? tot[s] : 0.0;
-      control_on(cs, d, l, kind, tot, R_, true);
-      if (kind == RED_HESS && slot >= 0) atomicAdd(d.hv_launch + slot, 1);
-    }
-    if (hs) post_status(hs, l, seq, act && cs.phase == PH_TCG);
-  }
-  if (!act) return;
-  __syncthreads();
-  if (threadIdx.x < CW)
-    reinterpret_cast<double*>(d.ctl + l)[threadIdx.x] = reinterpret_cast<const double*>(&cs)[threadIdx.x];
-}
-
 template <int R, int RW, int RM>
 __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_hess(Dev d, int first, int slot, HostStatus* hs,
                                                           unsigned long long seq) {
-  if constexpr (RM == RM_LAUNCH) {
-    if ((int)blockIdx.x >= d.ntiles) {
-      red_fused(d, RED_HESS, (int)blockIdx.x - d.ntiles, R, hs, seq, slot);
-      return;
-    }
-  }
   KMX_SMEM;
   body_hess<R, RW, RM>(d, first, slot, hs, seq, smem);
 }
 template <int R, int RM>
 __global__ __launch_bounds__(BLOCK) void k_update(Dev d, HostStatus* hs, unsigned long long seq, int slot) {
-  if constexpr (RM == RM_LAUNCH) {
-    if ((int)blockIdx.x >= d.ntiles) {
-      red_fused(d, RED_UPDATE, (int)blockIdx.x - d.ntiles, R, hs, seq, slot);
-      return;
-    }
-  }
   KMX_SMEM;
   body_update<R, RM>(d, hs, seq, slot, smem);
 }
@@ -2386,721 +2282,6 @@ __global__ __launch_bounds__(BLOCK, LB<R>::w) void k_cost(Dev d, const Ctl* src)
 template <int R>
 __global__ __launch_bounds__(BLOCK) void k_commit(Dev d, int fold, int final) {
   body_commit<R>(d, fold, final);
-}
-
-// ================================================ resident one-sync round ===
-// tcg_form KMX_TCG_FORM_RESIDENT (SURVEY.md §7
-// step 4, §8e): the whole block update of a small shard in ONE launch per
-// round — gradient, every one-sync tCG step, the trial point, its cost, the
-// accept decision and the commit — with one grid barrier where the launched
-// form (k_grad, k_step x J, k_cost, k_commit) has a kernel boundary. What it
-// removes per step is the launch's own latency chain (profiles/r04: ~17 us of
-// dependent steps per k_step at 12.5k poses, 4.4 us of it loading the tile's
-// own rows): each workgroup holds its tile's rows of y, g, r, z, Hz, delta,
-// H delta, w and eta in registers and its poses' D_i, M^-1 and S blocks in LDS
-// for the whole round, so a step reads only what crosses workgroups: the
-// robot's 8-wide partials and the neighbours' rows of w.
-// Arithmetic: body_step's and the oracle's tcg_onesync, expression for
-// expression (fused multiply-adds included), the robot sums in RobotSum8's
-// order, so a resident round equals the launched one-sync round on the same
-// tile cut bit for bit (tests/test_resident_gpu.py).
-// Hand-offs inside the launch (MI355X_MICROARCH.md "Valid forms", row 1):
-// every byte another workgroup reads in this launch — z, w, Xt rows and the
-// tile partials — is stored write-through (sc1 16-B buffer stores, 8-B agent
-// atomics) and loaded sc1; every storing wave drains (s_waitcnt vmcnt(0))
-// before the workgroup barrier behind which one lane arrives. Data written by
-// earlier launches (X, the public table, records, D_i, M^-1) are read plainly.
-// Grid barrier (MI355X_MICROARCH.md "Valid forms", the replicated-counter
-// row): every barrier b of the launch has its own counter, kept in GB_REP = 8
-// replicas on lines of their own. A workgroup arrives, after every wave's
-// write-through stores have drained and a workgroup barrier, with ONE wave
-// instruction whose 8 lanes add to the 8 replicas (no-return agent atomics):
-// 1 per arrival, + 0x10000 when it formed a tCG step the next step consumes.
-// One lane per workgroup polls the replica of its XCD (block % 8 under
-// round-robin placement: speed only) with sc1 loads until the count reaches
-// the grid; the high half then says whether any workgroup formed a step. The
-// chain from the last arrival is one atomic landing and one poll (the
-// two-level counter tree with a separate continue word, round 5's first form,
-// was four dependent round trips: 7-9 us per tCG step after the step's
-// stores, profiles/r05/resident/). Counters are zeroed by k_begin before each
-// round. Every spin is bounded (KMX_RES_SPIN ticks of the 100 MHz clock): a
-// workgroup that gives up writes the host-mapped fail word and leaves; the
-// host turns it into an error at the next sync. All workgroups must be
-// resident: set_graph checks the occupancy query and runs a census launch.
-constexpr int GB_STRIDE = 32;                // one 128-B line per word
-constexpr int GB_REP = 8;                    // replicas per barrier counter
-constexpr int GB_BMAX = 64;                  // barriers per launch (tcg_max + 3 <= GB_BMAX: resident_setup)
-constexpr int GB_WORDS = GB_BMAX * GB_REP * GB_STRIDE;
-constexpr unsigned long long KMX_RES_SPIN = 200000000ull;  // 2 s
-
-#ifdef KMX_RES_STAMPS
-constexpr int RES_STAMP_TILES = 2048;
-constexpr int RES_STAMPS = 128;  // per tile: 0..95 the phases (body_round), 96 + 2 b / 97 + 2 b barrier b < 16
-__device__ unsigned long long g_res_stamp[RES_STAMPS * RES_STAMP_TILES];
-#endif
-
-__device__ __forceinline__ unsigned gb_load(unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One grid barrier (index b within the launch). `cont`: this workgroup's robot
-// formed a tCG step whose partials the next step consumes; *any: some
-// workgroup arrived with cont. Returns false when the wait gave up.
-// `during`: work of thread 0 between its arrival and its poll (it must not
-// touch anything another workgroup reads after this barrier)
-template <typename F>
-__device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, bool* any, unsigned* fail, int* sflag,
-                                          F&& during) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
-  __syncthreads();
-#ifdef KMX_RES_STAMPS
-  const unsigned long long ts0 = wall_clock64();
-#endif
-  if (threadIdx.x < 64) {
-    const int ln = threadIdx.x;
-    if (b < GB_BMAX && ln < GB_REP)  // one instruction, 8 lanes, one replica each
-      (void)__hip_atomic_fetch_add(gb + (b * GB_REP + ln) * GB_STRIDE, cont ? 0x10001u : 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-    if (ln == 0) {
-      during();
-      int ok = b < GB_BMAX;
-      unsigned v = 0;
-      if (ok) {
-        unsigned* pw = gb + (b * GB_REP + (blockIdx.x & (GB_REP - 1))) * GB_STRIDE;
-        const unsigned n = gridDim.x;
-        const unsigned long long t0 = wall_clock64();
-        while (((v = gb_load(pw)) & 0xffffu) < n) {
-          __builtin_amdgcn_s_sleep(1);
-          if (wall_clock64() - t0 > KMX_RES_SPIN) {
-            ok = 0;
-            break;
-          }
-        }
-      }
-      if (!ok) __hip_atomic_store(fail, 1u + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      *sflag = ok ? (1 | ((v >> 16) ? 2 : 0)) : 0;
-#ifdef KMX_RES_STAMPS
-      const int tl = blockIdx.x;  // (stamps by launch block; res_stamps.py maps them)
-      if (tl < RES_STAMP_TILES && b < 16) {
-        g_res_stamp[tl * RES_STAMPS + 96 + 2 * b] = ts0;
-        g_res_stamp[tl * RES_STAMPS + 97 + 2 * b] = wall_clock64();
-      }
-#endif
-    }
-  }
-  __syncthreads();
-  const int f = *sflag;
-  *any = (f & 2) != 0;
-  return (f & 1) != 0;
-}
-__device__ __forceinline__ bool grid_sync(unsigned* gb, unsigned b, bool cont, bool* any, unsigned* fail, int* sflag) {
-  return grid_sync(gb, b, cont, any, fail, sflag, []() {});
-}
-
-// write-through row I/O: 16-B buffer loads / stores with the sc1 bit (aux 16)
-// through a descriptor built from a kernel-argument base (wave-uniform)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const double* base, long long doubles) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, (int)(doubles * 8), 0x00020000);
-}
-__device__ __forceinline__ double2 wt_ld2(__amdgpu_buffer_rsrc_t rs, unsigned off) {
-  const kmx_u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
-  return __builtin_bit_cast(double2, v);
-}
-__device__ __forceinline__ void wt_st4(__amdgpu_buffer_rsrc_t rs, unsigned off, const double v[4]) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kmx_u4, make_double2(v[0], v[1])), rs, off, 0, 16);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kmx_u4, make_double2(v[2], v[3])), rs, off + 16, 0, 16);
-}
-// the gathered rows of a vector another workgroup of this launch wrote
-template <int R>
-struct WtRows {
-  __amdgpu_buffer_rsrc_t rs;
-  __device__ __forceinline__ void nbr(int o, double2 vr[2 * R]) const {
-    const unsigned b = (unsigned)max(o, 0) * (unsigned)(32 * R);
-#pragma unroll
-    for (int i = 0; i < 2 * R; ++i) vr[i] = wt_ld2(rs, b + 16u * i);
-  }
-  __device__ __forceinline__ void own(int, int, double*) {}  // (DIAG = false: the caller's registers)
-};
-
-// the tile's partials, written through (the robot sums read them sc1)
-template <int NV, int W>
-__device__ __forceinline__ void wt_tile_partials(const double* vals, double* dst, double* lds) {
-#pragma unroll
-  for (int s = 0; s < NV; ++s) {
-    const double w = wave_sum(vals[s]);
-    if ((threadIdx.x & 63) == 0) lds[s * W + (threadIdx.x >> 6)] = w;
-  }
-  __syncthreads();
-  if (threadIdx.x < NV) {
-    double t = 0.0;
-#pragma unroll
-    for (int w = 0; w < W; ++w) t += lds[threadIdx.x * W + w];
-    wt_st1(dst + threadIdx.x, t);
-  }
-}
-
-template <int R, int W>
-struct SmemRes {  // the gathers' layouts at 0 (the largest of k_grad's, k_step's, k_cost's), then per pose D, M^-1, S
-  static constexpr int TP = W * (64 / R);
-  static constexpr int a0 = SmemHG<R, W>::bytes > SmemF<R, W>::bytes ? SmemHG<R, W>::bytes : SmemF<R, W>::bytes;
-  static constexpr int a1 = a0 > SmemC<R, W>::bytes ? a0 : SmemC<R, W>::bytes;
-  static constexpr int d_off = (a1 + 15) / 16 * 16;  // double[TP][16]
-  static constexpr int p_off = d_off + TP * 16 * 8;  // double[TP][16]
-  static constexpr int s_off = p_off + TP * 16 * 8;  // double[TP][9]
-  static constexpr int g_off = s_off + TP * 9 * 8;   // double[TP][R][4]: g, then the trial point
-  static constexpr int CH = SmemH<R, W>::CH;          // a resident tile holds at most two chunks
-  template <int RW>
-  static constexpr int rec_off = g_off + TP * R * 32;  // double[2 CH][RW]: the tile's incidence records
-  template <int RW>
-  static constexpr int sp_off = rec_off<RW> + 2 * CH * RW * 8;  // int[TP + 1]: the tile's CSR offsets
-  template <int RW>
-  static constexpr int red_off = sp_off<RW> + ((TP + 1) * 4 + 15) / 16 * 16;  // double[8 * W]
-  template <int RW>
-  static constexpr int base_bytes = red_off<RW> + 8 * 8 * W;
-  // Hz and eta: in LDS when they fit (two fewer register-resident vectors for
-  // the 5-wave form, whose SIMDs host two waves: 256 VGPRs), else in registers
-  template <int RW>
-  static constexpr bool lv = W > 4 && base_bytes<RW> + 2 * TP * R * 32 + 304 <= 160 * 1024;
-  template <int RW>
-  static constexpr int hz_off = base_bytes<RW>;  // double[TP][R][4] (lv)
-  template <int RW>
-  static constexpr int et_off = hz_off<RW> + TP * R * 32;  // double[TP][R][4] (lv)
-  template <int RW>
-  static constexpr int bytes = base_bytes<RW> + (lv<RW> ? 2 * TP * R * 32 : 0);
-  static_assert(64 * W * 6 * 8 <= SmemH<R, W>::ptr_off, "group-op scratch inside the chunk area");
-  static_assert(bytes<16> + 304 <= 160 * 1024, "one resident workgroup per CU");
-};
-
-// KMX_RES_STAMPS builds (diagnostic, `make res_stamps`): thread 0 of every
-// workgroup records the wall clock (100 MHz) at the phases of the last round
-// (kmx_pgo_debug_step_stamps; scripts/res_stamps.py): 0 entry, 1 prologue, 2
-// gradient; per tCG pass jl < 17 at 4 + 5 jl: barrier arrival, release,
-// decision, gather, step end; 90 cost start, 91 cost end, 92 final release,
-// 93 exit; 94 tile poses, 95 tile incidences.
-#ifdef KMX_RES_STAMPS
-#define KMX_RS(i)                                                                                  \
-  do {                                                                                             \
-    const int i_ = (i);                                                                            \
-    if (threadIdx.x == 0 && blockIdx.x < RES_STAMP_TILES && i_ < 96)                               \
-      g_res_stamp[blockIdx.x * RES_STAMPS + i_] = wall_clock64();                                  \
-  } while (0)
-#else
-#define KMX_RS(i) do {} while (0)
-#endif
-
-// Scalar decisions of one tCG step, taken by thread 0 on the workgroup's copy
-// of its robot's state and broadcast through LDS.
-struct ResStep {
-  double coef, al, be;
-  int go;
-};
-// the round's static LDS besides the Ctl copy: 48 B, so the statics stay a
-// multiple of 16 B and the dynamic area 16-B aligned (Guideline 17)
-struct alignas(16) ResShared {
-  ResStep st;
-  int flag, pad[3];
-};
-
-// The resident round's Hessian gather (hinc_gather_src's arithmetic, sums and
-// order): the tile's records and CSR offsets are in LDS for the whole round,
-// so both chunks' neighbour rows are requested right after the decision — one
-// dependent round trip per tCG step instead of record -> row per chunk.
-// acc = the off-diagonal part of (Q V) for the lane's row; false: sync() or
-// pre() said the robot does not step (nothing gathered). sync() is the step's
-// grid barrier (it also issues the robot sums' loads), pre() waits for the
-// sums and takes the decision. EARLY: the neighbour rows are requested between
-// the two, so the decision's latency hides behind the rows' (a robot that
-// stops at the decision has loaded its rows for nothing) — where the
-// registers allow it: the 4-wave form (one wave per SIMD); the 5-wave form
-// (two waves on one SIMD, 256 VGPRs) spilled 70 -> 247 VGPRs with it.
-template <int R, int RW, int W, bool EARLY, typename Sync, typename Pre>
-__device__ __forceinline__ bool res_gather(const Lane& L, const double* recs, const int* sptr, const WtRows<R>& src,
-                                           double acc[4], double* Cs, Sync&& sync, Pre&& pre) {
-  using RC = Rec<RW>;
-  constexpr int CH = SmemH<R, W>::CH;
-  constexpr int OI = RW == 10 ? 9 : 14;  // the {other, edge | tail} word of a record
-  const int tid = threadIdx.x, n = L.n, pl = L.pose - L.p0;
-  acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
-  if (!sync()) return false;
-  if constexpr (!EARLY) {
-    if (!pre()) return false;
-  }
-  const int lt = min(tid, CH - 1);
-  auto other = [&](int k) { return unpack_int2(recs[(size_t)RW * max(min(k, n - 1), 0) + OI]).x; };
-  double2 v0[2 * R], v1[2 * R];
-  const bool two = n > CH;  // uniform
-  src.nbr(other(lt), v0);
-  if (two) src.nbr(other(CH + lt), v1);
-  if constexpr (EARLY) {
-    if (!pre()) return false;
-  }
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    if (c == 1 && !two) break;
-    const int k = c * CH + lt;
-    double2 q[RC::Q];
-    {
-      const double2* p2 = reinterpret_cast<const double2*>(recs + (size_t)RW * max(min(k, n - 1), 0));
-#pragma unroll
-      for (int i = 0; i < RC::Q; ++i) q[i] = p2[i];
-    }
-    Edge E;
-    RC::edge(q, E);
-    const int2 in = RC::inc(q);
-    const int o = in.x;
-    const bool tail = (in.y >> 31) & 1;
-    const double2* vr = c == 0 ? v0 : v1;
-    if (tid < CH && k < n) {
-      const double wk = (o >= 0) ? E.wk : 0.0, wt = (o >= 0) ? E.wt : 0.0;
-#pragma unroll
-      for (int a = 0; a < R; ++a) {
-        const double x0 = vr[2 * a].x, x1 = vr[2 * a].y, x2 = vr[2 * a + 1].x, x3 = vr[2 * a + 1].y;
-        double h[4];
-        if (tail) {
-#pragma unroll
-          for (int cc = 0; cc < 3; ++cc)
-            h[cc] = -(wk * (x0 * E.R[cc * 3 + 0] + x1 * E.R[cc * 3 + 1] + x2 * E.R[cc * 3 + 2]) + wt * x3 * E.t[cc]);
-          h[3] = -(wt * x3);
-        } else {
-#pragma unroll
-          for (int cc = 0; cc < 3; ++cc)
-            h[cc] = -(wk * (x0 * E.R[0 * 3 + cc] + x1 * E.R[1 * 3 + cc] + x2 * E.R[2 * 3 + cc]));
-          h[3] = -(wt * (x3 + (x0 * E.t[0] + x1 * E.t[1] + x2 * E.t[2])));
-        }
-        store4(Cs + (tid * R + a) * 4, h);
-      }
-    }
-    lds_barrier();
-    if (L.valid) {
-      const int c0 = c * CH;
-      const int j0 = max(sptr[pl], c0) - c0, j1 = min(sptr[pl + 1], c0 + CH) - c0;
-#pragma unroll 4
-      for (int j = j0; j < j1; ++j) {
-        double h[4];
-        load4(Cs + (j * R + L.a) * 4, h);
-        acc[0] += h[0]; acc[1] += h[1]; acc[2] += h[2]; acc[3] += h[3];
-      }
-    }
-    lds_barrier();
-  }
-  return true;
-}
-
-template <int R, int RW, int W>
-__device__ __forceinline__ void body_round(const Dev& d, unsigned* gb, unsigned* fail, int census, char* smem) {
-  using SM = SmemRes<R, W>;
-  __shared__ Ctl cs;
-  __shared__ ResShared rsh;
-  int& sflag = rsh.flag;
-  unsigned b = 0;
-  bool any;
-  if (census) {  // residency check: every workgroup must reach one barrier
-    (void)grid_sync(gb, 0, false, &any, fail, &sflag);
-    return;
-  }
-  const Lane L = lane_map<R>(d);
-  KMX_RS(0);
-#ifdef KMX_RES_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < RES_STAMP_TILES) {
-    g_res_stamp[blockIdx.x * RES_STAMPS + 94] = L.np;
-    g_res_stamp[blockIdx.x * RES_STAMPS + 95] = L.n;
-  }
-#endif
-  const size_t o = (size_t)L.pose * 4 * R + 4 * L.a;
-  const unsigned ob = (unsigned)o * 8u;  // byte offset of the lane's row
-  const int pl = L.pose - L.p0;
-  const bool writer = L.tile == L.rt0;
-  double* Dl = reinterpret_cast<double*>(smem + SM::d_off);
-  double* Pl = reinterpret_cast<double*>(smem + SM::p_off);
-  double* Sl = reinterpret_cast<double*>(smem + SM::s_off);
-  double* gx = reinterpret_cast<double*>(smem + SM::g_off) + 4 * (pl * R + L.a);  // this lane's row of g / Xt
-  double* recs = reinterpret_cast<double*>(smem + SM::template rec_off<RW>);
-  int* sptr = reinterpret_cast<int*>(smem + SM::template sp_off<RW>);
-  double* red = reinterpret_cast<double*>(smem + SM::template red_off<RW>);
-  double* rl = red;  // robot sums' scratch (8 x WAVES), used after the tile partials are out
-  double* scr = reinterpret_cast<double*>(smem);  // group-op scratch (the chunk area, between gathers)
-  const __amdgpu_buffer_rsrc_t rz = wt_rsrc(d.z, d.vec), rw0 = wt_rsrc(d.w0, d.vec), rw1 = wt_rsrc(d.w1, d.vec),
-                               rxt = wt_rsrc(d.Xt, d.vec);
-  // the robot's state (k_begin's), one copy per workgroup; GNC state commit
-  if (threadIdx.x < (int)(sizeof(Ctl) / 8))
-    reinterpret_cast<double*>(&cs)[threadIdx.x] = reinterpret_cast<const double*>(d.ctl + L.l)[threadIdx.x];
-  if (blockIdx.x == 0 && threadIdx.x == 0) store_gnc(d.gnc, load_gnc(d.gnc_next));
-  if (d.gnc_next->fired) {  // k_begin re-weighted: this tile's D_i and M^-1 (k_grad's gated prologue)
-    for (int t = threadIdx.x; t < L.np; t += blockDim.x) pose_precond<RW>(d, L.p0 + t);
-  }
-  __syncthreads();
-  // per-pose blocks into LDS (the tile's own poses, rebuilt above by this workgroup or by an earlier launch)
-  for (int i = threadIdx.x; i < L.np * 2; i += blockDim.x) {
-    const int p = i >> 1;
-    double M[16];
-    load_sym4((i & 1 ? d.Pinv : d.hD) + SYM4 * (size_t)(L.p0 + p), M);
-    double* dst = (i & 1 ? Pl : Dl) + 16 * p;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[k] = M[k];
-  }
-  // the tile's records and CSR offsets, for every tCG step's gather (the host
-  // keeps a resident tile within two chunks)
-  {
-    double2* dst2 = reinterpret_cast<double2*>(recs);  // the register form, 16-B parts
-    for (int i = threadIdx.x; i < L.n; i += blockDim.x) {
-      double2 q[Rec<RW>::Q];
-      Rec<RW>::load(d, (size_t)(L.k0 + i), q);
-#pragma unroll
-      for (int j = 0; j < Rec<RW>::Q; ++j) dst2[(size_t)i * Rec<RW>::Q + j] = q[j];
-    }
-    if (threadIdx.x <= L.np) sptr[threadIdx.x] = d.inc_ptr[L.p0 + threadIdx.x] - L.k0;
-  }
-  const int ph0 = cs.phase;  // (read before any barrier of this launch: every thread sees k_begin's value)
-  KMX_RS(1);
-  // -------- gradient (body_grad's arithmetic; X and the public table are the round's start) --------
-  double y[4] = {0, 0, 0, 0}, rn[4] = {0, 0, 0, 0}, zn[4] = {0, 0, 0, 0};
-  const bool grad = ph0 == PH_START;
-  if (grad) {
-    double G[4], cost = 0.0;
-    hinc_grad<R, RW, W>(d, L, d.X, d.pub, G, &cost, smem);
-    if (L.valid) load4(d.X + o, y);
-    double S[9], gr[4];
-    group_symYtG<R, true>(y, G, L.base, S, scr);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) gr[c] = G[c] - (y[0] * S[0 * 3 + c] + y[1] * S[1 * 3 + c] + y[2] * S[2 * 3 + c]);
-    gr[3] = G[3];
-    // S as k_grad stores it (6 entries) and k_step reads it back (load_sym3)
-    if (L.valid && L.a == 0) {
-      double* Sp = Sl + 9 * pl;
-      Sp[0] = S[0]; Sp[1] = S[1]; Sp[2] = S[2]; Sp[3] = S[4]; Sp[4] = S[5]; Sp[5] = S[8];
-    }
-    double Pm[16];
-    if (L.valid) {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) Pm[k] = Pl[16 * pl + k];
-    }
-    group_precon<R, true>(d, L.pose, L.valid, y, gr, L.base, zn, scr, Pm, L.valid);
-    double vals[3] = {cost, 0.0, 0.0};
-    if (L.valid) {
-      vals[1] = gr[0] * gr[0] + gr[1] * gr[1] + gr[2] * gr[2] + gr[3] * gr[3];
-      vals[2] = zn[0] * gr[0] + zn[1] * gr[1] + zn[2] * gr[2] + zn[3] * gr[3];
-      wt_st4(rz, ob, zn);  // z_0: step 0 gathers it
-#pragma unroll
-      for (int c = 0; c < 4; ++c) gx[c] = gr[c];  // g waits in LDS for the model decrease
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) rn[c] = gr[c];  // r_0 = g
-    wt_tile_partials<3, W>(vals, d.part + (size_t)L.tile * NPART, red);
-  }
-  KMX_RS(2);
-  // -------- tCG, one barrier per step (body_step's arithmetic) --------
-  constexpr bool LV = SM::template lv<RW>;
-  double* hzl = reinterpret_cast<double*>(smem + SM::template hz_off<RW>) + 4 * (pl * R + L.a);
-  double* etl = reinterpret_cast<double*>(smem + SM::template et_off<RW>) + 4 * (pl * R + L.a);
-  double hzr[4] = {0, 0, 0, 0}, dl[4] = {0, 0, 0, 0}, hdl[4] = {0, 0, 0, 0}, wn[4] = {0, 0, 0, 0},
-         etr[4] = {0, 0, 0, 0};
-  if constexpr (LV) {  // eta starts at 0
-    if (L.valid) store4(etl, etr);
-  }
-  bool formed = grad;   // this workgroup's robot formed the step the next barrier's consumers need
-  bool trial = false;   // its tCG ended this round: the trial point is in LDS (gx) and published
-  int k = -1;           // the step whose partials the next decision consumes
-  // Every thread takes the step's decision from the robot sums and the
-  // state's copy (as k_step's workgroups do); thread 0 applies the same
-  // control steps to the copy (control_core: counters, coefh, team status
-  // through the robot's first tile) between its arrival at the next barrier
-  // and its poll, off the critical path.
-  int pend = 0;         // thread 0: 1 a gradient, 2 a tCG step's control update waits for the next barrier
-  double pq[4] = {0.0, 0.0, 0.0, 0.0};
-  auto apply_pending = [&]() {
-    if (pend == 1) {
-      double t4[NPART] = {pq[0], pq[1], pq[2], 0.0};
-      control_core(cs, d, L.l, RED_GRAD, t4, R, writer);
-    } else if (pend == 2) {
-      cs.z_r = pq[1];
-      double th[NPART] = {pq[0], 0.0, 0.0, 0.0};
-      control_core(cs, d, L.l, RED_HESS, th, R, writer);
-      double tu[NPART] = {pq[2], pq[3], 0.0, 0.0};
-      control_core(cs, d, L.l, RED_UPDATE, tu, R, writer);
-    }
-    pend = 0;
-  };
-  for (int jl = 0;; ++jl) {
-    bool go = false;
-    double coef = 0.0, al = 0.0, be = 0.0;
-    RobotSum<3, 2, true> rg;  // (<= 512 tiles per robot: one pass)
-    RobotSum8<2, true> rf;
-    const double* pf_in = d.part_f + (size_t)((k & 1) * d.ntiles) * 8;
-    constexpr bool EARLY = W == 4;  // res_gather: the rows requested before the decision
-    auto sync = [&]() -> bool {
-      KMX_RS(4 + 5 * jl);
-      if (!grid_sync(gb, b++, formed, &any, fail, &sflag, apply_pending)) return false;
-      KMX_RS(5 + 5 * jl);
-      if (!any) return false;
-      if (!formed) return false;  // not in tCG (skipped, idle, or stopped earlier)
-      if constexpr (EARLY) {
-        if (jl == 0) rg.issue(d.part, NPART, L.rt0, L.rt1);
-        else rf.issue(pf_in, L.rt0, L.rt1);
-      }
-      return true;
-    };
-    auto decide = [&]() -> bool {
-      if (jl == 0) {
-        double t4[NPART];
-        if constexpr (EARLY) {
-          rg.finish(d.part, NPART, rl, t4);
-        } else {  // (the sums' registers scoped to this branch: the 5-wave form's VGPR budget)
-          RobotSum<3, 2, true> rg2;
-          rg2.issue(d.part, NPART, L.rt0, L.rt1);
-          rg2.finish(d.part, NPART, rl, t4);
-        }
-        go = !(sqrt(t4[1]) < d.p.gn_tol);  // control_core's RED_GRAD test (RTR: the tCG starts)
-        if (threadIdx.x == 0) {
-          pend = 1;
-          pq[0] = t4[0]; pq[1] = t4[1]; pq[2] = t4[2];
-        }
-      } else {
-        double tot[8];
-        if constexpr (EARLY) {
-          rf.finish(pf_in, rl, tot);
-        } else {
-          RobotSum8<2, true> rf2;
-          rf2.issue(pf_in, L.rt0, L.rt1);
-          rf2.finish(pf_in, rl, tot);
-        }
-        const double zr = tot[1];
-        const HessStep hx = hess_step(zr, cs.e_Pe, cs.e_Pd, cs.d_Pd, cs.Delta, tot[0]);
-        double rrn, zrn;
-        onesync_scalars(hx.alpha, tot, &rrn, &zrn);
-        const UpdStep u = upd_step(hx.boundary ? MODE_BOUNDARY : MODE_INTERIOR, cs.r_stop, cs.lin_stop, zr, k + 1,
-                                   rrn, zrn, d.p);
-        coef = hx.coef;
-        al = hx.alpha;
-        be = u.beta;
-        go = !u.done;
-        if (threadIdx.x == 0) {
-          pend = 2;
-          pq[0] = tot[0]; pq[1] = zr; pq[2] = rrn; pq[3] = zrn;
-        }
-      }
-      KMX_RS(6 + 5 * jl);
-      return go;
-    };
-    double H[4];
-    WtRows<R> src{jl == 0 ? rz : ((k & 1) ? rw1 : rw0)};
-    res_gather<R, RW, W, EARLY>(L, recs, sptr, src, H, reinterpret_cast<double*>(smem), sync, decide);
-    if (sflag == 0) return;  // a barrier gave up (the fail word is set)
-    KMX_RS(7 + 5 * jl);
-    if (!any) break;
-    if (formed && !go && jl > 0) {
-      // the robot's tCG ends here: the last residual, eta's last direction
-      // (this decision's coefficient), the trial point and the model partials
-#pragma unroll
-      for (int c = 0; c < 4; ++c) rn[c] = fma(coef, hdl[c], rn[c]);
-      double et[4] = {etr[0], etr[1], etr[2], etr[3]};
-      if constexpr (LV) {
-        if (L.valid) load4(etl, et);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) et[c] += coef * dl[c];
-      double xt[4];
-      group_retract<R>(y, et, L.base, xt);
-      double vals[2] = {0.0, 0.0};
-      if (L.valid) {
-        wt_st4(rxt, ob, xt);
-        double m = 0.0, ch = 0.0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          m += et[c] * (gx[c] + rn[c]);
-          const double dd = xt[c] - y[c];
-          ch += dd * dd;
-        }
-        vals[0] = m;
-        vals[1] = ch;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) gx[c] = xt[c];  // the trial cost's own row (and the commit's)
-      }
-      wt_tile_partials<2, W>(vals, d.part + (size_t)L.tile * NPART + 2, red);
-      trial = true;
-    }
-    formed = go;
-    if (!go) continue;
-    const int kn = k + 1;  // the step this pass forms
-    double v[4], S[9];
-    if (jl == 0) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] = zn[c];
-    } else {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] = wn[c];
-    }
-    if (L.valid) {
-      const double* Dp = Dl + 16 * pl;
-#pragma unroll
-      for (int c = 0; c < 4; ++c)  // the diagonal block (hinc_gather's DIAG term, same expression)
-        H[c] += v[0] * Dp[4 * c] + v[1] * Dp[4 * c + 1] + v[2] * Dp[4 * c + 2] + v[3] * Dp[4 * c + 3];
-      load_sym3(Sl + 9 * pl, S);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 9; ++i) S[i] = 0.0;
-    }
-    __syncthreads();  // the chunk area (group-op scratch) is free: every wave left the gather's last LDS read
-    double hv[4];
-    group_rhess<R, true>(y, v, H, S, L.base, hv, scr);
-    if (jl == 0) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        hzr[c] = hv[c];
-        dl[c] = -v[c];
-        hdl[c] = -hv[c];
-      }
-      if constexpr (LV) {
-        if (L.valid) store4(hzl, hzr);
-      }
-    } else {
-      // eta += coef_k delta_k (the serial order of the folds), then the step's recurrences
-      double et[4] = {etr[0], etr[1], etr[2], etr[3]}, hzn[4] = {hzr[0], hzr[1], hzr[2], hzr[3]};
-      if constexpr (LV) {
-        if (L.valid) {
-          load4(etl, et);
-          load4(hzl, hzn);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) et[c] += coef * dl[c];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const double hold = hdl[c], dold = dl[c];
-        rn[c] = fma(coef, hold, rn[c]);
-        zn[c] = fma(al, v[c], zn[c]);
-        hzn[c] = fma(al, hv[c], hzn[c]);
-        dl[c] = fma(be, dold, -zn[c]);
-        hdl[c] = fma(be, hold, -hzn[c]);
-      }
-      if constexpr (LV) {
-        if (L.valid) {
-          store4(etl, et);
-          store4(hzl, hzn);
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          etr[c] = et[c];
-          hzr[c] = hzn[c];
-        }
-      }
-    }
-    double Pm[16];
-    if (L.valid) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) Pm[i] = Pl[16 * pl + i];
-    }
-    group_precon<R, true>(d, L.pose, L.valid, y, hdl, L.base, wn, scr, Pm, L.valid);
-    double pv[7] = {0, 0, 0, 0, 0, 0, 0};
-    if (L.valid) {
-      pv[0] = dot4(dl, hdl);
-      pv[1] = dot4(rn, zn);
-      pv[2] = dot4(rn, rn);
-      pv[3] = dot4(rn, wn) + dot4(hdl, zn);
-      pv[4] = dot4(hdl, wn);
-      pv[5] = dot4(rn, hdl);
-      pv[6] = dot4(hdl, hdl);
-      wt_st4((kn & 1) ? rw1 : rw0, ob, wn);
-    }
-    wt_tile_partials<7, W>(pv, d.part_f + ((size_t)(kn & 1) * d.ntiles + L.tile) * 8, red);
-    KMX_RS(8 + 5 * jl);
-    k = kn;
-  }
-  // -------- trial cost, accept, commit (body_cost + body_commit's fold) --------
-  KMX_RS(90);
-  if (trial) {  // uniform per robot: the owner incidences' cost of the trial point
-    using SC = SmemC<R, W>;
-    int* sptr = reinterpret_cast<int*>(smem + SC::ptr_off);
-    const double2* xs = reinterpret_cast<const double2*>(smem + SM::g_off);  // the tile's trial rows
-    const int tid = threadIdx.x, np = L.np, K0 = L.k0, n = L.n;
-    __syncthreads();
-    if (tid <= np) sptr[tid] = d.inc_ptr[L.p0 + tid] - K0;
-    __syncthreads();
-    double cost = 0.0;
-    using RC = Rec<RW>;
-    for (int kk = tid; kk < n; kk += 64 * W) {
-      double2 q[RC::Q];
-      RC::load(d, (size_t)(K0 + kk), q);
-      const int2 in = RC::inc(q);
-      const int ot = in.x;
-      const bool tail = (in.y >> 31) & 1;
-      if (ot >= 0 && !tail) continue;
-      int lo = 0, hi = np;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (sptr[mid] <= kk) lo = mid;
-        else hi = mid;
-      }
-      const double2* s2 = xs + lo * 2 * R;
-      double2 vs2[2 * R], vo2[2 * R];
-      if (ot >= 0) {
-        const unsigned bo = (unsigned)ot * (unsigned)(32 * R);
-#pragma unroll
-        for (int i = 0; i < 2 * R; ++i) vo2[i] = wt_ld2(rxt, bo + 16u * i);
-      } else {
-        const double2* o2 = reinterpret_cast<const double2*>(d.pub + (size_t)(-1 - ot) * 4 * R);
-#pragma unroll
-        for (int i = 0; i < 2 * R; ++i) vo2[i] = o2[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 2 * R; ++i) vs2[i] = s2[i];
-      Edge E;
-      RC::edge(q, E);
-      double c = 0.0;
-#pragma unroll
-      for (int a = 0; a < R; ++a) {
-        const double vs[4] = {vs2[2 * a].x, vs2[2 * a].y, vs2[2 * a + 1].x, vs2[2 * a + 1].y};
-        const double vo[4] = {vo2[2 * a].x, vo2[2 * a].y, vo2[2 * a + 1].x, vo2[2 * a + 1].y};
-        double dummy[4] = {0.0, 0.0, 0.0, 0.0};
-        c += incidence_row(E, tail, vs, vo, dummy);
-      }
-      cost += c;
-    }
-    wt_tile_partials<1, W>(&cost, d.part + (size_t)L.tile * NPART, red);
-  }
-  KMX_RS(91);
-  if (!grid_sync(gb, b++, false, &any, fail, &sflag)) return;
-  KMX_RS(92);
-  bool commit = false;
-  if (trial) {
-    RobotSum<NPART, 2, true> rs;
-    rs.issue(d.part, NPART, L.rt0, L.rt1);
-    double tot[NPART] = {0.0, 0.0, 0.0, 0.0};
-    rs.finish(d.part, NPART, rl, tot);
-    {  // control_on's RED_COST acceptance test (body_commit's fold)
-      const double model_dec = -0.5 * tot[2];
-      const double rho = (model_dec > 0.0) ? (cs.f_cur - tot[0]) / model_dec : -1.0;
-      commit = rho > d.p.accept_rho;
-    }
-    if (threadIdx.x == 0) {
-      control_core(cs, d, L.l, RED_COST, tot, R, writer);
-      cs.phase = PH_STEP;
-    }
-  }
-  __syncthreads();
-  if (writer && threadIdx.x < (int)(sizeof(Ctl) / 8))
-    reinterpret_cast<double*>(d.ctl + L.l)[threadIdx.x] = reinterpret_cast<const double*>(&cs)[threadIdx.x];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    d.gnc->inner += 1;
-    d.gnc->rounds += 1;
-  }
-  KMX_RS(93);
-  if (!commit || !L.valid) return;
-  double xt[4] = {gx[0], gx[1], gx[2], gx[3]};
-  store4(d.X + o, xt);
-  const int s = d.pose_slot[L.pose];
-  if (s >= 0) store4(d.pub + (size_t)s * 4 * R + 4 * L.a, xt);
-}
-
-// W = 4: up to two workgroups per CU (2 waves per SIMD); W = 5 (r = 5 only):
-// 60-pose tiles, one workgroup per CU (a SIMD hosts two of its waves), so a
-// 12.5k-pose shard needs fewer workgroups than the device has CUs and no CU
-// runs two tiles (a CU with two took ~10 us more per tCG step than one with
-// one: the barrier waits for it; profiles/r05/resident/)
-template <int R, int RW, int W>
-__global__ __launch_bounds__(64 * W, W > 4 ? 2 : 1) void k_round(Dev d, unsigned* gb, unsigned* fail, int census) {
-  KMX_SMEM;
-  body_round<R, RW, W>(d, gb, fail, census, smem);
 }
 
 // ------------------------------------------------- round begin + GNC-TLS ---
@@ -3188,8 +2369,6 @@ __global__ void k_begin(Dev d, const unsigned char* active, int mode, int R_) {
   const bool fire = d.p.robust && ((mode & BEGIN_FORCE_GNC) ? true : gnc_should_update(d));
   const double mu = d.gnc->mu;
   if (blockIdx.x == 0) {
-    if (d.gbar)  // the resident round's barrier counters start every round at zero (word 0 of each line)
-      for (int i = threadIdx.x; i < GB_BMAX * GB_REP; i += blockDim.x) d.gbar[i * GB_STRIDE] = 0u;
     if (mode & BEGIN_ROUND)
       for (int l = threadIdx.x; l < d.L; l += blockDim.x) begin_robot(d, active, l);
     if (threadIdx.x == 0) {
@@ -3624,6 +2803,16 @@ struct kmx_pgo {
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
   bool xchg = false, xchg_self_p2p = false;
+  // KMX_XCHG_LAG=1 (a measurement mode, off by default):
+  // the exchange of the rows published after round i-1 runs on xstream while
+  // round i computes, and round i+1 installs them — a one-round-stale public
+  // table (round k >= 2 reads the peers' rows of X^(k-2)). It changes the
+  // iterate sequence and lets the ranks' GNC decisions drift apart (a peer's
+  // status word is a round older too), so it is a timing instrument only.
+  int xchg_lag = 0;
+  bool x_inflight = false;
+  hipStream_t xstream = nullptr;
+  hipEvent_t ev_xg = nullptr, ev_xd = nullptr;
   int *d_xs_slots = nullptr, *d_xr_slots = nullptr, *d_xs_seg = nullptr, *d_xr_seg = nullptr;
   int *d_xs_rseg = nullptr, *d_xr_rseg = nullptr;  // segment index of every row
   double *d_xsbuf = nullptr, *d_xrbuf = nullptr;
@@ -3631,6 +2820,17 @@ struct kmx_pgo {
   std::vector<long long> xs_cnt, xr_cnt, xs_off, xr_off;  // per peer, in doubles (rows * 4r + 1 status)
   int blind_left = 0;
   static constexpr int BLIND_SLACK = 2, BLIND_WINDOW = 8;
+  // Gated k_hess launches (KMX_HESS_GATE=0: off): every k_hess launch after a
+  // tCG's first tests its robot's phase before its first record chunk is
+  // fetched. Ungated, a launch enqueued before the host knows whether any robot
+  // is still in tCG fetched that chunk before the test (the records' round
+  // trip overlapping the state's), so a launch every robot skips still read
+  // ~42 MB at configs[3]. Measured (profiles/r06/hess_gate/, two runs each):
+  // gating every launch after the first 0.685 / 0.683 ms per round, ungated
+  // 0.692 / 0.691, gating only the steps at or past where the last polled loop
+  // stopped 0.691 / 0.691 — the state's round trip costs a gated launch less
+  // than a skipped launch's record fetch costs the round.
+  bool hess_gate = true;
   // (measured and removed: a hipStreamQuery before the status spin put a ~5 us
   // bubble before the next tCG step's first kernel, profiles/r02/ab_query)
   // reduction mode: set per graph (below) unless KMX_RED forces one (0 launch,
@@ -3653,19 +2853,6 @@ struct kmx_pgo {
   // Nesterov acceleration (P.acceleration): momentum V and this round's Y
   // (allocated only when enabled), gamma and the restart counter on the host
   double *d_accV = nullptr, *d_accY = nullptr;
-  // KMX_TCG_FORM_RESIDENT: one persistent launch per round (k_round) when every
-  // tile fits resident (decided at set_graph: occupancy query + census launch)
-  bool res_on = false;
-  int res_w = 4;               // waves per workgroup of the resident round (the tile cut's)
-  int max_tile_inc = 0;        // incidences of the largest tile
-  int res_cap = 0;             // workgroups of k_round resident on the device
-  std::string res_reason = "tcg_form is not KMX_TCG_FORM_RESIDENT";
-  unsigned* d_gbar = nullptr;  // grid-barrier words (GB_WORDS)
-  unsigned* h_fail = nullptr;  // host-mapped: nonzero when a barrier wait gave up (1 + its index)
-  bool fuse_red = false;       // RM_LAUNCH tCG launches carry their reducers (Dev::fuse_red; KMX_FUSE_RED=1: on)
-  bool fuse_forced_off = true;  // opt-in: level with the k_reduce launches at 100k (8.72-8.75e8 vs 8.70e8, one box)
-                                // while each launch then holds the reduction's ~3 us tail (profiles/r05/fused_red/)
-  unsigned* d_red_cnt = nullptr;
   double acc_gamma = 0.0;
   int acc_k = 0;
   bool acc_ready = false, acc_started = false;
@@ -3714,6 +2901,8 @@ int dalloc(T** p, size_t count) {
 }
 
 void free_xchg(kmx_pgo* h) {
+  if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+  h->x_inflight = false;
   void* ptrs[] = {h->d_xs_slots, h->d_xr_slots, h->d_xs_seg, h->d_xr_seg, h->d_xs_rseg, h->d_xr_rseg,
                   h->d_xsbuf, h->d_xrbuf};
   for (void* q : ptrs)
@@ -3730,7 +2919,7 @@ void free_dev(kmx_pgo* h) {
                   h->d_pose_slot, h->d_gnc_edge, h->d_gnc_ends, h->d_sh_edge, h->d_sh_idx, h->d_osh_edge,
                   h->d_osh_idx, h->d_relc, h->d_gnc, h->d_ext, h->d_active, h->d_scratch, h->d_hv_launch,
                   h->d_accV, h->d_accY, h->d_ctl2, h->d_part_h,
-                  h->d_part_u, h->d_coefh, h->d_part_f, h->d_gbar, h->d_red_cnt};
+                  h->d_part_u, h->d_coefh, h->d_part_f};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   h->d_tile = nullptr;
@@ -3758,9 +2947,6 @@ void free_dev(kmx_pgo* h) {
   h->d_coefh = nullptr;
   h->d_part_h = h->d_part_u = nullptr;
   h->d_part_f = nullptr;
-  h->d_gbar = nullptr;
-  h->d_red_cnt = nullptr;
-  h->res_on = false;
 }
 
 hipEvent_t next_event(kmx_pgo* h) {
@@ -3777,8 +2963,7 @@ bool ready(kmx_pgo* h) { return h && h->d_vec != nullptr; }
 // Vectors of d_vec: X Xt g r z hd eta + the tCG directions kept for k_retract
 // (+ Hz, w_0, w_1 for the one-sync tCG, which needs two directions).
 bool onesync(const kmx_pgo* h) {
-  return (h->P.tcg_form == KMX_TCG_FORM_ONESYNC || h->P.tcg_form == KMX_TCG_FORM_RESIDENT) &&
-         h->P.method == KMX_METHOD_RTR;
+  return h->P.tcg_form == KMX_TCG_FORM_ONESYNC && h->P.method == KMX_METHOD_RTR;
 }
 int dh_count(const kmx_pgo* h) {
   return std::max(onesync(h) ? 2 : 1, std::min(h->P.tcg_max_iterations, DHMAX));
@@ -3976,13 +3161,15 @@ void enqueue_tcg_t(kmx_pgo* h) {
     poll = poll && h->poll;  // a poll timeout inside wait_running switches to blind
     const unsigned long long seq = poll ? ++h->seq : 0;
     HostStatus* hs = poll ? h->hstat : nullptr;
+    const bool gate = j > 0 && h->hess_gate;
+    const int fl = (j == 0 ? 1 : 0) | (gate ? 2 : 0);
     if constexpr (RM == RM_CONSUMER) {
       // k_hess reports the stop test of the previous step's update
       if (slot >= 0)  // the events take the dispatch's own start / end timestamps
         hipExtLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, e0, e1, 0u, h->dv,
-                              j == 0 ? 1 : 0, slot, hs, seq);
+                              fl, slot, hs, seq);
       else
-        hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
+        hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, fl, slot,
                            hs, seq);
       hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, 0ull, slot);
       if (poll && j > 0 && !wait_running(h, seq)) {
@@ -3992,26 +3179,14 @@ void enqueue_tcg_t(kmx_pgo* h) {
       }
       continue;
     }
-    if (h->fuse_red) {  // each launch carries its robots' reducers (red_fused)
-      const dim3 gr(h->ntiles + h->dv.L);
-      if (slot >= 0)
-        hipExtLaunchKernelGGL((k_hess<R, RW, RM>), gr, blk, SmemH<R>::bytes, h->stream, e0, e1, 0u, h->dv,
-                              j == 0 ? 1 : 0, slot, (HostStatus*)nullptr, 0ull);
-      else
-        hipLaunchKernelGGL((k_hess<R, RW, RM>), gr, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
-                           nullptr, 0ull);
-      hipLaunchKernelGGL((k_update<R, RM>), gr, blk, SmemU::bytes, h->stream, h->dv, hs, seq, -1);
-    } else {
-      if (slot >= 0)
-        hipExtLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, e0, e1, 0u, h->dv,
-                              j == 0 ? 1 : 0, slot, (HostStatus*)nullptr, 0ull);
-      else
-        hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, j == 0 ? 1 : 0, slot,
-                           nullptr, 0ull);
-      red_t<R, RM>(h, RED_HESS, nullptr, 0, slot);
-      hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, seq, -1);
-      red_t<R, RM>(h, RED_UPDATE, hs, seq, -1, nullptr);
-    }
+    if (slot >= 0)
+      hipExtLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, e0, e1, 0u, h->dv, fl, slot,
+                            (HostStatus*)nullptr, 0ull);
+    else
+      hipLaunchKernelGGL((k_hess<R, RW, RM>), grid, blk, SmemH<R>::bytes, h->stream, h->dv, fl, slot, nullptr, 0ull);
+    red_t<R, RM>(h, RED_HESS, nullptr, 0, slot);
+    hipLaunchKernelGGL((k_update<R, RM>), grid, blk, SmemU::bytes, h->stream, h->dv, nullptr, seq, -1);
+    red_t<R, RM>(h, RED_UPDATE, hs, seq, -1, nullptr);
     if (poll) {
       if (j > 0 && !wait_running(h, prev)) {
         steps = j + 1;
@@ -4045,122 +3220,8 @@ void enqueue_trial_t(kmx_pgo* h, bool rgd) {
   if (!fold_cost<RM>(h)) red_t<R, RM>(h, RED_COST);
 }
 
-// KMX_TCG_FORM_RESIDENT: the round begin (GNC decision and re-weighting; the
-// preconditioner rebuild is left to k_round), then the whole block update.
-template <int R, int RW, int W>
-void launch_round(kmx_pgo* h, int census) {
-  hipLaunchKernelGGL((k_round<R, RW, W>), dim3(h->ntiles), dim3(64 * W), (SmemRes<R, W>::template bytes<RW>), h->stream, h->dv,
-                     h->d_gbar, h->h_fail, census);
-}
-template <int R, int RW>
-void launch_round_w(kmx_pgo* h, int census) {
-  if constexpr (R == 5) {
-    if (h->res_w == 5) return launch_round<R, RW, 5>(h, census);
-  }
-  launch_round<R, RW, 4>(h, census);
-}
-template <int R, int RW>
-void enqueue_resident_t(kmx_pgo* h, const unsigned char* d_active) {
-  (void)enqueue_begin(h, d_active, BEGIN_ROUND, true);
-  launch_round_w<R, RW>(h, 0);
-}
-
-// Whether the resident round can run on this handle: RTR with one RTR
-// iteration, every robot's tiles within one pass of the robot sums, and every
-// tile resident at once — the occupancy query's workgroups per CU times the
-// CUs, then a census launch in which every workgroup must reach one grid
-// barrier (a workgroup that does not fit would leave the others spinning until
-// the bounded wait gives up: MI355X_MICROARCH.md "Residency").
-template <int R, int RW>
-int resident_setup_t(kmx_pgo* h) {
-  h->res_on = false;
-  if (h->P.method != KMX_METHOD_RTR) { h->res_reason = "RGD method"; return 0; }
-  if (h->P.rtr_iterations != 1) { h->res_reason = "rtr_iterations != 1"; return 0; }
-  if (h->P.tcg_max_iterations + 3 > GB_BMAX) {  // a barrier per tCG pass, the gradient's and the cost's
-    h->res_reason = "tcg_max_iterations > " + std::to_string(GB_BMAX - 3);
-    return 0;
-  }
-  if (h->max_tile_inc > 2 * h->res_w * (64 / R) * R) {
-    h->res_reason = "a tile holds more than two gather chunks (tile_incidences " +
-                    std::to_string(h->P.tile_incidences) + ")";
-    return 0;
-  }
-  for (size_t l = 0; l + 1 < h->rt0_h.size(); ++l)
-    if (h->rt0_h[l + 1] - h->rt0_h[l] > 2 * RBLOCK) {
-      h->res_reason = "a robot has more than 512 tiles";
-      return 0;
-    }
-  int nb = 0, cus = 0;
-  if constexpr (R == 5) {
-    if (h->res_w == 5) {
-      if (SmemRes<R, 5>::template bytes<RW> > 65536)
-        KMX_HIP(hipFuncSetAttribute((const void*)k_round<R, RW, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    SmemRes<R, 5>::template bytes<RW>));
-      KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_round<R, RW, 5>, 64 * 5,
-                                                           SmemRes<R, 5>::template bytes<RW>));
-    }
-  }
-  if (h->res_w != 5) {
-    if (SmemRes<R, 4>::template bytes<RW> > 65536)
-      KMX_HIP(hipFuncSetAttribute((const void*)k_round<R, RW, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  SmemRes<R, 4>::template bytes<RW>));
-    KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_round<R, RW, 4>, 64 * 4,
-                                                         SmemRes<R, 4>::template bytes<RW>));
-  }
-  KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
-  h->res_cap = nb * cus;
-  if (h->ntiles > h->res_cap) {
-    h->res_reason = std::to_string(h->ntiles) + " tiles > " + std::to_string(h->res_cap) + " resident workgroups (" +
-                    std::to_string(nb) + " per CU)";
-    return 0;
-  }
-  if (!h->d_gbar)
-    if (int rc = dalloc(&h->d_gbar, GB_WORDS)) return rc;
-  if (!h->h_fail) {
-    KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_fail), sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
-  }
-  *h->h_fail = 0;
-  KMX_HIP(hipMemsetAsync(h->d_gbar, 0, sizeof(unsigned) * GB_WORDS, h->stream));
-  launch_round_w<R, RW>(h, 1);
-  KMX_HIP(hipGetLastError());
-  KMX_HIP(hipStreamSynchronize(h->stream));
-  if (__atomic_load_n(h->h_fail, __ATOMIC_ACQUIRE) != 0) {
-    *h->h_fail = 0;
-    h->res_reason = "census: the " + std::to_string(h->ntiles) + " workgroups were not all resident";
-    return 0;
-  }
-  h->dv.gbar = h->d_gbar;
-  h->res_on = true;
-  h->res_reason = "";
-  return 0;
-}
-template <int R>
-int resident_setup_r(kmx_pgo* h) {
-  return h->rw == 10 ? resident_setup_t<R, 10>(h) : resident_setup_t<R, 16>(h);
-}
-int resident_setup(kmx_pgo* h) {
-  h->dv.gbar = nullptr;
-  h->res_on = false;
-  if (h->P.tcg_form != KMX_TCG_FORM_RESIDENT) {
-    h->res_reason = "tcg_form is not KMX_TCG_FORM_RESIDENT";
-    return 0;
-  }
-  switch (h->P.r) {
-    case 3: return resident_setup_r<3>(h);
-    case 4: return resident_setup_r<4>(h);
-    case 5: return resident_setup_r<5>(h);
-    case 6: return resident_setup_r<6>(h);
-    case 7: return resident_setup_r<7>(h);
-    default: return resident_setup_r<8>(h);
-  }
-}
-
 template <int R, int RW, int RM>
 void enqueue_round_t(kmx_pgo* h, const unsigned char* d_active) {
-  if (h->res_on) {
-    enqueue_resident_t<R, RW>(h, d_active);
-    return;
-  }
   // no tiles: nothing would run the deferred rebuild
   const bool pend = enqueue_begin(h, d_active, BEGIN_ROUND, h->ntiles > 0);
   const bool rgd = h->P.method == KMX_METHOD_RGD;
@@ -4268,9 +3329,9 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
             "acceleration is 0 or 1, restart_interval >= 0");
   KMX_CHECK(params->method == KMX_METHOD_RTR || params->method == KMX_METHOD_RGD, KMX_EUNSUP,
             "method must be KMX_METHOD_RTR or KMX_METHOD_RGD");
-  KMX_CHECK(params->tcg_form == KMX_TCG_FORM_STANDARD || params->tcg_form == KMX_TCG_FORM_ONESYNC ||
-                params->tcg_form == KMX_TCG_FORM_RESIDENT,
-            KMX_EINVAL, "tcg_form must be KMX_TCG_FORM_STANDARD, _ONESYNC or _RESIDENT");
+  // (tcg_form 2, the resident round of ABI 7, was removed in ABI 8: DESIGN.md section 10)
+  KMX_CHECK(params->tcg_form == KMX_TCG_FORM_STANDARD || params->tcg_form == KMX_TCG_FORM_ONESYNC, KMX_EINVAL,
+            "tcg_form must be KMX_TCG_FORM_STANDARD or KMX_TCG_FORM_ONESYNC");
   KMX_CHECK(params->method != KMX_METHOD_RGD || params->rgd_stepsize > 0.0, KMX_EINVAL, "rgd_stepsize must be > 0");
   KMX_CHECK(params->tile_incidences >= 0, KMX_EINVAL, "tile_incidences must be >= 0 (0: automatic)");
   int ndev = 0;
@@ -4290,6 +3351,7 @@ extern "C" int kmx_pgo_create(const kmx_pgo_params* params, int device, kmx_pgo*
     const int m = std::atoi(v);
     h->rm_forced = m == 0 ? RM_LAUNCH : m == 2 ? RM_CONSUMER : -1;  // 1 and 3 (tickets, half) were removed
   }
+  if (const char* v = std::getenv("KMX_HESS_GATE")) h->hess_gate = std::atoi(v) != 0;
   *out = h;
   return KMX_OK;
   KMX_GUARD_END
@@ -4305,7 +3367,11 @@ extern "C" int kmx_pgo_destroy(kmx_pgo* h) {
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   if (h->hstat) (void)hipHostFree(h->hstat);
-  if (h->h_fail) (void)hipHostFree(h->h_fail);
+  if (h->xstream) {
+    (void)hipStreamDestroy(h->xstream);
+    (void)hipEventDestroy(h->ev_xg);
+    (void)hipEventDestroy(h->ev_xd);
+  }
   delete h;
   return KMX_OK;
 }
@@ -4563,32 +3629,12 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
       }
     }
   };
-  h->res_w = WAVES;
-  h->max_tile_inc = 0;
   {
     const int TP = WAVES * (64 / r);
     int64_t tilecap = std::min<int64_t>(2 * (int64_t)TP * r,
                                         std::max<int64_t>(180, (inc_all + TILES_TARGET - 1) / TILES_TARGET));
-    // the resident round keeps one tile per workgroup for the whole round: full
-    // tiles (two chunks), so the cut needs the fewest resident workgroups
-    if (h->P.tcg_form == KMX_TCG_FORM_RESIDENT) tilecap = 2 * (int64_t)TP * r;
     if (h->P.tile_incidences > 0) tilecap = std::max(16, h->P.tile_incidences);
     cut(TP, tilecap);
-    int cus = 0;
-    KMX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
-    if (h->P.tcg_form == KMX_TCG_FORM_RESIDENT && r == 5 && (int)tr.size() > cus) {
-      // more 48-pose tiles than CUs: 5-wave workgroups of 60 poses, one per
-      // CU, when that cut fits (k_round W = 5)
-      const int TP5 = 5 * (64 / r);
-      const int64_t cap5 = h->P.tile_incidences > 0 ? std::max(16, h->P.tile_incidences) : 2 * (int64_t)TP5 * r;
-      std::vector<int> tr4 = tr, tp04 = tp0, tnp4 = tnp, rt04 = rt0;
-      cut(TP5, cap5);
-      if ((int)tr.size() <= cus) {
-        h->res_w = 5;
-      } else {
-        tr = tr4; tp0 = tp04; tnp = tnp4; rt0 = rt04;
-      }
-    }
   }
   rt0[L] = (int)tr.size();
   h->rt0_h = rt0;
@@ -4608,7 +3654,6 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     td.k0 = inc_ptr[tp0[t]];
     const int ninc = inc_ptr[tp0[t] + tnp[t]] - td.k0;
     KMX_CHECK(tnp[t] < 256 && ninc < (1 << 23), KMX_EINVAL, "tile too large");
-    h->max_tile_inc = std::max(h->max_tile_inc, ninc);
     td.np_n = tnp[t] | (ninc << 8);
     td.rt0 = rt0[tr[t]];
     td.rt1 = rt0[tr[t] + 1];
@@ -4724,33 +3769,11 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
     d.hz = h->d_vec + v0 * vec; d.w0 = h->d_vec + (v0 + 1) * vec; d.w1 = h->d_vec + (v0 + 2) * vec;
     d.part_f = h->d_part_f;
   }
-  // fused reducers (RM_LAUNCH tCG launches; every robot's tiles within one
-  // RobotSum pass). Opt-in, KMX_FUSE_RED=1 (A/B switch)
-  h->fuse_red = false;
-  if (h->rm == RM_LAUNCH && !h->fuse_forced_off) {
-    bool fits = true;
-    for (size_t l = 0; l + 1 < h->rt0_h.size(); ++l) fits = fits && h->rt0_h[l + 1] - h->rt0_h[l] <= 2 * RBLOCK;
-    if (fits) {
-      if (!h->d_red_cnt)
-        if (int rc = dalloc(&h->d_red_cnt, (size_t)1024 * RC_STRIDE)) return rc;
-      KMX_HIP(hipMemsetAsync(h->d_red_cnt, 0, sizeof(unsigned) * 1024 * RC_STRIDE, h->stream));
-      if (!h->h_fail) {
-        KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_fail), sizeof(unsigned),
-                              hipHostMallocMapped | hipHostMallocCoherent));
-        *h->h_fail = 0;
-      }
-      h->fuse_red = true;
-    }
-  }
-  d.fuse_red = h->fuse_red ? 1 : 0;
-  d.red_cnt = h->d_red_cnt;
-  d.fail = h->h_fail;
   h->n_ext = 0;
   sync_params(h);
   enqueue_precond(h, 0);
   KMX_HIP(hipGetLastError());
   KMX_HIP(hipStreamSynchronize(h->stream));
-  if (int rc2 = resident_setup(h)) return rc2;
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -4894,8 +3917,10 @@ int nccl_settle(kmx_pgo* h, ncclResult_t r, const char* what) {
 // one group on the handle's stream, then the received rows land in the public
 // table and the peers' status words in ext. Segment layout as
 // kmx_pgo_exchange_pack / _unpack.
+int enqueue_exchange_lag(kmx_pgo* h);
 int enqueue_exchange(kmx_pgo* h) {
   if (!h->xchg) return KMX_OK;
+  if (h->xchg_lag) return enqueue_exchange_lag(h);
   const int ps = 4 * h->P.r, W = h->world;
   const long long ts = h->xn_send * ps + W, tr = h->xn_recv * ps + W;
   hipLaunchKernelGGL(k_xgather, dim3((unsigned)((ts + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
@@ -4915,6 +3940,59 @@ int enqueue_exchange(kmx_pgo* h) {
                            sizeof(double) * h->xs_cnt[h->rank], hipMemcpyDeviceToDevice, h->stream));
   hipLaunchKernelGGL(k_xscatter, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, h->stream, h->d_pub,
                      h->d_xr_slots, h->d_xr_rseg, h->xn_recv, (const double*)h->d_xrbuf, ps, h->d_xr_seg, W, h->d_ext);
+  if (h->n_ext != W) {
+    h->n_ext = W;
+    sync_params(h);
+  }
+  KMX_HIP(hipGetLastError());
+  return KMX_OK;
+}
+
+// KMX_XCHG_LAG: the previous round's exchange (done on xstream while that
+// round computed) is installed, then this round's rows are gathered and sent
+// on xstream behind an event, and the round runs without waiting for them.
+// The first round of a sequence waits (round 1 reads X^0 as in the in-round
+// form). The send / receive buffers need no second copy: the scatter of
+// exchange i-1 and the gather of exchange i both wait for exchange i-1 to
+// finish, and exchange i starts after both.
+int enqueue_exchange_lag(kmx_pgo* h) {
+  const int ps = 4 * h->P.r, W = h->world;
+  const long long ts = h->xn_send * ps + W, tr = h->xn_recv * ps + W;
+  if (!h->xstream) {
+    KMX_HIP(hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
+    KMX_HIP(hipEventCreateWithFlags(&h->ev_xg, hipEventDisableTiming));
+    KMX_HIP(hipEventCreateWithFlags(&h->ev_xd, hipEventDisableTiming));
+  }
+  auto scatter = [&]() {
+    hipLaunchKernelGGL(k_xscatter, dim3((unsigned)((tr + 255) / 256)), dim3(256), 0, h->stream, h->d_pub,
+                       h->d_xr_slots, h->d_xr_rseg, h->xn_recv, (const double*)h->d_xrbuf, ps, h->d_xr_seg, W,
+                       h->d_ext);
+  };
+  if (h->x_inflight) {
+    KMX_HIP(hipStreamWaitEvent(h->stream, h->ev_xd, 0));
+    scatter();
+  }
+  hipLaunchKernelGGL(k_xgather, dim3((unsigned)((ts + 255) / 256)), dim3(256), 0, h->stream, h->d_vec,
+                     h->d_pub_src, h->d_xs_slots, h->d_xs_rseg, h->xn_send, h->d_xsbuf, ps, h->d_xs_seg, W,
+                     (const double*)h->d_relc, h->dv.L);
+  KMX_HIP(hipEventRecord(h->ev_xg, h->stream));
+  KMX_HIP(hipStreamWaitEvent(h->xstream, h->ev_xg, 0));
+  KMX_NCCL(ncclGroupStart());
+  for (int q = 0; q < W; ++q) {
+    if (q == h->rank && !h->xchg_self_p2p) continue;
+    KMX_NCCL(ncclSend(h->d_xsbuf + h->xs_off[q], (size_t)h->xs_cnt[q], ncclDouble, q, h->comm, h->xstream));
+    KMX_NCCL(ncclRecv(h->d_xrbuf + h->xr_off[q], (size_t)h->xr_cnt[q], ncclDouble, q, h->comm, h->xstream));
+  }
+  if (int rc = nccl_settle(h, ncclGroupEnd(), "ncclGroupEnd")) return rc;
+  if (!h->xchg_self_p2p)
+    KMX_HIP(hipMemcpyAsync(h->d_xrbuf + h->xr_off[h->rank], h->d_xsbuf + h->xs_off[h->rank],
+                           sizeof(double) * h->xs_cnt[h->rank], hipMemcpyDeviceToDevice, h->xstream));
+  KMX_HIP(hipEventRecord(h->ev_xd, h->xstream));
+  if (!h->x_inflight) {  // the first round: its own exchange's rows
+    KMX_HIP(hipStreamWaitEvent(h->stream, h->ev_xd, 0));
+    scatter();
+  }
+  h->x_inflight = true;
   if (h->n_ext != W) {
     h->n_ext = W;
     sync_params(h);
@@ -4989,7 +4067,7 @@ extern "C" int kmx_pgo_comm_init(kmx_pgo* h, const void* unique_id, int world, i
   h->world = world;
   h->rank = rank;
   if (const char* v = std::getenv("KMX_XCHG_SELF_P2P")) h->xchg_self_p2p = std::atoi(v) != 0;
-  if (const char* v = std::getenv("KMX_FUSE_RED")) h->fuse_forced_off = std::atoi(v) == 0;
+  if (const char* v = std::getenv("KMX_XCHG_LAG")) h->xchg_lag = std::atoi(v) != 0;
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -5017,15 +4095,15 @@ extern "C" int kmx_pgo_comm_destroy(kmx_pgo* h) {
 
 // The handle's stream drained within timeout_s (polled), or KMX_ETIMEOUT: a
 // bounded wait for a round whose exchange depends on peers.
-static int check_resident_fail(kmx_pgo* h);
 extern "C" int kmx_pgo_sync_timeout(kmx_pgo* h, double timeout_s) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_CHECK(timeout_s > 0.0, KMX_EINVAL, "timeout_s must be > 0");
   KMX_HIP(hipSetDevice(h->device));
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
-    const hipError_t e = hipStreamQuery(h->stream);
-    if (e == hipSuccess) return check_resident_fail(h);
+    hipError_t e = hipStreamQuery(h->stream);
+    if (e == hipSuccess && h->xstream) e = hipStreamQuery(h->xstream);  // a lagged exchange in flight
+    if (e == hipSuccess) return KMX_OK;
     if (e != hipErrorNotReady) return kmx::fail(KMX_EHIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
     if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
       return kmx::fail(KMX_ETIMEOUT, "the stream did not drain within the timeout (an exchange peer is missing?)");
@@ -5177,7 +4255,6 @@ extern "C" int kmx_pgo_iterate(kmx_pgo* h, const uint8_t* active, kmx_iter_stats
   std::vector<unsigned char> ones(L, 1);
   KMX_HIP(hipMemcpyAsync(h->d_active, ones.data(), L, hipMemcpyHostToDevice, h->stream));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  if (int rc = check_resident_fail(h)) return rc;
   if (stats) {
     for (int a = 0; a < h->n_robots; ++a) std::memset(&stats[a], 0, sizeof(kmx_iter_stats));
     for (int l = 0; l < L; ++l) {
@@ -5218,36 +4295,11 @@ extern "C" int kmx_pgo_iterate_async(kmx_pgo* h, int rounds, int refresh_local) 
   return KMX_OK;
 }
 
-// After a synchronisation: a resident round whose grid barrier gave up (a
-// workgroup not resident, or a fault that stopped a workgroup) left the round
-// incomplete; report it once.
-static int check_resident_fail(kmx_pgo* h) {
-  if (!h->h_fail) return KMX_OK;
-  const unsigned f = __atomic_load_n(h->h_fail, __ATOMIC_ACQUIRE);
-  if (f == 0) return KMX_OK;
-  *h->h_fail = 0;
-  return kmx::fail(KMX_EHIP, "resident round: grid barrier " + std::to_string(f - 1) +
-                                 " gave up waiting (the round is incomplete)");
-}
-
 extern "C" int kmx_pgo_sync(kmx_pgo* h) {
   KMX_CHECK(h, KMX_EINVAL, "null handle");
   KMX_HIP(hipSetDevice(h->device));
   KMX_HIP(hipStreamSynchronize(h->stream));
-  return check_resident_fail(h);
-}
-
-extern "C" int kmx_pgo_resident_info(kmx_pgo* h, int* resident, int* ntiles, int* capacity, char* reason,
-                                     int64_t nbytes) {
-  KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
-  if (resident) *resident = h->res_on ? 1 : 0;
-  if (ntiles) *ntiles = h->ntiles;
-  if (capacity) *capacity = h->res_cap;
-  if (reason && nbytes > 0) {
-    const size_t n = std::min<size_t>((size_t)nbytes - 1, h->res_reason.size());
-    std::memcpy(reason, h->res_reason.data(), n);
-    reason[n] = 0;
-  }
+  if (h->xstream) KMX_HIP(hipStreamSynchronize(h->xstream));
   return KMX_OK;
 }
 
@@ -5536,12 +4588,6 @@ extern "C" int kmx_pgo_read_counters(kmx_pgo* h, kmx_pgo_counters* out) {
 // KMX_EUNSUP in the product build.
 extern "C" int kmx_pgo_debug_step_stamps(uint64_t* out, int64_t n) {
   KMX_GUARD_BEGIN
-#ifdef KMX_RES_STAMPS
-  KMX_CHECK(out && n >= 0, KMX_EINVAL, "null buffer");
-  const int64_t m = std::min<int64_t>(n, RES_STAMPS * (int64_t)RES_STAMP_TILES);
-  KMX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_stamp), sizeof(uint64_t) * m, 0, hipMemcpyDeviceToHost));
-  return KMX_OK;
-#endif
 #ifdef KMX_STEP_STAMPS
   KMX_CHECK(out && n >= 0, KMX_EINVAL, "null buffer");
   const int64_t m = std::min<int64_t>(n, 16 * (int64_t)STEP_STAMP_TILES);

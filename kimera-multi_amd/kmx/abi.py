@@ -18,7 +18,7 @@ _LIB_PATH = Path(__file__).resolve().parent / "libkmx.so"
 
 KMX_OK = 0
 KMX_ETIMEOUT = -6
-ABI_VERSION = 7  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
+ABI_VERSION = 8  # include/kmx_abi.h KMX_ABI_VERSION this binding is written for
 KMX_COST_L2 = 0
 KMX_COMM_ID_BYTES = 128  # include/kmx_abi.h (ncclUniqueId)
 KMX_COST_GNC_TLS = 1
@@ -164,8 +164,6 @@ def lib() -> C.CDLL:
         "kmx_pgo_sync": ([P], C.c_int),
         "kmx_pgo_sync_timeout": ([P, f64], C.c_int),
         "kmx_pgo_debug_step_stamps": ([P, i64], C.c_int),
-        "kmx_pgo_resident_info": ([P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, i64],
-                                  C.c_int),
         "kmx_pgo_update_weights": ([P, pf64], C.c_int),
         "kmx_pgo_get_mu": ([P, pf64], C.c_int),
         "kmx_pgo_set_mu": ([P, f64], C.c_int),

@@ -92,18 +92,12 @@ def exchange_plan(graph, world: int, rank: int):
 TILES_TARGET = 736  # csrc/pgo.hip: the tile count the cut of small problems aims at
 
 
-def team_tile_incidences(graph, world: int, r: int, form: str = "standard") -> int:
+def team_tile_incidences(graph, world: int, r: int) -> int:
     """The tile cut (incidences per workgroup tile) kmx_pgo_set_graph picks
     automatically for a handle holding 1/world of the team's incidences; the
     multi-rank driver passes it to every rank, so all ranks cut their robots
-    alike whatever their share (csrc/pgo.hip set_graph). The resident round
-    (tCG_form "resident") cuts each rank's shard itself (0: automatic): full
-    tiles of two gather chunks, 4- or 5-wave workgroups by what the shard
-    needs to keep one tile per CU, so its summation order (the last bits, not
-    the parity bar) depends on the poses per GPU."""
+    alike whatever their share (csrc/pgo.hip set_graph)."""
     tp = 4 * (64 // r)
-    if form == "resident":
-        return 0
     inc = 2 * int(graph.m) // max(world, 1)
     return min(2 * tp * r, max(180, -(-inc // TILES_TARGET)))
 
@@ -133,7 +127,7 @@ class RBCDDriver:
         if solver is None and world > 1 and params.tileIncidences == 0:
             import dataclasses
             params = dataclasses.replace(params, tileIncidences=team_tile_incidences(
-                graph, world, params.r, params.localOptimizationParams.tCG_form))
+                graph, world, params.r))
             self.params = params
         self.solver = solver if solver is not None else BlockSolver(params, device)
         self.executing = ExecutingRobot(params.updateRule, params.randomSeed)

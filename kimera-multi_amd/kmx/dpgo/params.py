@@ -55,10 +55,8 @@ class ROptParameters:
     gradnorm_tol: float = 1e-2
     use_preconditioner: bool = True
     precond_shift: float = 1e-1
-    # kmx opt-in: "standard" (ROPTLIB's tCG), "onesync" (one reduction and one
-    # kernel per tCG step, KMX_TCG_FORM_ONESYNC; parity at convergence only) or
-    # "resident" (the one-sync arithmetic, the whole block update in one
-    # persistent launch per round for small shards, KMX_TCG_FORM_RESIDENT)
+    # kmx opt-in: "standard" (ROPTLIB's tCG) or "onesync" (one reduction and
+    # one kernel per tCG step, KMX_TCG_FORM_ONESYNC; parity at convergence only)
     tCG_form: str = "standard"
 
 
@@ -106,7 +104,7 @@ class PGOAgentParameters:
         p.acceleration = 1 if self.acceleration else 0
         p.restart_interval = int(self.restartInterval)
         p.tile_incidences = int(self.tileIncidences)
-        forms = {"standard": 0, "onesync": 1, "resident": 2}
+        forms = {"standard": 0, "onesync": 1}
         if lo.tCG_form not in forms:
             raise ValueError(f"tCG_form must be one of {sorted(forms)}, got {lo.tCG_form!r}")
         p.tcg_form = forms[lo.tCG_form]

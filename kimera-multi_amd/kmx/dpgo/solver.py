@@ -236,16 +236,6 @@ class BlockSolver:
         v = np.ascontiguousarray(v, dtype=np.float64)
         check(self.L.kmx_pgo_set_status(self.h, fptr(v)), "kmx_pgo_set_status")
 
-    def resident_info(self) -> dict:
-        """KMX_TCG_FORM_RESIDENT: whether rounds run as one persistent launch,
-        the tile cut against the device's resident workgroups, and why not."""
-        res, nt, cap = C.c_int(), C.c_int(), C.c_int()
-        buf = C.create_string_buffer(256)
-        check(self.L.kmx_pgo_resident_info(self.h, C.byref(res), C.byref(nt), C.byref(cap), buf, 256),
-              "kmx_pgo_resident_info")
-        return {"resident": bool(res.value), "ntiles": nt.value, "capacity": cap.value,
-                "reason": buf.value.decode()}
-
     def memory(self) -> tuple[int, int]:
         """(resident device bytes, bytes per incidence record)."""
         b, rb = C.c_int64(), C.c_int()

@@ -348,11 +348,50 @@ class LoopClosureDetector:
         return int(vertex)
 
     # ------------------------------------------- reference-shaped single calls --
+    def _one(self):
+        """Buffers and ctypes pointers of the one-candidate calls, made once per
+        pool stride: the reference's verification thread makes three calls per
+        candidate (verifyLoopSpin, drawio:2638-2657), so their host side is kept
+        to filling two ids and one count."""
+        N = max(self.max_feats, 1)
+        o = getattr(self, "_one_bufs", None)
+        if o is None or o["N"] != N:
+            o = {"N": N, "cq": np.zeros(1, np.int32), "cm": np.zeros(1, np.int32),
+                 "mptr": np.zeros(2, np.int64), "pairs": np.zeros((1, N, 2), np.int32), "k": np.zeros(1, np.int32),
+                 "masks": np.zeros((1, N), np.uint8), "res": (abi.LcdResult * 1)(), "zero": np.zeros(1, np.int32),
+                 "prior": np.zeros(12, np.float64)}
+            for key in ("cq", "cm", "pairs", "k", "zero"):
+                o[key + "_p"] = abi.iptr(o[key])
+            o["mptr_p"], o["masks_p"], o["prior_p"] = abi.i64ptr(o["mptr"]), abi.u8ptr(o["masks"]), abi.fptr(o["prior"])
+            self._one_bufs = o
+        return o
+
+    def _verify_one(self, vertex_query, vertex_match, iq, im, stages, prior=None):
+        """kmx_lcd_verify_matches for one candidate through the _one buffers:
+        (result record, inlier-mask row over the given pairs)."""
+        o = self._one()
+        o["cq"][0], o["cm"][0] = self.frame_id(vertex_query), self.frame_id(vertex_match)
+        n = iq.shape[0]
+        if im.shape[0] != n:
+            raise ValueError("i_query and i_match differ in length")
+        o["mptr"][1] = n
+        pp = None
+        if prior is not None:
+            o["prior"][:] = prior
+            pp = o["prior_p"]
+        check(self.L.kmx_lcd_verify_matches(self.h, 1, o["cq_p"], o["cm_p"], o["mptr_p"],
+                                            abi.iptr(iq) if n else o["zero_p"], abi.iptr(im) if n else o["zero_p"],
+                                            int(stages), pp, o["res"], o["masks_p"]), "kmx_lcd_verify_matches")
+        return o["res"][0], o["masks"][0, :n]
+
     def computeMatchedIndices(self, vertex_query, vertex_match):
         """LoopClosureDetector::computeMatchedIndices (drawio:2583-2586) on two
         resident frames: (i_query, i_match) int32 arrays in query order."""
-        pairs, k = self.match([self.frame_id(vertex_query)], [self.frame_id(vertex_match)])
-        return pairs[0, : k[0], 0].copy(), pairs[0, : k[0], 1].copy()
+        o = self._one()
+        o["cq"][0], o["cm"][0] = self.frame_id(vertex_query), self.frame_id(vertex_match)
+        check(self.L.kmx_lcd_match(self.h, 1, o["cq_p"], o["cm_p"], o["pairs_p"], o["k_p"]), "kmx_lcd_match")
+        k = int(o["k"][0])
+        return o["pairs"][0, :k, 0].copy(), o["pairs"][0, :k, 1].copy()
 
     def geometricVerificationNister(self, vertex_query, vertex_match, i_query, i_match):
         """geometricVerificationNister (drawio:2589-2592): the 2D-2D RANSAC on
@@ -362,10 +401,9 @@ class LoopClosureDetector:
         writes back into i_query / i_match."""
         iq = np.ascontiguousarray(i_query, np.int32)
         im = np.ascontiguousarray(i_match, np.int32)
-        out, masks = self.verify_matches([self.frame_id(vertex_query)], [self.frame_id(vertex_match)], [(iq, im)],
-                                         stages=abi.KMX_LCD_STAGE_2D2D, with_masks=True)
-        keep = (masks[0, : iq.shape[0]] & 1).astype(bool)
-        return out[0]["accepted"], iq[keep], im[keep], _T4(out[0]["T_query_match"])
+        r, mask = self._verify_one(vertex_query, vertex_match, iq, im, abi.KMX_LCD_STAGE_2D2D)
+        keep = (mask & 1).astype(bool)
+        return bool(r.accepted), iq[keep], im[keep], _T4(r.T_query_match)
 
     def recoverPose(self, vertex_query, vertex_match, i_query, i_match, T_query_match_mono=None):
         """recoverPose (drawio:2595-2598) on geometricVerificationNister's
@@ -377,10 +415,9 @@ class LoopClosureDetector:
         prior = None
         if T_query_match_mono is not None:
             T = np.asarray(T_query_match_mono, np.float64)
-            prior = np.concatenate([T[:3, :3].reshape(9), T[:3, 3]])[None]
-        out, masks = self.verify_matches([self.frame_id(vertex_query)], [self.frame_id(vertex_match)], [(iq, im)],
-                                         stages=abi.KMX_LCD_STAGE_RECOVER, T_prior=prior, with_masks=True)
-        return out[0]["accepted"], _T4(out[0]["T_query_match"]), (masks[0, : iq.shape[0]] & 2).astype(bool)
+            prior = np.concatenate([T[:3, :3].reshape(9), T[:3, 3]])
+        r, mask = self._verify_one(vertex_query, vertex_match, iq, im, abi.KMX_LCD_STAGE_RECOVER, prior)
+        return bool(r.accepted), _T4(r.T_query_match), (mask & 2).astype(bool)
 
     # --------------------------------------------------------------- batched --
     def match(self, cand_query, cand_match):
@@ -514,6 +551,5 @@ def _results(res, n: int, refines: bool = False) -> list:
 
 def _T4(t12) -> np.ndarray:
     T = np.eye(4)
-    T[:3, :3] = np.asarray(t12[:9]).reshape(3, 3)
-    T[:3, 3] = t12[9:12]
+    T[:3, :4] = np.ctypeslib.as_array(t12, (12,))[[0, 1, 2, 9, 3, 4, 5, 10, 6, 7, 8, 11]].reshape(3, 4)
     return T

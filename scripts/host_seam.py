@@ -16,7 +16,7 @@ table (rows gathered once) and times rounds under:
          peers' — timing only), all rounds from one iterate_async call
 The handle's tCG enqueueing is the default adaptive mode
 (kmx_pgo_set_tcg_poll(-1)); KMX_SEAM_POLL=0 / 1 sets blind / polled.
-usage: python scripts/host_seam.py N [rounds] [standard|onesync|resident]  (the tCG form)
+usage: python scripts/host_seam.py N [rounds] [standard|onesync]  (the tCG form)
 """
 import os
 import sys
@@ -46,7 +46,7 @@ dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cu
 g = config("synth100k", seed=0)
 P = bench.params()
 P.localOptimizationParams.tCG_form = sys.argv[3] if len(sys.argv) > 3 else "standard"
-P = dataclasses.replace(P, tileIncidences=team_tile_incidences(g, N, P.r, P.localOptimizationParams.tCG_form))
+P = dataclasses.replace(P, tileIncidences=team_tile_incidences(g, N, P.r))
 Y = lifting_matrix(5, seed=1)
 lo, hi = robot_ranges(g.n_robots, N)[0]
 local = np.zeros(g.n_robots, np.uint8)
@@ -80,18 +80,17 @@ sbuf = torch.zeros(n_send * ps + N, dtype=torch.float64, device=dev)
 rbuf = torch.zeros(n_recv * ps + N, dtype=torch.float64, device=dev)
 wire_in = torch.zeros(n_recv * ps + N, dtype=torch.float64, device=dev)
 wire_out = torch.zeros_like(wire_in)
-if P.localOptimizationParams.tCG_form == "resident":
-    _s = make()
-    print("resident:", _s.resident_info(), flush=True)
-    _s.close()
 print(f"N={N}: rank 0 holds robots {lo}..{hi - 1}, {int(g.n_poses[lo:hi].sum())} poses; "
       f"sends {n_send} rows, receives {n_recv} rows ({n_recv * ps * 8 / 1e6:.2f} MB) per round; "
       f"adaptive tCG enqueueing, {P.localOptimizationParams.tCG_form} tCG", flush=True)
 
-for mode in ("batch", "seam", "native"):
+modes = ("batch", "seam", "native", "lagged") if os.environ.get("KMX_SEAM_LAG") else ("batch", "seam", "native")
+for mode in modes:
     s = make()
-    if mode == "native":
+    if mode in ("native", "lagged"):
         os.environ["KMX_XCHG_SELF_P2P"] = "1"
+        # lagged: the one-round-stale exchange (KMX_XCHG_LAG, pgo.hip enqueue_exchange_lag) on its own stream
+        os.environ["KMX_XCHG_LAG"] = "1" if mode == "lagged" else "0"
         k = min(n_send, n_recv)
         s.comm_init(s.comm_unique_id(), 1, 0)
         s.set_exchange(ss[:k], [k], rs[:k], [k])
@@ -109,7 +108,7 @@ for mode in ("batch", "seam", "native"):
     s.read_counters()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if mode in ("batch", "native"):
+    if mode in ("batch", "native", "lagged"):
         s.iterate_async(n_rounds, refresh_local=False)
     else:
         for _ in range(n_rounds):

@@ -183,4 +183,3 @@ def test_team_tile_incidences_rule():
     assert team_tile_incidences(g, 4, 5) == 340       # ceil(250000 / 736)
     assert team_tile_incidences(g, 8, 5) == 180       # not below 180
     assert team_tile_incidences(g, 1, 3) == 2 * 4 * 21 * 3  # r = 3: tiles of 84 poses
-    assert team_tile_incidences(g, 8, 5, "resident") == 0  # the resident round: each rank's own automatic cut

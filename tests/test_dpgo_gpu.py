@@ -449,15 +449,15 @@ def test_reduction_forms_agree_bitwise(gpu, monkeypatch):
     """The consumer kernels reduce every robot's partials in k_reduce's order and
     take the same decisions, so both forms give the same iterates bit for bit
     (what keeps a team's result independent of how its ranks' sizes fall on
-    either side of the form's size threshold). So does the launched form with
-    fused reducers (KMX_FUSE_RED=1: the tCG launches' extra per-robot
-    workgroups wait for the robot's tiles and sum their write-through partials
-    in k_reduce's order)."""
+    either side of the form's size threshold). Gated k_hess launches
+    (KMX_HESS_GATE: the phase test before the first records are fetched in
+    every launch after a tCG's first; 0 turns it off) only reorder loads, so
+    both give the same bits in both forms."""
     g, P, X0 = _setup(robust=True, seed=4)
     out = []
-    for red, fuse in (("0", "0"), ("2", "0"), ("0", "1")):
+    for red, gate in (("0", "1"), ("2", "1"), ("0", "0"), ("2", "0")):
         monkeypatch.setenv("KMX_RED", red)
-        monkeypatch.setenv("KMX_FUSE_RED", fuse)
+        monkeypatch.setenv("KMX_HESS_GATE", gate)
         s = BlockSolver(P, 0)
         s.set_graph_data(g)
         s.set_gnc_schedule(True, 3, 50, P.relChangeTol)
@@ -472,16 +472,17 @@ def test_reduction_forms_agree_bitwise(gpu, monkeypatch):
             assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("red", ["0", "2", "fused"])
+@pytest.mark.parametrize("red", ["0", "2", "ungated"])
 def test_tcg_poll_modes_agree_bitwise(gpu, monkeypatch, red):
     """Polled, blind and adaptive tCG enqueueing (kmx_pgo_set_tcg_poll 1 / 0 /
     -1) launch the same work that matters: a blind step of a robot that already
     left tCG exits at once. Iterates, GNC weights and work counters agree bit
     for bit over rounds that cross GNC updates, in both reduction forms, and
-    the team status a multi-rank exchange carries is the same (with fused
-    reducers the polled status comes from the k_update launch's reducers)."""
-    monkeypatch.setenv("KMX_RED", "0" if red == "fused" else red)
-    monkeypatch.setenv("KMX_FUSE_RED", "1" if red == "fused" else "0")
+    the team status a multi-rank exchange carries is the same ("ungated":
+    KMX_HESS_GATE=0, every k_hess launch fetches its first records before the
+    phase test)."""
+    monkeypatch.setenv("KMX_RED", "0" if red == "ungated" else red)
+    monkeypatch.setenv("KMX_HESS_GATE", "0" if red == "ungated" else "1")
     g, P, X0 = _setup(robust=True, seed=6)
     out = []
     for mode in (1, 0, -1):

@@ -200,3 +200,55 @@ def test_concurrent_slots_mixed_sizes(gpu, monkeypatch, env):
     assert np.array_equal(gm, wm)
     for g, w in zip(got, want):
         assert all(np.array_equal(g[k], w[k]) for k in g)
+
+
+@pytest.mark.parametrize("norm", ["l1", "hamming"])
+def test_split_knn2_matches_oracle(gpu, monkeypatch, norm):
+    """kmx_lcd_match on resident frames: the small-call kNN2 (k_knn2s, a
+    candidate's queries over ceil(N / 64) workgroups, each query's match set
+    over 4 waves, merged as ordered keys; KMX_LCD_KSPLIT) gives k_knn2's rows
+    and counts bit for bit, and both give the restatement's, across feature
+    counts that end a 64-query block or a match quarter part way, frames with
+    0 / 1 features, planted near-duplicates and exact ties, at N = 1024 (16
+    blocks) — and a call of 65 candidates takes k_knn2."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(11)
+    N = 1024
+    counts = [0, 1, 2, 3, 63, 64, 65, 127, 300, 500, 1023, 1024]
+    F = len(counts)
+    desc = rng.integers(0, 256, (F, N, 32), dtype=np.uint8)
+    for f in range(1, F):  # near-duplicates of frame f - 1 and an exact tie
+        k = min(counts[f], counts[f - 1]) // 2
+        desc[f, :k] = desc[f - 1, :k] ^ (rng.random((k, 32)) < 0.02).astype(np.uint8)
+        if counts[f] > 3:
+            desc[f, counts[f] - 1] = desc[f, 0]
+    bear = np.zeros((F, N, 3))
+    bear[..., 2] = 1.0
+    pts = np.ones((F, N, 3))
+    p = LcdParams(norm=norm)
+    cand = [(a, b) for a in range(F) for b in range(F) if a != b]
+    res = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("KMX_LCD_KSPLIT", split)
+        d = LoopClosureDetector(p)
+        d.add_frames(np.array(counts, np.int32), desc, bear, pts)
+        out = []
+        for i in range(0, len(cand), 40):  # calls of 40 candidates (split), then one of 65 (k_knn2)
+            cq = np.array([c[0] for c in cand[i:i + 40]], np.int32)
+            cm = np.array([c[1] for c in cand[i:i + 40]], np.int32)
+            out.append(d.match(cq, cm))
+        cq = np.array([c[0] for c in cand[:65]], np.int32)
+        cm = np.array([c[1] for c in cand[:65]], np.int32)
+        out.append(d.match(cq, cm))
+        d.close()
+        res[split] = out
+    for (pa, ka), (pb, kb) in zip(res["1"], res["0"]):
+        assert np.array_equal(ka, kb)
+        for i in range(len(ka)):
+            assert np.array_equal(pa[i, :ka[i]], pb[i, :kb[i]]), i
+    nrm = 1 if norm == "hamming" else 0
+    for i, (a, b) in enumerate(cand):
+        pa, ka = res["1"][i // 40]
+        ref = O.knn2(nrm, 0.7, desc[a, :counts[a]], desc[b, :counts[b]])
+        got = pa[i % 40, :ka[i % 40]]
+        assert np.array_equal(got[:, 0], ref[:, 0]) and np.array_equal(got[:, 1], ref[:, 1]), (a, b)
