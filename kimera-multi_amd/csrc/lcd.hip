@@ -2221,14 +2221,35 @@ __device__ __forceinline__ void ransac_tail(int c, WS& w, double* F1, double* F2
   unsigned char* valid = reinterpret_cast<unsigned char*>(F1) + sizeof(int) * (size_t)N;
   // note: F1's first N ints hold idx; valid bytes follow within F1's 3N doubles
   wsync();
-  for (int k = lane; k < n3; k += RS_BLOCK) {
-    const int j = idx[k];
-    const int2 pr = pl[j];
-    const double* a = points + ((size_t)q * N + pr.x) * 3;
-    const double* b = points + ((size_t)m * N + pr.y) * 3;
-    const bool v = !(isnan(a[0]) || isnan(a[1]) || isnan(a[2]) || isnan(b[0]) || isnan(b[1]) || isnan(b[2]));
-    valid[k] = v ? 1 : 0;
-    for (int i = 0; i < 3; ++i) T[3 * k + i] = a[i] - (Rb[i * 3 + 0] * b[0] + Rb[i * 3 + 1] * b[1] + Rb[i * 3 + 2] * b[2]);
+  // (WAVE: four inliers per lane per pass, the idx -> pair -> point loads of
+  // the pass issued before their uses: three dependent round trips per pass
+  // instead of per inlier)
+  constexpr int TU = WAVE ? 4 : 1;
+  for (int k0 = lane; k0 < n3; k0 += TU * RS_BLOCK) {
+    int jj[TU];
+#pragma unroll
+    for (int u = 0; u < TU; ++u) jj[u] = idx[min(k0 + u * RS_BLOCK, n3 - 1)];
+    int2 pr[TU];
+#pragma unroll
+    for (int u = 0; u < TU; ++u) pr[u] = pl[jj[u]];
+    double a[TU][3], b[TU][3];
+#pragma unroll
+    for (int u = 0; u < TU; ++u)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        a[u][i] = points[((size_t)q * N + pr[u].x) * 3 + i];
+        b[u][i] = points[((size_t)m * N + pr[u].y) * 3 + i];
+      }
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int k = k0 + u * RS_BLOCK;
+      if (k >= n3) break;
+      const bool v = !(isnan(a[u][0]) || isnan(a[u][1]) || isnan(a[u][2]) || isnan(b[u][0]) || isnan(b[u][1]) ||
+                       isnan(b[u][2]));
+      valid[k] = v ? 1 : 0;
+      for (int i = 0; i < 3; ++i)
+        T[3 * k + i] = a[u][i] - (Rb[i * 3 + 0] * b[u][0] + Rb[i * 3 + 1] * b[u][1] + Rb[i * 3 + 2] * b[u][2]);
+    }
   }
   __threadfence_block();
   wsync();
@@ -2329,33 +2350,55 @@ __device__ __forceinline__ void ransac_tail(int c, WS& w, double* F1, double* F2
     const double tb[3] = {Tl[3 * best], Tl[3 * best + 1], Tl[3 * best + 2]};
     const bool refine = P.refine != 0;
     int cc = 0;
-    for (int j0 = 0; j0 < n3; j0 += RS_BLOCK) {
-      const int j = j0 + lane;
-      bool in = false;
-      double tj[3] = {0.0, 0.0, 0.0};
-      if (j < n3 && vl[j]) {
-        for (int k = 0; k < 3; ++k) tj[k] = Tl[3 * j + k];
-        const double dx = tj[0] - tb[0], dy = tj[1] - tb[1], dz = tj[2] - tb[2];
-        in = dx * dx + dy * dy + dz * dz < thr2;
-      }
-      if (j < n3 && mask) mask[idx[j]] = in ? 3 : 1;  // idx lists 2D-2D inliers (mask 1): | 2
-      const unsigned long long im = __ballot(in);
-      if (in) {
-        const int pos = cc + __popcll(im & ((1ull << lane) - 1ull));
-        double* o = Pc + 6 * (size_t)pos;
-        if (refine) {
-          const int2 pr = pl[idx[j]];
-          const double* a = points + ((size_t)q * N + pr.x) * 3;
-          const double* b = points + ((size_t)m * N + pr.y) * 3;
+    // four passes of the wave at a time, their idx -> pair -> point loads
+    // issued before the passes' ballots (three dependent round trips per four
+    // passes instead of per pass)
+    constexpr int FU = 4;
+    for (int j00 = 0; j00 < n3; j00 += FU * RS_BLOCK) {
+      int jx[FU];
+      int2 pr[FU];
+      double pa[FU][3], pb[FU][3];
+#pragma unroll
+      for (int u = 0; u < FU; ++u) jx[u] = idx[min(j00 + u * RS_BLOCK + lane, n3 - 1)];
+      if (refine) {
+#pragma unroll
+        for (int u = 0; u < FU; ++u) pr[u] = pl[jx[u]];
+#pragma unroll
+        for (int u = 0; u < FU; ++u)
+#pragma unroll
           for (int k = 0; k < 3; ++k) {
-            o[k] = a[k];
-            o[3 + k] = b[k];
+            pa[u][k] = points[((size_t)q * N + pr[u].x) * 3 + k];
+            pb[u][k] = points[((size_t)m * N + pr[u].y) * 3 + k];
           }
-        } else {
-          for (int k = 0; k < 3; ++k) o[k] = tj[k];
-        }
       }
-      cc += __popcll(im);
+#pragma unroll
+      for (int u = 0; u < FU; ++u) {
+        const int j0 = j00 + u * RS_BLOCK;
+        if (j0 >= n3) break;
+        const int j = j0 + lane;
+        bool in = false;
+        double tj[3] = {0.0, 0.0, 0.0};
+        if (j < n3 && vl[j]) {
+          for (int k = 0; k < 3; ++k) tj[k] = Tl[3 * j + k];
+          const double dx = tj[0] - tb[0], dy = tj[1] - tb[1], dz = tj[2] - tb[2];
+          in = dx * dx + dy * dy + dz * dz < thr2;
+        }
+        if (j < n3 && mask) mask[jx[u]] = in ? 3 : 1;  // idx lists 2D-2D inliers (mask 1): | 2
+        const unsigned long long im = __ballot(in);
+        if (in) {
+          const int pos = cc + __popcll(im & ((1ull << lane) - 1ull));
+          double* o = Pc + 6 * (size_t)pos;
+          if (refine) {
+            for (int k = 0; k < 3; ++k) {
+              o[k] = pa[u][k];
+              o[3 + k] = pb[u][k];
+            }
+          } else {
+            for (int k = 0; k < 3; ++k) o[k] = tj[k];
+          }
+        }
+        cc += __popcll(im);
+      }
     }
     wsync();
     // Each ordered sum below is one lane's serial chain (the serial loop's
@@ -2657,10 +2700,9 @@ struct RsState {  // the serial loop's control between passes
 };
 constexpr int SPREAD_PER_NISTER = 2;  // Nister hypotheses per wave (one at a time)
 
-__global__ void k_rs_init(RsState* st, int n, int stages, unsigned* more, int nmore) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < nmore) more[c] = 0u;  // the ranges' flags (k_rs_replay)
-  if (c >= n) return;
+// Candidate c's serial-loop state before its first range, and its wave
+// arrival counter (k_rs_hyps: the last wave of a range replays it).
+__device__ __forceinline__ void rs_init_c(RsState* st, unsigned* hcnt, int c, int stages) {
   RsState s;
   s.kk = 1.0;
   for (int i = 0; i < 12; ++i) s.best[i] = 0.0;
@@ -2668,6 +2710,12 @@ __global__ void k_rs_init(RsState* st, int n, int stages, unsigned* more, int nm
   s.best_cnt = -INT_MAX;
   s.done = (stages & KMX_LCD_STAGE_2D2D) ? 0 : 1;
   st[c] = s;
+  hcnt[c] = 0u;
+}
+__global__ void k_rs_init(RsState* st, unsigned* hcnt, int n, int stages, unsigned* more, int nmore) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < nmore) more[c] = 0u;  // the ranges' flags (the replay)
+  if (c < n) rs_init_c(st, hcnt, c, stages);
 }
 
 // The candidate's compact bearings (ransac_candidate's layout) and the LDS
@@ -2676,11 +2724,32 @@ template <typename WS>
 __device__ __forceinline__ void rs_compact(WS& w, double* F1, const double* bearings, int N, int q, int m,
                                            const int2* pl, int K, int lane) {
   double* F2 = F1 + 3 * N;
-  for (int j = lane; j < K; j += RS_BLOCK) {
-    const int2 pr = pl[j];
-    for (int k = 0; k < 3; ++k) {
-      F1[(size_t)k * N + j] = bearings[((size_t)q * N + pr.x) * 3 + k];
-      F2[(size_t)k * N + j] = bearings[((size_t)m * N + pr.y) * 3 + k];
+  // four pairs per lane per pass, every load of the pass issued before its
+  // stores (the stores may alias the bearings for the compiler, which then
+  // kept one dependent pair -> bearing round trip per pair: ~7 us of a lone
+  // wave's hypothesis at K = 350)
+  constexpr int U = 4;
+  for (int j0 = lane; j0 < K; j0 += U * RS_BLOCK) {
+    int2 pr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) pr[u] = pl[min(j0 + u * RS_BLOCK, K - 1)];
+    double a[U][3], b[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        a[u][k] = bearings[((size_t)q * N + pr[u].x) * 3 + k];
+        b[u][k] = bearings[((size_t)m * N + pr[u].y) * 3 + k];
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * RS_BLOCK;
+      if (j < K)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          F1[(size_t)k * N + j] = a[u][k];
+          F2[(size_t)k * N + j] = b[u][k];
+        }
     }
   }
   for (int t = lane; t < 40; t += RS_BLOCK) (&w.t11[0][0][0])[t] = (&T11[0][0][0])[t];
@@ -2689,17 +2758,23 @@ __device__ __forceinline__ void rs_compact(WS& w, double* F1, const double* bear
   wsync();
 }
 
+__device__ __forceinline__ void rs_replay_c(int c, int lane, const int* Kin, const RsParams& P, RsState* st,
+                                            const HypOut* hout, int pb, unsigned* more);
+// The last of a candidate's G waves to finish (hcnt: an agent-scope arrival
+// counter, every wave's HypOut stores fenced before its arrival) replays the
+// serial loop over the range at once: no k_rs_replay launch behind the range.
 // Hypotheses [pa, pb) of every candidate still running: wave b works on
 // candidate b / G, hypotheses pa + (b % G) * per ... (+ per).
 template <bool STEW>
 __global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, int N, const int* cq, const int* cm,
                                                       const int2* pairs, const int* Kin, const short* table,
-                                                      RsParams P, const RsState* st, HypOut* hout, int pa, int pb,
-                                                      int G, int per, double* fbuf) {
+                                                      RsParams P, RsState* st, HypOut* hout, int pa, int pb,
+                                                      int G, int per, double* fbuf, unsigned* hcnt, unsigned* more) {
   __shared__ typename std::conditional<STEW, CoopWSS, CoopWS>::type w;
   __shared__ typename std::conditional<STEW, StewBatch, int>::type sb;
   const int c = blockIdx.x / G, g = blockIdx.x % G;
   const int lane = fresh_lane(threadIdx.x);
+  [&]() {
   const int K = Kin[c];
   if (K < 5 || st[c].done) return;
   const int p_lo = pa + g * per, p_hi = min(min(p_lo + per, pb), P.pmax);
@@ -2758,6 +2833,15 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, in
     atomicAdd(&g_phase[11], wall_clock64() - t_wave);
     atomicAdd(&g_phase[15], 1ull);
   }
+  }();
+  __threadfence();
+  unsigned last = 0;
+  if (lane == 0) last = atomicAdd(hcnt + c, 1u) == (unsigned)(G - 1);
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  __threadfence();
+  if (lane == 0) hcnt[c] = 0u;  // the next range's count starts at zero
+  rs_replay_c(c, lane, Kin, P, st, hout, pb, more);
 }
 
 // The serial loop's control (ransac_candidate: the stop test, then account)
@@ -2768,10 +2852,8 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hyps(const double* bearings, in
 // no dependent global load per hypothesis (one thread per candidate spent
 // ~0.3 us per hypothesis waiting for it: 136 us for a 444-hypothesis range).
 // The best model's 12 values are copied once, after the scan.
-__global__ __launch_bounds__(64) void k_rs_replay(const int* Kin, RsParams P, RsState* st, const HypOut* hout,
-                                                  int pb, int n, unsigned* more) {
-  const int c = blockIdx.x, lane = threadIdx.x;
-  if (c >= n) return;
+__device__ __forceinline__ void rs_replay_c(int c, int lane, const int* Kin, const RsParams& P, RsState* st,
+                                            const HypOut* hout, int pb, unsigned* more) {
   RsState* sp = st + c;
   if (sp->done) return;
   const int K = Kin[c];
@@ -2886,12 +2968,18 @@ __global__ __launch_bounds__(RS_BLOCK * RS_FIN) void k_rs_finish(const double* b
                                                                  const int* cq, const int* cm, const int2* pairs,
                                                                  const int* Kin, RsParams P, const RsState* st,
                                                                  kmx_lcd_result* res, unsigned char* masks,
-                                                                 double* fbuf, const unsigned* skip) {
+                                                                 double* fbuf, const unsigned* skip,
+                                                                 unsigned* skip_host) {
   __shared__ CoopWS w;
   __shared__ int fin_go;
   __shared__ int cnt[MAX_FEATS];
   extern __shared__ double tail_lds[];  // tail_lds_doubles(N)
-  if (skip && *skip) return;  // (uniform over the launch)
+  if (skip) {
+    const unsigned sk = *skip;
+    // the word the host reads after the call (coherent host memory: no copy)
+    if (skip_host && blockIdx.x == 0 && threadIdx.x == 0) *skip_host = sk;
+    if (sk) return;  // (uniform over the launch)
+  }
   const int wave = threadIdx.x / RS_BLOCK;
   const int lane = fresh_lane(threadIdx.x % RS_BLOCK);
   if (wave > 0) {
@@ -3231,6 +3319,7 @@ struct kmx_lcd {
   HypOut* d_hout = nullptr;
   double* d_sfbuf = nullptr;
   unsigned* d_more = nullptr;  // [more_cap] one word per range: some candidate needs the next range
+  unsigned* d_hcnt = nullptr;  // [spread_cap] k_rs_hyps' wave arrivals per candidate (zero between ranges)
   int more_cap = 0;
   unsigned* h_more = nullptr;  // pinned copy of the word just read
   // k_knn2s (synchronous calls of <= KS_MAX candidates): per-query results and
@@ -3244,7 +3333,9 @@ struct kmx_lcd {
   // output through pinned memory (a pageable copy is a blocking staged copy
   // each; the call-for-call chain made five to seven of them per call)
   size_t io_cap = 0;
-  char* h_io = nullptr;  // pinned host
+  char* h_io = nullptr;  // pinned host, coherent and mapped
+  char* z_io = nullptr;  // h_io's device pointer: the small synchronous calls' kernels read their
+                         // inputs and write their outputs there (zero-copy: no blit per copy)
   char* d_io = nullptr;
   int prof = 0;              // KMX_RS_PROF: phase timers in k_ransac_coop
   // kmx_lcd_enable_timing: events around the kNN2 and the RANSAC launches
@@ -3293,12 +3384,12 @@ void lcd_free_cand(kmx_lcd* h) {
   h->d_order = nullptr;
   for (bool& e : h->ev_rs_set) e = false;
   h->cap = 0;
-  void* q[] = {h->d_st, h->d_hout, h->d_sfbuf, h->d_more, h->d_kqb, h->d_kcnt};
+  void* q[] = {h->d_st, h->d_hout, h->d_sfbuf, h->d_more, h->d_kqb, h->d_kcnt, h->d_hcnt};
   for (void* x : q)
     if (x) (void)hipFree(x);
   if (h->h_more) (void)hipHostFree(h->h_more);
   h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_more = nullptr; h->h_more = nullptr;
-  h->d_kqb = nullptr; h->d_kcnt = nullptr; h->kqb_N = 0;
+  h->d_kqb = nullptr; h->d_kcnt = nullptr; h->kqb_N = 0; h->d_hcnt = nullptr;
   h->spread_cap = 0;
   h->more_cap = 0;
 }
@@ -3310,10 +3401,11 @@ int io_reserve(kmx_lcd* h, size_t bytes) {
   sync_rsx(h);
   if (h->h_io) (void)hipHostFree(h->h_io);
   if (h->d_io) (void)hipFree(h->d_io);
-  h->h_io = nullptr; h->d_io = nullptr;
+  h->h_io = nullptr; h->d_io = nullptr; h->z_io = nullptr;
   h->io_cap = 0;
   const size_t cap = std::max<size_t>(bytes, 256 * 1024);
-  KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_io), cap, hipHostMallocDefault));
+  KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_io), cap, hipHostMallocMapped | hipHostMallocCoherent));
+  KMX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->z_io), h->h_io, 0));
   KMX_HIP(hipMalloc(reinterpret_cast<void**>(&h->d_io), cap));
   h->io_cap = cap;
   return 0;
@@ -3352,7 +3444,7 @@ void lcd_free_pairs(kmx_lcd* h) {
   h->d_row = nullptr;
   if (h->h_io) (void)hipHostFree(h->h_io);
   if (h->d_io) (void)hipFree(h->d_io);
-  h->h_io = nullptr; h->d_io = nullptr;
+  h->h_io = nullptr; h->d_io = nullptr; h->z_io = nullptr;
   h->io_cap = 0;
 }
 
@@ -3481,10 +3573,18 @@ int ensure_cap(kmx_lcd* h, int n, bool async) {
 // CSR correspondences -> the per-candidate pair rows of k_ransac_coop
 // (pairs[c][k], K[c]); one workgroup per candidate, which also moves the
 // candidate's frame ids (and its prior) from the staging block to the slot.
+// st != null (a spread-form call): also the spread form's initial state of
+// candidate c and, over the grid, the ranges' more words (k_rs_init's work).
 __global__ __launch_bounds__(256) void k_scatter_pairs(const int64_t* mptr, const int* iq, const int* im, int N,
                                                        int2* pairs, int* Kout, const int* cq_in, const int* cm_in,
-                                                       const double* prior_in, int* cq, int* cm, double* prior) {
+                                                       const double* prior_in, int* cq, int* cm, double* prior,
+                                                       RsState* st, unsigned* hcnt, int stages, unsigned* more,
+                                                       int nmore) {
   const int c = blockIdx.x;
+  if (st) {
+    if (threadIdx.x == 0) rs_init_c(st, hcnt, c, stages);
+    for (int i = c * blockDim.x + threadIdx.x; i < nmore; i += gridDim.x * blockDim.x) more[i] = 0u;
+  }
   const int64_t b = mptr[c];
   const int K = (int)(mptr[c + 1] - b);
   for (int k = threadIdx.x; k < K; k += blockDim.x) pairs[(size_t)c * N + k] = make_int2(iq[b + k], im[b + k]);
@@ -3665,20 +3765,22 @@ int verify_ordered(kmx_lcd* h, int n, int stages, bool masks) {
 // loop closure: ~30 of 66 or 510 hypotheses) then costs one host round trip
 // instead of two, and *copied says the results are on their way.
 constexpr int SPREAD_WAVES = 1024;  // waves of one k_rs_hyps launch at most
-int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::function<int()>* copy_out = nullptr,
-                  bool* copied = nullptr) {
-  const RsParams rp = rs_params(h, stages);
-  const bool masks = want_masks || rp.pnp;
+// res_dst / mask_dst (zero-copy callers): where k_rs_finish writes the results
+// and masks (host-mapped memory) in place of the slot's device buffers; the
+// speculative finish then also writes the range's `more` word to h_more.
+// The spread form's buffers for n candidates (grow-only).
+int spread_alloc(kmx_lcd* h, int n) {
   hipStream_t st = rs_stream(h);
   if (n > h->spread_cap) {
-    void* q[] = {h->d_st, h->d_hout, h->d_sfbuf};
+    void* q[] = {h->d_st, h->d_hout, h->d_sfbuf, h->d_hcnt};
     KMX_HIP(hipStreamSynchronize(st));
     for (void* x : q)
       if (x) (void)hipFree(x);
-    h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr;
+    h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_hcnt = nullptr;
     h->spread_cap = 0;
     const int cap = std::max(n, h->spread_max);
     KMX_HIP(hipMalloc(&h->d_st, sizeof(RsState) * cap));
+    KMX_HIP(hipMalloc(&h->d_hcnt, sizeof(unsigned) * cap));
     KMX_HIP(hipMalloc(&h->d_hout, sizeof(HypOut) * (size_t)cap * h->pmax));
     KMX_HIP(hipMalloc(&h->d_sfbuf, sizeof(double) * (6 * (size_t)h->N + STASH) * std::max(SPREAD_WAVES, cap)));
     h->spread_cap = cap;
@@ -3692,11 +3794,23 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::fun
     h->more_cap = h->pmax + 1;
   }
   if (!h->h_more)
-    KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_more), sizeof(unsigned), hipHostMallocDefault));
+    KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_more), sizeof(unsigned),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  return 0;
+}
+// inited: the caller's k_scatter_pairs already initialised the state (no k_rs_init launch)
+int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::function<int()>* copy_out = nullptr,
+                  bool* copied = nullptr, kmx_lcd_result* res_dst = nullptr, unsigned char* mask_dst = nullptr,
+                  bool inited = false) {
+  const RsParams rp = rs_params(h, stages);
+  const bool masks = want_masks || rp.pnp;
+  hipStream_t st = rs_stream(h);
+  if (int rc = spread_alloc(h, n)) return rc;
   const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
   const int per_max = stew ? SG : SPREAD_PER_NISTER;
-  hipLaunchKernelGGL(k_rs_init, dim3((std::max(n, h->more_cap) + 63) / 64), dim3(64), 0, st, h->d_st, n, stages,
-                     h->d_more, h->more_cap);
+  if (!inited)
+    hipLaunchKernelGGL(k_rs_init, dim3((std::max(n, h->more_cap) + 63) / 64), dim3(64), 0, st, h->d_st, h->d_hcnt, n,
+                       stages, h->d_more, h->more_cap);
   int pa = 0;
   // the first range: a true loop closure's loop (~30 iterations) in one pass;
   // where the launch has the waves for it (one or two candidates), a whole
@@ -3706,11 +3820,16 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::fun
   const size_t tail_bytes = sizeof(double) * tail_lds_doubles(h->N);
   if (tail_bytes > 65536 - 16384)  // (max_feats near 1024: 75 KB, + 8.8 KB static: workspace, counts)
     KMX_HIP(hipFuncSetAttribute((const void*)k_rs_finish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tail_bytes));
+  const bool zc = res_dst != nullptr;
+  unsigned* z_more = nullptr;
+  if (zc) KMX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&z_more), h->h_more, 0));
   auto finish = [&](const unsigned* skip) {
     hipLaunchKernelGGL(k_rs_finish, dim3(n), dim3(RS_BLOCK * RS_FIN), tail_bytes, st,
                        (const double*)h->d_bear, (const double*)h->d_pts,
                        h->N, (const int*)h->d_cq, (const int*)h->d_cm, (const int2*)h->d_pairs, (const int*)h->d_K, rp,
-                       (const RsState*)h->d_st, h->d_res, masks ? h->d_mask : nullptr, h->d_sfbuf, skip);
+                       (const RsState*)h->d_st, zc ? res_dst : h->d_res,
+                       masks ? (zc && mask_dst ? mask_dst : h->d_mask) : nullptr, h->d_sfbuf, skip,
+                       skip && zc ? z_more : nullptr);
   };
   const bool spec = copy_out && copied && !rp.pnp;
   if (copied) *copied = false;
@@ -3725,14 +3844,13 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::fun
     hipLaunchKernelGGL(stew ? k_rs_hyps<true> : k_rs_hyps<false>, dim3(n * G), dim3(RS_BLOCK), 0, st,
                        (const double*)h->d_bear, h->N, (const int*)h->d_cq, (const int*)h->d_cm,
                        (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp,
-                       (const RsState*)h->d_st, h->d_hout, pa, pb, G, per, h->d_sfbuf);
-    hipLaunchKernelGGL(k_rs_replay, dim3(n), dim3(64), 0, st, (const int*)h->d_K, rp, h->d_st,
-                       (const HypOut*)h->d_hout, pb, n, h->d_more + it);
+                       h->d_st, h->d_hout, pa, pb, G, per, h->d_sfbuf, h->d_hcnt, h->d_more + it);
+    const bool zc_more = spec && it == 0 && zc;  // the speculative finish writes the word itself
     if (spec && it == 0) {
       finish(h->d_more);
       if (int rc = (*copy_out)()) return rc;
     }
-    KMX_HIP(hipMemcpyAsync(h->h_more, h->d_more + it, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    if (!zc_more) KMX_HIP(hipMemcpyAsync(h->h_more, h->d_more + it, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     KMX_HIP(hipStreamSynchronize(st));
     if (!*h->h_more) {
       if (spec && it == 0) {
@@ -3756,10 +3874,12 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::fun
 // sync_ok: the caller synchronises on the results (kmx_lcd_verify,
 // kmx_lcd_verify_matches), so a small call may take the spread form.
 int enqueue_ransac(kmx_lcd* h, int n, int stages, bool want_masks, bool sync_ok = false,
-                   const std::function<int()>* copy_out = nullptr, bool* copied = nullptr) {
+                   const std::function<int()>* copy_out = nullptr, bool* copied = nullptr,
+                   kmx_lcd_result* res_dst = nullptr, unsigned char* mask_dst = nullptr, bool inited = false) {
   if (copied) *copied = false;
   if (h->P.rng_stream) return verify_ordered(h, n, stages, want_masks);
-  if (sync_ok && n > 0 && n <= h->spread_max) return ransac_spread(h, n, stages, want_masks, copy_out, copied);
+  if (sync_ok && n > 0 && n <= h->spread_max)
+    return ransac_spread(h, n, stages, want_masks, copy_out, copied, res_dst, mask_dst, inited);
   const RsParams rp = rs_params(h, stages);
   if (int rc = launch_ransac(h, n, rp, h->d_table, 0, want_masks || rp.pnp)) return rc;
   if (rp.pnp && (stages & KMX_LCD_STAGE_RECOVER))
@@ -3780,7 +3900,8 @@ int slot_upload(kmx_lcd* h, int n, const int32_t* cq, const int32_t* cm) {
 // The kNN2 of n candidates (ids at dcq / dcm) on stream st: k_knn2, or for a
 // synchronous call of <= KS_MAX candidates the split form k_knn2s (same rows).
 constexpr int KS_MAX = 64;
-int launch_knn2(kmx_lcd* h, int n, const int* dcq, const int* dcm, hipStream_t st, bool sync_call) {
+int launch_knn2(kmx_lcd* h, int n, const int* dcq, const int* dcm, hipStream_t st, bool sync_call,
+                int2* pairs_dst = nullptr, int* k_dst = nullptr) {
   if (sync_call && h->knn_split && n <= KS_MAX) {
     if (h->kqb_N < h->N) {
       KMX_HIP(hipStreamSynchronize(st));
@@ -3798,7 +3919,8 @@ int launch_knn2(kmx_lcd* h, int n, const int* dcq, const int* dcm, hipStream_t s
     const size_t smem = (size_t)h->N * 32 + sizeof(uint32_t) * 4 * KS_Q * 2 + sizeof(int) * (KNN_BLOCK + 1);
     hipLaunchKernelGGL(h->P.norm == KMX_NORM_HAMMING ? k_knn2s<true> : k_knn2s<false>, dim3(n * S), dim3(KNN_BLOCK),
                        smem, st, (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, dcq, dcm,
-                       h->P.lowe_ratio, h->d_pairs, h->d_K, h->d_kqb, h->d_kcnt, S);
+                       h->P.lowe_ratio, pairs_dst ? pairs_dst : h->d_pairs, k_dst ? k_dst : h->d_K, h->d_kqb,
+                       h->d_kcnt, S);
   } else {
     hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1), st,
                        (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, dcq, dcm, h->P.norm,
@@ -4074,20 +4196,29 @@ extern "C" int kmx_lcd_match(kmx_lcd* h, int32_t n, const int32_t* cq, const int
   KMX_HIP(hipSetDevice(h->device));
   if (int rc = ensure_cap(h, n, false)) return rc;
   if (int rc = rs_wait_slot(h)) return rc;
-  // pinned staging: [cq][cm] in, [pairs][K] out
-  const size_t pb = sizeof(int2) * (size_t)n * h->N, kin = al16(sizeof(int) * n);
-  if (int rc = io_reserve(h, std::max(2 * kin, pb + kin))) return rc;
+  // pinned staging: [cq][cm] in, [pairs][K] out. The split kNN2 (small calls)
+  // reads the ids from the mapped staging and writes the rows there
+  // (zero-copy); k_knn2 goes through the device buffers and copies.
+  const size_t pb = sizeof(int2) * (size_t)n * h->N, kin = al16(sizeof(int) * n), o_out = 2 * kin;
+  if (int rc = io_reserve(h, o_out + pb + kin)) return rc;
   std::memcpy(h->h_io, cq, sizeof(int) * n);
   std::memcpy(h->h_io + kin, cm, sizeof(int) * n);
-  KMX_HIP(hipMemcpyAsync(h->d_io, h->h_io, 2 * kin, hipMemcpyHostToDevice, rs_stream(h)));
-  if (int rc = launch_knn2(h, n, (const int*)h->d_io, (const int*)(h->d_io + kin), rs_stream(h), true)) return rc;
+  const bool zc = h->knn_split && n <= KS_MAX;
+  if (zc) {
+    if (int rc = launch_knn2(h, n, (const int*)h->z_io, (const int*)(h->z_io + kin), rs_stream(h), true,
+                             (int2*)(h->z_io + o_out), (int*)(h->z_io + o_out + pb)))
+      return rc;
+  } else {
+    KMX_HIP(hipMemcpyAsync(h->d_io, h->h_io, 2 * kin, hipMemcpyHostToDevice, rs_stream(h)));
+    if (int rc = launch_knn2(h, n, (const int*)h->d_io, (const int*)(h->d_io + kin), rs_stream(h), true)) return rc;
+    KMX_HIP(hipMemcpyAsync(h->h_io + o_out, h->d_pairs, pb, hipMemcpyDeviceToHost, rs_stream(h)));
+    KMX_HIP(hipMemcpyAsync(h->h_io + o_out + pb, h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, rs_stream(h)));
+  }
   KMX_HIP(hipGetLastError());
-  KMX_HIP(hipMemcpyAsync(h->h_io, h->d_pairs, pb, hipMemcpyDeviceToHost, rs_stream(h)));
-  KMX_HIP(hipMemcpyAsync(h->h_io + pb, h->d_K, sizeof(int) * n, hipMemcpyDeviceToHost, rs_stream(h)));
   if (int rc = mark_slot(h)) return rc;
   KMX_HIP(hipStreamSynchronize(rs_stream(h)));
-  std::memcpy(pairs_out, h->h_io, pb);
-  std::memcpy(k_out, h->h_io + pb, sizeof(int) * n);
+  std::memcpy(pairs_out, h->h_io + o_out, pb);
+  std::memcpy(k_out, h->h_io + o_out + pb, sizeof(int) * n);
   return KMX_OK;
   KMX_GUARD_END
 }
@@ -4127,7 +4258,8 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
                o_iq = o_cm + al16(sizeof(int) * n), o_im = o_iq + al16(sizeof(int) * total),
                o_pr = o_im + al16(sizeof(int) * total), in_bytes = o_pr + (T_prior ? sizeof(double) * 12 * n : 0);
   const size_t rb = al16(sizeof(kmx_lcd_result) * n), out_bytes = rb + (inlier_masks ? (size_t)n * h->N : 0);
-  if (int rc = io_reserve(h, std::max(in_bytes, out_bytes))) return rc;
+  const size_t o_out = al16(in_bytes);  // outputs after the inputs (zero-copy kernels read and write at once)
+  if (int rc = io_reserve(h, o_out + out_bytes)) return rc;
   {
     int64_t* mp = reinterpret_cast<int64_t*>(h->h_io);
     for (int i = 0; i <= n; ++i) mp[i] = mptr[i] - base;
@@ -4139,27 +4271,45 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
     }
     if (T_prior) std::memcpy(h->h_io + o_pr, T_prior, sizeof(double) * 12 * n);
   }
-  KMX_HIP(hipMemcpyAsync(h->d_io, h->h_io, in_bytes, hipMemcpyHostToDevice, rs_stream(h)));
-  hipLaunchKernelGGL(k_scatter_pairs, dim3(n), dim3(256), 0, rs_stream(h), (const int64_t*)h->d_io,
-                     (const int*)(h->d_io + o_iq), (const int*)(h->d_io + o_im), h->N, h->d_pairs, h->d_K,
-                     (const int*)(h->d_io + o_cq), (const int*)(h->d_io + o_cm),
-                     T_prior ? (const double*)(h->d_io + o_pr) : nullptr, h->d_cq, h->d_cm, h->d_prior);
+  // a spread-form call (small, synchronous) reads its inputs from the mapped
+  // staging and, without PnP (k_recover writes through the device buffers),
+  // its finish writes the results there: no copy in either direction
+  const bool spread = !h->P.rng_stream && n <= h->spread_max;
+  const bool zc_out = spread && !rs_params(h, stages).pnp;
+  const char* src = spread ? h->z_io : h->d_io;
+  if (spread) {
+    if (int rc = spread_alloc(h, n)) return rc;
+  } else {
+    KMX_HIP(hipMemcpyAsync(h->d_io, h->h_io, in_bytes, hipMemcpyHostToDevice, rs_stream(h)));
+  }
+  hipLaunchKernelGGL(k_scatter_pairs, dim3(n), dim3(256), 0, rs_stream(h), (const int64_t*)src,
+                     (const int*)(src + o_iq), (const int*)(src + o_im), h->N, h->d_pairs, h->d_K,
+                     (const int*)(src + o_cq), (const int*)(src + o_cm),
+                     T_prior ? (const double*)(src + o_pr) : nullptr, h->d_cq, h->d_cm, h->d_prior,
+                     spread ? h->d_st : nullptr, h->d_hcnt, stages, h->d_more, h->more_cap);
   KMX_HIP(hipGetLastError());
   const std::function<int()> copy_out = [&]() -> int {
-    KMX_HIP(hipMemcpyAsync(h->h_io, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost, rs_stream(h)));
+    if (zc_out) return 0;
+    KMX_HIP(hipMemcpyAsync(h->h_io + o_out, h->d_res, sizeof(kmx_lcd_result) * n, hipMemcpyDeviceToHost,
+                           rs_stream(h)));
     if (inlier_masks)
-      KMX_HIP(hipMemcpyAsync(h->h_io + rb, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost, rs_stream(h)));
+      KMX_HIP(hipMemcpyAsync(h->h_io + o_out + rb, h->d_mask, (size_t)n * h->N, hipMemcpyDeviceToHost,
+                             rs_stream(h)));
     return 0;
   };
   bool copied = false;
-  if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr, true, &copy_out, &copied)) return rc;
+  if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr, true, &copy_out, &copied,
+                              zc_out ? reinterpret_cast<kmx_lcd_result*>(h->z_io + o_out) : nullptr,
+                              zc_out && inlier_masks ? reinterpret_cast<unsigned char*>(h->z_io + o_out + rb) : nullptr,
+                              spread))
+    return rc;
   KMX_HIP(hipGetLastError());
   if (!copied)
     if (int rc = copy_out()) return rc;
   if (int rc = mark_slot(h)) return rc;
   KMX_HIP(hipStreamSynchronize(rs_stream(h)));
-  std::memcpy(results, h->h_io, sizeof(kmx_lcd_result) * n);
-  if (inlier_masks) std::memcpy(inlier_masks, h->h_io + rb, (size_t)n * h->N);
+  std::memcpy(results, h->h_io + o_out, sizeof(kmx_lcd_result) * n);
+  if (inlier_masks) std::memcpy(inlier_masks, h->h_io + o_out + rb, (size_t)n * h->N);
   return KMX_OK;
   KMX_GUARD_END
 }

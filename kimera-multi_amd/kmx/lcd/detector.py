@@ -348,48 +348,73 @@ class LoopClosureDetector:
         return int(vertex)
 
     # ------------------------------------------- reference-shaped single calls --
+    # the one-candidate entry points with raw-address arguments (ctypes'
+    # data_as costs ~6 us per array, more than the kernels it feeds)
+    _VP = C.c_void_p
+    _VM1 = C.CFUNCTYPE(C.c_int, _VP, C.c_int32, _VP, _VP, _VP, _VP, _VP, C.c_int, _VP, _VP, _VP)
+    _M1 = C.CFUNCTYPE(C.c_int, _VP, C.c_int32, _VP, _VP, _VP, _VP)
+
     def _one(self):
-        """Buffers and ctypes pointers of the one-candidate calls, made once per
-        pool stride: the reference's verification thread makes three calls per
-        candidate (verifyLoopSpin, drawio:2638-2657), so their host side is kept
-        to filling two ids and one count."""
+        """Buffers, addresses and call objects of the one-candidate calls, made
+        once per pool stride: the reference's verification thread makes three
+        calls per candidate (verifyLoopSpin, drawio:2638-2657), so their host
+        side is kept to filling two ids, a count and the pairs."""
         N = max(self.max_feats, 1)
         o = getattr(self, "_one_bufs", None)
         if o is None or o["N"] != N:
             o = {"N": N, "cq": np.zeros(1, np.int32), "cm": np.zeros(1, np.int32),
                  "mptr": np.zeros(2, np.int64), "pairs": np.zeros((1, N, 2), np.int32), "k": np.zeros(1, np.int32),
-                 "masks": np.zeros((1, N), np.uint8), "res": (abi.LcdResult * 1)(), "zero": np.zeros(1, np.int32),
-                 "prior": np.zeros(12, np.float64)}
-            for key in ("cq", "cm", "pairs", "k", "zero"):
-                o[key + "_p"] = abi.iptr(o[key])
-            o["mptr_p"], o["masks_p"], o["prior_p"] = abi.i64ptr(o["mptr"]), abi.u8ptr(o["masks"]), abi.fptr(o["prior"])
+                 "masks": np.zeros((1, N), np.uint8), "res": (abi.LcdResult * 1)(),
+                 "iq": np.zeros(N, np.int32), "im": np.zeros(N, np.int32), "prior": np.zeros(12, np.float64),
+                 "T": np.eye(4)}
+            a = {k: o[k].ctypes.data for k in ("cq", "cm", "mptr", "pairs", "k", "masks", "iq", "im", "prior")}
+            a["res"] = C.addressof(o["res"])
+            o["a"] = a
+            o["vm"] = self._VM1(("kmx_lcd_verify_matches", self.L))
+            o["m"] = self._M1(("kmx_lcd_match", self.L))
+            o["t12"] = np.frombuffer(o["res"][0].T_query_match, np.float64)
             self._one_bufs = o
         return o
 
     def _verify_one(self, vertex_query, vertex_match, iq, im, stages, prior=None):
         """kmx_lcd_verify_matches for one candidate through the _one buffers:
-        (result record, inlier-mask row over the given pairs)."""
+        (result record, inlier-mask row over the given pairs; both views of
+        the buffers, valid until the next call)."""
         o = self._one()
-        o["cq"][0], o["cm"][0] = self.frame_id(vertex_query), self.frame_id(vertex_match)
-        n = iq.shape[0]
-        if im.shape[0] != n:
+        n = len(iq)
+        if len(im) != n:
             raise ValueError("i_query and i_match differ in length")
+        if n > o["N"]:
+            raise ValueError("more pairs than the pool's max_feats")
+        o["cq"][0], o["cm"][0] = self.frame_id(vertex_query), self.frame_id(vertex_match)
         o["mptr"][1] = n
-        pp = None
+        o["iq"][:n] = iq
+        o["im"][:n] = im
+        a = o["a"]
+        pa = None
         if prior is not None:
             o["prior"][:] = prior
-            pp = o["prior_p"]
-        check(self.L.kmx_lcd_verify_matches(self.h, 1, o["cq_p"], o["cm_p"], o["mptr_p"],
-                                            abi.iptr(iq) if n else o["zero_p"], abi.iptr(im) if n else o["zero_p"],
-                                            int(stages), pp, o["res"], o["masks_p"]), "kmx_lcd_verify_matches")
+            pa = a["prior"]
+        check(o["vm"](self.h, 1, a["cq"], a["cm"], a["mptr"], a["iq"], a["im"], int(stages), pa, a["res"], a["masks"]),
+              "kmx_lcd_verify_matches")
         return o["res"][0], o["masks"][0, :n]
+
+    _T4_POS = np.array([0, 1, 2, 4, 5, 6, 8, 9, 10, 3, 7, 11])  # (R row-major, t) -> [R | t] rows
+
+    def _T4_one(self):
+        """T_query_match of the last one-candidate result as a fresh 4x4."""
+        o = self._one_bufs
+        T = o["T"].copy()
+        T.ravel()[self._T4_POS] = o["t12"]
+        return T
 
     def computeMatchedIndices(self, vertex_query, vertex_match):
         """LoopClosureDetector::computeMatchedIndices (drawio:2583-2586) on two
         resident frames: (i_query, i_match) int32 arrays in query order."""
         o = self._one()
         o["cq"][0], o["cm"][0] = self.frame_id(vertex_query), self.frame_id(vertex_match)
-        check(self.L.kmx_lcd_match(self.h, 1, o["cq_p"], o["cm_p"], o["pairs_p"], o["k_p"]), "kmx_lcd_match")
+        a = o["a"]
+        check(o["m"](self.h, 1, a["cq"], a["cm"], a["pairs"], a["k"]), "kmx_lcd_match")
         k = int(o["k"][0])
         return o["pairs"][0, :k, 0].copy(), o["pairs"][0, :k, 1].copy()
 
@@ -399,25 +424,26 @@ class LoopClosureDetector:
         i_match_inliers, T_query_match 4x4 with unit-norm t); ok = at least
         min_nr_2d2d_inliers inliers. The inlier lists are what the reference
         writes back into i_query / i_match."""
-        iq = np.ascontiguousarray(i_query, np.int32)
-        im = np.ascontiguousarray(i_match, np.int32)
+        iq = np.asarray(i_query, np.int32)
+        im = np.asarray(i_match, np.int32)
         r, mask = self._verify_one(vertex_query, vertex_match, iq, im, abi.KMX_LCD_STAGE_2D2D)
-        keep = (mask & 1).astype(bool)
-        return bool(r.accepted), iq[keep], im[keep], _T4(r.T_query_match)
+        keep = (mask & 1).view(bool)
+        return bool(r.accepted), iq[keep], im[keep], self._T4_one()
 
     def recoverPose(self, vertex_query, vertex_match, i_query, i_match, T_query_match_mono=None):
         """recoverPose (drawio:2595-2598) on geometricVerificationNister's
         inliers: the 3D-3D recovery (1-point given the 2D-2D rotation of
         T_query_match_mono, or Arun) or EPnP, per LcdParams. Returns (ok,
         T_query_match 4x4, inlier mask over the given pairs)."""
-        iq = np.ascontiguousarray(i_query, np.int32)
-        im = np.ascontiguousarray(i_match, np.int32)
+        iq = np.asarray(i_query, np.int32)
+        im = np.asarray(i_match, np.int32)
         prior = None
         if T_query_match_mono is not None:
             T = np.asarray(T_query_match_mono, np.float64)
-            prior = np.concatenate([T[:3, :3].reshape(9), T[:3, 3]])
+            prior = self._one()["prior"]
+            prior[:] = T[:3].ravel()[self._T4_POS]
         r, mask = self._verify_one(vertex_query, vertex_match, iq, im, abi.KMX_LCD_STAGE_RECOVER, prior)
-        return bool(r.accepted), _T4(r.T_query_match), (mask & 2).astype(bool)
+        return bool(r.accepted), self._T4_one(), (mask & 2) != 0
 
     # --------------------------------------------------------------- batched --
     def match(self, cand_query, cand_match):
