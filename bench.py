@@ -223,18 +223,20 @@ def gpu_parity(drv, snap, cpu):
 PEAK_FP64 = 78.6e12  # 256 CU x 64 fp64 FMA lanes x 2 flops x 2.4 GHz (not in the in-container guide)
 
 
-def ransac_roofline(algo, n_cand, tk):
+def ransac_roofline(algo, n_cand, tk, ratio="lcd_fp64_stewenius.json"):
     """The dominant LCD kernel, k_ransac_coop (95 % of the verification time):
     issued fp64 lane-flops per candidate from the PMC passes of the same
     workload shape (profiles/lcd_fp64_stewenius.json, scripts/gpu_lcd_pmc3.sh
     + scripts/lcd_pmc_summary.py: a stored ratio, not a counter of this run)
     times this step's candidates over its evented RANSAC time, against the fp64
-    vector peak."""
+    vector peak. `ratio`: the stored file for the workload (the hard leg's
+    look-alikes run 500 hypotheses each: profiles/lcd_fp64_stewenius_hard.json,
+    scripts/gpu_lcd_pmc3.sh TAG scripts/lcd_hard_timing.py N)."""
     out = {"kernel": "k_ransac_coop (2D-2D 5-point RANSAC)", "bound": "fp64 valu", "unit": "FLOP/s",
            "peak": PEAK_FP64, "ransac_ms": tk["ransac_ms"], "knn_ms": tk["knn_ms"],
            "ransac_share": tk["ransac_ms"] / max(tk["knn_ms"] + tk["ransac_ms"], 1e-12),
            "achieved": None, "frac": None}
-    f = ROOT / "profiles" / "lcd_fp64_stewenius.json"
+    f = ROOT / "profiles" / ratio
     if algo != 0 or not f.exists() or tk["ransac_ms"] <= 0:
         out["note"] = "no stored fp64 counts for this solver"
         return out
@@ -248,7 +250,7 @@ def ransac_roofline(algo, n_cand, tk):
     out.update({"achieved": ach, "frac": ach / PEAK_FP64, "valu_issue_frac": valu_issue,
                 "valu_issue_rule": f"{per['valu_insts']:.4g} VALU wave-instructions per candidate (stored PMC ratio) "
                                    "x 2 SIMD cycles each (SIMD-32) / (1024 SIMDs x 2.4 GHz)",
-                "flops_source": "stored PMC ratio (profiles/lcd_fp64_stewenius.json): "
+                "flops_source": f"stored PMC ratio (profiles/{ratio}, {d.get('commit', 'commit not recorded')}): "
                                 f"{per['fp64_issued_flops']:.4g} issued fp64 lane-flops per candidate (64 lanes per "
                                 "wave instruction, 2 per FMA, whatever the exec mask)",
                 "fp64_share_of_valu_insts": d["fractions"]["fp64_share_of_valu_insts"],
@@ -368,6 +370,7 @@ def hard_leg(args, params, rank, world, barrier_sync):
     out = {"metric": "LC candidates verified/sec (hard: look-alikes that fail geometry)", "unit": "candidates/s",
            "value": steps * len(cq) / el * world, "n_local": int(len(cq)), "steps": steps, "elapsed": el,
            "ransac_ms": tk["ransac_ms"], "knn_ms": tk["knn_ms"],
+           "roofline": ransac_roofline(args.lcd_algo, len(cq), tk, "lcd_fp64_stewenius_hard.json"),
            "first512": {"accepted": int(sum(r["accepted"] for r in res)), "iterations_2d2d_mean": float(its.mean()),
                         "iterations_2d2d_min": int(its.min()), "matches_after_lowe_mean": float(nm.mean())},
            "workload": f"{len(cq)} candidates of {2 * C_} synthetic frames x 500 ORB features: 150 look-alike "
