@@ -437,7 +437,7 @@ def single_leg(args, params, pool, hard_pool):
                      "gpu_over_cpu_latency": (float(np.median(lat)) / (np.median(cpu) * 1e3)) if cpu else None}
     out["note"] = ("one candidate per call chain (computeMatchedIndices, geometricVerificationNister, recoverPose), "
                    "as the reference's verification thread; a call this small takes the spread form (its hypotheses "
-                   "on many waves at once, the serial loop's control replayed: lcd.hip k_rs_hyps / k_rs_replay / "
+                   "on many waves at once, the serial loop's control replayed: lcd.hip k_rs_hyps (its last wave per candidate replays) / "
                    "k_rs_finish)")
     return out
 

@@ -2678,7 +2678,8 @@ __global__ __launch_bounds__(RS_BLOCK, LB) void k_ransac_coop(const double* bear
 //      (k_rs_hyps: SG per wave for Stewenius, as one batch of the work-queue
 //      kernel; per hypothesis the same operations, so the same bits), scoring
 //      each model over the candidate's pairs;
-//   2. replays the serial loop's control over them in order (k_rs_replay: the
+//   2. replays the serial loop's control over them in order (rs_replay_c, by the
+//      range's last wave per candidate: the
 //      `account` arithmetic of ransac_candidate, one thread per candidate),
 //      stopping where the serial loop stops;
 //   3. computes the next range only for candidates whose replay ran past the

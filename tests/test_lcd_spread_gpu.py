@@ -1,4 +1,4 @@
-"""The spread form of the 2D-2D RANSAC (lcd.hip k_rs_hyps / k_rs_replay /
+"""The spread form of the 2D-2D RANSAC (lcd.hip k_rs_hyps, whose last wave per candidate replays the control, /
 k_rs_finish): a synchronous call of a few candidates — the
 reference verifies one candidate per call — computes ranges of each
 candidate's hypotheses on many waves at once and replays the serial loop's
