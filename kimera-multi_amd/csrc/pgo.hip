@@ -305,34 +305,40 @@ __device__ __forceinline__ int2 unpack_int2(double v) {
   return make_int2((int)(b & 0xffffffffll), (int)(b >> 32));
 }
 
-// RW = 10: compact record (unit quaternion of R, t, w kappa, +-w tau) — 72 B
-// in HBM (GS = 9 doubles), the sign bit of w tau is the tail flag (w tau >= 0;
-// a zero weight is +-0.0), the other endpoint in Dev::rec_o (4 B): 76 B per
-// incidence. In registers it is the
-// 10-word form (..., w tau, {other, tail << 31}), five 16-B parts; the gathers
-// rebuild R from the quaternion (R R^T = I to rounding, as the preconditioner
-// assumes).
+// RW = 10: compact record — 64 B in HBM (GS = 8 doubles, four 16-B parts):
+// three components of the unit quaternion of R (all but its largest, which is
+// made >= 0 and rebuilt as sqrt(1 - the others' squares): well conditioned,
+// since it is >= 1/2), t, w kappa, +-w tau (the sign bit is the tail flag; w
+// tau >= 0, a zero weight is +-0.0); Dev::rec_o (4 B) holds the other endpoint
+// in its low 29 bits (two's complement) and the rebuilt component's index in
+// bits 29-31: 68 B per incidence (round 5: the whole quaternion, 76 B). In
+// registers it is the 10-word form (w, x, y, z, t, w kappa, w tau, {other,
+// tail << 31}), five 16-B parts; the gathers rebuild R from the quaternion
+// (R R^T = I to rounding, as the preconditioner assumes).
 // RW = 16: full record (R, t, w kappa, w tau, {other, edge|tail}, pad), for
 // measurement rotations off SO(3).
-struct alignas(8) DPair {  // two doubles at 8-B alignment (a 72-B record's parts)
-  double x, y;
-};
 template <int RW>
 struct Rec {
   static constexpr int Q = RW / 2;        // 16-B parts in registers
-  static constexpr int GS = RW == 10 ? 9 : 16;  // doubles per record in HBM
-  static constexpr int WK = RW == 10 ? 7 : 12;  // index of w kappa (w tau follows)
+  static constexpr int GS = RW == 10 ? 8 : 16;  // doubles per record in HBM
+  static constexpr int WK = RW == 10 ? 6 : 12;  // index of w kappa (w tau follows)
   __device__ static __forceinline__ void load(const Dev& d, size_t k, double2 q[Q]) {
     if constexpr (RW == 10) {
-      const double* p = d.rec + (size_t)GS * k;
-      const DPair* p2 = reinterpret_cast<const DPair*>(p);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const DPair v = p2[i];
-        q[i] = make_double2(v.x, v.y);
-      }
-      const double wt = p[8];
-      const long long bits = (long long)(unsigned)d.rec_o[k] | (std::signbit(wt) ? (1ll << 63) : 0ll);
+      const double2* p2 = reinterpret_cast<const double2*>(d.rec + (size_t)GS * k);
+      const double2 a0 = p2[0], a1 = p2[1], a2 = p2[2], a3 = p2[3];  // (qa, qb) (qc, t0) (t1, t2) (wk, +-wt)
+      const unsigned raw = (unsigned)d.rec_o[k];
+      const int other = (int)(raw << 3) >> 3;
+      const unsigned big = raw >> 29;
+      const double qa = a0.x, qb = a0.y, qc = a1.x;
+      const double ql = sqrt(1.0 - (qa * qa + qb * qb + qc * qc));
+      const double w = big == 0 ? ql : qa, x = big == 0 ? qa : (big == 1 ? ql : qb);
+      const double y = big <= 1 ? qb : (big == 2 ? ql : qc), z = big == 3 ? ql : qc;
+      q[0] = make_double2(w, x);
+      q[1] = make_double2(y, z);
+      q[2] = make_double2(a1.y, a2.x);
+      q[3] = make_double2(a2.y, a3.x);
+      const double wt = a3.y;
+      const long long bits = (long long)(unsigned)other | (std::signbit(wt) ? (1ll << 63) : 0ll);
       q[4] = make_double2(std::fabs(wt), __longlong_as_double(bits));
     } else {
       const double2* q2 = reinterpret_cast<const double2*>(d.rec + (size_t)GS * k);
@@ -2881,6 +2887,22 @@ void rot_to_quat(const double* R, double* q) {
   const double n = std::sqrt(w * w + x * x + y * y + z * z);
   q[0] = w / n; q[1] = x / n; q[2] = y / n; q[3] = z / n;
 }
+// Rec<10>'s three stored components: all but the largest (made >= 0 by
+// negating the quaternion, which leaves R unchanged), whose index goes to
+// rec_o's bits 29-31; and the device's rebuild of the fourth (Rec<10>::load).
+int quat_pack(const double* q, double* q3) {
+  int big = 0;
+  for (int i = 1; i < 4; ++i)
+    if (std::fabs(q[i]) > std::fabs(q[big])) big = i;
+  const double sg = q[big] < 0.0 ? -1.0 : 1.0;
+  for (int i = 0, j = 0; i < 4; ++i)
+    if (i != big) q3[j++] = sg * q[i];
+  return big;
+}
+void quat_unpack(const double* q3, int big, double* q) {
+  const double ql = std::sqrt(1.0 - (q3[0] * q3[0] + q3[1] * q3[1] + q3[2] * q3[2]));
+  for (int i = 0, j = 0; i < 4; ++i) q[i] = i == big ? ql : q3[j++];
+}
 // the device's Rec<10>::edge expressions
 void quat_to_rot(const double* q, double* R) {
   const double w = q[0], x = q[1], y = q[2], z = q[3];
@@ -3496,15 +3518,20 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   }
   // record width: compact (quaternion) when every local measurement rotation
   // is rebuilt from its unit quaternion to 1e-12 (a rotation), full otherwise
-  std::vector<double> quat((size_t)std::max(h->mloc, 1) * 4);
+  // (the three stored components per edge, and the rebuilt one's index)
+  std::vector<double> quat((size_t)std::max(h->mloc, 1) * 3);
+  std::vector<int> qbig(std::max(h->mloc, 1), 0);
   {
-    bool ok = true;
+    // (the other endpoint takes rec_o's low 29 bits: local poses and public
+    // slots below 2^28, far above any single GPU's share)
+    bool ok = nloc < (1 << 28) && h->npub < (1 << 28);
     for (int k = 0; k < h->mloc && ok; ++k) {
       const double* Q = R + 9 * ledges[k];
-      double* qk = &quat[4 * (size_t)k];
-      rot_to_quat(Q, qk);
-      double Rq[9];
-      quat_to_rot(qk, Rq);
+      double q4[4], qr[4], Rq[9];
+      rot_to_quat(Q, q4);
+      qbig[k] = quat_pack(q4, &quat[3 * (size_t)k]);
+      quat_unpack(&quat[3 * (size_t)k], qbig[k], qr);
+      quat_to_rot(qr, Rq);
       for (int i = 0; i < 9 && ok; ++i) ok = std::fabs(Rq[i] - Q[i]) <= 1e-12;
     }
     h->rw = ok ? 10 : 16;
@@ -3513,22 +3540,22 @@ extern "C" int kmx_pgo_set_graph(kmx_pgo* h, int n_robots, const int32_t* n_pose
   std::vector<int> inc_ptr(nloc + 1, 0);
   for (int i = 0; i < nloc; ++i) inc_ptr[i + 1] = inc_ptr[i] + deg[i];
   h->ninc = inc_ptr[nloc];
-  const int GS = RW == 10 ? 9 : 16;  // Rec<RW>::GS
+  const int GS = RW == 10 ? 8 : 16;  // Rec<RW>::GS
   std::vector<double> rec((size_t)(h->ninc + 1) * GS, 0.0);  // + one zero pad record
   std::vector<int> rec_o(RW == 10 ? h->ninc + 1 : 1, 0);
   std::vector<int2> eipos(std::max(h->mloc, 1), make_int2(-1, -1));
   std::vector<int> fill(inc_ptr.begin(), inc_ptr.end() - 1);
   auto put_rec = [&](int pos, int k, int64_t e, int other, int code) {
     double* c = &rec[(size_t)pos * GS];
-    const double* Q = RW == 10 ? &quat[4 * (size_t)k] : R + 9 * e;
+    const double* Q = RW == 10 ? &quat[3 * (size_t)k] : R + 9 * e;
     int j = 0;
-    for (int q = 0; q < (RW == 10 ? 4 : 9); ++q) c[j++] = Q[q];
+    for (int q = 0; q < (RW == 10 ? 3 : 9); ++q) c[j++] = Q[q];
     for (int q = 0; q < 3; ++q) c[j++] = t[3 * e + q];
     c[j++] = weight[e] * kappa[e];
     const double wt = weight[e] * tau[e];
     if (RW == 10) {  // compact: the tail flag in w tau's sign bit, the other endpoint apart
       c[j++] = (code & 0x80000000) ? -wt : wt;
-      rec_o[pos] = other;
+      rec_o[pos] = (int)(((unsigned)other & 0x1fffffffu) | ((unsigned)qbig[k] << 29));
     } else {
       c[j++] = wt;
       const long long bits = (long long)(unsigned)other | ((long long)code << 32);
@@ -4530,7 +4557,7 @@ extern "C" int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_byt
   KMX_CHECK(ready(h), KMX_ESTATE, "set_graph first");
   const int64_t L = (int64_t)h->robots.size(), n = std::max(h->nloc, 1), ps = 4 * h->P.r;
   int64_t b = 0;
-  const int rb = h->rw == 10 ? 9 * 8 + 4 : 128;  // bytes per incidence record (compact: 72 + the 4-B other endpoint)
+  const int rb = h->rw == 10 ? 8 * 8 + 4 : 128;  // bytes per incidence record (compact: 64 + the 4-B other endpoint)
   b += (int64_t)(h->ninc + 1) * rb + (int64_t)(h->nloc + 1) * 4;         // records, CSR
   b += (int64_t)std::max(h->mloc, 1) * (3 * 8 + 8);                      // kappa, tau, w, positions
   b += n * ps * 8 * (int64_t)nvec(h) + n * (6 + 3 * SYM4) * 8;         // vectors, S, Pinv, D, D - S

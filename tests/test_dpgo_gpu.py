@@ -113,13 +113,13 @@ def test_zero_weights_keep_incidence_direction(gpu, records):
 
 @pytest.mark.parametrize("robust,records", [(False, "compact"), (True, "compact"), (True, "full")])
 def test_rounds_match_oracle(gpu, robust, records):
-    """compact: 76-B records (SO(3) input, rotation rebuilt from its quaternion); full: the
+    """compact: 68-B records (SO(3) input, rotation rebuilt from its quaternion); full: the
     128-B records of a graph with a non-rotation measurement."""
     g, P, X0 = _setup(robust=robust)
     if records == "full":
         _full_records(g)
     s, o = _pair(g, P, X0)
-    assert s.memory()[1] == (76 if records == "compact" else 128)
+    assert s.memory()[1] == (68 if records == "compact" else 128)
     for it in range(12):
         s.refresh_local()
         sg = s.iterate()
