@@ -9,7 +9,9 @@ TAG=${1:-pmc}
 CFG=${2:-synth100k}
 mkdir -p gpurun_out/$TAG
 i=0
-for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+# PASSES (optional): ";"-separated counter sets replacing the three traffic passes
+IFS=';' read -ra SETS <<< "${PASSES:-FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum}"
+for C in "${SETS[@]}"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $C -d gpurun_out/$TAG/p$i -o run --output-format csv -- python3 bench.py --config $CFG --burn-in ${BURN:-40} --steps ${STEPS:-10} --warmup 0 --profile --no-cpu --no-lcd > gpurun_out/$TAG/p$i.json 2> gpurun_out/$TAG/p$i.err
   rc=$?; echo "pmc pass $i ($C) rc=$rc"
