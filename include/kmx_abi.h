@@ -346,9 +346,10 @@ int kmx_pgo_eval(kmx_pgo* h, int robot, int mode, const double* V, double* out,
 /* Edges in robot `robot`'s local problem (private + shared incident edges). */
 int kmx_pgo_local_edges(kmx_pgo* h, int robot, int64_t* m_local);
 /* Resident device bytes of the handle and the bytes of one incidence record
- * (76: compact — the rotation's unit quaternion, t, w kappa, w tau with the
- * tail flag in its sign, and the 4-B other endpoint; 128: full rotation, when
- * some measurement rotation is not in SO(3) to 1e-12). */
+ * (68: compact — three components of the rotation's unit quaternion, t,
+ * w kappa, w tau with the tail flag in its sign, and the 4-B other endpoint
+ * with the fourth component's index; 128: full rotation, when some measurement
+ * rotation is not in SO(3) to 1e-12). */
 int kmx_pgo_memory(kmx_pgo* h, int64_t* device_bytes, int* record_bytes);
 /* Live instrumentation of the dominant kernel (the Hessian-vector product of
  * the tCG loop). When enabled, every Hessian-vector launch enqueued by
