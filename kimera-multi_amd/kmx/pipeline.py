@@ -116,10 +116,16 @@ class Accepted:
 
 
 def accepted_from_results(stream: LcStream, sel: np.ndarray, results) -> Accepted:
-    """Turn kmx_lcd_result records (dicts of LoopClosureDetector.verify) of the
-    candidates `sel` into loop-closure measurements."""
-    ok = np.array([r["accepted"] for r in results], bool)
-    T = np.array([r["T_query_match"] for r in results], np.float64).reshape(-1, 12)
+    """Turn kmx_lcd_result records of the candidates `sel` into loop-closure
+    measurements: the structured array of LoopClosureDetector.verify_arrays,
+    or a list of result dicts (LoopClosureDetector.verify, the CPU tests'
+    restatement)."""
+    if isinstance(results, np.ndarray) and results.dtype.names:
+        ok = results["accepted"] != 0
+        T = np.asarray(results["T_query_match"], np.float64).reshape(-1, 12)
+    else:
+        ok = np.array([r["accepted"] for r in results], bool)
+        T = np.array([r["T_query_match"] for r in results], np.float64).reshape(-1, 12)
     s = sel[ok]
     return Accepted(r1=stream.r_q[s], p1=stream.p_q[s], r2=stream.r_m[s], p2=stream.p_m[s],
                     R=T[ok, :9].reshape(-1, 3, 3), t=T[ok, 9:].reshape(-1, 3), truth=stream.truth[s],
@@ -260,13 +266,15 @@ def run_pipeline(g0: PoseGraphData, stream: LcStream, params, lcd_params, *, ran
     lo, hi = robot_ranges(g0.n_robots, world)[rank]
     sel = np.nonzero((stream.r_q >= lo) & (stream.r_q < hi))[0]
     out = {"rank": rank, "world": world, "candidates": int(stream.truth.shape[0])}
-    # 1. LCD (candidates of this rank's query robots; pool upload outside the timed region)
+    # 1. LCD (candidates of this rank's query robots; pool upload and a warm-up call outside the timed region)
     if verifier is None:
         from .lcd import LoopClosureDetector
         det = LoopClosureDetector(lcd_params, device=device)
         det.set_pool(stream.pool)
+        if sel.size:  # one small untimed call: the kernels' first launch (code-object load, scratch)
+            det.verify(stream.cand_query[sel[:64]], stream.cand_match[sel[:64]])
         det.sync()
-        verifier = lambda q, m: det.verify(q, m)[0]  # noqa: E731
+        verifier = det.verify_arrays
     t0 = time.perf_counter()
     results = verifier(stream.cand_query[sel], stream.cand_match[sel])
     t_lcd = time.perf_counter() - t0
