@@ -464,9 +464,10 @@ def stream_leg(det, pool, cq, cm, args):
     ts = np.array(ts) * 1e6
     info = det.pool_info()
     out = {"frames_added": n_add, "us_per_frame": el * 1e6 / n_add, "us_per_frame_median": float(np.median(ts)),
-           "us_first_append": float(ts[0]), "bytes_per_frame": int(pool.max_feats * (32 + 48 + 48) + 4),
+           "us_first_append": float(ts[0]), "bytes_per_frame": int(pool.max_feats * (32 + 24 + 24) + 4),
            "pool_after": info,
-           "note": "one kmx_lcd_add_frames call per frame from pageable host memory; the first call doubles the "
+           "note": "one kmx_lcd_add_frames call per frame from pageable host memory (copied into a pinned, "
+                   "mapped staging area and scattered into the pool by one kernel); the first call doubles the "
                    "resident pool (device-to-device copy)"}
     pairs, k = det.match(cq, cm)
     mptr = np.zeros(len(cq) + 1, np.int64)

@@ -3334,6 +3334,12 @@ struct kmx_lcd {
   // output through pinned memory (a pageable copy is a blocking staged copy
   // each; the call-for-call chain made five to seven of them per call)
   size_t io_cap = 0;
+  // small frame uploads (add_frames: one keyframe per call) are staged here
+  // (pinned, mapped) and scattered into the pool by one kernel that reads the
+  // mapped pages, instead of four pageable copies
+  char* h_fst = nullptr;
+  char* z_fst = nullptr;
+  size_t fst_cap = 0;
   char* h_io = nullptr;  // pinned host, coherent and mapped
   char* z_io = nullptr;  // h_io's device pointer: the small synchronous calls' kernels read their
                          // inputs and write their outputs there (zero-copy: no blit per copy)
@@ -3447,6 +3453,9 @@ void lcd_free_pairs(kmx_lcd* h) {
   if (h->d_io) (void)hipFree(h->d_io);
   h->h_io = nullptr; h->d_io = nullptr; h->z_io = nullptr;
   h->io_cap = 0;
+  if (h->h_fst) (void)hipHostFree(h->h_fst);
+  h->h_fst = h->z_fst = nullptr;
+  h->fst_cap = 0;
 }
 
 // One pass of opengv's drawIndexSample: S swaps of the persistent shuffle over
@@ -3998,11 +4007,58 @@ int grow_pool(kmx_lcd* h, int need) {
   return 0;
 }
 
+// The staged frames (mapped host pages: desc | bearings | points | n_feats)
+// into the pool: 8-B words, n_feats 4-B.
+__global__ __launch_bounds__(256) void k_put_frames(const unsigned long long* src, size_t w_desc, size_t w_bear,
+                                                    unsigned long long* desc, unsigned long long* bear,
+                                                    unsigned long long* pts, const int* nf_src, int* nf, int n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t tot = w_desc + 2 * w_bear;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
+    const unsigned long long v = src[i];
+    if (i < w_desc) desc[i] = v;
+    else if (i < w_desc + w_bear) bear[i - w_desc] = v;
+    else pts[i - w_desc - w_bear] = v;
+  }
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n; i += stride) nf[i] = nf_src[i];
+}
+constexpr size_t FRAME_STAGE_MAX = 16u << 20;  // larger uploads (set_pool) copy from the caller's pages
+
 // Frames [F, F + n) from host arrays (desc [n][N][32], bearings / points
 // [n][N][3]); the caller has grown the pool.
 int upload_frames(kmx_lcd* h, int n, const int32_t* n_feats, const uint8_t* desc, const double* bearings,
                   const double* points) {
   const size_t at = (size_t)h->F * h->N, FN = (size_t)n * h->N;
+  const size_t b_desc = FN * 32, b_bear = FN * 3 * sizeof(double), b_nf = sizeof(int) * n;
+  const size_t b_all = b_desc + 2 * b_bear + b_nf;
+  if (b_all <= FRAME_STAGE_MAX) {
+    if (b_all > h->fst_cap) {  // grow-only; the previous upload has completed (synchronised below)
+      if (h->h_fst) (void)hipHostFree(h->h_fst);
+      h->h_fst = h->z_fst = nullptr;
+      h->fst_cap = 0;
+      const size_t cap = std::max<size_t>(b_all, 256 * 1024);
+      KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_fst), cap, hipHostMallocMapped | hipHostMallocCoherent));
+      KMX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->z_fst), h->h_fst, 0));
+      h->fst_cap = cap;
+    }
+    std::memcpy(h->h_fst, desc, b_desc);
+    std::memcpy(h->h_fst + b_desc, bearings, b_bear);
+    std::memcpy(h->h_fst + b_desc + b_bear, points, b_bear);
+    std::memcpy(h->h_fst + b_desc + 2 * b_bear, n_feats, b_nf);
+    const size_t words = (b_desc + 2 * b_bear) / 8;
+    const int blocks = (int)std::min<size_t>((words + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_put_frames, dim3(std::max(blocks, 1)), dim3(256), 0, h->stream,
+                       reinterpret_cast<const unsigned long long*>(h->z_fst), b_desc / 8, b_bear / 8,
+                       reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(h->d_desc) + at * 32),
+                       reinterpret_cast<unsigned long long*>(h->d_bear + at * 3),
+                       reinterpret_cast<unsigned long long*>(h->d_pts + at * 3),
+                       reinterpret_cast<const int*>(h->z_fst + b_desc + 2 * b_bear), h->d_nfeat + h->F, n);
+    KMX_HIP(hipGetLastError());
+    KMX_HIP(hipStreamSynchronize(h->stream));  // the staging area is reused by the next call
+    h->h_nfeat.insert(h->h_nfeat.end(), n_feats, n_feats + n);
+    h->F += n;
+    return 0;
+  }
   KMX_HIP(hipMemcpyAsync(reinterpret_cast<uint8_t*>(h->d_desc) + at * 32, desc, FN * 32, hipMemcpyHostToDevice,
                          h->stream));
   KMX_HIP(hipMemcpyAsync(h->d_bear + at * 3, bearings, FN * 3 * sizeof(double), hipMemcpyHostToDevice, h->stream));
