@@ -480,10 +480,12 @@ class LoopClosureDetector:
         return self.verify_matches_csr(cand_query, cand_match, mptr, iq, im, stages, T_prior, with_masks)
 
     def verify_matches_csr(self, cand_query, cand_match, mptr, i_query, i_match, stages: int = 3, T_prior=None,
-                           with_masks: bool = False):
+                           with_masks: bool = False, as_arrays: bool = False):
         """verify_matches with the correspondences already in CSR form: candidate
         i's pairs are (i_query[k], i_match[k]) for k in [mptr[i], mptr[i+1])
-        (kmx_lcd_verify_matches' own layout; no per-candidate Python lists)."""
+        (kmx_lcd_verify_matches' own layout; no per-candidate Python lists).
+        as_arrays: the results as one structured array (verify_arrays' form)
+        instead of a list of dicts."""
         cq = np.ascontiguousarray(cand_query, dtype=np.int32)
         cm = np.ascontiguousarray(cand_match, dtype=np.int32)
         n = cq.shape[0]
@@ -506,7 +508,8 @@ class LoopClosureDetector:
                                             abi.iptr(im), int(stages), abi.fptr(pr) if pr is not None else None,
                                             res, abi.u8ptr(masks) if with_masks else None),
               "kmx_lcd_verify_matches")
-        return _results(res, n, self._refines(stages)), (masks[:n] if with_masks else None)
+        out = np.frombuffer(res, dtype=_RES_DT, count=n).copy() if as_arrays else _results(res, n, self._refines(stages))
+        return out, (masks[:n] if with_masks else None)
 
     def verify(self, cand_query, cand_match, with_masks: bool = False):
         """Verify candidates; returns (list of result dicts, masks or None).

@@ -160,6 +160,31 @@ def test_verify_matches_stages_match_oracle(gpu, recovery, algo):
             assert np.array_equal(g2[i]["T_query_match"], full[i]["T_query_match"]), i
 
 
+def test_structured_results_equal_dicts(gpu):
+    """verify_arrays and verify_matches_csr(as_arrays=True) return the same
+    kmx_lcd_result records as the dict forms, field for field."""
+    pool = make_lcd_pool(16, 200, seed=5)
+    det = LoopClosureDetector(LcdParams())
+    det.set_pool(pool)
+    cq, cm = pool.cand_query, pool.cand_match
+    full, _ = det.verify(cq, cm)
+    arr = det.verify_arrays(cq, cm)
+    pairs, k = det.match(cq, cm)
+    mptr = np.r_[0, np.cumsum(k)].astype(np.int64)
+    sel = np.arange(pairs.shape[1])[None, :] < k[:, None]
+    iq, im = pairs[:, :, 0][sel], pairs[:, :, 1][sel]
+    dres, _ = det.verify_matches_csr(cq, cm, mptr, iq, im)
+    ares, _ = det.verify_matches_csr(cq, cm, mptr, iq, im, as_arrays=True)
+    assert arr.shape == (len(cq),) and ares.shape == (len(cq),) and sum(r["accepted"] for r in full) > 0
+    for d, a in ((full, arr), (dres, ares)):
+        for i, r in enumerate(d):
+            for f in ("n_matches", "mono_inliers", "stereo_inliers", "pnp_inliers", "iterations_2d2d"):
+                assert r[f] == int(a[f][i]), (f, i)
+            assert r["accepted"] == bool(a["accepted"][i])
+            assert np.array_equal(r["T_query_match"], a["T_query_match"][i])
+    assert det.verify_arrays(cq[:0], cm[:0]).shape == (0,)
+
+
 def test_reference_shaped_single_calls(gpu):
     """computeMatchedIndices -> geometricVerificationNister -> recoverPose on
     vertices, as verifyLoopSpin calls them (drawio:2638-2657)."""
