@@ -77,6 +77,34 @@ def test_primitives_match_oracle(gpu, r, records):
             assert abs(gs - os_) <= 1e-10 * max(1.0, abs(os_)), (mode, gs, os_)
 
 
+def _rot(axis, angle):
+    return _expm_so3((np.asarray(axis, float) / np.linalg.norm(axis) * angle)[None])[0]
+
+
+def test_compact_record_quaternion_cases(gpu):
+    """The 68-B record stores three quaternion components and rebuilds the
+    largest: measurement rotations whose largest component is each of w, x, y,
+    z, of either sign before the flip, and ties (180 degrees about a diagonal:
+    |x| = |y|), against the restatement's primitives to 1e-12."""
+    g, P, X0 = _setup(robust=False)
+    cases = [np.eye(3), _rot([1, 0, 0], np.pi), _rot([0, 1, 0], np.pi), _rot([0, 0, 1], np.pi),
+             _rot([1, 1, 0], np.pi), _rot([1, 1, 1], np.pi), _rot([0, 1, 1], 2.0), _rot([1, 0, 0], 3.0),
+             _rot([0, -1, 0], 3.1), _rot([0, 0, -1], 2.9), _rot([-1, 2, 0.5], -2.5), _rot([1, 1, 1], 2 * np.pi / 3)]
+    for i, R in enumerate(cases * 4):
+        g.R[7 * i + 3] = R
+    s, o = _pair(g, P, X0)
+    assert s.memory()[1] == 68
+    rng = np.random.default_rng(2)
+    for a in range(g.n_robots):
+        V = rng.standard_normal(X0[a].shape)
+        for mode in (abi.KMX_EVAL_COST_EGRAD, abi.KMX_EVAL_EHESS):
+            Vin = X0[a] if mode == abi.KMX_EVAL_COST_EGRAD else V
+            gout, gs = s.eval(a, mode, Vin)
+            oout, os_ = o.eval(a, mode, Vin)
+            assert np.abs(gout - oout).max() <= 1e-12 * max(1.0, np.abs(oout).max()), mode
+    s.close()
+
+
 @pytest.mark.parametrize("records", ["compact", "full"])
 def test_zero_weights_keep_incidence_direction(gpu, records):
     """The compact record keeps the tail flag in w tau's sign bit (a zero weight
