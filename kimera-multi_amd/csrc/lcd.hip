@@ -155,6 +155,84 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_knn2(const uint32_t* desc, const 
   else knn2_body<false>(desc, nfeat, N, cq, cm, lowe, pairs, Kout, sm_u32);
 }
 
+// k_knn2 with four queries per thread (N <= 512; used for Hamming, see
+// kmx_lcd::knn_q): each match descriptor read
+// from LDS serves four queries instead of two, which halves the LDS-to-VGPR
+// traffic per descriptor pair (2 x 16-B broadcast reads per match and wave);
+// two waves per candidate. Query i lives on thread i / 4, so the compaction in
+// thread order is query order: the same rows and K as k_knn2.
+constexpr int KQ_BLOCK = 128, KQ_Q = 4;
+template <bool HAMMING>
+__global__ __launch_bounds__(KQ_BLOCK) void k_knn2q(const uint32_t* desc, const int* nfeat, int N, const int* cq,
+                                                    const int* cm, double lowe, int2* pairs, int* Kout) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm_u32[];
+  uint4* sdesc = reinterpret_cast<uint4*>(sm_u32);  // [nm][2]
+  __shared__ int wtot[KQ_BLOCK / 64];
+  const int c = blockIdx.x;
+  const int q = cq[c], m = cm[c];
+  const int nq = nfeat[q], nm = nfeat[m];
+  const int tid = threadIdx.x;
+  const uint4* dm = reinterpret_cast<const uint4*>(desc + (size_t)m * N * 8);
+  for (int i = tid; i < nm * 2; i += KQ_BLOCK) sdesc[i] = dm[i];
+  const int i0 = tid * KQ_Q;
+  uint32_t a[KQ_Q][8];
+#pragma unroll
+  for (int u = 0; u < KQ_Q; ++u) {
+    const uint4* d4 = reinterpret_cast<const uint4*>(desc + ((size_t)q * N + min(i0 + u, max(nq - 1, 0))) * 8);
+    const uint4 x = d4[0], y = d4[1];
+    a[u][0] = x.x; a[u][1] = x.y; a[u][2] = x.z; a[u][3] = x.w;
+    a[u][4] = y.x; a[u][5] = y.y; a[u][6] = y.z; a[u][7] = y.w;
+  }
+  __syncthreads();
+  uint32_t k0[KQ_Q], k1[KQ_Q];
+#pragma unroll
+  for (int u = 0; u < KQ_Q; ++u) k0[u] = k1[u] = 0xffffffffu;
+  if (nm >= 2 && i0 < nq) {
+    for (int j = 0; j < nm; ++j) {
+      const uint4 x = sdesc[2 * j], y = sdesc[2 * j + 1];
+      const uint32_t b[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int u = 0; u < KQ_Q; ++u) {
+        uint32_t d = 0;
+        if constexpr (HAMMING) {
+#pragma unroll
+          for (int w = 0; w < 8; ++w) d += __popc(a[u][w] ^ b[w]);
+        } else {
+#pragma unroll
+          for (int w = 0; w < 8; ++w) d = __builtin_amdgcn_sad_u8(a[u][w], b[w], d);
+        }
+        two_nearest(k0[u], k1[u], (d << 10) | (uint32_t)j);
+      }
+    }
+  }
+  int found = 0;
+  bool pass[KQ_Q];
+#pragma unroll
+  for (int u = 0; u < KQ_Q; ++u) {
+    const int d0 = (int)(k0[u] >> 10), d1 = (int)(k1[u] >> 10);
+    pass[u] = nm >= 2 && i0 + u < nq && (double)(float)d0 < lowe * (double)(float)d1;
+    found += pass[u] ? 1 : 0;
+  }
+  // exclusive prefix of the per-thread counts in thread (= query) order
+  const int lane = tid & 63, wv = tid >> 6;
+  int incl = found;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wtot[wv] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wv; ++w) base += wtot[w];
+  int pos = base + incl - found;
+  int2* out = pairs + (size_t)c * N;
+#pragma unroll
+  for (int u = 0; u < KQ_Q; ++u)
+    if (pass[u]) out[pos++] = make_int2(i0 + u, (int)(k0[u] & 1023u));
+  if (tid == KQ_BLOCK - 1) Kout[c] = base + incl;
+}
+
 // kNN2 of a small synchronous call (the reference's verification thread
 // matches ONE candidate per call: computeMatchedIndices, drawio:2583-2586).
 // k_knn2 gives a candidate one workgroup, whose 4 waves scan every match
@@ -3326,6 +3404,12 @@ struct kmx_lcd {
   // k_knn2s (synchronous calls of <= KS_MAX candidates): per-query results and
   // the per-candidate arrival counters (zero between calls; KMX_LCD_KSPLIT=0: off)
   bool knn_split = true;
+  // k_knn2q (4 queries per thread) for the Hamming matcher at N <= 512
+  // (configs[2], same box: 6.72 vs 7.01 ms per 50k kNN2, 1.442e6 vs 1.416e6
+  // candidates/s); the L1 matcher stays on k_knn2 (4.33 vs 4.16 ms: the
+  // two-wave candidates run five waves per SIMD instead of eight, and the
+  // v_sad_u8 chains need them). KMX_LCD_KNNQ=0: k_knn2 for both.
+  bool knn_q = true;
   int* d_kqb = nullptr;
   unsigned* d_kcnt = nullptr;
   int kqb_N = 0;
@@ -3931,10 +4015,14 @@ int launch_knn2(kmx_lcd* h, int n, const int* dcq, const int* dcm, hipStream_t s
                        smem, st, (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, dcq, dcm,
                        h->P.lowe_ratio, pairs_dst ? pairs_dst : h->d_pairs, k_dst ? k_dst : h->d_K, h->d_kqb,
                        h->d_kcnt, S);
+  } else if (h->knn_q && h->P.norm == KMX_NORM_HAMMING && h->N <= KQ_BLOCK * KQ_Q) {
+    hipLaunchKernelGGL(k_knn2q<true>, dim3(n), dim3(KQ_BLOCK),
+                       (size_t)h->N * 32, st, (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, dcq, dcm,
+                       h->P.lowe_ratio, pairs_dst ? pairs_dst : h->d_pairs, k_dst ? k_dst : h->d_K);
   } else {
     hipLaunchKernelGGL(k_knn2, dim3(n), dim3(KNN_BLOCK), (size_t)h->N * 32 + sizeof(int) * (KNN_BLOCK + 1), st,
                        (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, dcq, dcm, h->P.norm,
-                       h->P.lowe_ratio, h->d_pairs, h->d_K);
+                       h->P.lowe_ratio, pairs_dst ? pairs_dst : h->d_pairs, k_dst ? k_dst : h->d_K);
   }
   return 0;
 }
@@ -4099,6 +4187,7 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
   h->own_stream = true;
   if (const char* e = std::getenv("KMX_LCD_RSX")) h->rs_conc = std::atoi(e) != 0;
   if (const char* e = std::getenv("KMX_LCD_KSPLIT")) h->knn_split = std::atoi(e) != 0;
+  if (const char* e = std::getenv("KMX_LCD_KNNQ")) h->knn_q = std::atoi(e) != 0;
   bool ok = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking) == hipSuccess;
   for (int i = 1; i < LCD_SLOTS && ok; ++i) ok = hipStreamCreateWithFlags(&h->rsx[i], hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; i < LCD_SLOTS && ok; ++i)

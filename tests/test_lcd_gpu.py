@@ -252,3 +252,41 @@ def test_split_knn2_matches_oracle(gpu, monkeypatch, norm):
         ref = O.knn2(nrm, 0.7, desc[a, :counts[a]], desc[b, :counts[b]])
         got = pa[i % 40, :ka[i % 40]]
         assert np.array_equal(got[:, 0], ref[:, 0]) and np.array_equal(got[:, 1], ref[:, 1]), (a, b)
+
+
+@pytest.mark.parametrize("N", [300, 512, 513])
+def test_knn2q_hamming_matches_oracle(gpu, monkeypatch, N):
+    """The Hamming matcher's batched kNN2 (k_knn2q: four queries per thread,
+    N <= 512; above it, and with KMX_LCD_KNNQ=0, k_knn2): calls of more than
+    64 candidates, feature counts that end a thread's four queries part way,
+    frames with 0 / 1 features, near-duplicates and exact ties — the
+    restatement's rows and counts, and k_knn2's."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(17)
+    counts = [0, 1, 2, 3, 5, 127, 128, 129, min(N, 300), N - 1, N]
+    F = len(counts)
+    desc = rng.integers(0, 256, (F, N, 32), dtype=np.uint8)
+    for f in range(1, F):
+        k = min(counts[f], counts[f - 1]) // 2
+        desc[f, :k] = desc[f - 1, :k] ^ (rng.random((k, 32)) < 0.02).astype(np.uint8)
+        if counts[f] > 3:
+            desc[f, counts[f] - 1] = desc[f, 0]
+    bear = np.zeros((F, N, 3))
+    bear[..., 2] = 1.0
+    pts = np.ones((F, N, 3))
+    cand = [(a, b) for a in range(F) for b in range(F) if a != b]  # 110 > 64: the batched kernels
+    cq = np.array([c[0] for c in cand], np.int32)
+    cm = np.array([c[1] for c in cand], np.int32)
+    res = {}
+    for q in ("1", "0"):
+        monkeypatch.setenv("KMX_LCD_KNNQ", q)
+        d = LoopClosureDetector(LcdParams(norm="hamming"))
+        d.add_frames(np.array(counts, np.int32), desc, bear, pts)
+        res[q] = d.match(cq, cm)
+        d.close()
+    (pa, ka), (pb, kb) = res["1"], res["0"]
+    assert np.array_equal(ka, kb)
+    for i, (a, b) in enumerate(cand):
+        assert np.array_equal(pa[i, :ka[i]], pb[i, :kb[i]]), (a, b)
+        ref = O.knn2(1, 0.7, desc[a, :counts[a]], desc[b, :counts[b]])
+        assert np.array_equal(pa[i, :ka[i], 0], ref[:, 0]) and np.array_equal(pa[i, :ka[i], 1], ref[:, 1]), (a, b)
