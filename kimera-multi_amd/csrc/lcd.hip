@@ -2208,8 +2208,13 @@ __host__ __device__ constexpr size_t tail_lds_doubles(int N) { return 3 * ((size
 struct NoCount {  // the work-queue kernel: no multi-wave count
   __device__ int operator()(const double*, const unsigned char*, int, double) const { return -1; }
 };
+// Not inlined: the tail runs once per candidate, and as a call of its own its
+// registers are allocated apart from the hypothesis loop's, so the Stewenius
+// work queue fits 128 VGPRs (four waves per SIMD) with 200 spilled instead of
+// 308 inlined; same box, 20k candidates: 1.514e6 -> 1.543e6 candidates/s, the
+// hard leg 7.89e4 -> 8.24e4 (profiles/r06/lcd_lb4/).
 template <bool WAVE, typename WS, typename Count = NoCount>
-__device__ __forceinline__ void ransac_tail(int c, WS& w, double* F1, double* F2, const double* points, int N,
+__device__ __noinline__ void ransac_tail(int c, WS& w, double* F1, double* F2, const double* points, int N,
                                             int q, int m, const int2* pl, int K, const RsParams& P,
                                             kmx_lcd_result* R_, unsigned char* mask, int have, int iterations,
                                             int lane, double* lds = nullptr, Count&& count_best = Count{}) {
@@ -3753,8 +3758,11 @@ int launch_ransac(kmx_lcd* h, int n, const RsParams& rp, const short* table, int
   // order (measured with -Rpass-analysis=kernel-resource-usage, round 4; the
   // RANSAC step took ~11 % longer without them).
   const bool stew = rp.algo == KMX_ALGO_STEWENIUS;
-  auto kc = stew ? k_ransac_coop<3, true> : k_ransac_coop<4, false>;
-  if (rp.pmax < 0) kc = stew ? k_ransac_coop<2, true> : k_ransac_coop<3, false>;  // never: keeps them compiled
+  // four waves per SIMD for both solvers (Stewenius: 128 VGPRs and 10.2 KB of
+  // LDS, 16 per CU; no other Stewenius instance is compiled, so the tail's
+  // call sees only this bound)
+  auto kc = stew ? k_ransac_coop<4, true> : k_ransac_coop<4, false>;
+  if (rp.pmax < 0) kc = k_ransac_coop<3, false>;  // never: keeps the Nister 3-wave form compiled
   // one wave per resident slot (<= RS_MAX_SLOTS: the scratch is sized for it)
   int per_cu = 0, dev = 0, cus = 0;
   KMX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kc, RS_BLOCK, 0));
