@@ -139,3 +139,37 @@ def test_run_pipeline_world2_equals_world1():
         assert out["dpgo"]["ate_m"] == ref["dpgo"]["ate_m"]
         for a, (R, t) in ref["trajectory"].items():
             assert np.array_equal(out["trajectory"][a][0], R) and np.array_equal(out["trajectory"][a][1], t), (rank, a)
+
+
+def test_lcd_results_columnwise_and_structured():
+    """kmx_lcd_result records read column by column (detector._results) keep
+    every field of the ctypes records, and accepted_from_results takes the
+    structured-array form (LoopClosureDetector.verify_arrays) and the dict form
+    to the same loop closures."""
+    from kmx import abi
+    from kmx.lcd.detector import _RES_DT, _results
+    n = 37
+    res = (abi.LcdResult * n)()
+    rng = np.random.default_rng(3)
+    for i in range(n):
+        r = res[i]
+        r.n_matches, r.mono_inliers, r.stereo_inliers = 3 * i, 2 * i, i
+        r.pnp_inliers, r.iterations_2d2d, r.accepted = i % 5, 7 * i, int(i % 3 == 0)
+        for k in range(12):
+            r.T_query_match[k] = rng.standard_normal()
+    d = _results(res, n, refines=True)
+    for i in range(n):
+        r = res[i]
+        assert (d[i]["n_matches"], d[i]["mono_inliers"], d[i]["stereo_inliers"], d[i]["pnp_inliers"],
+                d[i]["iterations_2d2d"]) == (r.n_matches, r.mono_inliers, r.stereo_inliers, r.pnp_inliers,
+                                            r.iterations_2d2d)
+        assert d[i]["accepted"] is bool(r.accepted) and d[i]["pose_refined"] is bool(r.accepted)
+        assert np.array_equal(d[i]["T_query_match"], np.array(r.T_query_match[:]))
+    assert _results(res, 0) == []
+    arr = np.frombuffer(res, dtype=_RES_DT, count=n).copy()
+    stream = PL.make_lc_stream(_team(), n, 0, n_feats=60, seed=1)
+    sel = np.arange(n)
+    a1, a2 = PL.accepted_from_results(stream, sel, d), PL.accepted_from_results(stream, sel, arr)
+    for k in ("r1", "p1", "r2", "p2", "R", "t", "truth"):
+        assert np.array_equal(getattr(a1, k), getattr(a2, k)), k
+    assert a1.r1.shape[0] == sum(i % 3 == 0 for i in range(n))
