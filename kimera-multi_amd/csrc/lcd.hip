@@ -28,6 +28,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <functional>
 #include <random>
@@ -249,7 +250,7 @@ constexpr int KS_Q = 64;  // queries per workgroup of k_knn2s
 template <bool HAMMING>
 __global__ __launch_bounds__(KNN_BLOCK) void k_knn2s(const uint32_t* desc, const int* nfeat, int N, const int* cq,
                                                      const int* cm, double lowe, int2* pairs, int* Kout, int* qbest,
-                                                     unsigned* cnt, int S) {
+                                                     unsigned* cnt, int S, unsigned* done, unsigned seq) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm_u32[];
   uint32_t* sdesc = sm_u32;                                        // [nm][8]
   uint32_t* mk = sm_u32 + (size_t)N * 8;                           // [4][KS_Q][2] the quarters' keys
@@ -334,6 +335,11 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_knn2s(const uint32_t* desc, const
     if (j >= 0) out[pos++] = make_int2(i, j);
   }
   if (tid == 0) Kout[c] = scnt[KNN_BLOCK];
+  if (done) {  // a one-candidate call's completion word (wait_done), after every row
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // --------------------------------------------------- small linear algebra --
@@ -3053,7 +3059,7 @@ __global__ __launch_bounds__(RS_BLOCK * RS_FIN) void k_rs_finish(const double* b
                                                                  const int* Kin, RsParams P, const RsState* st,
                                                                  kmx_lcd_result* res, unsigned char* masks,
                                                                  double* fbuf, const unsigned* skip,
-                                                                 unsigned* skip_host) {
+                                                                 unsigned* skip_host, unsigned* done, unsigned seq) {
   __shared__ CoopWS w;
   __shared__ int fin_go;
   __shared__ int cnt[MAX_FEATS];
@@ -3062,7 +3068,13 @@ __global__ __launch_bounds__(RS_BLOCK * RS_FIN) void k_rs_finish(const double* b
     const unsigned sk = *skip;
     // the word the host reads after the call (coherent host memory: no copy)
     if (skip_host && blockIdx.x == 0 && threadIdx.x == 0) *skip_host = sk;
-    if (sk) return;  // (uniform over the launch)
+    if (sk) {  // (uniform over the launch)
+      if (done && threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      return;
+    }
   }
   const int wave = threadIdx.x / RS_BLOCK;
   const int lane = fresh_lane(threadIdx.x % RS_BLOCK);
@@ -3128,6 +3140,12 @@ __global__ __launch_bounds__(RS_BLOCK * RS_FIN) void k_rs_finish(const double* b
   if (!met) {
     if (lane == 0) fin_go = -1;
     __syncthreads();  // A for the waves that wait to count
+  }
+  // a one-candidate call's completion word (wait_done): wave 0 wrote the
+  // result and the mask; its stores are complete before lane 0's release
+  if (done) {
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -3406,6 +3424,11 @@ struct kmx_lcd {
   unsigned* d_hcnt = nullptr;  // [spread_cap] k_rs_hyps' wave arrivals per candidate (zero between ranges)
   int more_cap = 0;
   unsigned* h_more = nullptr;  // pinned copy of the word just read
+  // a one-candidate call's completion word (mapped; wait_done) and its sequence
+  unsigned* h_done = nullptr;
+  unsigned* z_done = nullptr;
+  unsigned done_seq = 0;
+  bool spin_wait = true;  // KMX_LCD_SPINWAIT=0: hipStreamSynchronize instead
   // k_knn2s (synchronous calls of <= KS_MAX candidates): per-query results and
   // the per-candidate arrival counters (zero between calls; KMX_LCD_KSPLIT=0: off)
   bool knn_split = true;
@@ -3506,6 +3529,42 @@ int io_reserve(kmx_lcd* h, size_t bytes) {
   h->io_cap = cap;
   return 0;
 }
+// One-candidate calls (the reference's verifyLoopSpin pattern) end in a kernel
+// that stores a fresh sequence number to a mapped word after its outputs
+// (system-scope release): spinning on that word returns ~6 us sooner than
+// hipStreamSynchronize, which also waits for the dispatch's end-of-kernel
+// signal (scripts/probe/sync_latency.hip: 30.5 vs 36.2 us around a 25-us
+// kernel). next_done gives the word and the sequence (nullptr: not used).
+unsigned* next_done(kmx_lcd* h, unsigned* seq) {
+  if (!h->spin_wait) return nullptr;
+  if (!h->h_done) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->h_done), 64, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&h->z_done), h->h_done, 0) != hipSuccess) {
+      if (h->h_done) (void)hipHostFree(h->h_done);
+      h->h_done = h->z_done = nullptr;
+      h->spin_wait = false;
+      return nullptr;
+    }
+    __atomic_store_n(h->h_done, 0u, __ATOMIC_RELEASE);
+  }
+  *seq = ++h->done_seq == 0 ? ++h->done_seq : h->done_seq;  // never 0
+  return h->z_done;
+}
+// Wait for `seq` in the completion word; past 2 s of spinning, synchronise
+// the stream (a faulted or hung kernel surfaces there) and require the word.
+int wait_done(kmx_lcd* h, hipStream_t st, unsigned seq) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) != seq) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      KMX_HIP(hipStreamSynchronize(st));
+      KMX_CHECK(__atomic_load_n(h->h_done, __ATOMIC_ACQUIRE) == seq, KMX_EHIP,
+                "a one-candidate call's kernel finished without its completion word");
+      return 0;
+    }
+  }
+  return 0;
+}
 inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 // The next call's slot: its buffers become d_cq .. d_order.
 void use_next_slot(kmx_lcd* h) {
@@ -3545,6 +3604,8 @@ void lcd_free_pairs(kmx_lcd* h) {
   if (h->h_fst) (void)hipHostFree(h->h_fst);
   h->h_fst = h->z_fst = nullptr;
   h->fst_cap = 0;
+  if (h->h_done) (void)hipHostFree(h->h_done);
+  h->h_done = h->z_done = nullptr;
 }
 
 // One pass of opengv's drawIndexSample: S swaps of the persistent shuffle over
@@ -3901,9 +3962,11 @@ int spread_alloc(kmx_lcd* h, int n) {
   return 0;
 }
 // inited: the caller's k_scatter_pairs already initialised the state (no k_rs_init launch)
+// fseq (a zero-copy call of one candidate): the sequence its last kernel
+// stores to the completion word, for the caller's wait_done (0: none).
 int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::function<int()>* copy_out = nullptr,
                   bool* copied = nullptr, kmx_lcd_result* res_dst = nullptr, unsigned char* mask_dst = nullptr,
-                  bool inited = false) {
+                  bool inited = false, unsigned* fseq = nullptr) {
   const RsParams rp = rs_params(h, stages);
   const bool masks = want_masks || rp.pnp;
   hipStream_t st = rs_stream(h);
@@ -3925,13 +3988,18 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::fun
   const bool zc = res_dst != nullptr;
   unsigned* z_more = nullptr;
   if (zc) KMX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&z_more), h->h_more, 0));
-  auto finish = [&](const unsigned* skip) {
+  if (fseq) *fseq = 0;
+  const bool one = zc && n == 1 && fseq;  // a one-candidate call: its finishes store the completion word
+  auto finish = [&](const unsigned* skip, unsigned* seq_out) {
+    unsigned seq = 0;
+    unsigned* done = one && seq_out ? next_done(h, &seq) : nullptr;
+    if (seq_out) *seq_out = done ? seq : 0;
     hipLaunchKernelGGL(k_rs_finish, dim3(n), dim3(RS_BLOCK * RS_FIN), tail_bytes, st,
                        (const double*)h->d_bear, (const double*)h->d_pts,
                        h->N, (const int*)h->d_cq, (const int*)h->d_cm, (const int2*)h->d_pairs, (const int*)h->d_K, rp,
                        (const RsState*)h->d_st, zc ? res_dst : h->d_res,
                        masks ? (zc && mask_dst ? mask_dst : h->d_mask) : nullptr, h->d_sfbuf, skip,
-                       skip && zc ? z_more : nullptr);
+                       skip && zc ? z_more : nullptr, done, seq);
   };
   const bool spec = copy_out && copied && !rp.pnp;
   if (copied) *copied = false;
@@ -3948,15 +4016,21 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::fun
                        (const int2*)h->d_pairs, (const int*)h->d_K, (const short*)h->d_table, rp,
                        h->d_st, h->d_hout, pa, pb, G, per, h->d_sfbuf, h->d_hcnt, h->d_more + it);
     const bool zc_more = spec && it == 0 && zc;  // the speculative finish writes the word itself
+    unsigned sseq = 0;
     if (spec && it == 0) {
-      finish(h->d_more);
+      finish(h->d_more, zc_more ? &sseq : nullptr);
       if (int rc = (*copy_out)()) return rc;
     }
     if (!zc_more) KMX_HIP(hipMemcpyAsync(h->h_more, h->d_more + it, sizeof(unsigned), hipMemcpyDeviceToHost, st));
-    KMX_HIP(hipStreamSynchronize(st));
+    if (sseq) {  // the finish stored the more word before its completion word
+      if (int rc = wait_done(h, st, sseq)) return rc;
+    } else {
+      KMX_HIP(hipStreamSynchronize(st));
+    }
     if (!*h->h_more) {
       if (spec && it == 0) {
         *copied = true;
+        if (fseq) *fseq = sseq;
         KMX_HIP(hipGetLastError());
         return 0;
       }
@@ -3965,7 +4039,7 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::fun
     pa = pb;
     range = pa < 510 ? 510 - pa : 1500;  // then the rest of a 500-iteration loop, then its skips
   }
-  finish(nullptr);
+  finish(nullptr, fseq);
   if (rp.pnp && (stages & KMX_LCD_STAGE_RECOVER))
     if (int rc = launch_recover(h, n, pnp_params(h, stages), h->d_table_rec, 0)) return rc;
   KMX_HIP(hipGetLastError());
@@ -3977,11 +4051,13 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::fun
 // kmx_lcd_verify_matches), so a small call may take the spread form.
 int enqueue_ransac(kmx_lcd* h, int n, int stages, bool want_masks, bool sync_ok = false,
                    const std::function<int()>* copy_out = nullptr, bool* copied = nullptr,
-                   kmx_lcd_result* res_dst = nullptr, unsigned char* mask_dst = nullptr, bool inited = false) {
+                   kmx_lcd_result* res_dst = nullptr, unsigned char* mask_dst = nullptr, bool inited = false,
+                   unsigned* fseq = nullptr) {
   if (copied) *copied = false;
+  if (fseq) *fseq = 0;
   if (h->P.rng_stream) return verify_ordered(h, n, stages, want_masks);
   if (sync_ok && n > 0 && n <= h->spread_max)
-    return ransac_spread(h, n, stages, want_masks, copy_out, copied, res_dst, mask_dst, inited);
+    return ransac_spread(h, n, stages, want_masks, copy_out, copied, res_dst, mask_dst, inited, fseq);
   const RsParams rp = rs_params(h, stages);
   if (int rc = launch_ransac(h, n, rp, h->d_table, 0, want_masks || rp.pnp)) return rc;
   if (rp.pnp && (stages & KMX_LCD_STAGE_RECOVER))
@@ -4003,7 +4079,7 @@ int slot_upload(kmx_lcd* h, int n, const int32_t* cq, const int32_t* cm) {
 // synchronous call of <= KS_MAX candidates the split form k_knn2s (same rows).
 constexpr int KS_MAX = 64;
 int launch_knn2(kmx_lcd* h, int n, const int* dcq, const int* dcm, hipStream_t st, bool sync_call,
-                int2* pairs_dst = nullptr, int* k_dst = nullptr) {
+                int2* pairs_dst = nullptr, int* k_dst = nullptr, unsigned* done = nullptr, unsigned seq = 0) {
   if (sync_call && h->knn_split && n <= KS_MAX) {
     if (h->kqb_N < h->N) {
       KMX_HIP(hipStreamSynchronize(st));
@@ -4022,7 +4098,7 @@ int launch_knn2(kmx_lcd* h, int n, const int* dcq, const int* dcm, hipStream_t s
     hipLaunchKernelGGL(h->P.norm == KMX_NORM_HAMMING ? k_knn2s<true> : k_knn2s<false>, dim3(n * S), dim3(KNN_BLOCK),
                        smem, st, (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, dcq, dcm,
                        h->P.lowe_ratio, pairs_dst ? pairs_dst : h->d_pairs, k_dst ? k_dst : h->d_K, h->d_kqb,
-                       h->d_kcnt, S);
+                       h->d_kcnt, S, done, seq);
   } else if (h->knn_q && h->P.norm == KMX_NORM_HAMMING && h->N <= KQ_BLOCK * KQ_Q) {
     hipLaunchKernelGGL(k_knn2q<true>, dim3(n), dim3(KQ_BLOCK),
                        (size_t)h->N * 32, st, (const uint32_t*)h->d_desc, (const int*)h->d_nfeat, h->N, dcq, dcm,
@@ -4196,6 +4272,7 @@ extern "C" int kmx_lcd_create(const kmx_lcd_params* params, int device, kmx_lcd*
   if (const char* e = std::getenv("KMX_LCD_RSX")) h->rs_conc = std::atoi(e) != 0;
   if (const char* e = std::getenv("KMX_LCD_KSPLIT")) h->knn_split = std::atoi(e) != 0;
   if (const char* e = std::getenv("KMX_LCD_KNNQ")) h->knn_q = std::atoi(e) != 0;
+  if (const char* e = std::getenv("KMX_LCD_SPINWAIT")) h->spin_wait = std::atoi(e) != 0;
   bool ok = hipStreamCreateWithFlags(&h->kstream, hipStreamNonBlocking) == hipSuccess;
   for (int i = 1; i < LCD_SLOTS && ok; ++i) ok = hipStreamCreateWithFlags(&h->rsx[i], hipStreamNonBlocking) == hipSuccess;
   for (int i = 0; i < LCD_SLOTS && ok; ++i)
@@ -4358,9 +4435,11 @@ extern "C" int kmx_lcd_match(kmx_lcd* h, int32_t n, const int32_t* cq, const int
   std::memcpy(h->h_io, cq, sizeof(int) * n);
   std::memcpy(h->h_io + kin, cm, sizeof(int) * n);
   const bool zc = h->knn_split && n <= KS_MAX;
+  unsigned seq = 0;
+  unsigned* done = zc && n == 1 ? next_done(h, &seq) : nullptr;  // one candidate: spin on the completion word
   if (zc) {
     if (int rc = launch_knn2(h, n, (const int*)h->z_io, (const int*)(h->z_io + kin), rs_stream(h), true,
-                             (int2*)(h->z_io + o_out), (int*)(h->z_io + o_out + pb)))
+                             (int2*)(h->z_io + o_out), (int*)(h->z_io + o_out + pb), done, seq))
       return rc;
   } else {
     KMX_HIP(hipMemcpyAsync(h->d_io, h->h_io, 2 * kin, hipMemcpyHostToDevice, rs_stream(h)));
@@ -4370,7 +4449,11 @@ extern "C" int kmx_lcd_match(kmx_lcd* h, int32_t n, const int32_t* cq, const int
   }
   KMX_HIP(hipGetLastError());
   if (int rc = mark_slot(h)) return rc;
-  KMX_HIP(hipStreamSynchronize(rs_stream(h)));
+  if (done) {
+    if (int rc = wait_done(h, rs_stream(h), seq)) return rc;
+  } else {
+    KMX_HIP(hipStreamSynchronize(rs_stream(h)));
+  }
   std::memcpy(pairs_out, h->h_io + o_out, pb);
   std::memcpy(k_out, h->h_io + o_out + pb, sizeof(int) * n);
   return KMX_OK;
@@ -4452,16 +4535,21 @@ extern "C" int kmx_lcd_verify_matches(kmx_lcd* h, int32_t n, const int32_t* cq, 
     return 0;
   };
   bool copied = false;
+  unsigned fseq = 0;  // the last kernel's completion word (one zero-copy candidate)
   if (int rc = enqueue_ransac(h, n, stages, inlier_masks != nullptr, true, &copy_out, &copied,
                               zc_out ? reinterpret_cast<kmx_lcd_result*>(h->z_io + o_out) : nullptr,
                               zc_out && inlier_masks ? reinterpret_cast<unsigned char*>(h->z_io + o_out + rb) : nullptr,
-                              spread))
+                              spread, &fseq))
     return rc;
   KMX_HIP(hipGetLastError());
   if (!copied)
     if (int rc = copy_out()) return rc;
   if (int rc = mark_slot(h)) return rc;
-  KMX_HIP(hipStreamSynchronize(rs_stream(h)));
+  if (fseq) {
+    if (int rc = wait_done(h, rs_stream(h), fseq)) return rc;
+  } else {
+    KMX_HIP(hipStreamSynchronize(rs_stream(h)));
+  }
   std::memcpy(results, h->h_io + o_out, sizeof(kmx_lcd_result) * n);
   if (inlier_masks) std::memcpy(inlier_masks, h->h_io + o_out + rb, (size_t)n * h->N);
   return KMX_OK;
