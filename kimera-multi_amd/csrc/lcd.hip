@@ -3424,6 +3424,7 @@ struct kmx_lcd {
   unsigned* d_hcnt = nullptr;  // [spread_cap] k_rs_hyps' wave arrivals per candidate (zero between ranges)
   int more_cap = 0;
   unsigned* h_more = nullptr;  // pinned copy of the word just read
+  unsigned* z_more = nullptr;  // its device pointer (looked up once)
   // a one-candidate call's completion word (mapped; wait_done) and its sequence
   unsigned* h_done = nullptr;
   unsigned* z_done = nullptr;
@@ -3507,7 +3508,7 @@ void lcd_free_cand(kmx_lcd* h) {
   for (void* x : q)
     if (x) (void)hipFree(x);
   if (h->h_more) (void)hipHostFree(h->h_more);
-  h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_more = nullptr; h->h_more = nullptr;
+  h->d_st = nullptr; h->d_hout = nullptr; h->d_sfbuf = nullptr; h->d_more = nullptr; h->h_more = nullptr; h->z_more = nullptr;
   h->d_kqb = nullptr; h->d_kcnt = nullptr; h->kqb_N = 0; h->d_hcnt = nullptr;
   h->spread_cap = 0;
   h->more_cap = 0;
@@ -3956,9 +3957,11 @@ int spread_alloc(kmx_lcd* h, int n) {
     KMX_HIP(hipMalloc(&h->d_more, sizeof(unsigned) * (h->pmax + 1)));
     h->more_cap = h->pmax + 1;
   }
-  if (!h->h_more)
+  if (!h->h_more) {
     KMX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_more), sizeof(unsigned),
                           hipHostMallocMapped | hipHostMallocCoherent));
+    KMX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->z_more), h->h_more, 0));
+  }
   return 0;
 }
 // inited: the caller's k_scatter_pairs already initialised the state (no k_rs_init launch)
@@ -3986,8 +3989,7 @@ int ransac_spread(kmx_lcd* h, int n, int stages, bool want_masks, const std::fun
   if (tail_bytes > 65536 - 16384)  // (max_feats near 1024: 75 KB, + 8.8 KB static: workspace, counts)
     KMX_HIP(hipFuncSetAttribute((const void*)k_rs_finish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tail_bytes));
   const bool zc = res_dst != nullptr;
-  unsigned* z_more = nullptr;
-  if (zc) KMX_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&z_more), h->h_more, 0));
+  unsigned* z_more = zc ? h->z_more : nullptr;
   if (fseq) *fseq = 0;
   const bool one = zc && n == 1 && fseq;  // a one-candidate call: its finishes store the completion word
   auto finish = [&](const unsigned* skip, unsigned* seq_out) {
