@@ -74,6 +74,11 @@ for i, ctr in ((1, "FETCH_SIZE"), (2, "WRITE_SIZE"), (3, None)):
         out["fetch_bytes_per_launch_r3_method"] = (sum(full) + sum(empty)) / n
 out["bytes_per_launch"] = out["fetch_bytes_per_launch"] + out["write_bytes_per_launch"]
 out["traffic_over_alg"] = out["bytes_per_launch"] / out["alg_bytes_per_launch"]
+# the duration split must find the bench's Hess-vec launches: more long dispatches than
+# launches means skipped launches ran past --min-us and are averaged in (round 5's 1M file)
+out["split_ok"] = all(v["long_dispatches"] <= v["bench"] + 1 for k, v in out.items() if k.endswith("_pass_launches"))
+if not out["split_ok"]:
+    print("warning: more long dispatches than Hess-vec launches; raise --min-us", file=sys.stderr)
 print(json.dumps(out, indent=1))
 if len(args) > 1:
     Path(args[1]).write_text(json.dumps(out, indent=1) + "\n")
